@@ -1,0 +1,949 @@
+"""ORACLE — test infrastructure only.  Never imported by the product path.
+
+Object-level, pure-Python restatement of the vendored kube-scheduler v1.10 per-pod
+scheduling cycle that xiaoxubeii/kubernetes-schedule-simulator drives, written for
+small cases (a few hundred nodes / pods).  It works on Kubernetes-shaped dicts
+(``v1.Node`` / ``v1.Pod`` JSON), independent of the product's interning/SoA
+ingest, so that parity tests exercise the whole product path.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg
+may import this module, and only as the checker.
+
+Citation aliases (paths relative to the reference tree):
+  S/  = vendor/k8s.io/kubernetes/pkg/scheduler/
+  K/  = vendor/k8s.io/kubernetes/
+  AM/ = vendor/k8s.io/apimachinery/
+
+Parity pinning: each function below is checked against the golden vectors
+transcribed from the reference's own Go tests (tests/golden/, see
+tests/golden/make_golden.py).  The Go toolchain is absent from this image, so the
+reference itself cannot be run.
+"""
+from __future__ import annotations
+
+import math
+import re
+from fractions import Fraction
+
+# --------------------------------------------------------------------------
+# Quantity  (AM/pkg/api/resource/quantity.go:157-400 parse, :695-713 Value)
+# --------------------------------------------------------------------------
+_BIN = {"Ki": 10, "Mi": 20, "Gi": 30, "Ti": 40, "Pi": 50, "Ei": 60}
+_DEC = {"n": -9, "u": -6, "m": -3, "": 0, "k": 3, "M": 6, "G": 9, "T": 12, "P": 15, "E": 18}
+_QRE = re.compile(r"^([+-]?)([0-9]*)(?:\.([0-9]*))?(.*)$")
+
+
+def parse_quantity(s) -> Fraction:
+    """Exact value of a Quantity string, rounded up to 1e-9 (quantity.go:365-380)."""
+    if isinstance(s, (int,)):
+        return Fraction(s)
+    s = str(s)
+    if s == "":
+        raise ValueError("quantity: empty")
+    m = _QRE.match(s)
+    if not m:
+        raise ValueError("quantity: bad format %r" % s)
+    sign, num, den, suf = m.group(1), m.group(2), m.group(3) or "", m.group(4)
+    if num == "" and den == "":
+        raise ValueError("quantity: no digits %r" % s)
+    mant = Fraction(int(num or "0")) + (Fraction(int(den), 10 ** len(den)) if den else 0)
+    if suf in _BIN:
+        v = mant * (2 ** _BIN[suf])
+    elif suf in _DEC:
+        v = mant * Fraction(10) ** _DEC[suf]
+    elif suf[:1] in ("e", "E") and re.fullmatch(r"[eE][+-]?[0-9]+", suf):
+        v = mant * Fraction(10) ** int(suf[1:])
+    else:
+        raise ValueError("quantity: bad suffix %r" % s)
+    # round non-zero values up to the nano scale (quantity.go:365-372)
+    nano = v * 10 ** 9
+    if nano.denominator != 1:
+        v = Fraction(math.ceil(nano), 10 ** 9)
+    return -v if sign == "-" else v
+
+
+def q_value(s) -> int:
+    """Quantity.Value(): ceil(q) (quantity.go:695-713, ScaledValue rounds up)."""
+    return math.ceil(parse_quantity(s))
+
+
+def q_milli(s) -> int:
+    """Quantity.MilliValue(): ceil(q*1000)."""
+    return math.ceil(parse_quantity(s) * 1000)
+
+
+# --------------------------------------------------------------------------
+# Resource (S/schedulercache/node_info.go:66-109)
+# --------------------------------------------------------------------------
+CPU, MEM, GPU, EPH, PODS = "cpu", "memory", "alpha.kubernetes.io/nvidia-gpu", "ephemeral-storage", "pods"
+
+
+def is_scalar_resource_name(name: str) -> bool:
+    """IsScalarResourceName (K/pkg/apis/core/v1/helper/helpers.go:38-96):
+    extended (has '/', not in *kubernetes.io/, not requests.*, and
+    'requests.'+name is a qualified name) or hugepages-*."""
+    if name.startswith("hugepages-"):
+        return True
+    if "/" not in name or "kubernetes.io/" in name or name.startswith("requests."):
+        return False
+    return valid_label_key("requests." + name)
+
+
+class Resource:
+    __slots__ = ("cpu", "mem", "gpu", "eph", "pods", "scalar")
+
+    def __init__(self):
+        self.cpu = self.mem = self.gpu = self.eph = self.pods = 0
+        self.scalar = {}
+
+    def add(self, rl: dict):
+        """Resource.Add (node_info.go:86-109)."""
+        for name, q in (rl or {}).items():
+            if name == CPU:
+                self.cpu += q_milli(q)
+            elif name == MEM:
+                self.mem += q_value(q)
+            elif name == GPU:
+                self.gpu += q_value(q)
+            elif name == PODS:
+                self.pods += q_value(q)
+            elif name == EPH:
+                self.eph += q_value(q)
+            elif is_scalar_resource_name(name):
+                self.scalar[name] = self.scalar.get(name, 0) + q_value(q)
+
+
+def _containers(pod, key="containers"):
+    return (pod.get("spec") or {}).get(key) or []
+
+
+def _requests(c):
+    return ((c.get("resources") or {}).get("requests")) or {}
+
+
+def _limits(c):
+    return ((c.get("resources") or {}).get("limits")) or {}
+
+
+def get_resource_request(pod) -> Resource:
+    """predicates.go:659-697: sum of containers, max'd with each init container."""
+    r = Resource()
+    for c in _containers(pod):
+        r.add(_requests(c))
+    for c in _containers(pod, "initContainers"):
+        for name, q in _requests(c).items():
+            if name == MEM:
+                r.mem = max(r.mem, q_value(q))
+            elif name == EPH:
+                r.eph = max(r.eph, q_value(q))
+            elif name == CPU:
+                r.cpu = max(r.cpu, q_milli(q))
+            elif name == GPU:
+                r.gpu = max(r.gpu, q_value(q))
+            elif is_scalar_resource_name(name):
+                v = q_value(q)
+                if v > r.scalar.get(name, 0):
+                    r.scalar[name] = v
+    return r
+
+
+DEFAULT_MILLI_CPU = 100                 # priorities/util/non_zero.go:31
+DEFAULT_MEMORY = 200 * 1024 * 1024      # priorities/util/non_zero.go:33
+
+
+def nonzero_requests(reqs: dict):
+    """GetNonzeroRequests (priorities/util/non_zero.go:38-53)."""
+    cpu = DEFAULT_MILLI_CPU if CPU not in reqs else q_milli(reqs[CPU])
+    mem = DEFAULT_MEMORY if MEM not in reqs else q_value(reqs[MEM])
+    return cpu, mem
+
+
+def calculate_resource(pod):
+    """node_info.go:400-412: containers only; returns (Resource, nzcpu, nzmem)."""
+    r = Resource()
+    nzc = nzm = 0
+    for c in _containers(pod):
+        r.add(_requests(c))
+        a, b = nonzero_requests(_requests(c))
+        nzc += a
+        nzm += b
+    return r, nzc, nzm
+
+
+def get_nonzero_pod(pod):
+    """priorities/resource_allocation.go:76-85."""
+    nzc = nzm = 0
+    for c in _containers(pod):
+        a, b = nonzero_requests(_requests(c))
+        nzc += a
+        nzm += b
+    return nzc, nzm
+
+
+def is_best_effort(pod) -> bool:
+    """K/pkg/apis/core/v1/helper/qos/qos.go:39-85 (BestEffort iff no positive
+    cpu/memory request or limit in any container)."""
+    for c in _containers(pod):
+        for rl in (_requests(c), _limits(c)):
+            for name, q in rl.items():
+                if name in (CPU, MEM) and parse_quantity(q) > 0:
+                    return False
+    return True
+
+
+# --------------------------------------------------------------------------
+# Host ports (S/util/utils.go:31-155)
+# --------------------------------------------------------------------------
+def _sanitize(ip, proto):
+    return (ip or "0.0.0.0"), (proto or "TCP")
+
+
+def pod_ports(pod):
+    """GetContainerPorts (S/util/utils.go:144-155)."""
+    out = []
+    for c in _containers(pod):
+        for p in c.get("ports") or []:
+            out.append((p.get("hostIP", ""), p.get("protocol", ""), int(p.get("hostPort", 0) or 0)))
+    return out
+
+
+def check_conflict(used: set, ip, proto, port) -> bool:
+    """HostPortInfo.CheckConflict (S/util/utils.go:101-130)."""
+    if port <= 0:
+        return False
+    ip, proto = _sanitize(ip, proto)
+    if ip == "0.0.0.0":
+        return any((p == proto and n == port) for (_i, p, n) in used)
+    return ("0.0.0.0", proto, port) in used or (ip, proto, port) in used
+
+
+# --------------------------------------------------------------------------
+# Labels (AM/pkg/labels/selector.go)
+# --------------------------------------------------------------------------
+_QN_NAME = re.compile(r"^([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9]$")
+_DNS1123_SUB = re.compile(r"^[a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*$")
+_LABEL_VALUE = re.compile(r"^(([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9])?$")
+
+
+def valid_label_key(k: str) -> bool:
+    """validateLabelKey → IsQualifiedName (apimachinery/pkg/util/validation)."""
+    parts = k.split("/")
+    if len(parts) == 1:
+        name = parts[0]
+    elif len(parts) == 2:
+        prefix, name = parts
+        if len(prefix) == 0 or len(prefix) > 253 or not _DNS1123_SUB.match(prefix):
+            return False
+    else:
+        return False
+    return 0 < len(name) <= 63 and bool(_QN_NAME.match(name))
+
+
+def valid_label_value(v: str) -> bool:
+    return len(v) <= 63 and bool(_LABEL_VALUE.match(v))
+
+
+class Requirement:
+    """labels.Requirement (selector.go:130-235)."""
+
+    def __init__(self, key, op, values):
+        self.key, self.op, self.values = key, op, list(values)
+
+    def matches(self, labels: dict) -> bool:
+        op = self.op
+        if op in ("In", "=", "=="):
+            return self.key in labels and labels[self.key] in self.values
+        if op in ("NotIn", "!="):
+            return self.key not in labels or labels[self.key] not in self.values
+        if op == "Exists":
+            return self.key in labels
+        if op == "DoesNotExist":
+            return self.key not in labels
+        if op in ("Gt", "Lt"):
+            if self.key not in labels:
+                return False
+            try:
+                lv = _parse_int64(labels[self.key])
+            except ValueError:
+                return False
+            if len(self.values) != 1:
+                return False
+            rv = _parse_int64(self.values[0])
+            return (op == "Gt" and lv > rv) or (op == "Lt" and lv < rv)
+        return False
+
+
+def _parse_int64(s: str) -> int:
+    """strconv.ParseInt(s, 10, 64)."""
+    if not re.fullmatch(r"[+-]?[0-9]+", s):
+        raise ValueError(s)
+    v = int(s)
+    if v < -(2 ** 63) or v > 2 ** 63 - 1:
+        raise ValueError(s)
+    return v
+
+
+def new_requirement(key, op, vals):
+    """NewRequirement validation (selector.go:130-178); raises on error."""
+    if not valid_label_key(key):
+        raise ValueError("bad key")
+    if op in ("In", "NotIn"):
+        if len(vals) == 0:
+            raise ValueError("empty values")
+    elif op in ("=", "==", "!="):
+        if len(vals) != 1:
+            raise ValueError("one value")
+    elif op in ("Exists", "DoesNotExist"):
+        if len(vals) != 0:
+            raise ValueError("no values")
+    elif op in ("Gt", "Lt"):
+        if len(vals) != 1:
+            raise ValueError("one value")
+        _parse_int64(vals[0])
+    else:
+        raise ValueError("bad op")
+    for v in vals:
+        if not valid_label_value(v):
+            raise ValueError("bad value")
+    return Requirement(key, op, sorted(vals))
+
+
+def selector_from_set(s: dict):
+    """SelectorFromSet (selector.go:837-853): invalid entry → Everything()."""
+    reqs = []
+    for k, v in (s or {}).items():
+        try:
+            reqs.append(new_requirement(k, "=", [v]))
+        except ValueError:
+            return []
+    return reqs
+
+
+def selector_matches(reqs, labels) -> bool:
+    return all(r.matches(labels) for r in reqs)
+
+
+def node_selector_requirements_as_selector(exprs):
+    """K/pkg/apis/core/v1/helper/helpers.go:215-245. Returns None for Nothing()."""
+    if not exprs:
+        return None
+    reqs = []
+    for e in exprs:
+        op = e.get("operator")
+        if op not in ("In", "NotIn", "Exists", "DoesNotExist", "Gt", "Lt"):
+            raise ValueError("bad operator")
+        reqs.append(new_requirement(e.get("key", ""), op, e.get("values") or []))
+    return reqs
+
+
+def node_matches_terms(labels, terms) -> bool:
+    """predicates.go:780-793 nodeMatchesNodeSelectorTerms."""
+    for t in terms or []:
+        try:
+            sel = node_selector_requirements_as_selector(t.get("matchExpressions") or [])
+        except ValueError:
+            return False
+        if sel is not None and selector_matches(sel, labels):
+            return True
+    return False
+
+
+def pod_matches_node_labels(pod, node) -> bool:
+    """predicates.go:795-838."""
+    spec = pod.get("spec") or {}
+    labels = (node.get("metadata") or {}).get("labels") or {}
+    ns = spec.get("nodeSelector") or {}
+    if len(ns) > 0:
+        if not selector_matches(selector_from_set(ns), labels):
+            return False
+    aff = spec.get("affinity") or {}
+    na = aff.get("nodeAffinity")
+    if na is not None:
+        req = na.get("requiredDuringSchedulingIgnoredDuringExecution")
+        if req is None:
+            return True
+        return node_matches_terms(labels, req.get("nodeSelectorTerms") or [])
+    return True
+
+
+# --------------------------------------------------------------------------
+# Taints / tolerations (vendor/k8s.io/api/core/v1/toleration.go:37-56,
+# K/pkg/apis/core/v1/helper/helpers.go:282-313)
+# --------------------------------------------------------------------------
+def tolerates_taint(tol, taint) -> bool:
+    eff = tol.get("effect", "")
+    if eff and eff != taint.get("effect", ""):
+        return False
+    key = tol.get("key", "")
+    if key and key != taint.get("key", ""):
+        return False
+    op = tol.get("operator", "")
+    if op in ("", "Equal"):
+        return tol.get("value", "") == taint.get("value", "")
+    if op == "Exists":
+        return True
+    return False
+
+
+def tolerations_tolerate_taint(tols, taint) -> bool:
+    return any(tolerates_taint(t, taint) for t in tols)
+
+
+def tolerations_tolerate_taints_with_filter(tols, taints, filt) -> bool:
+    for t in taints or []:
+        if filt is not None and not filt(t):
+            continue
+        if not tolerations_tolerate_taint(tols, t):
+            return False
+    return True
+
+
+# --------------------------------------------------------------------------
+# NodeInfo (S/schedulercache/node_info.go)
+# --------------------------------------------------------------------------
+class NodeInfo:
+    def __init__(self, node=None):
+        self.node = None
+        self.pods = []
+        self.requested = Resource()
+        self.nonzero_cpu = 0
+        self.nonzero_mem = 0
+        self.allocatable = Resource()
+        self.used_ports = set()
+        self.taints = []
+        self.mem_pressure = ""
+        self.disk_pressure = ""
+        if node is not None:
+            self.set_node(node)
+
+    @property
+    def name(self):
+        return (self.node.get("metadata") or {}).get("name", "") if self.node else ""
+
+    def set_node(self, node):
+        """SetNode (node_info.go:429-448)."""
+        self.node = node
+        self.allocatable = Resource()
+        self.allocatable.add((node.get("status") or {}).get("allocatable") or {})
+        self.taints = (node.get("spec") or {}).get("taints") or []
+        for c in (node.get("status") or {}).get("conditions") or []:
+            if c.get("type") == "MemoryPressure":
+                self.mem_pressure = c.get("status", "")
+            elif c.get("type") == "DiskPressure":
+                self.disk_pressure = c.get("status", "")
+
+    def add_pod(self, pod):
+        """AddPod (node_info.go:318-341)."""
+        res, nzc, nzm = calculate_resource(pod)
+        self.requested.cpu += res.cpu
+        self.requested.mem += res.mem
+        self.requested.gpu += res.gpu
+        self.requested.eph += res.eph
+        for k, v in res.scalar.items():
+            self.requested.scalar[k] = self.requested.scalar.get(k, 0) + v
+        self.nonzero_cpu += nzc
+        self.nonzero_mem += nzm
+        self.pods.append(pod)
+        for ip, proto, port in pod_ports(pod):
+            if port > 0:
+                self.used_ports.add(_sanitize(ip, proto) + (port,))
+
+
+# --------------------------------------------------------------------------
+# Predicates (S/algorithm/predicates/predicates.go)
+# --------------------------------------------------------------------------
+R_NOT_READY = "node(s) were not ready"
+R_OUT_OF_DISK = "node(s) were out of disk space"
+R_NET_UNAVAIL = "node(s) had unavailable network"
+R_UNSCHED = "node(s) were unschedulable"
+R_HOSTNAME = "node(s) didn't match the requested hostname"
+R_PORTS = "node(s) didn't have free ports for the requested pod ports"
+R_SELECTOR = "node(s) didn't match node selector"
+R_TAINTS = "node(s) had taints that the pod didn't tolerate"
+R_MEM_PRESSURE = "node(s) had memory pressure"
+R_DISK_PRESSURE = "node(s) had disk pressure"
+
+
+def insufficient(name):
+    return "Insufficient " + name
+
+
+def pred_check_node_condition(pod, ni):
+    """predicates.go:1534-1568."""
+    reasons = []
+    node = ni.node
+    for c in (node.get("status") or {}).get("conditions") or []:
+        t, s = c.get("type"), c.get("status")
+        if t == "Ready" and s != "True":
+            reasons.append(R_NOT_READY)
+        elif t == "OutOfDisk" and s != "False":
+            reasons.append(R_OUT_OF_DISK)
+        elif t == "NetworkUnavailable" and s != "False":
+            reasons.append(R_NET_UNAVAIL)
+    if (node.get("spec") or {}).get("unschedulable"):
+        reasons.append(R_UNSCHED)
+    return not reasons, reasons
+
+
+def pred_check_node_unschedulable(pod, ni):
+    """predicates.go CheckNodeUnschedulablePredicate."""
+    if (ni.node.get("spec") or {}).get("unschedulable"):
+        return False, [R_UNSCHED]
+    return True, []
+
+
+def pred_pod_fits_resources(pod, ni):
+    """predicates.go:706-778."""
+    fails = []
+    allowed = ni.allocatable.pods
+    if len(ni.pods) + 1 > allowed:
+        fails.append(insufficient(PODS))
+    req = get_resource_request(pod)
+    if req.cpu == 0 and req.mem == 0 and req.gpu == 0 and req.eph == 0 and len(req.scalar) == 0:
+        return not fails, fails
+    a, r = ni.allocatable, ni.requested
+    if a.cpu < req.cpu + r.cpu:
+        fails.append(insufficient(CPU))
+    if a.mem < req.mem + r.mem:
+        fails.append(insufficient(MEM))
+    if a.gpu < req.gpu + r.gpu:
+        fails.append(insufficient(GPU))
+    if a.eph < req.eph + r.eph:
+        fails.append(insufficient(EPH))
+    for name in sorted(req.scalar):
+        if a.scalar.get(name, 0) < req.scalar[name] + r.scalar.get(name, 0):
+            fails.append(insufficient(name))
+    return not fails, fails
+
+
+def pred_pod_fits_host(pod, ni):
+    """predicates.go:853-866."""
+    nn = (pod.get("spec") or {}).get("nodeName", "")
+    if not nn:
+        return True, []
+    if nn == ni.name:
+        return True, []
+    return False, [R_HOSTNAME]
+
+
+def pred_pod_fits_host_ports(pod, ni):
+    """predicates.go:1019-1039 + utils.go:138-148."""
+    want = pod_ports(pod)
+    if not want:
+        return True, []
+    for ip, proto, port in want:
+        if check_conflict(ni.used_ports, ip, proto, port):
+            return False, [R_PORTS]
+    return True, []
+
+
+def pred_match_node_selector(pod, ni):
+    """predicates.go:841-850."""
+    if pod_matches_node_labels(pod, ni.node):
+        return True, []
+    return False, [R_SELECTOR]
+
+
+def pred_general(pod, ni):
+    """predicates.go:1059-1120: resources, then host, ports, selector; no short-circuit."""
+    fails = []
+    for f in (pred_pod_fits_resources, pred_pod_fits_host, pred_pod_fits_host_ports, pred_match_node_selector):
+        ok, rs = f(pod, ni)
+        if not ok:
+            fails.extend(rs)
+    return not fails, fails
+
+
+def pred_tolerates_taints(pod, ni):
+    """predicates.go:1465-1474."""
+    tols = (pod.get("spec") or {}).get("tolerations") or []
+    if tolerations_tolerate_taints_with_filter(tols, ni.taints, lambda t: t.get("effect") in ("NoSchedule", "NoExecute")):
+        return True, []
+    return False, [R_TAINTS]
+
+
+def pred_tolerates_noexec_taints(pod, ni):
+    tols = (pod.get("spec") or {}).get("tolerations") or []
+    if tolerations_tolerate_taints_with_filter(tols, ni.taints, lambda t: t.get("effect") == "NoExecute"):
+        return True, []
+    return False, [R_TAINTS]
+
+
+def pred_memory_pressure(pod, ni):
+    """predicates.go:1502-1521."""
+    if not is_best_effort(pod):
+        return True, []
+    if ni.mem_pressure == "True":
+        return False, [R_MEM_PRESSURE]
+    return True, []
+
+
+def pred_disk_pressure(pod, ni):
+    """predicates.go:1524-1530."""
+    if ni.disk_pressure == "True":
+        return False, [R_DISK_PRESSURE]
+    return True, []
+
+
+def pred_true(pod, ni):
+    return True, []
+
+
+PREDICATES = {
+    "CheckNodeCondition": pred_check_node_condition,
+    "CheckNodeUnschedulable": pred_check_node_unschedulable,
+    "GeneralPredicates": pred_general,
+    "HostName": pred_pod_fits_host,
+    "PodFitsHostPorts": pred_pod_fits_host_ports,
+    "PodFitsPorts": pred_pod_fits_host_ports,
+    "MatchNodeSelector": pred_match_node_selector,
+    "PodFitsResources": pred_pod_fits_resources,
+    "NoDiskConflict": pred_true,
+    "PodToleratesNodeTaints": pred_tolerates_taints,
+    "PodToleratesNodeNoExecuteTaints": pred_tolerates_noexec_taints,
+    "MaxEBSVolumeCount": pred_true,
+    "MaxGCEPDVolumeCount": pred_true,
+    "MaxAzureDiskVolumeCount": pred_true,
+    "CheckVolumeBinding": pred_true,
+    "NoVolumeZoneConflict": pred_true,
+    "CheckNodeMemoryPressure": pred_memory_pressure,
+    "CheckNodeDiskPressure": pred_disk_pressure,
+    "MatchInterPodAffinity": pred_true,
+}
+
+# predicates.go:129-138 (PodFitsPorts is registered under its own key but is not
+# in the ordering list, so it never runs from podFitsOnNode)
+ORDERING = ["CheckNodeCondition", "CheckNodeUnschedulable", "GeneralPredicates", "HostName",
+            "PodFitsHostPorts", "MatchNodeSelector", "PodFitsResources", "NoDiskConflict",
+            "PodToleratesNodeTaints", "PodToleratesNodeNoExecuteTaints", "CheckNodeLabelPresence",
+            "CheckServiceAffinity", "MaxEBSVolumeCount", "MaxGCEPDVolumeCount",
+            "MaxAzureDiskVolumeCount", "CheckVolumeBinding", "NoVolumeZoneConflict",
+            "CheckNodeMemoryPressure", "CheckNodeDiskPressure", "MatchInterPodAffinity"]
+
+
+def pod_fits_on_node(pod, ni, keys):
+    """S/core/generic_scheduler.go:420-534 (nominated-pod pass inert; no ecache)."""
+    for k in ORDERING:
+        if k in keys:
+            ok, rs = PREDICATES[k](pod, ni)
+            if not ok:
+                return False, rs
+    return True, []
+
+
+# --------------------------------------------------------------------------
+# Priorities (S/algorithm/priorities/*)
+# --------------------------------------------------------------------------
+MAX_PRIORITY = 10
+
+
+def _least_score(req, cap):
+    """least_requested.go:44-53 (Go int64 truncating division)."""
+    if cap == 0 or req > cap:
+        return 0
+    return ((cap - req) * MAX_PRIORITY) // cap
+
+
+def _most_score(req, cap):
+    """most_requested.go:45-55."""
+    if cap == 0 or req > cap:
+        return 0
+    return (req * MAX_PRIORITY) // cap
+
+
+def _fraction(req, cap):
+    """balanced_resource_allocation.go:57-61."""
+    if cap == 0:
+        return 1.0
+    return float(req) / float(cap)
+
+
+def _resource_requested(pod, ni):
+    nzc, nzm = get_nonzero_pod(pod)
+    return nzc + ni.nonzero_cpu, nzm + ni.nonzero_mem
+
+
+def prio_least_requested(pod, ni):
+    """resource_allocation.go:37-74 + least_requested.go:36-42."""
+    c, m = _resource_requested(pod, ni)
+    return (_least_score(c, ni.allocatable.cpu) + _least_score(m, ni.allocatable.mem)) // 2
+
+
+def prio_most_requested(pod, ni):
+    c, m = _resource_requested(pod, ni)
+    return (_most_score(c, ni.allocatable.cpu) + _most_score(m, ni.allocatable.mem)) // 2
+
+
+def prio_balanced(pod, ni):
+    """balanced_resource_allocation.go:39-55 (IEEE doubles, trunc to int64)."""
+    c, m = _resource_requested(pod, ni)
+    fc = _fraction(c, ni.allocatable.cpu)
+    fm = _fraction(m, ni.allocatable.mem)
+    if fc >= 1 or fm >= 1:
+        return 0
+    diff = abs(fc - fm)
+    return int((1 - diff) * float(MAX_PRIORITY))
+
+
+def prio_taint_toleration_map(pod, ni):
+    """taint_toleration.go:29-73."""
+    tols = [t for t in ((pod.get("spec") or {}).get("tolerations") or [])
+            if t.get("effect", "") in ("", "PreferNoSchedule")]
+    cnt = 0
+    for taint in ni.taints:
+        if taint.get("effect") != "PreferNoSchedule":
+            continue
+        if not tolerations_tolerate_taint(tols, taint):
+            cnt += 1
+    return cnt
+
+
+def prio_node_affinity_map(pod, ni):
+    """node_affinity.go:34-75."""
+    aff = ((pod.get("spec") or {}).get("affinity") or {}).get("nodeAffinity") or {}
+    labels = (ni.node.get("metadata") or {}).get("labels") or {}
+    count = 0
+    for term in aff.get("preferredDuringSchedulingIgnoredDuringExecution") or []:
+        w = int(term.get("weight", 0))
+        if w == 0:
+            continue
+        sel = node_selector_requirements_as_selector((term.get("preference") or {}).get("matchExpressions") or [])
+        if sel is not None and selector_matches(sel, labels):
+            count += w
+    return count
+
+
+def normalize_reduce(scores, reverse):
+    """reduce.go:29-64 (Go int truncating division)."""
+    mx = 0
+    for s in scores:
+        if s > mx:
+            mx = s
+    if mx == 0:
+        return [MAX_PRIORITY] * len(scores) if reverse else list(scores)
+    out = []
+    for s in scores:
+        v = _go_div(MAX_PRIORITY * s, mx)
+        out.append(MAX_PRIORITY - v if reverse else v)
+    return out
+
+
+def _go_div(a, b):
+    q = abs(a) // abs(b)
+    return q if (a >= 0) == (b >= 0) else -q
+
+
+def spread_reduce(scores, zones):
+    """selector_spreading.go:121-174 with the map already computed."""
+    counts_by_zone = {}
+    max_node = 0
+    for s, z in zip(scores, zones):
+        if s > max_node:
+            max_node = s
+        if z == "":
+            continue
+        counts_by_zone[z] = counts_by_zone.get(z, 0) + s
+    max_zone = 0
+    for v in counts_by_zone.values():
+        if v > max_zone:
+            max_zone = v
+    have_zones = len(counts_by_zone) != 0
+    zw = 2.0 / 3.0
+    out = []
+    for s, z in zip(scores, zones):
+        f = float(MAX_PRIORITY)
+        if max_node > 0:
+            f = float(MAX_PRIORITY) * (float(max_node - s) / float(max_node))
+        if have_zones and z != "":
+            zs = float(MAX_PRIORITY)
+            if max_zone > 0:
+                zs = float(MAX_PRIORITY) * (float(max_zone - counts_by_zone[z]) / float(max_zone))
+            f = (f * (1.0 - zw)) + (zw * zs)
+        out.append(int(f))
+    return out
+
+
+def zone_key(node):
+    """K/pkg/util/node GetZoneKey: region:\\x00:zone from failure-domain labels."""
+    labels = (node.get("metadata") or {}).get("labels") or {}
+    region = labels.get("failure-domain.beta.kubernetes.io/region", "")
+    zone = labels.get("failure-domain.beta.kubernetes.io/zone", "")
+    if region == "" and zone == "":
+        return ""
+    return region + ":\x00:" + zone
+
+
+# Priority configs: name -> (kind, fn).  "map" = plain map; "reduce-rev"/"reduce-fwd"
+# = NormalizeReduce; "spread" = selector spreading with no selectors in the
+# simulator's store (map 0 → reduce); "const" = evaluates the same for every node
+# under the simulator's inputs (documented in DESIGN.md).
+def _prio_zero(pod, ni):
+    return 0
+
+
+def _prio_prefer_avoid(pod, ni):
+    """node_prefer_avoid_pods.go:32-68: pods without an RC/RS controllerRef → 10."""
+    for o in ((pod.get("metadata") or {}).get("ownerReferences") or []):
+        if o.get("controller") and o.get("kind") in ("ReplicationController", "ReplicaSet"):
+            raise NotImplementedError("NodePreferAvoidPods with controller refs")
+    return MAX_PRIORITY
+
+
+def _prio_equal(pod, ni):
+    return 1
+
+
+PRIORITIES = {
+    "LeastRequestedPriority": ("map", prio_least_requested),
+    "MostRequestedPriority": ("map", prio_most_requested),
+    "BalancedResourceAllocation": ("map", prio_balanced),
+    "TaintTolerationPriority": ("reduce-rev", prio_taint_toleration_map),
+    "NodeAffinityPriority": ("reduce-fwd", prio_node_affinity_map),
+    "NodePreferAvoidPodsPriority": ("map", _prio_prefer_avoid),
+    "SelectorSpreadPriority": ("spread", _prio_zero),
+    "ServiceSpreadingPriority": ("spread", _prio_zero),
+    "InterPodAffinityPriority": ("map", _prio_zero),
+    "EqualPriority": ("map", _prio_equal),
+}
+
+
+def prioritize_nodes(pod, infos, configs):
+    """S/core/generic_scheduler.go:542-676.  configs: list of (name, weight)."""
+    if not configs:
+        return [1 for _ in infos]          # EqualPriorityMap
+    total = [0] * len(infos)
+    for name, weight in configs:
+        kind, fn = PRIORITIES[name]
+        scores = [fn(pod, ni) for ni in infos]
+        if kind == "reduce-rev":
+            scores = normalize_reduce(scores, True)
+        elif kind == "reduce-fwd":
+            scores = normalize_reduce(scores, False)
+        elif kind == "spread":
+            scores = spread_reduce(scores, [zone_key(ni.node) for ni in infos])
+        for i, s in enumerate(scores):
+            total[i] += s * weight
+    return total
+
+
+# --------------------------------------------------------------------------
+# Providers (S/algorithmprovider/defaults/defaults.go:113-259)
+# --------------------------------------------------------------------------
+DEFAULT_PREDICATES = {"NoVolumeZoneConflict", "MaxEBSVolumeCount", "MaxGCEPDVolumeCount",
+                      "MaxAzureDiskVolumeCount", "MatchInterPodAffinity", "NoDiskConflict",
+                      "GeneralPredicates", "CheckNodeMemoryPressure", "CheckNodeDiskPressure",
+                      "CheckNodeCondition", "PodToleratesNodeTaints", "CheckVolumeBinding"}
+DEFAULT_PRIORITIES = [("SelectorSpreadPriority", 1), ("InterPodAffinityPriority", 1),
+                      ("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1),
+                      ("NodePreferAvoidPodsPriority", 10000), ("NodeAffinityPriority", 1),
+                      ("TaintTolerationPriority", 1)]
+
+
+def provider(name):
+    pri = list(DEFAULT_PRIORITIES)
+    if name in ("ClusterAutoscalerProvider", "TalkintDataProvider"):
+        pri = [("MostRequestedPriority", 1) if n == "LeastRequestedPriority" else (n, w) for n, w in pri]
+    elif name != "DefaultProvider":
+        raise KeyError(name)
+    return set(DEFAULT_PREDICATES), pri
+
+
+# --------------------------------------------------------------------------
+# Generic scheduler (S/core/generic_scheduler.go:112-198)
+# --------------------------------------------------------------------------
+class FitError(Exception):
+    def __init__(self, num_nodes, failed):
+        self.num_nodes = num_nodes
+        self.failed = failed      # node name -> [reasons]
+
+    def histogram(self):
+        h = {}
+        for rs in self.failed.values():
+            for r in rs:
+                h[r] = h.get(r, 0) + 1
+        return h
+
+    def __str__(self):
+        """FitError.Error (generic_scheduler.go:72-90)."""
+        parts = sorted("%d %s" % (v, k) for k, v in self.histogram().items())
+        return "0/%d nodes are available: %s." % (self.num_nodes, ", ".join(parts))
+
+
+class GenericScheduler:
+    def __init__(self, predicate_keys, priority_configs):
+        self.predicates = set(predicate_keys)
+        self.prioritizers = list(priority_configs)
+        self.last_node_index = 0          # uint64 (generic_scheduler.go:102)
+
+    def schedule(self, pod, infos):
+        """Schedule (generic_scheduler.go:112-167). infos: list of NodeInfo in any order."""
+        if not infos:
+            raise RuntimeError("no nodes available to schedule pods")
+        filtered, failed = [], {}
+        for ni in infos:
+            ok, rs = pod_fits_on_node(pod, ni, self.predicates) if self.predicates else (True, [])
+            if ok:
+                filtered.append(ni)
+            else:
+                failed[ni.name] = rs
+        if not filtered:
+            raise FitError(len(infos), failed)
+        if len(filtered) == 1:
+            return filtered[0].name
+        scores = prioritize_nodes(pod, filtered, self.prioritizers)
+        return self.select_host([(ni.name, s) for ni, s in zip(filtered, scores)])
+
+    def select_host(self, plist):
+        """selectHost (generic_scheduler.go:183-198) + HostPriorityList.Less (S/api/types.go:272-277).
+        Host names compare bytewise (Go string <)."""
+        lst = sorted(plist, key=lambda hs: (hs[1], hs[0].encode()), reverse=True)
+        mx = lst[0][1]
+        first_after = next((i for i, hs in enumerate(lst) if hs[1] < mx), len(lst))
+        ix = self.last_node_index % first_after
+        self.last_node_index = (self.last_node_index + 1) % (1 << 64)
+        return lst[ix][0]
+
+
+# --------------------------------------------------------------------------
+# Simulator (pkg/scheduler/simulator.go:108-223, pkg/framework/store/store.go:212-241)
+# --------------------------------------------------------------------------
+def expand_simulation_pods(spec_list):
+    """cmd/app/options/options.go:73-99: each SimulationPod repeated Num times,
+    labelled SimulationName=<name>, namespace "" (names are uuids in Go; here
+    deterministic <name>-<i>)."""
+    out = []
+    for sp in spec_list:
+        for i in range(int(sp.get("num", 0))):
+            pod = {"metadata": {"name": "%s-%d" % (sp["name"], i), "namespace": "",
+                                "labels": {"SimulationName": sp["name"]}},
+                   "spec": (sp.get("pod") or {}).get("spec") or {}}
+            out.append(pod)
+    return out
+
+
+def simulate(nodes, running_pods, sim_pods, predicate_keys, priority_configs):
+    """Runs the ClusterCapacity loop: pods are popped LIFO (store.go:223-233),
+    each is scheduled, bound pods are assumed into the node cache (scheduler.go:366
+    → cache.go:125 → node_info.go:318), unschedulable pods are recorded and the
+    loop continues (simulator.go:163-185) until the queue is empty.
+    Returns list of (pod_name, node_name or None, fit_error_message or None)."""
+    infos = [NodeInfo(n) for n in nodes]
+    by_name = {ni.name: ni for ni in infos}
+    for p in running_pods:
+        nn = (p.get("spec") or {}).get("nodeName", "")
+        if nn in by_name:
+            by_name[nn].add_pod(p)
+    sched = GenericScheduler(predicate_keys, priority_configs)
+    queue = list(sim_pods)
+    out = []
+    while queue:
+        pod = queue.pop()
+        name = (pod.get("metadata") or {}).get("name", "")
+        try:
+            host = sched.schedule(pod, infos)
+        except FitError as e:
+            out.append((name, None, str(e)))
+            continue
+        by_name[host].add_pod(pod)
+        out.append((name, host, None))
+    return out, sched.last_node_index

@@ -1,0 +1,592 @@
+"""Generates tests/golden/*.json — golden vectors hand-transcribed from the reference's
+own Go unit tests (the vendored kube-scheduler v1.10 tests under
+/root/reference/vendor/k8s.io/kubernetes/pkg/scheduler/).  Each case records the Go
+test function and file:line it was transcribed from.  Inputs are rebuilt here as
+Kubernetes-shaped JSON objects with the helpers the Go tests use (makeNode,
+newResourcePod, newPod, ...); expected outputs are copied verbatim.
+
+Run:  python tests/golden/make_golden.py      (rewrites the JSON files)
+"""
+import json
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+S = "vendor/k8s.io/kubernetes/pkg/scheduler/"
+
+
+# ---------------------------------------------------------------- helpers
+def node(name="", cpu_m=None, mem=None, pods=None, labels=None, taints=None, conditions=None,
+         unschedulable=None, alloc_extra=None):
+    n = {"metadata": {"name": name}, "spec": {}, "status": {}}
+    alloc = {}
+    if cpu_m is not None:
+        alloc["cpu"] = "%dm" % cpu_m
+    if mem is not None:
+        alloc["memory"] = "%d" % mem
+    if pods is not None:
+        alloc["pods"] = "%d" % pods
+    if alloc_extra:
+        alloc.update(alloc_extra)
+    if alloc:
+        n["status"]["allocatable"] = alloc
+    if labels is not None:
+        n["metadata"]["labels"] = labels
+    if taints is not None:
+        n["spec"]["taints"] = taints
+    if conditions is not None:
+        n["status"]["conditions"] = [{"type": t, "status": s} for t, s in conditions]
+    if unschedulable is not None:
+        n["spec"]["unschedulable"] = unschedulable
+    return n
+
+
+def ctr(cpu=None, mem=None, extra=None, ports=None):
+    """A container whose requests hold exactly the given quantity strings."""
+    req = {}
+    if cpu is not None:
+        req["cpu"] = cpu
+    if mem is not None:
+        req["memory"] = mem
+    if extra:
+        req.update(extra)
+    c = {"resources": {"requests": req}} if (req or cpu is not None or mem is not None) else {}
+    if ports:
+        c["ports"] = ports
+    return c
+
+
+def pod(containers=None, init=None, node_name=None, name=None, labels=None, **spec):
+    p = {"metadata": {}, "spec": {}}
+    if name:
+        p["metadata"]["name"] = name
+    if labels:
+        p["metadata"]["labels"] = labels
+    if containers is not None:
+        p["spec"]["containers"] = containers
+    if init is not None:
+        p["spec"]["initContainers"] = init
+    if node_name:
+        p["spec"]["nodeName"] = node_name
+    p["spec"].update(spec)
+    return p
+
+
+def res_ctr(cpu_m=0, mem=0, scalar=None, eph=None):
+    """Container built from schedulercache.Resource.ResourceList() (node_info.go:111-127):
+    cpu, memory, nvidia-gpu, pods and ephemeral-storage are ALWAYS present (zero or not)."""
+    req = {"cpu": "%dm" % cpu_m, "memory": "%d" % mem, "alpha.kubernetes.io/nvidia-gpu": "0",
+           "pods": "0", "ephemeral-storage": "%d" % (eph or 0)}
+    for k, v in (scalar or {}).items():
+        req[k] = "%d" % v
+    return {"resources": {"requests": req}}
+
+
+cases = {}
+
+
+def add(group, case):
+    cases.setdefault(group, []).append(case)
+
+
+# ------------------------------------------------ priorities: LR / MR / BRA
+# least_requested_test.go:30-245, most_requested_test.go:30-206,
+# balanced_resource_allocation_test.go:30-264 share these pod specs.
+no_resources = pod(containers=[])
+cpu_only = pod(node_name="machine1", containers=[ctr("1000m", "0"), ctr("2000m", "0")])
+cpu_only2 = pod(node_name="machine2", containers=[ctr("1000m", "0"), ctr("2000m", "0")])
+cpu_and_memory = pod(node_name="machine2", containers=[ctr("1000m", "2000"), ctr("2000m", "3000")])
+big_cpu_and_memory = pod(node_name="machine1", containers=[ctr("2000m", "4000"), ctr("3000m", "5000")])
+m1 = pod(node_name="machine1")
+m2 = pod(node_name="machine2")
+
+
+def mk(name, c, m):   # priorities/test_util.go:28 makeNode (no pods entry)
+    return node(name, c, m)
+
+
+def prio_case(src, prio, test, p, nodes, expect, pods=()):
+    add("priorities", {"source": src, "test": test, "priority": prio, "pod": p,
+                       "nodes": nodes, "pods": list(pods), "expect": expect})
+
+
+LRsrc = S + "algorithm/priorities/least_requested_test.go"
+prio_case(LRsrc + ":111", "LeastRequestedPriority", "nothing scheduled, nothing requested", no_resources,
+          [mk("machine1", 4000, 10000), mk("machine2", 4000, 10000)], [["machine1", 10], ["machine2", 10]])
+prio_case(LRsrc + ":125", "LeastRequestedPriority", "nothing scheduled, resources requested, differently sized machines",
+          cpu_and_memory, [mk("machine1", 4000, 10000), mk("machine2", 6000, 10000)], [["machine1", 3], ["machine2", 5]])
+prio_case(LRsrc + ":139", "LeastRequestedPriority", "no resources requested, pods scheduled", no_resources,
+          [mk("machine1", 4000, 10000), mk("machine2", 4000, 10000)], [["machine1", 10], ["machine2", 10]],
+          [m1, m1, m2, m2])
+prio_case(LRsrc + ":159", "LeastRequestedPriority", "no resources requested, pods scheduled with resources", no_resources,
+          [mk("machine1", 10000, 20000), mk("machine2", 10000, 20000)], [["machine1", 7], ["machine2", 5]],
+          [cpu_only, cpu_only, cpu_only2, cpu_and_memory])
+prio_case(LRsrc + ":179", "LeastRequestedPriority", "resources requested, pods scheduled with resources", cpu_and_memory,
+          [mk("machine1", 10000, 20000), mk("machine2", 10000, 20000)], [["machine1", 5], ["machine2", 4]],
+          [cpu_only, cpu_and_memory])
+prio_case(LRsrc + ":197", "LeastRequestedPriority", "resources requested, pods scheduled with resources, differently sized machines",
+          cpu_and_memory, [mk("machine1", 10000, 20000), mk("machine2", 10000, 50000)], [["machine1", 5], ["machine2", 6]],
+          [cpu_only, cpu_and_memory])
+prio_case(LRsrc + ":215", "LeastRequestedPriority", "requested resources exceed node capacity", cpu_only,
+          [mk("machine1", 4000, 10000), mk("machine2", 4000, 10000)], [["machine1", 5], ["machine2", 2]],
+          [cpu_only, cpu_and_memory])
+prio_case(LRsrc + ":224", "LeastRequestedPriority", "zero node resources, pods scheduled with resources", no_resources,
+          [mk("machine1", 0, 0), mk("machine2", 0, 0)], [["machine1", 0], ["machine2", 0]],
+          [cpu_only, cpu_and_memory])
+
+MRsrc = S + "algorithm/priorities/most_requested_test.go"
+prio_case(MRsrc + ":128", "MostRequestedPriority", "nothing scheduled, nothing requested", no_resources,
+          [mk("machine1", 4000, 10000), mk("machine2", 4000, 10000)], [["machine1", 0], ["machine2", 0]])
+prio_case(MRsrc + ":142", "MostRequestedPriority", "nothing scheduled, resources requested, differently sized machines",
+          cpu_and_memory, [mk("machine1", 4000, 10000), mk("machine2", 6000, 10000)], [["machine1", 6], ["machine2", 5]])
+prio_case(MRsrc + ":156", "MostRequestedPriority", "no resources requested, pods scheduled with resources", no_resources,
+          [mk("machine1", 10000, 20000), mk("machine2", 10000, 20000)], [["machine1", 3], ["machine2", 4]],
+          [cpu_only, cpu_only, cpu_only2, cpu_and_memory])
+prio_case(MRsrc + ":176", "MostRequestedPriority", "resources requested, pods scheduled with resources", cpu_and_memory,
+          [mk("machine1", 10000, 20000), mk("machine2", 10000, 20000)], [["machine1", 4], ["machine2", 5]],
+          [cpu_only, cpu_and_memory])
+prio_case(MRsrc + ":194", "MostRequestedPriority", "resources requested with more than the node, pods scheduled with resources",
+          big_cpu_and_memory, [mk("machine1", 4000, 10000), mk("machine2", 10000, 8000)], [["machine1", 4], ["machine2", 2]])
+
+BRsrc = S + "algorithm/priorities/balanced_resource_allocation_test.go"
+prio_case(BRsrc + ":116", "BalancedResourceAllocation", "nothing scheduled, nothing requested", no_resources,
+          [mk("machine1", 4000, 10000), mk("machine2", 4000, 10000)], [["machine1", 10], ["machine2", 10]])
+prio_case(BRsrc + ":133", "BalancedResourceAllocation", "nothing scheduled, resources requested, differently sized machines",
+          cpu_and_memory, [mk("machine1", 4000, 10000), mk("machine2", 6000, 10000)], [["machine1", 7], ["machine2", 10]])
+prio_case(BRsrc + ":150", "BalancedResourceAllocation", "no resources requested, pods scheduled", no_resources,
+          [mk("machine1", 4000, 10000), mk("machine2", 4000, 10000)], [["machine1", 10], ["machine2", 10]],
+          [m1, m1, m2, m2])
+prio_case(BRsrc + ":173", "BalancedResourceAllocation", "no resources requested, pods scheduled with resources", no_resources,
+          [mk("machine1", 10000, 20000), mk("machine2", 10000, 20000)], [["machine1", 4], ["machine2", 6]],
+          [cpu_only, cpu_only, cpu_only2, cpu_and_memory])
+prio_case(BRsrc + ":196", "BalancedResourceAllocation", "resources requested, pods scheduled with resources", cpu_and_memory,
+          [mk("machine1", 10000, 20000), mk("machine2", 10000, 20000)], [["machine1", 6], ["machine2", 9]],
+          [cpu_only, cpu_and_memory])
+prio_case(BRsrc + ":217", "BalancedResourceAllocation", "resources requested, pods scheduled with resources, differently sized machines",
+          cpu_and_memory, [mk("machine1", 10000, 20000), mk("machine2", 10000, 50000)], [["machine1", 6], ["machine2", 6]],
+          [cpu_only, cpu_and_memory])
+prio_case(BRsrc + ":238", "BalancedResourceAllocation", "requested resources exceed node capacity", cpu_only,
+          [mk("machine1", 4000, 10000), mk("machine2", 4000, 10000)], [["machine1", 0], ["machine2", 0]],
+          [cpu_only, cpu_and_memory])
+prio_case(BRsrc + ":247", "BalancedResourceAllocation", "zero node resources, pods scheduled with resources", no_resources,
+          [mk("machine1", 0, 0), mk("machine2", 0, 0)], [["machine1", 0], ["machine2", 0]],
+          [cpu_only, cpu_and_memory])
+
+# ------------------------------------------------ TaintToleration priority
+TTsrc = S + "algorithm/priorities/taint_toleration_test.go"
+
+
+def tnode(name, taints):
+    return node(name, taints=taints)
+
+
+def taint(k, v, e):
+    return {"key": k, "value": v, "effect": e}
+
+
+def tol(k, op, v, e):
+    d = {"key": k, "operator": op, "value": v}
+    if e:
+        d["effect"] = e
+    return d
+
+
+prio_case(TTsrc + ":51", "TaintTolerationPriority",
+          "node with taints tolerated by the pod, gets a higher score than those node with intolerable taints",
+          pod(tolerations=[tol("foo", "Equal", "bar", "PreferNoSchedule")]),
+          [tnode("nodeA", [taint("foo", "bar", "PreferNoSchedule")]), tnode("nodeB", [taint("foo", "blah", "PreferNoSchedule")])],
+          [["nodeA", 10], ["nodeB", 0]])
+prio_case(TTsrc + ":75", "TaintTolerationPriority",
+          "the nodes that all of their taints are tolerated by the pod, get the same score, no matter how many tolerable taints a node has",
+          pod(tolerations=[tol("cpu-type", "Equal", "arm64", "PreferNoSchedule"), tol("disk-type", "Equal", "ssd", "PreferNoSchedule")]),
+          [tnode("nodeA", []), tnode("nodeB", [taint("cpu-type", "arm64", "PreferNoSchedule")]),
+           tnode("nodeC", [taint("cpu-type", "arm64", "PreferNoSchedule"), taint("disk-type", "ssd", "PreferNoSchedule")])],
+          [["nodeA", 10], ["nodeB", 10], ["nodeC", 10]])
+prio_case(TTsrc + ":118", "TaintTolerationPriority", "the more intolerable taints a node has, the lower score it gets.",
+          pod(tolerations=[tol("foo", "Equal", "bar", "PreferNoSchedule")]),
+          [tnode("nodeA", []), tnode("nodeB", [taint("cpu-type", "arm64", "PreferNoSchedule")]),
+           tnode("nodeC", [taint("cpu-type", "arm64", "PreferNoSchedule"), taint("disk-type", "ssd", "PreferNoSchedule")])],
+          [["nodeA", 10], ["nodeB", 5], ["nodeC", 0]])
+prio_case(TTsrc + ":154", "TaintTolerationPriority",
+          "only taints and tolerations that have effect PreferNoSchedule are checked by taints-tolerations priority function",
+          pod(tolerations=[tol("cpu-type", "Equal", "arm64", "NoSchedule"), tol("disk-type", "Equal", "ssd", "NoSchedule")]),
+          [tnode("nodeA", []), tnode("nodeB", [taint("cpu-type", "arm64", "NoSchedule")]),
+           tnode("nodeC", [taint("cpu-type", "arm64", "PreferNoSchedule"), taint("disk-type", "ssd", "PreferNoSchedule")])],
+          [["nodeA", 10], ["nodeB", 10], ["nodeC", 0]])
+prio_case(TTsrc + ":196", "TaintTolerationPriority", "Default behaviour No taints and tolerations, lands on node with no taints",
+          pod(tolerations=[]),
+          [tnode("nodeA", []), tnode("nodeB", [taint("cpu-type", "arm64", "PreferNoSchedule")])],
+          [["nodeA", 10], ["nodeB", 0]])
+
+# ------------------------------------------------ NodeAffinity priority
+NAsrc = S + "algorithm/priorities/node_affinity_test.go"
+
+
+def pref(w, exprs):
+    return {"weight": w, "preference": {"matchExpressions": exprs}}
+
+
+def expr(k, op, vals=None):
+    e = {"key": k, "operator": op}
+    if vals is not None:
+        e["values"] = vals
+    return e
+
+
+aff1 = {"nodeAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [pref(2, [expr("foo", "In", ["bar"])])]}}
+aff2 = {"nodeAffinity": {"preferredDuringSchedulingIgnoredDuringExecution": [
+    pref(2, [expr("foo", "In", ["bar"])]), pref(4, [expr("key", "In", ["value"])]),
+    pref(5, [expr("foo", "In", ["bar"]), expr("key", "In", ["value"]), expr("az", "In", ["az1"])])]}}
+L1, L2, L3 = {"foo": "bar"}, {"key": "value"}, {"az": "az1"}
+L4 = {"abc": "az11", "def": "az22"}
+L5 = {"foo": "bar", "key": "value", "az": "az1"}
+prio_case(NAsrc + ":127", "NodeAffinityPriority", "all machines are same priority as NodeAffinity is nil", pod(),
+          [node("machine1", labels=L1), node("machine2", labels=L2), node("machine3", labels=L3)],
+          [["machine1", 0], ["machine2", 0], ["machine3", 0]])
+prio_case(NAsrc + ":141", "NodeAffinityPriority",
+          "no machine macthes preferred scheduling requirements in NodeAffinity of pod so all machines' priority is zero",
+          pod(affinity=aff1), [node("machine1", labels=L4), node("machine2", labels=L2), node("machine3", labels=L3)],
+          [["machine1", 0], ["machine2", 0], ["machine3", 0]])
+prio_case(NAsrc + ":155", "NodeAffinityPriority", "only machine1 matches the preferred scheduling requirements of pod",
+          pod(affinity=aff1), [node("machine1", labels=L1), node("machine2", labels=L2), node("machine3", labels=L3)],
+          [["machine1", 10], ["machine2", 0], ["machine3", 0]])
+prio_case(NAsrc + ":169", "NodeAffinityPriority",
+          "all machines matches the preferred scheduling requirements of pod but with different priorities ",
+          pod(affinity=aff2), [node("machine1", labels=L1), node("machine5", labels=L5), node("machine2", labels=L2)],
+          [["machine1", 1], ["machine5", 10], ["machine2", 3]])
+
+# ------------------------------------------------ PodFitsResources
+PFsrc = S + "algorithm/predicates/predicates_test.go"
+EXT_A, EXT_B, HUGE_A = "example.com/aaa", "example.com/bbb", "hugepages-2Mi"
+
+
+def alloc(cpu, mem, gpu, pods, ext_a, eph, huge_a):   # predicates_test.go:62-72
+    return {"cpu": "%dm" % cpu, "memory": "%d" % mem, "pods": "%d" % pods,
+            "alpha.kubernetes.io/nvidia-gpu": "%d" % gpu, EXT_A: "%d" % ext_a,
+            "ephemeral-storage": "%d" % eph, HUGE_A: "%d" % huge_a}
+
+
+def rpod(*usages, init=None):
+    p = pod(containers=[res_ctr(**u) for u in usages])
+    if init is not None:
+        p["spec"]["initContainers"] = [res_ctr(**u) for u in init]
+    return p
+
+
+def R(c=0, m=0, **kw):
+    d = {"cpu_m": c, "mem": m}
+    d.update(kw)
+    return d
+
+
+def fit_case(src, test, p, existing, nalloc, fits, reasons=()):
+    n = {"metadata": {"name": "n"}, "spec": {}, "status": {"allocatable": nalloc}}
+    ex = []
+    for e in existing:
+        e = json.loads(json.dumps(e))
+        e["spec"]["nodeName"] = "n"
+        ex.append(e)
+    add("predicates", {"source": src, "test": test, "predicate": "PodFitsResources", "pod": p,
+                       "node": n, "pods": ex, "fits": fits, "reasons": list(reasons)})
+
+
+A32 = alloc(10, 20, 0, 32, 5, 20, 5)
+IC, IM, IP, IE = "Insufficient cpu", "Insufficient memory", "Insufficient pods", "Insufficient ephemeral-storage"
+fit_case(PFsrc + ":104", "no resources requested always fits", pod(), [rpod(R(10, 20))], A32, True)
+fit_case(PFsrc + ":111", "too many resources fails", rpod(R(1, 1)), [rpod(R(10, 20))], A32, False, [IC, IM])
+fit_case(PFsrc + ":121", "too many resources fails due to init container cpu", rpod(R(1, 1), init=[R(3, 1)]),
+         [rpod(R(8, 19))], A32, False, [IC])
+fit_case(PFsrc + ":128", "too many resources fails due to highest init container cpu",
+         rpod(R(1, 1), init=[R(3, 1), R(2, 1)]), [rpod(R(8, 19))], A32, False, [IC])
+fit_case(PFsrc + ":135", "too many resources fails due to init container memory", rpod(R(1, 1), init=[R(1, 3)]),
+         [rpod(R(9, 19))], A32, False, [IM])
+fit_case(PFsrc + ":142", "too many resources fails due to highest init container memory",
+         rpod(R(1, 1), init=[R(1, 3), R(1, 2)]), [rpod(R(9, 19))], A32, False, [IM])
+fit_case(PFsrc + ":149", "init container fits because it's the max, not sum, of containers and init containers",
+         rpod(R(1, 1), init=[R(1, 1)]), [rpod(R(9, 19))], A32, True)
+fit_case(PFsrc + ":155", "multiple init containers fit because it's the max, not sum, of containers and init containers",
+         rpod(R(1, 1), init=[R(1, 1), R(1, 1)]), [rpod(R(9, 19))], A32, True)
+fit_case(PFsrc + ":161", "both resources fit", rpod(R(1, 1)), [rpod(R(5, 5))], A32, True)
+fit_case(PFsrc + ":167", "one resource memory fits", rpod(R(2, 1)), [rpod(R(9, 5))], A32, False, [IC])
+fit_case(PFsrc + ":174", "one resource cpu fits", rpod(R(1, 2)), [rpod(R(5, 19))], A32, False, [IM])
+fit_case(PFsrc + ":181", "equal edge case", rpod(R(5, 1)), [rpod(R(5, 19))], A32, True)
+fit_case(PFsrc + ":187", "equal edge case for init container", rpod(R(4, 1), init=[R(5, 1)]), [rpod(R(5, 19))], A32, True)
+fit_case(PFsrc + ":193", "extended resource fits", rpod(R(scalar={EXT_A: 1})), [rpod(R())], A32, True)
+fit_case(PFsrc + ":199", "extended resource fits for init container", rpod(R(), init=[R(scalar={EXT_A: 1})]),
+         [rpod(R())], A32, True)
+fit_case(PFsrc + ":205", "extended resource capacity enforced", rpod(R(1, 1, scalar={EXT_A: 10})),
+         [rpod(R(0, 0, scalar={EXT_A: 0}))], A32, False, ["Insufficient " + EXT_A])
+fit_case(PFsrc + ":214", "extended resource capacity enforced for init container",
+         rpod(R(), init=[R(1, 1, scalar={EXT_A: 10})]), [rpod(R(0, 0, scalar={EXT_A: 0}))], A32, False,
+         ["Insufficient " + EXT_A])
+fit_case(PFsrc + ":223", "extended resource allocatable enforced", rpod(R(1, 1, scalar={EXT_A: 1})),
+         [rpod(R(0, 0, scalar={EXT_A: 5}))], A32, False, ["Insufficient " + EXT_A])
+fit_case(PFsrc + ":232", "extended resource allocatable enforced for init container",
+         rpod(R(), init=[R(1, 1, scalar={EXT_A: 1})]), [rpod(R(0, 0, scalar={EXT_A: 5}))], A32, False,
+         ["Insufficient " + EXT_A])
+fit_case(PFsrc + ":241", "extended resource allocatable enforced for multiple containers",
+         rpod(R(1, 1, scalar={EXT_A: 3}), R(1, 1, scalar={EXT_A: 3})), [rpod(R(0, 0, scalar={EXT_A: 2}))], A32, False,
+         ["Insufficient " + EXT_A])
+fit_case(PFsrc + ":251", "extended resource allocatable admits multiple init containers",
+         rpod(R(), init=[R(1, 1, scalar={EXT_A: 3}), R(1, 1, scalar={EXT_A: 3})]), [rpod(R(0, 0, scalar={EXT_A: 2}))],
+         A32, True)
+fit_case(PFsrc + ":260", "extended resource allocatable enforced for multiple init containers",
+         rpod(R(), init=[R(1, 1, scalar={EXT_A: 6}), R(1, 1, scalar={EXT_A: 3})]), [rpod(R(0, 0, scalar={EXT_A: 2}))],
+         A32, False, ["Insufficient " + EXT_A])
+fit_case(PFsrc + ":270", "extended resource allocatable enforced for unknown resource",
+         rpod(R(1, 1, scalar={EXT_B: 1})), [rpod(R(0, 0))], A32, False, ["Insufficient " + EXT_B])
+fit_case(PFsrc + ":279", "extended resource allocatable enforced for unknown resource for init container",
+         rpod(R(), init=[R(1, 1, scalar={EXT_B: 1})]), [rpod(R(0, 0))], A32, False, ["Insufficient " + EXT_B])
+fit_case(PFsrc + ":288", "hugepages resource capacity enforced", rpod(R(1, 1, scalar={HUGE_A: 10})),
+         [rpod(R(0, 0, scalar={HUGE_A: 0}))], A32, False, ["Insufficient " + HUGE_A])
+fit_case(PFsrc + ":297", "hugepages resource capacity enforced for init container",
+         rpod(R(), init=[R(1, 1, scalar={HUGE_A: 10})]), [rpod(R(0, 0, scalar={HUGE_A: 0}))], A32, False,
+         ["Insufficient " + HUGE_A])
+fit_case(PFsrc + ":306", "hugepages resource allocatable enforced for multiple containers",
+         rpod(R(1, 1, scalar={HUGE_A: 3}), R(1, 1, scalar={HUGE_A: 3})), [rpod(R(0, 0, scalar={HUGE_A: 2}))], A32, False,
+         ["Insufficient " + HUGE_A])
+# (:316 "skip checking ignored extended resource" needs extender-managed resources: out of scope)
+A1 = alloc(10, 20, 0, 1, 0, 0, 0)
+fit_case(PFsrc + ":349", "even without specified resources predicate fails when there's no space for additional pod",
+         pod(), [rpod(R(10, 20))], A1, False, [IP])
+fit_case(PFsrc + ":356", "even if both resources fit predicate fails when there's no space for additional pod",
+         rpod(R(1, 1)), [rpod(R(5, 5))], A1, False, [IP])
+fit_case(PFsrc + ":363", "even for equal edge case predicate fails when there's no space for additional pod",
+         rpod(R(5, 1)), [rpod(R(5, 19))], A1, False, [IP])
+fit_case(PFsrc + ":370", "even for equal edge case predicate fails when there's no space for additional pod due to init container",
+         rpod(R(5, 1), init=[R(5, 1)]), [rpod(R(5, 19))], A1, False, [IP])
+fit_case(PFsrc + ":401", "due to container scratch disk", rpod(R(1, 1)), [rpod(R(10, 10))], A32, False, [IC])
+fit_case(PFsrc + ":410", "pod fit", rpod(R(1, 1)), [rpod(R(2, 10))], A32, True)
+fit_case(PFsrc + ":416", "storage ephemeral local storage request exceeds allocatable", rpod(R(eph=25)),
+         [rpod(R(2, 2))], A32, False, [IE])
+fit_case(PFsrc + ":425", "pod fits", rpod(R(eph=10)), [rpod(R(2, 2))], A32, True)
+
+
+# ------------------------------------------------ PodFitsHost
+def pred_case(pred, src, test, p, n, fits, reasons, existing=()):
+    ex = []
+    for e in existing:
+        e = json.loads(json.dumps(e))
+        e["spec"]["nodeName"] = n["metadata"].get("name", "")
+        ex.append(e)
+    add("predicates", {"source": src, "test": test, "predicate": pred, "pod": p, "node": n,
+                       "pods": ex, "fits": fits, "reasons": list(reasons) if not fits else []})
+
+
+HN = "node(s) didn't match the requested hostname"
+pred_case("HostName", PFsrc + ":478", "no host specified", pod(), node(""), True, [])
+pred_case("HostName", PFsrc + ":484", "host matches", pod(node_name="foo"), node("foo"), True, [])
+pred_case("HostName", PFsrc + ":497", "host doesn't match", pod(node_name="bar"), node("foo"), False, [HN])
+
+
+# ------------------------------------------------ PodFitsHostPorts (predicates_test.go:533-667)
+def ppod(*infos):
+    ports = []
+    for s in infos:
+        proto, ip, port = s.split("/")
+        ports.append({"hostIP": ip, "hostPort": int(port), "protocol": proto})
+    return pod(node_name="m1", containers=[{"ports": ports}])
+
+
+HP = "node(s) didn't have free ports for the requested pod ports"
+for ln, test, want, have, fits in [
+        (563, "nothing running", None, None, True),
+        (569, "other port", ["UDP/127.0.0.1/8080"], ["UDP/127.0.0.1/9090"], True),
+        (576, "same udp port", ["UDP/127.0.0.1/8080"], ["UDP/127.0.0.1/8080"], False),
+        (583, "same tcp port", ["TCP/127.0.0.1/8080"], ["TCP/127.0.0.1/8080"], False),
+        (590, "different host ip", ["TCP/127.0.0.1/8080"], ["TCP/127.0.0.2/8080"], True),
+        (597, "different protocol", ["UDP/127.0.0.1/8080"], ["TCP/127.0.0.1/8080"], True),
+        (604, "second udp port conflict", ["UDP/127.0.0.1/8000", "UDP/127.0.0.1/8080"], ["UDP/127.0.0.1/8080"], False),
+        (611, "first tcp port conflict", ["TCP/127.0.0.1/8001", "UDP/127.0.0.1/8080"],
+         ["TCP/127.0.0.1/8001", "UDP/127.0.0.1/8081"], False),
+        (618, "first tcp port conflict due to 0.0.0.0 hostIP", ["TCP/0.0.0.0/8001"], ["TCP/127.0.0.1/8001"], False),
+        (625, "TCP hostPort conflict due to 0.0.0.0 hostIP", ["TCP/10.0.10.10/8001", "TCP/0.0.0.0/8001"],
+         ["TCP/127.0.0.1/8001"], False),
+        (632, "second tcp port conflict to 0.0.0.0 hostIP", ["TCP/127.0.0.1/8001"], ["TCP/0.0.0.0/8001"], False),
+        (639, "second different protocol", ["UDP/127.0.0.1/8001"], ["TCP/0.0.0.0/8001"], True),
+        (646, "UDP hostPort conflict due to 0.0.0.0 hostIP", ["UDP/127.0.0.1/8001"],
+         ["TCP/0.0.0.0/8001", "UDP/0.0.0.0/8001"], False)]:
+    p = pod() if want is None else ppod(*want)
+    ex = [] if have is None else [ppod(*have)]
+    pred_case("PodFitsHostPorts", PFsrc + ":%d" % ln, test, p, node("m1"), fits, [HP], ex)
+
+# ------------------------------------------------ PodMatchNodeSelector (predicates_test.go:894-1391)
+NS = "node(s) didn't match node selector"
+
+
+def req_aff(terms):
+    return {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {"nodeSelectorTerms": terms}}}
+
+
+def term(*exprs):
+    return {"matchExpressions": list(exprs)}
+
+
+for ln, test, p, labels, fits in [
+        (901, "no selector", pod(), None, True),
+        (906, "missing labels", pod(nodeSelector={"foo": "bar"}), None, False),
+        (916, "same labels", pod(nodeSelector={"foo": "bar"}), {"foo": "bar"}, True),
+        (929, "node labels are superset", pod(nodeSelector={"foo": "bar"}), {"foo": "bar", "baz": "blah"}, True),
+        (943, "node labels are subset", pod(nodeSelector={"foo": "bar", "baz": "blah"}), {"foo": "bar"}, False),
+        (957, "Pod with matchExpressions using In operator that matches the existing node",
+         pod(affinity=req_aff([term(expr("foo", "In", ["bar", "value2"]))])), {"foo": "bar"}, True),
+        (984, "Pod with matchExpressions using Gt operator that matches the existing node",
+         pod(affinity=req_aff([term(expr("kernel-version", "Gt", ["0204"]))])), {"kernel-version": "0206"}, True),
+        (1012, "Pod with matchExpressions using NotIn operator that matches the existing node",
+         pod(affinity=req_aff([term(expr("mem-type", "NotIn", ["DDR", "DDR2"]))])), {"mem-type": "DDR3"}, True),
+        (1039, "Pod with matchExpressions using Exists operator that matches the existing node",
+         pod(affinity=req_aff([term(expr("GPU", "Exists"))])), {"GPU": "NVIDIA-GRID-K1"}, True),
+        (1065, "Pod with affinity that don't match node's labels won't schedule onto the node",
+         pod(affinity=req_aff([term(expr("foo", "In", ["value1", "value2"]))])), {"foo": "bar"}, False),
+        (1092, "Pod with a nil []NodeSelectorTerm in affinity, can't match the node's labels and won't schedule onto the node",
+         pod(affinity=req_aff(None)), {"foo": "bar"}, False),
+        (1110, "Pod with an empty []NodeSelectorTerm in affinity, can't match the node's labels and won't schedule onto the node",
+         pod(affinity=req_aff([])), {"foo": "bar"}, False),
+        (1128, "Pod with empty MatchExpressions is not a valid value will match no objects and won't schedule onto the node",
+         pod(affinity=req_aff([term()])), {"foo": "bar"}, False),
+        (1146, "Pod with no Affinity will schedule onto a node", pod(), {"foo": "bar"}, True),
+        (1153, "Pod with Affinity but nil NodeSelector will schedule onto a node",
+         pod(affinity={"nodeAffinity": {}}), {"foo": "bar"}, True),
+        (1169, "Pod with multiple matchExpressions ANDed that matches the existing node",
+         pod(affinity=req_aff([term(expr("GPU", "Exists"), expr("GPU", "NotIn", ["AMD", "INTER"]))])),
+         {"GPU": "NVIDIA-GRID-K1"}, True),
+        (1200, "Pod with multiple matchExpressions ANDed that doesn't match the existing node",
+         pod(affinity=req_aff([term(expr("GPU", "Exists"), expr("GPU", "In", ["AMD", "INTER"]))])),
+         {"GPU": "NVIDIA-GRID-K1"}, False),
+        (1231, "Pod with multiple NodeSelectorTerms ORed in affinity, matches the node's labels and will schedule onto the node",
+         pod(affinity=req_aff([term(expr("foo", "In", ["bar", "value2"])), term(expr("diffkey", "In", ["wrong", "value2"]))])),
+         {"foo": "bar"}, True),
+        (1269, "Pod with an Affinity and a PodSpec.NodeSelector(the old thing that we are deprecating) both are satisfied, will schedule onto the node",
+         pod(nodeSelector={"foo": "bar"}, affinity=req_aff([term(expr("foo", "Exists"))])), {"foo": "bar"}, True),
+        (1300, "Pod with an Affinity matches node's labels but the PodSpec.NodeSelector(the old thing that we are deprecating) is not satisfied, won't schedule onto the node",
+         pod(nodeSelector={"foo": "bar"}, affinity=req_aff([term(expr("foo", "Exists"))])), {"foo": "barrrrrr"}, False),
+        (1331, "Pod with an invalid value in Affinity term won't be scheduled onto the node",
+         pod(affinity=req_aff([term(expr("foo", "NotIn", ["invalid value: ___@#$%^"]))])), {"foo": "bar"}, False)]:
+    if p["spec"].get("affinity", {}).get("nodeAffinity", {}).get("requiredDuringSchedulingIgnoredDuringExecution", {}) \
+            and p["spec"]["affinity"]["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"].get("nodeSelectorTerms", 0) is None:
+        p["spec"]["affinity"]["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"] = {}
+    pred_case("MatchNodeSelector", PFsrc + ":%d" % ln, test, p, node("", labels=labels), fits, [NS])
+
+# ------------------------------------------------ PodToleratesNodeTaints (predicates_test.go:3221-3422)
+TX = "node(s) had taints that the pod didn't tolerate"
+for ln, test, tols, taints, fits in [
+        (3229, "a pod having no tolerations can't be scheduled onto a node with nonempty taints", None,
+         [taint("dedicated", "user1", "NoSchedule")], False),
+        (3243, "a pod which can be scheduled on a dedicated node assigned to user1 with effect NoSchedule",
+         [{"key": "dedicated", "value": "user1", "effect": "NoSchedule"}], [taint("dedicated", "user1", "NoSchedule")], True),
+        (3260, "a pod which can't be scheduled on a dedicated node assigned to user2 with effect NoSchedule",
+         [tol("dedicated", "Equal", "user2", "NoSchedule")], [taint("dedicated", "user1", "NoSchedule")], False),
+        (3277, "a pod can be scheduled onto the node, with a toleration uses operator Exists that tolerates the taints on the node",
+         [{"key": "foo", "operator": "Exists", "effect": "NoSchedule"}], [taint("foo", "bar", "NoSchedule")], True),
+        (3294, "a pod has multiple tolerations, node has multiple taints, all the taints are tolerated, pod can be scheduled onto the node",
+         [tol("dedicated", "Equal", "user2", "NoSchedule"), {"key": "foo", "operator": "Exists", "effect": "NoSchedule"}],
+         [taint("dedicated", "user2", "NoSchedule"), taint("foo", "bar", "NoSchedule")], True),
+        (3317, "a pod has a toleration that keys and values match the taint on the node, but (non-empty) effect doesn't match, can't be scheduled onto the node",
+         [tol("foo", "Equal", "bar", "PreferNoSchedule")], [taint("foo", "bar", "NoSchedule")], False),
+        (3337, "The pod has a toleration that keys and values match the taint on the node, the effect of toleration is empty, and the effect of taint is NoSchedule. Pod can be scheduled onto the node",
+         [tol("foo", "Equal", "bar", None)], [taint("foo", "bar", "NoSchedule")], True),
+        (3357, "The pod has a toleration that key and value don't match the taint on the node, but the effect of taint on node is PreferNochedule. Pod can be scheduled onto the node",
+         [tol("dedicated", "Equal", "user2", "NoSchedule")], [taint("dedicated", "user1", "PreferNoSchedule")], True),
+        (3377, "The pod has no toleration, but the effect of taint on node is PreferNochedule. Pod can be scheduled onto the node",
+         None, [taint("dedicated", "user1", "PreferNoSchedule")], True)]:
+    p = pod(containers=[{"image": "img"}]) if tols is None else pod(containers=[{"image": "img"}], tolerations=tols)
+    pred_case("PodToleratesNodeTaints", PFsrc + ":%d" % ln, test, p, node("", taints=taints), fits, [TX])
+
+# ------------------------------------------------ memory / disk pressure (predicates_test.go:3428-3602)
+be_pod = pod(containers=[{"name": "container", "image": "image", "resources": {}}])
+nbe_pod = pod(containers=[{"name": "container", "image": "image",
+                           "resources": {"requests": alloc(100, 100, 100, 100, 0, 0, 0)}}])
+MP, DP = "node(s) had memory pressure", "node(s) had disk pressure"
+no_mp = node("", conditions=[("Ready", "True")])
+mp = node("", conditions=[("MemoryPressure", "True")])
+for ln, test, p, n, fits in [
+        (3479, "best-effort pod schedulable on node without memory pressure condition on", be_pod, no_mp, True),
+        (3485, "best-effort pod not schedulable on node with memory pressure condition on", be_pod, mp, False),
+        (3491, "non best-effort pod schedulable on node with memory pressure condition on", nbe_pod, mp, True),
+        (3497, "non best-effort pod schedulable on node without memory pressure condition on", nbe_pod, no_mp, True)]:
+    pred_case("CheckNodeMemoryPressure", PFsrc + ":%d" % ln, test, p, n, fits, [MP])
+dp = node("", conditions=[("DiskPressure", "True")])
+no_dp = node("", conditions=[("Ready", "True")])
+simple = pod(containers=[{"name": "container", "image": "image", "imagePullPolicy": "Always"}])
+pred_case("CheckNodeDiskPressure", PFsrc + ":3574", "pod schedulable on node without pressure condition on", simple, no_dp, True, [DP])
+pred_case("CheckNodeDiskPressure", PFsrc + ":3580", "pod not schedulable on node with pressure condition on", simple, dp, False, [DP])
+
+# ------------------------------------------------ CheckNodeCondition (predicates_test.go:3604-3676)
+for i, (conds, unsched, ok) in enumerate([
+        ([("Ready", "True")], None, True), ([("Ready", "False")], None, False), ([("OutOfDisk", "True")], None, False),
+        ([("OutOfDisk", "False")], None, True), ([("Ready", "True"), ("OutOfDisk", "True")], None, False),
+        ([("Ready", "True"), ("OutOfDisk", "False")], None, True), ([("Ready", "False"), ("OutOfDisk", "True")], None, False),
+        ([("Ready", "False"), ("OutOfDisk", "False")], None, False), (None, True, False), (None, False, True),
+        (None, None, True)]):
+    n = node("node%d" % (i + 1), conditions=conds, unschedulable=unsched)
+    add("predicates", {"source": PFsrc + ":%d" % (3611 + 5 * i), "test": "node%d" % (i + 1),
+                       "predicate": "CheckNodeCondition", "pod": pod(), "node": n, "pods": [], "fits": ok,
+                       "reasons": None})
+
+# ------------------------------------------------ NodeInfo.AddPod (schedulercache/node_info_test.go:449-600)
+ni_pods = [pod(name="test-1", node_name="test-node", containers=[
+    {"resources": {"requests": {"cpu": "100m", "memory": "500"}},
+     "ports": [{"hostIP": "127.0.0.1", "hostPort": 80, "protocol": "TCP"}]}]),
+    pod(name="test-2", node_name="test-node", containers=[
+        {"resources": {"requests": {"cpu": "200m", "memory": "1Ki"}},
+         "ports": [{"hostIP": "127.0.0.1", "hostPort": 8080, "protocol": "TCP"}]}])]
+add("node_info", {"source": S + "schedulercache/node_info_test.go:449", "test": "TestNodeInfoAddPod",
+                  "node": node("test-node"), "pods": ni_pods,
+                  "expect": {"requested_cpu": 300, "requested_mem": 1524, "nonzero_cpu": 300, "nonzero_mem": 1524,
+                             "pod_count": 2,
+                             "used_ports": [["127.0.0.1", "TCP", 80], ["127.0.0.1", "TCP", 8080]]}})
+
+# ------------------------------------------------ TestZeroRequest (core/generic_scheduler_test.go:534-660)
+DM, DC = 200 * 1024 * 1024, 100
+zr_none = {"containers": [{}]}
+
+
+def zpod(spec, nn=None):
+    p = {"metadata": {}, "spec": json.loads(json.dumps(spec))}
+    if nn:
+        p["spec"]["nodeName"] = nn
+    return p
+
+
+small = {"containers": [ctr("%dm" % DC, "%d" % DM)]}
+large = {"containers": [ctr("%dm" % (DC * 3), "%d" % (DM * 3))]}
+zr_nodes = [node("machine1", 1000, DM * 10, pods=100), node("machine2", 1000, DM * 10, pods=100)]
+zr_pods = [zpod(large, "machine1"), zpod(zr_none, "machine1"), zpod(large, "machine2"), zpod(small, "machine2")]
+ZRsrc = S + "core/generic_scheduler_test.go"
+for ln, test, p, eq in [
+        (577, "test priority of zero-request pod with machine with zero-request pod", zpod(zr_none), True),
+        (587, "test priority of nonzero-request pod with machine with zero-request pod", zpod(small), True),
+        (598, "test priority of larger pod with machine with zero-request pod", zpod(large), False)]:
+    add("prioritize", {"source": ZRsrc + ":%d" % ln, "test": test, "pod": p, "nodes": zr_nodes, "pods": zr_pods,
+                       "configs": [["LeastRequestedPriority", 1], ["BalancedResourceAllocation", 1],
+                                   ["SelectorSpreadPriority", 1]],
+                       "expect_all_equal" if eq else "expect_none_equal": 25})
+
+# ------------------------------------------------ TestSelectHost (core/generic_scheduler_test.go:121-185)
+for ln, lst, possible in [
+        (129, [["machine1.1", 1], ["machine2.1", 2]], ["machine2.1"]),
+        (137, [["machine1.1", 1], ["machine1.2", 2], ["machine1.3", 2], ["machine2.1", 2]],
+         ["machine1.2", "machine1.3", "machine2.1"]),
+        (147, [["machine1.1", 3], ["machine1.2", 3], ["machine2.1", 2], ["machine3.1", 1], ["machine1.3", 3]],
+         ["machine1.1", "machine1.2", "machine1.3"])]:
+    add("select_host", {"source": ZRsrc + ":%d" % ln, "list": lst, "possible": possible, "calls": 10})
+
+# ------------------------------------------------ TestHumanReadableFitError (core/generic_scheduler_test.go:508-523)
+add("fit_error", {"source": ZRsrc + ":508", "num_nodes": 3,
+                  "failed": {"1": ["node(s) had memory pressure"], "2": ["node(s) had disk pressure"],
+                             "3": ["node(s) had disk pressure"]},
+                  "contains": ["0/3 nodes are available", "2 node(s) had disk pressure", "1 node(s) had memory pressure"]})
+
+# ------------------------------------------------ Quantity → int64 (AM/pkg/api/resource/quantity.go:695-713;
+# expected values follow the documented ceil semantics and the fixtures the scheduler tests rely on)
+for s, milli, val in [("1", 1000, 1), ("100m", 100, 1), ("1000m", 1000, 1), ("2000", 2000000, 2000),
+                      ("1Ki", 1024000, 1024), ("128Mi", 134217728000, 134217728), ("1Gi", 1073741824000, 1073741824),
+                      ("0.1", 100, 1), ("1.5", 1500, 2), ("0", 0, 0), ("1e3", 1000000, 1000), ("1k", 1000000, 1000),
+                      ("0.0001", 1, 1), ("250m", 250, 1), ("209715200", 209715200000, 209715200)]:
+    add("quantity", {"source": "vendor/k8s.io/apimachinery/pkg/api/resource/quantity.go:695", "q": s,
+                     "milli": milli, "value": val})
+
+if __name__ == "__main__":
+    for group, lst in cases.items():
+        with open(os.path.join(HERE, group + ".json"), "w") as f:
+            json.dump(lst, f, indent=1, sort_keys=True)
+        print(group, len(lst))
