@@ -1,0 +1,261 @@
+/*
+ * ksim.h — C-ABI of the MI355X-native per-pod scheduling cycle (libksim.so).
+ *
+ * Drop-in boundary for the vendored kube-scheduler v1.10 hot path that
+ * xiaoxubeii/kubernetes-schedule-simulator drives.  The reference interface being
+ * replaced is algorithm.ScheduleAlgorithm
+ *   (vendor/k8s.io/kubernetes/pkg/scheduler/algorithm/scheduler_interface.go:52-65),
+ * installed as scheduler.Config.Algorithm (pkg/scheduler/scheduler.go:109) and built by
+ * CreateFromKeys (pkg/scheduler/factory/factory.go:1021-1060) from predicate/priority key
+ * sets.  Everything is plain C: fixed-width integers, caller-owned buffers copied in,
+ * results written to caller-provided arrays; no pointer is retained past a call (cgo rule).
+ * Status: 0 = KSIM_OK, negative = KSIM_E_*, message via ksim_last_error().
+ *
+ * Node order: every node table is in ascending BYTEWISE name order (Go string <), so a
+ * node index is its name rank; selectHost's (score, host) descending sort
+ * (core/generic_scheduler.go:183-198, api/types.go:272-277) becomes "largest index first"
+ * among the max-score nodes.
+ */
+#ifndef KSIM_H
+#define KSIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KSIM_ABI_VERSION 1
+
+/* ---- status codes ---- */
+#define KSIM_OK 0
+#define KSIM_E_INVAL (-1)       /* bad argument / shape */
+#define KSIM_E_DEVICE (-2)      /* HIP runtime error */
+#define KSIM_E_NOMEM (-3)       /* device allocation failed */
+#define KSIM_E_UNSUPPORTED (-4) /* configuration outside the supported key set */
+#define KSIM_E_STATE (-5)       /* call order (e.g. schedule before load) */
+#define KSIM_E_OVERFLOW (-6)    /* a node's host-port slots overflowed on commit */
+
+#define KSIM_MAX_SCALAR 8   /* extended / hugepage resource columns */
+#define KSIM_MAX_RCLASS 16  /* reduce classes per pod (TaintToleration x NodeAffinity) */
+#define KSIM_NREASONS 24    /* failure-reason histogram slots */
+
+/* ---- predicate key bits: the FitPredicate keys of predicates.go:129-138 that carry
+ *      logic for supported pods.  The volume / inter-pod-affinity keys (NoDiskConflict,
+ *      MaxEBS/GCEPD/AzureDiskVolumeCount, CheckVolumeBinding, NoVolumeZoneConflict,
+ *      MatchInterPodAffinity) are true for pods without volumes or affinity terms and
+ *      need no bit: the host rejects pods that would make them non-trivial. ---- */
+#define KSIM_P_CHECK_NODE_CONDITION (1u << 0)     /* predicates.go:1534 */
+#define KSIM_P_CHECK_NODE_UNSCHEDULABLE (1u << 1) /* CheckNodeUnschedulablePredicate */
+#define KSIM_P_GENERAL (1u << 2)                  /* predicates.go:1059 */
+#define KSIM_P_HOSTNAME (1u << 3)                 /* predicates.go:853 */
+#define KSIM_P_HOST_PORTS (1u << 4)               /* predicates.go:1019 */
+#define KSIM_P_NODE_SELECTOR (1u << 5)            /* predicates.go:841 */
+#define KSIM_P_RESOURCES (1u << 6)                /* predicates.go:706 */
+#define KSIM_P_TAINTS (1u << 7)                   /* predicates.go:1465 */
+#define KSIM_P_NOEXEC_TAINTS (1u << 8)            /* PodToleratesNodeNoExecuteTaints */
+#define KSIM_P_MEM_PRESSURE (1u << 9)             /* predicates.go:1502 */
+#define KSIM_P_DISK_PRESSURE (1u << 10)           /* predicates.go:1524 */
+
+/* ---- priority weight slots (0 = not configured).  Priorities that evaluate to the
+ *      same value on every node under supported inputs (SelectorSpread /
+ *      ServiceSpreading with no selectors, NodePreferAvoidPods for pods without an
+ *      RC/RS owner, InterPodAffinity without affinity terms, EqualPriority) do not
+ *      change placements; their sum goes in ksim_config.const_score. ---- */
+#define KSIM_W_LEAST_REQUESTED 0     /* least_requested.go:36 */
+#define KSIM_W_MOST_REQUESTED 1      /* most_requested.go:34 */
+#define KSIM_W_BALANCED 2            /* balanced_resource_allocation.go:39 */
+#define KSIM_W_TAINT_TOLERATION 3    /* taint_toleration.go:55 + NormalizeReduce(10,true) */
+#define KSIM_W_NODE_AFFINITY 4       /* node_affinity.go:34 + NormalizeReduce(10,false) */
+#define KSIM_NW 5
+
+/* ---- node condition / dynamic flags (ksim_node_table.flags) ---- */
+#define KSIM_N_NOT_READY (1u << 0)      /* Ready condition present, status != True */
+#define KSIM_N_OUT_OF_DISK (1u << 1)    /* OutOfDisk present, status != False */
+#define KSIM_N_NET_UNAVAIL (1u << 2)    /* NetworkUnavailable present, != False */
+#define KSIM_N_UNSCHEDULABLE (1u << 3)  /* spec.unschedulable */
+#define KSIM_N_MEM_PRESSURE (1u << 4)   /* MemoryPressure == True */
+#define KSIM_N_DISK_PRESSURE (1u << 5)  /* DiskPressure == True */
+#define KSIM_N_GPU_OVER (1u << 8)       /* alloc.gpu < requested.gpu  (maintained by the library) */
+#define KSIM_N_EPH_OVER (1u << 9)       /* alloc.eph < requested.eph  (maintained by the library) */
+
+/* ---- pod flags (ksim_pod.flags) ---- */
+#define KSIM_POD_ANY_REQUEST (1u << 0)  /* PodFitsResources does the resource checks (:731-736) */
+#define KSIM_POD_BEST_EFFORT (1u << 1)  /* qos.go:39 BestEffort */
+#define KSIM_POD_NEED_SELECTOR (1u << 2)/* nodeSelector/required affinity not matching every label set */
+#define KSIM_POD_NEED_TAINTS (1u << 3)  /* some taint set is not tolerated */
+
+/* ---- failure reasons: bit r of a node's reason mask / slot r of a histogram ---- */
+#define KSIM_R_NOT_READY 0
+#define KSIM_R_OUT_OF_DISK 1
+#define KSIM_R_NET_UNAVAIL 2
+#define KSIM_R_UNSCHEDULABLE 3
+#define KSIM_R_INSUFFICIENT_PODS 4
+#define KSIM_R_INSUFFICIENT_CPU 5
+#define KSIM_R_INSUFFICIENT_MEMORY 6
+#define KSIM_R_INSUFFICIENT_GPU 7
+#define KSIM_R_INSUFFICIENT_EPHEMERAL 8
+#define KSIM_R_HOSTNAME 9
+#define KSIM_R_HOST_PORTS 10
+#define KSIM_R_NODE_SELECTOR 11
+#define KSIM_R_TAINTS 12
+#define KSIM_R_MEM_PRESSURE 13
+#define KSIM_R_DISK_PRESSURE 14
+#define KSIM_R_INSUFFICIENT_SCALAR0 16 /* +column, up to KSIM_MAX_SCALAR */
+
+/* ---- execution modes ---- */
+#define KSIM_MODE_AUTO 0        /* library picks (persistent when it fits) */
+#define KSIM_MODE_LAUNCH 1      /* one scan launch per pod, replayed from a hipGraph */
+#define KSIM_MODE_PERSISTENT 2  /* one persistent launch walks the whole pod queue */
+
+typedef struct {
+  int32_t device;                 /* HIP device ordinal */
+  int32_t mode;                   /* KSIM_MODE_* */
+  uint32_t predicates;            /* KSIM_P_* bits of the configured key set */
+  int64_t weights[KSIM_NW];       /* PriorityConfig.Weight per slot (Go int) */
+  int32_t no_priorities;          /* 1: empty prioritizer list -> EqualPriorityMap */
+  int32_t collect_reasons;        /* 1: fill failure histograms for unschedulable pods */
+  int64_t const_score;            /* sum of constant-valued priorities (reporting only) */
+  uint64_t last_node_index;       /* initial genericScheduler.lastNodeIndex */
+} ksim_config;
+
+/* Node table in name-rank order.  Column arrays have n_nodes entries; scalar columns are
+ * [n_scalar][n_nodes]; ports are slot-major [port_slots][n_nodes] with 0 = empty. */
+typedef struct {
+  int64_t n_nodes;
+  int32_t n_scalar;
+  int32_t port_slots;
+  /* static (NodeInfo.SetNode, node_info.go:429-448) */
+  const int64_t* alloc_cpu;   /* milli */
+  const int64_t* alloc_mem;
+  const int64_t* alloc_gpu;
+  const int64_t* alloc_eph;
+  const int32_t* allowed_pods;
+  const uint32_t* flags;      /* KSIM_N_* condition bits (the library derives _OVER bits) */
+  const int32_t* label_set;   /* interned label-set id */
+  const int32_t* taint_set;   /* interned taint-set id */
+  const int64_t* alloc_scalar;
+  /* dynamic (NodeInfo.AddPod, node_info.go:318-341) — state from already running pods */
+  const int64_t* req_cpu;
+  const int64_t* req_mem;
+  const int64_t* req_gpu;
+  const int64_t* req_eph;
+  const int64_t* nz_cpu;
+  const int64_t* nz_mem;
+  const int32_t* pod_count;
+  const int64_t* req_scalar;
+  const uint64_t* ports;      /* KSIM_PORT_KEY(ip_id, proto_id, port) */
+  const int32_t* port_count;
+} ksim_node_table;
+
+#define KSIM_PORT_KEY(ip, proto, port) \
+  ((((uint64_t)(ip)) << 40) | (((uint64_t)(proto)) << 32) | (uint64_t)(uint32_t)(port))
+
+/* Per pod-class tables (pods with identical specs share a class).  Bit tables are
+ * [n_classes][words] with words = ceil(n_sets/32); byte tables are [n_classes][n_sets]. */
+typedef struct {
+  int32_t n_classes;
+  int32_t n_label_sets;
+  int32_t n_taint_sets;
+  const uint32_t* sel_ok;      /* podMatchesNodeLabels per label set (predicates.go:795) */
+  const uint32_t* taint_ok;    /* NoSchedule+NoExecute tolerated per taint set (:1465) */
+  const uint32_t* noexec_ok;   /* NoExecute tolerated per taint set */
+  const uint8_t* tt_class;     /* reduce class of each taint set (intolerable PreferNoSchedule count) */
+  const uint8_t* na_class;     /* reduce class of each label set (preferred node-affinity weight) */
+  const int32_t* n_tt;         /* [n_classes] number of TaintToleration classes K1 */
+  const int32_t* n_na;         /* [n_classes] number of NodeAffinity classes K2 (K1*K2 <= 16) */
+  const int64_t* tt_val;       /* [n_classes][KSIM_MAX_RCLASS] map value of each class */
+  const int64_t* na_val;       /* [n_classes][KSIM_MAX_RCLASS] */
+} ksim_class_tables;
+
+/* Pod descriptor, 128 bytes.  The three request vectors follow the reference exactly:
+ * req_* = GetResourceRequest (predicates.go:659-697, init containers max'd in),
+ * add_* = calculateResource (node_info.go:400-412, containers only),
+ * nz_*  = non-zero requests (priorities/util/non_zero.go:38-53). */
+typedef struct {
+  int64_t req_cpu, req_mem, req_gpu, req_eph;
+  int64_t add_cpu, add_mem, add_gpu, add_eph;
+  int64_t nz_cpu, nz_mem;
+  int32_t cls;         /* pod class */
+  int32_t host;        /* spec.nodeName: -1 none, >=0 node index, -2 names no node */
+  uint32_t flags;      /* KSIM_POD_* */
+  int32_t port_off;    /* into the pod-port array */
+  int32_t port_cnt;
+  int32_t scalar_off;  /* into the scalar-request array */
+  int32_t scalar_cnt;
+  int32_t reserved[5];
+} ksim_pod;
+
+typedef struct {
+  int32_t col;     /* scalar column */
+  int32_t pad;
+  int64_t req;     /* predicate request */
+  int64_t add;     /* commit delta */
+} ksim_scalar_req;
+
+typedef struct {
+  int64_t pods;            /* pods processed by the call */
+  int64_t scheduled;       /* pods bound */
+  int64_t node_evals;      /* sum over pods of nodes scanned */
+  double device_ms;        /* HIP-event time of the call's device work */
+  double kernel_ms;        /* HIP-event time of the dominant (scan) kernel(s) */
+  int64_t kernel_launches; /* launches of the dominant kernel */
+  int32_t mode;            /* mode actually used */
+  int32_t blocks;          /* grid size of the dominant kernel */
+} ksim_stats;
+
+/* Dynamic node columns read back by ksim_read_nodes (caller-provided arrays or NULL). */
+typedef struct {
+  int64_t* req_cpu;
+  int64_t* req_mem;
+  int64_t* req_gpu;
+  int64_t* req_eph;
+  int64_t* nz_cpu;
+  int64_t* nz_mem;
+  int32_t* pod_count;
+  int64_t* req_scalar;   /* [n_scalar][n_nodes] */
+  uint64_t* ports;       /* [port_slots][n_nodes] */
+  int32_t* port_count;
+} ksim_node_state;
+
+typedef struct ksim_handle ksim_handle;
+
+int ksim_abi_version(void);
+const char* ksim_last_error(const ksim_handle* h);   /* h may be NULL (global error) */
+
+/* Create a handle bound to cfg->device; replaces algorithm.ScheduleAlgorithm construction
+ * (core/generic_scheduler.go:1088 NewGenericScheduler). */
+int ksim_create(const ksim_config* cfg, ksim_handle** out);
+void ksim_destroy(ksim_handle* h);
+
+/* Snapshot ingest: the node cache (schedulercache UpdateNodeNameToInfoMap, cache.go:83). */
+int ksim_load_nodes(ksim_handle* h, const ksim_node_table* nodes);
+int ksim_load_classes(ksim_handle* h, const ksim_class_tables* classes);
+/* Pod queue in scheduling order (the simulator's LIFO PodQueue.Pop order, store.go:223). */
+int ksim_load_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const uint64_t* ports,
+                   int64_t n_ports, const ksim_scalar_req* scalars, int64_t n_scalars);
+
+/* Schedule pods [first, first+count) of the loaded queue in order, committing each
+ * placement (Scheduler.assume → NodeInfo.AddPod) before the next pod.  out_node[i] is the
+ * node index or -1 (FitError).  out_reasons (optional, [count][KSIM_NREASONS]) receives the
+ * FitError reason histogram of unschedulable pods (generic_scheduler.go:72-90). */
+int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_node,
+                  int32_t* out_reasons, ksim_stats* stats);
+
+/* Evaluate one loaded pod against the current node state without committing and without
+ * touching lastNodeIndex: per-node fit, reason mask (first failing predicate in
+ * predicatesOrdering), map score and reduce class. */
+int ksim_evaluate(ksim_handle* h, int64_t pod, uint8_t* out_fit, uint32_t* out_reasons,
+                  int64_t* out_score, uint8_t* out_rclass);
+
+/* Commit one loaded pod to a node (Scheduler.assume / cache.AssumePod). */
+int ksim_assume(ksim_handle* h, int64_t pod, int64_t node);
+
+int ksim_read_nodes(ksim_handle* h, ksim_node_state* out);
+int ksim_get_counter(ksim_handle* h, uint64_t* out);
+int ksim_set_counter(ksim_handle* h, uint64_t value);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KSIM_H */

@@ -1,0 +1,308 @@
+// ksim_common.h — device-side data layout and the per-node predicate/priority evaluation
+// shared by the launch-mode and persistent kernels (gfx950 / CDNA4, wave64).
+//
+// One node per lane.  Everything a resource-only pod reads per node is the 60-byte
+// "row": alloc cpu/mem, requested cpu/mem, non-zero requested cpu/mem (6 x i64),
+// allowed pods + pod count (2 x i32) and the flags word (u32) that carries both the
+// static condition bits and the library-maintained "gpu/ephemeral already
+// over-committed" bits, so pods that request no gpu/ephemeral storage never read those
+// columns (PodFitsResources compares alloc < podReq + requested even for a zero
+// request, predicates.go:739-751).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/ksim.h"
+
+#define KSIM_BLOCK 256
+#define KSIM_WAVES (KSIM_BLOCK / 64)
+
+// predicate reasons that are copied straight from the node condition bits
+#define KSIM_COND_REASON_MASK (KSIM_N_NOT_READY | KSIM_N_OUT_OF_DISK | KSIM_N_NET_UNAVAIL | KSIM_N_UNSCHEDULABLE)
+
+struct __attribute__((aligned(16))) KsimPartial {
+  int64_t mx[KSIM_MAX_RCLASS];   // max map score among fit nodes of each reduce class
+  int32_t cnt[KSIM_MAX_RCLASS];  // nodes at that max
+  int32_t fit;                   // fit nodes in the block
+  int32_t pad[3];
+  int32_t hist[KSIM_NREASONS];   // failure reasons (only when collecting)
+};
+
+struct KsimCtx {
+  // ---- node table (name-rank order) ----
+  int64_t n;
+  const int64_t* __restrict__ alloc_cpu;
+  const int64_t* __restrict__ alloc_mem;
+  const int64_t* __restrict__ alloc_gpu;
+  const int64_t* __restrict__ alloc_eph;
+  const int32_t* __restrict__ allowed_pods;
+  uint32_t* flags;
+  const int32_t* __restrict__ label_set;
+  const int32_t* __restrict__ taint_set;
+  const int64_t* __restrict__ alloc_scalar;
+  int64_t* req_cpu;
+  int64_t* req_mem;
+  int64_t* req_gpu;
+  int64_t* req_eph;
+  int64_t* nz_cpu;
+  int64_t* nz_mem;
+  int32_t* pod_count;
+  int64_t* req_scalar;
+  uint64_t* ports;       // slot-major [port_slots][n]
+  int32_t* port_count;
+  int32_t port_slots;
+  int32_t n_scalar;
+  // ---- pod-class tables ----
+  const uint32_t* __restrict__ sel_ok;
+  const uint32_t* __restrict__ taint_ok;
+  const uint32_t* __restrict__ noexec_ok;
+  const uint8_t* __restrict__ tt_class;
+  const uint8_t* __restrict__ na_class;
+  const int32_t* __restrict__ n_tt;
+  const int32_t* __restrict__ n_na;
+  const int64_t* __restrict__ tt_val;
+  const int64_t* __restrict__ na_val;
+  int32_t lwords, twords, n_label_sets, n_taint_sets;
+  // ---- pod queue ----
+  const ksim_pod* __restrict__ pods;
+  const uint64_t* __restrict__ pod_ports;
+  const ksim_scalar_req* __restrict__ pod_scalars;
+  // ---- configuration ----
+  uint32_t preds;
+  int32_t no_prio;
+  int32_t collect;
+  int32_t pad0;
+  int64_t w[KSIM_NW];
+  // ---- run state ----
+  int64_t* cursor;        // next pod to schedule (device)
+  int64_t first, end;     // [first, end) of this call
+  uint64_t* counter;      // genericScheduler.lastNodeIndex
+  uint32_t* ticket;       // last-block arrival counter
+  KsimPartial* partials;  // [grid]
+  int32_t* out_node;      // [end-first]
+  int32_t* out_reasons;   // [end-first][KSIM_NREASONS]
+  int32_t* err;           // sticky error word
+  int64_t chunk;          // nodes per block
+};
+
+// ((a*10)/b) with Go int64 semantics (wrapping multiply, truncating divide), b > 0.
+// Quotients here are 0..10, so for a < 2^49 a correctly rounded double divide plus one
+// integer correction is exact; larger values take the native (slow) 64-bit divide.
+__device__ __forceinline__ int64_t ksim_mul10_div(int64_t a, int64_t b) {
+  if (a >= 0 && a < (int64_t(1) << 49) && b > 0) {
+    const int64_t x = a * 10;
+    int64_t q = (int64_t)((double)x / (double)b);
+    if (q * b > x) q -= 1;
+    else if ((q + 1) * b <= x) q += 1;
+    return q;
+  }
+  const int64_t x = (int64_t)((uint64_t)a * 10ull);
+  return x / b;
+}
+
+// least_requested.go:44-53
+__device__ __forceinline__ int64_t ksim_least(int64_t req, int64_t cap) {
+  if (cap == 0 || req > cap) return 0;
+  return ksim_mul10_div(cap - req, cap);
+}
+// most_requested.go:45-55
+__device__ __forceinline__ int64_t ksim_most(int64_t req, int64_t cap) {
+  if (cap == 0 || req > cap) return 0;
+  return ksim_mul10_div(req, cap);
+}
+// balanced_resource_allocation.go:39-61 — IEEE f64, compiled with -ffp-contract=off
+__device__ __forceinline__ int64_t ksim_balanced(int64_t rc, int64_t cc, int64_t rm, int64_t cm) {
+  const double fc = cc == 0 ? 1.0 : (double)rc / (double)cc;
+  const double fm = cm == 0 ? 1.0 : (double)rm / (double)cm;
+  if (fc >= 1.0 || fm >= 1.0) return 0;
+  const double diff = fabs(fc - fm);
+  return (int64_t)((1.0 - diff) * 10.0);
+}
+
+__device__ __forceinline__ bool ksim_bit(const uint32_t* tab, int64_t row, int32_t words, int32_t idx) {
+  return (tab[row * words + (idx >> 5)] >> (idx & 31)) & 1u;
+}
+
+// HostPortInfo.CheckConflict (pkg/scheduler/util/utils.go:101-130) against one node.
+__device__ __forceinline__ bool ksim_port_conflict(const KsimCtx& c, int64_t i, uint64_t want) {
+  const int32_t cnt = c.port_count[i];
+  const uint32_t wip = (uint32_t)(want >> 40);
+  const uint64_t wpp = want & 0xFFFFFFFFFFull;  // proto + port
+  for (int32_t s = 0; s < cnt; ++s) {
+    const uint64_t e = c.ports[(int64_t)s * c.n + i];
+    if ((e & 0xFFFFFFFFFFull) != wpp) continue;
+    const uint32_t eip = (uint32_t)(e >> 40);
+    if (wip == 0 || eip == 0 || eip == wip) return true;
+  }
+  return false;
+}
+
+// One node's row, loaded up front so the loads issue together.
+struct KsimRow {
+  int64_t ac, am, rc, rm, zc, zm;
+  int32_t allowed, count;
+  uint32_t fl;
+};
+
+__device__ __forceinline__ KsimRow ksim_load_row(const KsimCtx& c, int64_t i) {
+  KsimRow r;
+  r.ac = c.alloc_cpu[i];
+  r.am = c.alloc_mem[i];
+  r.rc = c.req_cpu[i];
+  r.rm = c.req_mem[i];
+  r.zc = c.nz_cpu[i];
+  r.zm = c.nz_mem[i];
+  r.allowed = c.allowed_pods[i];
+  r.count = c.pod_count[i];
+  r.fl = c.flags[i];
+  return r;
+}
+
+// PodFitsResources (predicates.go:706-778) reason mask.
+__device__ __forceinline__ uint32_t ksim_resources(const KsimCtx& c, const ksim_pod& P, int64_t i,
+                                                   const KsimRow& r) {
+  uint32_t m = 0;
+  if (r.count + 1 > r.allowed) m |= 1u << KSIM_R_INSUFFICIENT_PODS;
+  if (!(P.flags & KSIM_POD_ANY_REQUEST)) return m;
+  if (r.ac < P.req_cpu + r.rc) m |= 1u << KSIM_R_INSUFFICIENT_CPU;
+  if (r.am < P.req_mem + r.rm) m |= 1u << KSIM_R_INSUFFICIENT_MEMORY;
+  if (P.req_gpu == 0) {
+    if (r.fl & KSIM_N_GPU_OVER) m |= 1u << KSIM_R_INSUFFICIENT_GPU;
+  } else if (c.alloc_gpu[i] < P.req_gpu + c.req_gpu[i]) {
+    m |= 1u << KSIM_R_INSUFFICIENT_GPU;
+  }
+  if (P.req_eph == 0) {
+    if (r.fl & KSIM_N_EPH_OVER) m |= 1u << KSIM_R_INSUFFICIENT_EPHEMERAL;
+  } else if (c.alloc_eph[i] < P.req_eph + c.req_eph[i]) {
+    m |= 1u << KSIM_R_INSUFFICIENT_EPHEMERAL;
+  }
+  for (int32_t s = 0; s < P.scalar_cnt; ++s) {
+    const ksim_scalar_req q = c.pod_scalars[P.scalar_off + s];
+    const int64_t off = (int64_t)q.col * c.n + i;
+    if (c.alloc_scalar[off] < q.req + c.req_scalar[off]) m |= 1u << (KSIM_R_INSUFFICIENT_SCALAR0 + q.col);
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint32_t ksim_hostname(const ksim_pod& P, int64_t i) {
+  return (P.host == -1 || P.host == i) ? 0u : (1u << KSIM_R_HOSTNAME);
+}
+
+__device__ __forceinline__ uint32_t ksim_hostports(const KsimCtx& c, const ksim_pod& P, int64_t i) {
+  for (int32_t k = 0; k < P.port_cnt; ++k)
+    if (ksim_port_conflict(c, i, c.pod_ports[P.port_off + k])) return 1u << KSIM_R_HOST_PORTS;
+  return 0;
+}
+
+__device__ __forceinline__ uint32_t ksim_selector(const KsimCtx& c, const ksim_pod& P, int64_t i) {
+  if (!(P.flags & KSIM_POD_NEED_SELECTOR)) return 0;
+  return ksim_bit(c.sel_ok, P.cls, c.lwords, c.label_set[i]) ? 0u : (1u << KSIM_R_NODE_SELECTOR);
+}
+
+// Reason mask of the first failing predicate in predicatesOrdering (predicates.go:129-138,
+// core/generic_scheduler.go:467-528); 0 = fits.
+__device__ __forceinline__ uint32_t ksim_predicates(const KsimCtx& c, const ksim_pod& P, int64_t i,
+                                                    const KsimRow& r) {
+  const uint32_t pr = c.preds;
+  uint32_t m;
+  if (pr & KSIM_P_CHECK_NODE_CONDITION) {
+    m = r.fl & KSIM_COND_REASON_MASK;  // bit positions coincide with KSIM_R_*
+    if (m) return m;
+  }
+  if ((pr & KSIM_P_CHECK_NODE_UNSCHEDULABLE) && (r.fl & KSIM_N_UNSCHEDULABLE)) return 1u << KSIM_R_UNSCHEDULABLE;
+  if (pr & KSIM_P_GENERAL) {
+    m = ksim_resources(c, P, i, r) | ksim_hostname(P, i);
+    if (P.port_cnt) m |= ksim_hostports(c, P, i);
+    m |= ksim_selector(c, P, i);
+    if (m) return m;
+  }
+  if (pr & KSIM_P_HOSTNAME) {
+    m = ksim_hostname(P, i);
+    if (m) return m;
+  }
+  if ((pr & KSIM_P_HOST_PORTS) && P.port_cnt) {
+    m = ksim_hostports(c, P, i);
+    if (m) return m;
+  }
+  if (pr & KSIM_P_NODE_SELECTOR) {
+    m = ksim_selector(c, P, i);
+    if (m) return m;
+  }
+  if (pr & KSIM_P_RESOURCES) {
+    m = ksim_resources(c, P, i, r);
+    if (m) return m;
+  }
+  if ((pr & KSIM_P_TAINTS) && (P.flags & KSIM_POD_NEED_TAINTS)) {
+    if (!ksim_bit(c.taint_ok, P.cls, c.twords, c.taint_set[i])) return 1u << KSIM_R_TAINTS;
+  }
+  if ((pr & KSIM_P_NOEXEC_TAINTS) && (P.flags & KSIM_POD_NEED_TAINTS)) {
+    if (!ksim_bit(c.noexec_ok, P.cls, c.twords, c.taint_set[i])) return 1u << KSIM_R_TAINTS;
+  }
+  if ((pr & KSIM_P_MEM_PRESSURE) && (P.flags & KSIM_POD_BEST_EFFORT) && (r.fl & KSIM_N_MEM_PRESSURE))
+    return 1u << KSIM_R_MEM_PRESSURE;
+  if ((pr & KSIM_P_DISK_PRESSURE) && (r.fl & KSIM_N_DISK_PRESSURE)) return 1u << KSIM_R_DISK_PRESSURE;
+  return 0;
+}
+
+// Weighted sum of the map-type priorities (core/generic_scheduler.go:632-639); the reduce
+// priorities are added per reduce class once their global maxima are known.
+__device__ __forceinline__ int64_t ksim_map_score(const KsimCtx& c, const ksim_pod& P, const KsimRow& r) {
+  if (c.no_prio) return 0;
+  const int64_t rc = P.nz_cpu + r.zc;  // resource_allocation.go:58-59
+  const int64_t rm = P.nz_mem + r.zm;
+  uint64_t s = 0;  // Go int: wrapping
+  if (c.w[KSIM_W_LEAST_REQUESTED])
+    s += (uint64_t)c.w[KSIM_W_LEAST_REQUESTED] * (uint64_t)((ksim_least(rc, r.ac) + ksim_least(rm, r.am)) / 2);
+  if (c.w[KSIM_W_MOST_REQUESTED])
+    s += (uint64_t)c.w[KSIM_W_MOST_REQUESTED] * (uint64_t)((ksim_most(rc, r.ac) + ksim_most(rm, r.am)) / 2);
+  if (c.w[KSIM_W_BALANCED])
+    s += (uint64_t)c.w[KSIM_W_BALANCED] * (uint64_t)ksim_balanced(rc, r.ac, rm, r.am);
+  return (int64_t)s;
+}
+
+__device__ __forceinline__ int ksim_rclass(const KsimCtx& c, const ksim_pod& P, int64_t i, int k1, int k2) {
+  int a = 0, b = 0;
+  if (k1 > 1) a = c.tt_class[(int64_t)P.cls * c.n_taint_sets + c.taint_set[i]];
+  if (k2 > 1) b = c.na_class[(int64_t)P.cls * c.n_label_sets + c.label_set[i]];
+  return a * k2 + b;
+}
+
+// NormalizeReduce (priorities/reduce.go:29-64) applied to one class value.
+__device__ __forceinline__ int64_t ksim_norm(int64_t v, int64_t mx, bool reverse) {
+  if (mx == 0) return reverse ? 10 : v;
+  int64_t s = (int64_t)((uint64_t)10 * (uint64_t)v) / mx;
+  return reverse ? 10 - s : s;
+}
+
+// Commit pod P to node w: NodeInfo.AddPod (node_info.go:318-341) + HostPortInfo.Add
+// (utils.go:45-60).  Single thread.
+__device__ __forceinline__ void ksim_commit(const KsimCtx& c, const ksim_pod& P, int64_t w) {
+  c.req_cpu[w] += P.add_cpu;
+  c.req_mem[w] += P.add_mem;
+  const int64_t g = c.req_gpu[w] + P.add_gpu;
+  const int64_t e = c.req_eph[w] + P.add_eph;
+  c.req_gpu[w] = g;
+  c.req_eph[w] = e;
+  c.nz_cpu[w] += P.nz_cpu;
+  c.nz_mem[w] += P.nz_mem;
+  c.pod_count[w] += 1;
+  uint32_t fl = c.flags[w] & ~(KSIM_N_GPU_OVER | KSIM_N_EPH_OVER);
+  if (c.alloc_gpu[w] < g) fl |= KSIM_N_GPU_OVER;
+  if (c.alloc_eph[w] < e) fl |= KSIM_N_EPH_OVER;
+  c.flags[w] = fl;
+  for (int32_t s = 0; s < P.scalar_cnt; ++s) {
+    const ksim_scalar_req q = c.pod_scalars[P.scalar_off + s];
+    c.req_scalar[(int64_t)q.col * c.n + w] += q.add;
+  }
+  for (int32_t k = 0; k < P.port_cnt; ++k) {
+    const uint64_t key = c.pod_ports[P.port_off + k];
+    int32_t cnt = c.port_count[w];
+    bool dup = false;
+    for (int32_t s = 0; s < cnt; ++s)
+      if (c.ports[(int64_t)s * c.n + w] == key) { dup = true; break; }
+    if (dup) continue;
+    if (cnt >= c.port_slots) { atomicOr(c.err, 1); continue; }
+    c.ports[(int64_t)cnt * c.n + w] = key;
+    c.port_count[w] = cnt + 1;
+  }
+}

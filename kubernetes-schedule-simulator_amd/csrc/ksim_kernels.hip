@@ -1,0 +1,409 @@
+// ksim_kernels.hip — gfx950 kernels of the per-pod scheduling cycle.
+//
+// Launch mode (KSIM_MODE_LAUNCH): one launch of ksim_scan_kernel per pod.  Every block
+// evaluates a contiguous, name-ordered chunk of nodes (one node per lane per step),
+// reduces it to a per-reduce-class (max map score, count at max) + fit count (+ reason
+// histogram) partial, publishes it, and takes an arrival ticket.  The last block to
+// arrive acquires, combines all partials into the global decision (findNodesThatFit
+// → PrioritizeNodes → selectHost, core/generic_scheduler.go:112-198), locates the
+// selected node by walking block counts from the highest name rank down, re-evaluates
+// only that block to pick the exact node, commits the pod (NodeInfo.AddPod) and advances
+// the device-side pod cursor.  Launches are replayed from a hipGraph, so per-pod host
+// work is zero and no PCIe traffic happens between pods.
+#include "ksim_common.h"
+
+namespace {
+
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+
+__device__ __forceinline__ int32_t wave_sum_i32(int32_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// inclusive prefix sum over the 256-thread block (4 waves)
+__device__ __forceinline__ int64_t block_incl_scan(int64_t v, int64_t* s_w) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t t = __shfl_up(v, o, 64);
+    if (lane >= o) v += t;
+  }
+  if (lane == 63) s_w[wv] = v;
+  __syncthreads();
+  int64_t add = 0;
+  for (int k = 0; k < wv; ++k) add += s_w[k];
+  __syncthreads();
+  return v + add;
+}
+
+struct Decision {
+  int64_t pod;
+  int32_t K, K2;
+  int32_t fitTotal;
+  int32_t mode;      // 0: none fit, 1: single fit, 2: select among winners
+  uint32_t winners;  // reduce classes whose total equals the max
+  int64_t M[KSIM_MAX_RCLASS];
+  int64_t ix;        // rank from the top (largest name rank)
+  int64_t blk;       // selected block
+  int64_t rank;      // rank within the selected block from the top
+  int64_t node;
+};
+
+}  // namespace
+
+// Evaluate one node for the scan: fit, map score, reduce class, reason mask.
+template <bool COLLECT>
+__device__ __forceinline__ void eval_one(const KsimCtx& c, const ksim_pod& P, int64_t i, int k1, int k2,
+                                         bool& fit, int64_t& score, int& cls, uint32_t& rmask) {
+  fit = false; score = 0; cls = 0; rmask = 0;
+  if (i >= c.n) return;
+  const KsimRow r = ksim_load_row(c, i);
+  const uint32_t m = ksim_predicates(c, P, i, r);
+  fit = (m == 0);
+  if (COLLECT) rmask = m;
+  score = ksim_map_score(c, P, r);
+  cls = (k1 * k2 > 1) ? ksim_rclass(c, P, i, k1, k2) : 0;
+}
+
+template <int NPT, bool COLLECT>
+__global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
+  __shared__ int64_t s_mx[KSIM_WAVES][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_cnt[KSIM_WAVES][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_fit[KSIM_WAVES];
+  __shared__ int32_t s_hist[KSIM_NREASONS];
+  __shared__ int64_t s_scan[KSIM_WAVES];
+  __shared__ uint64_t s_ball[NPT][KSIM_WAVES];
+  __shared__ int s_last;
+  __shared__ Decision D;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t pod = *c.cursor;
+  if (pod >= c.end) return;  // uniform: graph replay past the end of the queue
+  const ksim_pod P = c.pods[pod];
+  const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
+  const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
+  const int K = k1 * k2;
+  const int64_t base = (int64_t)blockIdx.x * c.chunk;
+
+  if (COLLECT && tid < KSIM_NREASONS) s_hist[tid] = 0;
+
+  // ---------------- phase 1: evaluate this block's chunk ----------------
+  bool fit[NPT];
+  int64_t sc[NPT];
+  int cl[NPT];
+  uint32_t rm[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) eval_one<COLLECT>(c, P, base + k * KSIM_BLOCK + tid, k1, k2, fit[k], sc[k], cl[k], rm[k]);
+
+  int32_t nfit = 0;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) nfit += __popcll(__ballot(fit[k]));
+  if (lane == 0) s_fit[wv] = nfit;
+
+#pragma unroll
+  for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
+    if (q >= K) break;
+    int64_t v = INT64_MIN;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k)
+      if (fit[k] && cl[k] == q && sc[k] > v) v = sc[k];
+    const int64_t wm = wave_max_i64(v);
+    int32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) n += __popcll(__ballot(fit[k] && cl[k] == q && sc[k] == wm));
+    if (lane == 0) { s_mx[wv][q] = wm; s_cnt[wv][q] = (wm == INT64_MIN) ? 0 : n; }
+  }
+  if (COLLECT) {
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      if (__ballot(rm[k] != 0)) {
+        for (int r = 0; r < KSIM_NREASONS; ++r) {
+          const int32_t n = __popcll(__ballot((rm[k] >> r) & 1u));
+          if (lane == 0 && n) atomicAdd(&s_hist[r], n);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---------------- publish the partial, take a ticket ----------------
+  if (tid == 0) {
+    KsimPartial* p = &c.partials[blockIdx.x];
+    int32_t f = 0;
+    for (int w = 0; w < KSIM_WAVES; ++w) f += s_fit[w];
+    p->fit = f;
+    for (int q = 0; q < K; ++q) {
+      int64_t m = INT64_MIN;
+      int32_t n = 0;
+      for (int w = 0; w < KSIM_WAVES; ++w) {
+        if (s_cnt[w][q] == 0) continue;
+        if (s_mx[w][q] > m) { m = s_mx[w][q]; n = s_cnt[w][q]; }
+        else if (s_mx[w][q] == m) n += s_cnt[w][q];
+      }
+      p->mx[q] = m;
+      p->cnt[q] = n;
+    }
+    if (COLLECT)
+      for (int r = 0; r < KSIM_NREASONS; ++r) p->hist[r] = s_hist[r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(c.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (old == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+
+  // ---------------- last block: the global decision ----------------
+  if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int G = gridDim.x;
+  // combine partials: each thread a strided set of blocks
+  int64_t lm[KSIM_MAX_RCLASS];
+  int32_t ln[KSIM_MAX_RCLASS];
+  int32_t lf = 0;
+#pragma unroll
+  for (int q = 0; q < KSIM_MAX_RCLASS; ++q) { lm[q] = INT64_MIN; ln[q] = 0; }
+  for (int b = tid; b < G; b += KSIM_BLOCK) {
+    const KsimPartial* p = &c.partials[b];
+    lf += p->fit;
+#pragma unroll
+    for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
+      if (q >= K) break;
+      const int32_t n = p->cnt[q];
+      if (n == 0) continue;
+      const int64_t m = p->mx[q];
+      if (m > lm[q]) { lm[q] = m; ln[q] = n; }
+      else if (m == lm[q]) ln[q] += n;
+    }
+  }
+  const int32_t wf = wave_sum_i32(lf);
+  if (lane == 0) s_fit[wv] = wf;
+#pragma unroll
+  for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
+    if (q >= K) break;
+    const int64_t wm = wave_max_i64(ln[q] ? lm[q] : INT64_MIN);
+    const int32_t wn = wave_sum_i32((ln[q] && lm[q] == wm) ? ln[q] : 0);
+    if (lane == 0) { s_mx[wv][q] = wm; s_cnt[wv][q] = wn; }
+  }
+  __syncthreads();
+
+  if (tid == 0) {
+    D.pod = pod;
+    D.K = K;
+    D.K2 = k2;
+    int32_t F = 0;
+    for (int w = 0; w < KSIM_WAVES; ++w) F += s_fit[w];
+    D.fitTotal = F;
+    D.node = -1;
+    D.blk = -1;
+    D.rank = 0;
+    if (F == 0) {
+      D.mode = 0;
+    } else if (F == 1) {  // generic_scheduler.go:153-156: no selectHost, no counter bump
+      D.mode = 1;
+      D.ix = 0;
+    } else {
+      D.mode = 2;
+      int64_t Mq[KSIM_MAX_RCLASS];
+      int32_t Cq[KSIM_MAX_RCLASS];
+      for (int q = 0; q < K; ++q) {
+        int64_t m = INT64_MIN;
+        int32_t n = 0;
+        for (int w = 0; w < KSIM_WAVES; ++w) {
+          if (s_cnt[w][q] == 0) continue;
+          if (s_mx[w][q] > m) { m = s_mx[w][q]; n = s_cnt[w][q]; }
+          else if (s_mx[w][q] == m) n += s_cnt[w][q];
+        }
+        Mq[q] = m;
+        Cq[q] = n;
+      }
+      // reduce priorities over the filtered set (NormalizeReduce)
+      int64_t mxT = 0, mxA = 0;
+      for (int q = 0; q < K; ++q) {
+        if (Cq[q] == 0) continue;
+        const int64_t tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2];
+        const int64_t av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];
+        if (k1 > 1 || c.w[KSIM_W_TAINT_TOLERATION]) mxT = tv > mxT ? tv : mxT;
+        if (k2 > 1 || c.w[KSIM_W_NODE_AFFINITY]) mxA = av > mxA ? av : mxA;
+      }
+      int64_t best = INT64_MIN;
+      int64_t tot[KSIM_MAX_RCLASS];
+      for (int q = 0; q < K; ++q) {
+        if (Cq[q] == 0) continue;
+        uint64_t t = (uint64_t)Mq[q];
+        if (c.w[KSIM_W_TAINT_TOLERATION]) {
+          const int64_t tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2];
+          t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(tv, mxT, true);
+        }
+        if (c.w[KSIM_W_NODE_AFFINITY]) {
+          const int64_t av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];
+          t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(av, mxA, false);
+        }
+        tot[q] = (int64_t)t;
+        if (tot[q] > best) best = tot[q];
+      }
+      uint32_t win = 0;
+      int64_t C = 0;
+      for (int q = 0; q < K; ++q)
+        if (Cq[q] && tot[q] == best) { win |= 1u << q; C += Cq[q]; }
+      D.winners = win;
+      for (int q = 0; q < K; ++q) D.M[q] = Mq[q];
+      const uint64_t li = *c.counter;           // generic_scheduler.go:192-195
+      D.ix = (int64_t)(li % (uint64_t)C);
+      *c.counter = li + 1;
+    }
+  }
+  __syncthreads();
+
+  if (D.mode == 0) {
+    if (COLLECT && c.out_reasons) {
+      for (int r = 0; r < KSIM_NREASONS; ++r) {
+        int32_t v = 0;
+        for (int b = tid; b < G; b += KSIM_BLOCK) v += c.partials[b].hist[r];
+        v = wave_sum_i32(v);
+        if (lane == 0) s_cnt[wv][0] = v;
+        __syncthreads();
+        if (tid == 0) c.out_reasons[pod * KSIM_NREASONS + r] = s_cnt[0][0] + s_cnt[1][0] + s_cnt[2][0] + s_cnt[3][0];
+        __syncthreads();
+      }
+    }
+  } else {
+    // ---- locate the block holding the ix-th match counted from the top ----
+    const int64_t per = (G + KSIM_BLOCK - 1) / KSIM_BLOCK;
+    const int tr = KSIM_BLOCK - 1 - tid;  // reversed: thread 0 owns the highest blocks
+    const int64_t b0 = (int64_t)tr * per, b1 = (b0 + per < G) ? b0 + per : G;
+    int64_t s = 0;
+    for (int64_t b = b0; b < b1; ++b) {
+      const KsimPartial* p = &c.partials[b];
+      if (D.mode == 1) {
+        s += p->fit;
+      } else {
+        for (int q = 0; q < K; ++q)
+          if (((D.winners >> q) & 1u) && p->cnt[q] && p->mx[q] == D.M[q]) s += p->cnt[q];
+      }
+    }
+    const int64_t incl = block_incl_scan(s, s_scan);
+    const int64_t above = incl - s;
+    if (s > 0 && D.ix >= above && D.ix < incl) {
+      int64_t r = D.ix - above;
+      for (int64_t b = b1 - 1; b >= b0; --b) {
+        const KsimPartial* p = &c.partials[b];
+        int64_t cb = 0;
+        if (D.mode == 1) {
+          cb = p->fit;
+        } else {
+          for (int q = 0; q < K; ++q)
+            if (((D.winners >> q) & 1u) && p->cnt[q] && p->mx[q] == D.M[q]) cb += p->cnt[q];
+        }
+        if (r < cb) { D.blk = b; D.rank = r; break; }
+        r -= cb;
+      }
+    }
+    __syncthreads();
+    if (D.blk < 0) {  // inconsistent partials: must never happen
+      if (tid == 0) { atomicOr(c.err, 2); c.out_node[pod] = -1; *c.cursor = pod + 1; *c.ticket = 0; }
+      return;
+    }
+    // ---- re-evaluate the selected block, pick the exact node ----
+    const int64_t bb = D.blk * c.chunk;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      bool f; int64_t sc1; int cl1; uint32_t rm1;
+      eval_one<false>(c, P, bb + k * KSIM_BLOCK + tid, k1, k2, f, sc1, cl1, rm1);
+      bool match = f;
+      if (D.mode == 2) match = f && ((D.winners >> cl1) & 1u) && sc1 == D.M[cl1];
+      const uint64_t bal = __ballot(match);
+      if (lane == 0) s_ball[k][wv] = bal;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      int64_t r = D.rank;
+      int64_t node = -1;
+      for (int k = NPT - 1; k >= 0 && node < 0; --k) {
+        for (int w = KSIM_WAVES - 1; w >= 0; --w) {
+          uint64_t m = s_ball[k][w];
+          const int n = __popcll(m);
+          if (r >= n) { r -= n; continue; }
+          for (int64_t j = 0; j < r; ++j) m &= ~(1ull << (63 - __clzll(m)));
+          node = bb + (int64_t)k * KSIM_BLOCK + w * 64 + (63 - __clzll(m));
+          break;
+        }
+      }
+      if (node < 0) atomicOr(c.err, 2);  // inconsistent partials: must never happen
+      D.node = node;
+      if (node >= 0) ksim_commit(c, P, node);
+    }
+  }
+  if (tid == 0) {
+    c.out_node[pod] = (int32_t)D.node;
+    *c.cursor = pod + 1;
+    *c.ticket = 0;
+  }
+}
+
+// Per-node evaluation of one pod without commit (ksim_evaluate).
+__global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_t pod, uint8_t* fit, uint32_t* reasons,
+                                                             int64_t* score, uint8_t* rcls) {
+  const int64_t i = (int64_t)blockIdx.x * KSIM_BLOCK + threadIdx.x;
+  if (i >= c.n) return;
+  const ksim_pod P = c.pods[pod];
+  const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
+  const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
+  const KsimRow r = ksim_load_row(c, i);
+  const uint32_t m = ksim_predicates(c, P, i, r);
+  fit[i] = m == 0;
+  reasons[i] = m;
+  score[i] = ksim_map_score(c, P, r);
+  rcls[i] = (uint8_t)((k1 * k2 > 1) ? ksim_rclass(c, P, i, k1, k2) : 0);
+}
+
+// Commit one pod to one node (ksim_assume).
+__global__ void ksim_assume_kernel(KsimCtx c, int64_t pod, int64_t node) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) ksim_commit(c, c.pods[pod], node);
+}
+
+// Launch-mode entry points used by the host runtime (ksim_runtime.cpp).
+extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, int grid, hipStream_t s) {
+#define KSIM_L(N, C) hipLaunchKernelGGL((ksim_scan_kernel<N, C>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c)
+  if (collect) {
+    switch (npt) {
+      case 1: KSIM_L(1, true); break;
+      case 2: KSIM_L(2, true); break;
+      case 4: KSIM_L(4, true); break;
+      default: KSIM_L(8, true); break;
+    }
+  } else {
+    switch (npt) {
+      case 1: KSIM_L(1, false); break;
+      case 2: KSIM_L(2, false); break;
+      case 4: KSIM_L(4, false); break;
+      default: KSIM_L(8, false); break;
+    }
+  }
+#undef KSIM_L
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* fit, uint32_t* reasons, int64_t* score,
+                                       uint8_t* rcls, hipStream_t s) {
+  const int grid = (int)((c->n + KSIM_BLOCK - 1) / KSIM_BLOCK);
+  hipLaunchKernelGGL(ksim_eval_kernel, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, pod, fit, reasons, score, rcls);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, hipStream_t s) {
+  hipLaunchKernelGGL(ksim_assume_kernel, dim3(1), dim3(64), 0, s, *c, pod, node);
+  return hipGetLastError();
+}

@@ -1,0 +1,497 @@
+// ksim_runtime.cpp — host side of libksim.so: the C-ABI declared in include/ksim.h.
+//
+// Owns the device-resident node table (SoA columns in HBM), the pod-class tables, the
+// pod queue and the run state, and drives the scan kernels on one HIP stream per handle.
+// No torch types cross this boundary; every entry point calls hipSetDevice (cgo calls may
+// land on any OS thread) and returns a KSIM_* status.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ksim_common.h"
+
+extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, int grid, hipStream_t s);
+extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* fit, uint32_t* reasons, int64_t* score,
+                                       uint8_t* rcls, hipStream_t s);
+extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, hipStream_t s);
+extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, int grid, int lds_rows, hipStream_t s);
+extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows);
+
+namespace {
+
+thread_local std::string g_err;
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace
+
+struct ksim_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  ksim_config cfg{};
+  std::string err;
+  std::vector<DevBuf> bufs;
+  KsimCtx ctx{};
+  bool have_nodes = false, have_classes = false, have_pods = false;
+  int64_t n_pods = 0;
+  int32_t n_classes = 0;
+  int32_t n_ports_total = 0;
+  // launch-mode graph
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+  int g_batch = 0, g_npt = 0, g_collect = -1, part_cap = 0;
+  int64_t g_first = -1, g_end = -1;
+  // host-side copies needed for validation
+  std::vector<int32_t> h_n_tt, h_n_na;
+};
+
+static int fail(ksim_handle* h, int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  if (h) h->err = buf;
+  g_err = buf;
+  return code;
+}
+
+#define HIPCHK(h, x)                                                                         \
+  do {                                                                                       \
+    hipError_t e_ = (x);                                                                     \
+    if (e_ != hipSuccess) return fail((h), KSIM_E_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+static int dev_alloc(ksim_handle* h, T** out, size_t count) {
+  *out = nullptr;
+  size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e != hipSuccess) return fail(h, KSIM_E_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  h->bufs.push_back({p, bytes});
+  *out = reinterpret_cast<T*>(p);
+  return KSIM_OK;
+}
+
+template <class T>
+static int dev_upload(ksim_handle* h, T** out, const T* src, size_t count, bool zero_if_null = true) {
+  int rc = dev_alloc(h, out, count);
+  if (rc) return rc;
+  if (src && count) {
+    HIPCHK(h, hipMemcpyAsync(*out, src, count * sizeof(T), hipMemcpyHostToDevice, h->stream));
+  } else if (zero_if_null && count) {
+    HIPCHK(h, hipMemsetAsync(*out, 0, count * sizeof(T), h->stream));
+  }
+  return KSIM_OK;
+}
+
+extern "C" {
+
+int ksim_abi_version(void) { return KSIM_ABI_VERSION; }
+
+const char* ksim_last_error(const ksim_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
+
+int ksim_create(const ksim_config* cfg, ksim_handle** out) {
+  if (!cfg || !out) return fail(nullptr, KSIM_E_INVAL, "ksim_create: null argument");
+  *out = nullptr;
+  int ndev = 0;
+  hipError_t e = hipGetDeviceCount(&ndev);
+  if (e != hipSuccess || ndev == 0)
+    return fail(nullptr, KSIM_E_DEVICE, "ksim_create: no HIP device (%s)", hipGetErrorString(e));
+  if (cfg->device < 0 || cfg->device >= ndev) return fail(nullptr, KSIM_E_INVAL, "ksim_create: bad device %d", cfg->device);
+  for (int k = 0; k < KSIM_NW; ++k)
+    if (cfg->weights[k] < 0) return fail(nullptr, KSIM_E_INVAL, "ksim_create: negative weight in slot %d", k);
+  const uint32_t known = (1u << 11) - 1;
+  if (cfg->predicates & ~known) return fail(nullptr, KSIM_E_UNSUPPORTED, "ksim_create: unknown predicate bits");
+  ksim_handle* h = new ksim_handle();
+  h->device = cfg->device;
+  h->cfg = *cfg;
+  if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
+    delete h;
+    return fail(nullptr, KSIM_E_DEVICE, "ksim_create: stream/event creation failed");
+  }
+  KsimCtx& c = h->ctx;
+  c.preds = cfg->predicates;
+  c.no_prio = cfg->no_priorities;
+  c.collect = cfg->collect_reasons;
+  for (int k = 0; k < KSIM_NW; ++k) c.w[k] = cfg->weights[k];
+  int rc;
+  if ((rc = dev_alloc(h, &c.cursor, 1)) || (rc = dev_alloc(h, &c.counter, 1)) || (rc = dev_alloc(h, &c.ticket, 4)) ||
+      (rc = dev_alloc(h, &c.err, 4))) {
+    ksim_destroy(h);
+    return rc;
+  }
+  (void)hipMemsetAsync(c.ticket, 0, 16, h->stream);
+  (void)hipMemsetAsync(c.err, 0, 16, h->stream);
+  (void)hipMemcpyAsync(c.counter, &cfg->last_node_index, 8, hipMemcpyHostToDevice, h->stream);
+  if (hipStreamSynchronize(h->stream) != hipSuccess) {
+    ksim_destroy(h);
+    return fail(nullptr, KSIM_E_DEVICE, "ksim_create: initial copies failed");
+  }
+  *out = h;
+  return KSIM_OK;
+}
+
+void ksim_destroy(ksim_handle* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+  if (h->graph) (void)hipGraphDestroy(h->graph);
+  for (auto& b : h->bufs) (void)hipFree(b.p);
+  if (h->ev0) (void)hipEventDestroy(h->ev0);
+  if (h->ev1) (void)hipEventDestroy(h->ev1);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+int ksim_load_nodes(ksim_handle* h, const ksim_node_table* t) {
+  if (!h || !t) return fail(h, KSIM_E_INVAL, "ksim_load_nodes: null argument");
+  if (h->have_nodes) return fail(h, KSIM_E_STATE, "ksim_load_nodes: node table already loaded");
+  HIPCHK(h, hipSetDevice(h->device));
+  const int64_t n = t->n_nodes;
+  if (n <= 0) return fail(h, KSIM_E_INVAL, "no nodes available to schedule pods");
+  if (n > (int64_t)INT32_MAX) return fail(h, KSIM_E_INVAL, "ksim_load_nodes: too many nodes");
+  if (t->n_scalar < 0 || t->n_scalar > KSIM_MAX_SCALAR) return fail(h, KSIM_E_UNSUPPORTED, "n_scalar %d > %d", t->n_scalar, KSIM_MAX_SCALAR);
+  if (t->port_slots < 0 || t->port_slots > 4096) return fail(h, KSIM_E_INVAL, "port_slots out of range");
+  if (!t->alloc_cpu || !t->alloc_mem || !t->allowed_pods) return fail(h, KSIM_E_INVAL, "ksim_load_nodes: missing column");
+  KsimCtx& c = h->ctx;
+  c.n = n;
+  c.n_scalar = t->n_scalar;
+  c.port_slots = t->port_slots;
+  // derive the library-maintained over-commit bits
+  std::vector<uint32_t> fl(n, 0);
+  for (int64_t i = 0; i < n; ++i) {
+    uint32_t f = t->flags ? (t->flags[i] & 0xFFu) : 0u;
+    const int64_t ag = t->alloc_gpu ? t->alloc_gpu[i] : 0, rg = t->req_gpu ? t->req_gpu[i] : 0;
+    const int64_t ae = t->alloc_eph ? t->alloc_eph[i] : 0, re = t->req_eph ? t->req_eph[i] : 0;
+    if (ag < rg) f |= KSIM_N_GPU_OVER;
+    if (ae < re) f |= KSIM_N_EPH_OVER;
+    fl[i] = f;
+  }
+  if (t->port_count && t->ports) {
+    for (int64_t i = 0; i < n; ++i)
+      if (t->port_count[i] < 0 || t->port_count[i] > t->port_slots) return fail(h, KSIM_E_INVAL, "port_count[%lld] out of range", (long long)i);
+  }
+  const size_t S = (size_t)t->n_scalar;
+  int rc;
+  int64_t *ac, *am, *ag, *ae, *as;
+  int32_t *ap, *ls, *ts;
+  if ((rc = dev_upload(h, &ac, t->alloc_cpu, n)) || (rc = dev_upload(h, &am, t->alloc_mem, n)) ||
+      (rc = dev_upload(h, &ag, t->alloc_gpu, n)) || (rc = dev_upload(h, &ae, t->alloc_eph, n)) ||
+      (rc = dev_upload(h, &ap, t->allowed_pods, n)) || (rc = dev_upload(h, &c.flags, fl.data(), n)) ||
+      (rc = dev_upload(h, &ls, t->label_set, n)) || (rc = dev_upload(h, &ts, t->taint_set, n)) ||
+      (rc = dev_upload(h, &as, t->alloc_scalar, S * n)) || (rc = dev_upload(h, &c.req_cpu, t->req_cpu, n)) ||
+      (rc = dev_upload(h, &c.req_mem, t->req_mem, n)) || (rc = dev_upload(h, &c.req_gpu, t->req_gpu, n)) ||
+      (rc = dev_upload(h, &c.req_eph, t->req_eph, n)) || (rc = dev_upload(h, &c.nz_cpu, t->nz_cpu, n)) ||
+      (rc = dev_upload(h, &c.nz_mem, t->nz_mem, n)) || (rc = dev_upload(h, &c.pod_count, t->pod_count, n)) ||
+      (rc = dev_upload(h, &c.req_scalar, t->req_scalar, S * n)) ||
+      (rc = dev_upload(h, &c.ports, t->ports, (size_t)t->port_slots * n)) ||
+      (rc = dev_upload(h, &c.port_count, t->ports ? t->port_count : nullptr, n)))
+    return rc;
+  c.alloc_cpu = ac; c.alloc_mem = am; c.alloc_gpu = ag; c.alloc_eph = ae; c.alloc_scalar = as;
+  c.allowed_pods = ap; c.label_set = ls; c.taint_set = ts;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->have_nodes = true;
+  return KSIM_OK;
+}
+
+int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
+  if (!h || !t) return fail(h, KSIM_E_INVAL, "ksim_load_classes: null argument");
+  if (h->have_classes) return fail(h, KSIM_E_STATE, "ksim_load_classes: already loaded");
+  HIPCHK(h, hipSetDevice(h->device));
+  if (t->n_classes <= 0 || t->n_label_sets <= 0 || t->n_taint_sets <= 0)
+    return fail(h, KSIM_E_INVAL, "ksim_load_classes: empty tables");
+  const size_t C = t->n_classes, L = t->n_label_sets, T = t->n_taint_sets;
+  const size_t lw = (L + 31) / 32, tw = (T + 31) / 32;
+  for (size_t k = 0; k < C; ++k) {
+    const int a = t->n_tt ? t->n_tt[k] : 1, b = t->n_na ? t->n_na[k] : 1;
+    if (a < 1 || b < 1 || a * b > KSIM_MAX_RCLASS)
+      return fail(h, KSIM_E_UNSUPPORTED, "class %zu: %d x %d reduce classes exceed %d", k, a, b, KSIM_MAX_RCLASS);
+  }
+  KsimCtx& c = h->ctx;
+  int rc;
+  uint32_t *so, *to, *no;
+  uint8_t *tc, *nc;
+  int32_t *ntt, *nna;
+  int64_t *tv, *nv;
+  std::vector<int32_t> ones(C, 1);
+  if ((rc = dev_upload(h, &so, t->sel_ok, C * lw)) || (rc = dev_upload(h, &to, t->taint_ok, C * tw)) ||
+      (rc = dev_upload(h, &no, t->noexec_ok, C * tw)) || (rc = dev_upload(h, &tc, t->tt_class, C * T)) ||
+      (rc = dev_upload(h, &nc, t->na_class, C * L)) ||
+      (rc = dev_upload(h, &ntt, t->n_tt ? t->n_tt : ones.data(), C)) ||
+      (rc = dev_upload(h, &nna, t->n_na ? t->n_na : ones.data(), C)) ||
+      (rc = dev_upload(h, &tv, t->tt_val, C * KSIM_MAX_RCLASS)) || (rc = dev_upload(h, &nv, t->na_val, C * KSIM_MAX_RCLASS)))
+    return rc;
+  c.sel_ok = so; c.taint_ok = to; c.noexec_ok = no; c.tt_class = tc; c.na_class = nc;
+  c.n_tt = ntt; c.n_na = nna; c.tt_val = tv; c.na_val = nv;
+  c.lwords = (int32_t)lw; c.twords = (int32_t)tw;
+  c.n_label_sets = (int32_t)L; c.n_taint_sets = (int32_t)T;
+  h->n_classes = t->n_classes;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->have_classes = true;
+  return KSIM_OK;
+}
+
+int ksim_load_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const uint64_t* ports, int64_t n_ports,
+                   const ksim_scalar_req* scalars, int64_t n_scalars) {
+  if (!h || (!pods && n_pods)) return fail(h, KSIM_E_INVAL, "ksim_load_pods: null argument");
+  if (!h->have_nodes || !h->have_classes) return fail(h, KSIM_E_STATE, "ksim_load_pods: load nodes and classes first");
+  if (h->have_pods) return fail(h, KSIM_E_STATE, "ksim_load_pods: pod queue already loaded");
+  if (n_pods < 0 || n_ports < 0 || n_scalars < 0) return fail(h, KSIM_E_INVAL, "ksim_load_pods: negative size");
+  HIPCHK(h, hipSetDevice(h->device));
+  KsimCtx& c = h->ctx;
+  for (int64_t i = 0; i < n_pods; ++i) {
+    const ksim_pod& p = pods[i];
+    if (p.cls < 0 || p.cls >= h->n_classes) return fail(h, KSIM_E_INVAL, "pod %lld: class %d out of range", (long long)i, p.cls);
+    if (p.host < -2 || p.host >= c.n) return fail(h, KSIM_E_INVAL, "pod %lld: host %d out of range", (long long)i, p.host);
+    if (p.port_cnt < 0 || p.port_off < 0 || (int64_t)p.port_off + p.port_cnt > n_ports)
+      return fail(h, KSIM_E_INVAL, "pod %lld: port range out of bounds", (long long)i);
+    if (p.scalar_cnt < 0 || p.scalar_off < 0 || (int64_t)p.scalar_off + p.scalar_cnt > n_scalars)
+      return fail(h, KSIM_E_INVAL, "pod %lld: scalar range out of bounds", (long long)i);
+    if (p.port_cnt > 0 && c.port_slots == 0)
+      return fail(h, KSIM_E_INVAL, "pod %lld requests host ports but the node table has no port slots", (long long)i);
+  }
+  for (int64_t s = 0; s < n_scalars; ++s)
+    if (scalars[s].col < 0 || scalars[s].col >= c.n_scalar)
+      return fail(h, KSIM_E_INVAL, "scalar request %lld: column out of range", (long long)s);
+  int rc;
+  ksim_pod* dp;
+  uint64_t* pp;
+  ksim_scalar_req* sp;
+  if ((rc = dev_upload(h, &dp, pods, n_pods)) || (rc = dev_upload(h, &pp, ports, n_ports)) ||
+      (rc = dev_upload(h, &sp, scalars, n_scalars)) || (rc = dev_alloc(h, &c.out_node, n_pods)) ||
+      (rc = dev_alloc(h, &c.out_reasons, c.collect ? n_pods * KSIM_NREASONS : 1)))
+    return rc;
+  c.pods = dp; c.pod_ports = pp; c.pod_scalars = sp;
+  if (c.collect) HIPCHK(h, hipMemsetAsync(c.out_reasons, 0, n_pods * KSIM_NREASONS * sizeof(int32_t), h->stream));
+  h->n_pods = n_pods;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  h->have_pods = true;
+  return KSIM_OK;
+}
+
+static int pick_npt(int64_t n) {
+  for (int npt : {1, 2, 4, 8})
+    if ((n + (int64_t)KSIM_BLOCK * npt - 1) / ((int64_t)KSIM_BLOCK * npt) <= 1024) return npt;
+  return 8;
+}
+
+static int ensure_partials(ksim_handle* h, int grid) {
+  KsimCtx& c = h->ctx;
+  if (c.partials && h->part_cap >= grid) return KSIM_OK;
+  KsimPartial* p;
+  int rc = dev_alloc(h, &p, (size_t)std::max(grid, 1024));
+  if (rc) return rc;
+  c.partials = p;
+  h->part_cap = std::max(grid, 1024);
+  return KSIM_OK;
+}
+
+static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
+  KsimCtx& c = h->ctx;
+  const int npt = pick_npt(c.n);
+  c.chunk = (int64_t)KSIM_BLOCK * npt;
+  const int grid = (int)((c.n + c.chunk - 1) / c.chunk);
+  int rc = ensure_partials(h, grid);
+  if (rc) return rc;
+  c.first = first;
+  c.end = first + count;
+  HIPCHK(h, hipMemcpyAsync(c.cursor, &first, 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemsetAsync(c.ticket, 0, 16, h->stream));
+  const int batch = (int)std::min<int64_t>(count, 256);
+  if (!h->gexec || h->g_batch != batch || h->g_npt != npt || h->g_collect != c.collect || h->g_first != first ||
+      h->g_end != c.end) {
+    if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
+    if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    for (int k = 0; k < batch; ++k) {
+      hipError_t e = ksim_launch_scan(&c, npt, c.collect, grid, h->stream);
+      if (e != hipSuccess) {
+        hipGraph_t g = nullptr;
+        (void)hipStreamEndCapture(h->stream, &g);
+        if (g) (void)hipGraphDestroy(g);
+        return fail(h, KSIM_E_DEVICE, "scan launch during capture: %s", hipGetErrorString(e));
+      }
+    }
+    HIPCHK(h, hipStreamEndCapture(h->stream, &h->graph));
+    HIPCHK(h, hipGraphInstantiate(&h->gexec, h->graph, nullptr, nullptr, 0));
+    h->g_batch = batch; h->g_npt = npt; h->g_collect = c.collect; h->g_first = first; h->g_end = c.end;
+  }
+  const int64_t reps = (count + batch - 1) / batch;
+  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+  for (int64_t r = 0; r < reps; ++r) HIPCHK(h, hipGraphLaunch(h->gexec, h->stream));
+  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+  HIPCHK(h, hipEventSynchronize(h->ev1));
+  float ms = 0.f;
+  HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+  if (st) {
+    st->device_ms = ms;
+    st->kernel_ms = ms;
+    st->kernel_launches = reps * batch;
+    st->mode = KSIM_MODE_LAUNCH;
+    st->blocks = grid;
+  }
+  return KSIM_OK;
+}
+
+static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
+  KsimCtx& c = h->ctx;
+  int grid = 0, lds_rows = 0;
+  if (!ksim_persistent_config(c.n, &grid, &lds_rows))
+    return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: node table does not fit the persistent layout");
+  int rc = ensure_partials(h, 2 * grid);
+  if (rc) return rc;
+  c.first = first;
+  c.end = first + count;
+  c.chunk = (c.n + grid - 1) / grid;
+  HIPCHK(h, hipMemcpyAsync(c.cursor, &first, 8, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemsetAsync(c.ticket, 0, 16, h->stream));
+  HIPCHK(h, hipMemsetAsync(c.partials, 0, sizeof(KsimPartial) * 2 * grid, h->stream));
+  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+  hipError_t e = ksim_launch_persistent(&c, grid, lds_rows, h->stream);
+  if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+  HIPCHK(h, hipEventSynchronize(h->ev1));
+  float ms = 0.f;
+  HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+  if (st) {
+    st->device_ms = ms;
+    st->kernel_ms = ms;
+    st->kernel_launches = 1;
+    st->mode = KSIM_MODE_PERSISTENT;
+    st->blocks = grid;
+  }
+  return KSIM_OK;
+}
+
+int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_node, int32_t* out_reasons,
+                  ksim_stats* st) {
+  if (!h) return fail(h, KSIM_E_INVAL, "ksim_schedule: null handle");
+  if (!h->have_pods) return fail(h, KSIM_E_STATE, "ksim_schedule: load nodes, classes and pods first");
+  if (first < 0 || count < 0 || first + count > h->n_pods) return fail(h, KSIM_E_INVAL, "ksim_schedule: range out of bounds");
+  HIPCHK(h, hipSetDevice(h->device));
+  if (st) memset(st, 0, sizeof *st);
+  if (count == 0) return KSIM_OK;
+  KsimCtx& c = h->ctx;
+  int mode = h->cfg.mode;
+  if (mode == KSIM_MODE_AUTO) {
+    int g, l;
+    mode = ksim_persistent_config(c.n, &g, &l) ? KSIM_MODE_PERSISTENT : KSIM_MODE_LAUNCH;
+  }
+  int rc = (mode == KSIM_MODE_PERSISTENT) ? run_persistent_mode(h, first, count, st) : run_launch_mode(h, first, count, st);
+  if (rc) return rc;
+  int32_t err = 0;
+  HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
+  if (out_node) HIPCHK(h, hipMemcpy(out_node, c.out_node + first, count * sizeof(int32_t), hipMemcpyDeviceToHost));
+  if (out_reasons && c.collect)
+    HIPCHK(h, hipMemcpy(out_reasons, c.out_reasons + first * KSIM_NREASONS, count * KSIM_NREASONS * sizeof(int32_t),
+                        hipMemcpyDeviceToHost));
+  if (st) {
+    st->pods = count;
+    st->node_evals = count * c.n;
+    if (out_node) {
+      int64_t s = 0;
+      for (int64_t i = 0; i < count; ++i) s += out_node[i] >= 0;
+      st->scheduled = s;
+    }
+  }
+  if (err & 1) return fail(h, KSIM_E_OVERFLOW, "a node's host-port slots overflowed (raise port_slots)");
+  if (err & ~1) return fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
+  return KSIM_OK;
+}
+
+int ksim_evaluate(ksim_handle* h, int64_t pod, uint8_t* out_fit, uint32_t* out_reasons, int64_t* out_score,
+                  uint8_t* out_rclass) {
+  if (!h) return fail(h, KSIM_E_INVAL, "ksim_evaluate: null handle");
+  if (!h->have_pods) return fail(h, KSIM_E_STATE, "ksim_evaluate: nothing loaded");
+  if (pod < 0 || pod >= h->n_pods) return fail(h, KSIM_E_INVAL, "ksim_evaluate: pod out of range");
+  HIPCHK(h, hipSetDevice(h->device));
+  KsimCtx& c = h->ctx;
+  const int64_t n = c.n;
+  uint8_t *f, *rcl;
+  uint32_t* r;
+  int64_t* s;
+  // scratch buffers (kept for the handle's lifetime; small compared with the table)
+  int rc;
+  if ((rc = dev_alloc(h, &f, n)) || (rc = dev_alloc(h, &r, n)) || (rc = dev_alloc(h, &s, n)) || (rc = dev_alloc(h, &rcl, n)))
+    return rc;
+  hipError_t e = ksim_launch_eval(&c, pod, f, r, s, rcl, h->stream);
+  if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "eval launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (out_fit) HIPCHK(h, hipMemcpy(out_fit, f, n, hipMemcpyDeviceToHost));
+  if (out_reasons) HIPCHK(h, hipMemcpy(out_reasons, r, n * 4, hipMemcpyDeviceToHost));
+  if (out_score) HIPCHK(h, hipMemcpy(out_score, s, n * 8, hipMemcpyDeviceToHost));
+  if (out_rclass) HIPCHK(h, hipMemcpy(out_rclass, rcl, n, hipMemcpyDeviceToHost));
+  // release the scratch buffers again
+  for (void* p : {(void*)f, (void*)r, (void*)s, (void*)rcl}) {
+    (void)hipFree(p);
+    h->bufs.erase(std::remove_if(h->bufs.begin(), h->bufs.end(), [p](const DevBuf& b) { return b.p == p; }), h->bufs.end());
+  }
+  return KSIM_OK;
+}
+
+int ksim_assume(ksim_handle* h, int64_t pod, int64_t node) {
+  if (!h) return fail(h, KSIM_E_INVAL, "ksim_assume: null handle");
+  if (!h->have_pods) return fail(h, KSIM_E_STATE, "ksim_assume: nothing loaded");
+  if (pod < 0 || pod >= h->n_pods || node < 0 || node >= h->ctx.n) return fail(h, KSIM_E_INVAL, "ksim_assume: out of range");
+  HIPCHK(h, hipSetDevice(h->device));
+  hipError_t e = ksim_launch_assume(&h->ctx, pod, node, h->stream);
+  if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "assume launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  int32_t err = 0;
+  HIPCHK(h, hipMemcpy(&err, h->ctx.err, 4, hipMemcpyDeviceToHost));
+  if (err & 1) return fail(h, KSIM_E_OVERFLOW, "a node's host-port slots overflowed (raise port_slots)");
+  return KSIM_OK;
+}
+
+int ksim_read_nodes(ksim_handle* h, ksim_node_state* o) {
+  if (!h || !o) return fail(h, KSIM_E_INVAL, "ksim_read_nodes: null argument");
+  if (!h->have_nodes) return fail(h, KSIM_E_STATE, "ksim_read_nodes: no node table");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const KsimCtx& c = h->ctx;
+  const size_t n = c.n;
+  if (o->req_cpu) HIPCHK(h, hipMemcpy(o->req_cpu, c.req_cpu, n * 8, hipMemcpyDeviceToHost));
+  if (o->req_mem) HIPCHK(h, hipMemcpy(o->req_mem, c.req_mem, n * 8, hipMemcpyDeviceToHost));
+  if (o->req_gpu) HIPCHK(h, hipMemcpy(o->req_gpu, c.req_gpu, n * 8, hipMemcpyDeviceToHost));
+  if (o->req_eph) HIPCHK(h, hipMemcpy(o->req_eph, c.req_eph, n * 8, hipMemcpyDeviceToHost));
+  if (o->nz_cpu) HIPCHK(h, hipMemcpy(o->nz_cpu, c.nz_cpu, n * 8, hipMemcpyDeviceToHost));
+  if (o->nz_mem) HIPCHK(h, hipMemcpy(o->nz_mem, c.nz_mem, n * 8, hipMemcpyDeviceToHost));
+  if (o->pod_count) HIPCHK(h, hipMemcpy(o->pod_count, c.pod_count, n * 4, hipMemcpyDeviceToHost));
+  if (o->req_scalar && c.n_scalar)
+    HIPCHK(h, hipMemcpy(o->req_scalar, c.req_scalar, (size_t)c.n_scalar * n * 8, hipMemcpyDeviceToHost));
+  if (o->ports && c.port_slots) HIPCHK(h, hipMemcpy(o->ports, c.ports, (size_t)c.port_slots * n * 8, hipMemcpyDeviceToHost));
+  if (o->port_count) HIPCHK(h, hipMemcpy(o->port_count, c.port_count, n * 4, hipMemcpyDeviceToHost));
+  return KSIM_OK;
+}
+
+int ksim_get_counter(ksim_handle* h, uint64_t* out) {
+  if (!h || !out) return fail(h, KSIM_E_INVAL, "ksim_get_counter: null argument");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipMemcpy(out, h->ctx.counter, 8, hipMemcpyDeviceToHost));
+  return KSIM_OK;
+}
+
+int ksim_set_counter(ksim_handle* h, uint64_t v) {
+  if (!h) return fail(h, KSIM_E_INVAL, "ksim_set_counter: null handle");
+  HIPCHK(h, hipSetDevice(h->device));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipMemcpy(h->ctx.counter, &v, 8, hipMemcpyHostToDevice));
+  return KSIM_OK;
+}
+
+}  // extern "C"

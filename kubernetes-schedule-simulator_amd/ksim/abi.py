@@ -1,0 +1,199 @@
+"""ctypes binding of libksim.so (include/ksim.h).  This is the only module that touches
+the native library; it fails loudly when the library is missing — there is no CPU
+fallback on the product path."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libksim.so")
+
+KSIM_OK = 0
+E_INVAL, E_DEVICE, E_NOMEM, E_UNSUPPORTED, E_STATE, E_OVERFLOW = -1, -2, -3, -4, -5, -6
+MAX_SCALAR = 8
+MAX_RCLASS = 16
+NREASONS = 24
+
+# predicate bits
+P_CHECK_NODE_CONDITION = 1 << 0
+P_CHECK_NODE_UNSCHEDULABLE = 1 << 1
+P_GENERAL = 1 << 2
+P_HOSTNAME = 1 << 3
+P_HOST_PORTS = 1 << 4
+P_NODE_SELECTOR = 1 << 5
+P_RESOURCES = 1 << 6
+P_TAINTS = 1 << 7
+P_NOEXEC_TAINTS = 1 << 8
+P_MEM_PRESSURE = 1 << 9
+P_DISK_PRESSURE = 1 << 10
+
+W_LEAST, W_MOST, W_BALANCED, W_TAINT_TOL, W_NODE_AFF = range(5)
+NW = 5
+
+N_NOT_READY, N_OUT_OF_DISK, N_NET_UNAVAIL, N_UNSCHEDULABLE = 1, 2, 4, 8
+N_MEM_PRESSURE, N_DISK_PRESSURE = 16, 32
+
+POD_ANY_REQUEST, POD_BEST_EFFORT, POD_NEED_SELECTOR, POD_NEED_TAINTS = 1, 2, 4, 8
+
+MODE_AUTO, MODE_LAUNCH, MODE_PERSISTENT = 0, 1, 2
+
+R_NOT_READY, R_OUT_OF_DISK, R_NET_UNAVAIL, R_UNSCHEDULABLE = 0, 1, 2, 3
+R_PODS, R_CPU, R_MEMORY, R_GPU, R_EPHEMERAL = 4, 5, 6, 7, 8
+R_HOSTNAME, R_HOST_PORTS, R_NODE_SELECTOR, R_TAINTS = 9, 10, 11, 12
+R_MEM_PRESSURE, R_DISK_PRESSURE = 13, 14
+R_SCALAR0 = 16
+
+_i64p = C.POINTER(C.c_int64)
+_i32p = C.POINTER(C.c_int32)
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+_u8p = C.POINTER(C.c_uint8)
+
+
+class Config(C.Structure):
+    _fields_ = [("device", C.c_int32), ("mode", C.c_int32), ("predicates", C.c_uint32),
+                ("weights", C.c_int64 * NW), ("no_priorities", C.c_int32), ("collect_reasons", C.c_int32),
+                ("const_score", C.c_int64), ("last_node_index", C.c_uint64)]
+
+
+class NodeTable(C.Structure):
+    _fields_ = [("n_nodes", C.c_int64), ("n_scalar", C.c_int32), ("port_slots", C.c_int32),
+                ("alloc_cpu", _i64p), ("alloc_mem", _i64p), ("alloc_gpu", _i64p), ("alloc_eph", _i64p),
+                ("allowed_pods", _i32p), ("flags", _u32p), ("label_set", _i32p), ("taint_set", _i32p),
+                ("alloc_scalar", _i64p), ("req_cpu", _i64p), ("req_mem", _i64p), ("req_gpu", _i64p),
+                ("req_eph", _i64p), ("nz_cpu", _i64p), ("nz_mem", _i64p), ("pod_count", _i32p),
+                ("req_scalar", _i64p), ("ports", _u64p), ("port_count", _i32p)]
+
+
+class ClassTables(C.Structure):
+    _fields_ = [("n_classes", C.c_int32), ("n_label_sets", C.c_int32), ("n_taint_sets", C.c_int32),
+                ("sel_ok", _u32p), ("taint_ok", _u32p), ("noexec_ok", _u32p), ("tt_class", _u8p),
+                ("na_class", _u8p), ("n_tt", _i32p), ("n_na", _i32p), ("tt_val", _i64p), ("na_val", _i64p)]
+
+
+class Pod(C.Structure):
+    _fields_ = [("req_cpu", C.c_int64), ("req_mem", C.c_int64), ("req_gpu", C.c_int64), ("req_eph", C.c_int64),
+                ("add_cpu", C.c_int64), ("add_mem", C.c_int64), ("add_gpu", C.c_int64), ("add_eph", C.c_int64),
+                ("nz_cpu", C.c_int64), ("nz_mem", C.c_int64), ("cls", C.c_int32), ("host", C.c_int32),
+                ("flags", C.c_uint32), ("port_off", C.c_int32), ("port_cnt", C.c_int32),
+                ("scalar_off", C.c_int32), ("scalar_cnt", C.c_int32), ("reserved", C.c_int32 * 5)]
+
+
+class ScalarReq(C.Structure):
+    _fields_ = [("col", C.c_int32), ("pad", C.c_int32), ("req", C.c_int64), ("add", C.c_int64)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("pods", C.c_int64), ("scheduled", C.c_int64), ("node_evals", C.c_int64),
+                ("device_ms", C.c_double), ("kernel_ms", C.c_double), ("kernel_launches", C.c_int64),
+                ("mode", C.c_int32), ("blocks", C.c_int32)]
+
+
+class NodeState(C.Structure):
+    _fields_ = [("req_cpu", _i64p), ("req_mem", _i64p), ("req_gpu", _i64p), ("req_eph", _i64p),
+                ("nz_cpu", _i64p), ("nz_mem", _i64p), ("pod_count", _i32p), ("req_scalar", _i64p),
+                ("ports", _u64p), ("port_count", _i32p)]
+
+
+# numpy dtype matching ksim_pod (128 B) so pod queues are built vectorised
+POD_DTYPE = np.dtype([("req_cpu", "<i8"), ("req_mem", "<i8"), ("req_gpu", "<i8"), ("req_eph", "<i8"),
+                      ("add_cpu", "<i8"), ("add_mem", "<i8"), ("add_gpu", "<i8"), ("add_eph", "<i8"),
+                      ("nz_cpu", "<i8"), ("nz_mem", "<i8"), ("cls", "<i4"), ("host", "<i4"), ("flags", "<u4"),
+                      ("port_off", "<i4"), ("port_cnt", "<i4"), ("scalar_off", "<i4"), ("scalar_cnt", "<i4"),
+                      ("reserved", "<i4", (5,))])
+SCALAR_DTYPE = np.dtype([("col", "<i4"), ("pad", "<i4"), ("req", "<i8"), ("add", "<i8")])
+assert POD_DTYPE.itemsize == C.sizeof(Pod) == 128
+assert SCALAR_DTYPE.itemsize == C.sizeof(ScalarReq)
+
+EXPORTS = ["ksim_abi_version", "ksim_last_error", "ksim_create", "ksim_destroy", "ksim_load_nodes",
+           "ksim_load_classes", "ksim_load_pods", "ksim_schedule", "ksim_evaluate", "ksim_assume",
+           "ksim_read_nodes", "ksim_get_counter", "ksim_set_counter"]
+
+
+class KsimError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("ksim error %d: %s" % (code, msg))
+        self.code = code
+
+
+class KsimUnsupported(KsimError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    """Load libksim.so (raises if it was not built — the product has no fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError("libksim.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+    L = C.CDLL(LIB_PATH)
+    L.ksim_abi_version.restype = C.c_int
+    L.ksim_last_error.restype = C.c_char_p
+    L.ksim_last_error.argtypes = [C.c_void_p]
+    L.ksim_create.argtypes = [C.POINTER(Config), C.POINTER(C.c_void_p)]
+    L.ksim_destroy.argtypes = [C.c_void_p]
+    L.ksim_destroy.restype = None
+    L.ksim_load_nodes.argtypes = [C.c_void_p, C.POINTER(NodeTable)]
+    L.ksim_load_classes.argtypes = [C.c_void_p, C.POINTER(ClassTables)]
+    L.ksim_load_pods.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
+    L.ksim_schedule.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p, C.POINTER(Stats)]
+    L.ksim_evaluate.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]
+    L.ksim_assume.argtypes = [C.c_void_p, C.c_int64, C.c_int64]
+    L.ksim_read_nodes.argtypes = [C.c_void_p, C.POINTER(NodeState)]
+    L.ksim_get_counter.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
+    L.ksim_set_counter.argtypes = [C.c_void_p, C.c_uint64]
+    for name in EXPORTS:
+        if name not in ("ksim_destroy", "ksim_last_error", "ksim_abi_version") and getattr(L, name).restype is C.c_int:
+            pass
+    if L.ksim_abi_version() != 1:
+        raise ImportError("libksim.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def ptr(a, ctype):
+    if a is None:
+        return None
+    return a.ctypes.data_as(C.POINTER(ctype))
+
+
+def vptr(a):
+    return None if a is None else C.c_void_p(a.ctypes.data)
+
+
+class Handle:
+    """RAII wrapper around ksim_handle* (one per device / host thread)."""
+
+    def __init__(self, cfg: Config):
+        self._L = lib()
+        h = C.c_void_p()
+        self._check(self._L.ksim_create(C.byref(cfg), C.byref(h)), None)
+        self.h = h
+        self._keep = []
+
+    def _check(self, rc, h):
+        if rc != KSIM_OK:
+            msg = self._L.ksim_last_error(h).decode(errors="replace")
+            cls = KsimUnsupported if rc == E_UNSUPPORTED else KsimError
+            raise cls(rc, msg)
+
+    def call(self, fn, *args):
+        self._check(getattr(self._L, fn)(self.h, *args), self.h)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self._L.ksim_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

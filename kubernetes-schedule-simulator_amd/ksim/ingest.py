@@ -1,0 +1,458 @@
+"""Snapshot ingest: Kubernetes-shaped v1.Node / v1.Pod objects → the device layout.
+
+Nodes become a struct-of-arrays table in ascending bytewise name order (so a node index is
+its name rank, which is what selectHost's tie order needs).  Strings never reach the
+device: label sets, taint sets, scalar resource names, host IPs and protocols are interned
+here, and every string comparison the scheduler makes (label selectors, tolerations) is
+evaluated once per (pod class, label set / taint set) into bit and byte tables.
+
+Reference semantics implemented here (file:line under vendor/k8s.io/kubernetes/pkg/scheduler/):
+- NodeInfo.SetNode (schedulercache/node_info.go:429-448), Resource.Add (:86-109)
+- NodeInfo.AddPod for pods already running (node_info.go:318-341, calculateResource :400-412)
+- GetResourceRequest (algorithm/predicates/predicates.go:659-697)
+- GetNonzeroRequests (algorithm/priorities/util/non_zero.go:38-53)
+- isPodBestEffort → GetPodQOS (K/pkg/apis/core/v1/helper/qos/qos.go:39-85)
+- GetContainerPorts + HostPortInfo sanitising (util/utils.go:31-155)
+- CheckNodeConditionPredicate's condition rules (predicates.go:1534-1568)
+- podMatchesNodeLabels (predicates.go:795-838), PodToleratesNodeTaints (:1465-1494),
+  ToleratesTaint (vendor/k8s.io/api/core/v1/toleration.go:37-56)
+- TaintToleration / NodeAffinity priority map values (priorities/taint_toleration.go:29-73,
+  priorities/node_affinity.go:34-75)
+"""
+from __future__ import annotations
+
+import json
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi, labels, quantity
+
+CPU, MEM, GPU, EPH, PODS = "cpu", "memory", "alpha.kubernetes.io/nvidia-gpu", "ephemeral-storage", "pods"
+DEFAULT_MILLI_CPU = 100
+DEFAULT_MEMORY = 200 * 1024 * 1024
+PREFER_AVOID_ANNOTATION = "scheduler.alpha.kubernetes.io/preferAvoidPods"
+_UNSUPPORTED_VOLUMES = ("gcePersistentDisk", "awsElasticBlockStore", "rbd", "iscsi", "azureDisk",
+                        "persistentVolumeClaim")
+
+
+class Unsupported(abi.KsimUnsupported):
+    def __init__(self, msg):
+        super().__init__(abi.E_UNSUPPORTED, msg)
+
+
+def is_scalar_resource(name: str) -> bool:
+    """IsScalarResourceName (K/pkg/apis/core/v1/helper/helpers.go:38-96)."""
+    if name.startswith("hugepages-"):
+        return True
+    if "/" not in name or "kubernetes.io/" in name or name.startswith("requests."):
+        return False
+    return labels.qualified_name("requests." + name)
+
+
+class ResourceVec:
+    """schedulercache.Resource; scalar keeps map *presence* (a zero entry still counts)."""
+    __slots__ = ("cpu", "mem", "gpu", "eph", "pods", "scalar")
+
+    def __init__(self):
+        self.cpu = self.mem = self.gpu = self.eph = self.pods = 0
+        self.scalar = {}
+
+    def add(self, rl):
+        for name, q in (rl or {}).items():
+            if name == CPU:
+                self.cpu += quantity.milli_value(q)
+            elif name == MEM:
+                self.mem += quantity.value(q)
+            elif name == GPU:
+                self.gpu += quantity.value(q)
+            elif name == PODS:
+                self.pods += quantity.value(q)
+            elif name == EPH:
+                self.eph += quantity.value(q)
+            elif is_scalar_resource(name):
+                self.scalar[name] = self.scalar.get(name, 0) + quantity.value(q)
+
+
+def _spec(obj):
+    return obj.get("spec") or {}
+
+
+def _meta(obj):
+    return obj.get("metadata") or {}
+
+
+def _reqs(c):
+    return (c.get("resources") or {}).get("requests") or {}
+
+
+def container_requests(pod):
+    """(predicate request, commit delta, nz cpu, nz mem) of a pod."""
+    spec = _spec(pod)
+    pred, add = ResourceVec(), ResourceVec()
+    nzc = nzm = 0
+    for c in spec.get("containers") or []:
+        r = _reqs(c)
+        pred.add(r)
+        add.add(r)
+        nzc += DEFAULT_MILLI_CPU if CPU not in r else quantity.milli_value(r[CPU])
+        nzm += DEFAULT_MEMORY if MEM not in r else quantity.value(r[MEM])
+    for c in spec.get("initContainers") or []:
+        for name, q in _reqs(c).items():
+            if name == MEM:
+                pred.mem = max(pred.mem, quantity.value(q))
+            elif name == EPH:
+                pred.eph = max(pred.eph, quantity.value(q))
+            elif name == CPU:
+                pred.cpu = max(pred.cpu, quantity.milli_value(q))
+            elif name == GPU:
+                pred.gpu = max(pred.gpu, quantity.value(q))
+            elif is_scalar_resource(name):
+                v = quantity.value(q)
+                if v > pred.scalar.get(name, 0):
+                    pred.scalar[name] = v
+    return pred, add, nzc, nzm
+
+
+def best_effort(pod) -> bool:
+    for c in _spec(pod).get("containers") or []:
+        res = c.get("resources") or {}
+        for rl in (res.get("requests") or {}, res.get("limits") or {}):
+            for name, q in rl.items():
+                if name in (CPU, MEM) and quantity.positive(q):
+                    return False
+    return True
+
+
+def host_ports(pod):
+    """[(ip, proto, port)] with HostPortInfo sanitising; port <= 0 never conflicts and is
+    never recorded (utils.go:45-48, :101-104), so it is dropped here."""
+    out = []
+    for c in _spec(pod).get("containers") or []:
+        for p in c.get("ports") or []:
+            port = int(p.get("hostPort") or 0)
+            if port <= 0:
+                continue
+            out.append((p.get("hostIP") or "0.0.0.0", p.get("protocol") or "TCP", port))
+    return out
+
+
+def tolerates(tol, taint) -> bool:
+    eff = tol.get("effect") or ""
+    if eff and eff != (taint.get("effect") or ""):
+        return False
+    key = tol.get("key") or ""
+    if key and key != (taint.get("key") or ""):
+        return False
+    op = tol.get("operator") or ""
+    if op in ("", "Equal"):
+        return (tol.get("value") or "") == (taint.get("value") or "")
+    return op == "Exists"
+
+
+def check_pod_supported(pod, where="pod"):
+    spec = _spec(pod)
+    aff = spec.get("affinity") or {}
+    if aff.get("podAffinity") or aff.get("podAntiAffinity"):
+        raise Unsupported("%s %r: inter-pod affinity is outside the supported key set" % (where, _meta(pod).get("name")))
+    for v in spec.get("volumes") or []:
+        for k in _UNSUPPORTED_VOLUMES:
+            if v.get(k) is not None:
+                raise Unsupported("%s %r: %s volumes are outside the supported key set" % (where, _meta(pod).get("name"), k))
+
+
+@dataclass
+class Interner:
+    ids: dict = field(default_factory=dict)
+    items: list = field(default_factory=list)
+
+    def get(self, key, item=None):
+        i = self.ids.get(key)
+        if i is None:
+            i = len(self.items)
+            self.ids[key] = i
+            self.items.append(key if item is None else item)
+        return i
+
+
+def _canon(x):
+    return json.dumps(x, sort_keys=True, separators=(",", ":"))
+
+
+class Cluster:
+    """Node table + pod queue in device layout.  Build with from_objects() or from arrays."""
+
+    def __init__(self):
+        self.names = []
+        self.index = {}
+        self.cols = {}
+        self.label_sets = Interner()
+        self.taint_sets = Interner()
+        self.scalar_names = Interner()
+        self.ips = Interner()
+        self.protos = Interner()
+        self.port_slots = 0
+        self.classes = Interner()
+        self.class_specs = []
+        self.pods = None
+        self.pod_ports = np.zeros(0, np.uint64)
+        self.pod_scalars = np.zeros(0, abi.SCALAR_DTYPE)
+        self.pod_names = []
+        self.tables = None
+        self.prefer_avoid_nodes = False
+        self.bad_affinity_classes = set()   # preferred terms that fail to parse
+
+    # ------------------------------------------------------------------ nodes
+    @classmethod
+    def from_objects(cls, nodes, running_pods=(), pods=(), port_slots=None):
+        """nodes / running_pods / pods: Kubernetes-shaped dicts; pods are in SCHEDULING
+        order (the caller resolves the simulator's LIFO queue)."""
+        self = cls()
+        self.ips.get("0.0.0.0")     # id 0 = wildcard
+        self.protos.get("TCP")      # id 0 = default protocol
+        nodes = sorted(nodes, key=lambda n: _meta(n).get("name", "").encode())
+        n = len(nodes)
+        self.names = [_meta(x).get("name", "") for x in nodes]
+        if len(set(self.names)) != n:
+            raise abi.KsimError(abi.E_INVAL, "duplicate node names")
+        self.index = {nm: i for i, nm in enumerate(self.names)}
+        running = [p for p in running_pods if _spec(p).get("nodeName") in self.index]
+        for p in running:
+            check_pod_supported(p, "running pod")
+        # scalar columns: every scalar name any node or pod mentions
+        for x in nodes:
+            for name in ((x.get("status") or {}).get("allocatable") or {}):
+                if is_scalar_resource(name):
+                    self.scalar_names.get(name)
+        compiled = []
+        for p in list(running) + list(pods):
+            pred, add, nzc, nzm = container_requests(p)
+            for name in list(pred.scalar) + list(add.scalar):
+                self.scalar_names.get(name)
+            compiled.append((pred, add, nzc, nzm))
+        if len(self.scalar_names.items) > abi.MAX_SCALAR:
+            raise Unsupported("more than %d scalar resources" % abi.MAX_SCALAR)
+        S = len(self.scalar_names.items)
+        z64 = lambda: np.zeros(n, np.int64)
+        c = dict(alloc_cpu=z64(), alloc_mem=z64(), alloc_gpu=z64(), alloc_eph=z64(),
+                 allowed_pods=np.zeros(n, np.int32), flags=np.zeros(n, np.uint32),
+                 label_set=np.zeros(n, np.int32), taint_set=np.zeros(n, np.int32),
+                 alloc_scalar=np.zeros((S, n), np.int64), req_cpu=z64(), req_mem=z64(), req_gpu=z64(),
+                 req_eph=z64(), nz_cpu=z64(), nz_mem=z64(), pod_count=np.zeros(n, np.int32),
+                 req_scalar=np.zeros((S, n), np.int64))
+        node_taints = []
+        for i, x in enumerate(nodes):
+            st, sp, md = x.get("status") or {}, _spec(x), _meta(x)
+            r = ResourceVec()
+            r.add(st.get("allocatable") or {})
+            c["alloc_cpu"][i], c["alloc_mem"][i], c["alloc_gpu"][i], c["alloc_eph"][i] = r.cpu, r.mem, r.gpu, r.eph
+            c["allowed_pods"][i] = r.pods
+            for name, v in r.scalar.items():
+                c["alloc_scalar"][self.scalar_names.ids[name], i] = v
+            f = 0
+            for cond in st.get("conditions") or []:
+                t, s = cond.get("type"), cond.get("status")
+                if t == "Ready" and s != "True":
+                    f |= abi.N_NOT_READY
+                elif t == "OutOfDisk" and s != "False":
+                    f |= abi.N_OUT_OF_DISK
+                elif t == "NetworkUnavailable" and s != "False":
+                    f |= abi.N_NET_UNAVAIL
+                if t == "MemoryPressure":    # SetNode keeps the last such condition
+                    f = (f | abi.N_MEM_PRESSURE) if s == "True" else (f & ~abi.N_MEM_PRESSURE)
+                elif t == "DiskPressure":
+                    f = (f | abi.N_DISK_PRESSURE) if s == "True" else (f & ~abi.N_DISK_PRESSURE)
+            if sp.get("unschedulable"):
+                f |= abi.N_UNSCHEDULABLE
+            c["flags"][i] = f
+            lab = md.get("labels") or {}
+            c["label_set"][i] = self.label_sets.get(_canon(lab), dict(lab))
+            taints = [{"key": t.get("key") or "", "value": t.get("value") or "", "effect": t.get("effect") or ""}
+                      for t in (sp.get("taints") or [])]
+            c["taint_set"][i] = self.taint_sets.get(_canon(taints), taints)
+            if PREFER_AVOID_ANNOTATION in (md.get("annotations") or {}):
+                self.prefer_avoid_nodes = True
+            node_taints.append(taints)
+        # running pods: NodeInfo.AddPod
+        used_ports = [dict() for _ in range(n)]
+        for p, (pred, add, nzc, nzm) in zip(running, compiled[:len(running)]):
+            i = self.index[_spec(p)["nodeName"]]
+            c["req_cpu"][i] += add.cpu
+            c["req_mem"][i] += add.mem
+            c["req_gpu"][i] += add.gpu
+            c["req_eph"][i] += add.eph
+            for name, v in add.scalar.items():
+                c["req_scalar"][self.scalar_names.ids[name], i] += v
+            c["nz_cpu"][i] += nzc
+            c["nz_mem"][i] += nzm
+            c["pod_count"][i] += 1
+            for ip, proto, port in host_ports(p):
+                used_ports[i][abi_port_key(self.ips.get(ip), self.protos.get(proto), port)] = True
+        self.cols = c
+        # pod queue
+        self._compile_pods(list(pods), compiled[len(running):])
+        # port slots: enough for everything that could land on one node
+        need = max([len(u) for u in used_ports] + [0])
+        if self.pods is not None and len(self.pods):
+            per_pod = int(self.pods["port_cnt"].max()) if len(self.pods) else 0
+            if per_pod:
+                distinct = len(set(int(k) for k in self.pod_ports))
+                need += distinct
+        self.port_slots = int(port_slots if port_slots is not None else max(need, 0))
+        P = self.port_slots
+        ports = np.zeros((P, n), np.uint64)
+        pc = np.zeros(n, np.int32)
+        for i, u in enumerate(used_ports):
+            if len(u) > P:
+                raise abi.KsimError(abi.E_INVAL, "port_slots too small for running pods")
+            for s, k in enumerate(u):
+                ports[s, i] = k
+            pc[i] = len(u)
+        c["ports"], c["port_count"] = ports, pc
+        self._build_tables()
+        return self
+
+    # ------------------------------------------------------------------- pods
+    def _compile_pods(self, pods, compiled):
+        m = len(pods)
+        arr = np.zeros(m, abi.POD_DTYPE)
+        ports, scalars = [], []
+        self.pod_names = []
+        for k, (p, (pred, add, nzc, nzm)) in enumerate(zip(pods, compiled)):
+            check_pod_supported(p)
+            spec, md = _spec(p), _meta(p)
+            if self.prefer_avoid_nodes:
+                for o in md.get("ownerReferences") or []:
+                    if o.get("controller") and o.get("kind") in ("ReplicationController", "ReplicaSet"):
+                        raise Unsupported("NodePreferAvoidPods with RC/RS-owned pods and preferAvoidPods annotations")
+            self.pod_names.append(md.get("name", ""))
+            row = arr[k]
+            row["req_cpu"], row["req_mem"], row["req_gpu"], row["req_eph"] = pred.cpu, pred.mem, pred.gpu, pred.eph
+            row["add_cpu"], row["add_mem"], row["add_gpu"], row["add_eph"] = add.cpu, add.mem, add.gpu, add.eph
+            row["nz_cpu"], row["nz_mem"] = nzc, nzm
+            flags = 0
+            if pred.cpu or pred.mem or pred.gpu or pred.eph or pred.scalar:
+                flags |= abi.POD_ANY_REQUEST
+            if best_effort(p):
+                flags |= abi.POD_BEST_EFFORT
+            nn = spec.get("nodeName") or ""
+            row["host"] = -1 if not nn else self.index.get(nn, -2)
+            key = _canon({"ns": spec.get("nodeSelector") or {}, "na": (spec.get("affinity") or {}).get("nodeAffinity"),
+                          "tol": spec.get("tolerations") or []})
+            row["cls"] = self.classes.get(key, spec)
+            row["flags"] = flags
+            hp = host_ports(p)
+            row["port_off"], row["port_cnt"] = len(ports), len(hp)
+            for ip, proto, port in hp:
+                ports.append(abi_port_key(self.ips.get(ip), self.protos.get(proto), port))
+            row["scalar_off"], row["scalar_cnt"] = len(scalars), len(pred.scalar)
+            for name, v in pred.scalar.items():
+                scalars.append((self.scalar_names.ids[name], 0, v, add.scalar.get(name, 0)))
+        self.pods = arr
+        self.pod_ports = np.array(ports, np.uint64)
+        self.pod_scalars = np.array(scalars, abi.SCALAR_DTYPE) if scalars else np.zeros(0, abi.SCALAR_DTYPE)
+
+    # ----------------------------------------------------------------- tables
+    def _build_tables(self):
+        L, T = len(self.label_sets.items), len(self.taint_sets.items)
+        specs = self.classes.items or [{}]
+        Cn = len(specs)
+        lw, tw = (L + 31) // 32, (T + 31) // 32
+        sel = np.zeros((Cn, lw), np.uint32)
+        tok = np.zeros((Cn, tw), np.uint32)
+        nok = np.zeros((Cn, tw), np.uint32)
+        ttc = np.zeros((Cn, T), np.uint8)
+        nac = np.zeros((Cn, L), np.uint8)
+        ntt = np.ones(Cn, np.int32)
+        nna = np.ones(Cn, np.int32)
+        ttv = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
+        nav = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
+        need = np.zeros(Cn, np.uint32)
+        for k, spec in enumerate(specs):
+            tols = spec.get("tolerations") or []
+            prefer_tols = [t for t in tols if (t.get("effect") or "") in ("", "PreferNoSchedule")]
+            all_sel = all_taint = True
+            weights = []
+            for li, lab in enumerate(self.label_sets.items):
+                ok = labels.pod_matches_node_labels(spec, lab)
+                if ok:
+                    sel[k, li >> 5] |= np.uint32(1 << (li & 31))
+                all_sel &= ok
+                try:
+                    weights.append(labels.preferred_weight(spec, lab))
+                except labels.SelectorError:
+                    # CalculateNodeAffinityPriorityMap returns an error: only fatal when
+                    # NodeAffinityPriority is configured (checked by the scheduler layer)
+                    self.bad_affinity_classes.add(k)
+                    weights.append(0)
+            counts = []
+            for ti, taints in enumerate(self.taint_sets.items):
+                ok = all(any(tolerates(t, x) for t in tols) for x in taints
+                         if x["effect"] in ("NoSchedule", "NoExecute"))
+                ok2 = all(any(tolerates(t, x) for t in tols) for x in taints if x["effect"] == "NoExecute")
+                if ok:
+                    tok[k, ti >> 5] |= np.uint32(1 << (ti & 31))
+                if ok2:
+                    nok[k, ti >> 5] |= np.uint32(1 << (ti & 31))
+                all_taint &= ok and ok2
+                counts.append(sum(1 for x in taints if x["effect"] == "PreferNoSchedule"
+                                  and not any(tolerates(t, x) for t in prefer_tols)))
+            tv = sorted(set(counts))
+            av = sorted(set(weights))
+            if len(tv) * len(av) > abi.MAX_RCLASS:
+                raise Unsupported("pod class needs %d x %d reduce classes (> %d)" % (len(tv), len(av), abi.MAX_RCLASS))
+            ntt[k], nna[k] = len(tv), len(av)
+            ttv[k, :len(tv)] = tv
+            nav[k, :len(av)] = av
+            ttc[k, :] = [tv.index(x) for x in counts]
+            nac[k, :] = [av.index(x) for x in weights]
+            f = 0
+            if not all_sel:
+                f |= abi.POD_NEED_SELECTOR
+            if not all_taint:
+                f |= abi.POD_NEED_TAINTS
+            need[k] = f
+        self.tables = dict(n_classes=Cn, n_label_sets=L, n_taint_sets=T, sel_ok=sel, taint_ok=tok, noexec_ok=nok,
+                           tt_class=ttc, na_class=nac, n_tt=ntt, n_na=nna, tt_val=ttv, na_val=nav)
+        if self.pods is not None and len(self.pods):
+            self.pods["flags"] |= need[self.pods["cls"]]
+
+    # ------------------------------------------------------------ ABI structs
+    def node_table(self):
+        c = self.cols
+        t = abi.NodeTable()
+        t.n_nodes = len(self.names) if self.names else len(c["alloc_cpu"])
+        t.n_scalar = c["alloc_scalar"].shape[0]
+        t.port_slots = self.port_slots
+        for name, ct in (("alloc_cpu", abi.C.c_int64), ("alloc_mem", abi.C.c_int64), ("alloc_gpu", abi.C.c_int64),
+                         ("alloc_eph", abi.C.c_int64), ("allowed_pods", abi.C.c_int32), ("flags", abi.C.c_uint32),
+                         ("label_set", abi.C.c_int32), ("taint_set", abi.C.c_int32), ("alloc_scalar", abi.C.c_int64),
+                         ("req_cpu", abi.C.c_int64), ("req_mem", abi.C.c_int64), ("req_gpu", abi.C.c_int64),
+                         ("req_eph", abi.C.c_int64), ("nz_cpu", abi.C.c_int64), ("nz_mem", abi.C.c_int64),
+                         ("pod_count", abi.C.c_int32), ("req_scalar", abi.C.c_int64), ("ports", abi.C.c_uint64),
+                         ("port_count", abi.C.c_int32)):
+            a = c.get(name)
+            if a is not None:
+                a = np.ascontiguousarray(a)
+                c[name] = a
+                setattr(t, name, abi.ptr(a, ct))
+        return t
+
+    def class_tables(self):
+        d = self.tables
+        t = abi.ClassTables()
+        t.n_classes, t.n_label_sets, t.n_taint_sets = d["n_classes"], d["n_label_sets"], d["n_taint_sets"]
+        for name, ct in (("sel_ok", abi.C.c_uint32), ("taint_ok", abi.C.c_uint32), ("noexec_ok", abi.C.c_uint32),
+                         ("tt_class", abi.C.c_uint8), ("na_class", abi.C.c_uint8), ("n_tt", abi.C.c_int32),
+                         ("n_na", abi.C.c_int32), ("tt_val", abi.C.c_int64), ("na_val", abi.C.c_int64)):
+            d[name] = np.ascontiguousarray(d[name])
+            setattr(t, name, abi.ptr(d[name], ct))
+        return t
+
+    @property
+    def n_nodes(self):
+        return len(self.cols["alloc_cpu"])
+
+
+def abi_port_key(ip_id, proto_id, port):
+    return (int(ip_id) << 40) | (int(proto_id) << 32) | (int(port) & 0xFFFFFFFF)

@@ -1,0 +1,297 @@
+"""Host-side mirror of the reference's ScheduleAlgorithm plugin surface and simulator loop.
+
+- Predicate / priority key sets and weights, exactly as the algorithm providers register
+  them (vendor/k8s.io/kubernetes/pkg/scheduler/algorithmprovider/defaults/defaults.go:
+  113-259, the TalkintDataProvider added at :36,214-216) or as a Policy lists them.
+  Every supported key maps to a kernel feature bit or weight slot; any other key raises
+  Unsupported (never a silently different result).
+- GenericScheduler: the batch form of genericScheduler.Schedule + Scheduler.assume over a
+  device-resident cluster (core/generic_scheduler.go:112-198, scheduler.go:366).
+- FitError: message format of core/generic_scheduler.go:72-90.
+- ClusterCapacity: the simulator's loop (pkg/scheduler/simulator.go:108-223): pods are
+  popped LIFO from the expanded pod list (pkg/framework/store/store.go:223-233), each is
+  scheduled and committed before the next; unschedulable pods are recorded and the run
+  continues until the queue is empty.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass, field
+
+import numpy as np
+
+from . import abi
+from .ingest import Cluster, Unsupported
+
+# predicates.go:129-138 keys → kernel bits
+PREDICATE_BITS = {
+    "CheckNodeCondition": abi.P_CHECK_NODE_CONDITION,
+    "CheckNodeUnschedulable": abi.P_CHECK_NODE_UNSCHEDULABLE,
+    "GeneralPredicates": abi.P_GENERAL,
+    "HostName": abi.P_HOSTNAME,
+    "PodFitsHostPorts": abi.P_HOST_PORTS,
+    "MatchNodeSelector": abi.P_NODE_SELECTOR,
+    "PodFitsResources": abi.P_RESOURCES,
+    "PodToleratesNodeTaints": abi.P_TAINTS,
+    "PodToleratesNodeNoExecuteTaints": abi.P_NOEXEC_TAINTS,
+    "CheckNodeMemoryPressure": abi.P_MEM_PRESSURE,
+    "CheckNodeDiskPressure": abi.P_DISK_PRESSURE,
+}
+# keys that are true for every pod ingest accepts (no volumes of those kinds, no inter-pod
+# affinity); "PodFitsPorts" is registered but absent from predicatesOrdering, so it never runs
+TRIVIAL_PREDICATES = {"NoDiskConflict", "MaxEBSVolumeCount", "MaxGCEPDVolumeCount", "MaxAzureDiskVolumeCount",
+                      "CheckVolumeBinding", "NoVolumeZoneConflict", "MatchInterPodAffinity", "PodFitsPorts"}
+
+PRIORITY_SLOTS = {"LeastRequestedPriority": abi.W_LEAST, "MostRequestedPriority": abi.W_MOST,
+                  "BalancedResourceAllocation": abi.W_BALANCED, "TaintTolerationPriority": abi.W_TAINT_TOL,
+                  "NodeAffinityPriority": abi.W_NODE_AFF}
+# value on every node under supported inputs (no services/controllers in the simulator's store,
+# no RC/RS-owned pods next to preferAvoidPods annotations, no affinity terms)
+CONST_PRIORITIES = {"SelectorSpreadPriority": 10, "ServiceSpreadingPriority": 10, "NodePreferAvoidPodsPriority": 10,
+                    "InterPodAffinityPriority": 0, "EqualPriority": 1}
+
+DEFAULT_PREDICATES = ("NoVolumeZoneConflict", "MaxEBSVolumeCount", "MaxGCEPDVolumeCount", "MaxAzureDiskVolumeCount",
+                      "MatchInterPodAffinity", "NoDiskConflict", "GeneralPredicates", "CheckNodeMemoryPressure",
+                      "CheckNodeDiskPressure", "CheckNodeCondition", "PodToleratesNodeTaints", "CheckVolumeBinding")
+DEFAULT_PRIORITIES = (("SelectorSpreadPriority", 1), ("InterPodAffinityPriority", 1), ("LeastRequestedPriority", 1),
+                      ("BalancedResourceAllocation", 1), ("NodePreferAvoidPodsPriority", 10000),
+                      ("NodeAffinityPriority", 1), ("TaintTolerationPriority", 1))
+PROVIDERS = ("DefaultProvider", "ClusterAutoscalerProvider", "TalkintDataProvider")
+
+
+def provider(name: str):
+    """registerAlgorithmProvider (defaults.go:207-217)."""
+    if name not in PROVIDERS:
+        raise Unsupported("algorithm provider %r is not registered" % name)
+    pri = list(DEFAULT_PRIORITIES)
+    if name != "DefaultProvider":  # copyAndReplace(LeastRequested → MostRequested)
+        pri = [("MostRequestedPriority", w) if n == "LeastRequestedPriority" else (n, w) for n, w in pri]
+    return list(DEFAULT_PREDICATES), pri
+
+
+def make_config(predicates, priorities, device=0, mode=abi.MODE_AUTO, collect_reasons=True, last_node_index=0):
+    cfg = abi.Config()
+    cfg.device = device
+    cfg.mode = mode
+    bits = 0
+    for k in predicates:
+        if k in PREDICATE_BITS:
+            bits |= PREDICATE_BITS[k]
+        elif k not in TRIVIAL_PREDICATES:
+            raise Unsupported("predicate %r is outside the supported key set" % k)
+    cfg.predicates = bits
+    const = 0
+    seen = set()
+    for name, w in priorities:
+        if name in seen:
+            raise abi.KsimError(abi.E_INVAL, "duplicate priority %r" % name)
+        seen.add(name)
+        if w <= 0:
+            raise abi.KsimError(abi.E_INVAL, "priority %r: weight must be positive" % name)
+        if name in PRIORITY_SLOTS:
+            cfg.weights[PRIORITY_SLOTS[name]] = w
+        elif name in CONST_PRIORITIES:
+            const += CONST_PRIORITIES[name] * w
+        else:
+            raise Unsupported("priority %r is outside the supported key set" % name)
+    cfg.no_priorities = 1 if not priorities else 0
+    if not priorities:
+        const = 1
+    cfg.const_score = const
+    cfg.collect_reasons = 1 if collect_reasons else 0
+    cfg.last_node_index = last_node_index
+    return cfg
+
+
+REASON_TEXT = {
+    abi.R_NOT_READY: "node(s) were not ready",
+    abi.R_OUT_OF_DISK: "node(s) were out of disk space",
+    abi.R_NET_UNAVAIL: "node(s) had unavailable network",
+    abi.R_UNSCHEDULABLE: "node(s) were unschedulable",
+    abi.R_PODS: "Insufficient pods",
+    abi.R_CPU: "Insufficient cpu",
+    abi.R_MEMORY: "Insufficient memory",
+    abi.R_GPU: "Insufficient alpha.kubernetes.io/nvidia-gpu",
+    abi.R_EPHEMERAL: "Insufficient ephemeral-storage",
+    abi.R_HOSTNAME: "node(s) didn't match the requested hostname",
+    abi.R_HOST_PORTS: "node(s) didn't have free ports for the requested pod ports",
+    abi.R_NODE_SELECTOR: "node(s) didn't match node selector",
+    abi.R_TAINTS: "node(s) had taints that the pod didn't tolerate",
+    abi.R_MEM_PRESSURE: "node(s) had memory pressure",
+    abi.R_DISK_PRESSURE: "node(s) had disk pressure",
+}
+
+
+def reason_strings(mask: int, scalar_names=()):
+    out = []
+    for r in range(abi.NREASONS):
+        if (mask >> r) & 1:
+            out.append(reason_text(r, scalar_names))
+    return out
+
+
+def reason_text(r, scalar_names=()):
+    if r >= abi.R_SCALAR0:
+        return "Insufficient " + scalar_names[r - abi.R_SCALAR0]
+    return REASON_TEXT[r]
+
+
+def fit_error_message(num_nodes, hist, scalar_names=()):
+    """FitError.Error (core/generic_scheduler.go:72-90)."""
+    parts = sorted("%d %s" % (int(v), reason_text(r, scalar_names)) for r, v in enumerate(hist) if v)
+    return "0/%d nodes are available: %s." % (num_nodes, ", ".join(parts))
+
+
+class GenericScheduler:
+    """Batch drop-in for genericScheduler + Scheduler.assume on one MI355X."""
+
+    def __init__(self, cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO,
+                 collect_reasons=True, last_node_index=0):
+        self.cluster = cluster
+        self.predicates = list(predicates)
+        self.prioritizers = list(priorities)
+        if any(n == "NodeAffinityPriority" for n, _ in self.prioritizers) and cluster.bad_affinity_classes:
+            raise Unsupported("NodeAffinityPriority: a preferred node-affinity term does not parse")
+        self.cfg = make_config(predicates, priorities, device, mode, collect_reasons, last_node_index)
+        self.h = abi.Handle(self.cfg)
+        self.h.call("ksim_load_nodes", C.byref(cluster.node_table()))
+        self.h.call("ksim_load_classes", C.byref(cluster.class_tables()))
+        pods = np.ascontiguousarray(cluster.pods)
+        self._pods = pods
+        self.h.call("ksim_load_pods", abi.vptr(pods), len(pods), abi.vptr(cluster.pod_ports), len(cluster.pod_ports),
+                    abi.vptr(cluster.pod_scalars), len(cluster.pod_scalars))
+        self.last_stats = None
+
+    def schedule(self, first=0, count=None):
+        """Schedule + assume pods [first, first+count) in order.
+        Returns (node index per pod (-1 = FitError), reason histograms or None, stats)."""
+        n = len(self._pods)
+        count = n - first if count is None else count
+        out = np.zeros(count, np.int32)
+        reasons = np.zeros((count, abi.NREASONS), np.int32) if self.cfg.collect_reasons else None
+        st = abi.Stats()
+        self.h.call("ksim_schedule", first, count, abi.vptr(out), abi.vptr(reasons), C.byref(st))
+        self.last_stats = st
+        return out, reasons, st
+
+    def evaluate(self, pod):
+        """Per-node (fit, reason mask, map score, reduce class) for one loaded pod (no commit)."""
+        n = self.cluster.n_nodes
+        fit = np.zeros(n, np.uint8)
+        rs = np.zeros(n, np.uint32)
+        sc = np.zeros(n, np.int64)
+        rc = np.zeros(n, np.uint8)
+        self.h.call("ksim_evaluate", pod, abi.vptr(fit), abi.vptr(rs), abi.vptr(sc), abi.vptr(rc))
+        return fit.astype(bool), rs, sc, rc
+
+    def priority_scores(self, pod, over=None):
+        """Total priority score per node as PrioritizeNodes reports it (map + reduce + the
+        constant priorities) over the node subset `over` (default: fit nodes)."""
+        fit, _, sc, rc = self.evaluate(pod)
+        idx = np.nonzero(fit)[0] if over is None else np.asarray(over)
+        p = self.cluster.pods[pod]
+        t = self.cluster.tables
+        cls = int(p["cls"])
+        k2 = int(t["n_na"][cls]) if self.cfg.weights[abi.W_NODE_AFF] else 1
+        tv = t["tt_val"][cls][rc[idx] // k2]
+        av = t["na_val"][cls][rc[idx] % k2]
+        total = sc[idx].copy()
+        if self.cfg.weights[abi.W_TAINT_TOL]:
+            total += self.cfg.weights[abi.W_TAINT_TOL] * _normalize(tv, True)
+        if self.cfg.weights[abi.W_NODE_AFF]:
+            total += self.cfg.weights[abi.W_NODE_AFF] * _normalize(av, False)
+        return idx, total + self.cfg.const_score
+
+    def node_state(self):
+        n = self.cluster.n_nodes
+        S = self.cluster.cols["alloc_scalar"].shape[0]
+        P = self.cluster.port_slots
+        out = dict(req_cpu=np.zeros(n, np.int64), req_mem=np.zeros(n, np.int64), req_gpu=np.zeros(n, np.int64),
+                   req_eph=np.zeros(n, np.int64), nz_cpu=np.zeros(n, np.int64), nz_mem=np.zeros(n, np.int64),
+                   pod_count=np.zeros(n, np.int32), req_scalar=np.zeros((S, n), np.int64),
+                   ports=np.zeros((P, n), np.uint64), port_count=np.zeros(n, np.int32))
+        st = abi.NodeState()
+        for k, ct in (("req_cpu", C.c_int64), ("req_mem", C.c_int64), ("req_gpu", C.c_int64), ("req_eph", C.c_int64),
+                      ("nz_cpu", C.c_int64), ("nz_mem", C.c_int64), ("pod_count", C.c_int32),
+                      ("req_scalar", C.c_int64), ("ports", C.c_uint64), ("port_count", C.c_int32)):
+            setattr(st, k, abi.ptr(out[k], ct))
+        self.h.call("ksim_read_nodes", C.byref(st))
+        return out
+
+    @property
+    def last_node_index(self):
+        v = C.c_uint64()
+        self.h.call("ksim_get_counter", C.byref(v))
+        return v.value
+
+    def close(self):
+        self.h.close()
+
+
+def _normalize(vals, reverse):
+    """NormalizeReduce over a value vector (priorities/reduce.go:29-64)."""
+    vals = np.asarray(vals, np.int64)
+    mx = int(vals.max()) if len(vals) else 0
+    if mx == 0:
+        return np.full(len(vals), 10, np.int64) if reverse else vals.copy()
+    s = (10 * vals) // mx
+    return 10 - s if reverse else s
+
+
+# ----------------------------------------------------------------------------- simulator
+def expand_simulation_pods(spec_list, namespace=""):
+    """ParseSimulationPod (cmd/app/options/options.go:73-99).  Names are uuids in Go; here
+    they are deterministic <SimulationName>-<i>."""
+    out = []
+    for sp in spec_list:
+        for i in range(int(sp.get("num", 0))):
+            out.append({"metadata": {"name": "%s-%d" % (sp["name"], i), "namespace": namespace,
+                                     "labels": {"SimulationName": sp["name"]}},
+                        "spec": dict((sp.get("pod") or {}).get("spec") or {})})
+    return out
+
+
+def load_podspec(path):
+    """The --podspec file: a YAML or JSON list of SimulationPod{name, num, pod}
+    (pkg/api/api.go:79-83)."""
+    import yaml
+    with open(path) as f:
+        return yaml.safe_load(f)
+
+
+@dataclass
+class Report:
+    """framework.GetReport's content (pkg/framework/report.go:168-174)."""
+    successful: list = field(default_factory=list)   # (pod name, node name) in bind order
+    failed: list = field(default_factory=list)       # (pod name, FitError message)
+    stop_reason: str = "No pods left"
+    stats: object = None
+    last_node_index: int = 0
+
+
+class ClusterCapacity:
+    def __init__(self, nodes, running_pods, simulation_pods, provider_name="DefaultProvider",
+                 predicates=None, priorities=None, device=0, mode=abi.MODE_AUTO, collect_reasons=True):
+        if predicates is None or priorities is None:
+            p, q = provider(provider_name)
+            predicates = p if predicates is None else predicates
+            priorities = q if priorities is None else priorities
+        order = list(reversed(simulation_pods))   # PodQueue.Pop takes the last element
+        self.cluster = Cluster.from_objects(nodes, running_pods, order)
+        self.scheduler = GenericScheduler(self.cluster, predicates, priorities, device=device, mode=mode,
+                                          collect_reasons=collect_reasons)
+
+    def run(self) -> Report:
+        nodes, reasons, st = self.scheduler.schedule()
+        rep = Report(stats=st)
+        names = self.cluster.names
+        scal = self.cluster.scalar_names.items
+        for k, w in enumerate(nodes):
+            pod = self.cluster.pod_names[k]
+            if w >= 0:
+                rep.successful.append((pod, names[w]))
+            else:
+                msg = fit_error_message(len(names), reasons[k], scal) if reasons is not None else "unschedulable"
+                rep.failed.append((pod, msg))
+        rep.last_node_index = self.scheduler.last_node_index
+        return rep

@@ -1,0 +1,160 @@
+"""GPU parity: libksim.so (HIP, gfx950) against the CPU oracle and the golden vectors
+transcribed from the reference's Go tests.  Bit-exact is the bar for every integer result
+(placements, scores, reason histograms, node state, lastNodeIndex)."""
+import numpy as np
+import pytest
+
+import ksim_ref as R
+from golden_util import case_id, load
+from ksim import abi, ingest, scheduler
+from workloads import rnd_workload
+
+pytestmark = pytest.mark.gpu
+
+MODES = [abi.MODE_LAUNCH, abi.MODE_AUTO]
+
+
+def _sched(nodes, running, pods, preds, prios, mode=abi.MODE_AUTO, **kw):
+    cl = ingest.Cluster.from_objects(nodes, running, pods)
+    return cl, scheduler.GenericScheduler(cl, preds, prios, mode=mode, **kw)
+
+
+@pytest.mark.parametrize("c", load("priorities"), ids=case_id)
+def test_golden_priorities_on_gpu(c):
+    cl, g = _sched(c["nodes"], c["pods"], [c["pod"]], [], [(c["priority"], 1)])
+    idx, total = g.priority_scores(0, over=np.arange(cl.n_nodes))
+    got = {cl.names[i]: int(s) for i, s in zip(idx, total)}
+    assert [[h, got[h]] for h, _ in c["expect"]] == c["expect"]
+
+
+@pytest.mark.parametrize("c", load("predicates"), ids=case_id)
+def test_golden_predicates_on_gpu(c):
+    cl, g = _sched([c["node"]], c["pods"], [c["pod"]], [c["predicate"]], [("EqualPriority", 1)])
+    fit, rs, _, _ = g.evaluate(0)
+    assert bool(fit[0]) == c["fits"]
+    if not c["fits"] and c["reasons"] is not None:
+        got = scheduler.reason_strings(int(rs[0]), cl.scalar_names.items)
+        assert sorted(got) == sorted(c["reasons"])
+
+
+@pytest.mark.parametrize("c", load("prioritize"), ids=case_id)
+def test_golden_zero_request_on_gpu(c):
+    cl, g = _sched(c["nodes"], c["pods"], [c["pod"]], [], [tuple(x) for x in c["configs"]])
+    _, total = g.priority_scores(0, over=np.arange(cl.n_nodes))
+    if "expect_all_equal" in c:
+        assert all(int(s) == c["expect_all_equal"] for s in total)
+    else:
+        assert all(int(s) != c["expect_none_equal"] for s in total)
+
+
+def _oracle_run(nodes, running, pods, preds, prios):
+    out, lni = R.simulate(nodes, running, pods, set(preds), list(prios))
+    return out, lni
+
+
+def _gpu_run(nodes, running, pods, preds, prios, mode):
+    cc = scheduler.ClusterCapacity(nodes, running, pods, predicates=preds, priorities=prios, mode=mode)
+    rep = cc.run()
+    got = {}
+    for name, host in rep.successful:
+        got[name] = (host, None)
+    for name, msg in rep.failed:
+        got[name] = (None, msg)
+    return got, rep
+
+
+POLICIES = {
+    "default": scheduler.provider("DefaultProvider"),
+    "talkintdata": scheduler.provider("TalkintDataProvider"),
+    "lr_bra": (list(scheduler.DEFAULT_PREDICATES), [("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]),
+    "weighted": (["CheckNodeCondition", "PodFitsResources", "PodFitsHostPorts", "MatchNodeSelector", "HostName",
+                  "PodToleratesNodeTaints", "CheckNodeMemoryPressure"],
+                 [("MostRequestedPriority", 3), ("BalancedResourceAllocation", 2), ("TaintTolerationPriority", 5),
+                  ("NodeAffinityPriority", 2)]),
+    "equal": (["GeneralPredicates"], []),
+}
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("policy", sorted(POLICIES))
+@pytest.mark.parametrize("seed", range(4))
+def test_simulation_matches_oracle(seed, policy, mode):
+    nodes, running, pods = rnd_workload(seed, n_nodes=23 + seed * 17, n_pods=150)
+    preds, prios = POLICIES[policy]
+    want, want_lni = _oracle_run(nodes, running, pods, preds, prios)
+    got, rep = _gpu_run(nodes, running, pods, preds, prios, mode)
+    order = [name for name, _, _ in want]
+    assert [n for n, _ in rep.successful] == [n for n, h, _ in want if h is not None]  # bind order
+    for name, host, msg in want:
+        assert got[name] == (host, msg), name
+    assert rep.last_node_index == want_lni
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_round_robin_descending_names(mode):
+    """Derived pin (no reference test fixes the sequence): identical nodes, identical pods →
+    hosts visited in descending bytewise name order with period = number of ties."""
+    names = ["n-1", "n-10", "n-2"]
+    nodes = [{"metadata": {"name": n}, "status": {"allocatable": {"cpu": "100", "memory": "100Gi", "pods": "100"}}}
+             for n in names]
+    pods = [{"metadata": {"name": "p%d" % i}, "spec": {"containers": [{}]}} for i in range(6)]
+    cc = scheduler.ClusterCapacity(nodes, [], pods, predicates=["GeneralPredicates"], priorities=[("EqualPriority", 1)],
+                                   mode=mode)
+    rep = cc.run()
+    assert [h for _, h in rep.successful] == ["n-2", "n-10", "n-1"] * 2
+    assert rep.last_node_index == 6
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_single_fit_does_not_advance_counter(mode):
+    nodes = [{"metadata": {"name": "a"}, "status": {"allocatable": {"cpu": "1", "memory": "1Gi", "pods": "10"}}},
+             {"metadata": {"name": "b"}, "status": {"allocatable": {"cpu": "4", "memory": "1Gi", "pods": "10"}}}]
+    pods = [{"metadata": {"name": "big"}, "spec": {"containers": [{"resources": {"requests": {"cpu": "2"}}}]}}]
+    cc = scheduler.ClusterCapacity(nodes, [], pods, mode=mode)
+    rep = cc.run()
+    assert rep.successful == [("big", "b")]
+    assert rep.last_node_index == 0
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_readme_shape_small(mode):
+    """etc/pod.yaml (A: cpu 1 / mem 1, B: cpu 100 / mem 1000) on test-{i}.test.com nodes,
+    default provider, LIFO: the B pods are tried first and fail, then A fills the nodes."""
+    n = 60
+    nodes = [{"metadata": {"name": "test-%d.test.com" % i},
+              "status": {"allocatable": {"cpu": "32", "memory": "128Gi", "pods": "110"},
+                         "conditions": [{"type": "Ready", "status": "True"}]}} for i in range(n)]
+    spec = [{"name": "A", "num": 32 * n + 5, "pod": {"spec": {"containers": [{"resources": {"requests": {"cpu": 1, "memory": 1}}}]}}},
+            {"name": "B", "num": 10, "pod": {"spec": {"containers": [{"resources": {"requests": {"cpu": 100, "memory": 1000}}}]}}}]
+    pods = scheduler.expand_simulation_pods(spec)
+    preds, prios = scheduler.provider("DefaultProvider")
+    want, want_lni = _oracle_run(nodes, [], pods, preds, prios)
+    got, rep = _gpu_run(nodes, [], pods, preds, prios, mode)
+    assert len(rep.successful) == 32 * n
+    for name, host, msg in want:
+        assert got[name] == (host, msg), name
+    assert rep.last_node_index == want_lni
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_node_state_after_run(mode):
+    nodes, running, pods = rnd_workload(7, n_nodes=40, n_pods=200)
+    preds, prios = scheduler.provider("DefaultProvider")
+    want, _ = _oracle_run(nodes, running, pods, preds, prios)
+    cc = scheduler.ClusterCapacity(nodes, running, pods, predicates=preds, priorities=prios, mode=mode)
+    cc.run()
+    st = cc.scheduler.node_state()
+    infos = {ni.name: ni for ni in [R.NodeInfo(x) for x in nodes]}
+    for p in running:
+        if p["spec"]["nodeName"] in infos:
+            infos[p["spec"]["nodeName"]].add_pod(p)
+    byname = {p["metadata"]["name"]: p for p in pods}
+    for name, host, _ in want:
+        if host:
+            infos[host].add_pod(byname[name])
+    for i, nm in enumerate(cc.cluster.names):
+        ni = infos[nm]
+        assert st["req_cpu"][i] == ni.requested.cpu and st["req_mem"][i] == ni.requested.mem
+        assert st["nz_cpu"][i] == ni.nonzero_cpu and st["nz_mem"][i] == ni.nonzero_mem
+        assert st["pod_count"][i] == len(ni.pods)
+        assert st["port_count"][i] == len(ni.used_ports)
