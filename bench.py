@@ -1,0 +1,165 @@
+"""Benchmark of the MI355X per-pod scheduling cycle on BASELINE.json's headline workload.
+
+Workload (BASELINE.json configs[2], SURVEY.md §8d "C3"): 100,000 nodes, 1,000,000 mixed-size
+pods, default predicates + LeastRequested(1) + BalancedResourceAllocation(1).  A "step" is
+one ksim_schedule() call over the next `--batch` pods of the queue (each pod: predicates on
+every node, priorities, selectHost, commit — strictly one after another), with the node
+table and pod queue already resident in HBM.
+
+N GPUs (torchrun, one process per GPU): scenario-parallel replicas — every rank runs its own
+100k-node cluster with its own policy weights (a what-if sweep), no data-path
+collective; scaling "weak".  value = pods scheduled by all ranks / max-over-ranks time.
+
+The JSON line also carries the roofline of the dominant kernel (algorithmic bytes per launch
+÷ HIP-event launch duration, against the 8 TB/s HBM peak) and a cpu_baseline: the C oracle
+(oracle/cpu_ref.c, a port of the Go path) timed on a bounded prefix of the same queue, whose
+placements must equal the GPU's for the same prefix (reported as "parity").
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(ROOT, "kubernetes-schedule-simulator_amd")]
+
+BYTES_PER_NODE_EVAL = 60   # 6 x i64 + 2 x i32 + u32 flags, resource-only pods
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=4096, help="pods per step")
+    ap.add_argument("--nodes", type=int, default=100_000)
+    ap.add_argument("--pods", type=int, default=1_000_000)
+    ap.add_argument("--mode", default="auto", choices=["auto", "launch", "persistent"])
+    ap.add_argument("--cpu-sample", type=int, default=3000, help="pods in the CPU-baseline prefix (0 = skip)")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import numpy as np
+    import torch
+    from ksim import abi, scheduler, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    total_pods = (a.warmup + a.steps) * a.batch
+    if total_pods > a.pods:
+        raise SystemExit("warmup+steps x batch = %d exceeds the %d-pod queue" % (total_pods, a.pods))
+    cl, preds, prios = synth.config_c3(a.nodes, a.pods)
+    if rank > 0:  # what-if sweep: each replica scores with its own LeastRequested weight
+        prios = [("LeastRequestedPriority", 1 + rank), ("BalancedResourceAllocation", 1)]
+    mode = {"auto": abi.MODE_AUTO, "launch": abi.MODE_LAUNCH, "persistent": abi.MODE_PERSISTENT}[a.mode]
+    g = scheduler.GenericScheduler(cl, preds, prios, device=local, mode=mode, collect_reasons=False)
+
+    placements = []
+    first = 0
+    for _ in range(a.warmup):
+        out, _, _ = g.schedule(first, a.batch)
+        placements.append(out)
+        first += a.batch
+    barrier_sync()
+    t0 = time.perf_counter()
+    kernel_ms = 0.0
+    launches = 0
+    mode_used = blocks = 0
+    for _ in range(a.steps):
+        out, _, st = g.schedule(first, a.batch)
+        placements.append(out)
+        first += a.batch
+        kernel_ms += st.kernel_ms
+        launches += st.kernel_launches
+        mode_used, blocks = st.mode, st.blocks
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    placements = np.concatenate(placements)
+    bound = int((placements >= 0).sum())
+
+    pods_timed = a.steps * a.batch
+    value = world * pods_timed / elapsed
+    n = cl.n_nodes
+    # dominant kernel: the scan (launch mode: one launch per pod) or the persistent kernel
+    if mode_used == abi.MODE_LAUNCH:
+        pods_per_launch = 1
+        avg_launch_s = kernel_ms / 1e3 / max(pods_timed, 1)
+    else:
+        pods_per_launch = a.batch
+        avg_launch_s = kernel_ms / 1e3 / max(launches, 1)
+    achieved = BYTES_PER_NODE_EVAL * n * pods_per_launch / avg_launch_s / 1e9
+
+    cpu = None
+    parity = None
+    if rank == 0 and a.cpu_sample > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import cpu_ref
+        S = min(a.cpu_sample, len(placements))
+        threads = max(1, min(a.cpu_threads, len(os.sched_getaffinity(0))))
+        cfg = scheduler.make_config(preds, prios)
+        t1 = time.perf_counter()
+        ref_out, _, _, _ = cpu_ref.run(cl, cfg, 0, S, threads=threads)
+        cpu_s = time.perf_counter() - t1
+        cpu = {"value": round(S / cpu_s, 1), "unit": "pods/s", "cores": threads, "kind": "port",
+               "sample": "first %d pods of the same C3 queue on the same 100k-node cluster "
+                         "(oracle/cpu_ref.c, OpenMP node-parallel like workqueue.Parallelize), %.1f s" % (S, cpu_s),
+               "node_evals_per_s": round(S * n / cpu_s, 1)}
+        parity = {"prefix_pods": S, "match": bool(np.array_equal(ref_out, placements[:S]))}
+
+    if rank == 0:
+        line = {
+            "metric": "pods scheduled/sec + node-evals/sec at 100k nodes, 1/2/4/8 MI355X",
+            "value": round(value, 1),
+            "unit": "pods/s",
+            "node_evals_per_s": round(value * n, 1),
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "int64",
+            "data": "synthetic (splitmix64 seed 3, SURVEY.md §8d C3)",
+            "config": {"workload": "C3: %d nodes, %d-pod queue, default predicates + LeastRequested(1) + "
+                                   "BalancedResourceAllocation(1)" % (n, a.pods),
+                       "nodes": n, "pods_per_step": a.batch, "global_batch": a.batch * world,
+                       "mode": {1: "launch", 2: "persistent"}.get(mode_used, str(mode_used)), "blocks": blocks,
+                       "parallelism": "scenario-replicas x%d" % world if world > 1 else "single-gpu"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "bytes_per_node_eval": BYTES_PER_NODE_EVAL,
+                         "avg_launch_us": round(avg_launch_s * 1e6, 3), "pods_per_launch": pods_per_launch},
+            "cpu_baseline": cpu,
+            "parity": parity,
+            "pods_bound": bound,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

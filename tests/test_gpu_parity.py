@@ -158,3 +158,45 @@ def test_node_state_after_run(mode):
         assert st["nz_cpu"][i] == ni.nonzero_cpu and st["nz_mem"][i] == ni.nonzero_mem
         assert st["pod_count"][i] == len(ni.pods)
         assert st["port_count"][i] == len(ni.used_ports)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_c1_full_matches_c_oracle(mode):
+    """Full C1 (README shape, 1,500 nodes, 48,020 pods, DefaultProvider) against the C oracle."""
+    import cpu_ref
+    from ksim import synth
+    cl, p, q = synth.config_c1()
+    g = scheduler.GenericScheduler(cl, p, q, mode=mode)
+    out, reasons, st = g.schedule()
+    ref, ref_reasons, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), threads=8)
+    assert np.array_equal(out, ref)
+    assert (out >= 0).sum() == 1500 * 32  # cpu saturates at 32 A pods per node
+    failed = out < 0
+    assert np.array_equal(reasons[failed], ref_reasons[failed])
+    assert g.last_node_index == ref_ctr
+    s = g.node_state()
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+        assert np.array_equal(s[k], ref_state[k]), k
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_c3_prefix_matches_c_oracle(mode):
+    """100k-node C3 cluster: the first 3,000 pods against the C oracle, then size-independent
+    invariants over 60,000 pods (every pod bound, per-node sums conserved)."""
+    import cpu_ref
+    from ksim import synth
+    cl, p, q = synth.config_c3(100_000, 60_000)
+    g = scheduler.GenericScheduler(cl, p, q, mode=mode, collect_reasons=False)
+    out1, _, _ = g.schedule(0, 3000)
+    ref, _, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, 3000, threads=8)
+    assert np.array_equal(out1, ref)
+    assert g.last_node_index == ref_ctr
+    out2, _, _ = g.schedule(3000, 57000)
+    out = np.concatenate([out1, out2])
+    assert (out >= 0).all()
+    s = g.node_state()
+    assert s["pod_count"].sum() == 60000
+    assert s["req_cpu"].sum() == cl.pods["add_cpu"].sum()
+    assert s["req_mem"].sum() == cl.pods["add_mem"].sum()
+    assert np.array_equal(np.bincount(out, minlength=cl.n_nodes), s["pod_count"])
+    assert (s["req_cpu"] <= cl.cols["alloc_cpu"]).all() and (s["req_mem"] <= cl.cols["alloc_mem"]).all()
