@@ -1,15 +1,471 @@
-// ksim_persistent.hip — persistent-kernel mode (placeholder until the persistent
-// scheduler lands: reports "does not fit" so KSIM_MODE_AUTO uses launch mode).
+// ksim_persistent.hip — persistent-kernel mode (KSIM_MODE_PERSISTENT).
+//
+// One launch walks the whole pod queue.  Workgroup b owns the contiguous name-rank range
+// [b*chunk, (b+1)*chunk) of the node table and keeps the hot 60-byte rows of those nodes
+// in LDS for the whole launch (only the owner of a node ever reads or writes it, so node
+// state needs no cross-workgroup coherence).  Per pod:
+//   1. every workgroup evaluates its rows (predicates, map priorities, reduce class) and
+//      reduces them to a partial: fit count + per reduce class (max map score, count);
+//   2. it publishes the partial as tagged 8-byte granules (one agent-scope store each: the
+//      data is the flag — MI355X_MICROARCH.md "handoff-1to1" / "allgather");
+//   3. one wave per workgroup sweeps every workgroup's granules for this pod and computes
+//      the global decision redundantly (findNodesThatFit → PrioritizeNodes → selectHost,
+//      core/generic_scheduler.go:112-198; lastNodeIndex is replicated in every workgroup),
+//      so there is no second exchange and no grid barrier;
+//   4. the owner of the selected block picks the exact node from the scores it still holds
+//      in registers and commits the pod into its LDS rows (NodeInfo.AddPod).
+// Granules are double-buffered by pod parity and carry a 16-bit pod tag: a workgroup that
+// publishes pod p has seen every workgroup's pod p-1 partial, so nobody still reads the
+// p-2 slot it overwrites.  Every spin is bounded (2 s) and reports through the error word.
+//
+// Granule layout per workgroup and slot: [0] tag|fit:24|count(class 0):24,
+// [2q+1] tag|score(class q):48, [2q] tag|count(class q):24 for q >= 1.
 #include "ksim_common.h"
 
-extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows) {
-  (void)n;
-  *grid = 0;
-  *lds_rows = 0;
-  return 0;
+namespace {
+
+constexpr int GR = 2 * KSIM_MAX_RCLASS;           // granules per workgroup per slot
+constexpr int MAXB = 4;                            // workgroups per sweep lane (grid <= 256)
+constexpr uint64_t SPIN_LIMIT_TICKS = 200000000ull; // s_memrealtime ticks at 100 MHz = 2 s
+
+typedef __attribute__((address_space(1))) uint64_t gu64;
+
+__device__ __forceinline__ void store_granule(uint64_t* g, uint64_t v) {
+  __hip_atomic_store((gu64*)g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t load_granule(const uint64_t* g) {
+  return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t gtag(uint64_t v) { return (uint32_t)(v >> 48); }
+__device__ __forceinline__ int64_t gscore(uint64_t v) { return ((int64_t)(v << 16)) >> 16; }
+__device__ __forceinline__ int64_t glo24(uint64_t v) { return (int64_t)(v & 0xFFFFFF); }
+__device__ __forceinline__ int64_t ghi24(uint64_t v) { return (int64_t)((v >> 24) & 0xFFFFFF); }
+
+__device__ __forceinline__ int64_t wmax64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+__device__ __forceinline__ int64_t wsum64(int64_t v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// exclusive suffix sum over lanes (sum of v over lanes with a higher id)
+__device__ __forceinline__ int64_t wsuffix_excl(int64_t v, int lane) {
+  int64_t s = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int64_t t = __shfl_down(s, o, 64);
+    if (lane + o < 64) s += t;
+  }
+  return s - v;
 }
 
-extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, int grid, int lds_rows, hipStream_t s) {
-  (void)c; (void)grid; (void)lds_rows; (void)s;
-  return hipErrorNotSupported;
+struct PDecision {
+  int32_t mode;   // 0 none fit, 1 single fit, 2 select among winners, -1 abort
+  int32_t blk;    // owner workgroup of the selected node
+  int64_t rank;   // rank from the top (largest name rank) inside that workgroup
+  uint32_t winners;
+  int32_t pad;
+  int64_t M[KSIM_MAX_RCLASS];
+};
+
+struct Rows {  // LDS image of the owned rows (SoA)
+  int64_t *ac, *am, *rc, *rm, *zc, *zm;
+  int32_t *allowed, *count;
+  uint32_t* fl;
+};
+
+__device__ __forceinline__ Rows carve(char* smem, int rows) {
+  Rows r;
+  int64_t* p = reinterpret_cast<int64_t*>(smem);
+  r.ac = p; r.am = p + rows; r.rc = p + 2 * rows; r.rm = p + 3 * rows; r.zc = p + 4 * rows; r.zm = p + 5 * rows;
+  int32_t* q = reinterpret_cast<int32_t*>(p + 6 * rows);
+  r.allowed = q; r.count = q + rows;
+  r.fl = reinterpret_cast<uint32_t*>(q + 2 * rows);
+  return r;
+}
+
+// Commit of the columns that stay in HBM (gpu, ephemeral, scalars, ports) and of the
+// over-commit bits (node_info.go:318-341, utils.go:45-60).  Single thread of the owner.
+__device__ __forceinline__ uint32_t commit_side(const KsimCtx& c, const ksim_pod& P, int64_t w, uint32_t fl) {
+  const int64_t g = c.req_gpu[w] + P.add_gpu;
+  const int64_t e = c.req_eph[w] + P.add_eph;
+  c.req_gpu[w] = g;
+  c.req_eph[w] = e;
+  fl &= ~(KSIM_N_GPU_OVER | KSIM_N_EPH_OVER);
+  if (c.alloc_gpu[w] < g) fl |= KSIM_N_GPU_OVER;
+  if (c.alloc_eph[w] < e) fl |= KSIM_N_EPH_OVER;
+  for (int32_t s = 0; s < P.scalar_cnt; ++s) {
+    const ksim_scalar_req q = c.pod_scalars[P.scalar_off + s];
+    c.req_scalar[(int64_t)q.col * c.n + w] += q.add;
+  }
+  for (int32_t k = 0; k < P.port_cnt; ++k) {
+    const uint64_t key = c.pod_ports[P.port_off + k];
+    const int32_t cnt = c.port_count[w];
+    bool dup = false;
+    for (int32_t s = 0; s < cnt; ++s)
+      if (c.ports[(int64_t)s * c.n + w] == key) { dup = true; break; }
+    if (dup) continue;
+    if (cnt >= c.port_slots) { atomicOr(c.err, 1); continue; }
+    c.ports[(int64_t)cnt * c.n + w] = key;
+    c.port_count[w] = cnt + 1;
+  }
+  return fl;
+}
+
+}  // namespace
+
+template <int BS, int NPT>
+__global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t* granules) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int NW = BS / 64;
+  __shared__ int64_t s_mx[NW][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_cnt[NW][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_fit[NW];
+  __shared__ uint64_t s_ball[NPT][NW];
+  __shared__ int32_t s_hist[KSIM_NREASONS];
+  __shared__ PDecision D;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int G = gridDim.x;
+  const int64_t chunk = c.chunk;
+  const int64_t lo = (int64_t)blockIdx.x * chunk;
+  const int64_t hi = (lo + chunk < c.n) ? lo + chunk : c.n;
+  Rows R = carve(smem, (int)chunk);
+
+  for (int64_t j = tid; j < hi - lo; j += BS) {   // stage the owned rows into LDS
+    const int64_t i = lo + j;
+    R.ac[j] = c.alloc_cpu[i]; R.am[j] = c.alloc_mem[i];
+    R.rc[j] = c.req_cpu[i]; R.rm[j] = c.req_mem[i];
+    R.zc[j] = c.nz_cpu[i]; R.zm[j] = c.nz_mem[i];
+    R.allowed[j] = c.allowed_pods[i]; R.count[j] = c.pod_count[i]; R.fl[j] = c.flags[i];
+  }
+  uint64_t counter = *c.counter;   // replicated genericScheduler.lastNodeIndex
+  __syncthreads();
+
+  for (int64_t pod = c.first; pod < c.end; ++pod) {
+    const ksim_pod P = c.pods[pod];
+    const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
+    const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
+    const int K = k1 * k2;
+    const uint64_t tag = (uint64_t)((pod - c.first + 1) & 0xFFFF);
+    uint64_t* slot = granules + (pod & 1) * (int64_t)G * GR;
+
+    // ---------------- 1. evaluate the owned rows ----------------
+    bool fit[NPT];
+    int64_t sc[NPT];
+    int cl[NPT];
+    uint32_t rmask[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int64_t j = (int64_t)k * BS + tid;
+      fit[k] = false; sc[k] = 0; cl[k] = 0; rmask[k] = 0;
+      if (lo + j < hi) {
+        const int64_t i = lo + j;
+        KsimRow r;
+        r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j]; r.rm = R.rm[j]; r.zc = R.zc[j]; r.zm = R.zm[j];
+        r.allowed = R.allowed[j]; r.count = R.count[j]; r.fl = R.fl[j];
+        const uint32_t m = ksim_predicates(c, P, i, r);
+        fit[k] = (m == 0);
+        rmask[k] = m;
+        sc[k] = ksim_map_score(c, P, r);
+        cl[k] = (K > 1) ? ksim_rclass(c, P, i, k1, k2) : 0;
+      }
+    }
+    int32_t nf = 0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) nf += __popcll(__ballot(fit[k]));
+    if (lane == 0) s_fit[wv] = nf;
+    for (int q = 0; q < K; ++q) {
+      int64_t v = INT64_MIN;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k)
+        if (fit[k] && cl[k] == q && sc[k] > v) v = sc[k];
+      const int64_t wm = wmax64(v);
+      int32_t n = 0;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) n += __popcll(__ballot(fit[k] && cl[k] == q && sc[k] == wm));
+      if (lane == 0) { s_mx[wv][q] = wm; s_cnt[wv][q] = (wm == INT64_MIN) ? 0 : n; }
+    }
+    __syncthreads();
+
+    if (wv == 0) {
+      // ---------------- 2. publish: lane L stores granule L (L < 2K) ----------------
+      if (lane < 2 * K) {
+        const int q = lane >> 1;
+        int64_t m = INT64_MIN, n = 0;
+        for (int w = 0; w < NW; ++w) {
+          if (s_cnt[w][q] == 0) continue;
+          if (s_mx[w][q] > m) { m = s_mx[w][q]; n = s_cnt[w][q]; }
+          else if (s_mx[w][q] == m) n += s_cnt[w][q];
+        }
+        uint64_t g;
+        if (lane & 1) {
+          g = (tag << 48) | ((uint64_t)m & 0xFFFFFFFFFFFFull);
+        } else if (lane == 0) {
+          int64_t f = 0;
+          for (int w = 0; w < NW; ++w) f += s_fit[w];
+          g = (tag << 48) | ((uint64_t)n << 24) | (uint64_t)f;
+        } else {
+          g = (tag << 48) | (uint64_t)n;
+        }
+        store_granule(granules + ((pod & 1) * (int64_t)G + blockIdx.x) * GR + lane, g);
+      }
+
+      // ---------------- 3. sweep all partials (class 0 and fit in one pass) ----------------
+      int64_t bfit[MAXB], bcnt[MAXB], bsc[MAXB];
+      bool ok = false;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        bool mine = true;
+#pragma unroll
+        for (int j = 0; j < MAXB; ++j) {
+          const int b = lane + 64 * j;
+          bfit[j] = 0; bcnt[j] = 0; bsc[j] = INT64_MIN;
+          if (b < G) {
+            const uint64_t v0 = load_granule(slot + (int64_t)b * GR);
+            const uint64_t v1 = load_granule(slot + (int64_t)b * GR + 1);
+            mine &= gtag(v0) == tag && gtag(v1) == tag;
+            bfit[j] = glo24(v0);
+            bcnt[j] = ghi24(v0);
+            bsc[j] = gscore(v1);
+          }
+        }
+        if (__all(mine)) { ok = true; break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_LIMIT_TICKS) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      int64_t Mq[KSIM_MAX_RCLASS], Cq[KSIM_MAX_RCLASS];
+      int64_t F = 0;
+      if (ok) {
+        int64_t f = 0, m = INT64_MIN, n = 0;
+#pragma unroll
+        for (int j = 0; j < MAXB; ++j) {
+          f += bfit[j];
+          if (bcnt[j] == 0) continue;
+          if (bsc[j] > m) { m = bsc[j]; n = bcnt[j]; }
+          else if (bsc[j] == m) n += bcnt[j];
+        }
+        F = wsum64(f);
+        Mq[0] = wmax64(n ? m : INT64_MIN);
+        Cq[0] = wsum64((n && m == Mq[0]) ? n : 0);
+        for (int q = 1; q < K && ok; ++q) {   // further reduce classes: their own granules
+          int64_t mm = INT64_MIN, nn = 0;
+          for (int j = 0; j < MAXB; ++j) {
+            const int b = lane + 64 * j;
+            if (b >= G) break;
+            uint64_t vs = 0, vc = 0;
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            for (;;) {
+              vs = load_granule(slot + (int64_t)b * GR + 2 * q + 1);
+              vc = load_granule(slot + (int64_t)b * GR + 2 * q);
+              if (gtag(vs) == tag && gtag(vc) == tag) break;
+              if (__builtin_amdgcn_s_memrealtime() - t1 > SPIN_LIMIT_TICKS) { ok = false; break; }
+            }
+            const int64_t cnt = glo24(vc), s = gscore(vs);
+            if (cnt == 0) continue;
+            if (s > mm) { mm = s; nn = cnt; }
+            else if (s == mm) nn += cnt;
+          }
+          Mq[q] = wmax64(nn ? mm : INT64_MIN);
+          Cq[q] = wsum64((nn && mm == Mq[q]) ? nn : 0);
+        }
+      }
+      ok = __all(ok);
+      if (!ok) {
+        if (lane == 0) { D.mode = -1; atomicOr(c.err, 4); }
+      } else if (F == 0) {
+        if (lane == 0) D.mode = 0;
+      } else {
+        int mode = 1;
+        uint32_t win = 1;
+        int64_t ix = 0;
+        if (F > 1) {   // generic_scheduler.go:153-156: a single fit skips selectHost
+          mode = 2;
+          int64_t mxT = 0, mxA = 0;
+          for (int q = 0; q < K; ++q) {
+            if (Cq[q] == 0) continue;
+            const int64_t tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2];
+            const int64_t av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];
+            mxT = tv > mxT ? tv : mxT;
+            mxA = av > mxA ? av : mxA;
+          }
+          int64_t best = INT64_MIN;
+          int64_t tot[KSIM_MAX_RCLASS];
+          for (int q = 0; q < K; ++q) {
+            if (Cq[q] == 0) continue;
+            uint64_t t = (uint64_t)Mq[q];
+            if (c.w[KSIM_W_TAINT_TOLERATION])
+              t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] *
+                   (uint64_t)ksim_norm(c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2], mxT, true);
+            if (c.w[KSIM_W_NODE_AFFINITY])
+              t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] *
+                   (uint64_t)ksim_norm(c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2], mxA, false);
+            tot[q] = (int64_t)t;
+            best = tot[q] > best ? tot[q] : best;
+          }
+          win = 0;
+          int64_t C = 0;
+          for (int q = 0; q < K; ++q)
+            if (Cq[q] && tot[q] == best) { win |= 1u << q; C += Cq[q]; }
+          ix = (int64_t)(counter % (uint64_t)C);   // generic_scheduler.go:192-195
+          counter += 1;
+        }
+        // locate the workgroup holding the ix-th match counted from the top
+        int64_t above_hi = 0;
+        int found = -1;
+        int64_t found_above = 0;
+        for (int j = MAXB - 1; j >= 0; --j) {
+          if (j * 64 >= G) continue;
+          const int b = lane + 64 * j;
+          int64_t m = 0;
+          if (b < G) {
+            if (mode == 1) {
+              m = bfit[j];
+            } else {
+              if ((win & 1u) && bcnt[j] && bsc[j] == Mq[0]) m += bcnt[j];
+              for (int q = 1; q < K; ++q) {
+                if (!((win >> q) & 1u)) continue;
+                const uint64_t vs = load_granule(slot + (int64_t)b * GR + 2 * q + 1);
+                const uint64_t vc = load_granule(slot + (int64_t)b * GR + 2 * q);
+                if (glo24(vc) && gscore(vs) == Mq[q]) m += glo24(vc);
+              }
+            }
+          }
+          const int64_t above = above_hi + wsuffix_excl(m, lane);
+          const uint64_t bal = __ballot(m > 0 && ix >= above && ix < above + m);
+          if (bal) {
+            const int l = __ffsll((unsigned long long)bal) - 1;
+            found = j * 64 + l;
+            found_above = __shfl(above, l, 64);
+            break;
+          }
+          above_hi += wsum64(m);
+        }
+        if (lane == 0) {
+          D.mode = found < 0 ? -1 : mode;
+          D.winners = win;
+          D.blk = found;
+          D.rank = ix - found_above;
+          for (int q = 0; q < K; ++q) D.M[q] = Mq[q];
+          if (found < 0) atomicOr(c.err, 2);
+        }
+      }
+    }
+    __syncthreads();
+    const int mode = D.mode;
+    if (mode < 0) break;   // uniform across the workgroup; every workgroup ends the same way
+
+    if (mode == 0) {   // FitError: every workgroup adds its reasons; workgroup 0 records it
+      if (c.collect && c.out_reasons) {
+        if (tid < KSIM_NREASONS) s_hist[tid] = 0;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < NPT; ++k)
+          for (int r = 0; r < KSIM_NREASONS; ++r) {
+            const int32_t n = __popcll(__ballot((rmask[k] >> r) & 1u));
+            if (lane == 0 && n) atomicAdd(&s_hist[r], n);
+          }
+        __syncthreads();
+        if (tid < KSIM_NREASONS && s_hist[tid]) atomicAdd(&c.out_reasons[pod * KSIM_NREASONS + tid], s_hist[tid]);
+      }
+      if (blockIdx.x == 0 && tid == 0) c.out_node[pod] = -1;
+    } else if (D.blk == (int)blockIdx.x) {
+      // ---------------- 4. owner: exact node, commit into LDS ----------------
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        bool match = fit[k];
+        if (mode == 2) match = fit[k] && ((D.winners >> cl[k]) & 1u) && sc[k] == D.M[cl[k]];
+        const uint64_t bal = __ballot(match);
+        if (lane == 0) s_ball[k][wv] = bal;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int64_t r = D.rank;
+        int64_t j = -1;
+        for (int k = NPT - 1; k >= 0 && j < 0; --k) {
+          for (int w = NW - 1; w >= 0; --w) {
+            uint64_t m = s_ball[k][w];
+            const int nb = __popcll(m);
+            if (r >= nb) { r -= nb; continue; }
+            for (int64_t t = 0; t < r; ++t) m &= ~(1ull << (63 - __clzll(m)));
+            j = (int64_t)k * BS + w * 64 + (63 - __clzll(m));
+            break;
+          }
+        }
+        if (j < 0) {
+          atomicOr(c.err, 2);
+          c.out_node[pod] = -1;
+        } else {
+          const int64_t w = lo + j;
+          R.rc[j] += P.add_cpu;
+          R.rm[j] += P.add_mem;
+          R.zc[j] += P.nz_cpu;
+          R.zm[j] += P.nz_mem;
+          R.count[j] += 1;
+          if (P.add_gpu | P.add_eph | P.scalar_cnt | P.port_cnt) R.fl[j] = commit_side(c, P, w, R.fl[j]);
+          c.out_node[pod] = (int32_t)w;
+        }
+      }
+    }
+    __syncthreads();
+  }
+
+  // the table is authoritative in HBM between calls: write the owned rows back
+  for (int64_t j = tid; j < hi - lo; j += BS) {
+    const int64_t i = lo + j;
+    c.req_cpu[i] = R.rc[j]; c.req_mem[i] = R.rm[j];
+    c.nz_cpu[i] = R.zc[j]; c.nz_mem[i] = R.zm[j];
+    c.pod_count[i] = R.count[j]; c.flags[i] = R.fl[j];
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    *c.counter = counter;
+    *c.cursor = c.end;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+static constexpr int ROW_BYTES = 60;
+static constexpr int LDS_BUDGET = 96 * 1024;
+
+static int num_cus() {
+  int dev = 0;
+  hipDeviceProp_t p;
+  if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
+  return p.multiProcessorCount;
+}
+
+// One workgroup per CU (<= 256) so every workgroup is resident — the protocol spins on every
+// other workgroup — and chunk = ceil(n / grid) rows per workgroup held in LDS.
+extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows) {
+  int g = num_cus();
+  if (g <= 0 || n <= 0) return 0;
+  if (g > 64 * MAXB) g = 64 * MAXB;
+  if (n < (int64_t)g * 64) g = (int)((n + 63) / 64);   // >= 64 rows per workgroup
+  if (g < 1) g = 1;
+  const int64_t chunk = (n + g - 1) / g;
+  if (chunk * ROW_BYTES > LDS_BUDGET || chunk > 8 * 512) return 0;   // does not fit: launch mode
+  *grid = g;
+  *lds_rows = (int)chunk;
+  return 1;
+}
+
+extern "C" size_t ksim_persistent_granule_bytes(int grid) { return (size_t)2 * grid * GR * sizeof(uint64_t); }
+
+extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows,
+                                             hipStream_t s) {
+  const size_t lds = (size_t)lds_rows * 64;
+#define KSIM_PL(BS, NPT) \
+  hipLaunchKernelGGL((ksim_persistent_kernel<BS, NPT>), dim3(grid), dim3(BS), lds, s, *c, granules)
+  if (lds_rows <= 512) KSIM_PL(512, 1);
+  else if (lds_rows <= 1024) KSIM_PL(512, 2);
+  else if (lds_rows <= 2048) KSIM_PL(512, 4);
+  else KSIM_PL(512, 8);
+#undef KSIM_PL
+  return hipGetLastError();
 }

@@ -19,8 +19,9 @@ extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, i
 extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* fit, uint32_t* reasons, int64_t* score,
                                        uint8_t* rcls, hipStream_t s);
 extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, hipStream_t s);
-extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, int grid, int lds_rows, hipStream_t s);
+extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, hipStream_t s);
 extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows);
+extern "C" size_t ksim_persistent_granule_bytes(int grid);
 
 namespace {
 
@@ -49,6 +50,8 @@ struct ksim_handle {
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
   int g_batch = 0, g_npt = 0, g_collect = -1, part_cap = 0;
+  uint64_t* granules = nullptr;
+  size_t gran_bytes = 0;
   int64_t g_first = -1, g_end = -1;
   // host-side copies needed for validation
   std::vector<int32_t> h_n_tt, h_n_na;
@@ -347,21 +350,34 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
   return KSIM_OK;
 }
 
+// Scores travel as 48-bit granule payloads in persistent mode: bound the weights.
+static bool persistent_weights_ok(const KsimCtx& c) {
+  int64_t s = 0;
+  for (int k = 0; k < KSIM_NW; ++k) {
+    if (c.w[k] > ((int64_t)1 << 40)) return false;
+    s += c.w[k] * 10;
+  }
+  return s < ((int64_t)1 << 46);
+}
+
 static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   KsimCtx& c = h->ctx;
   int grid = 0, lds_rows = 0;
   if (!ksim_persistent_config(c.n, &grid, &lds_rows))
-    return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: node table does not fit the persistent layout");
-  int rc = ensure_partials(h, 2 * grid);
-  if (rc) return rc;
+    return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: node table does not fit the on-chip layout");
+  if (!persistent_weights_ok(c)) return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: weights exceed the 48-bit score range");
+  const size_t gb = ksim_persistent_granule_bytes(grid);
+  if (h->gran_bytes < gb) {
+    int rc = dev_alloc(h, &h->granules, gb / sizeof(uint64_t));
+    if (rc) return rc;
+    h->gran_bytes = gb;
+  }
   c.first = first;
   c.end = first + count;
   c.chunk = (c.n + grid - 1) / grid;
-  HIPCHK(h, hipMemcpyAsync(c.cursor, &first, 8, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemsetAsync(c.ticket, 0, 16, h->stream));
-  HIPCHK(h, hipMemsetAsync(c.partials, 0, sizeof(KsimPartial) * 2 * grid, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipError_t e = ksim_launch_persistent(&c, grid, lds_rows, h->stream);
+  hipError_t e = ksim_launch_persistent(&c, h->granules, grid, lds_rows, h->stream);
   if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   HIPCHK(h, hipEventSynchronize(h->ev1));
@@ -389,7 +405,7 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
   int mode = h->cfg.mode;
   if (mode == KSIM_MODE_AUTO) {
     int g, l;
-    mode = ksim_persistent_config(c.n, &g, &l) ? KSIM_MODE_PERSISTENT : KSIM_MODE_LAUNCH;
+    mode = (ksim_persistent_config(c.n, &g, &l) && persistent_weights_ok(c)) ? KSIM_MODE_PERSISTENT : KSIM_MODE_LAUNCH;
   }
   int rc = (mode == KSIM_MODE_PERSISTENT) ? run_persistent_mode(h, first, count, st) : run_launch_mode(h, first, count, st);
   if (rc) return rc;
