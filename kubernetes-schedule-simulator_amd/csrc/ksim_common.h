@@ -83,6 +83,7 @@ struct KsimCtx {
   int32_t* out_reasons;   // [end-first][KSIM_NREASONS]
   int32_t* err;           // sticky error word
   int64_t chunk;          // nodes per block
+  uint64_t* dbg;          // diagnostic stamp sums (KSIM_STAMPS builds only), else null
 };
 
 // ((a*10)/b) with Go int64 semantics (wrapping multiply, truncating divide), b > 0.

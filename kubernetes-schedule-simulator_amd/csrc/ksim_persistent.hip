@@ -20,13 +20,15 @@
 //
 // Granule layout per workgroup and slot: [0] tag|fit:24|count(class 0):24,
 // [2q+1] tag|score(class q):48, [2q] tag|count(class q):24 for q >= 1.
+// Sweep lane l reads workgroups [l*MAXB, l*MAXB+MAXB): name-rank order is lane-major, so
+// "how many matches above me" is one wave suffix scan.
 #include "ksim_common.h"
 
 namespace {
 
-constexpr int GR = 2 * KSIM_MAX_RCLASS;           // granules per workgroup per slot
-constexpr int MAXB = 4;                            // workgroups per sweep lane (grid <= 256)
-constexpr uint64_t SPIN_LIMIT_TICKS = 200000000ull; // s_memrealtime ticks at 100 MHz = 2 s
+constexpr int GR = 2 * KSIM_MAX_RCLASS;             // granules per workgroup per slot
+constexpr int MAXB = 4;                              // workgroups per sweep lane (grid <= 256)
+constexpr uint64_t SPIN_LIMIT_TICKS = 200000000ull;  // s_memrealtime ticks at 100 MHz = 2 s
 
 typedef __attribute__((address_space(1))) uint64_t gu64;
 
@@ -54,21 +56,35 @@ __device__ __forceinline__ int64_t wsum64(int64_t v) {
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
   return v;
 }
-// exclusive suffix sum over lanes (sum of v over lanes with a higher id)
-__device__ __forceinline__ int64_t wsuffix_excl(int64_t v, int lane) {
-  int64_t s = v;
+// inclusive suffix sum over lanes (sum of v over lanes with id >= mine)
+__device__ __forceinline__ int64_t wsuffix_incl(int64_t v, int lane) {
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
-    const int64_t t = __shfl_down(s, o, 64);
-    if (lane + o < 64) s += t;
+    const int64_t t = __shfl_down(v, o, 64);
+    if (lane + o < 64) v += t;
   }
-  return s - v;
+  return v;
 }
 
+#ifdef KSIM_STAMPS
+#define STAMP(k)                                         \
+  do {                                                   \
+    if (blockIdx.x == 0 && tid == 0) {                   \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+      c.dbg[k] += t_ - t_prev;                          \
+      t_prev = t_;                                      \
+    }                                                    \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
+#endif
+
 struct PDecision {
-  int32_t mode;   // 0 none fit, 1 single fit, 2 select among winners, -1 abort
-  int32_t blk;    // owner workgroup of the selected node
-  int64_t rank;   // rank from the top (largest name rank) inside that workgroup
+  int32_t mode;  // 0 none fit, 1 single fit, 2 select among winners, -1 abort
+  int32_t blk;   // owner workgroup of the selected node
+  int64_t rank;  // rank from the top (largest name rank) inside that workgroup
   uint32_t winners;
   int32_t pad;
   int64_t M[KSIM_MAX_RCLASS];
@@ -118,6 +134,20 @@ __device__ __forceinline__ uint32_t commit_side(const KsimCtx& c, const ksim_pod
   return fl;
 }
 
+// Total score of reduce class q once the per-class maxima over the filtered set are known
+// (NormalizeReduce, priorities/reduce.go:29-64; weighted sum generic_scheduler.go:632-639).
+__device__ __forceinline__ int64_t class_total(const KsimCtx& c, const ksim_pod& P, int q, int k2, int64_t base,
+                                               int64_t mxT, int64_t mxA) {
+  uint64_t t = (uint64_t)base;
+  if (c.w[KSIM_W_TAINT_TOLERATION])
+    t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] *
+         (uint64_t)ksim_norm(c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2], mxT, true);
+  if (c.w[KSIM_W_NODE_AFFINITY])
+    t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] *
+         (uint64_t)ksim_norm(c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2], mxA, false);
+  return (int64_t)t;
+}
+
 }  // namespace
 
 template <int BS, int NPT>
@@ -129,6 +159,8 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
   __shared__ int32_t s_fit[NW];
   __shared__ uint64_t s_ball[NPT][NW];
   __shared__ int32_t s_hist[KSIM_NREASONS];
+  __shared__ int64_t s_M[KSIM_MAX_RCLASS];   // wave-0 scratch: global class maxima
+  __shared__ int64_t s_C[KSIM_MAX_RCLASS];   //               counts at those maxima
   __shared__ PDecision D;
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -138,18 +170,23 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
   const int64_t hi = (lo + chunk < c.n) ? lo + chunk : c.n;
   Rows R = carve(smem, (int)chunk);
 
-  for (int64_t j = tid; j < hi - lo; j += BS) {   // stage the owned rows into LDS
+  for (int64_t j = tid; j < hi - lo; j += BS) {  // stage the owned rows into LDS
     const int64_t i = lo + j;
     R.ac[j] = c.alloc_cpu[i]; R.am[j] = c.alloc_mem[i];
     R.rc[j] = c.req_cpu[i]; R.rm[j] = c.req_mem[i];
     R.zc[j] = c.nz_cpu[i]; R.zm[j] = c.nz_mem[i];
     R.allowed[j] = c.allowed_pods[i]; R.count[j] = c.pod_count[i]; R.fl[j] = c.flags[i];
   }
-  uint64_t counter = *c.counter;   // replicated genericScheduler.lastNodeIndex
+  uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex
+  ksim_pod Pn = c.pods[c.first];  // descriptor of the next pod, loaded one pod ahead
   __syncthreads();
+#ifdef KSIM_STAMPS
+  uint64_t t_prev = __builtin_amdgcn_s_memtime();
+#endif
 
   for (int64_t pod = c.first; pod < c.end; ++pod) {
-    const ksim_pod P = c.pods[pod];
+    const ksim_pod P = Pn;
+    Pn = c.pods[pod + 1 < c.end ? pod + 1 : pod];
     const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
     const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
     const int K = k1 * k2;
@@ -193,12 +230,14 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
       if (lane == 0) { s_mx[wv][q] = wm; s_cnt[wv][q] = (wm == INT64_MIN) ? 0 : n; }
     }
     __syncthreads();
+    STAMP(0);
 
     if (wv == 0) {
       // ---------------- 2. publish: lane L stores granule L (L < 2K) ----------------
       if (lane < 2 * K) {
         const int q = lane >> 1;
         int64_t m = INT64_MIN, n = 0;
+#pragma unroll
         for (int w = 0; w < NW; ++w) {
           if (s_cnt[w][q] == 0) continue;
           if (s_mx[w][q] > m) { m = s_mx[w][q]; n = s_cnt[w][q]; }
@@ -209,6 +248,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
           g = (tag << 48) | ((uint64_t)m & 0xFFFFFFFFFFFFull);
         } else if (lane == 0) {
           int64_t f = 0;
+#pragma unroll
           for (int w = 0; w < NW; ++w) f += s_fit[w];
           g = (tag << 48) | ((uint64_t)n << 24) | (uint64_t)f;
         } else {
@@ -216,8 +256,9 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
         }
         store_granule(granules + ((pod & 1) * (int64_t)G + blockIdx.x) * GR + lane, g);
       }
+      STAMP(1);
 
-      // ---------------- 3. sweep all partials (class 0 and fit in one pass) ----------------
+      // ---------------- 3. sweep fit + class-0 granules of every workgroup ----------------
       int64_t bfit[MAXB], bcnt[MAXB], bsc[MAXB];
       bool ok = false;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -225,7 +266,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
         bool mine = true;
 #pragma unroll
         for (int j = 0; j < MAXB; ++j) {
-          const int b = lane + 64 * j;
+          const int b = lane * MAXB + j;
           bfit[j] = 0; bcnt[j] = 0; bsc[j] = INT64_MIN;
           if (b < G) {
             const uint64_t v0 = load_granule(slot + (int64_t)b * GR);
@@ -236,12 +277,16 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
             bsc[j] = gscore(v1);
           }
         }
+#ifdef KSIM_STAMPS
+        if (blockIdx.x == 0 && tid == 0) c.dbg[8] += 1;
+#endif
         if (__all(mine)) { ok = true; break; }
         if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_LIMIT_TICKS) break;
         __builtin_amdgcn_s_sleep(1);
       }
-      int64_t Mq[KSIM_MAX_RCLASS], Cq[KSIM_MAX_RCLASS];
-      int64_t F = 0;
+      STAMP(2);
+      ok = __all(ok);
+      int64_t F = 0, M0 = INT64_MIN, C0 = 0;
       if (ok) {
         int64_t f = 0, m = INT64_MIN, n = 0;
 #pragma unroll
@@ -252,12 +297,16 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
           else if (bsc[j] == m) n += bcnt[j];
         }
         F = wsum64(f);
-        Mq[0] = wmax64(n ? m : INT64_MIN);
-        Cq[0] = wsum64((n && m == Mq[0]) ? n : 0);
-        for (int q = 1; q < K && ok; ++q) {   // further reduce classes: their own granules
+        M0 = wmax64(n ? m : INT64_MIN);
+        C0 = wsum64((n && m == M0) ? n : 0);
+      }
+      // further reduce classes (TaintToleration x NodeAffinity): their own granules
+      if (ok && K > 1) {
+        if (lane == 0) { s_M[0] = M0; s_C[0] = C0; }
+        for (int q = 1; q < K; ++q) {
           int64_t mm = INT64_MIN, nn = 0;
           for (int j = 0; j < MAXB; ++j) {
-            const int b = lane + 64 * j;
+            const int b = lane * MAXB + j;
             if (b >= G) break;
             uint64_t vs = 0, vc = 0;
             const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
@@ -272,11 +321,12 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
             if (s > mm) { mm = s; nn = cnt; }
             else if (s == mm) nn += cnt;
           }
-          Mq[q] = wmax64(nn ? mm : INT64_MIN);
-          Cq[q] = wsum64((nn && mm == Mq[q]) ? nn : 0);
+          const int64_t Mq = wmax64(nn ? mm : INT64_MIN);
+          const int64_t Cq = wsum64((nn && mm == Mq) ? nn : 0);
+          if (lane == 0) { s_M[q] = Mq; s_C[q] = Cq; }
         }
+        ok = __all(ok);
       }
-      ok = __all(ok);
       if (!ok) {
         if (lane == 0) { D.mode = -1; atomicOr(c.err, 4); }
       } else if (F == 0) {
@@ -285,83 +335,85 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
         int mode = 1;
         uint32_t win = 1;
         int64_t ix = 0;
-        if (F > 1) {   // generic_scheduler.go:153-156: a single fit skips selectHost
+        if (F > 1) {  // generic_scheduler.go:153-156: a single fit skips selectHost
           mode = 2;
-          int64_t mxT = 0, mxA = 0;
-          for (int q = 0; q < K; ++q) {
-            if (Cq[q] == 0) continue;
-            const int64_t tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2];
-            const int64_t av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];
-            mxT = tv > mxT ? tv : mxT;
-            mxA = av > mxA ? av : mxA;
+          int64_t C = C0;
+          if (K > 1) {
+            int64_t mxT = 0, mxA = 0;
+            for (int q = 0; q < K; ++q) {
+              if (s_C[q] == 0) continue;
+              const int64_t tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2];
+              const int64_t av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];
+              mxT = tv > mxT ? tv : mxT;
+              mxA = av > mxA ? av : mxA;
+            }
+            int64_t best = INT64_MIN;
+            for (int q = 0; q < K; ++q)
+              if (s_C[q]) {
+                const int64_t t = class_total(c, P, q, k2, s_M[q], mxT, mxA);
+                best = t > best ? t : best;
+              }
+            win = 0;
+            C = 0;
+            for (int q = 0; q < K; ++q)
+              if (s_C[q] && class_total(c, P, q, k2, s_M[q], mxT, mxA) == best) { win |= 1u << q; C += s_C[q]; }
           }
-          int64_t best = INT64_MIN;
-          int64_t tot[KSIM_MAX_RCLASS];
-          for (int q = 0; q < K; ++q) {
-            if (Cq[q] == 0) continue;
-            uint64_t t = (uint64_t)Mq[q];
-            if (c.w[KSIM_W_TAINT_TOLERATION])
-              t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] *
-                   (uint64_t)ksim_norm(c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2], mxT, true);
-            if (c.w[KSIM_W_NODE_AFFINITY])
-              t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] *
-                   (uint64_t)ksim_norm(c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2], mxA, false);
-            tot[q] = (int64_t)t;
-            best = tot[q] > best ? tot[q] : best;
-          }
-          win = 0;
-          int64_t C = 0;
-          for (int q = 0; q < K; ++q)
-            if (Cq[q] && tot[q] == best) { win |= 1u << q; C += Cq[q]; }
-          ix = (int64_t)(counter % (uint64_t)C);   // generic_scheduler.go:192-195
+          ix = (int64_t)(counter % (uint64_t)C);  // generic_scheduler.go:192-195
           counter += 1;
         }
-        // locate the workgroup holding the ix-th match counted from the top
-        int64_t above_hi = 0;
-        int found = -1;
-        int64_t found_above = 0;
-        for (int j = MAXB - 1; j >= 0; --j) {
-          if (j * 64 >= G) continue;
-          const int b = lane + 64 * j;
+        // ---- locate the workgroup holding the ix-th match counted from the top ----
+        int64_t bm[MAXB];
+        int64_t tot = 0;
+#pragma unroll
+        for (int j = 0; j < MAXB; ++j) {
+          const int b = lane * MAXB + j;
           int64_t m = 0;
           if (b < G) {
             if (mode == 1) {
               m = bfit[j];
             } else {
-              if ((win & 1u) && bcnt[j] && bsc[j] == Mq[0]) m += bcnt[j];
+              if ((win & 1u) && bcnt[j] && bsc[j] == M0) m += bcnt[j];
               for (int q = 1; q < K; ++q) {
                 if (!((win >> q) & 1u)) continue;
                 const uint64_t vs = load_granule(slot + (int64_t)b * GR + 2 * q + 1);
                 const uint64_t vc = load_granule(slot + (int64_t)b * GR + 2 * q);
-                if (glo24(vc) && gscore(vs) == Mq[q]) m += glo24(vc);
+                if (glo24(vc) && gscore(vs) == s_M[q]) m += glo24(vc);
               }
             }
           }
-          const int64_t above = above_hi + wsuffix_excl(m, lane);
-          const uint64_t bal = __ballot(m > 0 && ix >= above && ix < above + m);
-          if (bal) {
-            const int l = __ffsll((unsigned long long)bal) - 1;
-            found = j * 64 + l;
-            found_above = __shfl(above, l, 64);
-            break;
-          }
-          above_hi += wsum64(m);
+          bm[j] = m;
+          tot += m;
         }
-        if (lane == 0) {
+        const int64_t incl = wsuffix_incl(tot, lane);  // matches in my workgroups and above
+        const int64_t above = incl - tot;
+        const bool hit = tot > 0 && ix >= above && ix < incl;
+        if (hit) {
+          int64_t r = ix - above;
+          int found = -1;
+#pragma unroll
+          for (int j = MAXB - 1; j >= 0; --j) {
+            if (found < 0) {
+              if (r < bm[j]) found = lane * MAXB + j;
+              else r -= bm[j];
+            }
+          }
           D.mode = found < 0 ? -1 : mode;
-          D.winners = win;
           D.blk = found;
-          D.rank = ix - found_above;
-          for (int q = 0; q < K; ++q) D.M[q] = Mq[q];
+          D.rank = r;
+          D.winners = win;
+          D.M[0] = M0;
           if (found < 0) atomicOr(c.err, 2);
         }
+        if (K > 1 && lane < K) D.M[lane] = s_M[lane];
+        if (__ballot(hit) == 0 && lane == 0) { D.mode = -1; atomicOr(c.err, 2); }
       }
     }
+    STAMP(3);
     __syncthreads();
     const int mode = D.mode;
-    if (mode < 0) break;   // uniform across the workgroup; every workgroup ends the same way
+    if (mode < 0) break;  // uniform across the workgroup; every workgroup ends the same way
 
-    if (mode == 0) {   // FitError: every workgroup adds its reasons; workgroup 0 records it
+    if (mode == 0) {  // FitError: every workgroup adds its reasons; workgroup 0 records it
       if (c.collect && c.out_reasons) {
         if (tid < KSIM_NREASONS) s_hist[tid] = 0;
         __syncthreads();
@@ -414,6 +466,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
       }
     }
     __syncthreads();
+    STAMP(4);
   }
 
   // the table is authoritative in HBM between calls: write the owned rows back
@@ -446,10 +499,10 @@ extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows) {
   int g = num_cus();
   if (g <= 0 || n <= 0) return 0;
   if (g > 64 * MAXB) g = 64 * MAXB;
-  if (n < (int64_t)g * 64) g = (int)((n + 63) / 64);   // >= 64 rows per workgroup
+  if (n < (int64_t)g * 64) g = (int)((n + 63) / 64);  // >= 64 rows per workgroup
   if (g < 1) g = 1;
   const int64_t chunk = (n + g - 1) / g;
-  if (chunk * ROW_BYTES > LDS_BUDGET || chunk > 8 * 512) return 0;   // does not fit: launch mode
+  if (chunk * ROW_BYTES > LDS_BUDGET || chunk > 8 * 512) return 0;  // does not fit: launch mode
   *grid = g;
   *lds_rows = (int)chunk;
   return 1;

@@ -131,12 +131,13 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
   for (int k = 0; k < KSIM_NW; ++k) c.w[k] = cfg->weights[k];
   int rc;
   if ((rc = dev_alloc(h, &c.cursor, 1)) || (rc = dev_alloc(h, &c.counter, 1)) || (rc = dev_alloc(h, &c.ticket, 4)) ||
-      (rc = dev_alloc(h, &c.err, 4))) {
+      (rc = dev_alloc(h, &c.err, 4)) || (rc = dev_alloc(h, &c.dbg, 16))) {
     ksim_destroy(h);
     return rc;
   }
   (void)hipMemsetAsync(c.ticket, 0, 16, h->stream);
   (void)hipMemsetAsync(c.err, 0, 16, h->stream);
+  (void)hipMemsetAsync(c.dbg, 0, 128, h->stream);
   (void)hipMemcpyAsync(c.counter, &cfg->last_node_index, 8, hipMemcpyHostToDevice, h->stream);
   if (hipStreamSynchronize(h->stream) != hipSuccess) {
     ksim_destroy(h);
@@ -383,6 +384,16 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
   HIPCHK(h, hipEventSynchronize(h->ev1));
   float ms = 0.f;
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+#ifdef KSIM_STAMPS
+  {
+    uint64_t d[16];
+    HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
+    fprintf(stderr, "[ksim stamps] pods=%lld cycles/pod: eval+reduce %.0f publish %.0f sweep %.0f decide %.0f commit+sync %.0f polls/pod %.2f (%.3f ms)\n",
+            (long long)count, d[0] / (double)count, d[1] / (double)count, d[2] / (double)count, d[3] / (double)count,
+            d[4] / (double)count, d[8] / (double)count, ms);
+  }
+#endif
   if (st) {
     st->device_ms = ms;
     st->kernel_ms = ms;

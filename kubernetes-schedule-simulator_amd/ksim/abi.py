@@ -9,7 +9,8 @@ import os
 import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "lib", "libksim.so")
+# KSIM_LIB selects another build of the same library (the diagnostic stamps build)
+LIB_PATH = os.environ.get("KSIM_LIB") or os.path.join(PKG_DIR, "lib", "libksim.so")
 
 KSIM_OK = 0
 E_INVAL, E_DEVICE, E_NOMEM, E_UNSUPPORTED, E_STATE, E_OVERFLOW = -1, -2, -3, -4, -5, -6
