@@ -255,6 +255,10 @@ int ksim_read_nodes(ksim_handle* h, ksim_node_state* out);
 int ksim_get_counter(ksim_handle* h, uint64_t* out);
 int ksim_set_counter(ksim_handle* h, uint64_t value);
 
+/* Device self-test of the wave64 DPP reduction/scan helpers the kernels use (diagnostic):
+ * returns the number of mismatching lanes against plain lane loops (0 = pass, <0 = error). */
+int ksim_selftest(void);
+
 #ifdef __cplusplus
 }
 #endif

@@ -353,12 +353,13 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
 
 // Scores travel as 48-bit granule payloads in persistent mode: bound the weights.
 static bool persistent_weights_ok(const KsimCtx& c) {
+  // map scores travel as int32 granule payloads: sum of map weights x MaxPriority < 2^31
   int64_t s = 0;
-  for (int k = 0; k < KSIM_NW; ++k) {
-    if (c.w[k] > ((int64_t)1 << 40)) return false;
+  for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED}) {
+    if (c.w[k] > ((int64_t)1 << 30)) return false;
     s += c.w[k] * 10;
   }
-  return s < ((int64_t)1 << 46);
+  return s < ((int64_t)1 << 31);
 }
 
 static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
@@ -366,7 +367,7 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
   int grid = 0, lds_rows = 0;
   if (!ksim_persistent_config(c.n, &grid, &lds_rows))
     return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: node table does not fit the on-chip layout");
-  if (!persistent_weights_ok(c)) return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: weights exceed the 48-bit score range");
+  if (!persistent_weights_ok(c)) return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: map-priority weights exceed the 31-bit score range");
   const size_t gb = ksim_persistent_granule_bytes(grid);
   if (h->gran_bytes < gb) {
     int rc = dev_alloc(h, &h->granules, gb / sizeof(uint64_t));

@@ -200,3 +200,8 @@ def test_c3_prefix_matches_c_oracle(mode):
     assert s["req_mem"].sum() == cl.pods["add_mem"].sum()
     assert np.array_equal(np.bincount(out, minlength=cl.n_nodes), s["pod_count"])
     assert (s["req_cpu"] <= cl.cols["alloc_cpu"]).all() and (s["req_mem"] <= cl.cols["alloc_mem"]).all()
+
+
+def test_wave_dpp_selftest():
+    """DPP wave reductions / prefix scan used by the persistent kernel vs plain lane loops."""
+    assert abi.lib().ksim_selftest() == 0
