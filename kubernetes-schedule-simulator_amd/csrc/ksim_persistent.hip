@@ -1,38 +1,43 @@
 // ksim_persistent.hip — persistent-kernel mode (KSIM_MODE_PERSISTENT).
 //
 // One launch walks the whole pod queue.  Workgroup b owns the contiguous name-rank range
-// [b*chunk, (b+1)*chunk) of the node table and keeps the hot 60-byte rows of those nodes in
-// LDS for the whole launch (only the owner of a node ever reads or writes it, so node state
-// needs no cross-workgroup coherence).  Per pod p:
-//   a. every workgroup publishes its partial for p — fit count + per reduce class (max map
-//      score, count at max) — as tagged 8-byte granules (one agent-scope store each: the data
-//      is the flag; MI355X_MICROARCH.md "handoff-1to1" / "allgather");
-//   b. it evaluates pod p+1 against its rows SPECULATIVELY (assuming p's winner is not in its
-//      range — true for all but one workgroup) while the other partials of p arrive;
-//   c. one wave per workgroup sweeps every workgroup's granules for p and computes the global
-//      decision redundantly (findNodesThatFit → PrioritizeNodes → selectHost,
-//      core/generic_scheduler.go:112-198, lastNodeIndex replicated in every workgroup) — no
-//      second exchange, no grid barrier;
-//   d. the owner of the selected range picks the exact node from the p scores it still holds
-//      in registers, commits the pod into LDS (NodeInfo.AddPod) and re-evaluates only that
-//      row for p+1, fixing its speculative partial.
-// The critical path per pod is therefore publish → sweep → decide → one-row fix-up; the
-// full-table evaluation of the next pod overlaps the exchange.
-// Granules are double-buffered by pod parity with an 8-bit pod tag: a workgroup that publishes
-// pod p has seen every workgroup's pod p-1 partial, so nobody still reads the p-2 slot it
-// overwrites.  Every spin is bounded (2 s) and reports through the error word.
+// [b*chunk, (b+1)*chunk) of the node table and keeps those rows in LDS for the whole launch
+// (only the owner of a node reads or writes it, so node state needs no cross-workgroup
+// coherence).  Each 512-thread workgroup splits into one CONTROL wave and seven ROW waves:
+//
+//   control wave (wave 0)                      row waves (1..7)
+//   a. publish the partial of pod p            b. evaluate pod p+1 against the rows,
+//      (tagged 8-byte granules)                   speculatively (as if p's winner were not
+//   c. sweep every workgroup's granules of p,     in this range — true for all workgroups
+//      decide (findNodesThatFit →                 but one); wave-level (max, count) into LDS
+//      PrioritizeNodes → selectHost,
+//      core/generic_scheduler.go:112-198)
+//   ------------------------------- barrier -------------------------------
+//   d. owner of p's winner only: pick the exact node from the p scores in registers, commit
+//      it into LDS (NodeInfo.AddPod), re-evaluate that one row for p+1 and redo its wave's
+//      partial.  Then the control wave combines the row waves' partials of p+1.
+//
+// so the full-table evaluation of the next pod runs concurrently with the exchange, and the
+// critical path per pod is publish → sweep → decide → (owner) one-row fix-up.
+// lastNodeIndex is replicated in every workgroup's control wave.  Granules are
+// double-buffered by pod parity with an 8-bit pod tag: a workgroup that publishes pod p has
+// seen every workgroup's pod p-1 partial, so nobody still reads the p-2 slot it overwrites.
+// Every spin is bounded (2 s) and reports through the error word.  Pod descriptors stream
+// through a 4-slot LDS ring two pods ahead, so no 128-byte descriptor is pinned in SGPRs.
 //
 // Granule q of a workgroup: tag:8 | fit:12 (q = 0 only) | count:12 | score:32 (class q max,
-// -1 = no fit node of that class).  Scores are < 2^31 and chunks <= 4095 rows (host checks).
+// -1 = no fit node of that class).  Scores < 2^31 and chunks <= 4095 rows (host checks).
 // Sweep lane l reads workgroups [l*MAXB, l*MAXB+MAXB): name-rank order is lane-major, so the
-// matches above a workgroup are one wave prefix sum away.
-#include "ksim_common.h"
+// matches above a workgroup are one DPP prefix sum away.
+#include "ksim_fast.h"
 #include "ksim_wave.h"
 
 namespace {
 
 constexpr int GR = KSIM_MAX_RCLASS;                  // granules per workgroup per slot
 constexpr int MAXB = 4;                              // workgroups per sweep lane (grid <= 256)
+constexpr int RING = 16;                             // pod-descriptor ring slots in LDS
+constexpr int RING_FILL = 8;                         // descriptors fetched per refill
 constexpr uint64_t SPIN_LIMIT_TICKS = 200000000ull;  // s_memrealtime ticks at 100 MHz = 2 s
 
 typedef __attribute__((address_space(1))) uint64_t gu64;
@@ -49,13 +54,12 @@ __device__ __forceinline__ int32_t gcnt(uint64_t v) { return (int32_t)((v >> 32)
 __device__ __forceinline__ int32_t gscore(uint64_t v) { return (int32_t)(uint32_t)v; }
 
 #ifdef KSIM_STAMPS
+// phase cycle sums kept in registers of block 0's control wave, written once at the end
 #define STAMP(k)                                         \
   do {                                                   \
-    if (blockIdx.x == 0 && tid == 0) {                   \
-      const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
-      c.dbg[k] += t_ - t_prev;                          \
-      t_prev = t_;                                      \
-    }                                                    \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+    st_acc[k] += t_ - t_prev;                           \
+    t_prev = t_;                                        \
   } while (0)
 #else
 #define STAMP(k) \
@@ -63,35 +67,42 @@ __device__ __forceinline__ int32_t gscore(uint64_t v) { return (int32_t)(uint32_
   } while (0)
 #endif
 
-struct PDecision {
-  int32_t mode;  // 0 none fit, 1 single fit, 2 select among winners, -1 abort
-  int32_t blk;   // owner workgroup of the selected node
-  int32_t rank;  // rank from the top (largest name rank) inside that workgroup
-  uint32_t winners;
-  int32_t row;   // owner only: committed row
-  int32_t pad;
-  int32_t M[KSIM_MAX_RCLASS];
-};
+// Packed evaluation of one row for one pod: -1 = does not fit, else class:4 | score:27
+// (map scores < 2^27, host-checked; reduce classes < 16).
+constexpr int EV_SHIFT = 27;
+__device__ __forceinline__ int32_t ev_pack(bool fit, int32_t cl, int32_t sc) { return fit ? (cl << EV_SHIFT) | sc : -1; }
+__device__ __forceinline__ int32_t ev_cls(int32_t e) { return e >> EV_SHIFT; }
+__device__ __forceinline__ int32_t ev_score(int32_t e) { return e & ((1 << EV_SHIFT) - 1); }
 
 struct Rows {  // LDS image of the owned rows (SoA)
   int64_t *ac, *am, *rc, *rm, *zc, *zm;
+  double *ic, *im;  // 1.0 / alloc (0 when alloc == 0): derived, for the fast path
   int32_t *allowed, *count;
   uint32_t* fl;
+  int32_t* ev[2];  // per pod parity: packed evaluation of the row (ev_pack)
 };
+
+constexpr int LDS_ROW_BYTES = 8 * 8 + 3 * 4 + 4 + 2 * 4;  // 88 with padding
 
 __device__ __forceinline__ Rows carve(char* smem, int rows) {
   Rows r;
   int64_t* p = reinterpret_cast<int64_t*>(smem);
   r.ac = p; r.am = p + rows; r.rc = p + 2 * rows; r.rm = p + 3 * rows; r.zc = p + 4 * rows; r.zm = p + 5 * rows;
-  int32_t* q = reinterpret_cast<int32_t*>(p + 6 * rows);
+  double* d = reinterpret_cast<double*>(p + 6 * rows);
+  r.ic = d; r.im = d + rows;
+  int32_t* q = reinterpret_cast<int32_t*>(d + 2 * rows);
   r.allowed = q; r.count = q + rows;
   r.fl = reinterpret_cast<uint32_t*>(q + 2 * rows);
+  r.ev[0] = q + 3 * rows;
+  r.ev[1] = q + 4 * rows;
   return r;
 }
 
 // Commit of the columns that stay in HBM (gpu, ephemeral, scalars, ports) and of the
 // over-commit bits (node_info.go:318-341, utils.go:45-60).  Single thread of the owner.
-__device__ __forceinline__ uint32_t commit_side(const KsimCtx& c, const ksim_pod& P, int64_t w, uint32_t fl) {
+__device__ __noinline__ uint32_t commit_side(const KsimCtx* __restrict__ cg, const ksim_pod* Pp, int64_t w, uint32_t fl) {
+  const KsimCtx& c = *cg;
+  const ksim_pod& P = *Pp;
   const int64_t g = c.req_gpu[w] + P.add_gpu;
   const int64_t e = c.req_eph[w] + P.add_eph;
   c.req_gpu[w] = g;
@@ -119,160 +130,219 @@ __device__ __forceinline__ uint32_t commit_side(const KsimCtx& c, const ksim_pod
 
 // Total score of reduce class q once the per-class maxima over the filtered set are known
 // (NormalizeReduce, priorities/reduce.go:29-64; weighted sum generic_scheduler.go:632-639).
-__device__ __forceinline__ int64_t class_total(const KsimCtx& c, const ksim_pod& P, int q, int k2, int64_t base,
-                                               int64_t mxT, int64_t mxA) {
+__device__ __forceinline__ int64_t class_total(const KsimCtx& c, int32_t cls, int q, int k2, int64_t base, int64_t mxT,
+                                               int64_t mxA) {
   uint64_t t = (uint64_t)base;
   if (c.w[KSIM_W_TAINT_TOLERATION])
     t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] *
-         (uint64_t)ksim_norm(c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2], mxT, true);
+         (uint64_t)ksim_norm(c.tt_val[(int64_t)cls * KSIM_MAX_RCLASS + q / k2], mxT, true);
   if (c.w[KSIM_W_NODE_AFFINITY])
     t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] *
-         (uint64_t)ksim_norm(c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2], mxA, false);
+         (uint64_t)ksim_norm(c.na_val[(int64_t)cls * KSIM_MAX_RCLASS + q % k2], mxA, false);
   return (int64_t)t;
 }
 
-// Per-lane evaluation state of one pod over this lane's NPT rows.
-template <int NPT>
-struct Eval {
-  bool fit[NPT];
-  int32_t sc[NPT];
-  int8_t cl[NPT];
-  uint32_t rm[NPT];
+// General per-row evaluation (any supported pod).  Reads the context through a pointer to
+// its device-memory copy, so no kernel-argument copy goes to scratch.
+struct RowEval {
+  int32_t sc;
+  uint32_t rm;
+  int32_t cl;
+  int32_t fit;
 };
 
-struct PodInfo {
-  int k1, k2, K;
-};
-
-__device__ __forceinline__ PodInfo pod_info(const KsimCtx& c, const ksim_pod& P) {
-  PodInfo I;
-  I.k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
-  I.k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
-  I.K = I.k1 * I.k2;
-  return I;
-}
-
-__device__ __forceinline__ void eval_row(const KsimCtx& c, const Rows& R, const ksim_pod& P, const PodInfo& I,
-                                         int64_t lo, int64_t j, bool& fit, int32_t& sc, int8_t& cl, uint32_t& rm) {
-  const int64_t i = lo + j;
+__device__ __noinline__ RowEval eval_row_general(const KsimCtx* __restrict__ cg, Rows R, const ksim_pod* Pp, int k1,
+                                                 int k2, int64_t i, int64_t j) {
+  const KsimCtx& c = *cg;
+  const ksim_pod& P = *Pp;
   KsimRow r;
   r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j]; r.rm = R.rm[j]; r.zc = R.zc[j]; r.zm = R.zm[j];
   r.allowed = R.allowed[j]; r.count = R.count[j]; r.fl = R.fl[j];
   const uint32_t m = ksim_predicates(c, P, i, r);
-  fit = (m == 0);
-  rm = m;
-  sc = (int32_t)ksim_map_score(c, P, r);
-  cl = (int8_t)((I.K > 1) ? ksim_rclass(c, P, i, I.k1, I.k2) : 0);
+  RowEval e;
+  e.fit = (m == 0);
+  e.rm = m;
+  e.sc = (int32_t)ksim_map_score(c, P, r);
+  e.cl = (k1 * k2 > 1) ? ksim_rclass(c, P, i, k1, k2) : 0;
+  return e;
 }
 
 }  // namespace
 
 template <int BS, int NPT>
-__global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t* granules) {
+__global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const KsimCtx* __restrict__ cg,
+                                                             uint64_t* granules) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NW = BS / 64;
-  __shared__ int32_t s_mx[NW][KSIM_MAX_RCLASS];
-  __shared__ int32_t s_cnt[NW][KSIM_MAX_RCLASS];
-  __shared__ int32_t s_fit[NW];
-  __shared__ uint64_t s_gran[KSIM_MAX_RCLASS];  // next partial to publish (payload, no tag)
-  __shared__ uint64_t s_ball[NPT][NW];
+  constexpr int RT = BS - 64;  // row threads
+  __shared__ int32_t s_mx[2][NW][KSIM_MAX_RCLASS];   // per row wave, double-buffered by pod parity
+  __shared__ int32_t s_cnt[2][NW][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_fit[2][NW];
+  __shared__ int32_t s_fix[2][2];  // per pod parity: {row the owner re-evaluated (-1 none), its reason mask}
   __shared__ int32_t s_hist[KSIM_NREASONS];
   __shared__ int32_t s_M[KSIM_MAX_RCLASS];
   __shared__ int32_t s_C[KSIM_MAX_RCLASS];
-  __shared__ PDecision D;
+  __shared__ int32_t s_mode;
+  __shared__ __attribute__((aligned(16))) ksim_pod s_pod[RING];
+#ifdef KSIM_STAMPS
+  uint64_t st_acc[16] = {};
+#endif
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int rt = tid - 64;  // row-thread index (row waves only)
   const int G = gridDim.x;
   const int64_t chunk = c.chunk;
   const int64_t lo = (int64_t)blockIdx.x * chunk;
   const int64_t hi = (lo + chunk < c.n) ? lo + chunk : c.n;
-  const int64_t nrows = hi - lo;
+  const int32_t nrows = (int32_t)(hi - lo);
   Rows R = carve(smem, (int)chunk);
+  const uint32_t preds = c.preds;
+  const int64_t wl = c.w[KSIM_W_LEAST_REQUESTED], wmr = c.w[KSIM_W_MOST_REQUESTED], wb = c.w[KSIM_W_BALANCED];
+  const bool no_prio = c.no_prio != 0;
 
-  for (int64_t j = tid; j < nrows; j += BS) {  // stage the owned rows into LDS
+  for (int32_t j = tid; j < nrows; j += BS) {  // stage the owned rows into LDS
     const int64_t i = lo + j;
-    R.ac[j] = c.alloc_cpu[i]; R.am[j] = c.alloc_mem[i];
+    const int64_t ac = c.alloc_cpu[i], am = c.alloc_mem[i];
+    R.ac[j] = ac; R.am[j] = am;
+    R.ic[j] = ac ? 1.0 / (double)ac : 0.0;
+    R.im[j] = am ? 1.0 / (double)am : 0.0;
     R.rc[j] = c.req_cpu[i]; R.rm[j] = c.req_mem[i];
     R.zc[j] = c.nz_cpu[i]; R.zm[j] = c.nz_mem[i];
     R.allowed[j] = c.allowed_pods[i]; R.count[j] = c.pod_count[i]; R.fl[j] = c.flags[i];
   }
-  uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex
+  // pod ring: RING_FILL descriptors (1 KiB) per refill, one 16-byte load per lane of wave 1
+  auto ring_load = [&](int64_t p0, uint4& v) {
+    const int64_t p = p0 + lane / 8;
+    if (p < c.end) v = reinterpret_cast<const uint4*>(&c.pods[p])[lane % 8];
+  };
+  auto ring_store = [&](int64_t p0, const uint4& v) {
+    const int64_t p = p0 + lane / 8;
+    if (p < c.end) reinterpret_cast<uint4*>(&s_pod[p % RING])[lane % 8] = v;
+  };
+  if (wv == 1) {
+    uint4 v;
+    ring_load(c.first, v);
+    ring_store(c.first, v);
+  }
+  if (tid == 0) s_fix[c.first & 1][0] = -1;
+  uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex (control wave)
   __syncthreads();
 
-  // evaluate all owned rows for pod Q into E
-  auto eval_all = [&](const ksim_pod& Q, const PodInfo& I, Eval<NPT>& E) {
+  auto pod_K = [&](const ksim_pod& P) -> int {
+    const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
+    const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
+    return k1 * k2;
+  };
+  // one row against pod P → packed entry + reason mask (fast path when the pod qualifies)
+  auto eval_one = [&](const ksim_pod& P, bool fast, int32_t j, uint32_t& rm) -> int32_t {
+    if (fast) {
+      KsimFastPod F{P.req_cpu, P.req_mem, P.nz_cpu, P.nz_mem, P.flags};
+      const int64_t ac = R.ac[j], am = R.am[j];
+      const uint32_t m = ksim_fast_predicates(preds, F, ac, am, R.rc[j], R.rm[j], R.allowed[j], R.count[j], R.fl[j]);
+      rm = m;
+      if (m) return -1;
+      return no_prio ? 0
+                     : (int32_t)ksim_fast_score(F.nz_c + R.zc[j], ac, R.ic[j], F.nz_m + R.zm[j], am, R.im[j], wl, wmr,
+                                                wb);
+    }
+    const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
+    const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
+    const RowEval e = eval_row_general(cg, R, &P, k1, k2, lo + j, j);
+    rm = e.rm;
+    return ev_pack(e.fit != 0, e.cl, e.sc);
+  };
+  // row wave: all rows of this lane for pod p → LDS entries + reason masks
+  auto eval_rows = [&](int64_t p, int32_t (&e)[NPT], uint32_t (&rm)[NPT], int32_t* ev) {
+    const ksim_pod& P = s_pod[p % RING];
+    const bool fast = ksim_is_fast_pod(P, pod_K(P));
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      const int64_t j = (int64_t)k * BS + tid;
-      E.fit[k] = false; E.sc[k] = -1; E.cl[k] = 0; E.rm[k] = 0;
-      if (j < nrows) eval_row(c, R, Q, I, lo, j, E.fit[k], E.sc[k], E.cl[k], E.rm[k]);
+      const int32_t j = k * RT + rt;
+      e[k] = -1;
+      rm[k] = 0;
+      if (j < nrows) {
+        e[k] = eval_one(P, fast, j, rm[k]);
+        ev[j] = e[k];
+      }
     }
   };
-  // block partial of E → s_gran (every thread calls; ends synchronised)
-  auto reduce = [&](const Eval<NPT>& E, int K) {
+  // (fit count, per-class max, count at max) of one row wave's entries → LDS slot w
+  auto partial = [&](const int32_t (&e)[NPT], int K, int buf, int w) {
     int32_t nf = 0;
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) nf += __popcll(__ballot(E.fit[k]));
-    if (lane == 0) s_fit[wv] = nf;
+    for (int k = 0; k < NPT; ++k) nf += __popcll(__ballot(e[k] >= 0));
+    if (K == 1) {  // class 0: the entry is the score
+      int32_t v = -1;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) v = e[k] > v ? e[k] : v;
+      const int32_t wm = ksimw::max_i32(v);
+      int32_t n = 0;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) n += __popcll(__ballot(e[k] == wm));
+      if (lane == 0) { s_fit[buf][w] = nf; s_mx[buf][w][0] = wm; s_cnt[buf][w][0] = wm < 0 ? 0 : n; }
+      return;
+    }
+    if (lane == 0) s_fit[buf][w] = nf;
     for (int q = 0; q < K; ++q) {
       int32_t v = -1;
 #pragma unroll
       for (int k = 0; k < NPT; ++k)
-        if (E.fit[k] && E.cl[k] == q && E.sc[k] > v) v = E.sc[k];
+        if (e[k] >= 0 && ev_cls(e[k]) == q && ev_score(e[k]) > v) v = ev_score(e[k]);
       const int32_t wm = ksimw::max_i32(v);
       int32_t n = 0;
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) n += __popcll(__ballot(E.fit[k] && E.cl[k] == q && E.sc[k] == wm));
-      if (lane == 0) { s_mx[wv][q] = wm; s_cnt[wv][q] = (wm < 0) ? 0 : n; }
+      for (int k = 0; k < NPT; ++k) n += __popcll(__ballot(e[k] >= 0 && ev_cls(e[k]) == q && ev_score(e[k]) == wm));
+      if (lane == 0) { s_mx[buf][w][q] = wm; s_cnt[buf][w][q] = (wm < 0) ? 0 : n; }
     }
-    __syncthreads();
-    if (wv == 0 && lane < K) {
-      int32_t m = -1, n = 0, f = 0;
-#pragma unroll
-      for (int w = 0; w < NW; ++w) {
-        f += s_fit[w];
-        const int32_t cw = s_cnt[w][lane];
-        if (cw == 0) continue;
-        if (s_mx[w][lane] > m) { m = s_mx[w][lane]; n = cw; }
-        else if (s_mx[w][lane] == m) n += cw;
-      }
-      s_gran[lane] = (lane == 0 ? ((uint64_t)f << 44) : 0) | ((uint64_t)n << 32) | (uint64_t)(uint32_t)m;
-    }
-    __syncthreads();
   };
-
-  ksim_pod P = c.pods[c.first];
-  PodInfo IP = pod_info(c, P);
-  Eval<NPT> A, B;
-  eval_all(P, IP, A);
-  reduce(A, IP.K);
-  ksim_pod Pn = c.pods[c.first + 1 < c.end ? c.first + 1 : c.first];
+  // control wave: combine the row waves' partials → granule payloads (lane q = class q)
+  auto combine = [&](int K, int buf) -> uint64_t {
+    const int q = lane < K ? lane : 0;
+    int32_t f = 0, mx[NW], cn[NW];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {  // all loads first: one LDS round trip
+      f += s_fit[buf][w];
+      mx[w] = s_mx[buf][w][q];
+      cn[w] = s_cnt[buf][w][q];
+    }
+    int32_t m = -1, n = 0;
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      const bool up = cn[w] != 0 && mx[w] > m, eq = cn[w] != 0 && mx[w] == m;
+      n = up ? cn[w] : (eq ? n + cn[w] : n);
+      m = up ? mx[w] : m;
+    }
+    if (lane >= K) return 0;
+    return (lane == 0 ? ((uint64_t)f << 44) : 0) | ((uint64_t)n << 32) | (uint64_t)(uint32_t)m;
+  };
+  // ---- prologue: partial of the first pod ----
+  uint32_t A_rm[NPT], B_rm[NPT];
+  if (wv > 0) {
+    int32_t e[NPT];
+    eval_rows(c.first, e, A_rm, R.ev[c.first & 1]);
+    partial(e, pod_K(s_pod[c.first % RING]), c.first & 1, wv);
+  }
+  __syncthreads();
+  uint64_t my_gran = (wv == 0) ? combine(pod_K(s_pod[c.first % RING]), c.first & 1) : 0;
 #ifdef KSIM_STAMPS
   uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
 
   for (int64_t pod = c.first; pod < c.end; ++pod) {
-    const int K = IP.K;
-    const uint64_t tag = (uint64_t)((pod - c.first + 1) & 0xFF);
-    uint64_t* slot = granules + (pod & 1) * (int64_t)G * GR;
-
-    // ---------------- a. publish the partial of pod ----------------
-    if (wv == 0 && lane < K) store_granule(slot + (int64_t)blockIdx.x * GR + lane, (tag << 56) | s_gran[lane]);
-    STAMP(1);
-
-    // ---------------- b. speculative evaluation of pod + 1 ----------------
     const bool has_next = pod + 1 < c.end;
-    const ksim_pod Q = Pn;
-    const PodInfo IQ = pod_info(c, Q);
-    if (has_next) {
-      Pn = c.pods[pod + 2 < c.end ? pod + 2 : pod + 1];
-      eval_all(Q, IQ, B);
-      reduce(B, IQ.K);
-    }
-    STAMP(0);
+    const int pb = (int)(pod & 1);        // LDS buffers of pod
+    const int nb = (int)((pod + 1) & 1);  // LDS buffers of pod + 1
+    int32_t jsel = -1;                    // control wave: row committed by this workgroup
 
-    // ---------------- c. sweep the partials of pod, decide ----------------
     if (wv == 0) {
+      const ksim_pod& P = s_pod[pod % RING];
+      const int K = pod_K(P);
+      // ---------------- a. publish ----------------
+      const uint64_t tag = (uint64_t)((pod - c.first + 1) & 0xFF);
+      uint64_t* slot = granules + (int64_t)pb * G * GR;
+      if (lane < K) store_granule(slot + (int64_t)blockIdx.x * GR + lane, (tag << 56) | my_gran);
+      STAMP(1);
+      // ---------------- c. sweep + decide ----------------
       uint64_t g[MAXB];
       bool ok = false;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -288,7 +358,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
           }
         }
 #ifdef KSIM_STAMPS
-        if (blockIdx.x == 0 && tid == 0) c.dbg[8] += 1;
+        st_acc[8] += 1;
 #endif
         if (__all(mine)) { ok = true; break; }
         if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_LIMIT_TICKS) break;
@@ -311,6 +381,8 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
         M0 = ksimw::max_i32(n ? m : -1);
         C0 = ksimw::sum_i32((n && m == M0) ? n : 0);
       }
+      STAMP(9);
+      const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
       if (ok && K > 1) {  // further reduce classes (TaintToleration x NodeAffinity)
         if (lane == 0) { s_M[0] = M0; s_C[0] = C0; }
         for (int q = 1; q < K; ++q) {
@@ -336,13 +408,13 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
         }
         ok = __all(ok);
       }
+      int mode = 0, blk = -1, rank = 0;
+      uint32_t win = 1;
       if (!ok) {
-        if (lane == 0) { D.mode = -1; atomicOr(c.err, 4); }
-      } else if (F == 0) {
-        if (lane == 0) D.mode = 0;
-      } else {
-        int mode = 1;
-        uint32_t win = 1;
+        mode = -1;
+        if (lane == 0) atomicOr(c.err, 4);
+      } else if (F > 0) {
+        mode = 1;
         int64_t ix = 0;
         if (F > 1) {  // generic_scheduler.go:153-156: a single fit skips selectHost
           mode = 2;
@@ -351,25 +423,26 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
             int64_t mxT = 0, mxA = 0;
             for (int q = 0; q < K; ++q) {
               if (s_C[q] == 0) continue;
-              const int64_t tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / IP.k2];
-              const int64_t av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % IP.k2];
+              const int64_t tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2];
+              const int64_t av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];
               mxT = tv > mxT ? tv : mxT;
               mxA = av > mxA ? av : mxA;
             }
             int64_t best = INT64_MIN;
             for (int q = 0; q < K; ++q)
               if (s_C[q]) {
-                const int64_t t = class_total(c, P, q, IP.k2, s_M[q], mxT, mxA);
+                const int64_t t = class_total(c, P.cls, q, k2, s_M[q], mxT, mxA);
                 best = t > best ? t : best;
               }
             win = 0;
             C = 0;
             for (int q = 0; q < K; ++q)
-              if (s_C[q] && class_total(c, P, q, IP.k2, s_M[q], mxT, mxA) == best) { win |= 1u << q; C += s_C[q]; }
+              if (s_C[q] && class_total(c, P.cls, q, k2, s_M[q], mxT, mxA) == best) { win |= 1u << q; C += s_C[q]; }
           }
-          ix = (int64_t)(counter % (uint64_t)C);  // generic_scheduler.go:192-195
-          counter += 1;
+          ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)C) : (int64_t)((uint32_t)counter % (uint32_t)C);
+          counter += 1;  // generic_scheduler.go:192-195
         }
+        STAMP(10);
         // ---- locate the workgroup holding the ix-th match counted from the top ----
         int32_t bm[MAXB];
         int32_t tot = 0;
@@ -396,105 +469,149 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
         const int32_t total = __builtin_amdgcn_readlane(pre, 63);
         const int64_t above = (int64_t)(total - pre);  // matches in workgroups of higher lanes
         const bool hit = tot > 0 && ix >= above && ix < above + tot;
+        int32_t found = -1, r = 0;
         if (hit) {
-          int64_t r = ix - above;
-          int found = -1;
+          int64_t rr = ix - above;
 #pragma unroll
           for (int j = MAXB - 1; j >= 0; --j) {
             if (found < 0) {
-              if (r < bm[j]) found = lane * MAXB + j;
-              else r -= bm[j];
+              if (rr < bm[j]) found = lane * MAXB + j;
+              else rr -= bm[j];
             }
           }
-          D.mode = found < 0 ? -1 : mode;
-          D.blk = found;
-          D.rank = (int32_t)r;
-          D.winners = win;
-          D.M[0] = M0;
-          if (found < 0) atomicOr(c.err, 2);
+          r = (int32_t)rr;
         }
-        if (K > 1 && lane > 0 && lane < K) D.M[lane] = s_M[lane];
-        if (__ballot(hit) == 0 && lane == 0) { D.mode = -1; atomicOr(c.err, 2); }
+        const uint64_t hb = __ballot(hit);
+        if (hb == 0) {
+          mode = -1;
+        } else {
+          const int src = __builtin_ffsll((long long)hb) - 1;
+          blk = __builtin_amdgcn_readlane(found, src);
+          rank = __builtin_amdgcn_readlane(r, src);
+          if (blk < 0) mode = -1;
+        }
+        if (mode < 0 && lane == 0) atomicOr(c.err, 2);
       }
+      STAMP(3);
+      if (mode > 0 && blk == (int)blockIdx.x) {
+        // ---------------- d. owner: exact row (rank from the top), commit ----------------
+        const int32_t* ev = R.ev[pb];
+        int32_t rr = rank;
+        const int nseg = (nrows + 63) / 64;
+        for (int s0 = nseg - 1; s0 >= 0 && jsel < 0; s0 -= 4) {
+          uint64_t bl[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            const int32_t j = (s0 - u) * 64 + lane;
+            const int32_t e = (s0 - u >= 0 && j < nrows) ? ev[j] : -1;
+            bool mt = e >= 0;
+            if (mode == 2 && mt) {
+              const int q = ev_cls(e);
+              mt = ((win >> q) & 1u) && ev_score(e) == (q == 0 ? M0 : s_M[q]);
+            }
+            bl[u] = __ballot(mt);
+          }
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            if (jsel >= 0) break;
+            uint64_t m = bl[u];
+            const int nbits = __popcll(m);
+            if (rr >= nbits) { rr -= nbits; continue; }
+            for (int t = 0; t < rr; ++t) m &= ~(1ull << (63 - __clzll(m)));
+            jsel = (s0 - u) * 64 + (63 - __clzll(m));
+          }
+        }
+        if (jsel < 0) {
+          mode = -1;
+          if (lane == 0) atomicOr(c.err, 2);
+        } else if (lane == 0) {
+          R.rc[jsel] += P.add_cpu;
+          R.rm[jsel] += P.add_mem;
+          R.zc[jsel] += P.nz_cpu;
+          R.zm[jsel] += P.nz_mem;
+          R.count[jsel] += 1;
+          if (P.add_gpu | P.add_eph | P.scalar_cnt | P.port_cnt) R.fl[jsel] = commit_side(cg, &P, lo + jsel, R.fl[jsel]);
+          c.out_node[pod] = (int32_t)(lo + jsel);
+        }
+      }
+      if (mode == 0 && blockIdx.x == 0 && lane == 0) c.out_node[pod] = -1;
+      if (lane == 0) s_mode = mode;
+      STAMP(6);
+    } else {
+      // ---------------- b. speculative evaluation of pod + 1 (row waves) ----------------
+      // wave 1 refills the descriptor ring every RING_FILL pods; the load's latency hides
+      // under the evaluation, the LDS store lands before the next barrier
+      const bool refill = wv == 1 && ((pod - c.first) % RING_FILL) == 0;
+      uint4 rv;
+      if (refill) ring_load(pod + RING_FILL, rv);
+#ifdef KSIM_STAMPS
+      const uint64_t te0 = __builtin_amdgcn_s_memtime();
+#endif
+      if (has_next) {
+        int32_t e[NPT];
+        eval_rows(pod + 1, e, B_rm, R.ev[nb]);
+        partial(e, pod_K(s_pod[(pod + 1) % RING]), nb, wv);
+      }
+#ifdef KSIM_STAMPS
+      if (tid == 64) st_acc[5] += __builtin_amdgcn_s_memtime() - te0;
+#endif
+      if (refill) ring_store(pod + RING_FILL, rv);
     }
-    STAMP(3);
     __syncthreads();
-    const int mode = D.mode;
+    STAMP(7);
+    const int mode = s_mode;
     if (mode < 0) break;  // uniform: every workgroup reaches the same verdict
 
-    if (mode == 0) {  // FitError: every workgroup adds its reasons; workgroup 0 records it
-      if (c.collect && c.out_reasons) {
-        if (tid < KSIM_NREASONS) s_hist[tid] = 0;
-        __syncthreads();
+    if (mode == 0 && c.collect && c.out_reasons) {  // FitError: every workgroup adds its reasons
+      if (tid < KSIM_NREASONS) s_hist[tid] = 0;
+      __syncthreads();
+      if (wv > 0) {
+        const int32_t fr = s_fix[pb][0];
+        const uint32_t fm = (uint32_t)s_fix[pb][1];
 #pragma unroll
-        for (int k = 0; k < NPT; ++k)
+        for (int k = 0; k < NPT; ++k) {
+          const uint32_t rm = (k * RT + rt == fr) ? fm : A_rm[k];
           for (int r = 0; r < KSIM_NREASONS; ++r) {
-            const int32_t n = __popcll(__ballot((A.rm[k] >> r) & 1u));
+            const int32_t n = __popcll(__ballot((rm >> r) & 1u));
             if (lane == 0 && n) atomicAdd(&s_hist[r], n);
           }
-        __syncthreads();
-        if (tid < KSIM_NREASONS && s_hist[tid]) atomicAdd(&c.out_reasons[pod * KSIM_NREASONS + tid], s_hist[tid]);
-      }
-      if (blockIdx.x == 0 && tid == 0) c.out_node[pod] = -1;
-    } else if (D.blk == (int)blockIdx.x) {
-      // ---------------- d. owner: exact node, commit, fix the speculative partial ----------
-#pragma unroll
-      for (int k = 0; k < NPT; ++k) {
-        bool match = A.fit[k];
-        if (mode == 2) match = A.fit[k] && ((D.winners >> A.cl[k]) & 1u) && A.sc[k] == D.M[A.cl[k]];
-        const uint64_t bal = __ballot(match);
-        if (lane == 0) s_ball[k][wv] = bal;
-      }
-      __syncthreads();
-      if (tid == 0) {
-        int32_t r = D.rank;
-        int32_t j = -1;
-        for (int k = NPT - 1; k >= 0 && j < 0; --k) {
-          for (int w = NW - 1; w >= 0; --w) {
-            uint64_t m = s_ball[k][w];
-            const int nb = __popcll(m);
-            if (r >= nb) { r -= nb; continue; }
-            for (int t = 0; t < r; ++t) m &= ~(1ull << (63 - __clzll(m)));
-            j = k * BS + w * 64 + (63 - __clzll(m));
-            break;
-          }
-        }
-        D.row = j;
-        if (j < 0) {
-          atomicOr(c.err, 2);
-          c.out_node[pod] = -1;
-        } else {
-          const int64_t w = lo + j;
-          R.rc[j] += P.add_cpu;
-          R.rm[j] += P.add_mem;
-          R.zc[j] += P.nz_cpu;
-          R.zm[j] += P.nz_mem;
-          R.count[j] += 1;
-          if (P.add_gpu | P.add_eph | P.scalar_cnt | P.port_cnt) R.fl[j] = commit_side(c, P, w, R.fl[j]);
-          c.out_node[pod] = (int32_t)w;
         }
       }
       __syncthreads();
-      const int32_t j = D.row;
-      if (has_next && j >= 0) {  // only row j changed: re-evaluate it for pod + 1, re-reduce
-        if (j % BS == tid) {
+      if (tid < KSIM_NREASONS && s_hist[tid]) atomicAdd(&c.out_reasons[pod * KSIM_NREASONS + tid], s_hist[tid]);
+    }
+    if (wv == 0 && has_next) {
+      // ---------------- e. owner fix-up of pod + 1, then pod + 1 becomes current ----------------
+      const ksim_pod& Q = s_pod[(pod + 1) % RING];
+      const int Kn = pod_K(Q);
+      if (jsel >= 0) {  // only row jsel changed: re-evaluate it and redo its row wave's partial
+        uint32_t rmj = 0;
+        const int32_t ej = eval_one(Q, ksim_is_fast_pod(Q, Kn), jsel, rmj);
+        const int w = 1 + (jsel % RT) / 64;
+        int32_t e[NPT];
 #pragma unroll
-          for (int k = 0; k < NPT; ++k)
-            if (k == j / BS) eval_row(c, R, Q, IQ, lo, j, B.fit[k], B.sc[k], B.cl[k], B.rm[k]);
+        for (int k = 0; k < NPT; ++k) {
+          const int32_t j = k * RT + (w - 1) * 64 + lane;
+          e[k] = (j == jsel) ? ej : (j < nrows ? R.ev[nb][j] : -1);
         }
-        reduce(B, IQ.K);
+        partial(e, Kn, nb, w);
+        if (lane == 0) { R.ev[nb][jsel] = ej; s_fix[nb][0] = jsel; s_fix[nb][1] = (int32_t)rmj; }
+      } else if (lane == 0) {
+        s_fix[nb][0] = -1;
       }
+      STAMP(11);
+      my_gran = combine(Kn, nb);
     }
     STAMP(4);
-    // ---------------- e. pod + 1 becomes current ----------------
-    A = B;
-    P = Q;
-    IP = IQ;
+    if (wv > 0) {
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) A_rm[k] = B_rm[k];
+    }
   }
 
   // the table is authoritative in HBM between calls: write the owned rows back
   __syncthreads();
-  for (int64_t j = tid; j < nrows; j += BS) {
+  for (int32_t j = tid; j < nrows; j += BS) {
     const int64_t i = lo + j;
     c.req_cpu[i] = R.rc[j]; c.req_mem[i] = R.rm[j];
     c.nz_cpu[i] = R.zc[j]; c.nz_mem[i] = R.zm[j];
@@ -504,6 +621,11 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, uint64_t
     *c.counter = counter;
     *c.cursor = c.end;
   }
+#ifdef KSIM_STAMPS
+  if (blockIdx.x == 0 && tid == 0)
+    for (int k = 0; k < 16; ++k) c.dbg[k] += (k == 5) ? 0 : st_acc[k];
+  if (blockIdx.x == 0 && tid == 64) c.dbg[5] += st_acc[5];
+#endif
 }
 
 // Checks the DPP wave helpers against plain lane loops (diagnostic, tests/ only).
@@ -516,8 +638,7 @@ __global__ void ksim_wave_selftest_kernel(int32_t* out) {
 }
 
 // ---------------------------------------------------------------------------------------
-static constexpr int ROW_BYTES = 60;
-static constexpr int LDS_BUDGET = 96 * 1024;
+static constexpr int LDS_BUDGET = 120 * 1024;
 
 static int num_cus() {
   int dev = 0;
@@ -535,7 +656,7 @@ extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows) {
   if (n < (int64_t)g * 64) g = (int)((n + 63) / 64);  // >= 64 rows per workgroup
   if (g < 1) g = 1;
   const int64_t chunk = (n + g - 1) / g;
-  if (chunk * ROW_BYTES > LDS_BUDGET || chunk > 4095) return 0;  // does not fit: launch mode
+  if (chunk * LDS_ROW_BYTES > LDS_BUDGET || chunk > 4095 || chunk > 8 * 448) return 0;  // launch mode
   *grid = g;
   *lds_rows = (int)chunk;
   return 1;
@@ -543,14 +664,14 @@ extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows) {
 
 extern "C" size_t ksim_persistent_granule_bytes(int grid) { return (size_t)2 * grid * GR * sizeof(uint64_t); }
 
-extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows,
-                                             hipStream_t s) {
-  const size_t lds = (size_t)lds_rows * 64;
+extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
+                                             int lds_rows, hipStream_t s) {
+  const size_t lds = (size_t)lds_rows * LDS_ROW_BYTES;
 #define KSIM_PL(BS, NPT) \
-  hipLaunchKernelGGL((ksim_persistent_kernel<BS, NPT>), dim3(grid), dim3(BS), lds, s, *c, granules)
-  if (lds_rows <= 512) KSIM_PL(512, 1);
-  else if (lds_rows <= 1024) KSIM_PL(512, 2);
-  else if (lds_rows <= 2048) KSIM_PL(512, 4);
+  hipLaunchKernelGGL((ksim_persistent_kernel<BS, NPT>), dim3(grid), dim3(BS), lds, s, *c, cdev, granules)
+  if (lds_rows <= 448) KSIM_PL(512, 1);
+  else if (lds_rows <= 896) KSIM_PL(512, 2);
+  else if (lds_rows <= 1792) KSIM_PL(512, 4);
   else KSIM_PL(512, 8);
 #undef KSIM_PL
   return hipGetLastError();
@@ -563,8 +684,7 @@ extern "C" int ksim_selftest(void) {
   hipLaunchKernelGGL(ksim_wave_selftest_kernel, dim3(nb), dim3(64), 0, 0, d);
   int32_t h[nb * 3 * 64];
   int bad = -1;
-  if (hipDeviceSynchronize() == hipSuccess &&
-      hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) == hipSuccess) {
+  if (hipDeviceSynchronize() == hipSuccess && hipMemcpy(h, d, sizeof h, hipMemcpyDeviceToHost) == hipSuccess) {
     bad = 0;
     for (int b = 0; b < nb; ++b) {
       int32_t v[64], mx = INT32_MIN, sum = 0, pre = 0;

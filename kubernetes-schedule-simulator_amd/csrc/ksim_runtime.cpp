@@ -19,7 +19,8 @@ extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, i
 extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* fit, uint32_t* reasons, int64_t* score,
                                        uint8_t* rcls, hipStream_t s);
 extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, hipStream_t s);
-extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, hipStream_t s);
+extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
+                                             int lds_rows, hipStream_t s);
 extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows);
 extern "C" size_t ksim_persistent_granule_bytes(int grid);
 
@@ -51,6 +52,7 @@ struct ksim_handle {
   hipGraph_t graph = nullptr;
   int g_batch = 0, g_npt = 0, g_collect = -1, part_cap = 0;
   uint64_t* granules = nullptr;
+  KsimCtx* ctx_dev = nullptr;  // device copy of ctx for non-inlined device functions
   size_t gran_bytes = 0;
   int64_t g_first = -1, g_end = -1;
   // host-side copies needed for validation
@@ -353,13 +355,14 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
 
 // Scores travel as 48-bit granule payloads in persistent mode: bound the weights.
 static bool persistent_weights_ok(const KsimCtx& c) {
-  // map scores travel as int32 granule payloads: sum of map weights x MaxPriority < 2^31
+  // map scores are packed into 27 bits of the per-row LDS entry: sum of map weights x
+  // MaxPriority < 2^27
   int64_t s = 0;
   for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED}) {
     if (c.w[k] > ((int64_t)1 << 30)) return false;
     s += c.w[k] * 10;
   }
-  return s < ((int64_t)1 << 31);
+  return s < ((int64_t)1 << 27);
 }
 
 static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
@@ -367,7 +370,7 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
   int grid = 0, lds_rows = 0;
   if (!ksim_persistent_config(c.n, &grid, &lds_rows))
     return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: node table does not fit the on-chip layout");
-  if (!persistent_weights_ok(c)) return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: map-priority weights exceed the 31-bit score range");
+  if (!persistent_weights_ok(c)) return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: map-priority weights exceed the 27-bit score range");
   const size_t gb = ksim_persistent_granule_bytes(grid);
   if (h->gran_bytes < gb) {
     int rc = dev_alloc(h, &h->granules, gb / sizeof(uint64_t));
@@ -377,9 +380,14 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
   c.first = first;
   c.end = first + count;
   c.chunk = (c.n + grid - 1) / grid;
+  if (!h->ctx_dev) {
+    int rc = dev_alloc(h, &h->ctx_dev, 1);
+    if (rc) return rc;
+  }
+  HIPCHK(h, hipMemcpyAsync(h->ctx_dev, &c, sizeof(KsimCtx), hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipError_t e = ksim_launch_persistent(&c, h->granules, grid, lds_rows, h->stream);
+  hipError_t e = ksim_launch_persistent(&c, h->ctx_dev, h->granules, grid, lds_rows, h->stream);
   if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   HIPCHK(h, hipEventSynchronize(h->ev1));
@@ -390,9 +398,13 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
     uint64_t d[16];
     HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
     HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
-    fprintf(stderr, "[ksim stamps] pods=%lld cycles/pod: eval+reduce %.0f publish %.0f sweep %.0f decide %.0f commit+sync %.0f polls/pod %.2f (%.3f ms)\n",
-            (long long)count, d[0] / (double)count, d[1] / (double)count, d[2] / (double)count, d[3] / (double)count,
-            d[4] / (double)count, d[8] / (double)count, ms);
+    // slots: 1 publish, 2 sweep, 9 reduce, 10 selectHost index, 3 locate, 6 select+commit,
+    // 7 barrier, 11 fix-up, 4 combine, 5 row-wave evaluation (concurrent), 8 polls
+    static const char* names[16] = {"", "publish", "sweep", "locate", "combine", "row-eval", "select+commit", "barrier",
+                                    "polls", "reduce", "ix", "fixup", "", "", "", ""};
+    fprintf(stderr, "[ksim stamps] pods=%lld (%.3f ms) cycles/pod:", (long long)count, ms);
+    for (int k : {1, 2, 9, 10, 3, 6, 7, 11, 4, 5, 8}) fprintf(stderr, " %s %.0f", names[k], d[k] / (double)count);
+    fprintf(stderr, "\n");
   }
 #endif
   if (st) {
