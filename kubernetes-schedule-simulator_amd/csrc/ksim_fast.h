@@ -6,15 +6,15 @@
 // CheckNodeMemoryPressure, CheckNodeDiskPressure.  (HostName, PodFitsHostPorts,
 // MatchNodeSelector and PodToleratesNodeTaints pass by construction.)
 //
-// Scores without a divide on the common path, still bit-exact:
+// Scores in straight-line float64, still bit-exact, for requests and capacities below 2^49
+// (larger operands take the int64 path of ksim_common.h):
 //  * LeastRequested / MostRequested (least_requested.go:44-53, most_requested.go:45-55) are
-//    floor(10*(cap-req)/cap) and floor(10*req/cap) in int64: an estimate from a per-node
-//    reciprocal is off by at most one and is corrected with two int64 multiplies.
-//  * BalancedResourceAllocation (balanced_resource_allocation.go:39-61) truncates
-//    (1-|fc-fm|)*10 computed from correctly rounded fc = req/cap, fm.  The reciprocal estimate
-//    is within ~1e-14 of the real value; whenever it is farther than 1e-9 from an integer (and
-//    from the fc/fm >= 1 boundary) the truncation equals the reference's, otherwise the exact
-//    IEEE divide sequence runs.
+//    floor(x / cap) with x = 10*(cap-req) or 10*req, integers below 2^53 and so exact in
+//    float64.  The correctly rounded quotient never crosses an integer: if x/cap lies in
+//    (k, k+1) then k+1 - x/cap >= 1/cap > 2^-49 >= ulp(k+1)/2 for k+1 <= 10, so truncating it
+//    gives the int64 quotient.
+//  * BalancedResourceAllocation (balanced_resource_allocation.go:39-61) is the reference's own
+//    float64 expression (correctly rounded divides, no FMA contraction: -ffp-contract=off).
 #pragma once
 #include "ksim_common.h"
 
@@ -24,20 +24,15 @@ struct KsimFastPod {
   uint32_t flags;       // KSIM_POD_*
 };
 
-__device__ __forceinline__ int64_t ksim_fix_q(int32_t q, int64_t x, int64_t b) {
-  // q in [0, 11] approximates floor(x / b), 0 <= x < 2^53, 0 < b < 2^49, |error| <= 1
-  q = q < 0 ? 0 : q;
-  const int64_t qb = (int64_t)q * b;
-  if (qb > x) return q - 1;
-  if (qb + b <= x) return q + 1;
-  return q;
-}
+// One node row as the fast path needs it (dac/dam = alloc as float64, exact below 2^53).
+struct KsimFastRow {
+  int64_t ac, am, rc, rm, zc, zm;
+  double dac, dam;
+  int32_t allowed, count;
+  uint32_t fl;
+};
 
-__device__ __noinline__ int64_t ksim_bra_exact(int64_t tc, int64_t ac, int64_t tm, int64_t am) {
-  return ksim_balanced(tc, ac, tm, am);
-}
-
-// Generic (divide-based) weighted score: operands beyond 2^49, kept out of line.
+// Generic (divide-based) weighted score: operands at or beyond 2^49, kept out of line.
 __device__ __noinline__ int64_t ksim_slow_score(int64_t tc, int64_t ac, int64_t tm, int64_t am, int64_t wl, int64_t wm,
                                                 int64_t wb) {
   uint64_t s = 0;
@@ -47,38 +42,29 @@ __device__ __noinline__ int64_t ksim_slow_score(int64_t tc, int64_t ac, int64_t 
   return (int64_t)s;
 }
 
-// Weighted map score (LR/MR/BRA) of one node; inv_* = 1.0 / alloc (0 when alloc == 0).
-__device__ __forceinline__ int64_t ksim_fast_score(int64_t tc, int64_t ac, double ic, int64_t tm, int64_t am, double im,
+// Weighted map score (LR/MR/BRA) of one node: tc/tm = pod non-zero request + node non-zero
+// requested (resource_allocation.go:58-59).
+__device__ __forceinline__ int64_t ksim_fast_score(int64_t tc, int64_t ac, double dac, int64_t tm, int64_t am, double dam,
                                                    int64_t wl, int64_t wm, int64_t wb) {
-  if (((tc | ac | tm | am) >> 49) != 0 || tc < 0 || tm < 0) return ksim_slow_score(tc, ac, tm, am, wl, wm, wb);
-  const double fc = ac ? (double)tc * ic : 1.0;  // estimates of req / cap
-  const double fm = am ? (double)tm * im : 1.0;
+  if (((uint64_t)(tc | ac | tm | am)) >> 49) return ksim_slow_score(tc, ac, tm, am, wl, wm, wb);
+  const double xc = (double)tc, xm = (double)tm;
+  const bool okc = ac != 0 && tc <= ac, okm = am != 0 && tm <= am;
+  const double bc = ac ? dac : 1.0, bm = am ? dam : 1.0;
   int64_t s = 0;
-  if (wl | wm) {
-    int64_t lc = 0, lm = 0, mc = 0, mm = 0;
-    if (ac != 0 && tc <= ac) {
-      lc = ksim_fix_q((int32_t)(10.0 - 10.0 * fc), (ac - tc) * 10, ac);
-      mc = ksim_fix_q((int32_t)(10.0 * fc), tc * 10, ac);
-    }
-    if (am != 0 && tm <= am) {
-      lm = ksim_fix_q((int32_t)(10.0 - 10.0 * fm), (am - tm) * 10, am);
-      mm = ksim_fix_q((int32_t)(10.0 * fm), tm * 10, am);
-    }
-    s += wl * ((lc + lm) / 2) + wm * ((mc + mm) / 2);
+  if (wl) {
+    const int32_t lc = okc ? (int32_t)((bc - xc) * 10.0 / bc) : 0;
+    const int32_t lm = okm ? (int32_t)((bm - xm) * 10.0 / bm) : 0;
+    s += wl * ((lc + lm) / 2);
+  }
+  if (wm) {
+    const int32_t mc = okc ? (int32_t)(xc * 10.0 / bc) : 0;
+    const int32_t mm = okm ? (int32_t)(xm * 10.0 / bm) : 0;
+    s += wm * ((mc + mm) / 2);
   }
   if (wb) {
-    int64_t b;
-    const bool near_one = fabs(fc - 1.0) < 1e-12 || fabs(fm - 1.0) < 1e-12;
-    if (near_one) {
-      b = ksim_bra_exact(tc, ac, tm, am);
-    } else if (fc >= 1.0 || fm >= 1.0) {
-      b = 0;
-    } else {
-      const double v = (1.0 - fabs(fc - fm)) * 10.0;
-      const double fl = floor(v);
-      const double fr = v - fl;
-      b = (fr < 1e-9 || fr > 1.0 - 1e-9) ? ksim_bra_exact(tc, ac, tm, am) : (int64_t)fl;
-    }
+    const double fc = ac ? xc / bc : 1.0;
+    const double fm = am ? xm / bm : 1.0;
+    const int32_t b = (fc >= 1.0 || fm >= 1.0) ? 0 : (int32_t)((1.0 - fabs(fc - fm)) * 10.0);
     s += wb * b;
   }
   return s;
@@ -88,25 +74,36 @@ __device__ __forceinline__ int64_t ksim_fast_score(int64_t tc, int64_t ac, doubl
 __device__ __forceinline__ uint32_t ksim_fast_predicates(uint32_t preds, const KsimFastPod& P, int64_t ac,
                                                          int64_t am, int64_t rc, int64_t rm, int32_t allowed,
                                                          int32_t count, uint32_t fl) {
-  if (preds & KSIM_P_CHECK_NODE_CONDITION) {
-    const uint32_t m = fl & KSIM_COND_REASON_MASK;
-    if (m) return m;
-  }
-  if ((preds & KSIM_P_CHECK_NODE_UNSCHEDULABLE) && (fl & KSIM_N_UNSCHEDULABLE)) return 1u << KSIM_R_UNSCHEDULABLE;
+  // evaluated branch-free, then the first failing predicate in order wins
+  const uint32_t cond = (preds & KSIM_P_CHECK_NODE_CONDITION) ? (fl & KSIM_COND_REASON_MASK) : 0u;
+  const uint32_t unsch =
+      ((preds & KSIM_P_CHECK_NODE_UNSCHEDULABLE) && (fl & KSIM_N_UNSCHEDULABLE)) ? (1u << KSIM_R_UNSCHEDULABLE) : 0u;
+  uint32_t res = 0;
   if (preds & (KSIM_P_GENERAL | KSIM_P_RESOURCES)) {
-    uint32_t m = (count + 1 > allowed) ? (1u << KSIM_R_INSUFFICIENT_PODS) : 0u;
+    res = (count + 1 > allowed) ? (1u << KSIM_R_INSUFFICIENT_PODS) : 0u;
     if (P.flags & KSIM_POD_ANY_REQUEST) {
-      if (ac < P.rq_c + rc) m |= 1u << KSIM_R_INSUFFICIENT_CPU;
-      if (am < P.rq_m + rm) m |= 1u << KSIM_R_INSUFFICIENT_MEMORY;
-      if (fl & KSIM_N_GPU_OVER) m |= 1u << KSIM_R_INSUFFICIENT_GPU;
-      if (fl & KSIM_N_EPH_OVER) m |= 1u << KSIM_R_INSUFFICIENT_EPHEMERAL;
+      res |= (ac < P.rq_c + rc) ? (1u << KSIM_R_INSUFFICIENT_CPU) : 0u;
+      res |= (am < P.rq_m + rm) ? (1u << KSIM_R_INSUFFICIENT_MEMORY) : 0u;
+      res |= (fl & KSIM_N_GPU_OVER) ? (1u << KSIM_R_INSUFFICIENT_GPU) : 0u;
+      res |= (fl & KSIM_N_EPH_OVER) ? (1u << KSIM_R_INSUFFICIENT_EPHEMERAL) : 0u;
     }
-    if (m) return m;
   }
-  if ((preds & KSIM_P_MEM_PRESSURE) && (P.flags & KSIM_POD_BEST_EFFORT) && (fl & KSIM_N_MEM_PRESSURE))
-    return 1u << KSIM_R_MEM_PRESSURE;
-  if ((preds & KSIM_P_DISK_PRESSURE) && (fl & KSIM_N_DISK_PRESSURE)) return 1u << KSIM_R_DISK_PRESSURE;
-  return 0;
+  const uint32_t memp = ((preds & KSIM_P_MEM_PRESSURE) && (P.flags & KSIM_POD_BEST_EFFORT) && (fl & KSIM_N_MEM_PRESSURE))
+                            ? (1u << KSIM_R_MEM_PRESSURE)
+                            : 0u;
+  const uint32_t diskp = ((preds & KSIM_P_DISK_PRESSURE) && (fl & KSIM_N_DISK_PRESSURE)) ? (1u << KSIM_R_DISK_PRESSURE) : 0u;
+  return cond ? cond : unsch ? unsch : res ? res : memp ? memp : diskp;
+}
+
+// Packed evaluation of a row for a resource-only pod (-1 = does not fit, else the score) and
+// its reason mask.
+__device__ __forceinline__ int32_t ksim_fast_eval(uint32_t preds, const KsimFastPod& F, const KsimFastRow& r,
+                                                  bool no_prio, int64_t wl, int64_t wm, int64_t wb, uint32_t& rm) {
+  const uint32_t m = ksim_fast_predicates(preds, F, r.ac, r.am, r.rc, r.rm, r.allowed, r.count, r.fl);
+  rm = m;
+  const int32_t sc =
+      no_prio ? 0 : (int32_t)ksim_fast_score(F.nz_c + r.zc, r.ac, r.dac, F.nz_m + r.zm, r.am, r.dam, wl, wm, wb);
+  return m ? -1 : sc;
 }
 
 // Does pod P qualify for the fast path under this configuration?

@@ -39,6 +39,8 @@ constexpr int MAXB = 4;                              // workgroups per sweep lan
 constexpr int RING = 16;                             // pod-descriptor ring slots in LDS
 constexpr int RING_FILL = 8;                         // descriptors fetched per refill
 constexpr uint64_t SPIN_LIMIT_TICKS = 200000000ull;  // s_memrealtime ticks at 100 MHz = 2 s
+constexpr int NSLOT = 4;                             // granule slots (pod mod NSLOT)
+constexpr int MAXG = 64 * MAXB;                      // workgroups a slot is sized for
 
 typedef __attribute__((address_space(1))) uint64_t gu64;
 
@@ -47,6 +49,16 @@ __device__ __forceinline__ void store_granule(uint64_t* g, uint64_t v) {
 }
 __device__ __forceinline__ uint64_t load_granule(const uint64_t* g) {
   return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// speculative partial of workgroup b for the pod in `slot`, and the previous owner's correction
+__device__ __forceinline__ uint64_t* spec_at(uint64_t* gr, int slot, int b, int q) {
+  return gr + ((int64_t)slot * MAXG + b) * GR + q;
+}
+__device__ __forceinline__ uint64_t* fix_at(uint64_t* gr, int slot, int q) {
+  return gr + (int64_t)NSLOT * MAXG * GR + (int64_t)slot * GR + q;
+}
+__device__ __forceinline__ uint64_t* gran_at(uint64_t* gr, int slot, int b, int q, int X) {
+  return b == X ? fix_at(gr, slot, q) : spec_at(gr, slot, b, q);
 }
 __device__ __forceinline__ uint32_t gtag(uint64_t v) { return (uint32_t)(v >> 56); }
 __device__ __forceinline__ int32_t gfit(uint64_t v) { return (int32_t)((v >> 44) & 0xFFF); }
@@ -61,7 +73,17 @@ __device__ __forceinline__ int32_t gscore(uint64_t v) { return (int32_t)(uint32_
     st_acc[k] += t_ - t_prev;                           \
     t_prev = t_;                                        \
   } while (0)
+// owner-side phase durations, summed over whichever workgroup owns each pod
+#define OSTAMP(k)                                                        \
+  do {                                                                   \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();                   \
+    if (lane == 0) atomicAdd((unsigned long long*)&c.dbg[k], t_ - o_prev); \
+    o_prev = t_;                                                         \
+  } while (0)
 #else
+#define OSTAMP(k) \
+  do {            \
+  } while (0)
 #define STAMP(k) \
   do {           \
   } while (0)
@@ -76,25 +98,26 @@ __device__ __forceinline__ int32_t ev_score(int32_t e) { return e & ((1 << EV_SH
 
 struct Rows {  // LDS image of the owned rows (SoA)
   int64_t *ac, *am, *rc, *rm, *zc, *zm;
-  double *ic, *im;  // 1.0 / alloc (0 when alloc == 0): derived, for the fast path
+  double *dac, *dam;  // alloc as float64 (derived, for the fast path)
   int32_t *allowed, *count;
   uint32_t* fl;
-  int32_t* ev[2];  // per pod parity: packed evaluation of the row (ev_pack)
+  int32_t* ev;  // [2][rows] per pod parity: packed evaluation of the row (ev_pack)
 };
 
 constexpr int LDS_ROW_BYTES = 8 * 8 + 3 * 4 + 4 + 2 * 4;  // 88 with padding
+
+extern __shared__ __attribute__((aligned(16))) char ksim_smem[];  // dynamic LDS: the row image
 
 __device__ __forceinline__ Rows carve(char* smem, int rows) {
   Rows r;
   int64_t* p = reinterpret_cast<int64_t*>(smem);
   r.ac = p; r.am = p + rows; r.rc = p + 2 * rows; r.rm = p + 3 * rows; r.zc = p + 4 * rows; r.zm = p + 5 * rows;
   double* d = reinterpret_cast<double*>(p + 6 * rows);
-  r.ic = d; r.im = d + rows;
+  r.dac = d; r.dam = d + rows;
   int32_t* q = reinterpret_cast<int32_t*>(d + 2 * rows);
   r.allowed = q; r.count = q + rows;
   r.fl = reinterpret_cast<uint32_t*>(q + 2 * rows);
-  r.ev[0] = q + 3 * rows;
-  r.ev[1] = q + 4 * rows;
+  r.ev = q + 3 * rows;
   return r;
 }
 
@@ -151,10 +174,11 @@ struct RowEval {
   int32_t fit;
 };
 
-__device__ __noinline__ RowEval eval_row_general(const KsimCtx* __restrict__ cg, Rows R, const ksim_pod* Pp, int k1,
+__device__ __noinline__ RowEval eval_row_general(const KsimCtx* __restrict__ cg, int chunk, const ksim_pod* Pp, int k1,
                                                  int k2, int64_t i, int64_t j) {
   const KsimCtx& c = *cg;
   const ksim_pod& P = *Pp;
+  const Rows R = carve(ksim_smem, chunk);
   KsimRow r;
   r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j]; r.rm = R.rm[j]; r.zc = R.zc[j]; r.zm = R.zm[j];
   r.allowed = R.allowed[j]; r.count = R.count[j]; r.fl = R.fl[j];
@@ -172,17 +196,19 @@ __device__ __noinline__ RowEval eval_row_general(const KsimCtx* __restrict__ cg,
 template <int BS, int NPT>
 __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const KsimCtx* __restrict__ cg,
                                                              uint64_t* granules) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int NW = BS / 64;
   constexpr int RT = BS - 64;  // row threads
   __shared__ int32_t s_mx[2][NW][KSIM_MAX_RCLASS];   // per row wave, double-buffered by pod parity
   __shared__ int32_t s_cnt[2][NW][KSIM_MAX_RCLASS];
   __shared__ int32_t s_fit[2][NW];
+  __shared__ uint64_t s_fm[2][NPT][NW];  // single-class pods: per 64-row segment, fit rows
+  __shared__ uint64_t s_bm[2][NPT][NW];  // ... and rows at the wave maximum
   __shared__ int32_t s_fix[2][2];  // per pod parity: {row the owner re-evaluated (-1 none), its reason mask}
   __shared__ int32_t s_hist[KSIM_NREASONS];
   __shared__ int32_t s_M[KSIM_MAX_RCLASS];
   __shared__ int32_t s_C[KSIM_MAX_RCLASS];
   __shared__ int32_t s_mode;
+  __shared__ int32_t s_arr;  // row-wave arrivals (the last one of a pod publishes)
   __shared__ __attribute__((aligned(16))) ksim_pod s_pod[RING];
 #ifdef KSIM_STAMPS
   uint64_t st_acc[16] = {};
@@ -195,7 +221,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   const int64_t lo = (int64_t)blockIdx.x * chunk;
   const int64_t hi = (lo + chunk < c.n) ? lo + chunk : c.n;
   const int32_t nrows = (int32_t)(hi - lo);
-  Rows R = carve(smem, (int)chunk);
+  Rows R = carve(ksim_smem, (int)chunk);
   const uint32_t preds = c.preds;
   const int64_t wl = c.w[KSIM_W_LEAST_REQUESTED], wmr = c.w[KSIM_W_MOST_REQUESTED], wb = c.w[KSIM_W_BALANCED];
   const bool no_prio = c.no_prio != 0;
@@ -204,8 +230,8 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     const int64_t i = lo + j;
     const int64_t ac = c.alloc_cpu[i], am = c.alloc_mem[i];
     R.ac[j] = ac; R.am[j] = am;
-    R.ic[j] = ac ? 1.0 / (double)ac : 0.0;
-    R.im[j] = am ? 1.0 / (double)am : 0.0;
+    R.dac[j] = (double)ac;
+    R.dam[j] = (double)am;
     R.rc[j] = c.req_cpu[i]; R.rm[j] = c.req_mem[i];
     R.zc[j] = c.nz_cpu[i]; R.zm[j] = c.nz_mem[i];
     R.allowed[j] = c.allowed_pods[i]; R.count[j] = c.pod_count[i]; R.fl[j] = c.flags[i];
@@ -224,7 +250,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     ring_load(c.first, v);
     ring_store(c.first, v);
   }
-  if (tid == 0) s_fix[c.first & 1][0] = -1;
+  if (tid == 0) { s_fix[c.first & 1][0] = -1; s_arr = 0; }
   uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex (control wave)
   __syncthreads();
 
@@ -234,20 +260,21 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     return k1 * k2;
   };
   // one row against pod P → packed entry + reason mask (fast path when the pod qualifies)
+  auto load_row = [&](int32_t j) -> KsimFastRow {
+    KsimFastRow r;
+    r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j]; r.rm = R.rm[j]; r.zc = R.zc[j]; r.zm = R.zm[j];
+    r.dac = R.dac[j]; r.dam = R.dam[j];
+    r.allowed = R.allowed[j]; r.count = R.count[j]; r.fl = R.fl[j];
+    return r;
+  };
   auto eval_one = [&](const ksim_pod& P, bool fast, int32_t j, uint32_t& rm) -> int32_t {
     if (fast) {
-      KsimFastPod F{P.req_cpu, P.req_mem, P.nz_cpu, P.nz_mem, P.flags};
-      const int64_t ac = R.ac[j], am = R.am[j];
-      const uint32_t m = ksim_fast_predicates(preds, F, ac, am, R.rc[j], R.rm[j], R.allowed[j], R.count[j], R.fl[j]);
-      rm = m;
-      if (m) return -1;
-      return no_prio ? 0
-                     : (int32_t)ksim_fast_score(F.nz_c + R.zc[j], ac, R.ic[j], F.nz_m + R.zm[j], am, R.im[j], wl, wmr,
-                                                wb);
+      const KsimFastPod F{P.req_cpu, P.req_mem, P.nz_cpu, P.nz_mem, P.flags};
+      return ksim_fast_eval(preds, F, load_row(j), no_prio, wl, wmr, wb, rm);
     }
     const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
     const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
-    const RowEval e = eval_row_general(cg, R, &P, k1, k2, lo + j, j);
+    const RowEval e = eval_row_general(cg, (int)chunk, &P, k1, k2, lo + j, j);
     rm = e.rm;
     return ev_pack(e.fit != 0, e.cl, e.sc);
   };
@@ -268,9 +295,13 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   };
   // (fit count, per-class max, count at max) of one row wave's entries → LDS slot w
   auto partial = [&](const int32_t (&e)[NPT], int K, int buf, int w) {
+    uint64_t fm[NPT];
     int32_t nf = 0;
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) nf += __popcll(__ballot(e[k] >= 0));
+    for (int k = 0; k < NPT; ++k) {
+      fm[k] = __ballot(e[k] >= 0);
+      nf += __popcll(fm[k]);
+    }
     if (K == 1) {  // class 0: the entry is the score
       int32_t v = -1;
 #pragma unroll
@@ -278,8 +309,12 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       const int32_t wm = ksimw::max_i32(v);
       int32_t n = 0;
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) n += __popcll(__ballot(e[k] == wm));
-      if (lane == 0) { s_fit[buf][w] = nf; s_mx[buf][w][0] = wm; s_cnt[buf][w][0] = wm < 0 ? 0 : n; }
+      for (int k = 0; k < NPT; ++k) {
+        const uint64_t bm = wm < 0 ? 0ull : __ballot(e[k] == wm);
+        n += __popcll(bm);
+        if (lane == 0) { s_fm[buf][k][w] = fm[k]; s_bm[buf][k][w] = bm; }
+      }
+      if (lane == 0) { s_fit[buf][w] = nf; s_mx[buf][w][0] = wm; s_cnt[buf][w][0] = n; }
       return;
     }
     if (lane == 0) s_fit[buf][w] = nf;
@@ -315,15 +350,31 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     if (lane >= K) return 0;
     return (lane == 0 ? ((uint64_t)f << 44) : 0) | ((uint64_t)n << 32) | (uint64_t)(uint32_t)m;
   };
+  auto ptag = [&](int64_t p) -> uint64_t { return (uint64_t)((p - c.first + 1) & 0xFF); };
+  // row waves: the last one to finish pod p's partial combines and publishes it
+  auto arrive_publish = [&](int64_t p, int K, int buf) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    int32_t old = 0;
+    if (lane == 0) old = atomicAdd(&s_arr, 1);
+    old = __builtin_amdgcn_readfirstlane(old);
+    if ((old + 1) % (NW - 1) == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+      const uint64_t v = combine(K, buf);
+      if (lane < K) store_granule(spec_at(granules, (int)(p % NSLOT), blockIdx.x, lane), (ptag(p) << 56) | v);
+    }
+  };
+
   // ---- prologue: partial of the first pod ----
   uint32_t A_rm[NPT], B_rm[NPT];
   if (wv > 0) {
     int32_t e[NPT];
-    eval_rows(c.first, e, A_rm, R.ev[c.first & 1]);
-    partial(e, pod_K(s_pod[c.first % RING]), c.first & 1, wv);
+    const int K0 = pod_K(s_pod[c.first % RING]);
+    eval_rows(c.first, e, A_rm, R.ev + (c.first & 1) * chunk);
+    partial(e, K0, c.first & 1, wv);
+    arrive_publish(c.first, K0, c.first & 1);
   }
+  int X = -1;  // control wave: owner workgroup of the previous pod's node (-1: none)
   __syncthreads();
-  uint64_t my_gran = (wv == 0) ? combine(pod_K(s_pod[c.first % RING]), c.first & 1) : 0;
 #ifdef KSIM_STAMPS
   uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
@@ -333,38 +384,60 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     const int pb = (int)(pod & 1);        // LDS buffers of pod
     const int nb = (int)((pod + 1) & 1);  // LDS buffers of pod + 1
     int32_t jsel = -1;                    // control wave: row committed by this workgroup
+    bool have_pre = false;                // ... and its pod + 1 evaluation, when computed early
+    int32_t ej_pre = -1;
+    uint32_t rm_pre = 0;
+#ifdef KSIM_STAMPS
+    uint64_t o_prev = 0;
+#endif
 
     if (wv == 0) {
       const ksim_pod& P = s_pod[pod % RING];
       const int K = pod_K(P);
-      // ---------------- a. publish ----------------
-      const uint64_t tag = (uint64_t)((pod - c.first + 1) & 0xFF);
-      uint64_t* slot = granules + (int64_t)pb * G * GR;
-      if (lane < K) store_granule(slot + (int64_t)blockIdx.x * GR + lane, (tag << 56) | my_gran);
+      // ---------------- a. sweep: every speculative partial of pod + the owner's correction ----
+      const uint64_t tag = ptag(pod);
+      const int slot = (int)(pod % NSLOT);
       STAMP(1);
-      // ---------------- c. sweep + decide ----------------
       uint64_t g[MAXB];
       bool ok = false;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+#ifdef KSIM_STAMPS
+      bool seen_spec = false, seen_fix = false;
+#endif
       for (;;) {
-        bool mine = true;
+        // unconditional loads (slots are sized for MAXG workgroups): one fabric round trip
+#pragma unroll
+        for (int j = 0; j < MAXB; ++j) g[j] = load_granule(spec_at(granules, slot, lane * MAXB + j, 0));
+        const uint64_t fx = load_granule(fix_at(granules, slot, 0));
+        bool mine = X < 0 || gtag(fx) == tag;
 #pragma unroll
         for (int j = 0; j < MAXB; ++j) {
           const int b = lane * MAXB + j;
-          g[j] = 0;
-          if (b < G) {
-            g[j] = load_granule(slot + (int64_t)b * GR);
-            mine &= gtag(g[j]) == tag;
-          }
+          mine &= (b >= G) || b == X || gtag(g[j]) == tag;
         }
 #ifdef KSIM_STAMPS
         st_acc[8] += 1;
+        {
+          bool sp = true;
+#pragma unroll
+          for (int j = 0; j < MAXB; ++j) sp &= (lane * MAXB + j >= G) || lane * MAXB + j == X || gtag(g[j]) == tag;
+          const uint64_t tn = __builtin_amdgcn_s_memtime();
+          if (!seen_spec && __all(sp)) { seen_spec = true; st_acc[12] += tn - t_prev; }
+          if (!seen_fix && (X < 0 || gtag(fx) == tag)) { seen_fix = true; st_acc[13] += tn - t_prev; }
+        }
 #endif
-        if (__all(mine)) { ok = true; break; }
+        if (__all(mine)) {
+          ok = true;
+#pragma unroll
+          for (int j = 0; j < MAXB; ++j) g[j] = (lane * MAXB + j == X) ? fx : g[j];
+          break;
+        }
         if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_LIMIT_TICKS) break;
         __builtin_amdgcn_s_sleep(1);
       }
       STAMP(2);
+#pragma unroll
+      for (int j = 0; j < MAXB; ++j) g[j] = (lane * MAXB + j < G) ? g[j] : 0;
       ok = __all(ok);
       int32_t F = 0, M0 = -1, C0 = 0;
       if (ok) {
@@ -393,7 +466,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
             uint64_t v = 0;
             const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
             for (;;) {
-              v = load_granule(slot + (int64_t)b * GR + q);
+              v = load_granule(gran_at(granules, slot, b, q, X));
               if (gtag(v) == tag) break;
               if (__builtin_amdgcn_s_memrealtime() - t1 > SPIN_LIMIT_TICKS) { ok = false; break; }
             }
@@ -457,7 +530,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
               if ((win & 1u) && gcnt(g[j]) && gscore(g[j]) == M0) m += gcnt(g[j]);
               for (int q = 1; q < K; ++q) {
                 if (!((win >> q) & 1u)) continue;
-                const uint64_t v = load_granule(slot + (int64_t)b * GR + q);
+                const uint64_t v = load_granule(gran_at(granules, slot, b, q, X));
                 if (gcnt(v) && gscore(v) == s_M[q]) m += gcnt(v);
               }
             }
@@ -493,49 +566,90 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         if (mode < 0 && lane == 0) atomicOr(c.err, 2);
       }
       STAMP(3);
+#ifdef KSIM_STAMPS
+      o_prev = __builtin_amdgcn_s_memtime();
+#endif
       if (mode > 0 && blk == (int)blockIdx.x) {
         // ---------------- d. owner: exact row (rank from the top), commit ----------------
-        const int32_t* ev = R.ev[pb];
-        int32_t rr = rank;
-        const int nseg = (nrows + 63) / 64;
-        for (int s0 = nseg - 1; s0 >= 0 && jsel < 0; s0 -= 4) {
-          uint64_t bl[4];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            const int32_t j = (s0 - u) * 64 + lane;
-            const int32_t e = (s0 - u >= 0 && j < nrows) ? ev[j] : -1;
-            bool mt = e >= 0;
-            if (mode == 2 && mt) {
-              const int q = ev_cls(e);
-              mt = ((win >> q) & 1u) && ev_score(e) == (q == 0 ? M0 : s_M[q]);
-            }
-            bl[u] = __ballot(mt);
+        if (K == 1) {
+          // lane t = t-th 64-row segment from the top (k descending, then wave descending)
+          constexpr int S = NPT * (NW - 1);
+          uint64_t m = 0;
+          if (lane < S) {
+            const int k = NPT - 1 - lane / (NW - 1), w = NW - 1 - lane % (NW - 1);
+            m = (mode == 1) ? s_fm[pb][k][w] : (s_mx[pb][w][0] == M0 ? s_bm[pb][k][w] : 0ull);
           }
+          const int32_t cnt = __popcll(m);
+          const int32_t pre = ksimw::prefix_incl_i32(cnt);
+          const uint64_t hm = __ballot(pre > rank);
+          if (hm) {
+            const int ts = __builtin_ffsll((long long)hm) - 1;
+            const int32_t r2 = rank - (__builtin_amdgcn_readlane(pre, ts) - __builtin_amdgcn_readlane(cnt, ts));
+            const uint64_t ms = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(m >> 32), ts) << 32) |
+                                (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)m, ts);
+            // the r2-th set bit counted from the top: set, with exactly r2 set bits above it
+            const bool is = ((ms >> lane) & 1ull) && __popcll((ms >> lane) >> 1) == r2;
+            const uint64_t bb = __ballot(is);
+            if (bb) {
+              const int ks = NPT - 1 - ts / (NW - 1), ws = NW - 1 - ts % (NW - 1);
+              jsel = ks * RT + (ws - 1) * 64 + (__builtin_ffsll((long long)bb) - 1);
+            }
+          }
+        } else {  // several reduce classes: scan the packed entries from the top
+          const int32_t* ev = R.ev + pb * chunk;
+          int32_t rr = rank;
+          const int nseg = (nrows + 63) / 64;
+          for (int s0 = nseg - 1; s0 >= 0 && jsel < 0; s0 -= 4) {
+            uint64_t bl[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            if (jsel >= 0) break;
-            uint64_t m = bl[u];
-            const int nbits = __popcll(m);
-            if (rr >= nbits) { rr -= nbits; continue; }
-            for (int t = 0; t < rr; ++t) m &= ~(1ull << (63 - __clzll(m)));
-            jsel = (s0 - u) * 64 + (63 - __clzll(m));
+            for (int u = 0; u < 4; ++u) {
+              const int32_t j = (s0 - u) * 64 + lane;
+              const int32_t e = (s0 - u >= 0 && j < nrows) ? ev[j] : -1;
+              bool mt = e >= 0;
+              if (mode == 2 && mt) {
+                const int q = ev_cls(e);
+                mt = ((win >> q) & 1u) && ev_score(e) == (q == 0 ? M0 : s_M[q]);
+              }
+              bl[u] = __ballot(mt);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+              if (jsel >= 0) break;
+              uint64_t m = bl[u];
+              const int nbits = __popcll(m);
+              if (rr >= nbits) { rr -= nbits; continue; }
+              for (int t = 0; t < rr; ++t) m &= ~(1ull << (63 - __clzll(m)));
+              jsel = (s0 - u) * 64 + (63 - __clzll(m));
+            }
           }
         }
         if (jsel < 0) {
           mode = -1;
           if (lane == 0) atomicOr(c.err, 2);
-        } else if (lane == 0) {
-          R.rc[jsel] += P.add_cpu;
-          R.rm[jsel] += P.add_mem;
-          R.zc[jsel] += P.nz_cpu;
-          R.zm[jsel] += P.nz_mem;
-          R.count[jsel] += 1;
-          if (P.add_gpu | P.add_eph | P.scalar_cnt | P.port_cnt) R.fl[jsel] = commit_side(cg, &P, lo + jsel, R.fl[jsel]);
-          c.out_node[pod] = (int32_t)(lo + jsel);
+        } else {
+          // commit (NodeInfo.AddPod); the committed row stays in registers for the fix-up
+          KsimFastRow r = load_row(jsel);
+          r.rc += P.add_cpu; r.rm += P.add_mem; r.zc += P.nz_cpu; r.zm += P.nz_mem; r.count += 1;
+          const bool side = (P.add_gpu | P.add_eph | P.scalar_cnt | P.port_cnt) != 0;
+          if (lane == 0) {
+            R.rc[jsel] = r.rc; R.rm[jsel] = r.rm; R.zc[jsel] = r.zc; R.zm[jsel] = r.zm; R.count[jsel] = r.count;
+            if (side) R.fl[jsel] = commit_side(cg, &P, lo + jsel, r.fl);
+            c.out_node[pod] = (int32_t)(lo + jsel);
+          }
+          if (has_next && !side) {  // pod + 1 against the committed row, before the barrier
+            const ksim_pod& Q = s_pod[(pod + 1) % RING];
+            if (ksim_is_fast_pod(Q, pod_K(Q))) {
+              const KsimFastPod F{Q.req_cpu, Q.req_mem, Q.nz_cpu, Q.nz_mem, Q.flags};
+              ej_pre = ksim_fast_eval(preds, F, r, no_prio, wl, wmr, wb, rm_pre);
+              have_pre = true;
+            }
+          }
         }
+        OSTAMP(16);
       }
       if (mode == 0 && blockIdx.x == 0 && lane == 0) c.out_node[pod] = -1;
       if (lane == 0) s_mode = mode;
+      X = mode > 0 ? blk : -1;
       STAMP(6);
     } else {
       // ---------------- b. speculative evaluation of pod + 1 (row waves) ----------------
@@ -549,8 +663,10 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
 #endif
       if (has_next) {
         int32_t e[NPT];
-        eval_rows(pod + 1, e, B_rm, R.ev[nb]);
-        partial(e, pod_K(s_pod[(pod + 1) % RING]), nb, wv);
+        const int Kn = pod_K(s_pod[(pod + 1) % RING]);
+        eval_rows(pod + 1, e, B_rm, R.ev + nb * chunk);
+        partial(e, Kn, nb, wv);
+        arrive_publish(pod + 1, Kn, nb);
       }
 #ifdef KSIM_STAMPS
       if (tid == 64) st_acc[5] += __builtin_amdgcn_s_memtime() - te0;
@@ -581,26 +697,33 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       if (tid < KSIM_NREASONS && s_hist[tid]) atomicAdd(&c.out_reasons[pod * KSIM_NREASONS + tid], s_hist[tid]);
     }
     if (wv == 0 && has_next) {
-      // ---------------- e. owner fix-up of pod + 1, then pod + 1 becomes current ----------------
-      const ksim_pod& Q = s_pod[(pod + 1) % RING];
-      const int Kn = pod_K(Q);
+      // ---------------- e. owner: fix-up of pod + 1, publish the correction ----------------
       if (jsel >= 0) {  // only row jsel changed: re-evaluate it and redo its row wave's partial
-        uint32_t rmj = 0;
-        const int32_t ej = eval_one(Q, ksim_is_fast_pod(Q, Kn), jsel, rmj);
+        OSTAMP(17);
+        const ksim_pod& Q = s_pod[(pod + 1) % RING];
+        const int Kn = pod_K(Q);
+        uint32_t rmj = rm_pre;
+        const int32_t ej = have_pre ? ej_pre : eval_one(Q, ksim_is_fast_pod(Q, Kn), jsel, rmj);
+        OSTAMP(18);
         const int w = 1 + (jsel % RT) / 64;
         int32_t e[NPT];
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
           const int32_t j = k * RT + (w - 1) * 64 + lane;
-          e[k] = (j == jsel) ? ej : (j < nrows ? R.ev[nb][j] : -1);
+          e[k] = (j == jsel) ? ej : (j < nrows ? R.ev[nb * chunk + j] : -1);
         }
         partial(e, Kn, nb, w);
-        if (lane == 0) { R.ev[nb][jsel] = ej; s_fix[nb][0] = jsel; s_fix[nb][1] = (int32_t)rmj; }
+        if (lane == 0) { R.ev[nb * chunk + jsel] = ej; s_fix[nb][0] = jsel; s_fix[nb][1] = (int32_t)rmj; }
+        OSTAMP(19);
+        const uint64_t v = combine(Kn, nb);
+        if (lane < Kn) store_granule(fix_at(granules, (int)((pod + 1) % NSLOT), lane), (ptag(pod + 1) << 56) | v);
+        OSTAMP(20);
+#ifdef KSIM_STAMPS
+        if (lane == 0) atomicAdd((unsigned long long*)&c.dbg[21], 1ull);
+#endif
       } else if (lane == 0) {
         s_fix[nb][0] = -1;
       }
-      STAMP(11);
-      my_gran = combine(Kn, nb);
     }
     STAMP(4);
     if (wv > 0) {
@@ -662,7 +785,9 @@ extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows) {
   return 1;
 }
 
-extern "C" size_t ksim_persistent_granule_bytes(int grid) { return (size_t)2 * grid * GR * sizeof(uint64_t); }
+extern "C" size_t ksim_persistent_granule_bytes(int) {
+  return (size_t)(NSLOT * MAXG * GR + NSLOT * GR) * sizeof(uint64_t);
+}
 
 extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
                                              int lds_rows, hipStream_t s) {

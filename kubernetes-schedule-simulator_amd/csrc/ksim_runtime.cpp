@@ -133,13 +133,13 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
   for (int k = 0; k < KSIM_NW; ++k) c.w[k] = cfg->weights[k];
   int rc;
   if ((rc = dev_alloc(h, &c.cursor, 1)) || (rc = dev_alloc(h, &c.counter, 1)) || (rc = dev_alloc(h, &c.ticket, 4)) ||
-      (rc = dev_alloc(h, &c.err, 4)) || (rc = dev_alloc(h, &c.dbg, 16))) {
+      (rc = dev_alloc(h, &c.err, 4)) || (rc = dev_alloc(h, &c.dbg, 32))) {
     ksim_destroy(h);
     return rc;
   }
   (void)hipMemsetAsync(c.ticket, 0, 16, h->stream);
   (void)hipMemsetAsync(c.err, 0, 16, h->stream);
-  (void)hipMemsetAsync(c.dbg, 0, 128, h->stream);
+  (void)hipMemsetAsync(c.dbg, 0, 32 * sizeof(uint64_t), h->stream);
   (void)hipMemcpyAsync(c.counter, &cfg->last_node_index, 8, hipMemcpyHostToDevice, h->stream);
   if (hipStreamSynchronize(h->stream) != hipSuccess) {
     ksim_destroy(h);
@@ -395,16 +395,18 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
 #ifdef KSIM_STAMPS
   {
-    uint64_t d[16];
+    uint64_t d[32];
     HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
     HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
     // slots: 1 publish, 2 sweep, 9 reduce, 10 selectHost index, 3 locate, 6 select+commit,
     // 7 barrier, 11 fix-up, 4 combine, 5 row-wave evaluation (concurrent), 8 polls
     static const char* names[16] = {"", "publish", "sweep", "locate", "combine", "row-eval", "select+commit", "barrier",
-                                    "polls", "reduce", "ix", "fixup", "", "", "", ""};
+                                    "polls", "reduce", "ix", "fixup", "spec-seen", "fix-seen", "", ""};
     fprintf(stderr, "[ksim stamps] pods=%lld (%.3f ms) cycles/pod:", (long long)count, ms);
-    for (int k : {1, 2, 9, 10, 3, 6, 7, 11, 4, 5, 8}) fprintf(stderr, " %s %.0f", names[k], d[k] / (double)count);
-    fprintf(stderr, "\n");
+    for (int k : {1, 2, 12, 13, 9, 10, 3, 6, 7, 11, 4, 5, 8}) fprintf(stderr, " %s %.0f", names[k], d[k] / (double)count);
+    fprintf(stderr, "\n[ksim stamps] owner (%llu fix-ups) cycles/fix-up: select+commit %.0f barrier %.0f eval-row %.0f partial %.0f combine+publish %.0f\n",
+            (unsigned long long)d[21], d[16] / (double)(d[21] ? d[21] : 1), d[17] / (double)(d[21] ? d[21] : 1),
+            d[18] / (double)(d[21] ? d[21] : 1), d[19] / (double)(d[21] ? d[21] : 1), d[20] / (double)(d[21] ? d[21] : 1));
   }
 #endif
   if (st) {

@@ -205,3 +205,39 @@ def test_c3_prefix_matches_c_oracle(mode):
 def test_wave_dpp_selftest():
     """DPP wave reductions / prefix scan used by the persistent kernel vs plain lane loops."""
     assert abi.lib().ksim_selftest() == 0
+
+
+BOUNDARY_ALLOC = [0, 1, 3, 7, 10, 999, 1000, 1001, 2 ** 20 + 1, 3 * 2 ** 30, 2 ** 48 - 1, 2 ** 48 + 12345,
+                  2 ** 49 - 1, 2 ** 49, 2 ** 50 + 7, 10 ** 15 + 3]
+BOUNDARY_REQ = [0, 1, 2, 3, 7, 100, 333, 1000, 2 ** 20, 2 ** 30 + 1, 2 ** 40, 2 ** 47, 2 ** 48 + 1]
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("prios", [[("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)],
+                                   [("MostRequestedPriority", 2), ("LeastRequestedPriority", 1),
+                                    ("BalancedResourceAllocation", 3)]], ids=["lr_bra", "mr_lr_bra"])
+def test_score_boundaries_match_c_oracle(prios, mode):
+    """Resource-only pods on capacities around the fast path's exactness bounds (2^49, exact
+    multiples, request == capacity, zero capacity): every placement, reason histogram and the
+    final node state equal the C oracle's."""
+    import cpu_ref
+    from ksim import synth
+    n, m = 700, 2500
+    r = synth.splitmix64(77, 2 * n + 2 * m)
+    cpu = synth._pick(r[0:n], BOUNDARY_ALLOC)
+    mem = synth._pick(r[n:2 * n], BOUNDARY_ALLOC)
+    pcpu = synth._pick(r[2 * n:2 * n + m], BOUNDARY_REQ)
+    pmem = synth._pick(r[2 * n + m:], BOUNDARY_REQ)
+    names = ["b-%05d" % i for i in range(n)]
+    cl = synth.resource_cluster(names, cpu, mem, np.full(n, 40, np.int32), pcpu, pmem)
+    preds = list(scheduler.DEFAULT_PREDICATES)
+    g = scheduler.GenericScheduler(cl, preds, prios, mode=mode)
+    out, reasons, _ = g.schedule()
+    ref, ref_reasons, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, prios), threads=8)
+    assert np.array_equal(out, ref)
+    assert np.array_equal(reasons, ref_reasons)
+    assert g.last_node_index == ref_ctr
+    s = g.node_state()
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+        assert np.array_equal(s[k], ref_state[k]), k
+    assert (out >= 0).sum() > m // 4  # the queue is not all FitErrors
