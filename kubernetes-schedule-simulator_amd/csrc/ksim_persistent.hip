@@ -51,8 +51,11 @@ __device__ __forceinline__ uint64_t load_granule(const uint64_t* g) {
   return __hip_atomic_load((gu64*)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // speculative partial of workgroup b for the pod in `slot`, and the previous owner's correction
+// Dense layout [slot][q][pos(b)]: one poll of class 0 touches 2 KiB (16 lines) instead of a
+// line per workgroup.  pos(b) = (b % MAXB) * 64 + b / MAXB, so the sweep's j-th load of lane l
+// (position j * 64 + l, coalesced across the wave) is workgroup l * MAXB + j.
 __device__ __forceinline__ uint64_t* spec_at(uint64_t* gr, int slot, int b, int q) {
-  return gr + ((int64_t)slot * MAXG + b) * GR + q;
+  return gr + ((int64_t)slot * GR + q) * MAXG + (b % MAXB) * 64 + b / MAXB;
 }
 __device__ __forceinline__ uint64_t* fix_at(uint64_t* gr, int slot, int q) {
   return gr + (int64_t)NSLOT * MAXG * GR + (int64_t)slot * GR + q;
@@ -623,6 +626,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
             }
           }
         }
+        OSTAMP(22);
         if (jsel < 0) {
           mode = -1;
           if (lane == 0) atomicOr(c.err, 2);
@@ -636,6 +640,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
             if (side) R.fl[jsel] = commit_side(cg, &P, lo + jsel, r.fl);
             c.out_node[pod] = (int32_t)(lo + jsel);
           }
+          OSTAMP(23);
           if (has_next && !side) {  // pod + 1 against the committed row, before the barrier
             const ksim_pod& Q = s_pod[(pod + 1) % RING];
             if (ksim_is_fast_pod(Q, pod_K(Q))) {

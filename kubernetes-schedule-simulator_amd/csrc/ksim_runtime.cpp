@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -23,6 +24,9 @@ extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cd
                                              int lds_rows, hipStream_t s);
 extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows);
 extern "C" size_t ksim_persistent_granule_bytes(int grid);
+extern "C" int ksim_pfast_config(int64_t n, int* grid, int* lds_rows);
+extern "C" size_t ksim_pfast_granule_bytes(void);
+extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, hipStream_t s);
 
 namespace {
 
@@ -57,6 +61,8 @@ struct ksim_handle {
   int64_t g_first = -1, g_end = -1;
   // host-side copies needed for validation
   std::vector<int32_t> h_n_tt, h_n_na;
+  // fast_pre[i] = resource-only pods among the first i of the queue (ksim_is_fast_pod)
+  std::vector<int64_t> fast_pre;
 };
 
 static int fail(ksim_handle* h, int code, const char* fmt, ...) {
@@ -245,6 +251,8 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
   c.lwords = (int32_t)lw; c.twords = (int32_t)tw;
   c.n_label_sets = (int32_t)L; c.n_taint_sets = (int32_t)T;
   h->n_classes = t->n_classes;
+  h->h_n_tt.assign(t->n_tt ? t->n_tt : ones.data(), (t->n_tt ? t->n_tt : ones.data()) + C);
+  h->h_n_na.assign(t->n_na ? t->n_na : ones.data(), (t->n_na ? t->n_na : ones.data()) + C);
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->have_classes = true;
   return KSIM_OK;
@@ -281,6 +289,17 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
       (rc = dev_alloc(h, &c.out_reasons, c.collect ? n_pods * KSIM_NREASONS : 1)))
     return rc;
   c.pods = dp; c.pod_ports = pp; c.pod_scalars = sp;
+  // host mirror of ksim_is_fast_pod (ksim_fast.h): decides per call whether the specialised
+  // persistent kernel (ksim_pfast.hip) may run
+  h->fast_pre.assign((size_t)n_pods + 1, 0);
+  for (int64_t i = 0; i < n_pods; ++i) {
+    const ksim_pod& p = pods[i];
+    const int k1 = c.w[KSIM_W_TAINT_TOLERATION] ? h->h_n_tt[p.cls] : 1;
+    const int k2 = c.w[KSIM_W_NODE_AFFINITY] ? h->h_n_na[p.cls] : 1;
+    const bool fast = k1 * k2 == 1 && p.host == -1 && p.port_cnt == 0 && p.scalar_cnt == 0 && p.req_gpu == 0 &&
+                      p.req_eph == 0 && !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS));
+    h->fast_pre[i + 1] = h->fast_pre[i] + (fast ? 1 : 0);
+  }
   if (c.collect) HIPCHK(h, hipMemsetAsync(c.out_reasons, 0, n_pods * KSIM_NREASONS * sizeof(int32_t), h->stream));
   h->n_pods = n_pods;
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -365,9 +384,55 @@ static bool persistent_weights_ok(const KsimCtx& c) {
   return s < ((int64_t)1 << 27);
 }
 
+// All pods of [first, first+count) resource-only: the specialised kernel (ksim_pfast.hip).
+static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid, int lds_rows, ksim_stats* st) {
+  KsimCtx& c = h->ctx;
+  const size_t gb = ksim_pfast_granule_bytes();
+  if (h->gran_bytes < gb) {
+    int rc = dev_alloc(h, &h->granules, gb / sizeof(uint64_t));
+    if (rc) return rc;
+    h->gran_bytes = gb;
+  }
+  c.first = first;
+  c.end = first + count;
+  c.chunk = (c.n + grid - 1) / grid;
+  HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
+  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+  hipError_t e = ksim_launch_pfast(&c, h->granules, grid, lds_rows, h->stream);
+  if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+  HIPCHK(h, hipEventSynchronize(h->ev1));
+  float ms = 0.f;
+  HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+#ifdef KSIM_STAMPS
+  {
+    uint64_t d[32];
+    HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
+    const double nf = (double)(d[21] ? d[21] : 1);
+    fprintf(stderr, "[ksim stamps] pfast pods=%lld (%.3f ms) cycles/pod: sweep %.0f decide %.0f owner %.0f barrier %.0f tail %.0f row-eval %.0f\n",
+            (long long)count, ms, d[2] / (double)count, d[3] / (double)count, d[6] / (double)count, d[7] / (double)count,
+            (d[4] + d[1]) / (double)count, d[5] / (double)count);
+    fprintf(stderr, "[ksim stamps] pfast owner (%llu fixes) cycles: select %.0f commit %.0f e_new %.0f barrier %.0f fix-publish %.0f restat %.0f\n",
+            (unsigned long long)d[21], d[22] / nf, d[23] / nf, d[16] / nf, d[17] / nf, d[18] / nf, d[19] / nf);
+  }
+#endif
+  if (st) {
+    st->device_ms = ms;
+    st->kernel_ms = ms;
+    st->kernel_launches = 1;
+    st->mode = KSIM_MODE_PERSISTENT;
+    st->blocks = grid;
+  }
+  return KSIM_OK;
+}
+
 static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   KsimCtx& c = h->ctx;
   int grid = 0, lds_rows = 0;
+  if (!getenv("KSIM_NO_PFAST") && count > 0 && h->fast_pre[first + count] - h->fast_pre[first] == count &&
+      persistent_weights_ok(c) && ksim_pfast_config(c.n, &grid, &lds_rows))
+    return run_pfast_mode(h, first, count, grid, lds_rows, st);
   if (!ksim_persistent_config(c.n, &grid, &lds_rows))
     return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: node table does not fit the on-chip layout");
   if (!persistent_weights_ok(c)) return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: map-priority weights exceed the 27-bit score range");
@@ -404,7 +469,9 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
                                     "polls", "reduce", "ix", "fixup", "spec-seen", "fix-seen", "", ""};
     fprintf(stderr, "[ksim stamps] pods=%lld (%.3f ms) cycles/pod:", (long long)count, ms);
     for (int k : {1, 2, 12, 13, 9, 10, 3, 6, 7, 11, 4, 5, 8}) fprintf(stderr, " %s %.0f", names[k], d[k] / (double)count);
-    fprintf(stderr, "\n[ksim stamps] owner (%llu fix-ups) cycles/fix-up: select+commit %.0f barrier %.0f eval-row %.0f partial %.0f combine+publish %.0f\n",
+    fprintf(stderr, "\n[ksim stamps] owner select %.0f commit %.0f", d[22] / (double)(d[21] ? d[21] : 1),
+            d[23] / (double)(d[21] ? d[21] : 1));
+    fprintf(stderr, "\n[ksim stamps] owner (%llu fix-ups) cycles/fix-up: pre-eval %.0f barrier %.0f eval-row %.0f partial %.0f combine+publish %.0f\n",
             (unsigned long long)d[21], d[16] / (double)(d[21] ? d[21] : 1), d[17] / (double)(d[21] ? d[21] : 1),
             d[18] / (double)(d[21] ? d[21] : 1), d[19] / (double)(d[21] ? d[21] : 1), d[20] / (double)(d[21] ? d[21] : 1));
   }
