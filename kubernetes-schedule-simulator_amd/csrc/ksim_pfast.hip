@@ -1,23 +1,30 @@
 // ksim_pfast.hip — persistent-kernel mode specialised for resource-only pods (the C1/C3/C4/C5
 // pod shape, ksim_is_fast_pod): used for a ksim_schedule() call whenever every pod of the call
-// qualifies; ksim_persistent.hip handles everything else.
+// qualifies and every cpu / memory quantity of the nodes and pods is below 2^48 (host check);
+// ksim_persistent.hip handles everything else.  A commit that takes a node's quantity to 2^48
+// or beyond stops the kernel before the next pod (uniformly, through the correction granule)
+// and the host finishes the call with the general kernel.
 //
 // Same protocol as ksim_persistent.hip — workgroup b keeps the name-rank range
 // [b*chunk, (b+1)*chunk) in LDS, one control wave (wave 0) decides every pod redundantly from
 // the tagged 8-byte granules all workgroups publish, seven row waves evaluate pod p+1 while
 // the control wave decides pod p — with a shorter critical path:
 //
-//  * scores without a divide: each row keeps y = RN(1/alloc) (alloc is static).
+//  * float64 rows.  Every quantity is an integer below 2^48 and every sum below 2^49, so sums, compares
+//    and the products below are exact in float64 and the Go int64 arithmetic is reproduced
+//    without 64-bit integer emulation.  Each row keeps y = RN(1/alloc) (alloc is static):
 //    LeastRequested / MostRequested floor(10x / cap) = trunc(x*y) corrected by the exact
 //    remainder fma(-q, cap, x) (least_requested.go:44-53, most_requested.go:45-55);
 //    BalancedResourceAllocation's float64(req)/float64(cap) (balanced_resource_allocation.go:
 //    39-61) = Markstein's RN(a/b): q = a*y, r = fma(-q, b, a) (exact), RN(q + r*y) — the
 //    correctly rounded quotient, bit-identical to the IEEE divide Go performs (y within half an
-//    ulp of 1/b, q within one ulp of a/b, no over/underflow: operands are integers < 2^49).
+//    ulp of 1/b, q within one ulp of a/b, no over/underflow).
+//  * the row waves also evaluate pod p+1 against "row + pod p" for every row (two independent
+//    evaluations per lane, overlapped), so the owner of pod p's node finds the post-commit
+//    evaluation in LDS;
 //  * O(1) owner fix-up: the row waves keep the workgroup's top two (score, count) pairs of
-//    pod p+1, so the owner of pod p's node removes that row's speculative evaluation and adds
-//    its post-commit one with scalar arithmetic; the wave-level bitmasks it needs only if it
-//    owns pod p+1 too are rebuilt after the correction is published.
+//    pod p+1, so the owner removes the committed row's pre-commit evaluation and adds its
+//    post-commit one with scalar arithmetic, publishes, and only then commits the row;
 //  * one prefix scan per decision: counts at the maximum give C (= its total) and the
 //    workgroup holding the ix-th match from the top (core/generic_scheduler.go:183-198).
 #include "ksim_fast.h"
@@ -52,13 +59,25 @@ __device__ __forceinline__ uint64_t* spec_at(uint64_t* gr, int slot, int b) {
 }
 __device__ __forceinline__ uint64_t* fix_at(uint64_t* gr, int slot) { return gr + NSLOT * MAXG + slot * FIXSTRIDE; }
 
-// granule: tag:8 | fit:12 | count:12 | score:32 (-1 = no fit node)
+// granule: tag:8 | stop:1 | fit:11 | count:12 | score:32 (-1 = no fit node); stop (correction
+// granules only): the committed node left the exact float64 range, end the call before this pod
+constexpr double EXACT_LIM = 281474976710656.0;  // 2^48
 __device__ __forceinline__ uint32_t gtag(uint64_t v) { return (uint32_t)(v >> 56); }
-__device__ __forceinline__ int32_t gfit(uint64_t v) { return (int32_t)((v >> 44) & 0xFFF); }
+__device__ __forceinline__ bool gstop(uint64_t v) { return (v >> 55) & 1; }
+__device__ __forceinline__ int32_t gfit(uint64_t v) { return (int32_t)((v >> 44) & 0x7FF); }
 __device__ __forceinline__ int32_t gcnt(uint64_t v) { return (int32_t)((v >> 32) & 0xFFF); }
 __device__ __forceinline__ int32_t gscore(uint64_t v) { return (int32_t)(uint32_t)v; }
 __device__ __forceinline__ uint64_t gpack(uint64_t tag, int32_t f, int32_t n, int32_t m) {
   return (tag << 56) | ((uint64_t)(uint32_t)f << 44) | ((uint64_t)(uint32_t)n << 32) | (uint64_t)(uint32_t)m;
+}
+
+// Workgroup barrier ordering LDS only: __syncthreads' fence would also drain this wave's
+// outstanding global operations (the granule store just published, a descriptor prefetch),
+// which other waves of the workgroup never read.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
 #ifdef KSIM_STAMPS
@@ -71,7 +90,7 @@ __device__ __forceinline__ uint64_t gpack(uint64_t tag, int32_t f, int32_t n, in
 #define OSTAMP(k)                                                          \
   do {                                                                     \
     const uint64_t t_ = __builtin_amdgcn_s_memtime();                     \
-    if (lane == 0) atomicAdd((unsigned long long*)&c.dbg[k], t_ - o_prev); \
+    if (lane == 0) atomicAdd((unsigned long long*)&a.dbg[k], t_ - o_prev); \
     o_prev = t_;                                                           \
   } while (0)
 #else
@@ -83,43 +102,102 @@ __device__ __forceinline__ uint64_t gpack(uint64_t tag, int32_t f, int32_t n, in
   } while (0)
 #endif
 
+}  // namespace
+
+// Kernel arguments: only what the fast path touches.
+struct PfArgs {
+  int64_t n, chunk, first, end;
+  const int64_t* alloc_cpu;
+  const int64_t* alloc_mem;
+  const int32_t* allowed_pods;
+  const uint32_t* flags;
+  int64_t* req_cpu;
+  int64_t* req_mem;
+  int64_t* nz_cpu;
+  int64_t* nz_mem;
+  int32_t* pod_count;
+  const ksim_pod* pods;
+  uint64_t* counter;
+  int64_t* cursor;
+  int32_t* out_node;
+  int32_t* out_reasons;
+  int32_t* err;
+  uint64_t* dbg;
+  uint64_t* granules;
+  uint32_t preds;
+  int32_t no_prio, collect;
+  int32_t wl, wm, wb;  // map weights (host-checked: sum x 10 < 2^27)
+};
+
+namespace {
+
 struct FRow {
-  int64_t ac, am, rc, rm, zc, zm;
-  double dac, dam, yc, ym;  // alloc as float64 and RN(1/alloc) (0 when alloc == 0)
+  double ac, am, rc, rm, zc, zm, yc, ym;  // y = RN(1/alloc) (0 when alloc == 0)
   int32_t allowed, count;
   uint32_t fl;
 };
 
-struct FRows {  // LDS image of the owned rows (SoA)
-  int64_t *ac, *am, *rc, *rm, *zc, *zm;
-  double *dac, *dam, *yc, *ym;
-  int32_t *allowed, *count;
-  uint32_t* fl;
-  int32_t* ev;  // [2][chunk]: packed evaluation of pod p (parity p & 1), -1 = does not fit
+// the pod fields the fast path reads, as float64 (wave-uniform)
+struct FPod {
+  double rq_c, rq_m, nz_c, nz_m, ad_c, ad_m;
+  uint32_t anyreq;  // ~0u when PodFitsResources does the resource checks (predicates.go:731-736)
+  uint32_t be;      // ~0u for a BestEffort pod (CheckNodeMemoryPressure, predicates.go:1502)
 };
 
-constexpr int LDS_ROW_BYTES = 10 * 8 + 3 * 4 + 2 * 4;  // 100
+// the configured predicate set and weights as masks / multipliers (no branches per row)
+struct EvCfg {
+  uint32_t condm;   // node-condition bits checked (CheckNodeCondition)
+  uint32_t unschm;  // KSIM_N_UNSCHEDULABLE if CheckNodeUnschedulable is configured
+  uint32_t resm;    // ~0u if PodFitsResources runs (GeneralPredicates / PodFitsResources)
+  uint32_t mempm;   // KSIM_N_MEM_PRESSURE if CheckNodeMemoryPressure is configured
+  uint32_t diskm;   // KSIM_N_DISK_PRESSURE if CheckNodeDiskPressure is configured
+  int32_t wl, wm, wb;  // 0 for every weight under an empty prioritizer list (EqualPriorityMap)
+};
+
+struct FRows {  // LDS image of the owned rows (SoA)
+  double *ac, *am, *rc, *rm, *zc, *zm, *yc, *ym;
+  int32_t *allowed, *count;
+  uint32_t* fl;
+  int32_t* ev;    // [2][chunk]: evaluation of pod p (parity p & 1), -1 = does not fit
+  int32_t* ev2;   // [chunk]: evaluation of pod p+1 against row + pod p
+  uint32_t* rm2;  // [chunk]: ... its reason mask
+};
+
+constexpr int LDS_ROW_BYTES = 8 * 8 + 7 * 4;  // 92
 
 extern __shared__ __attribute__((aligned(16))) char kf_smem[];
 
 __device__ __forceinline__ FRows carve(int rows) {
   FRows r;
-  int64_t* p = reinterpret_cast<int64_t*>(kf_smem);
-  r.ac = p; r.am = p + rows; r.rc = p + 2 * rows; r.rm = p + 3 * rows; r.zc = p + 4 * rows; r.zm = p + 5 * rows;
-  double* d = reinterpret_cast<double*>(p + 6 * rows);
-  r.dac = d; r.dam = d + rows; r.yc = d + 2 * rows; r.ym = d + 3 * rows;
-  int32_t* q = reinterpret_cast<int32_t*>(d + 4 * rows);
+  double* d = reinterpret_cast<double*>(kf_smem);
+  r.ac = d; r.am = d + rows; r.rc = d + 2 * rows; r.rm = d + 3 * rows;
+  r.zc = d + 4 * rows; r.zm = d + 5 * rows; r.yc = d + 6 * rows; r.ym = d + 7 * rows;
+  int32_t* q = reinterpret_cast<int32_t*>(d + 8 * rows);
   r.allowed = q; r.count = q + rows;
   r.fl = reinterpret_cast<uint32_t*>(q + 2 * rows);
   r.ev = q + 3 * rows;
+  r.ev2 = q + 5 * rows;
+  r.rm2 = reinterpret_cast<uint32_t*>(q + 6 * rows);
   return r;
 }
 
 __device__ __forceinline__ FRow load_frow(const FRows& R, int32_t j) {
   FRow r;
   r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j]; r.rm = R.rm[j]; r.zc = R.zc[j]; r.zm = R.zm[j];
-  r.dac = R.dac[j]; r.dam = R.dam[j]; r.yc = R.yc[j]; r.ym = R.ym[j];
+  r.yc = R.yc[j]; r.ym = R.ym[j];
   r.allowed = R.allowed[j]; r.count = R.count[j]; r.fl = R.fl[j];
+  return r;
+}
+
+__device__ __forceinline__ FPod load_fpod(const ksim_pod& P) {
+  return FPod{(double)P.req_cpu, (double)P.req_mem, (double)P.nz_cpu, (double)P.nz_mem,
+              (double)P.add_cpu, (double)P.add_mem, (P.flags & KSIM_POD_ANY_REQUEST) ? ~0u : 0u,
+              (P.flags & KSIM_POD_BEST_EFFORT) ? ~0u : 0u};
+}
+
+// row + pod (NodeInfo.AddPod, node_info.go:318-341, the columns the fast path keeps)
+__device__ __forceinline__ FRow plus(FRow r, const FPod& P) {
+  r.rc += P.ad_c; r.rm += P.ad_m; r.zc += P.nz_c; r.zm += P.nz_m; r.count += 1;
   return r;
 }
 
@@ -138,60 +216,55 @@ __device__ __forceinline__ double quot(double a, double b, double y) {
   return fma(r, y, q);
 }
 
-// Weighted LeastRequested / MostRequested / BalancedResourceAllocation score of one node,
-// tc/tm = pod non-zero request + node non-zero requested (resource_allocation.go:58-59).
-__device__ __forceinline__ int64_t fscore(int64_t tc, int64_t tm, const FRow& r, int64_t wl, int64_t wm, int64_t wb) {
-  if (((uint64_t)(tc | r.ac | tm | r.am)) >> 49) return ksim_slow_score(tc, r.ac, tm, r.am, wl, wm, wb);
-  const bool okc = r.ac != 0 && tc <= r.ac, okm = r.am != 0 && tm <= r.am;
-  int64_t s = 0;
-  if (wl) {
-    const int32_t lc = okc ? div_floor((double)(10 * (r.ac - tc)), r.dac, r.yc) : 0;
-    const int32_t lm = okm ? div_floor((double)(10 * (r.am - tm)), r.dam, r.ym) : 0;
-    s += wl * ((lc + lm) / 2);
-  }
-  if (wm) {
-    const int32_t mc = okc ? div_floor((double)(10 * tc), r.dac, r.yc) : 0;
-    const int32_t mm = okm ? div_floor((double)(10 * tm), r.dam, r.ym) : 0;
-    s += wm * ((mc + mm) / 2);
-  }
-  if (wb) {
-    const double fc = r.ac ? quot((double)tc, r.dac, r.yc) : 1.0;
-    const double fm = r.am ? quot((double)tm, r.dam, r.ym) : 1.0;
-    const int32_t b = (fc >= 1.0 || fm >= 1.0) ? 0 : (int32_t)((1.0 - fabs(fc - fm)) * 10.0);
-    s += wb * b;
-  }
-  return s;
+// Packed evaluation (-1 = does not fit, else the weighted map score) and reason mask of
+// one row, straight-line (a taken branch costs a single wave ~40 cycles): predicates in
+// predicatesOrdering order as ksim_fast_predicates — the first failing one's reason — then
+// LeastRequested / MostRequested / BalancedResourceAllocation on tc/tm = pod non-zero request
+// + node non-zero requested (resource_allocation.go:58-59), all three computed and weighted
+// (a weight of 0 drops a priority).
+__device__ __forceinline__ int32_t feval(const EvCfg& C, const FPod& P, const FRow& r, uint32_t& rmask) {
+  const uint32_t fl = r.fl;
+  const uint32_t cond = fl & C.condm;  // bit positions coincide with KSIM_R_*
+  const uint32_t unsch = (fl & C.unschm) ? (1u << KSIM_R_UNSCHEDULABLE) : 0u;
+  uint32_t rq = (r.ac < P.rq_c + r.rc) ? (1u << KSIM_R_INSUFFICIENT_CPU) : 0u;
+  rq |= (r.am < P.rq_m + r.rm) ? (1u << KSIM_R_INSUFFICIENT_MEMORY) : 0u;
+  rq |= (fl & KSIM_N_GPU_OVER) ? (1u << KSIM_R_INSUFFICIENT_GPU) : 0u;
+  rq |= (fl & KSIM_N_EPH_OVER) ? (1u << KSIM_R_INSUFFICIENT_EPHEMERAL) : 0u;
+  const uint32_t res = (((r.count + 1 > r.allowed) ? (1u << KSIM_R_INSUFFICIENT_PODS) : 0u) | (rq & P.anyreq)) & C.resm;
+  const uint32_t memp = (fl & C.mempm & P.be) ? (1u << KSIM_R_MEM_PRESSURE) : 0u;
+  const uint32_t diskp = (fl & C.diskm) ? (1u << KSIM_R_DISK_PRESSURE) : 0u;
+  const uint32_t m = cond ? cond : unsch ? unsch : res ? res : memp ? memp : diskp;
+  rmask = m;
+  const double tc = P.nz_c + r.zc, tm = P.nz_m + r.zm;
+  const bool okc = r.ac != 0.0 && tc <= r.ac, okm = r.am != 0.0 && tm <= r.am;
+  const int32_t lc = div_floor((r.ac - tc) * 10.0, r.ac, r.yc), lm = div_floor((r.am - tm) * 10.0, r.am, r.ym);
+  const int32_t mc = div_floor(tc * 10.0, r.ac, r.yc), mm = div_floor(tm * 10.0, r.am, r.ym);
+  const uint32_t lr = ((uint32_t)(okc ? lc : 0) + (uint32_t)(okm ? lm : 0)) >> 1;
+  const uint32_t mr = ((uint32_t)(okc ? mc : 0) + (uint32_t)(okm ? mm : 0)) >> 1;
+  const double qc = quot(tc, r.ac, r.yc), qm = quot(tm, r.am, r.ym);
+  const double fc = r.ac != 0.0 ? qc : 1.0, fm = r.am != 0.0 ? qm : 1.0;
+  const int32_t bt = (int32_t)((1.0 - fabs(fc - fm)) * 10.0);
+  const int32_t br = (fc >= 1.0 || fm >= 1.0) ? 0 : bt;
+  const int32_t sc = C.wl * (int32_t)lr + C.wm * (int32_t)mr + C.wb * br;
+  return m ? -1 : sc;
 }
 
-__device__ __forceinline__ int32_t feval(uint32_t preds, const KsimFastPod& P, const FRow& r, bool no_prio, int64_t wl,
-                                         int64_t wm, int64_t wb, uint32_t& rm) {
-  rm = ksim_fast_predicates(preds, P, r.ac, r.am, r.rc, r.rm, r.allowed, r.count, r.fl);
-  const int32_t sc = no_prio ? 0 : (int32_t)fscore(P.nz_c + r.zc, P.nz_m + r.zm, r, wl, wm, wb);
-  return rm ? -1 : sc;
-}
-
-// top-two (score, count) statistics of a set of packed evaluations
+// top-two (score, count) statistics of a set of evaluations
 struct Top2 {
   int32_t f, m1, c1, m2, c2;
 };
-__device__ __forceinline__ void top2_add(Top2& t, int32_t m, int32_t n) {  // merge (m, n), n > 0, m >= 0
-  if (m > t.m1) { t.m2 = t.m1; t.c2 = t.c1; t.m1 = m; t.c1 = n; }
-  else if (m == t.m1) { t.c1 += n; }
-  else if (m > t.m2) { t.m2 = m; t.c2 = n; }
-  else if (m == t.m2) { t.c2 += n; }
-}
 
 }  // namespace
 
 template <int NPT>
-__global__ __launch_bounds__(BS) void ksim_pfast_kernel(KsimCtx c, uint64_t* granules) {
+__global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   __shared__ int32_t s_wst[2][RW][5];         // per row wave: fit, m1, c1, m2, c2 (by pod parity)
   __shared__ uint64_t s_fm[2][NPT][RW];       // per 64-row segment: fit rows
   __shared__ uint64_t s_bm[2][NPT][RW];       // ... rows at the wave maximum
   __shared__ int32_t s_wg[2][5];              // workgroup top-two of the pod
-  __shared__ int32_t s_fix[2][2];             // {row the owner re-evaluated (-1 none), its reason mask}
+  __shared__ int32_t s_fix[2][2];             // {row the owner corrected (-1 none), its reason mask}
   __shared__ int32_t s_hist[KSIM_NREASONS];
-  __shared__ int32_t s_mode;
+  __shared__ int32_t s_mode[2], s_own[2];  // by pod parity: read after the barrier, rewritten two pods later
   __shared__ int32_t s_arr;
   __shared__ __attribute__((aligned(16))) ksim_pod s_pod[RING];
 #ifdef KSIM_STAMPS
@@ -202,49 +275,53 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(KsimCtx c, uint64_t* gra
   const int rt = tid - 64;
   const int G = gridDim.x;
   const int me = blockIdx.x;
-  const int64_t chunk = c.chunk;
+  const int64_t chunk = a.chunk;
   const int64_t lo = (int64_t)me * chunk;
-  const int64_t hi = (lo + chunk < c.n) ? lo + chunk : c.n;
+  const int64_t hi = (lo + chunk < a.n) ? lo + chunk : a.n;
   const int32_t nrows = (int32_t)(hi - lo);
   const FRows R = carve((int)chunk);
-  const uint32_t preds = c.preds;
-  const int64_t wl = c.w[KSIM_W_LEAST_REQUESTED], wmr = c.w[KSIM_W_MOST_REQUESTED], wb = c.w[KSIM_W_BALANCED];
-  const bool no_prio = c.no_prio != 0;
+  const uint32_t preds = a.preds;
+  const bool no_prio = a.no_prio != 0;
+  EvCfg EC;
+  EC.condm = (preds & KSIM_P_CHECK_NODE_CONDITION) ? KSIM_COND_REASON_MASK : 0u;
+  EC.unschm = (preds & KSIM_P_CHECK_NODE_UNSCHEDULABLE) ? KSIM_N_UNSCHEDULABLE : 0u;
+  EC.resm = (preds & (KSIM_P_GENERAL | KSIM_P_RESOURCES)) ? ~0u : 0u;
+  EC.mempm = (preds & KSIM_P_MEM_PRESSURE) ? KSIM_N_MEM_PRESSURE : 0u;
+  EC.diskm = (preds & KSIM_P_DISK_PRESSURE) ? KSIM_N_DISK_PRESSURE : 0u;
+  EC.wl = no_prio ? 0 : a.wl;
+  EC.wm = no_prio ? 0 : a.wm;
+  EC.wb = no_prio ? 0 : a.wb;
+  uint64_t* const granules = a.granules;
 
   for (int32_t j = tid; j < nrows; j += BS) {  // stage the owned rows into LDS
     const int64_t i = lo + j;
-    const int64_t ac = c.alloc_cpu[i], am = c.alloc_mem[i];
+    const double ac = (double)a.alloc_cpu[i], am = (double)a.alloc_mem[i];
     R.ac[j] = ac; R.am[j] = am;
-    R.dac[j] = (double)ac; R.dam[j] = (double)am;
-    R.yc[j] = ac ? 1.0 / (double)ac : 0.0;
-    R.ym[j] = am ? 1.0 / (double)am : 0.0;
-    R.rc[j] = c.req_cpu[i]; R.rm[j] = c.req_mem[i];
-    R.zc[j] = c.nz_cpu[i]; R.zm[j] = c.nz_mem[i];
-    R.allowed[j] = c.allowed_pods[i]; R.count[j] = c.pod_count[i]; R.fl[j] = c.flags[i];
+    R.yc[j] = ac != 0.0 ? 1.0 / ac : 0.0;
+    R.ym[j] = am != 0.0 ? 1.0 / am : 0.0;
+    R.rc[j] = (double)a.req_cpu[i]; R.rm[j] = (double)a.req_mem[i];
+    R.zc[j] = (double)a.nz_cpu[i]; R.zm[j] = (double)a.nz_mem[i];
+    R.allowed[j] = a.allowed_pods[i]; R.count[j] = a.pod_count[i]; R.fl[j] = a.flags[i];
   }
   auto ring_load = [&](int64_t p0, uint4& v) {
     const int64_t p = p0 + lane / 8;
-    if (p < c.end) v = reinterpret_cast<const uint4*>(&c.pods[p])[lane % 8];
+    if (p < a.end) v = reinterpret_cast<const uint4*>(&a.pods[p])[lane % 8];
   };
   auto ring_store = [&](int64_t p0, const uint4& v) {
     const int64_t p = p0 + lane / 8;
-    if (p < c.end) reinterpret_cast<uint4*>(&s_pod[p % RING])[lane % 8] = v;
+    if (p < a.end) reinterpret_cast<uint4*>(&s_pod[p % RING])[lane % 8] = v;
   };
   if (wv == 1) {
     uint4 v;
-    ring_load(c.first, v);
-    ring_store(c.first, v);
+    ring_load(a.first, v);
+    ring_store(a.first, v);
   }
-  if (tid == 0) { s_fix[c.first & 1][0] = -1; s_arr = 0; }
-  uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex
+  if (tid == 0) { s_fix[a.first & 1][0] = -1; s_arr = 0; }
+  uint64_t counter = *a.counter;  // replicated genericScheduler.lastNodeIndex
   __syncthreads();
 
-  auto fpod = [&](int64_t p) -> KsimFastPod {
-    const ksim_pod& P = s_pod[p % RING];
-    return KsimFastPod{P.req_cpu, P.req_mem, P.nz_cpu, P.nz_mem, P.flags};
-  };
-  auto ptag = [&](int64_t p) -> uint64_t { return (uint64_t)((p - c.first + 1) & 0xFF); };
-  // wave-level statistics of NPT entries per lane → LDS slot (buf, w)
+  auto ptag = [&](int64_t p) -> uint64_t { return (uint64_t)((p - a.first + 1) & 0xFF); };
+  // wave-level statistics of NPT evaluations per lane → LDS slot (buf, w)
   auto wave_stats = [&](const int32_t (&e)[NPT], int buf, int w) {
     int32_t v = -1, nf = 0;
 #pragma unroll
@@ -272,72 +349,65 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(KsimCtx c, uint64_t* gra
       s_wst[buf][w - 1][3] = m2; s_wst[buf][w - 1][4] = c2;
     }
   };
-  auto wg_top2 = [&](int buf) -> Top2 {
-    Top2 t{0, -1, 0, -1, 0};
-    int32_t s[RW][5];
-#pragma unroll
-    for (int w = 0; w < RW; ++w)
-#pragma unroll
-      for (int q = 0; q < 5; ++q) s[w][q] = s_wst[buf][w][q];
-#pragma unroll
-    for (int w = 0; w < RW; ++w) {
-      t.f += s[w][0];
-      if (s[w][2]) top2_add(t, s[w][1], s[w][2]);
-      if (s[w][4]) top2_add(t, s[w][3], s[w][4]);
-    }
-    return t;
-  };
   // row waves: the last one to finish pod p's statistics merges and publishes them
   auto arrive_publish = [&](int64_t p, int buf) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
     int32_t old = 0;
     if (lane == 0) old = atomicAdd(&s_arr, 1);
     old = __builtin_amdgcn_readfirstlane(old);
     if ((old + 1) % RW == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-      const Top2 t = wg_top2(buf);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      // lane w < RW holds row wave w's statistics; merged with wave reductions, no branches
+      const bool in = lane < RW;
+      const int w = in ? lane : 0;
+      const int32_t f = in ? s_wst[buf][w][0] : 0;
+      const int32_t a1 = s_wst[buf][w][1], n1 = in ? s_wst[buf][w][2] : 0;
+      const int32_t a2 = s_wst[buf][w][3], n2 = in ? s_wst[buf][w][4] : 0;
+      Top2 t;
+      t.f = ksimw::sum_i32(f);
+      t.m1 = ksimw::max_i32(n1 ? a1 : -1);
+      t.c1 = ksimw::sum_i32((n1 && a1 == t.m1) ? n1 : 0);
+      t.m2 = ksimw::max_i32(n1 && a1 < t.m1 ? a1 : (n2 ? a2 : -1));
+      t.c2 = ksimw::sum_i32(((n1 && a1 == t.m2) ? n1 : 0) + ((n2 && a2 == t.m2) ? n2 : 0));
+      if (t.m2 < 0) t.c2 = 0;
       if (lane == 0) {
         s_wg[buf][0] = t.f; s_wg[buf][1] = t.m1; s_wg[buf][2] = t.c1; s_wg[buf][3] = t.m2; s_wg[buf][4] = t.c2;
         store_granule(spec_at(granules, (int)(p % NSLOT), me), gpack(ptag(p), t.f, t.c1, t.m1));
       }
     }
   };
-  // row waves: evaluate pod p on every owned row
-  auto eval_rows = [&](int64_t p, int32_t (&e)[NPT], uint32_t (&rm)[NPT], int32_t* ev) {
-    const KsimFastPod F = fpod(p);
+
+  // ---- prologue: evaluations and statistics of the first pod ----
+  uint32_t A_rm[NPT], B_rm[NPT];
+  if (wv > 0) {
+    const FPod P0 = load_fpod(s_pod[a.first % RING]);
+    int32_t e[NPT];
+    int32_t* ev = R.ev + (a.first & 1) * chunk;
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int32_t j = k * RT + rt;
       e[k] = -1;
-      rm[k] = 0;
+      A_rm[k] = 0;
       if (j < nrows) {
-        e[k] = feval(preds, F, load_frow(R, j), no_prio, wl, wmr, wb, rm[k]);
+        e[k] = feval(EC, P0, load_frow(R, j), A_rm[k]);
         ev[j] = e[k];
       }
     }
-  };
-
-  // ---- prologue: statistics of the first pod ----
-  uint32_t A_rm[NPT], B_rm[NPT];
-  if (wv > 0) {
-    int32_t e[NPT];
-    eval_rows(c.first, e, A_rm, R.ev + (c.first & 1) * chunk);
-    wave_stats(e, (int)(c.first & 1), wv);
-    arrive_publish(c.first, (int)(c.first & 1));
+    wave_stats(e, (int)(a.first & 1), wv);
+    arrive_publish(a.first, (int)(a.first & 1));
   }
   int X = -1;  // control wave: owner workgroup of the previous pod's node (-1: none)
-  __syncthreads();
+  int64_t stop_at = a.end;  // first pod not scheduled by this call
+  lds_barrier();
 #ifdef KSIM_STAMPS
   uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
 
-  for (int64_t pod = c.first; pod < c.end; ++pod) {
-    const bool has_next = pod + 1 < c.end;
+  for (int64_t pod = a.first; pod < a.end; ++pod) {
+    const bool has_next = pod + 1 < a.end;
     const int pb = (int)(pod & 1);
     const int nb = (int)((pod + 1) & 1);
-    int32_t jsel = -1;     // control wave: row committed by this workgroup
-    int32_t e_new = -1;    // ... its evaluation of pod + 1 after the commit
-    uint32_t rm_new = 0;
+    int32_t jsel = -1;  // control wave: row this workgroup commits pod to
 #ifdef KSIM_STAMPS
     uint64_t o_prev = 0;
 #endif
@@ -347,13 +417,13 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(KsimCtx c, uint64_t* gra
       const uint64_t tag = ptag(pod);
       const int slot = (int)(pod % NSLOT);
       STAMP(1);
-      uint64_t g[MAXB];
+      uint64_t g[MAXB], fx = 0;
       bool ok = false;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
 #pragma unroll
         for (int j = 0; j < MAXB; ++j) g[j] = load_granule(granules + slot * MAXG + j * 64 + lane);
-        const uint64_t fx = load_granule(fix_at(granules, slot));
+        fx = load_granule(fix_at(granules, slot));
         bool mine = X < 0 || gtag(fx) == tag;
 #pragma unroll
         for (int j = 0; j < MAXB; ++j) {
@@ -383,7 +453,9 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(KsimCtx c, uint64_t* gra
       int mode = 0, blk = -1, rank = 0;
       if (!ok) {
         mode = -1;
-        if (lane == 0) atomicOr(c.err, 4);
+        if (lane == 0) atomicOr(a.err, 4);
+      } else if (X >= 0 && gstop(fx)) {
+        mode = -2;  // the previous commit left the exact range: the host takes over from pod
       } else if (F == 1) {  // generic_scheduler.go:153-156: a single fit node skips selectHost
         mode = 1;
         int32_t jf = -1;
@@ -427,14 +499,14 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(KsimCtx c, uint64_t* gra
           rank = __builtin_amdgcn_readlane(r, src);
           if (blk < 0) mode = -1;
         }
-        if (mode < 0 && lane == 0) atomicOr(c.err, 2);
+        if (mode < 0 && lane == 0) atomicOr(a.err, 2);
       }
       STAMP(3);
 #ifdef KSIM_STAMPS
       o_prev = __builtin_amdgcn_s_memtime();
 #endif
       if (mode > 0 && blk == me) {
-        // ---------------- c. owner: the rank-th row from the top, commit ----------------
+        // ---------------- c. owner: the rank-th row from the top ----------------
         constexpr int S = NPT * RW;  // lane t = t-th 64-row segment from the top
         uint64_t m = 0;
         if (lane < S) {
@@ -457,95 +529,144 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(KsimCtx c, uint64_t* gra
             jsel = ks * RT + ws * 64 + (__builtin_ffsll((long long)bb) - 1);
           }
         }
-        OSTAMP(22);
         if (jsel < 0 || jsel >= nrows) {
           jsel = -1;
           mode = -1;
-          if (lane == 0) atomicOr(c.err, 2);
-        } else {
-          const ksim_pod& P = s_pod[pod % RING];
-          FRow r = load_frow(R, jsel);
-          r.rc += P.add_cpu; r.rm += P.add_mem; r.zc += P.nz_cpu; r.zm += P.nz_mem; r.count += 1;
-          if (lane == 0) {
-            R.rc[jsel] = r.rc; R.rm[jsel] = r.rm; R.zc[jsel] = r.zc; R.zm[jsel] = r.zm; R.count[jsel] = r.count;
-            c.out_node[pod] = (int32_t)(lo + jsel);
-          }
-          OSTAMP(23);
-          if (has_next) e_new = feval(preds, fpod(pod + 1), r, no_prio, wl, wmr, wb, rm_new);
-          OSTAMP(16);
+          if (lane == 0) atomicOr(a.err, 2);
         }
+        OSTAMP(22);
       }
-      if (mode == 0 && me == 0 && lane == 0) c.out_node[pod] = -1;
-      if (lane == 0) s_mode = mode;
+      if (mode == 0 && me == 0 && lane == 0) a.out_node[pod] = -1;
+      if (lane == 0) { s_mode[pb] = mode; s_own[pb] = jsel; }
       X = mode > 0 ? blk : -1;
       STAMP(6);
-    } else {
-      // ---------------- row waves: speculative evaluation of pod + 1 ----------------
-      const bool refill = wv == 1 && ((pod - c.first) % RING_FILL) == 0;
+    } else if (has_next) {
+      // ---------------- row waves: evaluate pod + 1, and pod + 1 after pod on its candidates ------
+      const bool refill = wv == 1 && ((pod - a.first) % RING_FILL) == 0;
       uint4 rv;
       if (refill) ring_load(pod + RING_FILL, rv);
 #ifdef KSIM_STAMPS
       const uint64_t te0 = __builtin_amdgcn_s_memtime();
 #endif
-      if (has_next) {
-        int32_t e[NPT];
-        eval_rows(pod + 1, e, B_rm, R.ev + nb * chunk);
-        wave_stats(e, nb, wv);
-        arrive_publish(pod + 1, nb);
+      const FPod P = load_fpod(s_pod[pod % RING]);
+      const FPod Q = load_fpod(s_pod[(pod + 1) % RING]);
+      const int w = wv - 1;
+#ifdef KSIM_STAMPS
+      uint64_t tw = __builtin_amdgcn_s_memtime();
+      if (tid == 64) st_acc[8] += tw - te0;
+#define WSTAMP(k) do { const uint64_t t_ = __builtin_amdgcn_s_memtime(); if (tid == 64) st_acc[k] += t_ - tw; tw = t_; } while (0)
+#else
+#define WSTAMP(k) do { } while (0)
+#endif
+      (void)w;
+      // every row, as it stands and as it would stand after pod: two independent evaluations
+      // per lane (no divergence; only the winner's second one is ever read)
+      int32_t e[NPT];
+      int32_t* evn = R.ev + nb * chunk;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int32_t j = k * RT + rt;
+        e[k] = -1;
+        B_rm[k] = 0;
+        if (j < nrows) {
+          const FRow r = load_frow(R, j);
+          uint32_t m2;
+          e[k] = feval(EC, Q, r, B_rm[k]);
+          const int32_t e2 = feval(EC, Q, plus(r, P), m2);
+          evn[j] = e[k];
+          R.ev2[j] = e2;
+          R.rm2[j] = m2;
+        }
       }
+      WSTAMP(9);
+      wave_stats(e, nb, wv);
+      WSTAMP(10);
+      arrive_publish(pod + 1, nb);
+      WSTAMP(11);
 #ifdef KSIM_STAMPS
       if (tid == 64) st_acc[5] += __builtin_amdgcn_s_memtime() - te0;
 #endif
       if (refill) ring_store(pod + RING_FILL, rv);
     }
-    __syncthreads();
+    lds_barrier();
     STAMP(7);
-    const int mode = s_mode;
-    if (mode < 0) break;  // uniform: every workgroup reaches the same verdict
+    const int mode = s_mode[pb];
+    if (mode < 0) {  // uniform: every workgroup reaches the same verdict
+      if (mode == -2) stop_at = pod;
+      break;
+    }
+    const int32_t own = s_own[pb];
 
-    if (wv == 0 && jsel >= 0 && has_next) {
-      // ---------------- d. owner: correction of pod + 1's statistics, O(1) ----------------
-      OSTAMP(17);
-      const int32_t e_old = R.ev[nb * chunk + jsel];
-      Top2 t{s_wg[nb][0], s_wg[nb][1], s_wg[nb][2], s_wg[nb][3], s_wg[nb][4]};
-      if (e_old >= 0) {  // remove the speculative evaluation of the committed row
-        t.f -= 1;
-        if (e_old == t.m1) {
-          if (--t.c1 == 0) { t.m1 = t.m2; t.c1 = t.c2; t.m2 = -1; t.c2 = 0; }
-        } else if (e_old == t.m2) {
-          if (--t.c2 == 0) { t.m2 = -1; }  // (a lower third value is not tracked: m2 is only
-        }                                   //  consulted when the m1 row is removed, below)
+    if (own >= 0) {
+      // ---------------- d. owner: correction of pod + 1's statistics, O(1), then the commit ----
+      if (wv == 0) {
+        OSTAMP(17);
+        const int32_t e_new = has_next ? R.ev2[jsel] : -1;
+        uint64_t stopbit = 0;
+        {
+          const ksim_pod& Pp = s_pod[pod % RING];
+          stopbit = (R.rc[jsel] + (double)Pp.add_cpu >= EXACT_LIM || R.rm[jsel] + (double)Pp.add_mem >= EXACT_LIM ||
+                     R.zc[jsel] + (double)Pp.nz_cpu >= EXACT_LIM || R.zm[jsel] + (double)Pp.nz_mem >= EXACT_LIM)
+                        ? (1ull << 55)
+                        : 0ull;
+        }
+        if (has_next) {
+          const int32_t e_old = R.ev[nb * chunk + jsel];
+          Top2 t{s_wg[nb][0], s_wg[nb][1], s_wg[nb][2], s_wg[nb][3], s_wg[nb][4]};
+          if (e_old >= 0) {  // remove the committed row's pre-commit evaluation
+            t.f -= 1;
+            if (e_old == t.m1 && --t.c1 == 0) { t.m1 = t.m2; t.c1 = t.c2; }
+          }
+          if (e_new >= 0) {
+            t.f += 1;
+            if (e_new > t.m1 || t.c1 == 0) { t.m1 = e_new; t.c1 = 1; }
+            else if (e_new == t.m1) { t.c1 += 1; }
+          }
+          if (t.c1 == 0) t.m1 = -1;
+          if (lane == 0)
+            store_granule(fix_at(granules, (int)((pod + 1) % NSLOT)), gpack(ptag(pod + 1), t.f, t.c1, t.m1) | stopbit);
+        }
+        OSTAMP(18);
+        if (lane == 0) {  // commit: NodeInfo.AddPod into the LDS row
+          const ksim_pod& Pp = s_pod[pod % RING];
+          const double rc = R.rc[jsel] + (double)Pp.add_cpu, rm = R.rm[jsel] + (double)Pp.add_mem;
+          const double zc = R.zc[jsel] + (double)Pp.nz_cpu, zm = R.zm[jsel] + (double)Pp.nz_mem;
+          R.rc[jsel] = rc; R.rm[jsel] = rm; R.zc[jsel] = zc; R.zm[jsel] = zm;
+          R.count[jsel] += 1;
+          if (rc >= EXACT_LIM || rm >= EXACT_LIM || zc >= EXACT_LIM || zm >= EXACT_LIM) atomicOr(a.err, 8);
+          a.out_node[pod] = (int32_t)(lo + jsel);
+          if (has_next) {
+            R.ev[nb * chunk + jsel] = e_new;
+            s_fix[nb][0] = jsel;
+            s_fix[nb][1] = (int32_t)R.rm2[jsel];
+          } else {
+            s_fix[nb][0] = -1;
+          }
+        }
       }
-      int32_t F1 = t.f, M1 = t.m1, C1 = t.c1;
-      if (e_new >= 0) {
-        F1 += 1;
-        if (e_new > M1) { M1 = e_new; C1 = 1; }
-        else if (e_new == M1) { C1 += 1; }
-      }
-      if (C1 == 0) M1 = -1;
-      if (lane == 0) store_granule(fix_at(granules, (int)((pod + 1) % NSLOT)), gpack(ptag(pod + 1), F1, C1, M1));
-      OSTAMP(18);
-      // off the critical path: the evaluation entry, the reasons and the wave's bitmasks
-      const int w = 1 + (jsel % RT) / 64;
-      int32_t e[NPT];
+      lds_barrier();  // uniform (own is workgroup-wide): row waves see the commit
+      if (wv == 0 && has_next) {
+        // off the critical path: the corrected wave's statistics and bitmasks
+        const int w = 1 + (jsel % RT) / 64;
+        int32_t e[NPT];
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) {
-        const int32_t j = k * RT + (w - 1) * 64 + lane;
-        e[k] = (j == jsel) ? e_new : (j < nrows ? R.ev[nb * chunk + j] : -1);
-      }
-      wave_stats(e, nb, w);
-      if (lane == 0) { R.ev[nb * chunk + jsel] = e_new; s_fix[nb][0] = jsel; s_fix[nb][1] = (int32_t)rm_new; }
-      OSTAMP(19);
+        for (int k = 0; k < NPT; ++k) {
+          const int32_t j = k * RT + (w - 1) * 64 + lane;
+          e[k] = j < nrows ? R.ev[nb * chunk + j] : -1;
+        }
+        wave_stats(e, nb, w);
+        OSTAMP(19);
 #ifdef KSIM_STAMPS
-      if (lane == 0) atomicAdd((unsigned long long*)&c.dbg[21], 1ull);
+        if (lane == 0) atomicAdd((unsigned long long*)&a.dbg[21], 1ull);
 #endif
+      }
     } else if (wv == 0 && lane == 0) {
       s_fix[nb][0] = -1;
     }
 
-    if (mode == 0 && c.collect && c.out_reasons) {  // FitError: every workgroup adds its reasons
+    if (mode == 0 && a.collect && a.out_reasons) {  // FitError: every workgroup adds its reasons
       if (tid < KSIM_NREASONS) s_hist[tid] = 0;
-      __syncthreads();
+      lds_barrier();
       if (wv > 0) {
         const int32_t fr = s_fix[pb][0];
         const uint32_t fmk = (uint32_t)s_fix[pb][1];
@@ -558,8 +679,8 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(KsimCtx c, uint64_t* gra
           }
         }
       }
-      __syncthreads();
-      if (tid < KSIM_NREASONS && s_hist[tid]) atomicAdd(&c.out_reasons[pod * KSIM_NREASONS + tid], s_hist[tid]);
+      lds_barrier();
+      if (tid < KSIM_NREASONS && s_hist[tid]) atomicAdd(&a.out_reasons[pod * KSIM_NREASONS + tid], s_hist[tid]);
     }
     STAMP(4);
     if (wv > 0) {
@@ -572,18 +693,19 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(KsimCtx c, uint64_t* gra
   __syncthreads();
   for (int32_t j = tid; j < nrows; j += BS) {
     const int64_t i = lo + j;
-    c.req_cpu[i] = R.rc[j]; c.req_mem[i] = R.rm[j];
-    c.nz_cpu[i] = R.zc[j]; c.nz_mem[i] = R.zm[j];
-    c.pod_count[i] = R.count[j];
+    a.req_cpu[i] = (int64_t)R.rc[j]; a.req_mem[i] = (int64_t)R.rm[j];
+    a.nz_cpu[i] = (int64_t)R.zc[j]; a.nz_mem[i] = (int64_t)R.zm[j];
+    a.pod_count[i] = R.count[j];
   }
   if (me == 0 && tid == 0) {
-    *c.counter = counter;
-    *c.cursor = c.end;
+    *a.counter = counter;
+    *a.cursor = stop_at;
   }
 #ifdef KSIM_STAMPS
   if (me == 0 && tid == 0)
-    for (int k = 0; k < 16; ++k) c.dbg[k] += (k == 5) ? 0 : st_acc[k];
-  if (me == 0 && tid == 64) c.dbg[5] += st_acc[5];
+    for (int k = 0; k < 16; ++k) a.dbg[k] += (k == 5 || (k >= 8 && k <= 11)) ? 0 : st_acc[k];
+  if (me == 0 && tid == 64)
+    for (int k : {5, 8, 9, 10, 11}) a.dbg[k] += st_acc[k];
 #endif
 }
 
@@ -601,7 +723,7 @@ extern "C" int ksim_pfast_config(int64_t n, int* grid, int* lds_rows) {
   if (n < (int64_t)g * 64) g = (int)((n + 63) / 64);
   if (g < 1) g = 1;
   const int64_t chunk = (n + g - 1) / g;
-  if (chunk * LDS_ROW_BYTES > PF_LDS_BUDGET || chunk > 4 * RT || chunk > 4095) return 0;
+  if (chunk * LDS_ROW_BYTES > PF_LDS_BUDGET || chunk > 4 * RT || chunk > 2047) return 0;
   *grid = g;
   *lds_rows = (int)chunk;
   return 1;
@@ -610,9 +732,18 @@ extern "C" int ksim_pfast_config(int64_t n, int* grid, int* lds_rows) {
 extern "C" size_t ksim_pfast_granule_bytes(void) { return (size_t)(NSLOT * MAXG + NSLOT * FIXSTRIDE) * sizeof(uint64_t); }
 
 extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, hipStream_t s) {
+  PfArgs a;
+  a.n = c->n; a.chunk = c->chunk; a.first = c->first; a.end = c->end;
+  a.alloc_cpu = c->alloc_cpu; a.alloc_mem = c->alloc_mem; a.allowed_pods = c->allowed_pods; a.flags = c->flags;
+  a.req_cpu = c->req_cpu; a.req_mem = c->req_mem; a.nz_cpu = c->nz_cpu; a.nz_mem = c->nz_mem;
+  a.pod_count = c->pod_count; a.pods = c->pods; a.counter = c->counter; a.cursor = c->cursor;
+  a.out_node = c->out_node; a.out_reasons = c->out_reasons; a.err = c->err; a.dbg = c->dbg; a.granules = granules;
+  a.preds = c->preds; a.no_prio = c->no_prio; a.collect = c->collect;
+  a.wl = (int32_t)c->w[KSIM_W_LEAST_REQUESTED]; a.wm = (int32_t)c->w[KSIM_W_MOST_REQUESTED];
+  a.wb = (int32_t)c->w[KSIM_W_BALANCED];
   const size_t lds = (size_t)lds_rows * LDS_ROW_BYTES;
-  if (lds_rows <= RT) hipLaunchKernelGGL((ksim_pfast_kernel<1>), dim3(grid), dim3(BS), lds, s, *c, granules);
-  else if (lds_rows <= 2 * RT) hipLaunchKernelGGL((ksim_pfast_kernel<2>), dim3(grid), dim3(BS), lds, s, *c, granules);
-  else hipLaunchKernelGGL((ksim_pfast_kernel<4>), dim3(grid), dim3(BS), lds, s, *c, granules);
+  if (lds_rows <= RT) hipLaunchKernelGGL((ksim_pfast_kernel<1>), dim3(grid), dim3(BS), lds, s, a);
+  else if (lds_rows <= 2 * RT) hipLaunchKernelGGL((ksim_pfast_kernel<2>), dim3(grid), dim3(BS), lds, s, a);
+  else hipLaunchKernelGGL((ksim_pfast_kernel<4>), dim3(grid), dim3(BS), lds, s, a);
   return hipGetLastError();
 }

@@ -63,6 +63,9 @@ struct ksim_handle {
   std::vector<int32_t> h_n_tt, h_n_na;
   // fast_pre[i] = resource-only pods among the first i of the queue (ksim_is_fast_pod)
   std::vector<int64_t> fast_pre;
+  // the fast kernel computes in float64: every node cpu / memory quantity below 2^48 at load
+  // (pods: checked per pod in fast_pre); cleared for good once a commit reaches 2^48
+  bool pfast_off = false;
 };
 
 static int fail(ksim_handle* h, int code, const char* fmt, ...) {
@@ -215,6 +218,12 @@ int ksim_load_nodes(ksim_handle* h, const ksim_node_table* t) {
   c.alloc_cpu = ac; c.alloc_mem = am; c.alloc_gpu = ag; c.alloc_eph = ae; c.alloc_scalar = as;
   c.allowed_pods = ap; c.label_set = ls; c.taint_set = ts;
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  {
+    const int64_t lim = (int64_t)1 << 48;
+    for (const int64_t* col : {t->alloc_cpu, t->req_cpu, t->nz_cpu, t->alloc_mem, t->req_mem, t->nz_mem})
+      for (int64_t i = 0; col && i < n; ++i)
+        if (col[i] < 0 || col[i] >= lim) h->pfast_off = true;
+  }
   h->have_nodes = true;
   return KSIM_OK;
 }
@@ -296,10 +305,14 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
     const ksim_pod& p = pods[i];
     const int k1 = c.w[KSIM_W_TAINT_TOLERATION] ? h->h_n_tt[p.cls] : 1;
     const int k2 = c.w[KSIM_W_NODE_AFFINITY] ? h->h_n_na[p.cls] : 1;
-    const bool fast = k1 * k2 == 1 && p.host == -1 && p.port_cnt == 0 && p.scalar_cnt == 0 && p.req_gpu == 0 &&
-                      p.req_eph == 0 && !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS));
+    const int64_t lim = (int64_t)1 << 48;
+    bool in_range = true;
+    for (int64_t v : {p.req_cpu, p.req_mem, p.add_cpu, p.add_mem, p.nz_cpu, p.nz_mem}) in_range &= v >= 0 && v < lim;
+    const bool fast = in_range && k1 * k2 == 1 && p.host == -1 && p.port_cnt == 0 && p.scalar_cnt == 0 &&
+                      p.req_gpu == 0 && p.req_eph == 0 && !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS));
     h->fast_pre[i + 1] = h->fast_pre[i] + (fast ? 1 : 0);
   }
+
   if (c.collect) HIPCHK(h, hipMemsetAsync(c.out_reasons, 0, n_pods * KSIM_NREASONS * sizeof(int32_t), h->stream));
   h->n_pods = n_pods;
   HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -413,8 +426,10 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
     fprintf(stderr, "[ksim stamps] pfast pods=%lld (%.3f ms) cycles/pod: sweep %.0f decide %.0f owner %.0f barrier %.0f tail %.0f row-eval %.0f\n",
             (long long)count, ms, d[2] / (double)count, d[3] / (double)count, d[6] / (double)count, d[7] / (double)count,
             (d[4] + d[1]) / (double)count, d[5] / (double)count);
-    fprintf(stderr, "[ksim stamps] pfast owner (%llu fixes) cycles: select %.0f commit %.0f e_new %.0f barrier %.0f fix-publish %.0f restat %.0f\n",
-            (unsigned long long)d[21], d[22] / nf, d[23] / nf, d[16] / nf, d[17] / nf, d[18] / nf, d[19] / nf);
+    fprintf(stderr, "[ksim stamps] pfast row wave 1 cycles/pod: pods %.0f eval %.0f wave-stats %.0f publish %.0f\n",
+            d[8] / (double)count, d[9] / (double)count, d[10] / (double)count, d[11] / (double)count);
+    fprintf(stderr, "[ksim stamps] pfast owner (%llu fixes) cycles: select %.0f barrier %.0f fix-publish %.0f commit+barrier+restat %.0f\n",
+            (unsigned long long)d[21], d[22] / nf, d[17] / nf, d[18] / nf, d[19] / nf);
   }
 #endif
   if (st) {
@@ -430,9 +445,31 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
 static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   KsimCtx& c = h->ctx;
   int grid = 0, lds_rows = 0;
-  if (!getenv("KSIM_NO_PFAST") && count > 0 && h->fast_pre[first + count] - h->fast_pre[first] == count &&
-      persistent_weights_ok(c) && ksim_pfast_config(c.n, &grid, &lds_rows))
-    return run_pfast_mode(h, first, count, grid, lds_rows, st);
+  if (!getenv("KSIM_NO_PFAST") && count > 0 && !h->pfast_off && h->fast_pre[first + count] - h->fast_pre[first] == count &&
+      persistent_weights_ok(c) && ksim_pfast_config(c.n, &grid, &lds_rows)) {
+    int rc = run_pfast_mode(h, first, count, grid, lds_rows, st);
+    if (rc) return rc;
+    int32_t err = 0;
+    HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
+    if (!(err & 8)) return KSIM_OK;
+    // a node left the exact float64 range: the general kernel from now on
+    h->pfast_off = true;
+    int64_t cur = 0;
+    HIPCHK(h, hipMemcpy(&cur, c.cursor, 8, hipMemcpyDeviceToHost));
+    err &= ~8;
+    HIPCHK(h, hipMemcpy(c.err, &err, 4, hipMemcpyHostToDevice));
+    if (cur >= first + count) return KSIM_OK;
+    const double ms0 = st ? st->kernel_ms : 0.0;
+    ksim_stats s2{};
+    rc = run_persistent_mode(h, cur, first + count - cur, &s2);
+    if (rc) return rc;
+    if (st) {
+      st->device_ms += s2.device_ms;
+      st->kernel_ms = ms0 + s2.kernel_ms;
+      st->kernel_launches += s2.kernel_launches;
+    }
+    return KSIM_OK;
+  }
   if (!ksim_persistent_config(c.n, &grid, &lds_rows))
     return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: node table does not fit the on-chip layout");
   if (!persistent_weights_ok(c)) return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: map-priority weights exceed the 27-bit score range");
@@ -560,6 +597,13 @@ int ksim_assume(ksim_handle* h, int64_t pod, int64_t node) {
   hipError_t e = ksim_launch_assume(&h->ctx, pod, node, h->stream);
   if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "assume launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (!h->pfast_off) {  // keep the fast kernel's float64 range invariant (ksim_pfast.hip)
+    for (const int64_t* col : {h->ctx.req_cpu, h->ctx.req_mem, h->ctx.nz_cpu, h->ctx.nz_mem}) {
+      int64_t v = 0;
+      HIPCHK(h, hipMemcpy(&v, col + node, 8, hipMemcpyDeviceToHost));
+      if (v < 0 || v >= ((int64_t)1 << 48)) h->pfast_off = true;
+    }
+  }
   int32_t err = 0;
   HIPCHK(h, hipMemcpy(&err, h->ctx.err, 4, hipMemcpyDeviceToHost));
   if (err & 1) return fail(h, KSIM_E_OVERFLOW, "a node's host-port slots overflowed (raise port_slots)");

@@ -12,6 +12,6 @@ tail -2 $OUT/pytest_gpu.log
 timeout -k 10 300 python3 bench.py --cpu-sample 0 --steps 30 "$@" > $OUT/bench.json 2> $OUT/bench.err || { echo "bench failed"; tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
 if [ -f kubernetes-schedule-simulator_amd/lib/stamps/libksim.so ]; then
-  KSIM_LIB=kubernetes-schedule-simulator_amd/lib/stamps/libksim.so timeout -k 10 120 python3 bench.py --cpu-sample 0 --steps 3 --warmup 1 "$@" > $OUT/stamps.json 2> $OUT/stamps.err || { echo "stamps failed"; tail $OUT/stamps.err; exit 1; }
-  grep -A2 'ksim stamps\] pods' $OUT/stamps.err | tail -3
+  KSIM_LIB=kubernetes-schedule-simulator_amd/lib/stamps/libksim.so timeout -k 10 120 python3 bench.py --cpu-sample 0 --steps 30 "$@" > $OUT/stamps.json 2> $OUT/stamps.err || { echo "stamps failed"; tail $OUT/stamps.err; exit 1; }
+  grep 'ksim stamps' $OUT/stamps.err | tail -4
 fi
