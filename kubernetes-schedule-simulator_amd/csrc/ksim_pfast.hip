@@ -163,7 +163,7 @@ struct FRows {  // LDS image of the owned rows (SoA)
   uint32_t* rm2;  // [chunk]: ... its reason mask
 };
 
-constexpr int LDS_ROW_BYTES = 8 * 8 + 7 * 4;  // 92
+constexpr int LDS_ROW_BYTES = 8 * 8 + 8 * 4;  // 96: 8 float64 + allowed, count, flags, ev[2], ev2, rm2, top_list
 
 extern __shared__ __attribute__((aligned(16))) char kf_smem[];
 
@@ -259,12 +259,11 @@ struct Top2 {
 template <int NPT>
 __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   __shared__ int32_t s_wst[2][RW][5];         // per row wave: fit, m1, c1, m2, c2 (by pod parity)
-  __shared__ uint64_t s_fm[2][NPT][RW];       // per 64-row segment: fit rows
-  __shared__ uint64_t s_bm[2][NPT][RW];       // ... rows at the wave maximum
+  __shared__ uint64_t s_bm[2][NPT][RW];       // per 64-row segment: rows at the wave maximum
   __shared__ int32_t s_wg[2][5];              // workgroup top-two of the pod
   __shared__ int32_t s_fix[2][2];             // {row the owner corrected (-1 none), its reason mask}
   __shared__ int32_t s_hist[KSIM_NREASONS];
-  __shared__ int32_t s_mode[2], s_own[2];  // by pod parity: read after the barrier, rewritten two pods later
+  __shared__ int32_t s_mode[2], s_own[2];     // by pod parity: read after the barrier, rewritten two pods later
   __shared__ int32_t s_arr;
   __shared__ __attribute__((aligned(16))) ksim_pod s_pod[RING];
 #ifdef KSIM_STAMPS
@@ -280,6 +279,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   const int64_t hi = (lo + chunk < a.n) ? lo + chunk : a.n;
   const int32_t nrows = (int32_t)(hi - lo);
   const FRows R = carve((int)chunk);
+  int32_t* const top_list = reinterpret_cast<int32_t*>(R.rm2 + chunk);  // [chunk]: rows at the workgroup maximum, from the top
   const uint32_t preds = a.preds;
   const bool no_prio = a.no_prio != 0;
   EvCfg EC;
@@ -303,6 +303,8 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
     R.zc[j] = (double)a.nz_cpu[i]; R.zm[j] = (double)a.nz_mem[i];
     R.allowed[j] = a.allowed_pods[i]; R.count[j] = a.pod_count[i]; R.fl[j] = a.flags[i];
   }
+  // pod descriptors: RING_FILL (1 KiB) per refill, one 16-byte load per lane of wave 1, loaded
+  // a whole refill period before they are stored so the load latency never stalls a pod
   auto ring_load = [&](int64_t p0, uint4& v) {
     const int64_t p = p0 + lane / 8;
     if (p < a.end) v = reinterpret_cast<const uint4*>(&a.pods[p])[lane % 8];
@@ -311,9 +313,11 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
     const int64_t p = p0 + lane / 8;
     if (p < a.end) reinterpret_cast<uint4*>(&s_pod[p % RING])[lane % 8] = v;
   };
+  uint4 ring_next = make_uint4(0, 0, 0, 0);  // wave 1: descriptors of the next refill
   if (wv == 1) {
     uint4 v;
     ring_load(a.first, v);
+    ring_load(a.first + RING_FILL, ring_next);
     ring_store(a.first, v);
   }
   if (tid == 0) { s_fix[a.first & 1][0] = -1; s_arr = 0; }
@@ -326,9 +330,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
     int32_t v = -1, nf = 0;
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
-      const uint64_t fm = __ballot(e[k] >= 0);
-      nf += __popcll(fm);
-      if (lane == 0) s_fm[buf][k][w - 1] = fm;
+      nf += __popcll(__ballot(e[k] >= 0));
       v = e[k] > v ? e[k] : v;
     }
     const int32_t m1 = ksimw::max_i32(v);
@@ -376,6 +378,29 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       }
     }
   };
+  // control wave: rows at the workgroup maximum of the pod in `buf`, name rank descending,
+  // into top_list — so an owner turns its rank into a row with one LDS read
+  auto build_top_list = [&](int buf) {
+    constexpr int S = NPT * RW;  // lane t = t-th 64-row segment from the top
+    const int32_t M = s_wg[buf][1];
+    uint64_t m = 0;
+    if (lane < S) {
+      const int k = NPT - 1 - lane / RW, w = RW - 1 - lane % RW;
+      m = (M >= 0 && s_wst[buf][w][1] == M) ? s_bm[buf][k][w] : 0ull;
+    }
+    const int32_t cnt = __popcll(m);
+    const int32_t base = ksimw::prefix_incl_i32(cnt) - cnt;
+    uint64_t live = __ballot(cnt != 0);
+    while (live) {
+      const int t = __builtin_ctzll(live);
+      live &= live - 1;
+      const uint64_t ms = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(m >> 32), t) << 32) |
+                          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)m, t);
+      const int32_t b0 = __builtin_amdgcn_readlane(base, t);
+      const int k = NPT - 1 - t / RW, w = RW - 1 - t % RW;
+      if ((ms >> lane) & 1ull) top_list[b0 + __popcll(ms >> lane) - 1] = k * RT + w * 64 + lane;
+    }
+  };
 
   // ---- prologue: evaluations and statistics of the first pod ----
   uint32_t A_rm[NPT], B_rm[NPT];
@@ -407,16 +432,18 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
     const bool has_next = pod + 1 < a.end;
     const int pb = (int)(pod & 1);
     const int nb = (int)((pod + 1) & 1);
-    int32_t jsel = -1;  // control wave: row this workgroup commits pod to
+    int32_t jsel = -1;      // control wave: row this workgroup commits pod to
+    uint64_t stopbit = 0;   // ... and whether that commit leaves the exact float64 range
 #ifdef KSIM_STAMPS
     uint64_t o_prev = 0;
 #endif
 
     if (wv == 0) {
+      build_top_list(pb);
+      STAMP(1);
       // ---------------- a. sweep: every workgroup's granule of pod (+ the owner's fix) -------
       const uint64_t tag = ptag(pod);
       const int slot = (int)(pod % NSLOT);
-      STAMP(1);
       uint64_t g[MAXB], fx = 0;
       bool ok = false;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -441,6 +468,8 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       }
       STAMP(2);
       // ---------------- b. decide: findNodesThatFit count, max score, selectHost ------------
+      // One path for every F > 0: with a single fit node C = 1 and ix = 0 picks it, and only
+      // the counter increment differs (generic_scheduler.go:153-156 skips selectHost).
       int32_t f = 0, lm = -1;
 #pragma unroll
       for (int j = 0; j < MAXB; ++j) {
@@ -450,107 +479,72 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       }
       const int32_t F = ksimw::sum_i32(f);
       const int32_t M0 = ksimw::max_i32(lm);
-      int mode = 0, blk = -1, rank = 0;
-      if (!ok) {
-        mode = -1;
-        if (lane == 0) atomicOr(a.err, 4);
-      } else if (X >= 0 && gstop(fx)) {
-        mode = -2;  // the previous commit left the exact range: the host takes over from pod
-      } else if (F == 1) {  // generic_scheduler.go:153-156: a single fit node skips selectHost
-        mode = 1;
-        int32_t jf = -1;
+      int32_t bm[MAXB], tot = 0;
 #pragma unroll
-        for (int j = 0; j < MAXB; ++j) jf = gfit(g[j]) ? j : jf;
-        const uint64_t hb = __ballot(jf >= 0);
-        const int src = __builtin_ffsll((long long)hb) - 1;
-        blk = src * MAXB + __builtin_amdgcn_readlane(jf, src);
-      } else if (F > 1) {
-        mode = 2;
-        int32_t bm[MAXB], tot = 0;
-#pragma unroll
-        for (int j = 0; j < MAXB; ++j) {
-          bm[j] = (gcnt(g[j]) && gscore(g[j]) == M0) ? gcnt(g[j]) : 0;
-          tot += bm[j];
-        }
-        const int32_t pre = ksimw::prefix_incl_i32(tot);
-        const uint32_t C = (uint32_t)__builtin_amdgcn_readlane(pre, 63);
-        const int64_t ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)C) : (int64_t)((uint32_t)counter % C);
-        counter += 1;  // generic_scheduler.go:192-195
-        const int64_t above = (int64_t)C - pre;  // matches in workgroups of higher lanes
-        const bool hit = tot > 0 && ix >= above && ix < above + tot;
-        int32_t found = -1, r = 0;
-        if (hit) {
-          int64_t rr = ix - above;
-#pragma unroll
-          for (int j = MAXB - 1; j >= 0; --j) {
-            if (found < 0) {
-              if (rr < bm[j]) found = lane * MAXB + j;
-              else rr -= bm[j];
-            }
-          }
-          r = (int32_t)rr;
-        }
-        const uint64_t hb = __ballot(hit);
-        if (hb == 0) {
-          mode = -1;
-        } else {
-          const int src = __builtin_ffsll((long long)hb) - 1;
-          blk = __builtin_amdgcn_readlane(found, src);
-          rank = __builtin_amdgcn_readlane(r, src);
-          if (blk < 0) mode = -1;
-        }
-        if (mode < 0 && lane == 0) atomicOr(a.err, 2);
+      for (int j = 0; j < MAXB; ++j) {
+        bm[j] = (gcnt(g[j]) && gscore(g[j]) == M0) ? gcnt(g[j]) : 0;
+        tot += bm[j];
       }
+      const int32_t pre = ksimw::prefix_incl_i32(tot);
+      const uint32_t C = (uint32_t)__builtin_amdgcn_readlane(pre, 63);
+      const uint32_t Cs = C ? C : 1u;
+      const int64_t ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)Cs) : (int64_t)((uint32_t)counter % Cs);
+      const int64_t above = (int64_t)C - pre;  // matches in workgroups of higher lanes
+      const bool hit = tot > 0 && ix >= above && ix < above + tot;
+      int32_t found = -1;
+      int64_t rr = ix - above;
+#pragma unroll
+      for (int j = MAXB - 1; j >= 0; --j) {
+        const bool here = found < 0 && rr < bm[j];
+        found = here ? lane * MAXB + j : found;
+        rr = (found < 0) ? rr - bm[j] : rr;
+      }
+      const uint64_t hb = __ballot(hit);
+      const int src = __builtin_ffsll((long long)hb) - 1;
+      const int blk = hb ? __builtin_amdgcn_readlane(found, src) : -1;
+      const int rank = hb ? __builtin_amdgcn_readlane((int32_t)rr, src) : 0;
+      int mode;
+      if (!ok) mode = -1;
+      else if (X >= 0 && gstop(fx)) mode = -2;  // the previous commit left the exact range
+      else if (F == 0) mode = 0;
+      else mode = (hb && blk >= 0) ? 2 : -1;
+      if (mode == 2 && F > 1) counter += 1;  // generic_scheduler.go:192-195
+      if (lane == 0 && mode == -1) atomicOr(a.err, ok ? 2 : 4);
       STAMP(3);
 #ifdef KSIM_STAMPS
       o_prev = __builtin_amdgcn_s_memtime();
 #endif
-      if (mode > 0 && blk == me) {
+      if (mode == 2 && blk == me) {
         // ---------------- c. owner: the rank-th row from the top ----------------
-        constexpr int S = NPT * RW;  // lane t = t-th 64-row segment from the top
-        uint64_t m = 0;
-        if (lane < S) {
-          const int k = NPT - 1 - lane / RW, w = RW - 1 - lane % RW;
-          m = (mode == 1) ? s_fm[pb][k][w] : (s_wst[pb][w][1] == M0 ? s_bm[pb][k][w] : 0ull);
-        }
-        const int32_t cnt = __popcll(m);
-        const int32_t pre = ksimw::prefix_incl_i32(cnt);
-        const uint64_t hm = __ballot(pre > rank);
-        if (hm) {
-          const int ts = __builtin_ffsll((long long)hm) - 1;
-          const int32_t r2 = rank - (__builtin_amdgcn_readlane(pre, ts) - __builtin_amdgcn_readlane(cnt, ts));
-          const uint64_t ms = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(m >> 32), ts) << 32) |
-                              (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)m, ts);
-          // the r2-th set bit counted from the top
-          const bool is = ((ms >> lane) & 1ull) && __popcll((ms >> lane) >> 1) == r2;
-          const uint64_t bb = __ballot(is);
-          if (bb) {
-            const int ks = NPT - 1 - ts / RW, ws = RW - 1 - ts % RW;
-            jsel = ks * RT + ws * 64 + (__builtin_ffsll((long long)bb) - 1);
-          }
-        }
+        jsel = (rank < s_wg[pb][2]) ? top_list[rank] : -1;
         if (jsel < 0 || jsel >= nrows) {
           jsel = -1;
           mode = -1;
           if (lane == 0) atomicOr(a.err, 2);
+        } else {
+          const ksim_pod& Pp = s_pod[pod % RING];
+          stopbit = (R.rc[jsel] + (double)Pp.add_cpu >= EXACT_LIM || R.rm[jsel] + (double)Pp.add_mem >= EXACT_LIM ||
+                     R.zc[jsel] + (double)Pp.nz_cpu >= EXACT_LIM || R.zm[jsel] + (double)Pp.nz_mem >= EXACT_LIM)
+                        ? (1ull << 55)
+                        : 0ull;
         }
         OSTAMP(22);
       }
       if (mode == 0 && me == 0 && lane == 0) a.out_node[pod] = -1;
       if (lane == 0) { s_mode[pb] = mode; s_own[pb] = jsel; }
-      X = mode > 0 ? blk : -1;
+      X = mode == 2 ? blk : -1;
       STAMP(6);
     } else if (has_next) {
-      // ---------------- row waves: evaluate pod + 1, and pod + 1 after pod on its candidates ------
+      // ---------------- row waves: evaluate pod + 1, as the rows stand and after pod -----------
       const bool refill = wv == 1 && ((pod - a.first) % RING_FILL) == 0;
+      if (refill) ring_store(pod + RING_FILL, ring_next);  // loaded a refill period ago
       uint4 rv;
-      if (refill) ring_load(pod + RING_FILL, rv);
+      if (refill) ring_load(pod + 2 * RING_FILL, rv);
 #ifdef KSIM_STAMPS
       const uint64_t te0 = __builtin_amdgcn_s_memtime();
 #endif
       const FPod P = load_fpod(s_pod[pod % RING]);
       const FPod Q = load_fpod(s_pod[(pod + 1) % RING]);
-      const int w = wv - 1;
 #ifdef KSIM_STAMPS
       uint64_t tw = __builtin_amdgcn_s_memtime();
       if (tid == 64) st_acc[8] += tw - te0;
@@ -558,9 +552,8 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 #else
 #define WSTAMP(k) do { } while (0)
 #endif
-      (void)w;
-      // every row, as it stands and as it would stand after pod: two independent evaluations
-      // per lane (no divergence; only the winner's second one is ever read)
+      // two independent evaluations per lane (no divergence; only the winner's second one is
+      // ever read)
       int32_t e[NPT];
       int32_t* evn = R.ev + nb * chunk;
 #pragma unroll
@@ -586,7 +579,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 #ifdef KSIM_STAMPS
       if (tid == 64) st_acc[5] += __builtin_amdgcn_s_memtime() - te0;
 #endif
-      if (refill) ring_store(pod + RING_FILL, rv);
+      if (refill) ring_next = rv;
     }
     lds_barrier();
     STAMP(7);
@@ -601,42 +594,33 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       // ---------------- d. owner: correction of pod + 1's statistics, O(1), then the commit ----
       if (wv == 0) {
         OSTAMP(17);
-        const int32_t e_new = has_next ? R.ev2[jsel] : -1;
-        uint64_t stopbit = 0;
-        {
-          const ksim_pod& Pp = s_pod[pod % RING];
-          stopbit = (R.rc[jsel] + (double)Pp.add_cpu >= EXACT_LIM || R.rm[jsel] + (double)Pp.add_mem >= EXACT_LIM ||
-                     R.zc[jsel] + (double)Pp.nz_cpu >= EXACT_LIM || R.zm[jsel] + (double)Pp.nz_mem >= EXACT_LIM)
-                        ? (1ull << 55)
-                        : 0ull;
-        }
         if (has_next) {
-          const int32_t e_old = R.ev[nb * chunk + jsel];
-          Top2 t{s_wg[nb][0], s_wg[nb][1], s_wg[nb][2], s_wg[nb][3], s_wg[nb][4]};
-          if (e_old >= 0) {  // remove the committed row's pre-commit evaluation
-            t.f -= 1;
-            if (e_old == t.m1 && --t.c1 == 0) { t.m1 = t.m2; t.c1 = t.c2; }
+          // the workgroup's pod + 1 statistics without the committed row's pre-commit
+          // evaluation, with its post-commit one (straight-line selects)
+          const int32_t e_new = R.ev2[jsel], e_old = R.ev[nb * chunk + jsel];
+          const int32_t f0 = s_wg[nb][0], m1 = s_wg[nb][1], c1 = s_wg[nb][2], m2 = s_wg[nb][3], c2 = s_wg[nb][4];
+          const bool rem = e_old >= 0, add = e_new >= 0;
+          const int32_t c1a = c1 - ((rem && e_old == m1) ? 1 : 0);
+          const int32_t mb = c1a ? m1 : (c2 ? m2 : -1), cb = c1a ? c1a : c2;
+          const bool up = add && (cb == 0 || e_new > mb), eq = add && !up && e_new == mb;
+          const int32_t M = up ? e_new : mb, Cn = up ? 1 : cb + (eq ? 1 : 0);
+          const int32_t Ff = f0 - (rem ? 1 : 0) + (add ? 1 : 0);
+          if (lane == 0) {
+            store_granule(fix_at(granules, (int)((pod + 1) % NSLOT)),
+                          gpack(ptag(pod + 1), Ff, Cn, Cn ? M : -1) | stopbit);
+            s_wg[nb][0] = Ff; s_wg[nb][1] = Cn ? M : -1; s_wg[nb][2] = Cn;
           }
-          if (e_new >= 0) {
-            t.f += 1;
-            if (e_new > t.m1 || t.c1 == 0) { t.m1 = e_new; t.c1 = 1; }
-            else if (e_new == t.m1) { t.c1 += 1; }
-          }
-          if (t.c1 == 0) t.m1 = -1;
-          if (lane == 0)
-            store_granule(fix_at(granules, (int)((pod + 1) % NSLOT)), gpack(ptag(pod + 1), t.f, t.c1, t.m1) | stopbit);
         }
         OSTAMP(18);
         if (lane == 0) {  // commit: NodeInfo.AddPod into the LDS row
           const ksim_pod& Pp = s_pod[pod % RING];
-          const double rc = R.rc[jsel] + (double)Pp.add_cpu, rm = R.rm[jsel] + (double)Pp.add_mem;
-          const double zc = R.zc[jsel] + (double)Pp.nz_cpu, zm = R.zm[jsel] + (double)Pp.nz_mem;
-          R.rc[jsel] = rc; R.rm[jsel] = rm; R.zc[jsel] = zc; R.zm[jsel] = zm;
+          R.rc[jsel] += (double)Pp.add_cpu; R.rm[jsel] += (double)Pp.add_mem;
+          R.zc[jsel] += (double)Pp.nz_cpu; R.zm[jsel] += (double)Pp.nz_mem;
           R.count[jsel] += 1;
-          if (rc >= EXACT_LIM || rm >= EXACT_LIM || zc >= EXACT_LIM || zm >= EXACT_LIM) atomicOr(a.err, 8);
+          if (stopbit) atomicOr(a.err, 8);
           a.out_node[pod] = (int32_t)(lo + jsel);
           if (has_next) {
-            R.ev[nb * chunk + jsel] = e_new;
+            R.ev[nb * chunk + jsel] = R.ev2[jsel];
             s_fix[nb][0] = jsel;
             s_fix[nb][1] = (int32_t)R.rm2[jsel];
           } else {
