@@ -241,3 +241,58 @@ def test_score_boundaries_match_c_oracle(prios, mode):
     for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
         assert np.array_equal(s[k], ref_state[k]), k
     assert (out >= 0).sum() > m // 4  # the queue is not all FitErrors
+
+
+def test_fast_kernel_hands_over_at_exactness_bound():
+    """Resource-only pods whose commits take nodes' non-zero requested memory past 2^48: the
+    specialised float64 kernel (ksim_pfast.hip) stops before the next pod and the general
+    kernel finishes the call — placements, histograms, counter and node state equal the C
+    oracle's, and a later call (general kernel from the start) still agrees."""
+    import cpu_ref
+    from ksim import synth
+    n, m = 300, 3000
+    r = synth.splitmix64(91, n + m)
+    alloc_mem = np.full(n, 2 ** 48 - 1, np.int64)
+    alloc_cpu = synth._pick(r[:n], [4000, 8000, 16000]).astype(np.int64)
+    pcpu = synth._pick(r[n:], [100, 250, 500])
+    pmem = synth._pick(r[n:] >> np.uint64(7), [2 ** 30, 2 ** 40, 3 * 2 ** 40])
+    names = ["x-%04d" % i for i in range(n)]
+    cl = synth.resource_cluster(names, alloc_cpu, alloc_mem, np.full(n, 60, np.int32), pcpu, pmem)
+    cl.cols["nz_mem"][:] = 2 ** 48 - 5 * 2 ** 40  # already close to the bound
+    preds = list(scheduler.DEFAULT_PREDICATES)
+    prios = [("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
+    g = scheduler.GenericScheduler(cl, preds, prios)
+    out1, rs1, _ = g.schedule(0, 1500)
+    out2, rs2, _ = g.schedule(1500, 1500)
+    ref, ref_reasons, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, prios), threads=8)
+    assert np.array_equal(np.concatenate([out1, out2]), ref)
+    assert np.array_equal(np.concatenate([rs1, rs2]), ref_reasons)
+    assert g.last_node_index == ref_ctr
+    s = g.node_state()
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+        assert np.array_equal(s[k], ref_state[k]), k
+    assert s["nz_mem"].max() >= 2 ** 48  # the bound was actually crossed
+
+
+@pytest.mark.parametrize("seed", [3, 8])
+def test_fast_and_general_kernels_agree(seed, monkeypatch):
+    """The same resource-only queue through the specialised kernel and, with KSIM_NO_PFAST, the
+    general persistent kernel: identical placements, counter and node state (and both equal
+    the C oracle's)."""
+    import cpu_ref
+    from ksim import synth
+    res = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("KSIM_NO_PFAST", env)
+        cl, p, q = synth.config_c3(30_000, 4000, seed=seed)
+        g = scheduler.GenericScheduler(cl, p, q, mode=abi.MODE_PERSISTENT, collect_reasons=False)
+        out, _, _ = g.schedule(0, 4000)
+        res.append((out, g.last_node_index, g.node_state()))
+        monkeypatch.delenv("KSIM_NO_PFAST", raising=False)
+    (o1, c1, s1), (o2, c2, s2) = res
+    assert np.array_equal(o1, o2) and c1 == c2
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+        assert np.array_equal(s1[k], s2[k]), k
+    ref, _, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, 4000, threads=8)
+    assert np.array_equal(o1, ref) and c1 == ref_ctr
