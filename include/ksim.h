@@ -248,6 +248,17 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
 int ksim_evaluate(ksim_handle* h, int64_t pod, uint8_t* out_fit, uint32_t* out_reasons,
                   int64_t* out_score, uint8_t* out_rclass);
 
+/* Scenario sweep — the capacity-planning what-if (BASELINE configs[4]): n_scen
+ * independent copies of the current node state each schedule pods [first, first+count) in order
+ * under their own map-priority weights (weights[s*KSIM_NW + KSIM_W_LEAST_REQUESTED /
+ * _MOST_REQUESTED / _BALANCED]; the reduce slots must be 0), starting from the current
+ * lastNodeIndex, with the configured predicates.  Replaces running the simulator once per
+ * policy (pkg/scheduler/simulator.go:286 New, :187 Run).  Every pod must be resource-only;
+ * the handle's own state is left unchanged.  out_node: [n_scen][count] node index or -1;
+ * out_counters (optional): [n_scen] final lastNodeIndex. */
+int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t first, int64_t count,
+               int32_t* out_node, uint64_t* out_counters, ksim_stats* stats);
+
 /* Commit one loaded pod to a node (Scheduler.assume / cache.AssumePod). */
 int ksim_assume(ksim_handle* h, int64_t pod, int64_t node);
 

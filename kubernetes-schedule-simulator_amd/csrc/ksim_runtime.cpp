@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "ksim_common.h"
+#include "ksim_sweep.h"
 
 extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* fit, uint32_t* reasons, int64_t* score,
@@ -24,6 +25,11 @@ extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cd
                                              int lds_rows, hipStream_t s);
 extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows);
 extern "C" size_t ksim_persistent_granule_bytes(int grid);
+extern "C" hipError_t ksim_sweep_prepare(const int64_t* ac, const int64_t* am, int64_t n, double* dac, double* dam,
+                                         double* yc, double* ym, hipStream_t st);
+extern "C" hipError_t ksim_sweep_launch(const int64_t* rc0, const int64_t* rm0, const int64_t* zc0, const int64_t* zm0,
+                                        const int32_t* c0, const ksim_pod* pods, void* fpods, const SwArgs* args,
+                                        int32_t n_scen, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st);
 extern "C" int ksim_pfast_config(int64_t n, int* grid, int* lds_rows);
 extern "C" size_t ksim_pfast_granule_bytes(void);
 extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, hipStream_t s);
@@ -66,6 +72,11 @@ struct ksim_handle {
   // the fast kernel computes in float64: every node cpu / memory quantity below 2^48 at load
   // (pods: checked per pod in fast_pre); cleared for good once a commit reaches 2^48
   bool pfast_off = false;
+  std::vector<int64_t> pod_qmax;  // largest cpu / memory quantity of each pod (sweep bound)
+  // scenario sweep: static float64 columns (once) and per-call scratch (grown on demand)
+  double *sw_dac = nullptr, *sw_dam = nullptr, *sw_yc = nullptr, *sw_ym = nullptr;
+  void* sw_scratch = nullptr;
+  size_t sw_scratch_bytes = 0;
 };
 
 static int fail(ksim_handle* h, int code, const char* fmt, ...) {
@@ -311,6 +322,13 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
     const bool fast = in_range && k1 * k2 == 1 && p.host == -1 && p.port_cnt == 0 && p.scalar_cnt == 0 &&
                       p.req_gpu == 0 && p.req_eph == 0 && !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS));
     h->fast_pre[i + 1] = h->fast_pre[i] + (fast ? 1 : 0);
+  }
+  h->pod_qmax.assign((size_t)n_pods, 0);
+  for (int64_t i = 0; i < n_pods; ++i) {
+    const ksim_pod& p = pods[i];
+    int64_t m = 0;
+    for (int64_t v : {p.req_cpu, p.req_mem, p.add_cpu, p.add_mem, p.nz_cpu, p.nz_mem}) m = std::max(m, v);
+    h->pod_qmax[i] = m;
   }
 
   if (c.collect) HIPCHK(h, hipMemsetAsync(c.out_reasons, 0, n_pods * KSIM_NREASONS * sizeof(int32_t), h->stream));
@@ -607,6 +625,118 @@ int ksim_assume(ksim_handle* h, int64_t pod, int64_t node) {
   int32_t err = 0;
   HIPCHK(h, hipMemcpy(&err, h->ctx.err, 4, hipMemcpyDeviceToHost));
   if (err & 1) return fail(h, KSIM_E_OVERFLOW, "a node's host-port slots overflowed (raise port_slots)");
+  return KSIM_OK;
+}
+
+int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t first, int64_t count, int32_t* out_node,
+               uint64_t* out_counters, ksim_stats* st) {
+  if (!h || !weights || !out_node) return fail(h, KSIM_E_INVAL, "ksim_sweep: null argument");
+  if (!h->have_pods) return fail(h, KSIM_E_STATE, "ksim_sweep: load nodes, classes and pods first");
+  if (n_scen <= 0 || first < 0 || count <= 0 || first + count > h->n_pods || count > INT32_MAX)
+    return fail(h, KSIM_E_INVAL, "ksim_sweep: bad scenario count or pod range");
+  HIPCHK(h, hipSetDevice(h->device));
+  KsimCtx& c = h->ctx;
+  const int64_t n = c.n;
+  if (n > KSIM_SWEEP_MAX_NODES)
+    return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: %lld nodes exceed the %d-node scenario layout", (long long)n,
+                KSIM_SWEEP_MAX_NODES);
+  if (h->fast_pre[first + count] - h->fast_pre[first] != count)
+    return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: every pod must be resource-only (no ports, selectors, taints, "
+                                       "nodeName, gpu / ephemeral / extended requests)");
+  std::vector<int32_t> w3((size_t)n_scen * 3);
+  for (int32_t sidx = 0; sidx < n_scen; ++sidx) {
+    const int64_t* w = weights + (size_t)sidx * KSIM_NW;
+    if (w[KSIM_W_TAINT_TOLERATION] || w[KSIM_W_NODE_AFFINITY])
+      return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: scenario %d: reduce priorities are not swept", sidx);
+    int64_t tot = 0;
+    for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED}) {
+      if (w[k] < 0 || w[k] > 6553) return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: scenario %d: weight out of range", sidx);
+      tot += w[k];
+    }
+    if (tot * 10 >= 0xFFFF) return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: scenario %d: scores exceed 16 bits", sidx);
+    w3[3 * sidx] = (int32_t)w[KSIM_W_LEAST_REQUESTED];
+    w3[3 * sidx + 1] = (int32_t)w[KSIM_W_MOST_REQUESTED];
+    w3[3 * sidx + 2] = (int32_t)w[KSIM_W_BALANCED];
+  }
+  // float64 exactness: node quantities + count x the largest pod quantity stay below 2^48
+  {
+    int64_t qmax = 0, nmax = 0;
+    for (int64_t i = first; i < first + count; ++i) qmax = std::max(qmax, h->pod_qmax[i]);
+    std::vector<int64_t> col((size_t)n);
+    for (const int64_t* d : {c.alloc_cpu, c.alloc_mem, (const int64_t*)c.req_cpu, (const int64_t*)c.req_mem,
+                             (const int64_t*)c.nz_cpu, (const int64_t*)c.nz_mem}) {
+      HIPCHK(h, hipMemcpy(col.data(), d, (size_t)n * 8, hipMemcpyDeviceToHost));
+      for (int64_t v : col) nmax = std::max(nmax, v < 0 ? INT64_MAX / 2 : v);
+    }
+    const int64_t lim = (int64_t)1 << 48;
+    if (nmax >= lim || qmax >= lim || count > lim / std::max<int64_t>(qmax, 1) || nmax + count * qmax >= lim)
+      return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: quantities may leave the exact float64 range (2^48)");
+  }
+  int rc;
+  if (!h->sw_dac) {
+    if ((rc = dev_alloc(h, &h->sw_dac, n)) || (rc = dev_alloc(h, &h->sw_dam, n)) || (rc = dev_alloc(h, &h->sw_yc, n)) ||
+        (rc = dev_alloc(h, &h->sw_ym, n)))
+      return rc;
+    hipError_t e = ksim_sweep_prepare(c.alloc_cpu, c.alloc_mem, n, h->sw_dac, h->sw_dam, h->sw_yc, h->sw_ym, h->stream);
+    if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "sweep prepare: %s", hipGetErrorString(e));
+  }
+  // scratch: [S][n] x (4 float64 + int32), pods, weights, outputs
+  const size_t S = (size_t)n_scen, N = (size_t)n, P = (size_t)count;
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  const size_t b_dyn = al(S * N * 8), b_cnt = al(S * N * 4), b_pod = al(P * sizeof(kf64::FPod)), b_w = al(S * 12),
+               b_out = al(S * P * 4), b_ctr = al(S * 8);
+  const size_t need = 4 * b_dyn + b_cnt + b_pod + b_w + b_out + b_ctr;
+  if (h->sw_scratch_bytes < need) {
+    if (h->sw_scratch) {
+      for (auto& b : h->bufs)
+        if (b.p == h->sw_scratch) b.p = nullptr;
+      (void)hipFree(h->sw_scratch);
+      h->sw_scratch = nullptr;
+      h->sw_scratch_bytes = 0;
+    }
+    char* p = nullptr;
+    if ((rc = dev_alloc(h, &p, need))) return rc;
+    h->sw_scratch = p;
+    h->sw_scratch_bytes = need;
+  }
+  char* base = (char*)h->sw_scratch;
+  SwArgs a{};
+  a.n = n; a.n_pods = (int32_t)count; a.scen0 = 0;
+  a.dac = h->sw_dac; a.dam = h->sw_dam; a.yc = h->sw_yc; a.ym = h->sw_ym;
+  a.allowed = c.allowed_pods; a.flags = c.flags;
+  a.rc = (double*)base; a.rm = (double*)(base + b_dyn); a.zc = (double*)(base + 2 * b_dyn);
+  a.zm = (double*)(base + 3 * b_dyn);
+  a.count = (int32_t*)(base + 4 * b_dyn);
+  char* q = base + 4 * b_dyn + b_cnt;
+  a.pods = (const kf64::FPod*)q;
+  int32_t* dw = (int32_t*)(q + b_pod);
+  a.w = dw;
+  a.out_node = (int32_t*)(q + b_pod + b_w);
+  a.out_counter = (uint64_t*)(q + b_pod + b_w + b_out);
+  a.preds = c.preds; a.no_prio = c.no_prio;
+  HIPCHK(h, hipMemcpy(&a.counter0, c.counter, 8, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemcpyAsync(dw, w3.data(), S * 12, hipMemcpyHostToDevice, h->stream));
+  hipError_t e = ksim_sweep_launch(c.req_cpu, c.req_mem, c.nz_cpu, c.nz_mem, c.pod_count, c.pods + first,
+                                   (void*)a.pods, &a, n_scen, h->ev0, h->ev1, h->stream);
+  if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "sweep launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipEventSynchronize(h->ev1));
+  float ms = 0.f;
+  HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+  HIPCHK(h, hipMemcpy(out_node, a.out_node, S * P * 4, hipMemcpyDeviceToHost));
+  if (out_counters) HIPCHK(h, hipMemcpy(out_counters, a.out_counter, S * 8, hipMemcpyDeviceToHost));
+  if (st) {
+    memset(st, 0, sizeof *st);
+    st->pods = (int64_t)(S * P);
+    int64_t b = 0;
+    for (size_t k = 0; k < S * P; ++k) b += out_node[k] >= 0;
+    st->scheduled = b;
+    st->node_evals = (int64_t)(S * P) * n;
+    st->device_ms = ms;
+    st->kernel_ms = ms;
+    st->kernel_launches = 1;
+    st->mode = KSIM_MODE_PERSISTENT;
+    st->blocks = n_scen;
+  }
   return KSIM_OK;
 }
 

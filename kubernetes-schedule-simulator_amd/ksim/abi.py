@@ -111,7 +111,7 @@ assert SCALAR_DTYPE.itemsize == C.sizeof(ScalarReq)
 
 EXPORTS = ["ksim_abi_version", "ksim_last_error", "ksim_create", "ksim_destroy", "ksim_load_nodes",
            "ksim_load_classes", "ksim_load_pods", "ksim_schedule", "ksim_evaluate", "ksim_assume",
-           "ksim_read_nodes", "ksim_get_counter", "ksim_set_counter", "ksim_selftest"]
+           "ksim_read_nodes", "ksim_get_counter", "ksim_set_counter", "ksim_selftest", "ksim_sweep"]
 
 
 class KsimError(RuntimeError):
@@ -151,6 +151,8 @@ def lib():
     L.ksim_get_counter.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     L.ksim_set_counter.argtypes = [C.c_void_p, C.c_uint64]
     L.ksim_selftest.restype = C.c_int
+    L.ksim_sweep.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                             C.POINTER(Stats)]
     for name in EXPORTS:
         if name not in ("ksim_destroy", "ksim_last_error", "ksim_abi_version") and getattr(L, name).restype is C.c_int:
             pass

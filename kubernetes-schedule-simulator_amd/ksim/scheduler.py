@@ -174,6 +174,27 @@ class GenericScheduler:
         self.last_stats = st
         return out, reasons, st
 
+    def sweep(self, scenarios, first=0, count=None):
+        """Capacity-planning what-if (ksim_sweep): every scenario — a prioritizer list of map
+        priorities, e.g. [("LeastRequestedPriority", 3), ("BalancedResourceAllocation", 1)] —
+        schedules pods [first, first+count) on its own copy of the current node state, from the
+        current lastNodeIndex, with this scheduler's predicates.  The scheduler's own state is
+        unchanged.  Returns (placements [n_scen][count], final counters [n_scen], stats)."""
+        n = len(self._pods)
+        count = n - first if count is None else count
+        w = np.zeros((len(scenarios), abi.NW), np.int64)
+        for k, pri in enumerate(scenarios):
+            cfg = make_config(self.predicates, pri)
+            if cfg.no_priorities != self.cfg.no_priorities:
+                raise Unsupported("a sweep scenario needs a non-empty prioritizer list like the scheduler's")
+            w[k] = list(cfg.weights)
+        out = np.zeros((len(scenarios), count), np.int32)
+        ctr = np.zeros(len(scenarios), np.uint64)
+        st = abi.Stats()
+        self.h.call("ksim_sweep", abi.vptr(w), len(scenarios), first, count, abi.vptr(out), abi.vptr(ctr), C.byref(st))
+        self.last_stats = st
+        return out, ctr, st
+
     def evaluate(self, pod):
         """Per-node (fit, reason mask, map score, reduce class) for one loaded pod (no commit)."""
         n = self.cluster.n_nodes

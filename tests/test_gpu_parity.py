@@ -296,3 +296,53 @@ def test_fast_and_general_kernels_agree(seed, monkeypatch):
         assert np.array_equal(s1[k], s2[k]), k
     ref, _, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, 4000, threads=8)
     assert np.array_equal(o1, ref) and c1 == ref_ctr
+
+
+@pytest.mark.parametrize("n_nodes,n_pods", [(1500, 1200), (20_000, 300)])
+def test_sweep_matches_c_oracle_per_scenario(n_nodes, n_pods):
+    """Scenario sweep (C5 shape): every scenario's placements and final lastNodeIndex equal the
+    C oracle run under that scenario's weights; the scheduler's own state is untouched."""
+    import cpu_ref
+    from ksim import synth
+    cl, preds, scen = synth.config_c5(n_nodes, n_pods)
+    pick = [scen[i] for i in (0, 1, 17, 255, 256, 1000, 2047, 2500, 3071, 4095)]
+    pick.append([("MostRequestedPriority", 1)])
+    pick.append([("LeastRequestedPriority", 7)])
+    g = scheduler.GenericScheduler(cl, preds, scen[0], collect_reasons=False)
+    before = g.node_state()
+    out, ctr, st = g.sweep(pick, 0, n_pods)
+    assert st.node_evals == len(pick) * n_pods * n_nodes
+    for k, pri in enumerate(pick):
+        ref, _, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, pri), 0, n_pods, threads=8)
+        assert np.array_equal(out[k], ref), pri
+        assert int(ctr[k]) == ref_ctr, pri
+    after = g.node_state()
+    for k in before:
+        assert np.array_equal(before[k], after[k]), k
+    assert g.last_node_index == 0
+
+
+def test_sweep_until_unschedulable_and_from_mid_queue():
+    """A sweep over a queue that overflows a small cluster (FitErrors, single-fit pods) started
+    after a regular ksim_schedule prefix: continues from the scheduled state and counter."""
+    import cpu_ref
+    from ksim import synth
+    n = 64
+    cpu, mem = synth.c3_nodes(n, 11)
+    pcpu, pmem = synth.c3_pods(3000, 11)
+    cl = synth.resource_cluster(["s-%03d" % i for i in range(n)], cpu, mem, np.full(n, 30, np.int32), pcpu, pmem)
+    preds = list(scheduler.DEFAULT_PREDICATES)
+    base = [("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
+    g = scheduler.GenericScheduler(cl, preds, base, collect_reasons=False)
+    g.schedule(0, 500)
+    pick = [base, [("MostRequestedPriority", 2), ("BalancedResourceAllocation", 1)], [("LeastRequestedPriority", 3)]]
+    out, ctr, _ = g.sweep(pick, 500, 2500)
+    # reference: the same 500-pod prefix under the base policy, then each scenario's policy
+    _, _, state0, ctr0 = cpu_ref.run(cl, scheduler.make_config(preds, base), 0, 500, threads=4)
+    for k, pri in enumerate(pick):
+        state = {key: v.copy() for key, v in state0.items()}
+        ref, _, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, pri), 500, 2500, threads=4, state=state,
+                                         counter=ctr0)
+        assert np.array_equal(out[k], ref), pri
+        assert int(ctr[k]) == ref_ctr
+    assert (out < 0).any()  # the cluster fills up
