@@ -28,22 +28,45 @@ BYTES_PER_NODE_EVAL = 60   # 6 x i64 + 2 x i32 + u32 flags, reso
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
+def pmc_traffic(workload, evals_per_launch):
+    """HBM bytes per launch of the dominant kernel from the committed PMC profile
+    (profiles/pmc_<workload>.json: FETCH_SIZE x2 + WRITE_SIZE per node-eval, collected with
+    tools/gpu_pmc.sh / tools/gpu_c5.sh as MI355X_MICROARCH.md prescribes), or None."""
+    try:
+        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)))
+        return round(d["hbm_bytes_per_node_eval"] * evals_per_launch / 1e9, 6)  # GB per launch
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=100)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=None, help="default 100 (c3) / 3 (c5)")
+    ap.add_argument("--warmup", type=int, default=None, help="default 3 (c3) / 1 (c5)")
     ap.add_argument("--batch", type=int, default=4096, help="pods per step")
     ap.add_argument("--nodes", type=int, default=100_000)
     ap.add_argument("--pods", type=int, default=1_000_000)
     ap.add_argument("--mode", default="auto", choices=["auto", "launch", "persistent"])
     ap.add_argument("--cpu-sample", type=int, default=3000, help="pods in the CPU-baseline prefix (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    return ap.parse_args()
+    ap.add_argument("--workload", default="c3", choices=["c3", "c5"],
+                    help="c3: the headline metric (default); c5: the 4,096-scenario policy sweep")
+    ap.add_argument("--scenarios", type=int, default=4096, help="c5: total scenarios (split across ranks)")
+    ap.add_argument("--sweep-nodes", type=int, default=20_000, help="c5: nodes per scenario")
+    ap.add_argument("--sweep-pods", type=int, default=5000, help="c5: pods scheduled in every scenario")
+    a = ap.parse_args()
+    if a.steps is None:
+        a.steps = 3 if a.workload == "c5" else 100
+    if a.warmup is None:
+        a.warmup = 1 if a.workload == "c5" else 3
+    return a
 
 
 def main():
     a = parse()
+    if a.workload == "c5":
+        return main_c5(a)
     import numpy as np
     import torch
     from ksim import abi, scheduler, synth
@@ -149,12 +172,108 @@ def main():
                        "mode": {1: "launch", 2: "persistent"}.get(mode_used, str(mode_used)), "blocks": blocks,
                        "parallelism": "scenario-replicas x%d" % world if world > 1 else "single-gpu"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": pmc_traffic("c3", n * pods_per_launch), "traffic_unit": "GB per launch (PMC)",
                          "bytes_per_node_eval": BYTES_PER_NODE_EVAL,
                          "avg_launch_us": round(avg_launch_s * 1e6, 3), "pods_per_launch": pods_per_launch},
             "cpu_baseline": cpu,
             "parity": parity,
             "pods_bound": bound,
+        }
+        print(json.dumps(line))
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+def main_c5(a):
+    """C5 (BASELINE.json configs[4]): the 4,096-scenario policy/weight sweep on a 20k-node
+    cluster, scenario-parallel across ranks (rank r takes a contiguous share of the scenarios,
+    no collective).  A step = one ksim_sweep call: every local scenario schedules the first
+    --sweep-pods pods of the queue on its own copy of the snapshot (strong scaling: the total
+    scenario count is fixed).  value = scenario-pods scheduled by all ranks per second."""
+    import numpy as np
+    import torch
+    from ksim import scheduler, synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    def barrier_sync():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    cl, preds, scen = synth.config_c5(a.sweep_nodes, a.sweep_pods)
+    scen = scen[:a.scenarios]
+    lo, hi = rank * len(scen) // world, (rank + 1) * len(scen) // world
+    mine = scen[lo:hi]
+    g = scheduler.GenericScheduler(cl, preds, scen[0], device=local, collect_reasons=False)
+    for _ in range(a.warmup):
+        g.sweep(mine, 0, a.sweep_pods)
+    barrier_sync()
+    t0 = time.perf_counter()
+    kernel_ms = 0.0
+    for _ in range(a.steps):
+        out, ctr, st = g.sweep(mine, 0, a.sweep_pods)
+        kernel_ms += st.kernel_ms
+    barrier_sync()
+    elapsed = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([elapsed], device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    n = cl.n_nodes
+    scen_pods = len(scen) * a.sweep_pods * a.steps
+    value = scen_pods / elapsed
+    avg_launch_s = kernel_ms / 1e3 / a.steps
+    evals_per_launch = len(mine) * a.sweep_pods * n
+    achieved = BYTES_PER_NODE_EVAL * evals_per_launch / avg_launch_s / 1e9
+    cpu = parity = None
+    if rank == 0 and a.cpu_sample > 0:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import cpu_ref
+        threads = max(1, min(a.cpu_threads, len(os.sched_getaffinity(0))))
+        S = min(a.cpu_sample, a.sweep_pods)
+        t1 = time.perf_counter()
+        ref, _, _, _ = cpu_ref.run(cl, scheduler.make_config(preds, mine[0]), 0, S, threads=threads)
+        cpu_s = time.perf_counter() - t1
+        cpu = {"value": round(S / cpu_s, 1), "unit": "scenario-pods/s", "cores": threads, "kind": "port",
+               "sample": "scenario 0, first %d pods (oracle/cpu_ref.c, OpenMP node-parallel), %.1f s" % (S, cpu_s),
+               "node_evals_per_s": round(S * n / cpu_s, 1)}
+        parity = {"scenario": lo, "prefix_pods": S, "match": bool(np.array_equal(ref, out[0][:S]))}
+    if rank == 0:
+        line = {
+            "metric": "scenario-pods scheduled/sec + node-evals/sec, 4,096-scenario policy sweep on 20k nodes (C5)",
+            "value": round(value, 1),
+            "unit": "scenario-pods/s",
+            "node_evals_per_s": round(value * n, 1),
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(elapsed * 1e3 / a.steps, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64 (exact integer arithmetic below 2^48)",
+            "data": "synthetic (splitmix64 seed 5, SURVEY.md \u00a78d C5)",
+            "config": {"workload": "C5: %d scenarios (wLR 1..16 x wBRA 1..16 x wMR 0..15) x %d pods on %d nodes"
+                                   % (len(scen), a.sweep_pods, n),
+                       "nodes": n, "scenarios": len(scen), "scenarios_per_rank": len(mine),
+                       "pods_per_scenario": a.sweep_pods, "parallelism": "scenario-parallel x%d" % world},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": pmc_traffic("c5", evals_per_launch), "traffic_unit": "GB per launch (PMC)",
+                         "bytes_per_node_eval": BYTES_PER_NODE_EVAL, "avg_launch_us": round(avg_launch_s * 1e6, 3),
+                         "node_evals_per_launch": evals_per_launch},
+            "cpu_baseline": cpu,
+            "parity": parity,
         }
         print(json.dumps(line))
     if dist is not None:
