@@ -39,6 +39,7 @@ extern "C" {
 #define KSIM_MAX_SCALAR 8   /* extended / hugepage resource columns */
 #define KSIM_MAX_RCLASS 16  /* reduce classes per pod (TaintToleration x NodeAffinity) */
 #define KSIM_NREASONS 24    /* failure-reason histogram slots */
+#define KSIM_MAX_RANKS 8    /* devices of one node-sharded cluster */
 
 /* ---- predicate key bits: the FitPredicate keys of predicates.go:129-138 that carry
  *      logic for supported pods.  The volume / inter-pod-affinity keys (NoDiskConflict,
@@ -258,6 +259,24 @@ int ksim_evaluate(ksim_handle* h, int64_t pod, uint8_t* out_fit, uint32_t* out_r
  * out_counters (optional): [n_scen] final lastNodeIndex. */
 int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t first, int64_t count,
                int32_t* out_node, uint64_t* out_counters, ksim_stats* stats);
+
+/* ---- Node-sharded scheduling of one cluster across devices ----
+ * Rank r of `world` (one handle per device, one process or thread each) loads the contiguous
+ * name-rank shard [node_base, node_base + n_r) of the node table and the whole pod queue.
+ * Every rank then calls ksim_schedule with the same (first, count) sequence; per pod the
+ * ranks combine their (fit count, max score, count at max) through device-initiated writes
+ * into each other's exchange buffers (xGMI), reach the same findNodesThatFit / selectHost
+ * decision (core/generic_scheduler.go:112-198) and the owning rank commits.  out_node on
+ * rank r: the global node index if rank r holds it, -1 (FitError), -2 (another rank's node).
+ * Only resource-only pods are supported in this mode (KSIM_E_UNSUPPORTED otherwise). */
+#define KSIM_IPC_HANDLE_BYTES 64
+int ksim_shard_setup(ksim_handle* h, int32_t rank, int32_t world, int64_t node_base);
+/* IPC handle of this rank's exchange buffer, to be passed to every other rank. */
+int ksim_shard_export(ksim_handle* h, uint8_t* out_handle);
+/* Map rank `peer`'s exchange buffer (another process). */
+int ksim_shard_connect(ksim_handle* h, int32_t peer, const uint8_t* peer_handle);
+/* Same, for a rank driven from this process (its handle). */
+int ksim_shard_connect_local(ksim_handle* h, int32_t peer, ksim_handle* peer_h);
 
 /* Commit one loaded pod to a node (Scheduler.assume / cache.AssumePod). */
 int ksim_assume(ksim_handle* h, int64_t pod, int64_t node);

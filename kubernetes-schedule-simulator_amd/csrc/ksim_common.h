@@ -86,6 +86,16 @@ struct KsimCtx {
   uint64_t* dbg;          // diagnostic stamp sums (KSIM_STAMPS builds only), else null
 };
 
+// Node-sharded mode (ksim_shard_*): this rank's place in the world and every rank's exchange
+// buffer as mapped on this device.
+struct KsimShard {
+  int32_t rank, world;
+  int64_t node_base;
+  uint32_t xtag_base;
+  uint64_t* xchg;
+  uint64_t* peers[KSIM_MAX_RANKS];
+};
+
 // ((a*10)/b) with Go int64 semantics (wrapping multiply, truncating divide), b > 0.
 // Quotients here are 0..10, so for a < 2^49 a correctly rounded double divide plus one
 // integer correction is exact; larger values take the native (slow) 64-bit divide.

@@ -46,8 +46,17 @@ constexpr int FIXSTRIDE = 16;   // fix granules 128 B apart
 constexpr int RING = 16;        // pod-descriptor ring slots in LDS
 constexpr int RING_FILL = 8;    // descriptors fetched per refill
 constexpr uint64_t SPIN_LIMIT_TICKS = 200000000ull;  // s_memrealtime at 100 MHz = 2 s
+constexpr int ANSLOT = 8;       // aggregate slots per rank (pod mod ANSLOT)
 
 typedef __attribute__((address_space(1))) uint64_t gu64;
+
+// cross-device exchange (fine-grained memory written by peers over xGMI)
+__device__ __forceinline__ void sys_store(uint64_t* g, uint64_t v) {
+  __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t sys_load(const uint64_t* g) {
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __device__ __forceinline__ void store_granule(uint64_t* g, uint64_t v) {
   __hip_atomic_store((gu64*)g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -130,6 +139,14 @@ struct PfArgs {
   uint32_t preds;
   int32_t no_prio, collect;
   int32_t wl, wm, wb;  // map weights (host-checked: sum x 10 < 2^27)
+  // node-sharded mode (world > 1): this rank holds global name ranks
+  // [node_base, node_base + n); per pod, workgroup 0 publishes the rank's aggregate to every
+  // rank's exchange buffer (over xGMI) and every workgroup combines the world's aggregates
+  int32_t rank, world;
+  int64_t node_base;
+  uint32_t xtag_base;                 // exchange tag of pod first - 1 (host: running pod count)
+  uint64_t* xchg;                     // this rank's aggregate slots [ANSLOT][KSIM_MAX_RANKS][4]
+  uint64_t* peers[KSIM_MAX_RANKS];    // every rank's exchange buffer as mapped here (self included)
 };
 
 namespace {
@@ -389,22 +406,60 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
         f += gfit(g[j]);
         lm = (gcnt(g[j]) && gscore(g[j]) > lm) ? gscore(g[j]) : lm;
       }
-      const int32_t F = ksimw::sum_i32(f);
-      const int32_t M0 = ksimw::max_i32(lm);
+      const int32_t Fl = ksimw::sum_i32(f);
+      const int32_t Ml = ksimw::max_i32(lm);
       int32_t bm[MAXB], tot = 0;
 #pragma unroll
       for (int j = 0; j < MAXB; ++j) {
-        bm[j] = (gcnt(g[j]) && gscore(g[j]) == M0) ? gcnt(g[j]) : 0;
+        bm[j] = (gcnt(g[j]) && gscore(g[j]) == Ml) ? gcnt(g[j]) : 0;
         tot += bm[j];
       }
       const int32_t pre = ksimw::prefix_incl_i32(tot);
-      const uint32_t C = (uint32_t)__builtin_amdgcn_readlane(pre, 63);
+      const int32_t Cl = __builtin_amdgcn_readlane(pre, 63);
+      // this rank's (F, M, C); with world > 1, the world's, and the matches on higher ranks
+      int32_t F = Fl, M0 = Ml;
+      uint32_t C = (uint32_t)Cl;
+      int64_t above_r = 0;
+      bool stop_any = ok && X >= 0 && gstop(fx);
+      if (a.world > 1 && ok) {
+        // words (tag:32 | value:32): F, stop:1 | C:31, M — tags run across calls (xtag_base)
+        const uint64_t at = (uint64_t)(uint32_t)(a.xtag_base + (uint32_t)(pod - a.first) + 1u) << 32;
+        const int aslot = (int)(pod % ANSLOT);
+        if (me == 0 && lane < a.world) {
+          uint64_t* dst = a.peers[lane] + ((int64_t)aslot * KSIM_MAX_RANKS + a.rank) * 4;
+          sys_store(dst, at | (uint32_t)Fl);
+          sys_store(dst + 1, at | (stop_any ? 0x80000000ull : 0ull) | (uint32_t)Cl);
+          sys_store(dst + 2, at | (uint32_t)Ml);
+        }
+        const bool rl = lane < a.world;
+        const uint64_t* src = a.xchg + ((int64_t)aslot * KSIM_MAX_RANKS + (rl ? lane : 0)) * 4;
+        uint64_t w0 = 0, w1 = 0, w2 = 0;
+        const uint64_t hi = 0xFFFFFFFF00000000ull;
+        for (;;) {
+          w0 = sys_load(src);
+          w1 = sys_load(src + 1);
+          w2 = sys_load(src + 2);
+          if (__all(!rl || ((w0 & hi) == at && (w1 & hi) == at && (w2 & hi) == at))) break;
+          if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_LIMIT_TICKS) { ok = false; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        const int32_t Fr = rl ? (int32_t)(uint32_t)w0 : 0, Cr = rl ? (int32_t)((uint32_t)w1 & 0x7FFFFFFFu) : 0;
+        const int32_t Mr = (rl && Cr) ? (int32_t)(uint32_t)w2 : -1;
+        F = ksimw::sum_i32(Fr);
+        M0 = ksimw::max_i32(Mr);
+        const int32_t Cm = (Cr && Mr == M0) ? Cr : 0;
+        const int32_t pr = ksimw::prefix_incl_i32(Cm);
+        C = (uint32_t)__builtin_amdgcn_readlane(pr, 63);
+        above_r = (int64_t)C - __builtin_amdgcn_readlane(pr, a.rank);  // matches on higher ranks
+        stop_any = __any(rl && ((w1 >> 31) & 1));
+      }
       const uint32_t Cs = C ? C : 1u;
       const int64_t ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)Cs) : (int64_t)((uint32_t)counter % Cs);
-      const int64_t above = (int64_t)C - pre;  // matches in workgroups of higher lanes
-      const bool hit = tot > 0 && ix >= above && ix < above + tot;
+      const int64_t ixl = ix - above_r;  // index among this rank's matches, from the top
+      const int64_t above = (int64_t)Cl - pre;  // matches in workgroups of higher lanes
+      const bool hit = Ml == M0 && tot > 0 && ixl >= above && ixl < above + tot;
       int32_t found = -1;
-      int64_t rr = ix - above;
+      int64_t rr = ixl - above;
 #pragma unroll
       for (int j = MAXB - 1; j >= 0; --j) {
         const bool here = found < 0 && rr < bm[j];
@@ -417,10 +472,11 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       const int rank = hb ? __builtin_amdgcn_readlane((int32_t)rr, src) : 0;
       int mode;
       if (!ok) mode = -1;
-      else if (X >= 0 && gstop(fx)) mode = -2;  // the previous commit left the exact range
+      else if (stop_any) mode = -2;  // the previous commit left the exact range
       else if (F == 0) mode = 0;
-      else mode = (hb && blk >= 0) ? 2 : -1;
-      if (mode == 2 && F > 1) counter += 1;  // generic_scheduler.go:192-195
+      else if (hb) mode = blk >= 0 ? 2 : -1;
+      else mode = a.world > 1 ? 3 : -1;  // 3: another rank holds the node
+      if (mode >= 2 && F > 1) counter += 1;  // generic_scheduler.go:192-195
       if (lane == 0 && mode == -1) atomicOr(a.err, ok ? 2 : 4);
       STAMP(3);
 #ifdef KSIM_STAMPS
@@ -442,7 +498,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
         }
         OSTAMP(22);
       }
-      if (mode == 0 && me == 0 && lane == 0) a.out_node[pod] = -1;
+      if ((mode == 0 || mode == 3) && me == 0 && lane == 0) a.out_node[pod] = mode == 0 ? -1 : -2;
       if (lane == 0) { s_mode[pb] = mode; s_own[pb] = jsel; }
       X = mode == 2 ? blk : -1;
       STAMP(6);
@@ -530,7 +586,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           R.zc[jsel] += (double)Pp.nz_cpu; R.zm[jsel] += (double)Pp.nz_mem;
           R.count[jsel] += 1;
           if (stopbit) atomicOr(a.err, 8);
-          a.out_node[pod] = (int32_t)(lo + jsel);
+          a.out_node[pod] = (int32_t)(a.node_base + lo + jsel);
           if (has_next) {
             R.ev[nb * chunk + jsel] = R.ev2[jsel];
             s_fix[nb][0] = jsel;
@@ -609,11 +665,12 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 static constexpr int PF_LDS_BUDGET = 150 * 1024;
 
 // Same grid rule as ksim_persistent_config (one workgroup per CU, <= 256, >= 64 rows each).
-extern "C" int ksim_pfast_config(int64_t n, int* grid, int* lds_rows) {
+extern "C" int ksim_pfast_config(int64_t n, int max_grid, int* grid, int* lds_rows) {
   int dev = 0;
   hipDeviceProp_t p;
   if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
   int g = p.multiProcessorCount;
+  if (max_grid > 0 && g > max_grid) g = max_grid;
   if (g <= 0 || n <= 0) return 0;
   if (g > MAXG) g = MAXG;
   if (n < (int64_t)g * 64) g = (int)((n + 63) / 64);
@@ -627,8 +684,14 @@ extern "C" int ksim_pfast_config(int64_t n, int* grid, int* lds_rows) {
 
 extern "C" size_t ksim_pfast_granule_bytes(void) { return (size_t)(NSLOT * MAXG + NSLOT * FIXSTRIDE) * sizeof(uint64_t); }
 
-extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, hipStream_t s) {
+extern "C" size_t ksim_shard_xchg_bytes(void) { return (size_t)ANSLOT * KSIM_MAX_RANKS * 4 * sizeof(uint64_t); }
+
+extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows,
+                                        const KsimShard* sh, hipStream_t s) {
   PfArgs a;
+  a.rank = sh->rank; a.world = sh->world; a.node_base = sh->node_base; a.xtag_base = sh->xtag_base;
+  a.xchg = sh->xchg;
+  for (int r = 0; r < KSIM_MAX_RANKS; ++r) a.peers[r] = sh->peers[r];
   a.n = c->n; a.chunk = c->chunk; a.first = c->first; a.end = c->end;
   a.alloc_cpu = c->alloc_cpu; a.alloc_mem = c->alloc_mem; a.allowed_pods = c->allowed_pods; a.flags = c->flags;
   a.req_cpu = c->req_cpu; a.req_mem = c->req_mem; a.nz_cpu = c->nz_cpu; a.nz_mem = c->nz_mem;

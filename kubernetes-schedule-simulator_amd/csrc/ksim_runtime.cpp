@@ -30,9 +30,11 @@ extern "C" hipError_t ksim_sweep_prepare(const int64_t* ac, const int64_t* am, i
 extern "C" hipError_t ksim_sweep_launch(const int64_t* rc0, const int64_t* rm0, const int64_t* zc0, const int64_t* zm0,
                                         const int32_t* c0, const ksim_pod* pods, void* fpods, const SwArgs* args,
                                         int32_t n_scen, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st);
-extern "C" int ksim_pfast_config(int64_t n, int* grid, int* lds_rows);
+extern "C" int ksim_pfast_config(int64_t n, int max_grid, int* grid, int* lds_rows);
 extern "C" size_t ksim_pfast_granule_bytes(void);
-extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, hipStream_t s);
+extern "C" size_t ksim_shard_xchg_bytes(void);
+extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows,
+                                        const KsimShard* sh, hipStream_t s);
 
 namespace {
 
@@ -77,6 +79,10 @@ struct ksim_handle {
   double *sw_dac = nullptr, *sw_dam = nullptr, *sw_yc = nullptr, *sw_ym = nullptr;
   void* sw_scratch = nullptr;
   size_t sw_scratch_bytes = 0;
+  // node-sharded mode (ksim_shard_*): world == 1 is the ordinary single-device mode
+  KsimShard shard{0, 1, 0, 0, nullptr, {}};
+  void* ipc_mapped[KSIM_MAX_RANKS] = {};  // peers' exchange buffers opened through IPC
+  int max_grid = 0;                        // workgroups per launch (0 = one per CU)
 };
 
 static int fail(ksim_handle* h, int code, const char* fmt, ...) {
@@ -165,6 +171,7 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
     ksim_destroy(h);
     return fail(nullptr, KSIM_E_DEVICE, "ksim_create: initial copies failed");
   }
+  if (const char* g = getenv("KSIM_MAX_GRID")) h->max_grid = atoi(g);
   *out = h;
   return KSIM_OK;
 }
@@ -173,6 +180,9 @@ void ksim_destroy(ksim_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  for (void*& m : h->ipc_mapped)
+    if (m) { (void)hipIpcCloseMemHandle(m); m = nullptr; }
+  if (h->shard.xchg) { (void)hipFree(h->shard.xchg); h->shard.xchg = nullptr; }
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
   if (h->graph) (void)hipGraphDestroy(h->graph);
   for (auto& b : h->bufs) (void)hipFree(b.p);
@@ -429,7 +439,7 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
   c.chunk = (c.n + grid - 1) / grid;
   HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipError_t e = ksim_launch_pfast(&c, h->granules, grid, lds_rows, h->stream);
+  hipError_t e = ksim_launch_pfast(&c, h->granules, grid, lds_rows, &h->shard, h->stream);
   if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   HIPCHK(h, hipEventSynchronize(h->ev1));
@@ -464,7 +474,7 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
   KsimCtx& c = h->ctx;
   int grid = 0, lds_rows = 0;
   if (!getenv("KSIM_NO_PFAST") && count > 0 && !h->pfast_off && h->fast_pre[first + count] - h->fast_pre[first] == count &&
-      persistent_weights_ok(c) && ksim_pfast_config(c.n, &grid, &lds_rows)) {
+      persistent_weights_ok(c) && ksim_pfast_config(c.n, h->max_grid, &grid, &lds_rows)) {
     int rc = run_pfast_mode(h, first, count, grid, lds_rows, st);
     if (rc) return rc;
     int32_t err = 0;
@@ -550,6 +560,24 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
   if (st) memset(st, 0, sizeof *st);
   if (count == 0) return KSIM_OK;
   KsimCtx& c = h->ctx;
+  if (h->shard.world > 1) {  // node-sharded: the fast persistent kernel on every rank, in lockstep
+    for (int r = 0; r < h->shard.world; ++r)
+      if (!h->shard.peers[r]) return fail(h, KSIM_E_STATE, "ksim_schedule: rank %d is not connected", r);
+    int grid = 0, lds_rows = 0;
+    if (h->fast_pre[first + count] - h->fast_pre[first] != count || h->pfast_off || !persistent_weights_ok(c) ||
+        !ksim_pfast_config(c.n, h->max_grid, &grid, &lds_rows))
+      return fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling takes resource-only pods on shards that fit the "
+                                         "on-chip layout");
+    int rc = run_pfast_mode(h, first, count, grid, lds_rows, st);
+    h->shard.xtag_base += (uint32_t)count;
+    if (rc) return rc;
+    int32_t err = 0;
+    HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
+    if (err & 8) {
+      h->pfast_off = true;
+      return fail(h, KSIM_E_UNSUPPORTED, "node-sharded run stopped: a node's quantities left the exact float64 range");
+    }
+  } else {
   int mode = h->cfg.mode;
   if (mode == KSIM_MODE_AUTO) {
     int g, l;
@@ -557,6 +585,7 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
   }
   int rc = (mode == KSIM_MODE_PERSISTENT) ? run_persistent_mode(h, first, count, st) : run_launch_mode(h, first, count, st);
   if (rc) return rc;
+  }
   int32_t err = 0;
   HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
   if (out_node) HIPCHK(h, hipMemcpy(out_node, c.out_node + first, count * sizeof(int32_t), hipMemcpyDeviceToHost));
@@ -737,6 +766,71 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
     st->mode = KSIM_MODE_PERSISTENT;
     st->blocks = n_scen;
   }
+  return KSIM_OK;
+}
+
+int ksim_shard_setup(ksim_handle* h, int32_t rank, int32_t world, int64_t node_base) {
+  if (!h) return fail(h, KSIM_E_INVAL, "ksim_shard_setup: null handle");
+  if (world < 1 || world > KSIM_MAX_RANKS || rank < 0 || rank >= world || node_base < 0)
+    return fail(h, KSIM_E_INVAL, "ksim_shard_setup: rank %d of %d out of range", rank, world);
+  if (h->shard.xchg) return fail(h, KSIM_E_STATE, "ksim_shard_setup: already set up");
+  HIPCHK(h, hipSetDevice(h->device));
+  void* p = nullptr;
+  const size_t bytes = ksim_shard_xchg_bytes();
+  // fine-grained (uncached) so peers' writes over xGMI are seen by this device's polling loads
+  hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return fail(h, KSIM_E_NOMEM, "exchange buffer: %s", hipGetErrorString(e));
+  HIPCHK(h, hipMemset(p, 0, bytes));
+  h->shard.rank = rank;
+  h->shard.world = world;
+  h->shard.node_base = node_base;
+  h->shard.xtag_base = 0;
+  h->shard.xchg = (uint64_t*)p;
+  for (auto& q : h->shard.peers) q = nullptr;
+  h->shard.peers[rank] = h->shard.xchg;
+  return KSIM_OK;
+}
+
+int ksim_shard_export(ksim_handle* h, uint8_t* out_handle) {
+  if (!h || !out_handle) return fail(h, KSIM_E_INVAL, "ksim_shard_export: null argument");
+  if (!h->shard.xchg) return fail(h, KSIM_E_STATE, "ksim_shard_export: call ksim_shard_setup first");
+  HIPCHK(h, hipSetDevice(h->device));
+  hipIpcMemHandle_t m;
+  HIPCHK(h, hipIpcGetMemHandle(&m, h->shard.xchg));
+  static_assert(sizeof(m) <= KSIM_IPC_HANDLE_BYTES, "IPC handle size");
+  memset(out_handle, 0, KSIM_IPC_HANDLE_BYTES);
+  memcpy(out_handle, &m, sizeof m);
+  return KSIM_OK;
+}
+
+int ksim_shard_connect(ksim_handle* h, int32_t peer, const uint8_t* peer_handle) {
+  if (!h || !peer_handle) return fail(h, KSIM_E_INVAL, "ksim_shard_connect: null argument");
+  if (!h->shard.xchg) return fail(h, KSIM_E_STATE, "ksim_shard_connect: call ksim_shard_setup first");
+  if (peer < 0 || peer >= h->shard.world || peer == h->shard.rank)
+    return fail(h, KSIM_E_INVAL, "ksim_shard_connect: bad peer %d", peer);
+  HIPCHK(h, hipSetDevice(h->device));
+  hipIpcMemHandle_t m;
+  memcpy(&m, peer_handle, sizeof m);
+  void* p = nullptr;
+  HIPCHK(h, hipIpcOpenMemHandle(&p, m, hipIpcMemLazyEnablePeerAccess));
+  h->ipc_mapped[peer] = p;
+  h->shard.peers[peer] = (uint64_t*)p;
+  return KSIM_OK;
+}
+
+int ksim_shard_connect_local(ksim_handle* h, int32_t peer, ksim_handle* peer_h) {
+  if (!h || !peer_h) return fail(h, KSIM_E_INVAL, "ksim_shard_connect_local: null argument");
+  if (!h->shard.xchg || !peer_h->shard.xchg) return fail(h, KSIM_E_STATE, "ksim_shard_connect_local: set up both first");
+  if (peer < 0 || peer >= h->shard.world || peer == h->shard.rank || peer_h->shard.rank != peer)
+    return fail(h, KSIM_E_INVAL, "ksim_shard_connect_local: bad peer %d", peer);
+  HIPCHK(h, hipSetDevice(h->device));
+  if (peer_h->device != h->device) {
+    hipError_t e = hipDeviceEnablePeerAccess(peer_h->device, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+      return fail(h, KSIM_E_DEVICE, "peer access to device %d: %s", peer_h->device, hipGetErrorString(e));
+    (void)hipGetLastError();
+  }
+  h->shard.peers[peer] = peer_h->shard.xchg;
   return KSIM_OK;
 }
 

@@ -111,7 +111,10 @@ assert SCALAR_DTYPE.itemsize == C.sizeof(ScalarReq)
 
 EXPORTS = ["ksim_abi_version", "ksim_last_error", "ksim_create", "ksim_destroy", "ksim_load_nodes",
            "ksim_load_classes", "ksim_load_pods", "ksim_schedule", "ksim_evaluate", "ksim_assume",
-           "ksim_read_nodes", "ksim_get_counter", "ksim_set_counter", "ksim_selftest", "ksim_sweep"]
+           "ksim_read_nodes", "ksim_get_counter", "ksim_set_counter", "ksim_selftest", "ksim_sweep",
+           "ksim_shard_setup", "ksim_shard_export", "ksim_shard_connect", "ksim_shard_connect_local"]
+IPC_HANDLE_BYTES = 64
+MAX_RANKS = 8
 
 
 class KsimError(RuntimeError):
@@ -151,6 +154,10 @@ def lib():
     L.ksim_get_counter.argtypes = [C.c_void_p, C.POINTER(C.c_uint64)]
     L.ksim_set_counter.argtypes = [C.c_void_p, C.c_uint64]
     L.ksim_selftest.restype = C.c_int
+    L.ksim_shard_setup.argtypes = [C.c_void_p, C.c_int32, C.c_int32, C.c_int64]
+    L.ksim_shard_export.argtypes = [C.c_void_p, C.c_void_p]
+    L.ksim_shard_connect.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
+    L.ksim_shard_connect_local.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     L.ksim_sweep.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
                              C.POINTER(Stats)]
     for name in EXPORTS:

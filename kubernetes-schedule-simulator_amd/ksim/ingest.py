@@ -453,6 +453,17 @@ class Cluster:
     def n_nodes(self):
         return len(self.cols["alloc_cpu"])
 
+    def shard(self, lo, hi):
+        """The name-rank range [lo, hi) of the node table with the same pods and interned
+        tables (node-sharded mode: rank r loads its contiguous shard, ksim_shard_setup)."""
+        import copy
+        sub = copy.copy(self)
+        sub.cols = {k: (np.ascontiguousarray(v[..., lo:hi]) if isinstance(v, np.ndarray) else v)
+                    for k, v in self.cols.items()}
+        sub.names = list(self.names[lo:hi]) if self.names else self.names
+        sub.index = {}
+        return sub
+
 
 def abi_port_key(ip_id, proto_id, port):
     return (int(ip_id) << 40) | (int(proto_id) << 32) | (int(port) & 0xFFFFFFFF)

@@ -249,6 +249,56 @@ class GenericScheduler:
         self.h.close()
 
 
+class ShardedScheduler(GenericScheduler):
+    """Rank `rank` of a node-sharded scheduler: loads the contiguous
+    name-rank shard [rank*n/world, (rank+1)*n/world) of `cluster` and the whole pod queue;
+    all ranks call schedule() with the same ranges.  Connect the ranks first: connect_local
+    (ranks driven from this process) or export_handle / connect (one process per device)."""
+
+    def __init__(self, cluster: Cluster, predicates, priorities, rank, world, device=0, collect_reasons=False,
+                 last_node_index=0):
+        n = cluster.n_nodes
+        self.lo, self.hi = rank * n // world, (rank + 1) * n // world
+        self.rank, self.world = rank, world
+        super().__init__(cluster.shard(self.lo, self.hi), predicates, priorities, device=device,
+                         mode=abi.MODE_PERSISTENT, collect_reasons=collect_reasons, last_node_index=last_node_index)
+        self.full_cluster = cluster
+        self.h.call("ksim_shard_setup", rank, world, self.lo)
+
+    def export_handle(self) -> bytes:
+        buf = (C.c_uint8 * abi.IPC_HANDLE_BYTES)()
+        self.h.call("ksim_shard_export", buf)
+        return bytes(buf)
+
+    def connect(self, peer, handle: bytes):
+        buf = (C.c_uint8 * abi.IPC_HANDLE_BYTES).from_buffer_copy(handle)
+        self.h.call("ksim_shard_connect", peer, buf)
+
+    def connect_local(self, peer, other: "ShardedScheduler"):
+        self.h.call("ksim_shard_connect_local", peer, other.h.h)
+
+    def connect_torch(self, dist):
+        """Exchange IPC handles with every rank of an initialised torch.distributed group."""
+        hs = [None] * self.world
+        dist.all_gather_object(hs, self.export_handle())
+        for r, hb in enumerate(hs):
+            if r != self.rank:
+                self.connect(r, hb)
+
+
+def connect_local_world(scheds):
+    """Connect the ranks of a node-sharded scheduler driven from this process."""
+    for s in scheds:
+        for t in scheds:
+            if s is not t:
+                s.connect_local(t.rank, t)
+
+
+def merge_sharded(outs):
+    """Per-rank ksim_schedule outputs (-2 = another rank's node) → global placements."""
+    return np.max(np.stack(outs), axis=0)
+
+
 def _normalize(vals, reverse):
     """NormalizeReduce over a value vector (priorities/reduce.go:29-64)."""
     vals = np.asarray(vals, np.int64)

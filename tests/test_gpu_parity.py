@@ -346,3 +346,67 @@ def test_sweep_until_unschedulable_and_from_mid_queue():
         assert np.array_equal(out[k], ref), pri
         assert int(ctr[k]) == ref_ctr
     assert (out < 0).any()  # the cluster fills up
+
+
+def _run_sharded_threads(cl, preds, prios, world, ranges):
+    """world ranks of a node-sharded scheduler on this one device, driven from threads (the
+    kernels of all ranks must be co-resident: KSIM_MAX_GRID limits each to 256/world CUs)."""
+    import threading
+    scheds = [scheduler.ShardedScheduler(cl, preds, prios, r, world) for r in range(world)]
+    scheduler.connect_local_world(scheds)
+    outs = [[] for _ in range(world)]
+    for first, count in ranges:
+        errs = []
+
+        def go(r):
+            try:
+                outs[r].append(scheds[r].schedule(first, count)[0])
+            except Exception as e:  # noqa: BLE001 — surfaced below
+                errs.append(e)
+        ts = [threading.Thread(target=go, args=(r,)) for r in range(world)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert not errs, errs
+    merged = scheduler.merge_sharded([np.concatenate(o) for o in outs])
+    return scheds, merged
+
+
+@pytest.mark.parametrize("world", [2, 3])  # co-resident kernels need a HW queue each (GPU_MAX_HW_QUEUES=4)
+def test_node_sharded_in_process_matches_c_oracle(world, monkeypatch):
+    """One cluster split into `world` contiguous name-rank shards, one persistent kernel per
+    shard exchanging per-pod aggregates through each other's exchange buffers: the merged
+    placements, every rank's counter and the per-shard node state equal the C oracle's
+    unsharded run (two calls, so the exchange tags run across calls)."""
+    import cpu_ref
+    from ksim import synth
+    monkeypatch.setenv("KSIM_MAX_GRID", str(256 // world // 2))
+    cl, p, q = synth.config_c3(40_000, 3000, seed=5)
+    scheds, merged = _run_sharded_threads(cl, p, q, world, [(0, 1700), (1700, 1300)])
+    ref, _, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, 3000, threads=8)
+    assert np.array_equal(merged, ref)
+    for s in scheds:
+        assert s.last_node_index == ref_ctr
+        st = s.node_state()
+        for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+            assert np.array_equal(st[k], ref_state[k][s.lo:s.hi]), k
+
+
+def test_node_sharded_fills_cluster_with_fit_errors(monkeypatch):
+    """Sharded run over a queue that overflows the cluster: single-fit pods (no counter
+    increment), FitErrors on every rank, uneven shard sizes."""
+    import cpu_ref
+    from ksim import synth
+    monkeypatch.setenv("KSIM_MAX_GRID", "40")
+    n = 301
+    cpu, mem = synth.c3_nodes(n, 13)
+    pcpu, pmem = synth.c3_pods(9000, 13)
+    cl = synth.resource_cluster(["f-%04d" % i for i in range(n)], cpu, mem, np.full(n, 12, np.int32), pcpu, pmem)
+    preds = list(scheduler.DEFAULT_PREDICATES)
+    prios = [("LeastRequestedPriority", 2), ("BalancedResourceAllocation", 1)]
+    scheds, merged = _run_sharded_threads(cl, preds, prios, 3, [(0, 9000)])
+    ref, _, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, prios), 0, 9000, threads=8)
+    assert np.array_equal(merged, ref)
+    assert (ref < 0).sum() > 1000
+    assert all(s.last_node_index == ref_ctr for s in scheds)
