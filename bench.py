@@ -6,9 +6,14 @@ one ksim_schedule() call over the next `--batch` pods of the queue (each pod: pr
 every node, priorities, selectHost, commit — strictly one after another), with the node
 table and pod queue already resident in HBM.
 
-N GPUs (torchrun, one process per GPU): scenario-parallel replicas — every rank runs its own
-100k-node cluster with its own policy weights (a what-if sweep), no data-path
-collective; scaling "weak".  value = pods scheduled by all ranks / max-over-ranks time.
+N GPUs (torchrun, one process per GPU), two measurements in one run:
+  * headline `value` (--shard replicas, default): scenario-parallel replicas — every rank runs
+    its own 100k-node cluster with its own policy weights (a what-if sweep), no
+    data-path collective; scaling "weak".  value = pods scheduled by all ranks / max time.
+  * `node_sharded`: ONE 100k-node cluster split into N contiguous name-rank shards, one per
+    GPU, each pod decided jointly through the per-pod exchange over xGMI (ksim_shard_*);
+    pods/s of that one cluster (strong scaling), its placements checked against the
+    single-cluster run of rank 0.  With --shard nodes this is the headline instead.
 
 The JSON line also carries the roofline of the dominant kernel (algorithmic bytes per launch
 ÷ HIP-event launch duration, against the 8 TB/s HBM peak) and a cpu_baseline: the C oracle
@@ -55,12 +60,126 @@ def parse():
     ap.add_argument("--scenarios", type=int, default=4096, help="c5: total scenarios (split across ranks)")
     ap.add_argument("--sweep-nodes", type=int, default=20_000, help="c5: nodes per scenario")
     ap.add_argument("--sweep-pods", type=int, default=5000, help="c5: pods scheduled in every scenario")
+    ap.add_argument("--shard", default="replicas", choices=["replicas", "nodes", "none"],
+                    help="N>1 headline: replicas (weak) or one node-sharded cluster (strong); "
+                         "the other one is measured as well unless 'none'")
+    ap.add_argument("--shard-steps", type=int, default=20, help="timed steps of the node-sharded measurement")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal on a 1-GPU box: every rank on device 0 (gloo), grids split so the "
+                         "ranks' persistent kernels are co-resident")
     a = ap.parse_args()
     if a.steps is None:
         a.steps = 3 if a.workload == "c5" else 100
     if a.warmup is None:
         a.warmup = 1 if a.workload == "c5" else 3
     return a
+
+
+class Dist:
+    """torchrun environment: one process per GPU over RCCL, or (--one-device) every rank on
+    device 0 over gloo, the rehearsal a 1-GPU box allows."""
+
+    def __init__(self, a):
+        import torch
+        self.torch = torch
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local = int(os.environ.get("LOCAL_RANK", "0"))
+        self.one = a.one_device
+        self.dist = None
+        if self.one:
+            self.local = 0
+            if self.world > 1:  # persistent kernels of all ranks must be co-resident on the one device
+                os.environ.setdefault("KSIM_MAX_GRID", str(max(1, 256 // self.world // 2)))
+        if self.world > 1:
+            import torch.distributed as dist
+            self.dist = dist
+            if self.one:
+                dist.init_process_group("gloo")
+            else:
+                torch.cuda.set_device(self.local)
+                dist.init_process_group("nccl")
+
+    def sync(self):
+        self.torch.cuda.synchronize()
+        if self.dist is not None:
+            self.dist.barrier()
+        self.torch.cuda.synchronize()
+
+    def allmax(self, x):
+        if self.dist is None:
+            return x
+        t = self.torch.tensor([x], dtype=self.torch.float64, device="cpu" if self.one else "cuda")
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def gather(self, obj):
+        if self.dist is None:
+            return [obj]
+        out = [None] * self.world
+        self.dist.all_gather_object(out, obj)
+        return out
+
+    def close(self):
+        if self.dist is not None:
+            self.dist.barrier()
+            self.dist.destroy_process_group()
+
+
+def node_sharded(a, D, cl, preds, prios, ref):
+    """One cluster, node-sharded over the D.world ranks: rank r holds
+    name ranks [r*n/world, (r+1)*n/world); per pod the ranks exchange (fit count, max score,
+    count at max) by device-initiated writes into each other's exchange buffers and reach the
+    same selectHost decision.  Returns the measurement dict (identical collective sequence on
+    every rank, whatever fails)."""
+    import numpy as np
+    from ksim import scheduler
+    out, err, s = np.zeros(0, np.int32), None, None
+    try:
+        s = scheduler.ShardedScheduler(cl, preds, prios, D.rank, D.world, device=D.local)
+        s.connect_torch(D.dist)
+    except Exception as e:  # noqa: BLE001 — reported in the JSON line
+        err = "setup: %s" % e
+    errs = D.gather(err)
+    if any(errs):
+        return {"error": [e for e in errs if e][0]}
+    outs, first, kms, el = [], 0, 0.0, 0.0
+    try:
+        for _ in range(a.warmup):
+            outs.append(s.schedule(first, a.batch)[0])
+            first += a.batch
+        D.sync()
+        t0 = time.perf_counter()
+        for _ in range(a.shard_steps):
+            o, _, st = s.schedule(first, a.batch)
+            outs.append(o)
+            first += a.batch
+            kms += st.kernel_ms
+        D.sync()
+        el = time.perf_counter() - t0
+        out = np.concatenate(outs)
+    except Exception as e:  # noqa: BLE001
+        err = "schedule: %s" % e
+    errs = D.gather(err)
+    el = D.allmax(el)
+    kms = D.allmax(kms)
+    allouts = D.gather(out)
+    s.close()
+    if any(errs):
+        return {"error": [e for e in errs if e][0]}
+    merged = scheduler.merge_sharded(allouts)
+    pods = a.shard_steps * a.batch
+    res = {"value": round(pods / el, 1), "unit": "pods/s", "node_evals_per_s": round(pods * cl.n_nodes / el, 1),
+           "scaling": "strong", "ranks": D.world, "nodes": cl.n_nodes, "nodes_per_rank": cl.n_nodes // D.world,
+           "steps": a.shard_steps, "pods_per_step": a.batch, "ms_per_step": round(el * 1e3 / a.shard_steps, 4),
+           "avg_launch_us": round(kms * 1e3 / a.shard_steps, 3),
+           "exchange": "device-initiated system-scope stores into every rank's fine-grained exchange buffer (IPC)"
+                       + (", all ranks on device 0 (rehearsal)" if D.one else " over xGMI")}
+    if ref is not None:
+        S = min(len(ref), len(merged))
+        res["parity"] = {"pods": S, "vs": "single-GPU run of the same cluster and queue",
+                         "match": bool(np.array_equal(merged[:S], ref[:S]))}
+    return res
 
 
 def main():
@@ -71,25 +190,15 @@ def main():
     import torch
     from ksim import abi, scheduler, synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-
-    def barrier_sync():
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
+    D = Dist(a)
+    world, rank, local, dist = D.world, D.rank, D.local, D.dist
+    barrier_sync = D.sync
 
     total_pods = (a.warmup + a.steps) * a.batch
     if total_pods > a.pods:
         raise SystemExit("warmup+steps x batch = %d exceeds the %d-pod queue" % (total_pods, a.pods))
     cl, preds, prios = synth.config_c3(a.nodes, a.pods)
+    prios0 = list(prios)  # the one cluster's policy (rank 0's replica, the node-sharded run)
     if rank > 0:  # what-if sweep: each replica scores with its own LeastRequested weight
         prios = [("LeastRequestedPriority", 1 + rank), ("BalancedResourceAllocation", 1)]
     mode = {"auto": abi.MODE_AUTO, "launch": abi.MODE_LAUNCH, "persistent": abi.MODE_PERSISTENT}[a.mode]
@@ -114,16 +223,15 @@ def main():
         launches += st.kernel_launches
         mode_used, blocks = st.mode, st.blocks
     barrier_sync()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.allmax(time.perf_counter() - t0)
     placements = np.concatenate(placements)
     bound = int((placements >= 0).sum())
 
     pods_timed = a.steps * a.batch
     value = world * pods_timed / elapsed
+    sharded = None
+    if world > 1 and a.shard != "none":
+        sharded = node_sharded(a, D, cl, preds, prios0, placements if rank == 0 else None)
     n = cl.n_nodes
     # dominant kernel: the scan (launch mode: one launch per pod) or the persistent kernel
     if mode_used == abi.MODE_LAUNCH:
@@ -180,9 +288,15 @@ def main():
             "parity": parity,
             "pods_bound": bound,
         }
+        if sharded is not None:
+            line["node_sharded"] = sharded
+            if a.shard == "nodes" and "value" in sharded:  # the one node-sharded cluster as the headline
+                line["replicas"] = {"value": line["value"], "scaling": "weak", "ms_per_step": line["ms_per_step"]}
+                line.update(value=sharded["value"], node_evals_per_s=sharded["node_evals_per_s"], scaling="strong",
+                            steps=a.shard_steps, ms_per_step=sharded["ms_per_step"])
+                line["config"].update(parallelism="node-sharded x%d" % world, global_batch=a.batch)
         print(json.dumps(line))
-    if dist is not None:
-        dist.destroy_process_group()
+    D.close()
 
 
 def main_c5(a):
@@ -195,20 +309,9 @@ def main_c5(a):
     import torch
     from ksim import scheduler, synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
-
-    def barrier_sync():
-        torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
-        torch.cuda.synchronize()
+    D = Dist(a)
+    world, rank, local = D.world, D.rank, D.local
+    barrier_sync = D.sync
 
     cl, preds, scen = synth.config_c5(a.sweep_nodes, a.sweep_pods)
     scen = scen[:a.scenarios]
@@ -224,11 +327,7 @@ def main_c5(a):
         out, ctr, st = g.sweep(mine, 0, a.sweep_pods)
         kernel_ms += st.kernel_ms
     barrier_sync()
-    elapsed = time.perf_counter() - t0
-    if dist is not None:
-        t = torch.tensor([elapsed], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.allmax(time.perf_counter() - t0)
     n = cl.n_nodes
     scen_pods = len(scen) * a.sweep_pods * a.steps
     value = scen_pods / elapsed
@@ -276,8 +375,7 @@ def main_c5(a):
             "parity": parity,
         }
         print(json.dumps(line))
-    if dist is not None:
-        dist.destroy_process_group()
+    D.close()
 
 
 if __name__ == "__main__":

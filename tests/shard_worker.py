@@ -1,0 +1,33 @@
+"""Child process of tests/test_gpu_parity.py::test_node_sharded_multi_process: one rank of a
+node-sharded scheduler in its own process (the one-process-per-GPU layout), exchanging IPC
+handles over a gloo group, writing its placements to an .npz file."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "kubernetes-schedule-simulator_amd")]
+
+
+def main():
+    rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
+    device = int(sys.argv[5]) if len(sys.argv) > 5 else 0
+    import numpy as np
+    import torch.distributed as dist
+    from ksim import scheduler, synth
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%s" % port, rank=rank, world_size=world)
+    cl, p, q = synth.config_c3(40_000, 2500, seed=9)
+    s = scheduler.ShardedScheduler(cl, p, q, rank, world, device=device)
+    s.connect_torch(dist)
+    dist.barrier()
+    o1, _, _ = s.schedule(0, 1200)
+    dist.barrier()
+    o2, _, _ = s.schedule(1200, 1300)
+    st = s.node_state()
+    np.savez(out, out=np.concatenate([o1, o2]), ctr=np.uint64(s.last_node_index), lo=s.lo, hi=s.hi,
+             **{k: st[k] for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count")})
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

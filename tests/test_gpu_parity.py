@@ -1,6 +1,8 @@
 """GPU parity: libksim.so (HIP, gfx950) against the CPU oracle and the golden vectors
 transcribed from the reference's Go tests.  Bit-exact is the bar for every integer result
 (placements, scores, reason histograms, node state, lastNodeIndex)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -410,3 +412,33 @@ def test_node_sharded_fills_cluster_with_fit_errors(monkeypatch):
     assert np.array_equal(merged, ref)
     assert (ref < 0).sum() > 1000
     assert all(s.last_node_index == ref_ctr for s in scheds)
+
+
+def test_node_sharded_multi_process(tmp_path):
+    """Two ranks in two processes (the one-process-per-device layout; here both on device 0),
+    exchange buffers shared through hipIpcGetMemHandle / hipIpcOpenMemHandle over a gloo
+    group: merged placements, counters and node state equal the C oracle's."""
+    import socket
+    import subprocess
+    import sys
+    import cpu_ref
+    from ksim import synth
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    world = 2
+    env = dict(os.environ, KSIM_MAX_GRID="64")
+    worker = os.path.join(os.path.dirname(__file__), "shard_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(port), str(tmp_path / ("r%d.npz" % r))],
+                              env=env) for r in range(world)]
+    rcs = [pr.wait(timeout=100) for pr in procs]
+    assert rcs == [0] * world
+    res = [np.load(tmp_path / ("r%d.npz" % r)) for r in range(world)]
+    cl, p, q = synth.config_c3(40_000, 2500, seed=9)
+    ref, _, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, 2500, threads=8)
+    assert np.array_equal(scheduler.merge_sharded([r["out"] for r in res]), ref)
+    for r in res:
+        assert int(r["ctr"]) == ref_ctr
+        lo, hi = int(r["lo"]), int(r["hi"])
+        for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+            assert np.array_equal(r[k], ref_state[k][lo:hi]), k
