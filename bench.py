@@ -1,6 +1,7 @@
 """Benchmark of the MI355X per-pod scheduling cycle on BASELINE.json's headline workload.
 
-Workload (BASELINE.json configs[2], SURVEY.md §8d "C3"): 100,000 nodes, 1,000,000 mixed-size
+Workload (BASELINE.json configs[2], SURVEY.md §8d "C3", the default; --workload c2 / c4 / c5
+run the other configs the same way): 100,000 nodes, 1,000,000 mixed-size
 pods, default predicates + LeastRequested(1) + BalancedResourceAllocation(1).  A "step" is
 one ksim_schedule() call over the next `--batch` pods of the queue (each pod: predicates on
 every node, priorities, selectHost, commit — strictly one after another), with the node
@@ -47,16 +48,17 @@ def pmc_traffic(workload, evals_per_launch):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="default 100 (c3) / 3 (c5)")
-    ap.add_argument("--warmup", type=int, default=None, help="default 3 (c3) / 1 (c5)")
-    ap.add_argument("--batch", type=int, default=4096, help="pods per step")
-    ap.add_argument("--nodes", type=int, default=100_000)
-    ap.add_argument("--pods", type=int, default=1_000_000)
+    ap.add_argument("--steps", type=int, default=None, help="default: c3 100, c2 9, c4 10, c5 3")
+    ap.add_argument("--warmup", type=int, default=None, help="default: c3 3, c2 2, c4 1, c5 1")
+    ap.add_argument("--batch", type=int, default=None, help="pods per step (default: c3/c2 4096, c4 512)")
+    ap.add_argument("--nodes", type=int, default=None, help="default: c3 100,000, c2 5,000, c4 1,000,000")
+    ap.add_argument("--pods", type=int, default=None, help="queue length (default: c3 1M, c2 50k, c4 as needed)")
     ap.add_argument("--mode", default="auto", choices=["auto", "launch", "persistent"])
     ap.add_argument("--cpu-sample", type=int, default=3000, help="pods in the CPU-baseline prefix (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c5"],
-                    help="c3: the headline metric (default); c5: the 4,096-scenario policy sweep")
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"],
+                    help="c3: the headline metric (default); c2: 5k heterogeneous nodes with selectors, "
+                         "ports and taints; c4: 1M nodes; c5: the 4,096-scenario policy sweep")
     ap.add_argument("--scenarios", type=int, default=4096, help="c5: total scenarios (split across ranks)")
     ap.add_argument("--sweep-nodes", type=int, default=20_000, help="c5: nodes per scenario")
     ap.add_argument("--sweep-pods", type=int, default=5000, help="c5: pods scheduled in every scenario")
@@ -68,11 +70,22 @@ def parse():
                     help="rehearsal on a 1-GPU box: every rank on device 0 (gloo), grids split so the "
                          "ranks' persistent kernels are co-resident")
     a = ap.parse_args()
-    if a.steps is None:
-        a.steps = 3 if a.workload == "c5" else 100
-    if a.warmup is None:
-        a.warmup = 1 if a.workload == "c5" else 3
+    d = WORKLOADS[a.workload]
+    for k in ("steps", "warmup", "batch", "nodes", "pods"):
+        if getattr(a, k) is None:
+            setattr(a, k, d.get(k))
+    if a.pods is None:
+        a.pods = (a.warmup + max(a.steps, a.shard_steps)) * a.batch
     return a
+
+
+# per-workload defaults; bytes = algorithmic bytes per node-eval
+WORKLOADS = {
+    "c3": dict(steps=100, warmup=3, batch=4096, nodes=100_000, pods=1_000_000, bytes=60),
+    "c2": dict(steps=9, warmup=2, batch=4096, nodes=5000, pods=50_000, bytes=68),
+    "c4": dict(steps=10, warmup=1, batch=512, nodes=1_000_000, pods=None, bytes=60),
+    "c5": dict(steps=3, warmup=1, batch=0, nodes=20_000, pods=0, bytes=60),
+}
 
 
 class Dist:
@@ -197,10 +210,23 @@ def main():
     total_pods = (a.warmup + a.steps) * a.batch
     if total_pods > a.pods:
         raise SystemExit("warmup+steps x batch = %d exceeds the %d-pod queue" % (total_pods, a.pods))
-    cl, preds, prios = synth.config_c3(a.nodes, a.pods)
+    W = WORKLOADS[a.workload]
+    if a.workload == "c3":
+        cl, preds, prios = synth.config_c3(a.nodes, a.pods)
+        desc = "C3: %d nodes, %d-pod queue, default predicates + LeastRequested(1) + BalancedResourceAllocation(1)"
+        data = "synthetic (splitmix64 seed 3, SURVEY.md §8d C3)"
+    elif a.workload == "c4":
+        cl, preds, prios = synth.config_c4(a.nodes, a.pods)
+        desc = "C4: %d nodes, %d-pod queue, default predicates + LeastRequested(1) + BalancedResourceAllocation(1)"
+        data = "synthetic (splitmix64 seed 4, SURVEY.md §8d C4)"
+    else:
+        cl, preds, prios = synth.config_c2(a.nodes, a.pods)
+        desc = ("C2: %d heterogeneous nodes (labels, taints, NotReady), %d pods with nodeSelector, host ports, "
+                "tolerations, BestEffort; DefaultProvider")
+        data = "synthetic (random.Random seed 2 objects through ingest, SURVEY.md §8d C2)"
     prios0 = list(prios)  # the one cluster's policy (rank 0's replica, the node-sharded run)
     if rank > 0:  # what-if sweep: each replica scores with its own LeastRequested weight
-        prios = [("LeastRequestedPriority", 1 + rank), ("BalancedResourceAllocation", 1)]
+        prios = [(k, w + rank) if k == "LeastRequestedPriority" else (k, w) for k, w in prios0]
     mode = {"auto": abi.MODE_AUTO, "launch": abi.MODE_LAUNCH, "persistent": abi.MODE_PERSISTENT}[a.mode]
     g = scheduler.GenericScheduler(cl, preds, prios, device=local, mode=mode, collect_reasons=False)
 
@@ -230,7 +256,7 @@ def main():
     pods_timed = a.steps * a.batch
     value = world * pods_timed / elapsed
     sharded = None
-    if world > 1 and a.shard != "none":
+    if world > 1 and a.shard != "none" and a.workload != "c2":  # sharding takes resource-only pods
         sharded = node_sharded(a, D, cl, preds, prios0, placements if rank == 0 else None)
     n = cl.n_nodes
     # dominant kernel: the scan (launch mode: one launch per pod) or the persistent kernel
@@ -240,28 +266,29 @@ def main():
     else:
         pods_per_launch = a.batch
         avg_launch_s = kernel_ms / 1e3 / max(launches, 1)
-    achieved = BYTES_PER_NODE_EVAL * n * pods_per_launch / avg_launch_s / 1e9
+    achieved = W["bytes"] * n * pods_per_launch / avg_launch_s / 1e9
 
     cpu = None
     parity = None
     if rank == 0 and a.cpu_sample > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cpu_ref
-        S = min(a.cpu_sample, len(placements))
+        S = min(a.cpu_sample, len(placements), max(50, int(3e8 // n)))  # ~10-30 s of CPU work at most
         threads = max(1, min(a.cpu_threads, len(os.sched_getaffinity(0))))
         cfg = scheduler.make_config(preds, prios)
         t1 = time.perf_counter()
         ref_out, _, _, _ = cpu_ref.run(cl, cfg, 0, S, threads=threads)
         cpu_s = time.perf_counter() - t1
         cpu = {"value": round(S / cpu_s, 1), "unit": "pods/s", "cores": threads, "kind": "port",
-               "sample": "first %d pods of the same C3 queue on the same 100k-node cluster "
-                         "(oracle/cpu_ref.c, OpenMP node-parallel like workqueue.Parallelize), %.1f s" % (S, cpu_s),
+               "sample": "first %d pods of the same %s queue on the same %d-node cluster (oracle/cpu_ref.c, "
+                         "OpenMP node-parallel like workqueue.Parallelize), %.1f s" % (S, a.workload.upper(), n, cpu_s),
                "node_evals_per_s": round(S * n / cpu_s, 1)}
         parity = {"prefix_pods": S, "match": bool(np.array_equal(ref_out, placements[:S]))}
 
     if rank == 0:
         line = {
-            "metric": "pods scheduled/sec + node-evals/sec at 100k nodes, 1/2/4/8 MI355X",
+            "metric": ("pods scheduled/sec + node-evals/sec at 100k nodes, 1/2/4/8 MI355X" if a.workload == "c3" else
+                       "pods scheduled/sec + node-evals/sec, %s (%d nodes)" % (a.workload.upper(), n)),
             "value": round(value, 1),
             "unit": "pods/s",
             "node_evals_per_s": round(value * n, 1),
@@ -273,16 +300,16 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "int64",
-            "data": "synthetic (splitmix64 seed 3, SURVEY.md §8d C3)",
-            "config": {"workload": "C3: %d nodes, %d-pod queue, default predicates + LeastRequested(1) + "
-                                   "BalancedResourceAllocation(1)" % (n, a.pods),
+            "data": data,
+            "config": {"workload": desc % (n, a.pods),
                        "nodes": n, "pods_per_step": a.batch, "global_batch": a.batch * world,
                        "mode": {1: "launch", 2: "persistent"}.get(mode_used, str(mode_used)), "blocks": blocks,
                        "parallelism": "scenario-replicas x%d" % world if world > 1 else "single-gpu"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic("c3", n * pods_per_launch), "traffic_unit": "GB per launch (PMC)",
-                         "bytes_per_node_eval": BYTES_PER_NODE_EVAL,
+                         "traffic": pmc_traffic(a.workload + ("" if mode_used == abi.MODE_PERSISTENT else "_launch"),
+                                                n * pods_per_launch),
+                         "traffic_unit": "GB per launch (PMC)", "bytes_per_node_eval": W["bytes"],
                          "avg_launch_us": round(avg_launch_s * 1e6, 3), "pods_per_launch": pods_per_launch},
             "cpu_baseline": cpu,
             "parity": parity,

@@ -122,6 +122,59 @@ def config_c1(n_nodes=1500, n_a=48_010, n_b=10):
     return cl, p, q
 
 
+def c2_objects(n_nodes=5000, n_pods=50_000, seed=2):
+    """C2 (BASELINE.json configs[1]) as Kubernetes-shaped objects: heterogeneous
+    nodes with labels, NoSchedule / PreferNoSchedule taints and a few NotReady / unschedulable
+    ones; pods with nodeSelector, host ports, tolerations and some BestEffort.  Returns
+    (nodes, pods) with pods in SCHEDULING order."""
+    import random
+    rng = random.Random(seed)
+    nodes = []
+    for i in range(n_nodes):
+        node = {"metadata": {"name": "c2-node-%d" % i,  # lexical != numeric order
+                             "labels": {"tier": rng.choice("abc"), "disk": rng.choice(["ssd", "hdd"])}},
+                "spec": {},
+                "status": {"allocatable": {"cpu": str(rng.choice([8, 16, 32, 64])),
+                                           "memory": "%dGi" % rng.choice([32, 64, 128, 256]), "pods": "110"},
+                           "conditions": [{"type": "Ready", "status": "True"}]}}
+        r = rng.random()
+        if r < 0.10:
+            node["spec"]["taints"] = [{"key": "dedicated", "value": "gpu", "effect": "NoSchedule"}]
+        elif r < 0.20:
+            node["spec"]["taints"] = [{"key": "spot", "value": "true", "effect": "PreferNoSchedule"}]
+        r = rng.random()
+        if r < 0.01:
+            node["status"]["conditions"][0]["status"] = "False"
+        elif r < 0.02:
+            node["spec"]["unschedulable"] = True
+        nodes.append(node)
+    ports = [8080, 9090] + list(range(10250, 10260))
+    pods = []
+    for k in range(n_pods):
+        ctr = {}
+        if rng.random() >= 0.05:  # 5% BestEffort: no requests at all
+            ctr["resources"] = {"requests": {"cpu": rng.choice(["100m", "250m", "500m", "1", "2"]),
+                                             "memory": rng.choice(["128Mi", "256Mi", "512Mi", "1Gi", "2Gi"])}}
+        spec = {"containers": [ctr]}
+        if rng.random() < 0.30:
+            spec["nodeSelector"] = {"tier": rng.choice("abc")}
+        if rng.random() < 0.20:
+            ctr["ports"] = [{"containerPort": 80, "hostPort": rng.choice(ports), "protocol": "TCP"}]
+        if rng.random() < 0.15:
+            spec["tolerations"] = [{"key": "dedicated", "operator": "Equal", "value": "gpu", "effect": "NoSchedule"}]
+        pods.append({"metadata": {"name": "c2-pod-%d" % k, "namespace": "default"}, "spec": spec})
+    return nodes, pods
+
+
+def config_c2(n_nodes=5000, n_pods=50_000, seed=2):
+    """C2 through the object path (ingest.Cluster.from_objects): (cluster, predicates,
+    priorities) of the DefaultProvider."""
+    nodes, pods = c2_objects(n_nodes, n_pods, seed)
+    cl = Cluster.from_objects(nodes, (), pods)
+    p, q = scheduler.provider("DefaultProvider")
+    return cl, p, q
+
+
 def c5_scenarios():
     """4,096 (wLR, wBRA, wMR) policy points; wMR = 0 means MostRequested absent."""
     out = []

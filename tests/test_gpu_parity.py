@@ -182,6 +182,51 @@ def test_c1_full_matches_c_oracle(mode):
 
 
 @pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("n_nodes", [5000, 900])  # C2 as specified; shrunk so it overflows (FitErrors)
+def test_c2_matches_c_oracle(n_nodes, mode):
+    """C2 (BASELINE.json configs[1]): heterogeneous nodes, 50,000 pods with nodeSelector, host
+    ports, taints / tolerations and BestEffort pods, DefaultProvider, through the object
+    ingest path — placements, reason histograms, counter and node state (ports included)
+    equal the C oracle's."""
+    import cpu_ref
+    from ksim import synth
+    nodes, pods = synth.c2_objects(n_nodes, 50_000)
+    cl = ingest.Cluster.from_objects(nodes, (), pods)
+    p, q = scheduler.provider("DefaultProvider")
+    g = scheduler.GenericScheduler(cl, p, q, mode=mode)
+    out, reasons, _ = g.schedule()
+    ref, ref_reasons, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), threads=8)
+    assert np.array_equal(out, ref)
+    failed = out < 0
+    assert np.array_equal(reasons[failed], ref_reasons[failed])
+    assert g.last_node_index == ref_ctr
+    s = g.node_state()
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count", "port_count"):
+        assert np.array_equal(s[k], ref_state[k]), k
+    # port slots hold a set: compare per node as sets
+    assert all(set(s["ports"][:, i]) == set(ref_state["ports"][:, i]) for i in range(0, cl.n_nodes, 7))
+    assert (failed.sum() > 1000) == (n_nodes < 1000)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_c4_million_nodes_prefix_matches_c_oracle(mode):
+    """C4 scale on one device (BASELINE.json configs[3]: 1M nodes; the table no longer fits
+    on chip, so AUTO takes the HBM-streaming launch mode): the first 400 pods against the C
+    oracle."""
+    import cpu_ref
+    from ksim import synth
+    cl, p, q = synth.config_c4(1_000_000, 2000)
+    g = scheduler.GenericScheduler(cl, p, q, mode=mode, collect_reasons=False)
+    out, _, st = g.schedule(0, 400)
+    ref, _, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, 400, threads=8)
+    assert np.array_equal(out, ref)
+    assert g.last_node_index == ref_ctr
+    s = g.node_state()
+    for k in ("req_cpu", "req_mem", "pod_count"):
+        assert np.array_equal(s[k], ref_state[k]), k
+
+
+@pytest.mark.parametrize("mode", MODES)
 def test_c3_prefix_matches_c_oracle(mode):
     """100k-node C3 cluster: the first 3,000 pods against the C oracle, then size-independent
     invariants over 60,000 pods (every pod bound, per-node sums conserved)."""
