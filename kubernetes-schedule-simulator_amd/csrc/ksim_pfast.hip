@@ -27,6 +27,8 @@
 //    post-commit one with scalar arithmetic, publishes, and only then commits the row;
 //  * one prefix scan per decision: counts at the maximum give C (= its total) and the
 //    workgroup holding the ix-th match from the top (core/generic_scheduler.go:183-198).
+#include <algorithm>
+
 #include "ksim_f64.h"
 #include "ksim_fast.h"
 #include "ksim_wave.h"
@@ -71,16 +73,17 @@ __device__ __forceinline__ uint64_t* spec_at(uint64_t* gr, int slot, int b) {
 }
 __device__ __forceinline__ uint64_t* fix_at(uint64_t* gr, int slot) { return gr + NSLOT * MAXG + slot * FIXSTRIDE; }
 
-// granule: tag:8 | stop:1 | fit:11 | count:12 | score:32 (-1 = no fit node); stop (correction
-// granules only): the committed node left the exact float64 range, end the call before this pod
+// granule: tag:8 | stop:1 | fit:13 | count:13 | score:29 (two's complement, -1 = no fit node;
+// scores < 2^27, host-checked); stop (correction granules only): the committed node left the
+// exact float64 range, end the call before this pod.  A workgroup owns < 8192 rows.
 constexpr double EXACT_LIM = 281474976710656.0;  // 2^48
 __device__ __forceinline__ uint32_t gtag(uint64_t v) { return (uint32_t)(v >> 56); }
 __device__ __forceinline__ bool gstop(uint64_t v) { return (v >> 55) & 1; }
-__device__ __forceinline__ int32_t gfit(uint64_t v) { return (int32_t)((v >> 44) & 0x7FF); }
-__device__ __forceinline__ int32_t gcnt(uint64_t v) { return (int32_t)((v >> 32) & 0xFFF); }
-__device__ __forceinline__ int32_t gscore(uint64_t v) { return (int32_t)(uint32_t)v; }
+__device__ __forceinline__ int32_t gfit(uint64_t v) { return (int32_t)((v >> 42) & 0x1FFF); }
+__device__ __forceinline__ int32_t gcnt(uint64_t v) { return (int32_t)((v >> 29) & 0x1FFF); }
+__device__ __forceinline__ int32_t gscore(uint64_t v) { return ((int32_t)((uint32_t)v << 3)) >> 3; }
 __device__ __forceinline__ uint64_t gpack(uint64_t tag, int32_t f, int32_t n, int32_t m) {
-  return (tag << 56) | ((uint64_t)(uint32_t)f << 44) | ((uint64_t)(uint32_t)n << 32) | (uint64_t)(uint32_t)m;
+  return (tag << 56) | ((uint64_t)(uint32_t)f << 42) | ((uint64_t)(uint32_t)n << 29) | ((uint64_t)(uint32_t)m & 0x1FFFFFFFull);
 }
 
 // Workgroup barrier ordering LDS only: __syncthreads' fence would also drain this wave's
@@ -147,6 +150,9 @@ struct PfArgs {
   uint32_t xtag_base;                 // exchange tag of pod first - 1 (host: running pod count)
   uint64_t* xchg;                     // this rank's aggregate slots [ANSLOT][KSIM_MAX_RANKS][4]
   uint64_t* peers[KSIM_MAX_RANKS];    // every rank's exchange buffer as mapped here (self included)
+  // streaming form (tables beyond the LDS budget): float64 image of the table in HBM,
+  // [6][n] = alloc cpu, alloc mem, requested cpu, mem, non-zero cpu, mem
+  double* mirror;
 };
 
 namespace {
@@ -158,14 +164,34 @@ struct FRows {  // LDS image of the owned rows (SoA)
   int32_t* ev;    // [2][chunk]: evaluation of pod p (parity p & 1), -1 = does not fit
   int32_t* ev2;   // [chunk]: evaluation of pod p+1 against row + pod p
   uint32_t* rm2;  // [chunk]: ... its reason mask
+  uint32_t* rma;  // STREAM: [2][chunk] reason mask of ev (registers in the LDS form)
 };
 
 constexpr int LDS_ROW_BYTES = 8 * 8 + 8 * 4;  // 96: 8 float64 + allowed, count, flags, ev[2], ev2, rm2, top_list
+constexpr int LDS_ROW_BYTES_STREAM = 7 * 4;   // ev[2], ev2, rm2, top_list, rma[2] (rows stream from HBM)
 
 extern __shared__ __attribute__((aligned(16))) char kf_smem[];
 
-__device__ __forceinline__ FRows carve(int rows) {
+// STREAM: the rows are the workgroup's slice of the HBM float64 image (+ the int32 columns
+// themselves); only the per-row evaluations live in LDS.
+template <bool STREAM>
+__device__ __forceinline__ FRows carve(int rows, const PfArgs& a, int64_t lo) {
   FRows r;
+  if (STREAM) {
+    double* m = a.mirror + lo;
+    const int64_t n = a.n;
+    r.ac = m; r.am = m + n; r.rc = m + 2 * n; r.rm = m + 3 * n;
+    r.zc = m + 4 * n; r.zm = m + 5 * n; r.yc = nullptr; r.ym = nullptr;
+    r.allowed = const_cast<int32_t*>(a.allowed_pods) + lo;
+    r.count = a.pod_count + lo;
+    r.fl = const_cast<uint32_t*>(a.flags) + lo;
+    int32_t* q = reinterpret_cast<int32_t*>(kf_smem);
+    r.ev = q;
+    r.ev2 = q + 2 * rows;
+    r.rm2 = reinterpret_cast<uint32_t*>(q + 3 * rows);
+    r.rma = r.rm2 + 2 * rows;  // after top_list
+    return r;
+  }
   double* d = reinterpret_cast<double*>(kf_smem);
   r.ac = d; r.am = d + rows; r.rc = d + 2 * rows; r.rm = d + 3 * rows;
   r.zc = d + 4 * rows; r.zm = d + 5 * rows; r.yc = d + 6 * rows; r.ym = d + 7 * rows;
@@ -178,10 +204,18 @@ __device__ __forceinline__ FRows carve(int rows) {
   return r;
 }
 
+// STREAM: y = RN(1/alloc) is recomputed (IEEE divide) instead of read, so a row costs exactly
+// the 60 algorithmic bytes: 6 x 8 (alloc, requested, non-zero requested cpu / mem) + 3 x 4.
+template <bool STREAM>
 __device__ __forceinline__ FRow load_frow(const FRows& R, int32_t j) {
   FRow r;
   r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j]; r.rm = R.rm[j]; r.zc = R.zc[j]; r.zm = R.zm[j];
-  r.yc = R.yc[j]; r.ym = R.ym[j];
+  if (STREAM) {
+    r.yc = r.ac != 0.0 ? 1.0 / r.ac : 0.0;
+    r.ym = r.am != 0.0 ? 1.0 / r.am : 0.0;
+  } else {
+    r.yc = R.yc[j]; r.ym = R.ym[j];
+  }
   r.allowed = R.allowed[j]; r.count = R.count[j]; r.fl = R.fl[j];
   return r;
 }
@@ -193,7 +227,7 @@ struct Top2 {
 
 }  // namespace
 
-template <int NPT>
+template <int NPT, bool STREAM>
 __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   __shared__ int32_t s_wst[2][RW][5];         // per row wave: fit, m1, c1, m2, c2 (by pod parity)
   __shared__ uint64_t s_bm[2][NPT][RW];       // per 64-row segment: rows at the wave maximum
@@ -215,14 +249,14 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   const int64_t lo = (int64_t)me * chunk;
   const int64_t hi = (lo + chunk < a.n) ? lo + chunk : a.n;
   const int32_t nrows = (int32_t)(hi - lo);
-  const FRows R = carve((int)chunk);
+  const FRows R = carve<STREAM>((int)chunk, a, lo);
   int32_t* const top_list = reinterpret_cast<int32_t*>(R.rm2 + chunk);  // [chunk]: rows at the workgroup maximum, from the top
   const uint32_t preds = a.preds;
   const bool no_prio = a.no_prio != 0;
   const EvCfg EC = make_evcfg(preds, no_prio, a.wl, a.wm, a.wb);
   uint64_t* const granules = a.granules;
 
-  for (int32_t j = tid; j < nrows; j += BS) {  // stage the owned rows into LDS
+  for (int32_t j = tid; j < (STREAM ? 0 : nrows); j += BS) {  // stage the owned rows into LDS
     const int64_t i = lo + j;
     const double ac = (double)a.alloc_cpu[i], am = (double)a.alloc_mem[i];
     R.ac[j] = ac; R.am[j] = am;
@@ -332,7 +366,9 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   };
 
   // ---- prologue: evaluations and statistics of the first pod ----
-  uint32_t A_rm[NPT], B_rm[NPT];
+  // reason masks of the evaluations of pod p (A) and p + 1 (B): registers, or (STREAM, up to
+  // 9 rows per lane) R.rma in LDS to leave the registers to the row loads
+  uint32_t A_rm[STREAM ? 1 : NPT], B_rm[STREAM ? 1 : NPT];
   if (wv > 0) {
     const FPod P0 = load_fpod(s_pod[a.first % RING]);
     int32_t e[NPT];
@@ -341,9 +377,11 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
     for (int k = 0; k < NPT; ++k) {
       const int32_t j = k * RT + rt;
       e[k] = -1;
-      A_rm[k] = 0;
+      uint32_t& am = A_rm[STREAM ? 0 : k];
+      am = 0;
       if (j < nrows) {
-        e[k] = feval(EC, P0, load_frow(R, j), A_rm[k]);
+        e[k] = feval(EC, P0, load_frow<STREAM>(R, j), am);
+        if (STREAM) R.rma[(a.first & 1) * chunk + j] = am;
         ev[j] = e[k];
       }
     }
@@ -528,11 +566,13 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       for (int k = 0; k < NPT; ++k) {
         const int32_t j = k * RT + rt;
         e[k] = -1;
-        B_rm[k] = 0;
+        uint32_t& bm = B_rm[STREAM ? 0 : k];
+        bm = 0;
         if (j < nrows) {
-          const FRow r = load_frow(R, j);
+          const FRow r = load_frow<STREAM>(R, j);
           uint32_t m2;
-          e[k] = feval(EC, Q, r, B_rm[k]);
+          e[k] = feval(EC, Q, r, bm);
+          if (STREAM) R.rma[nb * chunk + j] = bm;
           const int32_t e2 = feval(EC, Q, plus(r, P), m2);
           evn[j] = e[k];
           R.ev2[j] = e2;
@@ -596,7 +636,9 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           }
         }
       }
-      lds_barrier();  // uniform (own is workgroup-wide): row waves see the commit
+      // uniform (own is workgroup-wide): row waves see the commit — in LDS, or (STREAM) the
+      // global row, for which the workgroup-scope release waits for the stores to complete
+      if (STREAM) __syncthreads(); else lds_barrier();
       if (wv == 0 && has_next) {
         // off the critical path: the corrected wave's statistics and bitmasks
         const int w = 1 + (jsel % RT) / 64;
@@ -624,7 +666,8 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
         const uint32_t fmk = (uint32_t)s_fix[pb][1];
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
-          const uint32_t rm = (k * RT + rt == fr) ? fmk : A_rm[k];
+          const int32_t j = k * RT + rt;
+          const uint32_t rm = (j == fr) ? fmk : !STREAM ? A_rm[STREAM ? 0 : k] : (j < nrows ? R.rma[pb * chunk + j] : 0u);
           for (int r = 0; r < KSIM_NREASONS; ++r) {
             const int32_t n = __popcll(__ballot((rm >> r) & 1u));
             if (lane == 0 && n) atomicAdd(&s_hist[r], n);
@@ -637,7 +680,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
     STAMP(4);
     if (wv > 0) {
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) A_rm[k] = B_rm[k];
+      for (int k = 0; k < (STREAM ? 0 : NPT); ++k) A_rm[k] = B_rm[k];
     }
   }
 
@@ -665,7 +708,10 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 static constexpr int PF_LDS_BUDGET = 150 * 1024;
 
 // Same grid rule as ksim_persistent_config (one workgroup per CU, <= 256, >= 64 rows each).
-extern "C" int ksim_pfast_config(int64_t n, int max_grid, int* grid, int* lds_rows) {
+// stream = 0: the rows live in LDS (up to ~400k nodes per device); stream = 1: the rows
+// stream from the HBM float64 image every pod and only the evaluations stay in LDS (up to
+// 9 rows per row thread: ~1M nodes per device).
+extern "C" int ksim_pfast_config(int64_t n, int max_grid, int stream, int* grid, int* lds_rows) {
   int dev = 0;
   hipDeviceProp_t p;
   if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&p, dev) != hipSuccess) return 0;
@@ -676,7 +722,11 @@ extern "C" int ksim_pfast_config(int64_t n, int max_grid, int* grid, int* lds_ro
   if (n < (int64_t)g * 64) g = (int)((n + 63) / 64);
   if (g < 1) g = 1;
   const int64_t chunk = (n + g - 1) / g;
-  if (chunk * LDS_ROW_BYTES > PF_LDS_BUDGET || chunk > 4 * RT || chunk > 2047) return 0;
+  if (stream) {
+    if (chunk * LDS_ROW_BYTES_STREAM > PF_LDS_BUDGET || chunk > 9 * RT) return 0;
+  } else if (chunk * LDS_ROW_BYTES > PF_LDS_BUDGET || chunk > 4 * RT) {
+    return 0;
+  }
   *grid = g;
   *lds_rows = (int)chunk;
   return 1;
@@ -686,7 +736,32 @@ extern "C" size_t ksim_pfast_granule_bytes(void) { return (size_t)(NSLOT * MAXG 
 
 extern "C" size_t ksim_shard_xchg_bytes(void) { return (size_t)ANSLOT * KSIM_MAX_RANKS * 4 * sizeof(uint64_t); }
 
-extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows,
+// float64 image of the node table for the streaming form: one pass over the int64 columns
+// (48 B read, 48 B written per node) before each streaming call.
+__global__ __launch_bounds__(256) void ksim_pstream_prepare_kernel(const int64_t* __restrict__ ac, const int64_t* __restrict__ am,
+                                                                    const int64_t* __restrict__ rc, const int64_t* __restrict__ rm,
+                                                                    const int64_t* __restrict__ zc, const int64_t* __restrict__ zm,
+                                                                    int64_t n, double* __restrict__ m) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double dac = (double)ac[i], dam = (double)am[i];
+    m[i] = dac;
+    m[n + i] = dam;
+    m[2 * n + i] = (double)rc[i];
+    m[3 * n + i] = (double)rm[i];
+    m[4 * n + i] = (double)zc[i];
+    m[5 * n + i] = (double)zm[i];
+  }
+}
+
+extern "C" hipError_t ksim_pstream_prepare(const KsimCtx* c, double* mirror, hipStream_t s) {
+  const int pg = (int)std::min<int64_t>((c->n + 255) / 256, 4096);
+  hipLaunchKernelGGL(ksim_pstream_prepare_kernel, dim3(pg), dim3(256), 0, s, c->alloc_cpu, c->alloc_mem,
+                     (const int64_t*)c->req_cpu, (const int64_t*)c->req_mem, (const int64_t*)c->nz_cpu,
+                     (const int64_t*)c->nz_mem, c->n, mirror);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, double* mirror,
                                         const KsimShard* sh, hipStream_t s) {
   PfArgs a;
   a.rank = sh->rank; a.world = sh->world; a.node_base = sh->node_base; a.xtag_base = sh->xtag_base;
@@ -700,9 +775,18 @@ extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, in
   a.preds = c->preds; a.no_prio = c->no_prio; a.collect = c->collect;
   a.wl = (int32_t)c->w[KSIM_W_LEAST_REQUESTED]; a.wm = (int32_t)c->w[KSIM_W_MOST_REQUESTED];
   a.wb = (int32_t)c->w[KSIM_W_BALANCED];
+  a.mirror = mirror;
+  if (mirror) {  // streaming form (image prepared by ksim_pstream_prepare on the same stream)
+    const size_t lds = (size_t)lds_rows * LDS_ROW_BYTES_STREAM;
+    if (lds_rows <= RT) hipLaunchKernelGGL((ksim_pfast_kernel<1, true>), dim3(grid), dim3(BS), lds, s, a);
+    else if (lds_rows <= 2 * RT) hipLaunchKernelGGL((ksim_pfast_kernel<2, true>), dim3(grid), dim3(BS), lds, s, a);
+    else if (lds_rows <= 4 * RT) hipLaunchKernelGGL((ksim_pfast_kernel<4, true>), dim3(grid), dim3(BS), lds, s, a);
+    else hipLaunchKernelGGL((ksim_pfast_kernel<9, true>), dim3(grid), dim3(BS), lds, s, a);
+    return hipGetLastError();
+  }
   const size_t lds = (size_t)lds_rows * LDS_ROW_BYTES;
-  if (lds_rows <= RT) hipLaunchKernelGGL((ksim_pfast_kernel<1>), dim3(grid), dim3(BS), lds, s, a);
-  else if (lds_rows <= 2 * RT) hipLaunchKernelGGL((ksim_pfast_kernel<2>), dim3(grid), dim3(BS), lds, s, a);
-  else hipLaunchKernelGGL((ksim_pfast_kernel<4>), dim3(grid), dim3(BS), lds, s, a);
+  if (lds_rows <= RT) hipLaunchKernelGGL((ksim_pfast_kernel<1, false>), dim3(grid), dim3(BS), lds, s, a);
+  else if (lds_rows <= 2 * RT) hipLaunchKernelGGL((ksim_pfast_kernel<2, false>), dim3(grid), dim3(BS), lds, s, a);
+  else hipLaunchKernelGGL((ksim_pfast_kernel<4, false>), dim3(grid), dim3(BS), lds, s, a);
   return hipGetLastError();
 }

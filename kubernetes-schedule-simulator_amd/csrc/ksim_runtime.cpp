@@ -30,10 +30,11 @@ extern "C" hipError_t ksim_sweep_prepare(const int64_t* ac, const int64_t* am, i
 extern "C" hipError_t ksim_sweep_launch(const int64_t* rc0, const int64_t* rm0, const int64_t* zc0, const int64_t* zm0,
                                         const int32_t* c0, const ksim_pod* pods, void* fpods, const SwArgs* args,
                                         int32_t n_scen, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st);
-extern "C" int ksim_pfast_config(int64_t n, int max_grid, int* grid, int* lds_rows);
+extern "C" int ksim_pfast_config(int64_t n, int max_grid, int stream, int* grid, int* lds_rows);
+extern "C" hipError_t ksim_pstream_prepare(const KsimCtx* c, double* mirror, hipStream_t s);
 extern "C" size_t ksim_pfast_granule_bytes(void);
 extern "C" size_t ksim_shard_xchg_bytes(void);
-extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows,
+extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, double* mirror,
                                         const KsimShard* sh, hipStream_t s);
 
 namespace {
@@ -83,6 +84,7 @@ struct ksim_handle {
   KsimShard shard{0, 1, 0, 0, nullptr, {}};
   void* ipc_mapped[KSIM_MAX_RANKS] = {};  // peers' exchange buffers opened through IPC
   int max_grid = 0;                        // workgroups per launch (0 = one per CU)
+  double* mirror = nullptr;                // streaming fast kernel: float64 image [6][n]
 };
 
 static int fail(ksim_handle* h, int code, const char* fmt, ...) {
@@ -425,9 +427,31 @@ static bool persistent_weights_ok(const KsimCtx& c) {
   return s < ((int64_t)1 << 27);
 }
 
+// Form of the specialised kernel (ksim_pfast.hip) for [first, first+count): 0 = not
+// applicable (a pod is not resource-only, weights or quantities out of its range), 1 = rows in
+// LDS, 2 = rows streamed from HBM (tables beyond the LDS budget, KSIM_FORCE_STREAM for tests).
+static int pfast_form(ksim_handle* h, int64_t first, int64_t count, int* grid, int* lds_rows) {
+  const KsimCtx& c = h->ctx;
+  if (getenv("KSIM_NO_PFAST") || count <= 0 || h->pfast_off || h->fast_pre[first + count] - h->fast_pre[first] != count ||
+      !persistent_weights_ok(c))
+    return 0;
+  if (!getenv("KSIM_FORCE_STREAM") && ksim_pfast_config(c.n, h->max_grid, 0, grid, lds_rows)) return 1;
+  if (ksim_pfast_config(c.n, h->max_grid, 1, grid, lds_rows)) return 2;
+  return 0;
+}
+
 // All pods of [first, first+count) resource-only: the specialised kernel (ksim_pfast.hip).
-static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid, int lds_rows, ksim_stats* st) {
+static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid, int lds_rows, bool stream,
+                          ksim_stats* st) {
   KsimCtx& c = h->ctx;
+  if (stream) {
+    if (!h->mirror) {
+      int rc = dev_alloc(h, &h->mirror, (size_t)6 * c.n);
+      if (rc) return rc;
+    }
+    hipError_t e = ksim_pstream_prepare(&c, h->mirror, h->stream);
+    if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "stream prepare: %s", hipGetErrorString(e));
+  }
   const size_t gb = ksim_pfast_granule_bytes();
   if (h->gran_bytes < gb) {
     int rc = dev_alloc(h, &h->granules, gb / sizeof(uint64_t));
@@ -439,7 +463,7 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
   c.chunk = (c.n + grid - 1) / grid;
   HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipError_t e = ksim_launch_pfast(&c, h->granules, grid, lds_rows, &h->shard, h->stream);
+  hipError_t e = ksim_launch_pfast(&c, h->granules, grid, lds_rows, stream ? h->mirror : nullptr, &h->shard, h->stream);
   if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   HIPCHK(h, hipEventSynchronize(h->ev1));
@@ -473,9 +497,8 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
 static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   KsimCtx& c = h->ctx;
   int grid = 0, lds_rows = 0;
-  if (!getenv("KSIM_NO_PFAST") && count > 0 && !h->pfast_off && h->fast_pre[first + count] - h->fast_pre[first] == count &&
-      persistent_weights_ok(c) && ksim_pfast_config(c.n, h->max_grid, &grid, &lds_rows)) {
-    int rc = run_pfast_mode(h, first, count, grid, lds_rows, st);
+  if (const int form = pfast_form(h, first, count, &grid, &lds_rows)) {
+    int rc = run_pfast_mode(h, first, count, grid, lds_rows, form == 2, st);
     if (rc) return rc;
     int32_t err = 0;
     HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
@@ -498,8 +521,12 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
     }
     return KSIM_OK;
   }
-  if (!ksim_persistent_config(c.n, &grid, &lds_rows))
+  if (!ksim_persistent_config(c.n, &grid, &lds_rows)) {
+    // the streaming fast kernel handed over (a node left the exact float64 range): the
+    // general kernel of a table this size is the launch form
+    if (h->pfast_off && h->cfg.mode == KSIM_MODE_AUTO) return run_launch_mode(h, first, count, st);
     return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: node table does not fit the on-chip layout");
+  }
   if (!persistent_weights_ok(c)) return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: map-priority weights exceed the 27-bit score range");
   const size_t gb = ksim_persistent_granule_bytes(grid);
   if (h->gran_bytes < gb) {
@@ -564,11 +591,11 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
     for (int r = 0; r < h->shard.world; ++r)
       if (!h->shard.peers[r]) return fail(h, KSIM_E_STATE, "ksim_schedule: rank %d is not connected", r);
     int grid = 0, lds_rows = 0;
-    if (h->fast_pre[first + count] - h->fast_pre[first] != count || h->pfast_off || !persistent_weights_ok(c) ||
-        !ksim_pfast_config(c.n, h->max_grid, &grid, &lds_rows))
-      return fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling takes resource-only pods on shards that fit the "
-                                         "on-chip layout");
-    int rc = run_pfast_mode(h, first, count, grid, lds_rows, st);
+    const int form = pfast_form(h, first, count, &grid, &lds_rows);
+    if (!form)
+      return fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling takes resource-only pods on shards of at most ~1M "
+                                         "nodes per device");
+    int rc = run_pfast_mode(h, first, count, grid, lds_rows, form == 2, st);
     h->shard.xtag_base += (uint32_t)count;
     if (rc) return rc;
     int32_t err = 0;
@@ -581,7 +608,9 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
   int mode = h->cfg.mode;
   if (mode == KSIM_MODE_AUTO) {
     int g, l;
-    mode = (ksim_persistent_config(c.n, &g, &l) && persistent_weights_ok(c)) ? KSIM_MODE_PERSISTENT : KSIM_MODE_LAUNCH;
+    mode = ((ksim_persistent_config(c.n, &g, &l) && persistent_weights_ok(c)) || pfast_form(h, first, count, &g, &l))
+               ? KSIM_MODE_PERSISTENT
+               : KSIM_MODE_LAUNCH;
   }
   int rc = (mode == KSIM_MODE_PERSISTENT) ? run_persistent_mode(h, first, count, st) : run_launch_mode(h, first, count, st);
   if (rc) return rc;

@@ -487,3 +487,73 @@ def test_node_sharded_multi_process(tmp_path):
         lo, hi = int(r["lo"]), int(r["hi"])
         for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
             assert np.array_equal(r[k], ref_state[k][lo:hi]), k
+
+
+@pytest.mark.parametrize("max_grid", [0, 128, 64, 28])  # rows per row thread: 1, 2, 4, 9
+def test_stream_form_matches_c_oracle(max_grid, monkeypatch):
+    """The streaming form of the fast kernel (rows read from the HBM float64 image every pod,
+    only the evaluations in LDS — the form for tables beyond the LDS budget, forced here at
+    100k nodes with every row-per-thread instantiation): two calls of a C3 prefix equal the C
+    oracle, node state included."""
+    import cpu_ref
+    from ksim import synth
+    monkeypatch.setenv("KSIM_FORCE_STREAM", "1")
+    if max_grid:
+        monkeypatch.setenv("KSIM_MAX_GRID", str(max_grid))
+    cl, p, q = synth.config_c3(100_000, 5000, seed=8)
+    g = scheduler.GenericScheduler(cl, p, q, collect_reasons=False)
+    out1, _, st = g.schedule(0, 2200)
+    assert st.mode == abi.MODE_PERSISTENT
+    out2, _, _ = g.schedule(2200, 2800)
+    ref, _, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, 5000, threads=8)
+    assert np.array_equal(np.concatenate([out1, out2]), ref)
+    assert g.last_node_index == ref_ctr
+    s = g.node_state()
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+        assert np.array_equal(s[k], ref_state[k]), k
+
+
+def test_stream_form_fills_cluster_with_fit_errors(monkeypatch):
+    """Streaming form over a queue that overflows the cluster: FitError reason histograms,
+    single-fit pods (no counter increment), pressure / NotReady nodes."""
+    import cpu_ref
+    from ksim import synth
+    monkeypatch.setenv("KSIM_FORCE_STREAM", "1")
+    n = 997
+    cpu, mem = synth.c3_nodes(n, 21)
+    pcpu, pmem = synth.c3_pods(30_000, 21)
+    pcpu[::11] = 0  # some BestEffort-shaped pods (no requests)
+    pmem[::11] = 0
+    cl = synth.resource_cluster(["s-%05d" % i for i in range(n)], cpu, mem, np.full(n, 25, np.int32), pcpu, pmem)
+    cl.pods["flags"][::11] |= abi.POD_BEST_EFFORT
+    cl.pods["nz_cpu"][::11] = 100           # non-zero defaults (priorities/util/non_zero.go:31-33)
+    cl.pods["nz_mem"][::11] = 200 * 1024 * 1024
+    cl.cols["flags"][::37] |= abi.N_MEM_PRESSURE
+    cl.cols["flags"][5::101] |= abi.N_NOT_READY
+    preds, prios = scheduler.provider("DefaultProvider")
+    g = scheduler.GenericScheduler(cl, preds, prios)
+    out, reasons, _ = g.schedule()
+    ref, ref_reasons, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, prios), threads=8)
+    assert np.array_equal(out, ref)
+    failed = out < 0
+    assert failed.sum() > 1000
+    assert np.array_equal(reasons[failed], ref_reasons[failed])
+    assert g.last_node_index == ref_ctr
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_node_sharded_stream_form_matches_c_oracle(world, monkeypatch):
+    """Node-sharded run whose shards use the streaming form (the 2- and 4-GPU layout of C4)."""
+    import cpu_ref
+    from ksim import synth
+    monkeypatch.setenv("KSIM_FORCE_STREAM", "1")
+    monkeypatch.setenv("KSIM_MAX_GRID", str(256 // world // 2))
+    cl, p, q = synth.config_c3(60_000, 3000, seed=15)
+    scheds, merged = _run_sharded_threads(cl, p, q, world, [(0, 1000), (1000, 2000)])
+    ref, _, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, 3000, threads=8)
+    assert np.array_equal(merged, ref)
+    for s in scheds:
+        assert s.last_node_index == ref_ctr
+        st = s.node_state()
+        for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+            assert np.array_equal(st[k], ref_state[k][s.lo:s.hi]), k
