@@ -236,6 +236,10 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   __shared__ int32_t s_hist[KSIM_NREASONS];
   __shared__ int32_t s_mode[2], s_own[2];     // by pod parity: read after the barrier, rewritten two pods later
   __shared__ int32_t s_arr;
+  // STREAM: commit of pod p deferred to the row waves of the next iteration (by pod parity):
+  // row (-1 none) and the AddPod deltas (add cpu, add mem, non-zero cpu, non-zero mem)
+  __shared__ int32_t s_prow[2];
+  __shared__ double s_pdel[2][4];
   __shared__ __attribute__((aligned(16))) ksim_pod s_pod[RING];
 #ifdef KSIM_STAMPS
   uint64_t st_acc[16] = {};
@@ -283,7 +287,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
     ring_load(a.first + RING_FILL, ring_next);
     ring_store(a.first, v);
   }
-  if (tid == 0) { s_fix[a.first & 1][0] = -1; s_arr = 0; }
+  if (tid == 0) { s_fix[a.first & 1][0] = -1; s_arr = 0; s_prow[0] = s_prow[1] = -1; }
   uint64_t counter = *a.counter;  // replicated genericScheduler.lastNodeIndex
   __syncthreads();
 
@@ -395,7 +399,9 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
 
+  int64_t last = a.first;  // last pod iterated
   for (int64_t pod = a.first; pod < a.end; ++pod) {
+    last = pod;
     const bool has_next = pod + 1 < a.end;
     const int pb = (int)(pod & 1);
     const int nb = (int)((pod + 1) & 1);
@@ -527,7 +533,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           jsel = -1;
           mode = -1;
           if (lane == 0) atomicOr(a.err, 2);
-        } else {
+        } else if (!STREAM) {  // STREAM: from the row waves' post-commit evaluation (section d)
           const ksim_pod& Pp = s_pod[pod % RING];
           stopbit = (R.rc[jsel] + (double)Pp.add_cpu >= EXACT_LIM || R.rm[jsel] + (double)Pp.add_mem >= EXACT_LIM ||
                      R.zc[jsel] + (double)Pp.nz_cpu >= EXACT_LIM || R.zm[jsel] + (double)Pp.nz_mem >= EXACT_LIM)
@@ -537,10 +543,41 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
         OSTAMP(22);
       }
       if ((mode == 0 || mode == 3) && me == 0 && lane == 0) a.out_node[pod] = mode == 0 ? -1 : -2;
-      if (lane == 0) { s_mode[pb] = mode; s_own[pb] = jsel; }
+      if (lane == 0) {
+        s_mode[pb] = mode;
+        s_own[pb] = jsel;
+        if (STREAM) {  // the commit itself is applied by the row lane that owns the row
+          s_prow[pb] = jsel;
+          if (jsel >= 0) {
+            const ksim_pod& Pp = s_pod[pod % RING];
+            s_pdel[pb][0] = (double)Pp.add_cpu; s_pdel[pb][1] = (double)Pp.add_mem;
+            s_pdel[pb][2] = (double)Pp.nz_cpu; s_pdel[pb][3] = (double)Pp.nz_mem;
+          }
+        }
+      }
       X = mode == 2 ? blk : -1;
       STAMP(6);
-    } else if (has_next) {
+    } else {
+      // STREAM: the deferred commit of pod - 1 to this workgroup's row prow (s_prow[nb]) —
+      // the lane that streams the row adds the deltas in registers and stores the row back, so
+      // neither the owner's critical path nor a barrier waits on HBM (same-lane program order
+      // makes its next load of the row see the store)
+      const int32_t prow = STREAM ? s_prow[nb] : -1;
+      auto apply_commit = [&](FRow& r, int32_t j) {
+        r.rc += s_pdel[nb][0]; r.rm += s_pdel[nb][1]; r.zc += s_pdel[nb][2]; r.zm += s_pdel[nb][3]; r.count += 1;
+        R.rc[j] = r.rc; R.rm[j] = r.rm; R.zc[j] = r.zc; R.zm[j] = r.zm; R.count[j] = r.count;
+      };
+      if (STREAM && !has_next && prow >= 0) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          const int32_t j = k * RT + rt;
+          if (j == prow) {
+            FRow r = load_frow<STREAM>(R, j);
+            apply_commit(r, j);
+          }
+        }
+      }
+      if (has_next) {
       // ---------------- row waves: evaluate pod + 1, as the rows stand and after pod -----------
       const bool refill = wv == 1 && ((pod - a.first) % RING_FILL) == 0;
       if (refill) ring_store(pod + RING_FILL, ring_next);  // loaded a refill period ago
@@ -569,11 +606,16 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
         uint32_t& bm = B_rm[STREAM ? 0 : k];
         bm = 0;
         if (j < nrows) {
-          const FRow r = load_frow<STREAM>(R, j);
+          FRow r = load_frow<STREAM>(R, j);
+          if (STREAM && j == prow) apply_commit(r, j);
           uint32_t m2;
           e[k] = feval(EC, Q, r, bm);
           if (STREAM) R.rma[nb * chunk + j] = bm;
-          const int32_t e2 = feval(EC, Q, plus(r, P), m2);
+          const FRow r2 = plus(r, P);
+          const int32_t e2 = feval(EC, Q, r2, m2);
+          // STREAM: bit 31 = committing pod to this row leaves the exact float64 range
+          if (STREAM && (r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM))
+            m2 |= 1u << 31;
           evn[j] = e[k];
           R.ev2[j] = e2;
           R.rm2[j] = m2;
@@ -588,6 +630,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       if (tid == 64) st_acc[5] += __builtin_amdgcn_s_memtime() - te0;
 #endif
       if (refill) ring_next = rv;
+      }
     }
     lds_barrier();
     STAMP(7);
@@ -603,6 +646,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       if (wv == 0) {
         OSTAMP(17);
         if (has_next) {
+          if (STREAM) stopbit = (R.rm2[jsel] >> 31) ? (1ull << 55) : 0ull;
           // the workgroup's pod + 1 statistics without the committed row's pre-commit
           // evaluation, with its post-commit one (straight-line selects)
           const int32_t e_new = R.ev2[jsel], e_old = R.ev[nb * chunk + jsel];
@@ -620,11 +664,13 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           }
         }
         OSTAMP(18);
-        if (lane == 0) {  // commit: NodeInfo.AddPod into the LDS row
-          const ksim_pod& Pp = s_pod[pod % RING];
-          R.rc[jsel] += (double)Pp.add_cpu; R.rm[jsel] += (double)Pp.add_mem;
-          R.zc[jsel] += (double)Pp.nz_cpu; R.zm[jsel] += (double)Pp.nz_mem;
-          R.count[jsel] += 1;
+        if (lane == 0) {  // commit: NodeInfo.AddPod into the LDS row (STREAM: deferred, s_prow)
+          if (!STREAM) {
+            const ksim_pod& Pp = s_pod[pod % RING];
+            R.rc[jsel] += (double)Pp.add_cpu; R.rm[jsel] += (double)Pp.add_mem;
+            R.zc[jsel] += (double)Pp.nz_cpu; R.zm[jsel] += (double)Pp.nz_mem;
+            R.count[jsel] += 1;
+          }
           if (stopbit) atomicOr(a.err, 8);
           a.out_node[pod] = (int32_t)(a.node_base + lo + jsel);
           if (has_next) {
@@ -636,9 +682,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           }
         }
       }
-      // uniform (own is workgroup-wide): row waves see the commit — in LDS, or (STREAM) the
-      // global row, for which the workgroup-scope release waits for the stores to complete
-      if (STREAM) __syncthreads(); else lds_barrier();
+      lds_barrier();  // uniform (own is workgroup-wide): row waves see the commit
       if (wv == 0 && has_next) {
         // off the critical path: the corrected wave's statistics and bitmasks
         const int w = 1 + (jsel % RT) / 64;
@@ -686,6 +730,18 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 
   // the table is authoritative in HBM between calls: write the owned rows back
   __syncthreads();
+  if (STREAM) {  // the deferred commit of the last pod iterated (s_prow is -1 after a stop)
+    if (tid == 0) {
+      const int32_t pr = s_prow[last & 1];
+      if (pr >= 0) {
+        const double* d = s_pdel[last & 1];
+        R.rc[pr] += d[0]; R.rm[pr] += d[1]; R.zc[pr] += d[2]; R.zm[pr] += d[3]; R.count[pr] += 1;
+        if (R.rc[pr] >= EXACT_LIM || R.rm[pr] >= EXACT_LIM || R.zc[pr] >= EXACT_LIM || R.zm[pr] >= EXACT_LIM)
+          atomicOr(a.err, 8);
+      }
+    }
+    __syncthreads();
+  }
   for (int32_t j = tid; j < nrows; j += BS) {
     const int64_t i = lo + j;
     a.req_cpu[i] = (int64_t)R.rc[j]; a.req_mem[i] = (int64_t)R.rm[j];
