@@ -156,16 +156,19 @@ __device__ __noinline__ uint32_t commit_side(const KsimCtx* __restrict__ cg, con
 
 // Total score of reduce class q once the per-class maxima over the filtered set are known
 // (NormalizeReduce, priorities/reduce.go:29-64; weighted sum generic_scheduler.go:632-639).
-__device__ __forceinline__ int64_t class_total(const KsimCtx& c, int32_t cls, int q, int k2, int64_t base, int64_t mxT,
+// tv / av: the class's TaintToleration / NodeAffinity map values (prefetched per pod).
+__device__ __forceinline__ int64_t class_total(const KsimCtx& c, int64_t tv, int64_t av, int64_t base, int64_t mxT,
                                                int64_t mxA) {
   uint64_t t = (uint64_t)base;
-  if (c.w[KSIM_W_TAINT_TOLERATION])
-    t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] *
-         (uint64_t)ksim_norm(c.tt_val[(int64_t)cls * KSIM_MAX_RCLASS + q / k2], mxT, true);
-  if (c.w[KSIM_W_NODE_AFFINITY])
-    t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] *
-         (uint64_t)ksim_norm(c.na_val[(int64_t)cls * KSIM_MAX_RCLASS + q % k2], mxA, false);
+  if (c.w[KSIM_W_TAINT_TOLERATION]) t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(tv, mxT, true);
+  if (c.w[KSIM_W_NODE_AFFINITY]) t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(av, mxA, false);
   return (int64_t)t;
+}
+
+// 64-bit value of lane q (wave-uniform q)
+__device__ __forceinline__ int64_t readlane64(int64_t v, int q) {
+  return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)((uint64_t)v >> 32), q) << 32) |
+                   (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)v, q));
 }
 
 // General per-row evaluation (any supported pod).  Reads the context through a pointer to
@@ -209,6 +212,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   __shared__ int32_t s_fix[2][2];  // per pod parity: {row the owner re-evaluated (-1 none), its reason mask}
   __shared__ int32_t s_hist[KSIM_NREASONS];
   __shared__ int32_t s_M[KSIM_MAX_RCLASS];
+  __shared__ uint64_t s_gq[KSIM_MAX_RCLASS - 1][MAXG];  // control wave: granules of classes >= 1 (by b)
   __shared__ int32_t s_C[KSIM_MAX_RCLASS];
   __shared__ int32_t s_mode;
   __shared__ int32_t s_arr;  // row-wave arrivals (the last one of a pod publishes)
@@ -397,6 +401,13 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     if (wv == 0) {
       const ksim_pod& P = s_pod[pod % RING];
       const int K = pod_K(P);
+      const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
+      // the reduce classes' map values (lane q = class q), loaded now, used after the sweep
+      int64_t tv_l = 0, av_l = 0;
+      if (K > 1 && lane < K) {
+        tv_l = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + lane / k2];
+        av_l = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + lane % k2];
+      }
       // ---------------- a. sweep: every speculative partial of pod + the owner's correction ----
       const uint64_t tag = ptag(pod);
       const int slot = (int)(pod % NSLOT);
@@ -458,22 +469,30 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         C0 = ksimw::sum_i32((n && m == M0) ? n : 0);
       }
       STAMP(9);
-      const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
       if (ok && K > 1) {  // further reduce classes (TaintToleration x NodeAffinity)
         if (lane == 0) { s_M[0] = M0; s_C[0] = C0; }
         for (int q = 1; q < K; ++q) {
-          int32_t mm = -1, nn = 0;
-          for (int j = 0; j < MAXB; ++j) {
-            const int b = lane * MAXB + j;
-            if (b >= G) break;
-            uint64_t v = 0;
-            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-            for (;;) {
-              v = load_granule(gran_at(granules, slot, b, q, X));
-              if (gtag(v) == tag) break;
-              if (__builtin_amdgcn_s_memrealtime() - t1 > SPIN_LIMIT_TICKS) { ok = false; break; }
+          // all of this class's granules in one round trip (published with class 0, so
+          // normally already visible), kept in LDS for the locate step
+          uint64_t v[MAXB];
+          const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+          for (;;) {
+            bool mine = true;
+#pragma unroll
+            for (int j = 0; j < MAXB; ++j) {
+              const int b = lane * MAXB + j;
+              v[j] = b < G ? load_granule(gran_at(granules, slot, b, q, X)) : 0;
+              mine &= b >= G || gtag(v[j]) == tag;
             }
-            const int32_t cnt = gcnt(v), s = gscore(v);
+            if (__all(mine)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t1 > SPIN_LIMIT_TICKS) { ok = false; break; }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          int32_t mm = -1, nn = 0;
+#pragma unroll
+          for (int j = 0; j < MAXB; ++j) {
+            s_gq[q - 1][lane * MAXB + j] = v[j];
+            const int32_t cnt = gcnt(v[j]), s = gscore(v[j]);
             if (cnt == 0) continue;
             if (s > mm) { mm = s; nn = cnt; }
             else if (s == mm) nn += cnt;
@@ -499,21 +518,23 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
             int64_t mxT = 0, mxA = 0;
             for (int q = 0; q < K; ++q) {
               if (s_C[q] == 0) continue;
-              const int64_t tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2];
-              const int64_t av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];
+              const int64_t tv = readlane64(tv_l, q), av = readlane64(av_l, q);
               mxT = tv > mxT ? tv : mxT;
               mxA = av > mxA ? av : mxA;
             }
             int64_t best = INT64_MIN;
             for (int q = 0; q < K; ++q)
               if (s_C[q]) {
-                const int64_t t = class_total(c, P.cls, q, k2, s_M[q], mxT, mxA);
+                const int64_t t = class_total(c, readlane64(tv_l, q), readlane64(av_l, q), s_M[q], mxT, mxA);
                 best = t > best ? t : best;
               }
             win = 0;
             C = 0;
             for (int q = 0; q < K; ++q)
-              if (s_C[q] && class_total(c, P.cls, q, k2, s_M[q], mxT, mxA) == best) { win |= 1u << q; C += s_C[q]; }
+              if (s_C[q] && class_total(c, readlane64(tv_l, q), readlane64(av_l, q), s_M[q], mxT, mxA) == best) {
+                win |= 1u << q;
+                C += s_C[q];
+              }
           }
           ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)C) : (int64_t)((uint32_t)counter % (uint32_t)C);
           counter += 1;  // generic_scheduler.go:192-195
@@ -533,7 +554,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
               if ((win & 1u) && gcnt(g[j]) && gscore(g[j]) == M0) m += gcnt(g[j]);
               for (int q = 1; q < K; ++q) {
                 if (!((win >> q) & 1u)) continue;
-                const uint64_t v = load_granule(gran_at(granules, slot, b, q, X));
+                const uint64_t v = s_gq[q - 1][b];
                 if (gcnt(v) && gscore(v) == s_M[q]) m += gcnt(v);
               }
             }

@@ -95,6 +95,13 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// critical-path probes (diagnostic builds only, tools/build_variants): ~500-cycle delay at point k
+#ifdef KSIM_PROBE
+#define PROBE(k) do { if (KSIM_PROBE == (k)) __builtin_amdgcn_s_sleep(8); } while (0)
+#else
+#define PROBE(k) do { } while (0)
+#endif
+
 #ifdef KSIM_STAMPS
 #define STAMP(k)                                       \
   do {                                                 \
@@ -440,6 +447,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
         __builtin_amdgcn_s_sleep(1);
       }
       STAMP(2);
+      PROBE(3);
       // ---------------- b. decide: findNodesThatFit count, max score, selectHost ------------
       // One path for every F > 0: with a single fit node C = 1 and ix = 0 picks it, and only
       // the counter increment differs (generic_scheduler.go:153-156 skips selectHost).
@@ -586,6 +594,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 #ifdef KSIM_STAMPS
       const uint64_t te0 = __builtin_amdgcn_s_memtime();
 #endif
+      PROBE(4);
       const FPod P = load_fpod(s_pod[pod % RING]);
       const FPod Q = load_fpod(s_pod[(pod + 1) % RING]);
 #ifdef KSIM_STAMPS
@@ -595,9 +604,12 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 #else
 #define WSTAMP(k) do { } while (0)
 #endif
-      // two independent evaluations per lane (no divergence; only the winner's second one is
-      // ever read)
+      // two evaluations per row: as it stands (the speculative statistics every workgroup
+      // waits for) and after committing pod (only the owner's correction reads it).  The LDS
+      // form publishes the statistics first and evaluates the second hypothesis afterwards,
+      // off the exchange's critical path; the streaming form does both per streamed row.
       int32_t e[NPT];
+      FRow rk[STREAM ? 1 : NPT];
       int32_t* evn = R.ev + nb * chunk;
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
@@ -608,23 +620,38 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
         if (j < nrows) {
           FRow r = load_frow<STREAM>(R, j);
           if (STREAM && j == prow) apply_commit(r, j);
-          uint32_t m2;
           e[k] = feval(EC, Q, r, bm);
-          if (STREAM) R.rma[nb * chunk + j] = bm;
-          const FRow r2 = plus(r, P);
-          const int32_t e2 = feval(EC, Q, r2, m2);
-          // STREAM: bit 31 = committing pod to this row leaves the exact float64 range
-          if (STREAM && (r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM))
-            m2 |= 1u << 31;
           evn[j] = e[k];
-          R.ev2[j] = e2;
-          R.rm2[j] = m2;
+          if (STREAM) {
+            R.rma[nb * chunk + j] = bm;
+            uint32_t m2;
+            const FRow r2 = plus(r, P);
+            const int32_t e2 = feval(EC, Q, r2, m2);
+            // bit 31 = committing pod to this row leaves the exact float64 range
+            if (r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM) m2 |= 1u << 31;
+            R.ev2[j] = e2;
+            R.rm2[j] = m2;
+          } else {
+            rk[STREAM ? 0 : k] = r;
+          }
         }
       }
       WSTAMP(9);
       wave_stats(e, nb, wv);
       WSTAMP(10);
+      PROBE(1);
       arrive_publish(pod + 1, nb);
+      if (!STREAM) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          const int32_t j = k * RT + rt;
+          if (j < nrows) {
+            uint32_t m2;
+            R.ev2[j] = feval(EC, Q, plus(rk[STREAM ? 0 : k], P), m2);
+            R.rm2[j] = m2;
+          }
+        }
+      }
       WSTAMP(11);
 #ifdef KSIM_STAMPS
       if (tid == 64) st_acc[5] += __builtin_amdgcn_s_memtime() - te0;
@@ -657,6 +684,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           const bool up = add && (cb == 0 || e_new > mb), eq = add && !up && e_new == mb;
           const int32_t M = up ? e_new : mb, Cn = up ? 1 : cb + (eq ? 1 : 0);
           const int32_t Ff = f0 - (rem ? 1 : 0) + (add ? 1 : 0);
+          PROBE(2);
           if (lane == 0) {
             store_granule(fix_at(granules, (int)((pod + 1) % NSLOT)),
                           gpack(ptag(pod + 1), Ff, Cn, Cn ? M : -1) | stopbit);
