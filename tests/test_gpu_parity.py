@@ -557,3 +557,63 @@ def test_node_sharded_stream_form_matches_c_oracle(world, monkeypatch):
         st = s.node_state()
         for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
             assert np.array_equal(st[k], ref_state[k][s.lo:s.hi]), k
+
+
+# ----------------------------------------------------------------------------- edge cases
+def test_no_nodes_is_err_no_nodes_available():
+    """genericScheduler.Schedule with an empty node list returns ErrNoNodesAvailable
+    (core/generic_scheduler.go:63-64,125): the C-ABI refuses the empty table with that text."""
+    pods = [{"metadata": {"name": "p"}, "spec": {"containers": [{}]}}]
+    with pytest.raises(abi.KsimError) as ei:
+        scheduler.ClusterCapacity([], [], pods)
+    assert "no nodes available to schedule pods" in str(ei.value)
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_empty_queue_and_empty_ranges(mode):
+    """No simulation pods: an empty report and an untouched counter; zero-length and
+    out-of-range schedule calls."""
+    nodes = [{"metadata": {"name": "n-%d" % i}, "status": {"allocatable": {"cpu": "4", "memory": "8Gi", "pods": "10"}}}
+             for i in range(5)]
+    rep = scheduler.ClusterCapacity(nodes, [], [], mode=mode).run()
+    assert rep.successful == [] and rep.failed == [] and rep.last_node_index == 0
+    pods = [{"metadata": {"name": "p%d" % i}, "spec": {"containers": [{}]}} for i in range(3)]
+    cc = scheduler.ClusterCapacity(nodes, [], pods, mode=mode)
+    out, _, st = cc.scheduler.schedule(1, 0)
+    assert len(out) == 0 and st.pods == 0
+    with pytest.raises(abi.KsimError):
+        cc.scheduler.schedule(2, 5)
+    assert cc.scheduler.last_node_index == 0
+
+
+@pytest.mark.parametrize("n_nodes", [1, 2, 63, 65])
+@pytest.mark.parametrize("force_stream", [False, True])
+def test_tiny_clusters_fast_kernel(n_nodes, force_stream, monkeypatch):
+    """Clusters smaller than one workgroup's rows (a single workgroup, partial waves) in both
+    forms of the fast kernel, filled past capacity, against the C oracle."""
+    import cpu_ref
+    from ksim import synth
+    if force_stream:
+        monkeypatch.setenv("KSIM_FORCE_STREAM", "1")
+    cpu, mem = synth.c3_nodes(n_nodes, 31)
+    pcpu, pmem = synth.c3_pods(40 * n_nodes + 20, 31)
+    cl = synth.resource_cluster(["t-%03d" % i for i in range(n_nodes)], cpu, mem, np.full(n_nodes, 30, np.int32),
+                                pcpu, pmem)
+    preds = list(scheduler.DEFAULT_PREDICATES)
+    prios = [("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
+    g = scheduler.GenericScheduler(cl, preds, prios)
+    out, reasons, st = g.schedule()
+    ref, ref_reasons, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, prios), threads=2)
+    assert st.mode == abi.MODE_PERSISTENT
+    assert np.array_equal(out, ref)
+    failed = out < 0
+    assert failed.sum() > 0 and np.array_equal(reasons[failed], ref_reasons[failed])
+    assert g.last_node_index == ref_ctr
+
+
+def test_single_node_fit_error_message():
+    """One node, a pod that does not fit: the FitError text (core/generic_scheduler.go:72-90)."""
+    nodes = [{"metadata": {"name": "only"}, "status": {"allocatable": {"cpu": "1", "memory": "1Gi", "pods": "5"}}}]
+    pods = [{"metadata": {"name": "big"}, "spec": {"containers": [{"resources": {"requests": {"cpu": "2", "memory": "2Gi"}}}]}}]
+    rep = scheduler.ClusterCapacity(nodes, [], pods).run()
+    assert rep.failed == [("big", "0/1 nodes are available: 1 Insufficient cpu, 1 Insufficient memory.")]
