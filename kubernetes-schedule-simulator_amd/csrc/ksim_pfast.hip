@@ -211,6 +211,27 @@ __device__ __forceinline__ FRows carve(int rows, const PfArgs& a, int64_t lo) {
   return r;
 }
 
+// STREAM, control wave: row j read from L2 (agent-scope relaxed loads, past this CU's L1), so a
+// store another wave of the workgroup completed before the last barrier is seen
+typedef __attribute__((address_space(1))) const uint64_t cgu64;
+typedef __attribute__((address_space(1))) const int32_t cgi32;
+__device__ __forceinline__ double ld_l2(const double* p) {
+  return __builtin_bit_cast(double, __hip_atomic_load((cgu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ int32_t ld_l2(const int32_t* p) {
+  return __hip_atomic_load((cgi32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ FRow load_frow_l2(const FRows& R, int32_t j) {
+  FRow r;
+  r.ac = ld_l2(R.ac + j); r.am = ld_l2(R.am + j); r.rc = ld_l2(R.rc + j); r.rm = ld_l2(R.rm + j);
+  r.zc = ld_l2(R.zc + j); r.zm = ld_l2(R.zm + j);
+  r.yc = r.ac != 0.0 ? 1.0 / r.ac : 0.0;
+  r.ym = r.am != 0.0 ? 1.0 / r.am : 0.0;
+  r.allowed = ld_l2(R.allowed + j); r.count = ld_l2(R.count + j);
+  r.fl = (uint32_t)ld_l2(reinterpret_cast<const int32_t*>(R.fl) + j);
+  return r;
+}
+
 // STREAM: y = RN(1/alloc) is recomputed (IEEE divide) instead of read, so a row costs exactly
 // the 60 algorithmic bytes: 6 x 8 (alloc, requested, non-zero requested cpu / mem) + 3 x 4.
 template <bool STREAM>
@@ -247,6 +268,8 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   // row (-1 none) and the AddPod deltas (add cpu, add mem, non-zero cpu, non-zero mem)
   __shared__ int32_t s_prow[2];
   __shared__ double s_pdel[2][4];
+  __shared__ double s_pval[4];   // STREAM: the deferred-commit row's dynamic values after applying it
+  __shared__ int32_t s_pcnt;
   __shared__ __attribute__((aligned(16))) ksim_pod s_pod[RING];
 #ifdef KSIM_STAMPS
   uint64_t st_acc[16] = {};
@@ -414,6 +437,9 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
     const int nb = (int)((pod + 1) & 1);
     int32_t jsel = -1;      // control wave: row this workgroup commits pod to
     uint64_t stopbit = 0;   // ... and whether that commit leaves the exact float64 range
+    FRow jrow;              // STREAM: that row as loaded by the owner
+    int32_t e_new = -1;     // STREAM: pod + 1 against the row after pod's commit
+    uint32_t m_new = 0;
 #ifdef KSIM_STAMPS
     uint64_t o_prev = 0;
 #endif
@@ -541,12 +567,22 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           jsel = -1;
           mode = -1;
           if (lane == 0) atomicOr(a.err, 2);
-        } else if (!STREAM) {  // STREAM: from the row waves' post-commit evaluation (section d)
+        } else if (!STREAM) {
           const ksim_pod& Pp = s_pod[pod % RING];
           stopbit = (R.rc[jsel] + (double)Pp.add_cpu >= EXACT_LIM || R.rm[jsel] + (double)Pp.add_mem >= EXACT_LIM ||
                      R.zc[jsel] + (double)Pp.nz_cpu >= EXACT_LIM || R.zm[jsel] + (double)Pp.nz_mem >= EXACT_LIM)
                         ? (1ull << 55)
                         : 0ull;
+        } else if (has_next) {
+          // STREAM: the row waves evaluate pod + 1 once per row; the owner evaluates the committed
+          // row after pod itself, loading it now while the row waves still stream (a row with a
+          // commit still pending from pod - 1 is finished in section d from the streaming lane's copy)
+          jrow = load_frow_l2(R, jsel);
+          if (jsel != s_prow[nb]) {
+            const FRow r2 = plus(jrow, load_fpod(s_pod[pod % RING]));
+            e_new = feval(EC, load_fpod(s_pod[(pod + 1) % RING]), r2, m_new);
+            stopbit = (r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM) ? (1ull << 55) : 0ull;
+          }
         }
         OSTAMP(22);
       }
@@ -574,6 +610,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       auto apply_commit = [&](FRow& r, int32_t j) {
         r.rc += s_pdel[nb][0]; r.rm += s_pdel[nb][1]; r.zc += s_pdel[nb][2]; r.zm += s_pdel[nb][3]; r.count += 1;
         R.rc[j] = r.rc; R.rm[j] = r.rm; R.zc[j] = r.zc; R.zm[j] = r.zm; R.count[j] = r.count;
+        s_pval[0] = r.rc; s_pval[1] = r.rm; s_pval[2] = r.zc; s_pval[3] = r.zm; s_pcnt = r.count;  // for the owner
       };
       if (STREAM && !has_next && prow >= 0) {
 #pragma unroll
@@ -604,10 +641,10 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 #else
 #define WSTAMP(k) do { } while (0)
 #endif
-      // two evaluations per row: as it stands (the speculative statistics every workgroup
-      // waits for) and after committing pod (only the owner's correction reads it).  The LDS
-      // form publishes the statistics first and evaluates the second hypothesis afterwards,
-      // off the exchange's critical path; the streaming form does both per streamed row.
+      // the LDS form evaluates every row twice: as it stands (the speculative statistics every
+      // workgroup waits for, published first) and after committing pod (only the owner's
+      // correction reads it, so it is computed after the publish); the streaming form evaluates
+      // once and its owner evaluates the committed row itself.
       int32_t e[NPT];
       FRow rk[STREAM ? 1 : NPT];
       int32_t* evn = R.ev + nb * chunk;
@@ -624,13 +661,6 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           evn[j] = e[k];
           if (STREAM) {
             R.rma[nb * chunk + j] = bm;
-            uint32_t m2;
-            const FRow r2 = plus(r, P);
-            const int32_t e2 = feval(EC, Q, r2, m2);
-            // bit 31 = committing pod to this row leaves the exact float64 range
-            if (r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM) m2 |= 1u << 31;
-            R.ev2[j] = e2;
-            R.rm2[j] = m2;
           } else {
             rk[STREAM ? 0 : k] = r;
           }
@@ -658,6 +688,9 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 #endif
       if (refill) ring_next = rv;
       }
+      // STREAM: the wave that applied pod - 1's deferred commit lets its stores reach L2 before
+      // the barrier: from the next pod on the owner may read that row (load_frow_l2)
+      if (STREAM && prow >= 0 && wv == 1 + (prow % RT) / 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_barrier();
     STAMP(7);
@@ -673,10 +706,17 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       if (wv == 0) {
         OSTAMP(17);
         if (has_next) {
-          if (STREAM) stopbit = (R.rm2[jsel] >> 31) ? (1ull << 55) : 0ull;
+          if (STREAM && jsel == s_prow[nb]) {  // pod - 1's deferred commit hit this row too
+            FRow r = jrow;
+            r.rc = s_pval[0]; r.rm = s_pval[1]; r.zc = s_pval[2]; r.zm = s_pval[3]; r.count = s_pcnt;
+            const FRow r2 = plus(r, load_fpod(s_pod[pod % RING]));
+            e_new = feval(EC, load_fpod(s_pod[(pod + 1) % RING]), r2, m_new);
+            stopbit = (r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM) ? (1ull << 55) : 0ull;
+          }
+          if (!STREAM) { e_new = R.ev2[jsel]; m_new = R.rm2[jsel]; }
           // the workgroup's pod + 1 statistics without the committed row's pre-commit
           // evaluation, with its post-commit one (straight-line selects)
-          const int32_t e_new = R.ev2[jsel], e_old = R.ev[nb * chunk + jsel];
+          const int32_t e_old = R.ev[nb * chunk + jsel];
           const int32_t f0 = s_wg[nb][0], m1 = s_wg[nb][1], c1 = s_wg[nb][2], m2 = s_wg[nb][3], c2 = s_wg[nb][4];
           const bool rem = e_old >= 0, add = e_new >= 0;
           const int32_t c1a = c1 - ((rem && e_old == m1) ? 1 : 0);
@@ -702,9 +742,9 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           if (stopbit) atomicOr(a.err, 8);
           a.out_node[pod] = (int32_t)(a.node_base + lo + jsel);
           if (has_next) {
-            R.ev[nb * chunk + jsel] = R.ev2[jsel];
+            R.ev[nb * chunk + jsel] = e_new;
             s_fix[nb][0] = jsel;
-            s_fix[nb][1] = (int32_t)R.rm2[jsel];
+            s_fix[nb][1] = (int32_t)m_new;
           } else {
             s_fix[nb][0] = -1;
           }
