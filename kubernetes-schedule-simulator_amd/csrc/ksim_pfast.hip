@@ -72,6 +72,16 @@ __device__ __forceinline__ uint64_t* spec_at(uint64_t* gr, int slot, int b) {
   return gr + slot * MAXG + (b % MAXB) * 64 + b / MAXB;
 }
 __device__ __forceinline__ uint64_t* fix_at(uint64_t* gr, int slot) { return gr + NSLOT * MAXG + slot * FIXSTRIDE; }
+// Every granule is written to NREP replicas of the whole array (lane r of the publishing wave
+// writes replica r) and workgroup b polls replica b % NREP: the 256 pollers spread over NREP
+// sets of lines instead of all sweeping the same 2 KB.
+#ifndef KSIM_NREP
+#define KSIM_NREP 8
+#endif
+constexpr int NREP = KSIM_NREP;
+
+constexpr int REP_STRIDE = 2112;  // uint64 words between replicas (16.5 KB, > one replica)
+static_assert(NSLOT * MAXG + NSLOT * FIXSTRIDE <= REP_STRIDE, "replica overlap");
 
 // granule: tag:8 | stop:1 | fit:13 | count:13 | score:29 (two's complement, -1 = no fit node;
 // scores < 2^27, host-checked); stop (correction granules only): the committed node left the
@@ -284,11 +294,13 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   const int64_t hi = (lo + chunk < a.n) ? lo + chunk : a.n;
   const int32_t nrows = (int32_t)(hi - lo);
   const FRows R = carve<STREAM>((int)chunk, a, lo);
-  int32_t* const top_list = reinterpret_cast<int32_t*>(R.rm2 + chunk);  // [chunk]: rows at the workgroup maximum, from the top
   const uint32_t preds = a.preds;
   const bool no_prio = a.no_prio != 0;
   const EvCfg EC = make_evcfg(preds, no_prio, a.wl, a.wm, a.wb);
+  int32_t* const top_list = reinterpret_cast<int32_t*>(R.rm2 + chunk);  // STREAM: [chunk] rows at the workgroup maximum, from the top
   uint64_t* const granules = a.granules;
+  constexpr int NR = STREAM ? 1 : NREP;  // (STREAM: one copy — the row loads own the registers)
+  uint64_t* const my_rep = NR == 1 ? granules : granules + (me % NR) * REP_STRIDE;
 
   for (int32_t j = tid; j < (STREAM ? 0 : nrows); j += BS) {  // stage the owned rows into LDS
     const int64_t i = lo + j;
@@ -371,12 +383,52 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       if (t.m2 < 0) t.c2 = 0;
       if (lane == 0) {
         s_wg[buf][0] = t.f; s_wg[buf][1] = t.m1; s_wg[buf][2] = t.c1; s_wg[buf][3] = t.m2; s_wg[buf][4] = t.c2;
-        store_granule(spec_at(granules, (int)(p % NSLOT), me), gpack(ptag(p), t.f, t.c1, t.m1));
+        if (NR == 1) store_granule(spec_at(granules, (int)(p % NSLOT), me), gpack(ptag(p), t.f, t.c1, t.m1));
       }
+      if (NR > 1 && lane < NR)
+        store_granule(spec_at(granules + lane * REP_STRIDE, (int)(p % NSLOT), me), gpack(ptag(p), t.f, t.c1, t.m1));
     }
   };
-  // control wave: rows at the workgroup maximum of the pod in `buf`, name rank descending,
-  // into top_list — so an owner turns its rank into a row with one LDS read
+  // LDS form, control wave: the 64-row segments holding rows at the workgroup maximum of the pod in `buf`
+  // (lane t = t-th segment from the top: its bitmask, count, and the matches in segments above
+  // it), read before the sweep; the owner turns its rank into a row with a few wave operations
+  struct Segs {
+    uint64_t m;
+    int32_t cnt, base, total;
+  };
+  auto seg_prepare = [&](int buf) -> Segs {
+    constexpr int S = NPT * RW;
+    const int32_t M = s_wg[buf][1];
+    Segs sg;
+    sg.m = 0;
+    if (lane < S) {
+      const int k = NPT - 1 - lane / RW, w = RW - 1 - lane % RW;
+      sg.m = (M >= 0 && s_wst[buf][w][1] == M) ? s_bm[buf][k][w] : 0ull;
+    }
+    sg.cnt = __popcll(sg.m);
+    const int32_t incl = ksimw::prefix_incl_i32(sg.cnt);
+    sg.base = incl - sg.cnt;
+    sg.total = __builtin_amdgcn_readlane(incl, 63);
+    return sg;
+  };
+  // the rank-th row from the top (-1 if none): the segment holding it, then the bit
+  auto seg_select = [&](const Segs& sg, int32_t rank) -> int32_t {
+    const uint64_t hs = __ballot(sg.cnt != 0 && rank >= sg.base && rank < sg.base + sg.cnt);
+    if (rank >= sg.total || !hs) return -1;
+    const int t = __builtin_ctzll(hs);
+    const uint64_t ms = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(sg.m >> 32), t) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)sg.m, t);
+    const int32_t r = rank - __builtin_amdgcn_readlane(sg.base, t);
+    const uint64_t hb = __ballot(((ms >> lane) & 1ull) && __popcll(ms >> lane) - 1 == r);
+    if (!hb) return -1;
+    const int k = NPT - 1 - t / RW, w = RW - 1 - t % RW;
+    return k * RT + w * 64 + __builtin_ctzll(hb);
+  };
+
+  // STREAM, control wave: rows at the workgroup maximum of the pod in `buf`, name rank
+  // descending, into top_list — so an owner turns its rank into a row with one LDS read (the
+  // list is built while the row waves stream, off the critical path; measured faster there
+  // than seg_select)
   auto build_top_list = [&](int buf) {
     constexpr int S = NPT * RW;  // lane t = t-th 64-row segment from the top
     const int32_t M = s_wg[buf][1];
@@ -445,7 +497,9 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 #endif
 
     if (wv == 0) {
-      build_top_list(pb);
+      Segs sg{};
+      if (STREAM) build_top_list(pb);
+      else sg = seg_prepare(pb);
       STAMP(1);
       // ---------------- a. sweep: every workgroup's granule of pod (+ the owner's fix) -------
       const uint64_t tag = ptag(pod);
@@ -455,8 +509,8 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
 #pragma unroll
-        for (int j = 0; j < MAXB; ++j) g[j] = load_granule(granules + slot * MAXG + j * 64 + lane);
-        fx = load_granule(fix_at(granules, slot));
+        for (int j = 0; j < MAXB; ++j) g[j] = load_granule(my_rep + slot * MAXG + j * 64 + lane);
+        fx = load_granule(fix_at(my_rep, slot));
         bool mine = X < 0 || gtag(fx) == tag;
 #pragma unroll
         for (int j = 0; j < MAXB; ++j) {
@@ -562,7 +616,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 #endif
       if (mode == 2 && blk == me) {
         // ---------------- c. owner: the rank-th row from the top ----------------
-        jsel = (rank < s_wg[pb][2]) ? top_list[rank] : -1;
+        jsel = STREAM ? (rank < s_wg[pb][2] ? top_list[rank] : -1) : seg_select(sg, rank);
         if (jsel < 0 || jsel >= nrows) {
           jsel = -1;
           mode = -1;
@@ -725,9 +779,12 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           const int32_t M = up ? e_new : mb, Cn = up ? 1 : cb + (eq ? 1 : 0);
           const int32_t Ff = f0 - (rem ? 1 : 0) + (add ? 1 : 0);
           PROBE(2);
-          if (lane == 0) {
-            store_granule(fix_at(granules, (int)((pod + 1) % NSLOT)),
+          if (NR > 1 && lane < NR)
+            store_granule(fix_at(granules + lane * REP_STRIDE, (int)((pod + 1) % NSLOT)),
                           gpack(ptag(pod + 1), Ff, Cn, Cn ? M : -1) | stopbit);
+          if (lane == 0) {
+            if (NR == 1)
+              store_granule(fix_at(granules, (int)((pod + 1) % NSLOT)), gpack(ptag(pod + 1), Ff, Cn, Cn ? M : -1) | stopbit);
             s_wg[nb][0] = Ff; s_wg[nb][1] = Cn ? M : -1; s_wg[nb][2] = Cn;
           }
         }
@@ -856,7 +913,7 @@ extern "C" int ksim_pfast_config(int64_t n, int max_grid, int stream, int* grid,
   return 1;
 }
 
-extern "C" size_t ksim_pfast_granule_bytes(void) { return (size_t)(NSLOT * MAXG + NSLOT * FIXSTRIDE) * sizeof(uint64_t); }
+extern "C" size_t ksim_pfast_granule_bytes(void) { return (size_t)NREP * REP_STRIDE * sizeof(uint64_t); }
 
 extern "C" size_t ksim_shard_xchg_bytes(void) { return (size_t)ANSLOT * KSIM_MAX_RANKS * 4 * sizeof(uint64_t); }
 
