@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--batch", type=int, default=None, help="pods per step (default: c3/c2 4096, c4 512)")
     ap.add_argument("--nodes", type=int, default=None, help="default: c3 100,000, c2 5,000, c4 1,000,000")
     ap.add_argument("--pods", type=int, default=None, help="queue length (default: c3 1M, c2 50k, c4 as needed)")
-    ap.add_argument("--mode", default="auto", choices=["auto", "launch", "persistent"])
+    ap.add_argument("--mode", default="auto", choices=["auto", "launch", "persistent", "tree"])
     ap.add_argument("--cpu-sample", type=int, default=3000, help="pods in the CPU-baseline prefix (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"],
@@ -227,7 +227,7 @@ def main():
     prios0 = list(prios)  # the one cluster's policy (rank 0's replica, the node-sharded run)
     if rank > 0:  # what-if sweep: each replica scores with its own LeastRequested weight
         prios = [(k, w + rank) if k == "LeastRequestedPriority" else (k, w) for k, w in prios0]
-    mode = {"auto": abi.MODE_AUTO, "launch": abi.MODE_LAUNCH, "persistent": abi.MODE_PERSISTENT}[a.mode]
+    mode = {"auto": abi.MODE_AUTO, "launch": abi.MODE_LAUNCH, "persistent": abi.MODE_PERSISTENT, "tree": abi.MODE_TREE}[a.mode]
     g = scheduler.GenericScheduler(cl, preds, prios, device=local, mode=mode, collect_reasons=False)
 
     placements = []
@@ -303,7 +303,7 @@ def main():
             "data": data,
             "config": {"workload": desc % (n, a.pods),
                        "nodes": n, "pods_per_step": a.batch, "global_batch": a.batch * world,
-                       "mode": {1: "launch", 2: "persistent"}.get(mode_used, str(mode_used)), "blocks": blocks,
+                       "mode": {1: "launch", 2: "persistent", 3: "tree"}.get(mode_used, str(mode_used)), "blocks": blocks,
                        "parallelism": "scenario-replicas x%d" % world if world > 1 else "single-gpu"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -108,6 +108,11 @@ extern "C" {
 #define KSIM_MODE_AUTO 0        /* library picks (persistent when it fits) */
 #define KSIM_MODE_LAUNCH 1      /* one scan launch per pod, replayed from a hipGraph */
 #define KSIM_MODE_PERSISTENT 2  /* one persistent launch walks the whole pod queue */
+/* Incremental per-pod-class selection trees: resource-only pods under
+ * map-only policies are decided from a tree that each commit updates along one leaf-to-root
+ * path, O(classes x log N) per pod instead of the O(N) scan; same placements.  Runs of other
+ * pods in the range, and tables/class sets beyond the tree's limits, take the AUTO path. */
+#define KSIM_MODE_TREE 3
 
 typedef struct {
   int32_t device;                 /* HIP device ordinal */

@@ -7,15 +7,18 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
 #include <string>
 #include <vector>
 
 #include "ksim_common.h"
 #include "ksim_sweep.h"
+#include "ksim_tree.h"
 
 extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* fit, uint32_t* reasons, int64_t* score,
@@ -36,6 +39,12 @@ extern "C" size_t ksim_pfast_granule_bytes(void);
 extern "C" size_t ksim_shard_xchg_bytes(void);
 extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, double* mirror,
                                         const KsimShard* sh, hipStream_t s);
+extern "C" hipError_t ksim_tree_build(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
+                                      const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
+                                      hipStream_t s);
+extern "C" hipError_t ksim_tree_launch(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
+                                       const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
+                                       hipStream_t s);
 
 namespace {
 
@@ -85,6 +94,17 @@ struct ksim_handle {
   void* ipc_mapped[KSIM_MAX_RANKS] = {};  // peers' exchange buffers opened through IPC
   int max_grid = 0;                        // workgroups per launch (0 = one per CU)
   double* mirror = nullptr;                // streaming fast kernel: float64 image [6][n]
+  // tree mode (ksim_tree.hip): tree class of every resource-only pod (-1 otherwise), the class
+  // inputs, the geometry and the device trees; tree_valid = the trees describe the current
+  // node table (any other commit path clears it)
+  int32_t n_tcls = 0;                      // -1: more classes than the tree supports
+  int32_t* tcls = nullptr;
+  KsimTreeClass* tclass = nullptr;
+  bool tree_planned = false, tree_ok = false, tree_valid = false;
+  KsimTreeGeo geo{};
+  int32_t* t_leaves = nullptr;
+  uint64_t* t_levels = nullptr;
+  int32_t* t_fit = nullptr;
 };
 
 static int fail(ksim_handle* h, int code, const char* fmt, ...) {
@@ -144,6 +164,8 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
   if (cfg->device < 0 || cfg->device >= ndev) return fail(nullptr, KSIM_E_INVAL, "ksim_create: bad device %d", cfg->device);
   for (int k = 0; k < KSIM_NW; ++k)
     if (cfg->weights[k] < 0) return fail(nullptr, KSIM_E_INVAL, "ksim_create: negative weight in slot %d", k);
+  if (cfg->mode < KSIM_MODE_AUTO || cfg->mode > KSIM_MODE_TREE)
+    return fail(nullptr, KSIM_E_INVAL, "ksim_create: unknown mode %d", cfg->mode);
   const uint32_t known = (1u << 11) - 1;
   if (cfg->predicates & ~known) return fail(nullptr, KSIM_E_UNSUPPORTED, "ksim_create: unknown predicate bits");
   ksim_handle* h = new ksim_handle();
@@ -335,6 +357,33 @@ int ksim_load_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
                       p.req_gpu == 0 && p.req_eph == 0 && !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS));
     h->fast_pre[i + 1] = h->fast_pre[i] + (fast ? 1 : 0);
   }
+  // tree classes: resource-only pods with identical predicate / priority inputs
+  {
+    std::vector<int32_t> tc((size_t)n_pods, -1);
+    std::vector<KsimTreeClass> cls;
+    std::map<std::array<int64_t, 5>, int32_t> keys;
+    for (int64_t i = 0; i < n_pods && h->n_tcls >= 0; ++i) {
+      if (h->fast_pre[i + 1] == h->fast_pre[i]) continue;
+      const ksim_pod& p = pods[i];
+      const std::array<int64_t, 5> key{p.req_cpu, p.req_mem, p.nz_cpu, p.nz_mem,
+                                       (int64_t)(p.flags & (KSIM_POD_ANY_REQUEST | KSIM_POD_BEST_EFFORT))};
+      auto it = keys.find(key);
+      int32_t c = it == keys.end() ? (int32_t)keys.size() : it->second;
+      if (it == keys.end()) {
+        if (c == KSIM_TREE_MAX_CLASSES) { h->n_tcls = -1; break; }
+        keys.emplace(key, c);
+        cls.push_back(KsimTreeClass{(double)p.req_cpu, (double)p.req_mem, (double)p.nz_cpu, (double)p.nz_mem,
+                                    (p.flags & KSIM_POD_ANY_REQUEST) ? ~0u : 0u, (p.flags & KSIM_POD_BEST_EFFORT) ? ~0u : 0u});
+      }
+      tc[i] = (int32_t)c;
+    }
+    if (h->n_tcls >= 0) {
+      h->n_tcls = (int32_t)keys.size();
+      if ((rc = dev_upload(h, &h->tcls, tc.data(), tc.size())) ||
+          (rc = dev_upload(h, &h->tclass, cls.data(), cls.size())))
+        return rc;
+    }
+  }
   h->pod_qmax.assign((size_t)n_pods, 0);
   for (int64_t i = 0; i < n_pods; ++i) {
     const ksim_pod& p = pods[i];
@@ -524,7 +573,7 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
   if (!ksim_persistent_config(c.n, &grid, &lds_rows)) {
     // the streaming fast kernel handed over (a node left the exact float64 range): the
     // general kernel of a table this size is the launch form
-    if (h->pfast_off && h->cfg.mode == KSIM_MODE_AUTO) return run_launch_mode(h, first, count, st);
+    if (h->pfast_off && h->cfg.mode != KSIM_MODE_PERSISTENT) return run_launch_mode(h, first, count, st);
     return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: node table does not fit the on-chip layout");
   }
   if (!persistent_weights_ok(c)) return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: map-priority weights exceed the 27-bit score range");
@@ -578,6 +627,133 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
   return KSIM_OK;
 }
 
+// AUTO dispatch: the persistent kernels when the table fits on chip (or the streaming fast
+// kernel can take the range), else the launch form.
+static int run_auto_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
+  int g, l;
+  const bool pers = (ksim_persistent_config(h->ctx.n, &g, &l) && persistent_weights_ok(h->ctx)) ||
+                    pfast_form(h, first, count, &g, &l);
+  h->tree_valid = false;  // these paths commit without maintaining the trees
+  return pers ? run_persistent_mode(h, first, count, st) : run_launch_mode(h, first, count, st);
+}
+
+// Can tree mode run at all on this handle (one device, class set and weights within the tree's
+// packing, every quantity exact in float64)?  Plans the geometry and allocates the trees once.
+static int tree_ready(ksim_handle* h, bool* ok) {
+  *ok = false;
+  const KsimCtx& c = h->ctx;
+  if (h->shard.world > 1 || h->n_tcls <= 0 || h->pfast_off || getenv("KSIM_NO_TREE")) return KSIM_OK;
+  if (!c.no_prio) {
+    int64_t s = 0;
+    for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED}) {
+      if (c.w[k] > 65535) return KSIM_OK;
+      s += c.w[k] * 10;
+    }
+    if (s > 65534) return KSIM_OK;  // (score + 1) packs into 16 bits
+  }
+  if (!h->tree_planned) {
+    h->tree_planned = true;
+    const char* lb = getenv("KSIM_TREE_LDS");  // tests: force global levels on small tables
+    const char* fm = getenv("KSIM_TREE_M");
+    h->tree_ok = ksim_tree_plan(c.n, h->n_tcls, lb ? atoll(lb) : 0, fm ? atoi(fm) : 0, &h->geo) != 0;
+    if (h->tree_ok) {
+      int rc;
+      if ((rc = dev_alloc(h, &h->t_leaves, (size_t)h->geo.K * h->geo.st[0])) ||
+          (rc = dev_alloc(h, &h->t_levels, (size_t)h->geo.level_entries)) ||
+          (rc = dev_alloc(h, &h->t_fit, (size_t)h->geo.K)))
+        return rc;
+    }
+  }
+  *ok = h->tree_ok;
+  return KSIM_OK;
+}
+
+static void add_stats(ksim_stats* st, const ksim_stats& s) {
+  if (!st) return;
+  st->device_ms += s.device_ms;
+  st->kernel_ms += s.kernel_ms;
+  st->kernel_launches += s.kernel_launches;
+  if (!st->mode) { st->mode = s.mode; st->blocks = s.blocks; }
+}
+
+// Tree mode (ksim_tree.hip): maximal runs of resource-only pods go to the tree kernel (trees
+// rebuilt first if another path committed since), other runs to the AUTO path.
+static int run_tree_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
+  KsimCtx& c = h->ctx;
+  bool ok = false;
+  int rc = tree_ready(h, &ok);
+  if (rc) return rc;
+  if (!ok) return run_auto_mode(h, first, count, st);
+  if (st) memset(st, 0, sizeof *st);
+  const int64_t end = first + count;
+  auto fast = [&](int64_t i) { return h->fast_pre[i + 1] != h->fast_pre[i]; };
+  int64_t i = first;
+  while (i < end) {
+    int64_t j = i;
+    while (j < end && fast(j)) ++j;
+    if (j == i || h->pfast_off) {  // a run of other pods (or the tree stopped for good)
+      if (j == i)
+        while (j < end && !fast(j)) ++j;
+      ksim_stats s2{};
+      if ((rc = run_auto_mode(h, i, j - i, &s2))) return rc;
+      add_stats(st, s2);
+      i = j;
+      continue;
+    }
+    HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+    if (!h->tree_valid) {
+      hipError_t e = ksim_tree_build(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->stream);
+      if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree build: %s", hipGetErrorString(e));
+    }
+    c.first = i;
+    c.end = j;
+    HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+    hipError_t e = ksim_tree_launch(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->stream);
+    if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree launch: %s", hipGetErrorString(e));
+    hipEvent_t ev2 = nullptr;
+    HIPCHK(h, hipEventCreate(&ev2));
+    HIPCHK(h, hipEventRecord(ev2, h->stream));
+    HIPCHK(h, hipEventSynchronize(ev2));
+    float build_ms = 0.f, run_ms = 0.f;
+    HIPCHK(h, hipEventElapsedTime(&build_ms, h->ev0, h->ev1));
+    HIPCHK(h, hipEventElapsedTime(&run_ms, h->ev1, ev2));
+    (void)hipEventDestroy(ev2);
+    if (st) {
+      st->device_ms += build_ms + run_ms;
+      st->kernel_ms += run_ms;
+      st->kernel_launches += 1;
+      st->mode = KSIM_MODE_TREE;
+      st->blocks = 1;
+    }
+#ifdef KSIM_STAMPS
+    {
+      uint64_t d[32];
+      HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
+      HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
+      const double np = (double)(d[8] ? d[8] : 1);
+      fprintf(stderr, "[ksim stamps] tree pods=%llu (%.3f ms) cycles/pod: decide %.0f walk %.0f barrier1 %.0f issue+row+eval+barrier "
+              "%.0f classes %.0f barrier3 %.0f\n", (unsigned long long)d[8], run_ms, d[0] / np, d[1] / np, d[2] / np, d[3] / np,
+              d[4] / np, d[5] / np);
+    }
+#endif
+    int32_t err = 0;
+    HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
+    if (err & 16) return fail(h, KSIM_E_DEVICE, "tree mode: tree inconsistent with its root (0x%x)", err);
+    h->tree_valid = true;
+    if (err & 8) {  // a node's quantities left the exact float64 range: the general kernels from now on
+      h->pfast_off = true;
+      h->tree_valid = false;
+      err &= ~8;
+      HIPCHK(h, hipMemcpy(c.err, &err, 4, hipMemcpyHostToDevice));
+      int64_t cur = 0;
+      HIPCHK(h, hipMemcpy(&cur, c.cursor, 8, hipMemcpyDeviceToHost));
+      j = cur;
+    }
+    i = j;
+  }
+  return KSIM_OK;
+}
+
 int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_node, int32_t* out_reasons,
                   ksim_stats* st) {
   if (!h) return fail(h, KSIM_E_INVAL, "ksim_schedule: null handle");
@@ -605,14 +781,12 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
       return fail(h, KSIM_E_UNSUPPORTED, "node-sharded run stopped: a node's quantities left the exact float64 range");
     }
   } else {
-  int mode = h->cfg.mode;
-  if (mode == KSIM_MODE_AUTO) {
-    int g, l;
-    mode = ((ksim_persistent_config(c.n, &g, &l) && persistent_weights_ok(c)) || pfast_form(h, first, count, &g, &l))
-               ? KSIM_MODE_PERSISTENT
-               : KSIM_MODE_LAUNCH;
-  }
-  int rc = (mode == KSIM_MODE_PERSISTENT) ? run_persistent_mode(h, first, count, st) : run_launch_mode(h, first, count, st);
+  const int mode = h->cfg.mode;
+  int rc = mode == KSIM_MODE_TREE         ? run_tree_mode(h, first, count, st)
+           : mode == KSIM_MODE_AUTO       ? run_auto_mode(h, first, count, st)
+           : mode == KSIM_MODE_PERSISTENT ? run_persistent_mode(h, first, count, st)
+                                          : run_launch_mode(h, first, count, st);
+  if (mode != KSIM_MODE_TREE) h->tree_valid = false;
   if (rc) return rc;
   }
   int32_t err = 0;
@@ -670,6 +844,7 @@ int ksim_assume(ksim_handle* h, int64_t pod, int64_t node) {
   if (!h->have_pods) return fail(h, KSIM_E_STATE, "ksim_assume: nothing loaded");
   if (pod < 0 || pod >= h->n_pods || node < 0 || node >= h->ctx.n) return fail(h, KSIM_E_INVAL, "ksim_assume: out of range");
   HIPCHK(h, hipSetDevice(h->device));
+  h->tree_valid = false;
   hipError_t e = ksim_launch_assume(&h->ctx, pod, node, h->stream);
   if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "assume launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipStreamSynchronize(h->stream));

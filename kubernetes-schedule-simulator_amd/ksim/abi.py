@@ -39,7 +39,7 @@ N_MEM_PRESSURE, N_DISK_PRESSURE = 16, 32
 
 POD_ANY_REQUEST, POD_BEST_EFFORT, POD_NEED_SELECTOR, POD_NEED_TAINTS = 1, 2, 4, 8
 
-MODE_AUTO, MODE_LAUNCH, MODE_PERSISTENT = 0, 1, 2
+MODE_AUTO, MODE_LAUNCH, MODE_PERSISTENT, MODE_TREE = 0, 1, 2, 3
 
 R_NOT_READY, R_OUT_OF_DISK, R_NET_UNAVAIL, R_UNSCHEDULABLE = 0, 1, 2, 3
 R_PODS, R_CPU, R_MEMORY, R_GPU, R_EPHEMERAL = 4, 5, 6, 7, 8

@@ -13,7 +13,7 @@ from workloads import rnd_workload
 
 pytestmark = pytest.mark.gpu
 
-MODES = [abi.MODE_LAUNCH, abi.MODE_AUTO]
+MODES = [abi.MODE_LAUNCH, abi.MODE_AUTO, abi.MODE_TREE]
 
 
 def _sched(nodes, running, pods, preds, prios, mode=abi.MODE_AUTO, **kw):
