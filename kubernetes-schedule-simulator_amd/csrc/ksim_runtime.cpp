@@ -41,10 +41,10 @@ extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, in
                                         const KsimShard* sh, hipStream_t s);
 extern "C" hipError_t ksim_tree_build(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
                                       const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
-                                      hipStream_t s);
+                                      double* ty, hipStream_t s);
 extern "C" hipError_t ksim_tree_launch(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
                                        const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
-                                       hipStream_t s);
+                                       double* ty, hipStream_t s);
 
 namespace {
 
@@ -105,6 +105,7 @@ struct ksim_handle {
   int32_t* t_leaves = nullptr;
   uint64_t* t_levels = nullptr;
   int32_t* t_fit = nullptr;
+  double* t_y = nullptr;
 };
 
 static int fail(ksim_handle* h, int code, const char* fmt, ...) {
@@ -660,7 +661,7 @@ static int tree_ready(ksim_handle* h, bool* ok) {
       int rc;
       if ((rc = dev_alloc(h, &h->t_leaves, (size_t)h->geo.K * h->geo.st[0])) ||
           (rc = dev_alloc(h, &h->t_levels, (size_t)h->geo.level_entries)) ||
-          (rc = dev_alloc(h, &h->t_fit, (size_t)h->geo.K)))
+          (rc = dev_alloc(h, &h->t_fit, (size_t)h->geo.K)) || (rc = dev_alloc(h, &h->t_y, (size_t)2 * c.n)))
         return rc;
     }
   }
@@ -702,13 +703,13 @@ static int run_tree_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stat
     }
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
     if (!h->tree_valid) {
-      hipError_t e = ksim_tree_build(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->stream);
+      hipError_t e = ksim_tree_build(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, h->stream);
       if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree build: %s", hipGetErrorString(e));
     }
     c.first = i;
     c.end = j;
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
-    hipError_t e = ksim_tree_launch(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->stream);
+    hipError_t e = ksim_tree_launch(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, h->stream);
     if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree launch: %s", hipGetErrorString(e));
     hipEvent_t ev2 = nullptr;
     HIPCHK(h, hipEventCreate(&ev2));
@@ -731,9 +732,9 @@ static int run_tree_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stat
       HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
       HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
       const double np = (double)(d[8] ? d[8] : 1);
-      fprintf(stderr, "[ksim stamps] tree pods=%llu (%.3f ms) cycles/pod: decide %.0f walk %.0f barrier1 %.0f issue+row+eval+barrier "
-              "%.0f classes %.0f barrier3 %.0f\n", (unsigned long long)d[8], run_ms, d[0] / np, d[1] / np, d[2] / np, d[3] / np,
-              d[4] / np, d[5] / np);
+      fprintf(stderr, "[ksim stamps] tree pods=%llu (%.3f ms) cycles/pod: decide %.0f walk %.0f row+eval %.0f paths %.0f; changed "
+              "classes %.2f, re-combined paths %.3f per pod\n", (unsigned long long)d[8], run_ms, d[0] / np, d[1] / np,
+              d[2] / np, d[3] / np, d[6] / np, d[7] / np);
     }
 #endif
     int32_t err = 0;

@@ -17,9 +17,8 @@
 #pragma once
 #include <stdint.h>
 
-#define KSIM_TREE_MAX_CLASSES 45  /* 15 updating waves x 3 classes */
+#define KSIM_TREE_MAX_CLASSES 64  /* one lane per class */
 #define KSIM_TREE_MAX_LEVELS 8
-#define KSIM_TREE_THREADS 1024
 
 struct KsimTreeGeo {
   int64_t n;                              // nodes (leaves per class)

@@ -15,11 +15,13 @@
 // in descending (score, name) order = the ix-th from the highest name rank, found by walking
 // down the tree with a suffix count per level.
 //
-// One workgroup of 1024 threads (one CU) runs the whole pod range: wave 0 walks the tree for
-// pod p (top levels in LDS, the rest in L2-resident HBM buffers), then all 16 waves commit: the
-// row update and, for every class, the new leaf and the path to the root (the sibling groups of
-// every level are loaded up front, one memory round trip).  No cross-CU traffic at all, so the
-// per-pod cost is a few dependent L2 round trips, independent of N.
+// One wave on one CU runs the whole pod range with no barrier per pod: it walks the tree for
+// pod p (top levels in LDS, the rest in L2/MALL-resident HBM buffers), commits the row,
+// evaluates the committed node for every class at once (lane c = class c), and updates each
+// changed class's leaf-to-root path lane-parallel with an O(1) parent rule, re-combining a
+// sibling group only where a unique maximum dropped.  A second wave streams pod descriptors
+// into an LDS ring ahead of it.  No cross-CU traffic at all: the per-pod cost is a few
+// dependent L2/MALL round trips plus one vector evaluation, independent of N.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -32,13 +34,10 @@
 
 namespace {
 
-constexpr int TB = KSIM_TREE_THREADS;
-constexpr int TW = TB / 64;                                   // waves
-constexpr int CW = TW - 1;                                    // waves 1..15 update the class paths
-constexpr int CPW = (KSIM_TREE_MAX_CLASSES + CW - 1) / CW;    // classes per wave in the commit
 constexpr int ML = KSIM_TREE_MAX_LEVELS;
+constexpr int LS = 2;  // LDS levels below the root (plan limit)
 constexpr int64_t LIM48 = (int64_t)1 << 48;
-constexpr int64_t TREE_LDS_DEFAULT = 140 * 1024;
+constexpr int64_t TREE_LDS_DEFAULT = 148 * 1024;  // + ~8.6 KB static LDS (classes, pod ring) < 160 KB
 
 struct TreeArgs {
   KsimTreeGeo g;
@@ -57,6 +56,7 @@ struct TreeArgs {
   int32_t* leaves;
   uint64_t* levels;
   int32_t* fitc;  // [K] fit count per class
+  double* ty;     // [2][n] RN(1/alloc cpu), RN(1/alloc mem) (0 for a zero allocatable)
   int64_t first, end;
   uint64_t* counter;
   int64_t* cursor;
@@ -144,6 +144,20 @@ __device__ __forceinline__ int pick_lane(uint32_t c, uint32_t& k) {
   return l;
 }
 
+constexpr int RING = 128;
+// x % c for selectHost's ix (c < 2^24): a float64 quotient corrected by the exact remainder
+// below 2^52, the 64-bit divide beyond
+__device__ __forceinline__ uint32_t mod_u64(uint64_t x, uint32_t c) {
+  if (x < (1ull << 52)) {
+    const double q = trunc((double)x / (double)c);
+    int64_t r = (int64_t)x - (int64_t)q * (int64_t)c;
+    if (r < 0) r += c;
+    else if (r >= (int64_t)c) r -= c;
+    return (uint32_t)r;
+  }
+  return (uint32_t)(x % c);
+}
+
 // ---------------------------------------------------------------- tree build (per call if stale)
 __global__ __launch_bounds__(256) void ksim_tree_leaf_kernel(TreeArgs a) {
   const int64_t st0 = a.g.st[0], tot = (int64_t)a.g.K * st0;
@@ -156,6 +170,10 @@ __global__ __launch_bounds__(256) void ksim_tree_leaf_kernel(TreeArgs a) {
       v = kf64::feval(a.cfg, class_pod(a.cls[k]), load_row(a, i), rmask);
     }
     a.leaves[t] = v;
+    if (k == 0 && i < a.g.n) {
+      a.ty[i] = a.ac[i] ? 1.0 / (double)a.ac[i] : 0.0;
+      a.ty[a.g.n + i] = a.am[i] ? 1.0 / (double)a.am[i] : 0.0;
+    }
   }
 }
 
@@ -204,15 +222,55 @@ __global__ __launch_bounds__(256) void ksim_tree_fit_kernel(TreeArgs a) {
 // ---------------------------------------------------------------- the per-pod loop
 extern __shared__ __attribute__((aligned(16))) uint64_t kt_lds[];  // levels hL..H
 
+// O(1) update of a parent entry P when one child's entry goes from co to cn (entries are
+// (max + 1) << 32 | count at max): false if the parent's maximum vanished from this child and
+// the siblings must be re-combined.
+__device__ __forceinline__ bool parent_rule(uint64_t P, uint64_t co, uint64_t cn, uint64_t& NP) {
+  const uint32_t ph = (uint32_t)(P >> 32), pc = (uint32_t)P;
+  const uint32_t oh = (uint32_t)(co >> 32), nh = (uint32_t)(cn >> 32);
+  if (nh > ph) { NP = cn; return true; }
+  const int64_t c = (int64_t)pc - (oh == ph ? (int64_t)(uint32_t)co : 0) + (nh == ph ? (int64_t)(uint32_t)cn : 0);
+  if (c > 0 || ph == 0) { NP = ((uint64_t)ph << 32) | (uint32_t)c; return true; }
+  return false;
+}
+__device__ __forceinline__ uint64_t leaf_entry(int32_t v) { return v < 0 ? 0ull : ((uint64_t)(v + 1) << 32) | 1u; }
+
+// Wave-cooperative re-combination of entry eh of level h for class c from its children (all
+// already updated this pod).
 template <int M, int GL>
-__global__ __launch_bounds__(TB) void ksim_tree_kernel(TreeArgs a) {
+__device__ __forceinline__ uint64_t rescan(const TreeArgs& a, const int32_t* s_st, const int32_t* s_off, int c, int h,
+                                           int eh, int lane) {
+  constexpr int hL = GL + 1;
+  if (h == 1) {
+    const int32_t* L = a.leaves + c * s_st[0] + eh * 64 * M + lane * M;
+    int32_t lv[M];
+#pragma unroll
+    for (int t = 0; t < M; ++t) lv[t] = ldw(L + t);
+    uint32_t hi, lo;
+    lane_leaves<M>(lv, hi, lo);
+    return wave_comb(hi, lo);
+  }
+  const int idx = s_off[h - 1] + c * s_st[h - 1] + eh * 64 + lane;
+  const uint64_t x = h - 1 >= hL ? kt_lds[idx] : ldw(a.levels + idx);
+  return wave_comb((uint32_t)(x >> 32), (uint32_t)x);
+}
+
+// One workgroup of two waves on one CU.  Wave 0 schedules every pod alone — no barrier on the
+// per-pod path: decide from the class root (LDS), walk down (LDS levels, then global levels and
+// the leaf group), commit the row, evaluate the committed node for every class (lane c = class
+// c), and update each changed class's path lane-parallel with the O(1) parent rule, re-combining
+// a sibling group (wave-cooperative) only where a unique maximum dropped.  Wave 1 streams pod
+// descriptors into an LDS ring ahead of wave 0.
+template <int M, int GL>
+__global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a) {
   __shared__ KsimTreeClass s_cls[KSIM_TREE_MAX_CLASSES];
   __shared__ int32_t s_fit[KSIM_TREE_MAX_CLASSES];   // fit count per class
-  __shared__ int32_t s_vnew[KSIM_TREE_MAX_CLASSES];  // the committed node's new leaf per class
   __shared__ int32_t s_st[ML + 1], s_off[ML + 1];    // stride; offset (LDS for h >= hL, else global)
   __shared__ int32_t s_hist[KSIM_NREASONS];
-  __shared__ int32_t s_sel, s_stop;
-  __shared__ uint64_t s_chg;                         // classes whose leaf changed
+  __shared__ int32_t s_rk[RING];                     // pod ring: tree class
+  __shared__ int64_t s_rd[4][RING];                  // pod ring: add_cpu, add_mem, nz_cpu, nz_mem
+  __shared__ int64_t s_rtag[RING];                   // pod ring: the pod a slot holds
+  __shared__ int64_t s_done;                         // pods wave 0 has finished
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int K = a.g.K, H = a.g.H;
   constexpr int hL = GL + 1;  // levels 1..GL in global memory, hL..H in LDS
@@ -220,8 +278,8 @@ __global__ __launch_bounds__(TB) void ksim_tree_kernel(TreeArgs a) {
   const int n = (int)a.g.n;
   const int gbase = (int)a.g.goff[hL];
   const int lds_entries = (int)a.g.lds_entries;
-  for (int t = tid; t < lds_entries; t += TB) kt_lds[t] = a.levels[gbase + t];
-  for (int t = tid; t < K; t += TB) {
+  for (int t = tid; t < lds_entries; t += 128) kt_lds[t] = a.levels[gbase + t];
+  for (int t = tid; t < K; t += 128) {
     s_cls[t] = a.cls[t];
     s_fit[t] = a.fitc[t];
   }
@@ -229,76 +287,101 @@ __global__ __launch_bounds__(TB) void ksim_tree_kernel(TreeArgs a) {
     s_st[tid] = (int)a.g.st[tid];
     s_off[tid] = tid >= hL ? (int)(a.g.goff[tid] - gbase) : (int)a.g.goff[tid];
   }
-  if (tid == 0) s_stop = 0;
+  for (int t = tid; t < RING; t += 128) s_rtag[t] = -1;
+  if (tid == 0) s_done = a.first;
+  __syncthreads();
+
+  if (wv == 1) {  // ---- pod ring producer: 64 pods at a time, at most RING ahead of wave 0
+    for (int64_t q0 = a.first; q0 < a.end; q0 += 64) {
+      uint32_t spins = 0;
+      int64_t done;
+      while ((done = __hip_atomic_load(&s_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < q0 + 64 - RING) {
+        __builtin_amdgcn_s_sleep(2);
+        if (++spins > (1u << 28)) { if (lane == 0) atomicOr(a.err, 32); return; }
+      }
+      if (done == INT64_MAX) return;  // wave 0 stopped early
+      const int64_t q = q0 + lane;
+      if (q < a.end) {
+        const int r = (int)(q & (RING - 1));
+        const ksim_pod& P = a.pods[q];
+        s_rk[r] = a.tcls[q];
+        s_rd[0][r] = P.add_cpu; s_rd[1][r] = P.add_mem; s_rd[2][r] = P.nz_cpu; s_rd[3][r] = P.nz_mem;
+        __hip_atomic_store(&s_rtag[r], q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
+    return;
+  }
+
+  // ---- wave 0: the scheduler
+  const int st0 = s_st[0];
+  const uint64_t* root = kt_lds + s_off[H];  // st[H] == 1: one root per class
   uint64_t counter = ldw(a.counter);
 #ifdef KSIM_STAMPS
   uint64_t ts_acc[8] = {}, ts_prev = __builtin_amdgcn_s_memtime();
 #endif
-  __syncthreads();
-  const int st0 = s_st[0];
-  const uint64_t* root = kt_lds + s_off[H];  // st[H] == 1: one root per class
   int hist_cls = -1;
   int64_t p = a.first;
-  int k_next = a.tcls[p];
-  int64_t row_j = -1, row_c = 0, row_m = 0, row_zc = 0, row_zm = 0;  // thread 0: deferred row store
-  int32_t row_n = 0;
   bool stop = false;
   while (p < a.end && !stop) {
-    const int k = k_next;
-    if (p + 1 < a.end) k_next = a.tcls[p + 1];
+    const int rs = (int)(p & (RING - 1));
+    {
+      uint32_t spins = 0;
+      while (__hip_atomic_load(&s_rtag[rs], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != p) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 28)) { if (lane == 0) atomicOr(a.err, 32); stop = true; break; }
+      }
+      if (stop) break;
+    }
+    const int k = s_rk[rs];
+    const int64_t pc = s_rd[0][rs], pm = s_rd[1][rs], pzc = s_rd[2][rs], pzm = s_rd[3][rs];  // commit deltas
     const uint32_t F = (uint32_t)s_fit[k];
     if (F == 0) {  // FitError: no commit, lastNodeIndex unchanged
-      if (tid == 0) a.out_node[p] = -1;
+      if (lane == 0) a.out_node[p] = -1;
       if (a.collect) {
         if (hist_cls != k) {  // histogram of first-failing-predicate reasons over every node
-          if (tid < KSIM_NREASONS) s_hist[tid] = 0;
-          if (tid == 0 && row_j >= 0) {
-            a.rc[row_j] = row_c; a.rm[row_j] = row_m; a.zc[row_j] = row_zc; a.zm[row_j] = row_zm; a.count[row_j] = row_n;
-            row_j = -1;
-          }
-          stores_done();
-          __syncthreads();
+          if (lane < KSIM_NREASONS) s_hist[lane] = 0;
           const kf64::FPod P = class_pod(s_cls[k]);
-          for (int i0 = 0; i0 < n; i0 += TB) {
-            const int i = i0 + tid;
+          for (int i0 = 0; i0 < n; i0 += 64) {
+            const int i = i0 + lane;
             uint32_t rm = 0;
             if (i < n) (void)kf64::feval(a.cfg, P, load_row(a, i), rm);
             if (__ballot(rm != 0))
               for (int r = 0; r < KSIM_NREASONS; ++r) {
                 const int nr = __popcll(__ballot((rm >> r) & 1u));
-                if (lane == 0 && nr) atomicAdd(&s_hist[r], nr);
+                if (lane == 0 && nr) s_hist[r] += nr;
               }
           }
-          __syncthreads();
           hist_cls = k;
         }
-        if (tid < KSIM_NREASONS) a.out_reasons[p * KSIM_NREASONS + tid] = s_hist[tid];
+        if (lane < KSIM_NREASONS) a.out_reasons[p * KSIM_NREASONS + lane] = s_hist[lane];
       }
       ++p;
+      if (lane == 0) __hip_atomic_store(&s_done, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       continue;
     }
     const uint64_t rt = root[k];
     const bool single = F == 1;
     uint32_t kth = 0;
     if (!single) {
-      const uint32_t C = (uint32_t)rt;
-      kth = (uint32_t)(counter % C);
+      kth = mod_u64(counter, (uint32_t)rt);
       ++counter;
     }
     const uint32_t Sp = (uint32_t)(rt >> 32);  // maximum score + 1
     TSTAMP(0);
-    if (wv == 0) {  // walk down: entry e of level h, kth match from the top
-      int e = 0;
-      bool bad = false;
-      for (int h = H - 1; h >= 1; --h) {
-        const int idx = s_off[h] + k * s_st[h] + e * 64 + lane;
-        const uint64_t v = h >= hL ? kt_lds[idx] : ldw(a.levels + idx);
-        const uint32_t vh = (uint32_t)(v >> 32);
-        const uint32_t c = single ? (vh != 0u ? 1u : 0u) : (vh == Sp ? (uint32_t)v : 0u);
-        const int l = pick_lane(c, kth);
-        bad |= l < 0;
-        e = e * 64 + (l < 0 ? 0 : l);
-      }
+    // ---- walk down: entry e of level h, kth match from the top ----
+    int e = 0;
+    bool bad = false;
+    for (int h = H - 1; h >= 1; --h) {
+      const int idx = s_off[h] + k * s_st[h] + e * 64 + lane;
+      const uint64_t v = h >= hL ? kt_lds[idx] : ldw(a.levels + idx);
+      const uint32_t vh = (uint32_t)(v >> 32);
+      const uint32_t c = single ? (vh != 0u ? 1u : 0u) : (vh == Sp ? (uint32_t)v : 0u);
+      const int l = pick_lane(c, kth);
+      bad |= l < 0;
+      e = e * 64 + (l < 0 ? 0 : l);
+    }
+    int j;
+    {
       const int32_t* L = a.leaves + k * st0 + e * G0 + lane * M;
       int32_t lv[M];
 #pragma unroll
@@ -319,156 +402,137 @@ __global__ __launch_bounds__(TB) void ksim_tree_kernel(TreeArgs a) {
         }
       }
       const int lsel = l < 0 ? 0 : l;
-      const int node = e * G0 + lsel * M + __builtin_amdgcn_readlane(sel, lsel);
-      if (lane == 0) {
-        if (bad || node >= n) atomicOr(a.err, 16);  // tree inconsistent with its root
-        s_sel = node < n ? node : 0;
-        a.out_node[p] = node;
+      j = e * G0 + lsel * M + __builtin_amdgcn_readlane(sel, lsel);
+      if (bad || j >= n) {  // tree inconsistent with its root
+        if (lane == 0) atomicOr(a.err, 16);
+        j = 0;
       }
     }
+    if (lane == 0) a.out_node[p] = j;
     TSTAMP(1);
-    if (tid == 0 && row_j >= 0) {  // the previous pod's row (every wave has read it)
-      a.rc[row_j] = row_c; a.rm[row_j] = row_m; a.zc[row_j] = row_zc; a.zm[row_j] = row_zm; a.count[row_j] = row_n;
-    }
-    stores_done();
-    __syncthreads();
-    TSTAMP(2);
     // ---- commit (Scheduler.assume -> NodeInfo.AddPod, node_info.go:318-341) ----
-    const int j = s_sel;
     const int e1 = j / G0;
-    const int lj = (j - e1 * G0) / M, sj = j % M;
-    // leaf groups and global-level sibling groups of this wave's classes (waves 1..15), issued
-    // now so they arrive while wave 0 evaluates the new row
-    int32_t lv[CPW][M];
-    uint64_t gsib[CPW][GL > 0 ? GL : 1];
+    const bool cl = lane < K;
+    const int cc = cl ? lane : 0;  // lane c = class c
+    const int64_t nrc = ldw(a.rc + j) + pc, nrm = ldw(a.rm + j) + pm;
+    const int64_t nzc = ldw(a.zc + j) + pzc, nzm = ldw(a.zm + j) + pzm;
+    const int32_t ncnt = ldw(a.count + j) + 1;
+    const int32_t vold = cl ? ldw(a.leaves + cc * st0 + j) : -1;
+    uint64_t gold[GL > 0 ? GL : 1];  // old global-level entries on the path
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const int kc = wv - 1 + q * CW;
-      if (wv > 0 && kc < K) {
-        const int32_t* L = a.leaves + kc * st0 + e1 * G0 + lane * M;
-#pragma unroll
-        for (int t = 0; t < M; ++t) lv[q][t] = ldw(L + t);
-        int e = e1;
-#pragma unroll
-        for (int h = 1; h <= GL; ++h) {
-          gsib[q][h - 1] = ldw(a.levels + s_off[h] + kc * s_st[h] + (e >> 6) * 64 + lane);
-          e >>= 6;
-        }
-      }
+    for (int h = 1; h <= GL; ++h) gold[h - 1] = ldw(a.levels + s_off[h] + cc * s_st[h] + (e1 >> (6 * (h - 1))));
+    kf64::FRow nr;
+    nr.ac = (double)a.ac[j];
+    nr.am = (double)a.am[j];
+    nr.yc = a.ty[j];
+    nr.ym = a.ty[n + j];
+    nr.rc = (double)nrc; nr.rm = (double)nrm; nr.zc = (double)nzc; nr.zm = (double)nzm;
+    nr.allowed = a.allowed[j];
+    nr.count = ncnt;
+    nr.fl = a.fl[j];
+    uint32_t rmask;
+    const int32_t vnew = kf64::feval(a.cfg, class_pod(s_cls[cc]), nr, rmask);
+    if (lane == 0) {
+      a.rc[j] = nrc; a.rm[j] = nrm; a.zc[j] = nzc; a.zm[j] = nzm; a.count[j] = ncnt;
     }
-    if (wv == 0) {  // the new row and every class's new leaf (lane c = class c)
-      const ksim_pod& P = a.pods[p];
-      const int64_t nrc = ldw(a.rc + j) + P.add_cpu, nrm = ldw(a.rm + j) + P.add_mem;
-      const int64_t nzc = ldw(a.zc + j) + P.nz_cpu, nzm = ldw(a.zm + j) + P.nz_mem;
-      const int32_t ncnt = ldw(a.count + j) + 1;
-      const int32_t vold = lane < K ? ldw(a.leaves + lane * st0 + j) : -1;
-      kf64::FRow nr;
-      nr.ac = (double)a.ac[j];
-      nr.am = (double)a.am[j];
-      nr.yc = nr.ac != 0.0 ? 1.0 / nr.ac : 0.0;
-      nr.ym = nr.am != 0.0 ? 1.0 / nr.am : 0.0;
-      nr.rc = (double)nrc; nr.rm = (double)nrm; nr.zc = (double)nzc; nr.zm = (double)nzm;
-      nr.allowed = a.allowed[j];
-      nr.count = ncnt;
-      nr.fl = a.fl[j];
-      uint32_t rmask;
-      const int32_t vnew = kf64::feval(a.cfg, class_pod(s_cls[lane < K ? lane : 0]), nr, rmask);
-      const bool chg = lane < K && vnew != vold;
-      const uint64_t cm = __ballot(chg);
-      if (lane < K) {
-        s_vnew[lane] = vnew;
-        s_fit[lane] += (vnew >= 0 ? 1 : 0) - (vold >= 0 ? 1 : 0);
-      }
-      if (chg) a.leaves[lane * st0 + j] = vnew;
-      if (lane == 0) {
-        s_chg = cm;
-        // quantities must stay exact in float64 (ksim_f64.h): stop after this pod otherwise
-        s_stop = nrc >= LIM48 || nrm >= LIM48 || nzc >= LIM48 || nzm >= LIM48;
-        row_j = j; row_c = nrc; row_m = nrm; row_zc = nzc; row_zm = nzm; row_n = ncnt;
-      }
+    const bool chg = cl && vnew != vold;
+    TSTAMP(2);
+    int resc_h = 0;       // level whose entry must be re-combined (0: none)
+    uint64_t resc_old = 0;
+    if (chg) {
+      a.leaves[cc * st0 + j] = vnew;
+      s_fit[cc] += (vnew >= 0 ? 1 : 0) - (vold >= 0 ? 1 : 0);
     }
-    __syncthreads();
-    TSTAMP(3);
-    const uint64_t chg = s_chg;
+    {
+      bool act = chg;
+      uint64_t co = leaf_entry(vold), cn = leaf_entry(vnew);
 #pragma unroll
-    for (int q = 0; q < CPW; ++q) {
-      const int kc = wv - 1 + q * CW;
-      if (wv > 0 && kc < K && ((chg >> kc) & 1ull)) {  // the path from leaf j up, until an entry is unchanged
-        const int32_t v = s_vnew[kc];
-        if (lane == lj) {
-#pragma unroll
-          for (int t = 0; t < M; ++t)
-            if (t == sj) lv[q][t] = v;
-        }
-        uint32_t hi, lo;
-        lane_leaves<M>(lv[q], hi, lo);
-        uint64_t acc = wave_comb(hi, lo);
-        int e = e1;
-        bool done = false;
-#pragma unroll
-        for (int h = 1; h <= GL; ++h) {  // global levels (h < hL <= H)
-          if (!done) {
-            const int sl = e & 63;
-            const uint64_t old = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(gsib[q][h - 1] >> 32), sl) << 32) |
-                                 (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)gsib[q][h - 1], sl);
-            if (old == acc) {
-              done = true;
+      for (int h = 1; h <= ML; ++h) {
+        if (h <= H && __ballot(act)) {
+          const int eh = e1 >> (6 * (h - 1));
+          if (act) {
+            const uint64_t P = h <= GL ? gold[h <= GL ? h - 1 : 0] : kt_lds[s_off[h] + cc * s_st[h] + eh];
+            uint64_t NP;
+            if (!parent_rule(P, co, cn, NP)) {
+              resc_h = h;
+              resc_old = P;
+              act = false;
+            } else if (NP == P) {
+              act = false;
             } else {
-              if (lane == 0) a.levels[s_off[h] + kc * s_st[h] + e] = acc;
-              const uint64_t x = lane == sl ? acc : gsib[q][h - 1];
-              acc = wave_comb((uint32_t)(x >> 32), (uint32_t)x);
-              e >>= 6;
+              if (h <= GL) a.levels[s_off[h] + cc * s_st[h] + eh] = NP;
+              else kt_lds[s_off[h] + cc * s_st[h] + eh] = NP;
+              co = P;
+              cn = NP;
             }
           }
         }
-        if (!done) {
-          for (int h = hL; h <= H; ++h) {  // LDS levels
-            const int base = s_off[h] + kc * s_st[h];
-            if (kt_lds[base + e] == acc) break;
-            if (lane == 0) kt_lds[base + e] = acc;
-            if (h == H) break;
-            const uint64_t x = lane == (e & 63) ? acc : kt_lds[base + (e >> 6) * 64 + lane];
-            acc = wave_comb((uint32_t)(x >> 32), (uint32_t)x);
-            e >>= 6;
-          }
-        }
       }
     }
-    TSTAMP(4);
+    // the rare paths whose unique maximum dropped: re-combine, then continue up (wave-wide)
+    const uint64_t rmk = __ballot(resc_h != 0);
+    if (rmk) stores_done();  // the leaves / entries just written are read back
+    for (uint64_t rm = rmk; rm; rm &= rm - 1) {
+      const int c = __builtin_ctzll(rm);
+      int h = __builtin_amdgcn_readlane(resc_h, c);
+      uint64_t oldv = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(resc_old >> 32), c) << 32) |
+                      (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)resc_old, c);
+      uint64_t newv = rescan<M, GL>(a, s_st, s_off, c, h, e1 >> (6 * (h - 1)), lane);
+      while (newv != oldv) {
+        const int eh = e1 >> (6 * (h - 1));
+        const int idx = s_off[h] + c * s_st[h] + eh;
+        if (lane == 0) {
+          if (h <= GL) a.levels[idx] = newv;
+          else kt_lds[idx] = newv;
+        }
+        if (h == H) break;
+        ++h;
+        const int pidx = s_off[h] + c * s_st[h] + (e1 >> (6 * (h - 1)));
+        const uint64_t P = h <= GL ? ldw(a.levels + pidx) : kt_lds[pidx];
+        uint64_t NP;
+        if (!parent_rule(P, oldv, newv, NP)) {
+          stores_done();  // the children just written are read back by the re-combination
+          NP = rescan<M, GL>(a, s_st, s_off, c, h, e1 >> (6 * (h - 1)), lane);
+        }
+        oldv = P;
+        newv = NP;
+      }
+    }
+    TSTAMP(3);
+#ifdef KSIM_STAMPS
+    ts_acc[6] += __popcll(__ballot(chg));
+    ts_acc[7] += __popcll(__ballot(resc_h != 0));
+#endif
     hist_cls = -1;
-    stop = s_stop != 0;
+    // quantities must stay exact in float64 (ksim_f64.h): stop after this pod otherwise
+    stop = nrc >= LIM48 || nrm >= LIM48 || nzc >= LIM48 || nzm >= LIM48;
     ++p;
-    stores_done();
-    __syncthreads();
-    TSTAMP(5);
+    if (lane == 0) __hip_atomic_store(&s_done, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
-  if (tid == 0 && row_j >= 0) {
-    a.rc[row_j] = row_c; a.rm[row_j] = row_m; a.zc[row_j] = row_zc; a.zm[row_j] = row_zm; a.count[row_j] = row_n;
-  }
+  if (lane == 0) __hip_atomic_store(&s_done, INT64_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   stores_done();
-  __syncthreads();
-  for (int t = tid; t < lds_entries; t += TB) a.levels[gbase + t] = kt_lds[t];
-  for (int t = tid; t < K; t += TB) a.fitc[t] = s_fit[t];
-  if (tid == 0) {
+  for (int t = lane; t < lds_entries; t += 64) a.levels[gbase + t] = kt_lds[t];
+  for (int t = lane; t < K; t += 64) a.fitc[t] = s_fit[t];
+  if (lane == 0) {
     __hip_atomic_store(a.counter, counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(a.cursor, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (stop) atomicOr(a.err, 8);
 #ifdef KSIM_STAMPS
-    for (int k = 0; k < 6; ++k) atomicAdd((unsigned long long*)&a.dbg[k], (unsigned long long)ts_acc[k]);
+    for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&a.dbg[k], (unsigned long long)ts_acc[k]);
     atomicAdd((unsigned long long*)&a.dbg[8], (unsigned long long)(p - a.first));
 #endif
   }
 }
 
 TreeArgs make_args(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls, const int32_t* tcls,
-                   int32_t* leaves, uint64_t* levels, int32_t* fitc) {
+                   int32_t* leaves, uint64_t* levels, int32_t* fitc, double* ty) {
   TreeArgs a{};
   a.g = *g;
   a.ac = c->alloc_cpu; a.am = c->alloc_mem;
   a.rc = c->req_cpu; a.rm = c->req_mem; a.zc = c->nz_cpu; a.zm = c->nz_mem;
   a.allowed = c->allowed_pods; a.count = c->pod_count; a.fl = c->flags;
   a.pods = c->pods; a.tcls = tcls; a.cls = cls;
-  a.leaves = leaves; a.levels = levels; a.fitc = fitc;
+  a.leaves = leaves; a.levels = levels; a.fitc = fitc; a.ty = ty;
   a.first = c->first; a.end = c->end;
   a.counter = c->counter; a.cursor = c->cursor; a.out_node = c->out_node; a.out_reasons = c->out_reasons;
   a.err = c->err;
@@ -508,6 +572,7 @@ extern "C" int ksim_tree_plan(int64_t n, int32_t K, int64_t budget, int32_t forc
       hL = h;
     }
     if (hL > H || hL - 1 > (m == 4 ? 0 : m == 2 ? 1 : 2)) continue;  // the instantiated <M, GL> forms (no scratch)
+    if (H - hL > LS) continue;
     if ((int64_t)K * g.st[0] >= INT32_MAX) continue;  // 32-bit indices in the kernel
     g.hL = hL;
     g.goff[1] = 0;
@@ -525,8 +590,8 @@ extern "C" int ksim_tree_plan(int64_t n, int32_t K, int64_t budget, int32_t forc
 
 extern "C" hipError_t ksim_tree_build(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
                                       const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
-                                      hipStream_t s) {
-  const TreeArgs a = make_args(c, g, cls, tcls, leaves, levels, fitc);
+                                      double* ty, hipStream_t s) {
+  const TreeArgs a = make_args(c, g, cls, tcls, leaves, levels, fitc, ty);
   const int64_t tl = (int64_t)g->K * g->st[0];
   hipLaunchKernelGGL(ksim_tree_leaf_kernel, dim3((unsigned)std::min<int64_t>((tl + 255) / 256, 8192)), dim3(256), 0, s, a);
   for (int h = 1; h <= g->H; ++h) {
@@ -539,11 +604,11 @@ extern "C" hipError_t ksim_tree_build(const KsimCtx* c, const KsimTreeGeo* g, co
 
 extern "C" hipError_t ksim_tree_launch(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
                                        const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
-                                       hipStream_t s) {
-  const TreeArgs a = make_args(c, g, cls, tcls, leaves, levels, fitc);
+                                       double* ty, hipStream_t s) {
+  const TreeArgs a = make_args(c, g, cls, tcls, leaves, levels, fitc, ty);
   const size_t lds = (size_t)g->lds_entries * sizeof(uint64_t);
 #define KT_CASE(MM, GG) \
-  if (g->m == MM && g->hL == GG + 1) { hipLaunchKernelGGL((ksim_tree_kernel<MM, GG>), dim3(1), dim3(TB), lds, s, a); return hipGetLastError(); }
+  if (g->m == MM && g->hL == GG + 1) { hipLaunchKernelGGL((ksim_tree_kernel<MM, GG>), dim3(1), dim3(128), lds, s, a); return hipGetLastError(); }
   KT_CASE(1, 0) KT_CASE(1, 1) KT_CASE(1, 2) KT_CASE(2, 0) KT_CASE(2, 1) KT_CASE(4, 0)
 #undef KT_CASE
   return hipErrorInvalidValue;
