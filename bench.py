@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--nodes", type=int, default=None, help="default: c3 100,000, c2 5,000, c4 1,000,000")
     ap.add_argument("--pods", type=int, default=None, help="queue length (default: c3 1M, c2 50k, c4 as needed)")
     ap.add_argument("--mode", default="auto", choices=["auto", "launch", "persistent", "tree"])
+    ap.add_argument("--no-tree", dest="tree", action="store_false",
+                    help="skip the tree-mode line measured beside the scan (c3/c4)")
     ap.add_argument("--cpu-sample", type=int, default=3000, help="pods in the CPU-baseline prefix (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"],
@@ -195,6 +197,36 @@ def node_sharded(a, D, cl, preds, prios, ref):
     return res
 
 
+def tree_mode(a, cl, preds, prios, device, ref):
+    """The same queue through tree mode (KSIM_MODE_TREE, SURVEY.md §8f f4: incremental
+    per-pod-class selection trees on one CU, O(classes x log N) per pod instead of the O(N)
+    scan): pods/s over the same timed steps, and its placements against the scan's."""
+    import numpy as np
+    from ksim import abi, scheduler
+    g = scheduler.GenericScheduler(cl, preds, prios, device=device, mode=abi.MODE_TREE, collect_reasons=False)
+    outs, first = [], 0
+    for _ in range(a.warmup):
+        outs.append(g.schedule(first, a.batch)[0])
+        first += a.batch
+    kms, mode_used = 0.0, 0
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        o, _, st = g.schedule(first, a.batch)
+        outs.append(o)
+        first += a.batch
+        kms += st.kernel_ms
+        mode_used = st.mode
+    el = time.perf_counter() - t0
+    out = np.concatenate(outs)
+    pods = a.steps * a.batch
+    return {"value": round(pods / el, 1), "unit": "pods/s", "ms_per_step": round(el * 1e3 / a.steps, 4),
+            "kernel_us_per_pod": round(kms * 1e3 / pods, 3),
+            "mode": {3: "tree"}.get(mode_used, str(mode_used)),
+            "parity_vs_scan": {"pods": int(len(out)), "match": bool(np.array_equal(out, ref[:len(out)]))},
+            "note": "one wave on one CU per cluster; placements identical to the scan's; the headline "
+                    "node-evals/s metric is defined on the full scan, so this is reported beside it"}
+
+
 def main():
     a = parse()
     if a.workload == "c5":
@@ -268,6 +300,10 @@ def main():
         avg_launch_s = kernel_ms / 1e3 / max(launches, 1)
     achieved = W["bytes"] * n * pods_per_launch / avg_launch_s / 1e9
 
+    tree = None
+    if rank == 0 and a.tree and a.mode != "tree" and a.workload in ("c3", "c4"):
+        tree = tree_mode(a, cl, preds, prios, local, placements)
+
     cpu = None
     parity = None
     if rank == 0 and a.cpu_sample > 0:
@@ -310,11 +346,15 @@ def main():
                          "traffic": pmc_traffic(a.workload + ("" if mode_used == abi.MODE_PERSISTENT else "_launch"),
                                                 n * pods_per_launch),
                          "traffic_unit": "GB per launch (PMC)", "bytes_per_node_eval": W["bytes"],
-                         "avg_launch_us": round(avg_launch_s * 1e6, 3), "pods_per_launch": pods_per_launch},
+                         "avg_launch_us": round(avg_launch_s * 1e6, 3), "pods_per_launch": pods_per_launch,
+                         **({"note": "tree mode reads O(classes x log N) bytes per pod: achieved is the scan-equivalent "
+                                     "rate, not HBM traffic"} if mode_used == abi.MODE_TREE else {})},
             "cpu_baseline": cpu,
             "parity": parity,
             "pods_bound": bound,
         }
+        if tree is not None:
+            line["tree_mode"] = tree
         if sharded is not None:
             line["node_sharded"] = sharded
             if a.shard == "nodes" and "value" in sharded:  # the one node-sharded cluster as the headline

@@ -87,6 +87,21 @@ template <class T>
 __device__ __forceinline__ T ldw(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// a lane's M consecutive leaves in one load (nontemporal: served by L2, like ldw)
+typedef int32_t v2i __attribute__((ext_vector_type(2)));
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+template <int M>
+__device__ __forceinline__ void ld_leaves(const int32_t* L, int32_t* lv) {
+  if constexpr (M == 4) {
+    const v4i x = __builtin_nontemporal_load((const v4i*)L);
+    lv[0] = x.x; lv[1] = x.y; lv[2] = x.z; lv[3] = x.w;
+  } else if constexpr (M == 2) {
+    const v2i x = __builtin_nontemporal_load((const v2i*)L);
+    lv[0] = x.x; lv[1] = x.y;
+  } else {
+    lv[0] = ldw(L);
+  }
+}
 // every store of this wave has reached L2 (gfx9 counts stores in vmcnt)
 __device__ __forceinline__ void stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -242,10 +257,8 @@ __device__ __forceinline__ uint64_t rescan(const TreeArgs& a, const int32_t* s_s
                                            int eh, int lane) {
   constexpr int hL = GL + 1;
   if (h == 1) {
-    const int32_t* L = a.leaves + c * s_st[0] + eh * 64 * M + lane * M;
     int32_t lv[M];
-#pragma unroll
-    for (int t = 0; t < M; ++t) lv[t] = ldw(L + t);
+    ld_leaves<M>(a.leaves + c * s_st[0] + eh * 64 * M + lane * M, lv);
     uint32_t hi, lo;
     lane_leaves<M>(lv, hi, lo);
     return wave_comb(hi, lo);
@@ -306,7 +319,8 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a) {
         const ksim_pod& P = a.pods[q];
         s_rk[r] = a.tcls[q];
         s_rd[0][r] = P.add_cpu; s_rd[1][r] = P.add_mem; s_rd[2][r] = P.nz_cpu; s_rd[3][r] = P.nz_mem;
-        __hip_atomic_store(&s_rtag[r], q, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");  // LDS only: no wait on global stores
+        __hip_atomic_store(&s_rtag[r], q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       }
     }
     return;
@@ -326,11 +340,12 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a) {
     const int rs = (int)(p & (RING - 1));
     {
       uint32_t spins = 0;
-      while (__hip_atomic_load(&s_rtag[rs], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != p) {
+      while (__hip_atomic_load(&s_rtag[rs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != p) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > (1u << 28)) { if (lane == 0) atomicOr(a.err, 32); stop = true; break; }
       }
       if (stop) break;
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     }
     const int k = s_rk[rs];
     const int64_t pc = s_rd[0][rs], pm = s_rd[1][rs], pzc = s_rd[2][rs], pzm = s_rd[3][rs];  // commit deltas
@@ -382,10 +397,8 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a) {
     }
     int j;
     {
-      const int32_t* L = a.leaves + k * st0 + e * G0 + lane * M;
       int32_t lv[M];
-#pragma unroll
-      for (int t = 0; t < M; ++t) lv[t] = ldw(L + t);
+      ld_leaves<M>(a.leaves + k * st0 + e * G0 + lane * M, lv);
       uint32_t c = 0;
 #pragma unroll
       for (int t = 0; t < M; ++t) c += single ? (lv[t] >= 0) : ((uint32_t)(lv[t] + 1) == Sp);
