@@ -63,6 +63,8 @@ def parse():
                          "ports and taints; c4: 1M nodes; c5: the 4,096-scenario policy sweep")
     ap.add_argument("--scenarios", type=int, default=4096, help="c5: total scenarios (split across ranks)")
     ap.add_argument("--sweep-nodes", type=int, default=20_000, help="c5: nodes per scenario")
+    ap.add_argument("--sweep-form", default="auto", choices=["auto", "scan"],
+                    help="c5: auto = tree form when eligible; scan = the per-scenario scan kernel")
     ap.add_argument("--sweep-pods", type=int, default=5000, help="c5: pods scheduled in every scenario")
     ap.add_argument("--shard", default="replicas", choices=["replicas", "nodes", "none"],
                     help="N>1 headline: replicas (weak) or one node-sharded cluster (strong); "
@@ -376,6 +378,8 @@ def main_c5(a):
     import torch
     from ksim import scheduler, synth
 
+    if a.sweep_form == "scan":
+        os.environ["KSIM_SWEEP_SCAN"] = "1"
     D = Dist(a)
     world, rank, local = D.world, D.rank, D.local
     barrier_sync = D.sync
@@ -393,6 +397,7 @@ def main_c5(a):
     for _ in range(a.steps):
         out, ctr, st = g.sweep(mine, 0, a.sweep_pods)
         kernel_ms += st.kernel_ms
+    tree = st.mode == 3  # KSIM_MODE_TREE: one tree-mode wave per scenario (ksim_tree.hip)
     barrier_sync()
     elapsed = D.allmax(time.perf_counter() - t0)
     n = cl.n_nodes
@@ -432,12 +437,16 @@ def main_c5(a):
             "config": {"workload": "C5: %d scenarios (wLR 1..16 x wBRA 1..16 x wMR 0..15) x %d pods on %d nodes"
                                    % (len(scen), a.sweep_pods, n),
                        "nodes": n, "scenarios": len(scen), "scenarios_per_rank": len(mine),
-                       "pods_per_scenario": a.sweep_pods, "parallelism": "scenario-parallel x%d" % world},
+                       "pods_per_scenario": a.sweep_pods, "parallelism": "scenario-parallel x%d" % world,
+                       "form": "tree (one tree-mode wave per scenario)" if tree else "scan (one workgroup per scenario)"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic("c5", evals_per_launch), "traffic_unit": "GB per launch (PMC)",
+                         "traffic": None if tree else pmc_traffic("c5", evals_per_launch),
+                         "traffic_unit": "GB per launch (PMC)",
                          "bytes_per_node_eval": BYTES_PER_NODE_EVAL, "avg_launch_us": round(avg_launch_s * 1e6, 3),
-                         "node_evals_per_launch": evals_per_launch},
+                         "node_evals_per_launch": evals_per_launch,
+                         **({"note": "tree form reads O(classes x log N) bytes per pod: achieved is the "
+                                     "scan-equivalent rate"} if tree else {})},
             "cpu_baseline": cpu,
             "parity": parity,
         }

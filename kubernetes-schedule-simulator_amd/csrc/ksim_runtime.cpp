@@ -19,6 +19,7 @@
 #include "ksim_common.h"
 #include "ksim_sweep.h"
 #include "ksim_tree.h"
+#include "ksim_f64.h"
 
 extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* fit, uint32_t* reasons, int64_t* score,
@@ -41,10 +42,11 @@ extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, in
                                         const KsimShard* sh, hipStream_t s);
 extern "C" hipError_t ksim_tree_build(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
                                       const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
-                                      double* ty, hipStream_t s);
+                                      double* ty, const KsimTreeSweep* sw, hipStream_t s);
+extern "C" hipError_t ksim_tree_sweep_init(const KsimCtx* c, const KsimTreeSweep* sw, hipStream_t s);
 extern "C" hipError_t ksim_tree_launch(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
                                        const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
-                                       double* ty, hipStream_t s);
+                                       double* ty, const KsimTreeSweep* sw, hipStream_t s);
 
 namespace {
 
@@ -106,6 +108,8 @@ struct ksim_handle {
   uint64_t* t_levels = nullptr;
   int32_t* t_fit = nullptr;
   double* t_y = nullptr;
+  void* swt_scratch = nullptr;  // tree sweep: per-scenario columns, trees, counters, outputs
+  size_t swt_bytes = 0;
 };
 
 static int fail(ksim_handle* h, int code, const char* fmt, ...) {
@@ -703,13 +707,13 @@ static int run_tree_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stat
     }
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
     if (!h->tree_valid) {
-      hipError_t e = ksim_tree_build(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, h->stream);
+      hipError_t e = ksim_tree_build(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, nullptr, h->stream);
       if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree build: %s", hipGetErrorString(e));
     }
     c.first = i;
     c.end = j;
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
-    hipError_t e = ksim_tree_launch(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, h->stream);
+    hipError_t e = ksim_tree_launch(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, nullptr, h->stream);
     if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree launch: %s", hipGetErrorString(e));
     hipEvent_t ev2 = nullptr;
     HIPCHK(h, hipEventCreate(&ev2));
@@ -907,6 +911,106 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
       return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: quantities may leave the exact float64 range (2^48)");
   }
   int rc;
+  // Tree form (ksim_tree.hip): one tree-mode wave per scenario, scenarios spread over the CUs.
+  if (!getenv("KSIM_SWEEP_SCAN") && h->n_tcls > 0 && n < ((int64_t)1 << 24) && !h->pfast_off) {
+    KsimTreeGeo g{};
+    // a small LDS plan: several scenarios' waves per CU hide each other's memory latency
+    const char* lb = getenv("KSIM_SWEEP_LDS");
+    if (ksim_tree_plan(n, h->n_tcls, lb ? atoll(lb) : 24 * 1024, 0, &g) || ksim_tree_plan(n, h->n_tcls, 0, 0, &g)) {
+      if (!h->t_y && (rc = dev_alloc(h, &h->t_y, (size_t)2 * n))) return rc;
+      auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+      const size_t N = (size_t)n, P = (size_t)count, K = (size_t)g.K;
+      const size_t per = al(4 * N * 8) + al(N * 4) + al(K * g.st[0] * 4) + al(g.level_entries * 8) + al(K * 4) + al(8) +
+                         al(P * 4) + al(sizeof(kf64::EvCfg));
+      const size_t budget = (size_t)24 << 30;  // all 4,096 C5 scenarios (~3.7 MB each) in one launch
+      int32_t chunk = (int32_t)std::max<size_t>(1, std::min<size_t>((size_t)n_scen, budget / per));
+      if (const char* ch = getenv("KSIM_SWEEP_CHUNK")) chunk = std::max(1, std::min(chunk, atoi(ch)));  // tests
+      const size_t C = (size_t)chunk;
+      const size_t need = C * (al(4 * N * 8) + al(N * 4)) + al(C * K * g.st[0] * 4) + al(C * g.level_entries * 8) +
+                          al(C * K * 4) + al(C * 8) + al(C * P * 4) + al(C * sizeof(kf64::EvCfg)) + 4096;
+      if (h->swt_bytes < need) {
+        if (h->swt_scratch) {
+          for (auto& b : h->bufs)
+            if (b.p == h->swt_scratch) b.p = nullptr;
+          (void)hipFree(h->swt_scratch);
+          h->swt_scratch = nullptr;
+          h->swt_bytes = 0;
+        }
+        char* p = nullptr;
+        if ((rc = dev_alloc(h, &p, need))) return rc;
+        h->swt_scratch = p;
+        h->swt_bytes = need;
+      }
+      char* q = (char*)h->swt_scratch;
+      auto take = [&](size_t b) { char* r = q; q += al(b); return r; };
+      KsimTreeSweep sw{};
+      sw.count_pods = count;
+      sw.rc = (int64_t*)take(C * N * 8); sw.rm = (int64_t*)take(C * N * 8);
+      sw.zc = (int64_t*)take(C * N * 8); sw.zm = (int64_t*)take(C * N * 8);
+      sw.count = (int32_t*)take(C * N * 4);
+      int32_t* leaves = (int32_t*)take(C * K * g.st[0] * 4);
+      uint64_t* levels = (uint64_t*)take(C * g.level_entries * 8);
+      int32_t* fitc = (int32_t*)take(C * K * 4);
+      sw.counter = (uint64_t*)take(C * 8);
+      sw.out_node = (int32_t*)take(C * P * 4);
+      kf64::EvCfg* dcfg = (kf64::EvCfg*)take(C * sizeof(kf64::EvCfg));
+      sw.cfg = dcfg;
+      std::vector<kf64::EvCfg> cfgs((size_t)n_scen);
+      for (int32_t sidx = 0; sidx < n_scen; ++sidx)
+        cfgs[sidx] = kf64::make_evcfg(c.preds, c.no_prio != 0, w3[3 * sidx], w3[3 * sidx + 1], w3[3 * sidx + 2]);
+      const int64_t save_first = c.first, save_end = c.end;
+      c.first = first;
+      c.end = first + count;
+      float kms = 0.f, dms = 0.f;
+      int32_t err0 = 0;
+      HIPCHK(h, hipMemcpy(&err0, c.err, 4, hipMemcpyDeviceToHost));
+      for (int32_t s0 = 0; s0 < n_scen; s0 += chunk) {
+        sw.nsc = std::min(chunk, n_scen - s0);
+        HIPCHK(h, hipMemcpyAsync(dcfg, cfgs.data() + s0, sw.nsc * sizeof(kf64::EvCfg), hipMemcpyHostToDevice, h->stream));
+        HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+        hipError_t e = ksim_tree_sweep_init(&c, &sw, h->stream);
+        if (e == hipSuccess) e = ksim_tree_build(&c, &g, h->tclass, h->tcls, leaves, levels, fitc, h->t_y, &sw, h->stream);
+        if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree sweep build: %s", hipGetErrorString(e));
+        HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+        e = ksim_tree_launch(&c, &g, h->tclass, h->tcls, leaves, levels, fitc, h->t_y, &sw, h->stream);
+        if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree sweep launch: %s", hipGetErrorString(e));
+        hipEvent_t ev2 = nullptr;
+        HIPCHK(h, hipEventCreate(&ev2));
+        HIPCHK(h, hipEventRecord(ev2, h->stream));
+        HIPCHK(h, hipEventSynchronize(ev2));
+        float b_ms = 0.f, r_ms = 0.f;
+        HIPCHK(h, hipEventElapsedTime(&b_ms, h->ev0, h->ev1));
+        HIPCHK(h, hipEventElapsedTime(&r_ms, h->ev1, ev2));
+        (void)hipEventDestroy(ev2);
+        kms += r_ms;
+        dms += b_ms + r_ms;
+        HIPCHK(h, hipMemcpy(out_node + (size_t)s0 * P, sw.out_node, (size_t)sw.nsc * P * 4, hipMemcpyDeviceToHost));
+        if (out_counters) HIPCHK(h, hipMemcpy(out_counters + s0, sw.counter, (size_t)sw.nsc * 8, hipMemcpyDeviceToHost));
+      }
+      c.first = save_first;
+      c.end = save_end;
+      int32_t err = 0;
+      HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
+      if (err != err0) {
+        HIPCHK(h, hipMemcpy(c.err, &err0, 4, hipMemcpyHostToDevice));
+        return fail(h, KSIM_E_DEVICE, "tree sweep: device consistency error 0x%x", err & ~err0);
+      }
+      if (st) {
+        memset(st, 0, sizeof *st);
+        st->pods = (int64_t)(n_scen * P);
+        int64_t b = 0;
+        for (size_t k = 0; k < (size_t)n_scen * P; ++k) b += out_node[k] >= 0;
+        st->scheduled = b;
+        st->node_evals = (int64_t)(n_scen * P) * n;
+        st->device_ms = dms;
+        st->kernel_ms = kms;
+        st->kernel_launches = (n_scen + chunk - 1) / chunk;
+        st->mode = KSIM_MODE_TREE;
+        st->blocks = chunk;
+      }
+      return KSIM_OK;
+    }
+  }
   if (!h->sw_dac) {
     if ((rc = dev_alloc(h, &h->sw_dac, n)) || (rc = dev_alloc(h, &h->sw_dam, n)) || (rc = dev_alloc(h, &h->sw_yc, n)) ||
         (rc = dev_alloc(h, &h->sw_ym, n)))

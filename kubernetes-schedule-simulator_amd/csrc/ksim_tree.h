@@ -41,6 +41,19 @@ struct KsimTreeClass {
   uint32_t anyreq, be;
 };
 
+// Scenario sweep through the trees (ksim_sweep): nsc independent copies of the cluster, each
+// with its own dynamic columns ([nsc][n]), counter, map weights (kf64::EvCfg, opaque here) and
+// output row of count_pods placements; trees laid out [nsc][...] in the same buffers.
+struct KsimTreeSweep {
+  int32_t nsc;
+  int64_t count_pods;
+  int64_t *rc, *rm, *zc, *zm;
+  int32_t* count;
+  uint64_t* counter;
+  int32_t* out_node;
+  const void* cfg;
+};
+
 #ifdef __cplusplus
 extern "C" {
 #endif

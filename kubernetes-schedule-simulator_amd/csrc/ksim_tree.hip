@@ -66,7 +66,24 @@ struct TreeArgs {
   uint64_t* dbg;  // per-phase cycle sums (KSIM_STAMPS builds)
   kf64::EvCfg cfg;
   int32_t collect;
+  // scenario sweep (ksim_sweep): nsc > 0 independent copies of the cluster, block / slice s =
+  // scenario s with its own dynamic columns, trees, counter, weights and output row
+  int32_t nsc;
+  const kf64::EvCfg* sw_cfg;
+  int64_t sw_count;  // output row length (pods of the call)
 };
+
+// Scenario s's view of the arguments (nsc > 0).
+__device__ __forceinline__ void scen_ptrs(TreeArgs& a, int s) {
+  const int64_t n = a.g.n;
+  a.rc += s * n; a.rm += s * n; a.zc += s * n; a.zm += s * n; a.count += s * n;
+  a.leaves += (int64_t)s * a.g.K * a.g.st[0];
+  a.levels += (int64_t)s * a.g.level_entries;
+  a.fitc += (int64_t)s * a.g.K;
+  a.counter += s;
+  a.out_node += (int64_t)s * a.sw_count - a.first;
+  a.cfg = a.sw_cfg[s];
+}
 
 #ifdef KSIM_STAMPS
 #define TSTAMP(k)                                      \
@@ -174,30 +191,38 @@ __device__ __forceinline__ uint32_t mod_u64(uint64_t x, uint32_t c) {
 }
 
 // ---------------------------------------------------------------- tree build (per call if stale)
-__global__ __launch_bounds__(256) void ksim_tree_leaf_kernel(TreeArgs a) {
-  const int64_t st0 = a.g.st[0], tot = (int64_t)a.g.K * st0;
+__global__ __launch_bounds__(256) void ksim_tree_leaf_kernel(TreeArgs a0) {
+  const int64_t st0 = a0.g.st[0], per = (int64_t)a0.g.K * st0, tot = per * max(1, a0.nsc);
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (int64_t)gridDim.x * blockDim.x) {
-    const int k = (int)(t / st0);
-    const int64_t i = t - (int64_t)k * st0;
+    const int sc = (int)(t / per);
+    const int64_t r = t - sc * per;
+    const int k = (int)(r / st0);
+    const int64_t i = r - (int64_t)k * st0;
+    TreeArgs a = a0;
+    if (a0.nsc) scen_ptrs(a, sc);
     int32_t v = -1;
     if (i < a.g.n) {
       uint32_t rmask;
       v = kf64::feval(a.cfg, class_pod(a.cls[k]), load_row(a, i), rmask);
     }
-    a.leaves[t] = v;
-    if (k == 0 && i < a.g.n) {
+    a.leaves[r] = v;
+    if (sc == 0 && k == 0 && i < a.g.n) {
       a.ty[i] = a.ac[i] ? 1.0 / (double)a.ac[i] : 0.0;
       a.ty[a.g.n + i] = a.am[i] ? 1.0 / (double)a.am[i] : 0.0;
     }
   }
 }
 
-__global__ __launch_bounds__(256) void ksim_tree_level_kernel(TreeArgs a, int h) {
-  const KsimTreeGeo& g = a.g;
+__global__ __launch_bounds__(256) void ksim_tree_level_kernel(TreeArgs a0, int h) {
+  const KsimTreeGeo& g = a0.g;
   const int lane = threadIdx.x & 63;
-  const int64_t sh = g.st[h], tot = (int64_t)g.K * sh;
+  const int64_t sh = g.st[h], per = (int64_t)g.K * sh, tot = per * max(1, a0.nsc);
   const int64_t wstep = ((int64_t)gridDim.x * blockDim.x) >> 6;
-  for (int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; e < tot; e += wstep) {
+  for (int64_t e0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; e0 < tot; e0 += wstep) {
+    const int sc = (int)(e0 / per);
+    const int64_t e = e0 - sc * per;
+    TreeArgs a = a0;
+    if (a0.nsc) scen_ptrs(a, sc);
     const int k = (int)(e / sh);
     const int64_t i = e - (int64_t)k * sh;
     uint64_t v = 0;
@@ -223,9 +248,11 @@ __global__ __launch_bounds__(256) void ksim_tree_level_kernel(TreeArgs a, int h)
 
 // fit count of every class (findNodesThatFit's len(filtered)); the tree kernel keeps it
 // current with one add per class and commit
-__global__ __launch_bounds__(256) void ksim_tree_fit_kernel(TreeArgs a) {
+__global__ __launch_bounds__(256) void ksim_tree_fit_kernel(TreeArgs a0) {
   __shared__ int32_t s_part[4];
-  const int k = blockIdx.x;
+  TreeArgs a = a0;
+  if (a0.nsc) scen_ptrs(a, blockIdx.x / a0.g.K);
+  const int k = blockIdx.x % a0.g.K;
   int32_t c = 0;
   for (int64_t i = threadIdx.x; i < a.g.n; i += 256) c += a.leaves[(int64_t)k * a.g.st[0] + i] >= 0;
   c = ksimw::sum_i32(c);
@@ -275,7 +302,9 @@ __device__ __forceinline__ uint64_t rescan(const TreeArgs& a, const int32_t* s_s
 // a sibling group (wave-cooperative) only where a unique maximum dropped.  Wave 1 streams pod
 // descriptors into an LDS ring ahead of wave 0.
 template <int M, int GL>
-__global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a) {
+__global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
+  TreeArgs a = a0;
+  if (a0.nsc) scen_ptrs(a, blockIdx.x);
   __shared__ KsimTreeClass s_cls[KSIM_TREE_MAX_CLASSES];
   __shared__ int32_t s_fit[KSIM_TREE_MAX_CLASSES];   // fit count per class
   __shared__ int32_t s_st[ML + 1], s_off[ML + 1];    // stride; offset (LDS for h >= hL, else global)
@@ -297,8 +326,8 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a) {
     s_fit[t] = a.fitc[t];
   }
   if (tid <= ML) {
-    s_st[tid] = (int)a.g.st[tid];
-    s_off[tid] = tid >= hL ? (int)(a.g.goff[tid] - gbase) : (int)a.g.goff[tid];
+    s_st[tid] = (int)a0.g.st[tid];
+    s_off[tid] = tid >= hL ? (int)(a0.g.goff[tid] - gbase) : (int)a0.g.goff[tid];
   }
   for (int t = tid; t < RING; t += 128) s_rtag[t] = -1;
   if (tid == 0) s_done = a.first;
@@ -430,7 +459,10 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a) {
     const int64_t nrc = ldw(a.rc + j) + pc, nrm = ldw(a.rm + j) + pm;
     const int64_t nzc = ldw(a.zc + j) + pzc, nzm = ldw(a.zm + j) + pzm;
     const int32_t ncnt = ldw(a.count + j) + 1;
-    const int32_t vold = cl ? ldw(a.leaves + cc * st0 + j) : -1;
+    // the committed node's old leaf per class: loaded (36 scattered lines) for one cluster; in a
+    // sweep, where hundreds of scenarios share the caches, re-evaluated from the old row instead
+    int32_t vold = -1;
+    if (!a.nsc && cl) vold = ldw(a.leaves + cc * st0 + j);
     uint64_t gold[GL > 0 ? GL : 1];  // old global-level entries on the path
 #pragma unroll
     for (int h = 1; h <= GL; ++h) gold[h - 1] = ldw(a.levels + s_off[h] + cc * s_st[h] + (e1 >> (6 * (h - 1))));
@@ -444,6 +476,13 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a) {
     nr.count = ncnt;
     nr.fl = a.fl[j];
     uint32_t rmask;
+    if (a.nsc) {
+      kf64::FRow orow = nr;
+      orow.rc = (double)(nrc - pc); orow.rm = (double)(nrm - pm); orow.zc = (double)(nzc - pzc);
+      orow.zm = (double)(nzm - pzm); orow.count = ncnt - 1;
+      const int32_t vo = kf64::feval(a.cfg, class_pod(s_cls[cc]), orow, rmask);
+      vold = cl ? vo : -1;
+    }
     const int32_t vnew = kf64::feval(a.cfg, class_pod(s_cls[cc]), nr, rmask);
     if (lane == 0) {
       a.rc[j] = nrc; a.rm[j] = nrm; a.zc[j] = nzc; a.zm[j] = nzm; a.count[j] = ncnt;
@@ -538,7 +577,7 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a) {
 }
 
 TreeArgs make_args(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls, const int32_t* tcls,
-                   int32_t* leaves, uint64_t* levels, int32_t* fitc, double* ty) {
+                   int32_t* leaves, uint64_t* levels, int32_t* fitc, double* ty, const KsimTreeSweep* sw) {
   TreeArgs a{};
   a.g = *g;
   a.ac = c->alloc_cpu; a.am = c->alloc_mem;
@@ -553,10 +592,39 @@ TreeArgs make_args(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* 
   a.cfg = kf64::make_evcfg(c->preds, c->no_prio != 0, (int32_t)c->w[KSIM_W_LEAST_REQUESTED],
                            (int32_t)c->w[KSIM_W_MOST_REQUESTED], (int32_t)c->w[KSIM_W_BALANCED]);
   a.collect = c->collect;
+  if (sw) {  // scenario sweep: per-scenario dynamic columns, counters, weights and outputs
+    a.nsc = sw->nsc;
+    a.rc = sw->rc; a.rm = sw->rm; a.zc = sw->zc; a.zm = sw->zm; a.count = sw->count;
+    a.counter = sw->counter;
+    a.out_node = sw->out_node;
+    a.sw_cfg = (const kf64::EvCfg*)sw->cfg;
+    a.sw_count = sw->count_pods;
+    a.collect = 0;
+  }
   return a;
 }
 
 }  // namespace
+
+// scenario copies of the handle's dynamic columns and counter
+__global__ __launch_bounds__(256) void ksim_tree_sweep_init_kernel(const int64_t* rc, const int64_t* rm, const int64_t* zc,
+                                                                    const int64_t* zm, const int32_t* cnt, const uint64_t* ctr,
+                                                                    int64_t n, KsimTreeSweep sw) {
+  const int64_t tot = n * sw.nsc;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < tot; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t % n;
+    sw.rc[t] = rc[i]; sw.rm[t] = rm[i]; sw.zc[t] = zc[i]; sw.zm[t] = zm[i]; sw.count[t] = cnt[i];
+    if (i == 0) sw.counter[t / n] = *ctr;
+  }
+}
+
+extern "C" hipError_t ksim_tree_sweep_init(const KsimCtx* c, const KsimTreeSweep* sw, hipStream_t s) {
+  const int64_t tot = c->n * sw->nsc;
+  hipLaunchKernelGGL(ksim_tree_sweep_init_kernel, dim3((unsigned)std::min<int64_t>((tot + 255) / 256, 16384)), dim3(256), 0, s,
+                     (const int64_t*)c->req_cpu, (const int64_t*)c->req_mem, (const int64_t*)c->nz_cpu,
+                     (const int64_t*)c->nz_mem, (const int32_t*)c->pod_count, (const uint64_t*)c->counter, c->n, *sw);
+  return hipGetLastError();
+}
 
 extern "C" int ksim_tree_plan(int64_t n, int32_t K, int64_t budget, int32_t force_m, KsimTreeGeo* out) {
   if (n <= 0 || n >= ((int64_t)1 << 24) || K <= 0 || K > KSIM_TREE_MAX_CLASSES || !out) return 0;
@@ -603,25 +671,28 @@ extern "C" int ksim_tree_plan(int64_t n, int32_t K, int64_t budget, int32_t forc
 
 extern "C" hipError_t ksim_tree_build(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
                                       const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
-                                      double* ty, hipStream_t s) {
-  const TreeArgs a = make_args(c, g, cls, tcls, leaves, levels, fitc, ty);
-  const int64_t tl = (int64_t)g->K * g->st[0];
+                                      double* ty, const KsimTreeSweep* sw, hipStream_t s) {
+  const TreeArgs a = make_args(c, g, cls, tcls, leaves, levels, fitc, ty, sw);
+  const int nsc = a.nsc;
+  const int64_t ns = std::max(1, nsc);
+  const int64_t tl = (int64_t)g->K * g->st[0] * ns;
   hipLaunchKernelGGL(ksim_tree_leaf_kernel, dim3((unsigned)std::min<int64_t>((tl + 255) / 256, 8192)), dim3(256), 0, s, a);
   for (int h = 1; h <= g->H; ++h) {
-    const int64_t waves = (int64_t)g->K * g->st[h];
+    const int64_t waves = (int64_t)g->K * g->st[h] * ns;
     hipLaunchKernelGGL(ksim_tree_level_kernel, dim3((unsigned)std::min<int64_t>((waves + 3) / 4, 8192)), dim3(256), 0, s, a, h);
   }
-  hipLaunchKernelGGL(ksim_tree_fit_kernel, dim3(g->K), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(ksim_tree_fit_kernel, dim3((unsigned)(g->K * ns)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
 extern "C" hipError_t ksim_tree_launch(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
                                        const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
-                                       double* ty, hipStream_t s) {
-  const TreeArgs a = make_args(c, g, cls, tcls, leaves, levels, fitc, ty);
+                                       double* ty, const KsimTreeSweep* sw, hipStream_t s) {
+  const TreeArgs a = make_args(c, g, cls, tcls, leaves, levels, fitc, ty, sw);
+  const unsigned grid = (unsigned)std::max(1, a.nsc);
   const size_t lds = (size_t)g->lds_entries * sizeof(uint64_t);
 #define KT_CASE(MM, GG) \
-  if (g->m == MM && g->hL == GG + 1) { hipLaunchKernelGGL((ksim_tree_kernel<MM, GG>), dim3(1), dim3(128), lds, s, a); return hipGetLastError(); }
+  if (g->m == MM && g->hL == GG + 1) { hipLaunchKernelGGL((ksim_tree_kernel<MM, GG>), dim3(grid), dim3(128), lds, s, a); return hipGetLastError(); }
   KT_CASE(1, 0) KT_CASE(1, 1) KT_CASE(1, 2) KT_CASE(2, 0) KT_CASE(2, 1) KT_CASE(4, 0)
 #undef KT_CASE
   return hipErrorInvalidValue;

@@ -345,12 +345,27 @@ def test_fast_and_general_kernels_agree(seed, monkeypatch):
     assert np.array_equal(o1, ref) and c1 == ref_ctr
 
 
+SWEEP_FORMS = ["tree", "tree-chunked", "scan"]
+
+
+def _sweep_form(form, monkeypatch):
+    """tree: one tree-mode wave per scenario (ksim_tree.hip); scan: the per-scenario scan kernel
+    (ksim_sweep.hip); tree-chunked: scenarios in launches of 5."""
+    if form == "scan":
+        monkeypatch.setenv("KSIM_SWEEP_SCAN", "1")
+    if form == "tree-chunked":
+        monkeypatch.setenv("KSIM_SWEEP_CHUNK", "5")
+    return abi.MODE_PERSISTENT if form == "scan" else abi.MODE_TREE
+
+
+@pytest.mark.parametrize("form", SWEEP_FORMS)
 @pytest.mark.parametrize("n_nodes,n_pods", [(1500, 1200), (20_000, 300)])
-def test_sweep_matches_c_oracle_per_scenario(n_nodes, n_pods):
+def test_sweep_matches_c_oracle_per_scenario(n_nodes, n_pods, form, monkeypatch):
     """Scenario sweep (C5 shape): every scenario's placements and final lastNodeIndex equal the
     C oracle run under that scenario's weights; the scheduler's own state is untouched."""
     import cpu_ref
     from ksim import synth
+    mode = _sweep_form(form, monkeypatch)
     cl, preds, scen = synth.config_c5(n_nodes, n_pods)
     pick = [scen[i] for i in (0, 1, 17, 255, 256, 1000, 2047, 2500, 3071, 4095)]
     pick.append([("MostRequestedPriority", 1)])
@@ -359,6 +374,7 @@ def test_sweep_matches_c_oracle_per_scenario(n_nodes, n_pods):
     before = g.node_state()
     out, ctr, st = g.sweep(pick, 0, n_pods)
     assert st.node_evals == len(pick) * n_pods * n_nodes
+    assert st.mode == mode
     for k, pri in enumerate(pick):
         ref, _, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, pri), 0, n_pods, threads=8)
         assert np.array_equal(out[k], ref), pri
@@ -369,11 +385,13 @@ def test_sweep_matches_c_oracle_per_scenario(n_nodes, n_pods):
     assert g.last_node_index == 0
 
 
-def test_sweep_until_unschedulable_and_from_mid_queue():
+@pytest.mark.parametrize("form", SWEEP_FORMS)
+def test_sweep_until_unschedulable_and_from_mid_queue(form, monkeypatch):
     """A sweep over a queue that overflows a small cluster (FitErrors, single-fit pods) started
     after a regular ksim_schedule prefix: continues from the scheduled state and counter."""
     import cpu_ref
     from ksim import synth
+    _sweep_form(form, monkeypatch)
     n = 64
     cpu, mem = synth.c3_nodes(n, 11)
     pcpu, pmem = synth.c3_pods(3000, 11)
