@@ -736,9 +736,10 @@ static int run_tree_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stat
       HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
       HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
       const double np = (double)(d[8] ? d[8] : 1);
-      fprintf(stderr, "[ksim stamps] tree pods=%llu (%.3f ms) cycles/pod: decide %.0f walk %.0f row+eval %.0f paths %.0f; changed "
-              "classes %.2f, re-combined paths %.3f per pod\n", (unsigned long long)d[8], run_ms, d[0] / np, d[1] / np,
-              d[2] / np, d[3] / np, d[6] / np, d[7] / np);
+      fprintf(stderr, "[ksim stamps] tree pods=%llu (%.3f ms) cycles/pod: decide %.0f walk (levels %.0f, leaf load %.0f, leaf "
+              "pick %.0f) row+eval %.0f paths %.0f; changed classes %.2f, re-combined paths %.3f per pod\n",
+              (unsigned long long)d[8], run_ms, d[0] / np, d[4] / np, d[5] / np, d[1] / np, d[2] / np, d[3] / np,
+              d[6] / np, d[7] / np);
     }
 #endif
     int32_t err = 0;

@@ -34,6 +34,9 @@
 
 namespace {
 
+#ifndef KSIM_TREE_VAR
+#define KSIM_TREE_VAR 0  // diagnostic variants of the stamps build (tools/gpu_tree_ab.sh)
+#endif
 constexpr int ML = KSIM_TREE_MAX_LEVELS;
 constexpr int LS = 2;  // LDS levels below the root (plan limit)
 constexpr int64_t LIM48 = (int64_t)1 << 48;
@@ -110,7 +113,11 @@ typedef int32_t v4i __attribute__((ext_vector_type(4)));
 template <int M>
 __device__ __forceinline__ void ld_leaves(const int32_t* L, int32_t* lv) {
   if constexpr (M == 4) {
+#if KSIM_TREE_VAR == 1
+    const v4i x = *(const volatile v4i*)L;
+#else
     const v4i x = __builtin_nontemporal_load((const v4i*)L);
+#endif
     lv[0] = x.x; lv[1] = x.y; lv[2] = x.z; lv[3] = x.w;
   } else if constexpr (M == 2) {
     const v2i x = __builtin_nontemporal_load((const v2i*)L);
@@ -358,27 +365,42 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
   // ---- wave 0: the scheduler
   const int st0 = s_st[0];
   const uint64_t* root = kt_lds + s_off[H];  // st[H] == 1: one root per class
-  uint64_t counter = ldw(a.counter);
+  // lastNodeIndex in scalar registers: loaded (and waited for) once, not a vector register whose
+  // pending load makes every pod wait for all of the previous pod's stores
+  uint64_t counter;
+  {
+    const uint64_t c0 = ldw(a.counter);
+    counter = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(c0 >> 32)) << 32) |
+              (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)c0);
+  }
 #ifdef KSIM_STAMPS
   uint64_t ts_acc[8] = {}, ts_prev = __builtin_amdgcn_s_memtime();
 #endif
+  // per-class root entry and fit count in registers, lane c = class c (K <= 64): the decision
+  // reads them with readlane instead of two dependent LDS loads; LDS keeps the root level too
+  uint64_t rootv = lane < K ? root[lane] : 0ull;
+  int32_t fitv = lane < K ? s_fit[lane] : 0;
   int hist_cls = -1;
   int64_t p = a.first;
+  int64_t ready = a.first;  // pods below this are in the ring
   bool stop = false;
   while (p < a.end && !stop) {
     const int rs = (int)(p & (RING - 1));
-    {
+    if (p >= ready) {  // once per producer batch: its last pod's tag (the producer's release fence
+                       // orders every lane's slot writes before any of the batch's tags)
+      const int64_t ql = min(a.first + ((p - a.first) & ~(int64_t)63) + 63, a.end - 1);
+      ready = ql + 1;
       uint32_t spins = 0;
-      while (__hip_atomic_load(&s_rtag[rs], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != p) {
+      while (__hip_atomic_load(&s_rtag[ql & (RING - 1)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != ql) {
         __builtin_amdgcn_s_sleep(1);
         if (++spins > (1u << 28)) { if (lane == 0) atomicOr(a.err, 32); stop = true; break; }
       }
       if (stop) break;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     }
-    const int k = s_rk[rs];
+    const int k = __builtin_amdgcn_readfirstlane(s_rk[rs]);
     const int64_t pc = s_rd[0][rs], pm = s_rd[1][rs], pzc = s_rd[2][rs], pzm = s_rd[3][rs];  // commit deltas
-    const uint32_t F = (uint32_t)s_fit[k];
+    const uint32_t F = (uint32_t)__builtin_amdgcn_readlane(fitv, k);
     if (F == 0) {  // FitError: no commit, lastNodeIndex unchanged
       if (lane == 0) a.out_node[p] = -1;
       if (a.collect) {
@@ -403,7 +425,8 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
       if (lane == 0) __hip_atomic_store(&s_done, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       continue;
     }
-    const uint64_t rt = root[k];
+    const uint64_t rt = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(rootv >> 32), k) << 32) |
+                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rootv, k);
     const bool single = F == 1;
     uint32_t kth = 0;
     if (!single) {
@@ -426,11 +449,16 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
     }
     int j;
     {
+      TSTAMP(4);
       int32_t lv[M];
       ld_leaves<M>(a.leaves + k * st0 + e * G0 + lane * M, lv);
       uint32_t c = 0;
 #pragma unroll
       for (int t = 0; t < M; ++t) c += single ? (lv[t] >= 0) : ((uint32_t)(lv[t] + 1) == Sp);
+#ifdef KSIM_STAMPS
+      asm volatile("" ::"v"(c));  // the leaf values are in
+#endif
+      TSTAMP(5);
       const int l = pick_lane(c, kth);
       bad |= l < 0;
       int sel = 0;
@@ -450,7 +478,6 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
         j = 0;
       }
     }
-    if (lane == 0) a.out_node[p] = j;
     TSTAMP(1);
     // ---- commit (Scheduler.assume -> NodeInfo.AddPod, node_info.go:318-341) ----
     const int e1 = j / G0;
@@ -484,7 +511,11 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
       vold = cl ? vo : -1;
     }
     const int32_t vnew = kf64::feval(a.cfg, class_pod(s_cls[cc]), nr, rmask);
+    // stores only after every row load is consumed: stores and loads retire in issue order
+    // (vmcnt), so a store issued ahead of the evaluation would make it wait for the store
+    asm volatile("" ::"v"(vnew) : "memory");
     if (lane == 0) {
+      a.out_node[p] = j;
       a.rc[j] = nrc; a.rm[j] = nrm; a.zc[j] = nzc; a.zm[j] = nzm; a.count[j] = ncnt;
     }
     const bool chg = cl && vnew != vold;
@@ -493,7 +524,7 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
     uint64_t resc_old = 0;
     if (chg) {
       a.leaves[cc * st0 + j] = vnew;
-      s_fit[cc] += (vnew >= 0 ? 1 : 0) - (vold >= 0 ? 1 : 0);
+      fitv += (vnew >= 0 ? 1 : 0) - (vold >= 0 ? 1 : 0);  // lane == class cc
     }
     {
       bool act = chg;
@@ -514,6 +545,7 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
             } else {
               if (h <= GL) a.levels[s_off[h] + cc * s_st[h] + eh] = NP;
               else kt_lds[s_off[h] + cc * s_st[h] + eh] = NP;
+              if (h == H) rootv = NP;
               co = P;
               cn = NP;
             }
@@ -537,7 +569,10 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
           if (h <= GL) a.levels[idx] = newv;
           else kt_lds[idx] = newv;
         }
-        if (h == H) break;
+        if (h == H) {
+          if (lane == c) rootv = newv;
+          break;
+        }
         ++h;
         const int pidx = s_off[h] + c * s_st[h] + (e1 >> (6 * (h - 1)));
         const uint64_t P = h <= GL ? ldw(a.levels + pidx) : kt_lds[pidx];
@@ -550,6 +585,9 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
         newv = NP;
       }
     }
+#if KSIM_TREE_VAR == 2
+    stores_done();
+#endif
     TSTAMP(3);
 #ifdef KSIM_STAMPS
     ts_acc[6] += __popcll(__ballot(chg));
@@ -564,7 +602,7 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
   if (lane == 0) __hip_atomic_store(&s_done, INT64_MAX, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   stores_done();
   for (int t = lane; t < lds_entries; t += 64) a.levels[gbase + t] = kt_lds[t];
-  for (int t = lane; t < K; t += 64) a.fitc[t] = s_fit[t];
+  if (lane < K) a.fitc[lane] = fitv;
   if (lane == 0) {
     __hip_atomic_store(a.counter, counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(a.cursor, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
