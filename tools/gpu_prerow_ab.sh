@@ -1,6 +1,7 @@
 #!/bin/bash
 # Tree-mode row-prefetch A/B: tree + sweep parity tests on the default library, then C3 / C4 / C5
-# tree bench lines for lib/v0 (KSIM_TREE_PREROW=0) and the default library, and the stamps build.
+# tree bench lines for lib/v0 (a HEAD build of ksim_tree.hip linked beside the other objects) and
+# the default library (the variant under test), and the stamps build.
 # Usage (from the repo root on the GPU box): tools/gpu_prerow_ab.sh <tag>
 set -o pipefail
 TAG=${1:-pr}
