@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 1
+#define KSIM_ABI_VERSION 2
 
 /* ---- status codes ---- */
 #define KSIM_OK 0
@@ -35,6 +35,7 @@ extern "C" {
 #define KSIM_E_UNSUPPORTED (-4) /* configuration outside the supported key set */
 #define KSIM_E_STATE (-5)       /* call order (e.g. schedule before load) */
 #define KSIM_E_OVERFLOW (-6)    /* a node's host-port slots overflowed on commit */
+#define KSIM_E_NO_NODES (-7)    /* core.ErrNoNodesAvailable (generic_scheduler.go:64,124-125) */
 
 #define KSIM_MAX_SCALAR 8   /* extended / hugepage resource columns */
 #define KSIM_MAX_RCLASS 16  /* reduce classes per pod (TaintToleration x NodeAffinity) */
@@ -236,6 +237,7 @@ void ksim_destroy(ksim_handle* h);
 
 /* Snapshot ingest: the node cache (schedulercache UpdateNodeNameToInfoMap, cache.go:83). */
 int ksim_load_nodes(ksim_handle* h, const ksim_node_table* nodes);
+/* May be called again with a superset (new pod classes, label sets, taint sets). */
 int ksim_load_classes(ksim_handle* h, const ksim_class_tables* classes);
 /* Pod queue in scheduling order (the simulator's LIFO PodQueue.Pop order, store.go:223). */
 int ksim_load_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const uint64_t* ports,
@@ -285,6 +287,74 @@ int ksim_shard_connect_local(ksim_handle* h, int32_t peer, ksim_handle* peer_h);
 
 /* Commit one loaded pod to a node (Scheduler.assume / cache.AssumePod). */
 int ksim_assume(ksim_handle* h, int64_t pod, int64_t node);
+
+/* ==== Per-pod drop-in and scheduler-cache sync ===========================================
+ * The reference calls ScheduleAlgorithm.Schedule(pod, nodeLister) once per pod
+ * (algorithm/scheduler_interface.go:52-65) from Scheduler.schedule (scheduler.go:188-204), then
+ * Scheduler.assume (scheduler.go:366) → schedulerCache.AssumePod (schedulercache/cache.go:125).
+ * Informer events keep the cache in sync: addPodToCache / deletePodFromCache
+ * (factory/factory.go:596,695) → cache.AddPod / RemovePod (cache.go:230,292), addNodeToCache /
+ * updateNodeInCache / deleteNodeFromCache (factory.go:740,755,841) → cache.AddNode / UpdateNode /
+ * RemoveNode (cache.go:354,366,378).  These entry points are that surface on the device-resident
+ * table: a pod is passed as a descriptor (its port_off / scalar_off index the arrays passed with
+ * it), nodes are addressed by name rank (the caller keeps the bytewise-sorted name list; an
+ * insert at rank r moves ranks >= r up by one).  None of them needs a loaded pod queue. */
+
+/* Result of one Schedule call. */
+typedef struct {
+  int32_t node;                    /* selected node (name rank), -1: FitError */
+  int32_t fit_nodes;               /* len(filtered) of findNodesThatFit (generic_scheduler.go:136) */
+  uint64_t last_node_index;        /* genericScheduler.lastNodeIndex after the call */
+  int32_t reasons[KSIM_NREASONS];  /* FitError.FailedPredicates histogram when node == -1 */
+} ksim_result;
+
+#define KSIM_SCHEDULE_ONLY 0    /* genericScheduler.Schedule: decide, leave the cache unchanged */
+#define KSIM_SCHEDULE_ASSUME 1  /* Schedule + Scheduler.assume (AssumePod on the chosen node) */
+
+/* One pod through findNodesThatFit → PrioritizeNodes → selectHost (one scan launch, no
+ * queue), optionally assumed.  ports [n_ports] / scalars [n_scalars] are the pod's host-port
+ * keys and scalar requests (pod->port_off / scalar_off index them).  Returns KSIM_OK with
+ * out->node == -1 for a FitError, KSIM_E_NO_NODES when the table is empty. */
+int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports, int32_t n_ports,
+                      const ksim_scalar_req* scalars, int32_t n_scalars, int32_t assume, ksim_result* out);
+
+/* NodeInfo.AddPod / RemovePod on node `node` (name rank) for a pod descriptor: cache.AddPod of a
+ * pod bound elsewhere, AssumePod after a KSIM_SCHEDULE_ONLY decision, cache.RemovePod
+ * (node_info.go:318-390).  The caller's cache mirror owns pod identity (the "no corresponding
+ * pod" error of RemovePod); the library applies the resource / port delta. */
+int ksim_pod_add(ksim_handle* h, int64_t node, const ksim_pod* pod, const uint64_t* ports, int32_t n_ports,
+                 const ksim_scalar_req* scalars, int32_t n_scalars);
+int ksim_pod_remove(ksim_handle* h, int64_t node, const ksim_pod* pod, const uint64_t* ports, int32_t n_ports,
+                    const ksim_scalar_req* scalars, int32_t n_scalars);
+
+/* One node's columns (the row of ksim_node_table): static ones as NodeInfo.SetNode derives them
+ * (node_info.go:429-448), dynamic ones for pods already on the node. */
+typedef struct {
+  int64_t alloc_cpu, alloc_mem, alloc_gpu, alloc_eph;
+  int32_t allowed_pods;
+  uint32_t flags;               /* KSIM_N_* condition bits */
+  int32_t label_set, taint_set; /* ids in the loaded class tables */
+  int64_t req_cpu, req_mem, req_gpu, req_eph, nz_cpu, nz_mem;
+  int32_t pod_count, port_count;
+  const int64_t* alloc_scalar;  /* [n_scalar] or NULL */
+  const int64_t* req_scalar;    /* [n_scalar] or NULL */
+  const uint64_t* ports;        /* [port_count] KSIM_PORT_KEY or NULL */
+} ksim_node_row;
+
+/* cache.AddNode of a node whose bytewise name rank among the listed nodes is `index`
+ * (0..n): rows index.. move up one, queued pods' spec.nodeName ranks follow. */
+int ksim_node_add(ksim_handle* h, int64_t index, const ksim_node_row* row);
+/* cache.UpdateNode → SetNode: the static columns of row `index` (dynamic ones are kept). */
+int ksim_node_update(ksim_handle* h, int64_t index, const ksim_node_row* row);
+/* cache.RemoveNode: the node leaves the listed set (nodeLister.List no longer returns it). */
+int ksim_node_remove(ksim_handle* h, int64_t index);
+int ksim_node_count(ksim_handle* h, int64_t* out);
+
+/* Append pods to the loaded queue (first call may also be ksim_load_pods): offsets in the
+ * new descriptors index the arrays passed with them.  New pod classes need the class tables
+ * reloaded first (ksim_load_classes may be called again with a superset). */
+int ksim_append_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const uint64_t* ports, int64_t n_ports,
+                     const ksim_scalar_req* scalars, int64_t n_scalars);
 
 int ksim_read_nodes(ksim_handle* h, ksim_node_state* out);
 int ksim_get_counter(ksim_handle* h, uint64_t* out);

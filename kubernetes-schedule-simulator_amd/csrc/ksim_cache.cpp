@@ -1,0 +1,418 @@
+// ksim_cache.cpp — the per-pod drop-in entry points and the scheduler-cache event mirror of
+// include/ksim.h (ksim_schedule_one, ksim_pod_add / remove, ksim_node_add / update / remove,
+// ksim_assume).
+//
+// Reference surface being served:
+//   ScheduleAlgorithm.Schedule           algorithm/scheduler_interface.go:52-65
+//   Scheduler.schedule / assume          scheduler.go:188-204, 366-397
+//   cache.AssumePod / AddPod / RemovePod schedulercache/cache.go:125, 230, 292
+//   cache.AddNode / UpdateNode / Remove  schedulercache/cache.go:354, 366, 378
+//   NodeInfo.AddPod / RemovePod / SetNode schedulercache/node_info.go:318-341, 343-390, 429-448
+//
+// A Schedule call is one scan launch (ksim_scan_kernel, the launch-mode kernel) over the
+// resident table against a staged pod descriptor: one packed host→device copy {cursor, result
+// block, pod, ports, scalars}, one kernel, one device→host copy of the result block.  Node
+// events relayout the table in one kernel (rows stay in name-rank order).
+#include "ksim_handle.h"
+#include "ksim_cache.h"
+
+namespace {
+
+// staging layout on the device (and its pinned host mirror)
+constexpr size_t STG_CURSOR = 0;
+constexpr size_t STG_RES = 16;
+constexpr size_t STG_POD = STG_RES + ((KSIM_RES_WORDS * 4 + 15) / 16) * 16;
+constexpr size_t STG_PORTS = STG_POD + sizeof(ksim_pod);
+
+int ensure_staging(ksim_handle* h, int32_t n_ports, int32_t n_scalars) {
+  const size_t need = STG_PORTS + (size_t)n_ports * 8 + (size_t)n_scalars * sizeof(ksim_scalar_req) +
+                      (size_t)KSIM_PK_WORDS(KSIM_MAX_SCALAR, 0) * 8;
+  if (h->stg_dev && h->stg_cap >= need) return KSIM_OK;
+  const size_t cap = std::max<size_t>(need * 2, 4096);
+  char* d = nullptr;
+  int rc = dev_alloc(h, &d, cap);
+  if (rc) return rc;
+  char* hst = nullptr;
+  HIPCHK(h, hipHostMalloc((void**)&hst, cap, hipHostMallocDefault));
+  dev_free(h, h->stg_dev);
+  if (h->stg_host) (void)hipHostFree(h->stg_host);
+  h->stg_dev = d;
+  h->stg_host = hst;
+  h->stg_cap = cap;
+  if (!h->res_host) {
+    HIPCHK(h, hipHostMalloc((void**)&h->res_host, KSIM_RES_WORDS * 4, hipHostMallocDefault));
+    HIPCHK(h, hipHostMalloc((void**)&h->ctr_host, 8, hipHostMallocDefault));
+  }
+  h->res_dev = reinterpret_cast<int32_t*>(d + STG_RES);
+  return KSIM_OK;
+}
+
+// Stage one pod: {cursor = 0, zeroed result block, pod (offsets rebased to the staged arrays),
+// ports, scalars} in one copy, and the context that points the scan / commit kernels at it.
+int stage_pod(ksim_handle* h, const ksim_pod& pod, const uint64_t* ports, const ksim_scalar_req* scalars,
+              KsimCtx* cs) {
+  int rc = ensure_staging(h, pod.port_cnt, pod.scalar_cnt);
+  if (rc) return rc;
+  char* hs = h->stg_host;
+  memset(hs, 0, STG_POD);
+  ksim_pod p = pod;
+  p.port_off = 0;
+  p.scalar_off = 0;
+  memcpy(hs + STG_POD, &p, sizeof p);
+  const size_t pb = (size_t)pod.port_cnt * 8, sb = (size_t)pod.scalar_cnt * sizeof(ksim_scalar_req);
+  if (pb) memcpy(hs + STG_PORTS, ports + pod.port_off, pb);
+  if (sb) memcpy(hs + STG_PORTS + pb, scalars + pod.scalar_off, sb);
+  HIPCHK(h, hipMemcpyAsync(h->stg_dev, hs, STG_PORTS + pb + sb, hipMemcpyHostToDevice, h->stream));
+  *cs = h->ctx;
+  cs->pods = reinterpret_cast<const ksim_pod*>(h->stg_dev + STG_POD);
+  cs->pod_ports = reinterpret_cast<const uint64_t*>(h->stg_dev + STG_PORTS);
+  cs->pod_scalars = reinterpret_cast<const ksim_scalar_req*>(h->stg_dev + STG_PORTS + pb);
+  cs->cursor = reinterpret_cast<int64_t*>(h->stg_dev + STG_CURSOR);
+  cs->out_node = h->res_dev + KSIM_RES_NODE;
+  cs->out_fit = h->res_dev + KSIM_RES_FIT;
+  cs->out_reasons = h->res_dev + KSIM_RES_REASONS;
+  cs->first = 0;
+  cs->end = 1;
+  return KSIM_OK;
+}
+
+// The node columns, in one place: (address of the ctx pointer, element bytes, slots).
+struct ColRef {
+  void** p;
+  int32_t esz;
+  int32_t slots;
+};
+
+std::vector<ColRef> node_cols(ksim_handle* h) {
+  KsimCtx& c = h->ctx;
+  const int32_t S = c.n_scalar, P = c.port_slots;
+  return {{(void**)&c.alloc_cpu, 8, 1},    {(void**)&c.alloc_mem, 8, 1},  {(void**)&c.alloc_gpu, 8, 1},
+          {(void**)&c.alloc_eph, 8, 1},    {(void**)&c.allowed_pods, 4, 1}, {(void**)&c.flags, 4, 1},
+          {(void**)&c.label_set, 4, 1},    {(void**)&c.taint_set, 4, 1},  {(void**)&c.alloc_scalar, 8, S},
+          {(void**)&c.req_cpu, 8, 1},      {(void**)&c.req_mem, 8, 1},    {(void**)&c.req_gpu, 8, 1},
+          {(void**)&c.req_eph, 8, 1},      {(void**)&c.nz_cpu, 8, 1},     {(void**)&c.nz_mem, 8, 1},
+          {(void**)&c.pod_count, 4, 1},    {(void**)&c.req_scalar, 8, S}, {(void**)&c.ports, 8, P},
+          {(void**)&c.port_count, 4, 1}};
+}
+
+// Copy the chosen columns into fresh buffers of n_new rows (op: KSIM_RELAY_*) and swap them in.
+// new_slots: per column, the slot count after (-1 = unchanged).
+int relayout(ksim_handle* h, const std::vector<ColRef>& cols, const std::vector<int32_t>& new_slots, int32_t op,
+             int64_t idx, int64_t n_new) {
+  KsimRelayout r{};
+  r.op = op;
+  r.n_old = h->ctx.n;
+  r.n_new = n_new;
+  r.idx = idx;
+  std::vector<void*> fresh(cols.size(), nullptr);
+  for (size_t k = 0; k < cols.size(); ++k) {
+    const int32_t ds = new_slots[k] < 0 ? cols[k].slots : new_slots[k];
+    int rc;
+    if (cols[k].esz == 8) {
+      uint64_t* q;
+      rc = dev_alloc(h, &q, (size_t)ds * n_new);
+      fresh[k] = q;
+    } else {
+      uint32_t* q;
+      rc = dev_alloc(h, &q, (size_t)ds * n_new);
+      fresh[k] = q;
+    }
+    if (rc) {
+      for (void* q : fresh) dev_free(h, q);
+      return rc;
+    }
+    r.col[r.ncol++] = KsimRelayCol{*cols[k].p, fresh[k], cols[k].esz, cols[k].slots, ds, 0};
+  }
+  hipError_t e = ksim_launch_relayout(&r, h->stream);
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "relayout launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (size_t k = 0; k < cols.size(); ++k) {
+    dev_free(h, *cols[k].p);
+    *cols[k].p = fresh[k];
+  }
+  return KSIM_OK;
+}
+
+// Grow the slot-major port column to `slots` slots per node (existing keys keep their slots).
+int grow_port_slots(ksim_handle* h, int32_t slots) {
+  KsimCtx& c = h->ctx;
+  if (slots <= c.port_slots) return KSIM_OK;
+  if (slots > 4096) return ksim_fail(h, KSIM_E_OVERFLOW, "a node would hold more than 4096 host ports");
+  std::vector<ColRef> cols{{(void**)&c.ports, 8, c.port_slots}};
+  int rc = relayout(h, cols, {slots}, KSIM_RELAY_SAME, 0, c.n);
+  if (rc) return rc;
+  c.port_slots = slots;
+  ksim_rt_invalidate_layout(h);
+  return KSIM_OK;
+}
+
+// The node table can take `need` more distinct host ports on its fullest node: otherwise
+// measure the real maximum and, if still short, grow the port column geometrically.
+int ensure_port_room(ksim_handle* h, int32_t need) {
+  KsimCtx& c = h->ctx;
+  if (need <= 0 || h->port_bound + need <= c.port_slots) return KSIM_OK;
+  if (c.n > 0) {
+    int rc = ensure_staging(h, 0, 0);
+    if (rc) return rc;
+    hipError_t e = ksim_launch_port_max(c.port_count, c.n, h->res_dev + KSIM_RES_STATUS, h->stream);
+    if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "port max: %s", hipGetErrorString(e));
+    HIPCHK(h, hipMemcpyAsync(h->res_host, h->res_dev, KSIM_RES_WORDS * 4, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->port_bound = h->res_host[KSIM_RES_STATUS];
+  } else {
+    h->port_bound = 0;
+  }
+  if (h->port_bound + need <= c.port_slots) return KSIM_OK;
+  return grow_port_slots(h, (int32_t)std::max<int64_t>({(int64_t)c.port_slots * 2, h->port_bound + need, 4}));
+}
+
+int check_ready(ksim_handle* h, const char* where) {
+  if (!h) return ksim_fail(h, KSIM_E_INVAL, "%s: null handle", where);
+  if (!h->have_nodes || !h->have_classes) return ksim_fail(h, KSIM_E_STATE, "%s: load nodes and classes first", where);
+  if (h->shard.world > 1) return ksim_fail(h, KSIM_E_UNSUPPORTED, "%s: not available on a node-sharded handle", where);
+  HIPCHK(h, hipSetDevice(h->device));
+  return KSIM_OK;
+}
+
+int check_pod_args(ksim_handle* h, const ksim_pod* pod, int32_t n_ports, int32_t n_scalars, const uint64_t* ports,
+                   const ksim_scalar_req* scalars, const char* where) {
+  if (!pod) return ksim_fail(h, KSIM_E_INVAL, "%s: null pod", where);
+  if (n_ports < 0 || n_scalars < 0 || (n_ports && !ports) || (n_scalars && !scalars))
+    return ksim_fail(h, KSIM_E_INVAL, "%s: bad port / scalar arrays", where);
+  if (pod->port_cnt < 0 || pod->port_off < 0 || (int64_t)pod->port_off + pod->port_cnt > n_ports)
+    return ksim_fail(h, KSIM_E_INVAL, "%s: port range out of bounds", where);
+  return KSIM_OK;
+}
+
+int after_commit(ksim_handle* h, int32_t port_cnt) {
+  h->tree_valid = false;  // the trees are maintained by the tree kernel only
+  h->port_bound += port_cnt;
+  if (h->res_host[KSIM_RES_STATUS] & 1) h->pfast_off = true;  // keep the fast kernels' float64 range
+  int32_t err = 0;
+  HIPCHK(h, hipMemcpy(&err, h->ctx.err, 4, hipMemcpyDeviceToHost));
+  if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port slots overflowed (raise port_slots)");
+  if (err & ~1) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
+  return KSIM_OK;
+}
+
+void pack_row(const KsimCtx& c, const ksim_node_row* r, std::vector<uint64_t>& pk) {
+  pk.assign(KSIM_PK_WORDS(c.n_scalar, c.port_slots), 0);
+  pk[KSIM_PK_ALLOC + 0] = (uint64_t)r->alloc_cpu;
+  pk[KSIM_PK_ALLOC + 1] = (uint64_t)r->alloc_mem;
+  pk[KSIM_PK_ALLOC + 2] = (uint64_t)r->alloc_gpu;
+  pk[KSIM_PK_ALLOC + 3] = (uint64_t)r->alloc_eph;
+  pk[KSIM_PK_ALLOWED] = (uint64_t)(uint32_t)r->allowed_pods;
+  pk[KSIM_PK_FLAGS] = r->flags;
+  pk[KSIM_PK_LABEL] = (uint64_t)(uint32_t)r->label_set;
+  pk[KSIM_PK_TAINT] = (uint64_t)(uint32_t)r->taint_set;
+  pk[KSIM_PK_REQ + 0] = (uint64_t)r->req_cpu;
+  pk[KSIM_PK_REQ + 1] = (uint64_t)r->req_mem;
+  pk[KSIM_PK_REQ + 2] = (uint64_t)r->req_gpu;
+  pk[KSIM_PK_REQ + 3] = (uint64_t)r->req_eph;
+  pk[KSIM_PK_NZ + 0] = (uint64_t)r->nz_cpu;
+  pk[KSIM_PK_NZ + 1] = (uint64_t)r->nz_mem;
+  pk[KSIM_PK_COUNT] = (uint64_t)(uint32_t)r->pod_count;
+  pk[KSIM_PK_PORTCNT] = (uint64_t)(uint32_t)r->port_count;
+  for (int32_t k = 0; k < c.n_scalar; ++k) {
+    pk[KSIM_PK_SCALAR + k] = r->alloc_scalar ? (uint64_t)r->alloc_scalar[k] : 0;
+    pk[KSIM_PK_SCALAR + c.n_scalar + k] = r->req_scalar ? (uint64_t)r->req_scalar[k] : 0;
+  }
+  for (int32_t k = 0; k < r->port_count; ++k) pk[KSIM_PK_SCALAR + 2 * c.n_scalar + k] = r->ports[k];
+}
+
+int check_row(ksim_handle* h, const ksim_node_row* r, bool full, const char* where) {
+  if (!r) return ksim_fail(h, KSIM_E_INVAL, "%s: null row", where);
+  if (r->label_set < 0 || r->label_set >= h->n_label_sets || r->taint_set < 0 || r->taint_set >= h->n_taint_sets)
+    return ksim_fail(h, KSIM_E_INVAL, "%s: label / taint set id outside the loaded class tables (reload them first)", where);
+  if (full && (r->port_count < 0 || (r->port_count && !r->ports) || r->pod_count < 0))
+    return ksim_fail(h, KSIM_E_INVAL, "%s: bad pod / port count", where);
+  return KSIM_OK;
+}
+
+// A node row inside the fast kernels' exact float64 range (ksim_pfast.hip, ksim_tree.hip)?
+bool row_exact(const ksim_node_row* r, bool full) {
+  const int64_t lim = (int64_t)1 << 48;
+  for (int64_t v : {r->alloc_cpu, r->alloc_mem})
+    if (v < 0 || v >= lim) return false;
+  if (full)
+    for (int64_t v : {r->req_cpu, r->req_mem, r->nz_cpu, r->nz_mem})
+      if (v < 0 || v >= lim) return false;
+  return true;
+}
+
+int set_row(ksim_handle* h, int64_t index, const ksim_node_row* row, bool full) {
+  std::vector<uint64_t> pk;
+  pack_row(h->ctx, row, pk);
+  int rc = ensure_staging(h, (int32_t)pk.size(), 0);
+  if (rc) return rc;
+  memcpy(h->stg_host + STG_PORTS, pk.data(), pk.size() * 8);
+  HIPCHK(h, hipMemcpyAsync(h->stg_dev + STG_PORTS, h->stg_host + STG_PORTS, pk.size() * 8, hipMemcpyHostToDevice, h->stream));
+  hipError_t e = ksim_launch_set_row(&h->ctx, index, reinterpret_cast<const uint64_t*>(h->stg_dev + STG_PORTS), full ? 1 : 0,
+                                     h->stream);
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "set_row launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (!row_exact(row, full)) h->pfast_off = true;
+  return KSIM_OK;
+}
+
+int node_shift(ksim_handle* h, int32_t op, int64_t index) {
+  KsimCtx& c = h->ctx;
+  const std::vector<ColRef> cols = node_cols(h);
+  const int64_t n_new = op == KSIM_RELAY_INSERT ? c.n + 1 : c.n - 1;
+  int rc = relayout(h, cols, std::vector<int32_t>(cols.size(), -1), op, index, n_new);
+  if (rc) return rc;
+  c.n = n_new;
+  if (h->have_pods && h->n_pods) {
+    hipError_t e = ksim_launch_remap_hosts(h->d_pods, h->n_pods, index, op, h->stream);
+    if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "remap launch: %s", hipGetErrorString(e));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
+  ksim_rt_invalidate_layout(h);
+  return KSIM_OK;
+}
+
+}  // namespace
+
+void ksim_rt_invalidate_layout(ksim_handle* h) {
+  if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
+  if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
+  for (void* q : {(void*)h->t_leaves, (void*)h->t_levels, (void*)h->t_fit, (void*)h->t_y, (void*)h->sw_dac,
+                  (void*)h->sw_dam, (void*)h->sw_yc, (void*)h->sw_ym, (void*)h->mirror})
+    dev_free(h, q);
+  h->t_leaves = nullptr; h->t_levels = nullptr; h->t_fit = nullptr; h->t_y = nullptr;
+  h->sw_dac = h->sw_dam = h->sw_yc = h->sw_ym = nullptr;
+  h->mirror = nullptr;
+  h->mirror_n = 0;
+  h->tree_planned = h->tree_ok = h->tree_valid = false;
+}
+
+extern "C" {
+
+int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports, int32_t n_ports,
+                      const ksim_scalar_req* scalars, int32_t n_scalars, int32_t assume, ksim_result* out) {
+  int rc = check_ready(h, "ksim_schedule_one");
+  if (rc) return rc;
+  if (!out) return ksim_fail(h, KSIM_E_INVAL, "ksim_schedule_one: null result");
+  if ((rc = check_pod_args(h, pod, n_ports, n_scalars, ports, scalars, "ksim_schedule_one"))) return rc;
+  KsimCtx& c = h->ctx;
+  if (c.n == 0) return ksim_fail(h, KSIM_E_NO_NODES, "no nodes available to schedule pods");
+  // room for the pod's ports if it is assumed (and at least one slot column to test against)
+  if ((assume || c.port_slots == 0) && (rc = ensure_port_room(h, pod->port_cnt))) return rc;
+  if ((rc = ksim_rt_check_pod(h, *pod, n_ports, n_scalars, scalars, "ksim_schedule_one"))) return rc;
+  KsimCtx cs;
+  if ((rc = stage_pod(h, *pod, ports, scalars, &cs))) return rc;
+  cs.collect = 1;  // the FitError histogram is part of the answer
+  cs.no_commit = assume ? 0 : 1;
+  const int npt = ksim_rt_pick_npt(c.n);
+  cs.chunk = (int64_t)KSIM_BLOCK * npt;
+  const int grid = (int)((c.n + cs.chunk - 1) / cs.chunk);
+  if ((rc = ksim_rt_ensure_partials(h, grid))) return rc;
+  cs.partials = c.partials;
+  hipError_t e = ksim_launch_scan(&cs, npt, 1, grid, h->stream);
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "scan launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipMemcpyAsync(h->res_host, h->res_dev, KSIM_RES_WORDS * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipMemcpyAsync(h->ctr_host, c.counter, 8, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  const int32_t* r = h->res_host;
+  memset(out, 0, sizeof *out);
+  out->node = r[KSIM_RES_NODE];
+  out->fit_nodes = r[KSIM_RES_FIT];
+  out->last_node_index = *h->ctr_host;
+  if (out->node < 0) memcpy(out->reasons, r + KSIM_RES_REASONS, sizeof out->reasons);
+  if (assume && out->node >= 0) return after_commit(h, pod->port_cnt);
+  int32_t err = 0;
+  HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
+  if (err) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
+  return KSIM_OK;
+}
+
+static int pod_delta(ksim_handle* h, int64_t node, const ksim_pod* pod, const uint64_t* ports, int32_t n_ports,
+                     const ksim_scalar_req* scalars, int32_t n_scalars, bool add, const char* where) {
+  int rc = check_ready(h, where);
+  if (rc) return rc;
+  if ((rc = check_pod_args(h, pod, n_ports, n_scalars, ports, scalars, where))) return rc;
+  if (node < 0 || node >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "%s: node %lld out of range", where, (long long)node);
+  if (add && (rc = ensure_port_room(h, pod->port_cnt))) return rc;
+  if ((rc = ksim_rt_check_pod(h, *pod, n_ports, n_scalars, scalars, where))) return rc;
+  KsimCtx cs;
+  if ((rc = stage_pod(h, *pod, ports, scalars, &cs))) return rc;
+  hipError_t e = add ? ksim_launch_assume(&cs, 0, node, h->res_dev + KSIM_RES_STATUS, h->stream)
+                     : ksim_launch_release(&cs, 0, node, h->stream);
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "%s launch: %s", where, hipGetErrorString(e));
+  HIPCHK(h, hipMemcpyAsync(h->res_host, h->res_dev, KSIM_RES_WORDS * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (!add) {  // a release can only shrink quantities, but never below zero in a consistent cache
+    h->tree_valid = false;
+    return KSIM_OK;
+  }
+  return after_commit(h, pod->port_cnt);
+}
+
+int ksim_pod_add(ksim_handle* h, int64_t node, const ksim_pod* pod, const uint64_t* ports, int32_t n_ports,
+                 const ksim_scalar_req* scalars, int32_t n_scalars) {
+  return pod_delta(h, node, pod, ports, n_ports, scalars, n_scalars, true, "ksim_pod_add");
+}
+
+int ksim_pod_remove(ksim_handle* h, int64_t node, const ksim_pod* pod, const uint64_t* ports, int32_t n_ports,
+                    const ksim_scalar_req* scalars, int32_t n_scalars) {
+  return pod_delta(h, node, pod, ports, n_ports, scalars, n_scalars, false, "ksim_pod_remove");
+}
+
+int ksim_assume(ksim_handle* h, int64_t pod, int64_t node) {
+  if (!h) return ksim_fail(h, KSIM_E_INVAL, "ksim_assume: null handle");
+  if (!h->have_pods) return ksim_fail(h, KSIM_E_STATE, "ksim_assume: nothing loaded");
+  if (pod < 0 || pod >= h->n_pods || node < 0 || node >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "ksim_assume: out of range");
+  HIPCHK(h, hipSetDevice(h->device));
+  int rc = ensure_staging(h, 0, 0);
+  if (rc) return rc;
+  HIPCHK(h, hipMemsetAsync(h->res_dev, 0, KSIM_RES_WORDS * 4, h->stream));
+  hipError_t e = ksim_launch_assume(&h->ctx, pod, node, h->res_dev + KSIM_RES_STATUS, h->stream);
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "assume launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipMemcpyAsync(h->res_host, h->res_dev, KSIM_RES_WORDS * 4, hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  return after_commit(h, 0);
+}
+
+int ksim_node_add(ksim_handle* h, int64_t index, const ksim_node_row* row) {
+  int rc = check_ready(h, "ksim_node_add");
+  if (rc) return rc;
+  if (index < 0 || index > h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "ksim_node_add: rank %lld out of range", (long long)index);
+  if (h->ctx.n >= (int64_t)INT32_MAX) return ksim_fail(h, KSIM_E_INVAL, "ksim_node_add: too many nodes");
+  if ((rc = check_row(h, row, true, "ksim_node_add"))) return rc;
+  if (row->port_count > h->ctx.port_slots &&
+      (rc = grow_port_slots(h, std::max({row->port_count, 2 * h->ctx.port_slots, 4}))))
+    return rc;
+  if ((rc = node_shift(h, KSIM_RELAY_INSERT, index))) return rc;
+  if ((rc = set_row(h, index, row, true))) return rc;
+  h->port_bound = std::max<int64_t>(h->port_bound, row->port_count);
+  h->max_label_set = std::max(h->max_label_set, row->label_set);
+  h->max_taint_set = std::max(h->max_taint_set, row->taint_set);
+  return KSIM_OK;
+}
+
+int ksim_node_update(ksim_handle* h, int64_t index, const ksim_node_row* row) {
+  int rc = check_ready(h, "ksim_node_update");
+  if (rc) return rc;
+  if (index < 0 || index >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "ksim_node_update: rank %lld out of range", (long long)index);
+  if ((rc = check_row(h, row, false, "ksim_node_update"))) return rc;
+  if ((rc = set_row(h, index, row, false))) return rc;
+  ksim_rt_invalidate_layout(h);  // allocatable feeds the trees' and sweeps' derived columns
+  h->max_label_set = std::max(h->max_label_set, row->label_set);
+  h->max_taint_set = std::max(h->max_taint_set, row->taint_set);
+  return KSIM_OK;
+}
+
+int ksim_node_remove(ksim_handle* h, int64_t index) {
+  int rc = check_ready(h, "ksim_node_remove");
+  if (rc) return rc;
+  if (index < 0 || index >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "ksim_node_remove: rank %lld out of range", (long long)index);
+  return node_shift(h, KSIM_RELAY_REMOVE, index);
+}
+
+int ksim_node_count(ksim_handle* h, int64_t* out) {
+  if (!h || !out) return ksim_fail(h, KSIM_E_INVAL, "ksim_node_count: null argument");
+  *out = h->have_nodes ? h->ctx.n : 0;
+  return KSIM_OK;
+}
+
+}  // extern "C"

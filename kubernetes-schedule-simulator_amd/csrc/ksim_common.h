@@ -71,7 +71,7 @@ struct KsimCtx {
   uint32_t preds;
   int32_t no_prio;
   int32_t collect;
-  int32_t pad0;
+  int32_t no_commit;      // 1: decide only (genericScheduler.Schedule without Scheduler.assume)
   int64_t w[KSIM_NW];
   // ---- run state ----
   int64_t* cursor;        // next pod to schedule (device)
@@ -84,6 +84,7 @@ struct KsimCtx {
   int32_t* err;           // sticky error word
   int64_t chunk;          // nodes per block
   uint64_t* dbg;          // diagnostic stamp sums (KSIM_STAMPS builds only), else null
+  int32_t* out_fit;       // optional (per-pod drop-in): [0] = len(filtered), [1] |= ksim_row_status
 };
 
 // Node-sharded mode (ksim_shard_*): this rank's place in the world and every rank's exchange
@@ -315,5 +316,48 @@ __device__ __forceinline__ void ksim_commit(const KsimCtx& c, const ksim_pod& P,
     if (cnt >= c.port_slots) { atomicOr(c.err, 1); continue; }
     c.ports[(int64_t)cnt * c.n + w] = key;
     c.port_count[w] = cnt + 1;
+  }
+}
+
+// Status of a committed row for the fast kernels' float64 arithmetic (ksim_pfast.hip,
+// ksim_tree.hip): bit 0 set when a cpu / memory quantity left [0, 2^48).
+__device__ __forceinline__ int32_t ksim_row_status(const KsimCtx& c, int64_t w) {
+  const int64_t lim = int64_t(1) << 48;
+  const int64_t a = c.req_cpu[w], b = c.req_mem[w], d = c.nz_cpu[w], e = c.nz_mem[w];
+  return (a < 0 || a >= lim || b < 0 || b >= lim || d < 0 || d >= lim || e < 0 || e >= lim) ? 1 : 0;
+}
+
+// Remove pod P from node w: NodeInfo.RemovePod (node_info.go:343-390) — the containers-only
+// requests and non-zero requests are subtracted, the pod count drops by one and the pod's
+// (ip, protocol, port) keys leave the node's HostPortInfo (HostPortInfo.Remove, utils.go:63-79,
+// set semantics: the key goes even if another pod added it too).  Single thread.
+__device__ __forceinline__ void ksim_uncommit(const KsimCtx& c, const ksim_pod& P, int64_t w) {
+  c.req_cpu[w] -= P.add_cpu;
+  c.req_mem[w] -= P.add_mem;
+  const int64_t g = c.req_gpu[w] - P.add_gpu;
+  const int64_t e = c.req_eph[w] - P.add_eph;
+  c.req_gpu[w] = g;
+  c.req_eph[w] = e;
+  c.nz_cpu[w] -= P.nz_cpu;
+  c.nz_mem[w] -= P.nz_mem;
+  c.pod_count[w] -= 1;
+  uint32_t fl = c.flags[w] & ~(KSIM_N_GPU_OVER | KSIM_N_EPH_OVER);
+  if (c.alloc_gpu[w] < g) fl |= KSIM_N_GPU_OVER;
+  if (c.alloc_eph[w] < e) fl |= KSIM_N_EPH_OVER;
+  c.flags[w] = fl;
+  for (int32_t s = 0; s < P.scalar_cnt; ++s) {
+    const ksim_scalar_req q = c.pod_scalars[P.scalar_off + s];
+    c.req_scalar[(int64_t)q.col * c.n + w] -= q.add;
+  }
+  for (int32_t k = 0; k < P.port_cnt; ++k) {
+    const uint64_t key = c.pod_ports[P.port_off + k];
+    const int32_t cnt = c.port_count[w];
+    for (int32_t s = 0; s < cnt; ++s) {
+      if (c.ports[(int64_t)s * c.n + w] != key) continue;
+      c.ports[(int64_t)s * c.n + w] = c.ports[(int64_t)(cnt - 1) * c.n + w];  // slot order is irrelevant
+      c.ports[(int64_t)(cnt - 1) * c.n + w] = 0;
+      c.port_count[w] = cnt - 1;
+      break;
+    }
   }
 }

@@ -1,0 +1,215 @@
+// ksim_handle.h — private host-side state of a ksim_handle, shared by the runtime
+// translation units (ksim_runtime.cpp: load / schedule / sweep / shard; ksim_cache.cpp: the
+// per-pod drop-in entry points and the scheduler-cache event mirror).  Not part of the C-ABI.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <array>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "ksim_common.h"
+#include "ksim_sweep.h"
+#include "ksim_tree.h"
+#include "ksim_f64.h"
+
+// ---- kernel launchers (the .hip translation units) ----
+extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, int grid, hipStream_t s);
+extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* fit, uint32_t* reasons, int64_t* score,
+                                       uint8_t* rcls, hipStream_t s);
+extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, int32_t* status, hipStream_t s);
+extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
+                                             int lds_rows, hipStream_t s);
+extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows);
+extern "C" size_t ksim_persistent_granule_bytes(int grid);
+extern "C" hipError_t ksim_sweep_prepare(const int64_t* ac, const int64_t* am, int64_t n, double* dac, double* dam,
+                                         double* yc, double* ym, hipStream_t st);
+extern "C" hipError_t ksim_sweep_launch(const int64_t* rc0, const int64_t* rm0, const int64_t* zc0, const int64_t* zm0,
+                                        const int32_t* c0, const ksim_pod* pods, void* fpods, const SwArgs* args,
+                                        int32_t n_scen, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st);
+extern "C" int ksim_pfast_config(int64_t n, int max_grid, int stream, int* grid, int* lds_rows);
+extern "C" hipError_t ksim_pstream_prepare(const KsimCtx* c, double* mirror, hipStream_t s);
+extern "C" size_t ksim_pfast_granule_bytes(void);
+extern "C" size_t ksim_shard_xchg_bytes(void);
+extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, double* mirror,
+                                        const KsimShard* sh, hipStream_t s);
+extern "C" hipError_t ksim_tree_build(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
+                                      const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
+                                      double* ty, const KsimTreeSweep* sw, hipStream_t s);
+extern "C" hipError_t ksim_tree_sweep_init(const KsimCtx* c, const KsimTreeSweep* sw, hipStream_t s);
+extern "C" hipError_t ksim_tree_launch(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
+                                       const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
+                                       double* ty, const KsimTreeSweep* sw, hipStream_t s);
+// scheduler-cache kernels (ksim_cache.hip)
+struct KsimRelayout;
+extern "C" hipError_t ksim_launch_relayout(const KsimRelayout* r, hipStream_t s);
+extern "C" hipError_t ksim_launch_set_row(const KsimCtx* c, int64_t node, const uint64_t* pack, int32_t full,
+                                          hipStream_t s);
+extern "C" hipError_t ksim_launch_release(const KsimCtx* c, int64_t pod, int64_t node, hipStream_t s);
+extern "C" hipError_t ksim_launch_remap_hosts(ksim_pod* pods, int64_t n_pods, int64_t idx, int32_t op, hipStream_t s);
+extern "C" hipError_t ksim_launch_port_max(const int32_t* port_count, int64_t n, int32_t* out, hipStream_t s);
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+// Per-pod staging area of the drop-in entry points (ksim_schedule_one, ksim_pod_add/remove):
+// one packed host->device upload {cursor, pod, ports, scalars} and one result block.
+#define KSIM_RES_NODE 0
+#define KSIM_RES_FIT 1
+#define KSIM_RES_STATUS 2   /* bit 0: a committed quantity left the fast kernels' exact range */
+#define KSIM_RES_REASONS 4
+#define KSIM_RES_WORDS (KSIM_RES_REASONS + KSIM_NREASONS)
+
+struct ksim_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  ksim_config cfg{};
+  std::string err;
+  std::vector<DevBuf> bufs;
+  KsimCtx ctx{};
+  bool have_nodes = false, have_classes = false, have_pods = false;
+  int64_t n_pods = 0, pod_cap = 0;
+  int64_t n_port_keys = 0, port_key_cap = 0;     // pod-port array (queue)
+  int64_t n_scalar_reqs = 0, scalar_req_cap = 0; // pod-scalar array (queue)
+  ksim_pod* d_pods = nullptr;                    // non-const views of the queue arrays in ctx
+  uint64_t* d_pod_ports = nullptr;
+  ksim_scalar_req* d_pod_scalars = nullptr;
+  int32_t n_classes = 0;
+  int32_t n_label_sets = 0, n_taint_sets = 0;   // of the loaded class tables
+  int32_t max_label_set = -1, max_taint_set = -1;  // largest ids the node table uses
+  std::vector<void*> class_bufs;                 // class-table buffers (replaced on reload)
+  // launch-mode graph
+  hipGraphExec_t gexec = nullptr;
+  hipGraph_t graph = nullptr;
+  int g_batch = 0, g_npt = 0, g_collect = -1, part_cap = 0;
+  uint64_t* granules = nullptr;
+  KsimCtx* ctx_dev = nullptr;  // device copy of ctx for non-inlined device functions
+  size_t gran_bytes = 0;
+  int64_t g_first = -1, g_end = -1;
+  // host-side copies needed for validation
+  std::vector<int32_t> h_n_tt, h_n_na;
+  // per queued pod: class and "resource-only apart from its reduce classes" (ksim_is_fast_pod)
+  std::vector<int32_t> q_cls;
+  std::vector<uint8_t> q_base;
+  // fast_pre[i] = resource-only pods among the first i of the queue (ksim_is_fast_pod)
+  std::vector<int64_t> fast_pre;
+  // the fast kernel computes in float64: every node cpu / memory quantity below 2^48 at load
+  // (pods: checked per pod in fast_pre); cleared for good once a commit reaches 2^48
+  bool pfast_off = false;
+  std::vector<int64_t> pod_qmax;  // largest cpu / memory quantity of each pod (sweep bound)
+  // scenario sweep: static float64 columns (once) and per-call scratch (grown on demand)
+  double *sw_dac = nullptr, *sw_dam = nullptr, *sw_yc = nullptr, *sw_ym = nullptr;
+  void* sw_scratch = nullptr;
+  size_t sw_scratch_bytes = 0;
+  // node-sharded mode (ksim_shard_*): world == 1 is the ordinary single-device mode
+  KsimShard shard{0, 1, 0, 0, nullptr, {}};
+  void* ipc_mapped[KSIM_MAX_RANKS] = {};  // peers' exchange buffers opened through IPC
+  uint64_t start_epoch = 0;                // host start handshake (node-sharded calls)
+  int max_grid = 0;                        // workgroups per launch (0 = one per CU)
+  double* mirror = nullptr;                // streaming fast kernel: float64 image [6][n]
+  int64_t mirror_n = 0;
+  // tree mode (ksim_tree.hip): tree class of every resource-only pod (-1 otherwise), the class
+  // inputs, the geometry and the device trees; tree_valid = the trees describe the current
+  // node table (any other commit path clears it)
+  int32_t n_tcls = 0;                      // -1: more classes than the tree supports
+  int32_t* tcls = nullptr;
+  int64_t tcls_cap = 0;
+  KsimTreeClass* tclass = nullptr;
+  std::map<std::array<int64_t, 5>, int32_t> tkeys;
+  std::vector<KsimTreeClass> tclass_h;
+  bool tree_planned = false, tree_ok = false, tree_valid = false;
+  KsimTreeGeo geo{};
+  int32_t* t_leaves = nullptr;
+  uint64_t* t_levels = nullptr;
+  int32_t* t_fit = nullptr;
+  double* t_y = nullptr;
+  void* swt_scratch = nullptr;  // tree sweep: per-scenario columns, trees, counters, outputs
+  size_t swt_bytes = 0;
+  // per-pod drop-in staging (ksim_cache.cpp)
+  char* stg_dev = nullptr;      // device: [int64 cursor][ksim_pod][ports][scalars]
+  char* stg_host = nullptr;     // pinned host mirror of the upload
+  size_t stg_cap = 0;
+  int32_t* res_dev = nullptr;   // device result block (KSIM_RES_*)
+  int32_t* res_host = nullptr;  // pinned
+  uint64_t* ctr_host = nullptr; // pinned copy of lastNodeIndex after a call
+  int64_t port_bound = 0;       // upper bound of max(port_count) over the nodes
+};
+
+int ksim_fail(ksim_handle* h, int code, const char* fmt, ...);
+
+#define HIPCHK(h, x)                                                                              \
+  do {                                                                                            \
+    hipError_t e_ = (x);                                                                          \
+    if (e_ != hipSuccess) return ksim_fail((h), KSIM_E_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
+  } while (0)
+
+template <class T>
+static int dev_alloc(ksim_handle* h, T** out, size_t count) {
+  *out = nullptr;
+  size_t bytes = std::max<size_t>(count * sizeof(T), 16);
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, bytes);
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  h->bufs.push_back({p, bytes});
+  *out = reinterpret_cast<T*>(p);
+  return KSIM_OK;
+}
+
+template <class T>
+static int dev_upload(ksim_handle* h, T** out, const T* src, size_t count, bool zero_if_null = true) {
+  int rc = dev_alloc(h, out, count);
+  if (rc) return rc;
+  if (src && count) {
+    HIPCHK(h, hipMemcpyAsync(*out, src, count * sizeof(T), hipMemcpyHostToDevice, h->stream));
+  } else if (zero_if_null && count) {
+    HIPCHK(h, hipMemsetAsync(*out, 0, count * sizeof(T), h->stream));
+  }
+  return KSIM_OK;
+}
+
+// Free one buffer of the handle (the stream is drained first: hipFree must not race queued work).
+static inline void dev_free(ksim_handle* h, const void* p) {
+  if (!p) return;
+  (void)hipStreamSynchronize(h->stream);
+  (void)hipFree(const_cast<void*>(p));
+  h->bufs.erase(std::remove_if(h->bufs.begin(), h->bufs.end(), [p](const DevBuf& b) { return b.p == p; }),
+                h->bufs.end());
+}
+
+// Grow a device array to new_cap elements keeping the first `keep` elements.
+template <class T>
+static int dev_grow(ksim_handle* h, T** p, size_t keep, size_t new_cap) {
+  T* q = nullptr;
+  int rc = dev_alloc(h, &q, new_cap);
+  if (rc) return rc;
+  if (*p && keep) HIPCHK(h, hipMemcpyAsync(q, *p, keep * sizeof(T), hipMemcpyDeviceToDevice, h->stream));
+  dev_free(h, *p);
+  *p = q;
+  return KSIM_OK;
+}
+
+// ---- runtime internals shared across translation units (ksim_runtime.cpp) ----
+// Append pods to the queue (first call: the initial load).  Validates, grows the device
+// arrays, extends the per-pod host bookkeeping (fast-kernel eligibility, tree classes).
+int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const uint64_t* ports, int64_t n_ports,
+                   const ksim_scalar_req* scalars, int64_t n_scalars);
+// Recompute fast_pre from q_cls / q_base after the class tables changed.
+void ksim_rt_recompute_fast(ksim_handle* h);
+// Everything derived from the node table's size, pointers or static columns is stale
+// (launch graph, tree geometry, sweep statics, streaming mirror).
+void ksim_rt_invalidate_layout(ksim_handle* h);
+// Validate one pod descriptor against the loaded tables (ports / scalars relative to the
+// passed arrays).
+int ksim_rt_check_pod(ksim_handle* h, const ksim_pod& p, int64_t n_ports, int64_t n_scalars,
+                      const ksim_scalar_req* scalars, const char* where);
+int ksim_rt_ensure_partials(ksim_handle* h, int grid);
+int ksim_rt_pick_npt(int64_t n);

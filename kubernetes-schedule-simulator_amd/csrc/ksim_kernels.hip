@@ -343,11 +343,15 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       }
       if (node < 0) atomicOr(c.err, 2);  // inconsistent partials: must never happen
       D.node = node;
-      if (node >= 0) ksim_commit(c, P, node);
+      if (node >= 0 && !c.no_commit) {
+        ksim_commit(c, P, node);
+        if (c.out_fit) c.out_fit[1] |= ksim_row_status(c, node);
+      }
     }
   }
   if (tid == 0) {
     c.out_node[pod] = (int32_t)D.node;
+    if (c.out_fit) c.out_fit[0] = D.fitTotal;
     *c.cursor = pod + 1;
     *c.ticket = 0;
   }
@@ -369,9 +373,12 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_
   rcls[i] = (uint8_t)((k1 * k2 > 1) ? ksim_rclass(c, P, i, k1, k2) : 0);
 }
 
-// Commit one pod to one node (ksim_assume).
-__global__ void ksim_assume_kernel(KsimCtx c, int64_t pod, int64_t node) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) ksim_commit(c, c.pods[pod], node);
+// Commit one pod to one node (ksim_assume, ksim_pod_add); status |= ksim_row_status.
+__global__ void ksim_assume_kernel(KsimCtx c, int64_t pod, int64_t node, int32_t* status) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    ksim_commit(c, c.pods[pod], node);
+    *status |= ksim_row_status(c, node);
+  }
 }
 
 // Launch-mode entry points used by the host runtime (ksim_runtime.cpp).
@@ -403,7 +410,7 @@ extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* f
   return hipGetLastError();
 }
 
-extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, hipStream_t s) {
-  hipLaunchKernelGGL(ksim_assume_kernel, dim3(1), dim3(64), 0, s, *c, pod, node);
+extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, int32_t* status, hipStream_t s) {
+  hipLaunchKernelGGL(ksim_assume_kernel, dim3(1), dim3(64), 0, s, *c, pod, node, status);
   return hipGetLastError();
 }

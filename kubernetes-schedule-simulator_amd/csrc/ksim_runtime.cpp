@@ -4,115 +4,13 @@
 // pod queue and the run state, and drives the scan kernels on one HIP stream per handle.
 // No torch types cross this boundary; every entry point calls hipSetDevice (cgo calls may
 // land on any OS thread) and returns a KSIM_* status.
-#include <hip/hip_runtime.h>
-
-#include <algorithm>
-#include <array>
-#include <cstdarg>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <map>
-#include <string>
-#include <vector>
-
-#include "ksim_common.h"
-#include "ksim_sweep.h"
-#include "ksim_tree.h"
-#include "ksim_f64.h"
-
-extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, int grid, hipStream_t s);
-extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* fit, uint32_t* reasons, int64_t* score,
-                                       uint8_t* rcls, hipStream_t s);
-extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, hipStream_t s);
-extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
-                                             int lds_rows, hipStream_t s);
-extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows);
-extern "C" size_t ksim_persistent_granule_bytes(int grid);
-extern "C" hipError_t ksim_sweep_prepare(const int64_t* ac, const int64_t* am, int64_t n, double* dac, double* dam,
-                                         double* yc, double* ym, hipStream_t st);
-extern "C" hipError_t ksim_sweep_launch(const int64_t* rc0, const int64_t* rm0, const int64_t* zc0, const int64_t* zm0,
-                                        const int32_t* c0, const ksim_pod* pods, void* fpods, const SwArgs* args,
-                                        int32_t n_scen, hipEvent_t ev0, hipEvent_t ev1, hipStream_t st);
-extern "C" int ksim_pfast_config(int64_t n, int max_grid, int stream, int* grid, int* lds_rows);
-extern "C" hipError_t ksim_pstream_prepare(const KsimCtx* c, double* mirror, hipStream_t s);
-extern "C" size_t ksim_pfast_granule_bytes(void);
-extern "C" size_t ksim_shard_xchg_bytes(void);
-extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, double* mirror,
-                                        const KsimShard* sh, hipStream_t s);
-extern "C" hipError_t ksim_tree_build(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
-                                      const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
-                                      double* ty, const KsimTreeSweep* sw, hipStream_t s);
-extern "C" hipError_t ksim_tree_sweep_init(const KsimCtx* c, const KsimTreeSweep* sw, hipStream_t s);
-extern "C" hipError_t ksim_tree_launch(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
-                                       const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
-                                       double* ty, const KsimTreeSweep* sw, hipStream_t s);
+#include "ksim_handle.h"
 
 namespace {
-
 thread_local std::string g_err;
-
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-};
-
 }  // namespace
 
-struct ksim_handle {
-  int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-  ksim_config cfg{};
-  std::string err;
-  std::vector<DevBuf> bufs;
-  KsimCtx ctx{};
-  bool have_nodes = false, have_classes = false, have_pods = false;
-  int64_t n_pods = 0;
-  int32_t n_classes = 0;
-  int32_t n_ports_total = 0;
-  // launch-mode graph
-  hipGraphExec_t gexec = nullptr;
-  hipGraph_t graph = nullptr;
-  int g_batch = 0, g_npt = 0, g_collect = -1, part_cap = 0;
-  uint64_t* granules = nullptr;
-  KsimCtx* ctx_dev = nullptr;  // device copy of ctx for non-inlined device functions
-  size_t gran_bytes = 0;
-  int64_t g_first = -1, g_end = -1;
-  // host-side copies needed for validation
-  std::vector<int32_t> h_n_tt, h_n_na;
-  // fast_pre[i] = resource-only pods among the first i of the queue (ksim_is_fast_pod)
-  std::vector<int64_t> fast_pre;
-  // the fast kernel computes in float64: every node cpu / memory quantity below 2^48 at load
-  // (pods: checked per pod in fast_pre); cleared for good once a commit reaches 2^48
-  bool pfast_off = false;
-  std::vector<int64_t> pod_qmax;  // largest cpu / memory quantity of each pod (sweep bound)
-  // scenario sweep: static float64 columns (once) and per-call scratch (grown on demand)
-  double *sw_dac = nullptr, *sw_dam = nullptr, *sw_yc = nullptr, *sw_ym = nullptr;
-  void* sw_scratch = nullptr;
-  size_t sw_scratch_bytes = 0;
-  // node-sharded mode (ksim_shard_*): world == 1 is the ordinary single-device mode
-  KsimShard shard{0, 1, 0, 0, nullptr, {}};
-  void* ipc_mapped[KSIM_MAX_RANKS] = {};  // peers' exchange buffers opened through IPC
-  int max_grid = 0;                        // workgroups per launch (0 = one per CU)
-  double* mirror = nullptr;                // streaming fast kernel: float64 image [6][n]
-  // tree mode (ksim_tree.hip): tree class of every resource-only pod (-1 otherwise), the class
-  // inputs, the geometry and the device trees; tree_valid = the trees describe the current
-  // node table (any other commit path clears it)
-  int32_t n_tcls = 0;                      // -1: more classes than the tree supports
-  int32_t* tcls = nullptr;
-  KsimTreeClass* tclass = nullptr;
-  bool tree_planned = false, tree_ok = false, tree_valid = false;
-  KsimTreeGeo geo{};
-  int32_t* t_leaves = nullptr;
-  uint64_t* t_levels = nullptr;
-  int32_t* t_fit = nullptr;
-  double* t_y = nullptr;
-  void* swt_scratch = nullptr;  // tree sweep: per-scenario columns, trees, counters, outputs
-  size_t swt_bytes = 0;
-};
-
-static int fail(ksim_handle* h, int code, const char* fmt, ...) {
+int ksim_fail(ksim_handle* h, int code, const char* fmt, ...) {
   char buf[512];
   va_list ap;
   va_start(ap, fmt);
@@ -123,36 +21,6 @@ static int fail(ksim_handle* h, int code, const char* fmt, ...) {
   return code;
 }
 
-#define HIPCHK(h, x)                                                                         \
-  do {                                                                                       \
-    hipError_t e_ = (x);                                                                     \
-    if (e_ != hipSuccess) return fail((h), KSIM_E_DEVICE, "%s: %s", #x, hipGetErrorString(e_)); \
-  } while (0)
-
-template <class T>
-static int dev_alloc(ksim_handle* h, T** out, size_t count) {
-  *out = nullptr;
-  size_t bytes = std::max<size_t>(count * sizeof(T), 16);
-  void* p = nullptr;
-  hipError_t e = hipMalloc(&p, bytes);
-  if (e != hipSuccess) return fail(h, KSIM_E_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
-  h->bufs.push_back({p, bytes});
-  *out = reinterpret_cast<T*>(p);
-  return KSIM_OK;
-}
-
-template <class T>
-static int dev_upload(ksim_handle* h, T** out, const T* src, size_t count, bool zero_if_null = true) {
-  int rc = dev_alloc(h, out, count);
-  if (rc) return rc;
-  if (src && count) {
-    HIPCHK(h, hipMemcpyAsync(*out, src, count * sizeof(T), hipMemcpyHostToDevice, h->stream));
-  } else if (zero_if_null && count) {
-    HIPCHK(h, hipMemsetAsync(*out, 0, count * sizeof(T), h->stream));
-  }
-  return KSIM_OK;
-}
-
 extern "C" {
 
 int ksim_abi_version(void) { return KSIM_ABI_VERSION; }
@@ -160,26 +28,26 @@ int ksim_abi_version(void) { return KSIM_ABI_VERSION; }
 const char* ksim_last_error(const ksim_handle* h) { return h ? h->err.c_str() : g_err.c_str(); }
 
 int ksim_create(const ksim_config* cfg, ksim_handle** out) {
-  if (!cfg || !out) return fail(nullptr, KSIM_E_INVAL, "ksim_create: null argument");
+  if (!cfg || !out) return ksim_fail(nullptr, KSIM_E_INVAL, "ksim_create: null argument");
   *out = nullptr;
   int ndev = 0;
   hipError_t e = hipGetDeviceCount(&ndev);
   if (e != hipSuccess || ndev == 0)
-    return fail(nullptr, KSIM_E_DEVICE, "ksim_create: no HIP device (%s)", hipGetErrorString(e));
-  if (cfg->device < 0 || cfg->device >= ndev) return fail(nullptr, KSIM_E_INVAL, "ksim_create: bad device %d", cfg->device);
+    return ksim_fail(nullptr, KSIM_E_DEVICE, "ksim_create: no HIP device (%s)", hipGetErrorString(e));
+  if (cfg->device < 0 || cfg->device >= ndev) return ksim_fail(nullptr, KSIM_E_INVAL, "ksim_create: bad device %d", cfg->device);
   for (int k = 0; k < KSIM_NW; ++k)
-    if (cfg->weights[k] < 0) return fail(nullptr, KSIM_E_INVAL, "ksim_create: negative weight in slot %d", k);
+    if (cfg->weights[k] < 0) return ksim_fail(nullptr, KSIM_E_INVAL, "ksim_create: negative weight in slot %d", k);
   if (cfg->mode < KSIM_MODE_AUTO || cfg->mode > KSIM_MODE_TREE)
-    return fail(nullptr, KSIM_E_INVAL, "ksim_create: unknown mode %d", cfg->mode);
+    return ksim_fail(nullptr, KSIM_E_INVAL, "ksim_create: unknown mode %d", cfg->mode);
   const uint32_t known = (1u << 11) - 1;
-  if (cfg->predicates & ~known) return fail(nullptr, KSIM_E_UNSUPPORTED, "ksim_create: unknown predicate bits");
+  if (cfg->predicates & ~known) return ksim_fail(nullptr, KSIM_E_UNSUPPORTED, "ksim_create: unknown predicate bits");
   ksim_handle* h = new ksim_handle();
   h->device = cfg->device;
   h->cfg = *cfg;
   if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
     delete h;
-    return fail(nullptr, KSIM_E_DEVICE, "ksim_create: stream/event creation failed");
+    return ksim_fail(nullptr, KSIM_E_DEVICE, "ksim_create: stream/event creation failed");
   }
   KsimCtx& c = h->ctx;
   c.preds = cfg->predicates;
@@ -198,7 +66,7 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
   (void)hipMemcpyAsync(c.counter, &cfg->last_node_index, 8, hipMemcpyHostToDevice, h->stream);
   if (hipStreamSynchronize(h->stream) != hipSuccess) {
     ksim_destroy(h);
-    return fail(nullptr, KSIM_E_DEVICE, "ksim_create: initial copies failed");
+    return ksim_fail(nullptr, KSIM_E_DEVICE, "ksim_create: initial copies failed");
   }
   if (const char* g = getenv("KSIM_MAX_GRID")) h->max_grid = atoi(g);
   *out = h;
@@ -215,6 +83,8 @@ void ksim_destroy(ksim_handle* h) {
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
   if (h->graph) (void)hipGraphDestroy(h->graph);
   for (auto& b : h->bufs) (void)hipFree(b.p);
+  for (void* q : {(void*)h->stg_host, (void*)h->res_host, (void*)h->ctr_host})
+    if (q) (void)hipHostFree(q);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -222,15 +92,15 @@ void ksim_destroy(ksim_handle* h) {
 }
 
 int ksim_load_nodes(ksim_handle* h, const ksim_node_table* t) {
-  if (!h || !t) return fail(h, KSIM_E_INVAL, "ksim_load_nodes: null argument");
-  if (h->have_nodes) return fail(h, KSIM_E_STATE, "ksim_load_nodes: node table already loaded");
+  if (!h || !t) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_nodes: null argument");
+  if (h->have_nodes) return ksim_fail(h, KSIM_E_STATE, "ksim_load_nodes: node table already loaded");
   HIPCHK(h, hipSetDevice(h->device));
   const int64_t n = t->n_nodes;
-  if (n <= 0) return fail(h, KSIM_E_INVAL, "no nodes available to schedule pods");
-  if (n > (int64_t)INT32_MAX) return fail(h, KSIM_E_INVAL, "ksim_load_nodes: too many nodes");
-  if (t->n_scalar < 0 || t->n_scalar > KSIM_MAX_SCALAR) return fail(h, KSIM_E_UNSUPPORTED, "n_scalar %d > %d", t->n_scalar, KSIM_MAX_SCALAR);
-  if (t->port_slots < 0 || t->port_slots > 4096) return fail(h, KSIM_E_INVAL, "port_slots out of range");
-  if (!t->alloc_cpu || !t->alloc_mem || !t->allowed_pods) return fail(h, KSIM_E_INVAL, "ksim_load_nodes: missing column");
+  if (n < 0) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_nodes: negative node count");
+  if (n > (int64_t)INT32_MAX) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_nodes: too many nodes");
+  if (t->n_scalar < 0 || t->n_scalar > KSIM_MAX_SCALAR) return ksim_fail(h, KSIM_E_UNSUPPORTED, "n_scalar %d > %d", t->n_scalar, KSIM_MAX_SCALAR);
+  if (t->port_slots < 0 || t->port_slots > 4096) return ksim_fail(h, KSIM_E_INVAL, "port_slots out of range");
+  if (n && (!t->alloc_cpu || !t->alloc_mem || !t->allowed_pods)) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_nodes: missing column");
   KsimCtx& c = h->ctx;
   c.n = n;
   c.n_scalar = t->n_scalar;
@@ -246,9 +116,20 @@ int ksim_load_nodes(ksim_handle* h, const ksim_node_table* t) {
     fl[i] = f;
   }
   if (t->port_count && t->ports) {
-    for (int64_t i = 0; i < n; ++i)
-      if (t->port_count[i] < 0 || t->port_count[i] > t->port_slots) return fail(h, KSIM_E_INVAL, "port_count[%lld] out of range", (long long)i);
+    for (int64_t i = 0; i < n; ++i) {
+      if (t->port_count[i] < 0 || t->port_count[i] > t->port_slots) return ksim_fail(h, KSIM_E_INVAL, "port_count[%lld] out of range", (long long)i);
+      h->port_bound = std::max<int64_t>(h->port_bound, t->port_count[i]);
+    }
   }
+  h->max_label_set = h->max_taint_set = -1;
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t ls = t->label_set ? t->label_set[i] : 0, ts = t->taint_set ? t->taint_set[i] : 0;
+    if (ls < 0 || ts < 0) return ksim_fail(h, KSIM_E_INVAL, "node %lld: negative label / taint set id", (long long)i);
+    h->max_label_set = std::max(h->max_label_set, ls);
+    h->max_taint_set = std::max(h->max_taint_set, ts);
+  }
+  if (h->have_classes && (h->max_label_set >= h->n_label_sets || h->max_taint_set >= h->n_taint_sets))
+    return ksim_fail(h, KSIM_E_INVAL, "ksim_load_nodes: label / taint set id beyond the loaded class tables");
   const size_t S = (size_t)t->n_scalar;
   int rc;
   int64_t *ac, *am, *ag, *ae, *as;
@@ -279,17 +160,21 @@ int ksim_load_nodes(ksim_handle* h, const ksim_node_table* t) {
 }
 
 int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
-  if (!h || !t) return fail(h, KSIM_E_INVAL, "ksim_load_classes: null argument");
-  if (h->have_classes) return fail(h, KSIM_E_STATE, "ksim_load_classes: already loaded");
+  if (!h || !t) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_classes: null argument");
   HIPCHK(h, hipSetDevice(h->device));
   if (t->n_classes <= 0 || t->n_label_sets <= 0 || t->n_taint_sets <= 0)
-    return fail(h, KSIM_E_INVAL, "ksim_load_classes: empty tables");
+    return ksim_fail(h, KSIM_E_INVAL, "ksim_load_classes: empty tables");
+  // a reload (new pod classes, label sets or taint sets) must still cover everything in use
+  if (h->have_nodes && (h->max_label_set >= t->n_label_sets || h->max_taint_set >= t->n_taint_sets))
+    return ksim_fail(h, KSIM_E_INVAL, "ksim_load_classes: the node table uses label / taint sets beyond the new tables");
+  for (int32_t k : h->q_cls)
+    if (k >= t->n_classes) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_classes: a queued pod uses class %d beyond the new tables", k);
   const size_t C = t->n_classes, L = t->n_label_sets, T = t->n_taint_sets;
   const size_t lw = (L + 31) / 32, tw = (T + 31) / 32;
   for (size_t k = 0; k < C; ++k) {
     const int a = t->n_tt ? t->n_tt[k] : 1, b = t->n_na ? t->n_na[k] : 1;
     if (a < 1 || b < 1 || a * b > KSIM_MAX_RCLASS)
-      return fail(h, KSIM_E_UNSUPPORTED, "class %zu: %d x %d reduce classes exceed %d", k, a, b, KSIM_MAX_RCLASS);
+      return ksim_fail(h, KSIM_E_UNSUPPORTED, "class %zu: %d x %d reduce classes exceed %d", k, a, b, KSIM_MAX_RCLASS);
   }
   KsimCtx& c = h->ctx;
   int rc;
@@ -298,6 +183,7 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
   int32_t *ntt, *nna;
   int64_t *tv, *nv;
   std::vector<int32_t> ones(C, 1);
+  const size_t nb0 = h->bufs.size();
   if ((rc = dev_upload(h, &so, t->sel_ok, C * lw)) || (rc = dev_upload(h, &to, t->taint_ok, C * tw)) ||
       (rc = dev_upload(h, &no, t->noexec_ok, C * tw)) || (rc = dev_upload(h, &tc, t->tt_class, C * T)) ||
       (rc = dev_upload(h, &nc, t->na_class, C * L)) ||
@@ -305,128 +191,232 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
       (rc = dev_upload(h, &nna, t->n_na ? t->n_na : ones.data(), C)) ||
       (rc = dev_upload(h, &tv, t->tt_val, C * KSIM_MAX_RCLASS)) || (rc = dev_upload(h, &nv, t->na_val, C * KSIM_MAX_RCLASS)))
     return rc;
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (void* q : h->class_bufs) dev_free(h, q);  // the previous tables (reload)
+  h->class_bufs.clear();
+  for (size_t k = nb0; k < h->bufs.size(); ++k) h->class_bufs.push_back(h->bufs[k].p);
   c.sel_ok = so; c.taint_ok = to; c.noexec_ok = no; c.tt_class = tc; c.na_class = nc;
   c.n_tt = ntt; c.n_na = nna; c.tt_val = tv; c.na_val = nv;
   c.lwords = (int32_t)lw; c.twords = (int32_t)tw;
   c.n_label_sets = (int32_t)L; c.n_taint_sets = (int32_t)T;
   h->n_classes = t->n_classes;
+  h->n_label_sets = t->n_label_sets;
+  h->n_taint_sets = t->n_taint_sets;
   h->h_n_tt.assign(t->n_tt ? t->n_tt : ones.data(), (t->n_tt ? t->n_tt : ones.data()) + C);
   h->h_n_na.assign(t->n_na ? t->n_na : ones.data(), (t->n_na ? t->n_na : ones.data()) + C);
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  // class pointers are baked into the launch graph's kernel arguments
+  if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
+  if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
+  if (h->have_classes) ksim_rt_recompute_fast(h);  // reduce-class counts decide fast-kernel eligibility
   h->have_classes = true;
   return KSIM_OK;
 }
 
 int ksim_load_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const uint64_t* ports, int64_t n_ports,
                    const ksim_scalar_req* scalars, int64_t n_scalars) {
-  if (!h || (!pods && n_pods)) return fail(h, KSIM_E_INVAL, "ksim_load_pods: null argument");
-  if (!h->have_nodes || !h->have_classes) return fail(h, KSIM_E_STATE, "ksim_load_pods: load nodes and classes first");
-  if (h->have_pods) return fail(h, KSIM_E_STATE, "ksim_load_pods: pod queue already loaded");
-  if (n_pods < 0 || n_ports < 0 || n_scalars < 0) return fail(h, KSIM_E_INVAL, "ksim_load_pods: negative size");
+  if (!h || (!pods && n_pods)) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_pods: null argument");
+  if (!h->have_nodes || !h->have_classes) return ksim_fail(h, KSIM_E_STATE, "ksim_load_pods: load nodes and classes first");
+  if (h->have_pods) return ksim_fail(h, KSIM_E_STATE, "ksim_load_pods: pod queue already loaded (use ksim_append_pods)");
+  return ksim_rt_append(h, pods, n_pods, ports, n_ports, scalars, n_scalars);
+}
+
+int ksim_append_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const uint64_t* ports, int64_t n_ports,
+                     const ksim_scalar_req* scalars, int64_t n_scalars) {
+  if (!h || (!pods && n_pods)) return ksim_fail(h, KSIM_E_INVAL, "ksim_append_pods: null argument");
+  if (!h->have_nodes || !h->have_classes) return ksim_fail(h, KSIM_E_STATE, "ksim_append_pods: load nodes and classes first");
+  return ksim_rt_append(h, pods, n_pods, ports, n_ports, scalars, n_scalars);
+}
+
+}  // extern "C"
+
+int ksim_rt_check_pod(ksim_handle* h, const ksim_pod& p, int64_t n_ports, int64_t n_scalars,
+                      const ksim_scalar_req* scalars, const char* where) {
+  const KsimCtx& c = h->ctx;
+  if (p.cls < 0 || p.cls >= h->n_classes) return ksim_fail(h, KSIM_E_INVAL, "%s: class %d out of range", where, p.cls);
+  if (p.host < -2 || p.host >= c.n) return ksim_fail(h, KSIM_E_INVAL, "%s: host %d out of range", where, p.host);
+  if (p.port_cnt < 0 || p.port_off < 0 || (int64_t)p.port_off + p.port_cnt > n_ports)
+    return ksim_fail(h, KSIM_E_INVAL, "%s: port range out of bounds", where);
+  if (p.scalar_cnt < 0 || p.scalar_off < 0 || (int64_t)p.scalar_off + p.scalar_cnt > n_scalars)
+    return ksim_fail(h, KSIM_E_INVAL, "%s: scalar range out of bounds", where);
+  if (p.port_cnt > 0 && c.port_slots == 0)
+    return ksim_fail(h, KSIM_E_INVAL, "%s requests host ports but the node table has no port slots", where);
+  for (int32_t s = 0; s < p.scalar_cnt; ++s)
+    if (scalars[p.scalar_off + s].col < 0 || scalars[p.scalar_off + s].col >= c.n_scalar)
+      return ksim_fail(h, KSIM_E_INVAL, "%s: scalar request column out of range", where);
+  return KSIM_OK;
+}
+
+// Fast-kernel eligibility of a pod apart from its reduce classes (ksim_is_fast_pod, ksim_fast.h).
+static bool fast_base(const ksim_pod& p) {
+  const int64_t lim = (int64_t)1 << 48;
+  bool in_range = true;
+  for (int64_t v : {p.req_cpu, p.req_mem, p.add_cpu, p.add_mem, p.nz_cpu, p.nz_mem}) in_range &= v >= 0 && v < lim;
+  return in_range && p.host == -1 && p.port_cnt == 0 && p.scalar_cnt == 0 && p.req_gpu == 0 && p.req_eph == 0 &&
+         !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS));
+}
+
+static bool fast_k(const ksim_handle* h, int32_t cls) {
+  const int k1 = h->ctx.w[KSIM_W_TAINT_TOLERATION] ? h->h_n_tt[cls] : 1;
+  const int k2 = h->ctx.w[KSIM_W_NODE_AFFINITY] ? h->h_n_na[cls] : 1;
+  return k1 * k2 == 1;
+}
+
+void ksim_rt_recompute_fast(ksim_handle* h) {
+  const int64_t n = (int64_t)h->q_cls.size();
+  h->fast_pre.assign((size_t)n + 1, 0);
+  for (int64_t i = 0; i < n; ++i)
+    h->fast_pre[i + 1] = h->fast_pre[i] + ((h->q_base[i] && fast_k(h, h->q_cls[i])) ? 1 : 0);
+}
+
+int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const uint64_t* ports, int64_t n_ports,
+                   const ksim_scalar_req* scalars, int64_t n_scalars) {
+  if (n_pods < 0 || n_ports < 0 || n_scalars < 0) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_pods: negative size");
+  if ((n_ports && !ports) || (n_scalars && !scalars)) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_pods: null array");
   HIPCHK(h, hipSetDevice(h->device));
   KsimCtx& c = h->ctx;
+  char where[64];
   for (int64_t i = 0; i < n_pods; ++i) {
-    const ksim_pod& p = pods[i];
-    if (p.cls < 0 || p.cls >= h->n_classes) return fail(h, KSIM_E_INVAL, "pod %lld: class %d out of range", (long long)i, p.cls);
-    if (p.host < -2 || p.host >= c.n) return fail(h, KSIM_E_INVAL, "pod %lld: host %d out of range", (long long)i, p.host);
-    if (p.port_cnt < 0 || p.port_off < 0 || (int64_t)p.port_off + p.port_cnt > n_ports)
-      return fail(h, KSIM_E_INVAL, "pod %lld: port range out of bounds", (long long)i);
-    if (p.scalar_cnt < 0 || p.scalar_off < 0 || (int64_t)p.scalar_off + p.scalar_cnt > n_scalars)
-      return fail(h, KSIM_E_INVAL, "pod %lld: scalar range out of bounds", (long long)i);
-    if (p.port_cnt > 0 && c.port_slots == 0)
-      return fail(h, KSIM_E_INVAL, "pod %lld requests host ports but the node table has no port slots", (long long)i);
+    snprintf(where, sizeof where, "pod %lld", (long long)(h->n_pods + i));
+    int rc = ksim_rt_check_pod(h, pods[i], n_ports, n_scalars, scalars, where);
+    if (rc) return rc;
   }
-  for (int64_t s = 0; s < n_scalars; ++s)
-    if (scalars[s].col < 0 || scalars[s].col >= c.n_scalar)
-      return fail(h, KSIM_E_INVAL, "scalar request %lld: column out of range", (long long)s);
+  if (h->n_pods + n_pods > (int64_t)INT32_MAX * 8) return ksim_fail(h, KSIM_E_INVAL, "pod queue too long");
+  const int64_t P0 = h->n_pods, np = P0 + n_pods;
+  const int64_t K0 = h->n_port_keys, S0 = h->n_scalar_reqs;
+  if (K0 + n_ports > INT32_MAX || S0 + n_scalars > INT32_MAX) return ksim_fail(h, KSIM_E_INVAL, "pod port / scalar arrays too long");
   int rc;
-  ksim_pod* dp;
-  uint64_t* pp;
-  ksim_scalar_req* sp;
-  if ((rc = dev_upload(h, &dp, pods, n_pods)) || (rc = dev_upload(h, &pp, ports, n_ports)) ||
-      (rc = dev_upload(h, &sp, scalars, n_scalars)) || (rc = dev_alloc(h, &c.out_node, n_pods)) ||
-      (rc = dev_alloc(h, &c.out_reasons, c.collect ? n_pods * KSIM_NREASONS : 1)))
-    return rc;
-  c.pods = dp; c.pod_ports = pp; c.pod_scalars = sp;
-  // host mirror of ksim_is_fast_pod (ksim_fast.h): decides per call whether the specialised
-  // persistent kernel (ksim_pfast.hip) may run
-  h->fast_pre.assign((size_t)n_pods + 1, 0);
+  // grow the device arrays geometrically (appends amortised); the first load is exact
+  auto cap_for = [&](int64_t have, int64_t need) { return have == 0 ? std::max<int64_t>(need, 1) : std::max(need, 2 * have); };
+  if (np > h->pod_cap) {
+    const int64_t cap = cap_for(h->pod_cap, np);
+    int32_t* on = c.out_node;
+    if ((rc = dev_grow(h, &h->d_pods, (size_t)P0, (size_t)cap)) || (rc = dev_grow(h, &on, (size_t)P0, (size_t)cap)))
+      return rc;
+    c.out_node = on;
+    if (c.collect) {
+      int32_t* orr = c.out_reasons;
+      if ((rc = dev_grow(h, &orr, (size_t)P0 * KSIM_NREASONS, (size_t)cap * KSIM_NREASONS))) return rc;
+      HIPCHK(h, hipMemsetAsync(orr + P0 * KSIM_NREASONS, 0, (size_t)(cap - P0) * KSIM_NREASONS * 4, h->stream));
+      c.out_reasons = orr;
+    } else if (!c.out_reasons) {
+      int32_t* orr;
+      if ((rc = dev_alloc(h, &orr, 1))) return rc;
+      c.out_reasons = orr;
+    }
+    h->pod_cap = cap;
+  }
+  if (K0 + n_ports > h->port_key_cap) {
+    const int64_t cap = cap_for(h->port_key_cap, K0 + n_ports);
+    if ((rc = dev_grow(h, &h->d_pod_ports, (size_t)K0, (size_t)cap))) return rc;
+    h->port_key_cap = cap;
+  }
+  if (S0 + n_scalars > h->scalar_req_cap) {
+    const int64_t cap = cap_for(h->scalar_req_cap, S0 + n_scalars);
+    if ((rc = dev_grow(h, &h->d_pod_scalars, (size_t)S0, (size_t)cap))) return rc;
+    h->scalar_req_cap = cap;
+  }
+  // the queue's port / scalar offsets are relative to the passed arrays: rebase them
+  std::vector<ksim_pod> v(pods, pods + n_pods);
+  for (auto& p : v) {
+    p.port_off += (int32_t)K0;
+    p.scalar_off += (int32_t)S0;
+  }
+  if (n_pods) HIPCHK(h, hipMemcpyAsync(h->d_pods + P0, v.data(), n_pods * sizeof(ksim_pod), hipMemcpyHostToDevice, h->stream));
+  if (n_ports) HIPCHK(h, hipMemcpyAsync(h->d_pod_ports + K0, ports, n_ports * 8, hipMemcpyHostToDevice, h->stream));
+  if (n_scalars)
+    HIPCHK(h, hipMemcpyAsync(h->d_pod_scalars + S0, scalars, n_scalars * sizeof(ksim_scalar_req), hipMemcpyHostToDevice, h->stream));
+  c.pods = h->d_pods; c.pod_ports = h->d_pod_ports; c.pod_scalars = h->d_pod_scalars;
+  // host bookkeeping: fast-kernel eligibility, tree classes, float64 bounds
+  h->q_cls.resize((size_t)np);
+  h->q_base.resize((size_t)np);
+  h->fast_pre.resize((size_t)np + 1);
+  h->pod_qmax.resize((size_t)np);
+  std::vector<int32_t> tc((size_t)n_pods, -1);
+  const int32_t ntc0 = h->n_tcls;
   for (int64_t i = 0; i < n_pods; ++i) {
     const ksim_pod& p = pods[i];
-    const int k1 = c.w[KSIM_W_TAINT_TOLERATION] ? h->h_n_tt[p.cls] : 1;
-    const int k2 = c.w[KSIM_W_NODE_AFFINITY] ? h->h_n_na[p.cls] : 1;
-    const int64_t lim = (int64_t)1 << 48;
-    bool in_range = true;
-    for (int64_t v : {p.req_cpu, p.req_mem, p.add_cpu, p.add_mem, p.nz_cpu, p.nz_mem}) in_range &= v >= 0 && v < lim;
-    const bool fast = in_range && k1 * k2 == 1 && p.host == -1 && p.port_cnt == 0 && p.scalar_cnt == 0 &&
-                      p.req_gpu == 0 && p.req_eph == 0 && !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS));
-    h->fast_pre[i + 1] = h->fast_pre[i] + (fast ? 1 : 0);
-  }
-  // tree classes: resource-only pods with identical predicate / priority inputs
-  {
-    std::vector<int32_t> tc((size_t)n_pods, -1);
-    std::vector<KsimTreeClass> cls;
-    std::map<std::array<int64_t, 5>, int32_t> keys;
-    for (int64_t i = 0; i < n_pods && h->n_tcls >= 0; ++i) {
-      if (h->fast_pre[i + 1] == h->fast_pre[i]) continue;
-      const ksim_pod& p = pods[i];
-      const std::array<int64_t, 5> key{p.req_cpu, p.req_mem, p.nz_cpu, p.nz_mem,
-                                       (int64_t)(p.flags & (KSIM_POD_ANY_REQUEST | KSIM_POD_BEST_EFFORT))};
-      auto it = keys.find(key);
-      int32_t c = it == keys.end() ? (int32_t)keys.size() : it->second;
-      if (it == keys.end()) {
-        if (c == KSIM_TREE_MAX_CLASSES) { h->n_tcls = -1; break; }
-        keys.emplace(key, c);
-        cls.push_back(KsimTreeClass{(double)p.req_cpu, (double)p.req_mem, (double)p.nz_cpu, (double)p.nz_mem,
-                                    (p.flags & KSIM_POD_ANY_REQUEST) ? ~0u : 0u, (p.flags & KSIM_POD_BEST_EFFORT) ? ~0u : 0u});
-      }
-      tc[i] = (int32_t)c;
-    }
-    if (h->n_tcls >= 0) {
-      h->n_tcls = (int32_t)keys.size();
-      if ((rc = dev_upload(h, &h->tcls, tc.data(), tc.size())) ||
-          (rc = dev_upload(h, &h->tclass, cls.data(), cls.size())))
-        return rc;
-    }
-  }
-  h->pod_qmax.assign((size_t)n_pods, 0);
-  for (int64_t i = 0; i < n_pods; ++i) {
-    const ksim_pod& p = pods[i];
+    const int64_t q = P0 + i;
+    h->q_cls[q] = p.cls;
+    h->q_base[q] = fast_base(p) ? 1 : 0;
+    const bool fast = h->q_base[q] && fast_k(h, p.cls);
+    h->fast_pre[q + 1] = h->fast_pre[q] + (fast ? 1 : 0);
     int64_t m = 0;
-    for (int64_t v : {p.req_cpu, p.req_mem, p.add_cpu, p.add_mem, p.nz_cpu, p.nz_mem}) m = std::max(m, v);
-    h->pod_qmax[i] = m;
+    for (int64_t x : {p.req_cpu, p.req_mem, p.add_cpu, p.add_mem, p.nz_cpu, p.nz_mem}) m = std::max(m, x);
+    h->pod_qmax[q] = m;
+    // tree class: resource-only pods with identical predicate / priority inputs
+    if (!fast || h->n_tcls < 0) continue;
+    const std::array<int64_t, 5> key{p.req_cpu, p.req_mem, p.nz_cpu, p.nz_mem,
+                                     (int64_t)(p.flags & (KSIM_POD_ANY_REQUEST | KSIM_POD_BEST_EFFORT))};
+    auto it = h->tkeys.find(key);
+    int32_t k = it == h->tkeys.end() ? (int32_t)h->tkeys.size() : it->second;
+    if (it == h->tkeys.end()) {
+      if (k == KSIM_TREE_MAX_CLASSES) { h->n_tcls = -1; continue; }
+      h->tkeys.emplace(key, k);
+      h->tclass_h.push_back(KsimTreeClass{(double)p.req_cpu, (double)p.req_mem, (double)p.nz_cpu, (double)p.nz_mem,
+                                          (p.flags & KSIM_POD_ANY_REQUEST) ? ~0u : 0u,
+                                          (p.flags & KSIM_POD_BEST_EFFORT) ? ~0u : 0u});
+    }
+    tc[i] = k;
   }
-
-  if (c.collect) HIPCHK(h, hipMemsetAsync(c.out_reasons, 0, n_pods * KSIM_NREASONS * sizeof(int32_t), h->stream));
-  h->n_pods = n_pods;
+  if (h->n_tcls >= 0) {
+    if (np > h->tcls_cap) {
+      const int64_t cap = cap_for(h->tcls_cap, np);
+      if ((rc = dev_grow(h, &h->tcls, (size_t)P0, (size_t)cap))) return rc;
+      h->tcls_cap = cap;
+    }
+    if (n_pods) HIPCHK(h, hipMemcpyAsync(h->tcls + P0, tc.data(), n_pods * 4, hipMemcpyHostToDevice, h->stream));
+    const int32_t ntc = (int32_t)h->tkeys.size();
+    if (ntc != ntc0 || !h->tclass) {  // new classes: re-upload the inputs, re-plan the trees
+      if (h->tclass) dev_free(h, h->tclass);
+      h->tclass = nullptr;
+      if ((rc = dev_upload(h, &h->tclass, h->tclass_h.data(), h->tclass_h.size()))) return rc;
+      if (ntc != ntc0 && h->tree_planned) {
+        for (void* q : {(void*)h->t_leaves, (void*)h->t_levels, (void*)h->t_fit}) dev_free(h, q);
+        h->t_leaves = nullptr; h->t_levels = nullptr; h->t_fit = nullptr;
+        h->tree_planned = h->tree_ok = h->tree_valid = false;
+      }
+      h->n_tcls = ntc;
+    }
+  } else if (h->tree_planned) {
+    h->tree_ok = h->tree_valid = false;
+  }
+  h->n_pods = np;
+  h->n_port_keys = K0 + n_ports;
+  h->n_scalar_reqs = S0 + n_scalars;
+  // queue pointers are baked into the launch graph's kernel arguments
+  if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
+  if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   h->have_pods = true;
   return KSIM_OK;
 }
 
-static int pick_npt(int64_t n) {
+int ksim_rt_pick_npt(int64_t n) {
   for (int npt : {1, 2, 4, 8})
     if ((n + (int64_t)KSIM_BLOCK * npt - 1) / ((int64_t)KSIM_BLOCK * npt) <= 1024) return npt;
   return 8;
 }
 
-static int ensure_partials(ksim_handle* h, int grid) {
+int ksim_rt_ensure_partials(ksim_handle* h, int grid) {
   KsimCtx& c = h->ctx;
   if (c.partials && h->part_cap >= grid) return KSIM_OK;
   KsimPartial* p;
   int rc = dev_alloc(h, &p, (size_t)std::max(grid, 1024));
   if (rc) return rc;
+  dev_free(h, c.partials);
   c.partials = p;
   h->part_cap = std::max(grid, 1024);
+  if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
+  if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
   return KSIM_OK;
 }
 
 static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   KsimCtx& c = h->ctx;
-  const int npt = pick_npt(c.n);
+  const int npt = ksim_rt_pick_npt(c.n);
   c.chunk = (int64_t)KSIM_BLOCK * npt;
   const int grid = (int)((c.n + c.chunk - 1) / c.chunk);
-  int rc = ensure_partials(h, grid);
+  int rc = ksim_rt_ensure_partials(h, grid);
   if (rc) return rc;
   c.first = first;
   c.end = first + count;
@@ -445,7 +435,7 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
         hipGraph_t g = nullptr;
         (void)hipStreamEndCapture(h->stream, &g);
         if (g) (void)hipGraphDestroy(g);
-        return fail(h, KSIM_E_DEVICE, "scan launch during capture: %s", hipGetErrorString(e));
+        return ksim_fail(h, KSIM_E_DEVICE, "scan launch during capture: %s", hipGetErrorString(e));
       }
     }
     HIPCHK(h, hipStreamEndCapture(h->stream, &h->graph));
@@ -504,7 +494,7 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
       if (rc) return rc;
     }
     hipError_t e = ksim_pstream_prepare(&c, h->mirror, h->stream);
-    if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "stream prepare: %s", hipGetErrorString(e));
+    if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "stream prepare: %s", hipGetErrorString(e));
   }
   const size_t gb = ksim_pfast_granule_bytes();
   if (h->gran_bytes < gb) {
@@ -518,7 +508,7 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
   HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
   hipError_t e = ksim_launch_pfast(&c, h->granules, grid, lds_rows, stream ? h->mirror : nullptr, &h->shard, h->stream);
-  if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   HIPCHK(h, hipEventSynchronize(h->ev1));
   float ms = 0.f;
@@ -579,9 +569,9 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
     // the streaming fast kernel handed over (a node left the exact float64 range): the
     // general kernel of a table this size is the launch form
     if (h->pfast_off && h->cfg.mode != KSIM_MODE_PERSISTENT) return run_launch_mode(h, first, count, st);
-    return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: node table does not fit the on-chip layout");
+    return ksim_fail(h, KSIM_E_UNSUPPORTED, "persistent mode: node table does not fit the on-chip layout");
   }
-  if (!persistent_weights_ok(c)) return fail(h, KSIM_E_UNSUPPORTED, "persistent mode: map-priority weights exceed the 27-bit score range");
+  if (!persistent_weights_ok(c)) return ksim_fail(h, KSIM_E_UNSUPPORTED, "persistent mode: map-priority weights exceed the 27-bit score range");
   const size_t gb = ksim_persistent_granule_bytes(grid);
   if (h->gran_bytes < gb) {
     int rc = dev_alloc(h, &h->granules, gb / sizeof(uint64_t));
@@ -599,7 +589,7 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
   HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
   hipError_t e = ksim_launch_persistent(&c, h->ctx_dev, h->granules, grid, lds_rows, h->stream);
-  if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   HIPCHK(h, hipEventSynchronize(h->ev1));
   float ms = 0.f;
@@ -708,13 +698,13 @@ static int run_tree_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stat
     HIPCHK(h, hipEventRecord(h->ev0, h->stream));
     if (!h->tree_valid) {
       hipError_t e = ksim_tree_build(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, nullptr, h->stream);
-      if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree build: %s", hipGetErrorString(e));
+      if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "tree build: %s", hipGetErrorString(e));
     }
     c.first = i;
     c.end = j;
     HIPCHK(h, hipEventRecord(h->ev1, h->stream));
     hipError_t e = ksim_tree_launch(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, nullptr, h->stream);
-    if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree launch: %s", hipGetErrorString(e));
+    if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "tree launch: %s", hipGetErrorString(e));
     hipEvent_t ev2 = nullptr;
     HIPCHK(h, hipEventCreate(&ev2));
     HIPCHK(h, hipEventRecord(ev2, h->stream));
@@ -744,7 +734,7 @@ static int run_tree_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stat
 #endif
     int32_t err = 0;
     HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
-    if (err & 16) return fail(h, KSIM_E_DEVICE, "tree mode: tree inconsistent with its root (0x%x)", err);
+    if (err & 16) return ksim_fail(h, KSIM_E_DEVICE, "tree mode: tree inconsistent with its root (0x%x)", err);
     h->tree_valid = true;
     if (err & 8) {  // a node's quantities left the exact float64 range: the general kernels from now on
       h->pfast_off = true;
@@ -760,22 +750,25 @@ static int run_tree_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stat
   return KSIM_OK;
 }
 
+extern "C" {
+
 int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_node, int32_t* out_reasons,
                   ksim_stats* st) {
-  if (!h) return fail(h, KSIM_E_INVAL, "ksim_schedule: null handle");
-  if (!h->have_pods) return fail(h, KSIM_E_STATE, "ksim_schedule: load nodes, classes and pods first");
-  if (first < 0 || count < 0 || first + count > h->n_pods) return fail(h, KSIM_E_INVAL, "ksim_schedule: range out of bounds");
+  if (!h) return ksim_fail(h, KSIM_E_INVAL, "ksim_schedule: null handle");
+  if (!h->have_pods) return ksim_fail(h, KSIM_E_STATE, "ksim_schedule: load nodes, classes and pods first");
+  if (first < 0 || count < 0 || first + count > h->n_pods) return ksim_fail(h, KSIM_E_INVAL, "ksim_schedule: range out of bounds");
   HIPCHK(h, hipSetDevice(h->device));
   if (st) memset(st, 0, sizeof *st);
   if (count == 0) return KSIM_OK;
   KsimCtx& c = h->ctx;
+  if (c.n == 0) return ksim_fail(h, KSIM_E_NO_NODES, "no nodes available to schedule pods");
   if (h->shard.world > 1) {  // node-sharded: the fast persistent kernel on every rank, in lockstep
     for (int r = 0; r < h->shard.world; ++r)
-      if (!h->shard.peers[r]) return fail(h, KSIM_E_STATE, "ksim_schedule: rank %d is not connected", r);
+      if (!h->shard.peers[r]) return ksim_fail(h, KSIM_E_STATE, "ksim_schedule: rank %d is not connected", r);
     int grid = 0, lds_rows = 0;
     const int form = pfast_form(h, first, count, &grid, &lds_rows);
     if (!form)
-      return fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling takes resource-only pods on shards of at most ~1M "
+      return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling takes resource-only pods on shards of at most ~1M "
                                          "nodes per device");
     int rc = run_pfast_mode(h, first, count, grid, lds_rows, form == 2, st);
     h->shard.xtag_base += (uint32_t)count;
@@ -784,7 +777,7 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
     HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
     if (err & 8) {
       h->pfast_off = true;
-      return fail(h, KSIM_E_UNSUPPORTED, "node-sharded run stopped: a node's quantities left the exact float64 range");
+      return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded run stopped: a node's quantities left the exact float64 range");
     }
   } else {
   const int mode = h->cfg.mode;
@@ -810,19 +803,20 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
       st->scheduled = s;
     }
   }
-  if (err & 1) return fail(h, KSIM_E_OVERFLOW, "a node's host-port slots overflowed (raise port_slots)");
-  if (err & ~1) return fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
+  if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port slots overflowed (raise port_slots)");
+  if (err & ~1) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
   return KSIM_OK;
 }
 
 int ksim_evaluate(ksim_handle* h, int64_t pod, uint8_t* out_fit, uint32_t* out_reasons, int64_t* out_score,
                   uint8_t* out_rclass) {
-  if (!h) return fail(h, KSIM_E_INVAL, "ksim_evaluate: null handle");
-  if (!h->have_pods) return fail(h, KSIM_E_STATE, "ksim_evaluate: nothing loaded");
-  if (pod < 0 || pod >= h->n_pods) return fail(h, KSIM_E_INVAL, "ksim_evaluate: pod out of range");
+  if (!h) return ksim_fail(h, KSIM_E_INVAL, "ksim_evaluate: null handle");
+  if (!h->have_pods) return ksim_fail(h, KSIM_E_STATE, "ksim_evaluate: nothing loaded");
+  if (pod < 0 || pod >= h->n_pods) return ksim_fail(h, KSIM_E_INVAL, "ksim_evaluate: pod out of range");
   HIPCHK(h, hipSetDevice(h->device));
   KsimCtx& c = h->ctx;
   const int64_t n = c.n;
+  if (n == 0) return ksim_fail(h, KSIM_E_NO_NODES, "no nodes available to schedule pods");
   uint8_t *f, *rcl;
   uint32_t* r;
   int64_t* s;
@@ -831,68 +825,44 @@ int ksim_evaluate(ksim_handle* h, int64_t pod, uint8_t* out_fit, uint32_t* out_r
   if ((rc = dev_alloc(h, &f, n)) || (rc = dev_alloc(h, &r, n)) || (rc = dev_alloc(h, &s, n)) || (rc = dev_alloc(h, &rcl, n)))
     return rc;
   hipError_t e = ksim_launch_eval(&c, pod, f, r, s, rcl, h->stream);
-  if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "eval launch: %s", hipGetErrorString(e));
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "eval launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (out_fit) HIPCHK(h, hipMemcpy(out_fit, f, n, hipMemcpyDeviceToHost));
   if (out_reasons) HIPCHK(h, hipMemcpy(out_reasons, r, n * 4, hipMemcpyDeviceToHost));
   if (out_score) HIPCHK(h, hipMemcpy(out_score, s, n * 8, hipMemcpyDeviceToHost));
   if (out_rclass) HIPCHK(h, hipMemcpy(out_rclass, rcl, n, hipMemcpyDeviceToHost));
   // release the scratch buffers again
-  for (void* p : {(void*)f, (void*)r, (void*)s, (void*)rcl}) {
-    (void)hipFree(p);
-    h->bufs.erase(std::remove_if(h->bufs.begin(), h->bufs.end(), [p](const DevBuf& b) { return b.p == p; }), h->bufs.end());
-  }
-  return KSIM_OK;
-}
-
-int ksim_assume(ksim_handle* h, int64_t pod, int64_t node) {
-  if (!h) return fail(h, KSIM_E_INVAL, "ksim_assume: null handle");
-  if (!h->have_pods) return fail(h, KSIM_E_STATE, "ksim_assume: nothing loaded");
-  if (pod < 0 || pod >= h->n_pods || node < 0 || node >= h->ctx.n) return fail(h, KSIM_E_INVAL, "ksim_assume: out of range");
-  HIPCHK(h, hipSetDevice(h->device));
-  h->tree_valid = false;
-  hipError_t e = ksim_launch_assume(&h->ctx, pod, node, h->stream);
-  if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "assume launch: %s", hipGetErrorString(e));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  if (!h->pfast_off) {  // keep the fast kernel's float64 range invariant (ksim_pfast.hip)
-    for (const int64_t* col : {h->ctx.req_cpu, h->ctx.req_mem, h->ctx.nz_cpu, h->ctx.nz_mem}) {
-      int64_t v = 0;
-      HIPCHK(h, hipMemcpy(&v, col + node, 8, hipMemcpyDeviceToHost));
-      if (v < 0 || v >= ((int64_t)1 << 48)) h->pfast_off = true;
-    }
-  }
-  int32_t err = 0;
-  HIPCHK(h, hipMemcpy(&err, h->ctx.err, 4, hipMemcpyDeviceToHost));
-  if (err & 1) return fail(h, KSIM_E_OVERFLOW, "a node's host-port slots overflowed (raise port_slots)");
+  for (void* p : {(void*)f, (void*)r, (void*)s, (void*)rcl}) dev_free(h, p);
   return KSIM_OK;
 }
 
 int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t first, int64_t count, int32_t* out_node,
                uint64_t* out_counters, ksim_stats* st) {
-  if (!h || !weights || !out_node) return fail(h, KSIM_E_INVAL, "ksim_sweep: null argument");
-  if (!h->have_pods) return fail(h, KSIM_E_STATE, "ksim_sweep: load nodes, classes and pods first");
+  if (!h || !weights || !out_node) return ksim_fail(h, KSIM_E_INVAL, "ksim_sweep: null argument");
+  if (!h->have_pods) return ksim_fail(h, KSIM_E_STATE, "ksim_sweep: load nodes, classes and pods first");
   if (n_scen <= 0 || first < 0 || count <= 0 || first + count > h->n_pods || count > INT32_MAX)
-    return fail(h, KSIM_E_INVAL, "ksim_sweep: bad scenario count or pod range");
+    return ksim_fail(h, KSIM_E_INVAL, "ksim_sweep: bad scenario count or pod range");
   HIPCHK(h, hipSetDevice(h->device));
   KsimCtx& c = h->ctx;
   const int64_t n = c.n;
+  if (n == 0) return ksim_fail(h, KSIM_E_NO_NODES, "no nodes available to schedule pods");
   if (n > KSIM_SWEEP_MAX_NODES)
-    return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: %lld nodes exceed the %d-node scenario layout", (long long)n,
+    return ksim_fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: %lld nodes exceed the %d-node scenario layout", (long long)n,
                 KSIM_SWEEP_MAX_NODES);
   if (h->fast_pre[first + count] - h->fast_pre[first] != count)
-    return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: every pod must be resource-only (no ports, selectors, taints, "
+    return ksim_fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: every pod must be resource-only (no ports, selectors, taints, "
                                        "nodeName, gpu / ephemeral / extended requests)");
   std::vector<int32_t> w3((size_t)n_scen * 3);
   for (int32_t sidx = 0; sidx < n_scen; ++sidx) {
     const int64_t* w = weights + (size_t)sidx * KSIM_NW;
     if (w[KSIM_W_TAINT_TOLERATION] || w[KSIM_W_NODE_AFFINITY])
-      return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: scenario %d: reduce priorities are not swept", sidx);
+      return ksim_fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: scenario %d: reduce priorities are not swept", sidx);
     int64_t tot = 0;
     for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED}) {
-      if (w[k] < 0 || w[k] > 6553) return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: scenario %d: weight out of range", sidx);
+      if (w[k] < 0 || w[k] > 6553) return ksim_fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: scenario %d: weight out of range", sidx);
       tot += w[k];
     }
-    if (tot * 10 >= 0xFFFF) return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: scenario %d: scores exceed 16 bits", sidx);
+    if (tot * 10 >= 0xFFFF) return ksim_fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: scenario %d: scores exceed 16 bits", sidx);
     w3[3 * sidx] = (int32_t)w[KSIM_W_LEAST_REQUESTED];
     w3[3 * sidx + 1] = (int32_t)w[KSIM_W_MOST_REQUESTED];
     w3[3 * sidx + 2] = (int32_t)w[KSIM_W_BALANCED];
@@ -909,7 +879,7 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
     }
     const int64_t lim = (int64_t)1 << 48;
     if (nmax >= lim || qmax >= lim || count > lim / std::max<int64_t>(qmax, 1) || nmax + count * qmax >= lim)
-      return fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: quantities may leave the exact float64 range (2^48)");
+      return ksim_fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: quantities may leave the exact float64 range (2^48)");
   }
   int rc;
   // Tree form (ksim_tree.hip): one tree-mode wave per scenario, scenarios spread over the CUs.
@@ -971,10 +941,10 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
         HIPCHK(h, hipEventRecord(h->ev0, h->stream));
         hipError_t e = ksim_tree_sweep_init(&c, &sw, h->stream);
         if (e == hipSuccess) e = ksim_tree_build(&c, &g, h->tclass, h->tcls, leaves, levels, fitc, h->t_y, &sw, h->stream);
-        if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree sweep build: %s", hipGetErrorString(e));
+        if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "tree sweep build: %s", hipGetErrorString(e));
         HIPCHK(h, hipEventRecord(h->ev1, h->stream));
         e = ksim_tree_launch(&c, &g, h->tclass, h->tcls, leaves, levels, fitc, h->t_y, &sw, h->stream);
-        if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "tree sweep launch: %s", hipGetErrorString(e));
+        if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "tree sweep launch: %s", hipGetErrorString(e));
         hipEvent_t ev2 = nullptr;
         HIPCHK(h, hipEventCreate(&ev2));
         HIPCHK(h, hipEventRecord(ev2, h->stream));
@@ -994,7 +964,7 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
       HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
       if (err != err0) {
         HIPCHK(h, hipMemcpy(c.err, &err0, 4, hipMemcpyHostToDevice));
-        return fail(h, KSIM_E_DEVICE, "tree sweep: device consistency error 0x%x", err & ~err0);
+        return ksim_fail(h, KSIM_E_DEVICE, "tree sweep: device consistency error 0x%x", err & ~err0);
       }
       if (st) {
         memset(st, 0, sizeof *st);
@@ -1017,7 +987,7 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
         (rc = dev_alloc(h, &h->sw_ym, n)))
       return rc;
     hipError_t e = ksim_sweep_prepare(c.alloc_cpu, c.alloc_mem, n, h->sw_dac, h->sw_dam, h->sw_yc, h->sw_ym, h->stream);
-    if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "sweep prepare: %s", hipGetErrorString(e));
+    if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "sweep prepare: %s", hipGetErrorString(e));
   }
   // scratch: [S][n] x (4 float64 + int32), pods, weights, outputs
   const size_t S = (size_t)n_scen, N = (size_t)n, P = (size_t)count;
@@ -1057,7 +1027,7 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
   HIPCHK(h, hipMemcpyAsync(dw, w3.data(), S * 12, hipMemcpyHostToDevice, h->stream));
   hipError_t e = ksim_sweep_launch(c.req_cpu, c.req_mem, c.nz_cpu, c.nz_mem, c.pod_count, c.pods + first,
                                    (void*)a.pods, &a, n_scen, h->ev0, h->ev1, h->stream);
-  if (e != hipSuccess) return fail(h, KSIM_E_DEVICE, "sweep launch: %s", hipGetErrorString(e));
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "sweep launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipEventSynchronize(h->ev1));
   float ms = 0.f;
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
@@ -1080,16 +1050,16 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
 }
 
 int ksim_shard_setup(ksim_handle* h, int32_t rank, int32_t world, int64_t node_base) {
-  if (!h) return fail(h, KSIM_E_INVAL, "ksim_shard_setup: null handle");
+  if (!h) return ksim_fail(h, KSIM_E_INVAL, "ksim_shard_setup: null handle");
   if (world < 1 || world > KSIM_MAX_RANKS || rank < 0 || rank >= world || node_base < 0)
-    return fail(h, KSIM_E_INVAL, "ksim_shard_setup: rank %d of %d out of range", rank, world);
-  if (h->shard.xchg) return fail(h, KSIM_E_STATE, "ksim_shard_setup: already set up");
+    return ksim_fail(h, KSIM_E_INVAL, "ksim_shard_setup: rank %d of %d out of range", rank, world);
+  if (h->shard.xchg) return ksim_fail(h, KSIM_E_STATE, "ksim_shard_setup: already set up");
   HIPCHK(h, hipSetDevice(h->device));
   void* p = nullptr;
   const size_t bytes = ksim_shard_xchg_bytes();
   // fine-grained (uncached) so peers' writes over xGMI are seen by this device's polling loads
   hipError_t e = hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached);
-  if (e != hipSuccess) return fail(h, KSIM_E_NOMEM, "exchange buffer: %s", hipGetErrorString(e));
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_NOMEM, "exchange buffer: %s", hipGetErrorString(e));
   HIPCHK(h, hipMemset(p, 0, bytes));
   h->shard.rank = rank;
   h->shard.world = world;
@@ -1102,8 +1072,8 @@ int ksim_shard_setup(ksim_handle* h, int32_t rank, int32_t world, int64_t node_b
 }
 
 int ksim_shard_export(ksim_handle* h, uint8_t* out_handle) {
-  if (!h || !out_handle) return fail(h, KSIM_E_INVAL, "ksim_shard_export: null argument");
-  if (!h->shard.xchg) return fail(h, KSIM_E_STATE, "ksim_shard_export: call ksim_shard_setup first");
+  if (!h || !out_handle) return ksim_fail(h, KSIM_E_INVAL, "ksim_shard_export: null argument");
+  if (!h->shard.xchg) return ksim_fail(h, KSIM_E_STATE, "ksim_shard_export: call ksim_shard_setup first");
   HIPCHK(h, hipSetDevice(h->device));
   hipIpcMemHandle_t m;
   HIPCHK(h, hipIpcGetMemHandle(&m, h->shard.xchg));
@@ -1114,10 +1084,10 @@ int ksim_shard_export(ksim_handle* h, uint8_t* out_handle) {
 }
 
 int ksim_shard_connect(ksim_handle* h, int32_t peer, const uint8_t* peer_handle) {
-  if (!h || !peer_handle) return fail(h, KSIM_E_INVAL, "ksim_shard_connect: null argument");
-  if (!h->shard.xchg) return fail(h, KSIM_E_STATE, "ksim_shard_connect: call ksim_shard_setup first");
+  if (!h || !peer_handle) return ksim_fail(h, KSIM_E_INVAL, "ksim_shard_connect: null argument");
+  if (!h->shard.xchg) return ksim_fail(h, KSIM_E_STATE, "ksim_shard_connect: call ksim_shard_setup first");
   if (peer < 0 || peer >= h->shard.world || peer == h->shard.rank)
-    return fail(h, KSIM_E_INVAL, "ksim_shard_connect: bad peer %d", peer);
+    return ksim_fail(h, KSIM_E_INVAL, "ksim_shard_connect: bad peer %d", peer);
   HIPCHK(h, hipSetDevice(h->device));
   hipIpcMemHandle_t m;
   memcpy(&m, peer_handle, sizeof m);
@@ -1129,15 +1099,15 @@ int ksim_shard_connect(ksim_handle* h, int32_t peer, const uint8_t* peer_handle)
 }
 
 int ksim_shard_connect_local(ksim_handle* h, int32_t peer, ksim_handle* peer_h) {
-  if (!h || !peer_h) return fail(h, KSIM_E_INVAL, "ksim_shard_connect_local: null argument");
-  if (!h->shard.xchg || !peer_h->shard.xchg) return fail(h, KSIM_E_STATE, "ksim_shard_connect_local: set up both first");
+  if (!h || !peer_h) return ksim_fail(h, KSIM_E_INVAL, "ksim_shard_connect_local: null argument");
+  if (!h->shard.xchg || !peer_h->shard.xchg) return ksim_fail(h, KSIM_E_STATE, "ksim_shard_connect_local: set up both first");
   if (peer < 0 || peer >= h->shard.world || peer == h->shard.rank || peer_h->shard.rank != peer)
-    return fail(h, KSIM_E_INVAL, "ksim_shard_connect_local: bad peer %d", peer);
+    return ksim_fail(h, KSIM_E_INVAL, "ksim_shard_connect_local: bad peer %d", peer);
   HIPCHK(h, hipSetDevice(h->device));
   if (peer_h->device != h->device) {
     hipError_t e = hipDeviceEnablePeerAccess(peer_h->device, 0);
     if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
-      return fail(h, KSIM_E_DEVICE, "peer access to device %d: %s", peer_h->device, hipGetErrorString(e));
+      return ksim_fail(h, KSIM_E_DEVICE, "peer access to device %d: %s", peer_h->device, hipGetErrorString(e));
     (void)hipGetLastError();
   }
   h->shard.peers[peer] = peer_h->shard.xchg;
@@ -1145,8 +1115,8 @@ int ksim_shard_connect_local(ksim_handle* h, int32_t peer, ksim_handle* peer_h) 
 }
 
 int ksim_read_nodes(ksim_handle* h, ksim_node_state* o) {
-  if (!h || !o) return fail(h, KSIM_E_INVAL, "ksim_read_nodes: null argument");
-  if (!h->have_nodes) return fail(h, KSIM_E_STATE, "ksim_read_nodes: no node table");
+  if (!h || !o) return ksim_fail(h, KSIM_E_INVAL, "ksim_read_nodes: null argument");
+  if (!h->have_nodes) return ksim_fail(h, KSIM_E_STATE, "ksim_read_nodes: no node table");
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   const KsimCtx& c = h->ctx;
@@ -1166,7 +1136,7 @@ int ksim_read_nodes(ksim_handle* h, ksim_node_state* o) {
 }
 
 int ksim_get_counter(ksim_handle* h, uint64_t* out) {
-  if (!h || !out) return fail(h, KSIM_E_INVAL, "ksim_get_counter: null argument");
+  if (!h || !out) return ksim_fail(h, KSIM_E_INVAL, "ksim_get_counter: null argument");
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hipMemcpy(out, h->ctx.counter, 8, hipMemcpyDeviceToHost));
@@ -1174,7 +1144,7 @@ int ksim_get_counter(ksim_handle* h, uint64_t* out) {
 }
 
 int ksim_set_counter(ksim_handle* h, uint64_t v) {
-  if (!h) return fail(h, KSIM_E_INVAL, "ksim_set_counter: null handle");
+  if (!h) return ksim_fail(h, KSIM_E_INVAL, "ksim_set_counter: null handle");
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   HIPCHK(h, hipMemcpy(h->ctx.counter, &v, 8, hipMemcpyHostToDevice));

@@ -13,7 +13,8 @@ PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LIB_PATH = os.environ.get("KSIM_LIB") or os.path.join(PKG_DIR, "lib", "libksim.so")
 
 KSIM_OK = 0
-E_INVAL, E_DEVICE, E_NOMEM, E_UNSUPPORTED, E_STATE, E_OVERFLOW = -1, -2, -3, -4, -5, -6
+E_INVAL, E_DEVICE, E_NOMEM, E_UNSUPPORTED, E_STATE, E_OVERFLOW, E_NO_NODES = -1, -2, -3, -4, -5, -6, -7
+ABI_VERSION = 2
 MAX_SCALAR = 8
 MAX_RCLASS = 16
 NREASONS = 24
@@ -93,6 +94,22 @@ class Stats(C.Structure):
                 ("mode", C.c_int32), ("blocks", C.c_int32)]
 
 
+class Result(C.Structure):
+    _fields_ = [("node", C.c_int32), ("fit_nodes", C.c_int32), ("last_node_index", C.c_uint64),
+                ("reasons", C.c_int32 * NREASONS)]
+
+
+class NodeRow(C.Structure):
+    _fields_ = [("alloc_cpu", C.c_int64), ("alloc_mem", C.c_int64), ("alloc_gpu", C.c_int64), ("alloc_eph", C.c_int64),
+                ("allowed_pods", C.c_int32), ("flags", C.c_uint32), ("label_set", C.c_int32), ("taint_set", C.c_int32),
+                ("req_cpu", C.c_int64), ("req_mem", C.c_int64), ("req_gpu", C.c_int64), ("req_eph", C.c_int64),
+                ("nz_cpu", C.c_int64), ("nz_mem", C.c_int64), ("pod_count", C.c_int32), ("port_count", C.c_int32),
+                ("alloc_scalar", _i64p), ("req_scalar", _i64p), ("ports", _u64p)]
+
+
+SCHEDULE_ONLY, SCHEDULE_ASSUME = 0, 1
+
+
 class NodeState(C.Structure):
     _fields_ = [("req_cpu", _i64p), ("req_mem", _i64p), ("req_gpu", _i64p), ("req_eph", _i64p),
                 ("nz_cpu", _i64p), ("nz_mem", _i64p), ("pod_count", _i32p), ("req_scalar", _i64p),
@@ -112,7 +129,9 @@ assert SCALAR_DTYPE.itemsize == C.sizeof(ScalarReq)
 EXPORTS = ["ksim_abi_version", "ksim_last_error", "ksim_create", "ksim_destroy", "ksim_load_nodes",
            "ksim_load_classes", "ksim_load_pods", "ksim_schedule", "ksim_evaluate", "ksim_assume",
            "ksim_read_nodes", "ksim_get_counter", "ksim_set_counter", "ksim_selftest", "ksim_sweep",
-           "ksim_shard_setup", "ksim_shard_export", "ksim_shard_connect", "ksim_shard_connect_local"]
+           "ksim_shard_setup", "ksim_shard_export", "ksim_shard_connect", "ksim_shard_connect_local",
+           "ksim_schedule_one", "ksim_pod_add", "ksim_pod_remove", "ksim_node_add", "ksim_node_update",
+           "ksim_node_remove", "ksim_node_count", "ksim_append_pods"]
 IPC_HANDLE_BYTES = 64
 MAX_RANKS = 8
 
@@ -125,6 +144,10 @@ class KsimError(RuntimeError):
 
 class KsimUnsupported(KsimError):
     pass
+
+
+class NoNodesAvailable(KsimError):
+    """core.ErrNoNodesAvailable (generic_scheduler.go:64): "no nodes available to schedule pods"."""
 
 
 _lib = None
@@ -160,10 +183,16 @@ def lib():
     L.ksim_shard_connect_local.argtypes = [C.c_void_p, C.c_int32, C.c_void_p]
     L.ksim_sweep.argtypes = [C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
                              C.POINTER(Stats)]
-    for name in EXPORTS:
-        if name not in ("ksim_destroy", "ksim_last_error", "ksim_abi_version") and getattr(L, name).restype is C.c_int:
-            pass
-    if L.ksim_abi_version() != 1:
+    podargs = [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_int32]
+    L.ksim_schedule_one.argtypes = [C.c_void_p] + podargs + [C.c_int32, C.POINTER(Result)]
+    L.ksim_pod_add.argtypes = [C.c_void_p, C.c_int64] + podargs
+    L.ksim_pod_remove.argtypes = [C.c_void_p, C.c_int64] + podargs
+    L.ksim_node_add.argtypes = [C.c_void_p, C.c_int64, C.POINTER(NodeRow)]
+    L.ksim_node_update.argtypes = [C.c_void_p, C.c_int64, C.POINTER(NodeRow)]
+    L.ksim_node_remove.argtypes = [C.c_void_p, C.c_int64]
+    L.ksim_node_count.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
+    L.ksim_append_pods.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
+    if L.ksim_abi_version() != ABI_VERSION:
         raise ImportError("libksim.so ABI version mismatch")
     _lib = L
     return L
@@ -192,7 +221,7 @@ class Handle:
     def _check(self, rc, h):
         if rc != KSIM_OK:
             msg = self._L.ksim_last_error(h).decode(errors="replace")
-            cls = KsimUnsupported if rc == E_UNSUPPORTED else KsimError
+            cls = KsimUnsupported if rc == E_UNSUPPORTED else (NoNodesAvailable if rc == E_NO_NODES else KsimError)
             raise cls(rc, msg)
 
     def call(self, fn, *args):

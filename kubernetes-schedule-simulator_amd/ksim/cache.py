@@ -1,0 +1,339 @@
+"""Per-pod drop-in: the scheduler cache + ScheduleAlgorithm surface over the device table.
+
+The reference scheduler calls Schedule(pod, nodeLister) once per pod
+(vendor/k8s.io/kubernetes/pkg/scheduler/algorithm/scheduler_interface.go:52-65, caller
+scheduler.go:188-204) and then Scheduler.assume (scheduler.go:366-397) → cache.AssumePod
+(schedulercache/cache.go:125).  Informer events keep the cache in sync
+(factory/factory.go:596 addPodToCache, :613 updatePodInCache, :695 deletePodFromCache, :740
+addNodeToCache, :755 updateNodeInCache, :841 deleteNodeFromCache → cache.go:230-393).
+
+SchedulerCache mirrors that surface with the same method names, arguments and error behaviour
+(cache.go's "already in added state", "not found in scheduler cache", ...), keeps what the
+device cannot (pod identity, node names, interned strings, residual pods of removed nodes) and
+drives libksim.so for everything on the hot path: one scan launch per Schedule
+(ksim_schedule_one), one small kernel per pod / node event (ksim_pod_add / remove,
+ksim_node_add / update / remove).  There is no CPU fallback: without the library or a device
+every call raises.
+"""
+from __future__ import annotations
+
+import bisect
+import ctypes as C
+
+import numpy as np
+
+from . import abi, ingest, scheduler
+from .ingest import Unsupported, _canon, _meta, _spec
+
+
+class FitError(Exception):
+    """core.FitError (generic_scheduler.go:51-90): NumAllNodes + the reason histogram."""
+
+    def __init__(self, num_nodes, hist, scalar_names=()):
+        self.num_nodes = num_nodes
+        self.hist = np.asarray(hist, np.int32)
+        super().__init__(scheduler.fit_error_message(num_nodes, self.hist, scalar_names))
+
+
+def pod_key(pod):
+    """getPodKey (node_info.go:497-503): the UID; pods without one are keyed by namespace/name."""
+    md = _meta(pod)
+    return md.get("uid") or "%s/%s" % (md.get("namespace", ""), md.get("name", ""))
+
+
+class _Info:
+    """What the host keeps per NodeInfo (cache.nodes entry): the node object (None after
+    RemoveNode or before AddNode), the pods on it with their encodings, the pressure status
+    SetNode carries over."""
+
+    __slots__ = ("node", "pods", "mem", "disk")
+
+    def __init__(self):
+        self.node = None
+        self.pods = {}
+        self.mem = self.disk = None
+
+
+class SchedulerCache:
+    """schedulercache.Cache + genericScheduler of one device.  `predicates` / `priorities` are
+    key sets and weights as a provider or Policy lists them (scheduler.provider / policy)."""
+
+    def __init__(self, predicates, priorities, device=0, mode=abi.MODE_AUTO, last_node_index=0, port_slots=4):
+        self.predicates = list(predicates)
+        self.prioritizers = list(priorities)
+        self.cfg = scheduler.make_config(predicates, priorities, device, mode, True, last_node_index)
+        self._need_na = any(n == "NodeAffinityPriority" for n, _ in self.prioritizers)
+        self.h = abi.Handle(self.cfg)
+        cl = self.cl = ingest.Cluster()
+        cl.ips.get("0.0.0.0")
+        cl.protos.get("TCP")
+        cl.label_sets.get(_canon({}), {})
+        cl.taint_sets.get(_canon([]), [])
+        cl.classes.get(ingest.pod_class_key({}), {})
+        self.names = []          # listed node names, ascending bytewise (= name rank)
+        self._keys = []          # the same as bytes
+        self._rank = None        # name -> rank (rebuilt lazily after node events)
+        self.infos = {}          # name -> _Info
+        self.pod_states = {}     # key -> (pod, node name)
+        self.assumed = set()
+        self._tables_for = None
+        self._load_tables()
+        S = abi.MAX_SCALAR       # scalar columns reserved up front (new names need no relayout)
+        t = abi.NodeTable()
+        t.n_nodes, t.n_scalar, t.port_slots = 0, S, port_slots
+        self._empty = {k: np.zeros(1, np.int64) for k in ("i64",)}
+        self.h.call("ksim_load_nodes", C.byref(t))
+
+    # ------------------------------------------------------------------ interning / tables
+    def _load_tables(self):
+        cl = self.cl
+        key = (len(cl.label_sets.items), len(cl.taint_sets.items), len(cl.classes.items))
+        if key == self._tables_for:
+            return
+        self.tables, self.need, bad = ingest.build_class_tables(cl.label_sets.items, cl.taint_sets.items,
+                                                                cl.classes.items)
+        cl.bad_affinity_classes = set(bad)
+        self.h.call("ksim_load_classes", C.byref(ingest.class_tables_struct(self.tables)))
+        self._tables_for = key
+
+    def _scalar_id(self, name):
+        i = self.cl.scalar_names.get(name)
+        if i >= abi.MAX_SCALAR:
+            raise Unsupported("more than %d scalar resources" % abi.MAX_SCALAR)
+        return i
+
+    def _ranks(self):
+        if self._rank is None:
+            self._rank = {n: i for i, n in enumerate(self.names)}
+        return self._rank
+
+    def _encode(self, pod):
+        """Pod → (ksim_pod record array of 1, ports, scalars); interns its class first."""
+        compiled = ingest.container_requests(pod)
+        pred, add = compiled[0], compiled[1]
+        for name in list(pred.scalar) + list(add.scalar):
+            self._scalar_id(name)
+        row = np.zeros(1, abi.POD_DTYPE)
+        ports, scalars = [], []
+        self.cl.encode_pod(pod, compiled, row[0], ports, scalars, index=self._ranks())
+        self._load_tables()
+        cls = int(row[0]["cls"])
+        if self._need_na and cls in self.cl.bad_affinity_classes:
+            raise Unsupported("NodeAffinityPriority: a preferred node-affinity term does not parse")
+        row[0]["flags"] |= self.need[cls]
+        p = np.array(ports, np.uint64)
+        s = np.array(scalars, abi.SCALAR_DTYPE) if scalars else np.zeros(0, abi.SCALAR_DTYPE)
+        return row, p, s
+
+    def _pod_args(self, enc):
+        row, p, s = enc
+        return (abi.vptr(row), abi.vptr(p) if len(p) else None, len(p), abi.vptr(s) if len(s) else None, len(s))
+
+    # ------------------------------------------------------------------ node rows
+    def _node_row(self, name, info, ns):
+        cl = self.cl
+        lid = cl.label_sets.get(_canon(ns.labels), dict(ns.labels))
+        tid = cl.taint_sets.get(_canon(ns.taints), ns.taints)
+        cl.prefer_avoid_nodes |= ns.prefer_avoid
+        alloc_s = np.zeros(abi.MAX_SCALAR, np.int64)
+        for k, v in ns.scalar.items():
+            alloc_s[self._scalar_id(k)] = v
+        self._load_tables()
+        r = abi.NodeRow()
+        r.alloc_cpu, r.alloc_mem, r.alloc_gpu, r.alloc_eph = ns.alloc
+        r.allowed_pods, r.flags, r.label_set, r.taint_set = ns.allowed, ns.flags, lid, tid
+        # pods already on the node (NodeInfo kept across RemoveNode / pods seen before AddNode)
+        req_s = np.zeros(abi.MAX_SCALAR, np.int64)
+        keys = {}
+        req = [0, 0, 0, 0]
+        nzc = nzm = 0
+        for pod, enc in info.pods.values():
+            d = enc[0][0]
+            req[0] += int(d["add_cpu"]); req[1] += int(d["add_mem"])
+            req[2] += int(d["add_gpu"]); req[3] += int(d["add_eph"])
+            nzc += int(d["nz_cpu"]); nzm += int(d["nz_mem"])
+            for sc in enc[2]:
+                req_s[int(sc["col"])] += int(sc["add"])
+            for k in enc[1]:
+                keys[int(k)] = True
+        r.req_cpu, r.req_mem, r.req_gpu, r.req_eph = req
+        r.nz_cpu, r.nz_mem = nzc, nzm
+        r.pod_count = len(info.pods)
+        ports = np.array(list(keys), np.uint64)
+        r.port_count = len(ports)
+        r.alloc_scalar = abi.ptr(alloc_s, C.c_int64)
+        r.req_scalar = abi.ptr(req_s, C.c_int64)
+        r.ports = abi.ptr(ports, C.c_uint64) if len(ports) else None
+        return r, (alloc_s, req_s, ports)
+
+    def _info(self, name):
+        info = self.infos.get(name)
+        if info is None:
+            info = self.infos[name] = _Info()
+        return info
+
+    def add_node(self, node):
+        """cache.AddNode (cache.go:354-363) → NodeInfo.SetNode."""
+        name = _meta(node).get("name", "")
+        info = self._info(name)
+        ns = ingest.node_static(node, info.mem, info.disk)
+        row, keep = self._node_row(name, info, ns)
+        if name in self._ranks():
+            self.h.call("ksim_node_update", self._ranks()[name], C.byref(row))
+        else:
+            k = name.encode()
+            rank = bisect.bisect_left(self._keys, k)
+            self.h.call("ksim_node_add", rank, C.byref(row))
+            self._keys.insert(rank, k)
+            self.names.insert(rank, name)
+            self._rank = None
+        info.node, info.mem, info.disk = node, ns.mem_pressure, ns.disk_pressure
+
+    def update_node(self, old, new):
+        """cache.UpdateNode (cache.go:366-375) → SetNode on the (possibly new) NodeInfo."""
+        self.add_node(new)
+
+    def remove_node(self, node):
+        """cache.RemoveNode (cache.go:378-393): the node leaves the listed set; its NodeInfo
+        stays while pods remain on it (their events may arrive later)."""
+        name = _meta(node).get("name", "")
+        if name not in self._ranks():
+            raise KeyError("node %s is not in the cache" % name)
+        rank = self._ranks()[name]
+        self.h.call("ksim_node_remove", rank)
+        del self.names[rank]
+        del self._keys[rank]
+        self._rank = None
+        info = self.infos[name]
+        info.node, info.mem, info.disk = None, "Unknown", "Unknown"
+        if not info.pods:
+            del self.infos[name]
+
+    # ------------------------------------------------------------------ pods
+    def _add(self, pod, enc=None):                          # cache.go:200-207
+        name = _spec(pod).get("nodeName", "")
+        enc = enc if enc is not None else self._encode(pod)
+        if name in self._ranks():
+            self.h.call("ksim_pod_add", self._ranks()[name], *self._pod_args(enc))
+        self._info(name).pods[pod_key(pod)] = (pod, enc)
+
+    def _remove(self, pod):                                 # cache.go:219-228
+        name = _spec(pod).get("nodeName", "")
+        info = self.infos.get(name)
+        key = pod_key(pod)
+        if info is None or key not in info.pods:
+            raise KeyError("no corresponding pod %s in pods of node %s" % (_meta(pod).get("name"), name))
+        _, enc = info.pods.pop(key)
+        if name in self._ranks():
+            self.h.call("ksim_pod_remove", self._ranks()[name], *self._pod_args(enc))
+        if not info.pods and info.node is None:
+            del self.infos[name]
+
+    def assume_pod(self, pod):
+        """cache.AssumePod (cache.go:125-143); pod.spec.nodeName is the chosen host."""
+        key = pod_key(pod)
+        if key in self.pod_states:
+            raise KeyError("pod %s is in the cache, so can't be assumed" % key)
+        self._add(pod)
+        self.pod_states[key] = pod
+        self.assumed.add(key)
+
+    def add_pod(self, pod):
+        """cache.AddPod (cache.go:230-262): confirms an assumed pod (moving it if it landed
+        elsewhere) or adds a pod bound by someone else."""
+        key = pod_key(pod)
+        cur = self.pod_states.get(key)
+        if cur is not None and key in self.assumed:
+            if _spec(cur).get("nodeName") != _spec(pod).get("nodeName"):
+                self._remove(cur)
+                self._add(pod)
+            self.assumed.discard(key)
+            self.pod_states[key] = pod
+        elif cur is None:
+            self._add(pod)
+            self.pod_states[key] = pod
+        else:
+            raise KeyError("pod %s was already in added state" % key)
+
+    def update_pod(self, old, new):
+        """cache.UpdatePod (cache.go:265-289) = removePod(old) + addPod(new)."""
+        key = pod_key(old)
+        if key not in self.pod_states or key in self.assumed:
+            raise KeyError("pod %s is not added to scheduler cache, so cannot be updated" % key)
+        self._remove(old)
+        self._add(new)
+        self.pod_states[key] = new
+
+    def remove_pod(self, pod):
+        """cache.RemovePod (cache.go:292-318)."""
+        key = pod_key(pod)
+        cur = self.pod_states.get(key)
+        if cur is None or key in self.assumed:
+            raise KeyError("pod %s is not found in scheduler cache, so cannot be removed from it" % key)
+        self._remove(cur)
+        del self.pod_states[key]
+
+    # ------------------------------------------------------------------ Schedule
+    def schedule(self, pod, assume=False):
+        """genericScheduler.Schedule (generic_scheduler.go:112-167): the host name, or raises
+        FitError / abi.NoNodesAvailable.  assume=True also runs Scheduler.assume
+        (scheduler.go:366): the pod enters the cache on that host, as an assumed pod."""
+        enc = self._encode(pod)
+        res = abi.Result()
+        self.h.call("ksim_schedule_one", *self._pod_args(enc), abi.SCHEDULE_ASSUME if assume else abi.SCHEDULE_ONLY,
+                    C.byref(res))
+        self.last_fit_nodes = res.fit_nodes
+        if res.node < 0:
+            raise FitError(len(self.names), list(res.reasons), self.cl.scalar_names.items)
+        host = self.names[res.node]
+        if assume:
+            assumed = dict(pod)
+            assumed["spec"] = dict(_spec(pod), nodeName=host)
+            key = pod_key(assumed)
+            if key in self.pod_states:
+                raise KeyError("pod %s is in the cache, so can't be assumed" % key)
+            # the device already holds the commit: record it host-side with the assumed encoding
+            enc2 = (enc[0].copy(), enc[1], enc[2])
+            enc2[0][0]["host"] = res.node
+            self._info(host).pods[key] = (assumed, enc2)
+            self.pod_states[key] = assumed
+            self.assumed.add(key)
+        return host
+
+    def schedule_one(self, pod):
+        """scheduleOne's schedule + assume (scheduler.go:431-484) for one pod: (host, None) or
+        (None, FitError message)."""
+        try:
+            return self.schedule(pod, assume=True), None
+        except FitError as e:
+            return None, str(e)
+
+    @property
+    def last_node_index(self):
+        v = C.c_uint64()
+        self.h.call("ksim_get_counter", C.byref(v))
+        return v.value
+
+    def node_count(self):
+        v = C.c_int64()
+        self.h.call("ksim_node_count", C.byref(v))
+        return v.value
+
+    def node_state(self):
+        """Dynamic columns read back from the device, in name-rank order."""
+        n = len(self.names)
+        S = abi.MAX_SCALAR
+        out = dict(req_cpu=np.zeros(n, np.int64), req_mem=np.zeros(n, np.int64), req_gpu=np.zeros(n, np.int64),
+                   req_eph=np.zeros(n, np.int64), nz_cpu=np.zeros(n, np.int64), nz_mem=np.zeros(n, np.int64),
+                   pod_count=np.zeros(n, np.int32), req_scalar=np.zeros((S, n), np.int64),
+                   port_count=np.zeros(n, np.int32))
+        st = abi.NodeState()
+        for k, ct in (("req_cpu", C.c_int64), ("req_mem", C.c_int64), ("req_gpu", C.c_int64), ("req_eph", C.c_int64),
+                      ("nz_cpu", C.c_int64), ("nz_mem", C.c_int64), ("pod_count", C.c_int32),
+                      ("req_scalar", C.c_int64), ("port_count", C.c_int32)):
+            setattr(st, k, abi.ptr(out[k], ct))
+        self.h.call("ksim_read_nodes", C.byref(st))
+        return out
+
+    def close(self):
+        self.h.close()

@@ -242,37 +242,16 @@ class Cluster:
                  req_scalar=np.zeros((S, n), np.int64))
         node_taints = []
         for i, x in enumerate(nodes):
-            st, sp, md = x.get("status") or {}, _spec(x), _meta(x)
-            r = ResourceVec()
-            r.add(st.get("allocatable") or {})
-            c["alloc_cpu"][i], c["alloc_mem"][i], c["alloc_gpu"][i], c["alloc_eph"][i] = r.cpu, r.mem, r.gpu, r.eph
-            c["allowed_pods"][i] = r.pods
-            for name, v in r.scalar.items():
+            ns = node_static(x)
+            c["alloc_cpu"][i], c["alloc_mem"][i], c["alloc_gpu"][i], c["alloc_eph"][i] = ns.alloc
+            c["allowed_pods"][i] = ns.allowed
+            for name, v in ns.scalar.items():
                 c["alloc_scalar"][self.scalar_names.ids[name], i] = v
-            f = 0
-            for cond in st.get("conditions") or []:
-                t, s = cond.get("type"), cond.get("status")
-                if t == "Ready" and s != "True":
-                    f |= abi.N_NOT_READY
-                elif t == "OutOfDisk" and s != "False":
-                    f |= abi.N_OUT_OF_DISK
-                elif t == "NetworkUnavailable" and s != "False":
-                    f |= abi.N_NET_UNAVAIL
-                if t == "MemoryPressure":    # SetNode keeps the last such condition
-                    f = (f | abi.N_MEM_PRESSURE) if s == "True" else (f & ~abi.N_MEM_PRESSURE)
-                elif t == "DiskPressure":
-                    f = (f | abi.N_DISK_PRESSURE) if s == "True" else (f & ~abi.N_DISK_PRESSURE)
-            if sp.get("unschedulable"):
-                f |= abi.N_UNSCHEDULABLE
-            c["flags"][i] = f
-            lab = md.get("labels") or {}
-            c["label_set"][i] = self.label_sets.get(_canon(lab), dict(lab))
-            taints = [{"key": t.get("key") or "", "value": t.get("value") or "", "effect": t.get("effect") or ""}
-                      for t in (sp.get("taints") or [])]
-            c["taint_set"][i] = self.taint_sets.get(_canon(taints), taints)
-            if PREFER_AVOID_ANNOTATION in (md.get("annotations") or {}):
-                self.prefer_avoid_nodes = True
-            node_taints.append(taints)
+            c["flags"][i] = ns.flags
+            c["label_set"][i] = self.label_sets.get(_canon(ns.labels), dict(ns.labels))
+            c["taint_set"][i] = self.taint_sets.get(_canon(ns.taints), ns.taints)
+            self.prefer_avoid_nodes |= ns.prefer_avoid
+            node_taints.append(ns.taints)
         # running pods: NodeInfo.AddPod
         used_ports = [dict() for _ in range(n)]
         for p, (pred, add, nzc, nzm) in zip(running, compiled[:len(running)]):
@@ -318,102 +297,51 @@ class Cluster:
         arr = np.zeros(m, abi.POD_DTYPE)
         ports, scalars = [], []
         self.pod_names = []
-        for k, (p, (pred, add, nzc, nzm)) in enumerate(zip(pods, compiled)):
-            check_pod_supported(p)
-            spec, md = _spec(p), _meta(p)
-            if self.prefer_avoid_nodes:
-                for o in md.get("ownerReferences") or []:
-                    if o.get("controller") and o.get("kind") in ("ReplicationController", "ReplicaSet"):
-                        raise Unsupported("NodePreferAvoidPods with RC/RS-owned pods and preferAvoidPods annotations")
-            self.pod_names.append(md.get("name", ""))
-            row = arr[k]
-            row["req_cpu"], row["req_mem"], row["req_gpu"], row["req_eph"] = pred.cpu, pred.mem, pred.gpu, pred.eph
-            row["add_cpu"], row["add_mem"], row["add_gpu"], row["add_eph"] = add.cpu, add.mem, add.gpu, add.eph
-            row["nz_cpu"], row["nz_mem"] = nzc, nzm
-            flags = 0
-            if pred.cpu or pred.mem or pred.gpu or pred.eph or pred.scalar:
-                flags |= abi.POD_ANY_REQUEST
-            if best_effort(p):
-                flags |= abi.POD_BEST_EFFORT
-            nn = spec.get("nodeName") or ""
-            row["host"] = -1 if not nn else self.index.get(nn, -2)
-            key = _canon({"ns": spec.get("nodeSelector") or {}, "na": (spec.get("affinity") or {}).get("nodeAffinity"),
-                          "tol": spec.get("tolerations") or []})
-            row["cls"] = self.classes.get(key, spec)
-            row["flags"] = flags
-            hp = host_ports(p)
-            row["port_off"], row["port_cnt"] = len(ports), len(hp)
-            for ip, proto, port in hp:
-                ports.append(abi_port_key(self.ips.get(ip), self.protos.get(proto), port))
-            row["scalar_off"], row["scalar_cnt"] = len(scalars), len(pred.scalar)
-            for name, v in pred.scalar.items():
-                scalars.append((self.scalar_names.ids[name], 0, v, add.scalar.get(name, 0)))
+        for k, (p, cr) in enumerate(zip(pods, compiled)):
+            self.pod_names.append(_meta(p).get("name", ""))
+            self.encode_pod(p, cr, arr[k], ports, scalars)
         self.pods = arr
         self.pod_ports = np.array(ports, np.uint64)
         self.pod_scalars = np.array(scalars, abi.SCALAR_DTYPE) if scalars else np.zeros(0, abi.SCALAR_DTYPE)
 
+    def encode_pod(self, p, compiled, row, ports, scalars, index=None):
+        """One pod → a ksim_pod record `row` (a POD_DTYPE element); its host-port keys and scalar
+        requests are appended to `ports` / `scalars` (offsets into those lists).  Interns the
+        pod's class (nodeSelector, node affinity, tolerations) and any new IP / protocol.
+        `index` maps spec.nodeName to a name rank (default: the cluster's own index)."""
+        pred, add, nzc, nzm = compiled
+        check_pod_supported(p)
+        spec, md = _spec(p), _meta(p)
+        if self.prefer_avoid_nodes:
+            for o in md.get("ownerReferences") or []:
+                if o.get("controller") and o.get("kind") in ("ReplicationController", "ReplicaSet"):
+                    raise Unsupported("NodePreferAvoidPods with RC/RS-owned pods and preferAvoidPods annotations")
+        row["req_cpu"], row["req_mem"], row["req_gpu"], row["req_eph"] = pred.cpu, pred.mem, pred.gpu, pred.eph
+        row["add_cpu"], row["add_mem"], row["add_gpu"], row["add_eph"] = add.cpu, add.mem, add.gpu, add.eph
+        row["nz_cpu"], row["nz_mem"] = nzc, nzm
+        flags = 0
+        if pred.cpu or pred.mem or pred.gpu or pred.eph or pred.scalar:
+            flags |= abi.POD_ANY_REQUEST
+        if best_effort(p):
+            flags |= abi.POD_BEST_EFFORT
+        nn = spec.get("nodeName") or ""
+        idx = self.index if index is None else index
+        row["host"] = -1 if not nn else idx.get(nn, -2)
+        row["cls"] = self.classes.get(pod_class_key(spec), spec)
+        row["flags"] = flags
+        hp = host_ports(p)
+        row["port_off"], row["port_cnt"] = len(ports), len(hp)
+        for ip, proto, port in hp:
+            ports.append(abi_port_key(self.ips.get(ip), self.protos.get(proto), port))
+        row["scalar_off"], row["scalar_cnt"] = len(scalars), len(pred.scalar)
+        for name, v in pred.scalar.items():
+            scalars.append((self.scalar_names.ids[name], 0, v, add.scalar.get(name, 0)))
+
     # ----------------------------------------------------------------- tables
     def _build_tables(self):
-        L, T = len(self.label_sets.items), len(self.taint_sets.items)
-        specs = self.classes.items or [{}]
-        Cn = len(specs)
-        lw, tw = (L + 31) // 32, (T + 31) // 32
-        sel = np.zeros((Cn, lw), np.uint32)
-        tok = np.zeros((Cn, tw), np.uint32)
-        nok = np.zeros((Cn, tw), np.uint32)
-        ttc = np.zeros((Cn, T), np.uint8)
-        nac = np.zeros((Cn, L), np.uint8)
-        ntt = np.ones(Cn, np.int32)
-        nna = np.ones(Cn, np.int32)
-        ttv = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
-        nav = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
-        need = np.zeros(Cn, np.uint32)
-        for k, spec in enumerate(specs):
-            tols = spec.get("tolerations") or []
-            prefer_tols = [t for t in tols if (t.get("effect") or "") in ("", "PreferNoSchedule")]
-            all_sel = all_taint = True
-            weights = []
-            for li, lab in enumerate(self.label_sets.items):
-                ok = labels.pod_matches_node_labels(spec, lab)
-                if ok:
-                    sel[k, li >> 5] |= np.uint32(1 << (li & 31))
-                all_sel &= ok
-                try:
-                    weights.append(labels.preferred_weight(spec, lab))
-                except labels.SelectorError:
-                    # CalculateNodeAffinityPriorityMap returns an error: only fatal when
-                    # NodeAffinityPriority is configured (checked by the scheduler layer)
-                    self.bad_affinity_classes.add(k)
-                    weights.append(0)
-            counts = []
-            for ti, taints in enumerate(self.taint_sets.items):
-                ok = all(any(tolerates(t, x) for t in tols) for x in taints
-                         if x["effect"] in ("NoSchedule", "NoExecute"))
-                ok2 = all(any(tolerates(t, x) for t in tols) for x in taints if x["effect"] == "NoExecute")
-                if ok:
-                    tok[k, ti >> 5] |= np.uint32(1 << (ti & 31))
-                if ok2:
-                    nok[k, ti >> 5] |= np.uint32(1 << (ti & 31))
-                all_taint &= ok and ok2
-                counts.append(sum(1 for x in taints if x["effect"] == "PreferNoSchedule"
-                                  and not any(tolerates(t, x) for t in prefer_tols)))
-            tv = sorted(set(counts))
-            av = sorted(set(weights))
-            if len(tv) * len(av) > abi.MAX_RCLASS:
-                raise Unsupported("pod class needs %d x %d reduce classes (> %d)" % (len(tv), len(av), abi.MAX_RCLASS))
-            ntt[k], nna[k] = len(tv), len(av)
-            ttv[k, :len(tv)] = tv
-            nav[k, :len(av)] = av
-            ttc[k, :] = [tv.index(x) for x in counts]
-            nac[k, :] = [av.index(x) for x in weights]
-            f = 0
-            if not all_sel:
-                f |= abi.POD_NEED_SELECTOR
-            if not all_taint:
-                f |= abi.POD_NEED_TAINTS
-            need[k] = f
-        self.tables = dict(n_classes=Cn, n_label_sets=L, n_taint_sets=T, sel_ok=sel, taint_ok=tok, noexec_ok=nok,
-                           tt_class=ttc, na_class=nac, n_tt=ntt, n_na=nna, tt_val=ttv, na_val=nav)
+        self.tables, need, bad = build_class_tables(self.label_sets.items, self.taint_sets.items,
+                                                    self.classes.items or [{}])
+        self.bad_affinity_classes |= bad
         if self.pods is not None and len(self.pods):
             self.pods["flags"] |= need[self.pods["cls"]]
 
@@ -439,15 +367,7 @@ class Cluster:
         return t
 
     def class_tables(self):
-        d = self.tables
-        t = abi.ClassTables()
-        t.n_classes, t.n_label_sets, t.n_taint_sets = d["n_classes"], d["n_label_sets"], d["n_taint_sets"]
-        for name, ct in (("sel_ok", abi.C.c_uint32), ("taint_ok", abi.C.c_uint32), ("noexec_ok", abi.C.c_uint32),
-                         ("tt_class", abi.C.c_uint8), ("na_class", abi.C.c_uint8), ("n_tt", abi.C.c_int32),
-                         ("n_na", abi.C.c_int32), ("tt_val", abi.C.c_int64), ("na_val", abi.C.c_int64)):
-            d[name] = np.ascontiguousarray(d[name])
-            setattr(t, name, abi.ptr(d[name], ct))
-        return t
+        return class_tables_struct(self.tables)
 
     @property
     def n_nodes(self):
@@ -463,6 +383,149 @@ class Cluster:
         sub.names = list(self.names[lo:hi]) if self.names else self.names
         sub.index = {}
         return sub
+
+
+@dataclass
+class NodeStatic:
+    alloc: tuple          # allocatable cpu (milli), memory, gpu, ephemeral
+    allowed: int          # allocatable pods
+    scalar: dict          # allocatable scalar resources
+    flags: int            # KSIM_N_* condition bits
+    labels: dict
+    taints: list
+    prefer_avoid: bool
+    mem_pressure: object  # status of the last MemoryPressure condition (None: absent)
+    disk_pressure: object
+
+
+def node_static(x, prev_mem=None, prev_disk=None):
+    """NodeInfo.SetNode (node_info.go:429-448) + the conditions CheckNodeConditionPredicate reads
+    (predicates.go:1534-1568).  SetNode overwrites the pressure status only when the node carries
+    that condition, so an update keeps the previous one otherwise (prev_mem / prev_disk)."""
+    st, sp, md = x.get("status") or {}, _spec(x), _meta(x)
+    r = ResourceVec()
+    r.add(st.get("allocatable") or {})
+    f = 0
+    mem, disk = prev_mem, prev_disk
+    seen = {}
+    for cond in st.get("conditions") or []:
+        t, s = cond.get("type"), cond.get("status")
+        bit = 0
+        if t == "Ready" and s != "True":
+            bit = abi.N_NOT_READY
+        elif t == "OutOfDisk" and s != "False":
+            bit = abi.N_OUT_OF_DISK
+        elif t == "NetworkUnavailable" and s != "False":
+            bit = abi.N_NET_UNAVAIL
+        if bit:
+            # CheckNodeConditionPredicate appends one reason per failing entry and FitError counts
+            # each: a repeated failing condition would count twice, which one bit cannot say
+            if seen.get(bit):
+                raise Unsupported("node %r: repeated failing %s condition" % (md.get("name"), t))
+            seen[bit] = True
+            f |= bit
+        if t == "MemoryPressure":    # SetNode keeps the last such condition
+            mem = s
+        elif t == "DiskPressure":
+            disk = s
+    if mem == "True":
+        f |= abi.N_MEM_PRESSURE
+    if disk == "True":
+        f |= abi.N_DISK_PRESSURE
+    if sp.get("unschedulable"):
+        f |= abi.N_UNSCHEDULABLE
+    taints = [{"key": t.get("key") or "", "value": t.get("value") or "", "effect": t.get("effect") or ""}
+              for t in (sp.get("taints") or [])]
+    return NodeStatic((r.cpu, r.mem, r.gpu, r.eph), r.pods, dict(r.scalar), f, dict(md.get("labels") or {}), taints,
+                      PREFER_AVOID_ANNOTATION in (md.get("annotations") or {}), mem, disk)
+
+
+def pod_class_key(spec):
+    """Pods whose nodeSelector, node affinity and tolerations are equal share a class."""
+    return _canon({"ns": spec.get("nodeSelector") or {}, "na": (spec.get("affinity") or {}).get("nodeAffinity"),
+                   "tol": spec.get("tolerations") or []})
+
+
+def build_class_tables(label_items, taint_items, specs):
+    """Per pod class × label set / taint set: podMatchesNodeLabels (predicates.go:795-838),
+    PodToleratesNodeTaints (:1465-1494, NoSchedule + NoExecute; NoExecute only), the
+    TaintToleration map value (intolerable PreferNoSchedule taints, taint_toleration.go:29-73)
+    and the NodeAffinity map value (preferred terms' weight, node_affinity.go:34-75) grouped
+    into reduce classes.  Returns (tables, POD_NEED_* flags per class, classes whose preferred
+    terms fail to parse)."""
+    L, T = len(label_items), len(taint_items)
+    Cn = len(specs)
+    lw, tw = (L + 31) // 32, (T + 31) // 32
+    sel = np.zeros((Cn, lw), np.uint32)
+    tok = np.zeros((Cn, tw), np.uint32)
+    nok = np.zeros((Cn, tw), np.uint32)
+    ttc = np.zeros((Cn, T), np.uint8)
+    nac = np.zeros((Cn, L), np.uint8)
+    ntt = np.ones(Cn, np.int32)
+    nna = np.ones(Cn, np.int32)
+    ttv = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
+    nav = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
+    need = np.zeros(Cn, np.uint32)
+    bad = set()
+    for k, spec in enumerate(specs):
+        tols = spec.get("tolerations") or []
+        prefer_tols = [t for t in tols if (t.get("effect") or "") in ("", "PreferNoSchedule")]
+        all_sel = all_taint = True
+        weights = []
+        for li, lab in enumerate(label_items):
+            ok = labels.pod_matches_node_labels(spec, lab)
+            if ok:
+                sel[k, li >> 5] |= np.uint32(1 << (li & 31))
+            all_sel &= ok
+            try:
+                weights.append(labels.preferred_weight(spec, lab))
+            except labels.SelectorError:
+                # CalculateNodeAffinityPriorityMap returns an error: only fatal when
+                # NodeAffinityPriority is configured (checked by the scheduler layer)
+                bad.add(k)
+                weights.append(0)
+        counts = []
+        for ti, taints in enumerate(taint_items):
+            ok = all(any(tolerates(t, x) for t in tols) for x in taints
+                     if x["effect"] in ("NoSchedule", "NoExecute"))
+            ok2 = all(any(tolerates(t, x) for t in tols) for x in taints if x["effect"] == "NoExecute")
+            if ok:
+                tok[k, ti >> 5] |= np.uint32(1 << (ti & 31))
+            if ok2:
+                nok[k, ti >> 5] |= np.uint32(1 << (ti & 31))
+            all_taint &= ok and ok2
+            counts.append(sum(1 for x in taints if x["effect"] == "PreferNoSchedule"
+                              and not any(tolerates(t, x) for t in prefer_tols)))
+        tv = sorted(set(counts))
+        av = sorted(set(weights))
+        if len(tv) * len(av) > abi.MAX_RCLASS:
+            raise Unsupported("pod class needs %d x %d reduce classes (> %d)" % (len(tv), len(av), abi.MAX_RCLASS))
+        ntt[k], nna[k] = len(tv), len(av)
+        ttv[k, :len(tv)] = tv
+        nav[k, :len(av)] = av
+        ttc[k, :] = [tv.index(x) for x in counts]
+        nac[k, :] = [av.index(x) for x in weights]
+        f = 0
+        if not all_sel:
+            f |= abi.POD_NEED_SELECTOR
+        if not all_taint:
+            f |= abi.POD_NEED_TAINTS
+        need[k] = f
+    tables = dict(n_classes=Cn, n_label_sets=L, n_taint_sets=T, sel_ok=sel, taint_ok=tok, noexec_ok=nok,
+                  tt_class=ttc, na_class=nac, n_tt=ntt, n_na=nna, tt_val=ttv, na_val=nav)
+    return tables, need, bad
+
+
+def class_tables_struct(d):
+    """ksim_class_tables over the arrays of a tables dict (kept alive by the dict)."""
+    t = abi.ClassTables()
+    t.n_classes, t.n_label_sets, t.n_taint_sets = d["n_classes"], d["n_label_sets"], d["n_taint_sets"]
+    for name, ct in (("sel_ok", abi.C.c_uint32), ("taint_ok", abi.C.c_uint32), ("noexec_ok", abi.C.c_uint32),
+                     ("tt_class", abi.C.c_uint8), ("na_class", abi.C.c_uint8), ("n_tt", abi.C.c_int32),
+                     ("n_na", abi.C.c_int32), ("tt_val", abi.C.c_int64), ("na_val", abi.C.c_int64)):
+        d[name] = np.ascontiguousarray(d[name])
+        setattr(t, name, abi.ptr(d[name], ct))
+    return t
 
 
 def abi_port_key(ip_id, proto_id, port):

@@ -448,6 +448,44 @@ class NodeInfo:
             if port > 0:
                 self.used_ports.add(_sanitize(ip, proto) + (port,))
 
+    def remove_pod(self, pod):
+        """RemovePod (node_info.go:343-390): the containers-only requests come off, the pod's
+        ports leave the HostPortInfo set (utils.go:63-79 Remove deletes the key)."""
+        key = pod_key(pod)
+        for i, p in enumerate(self.pods):
+            if pod_key(p) != key:
+                continue
+            self.pods[i] = self.pods[-1]
+            self.pods.pop()
+            res, nzc, nzm = calculate_resource(pod)
+            self.requested.cpu -= res.cpu
+            self.requested.mem -= res.mem
+            self.requested.gpu -= res.gpu
+            self.requested.eph -= res.eph
+            for k, v in res.scalar.items():
+                self.requested.scalar[k] = self.requested.scalar.get(k, 0) - v
+            self.nonzero_cpu -= nzc
+            self.nonzero_mem -= nzm
+            for ip, proto, port in pod_ports(pod):
+                if port > 0:
+                    self.used_ports.discard(_sanitize(ip, proto) + (port,))
+            return
+        raise KeyError("no corresponding pod %s in pods of node %s" % ((pod.get("metadata") or {}).get("name"), self.name))
+
+    def remove_node(self):
+        """RemoveNode (node_info.go:450-463)."""
+        self.node = None
+        self.allocatable = Resource()
+        self.taints = []
+        self.mem_pressure = "Unknown"
+        self.disk_pressure = "Unknown"
+
+
+def pod_key(pod):
+    """getPodKey (node_info.go:497-503) is the UID; pods without one are keyed by namespace/name."""
+    md = pod.get("metadata") or {}
+    return md.get("uid") or "%s/%s" % (md.get("namespace", ""), md.get("name", ""))
+
 
 # --------------------------------------------------------------------------
 # Predicates (S/algorithm/predicates/predicates.go)
@@ -902,6 +940,107 @@ class GenericScheduler:
         ix = self.last_node_index % first_after
         self.last_node_index = (self.last_node_index + 1) % (1 << 64)
         return lst[ix][0]
+
+
+# --------------------------------------------------------------------------
+# Scheduler cache (S/schedulercache/cache.go) driven by informer-style events, and the
+# scheduleOne loop's Schedule + assume (S/scheduler.go:188-204, 366-397)
+# --------------------------------------------------------------------------
+class SchedulerCache:
+    def __init__(self, predicate_keys, priority_configs):
+        self.nodes = {}          # name -> NodeInfo (cache.nodes)
+        self.listed = []         # names the node lister returns (added, not removed)
+        self.pod_states = {}     # key -> pod
+        self.assumed = set()
+        self.sched = GenericScheduler(predicate_keys, priority_configs)
+
+    def _info(self, name):
+        n = self.nodes.get(name)
+        if n is None:
+            n = self.nodes[name] = NodeInfo()
+        return n
+
+    def _add(self, pod):                                   # cache.go:200-207
+        self._info((pod.get("spec") or {}).get("nodeName", "")).add_pod(pod)
+
+    def _remove(self, pod):                                # cache.go:219-228
+        name = (pod.get("spec") or {}).get("nodeName", "")
+        n = self.nodes[name]
+        n.remove_pod(pod)
+        if not n.pods and n.node is None:
+            del self.nodes[name]
+
+    def assume_pod(self, pod):                             # cache.go:125-143
+        key = pod_key(pod)
+        if key in self.pod_states:
+            raise KeyError("pod %s is in the cache, so can't be assumed" % key)
+        self._add(pod)
+        self.pod_states[key] = pod
+        self.assumed.add(key)
+
+    def add_pod(self, pod):                                # cache.go:230-262
+        key = pod_key(pod)
+        cur = self.pod_states.get(key)
+        if cur is not None and key in self.assumed:
+            if (cur.get("spec") or {}).get("nodeName") != (pod.get("spec") or {}).get("nodeName"):
+                self._remove(cur)
+                self._add(pod)
+            self.assumed.discard(key)
+            self.pod_states[key] = pod
+        elif cur is None:
+            self._add(pod)
+            self.pod_states[key] = pod
+        else:
+            raise KeyError("pod %s was already in added state" % key)
+
+    def update_pod(self, old, new):                        # cache.go:265-289
+        key = pod_key(old)
+        if key not in self.pod_states or key in self.assumed:
+            raise KeyError("pod %s is not added to scheduler cache, so cannot be updated" % key)
+        self._remove(old)
+        self._add(new)
+        self.pod_states[key] = new
+
+    def remove_pod(self, pod):                             # cache.go:292-318
+        key = pod_key(pod)
+        cur = self.pod_states.get(key)
+        if cur is None or key in self.assumed:
+            raise KeyError("pod %s is not found in scheduler cache, so cannot be removed from it" % key)
+        self._remove(cur)
+        del self.pod_states[key]
+
+    def add_node(self, node):                              # cache.go:354-363
+        name = (node.get("metadata") or {}).get("name", "")
+        self._info(name).set_node(node)
+        if name not in self.listed:
+            self.listed.append(name)
+
+    def update_node(self, old, new):                       # cache.go:366-375
+        self.add_node(new)
+
+    def remove_node(self, node):                           # cache.go:378-393
+        name = (node.get("metadata") or {}).get("name", "")
+        n = self.nodes[name]
+        n.remove_node()
+        if not n.pods and n.node is None:
+            del self.nodes[name]
+        self.listed.remove(name)
+
+    def schedule(self, pod):
+        """genericScheduler.Schedule over the listed nodes (nodeLister.List, factory.go:1088)."""
+        return self.sched.schedule(pod, [self.nodes[n] for n in self.listed])
+
+    def schedule_one(self, pod):
+        """scheduleOne's schedule + assume (scheduler.go:431-484): returns the host, or the
+        FitError message; the assumed pod carries spec.nodeName = host."""
+        try:
+            host = self.schedule(pod)
+        except FitError as e:
+            return None, str(e)
+        assumed = dict(pod)
+        assumed["spec"] = dict(pod.get("spec") or {}, nodeName=host)
+        self.assume_pod(assumed)
+        return host, None
 
 
 # --------------------------------------------------------------------------

@@ -1,0 +1,91 @@
+"""Per-pod drop-in parity (GPU): the scheduleOne loop through ksim.cache.SchedulerCache
+(ksim_schedule_one + the cache-event entry points of include/ksim.h) against the object-level
+oracle's SchedulerCache (oracle/ksim_ref.py, restating schedulercache/cache.go and
+genericScheduler.Schedule), on seeded streams that interleave Schedule + assume with node add /
+update / remove and pod add / confirm / update / remove events.  Every decision (host or FitError
+text), lastNodeIndex and the final per-node state must be identical."""
+import pytest
+
+import ksim_ref as R
+from events import apply, event_stream
+from ksim import abi, scheduler
+from ksim.cache import SchedulerCache
+
+pytestmark = pytest.mark.gpu
+
+POLICIES = {
+    "default": scheduler.provider("DefaultProvider"),
+    "talkintdata": scheduler.provider("TalkintDataProvider"),
+    "lr_bra": (["GeneralPredicates", "CheckNodeCondition", "PodToleratesNodeTaints", "CheckNodeMemoryPressure",
+                "CheckNodeDiskPressure"], [("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]),
+    "no_priorities": (["GeneralPredicates", "CheckNodeCondition"], []),
+}
+
+
+def _drive(seed, policy, n_events, n_nodes, features=True, mode=abi.MODE_AUTO):
+    preds, prios = POLICIES[policy]
+    ref = R.SchedulerCache(set(preds), prios)
+    dut = SchedulerCache(preds, prios, device=0, mode=mode)
+    decisions = 0
+    try:
+        for ev in event_stream(seed, ref, n_events, n_nodes, features):
+            want = apply(ref, ev)
+            got = apply(dut, ev)
+            if ev[0] == "schedule":
+                decisions += 1
+                assert got == want, (ev[1]["metadata"]["name"], want, got)
+        assert dut.last_node_index == ref.sched.last_node_index
+        st = dut.node_state()
+        assert dut.names == sorted(ref.listed, key=lambda s: s.encode())
+        for i, name in enumerate(dut.names):
+            ni = ref.nodes[name]
+            got = (st["req_cpu"][i], st["req_mem"][i], st["nz_cpu"][i], st["nz_mem"][i], st["pod_count"][i],
+                   st["port_count"][i])
+            want = (ni.requested.cpu, ni.requested.mem, ni.nonzero_cpu, ni.nonzero_mem, len(ni.pods),
+                    len(ni.used_ports))
+            assert got == want, (name, want, got)
+    finally:
+        dut.close()
+    return decisions
+
+
+@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("policy", sorted(POLICIES))
+def test_event_stream_parity(seed, policy):
+    assert _drive(seed, policy, n_events=300, n_nodes=14) > 100
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_event_stream_resource_only(seed):
+    """Resource-only pods (the fast kernels' pod shape) through the same event mix."""
+    assert _drive(100 + seed, "lr_bra", n_events=400, n_nodes=20, features=False) > 150
+
+
+def test_empty_cache_is_err_no_nodes():
+    preds, prios = POLICIES["default"]
+    dut = SchedulerCache(preds, prios, device=0)
+    try:
+        with pytest.raises(abi.NoNodesAvailable):
+            dut.schedule({"metadata": {"name": "p"}, "spec": {"containers": [{}]}})
+        dut.add_node({"metadata": {"name": "n"}, "status": {"allocatable": {"cpu": "1", "memory": "1Gi", "pods": "2"}}})
+        assert dut.schedule({"metadata": {"name": "p"}, "spec": {"containers": [{}]}}) == "n"
+        assert dut.last_node_index == 0  # a single fit does not call selectHost
+    finally:
+        dut.close()
+
+
+def test_schedule_only_leaves_cache_unchanged():
+    preds, prios = POLICIES["lr_bra"]
+    dut = SchedulerCache(preds, prios, device=0)
+    try:
+        for i in range(3):
+            dut.add_node({"metadata": {"name": "n%d" % i},
+                          "status": {"allocatable": {"cpu": "4", "memory": "8Gi", "pods": "10"}}})
+        pod = {"metadata": {"name": "p"}, "spec": {"containers": [{"resources": {"requests": {"cpu": "1"}}}]}}
+        hosts = [dut.schedule(pod) for _ in range(3)]
+        assert hosts == ["n2", "n1", "n0"]  # ties rotate from the highest name; nothing committed
+        assert int(dut.node_state()["req_cpu"].sum()) == 0
+        assert dut.schedule(pod, assume=True) == "n2"
+        assert list(dut.node_state()["req_cpu"]) == [0, 0, 1000]
+    finally:
+        dut.close()
