@@ -1,25 +1,28 @@
 """Benchmark of the MI355X per-pod scheduling cycle on BASELINE.json's headline workload.
 
 Workload (BASELINE.json configs[2], SURVEY.md §8d "C3", the default; --workload c2 / c4 / c5
-run the other configs the same way): 100,000 nodes, 1,000,000 mixed-size
-pods, default predicates + LeastRequested(1) + BalancedResourceAllocation(1).  A "step" is
-one ksim_schedule() call over the next `--batch` pods of the queue (each pod: predicates on
-every node, priorities, selectHost, commit — strictly one after another), with the node
-table and pod queue already resident in HBM.
+run the other configs the same way): 100,000 nodes, a 1,000,000-pod queue of mixed sizes,
+default predicates + LeastRequested(1) + BalancedResourceAllocation(1).  A "step" is one
+ksim_schedule() call over the next slice of the queue (each pod: predicates on every node,
+priorities, selectHost, commit — strictly one after another), with the node table and pod
+queue resident in HBM.  The K timed steps cover the WHOLE queue (slice = queue / K pods); the
+W warmup steps run the head of the queue on a separate copy of the cluster first, so the
+timed run starts from the empty cluster and ends at the queue's last pod.
 
-N GPUs (torchrun, one process per GPU), two measurements in one run:
-  * headline `value` (--shard replicas, default): scenario-parallel replicas — every rank runs
-    its own 100k-node cluster with its own policy weights (a what-if sweep), no
-    data-path collective; scaling "weak".  value = pods scheduled by all ranks / max time.
-  * `node_sharded`: ONE 100k-node cluster split into N contiguous name-rank shards, one per
-    GPU, each pod decided jointly through the per-pod exchange over xGMI (ksim_shard_*);
-    pods/s of that one cluster (strong scaling), its placements checked against the
-    single-cluster run of rank 0.  With --shard nodes this is the headline instead.
+N GPUs (torchrun, one process per GPU):
+  * headline `value` (--shard nodes, the default): ONE 100k-node cluster split into N
+    contiguous name-rank shards, one per GPU; each pod is decided jointly through the per-pod
+    exchange over xGMI (ksim_shard_*), the owning rank commits.  pods/s of that one cluster
+    (scaling "strong"); placements checked against a single-GPU run of the same queue.
+  * `replicas`: every rank schedules its own cluster under its own LeastRequested weight (a
+    what-if sweep, no data-path collective; scaling "weak").  --shard replicas makes it the
+    headline instead.
 
-The JSON line also carries the roofline of the dominant kernel (algorithmic bytes per launch
-÷ HIP-event launch duration, against the 8 TB/s HBM peak) and a cpu_baseline: the C oracle
-(oracle/cpu_ref.c, a port of the Go path) timed on a bounded prefix of the same queue, whose
-placements must equal the GPU's for the same prefix (reported as "parity").
+The JSON line carries the roofline of the dominant kernel (algorithmic bytes per launch ÷ the
+HIP-event launch duration measured on the library's stream, against the 8 TB/s HBM peak; null
+for tree mode, whose kernel does not read the table per pod) and a cpu_baseline: the C port of
+the Go path (oracle/cpu_ref.c) timed on the host on bounded prefixes of the same queue at 1, 16
+and all threads, its placements equal to the GPU's for the same prefix ("parity").
 """
 import argparse
 import json
@@ -48,15 +51,16 @@ def pmc_traffic(workload, evals_per_launch):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=None, help="default: c3 100, c2 9, c4 10, c5 3")
-    ap.add_argument("--warmup", type=int, default=None, help="default: c3 3, c2 2, c4 1, c5 1")
-    ap.add_argument("--batch", type=int, default=None, help="pods per step (default: c3/c2 4096, c4 512)")
+    ap.add_argument("--steps", type=int, default=None, help="timed ksim_schedule calls (default: c3 20, c2 9, c4 10)")
+    ap.add_argument("--warmup", type=int, default=None, help="untimed calls on a separate cluster copy (default 2)")
+    ap.add_argument("--batch", type=int, default=None,
+                    help="pods per step (default: c3 / c2 the whole queue over the timed steps, c4 512)")
     ap.add_argument("--nodes", type=int, default=None, help="default: c3 100,000, c2 5,000, c4 1,000,000")
     ap.add_argument("--pods", type=int, default=None, help="queue length (default: c3 1M, c2 50k, c4 as needed)")
     ap.add_argument("--mode", default="auto", choices=["auto", "launch", "persistent", "tree"])
     ap.add_argument("--no-tree", dest="tree", action="store_false",
                     help="skip the tree-mode line measured beside the scan (c3/c4)")
-    ap.add_argument("--cpu-sample", type=int, default=3000, help="pods in the CPU-baseline prefix (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=3000, help="pods in the 16-thread CPU-baseline prefix (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"],
                     help="c3: the headline metric (default); c2: 5k heterogeneous nodes with selectors, "
@@ -66,27 +70,29 @@ def parse():
     ap.add_argument("--sweep-form", default="auto", choices=["auto", "scan"],
                     help="c5: auto = tree form when eligible; scan = the per-scenario scan kernel")
     ap.add_argument("--sweep-pods", type=int, default=5000, help="c5: pods scheduled in every scenario")
-    ap.add_argument("--shard", default="replicas", choices=["replicas", "nodes", "none"],
-                    help="N>1 headline: replicas (weak) or one node-sharded cluster (strong); "
-                         "the other one is measured as well unless 'none'")
-    ap.add_argument("--shard-steps", type=int, default=20, help="timed steps of the node-sharded measurement")
+    ap.add_argument("--shard", default="nodes", choices=["nodes", "replicas", "none"],
+                    help="N>1 headline: one node-sharded cluster (strong, default) or per-rank replicas "
+                         "(weak); the other one is measured beside it unless 'none'")
+    ap.add_argument("--replica-pods", type=int, default=200_000, help="N>1: queue prefix of the replica side line")
     ap.add_argument("--one-device", action="store_true",
                     help="rehearsal on a 1-GPU box: every rank on device 0 (gloo), grids split so the "
                          "ranks' persistent kernels are co-resident")
     a = ap.parse_args()
     d = WORKLOADS[a.workload]
-    for k in ("steps", "warmup", "batch", "nodes", "pods"):
+    for k in ("steps", "warmup", "nodes", "pods"):
         if getattr(a, k) is None:
             setattr(a, k, d.get(k))
+    if a.batch is None:
+        a.batch = d.get("batch") or -(-a.pods // a.steps)
     if a.pods is None:
-        a.pods = (a.warmup + max(a.steps, a.shard_steps)) * a.batch
+        a.pods = a.steps * a.batch
     return a
 
 
 # per-workload defaults; bytes = algorithmic bytes per node-eval
 WORKLOADS = {
-    "c3": dict(steps=100, warmup=3, batch=4096, nodes=100_000, pods=1_000_000, bytes=60),
-    "c2": dict(steps=9, warmup=2, batch=4096, nodes=5000, pods=50_000, bytes=68),
+    "c3": dict(steps=20, warmup=2, batch=None, nodes=100_000, pods=1_000_000, bytes=60),
+    "c2": dict(steps=9, warmup=2, batch=None, nodes=5000, pods=50_000, bytes=68),
     "c4": dict(steps=10, warmup=1, batch=512, nodes=1_000_000, pods=None, bytes=60),
     "c5": dict(steps=3, warmup=1, batch=0, nodes=20_000, pods=0, bytes=60),
 }
@@ -123,6 +129,10 @@ class Dist:
             self.dist.barrier()
         self.torch.cuda.synchronize()
 
+    def barrier(self):
+        if self.dist is not None:
+            self.dist.barrier()
+
     def allmax(self, x):
         if self.dist is None:
             return x
@@ -143,59 +153,88 @@ class Dist:
             self.dist.destroy_process_group()
 
 
-def node_sharded(a, D, cl, preds, prios, ref):
+def timed_queue(a, D, make, steps, batch, pods):
+    """Warm up on a separate scheduler (make()), then time `steps` calls of `batch` pods over the
+    first `pods` pods of a fresh one, bracketed by barrier + device sync on every rank.
+    Returns (placements, elapsed max over ranks, summed kernel ms, launches, last stats)."""
+    import numpy as np
+    w = make()
+    first = 0
+    for _ in range(a.warmup):
+        D.barrier()
+        w.schedule(first, min(batch, pods - first) if pods > first else 0)
+        first = min(pods, first + batch)
+    D.barrier()  # every rank's warmup kernels are done before any exchange buffer goes away
+    w.close()
+    g = make()
+    outs, first, kms, launches, st = [], 0, 0.0, 0, None
+    D.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        cnt = min(batch, pods - first)
+        if cnt <= 0:
+            break
+        o, _, st = g.schedule(first, cnt)
+        outs.append(o)
+        first += cnt
+        kms += st.kernel_ms
+        launches += st.kernel_launches
+    D.sync()
+    el = D.allmax(time.perf_counter() - t0)
+    return g, np.concatenate(outs), el, kms, launches, st, first
+
+
+class Local:
+    """Timing bracket of a run that involves this rank only (no barrier, no cross-rank max)."""
+    barrier = staticmethod(lambda: None)
+    allmax = staticmethod(lambda x: x)
+
+    @staticmethod
+    def sync():
+        import torch
+        torch.cuda.synchronize()
+
+
+def single_cluster(a, D, cl, preds, prios, mode, device):
+    """One cluster per rank (N = 1: the headline; N > 1: the replica side line, or rank 0's
+    single-GPU reference for the node-sharded run with D = Local)."""
+    from ksim import scheduler
+    make = lambda: scheduler.GenericScheduler(cl, preds, prios, device=device, mode=mode, collect_reasons=False)
+    g, out, el, kms, launches, st, pods = timed_queue(a, D, make, a.steps, a.batch, a.pods)
+    g.close()
+    return dict(out=out, elapsed=el, kernel_ms=kms, launches=launches, mode=st.mode, blocks=st.blocks, pods=pods)
+
+
+def node_sharded(a, D, cl, preds, prios):
     """One cluster, node-sharded over the D.world ranks: rank r holds
     name ranks [r*n/world, (r+1)*n/world); per pod the ranks exchange (fit count, max score,
     count at max) by device-initiated writes into each other's exchange buffers and reach the
-    same selectHost decision.  Returns the measurement dict (identical collective sequence on
-    every rank, whatever fails)."""
+    same selectHost decision.  Identical collective sequence on every rank, whatever fails."""
     import numpy as np
     from ksim import scheduler
-    out, err, s = np.zeros(0, np.int32), None, None
-    try:
+    scheds = []
+
+    def make():
         s = scheduler.ShardedScheduler(cl, preds, prios, D.rank, D.world, device=D.local)
         s.connect_torch(D.dist)
-    except Exception as e:  # noqa: BLE001 — reported in the JSON line
-        err = "setup: %s" % e
-    errs = D.gather(err)
-    if any(errs):
-        return {"error": [e for e in errs if e][0]}
-    outs, first, kms, el = [], 0, 0.0, 0.0
+        scheds.append(s)
+        return s
+
+    err = None
+    res = None
     try:
-        for _ in range(a.warmup):
-            outs.append(s.schedule(first, a.batch)[0])
-            first += a.batch
-        D.sync()
-        t0 = time.perf_counter()
-        for _ in range(a.shard_steps):
-            o, _, st = s.schedule(first, a.batch)
-            outs.append(o)
-            first += a.batch
-            kms += st.kernel_ms
-        D.sync()
-        el = time.perf_counter() - t0
-        out = np.concatenate(outs)
-    except Exception as e:  # noqa: BLE001
-        err = "schedule: %s" % e
+        g, out, el, kms, launches, st, pods = timed_queue(a, D, make, a.steps, a.batch, a.pods)
+        res = dict(out=out, elapsed=el, kernel_ms=D.allmax(kms), launches=launches, mode=st.mode, blocks=st.blocks,
+                   pods=pods, nodes_local=g.hi - g.lo)
+    except Exception as e:  # noqa: BLE001 — reported in the JSON line
+        err = "%s: %s" % (type(e).__name__, e)
     errs = D.gather(err)
-    el = D.allmax(el)
-    kms = D.allmax(kms)
-    allouts = D.gather(out)
-    s.close()
+    outs = D.gather(res["out"] if res else np.zeros(0, np.int32))
+    for s in scheds:
+        s.close()
     if any(errs):
         return {"error": [e for e in errs if e][0]}
-    merged = scheduler.merge_sharded(allouts)
-    pods = a.shard_steps * a.batch
-    res = {"value": round(pods / el, 1), "unit": "pods/s", "node_evals_per_s": round(pods * cl.n_nodes / el, 1),
-           "scaling": "strong", "ranks": D.world, "nodes": cl.n_nodes, "nodes_per_rank": cl.n_nodes // D.world,
-           "steps": a.shard_steps, "pods_per_step": a.batch, "ms_per_step": round(el * 1e3 / a.shard_steps, 4),
-           "avg_launch_us": round(kms * 1e3 / a.shard_steps, 3),
-           "exchange": "device-initiated system-scope stores into every rank's fine-grained exchange buffer (IPC)"
-                       + (", all ranks on device 0 (rehearsal)" if D.one else " over xGMI")}
-    if ref is not None:
-        S = min(len(ref), len(merged))
-        res["parity"] = {"pods": S, "vs": "single-GPU run of the same cluster and queue",
-                         "match": bool(np.array_equal(merged[:S], ref[:S]))}
+    res["merged"] = scheduler.merge_sharded(outs)
     return res
 
 
@@ -205,28 +244,49 @@ def tree_mode(a, cl, preds, prios, device, ref):
     scan): pods/s over the same timed steps, and its placements against the scan's."""
     import numpy as np
     from ksim import abi, scheduler
-    g = scheduler.GenericScheduler(cl, preds, prios, device=device, mode=abi.MODE_TREE, collect_reasons=False)
-    outs, first = [], 0
-    for _ in range(a.warmup):
-        outs.append(g.schedule(first, a.batch)[0])
-        first += a.batch
-    kms, mode_used = 0.0, 0
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        o, _, st = g.schedule(first, a.batch)
-        outs.append(o)
-        first += a.batch
-        kms += st.kernel_ms
-        mode_used = st.mode
-    el = time.perf_counter() - t0
-    out = np.concatenate(outs)
-    pods = a.steps * a.batch
+
+    make = lambda: scheduler.GenericScheduler(cl, preds, prios, device=device, mode=abi.MODE_TREE, collect_reasons=False)
+    g, out, el, kms, launches, st, pods = timed_queue(a, Local, make, a.steps, a.batch, a.pods)
+    g.close()
     return {"value": round(pods / el, 1), "unit": "pods/s", "ms_per_step": round(el * 1e3 / a.steps, 4),
             "kernel_us_per_pod": round(kms * 1e3 / pods, 3),
-            "mode": {3: "tree"}.get(mode_used, str(mode_used)),
+            "mode": {3: "tree"}.get(st.mode, str(st.mode)),
             "parity_vs_scan": {"pods": int(len(out)), "match": bool(np.array_equal(out, ref[:len(out)]))},
             "note": "one wave on one CU per cluster; placements identical to the scan's; the headline "
                     "node-evals/s metric is defined on the full scan, so this is reported beside it"}
+
+
+def cpu_baseline(a, cl, preds, prios, placements, unit="pods/s"):
+    """The C port of the Go path (oracle/cpu_ref.c, OpenMP node-parallel like
+    workqueue.Parallelize) on bounded prefixes of the same queue, at 1, 16 and all host threads;
+    parity = its placements equal the GPU's over the largest prefix."""
+    import numpy as np
+    from ksim import scheduler
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import cpu_ref
+    n = cl.n_nodes
+    cfg = scheduler.make_config(preds, prios)
+    avail = len(os.sched_getaffinity(0))
+    legs = []
+    for t, budget in ((1, 3e7), (min(a.cpu_threads, avail), 3e8), (min(avail, 64), 3e8)):
+        if any(t == x[0] for x in legs):
+            continue
+        S = int(min(a.cpu_sample, len(placements), max(20, budget // n)))
+        t1 = time.perf_counter()
+        ref, _, _, _ = cpu_ref.run(cl, cfg, 0, S, threads=t)
+        s = time.perf_counter() - t1
+        legs.append((t, S, s, bool(np.array_equal(ref, placements[:S]))))
+    main = max(legs, key=lambda x: (x[0] == min(a.cpu_threads, avail), x[1]))
+    t, S, s, match = main
+    cpu = {"value": round(S / s, 1), "unit": unit, "cores": t, "kind": "port",
+           "sample": "first %d pods of the same %s queue on the same %d-node cluster (oracle/cpu_ref.c, "
+                     "OpenMP node-parallel like workqueue.Parallelize), %.2f s" % (S, a.workload.upper(), n, s),
+           "node_evals_per_s": round(S * n / s, 1),
+           "by_threads": [{"cores": x[0], "pods": x[1], "seconds": round(x[2], 3), "value": round(x[1] / x[2], 1)}
+                          for x in legs],
+           "host_cpus_visible": avail}
+    parity = {"prefix_pods": max(x[1] for x in legs), "match": all(x[3] for x in legs)}
+    return cpu, parity
 
 
 def main():
@@ -234,16 +294,10 @@ def main():
     if a.workload == "c5":
         return main_c5(a)
     import numpy as np
-    import torch
-    from ksim import abi, scheduler, synth
+    from ksim import abi, synth
 
     D = Dist(a)
-    world, rank, local, dist = D.world, D.rank, D.local, D.dist
-    barrier_sync = D.sync
-
-    total_pods = (a.warmup + a.steps) * a.batch
-    if total_pods > a.pods:
-        raise SystemExit("warmup+steps x batch = %d exceeds the %d-pod queue" % (total_pods, a.pods))
+    world, rank, local = D.world, D.rank, D.local
     W = WORKLOADS[a.workload]
     if a.workload == "c3":
         cl, preds, prios = synth.config_c3(a.nodes, a.pods)
@@ -258,72 +312,68 @@ def main():
         desc = ("C2: %d heterogeneous nodes (labels, taints, NotReady), %d pods with nodeSelector, host ports, "
                 "tolerations, BestEffort; DefaultProvider")
         data = "synthetic (random.Random seed 2 objects through ingest, SURVEY.md §8d C2)"
-    prios0 = list(prios)  # the one cluster's policy (rank 0's replica, the node-sharded run)
-    if rank > 0:  # what-if sweep: each replica scores with its own LeastRequested weight
-        prios = [(k, w + rank) if k == "LeastRequestedPriority" else (k, w) for k, w in prios0]
-    mode = {"auto": abi.MODE_AUTO, "launch": abi.MODE_LAUNCH, "persistent": abi.MODE_PERSISTENT, "tree": abi.MODE_TREE}[a.mode]
-    g = scheduler.GenericScheduler(cl, preds, prios, device=local, mode=mode, collect_reasons=False)
-
-    placements = []
-    first = 0
-    for _ in range(a.warmup):
-        out, _, _ = g.schedule(first, a.batch)
-        placements.append(out)
-        first += a.batch
-    barrier_sync()
-    t0 = time.perf_counter()
-    kernel_ms = 0.0
-    launches = 0
-    mode_used = blocks = 0
-    for _ in range(a.steps):
-        out, _, st = g.schedule(first, a.batch)
-        placements.append(out)
-        first += a.batch
-        kernel_ms += st.kernel_ms
-        launches += st.kernel_launches
-        mode_used, blocks = st.mode, st.blocks
-    barrier_sync()
-    elapsed = D.allmax(time.perf_counter() - t0)
-    placements = np.concatenate(placements)
-    bound = int((placements >= 0).sum())
-
-    pods_timed = a.steps * a.batch
-    value = world * pods_timed / elapsed
-    sharded = None
-    if world > 1 and a.shard != "none" and a.workload != "c2":  # sharding takes resource-only pods
-        sharded = node_sharded(a, D, cl, preds, prios0, placements if rank == 0 else None)
     n = cl.n_nodes
-    # dominant kernel: the scan (launch mode: one launch per pod) or the persistent kernel
-    if mode_used == abi.MODE_LAUNCH:
-        pods_per_launch = 1
-        avg_launch_s = kernel_ms / 1e3 / max(pods_timed, 1)
-    else:
-        pods_per_launch = a.batch
-        avg_launch_s = kernel_ms / 1e3 / max(launches, 1)
-    achieved = W["bytes"] * n * pods_per_launch / avg_launch_s / 1e9
+    mode = {"auto": abi.MODE_AUTO, "launch": abi.MODE_LAUNCH, "persistent": abi.MODE_PERSISTENT, "tree": abi.MODE_TREE}[a.mode]
+    sharded_head = world > 1 and a.shard == "nodes" and a.workload != "c2"  # sharding takes resource-only pods
+
+    # ---- the one cluster: single GPU (N = 1), or node-sharded across the N ranks ----
+    single = None
+    if world == 1 or not sharded_head or rank == 0:
+        # N = 1 headline; with N > 1 rank 0's single-GPU run is the sharded run's parity reference
+        single = single_cluster(a, D if (world == 1 or not sharded_head) else Local, cl, preds, prios, mode, local)
+    D.barrier()
+    head = single
+    sharded = None
+    if sharded_head:
+        sharded = node_sharded(a, D, cl, preds, prios)
+        head = sharded
+    replicas = None
+    if world > 1 and a.shard != "none" and not (a.shard == "replicas" or a.workload == "c2"):
+        # side line: each rank its own cluster under its own LeastRequested weight (weak scaling)
+        prios_r = [(k, w + rank) if k == "LeastRequestedPriority" else (k, w) for k, w in prios]
+        r_args = argparse.Namespace(**vars(a))
+        r_args.pods = min(a.pods, a.replica_pods)
+        r_args.batch = -(-r_args.pods // a.steps)
+        rr = single_cluster(r_args, D, cl, preds, prios_r, mode, local)
+        replicas = {"value": round(world * rr["pods"] / rr["elapsed"], 1), "unit": "pods/s", "scaling": "weak",
+                    "ranks": world, "pods_per_rank": rr["pods"],
+                    "ms_per_step": round(rr["elapsed"] * 1e3 / a.steps, 4),
+                    "note": "every rank schedules its own %d-node cluster under LeastRequested weight 1 + rank "
+                            "(a what-if sweep), no data-path collective" % n}
+    if world > 1 and a.shard == "replicas":
+        prios_r = [(k, w + rank) if k == "LeastRequestedPriority" else (k, w) for k, w in prios]
+        head = single_cluster(a, D, cl, preds, prios_r, mode, local)
 
     tree = None
-    if rank == 0 and a.tree and a.mode != "tree" and a.workload in ("c3", "c4"):
-        tree = tree_mode(a, cl, preds, prios, local, placements)
-
-    cpu = None
-    parity = None
-    if rank == 0 and a.cpu_sample > 0:
-        sys.path.insert(0, os.path.join(ROOT, "oracle"))
-        import cpu_ref
-        S = min(a.cpu_sample, len(placements), max(50, int(3e8 // n)))  # ~10-30 s of CPU work at most
-        threads = max(1, min(a.cpu_threads, len(os.sched_getaffinity(0))))
-        cfg = scheduler.make_config(preds, prios)
-        t1 = time.perf_counter()
-        ref_out, _, _, _ = cpu_ref.run(cl, cfg, 0, S, threads=threads)
-        cpu_s = time.perf_counter() - t1
-        cpu = {"value": round(S / cpu_s, 1), "unit": "pods/s", "cores": threads, "kind": "port",
-               "sample": "first %d pods of the same %s queue on the same %d-node cluster (oracle/cpu_ref.c, "
-                         "OpenMP node-parallel like workqueue.Parallelize), %.1f s" % (S, a.workload.upper(), n, cpu_s),
-               "node_evals_per_s": round(S * n / cpu_s, 1)}
-        parity = {"prefix_pods": S, "match": bool(np.array_equal(ref_out, placements[:S]))}
+    if rank == 0 and a.tree and a.mode != "tree" and a.workload in ("c3", "c4") and single is not None:
+        tree = tree_mode(a, cl, preds, prios, local, single["out"])
+    cpu = parity = None
+    if rank == 0 and a.cpu_sample > 0 and single is not None:
+        cpu, parity = cpu_baseline(a, cl, preds, prios, single["out"])
 
     if rank == 0:
+        if "error" in head:
+            line = {"metric": "pods scheduled/sec + node-evals/sec at 100k nodes, 1/2/4/8 MI355X", "value": None,
+                    "error": head["error"], "n_gpus": world}
+            print(json.dumps(line))
+            D.close()
+            return
+        pods_timed = head["pods"]
+        elapsed = head["elapsed"]
+        value = (world if (world > 1 and a.shard == "replicas") else 1) * pods_timed / elapsed
+        mode_used = head["mode"]
+        n_local = head.get("nodes_local", n)
+        # dominant kernel: the scan (launch mode: one launch per pod) or the persistent kernel;
+        # per-launch average from HIP events on the library's stream (max over ranks when sharded)
+        if mode_used == abi.MODE_LAUNCH:
+            pods_per_launch = 1
+            avg_launch_s = head["kernel_ms"] / 1e3 / max(pods_timed, 1)
+        else:
+            pods_per_launch = a.batch
+            avg_launch_s = head["kernel_ms"] / 1e3 / max(head["launches"], 1)
+        achieved = W["bytes"] * n_local * min(pods_per_launch, pods_timed) / avg_launch_s / 1e9
+        tree_kernel = mode_used == abi.MODE_TREE
+        bound = int((head.get("merged", head["out"]) >= 0).sum())
         line = {
             "metric": ("pods scheduled/sec + node-evals/sec at 100k nodes, 1/2/4/8 MI355X" if a.workload == "c3" else
                        "pods scheduled/sec + node-evals/sec, %s (%d nodes)" % (a.workload.upper(), n)),
@@ -335,22 +385,29 @@ def main():
             "warmup": a.warmup,
             "ms_per_step": round(elapsed * 1e3 / a.steps, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if sharded_head else "weak",
             "vs_baseline": None,
             "dtype": "int64",
             "data": data,
             "config": {"workload": desc % (n, a.pods),
-                       "nodes": n, "pods_per_step": a.batch, "global_batch": a.batch * world,
-                       "mode": {1: "launch", 2: "persistent", 3: "tree"}.get(mode_used, str(mode_used)), "blocks": blocks,
-                       "parallelism": "scenario-replicas x%d" % world if world > 1 else "single-gpu"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": pmc_traffic(a.workload + ("" if mode_used == abi.MODE_PERSISTENT else "_launch"),
-                                                n * pods_per_launch),
+                       "nodes": n, "pods_timed": pods_timed, "pods_per_step": a.batch,
+                       "timed_region": "the whole %d-pod queue from the empty cluster (warmup on a separate copy)"
+                                       % pods_timed if pods_timed == a.pods else "the first %d pods" % pods_timed,
+                       "global_batch": a.batch,
+                       "mode": {1: "launch", 2: "persistent", 3: "tree"}.get(mode_used, str(mode_used)),
+                       "blocks": head["blocks"],
+                       "parallelism": ("node-sharded x%d" % world if sharded_head else
+                                       "scenario-replicas x%d" % world if world > 1 else "single-gpu")},
+            "roofline": {"bound": "hbm", "achieved": None if tree_kernel else round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": None if tree_kernel else round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None if (tree_kernel or world > 1) else
+                         pmc_traffic(a.workload + ("" if mode_used == abi.MODE_PERSISTENT else "_launch"),
+                                     n * pods_per_launch),
                          "traffic_unit": "GB per launch (PMC)", "bytes_per_node_eval": W["bytes"],
+                         "nodes_per_gpu": n_local,
                          "avg_launch_us": round(avg_launch_s * 1e6, 3), "pods_per_launch": pods_per_launch,
-                         **({"note": "tree mode reads O(classes x log N) bytes per pod: achieved is the scan-equivalent "
-                                     "rate, not HBM traffic"} if mode_used == abi.MODE_TREE else {})},
+                         **({"note": "tree mode reads O(classes x log N) bytes per pod, not the table: no HBM "
+                                     "roofline applies"} if tree_kernel else {})},
             "cpu_baseline": cpu,
             "parity": parity,
             "pods_bound": bound,
@@ -358,12 +415,17 @@ def main():
         if tree is not None:
             line["tree_mode"] = tree
         if sharded is not None:
-            line["node_sharded"] = sharded
-            if a.shard == "nodes" and "value" in sharded:  # the one node-sharded cluster as the headline
-                line["replicas"] = {"value": line["value"], "scaling": "weak", "ms_per_step": line["ms_per_step"]}
-                line.update(value=sharded["value"], node_evals_per_s=sharded["node_evals_per_s"], scaling="strong",
-                            steps=a.shard_steps, ms_per_step=sharded["ms_per_step"])
-                line["config"].update(parallelism="node-sharded x%d" % world, global_batch=a.batch)
+            ns = {"ranks": world, "nodes_per_rank": n_local, "scaling": "strong",
+                  "exchange": "device-initiated system-scope stores into every rank's fine-grained exchange buffer "
+                              "(IPC)" + (", all ranks on device 0 (rehearsal)" if D.one else " over xGMI")}
+            if single is not None:
+                S = min(len(single["out"]), len(sharded["merged"]))
+                ns["parity"] = {"pods": int(S), "vs": "single-GPU run of the same cluster and queue",
+                                "match": bool(np.array_equal(sharded["merged"][:S], single["out"][:S]))}
+                ns["single_gpu_value"] = round(single["pods"] / single["elapsed"], 1)
+            line["node_sharded"] = ns
+        if replicas is not None:
+            line["replicas"] = replicas
         print(json.dumps(line))
     D.close()
 
@@ -439,8 +501,9 @@ def main_c5(a):
                        "nodes": n, "scenarios": len(scen), "scenarios_per_rank": len(mine),
                        "pods_per_scenario": a.sweep_pods, "parallelism": "scenario-parallel x%d" % world,
                        "form": "tree (one tree-mode wave per scenario)" if tree else "scan (one workgroup per scenario)"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "roofline": {"bound": "hbm", "achieved": None if tree else round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s",
+                         "frac": None if tree else round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if tree else pmc_traffic("c5", evals_per_launch),
                          "traffic_unit": "GB per launch (PMC)",
                          "bytes_per_node_eval": BYTES_PER_NODE_EVAL, "avg_launch_us": round(avg_launch_s * 1e6, 3),

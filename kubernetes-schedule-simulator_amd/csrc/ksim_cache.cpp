@@ -333,9 +333,11 @@ static int pod_delta(ksim_handle* h, int64_t node, const ksim_pod* pod, const ui
   if ((rc = check_pod_args(h, pod, n_ports, n_scalars, ports, scalars, where))) return rc;
   if (node < 0 || node >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "%s: node %lld out of range", where, (long long)node);
   if (add && (rc = ensure_port_room(h, pod->port_cnt))) return rc;
-  if ((rc = ksim_rt_check_pod(h, *pod, n_ports, n_scalars, scalars, where))) return rc;
+  ksim_pod p = *pod;
+  p.host = -1;  // spec.nodeName plays no part in a resource delta (the node is given)
+  if ((rc = ksim_rt_check_pod(h, p, n_ports, n_scalars, scalars, where))) return rc;
   KsimCtx cs;
-  if ((rc = stage_pod(h, *pod, ports, scalars, &cs))) return rc;
+  if ((rc = stage_pod(h, p, ports, scalars, &cs))) return rc;
   hipError_t e = add ? ksim_launch_assume(&cs, 0, node, h->res_dev + KSIM_RES_STATUS, h->stream)
                      : ksim_launch_release(&cs, 0, node, h->stream);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "%s launch: %s", where, hipGetErrorString(e));

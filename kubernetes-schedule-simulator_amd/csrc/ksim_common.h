@@ -95,6 +95,10 @@ struct KsimShard {
   uint32_t xtag_base;
   uint64_t* xchg;
   uint64_t* peers[KSIM_MAX_RANKS];
+  // bound of the first pod's cross-rank wait of a call (s_memrealtime ticks, 100 MHz): the start
+  // handshake absorbs per-rank launch skew (first code-object load, ingest, a descheduled host
+  // process); later pods keep the 2 s per-pod bound
+  uint64_t start_ticks;
 };
 
 // ((a*10)/b) with Go int64 semantics (wrapping multiply, truncating divide), b > 0.

@@ -111,9 +111,8 @@ struct ksim_handle {
   void* sw_scratch = nullptr;
   size_t sw_scratch_bytes = 0;
   // node-sharded mode (ksim_shard_*): world == 1 is the ordinary single-device mode
-  KsimShard shard{0, 1, 0, 0, nullptr, {}};
+  KsimShard shard{0, 1, 0, 0, nullptr, {}, 0};
   void* ipc_mapped[KSIM_MAX_RANKS] = {};  // peers' exchange buffers opened through IPC
-  uint64_t start_epoch = 0;                // host start handshake (node-sharded calls)
   int max_grid = 0;                        // workgroups per launch (0 = one per CU)
   double* mirror = nullptr;                // streaming fast kernel: float64 image [6][n]
   int64_t mirror_n = 0;

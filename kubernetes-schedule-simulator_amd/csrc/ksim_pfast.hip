@@ -167,6 +167,7 @@ struct PfArgs {
   uint32_t xtag_base;                 // exchange tag of pod first - 1 (host: running pod count)
   uint64_t* xchg;                     // this rank's aggregate slots [ANSLOT][KSIM_MAX_RANKS][4]
   uint64_t* peers[KSIM_MAX_RANKS];    // every rank's exchange buffer as mapped here (self included)
+  uint64_t start_ticks;               // bound of the first pod's cross-rank wait (KsimShard)
   // streaming form (tables beyond the LDS budget): float64 image of the table in HBM,
   // [6][n] = alloc cpu, alloc mem, requested cpu, mem, non-zero cpu, mem
   double* mirror;
@@ -572,7 +573,9 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           w1 = sys_load(src + 1);
           w2 = sys_load(src + 2);
           if (__all(!rl || ((w0 & hi) == at && (w1 & hi) == at && (w2 & hi) == at))) break;
-          if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_LIMIT_TICKS) { ok = false; break; }
+          // the first pod of a call doubles as the start handshake: the peers' kernels may start late
+          const uint64_t lim = (pod == a.first) ? a.start_ticks : SPIN_LIMIT_TICKS;
+          if (__builtin_amdgcn_s_memrealtime() - t0 > lim) { ok = false; break; }
           __builtin_amdgcn_s_sleep(1);
         }
         const int32_t Fr = rl ? (int32_t)(uint32_t)w0 : 0, Cr = rl ? (int32_t)((uint32_t)w1 & 0x7FFFFFFFu) : 0;
@@ -948,6 +951,7 @@ extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, in
   a.rank = sh->rank; a.world = sh->world; a.node_base = sh->node_base; a.xtag_base = sh->xtag_base;
   a.xchg = sh->xchg;
   for (int r = 0; r < KSIM_MAX_RANKS; ++r) a.peers[r] = sh->peers[r];
+  a.start_ticks = sh->start_ticks > SPIN_LIMIT_TICKS ? sh->start_ticks : SPIN_LIMIT_TICKS;
   a.n = c->n; a.chunk = c->chunk; a.first = c->first; a.end = c->end;
   a.alloc_cpu = c->alloc_cpu; a.alloc_mem = c->alloc_mem; a.allowed_pods = c->allowed_pods; a.flags = c->flags;
   a.req_cpu = c->req_cpu; a.req_mem = c->req_mem; a.nz_cpu = c->nz_cpu; a.nz_mem = c->nz_mem;

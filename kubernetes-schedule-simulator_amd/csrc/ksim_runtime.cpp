@@ -1066,6 +1066,11 @@ int ksim_shard_setup(ksim_handle* h, int32_t rank, int32_t world, int64_t node_b
   h->shard.node_base = node_base;
   h->shard.xtag_base = 0;
   h->shard.xchg = (uint64_t*)p;
+  {  // start handshake bound (seconds): KSIM_SHARD_START_S, default 120
+    const char* e = getenv("KSIM_SHARD_START_S");
+    const double sec = e ? atof(e) : 120.0;
+    h->shard.start_ticks = (uint64_t)((sec > 2.0 ? sec : 2.0) * 1e8);
+  }
   for (auto& q : h->shard.peers) q = nullptr;
   h->shard.peers[rank] = h->shard.xchg;
   return KSIM_OK;

@@ -339,6 +339,10 @@ class Cluster:
 
     # ----------------------------------------------------------------- tables
     def _build_tables(self):
+        if not self.label_sets.items:   # an empty cluster still has well-formed tables
+            self.label_sets.get(_canon({}), {})
+        if not self.taint_sets.items:
+            self.taint_sets.get(_canon([]), [])
         self.tables, need, bad = build_class_tables(self.label_sets.items, self.taint_sets.items,
                                                     self.classes.items or [{}])
         self.bad_affinity_classes |= bad

@@ -477,23 +477,29 @@ def test_node_sharded_fills_cluster_with_fit_errors(monkeypatch):
     assert all(s.last_node_index == ref_ctr for s in scheds)
 
 
-def test_node_sharded_multi_process(tmp_path):
-    """Two ranks in two processes (the one-process-per-device layout; here both on device 0),
-    exchange buffers shared through hipIpcGetMemHandle / hipIpcOpenMemHandle over a gloo
-    group: merged placements, counters and node state equal the C oracle's."""
+@pytest.mark.parametrize("skew", [0.0, 3.5])
+def test_node_sharded_multi_process(tmp_path, skew):
+    """Two ranks in two processes (the one-process-per-device layout: rank r on device
+    r % device_count, so both on device 0 of a one-GPU box), exchange buffers shared through
+    hipIpcGetMemHandle / hipIpcOpenMemHandle over a gloo group: merged placements, counters and
+    node state equal the C oracle's.  skew: the last rank starts its first call 3.5 s late —
+    beyond the 2 s per-pod spin bound — which the first pod's start handshake must absorb."""
     import socket
     import subprocess
     import sys
+    import torch
     import cpu_ref
     from ksim import synth
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
     world = 2
-    env = dict(os.environ, KSIM_MAX_GRID="64")
+    env = dict(os.environ)
+    if torch.cuda.device_count() < world:  # ranks share a device: their persistent grids must co-reside
+        env["KSIM_MAX_GRID"] = "64"
     worker = os.path.join(os.path.dirname(__file__), "shard_worker.py")
-    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(port), str(tmp_path / ("r%d.npz" % r))],
-                              env=env) for r in range(world)]
+    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(port), str(tmp_path / ("r%d.npz" % r)),
+                               str(skew)], env=env) for r in range(world)]
     rcs = [pr.wait(timeout=100) for pr in procs]
     assert rcs == [0] * world
     res = [np.load(tmp_path / ("r%d.npz" % r)) for r in range(world)]
@@ -580,10 +586,11 @@ def test_node_sharded_stream_form_matches_c_oracle(world, monkeypatch):
 # ----------------------------------------------------------------------------- edge cases
 def test_no_nodes_is_err_no_nodes_available():
     """genericScheduler.Schedule with an empty node list returns ErrNoNodesAvailable
-    (core/generic_scheduler.go:63-64,125): the C-ABI refuses the empty table with that text."""
+    (core/generic_scheduler.go:63-64,125): the empty table loads, scheduling on it returns
+    KSIM_E_NO_NODES with that text."""
     pods = [{"metadata": {"name": "p"}, "spec": {"containers": [{}]}}]
-    with pytest.raises(abi.KsimError) as ei:
-        scheduler.ClusterCapacity([], [], pods)
+    with pytest.raises(abi.NoNodesAvailable) as ei:
+        scheduler.ClusterCapacity([], [], pods).run()
     assert "no nodes available to schedule pods" in str(ei.value)
 
 
