@@ -190,7 +190,7 @@ typedef struct {
   int32_t port_cnt;
   int32_t scalar_off;  /* into the scalar-request array */
   int32_t scalar_cnt;
-  int32_t reserved[5];
+  int32_t reserved[5]; /* library-owned scratch (callers pass anything; never read back) */
 } ksim_pod;
 
 typedef struct {

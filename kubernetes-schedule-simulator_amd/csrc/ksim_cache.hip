@@ -99,6 +99,19 @@ __global__ __launch_bounds__(256) void ksim_port_max_kernel(const int32_t* __res
   if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
 }
 
+// Per queued pod, its reduce-class counts k1 (TaintToleration) / k2 (NodeAffinity) into
+// reserved[0..1] (1 when the priority is not configured), read by the persistent kernel's
+// descriptor ring instead of the class tables.
+__global__ __launch_bounds__(256) void ksim_pod_k_kernel(ksim_pod* pods, int64_t n_pods, const int32_t* __restrict__ n_tt,
+                                                         const int32_t* __restrict__ n_na, int32_t use_tt, int32_t use_na) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n_pods; p += stride) {
+    const int32_t cls = pods[p].cls;
+    pods[p].reserved[0] = use_tt ? n_tt[cls] : 1;
+    pods[p].reserved[1] = use_na ? n_na[cls] : 1;
+  }
+}
+
 static int grid_for(int64_t n) {
   const int64_t g = (n + 255) / 256;
   return (int)(g < 1 ? 1 : (g > 2048 ? 2048 : g));
@@ -131,5 +144,12 @@ extern "C" hipError_t ksim_launch_port_max(const int32_t* port_count, int64_t n,
   hipError_t e = hipMemsetAsync(out, 0, 4, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(ksim_port_max_kernel, dim3(grid_for(n)), dim3(256), 0, s, port_count, n, out);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ksim_launch_pod_k(ksim_pod* pods, int64_t n_pods, const KsimCtx* c, hipStream_t s) {
+  if (n_pods <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ksim_pod_k_kernel, dim3(grid_for(n_pods)), dim3(256), 0, s, pods, n_pods, c->n_tt, c->n_na,
+                     c->w[KSIM_W_TAINT_TOLERATION] != 0 ? 1 : 0, c->w[KSIM_W_NODE_AFFINITY] != 0 ? 1 : 0);
   return hipGetLastError();
 }

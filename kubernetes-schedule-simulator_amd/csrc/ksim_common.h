@@ -63,6 +63,8 @@ struct KsimCtx {
   const int64_t* __restrict__ tt_val;
   const int64_t* __restrict__ na_val;
   int32_t lwords, twords, n_label_sets, n_taint_sets;
+  int32_t n_classes_dev;  // pod classes in the tables
+  int32_t pad1;
   // ---- pod queue ----
   const ksim_pod* __restrict__ pods;
   const uint64_t* __restrict__ pod_ports;
@@ -104,6 +106,13 @@ struct KsimShard {
 // ((a*10)/b) with Go int64 semantics (wrapping multiply, truncating divide), b > 0.
 // Quotients here are 0..10, so for a < 2^49 a correctly rounded double divide plus one
 // integer correction is exact; larger values take the native (slow) 64-bit divide.
+// The emulated 64-bit divide is ~100 instructions: kept out of line so the evaluations that
+// inline ksim_mul10_div stay small (instruction-cache footprint of the persistent kernels).
+__device__ __noinline__ int64_t ksim_mul10_div_slow(int64_t a, int64_t b) {
+  const int64_t x = (int64_t)((uint64_t)a * 10ull);
+  return x / b;
+}
+
 __device__ __forceinline__ int64_t ksim_mul10_div(int64_t a, int64_t b) {
   if (a >= 0 && a < (int64_t(1) << 49) && b > 0) {
     const int64_t x = a * 10;
@@ -112,8 +121,7 @@ __device__ __forceinline__ int64_t ksim_mul10_div(int64_t a, int64_t b) {
     else if ((q + 1) * b <= x) q += 1;
     return q;
   }
-  const int64_t x = (int64_t)((uint64_t)a * 10ull);
-  return x / b;
+  return ksim_mul10_div_slow(a, b);
 }
 
 // least_requested.go:44-53
@@ -204,21 +212,48 @@ __device__ __forceinline__ uint32_t ksim_hostname(const ksim_pod& P, int64_t i) 
   return (P.host == -1 || P.host == i) ? 0u : (1u << KSIM_R_HOSTNAME);
 }
 
-__device__ __forceinline__ uint32_t ksim_hostports(const KsimCtx& c, const ksim_pod& P, int64_t i) {
+// Where a general evaluation reads what is not in the 60-byte row: the node's label / taint
+// set and host ports, the pod class's selector / toleration bits and reduce-class bytes.  This
+// accessor reads the HBM table (launch mode, evaluate); the persistent kernel supplies one that
+// reads its LDS-staged copies (ksim_persistent.hip), so its row waves issue no global loads.
+struct KsimGlobalAcc {
+  const KsimCtx& c;
+  __device__ __forceinline__ bool sel_ok(const ksim_pod& P, int64_t i) const {
+    return ksim_bit(c.sel_ok, P.cls, c.lwords, c.label_set[i]);
+  }
+  __device__ __forceinline__ bool taint_ok(const ksim_pod& P, int64_t i) const {
+    return ksim_bit(c.taint_ok, P.cls, c.twords, c.taint_set[i]);
+  }
+  __device__ __forceinline__ bool noexec_ok(const ksim_pod& P, int64_t i) const {
+    return ksim_bit(c.noexec_ok, P.cls, c.twords, c.taint_set[i]);
+  }
+  __device__ __forceinline__ bool port_conflict(int64_t i, uint64_t want) const { return ksim_port_conflict(c, i, want); }
+  __device__ __forceinline__ int tt_class(const ksim_pod& P, int64_t i) const {
+    return c.tt_class[(int64_t)P.cls * c.n_taint_sets + c.taint_set[i]];
+  }
+  __device__ __forceinline__ int na_class(const ksim_pod& P, int64_t i) const {
+    return c.na_class[(int64_t)P.cls * c.n_label_sets + c.label_set[i]];
+  }
+};
+
+template <class A>
+__device__ __forceinline__ uint32_t ksim_hostports(const KsimCtx& c, const ksim_pod& P, int64_t i, const A& a) {
   for (int32_t k = 0; k < P.port_cnt; ++k)
-    if (ksim_port_conflict(c, i, c.pod_ports[P.port_off + k])) return 1u << KSIM_R_HOST_PORTS;
+    if (a.port_conflict(i, c.pod_ports[P.port_off + k])) return 1u << KSIM_R_HOST_PORTS;
   return 0;
 }
 
-__device__ __forceinline__ uint32_t ksim_selector(const KsimCtx& c, const ksim_pod& P, int64_t i) {
+template <class A>
+__device__ __forceinline__ uint32_t ksim_selector(const ksim_pod& P, int64_t i, const A& a) {
   if (!(P.flags & KSIM_POD_NEED_SELECTOR)) return 0;
-  return ksim_bit(c.sel_ok, P.cls, c.lwords, c.label_set[i]) ? 0u : (1u << KSIM_R_NODE_SELECTOR);
+  return a.sel_ok(P, i) ? 0u : (1u << KSIM_R_NODE_SELECTOR);
 }
 
 // Reason mask of the first failing predicate in predicatesOrdering (predicates.go:129-138,
 // core/generic_scheduler.go:467-528); 0 = fits.
-__device__ __forceinline__ uint32_t ksim_predicates(const KsimCtx& c, const ksim_pod& P, int64_t i,
-                                                    const KsimRow& r) {
+template <class A>
+__device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ksim_pod& P, int64_t i, const KsimRow& r,
+                                                      const A& a) {
   const uint32_t pr = c.preds;
   uint32_t m;
   if (pr & KSIM_P_CHECK_NODE_CONDITION) {
@@ -228,8 +263,8 @@ __device__ __forceinline__ uint32_t ksim_predicates(const KsimCtx& c, const ksim
   if ((pr & KSIM_P_CHECK_NODE_UNSCHEDULABLE) && (r.fl & KSIM_N_UNSCHEDULABLE)) return 1u << KSIM_R_UNSCHEDULABLE;
   if (pr & KSIM_P_GENERAL) {
     m = ksim_resources(c, P, i, r) | ksim_hostname(P, i);
-    if (P.port_cnt) m |= ksim_hostports(c, P, i);
-    m |= ksim_selector(c, P, i);
+    if (P.port_cnt) m |= ksim_hostports(c, P, i, a);
+    m |= ksim_selector(P, i, a);
     if (m) return m;
   }
   if (pr & KSIM_P_HOSTNAME) {
@@ -237,11 +272,11 @@ __device__ __forceinline__ uint32_t ksim_predicates(const KsimCtx& c, const ksim
     if (m) return m;
   }
   if ((pr & KSIM_P_HOST_PORTS) && P.port_cnt) {
-    m = ksim_hostports(c, P, i);
+    m = ksim_hostports(c, P, i, a);
     if (m) return m;
   }
   if (pr & KSIM_P_NODE_SELECTOR) {
-    m = ksim_selector(c, P, i);
+    m = ksim_selector(P, i, a);
     if (m) return m;
   }
   if (pr & KSIM_P_RESOURCES) {
@@ -249,15 +284,19 @@ __device__ __forceinline__ uint32_t ksim_predicates(const KsimCtx& c, const ksim
     if (m) return m;
   }
   if ((pr & KSIM_P_TAINTS) && (P.flags & KSIM_POD_NEED_TAINTS)) {
-    if (!ksim_bit(c.taint_ok, P.cls, c.twords, c.taint_set[i])) return 1u << KSIM_R_TAINTS;
+    if (!a.taint_ok(P, i)) return 1u << KSIM_R_TAINTS;
   }
   if ((pr & KSIM_P_NOEXEC_TAINTS) && (P.flags & KSIM_POD_NEED_TAINTS)) {
-    if (!ksim_bit(c.noexec_ok, P.cls, c.twords, c.taint_set[i])) return 1u << KSIM_R_TAINTS;
+    if (!a.noexec_ok(P, i)) return 1u << KSIM_R_TAINTS;
   }
   if ((pr & KSIM_P_MEM_PRESSURE) && (P.flags & KSIM_POD_BEST_EFFORT) && (r.fl & KSIM_N_MEM_PRESSURE))
     return 1u << KSIM_R_MEM_PRESSURE;
   if ((pr & KSIM_P_DISK_PRESSURE) && (r.fl & KSIM_N_DISK_PRESSURE)) return 1u << KSIM_R_DISK_PRESSURE;
   return 0;
+}
+
+__device__ __forceinline__ uint32_t ksim_predicates(const KsimCtx& c, const ksim_pod& P, int64_t i, const KsimRow& r) {
+  return ksim_predicates_a(c, P, i, r, KsimGlobalAcc{c});
 }
 
 // Weighted sum of the map-type priorities (core/generic_scheduler.go:632-639); the reduce
@@ -276,17 +315,32 @@ __device__ __forceinline__ int64_t ksim_map_score(const KsimCtx& c, const ksim_p
   return (int64_t)s;
 }
 
-__device__ __forceinline__ int ksim_rclass(const KsimCtx& c, const ksim_pod& P, int64_t i, int k1, int k2) {
+template <class A>
+__device__ __forceinline__ int ksim_rclass_a(const ksim_pod& P, int64_t i, int k1, int k2, const A& acc) {
   int a = 0, b = 0;
-  if (k1 > 1) a = c.tt_class[(int64_t)P.cls * c.n_taint_sets + c.taint_set[i]];
-  if (k2 > 1) b = c.na_class[(int64_t)P.cls * c.n_label_sets + c.label_set[i]];
+  if (k1 > 1) a = acc.tt_class(P, i);
+  if (k2 > 1) b = acc.na_class(P, i);
   return a * k2 + b;
+}
+
+__device__ __forceinline__ int ksim_rclass(const KsimCtx& c, const ksim_pod& P, int64_t i, int k1, int k2) {
+  return ksim_rclass_a(P, i, k1, k2, KsimGlobalAcc{c});
 }
 
 // NormalizeReduce (priorities/reduce.go:29-64) applied to one class value.
 __device__ __forceinline__ int64_t ksim_norm(int64_t v, int64_t mx, bool reverse) {
   if (mx == 0) return reverse ? 10 : v;
-  int64_t s = (int64_t)((uint64_t)10 * (uint64_t)v) / mx;
+  int64_t s;
+  if (v >= 0 && v < (int64_t(1) << 40) && mx > 0 && mx < (int64_t(1) << 40)) {
+    // map values are small: a correctly rounded float64 quotient plus one integer correction
+    // is Go's truncating int64 division (ksim_mul10_div), without the emulated 64-bit divide
+    const int64_t x = 10 * v;
+    s = (int64_t)((double)x / (double)mx);
+    if (s * mx > x) s -= 1;
+    else if ((s + 1) * mx <= x) s += 1;
+  } else {
+    s = ksim_mul10_div_slow(v, mx);
+  }
   return reverse ? 10 - s : s;
 }
 

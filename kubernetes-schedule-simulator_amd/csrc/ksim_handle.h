@@ -53,6 +53,7 @@ extern "C" hipError_t ksim_launch_set_row(const KsimCtx* c, int64_t node, const 
                                           hipStream_t s);
 extern "C" hipError_t ksim_launch_release(const KsimCtx* c, int64_t pod, int64_t node, hipStream_t s);
 extern "C" hipError_t ksim_launch_remap_hosts(ksim_pod* pods, int64_t n_pods, int64_t idx, int32_t op, hipStream_t s);
+extern "C" hipError_t ksim_launch_pod_k(ksim_pod* pods, int64_t n_pods, const KsimCtx* c, hipStream_t s);
 extern "C" hipError_t ksim_launch_port_max(const int32_t* port_count, int64_t n, int32_t* out, hipStream_t s);
 
 struct DevBuf {

@@ -41,6 +41,7 @@ constexpr int RING_FILL = 8;                         // descriptors fetched per 
 constexpr uint64_t SPIN_LIMIT_TICKS = 200000000ull;  // s_memrealtime ticks at 100 MHz = 2 s
 constexpr int NSLOT = 4;                             // granule slots (pod mod NSLOT)
 constexpr int MAXG = 64 * MAXB;                      // workgroups a slot is sized for
+constexpr int KF = 4;                                // reduce classes polled per round trip
 
 typedef __attribute__((address_space(1))) uint64_t gu64;
 
@@ -105,9 +106,11 @@ struct Rows {  // LDS image of the owned rows (SoA)
   int32_t *allowed, *count;
   uint32_t* fl;
   int32_t* ev;  // [2][rows] per pod parity: packed evaluation of the row (ev_pack)
+  int32_t *ls, *ts;  // label-set / taint-set id of the row
 };
 
-constexpr int LDS_ROW_BYTES = 8 * 8 + 3 * 4 + 4 + 2 * 4;  // 88 with padding
+// 6 x i64 + 2 x f64 + 3 x i32 + 2 x i32 evaluations + 2 x i32 set ids, padded
+constexpr int LDS_ROW_BYTES = 8 * 8 + 3 * 4 + 2 * 4 + 2 * 4 + 4;  // 96
 
 extern __shared__ __attribute__((aligned(16))) char ksim_smem[];  // dynamic LDS: the row image
 
@@ -121,12 +124,77 @@ __device__ __forceinline__ Rows carve(char* smem, int rows) {
   r.allowed = q; r.count = q + rows;
   r.fl = reinterpret_cast<uint32_t*>(q + 2 * rows);
   r.ev = q + 3 * rows;
+  r.ls = q + 5 * rows;
+  r.ts = q + 6 * rows;
   return r;
 }
 
+}  // namespace
+
+// Dynamic-LDS plan of a workgroup beyond the rows (host-computed in ksim_launch_persistent):
+// the rows' host ports and the pod-class tables are staged too when they fit, so the row waves
+// — the CU that polls the exchange — issue no global loads while evaluating (a loaded consumer
+// CU pays 2.5-2.9 us per hand-off instead of 1.1, MI355X_MICROARCH.md handoff-1to1).
+struct PLayout {
+  int32_t ps;          // port slots staged per row (0: ports read from HBM)
+  int32_t tables;      // 1: sel_ok / taint_ok / noexec_ok / tt_class / na_class staged
+  int32_t off_pc, off_pk, off_sel, off_tok, off_nok, off_ttc, off_nac;  // byte offsets in ksim_smem
+  int32_t off_ttv, off_nav;  // [C][KSIM_MAX_RCLASS] reduce-class map values (int64)
+};
+
+namespace {
+
+// The general evaluation's reads beyond the row, from LDS (KsimGlobalAcc's LDS twin).
+struct LdsAcc {
+  const KsimCtx& c;
+  const PLayout& L;
+  int64_t lo;
+  int rows;
+  const int32_t* ls;
+  const int32_t* ts;
+  __device__ __forceinline__ const uint32_t* sel() const {
+    return L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_sel) : c.sel_ok;
+  }
+  __device__ __forceinline__ bool sel_ok(const ksim_pod& P, int64_t i) const {
+    return ksim_bit(sel(), P.cls, c.lwords, ls[i - lo]);
+  }
+  __device__ __forceinline__ bool taint_ok(const ksim_pod& P, int64_t i) const {
+    const uint32_t* t = L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_tok) : c.taint_ok;
+    return ksim_bit(t, P.cls, c.twords, ts[i - lo]);
+  }
+  __device__ __forceinline__ bool noexec_ok(const ksim_pod& P, int64_t i) const {
+    const uint32_t* t = L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_nok) : c.noexec_ok;
+    return ksim_bit(t, P.cls, c.twords, ts[i - lo]);
+  }
+  __device__ __forceinline__ bool port_conflict(int64_t i, uint64_t want) const {
+    if (!L.ps) return ksim_port_conflict(c, i, want);
+    const int j = (int)(i - lo);
+    const int32_t cnt = reinterpret_cast<const int32_t*>(ksim_smem + L.off_pc)[j];
+    const uint64_t* pk = reinterpret_cast<const uint64_t*>(ksim_smem + L.off_pk);
+    const uint32_t wip = (uint32_t)(want >> 40);
+    const uint64_t wpp = want & 0xFFFFFFFFFFull;  // HostPortInfo.CheckConflict (utils.go:101-130)
+    for (int32_t s = 0; s < cnt; ++s) {
+      const uint64_t e = pk[s * rows + j];
+      if ((e & 0xFFFFFFFFFFull) != wpp) continue;
+      const uint32_t eip = (uint32_t)(e >> 40);
+      if (wip == 0 || eip == 0 || eip == wip) return true;
+    }
+    return false;
+  }
+  __device__ __forceinline__ int tt_class(const ksim_pod& P, int64_t i) const {
+    const uint8_t* t = L.tables ? reinterpret_cast<const uint8_t*>(ksim_smem + L.off_ttc) : c.tt_class;
+    return t[(int64_t)P.cls * c.n_taint_sets + ts[i - lo]];
+  }
+  __device__ __forceinline__ int na_class(const ksim_pod& P, int64_t i) const {
+    const uint8_t* t = L.tables ? reinterpret_cast<const uint8_t*>(ksim_smem + L.off_nac) : c.na_class;
+    return t[(int64_t)P.cls * c.n_label_sets + ls[i - lo]];
+  }
+};
+
 // Commit of the columns that stay in HBM (gpu, ephemeral, scalars, ports) and of the
 // over-commit bits (node_info.go:318-341, utils.go:45-60).  Single thread of the owner.
-__device__ __noinline__ uint32_t commit_side(const KsimCtx* __restrict__ cg, const ksim_pod* Pp, int64_t w, uint32_t fl) {
+__device__ __noinline__ uint32_t commit_side(const KsimCtx* __restrict__ cg, const ksim_pod* Pp, int64_t w, uint32_t fl,
+                                             int32_t ports) {
   const KsimCtx& c = *cg;
   const ksim_pod& P = *Pp;
   const int64_t g = c.req_gpu[w] + P.add_gpu;
@@ -140,7 +208,7 @@ __device__ __noinline__ uint32_t commit_side(const KsimCtx* __restrict__ cg, con
     const ksim_scalar_req q = c.pod_scalars[P.scalar_off + s];
     c.req_scalar[(int64_t)q.col * c.n + w] += q.add;
   }
-  for (int32_t k = 0; k < P.port_cnt; ++k) {
+  for (int32_t k = 0; ports && k < P.port_cnt; ++k) {
     const uint64_t key = c.pod_ports[P.port_off + k];
     const int32_t cnt = c.port_count[w];
     bool dup = false;
@@ -154,6 +222,30 @@ __device__ __noinline__ uint32_t commit_side(const KsimCtx* __restrict__ cg, con
   return fl;
 }
 
+// HostPortInfo.Add of the pod's ports on row j when the rows' ports are staged in LDS: the set
+// is read from LDS, new keys written to LDS and HBM (stores only, nothing waits on HBM).
+__device__ __noinline__ void commit_ports_lds(const KsimCtx* __restrict__ cg, const ksim_pod* Pp, int64_t w, int32_t j,
+                                              int32_t rows, int32_t off_pc, int32_t off_pk) {
+  const KsimCtx& c = *cg;
+  const ksim_pod& P = *Pp;
+  int32_t* pc = reinterpret_cast<int32_t*>(ksim_smem + off_pc);
+  uint64_t* pk = reinterpret_cast<uint64_t*>(ksim_smem + off_pk);
+  int32_t cnt = pc[j];
+  for (int32_t k = 0; k < P.port_cnt; ++k) {
+    const uint64_t key = c.pod_ports[P.port_off + k];
+    bool dup = false;
+    for (int32_t s = 0; s < cnt; ++s)
+      if (pk[s * rows + j] == key) { dup = true; break; }
+    if (dup) continue;
+    if (cnt >= c.port_slots) { atomicOr(c.err, 1); continue; }
+    pk[cnt * rows + j] = key;
+    c.ports[(int64_t)cnt * c.n + w] = key;
+    cnt += 1;
+  }
+  pc[j] = cnt;
+  c.port_count[w] = cnt;
+}
+
 // Total score of reduce class q once the per-class maxima over the filtered set are known
 // (NormalizeReduce, priorities/reduce.go:29-64; weighted sum generic_scheduler.go:632-639).
 // tv / av: the class's TaintToleration / NodeAffinity map values (prefetched per pod).
@@ -165,14 +257,27 @@ __device__ __forceinline__ int64_t class_total(const KsimCtx& c, int64_t tv, int
   return (int64_t)t;
 }
 
+// wave-wide maximum of a 64-bit value: the DPP int32 reduction when every lane's value fits
+// (the common case: counts, weights, scores), else a shuffle tree (ds_bpermute, ~10x slower)
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
+  if (__all(v >= INT32_MIN && v <= INT32_MAX)) return ksimw::max_i32((int32_t)v);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t t = __shfl_xor(v, o, 64);
+    v = t > v ? t : v;
+  }
+  return v;
+}
+
 // 64-bit value of lane q (wave-uniform q)
 __device__ __forceinline__ int64_t readlane64(int64_t v, int q) {
   return (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)((uint64_t)v >> 32), q) << 32) |
                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)v, q));
 }
 
-// General per-row evaluation (any supported pod).  Reads the context through a pointer to
-// its device-memory copy, so no kernel-argument copy goes to scratch.
+// General per-row evaluation (any supported pod), everything it reads in LDS (LdsAcc) except
+// the gpu / ephemeral / scalar columns of pods requesting them.  Reads the context through a
+// pointer to its device-memory copy, so no kernel-argument copy goes to scratch.
 struct RowEval {
   int32_t sc;
   uint32_t rm;
@@ -180,20 +285,32 @@ struct RowEval {
   int32_t fit;
 };
 
-__device__ __noinline__ RowEval eval_row_general(const KsimCtx* __restrict__ cg, int chunk, const ksim_pod* Pp, int k1,
-                                                 int k2, int64_t i, int64_t j) {
-  const KsimCtx& c = *cg;
-  const ksim_pod& P = *Pp;
+typedef __attribute__((address_space(3))) const KsimCtx lds_ctx;
+typedef __attribute__((address_space(3))) const PLayout lds_layout;
+typedef __attribute__((address_space(3))) const ksim_pod lds_pod;
+
+// One out-of-line copy shared by the row waves, the owner's pre-evaluation and its fix-up: its
+// context, layout and pod are LDS copies, so nothing it reads for a plain pod leaves the CU.
+__device__ __noinline__ RowEval eval_row_general(lds_ctx* cl, lds_layout* Ll, lds_pod* Pl, int chunk, int64_t i,
+                                                 int64_t j) {
+  const KsimCtx& c = *(const KsimCtx*)cl;
+  const PLayout& Lp = *(const PLayout*)Ll;
+  const ksim_pod& P = *(const ksim_pod*)Pl;
+  const int k1 = P.reserved[0], k2 = P.reserved[1];
   const Rows R = carve(ksim_smem, chunk);
+  const LdsAcc acc{c, Lp, i - j, chunk, R.ls, R.ts};
   KsimRow r;
   r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j]; r.rm = R.rm[j]; r.zc = R.zc[j]; r.zm = R.zm[j];
   r.allowed = R.allowed[j]; r.count = R.count[j]; r.fl = R.fl[j];
-  const uint32_t m = ksim_predicates(c, P, i, r);
+  const uint32_t m = ksim_predicates_a(c, P, i, r, acc);
   RowEval e;
   e.fit = (m == 0);
   e.rm = m;
-  e.sc = (int32_t)ksim_map_score(c, P, r);
-  e.cl = (k1 * k2 > 1) ? ksim_rclass(c, P, i, k1, k2) : 0;
+  // ksim_map_score through ksim_fast.h's float64 form (bit-identical; out-of-line beyond 2^49)
+  e.sc = c.no_prio ? 0
+                   : (int32_t)ksim_fast_score(P.nz_cpu + r.zc, r.ac, R.dac[j], P.nz_mem + r.zm, r.am, R.dam[j],
+                                              c.w[KSIM_W_LEAST_REQUESTED], c.w[KSIM_W_MOST_REQUESTED], c.w[KSIM_W_BALANCED]);
+  e.cl = (k1 * k2 > 1) ? ksim_rclass_a(P, i, k1, k2, acc) : 0;
   return e;
 }
 
@@ -201,7 +318,7 @@ __device__ __noinline__ RowEval eval_row_general(const KsimCtx* __restrict__ cg,
 
 template <int BS, int NPT>
 __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const KsimCtx* __restrict__ cg,
-                                                             uint64_t* granules) {
+                                                             uint64_t* granules, PLayout L) {
   constexpr int NW = BS / 64;
   constexpr int RT = BS - 64;  // row threads
   __shared__ int32_t s_mx[2][NW][KSIM_MAX_RCLASS];   // per row wave, double-buffered by pod parity
@@ -217,6 +334,8 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   __shared__ int32_t s_mode;
   __shared__ int32_t s_arr;  // row-wave arrivals (the last one of a pod publishes)
   __shared__ __attribute__((aligned(16))) ksim_pod s_pod[RING];
+  __shared__ PLayout s_L;
+  __shared__ KsimCtx s_ctx;  // the evaluation's copy of the context (LDS reads, no K$ misses)
 #ifdef KSIM_STAMPS
   uint64_t st_acc[16] = {};
 #endif
@@ -242,8 +361,32 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     R.rc[j] = c.req_cpu[i]; R.rm[j] = c.req_mem[i];
     R.zc[j] = c.nz_cpu[i]; R.zm[j] = c.nz_mem[i];
     R.allowed[j] = c.allowed_pods[i]; R.count[j] = c.pod_count[i]; R.fl[j] = c.flags[i];
+    R.ls[j] = c.label_set[i]; R.ts[j] = c.taint_set[i];
+    if (L.ps) {  // the rows' host ports (HostPortInfo), slot-major like the HBM column
+      reinterpret_cast<int32_t*>(ksim_smem + L.off_pc)[j] = c.port_count[i];
+      for (int32_t q = 0; q < L.ps; ++q)
+        reinterpret_cast<uint64_t*>(ksim_smem + L.off_pk)[q * chunk + j] = c.ports[(int64_t)q * c.n + i];
+    }
   }
+  if (L.tables) {  // the pod-class tables (selector / toleration bits, reduce-class bytes)
+    const int32_t C = c.n_classes_dev;
+    for (int32_t k = tid; k < C * c.lwords; k += BS) reinterpret_cast<uint32_t*>(ksim_smem + L.off_sel)[k] = c.sel_ok[k];
+    for (int32_t k = tid; k < C * c.twords; k += BS) {
+      reinterpret_cast<uint32_t*>(ksim_smem + L.off_tok)[k] = c.taint_ok[k];
+      reinterpret_cast<uint32_t*>(ksim_smem + L.off_nok)[k] = c.noexec_ok[k];
+    }
+    for (int32_t k = tid; k < C * c.n_taint_sets; k += BS) (ksim_smem + L.off_ttc)[k] = (char)c.tt_class[k];
+    for (int32_t k = tid; k < C * c.n_label_sets; k += BS) (ksim_smem + L.off_nac)[k] = (char)c.na_class[k];
+    for (int32_t k = tid; k < C * KSIM_MAX_RCLASS; k += BS) {
+      reinterpret_cast<int64_t*>(ksim_smem + L.off_ttv)[k] = c.tt_val[k];
+      reinterpret_cast<int64_t*>(ksim_smem + L.off_nav)[k] = c.na_val[k];
+    }
+  }
+  if (tid == 0) { s_L = L; s_ctx = c; }
   // pod ring: RING_FILL descriptors (1 KiB) per refill, one 16-byte load per lane of wave 1
+  // pod ring: RING_FILL descriptors (1 KiB) per refill, one 16-byte load per lane of wave 1.
+  // The reduce-class counts k1 (TaintToleration) / k2 (NodeAffinity) ride in each queued
+  // descriptor's reserved[0..1] (written by the library, ksim_launch_pod_k).
   auto ring_load = [&](int64_t p0, uint4& v) {
     const int64_t p = p0 + lane / 8;
     if (p < c.end) v = reinterpret_cast<const uint4*>(&c.pods[p])[lane % 8];
@@ -261,11 +404,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex (control wave)
   __syncthreads();
 
-  auto pod_K = [&](const ksim_pod& P) -> int {
-    const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
-    const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
-    return k1 * k2;
-  };
+  auto pod_K = [&](const ksim_pod& P) -> int { return P.reserved[0] * P.reserved[1]; };
   // one row against pod P → packed entry + reason mask (fast path when the pod qualifies)
   auto load_row = [&](int32_t j) -> KsimFastRow {
     KsimFastRow r;
@@ -279,9 +418,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       const KsimFastPod F{P.req_cpu, P.req_mem, P.nz_cpu, P.nz_mem, P.flags};
       return ksim_fast_eval(preds, F, load_row(j), no_prio, wl, wmr, wb, rm);
     }
-    const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
-    const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
-    const RowEval e = eval_row_general(cg, (int)chunk, &P, k1, k2, lo + j, j);
+    const RowEval e = eval_row_general((lds_ctx*)&s_ctx, (lds_layout*)&s_L, (lds_pod*)&P, (int)chunk, lo + j, j);
     rm = e.rm;
     return ev_pack(e.fit != 0, e.cl, e.sc);
   };
@@ -401,12 +538,14 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     if (wv == 0) {
       const ksim_pod& P = s_pod[pod % RING];
       const int K = pod_K(P);
-      const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
+      const int k2 = P.reserved[1];
       // the reduce classes' map values (lane q = class q), loaded now, used after the sweep
       int64_t tv_l = 0, av_l = 0;
       if (K > 1 && lane < K) {
-        tv_l = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + lane / k2];
-        av_l = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + lane % k2];
+        const int64_t* ttv = L.tables ? reinterpret_cast<const int64_t*>(ksim_smem + L.off_ttv) : c.tt_val;
+        const int64_t* nav = L.tables ? reinterpret_cast<const int64_t*>(ksim_smem + L.off_nav) : c.na_val;
+        tv_l = ttv[(int64_t)P.cls * KSIM_MAX_RCLASS + lane / k2];
+        av_l = nav[(int64_t)P.cls * KSIM_MAX_RCLASS + lane % k2];
       }
       // ---------------- a. sweep: every speculative partial of pod + the owner's correction ----
       const uint64_t tag = ptag(pod);
@@ -419,7 +558,8 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       bool seen_spec = false, seen_fix = false;
 #endif
       for (;;) {
-        // unconditional loads (slots are sized for MAXG workgroups): one fabric round trip
+        // unconditional loads (slots are sized for MAXG workgroups): one fabric round trip for
+        // class 0, the owner's correction and (KF at a time) the further reduce classes
 #pragma unroll
         for (int j = 0; j < MAXB; ++j) g[j] = load_granule(spec_at(granules, slot, lane * MAXB + j, 0));
         const uint64_t fx = load_granule(fix_at(granules, slot, 0));
@@ -428,6 +568,26 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         for (int j = 0; j < MAXB; ++j) {
           const int b = lane * MAXB + j;
           mine &= (b >= G) || b == X || gtag(g[j]) == tag;
+        }
+        for (int q0 = 1; q0 < K; q0 += KF) {  // classes >= 1 were published with class 0
+          uint64_t v[KF][MAXB];
+#pragma unroll
+          for (int u = 0; u < KF; ++u)
+#pragma unroll
+            for (int j = 0; j < MAXB; ++j) {
+              const int b = lane * MAXB + j;
+              v[u][j] = (q0 + u < K && b < G) ? load_granule(gran_at(granules, slot, b, q0 + u, X)) : 0;
+            }
+#pragma unroll
+          for (int u = 0; u < KF; ++u)
+#pragma unroll
+            for (int j = 0; j < MAXB; ++j) {
+              const int b = lane * MAXB + j;
+              if (q0 + u < K && b < G) {
+                mine &= gtag(v[u][j]) == tag;
+                s_gq[q0 + u - 1][b] = v[u][j];
+              }
+            }
         }
 #ifdef KSIM_STAMPS
         st_acc[8] += 1;
@@ -469,30 +629,16 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         C0 = ksimw::sum_i32((n && m == M0) ? n : 0);
       }
       STAMP(9);
-      if (ok && K > 1) {  // further reduce classes (TaintToleration x NodeAffinity)
+      if (ok && K > 1) {  // further reduce classes (TaintToleration x NodeAffinity), swept above
         if (lane == 0) { s_M[0] = M0; s_C[0] = C0; }
         for (int q = 1; q < K; ++q) {
-          // all of this class's granules in one round trip (published with class 0, so
-          // normally already visible), kept in LDS for the locate step
-          uint64_t v[MAXB];
-          const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-          for (;;) {
-            bool mine = true;
-#pragma unroll
-            for (int j = 0; j < MAXB; ++j) {
-              const int b = lane * MAXB + j;
-              v[j] = b < G ? load_granule(gran_at(granules, slot, b, q, X)) : 0;
-              mine &= b >= G || gtag(v[j]) == tag;
-            }
-            if (__all(mine)) break;
-            if (__builtin_amdgcn_s_memrealtime() - t1 > SPIN_LIMIT_TICKS) { ok = false; break; }
-            __builtin_amdgcn_s_sleep(1);
-          }
           int32_t mm = -1, nn = 0;
 #pragma unroll
           for (int j = 0; j < MAXB; ++j) {
-            s_gq[q - 1][lane * MAXB + j] = v[j];
-            const int32_t cnt = gcnt(v[j]), s = gscore(v[j]);
+            const int b = lane * MAXB + j;
+            if (b >= G) continue;
+            const uint64_t v = s_gq[q - 1][b];
+            const int32_t cnt = gcnt(v), s = gscore(v);
             if (cnt == 0) continue;
             if (s > mm) { mm = s; nn = cnt; }
             else if (s == mm) nn += cnt;
@@ -501,8 +647,8 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
           const int32_t Cq = ksimw::sum_i32((nn && mm == Mq) ? nn : 0);
           if (lane == 0) { s_M[q] = Mq; s_C[q] = Cq; }
         }
-        ok = __all(ok);
       }
+      STAMP(11);
       int mode = 0, blk = -1, rank = 0;
       uint32_t win = 1;
       if (!ok) {
@@ -515,26 +661,18 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
           mode = 2;
           int64_t C = C0;
           if (K > 1) {
-            int64_t mxT = 0, mxA = 0;
-            for (int q = 0; q < K; ++q) {
-              if (s_C[q] == 0) continue;
-              const int64_t tv = readlane64(tv_l, q), av = readlane64(av_l, q);
-              mxT = tv > mxT ? tv : mxT;
-              mxA = av > mxA ? av : mxA;
-            }
-            int64_t best = INT64_MIN;
-            for (int q = 0; q < K; ++q)
-              if (s_C[q]) {
-                const int64_t t = class_total(c, readlane64(tv_l, q), readlane64(av_l, q), s_M[q], mxT, mxA);
-                best = t > best ? t : best;
-              }
-            win = 0;
-            C = 0;
-            for (int q = 0; q < K; ++q)
-              if (s_C[q] && class_total(c, readlane64(tv_l, q), readlane64(av_l, q), s_M[q], mxT, mxA) == best) {
-                win |= 1u << q;
-                C += s_C[q];
-              }
+            // lane q = reduce class q, all at once: NormalizeReduce's maxima over the filtered
+            // set (classes with fit nodes), each class's weighted total, the best total and the
+            // classes that reach it (reduce.go:29-64, generic_scheduler.go:632-639)
+            const bool live = lane < K && s_C[lane < K ? lane : 0] != 0;
+            const int32_t cq = live ? s_C[lane] : 0;
+            const int64_t mq = live ? s_M[lane] : 0;
+            const int64_t mxT = wave_max_i64(live ? tv_l : 0), mxA = wave_max_i64(live ? av_l : 0);
+            const int64_t t = live ? class_total(c, tv_l, av_l, mq, mxT, mxA) : -1;  // totals are >= 0
+            const int64_t best = wave_max_i64(t);
+            const uint64_t wb = __ballot(live && t == best);
+            win = (uint32_t)wb;
+            C = ksimw::sum_i32((wb >> lane) & 1ull ? cq : 0);
           }
           ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)C) : (int64_t)((uint32_t)counter % (uint32_t)C);
           counter += 1;  // generic_scheduler.go:192-195
@@ -658,15 +796,30 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
           const bool side = (P.add_gpu | P.add_eph | P.scalar_cnt | P.port_cnt) != 0;
           if (lane == 0) {
             R.rc[jsel] = r.rc; R.rm[jsel] = r.rm; R.zc[jsel] = r.zc; R.zm[jsel] = r.zm; R.count[jsel] = r.count;
-            if (side) R.fl[jsel] = commit_side(cg, &P, lo + jsel, r.fl);
+            if (side) {
+              const bool lds_ports = P.port_cnt && L.ps;
+              if (P.add_gpu | P.add_eph | P.scalar_cnt | (P.port_cnt && !L.ps)) {
+                r.fl = commit_side(cg, &P, lo + jsel, r.fl, lds_ports ? 0 : 1);
+                R.fl[jsel] = r.fl;
+              }
+              if (lds_ports) commit_ports_lds(cg, &P, lo + jsel, jsel, (int32_t)chunk, L.off_pc, L.off_pk);
+            }
             c.out_node[pod] = (int32_t)(lo + jsel);
           }
           OSTAMP(23);
-          if (has_next && !side) {  // pod + 1 against the committed row, before the barrier
+          if (has_next) {  // pod + 1 against the committed row, before the barrier
             const ksim_pod& Q = s_pod[(pod + 1) % RING];
-            if (ksim_is_fast_pod(Q, pod_K(Q))) {
+            const int Kq = pod_K(Q);
+            if (ksim_is_fast_pod(Q, Kq) && !side) {
               const KsimFastPod F{Q.req_cpu, Q.req_mem, Q.nz_cpu, Q.nz_mem, Q.flags};
               ej_pre = ksim_fast_eval(preds, F, r, no_prio, wl, wmr, wb, rm_pre);
+              have_pre = true;
+            } else if (!ksim_is_fast_pod(Q, Kq)) {
+              // general pod: everything it reads is in LDS; lane 0's commit stores first
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+              ej_pre = eval_one(Q, false, jsel, rm_pre);
               have_pre = true;
             }
           }
@@ -691,7 +844,15 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         int32_t e[NPT];
         const int Kn = pod_K(s_pod[(pod + 1) % RING]);
         eval_rows(pod + 1, e, B_rm, R.ev + nb * chunk);
+#ifdef KSIM_STAMPS
+        const uint64_t te1 = __builtin_amdgcn_s_memtime();
+        if (tid == 64) st_acc[14] += te1 - te0;
+#endif
         partial(e, Kn, nb, wv);
+#ifdef KSIM_STAMPS
+        const uint64_t te2 = __builtin_amdgcn_s_memtime();
+        if (tid == 64) st_acc[15] += te2 - te1;
+#endif
         arrive_publish(pod + 1, Kn, nb);
       }
 #ifdef KSIM_STAMPS
@@ -773,7 +934,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
 #ifdef KSIM_STAMPS
   if (blockIdx.x == 0 && tid == 0)
     for (int k = 0; k < 16; ++k) c.dbg[k] += (k == 5) ? 0 : st_acc[k];
-  if (blockIdx.x == 0 && tid == 64) c.dbg[5] += st_acc[5];
+  if (blockIdx.x == 0 && tid == 64) { c.dbg[5] += st_acc[5]; c.dbg[24] += st_acc[14]; c.dbg[25] += st_acc[15]; }
 #endif
 }
 
@@ -815,17 +976,54 @@ extern "C" size_t ksim_persistent_granule_bytes(int) {
   return (size_t)(NSLOT * MAXG * GR + NSLOT * GR) * sizeof(uint64_t);
 }
 
+// Static LDS of the kernel instance (granule stash, rings, partials), for the dynamic budget.
+template <int BS, int NPT>
+static size_t static_lds() {
+  hipFuncAttributes fa;
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&ksim_persistent_kernel<BS, NPT>)) != hipSuccess) return 48 * 1024;
+  return fa.sharedSizeBytes;
+}
+
+template <int BS, int NPT>
+static hipError_t launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid, int lds_rows,
+                                    hipStream_t s) {
+  const size_t lds_max = 160 * 1024 - static_lds<BS, NPT>();
+  auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
+  size_t off = al((size_t)lds_rows * LDS_ROW_BYTES);
+  if (off > lds_max) return hipErrorInvalidValue;  // ksim_persistent_config keeps rows within budget
+  PLayout L{};
+  // the rows' host ports, when the node table has any and they fit
+  const size_t pbytes = al((size_t)lds_rows * 4) + al((size_t)lds_rows * 8 * c->port_slots);
+  if (c->port_slots > 0 && off + pbytes <= lds_max) {
+    L.ps = c->port_slots;
+    L.off_pc = (int32_t)off;
+    L.off_pk = (int32_t)(off + al((size_t)lds_rows * 4));
+    off += pbytes;
+  }
+  // the pod-class tables, when they fit
+  const size_t C = (size_t)c->n_classes_dev;
+  const size_t tb = al(C * c->lwords * 4) + 2 * al(C * c->twords * 4) + al(C * c->n_taint_sets) + al(C * c->n_label_sets) +
+                    2 * al(C * KSIM_MAX_RCLASS * 8);
+  if (C > 0 && off + tb <= lds_max) {
+    L.tables = 1;
+    L.off_sel = (int32_t)off; off += al(C * c->lwords * 4);
+    L.off_tok = (int32_t)off; off += al(C * c->twords * 4);
+    L.off_nok = (int32_t)off; off += al(C * c->twords * 4);
+    L.off_ttc = (int32_t)off; off += al(C * c->n_taint_sets);
+    L.off_nac = (int32_t)off; off += al(C * c->n_label_sets);
+    L.off_ttv = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
+    L.off_nav = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
+  }
+  hipLaunchKernelGGL((ksim_persistent_kernel<BS, NPT>), dim3(grid), dim3(BS), off, s, *c, cdev, granules, L);
+  return hipGetLastError();
+}
+
 extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
                                              int lds_rows, hipStream_t s) {
-  const size_t lds = (size_t)lds_rows * LDS_ROW_BYTES;
-#define KSIM_PL(BS, NPT) \
-  hipLaunchKernelGGL((ksim_persistent_kernel<BS, NPT>), dim3(grid), dim3(BS), lds, s, *c, cdev, granules)
-  if (lds_rows <= 448) KSIM_PL(512, 1);
-  else if (lds_rows <= 896) KSIM_PL(512, 2);
-  else if (lds_rows <= 1792) KSIM_PL(512, 4);
-  else KSIM_PL(512, 8);
-#undef KSIM_PL
-  return hipGetLastError();
+  if (lds_rows <= 448) return launch_persistent<512, 1>(c, cdev, granules, grid, lds_rows, s);
+  if (lds_rows <= 896) return launch_persistent<512, 2>(c, cdev, granules, grid, lds_rows, s);
+  if (lds_rows <= 1792) return launch_persistent<512, 4>(c, cdev, granules, grid, lds_rows, s);
+  return launch_persistent<512, 8>(c, cdev, granules, grid, lds_rows, s);
 }
 
 extern "C" int ksim_selftest(void) {

@@ -199,6 +199,7 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
   c.n_tt = ntt; c.n_na = nna; c.tt_val = tv; c.na_val = nv;
   c.lwords = (int32_t)lw; c.twords = (int32_t)tw;
   c.n_label_sets = (int32_t)L; c.n_taint_sets = (int32_t)T;
+  c.n_classes_dev = t->n_classes;
   h->n_classes = t->n_classes;
   h->n_label_sets = t->n_label_sets;
   h->n_taint_sets = t->n_taint_sets;
@@ -208,6 +209,11 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
   if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
   if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
   if (h->have_classes) ksim_rt_recompute_fast(h);  // reduce-class counts decide fast-kernel eligibility
+  if (h->n_pods) {  // and ride in the queued descriptors (ksim_persistent.hip's ring)
+    hipError_t e = ksim_launch_pod_k(h->d_pods, h->n_pods, &c, h->stream);
+    if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pod k launch: %s", hipGetErrorString(e));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+  }
   h->have_classes = true;
   return KSIM_OK;
 }
@@ -326,6 +332,10 @@ int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
   if (n_scalars)
     HIPCHK(h, hipMemcpyAsync(h->d_pod_scalars + S0, scalars, n_scalars * sizeof(ksim_scalar_req), hipMemcpyHostToDevice, h->stream));
   c.pods = h->d_pods; c.pod_ports = h->d_pod_ports; c.pod_scalars = h->d_pod_scalars;
+  {
+    hipError_t e = ksim_launch_pod_k(h->d_pods + P0, n_pods, &c, h->stream);
+    if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pod k launch: %s", hipGetErrorString(e));
+  }
   // host bookkeeping: fast-kernel eligibility, tree classes, float64 bounds
   h->q_cls.resize((size_t)np);
   h->q_base.resize((size_t)np);
@@ -602,9 +612,10 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
     // slots: 1 publish, 2 sweep, 9 reduce, 10 selectHost index, 3 locate, 6 select+commit,
     // 7 barrier, 11 fix-up, 4 combine, 5 row-wave evaluation (concurrent), 8 polls
     static const char* names[16] = {"", "publish", "sweep", "locate", "combine", "row-eval", "select+commit", "barrier",
-                                    "polls", "reduce", "ix", "fixup", "spec-seen", "fix-seen", "", ""};
+                                    "polls", "reduce", "ix", "classes", "spec-seen", "fix-seen", "", ""};
     fprintf(stderr, "[ksim stamps] pods=%lld (%.3f ms) cycles/pod:", (long long)count, ms);
-    for (int k : {1, 2, 12, 13, 9, 10, 3, 6, 7, 11, 4, 5, 8}) fprintf(stderr, " %s %.0f", names[k], d[k] / (double)count);
+    for (int k : {1, 2, 12, 13, 9, 11, 10, 3, 6, 7, 4, 5, 8}) fprintf(stderr, " %s %.0f", names[k], d[k] / (double)count);
+    fprintf(stderr, "\n[ksim stamps] row wave 1: eval %.0f partial %.0f", d[24] / (double)count, d[25] / (double)count);
     fprintf(stderr, "\n[ksim stamps] owner select %.0f commit %.0f", d[22] / (double)(d[21] ? d[21] : 1),
             d[23] / (double)(d[21] ? d[21] : 1));
     fprintf(stderr, "\n[ksim stamps] owner (%llu fix-ups) cycles/fix-up: pre-eval %.0f barrier %.0f eval-row %.0f partial %.0f combine+publish %.0f\n",
