@@ -122,6 +122,22 @@ def config_c1(n_nodes=1500, n_a=48_010, n_b=10):
     return cl, p, q
 
 
+def c1_objects(n_nodes=1500, n_a=48_010, n_b=10):
+    """C1 as Kubernetes-shaped objects: the README's nodes test-{i}.test.com (32 cpu, 128Gi,
+    110 pods, Ready) and etc/pod.yaml's SimulationPod list (A: cpu 1 / memory 1 x n_a, then
+    B: cpu 100 / memory 1000 x n_b) expanded by ParseSimulationPod (cmd/app/options/options.go:73-99).
+    Returns (nodes, expanded pod list); the simulator pops the list from the end (LIFO)."""
+    from .scheduler import expand_simulation_pods
+    nodes = [{"metadata": {"name": "test-%d.test.com" % i},
+              "status": {"allocatable": {"cpu": "32", "memory": "128Gi", "pods": "110"},
+                         "conditions": [{"type": "Ready", "status": "True"}]}} for i in range(n_nodes)]
+    spec = [{"name": "A", "num": n_a, "pod": {"spec": {"containers": [
+                {"name": "a", "resources": {"requests": {"cpu": "1", "memory": "1"}}}]}}},
+            {"name": "B", "num": n_b, "pod": {"spec": {"containers": [
+                {"name": "b", "resources": {"requests": {"cpu": "100", "memory": "1000"}}}]}}}]
+    return nodes, expand_simulation_pods(spec)
+
+
 def c2_objects(n_nodes=5000, n_pods=50_000, seed=2):
     """C2 (BASELINE.json configs[1]) as Kubernetes-shaped objects: heterogeneous
     nodes with labels, NoSchedule / PreferNoSchedule taints and a few NotReady / unschedulable

@@ -22,6 +22,7 @@ reference itself cannot be run.
 from __future__ import annotations
 
 import math
+import functools
 import re
 from fractions import Fraction
 
@@ -34,10 +35,16 @@ _QRE = re.compile(r"^([+-]?)([0-9]*)(?:\.([0-9]*))?(.*)$")
 
 
 def parse_quantity(s) -> Fraction:
-    """Exact value of a Quantity string, rounded up to 1e-9 (quantity.go:365-380)."""
+    """Exact value of a Quantity string, rounded up to 1e-9 (quantity.go:365-380).  A pure
+    function of its argument, memoised (the large parity tests re-parse the same strings for
+    every node evaluation)."""
     if isinstance(s, (int,)):
         return Fraction(s)
-    s = str(s)
+    return _parse_quantity_str(str(s))
+
+
+@functools.lru_cache(maxsize=65536)
+def _parse_quantity_str(s) -> Fraction:
     if s == "":
         raise ValueError("quantity: empty")
     m = _QRE.match(s)
@@ -62,11 +69,13 @@ def parse_quantity(s) -> Fraction:
     return -v if sign == "-" else v
 
 
+@functools.lru_cache(maxsize=65536)
 def q_value(s) -> int:
     """Quantity.Value(): ceil(q) (quantity.go:695-713, ScaledValue rounds up)."""
     return math.ceil(parse_quantity(s))
 
 
+@functools.lru_cache(maxsize=65536)
 def q_milli(s) -> int:
     """Quantity.MilliValue(): ceil(q*1000)."""
     return math.ceil(parse_quantity(s) * 1000)

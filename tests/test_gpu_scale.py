@@ -1,0 +1,94 @@
+"""Parity at BASELINE.json's full sizes, where the cluster is no longer empty: the GPU drives the
+C3 cluster past saturation (cpu runs out at ~2.85M of the C3 pod distribution), the C4 cluster
+through 3,000 pods, and C5's scenarios through their full 5,000 pods — and the C oracle
+(oracle/cpu_ref.c, pinned to the object oracle by tests/test_oracle_c.py and
+tests/test_oracle_scale.py) continues from the GPU's read-back node state and lastNodeIndex over
+the next window.  High-occupancy tails are where fit counts collapse, ties multiply, the 1-fit
+shortcut is taken and FitErrors dominate."""
+import numpy as np
+import pytest
+
+import cpu_ref
+from ksim import abi, scheduler, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _invariants(cl, out, s):
+    """Size-independent checks over a whole run: per-node sums conserved, nothing overcommitted."""
+    bound = out >= 0
+    assert s["pod_count"].sum() == bound.sum()
+    assert s["req_cpu"].sum() == cl.pods["add_cpu"][:len(out)][bound].sum()
+    assert s["req_mem"].sum() == cl.pods["add_mem"][:len(out)][bound].sum()
+    assert np.array_equal(np.bincount(out[bound], minlength=cl.n_nodes), s["pod_count"])
+    assert (s["req_cpu"] <= cl.cols["alloc_cpu"]).all() and (s["req_mem"] <= cl.cols["alloc_mem"]).all()
+
+
+@pytest.mark.parametrize("mode", [abi.MODE_AUTO, abi.MODE_TREE], ids=["scan", "tree"])
+def test_c3_saturated_tail_matches_c_oracle(mode):
+    """C3 (100k nodes): 2,950,000 pods on the GPU (past cpu saturation), then the next 3,000 on
+    the GPU and on the C oracle from the GPU's state: placements, FitError histograms, counter,
+    final node state."""
+    head, tail = 2_950_000, 3000
+    cl, p, q = synth.config_c3(100_000, head + tail)
+    g = scheduler.GenericScheduler(cl, p, q, mode=mode, collect_reasons=True)
+    out_head, _, _ = g.schedule(0, head)
+    state, ctr = g.node_state(), g.last_node_index
+    _invariants(cl, out_head, state)
+    assert (out_head < 0).sum() > 10_000  # saturated: many FitErrors already
+    out, reasons, _ = g.schedule(head, tail)
+    ref, ref_reasons, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), head, tail, threads=16,
+                                                       state=state, counter=ctr)
+    assert np.array_equal(out, ref)
+    failed = out < 0
+    assert failed.sum() > tail // 10
+    assert np.array_equal(reasons[failed], ref_reasons[failed])
+    assert g.last_node_index == ref_ctr
+    s = g.node_state()
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+        assert np.array_equal(s[k], ref_state[k]), k
+    g.close()
+
+
+@pytest.mark.parametrize("mode", [abi.MODE_AUTO, abi.MODE_TREE], ids=["scan", "tree"])
+def test_c4_3000_pods_match_c_oracle(mode):
+    """C4 (1M nodes on one device: the streaming form of the fast kernel, or tree mode): 3,000
+    pods against the C oracle, node state included."""
+    cl, p, q = synth.config_c4(1_000_000, 3000)
+    g = scheduler.GenericScheduler(cl, p, q, mode=mode, collect_reasons=False)
+    out1, _, _ = g.schedule(0, 1000)
+    out2, _, _ = g.schedule(1000, 2000)
+    ref, _, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, 3000, threads=16)
+    assert np.array_equal(np.concatenate([out1, out2]), ref)
+    assert g.last_node_index == ref_ctr
+    s = g.node_state()
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+        assert np.array_equal(s[k], ref_state[k]), k
+    g.close()
+
+
+C5_EXTREMES = [(1, 1, 0), (16, 16, 15), (1, 16, 0), (16, 1, 0), (1, 1, 15), (16, 16, 0), (1, 16, 15), (16, 1, 15),
+               (8, 3, 7)]
+
+
+@pytest.mark.parametrize("form", ["tree", "scan"])
+def test_c5_full_pods_weight_extremes(form, monkeypatch):
+    """C5 (20k nodes): nine scenarios at the corners of the (wLR, wBRA, wMR) grid, each through
+    all 5,000 pods of the sweep, against the C oracle run under that scenario's weights."""
+    if form == "scan":
+        monkeypatch.setenv("KSIM_SWEEP_SCAN", "1")
+    cl, preds, _ = synth.config_c5(20_000, 5000)
+    pick = []
+    for a, b, m in C5_EXTREMES:
+        pri = [("LeastRequestedPriority", a), ("BalancedResourceAllocation", b)]
+        if m:
+            pri.append(("MostRequestedPriority", m))
+        pick.append(pri)
+    g = scheduler.GenericScheduler(cl, preds, pick[0], collect_reasons=False)
+    out, ctr, st = g.sweep(pick, 0, 5000)
+    assert st.mode == (abi.MODE_TREE if form == "tree" else abi.MODE_PERSISTENT)
+    for k, pri in enumerate(pick):
+        ref, _, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, pri), 0, 5000, threads=16)
+        assert np.array_equal(out[k], ref), pri
+        assert int(ctr[k]) == ref_ctr, pri
+    g.close()
