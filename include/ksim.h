@@ -58,6 +58,9 @@ extern "C" {
 #define KSIM_P_NOEXEC_TAINTS (1u << 8)            /* PodToleratesNodeNoExecuteTaints */
 #define KSIM_P_MEM_PRESSURE (1u << 9)             /* predicates.go:1502 */
 #define KSIM_P_DISK_PRESSURE (1u << 10)           /* predicates.go:1524 */
+#define KSIM_P_LABEL_PRESENCE (1u << 11)          /* CheckNodeLabelPresence with a labelsPresence
+                                                     argument (predicates.go:875-910); the node's
+                                                     verdict is the KSIM_N_LABEL_PRESENCE bit */
 
 /* ---- priority weight slots (0 = not configured).  Priorities that evaluate to the
  *      same value on every node under supported inputs (SelectorSpread /
@@ -78,6 +81,7 @@ extern "C" {
 #define KSIM_N_UNSCHEDULABLE (1u << 3)  /* spec.unschedulable */
 #define KSIM_N_MEM_PRESSURE (1u << 4)   /* MemoryPressure == True */
 #define KSIM_N_DISK_PRESSURE (1u << 5)  /* DiskPressure == True */
+#define KSIM_N_LABEL_PRESENCE (1u << 6) /* the node fails the policy's CheckNodeLabelPresence */
 #define KSIM_N_GPU_OVER (1u << 8)       /* alloc.gpu < requested.gpu  (maintained by the library) */
 #define KSIM_N_EPH_OVER (1u << 9)       /* alloc.eph < requested.eph  (maintained by the library) */
 
@@ -103,6 +107,7 @@ extern "C" {
 #define KSIM_R_TAINTS 12
 #define KSIM_R_MEM_PRESSURE 13
 #define KSIM_R_DISK_PRESSURE 14
+#define KSIM_R_LABEL_PRESENCE 15
 #define KSIM_R_INSUFFICIENT_SCALAR0 16 /* +column, up to KSIM_MAX_SCALAR */
 
 /* ---- execution modes ---- */

@@ -289,6 +289,7 @@ __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ks
   if ((pr & KSIM_P_NOEXEC_TAINTS) && (P.flags & KSIM_POD_NEED_TAINTS)) {
     if (!a.noexec_ok(P, i)) return 1u << KSIM_R_TAINTS;
   }
+  if ((pr & KSIM_P_LABEL_PRESENCE) && (r.fl & KSIM_N_LABEL_PRESENCE)) return 1u << KSIM_R_LABEL_PRESENCE;
   if ((pr & KSIM_P_MEM_PRESSURE) && (P.flags & KSIM_POD_BEST_EFFORT) && (r.fl & KSIM_N_MEM_PRESSURE))
     return 1u << KSIM_R_MEM_PRESSURE;
   if ((pr & KSIM_P_DISK_PRESSURE) && (r.fl & KSIM_N_DISK_PRESSURE)) return 1u << KSIM_R_DISK_PRESSURE;

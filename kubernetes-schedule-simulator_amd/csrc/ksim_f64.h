@@ -36,6 +36,7 @@ struct EvCfg {
   uint32_t resm;    // ~0u if PodFitsResources runs (GeneralPredicates / PodFitsResources)
   uint32_t mempm;   // KSIM_N_MEM_PRESSURE if CheckNodeMemoryPressure is configured
   uint32_t diskm;   // KSIM_N_DISK_PRESSURE if CheckNodeDiskPressure is configured
+  uint32_t lpm;     // KSIM_N_LABEL_PRESENCE if CheckNodeLabelPresence is configured
   int32_t wl, wm, wb;  // 0 for every weight under an empty prioritizer list (EqualPriorityMap)
 };
 
@@ -46,6 +47,7 @@ __host__ __device__ inline EvCfg make_evcfg(uint32_t preds, bool no_prio, int32_
   C.resm = (preds & (KSIM_P_GENERAL | KSIM_P_RESOURCES)) ? ~0u : 0u;
   C.mempm = (preds & KSIM_P_MEM_PRESSURE) ? KSIM_N_MEM_PRESSURE : 0u;
   C.diskm = (preds & KSIM_P_DISK_PRESSURE) ? KSIM_N_DISK_PRESSURE : 0u;
+  C.lpm = (preds & KSIM_P_LABEL_PRESENCE) ? KSIM_N_LABEL_PRESENCE : 0u;
   C.wl = no_prio ? 0 : wl;
   C.wm = no_prio ? 0 : wm;
   C.wb = no_prio ? 0 : wb;
@@ -96,7 +98,8 @@ __device__ __forceinline__ int32_t feval(const EvCfg& C, const FPod& P, const FR
   const uint32_t res = (((r.count + 1 > r.allowed) ? (1u << KSIM_R_INSUFFICIENT_PODS) : 0u) | (rq & P.anyreq)) & C.resm;
   const uint32_t memp = (fl & C.mempm & P.be) ? (1u << KSIM_R_MEM_PRESSURE) : 0u;
   const uint32_t diskp = (fl & C.diskm) ? (1u << KSIM_R_DISK_PRESSURE) : 0u;
-  const uint32_t m = cond ? cond : unsch ? unsch : res ? res : memp ? memp : diskp;
+  const uint32_t lp = (fl & C.lpm) ? (1u << KSIM_R_LABEL_PRESENCE) : 0u;
+  const uint32_t m = cond ? cond : unsch ? unsch : res ? res : lp ? lp : memp ? memp : diskp;
   rmask = m;
   const double tc = P.nz_c + r.zc, tm = P.nz_m + r.zm;
   const bool okc = r.ac != 0.0 && tc <= r.ac, okm = r.am != 0.0 && tm <= r.am;

@@ -88,11 +88,12 @@ __device__ __forceinline__ uint32_t ksim_fast_predicates(uint32_t preds, const K
       res |= (fl & KSIM_N_EPH_OVER) ? (1u << KSIM_R_INSUFFICIENT_EPHEMERAL) : 0u;
     }
   }
+  const uint32_t lp = ((preds & KSIM_P_LABEL_PRESENCE) && (fl & KSIM_N_LABEL_PRESENCE)) ? (1u << KSIM_R_LABEL_PRESENCE) : 0u;
   const uint32_t memp = ((preds & KSIM_P_MEM_PRESSURE) && (P.flags & KSIM_POD_BEST_EFFORT) && (fl & KSIM_N_MEM_PRESSURE))
                             ? (1u << KSIM_R_MEM_PRESSURE)
                             : 0u;
   const uint32_t diskp = ((preds & KSIM_P_DISK_PRESSURE) && (fl & KSIM_N_DISK_PRESSURE)) ? (1u << KSIM_R_DISK_PRESSURE) : 0u;
-  return cond ? cond : unsch ? unsch : res ? res : memp ? memp : diskp;
+  return cond ? cond : unsch ? unsch : res ? res : lp ? lp : memp ? memp : diskp;
 }
 
 // Packed evaluation of a row for a resource-only pod (-1 = does not fit, else the score) and

@@ -31,12 +31,13 @@ P_TAINTS = 1 << 7
 P_NOEXEC_TAINTS = 1 << 8
 P_MEM_PRESSURE = 1 << 9
 P_DISK_PRESSURE = 1 << 10
+P_LABEL_PRESENCE = 1 << 11
 
 W_LEAST, W_MOST, W_BALANCED, W_TAINT_TOL, W_NODE_AFF = range(5)
 NW = 5
 
 N_NOT_READY, N_OUT_OF_DISK, N_NET_UNAVAIL, N_UNSCHEDULABLE = 1, 2, 4, 8
-N_MEM_PRESSURE, N_DISK_PRESSURE = 16, 32
+N_MEM_PRESSURE, N_DISK_PRESSURE, N_LABEL_PRESENCE = 16, 32, 64
 
 POD_ANY_REQUEST, POD_BEST_EFFORT, POD_NEED_SELECTOR, POD_NEED_TAINTS = 1, 2, 4, 8
 
@@ -45,7 +46,7 @@ MODE_AUTO, MODE_LAUNCH, MODE_PERSISTENT, MODE_TREE = 0, 1, 2, 3
 R_NOT_READY, R_OUT_OF_DISK, R_NET_UNAVAIL, R_UNSCHEDULABLE = 0, 1, 2, 3
 R_PODS, R_CPU, R_MEMORY, R_GPU, R_EPHEMERAL = 4, 5, 6, 7, 8
 R_HOSTNAME, R_HOST_PORTS, R_NODE_SELECTOR, R_TAINTS = 9, 10, 11, 12
-R_MEM_PRESSURE, R_DISK_PRESSURE = 13, 14
+R_MEM_PRESSURE, R_DISK_PRESSURE, R_LABEL_PRESENCE = 13, 14, 15
 R_SCALAR0 = 16
 
 _i64p = C.POINTER(C.c_int64)

@@ -200,6 +200,7 @@ class Cluster:
         self.pod_names = []
         self.tables = None
         self.prefer_avoid_nodes = False
+        self.node_images = False   # some node lists status.images (ImageLocalityPriority not constant)
         self.bad_affinity_classes = set()   # preferred terms that fail to parse
 
     # ------------------------------------------------------------------ nodes
@@ -251,6 +252,7 @@ class Cluster:
             c["label_set"][i] = self.label_sets.get(_canon(ns.labels), dict(ns.labels))
             c["taint_set"][i] = self.taint_sets.get(_canon(ns.taints), ns.taints)
             self.prefer_avoid_nodes |= ns.prefer_avoid
+            self.node_images |= bool((x.get("status") or {}).get("images"))
             node_taints.append(ns.taints)
         # running pods: NodeInfo.AddPod
         used_ports = [dict() for _ in range(n)]

@@ -8,6 +8,7 @@ decimal-exponent suffix, non-zero values rounded up to 1e-9) and ScaledValue
 """
 from __future__ import annotations
 
+import math
 import re
 from fractions import Fraction
 from functools import lru_cache
@@ -72,3 +73,60 @@ def milli_value(q) -> int:
 
 def positive(q) -> bool:
     return parse(q) > 0
+
+
+# ---------------------------------------------------------------------------- formatting
+# Quantity.String (quantity.go:605-615) → CanonicalizeBytes (:417-454): the format a string was
+# parsed with (binary-SI suffix → BinarySI, an 'e' exponent → DecimalExponent, else DecimalSI),
+# BinarySI shown as DecimalSI below 1024 or when not an integer; decimal mantissa with its
+# exponent moved to a multiple of 3 (amount.go:219-243), base-1024 mantissa (:248-255).
+DECIMAL_SI, BINARY_SI, DECIMAL_EXPONENT = "DecimalSI", "BinarySI", "DecimalExponent"
+_DEC_SUFFIX = {-9: "n", -6: "u", -3: "m", 0: "", 3: "k", 6: "M", 9: "G", 12: "T", 15: "P", 18: "E"}
+_BIN_SUFFIX = {0: "", 1: "Ki", 2: "Mi", 3: "Gi", 4: "Ti", 5: "Pi", 6: "Ei"}
+
+
+def fmt(q) -> str:
+    """The Format a quantity string parses with."""
+    if isinstance(q, int):
+        return DECIMAL_SI
+    m = _NUM.match(str(q))
+    rest = str(q)[m.end():] if m else ""
+    if rest in ("Ki", "Mi", "Gi", "Ti", "Pi", "Ei"):
+        return BINARY_SI
+    if _EXP.fullmatch(rest):
+        return DECIMAL_EXPONENT
+    return DECIMAL_SI
+
+
+def canonical(v: Fraction, form: str) -> str:
+    """The canonical string of value v in format `form` (CanonicalizeBytes)."""
+    if v == 0:
+        return "0"
+    if form == BINARY_SI:
+        if -1024 < v < 1024 or v.denominator != 1:
+            form = DECIMAL_SI
+        else:
+            n, e = int(v), 0
+            while n % 1024 == 0 and e < 6:
+                n //= 1024
+                e += 1
+            return "%d%s" % (n, _BIN_SUFFIX[e])
+    # decimal: v = mantissa * 10^exp with no factor of 10 left in the mantissa
+    num, den = v.numerator, v.denominator
+    exp = 0
+    while den != 1:           # values are multiples of 1e-9 (ParseQuantity rounds up to nano)
+        num *= 10
+        exp -= 1
+        g = math.gcd(num, den)
+        num, den = num // g, den // g
+    while num % 10 == 0:
+        num //= 10
+        exp += 1
+    while exp % 3:
+        num *= 10
+        exp -= 1
+    if form == DECIMAL_EXPONENT:
+        return "%d%s" % (num, "" if exp == 0 else "e%d" % exp)
+    if exp in _DEC_SUFFIX:
+        return "%d%s" % (num, _DEC_SUFFIX[exp])
+    return "%de%d" % (num, exp)

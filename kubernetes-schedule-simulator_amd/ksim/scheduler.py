@@ -36,7 +36,10 @@ PREDICATE_BITS = {
     "PodToleratesNodeNoExecuteTaints": abi.P_NOEXEC_TAINTS,
     "CheckNodeMemoryPressure": abi.P_MEM_PRESSURE,
     "CheckNodeDiskPressure": abi.P_DISK_PRESSURE,
+    "CheckNodeLabelPresence": abi.P_LABEL_PRESENCE,   # with a Policy labelsPresence argument
 }
+# factory/plugins.go:401-406 + defaults.go:165: part of every predicate map
+MANDATORY_PREDICATES = ("CheckNodeCondition",)
 # keys that are true for every pod ingest accepts (no volumes of those kinds, no inter-pod
 # affinity); "PodFitsPorts" is registered but absent from predicatesOrdering, so it never runs
 TRIVIAL_PREDICATES = {"NoDiskConflict", "MaxEBSVolumeCount", "MaxGCEPDVolumeCount", "MaxAzureDiskVolumeCount",
@@ -48,7 +51,9 @@ PRIORITY_SLOTS = {"LeastRequestedPriority": abi.W_LEAST, "MostRequestedPriority"
 # value on every node under supported inputs (no services/controllers in the simulator's store,
 # no RC/RS-owned pods next to preferAvoidPods annotations, no affinity terms)
 CONST_PRIORITIES = {"SelectorSpreadPriority": 10, "ServiceSpreadingPriority": 10, "NodePreferAvoidPodsPriority": 10,
-                    "InterPodAffinityPriority": 0, "EqualPriority": 1}
+                    "InterPodAffinityPriority": 0, "EqualPriority": 1,
+                    # image_locality.go:39-69: 0 on every node when no node lists status.images
+                    "ImageLocalityPriority": 0}
 
 DEFAULT_PREDICATES = ("NoVolumeZoneConflict", "MaxEBSVolumeCount", "MaxGCEPDVolumeCount", "MaxAzureDiskVolumeCount",
                       "MatchInterPodAffinity", "NoDiskConflict", "GeneralPredicates", "CheckNodeMemoryPressure",
@@ -74,7 +79,7 @@ def make_config(predicates, priorities, device=0, mode=abi.MODE_AUTO, collect_re
     cfg.device = device
     cfg.mode = mode
     bits = 0
-    for k in predicates:
+    for k in list(predicates) + list(MANDATORY_PREDICATES):
         if k in PREDICATE_BITS:
             bits |= PREDICATE_BITS[k]
         elif k not in TRIVIAL_PREDICATES:
@@ -119,6 +124,7 @@ REASON_TEXT = {
     abi.R_TAINTS: "node(s) had taints that the pod didn't tolerate",
     abi.R_MEM_PRESSURE: "node(s) had memory pressure",
     abi.R_DISK_PRESSURE: "node(s) had disk pressure",
+    abi.R_LABEL_PRESENCE: "node(s) didn't have the requested labels",
 }
 
 
@@ -142,19 +148,39 @@ def fit_error_message(num_nodes, hist, scalar_names=()):
     return "0/%d nodes are available: %s." % (num_nodes, ", ".join(parts))
 
 
+def label_presence_flags(label_sets, label_set_ids, label_presence):
+    """KSIM_N_LABEL_PRESENCE per node: CheckNodeLabelPresence (predicates.go:875-910) fails when
+    a listed label's presence differs from `presence`; a function of the node's label set."""
+    labels_, presence = label_presence
+    bad = np.array([any((k in ls) != presence for k in labels_) for ls in label_sets], bool)
+    return np.where(bad[np.asarray(label_set_ids)], abi.N_LABEL_PRESENCE, 0).astype(np.uint32)
+
+
 class GenericScheduler:
-    """Batch drop-in for genericScheduler + Scheduler.assume on one MI355X."""
+    """Batch drop-in for genericScheduler + Scheduler.assume on one MI355X.  label_presence:
+    (labels, presence) of a Policy's CheckNodeLabelPresence predicate (policy.key_sets)."""
 
     def __init__(self, cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO,
-                 collect_reasons=True, last_node_index=0):
+                 collect_reasons=True, last_node_index=0, label_presence=None):
         self.cluster = cluster
         self.predicates = list(predicates)
         self.prioritizers = list(priorities)
         if any(n == "NodeAffinityPriority" for n, _ in self.prioritizers) and cluster.bad_affinity_classes:
             raise Unsupported("NodeAffinityPriority: a preferred node-affinity term does not parse")
-        self.cfg = make_config(predicates, priorities, device, mode, collect_reasons, last_node_index)
+        if any(n == "ImageLocalityPriority" for n, _ in self.prioritizers) and cluster.node_images:
+            raise Unsupported("ImageLocalityPriority with nodes that list status.images")
+        if "CheckNodeLabelPresence" in self.predicates and label_presence is None:
+            raise Unsupported("CheckNodeLabelPresence needs its labelsPresence argument")
+        self.cfg = make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence], priorities,
+                               device, mode, collect_reasons, last_node_index)
         self.h = abi.Handle(self.cfg)
-        self.h.call("ksim_load_nodes", C.byref(cluster.node_table()))
+        table = cluster.node_table()
+        if label_presence is not None and "CheckNodeLabelPresence" in self.predicates:
+            fl = cluster.cols["flags"] | label_presence_flags(cluster.label_sets.items, cluster.cols["label_set"],
+                                                                label_presence)
+            self._flags = np.ascontiguousarray(fl, np.uint32)
+            table.flags = abi.ptr(self._flags, C.c_uint32)
+        self.h.call("ksim_load_nodes", C.byref(table))
         self.h.call("ksim_load_classes", C.byref(cluster.class_tables()))
         pods = np.ascontiguousarray(cluster.pods)
         self._pods = pods
@@ -310,59 +336,118 @@ def _normalize(vals, reverse):
 
 
 # ----------------------------------------------------------------------------- simulator
-def expand_simulation_pods(spec_list, namespace=""):
-    """ParseSimulationPod (cmd/app/options/options.go:73-99).  Names are uuids in Go; here
-    they are deterministic <SimulationName>-<i>."""
+def expand_simulation_pods(spec_list, namespace="", uid=None):
+    """ParseSimulationPod (cmd/app/options/options.go:73-99): each SimulationPod's pod deep-copied
+    `num` times with UID = name = a fresh uuid, labels replaced by {SimulationName: name} and the
+    namespace set.  uid: None → deterministic "<SimulationName>-<i>" (so runs are reproducible);
+    "uuid" → uuid4 strings as the reference makes them; or a callable (sp name, i) → str."""
+    import copy
+    import uuid as _uuid
     out = []
     for sp in spec_list:
         for i in range(int(sp.get("num", 0))):
-            out.append({"metadata": {"name": "%s-%d" % (sp["name"], i), "namespace": namespace,
-                                     "labels": {"SimulationName": sp["name"]}},
-                        "spec": dict((sp.get("pod") or {}).get("spec") or {})})
+            if uid is None:
+                u = "%s-%d" % (sp["name"], i)
+            elif uid == "uuid":
+                u = str(_uuid.uuid4())
+            else:
+                u = uid(sp["name"], i)
+            pod = copy.deepcopy(sp.get("pod") or {})
+            meta = pod.setdefault("metadata", {})
+            meta.update({"uid": u, "name": u, "namespace": namespace, "labels": {"SimulationName": sp["name"]}})
+            pod.setdefault("spec", {})
+            out.append(pod)
     return out
 
 
 def load_podspec(path):
     """The --podspec file: a YAML or JSON list of SimulationPod{name, num, pod}
-    (pkg/api/api.go:79-83)."""
+    (pkg/api/api.go:79-83, cmd/app/options/options.go:73-99)."""
     import yaml
     with open(path) as f:
         return yaml.safe_load(f)
 
 
+def load_checkpoint(nodes_path, pods_path=None):
+    """The offline snapshot (pkg/main.go:147-179 getNodeCheckPoint / getPodsCheckPoint): JSON
+    arrays of v1.Node and v1.Pod.  Returns (nodes, pods)."""
+    import json
+    with open(nodes_path) as f:
+        nodes = json.load(f)
+    pods = []
+    if pods_path:
+        with open(pods_path) as f:
+            pods = json.load(f)
+    if not isinstance(nodes, list) or not isinstance(pods, list):
+        raise abi.KsimError(abi.E_INVAL, "checkpoint files must hold JSON arrays of v1.Node / v1.Pod")
+    return nodes, pods
+
+
 @dataclass
 class Report:
-    """framework.GetReport's content (pkg/framework/report.go:168-174)."""
+    """The simulation's outcome: (pod, node) in bind order, (pod, FitError text) for failed pods,
+    the framework.Status the reference reports from (report.status, pod objects as the
+    simulator leaves them) and GetReport's review (report.review)."""
     successful: list = field(default_factory=list)   # (pod name, node name) in bind order
     failed: list = field(default_factory=list)       # (pod name, FitError message)
-    stop_reason: str = "No pods left"
+    stop_reason: str = ""
     stats: object = None
     last_node_index: int = 0
+    status: object = None
+    review: object = None
+
+    def text(self) -> str:
+        """ClusterCapacityReviewPrint's output."""
+        from .report import review_text
+        return review_text(self.review)
 
 
 class ClusterCapacity:
+    """The simulator (pkg/scheduler/simulator.go:286-342 New, :187-213 Run): nodes and running
+    pods of a snapshot, the simulation pods popped LIFO from the expanded podspec list
+    (pkg/framework/store/store.go:223-233), each scheduled and committed before the next; a
+    provider name, explicit key lists or a Policy (policy.key_sets) configure the algorithm."""
+
     def __init__(self, nodes, running_pods, simulation_pods, provider_name="DefaultProvider",
-                 predicates=None, priorities=None, device=0, mode=abi.MODE_AUTO, collect_reasons=True):
+                 predicates=None, priorities=None, device=0, mode=abi.MODE_AUTO, collect_reasons=True,
+                 policy_obj=None):
+        label_presence = None
+        if policy_obj is not None:
+            from .policy import key_sets
+            predicates, priorities, label_presence = key_sets(policy_obj)
         if predicates is None or priorities is None:
             p, q = provider(provider_name)
             predicates = p if predicates is None else predicates
             priorities = q if priorities is None else priorities
-        order = list(reversed(simulation_pods))   # PodQueue.Pop takes the last element
-        self.cluster = Cluster.from_objects(nodes, running_pods, order)
+        self.order = list(reversed(simulation_pods))   # PodQueue.Pop takes the last element
+        self.running = list(running_pods)
+        self.cluster = Cluster.from_objects(nodes, running_pods, self.order)
         self.scheduler = GenericScheduler(self.cluster, predicates, priorities, device=device, mode=mode,
-                                          collect_reasons=collect_reasons)
+                                          collect_reasons=collect_reasons, label_presence=label_presence)
 
     def run(self) -> Report:
-        nodes, reasons, st = self.scheduler.schedule()
-        rep = Report(stats=st)
+        from .report import ERR_NO_NODES, get_report, simulation_status
+        rep = Report()
         names = self.cluster.names
         scal = self.cluster.scalar_names.items
-        for k, w in enumerate(nodes):
-            pod = self.cluster.pod_names[k]
-            if w >= 0:
-                rep.successful.append((pod, names[w]))
-            else:
-                msg = fit_error_message(len(names), reasons[k], scal) if reasons is not None else "unschedulable"
-                rep.failed.append((pod, msg))
+        try:
+            nodes, reasons, st = self.scheduler.schedule()
+            rep.stats = st
+            msgs = [None if w >= 0 else (fit_error_message(len(names), reasons[k], scal) if reasons is not None
+                                         else "unschedulable") for k, w in enumerate(nodes)]
+        except abi.NoNodesAvailable:
+            # ErrNoNodesAvailable (generic_scheduler.go:63-64,124-125) for every pod: nothing is
+            # ever bound, so each pod in turn fails the same way and goes through Update
+            nodes, msgs = np.full(len(self.order), -1, np.int32), [ERR_NO_NODES] * len(self.order)
         rep.last_node_index = self.scheduler.last_node_index
+        outcomes = [(names[w] if w >= 0 else None, m) for w, m in zip(nodes, msgs)]
+        for k, (node, msg) in enumerate(outcomes):
+            name = self.cluster.pod_names[k]
+            if node is not None:
+                rep.successful.append((name, node))
+            else:
+                rep.failed.append((name, msg))
+        rep.status = simulation_status(self.order, self.running, outcomes)
+        rep.stop_reason = rep.status.stop_reason
+        rep.review = get_report(rep.status)
         return rep

@@ -138,6 +138,7 @@ static uint32_t pod_fits_on_node(uint32_t preds, const RefNodes* N, const RefTab
   if ((preds & KSIM_P_RESOURCES) && (m = pred_resources(N, P, sc, i))) return m;
   if ((preds & KSIM_P_TAINTS) && !bit(T->T->taint_ok, P->cls, T->tw, N->taint_set[i])) return 1u << KSIM_R_TAINTS;
   if ((preds & KSIM_P_NOEXEC_TAINTS) && !bit(T->T->noexec_ok, P->cls, T->tw, N->taint_set[i])) return 1u << KSIM_R_TAINTS;
+  if ((preds & KSIM_P_LABEL_PRESENCE) && (fl & KSIM_N_LABEL_PRESENCE)) return 1u << KSIM_R_LABEL_PRESENCE;
   if ((preds & KSIM_P_MEM_PRESSURE) && (P->flags & KSIM_POD_BEST_EFFORT) && (fl & KSIM_N_MEM_PRESSURE))
     return 1u << KSIM_R_MEM_PRESSURE;
   if ((preds & KSIM_P_DISK_PRESSURE) && (fl & KSIM_N_DISK_PRESSURE)) return 1u << KSIM_R_DISK_PRESSURE;

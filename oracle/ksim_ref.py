@@ -668,11 +668,32 @@ ORDERING = ["CheckNodeCondition", "CheckNodeUnschedulable", "GeneralPredicates",
             "CheckNodeMemoryPressure", "CheckNodeDiskPressure", "MatchInterPodAffinity"]
 
 
-def pod_fits_on_node(pod, ni, keys):
-    """S/core/generic_scheduler.go:420-534 (nominated-pod pass inert; no ecache)."""
+R_LABEL_PRESENCE = "node(s) didn't have the requested labels"
+
+
+def new_node_label_predicate(labels, presence):
+    """NewNodeLabelPredicate / CheckNodeLabelPresence (predicates.go:875-910): every listed
+    label present (presence=True) or absent (False), values ignored."""
+    def pred(pod, ni):
+        node_labels = (ni.node.get("metadata") or {}).get("labels") or {}
+        for label in labels:
+            if (label in node_labels) != presence:
+                return False, [R_LABEL_PRESENCE]
+        return True, []
+    return pred
+
+
+# factory/plugins.go:401-406 + defaults.go:165: always part of the predicate map
+MANDATORY_PREDICATES = ("CheckNodeCondition",)
+
+
+def pod_fits_on_node(pod, ni, keys, custom=None):
+    """S/core/generic_scheduler.go:420-534 (nominated-pod pass inert; no ecache).  `custom`:
+    predicates registered from a Policy argument (plugins.go:199-239), by key."""
     for k in ORDERING:
         if k in keys:
-            ok, rs = PREDICATES[k](pod, ni)
+            fn = custom[k] if custom and k in custom else PREDICATES[k]
+            ok, rs = fn(pod, ni)
             if not ok:
                 return False, rs
     return True, []
@@ -851,7 +872,30 @@ PRIORITIES = {
     "ServiceSpreadingPriority": ("spread", _prio_zero),
     "InterPodAffinityPriority": ("map", _prio_zero),
     "EqualPriority": ("map", _prio_equal),
+    "ImageLocalityPriority": ("map", None),  # set below
 }
+
+
+MB = 1024 * 1024
+MIN_IMG_SIZE, MAX_IMG_SIZE = 23 * MB, 1000 * MB   # image_locality.go:30-31
+
+
+def prio_image_locality(pod, ni):
+    """ImageLocalityPriorityMap (image_locality.go:39-88): the summed size of the pod's
+    container images the node lists in status.images, bucketed 0..10."""
+    sizes = {}
+    for img in (ni.node.get("status") or {}).get("images") or []:
+        for name in img.get("names") or []:
+            sizes[name] = int(img.get("sizeBytes", 0))
+    total = sum(sizes.get(c.get("image"), 0) for c in _containers(pod))
+    if total == 0 or total < MIN_IMG_SIZE:
+        return 0
+    if total >= MAX_IMG_SIZE:
+        return MAX_PRIORITY
+    return (MAX_PRIORITY * (total - MIN_IMG_SIZE)) // (MAX_IMG_SIZE - MIN_IMG_SIZE) + 1
+
+
+PRIORITIES["ImageLocalityPriority"] = ("map", prio_image_locality)
 
 
 def prioritize_nodes(pod, infos, configs):
@@ -917,8 +961,9 @@ class FitError(Exception):
 
 
 class GenericScheduler:
-    def __init__(self, predicate_keys, priority_configs):
-        self.predicates = set(predicate_keys)
+    def __init__(self, predicate_keys, priority_configs, custom_predicates=None):
+        self.predicates = set(predicate_keys) | set(MANDATORY_PREDICATES)
+        self.custom = dict(custom_predicates or {})
         self.prioritizers = list(priority_configs)
         self.last_node_index = 0          # uint64 (generic_scheduler.go:102)
 
@@ -928,7 +973,7 @@ class GenericScheduler:
             raise RuntimeError("no nodes available to schedule pods")
         filtered, failed = [], {}
         for ni in infos:
-            ok, rs = pod_fits_on_node(pod, ni, self.predicates) if self.predicates else (True, [])
+            ok, rs = pod_fits_on_node(pod, ni, self.predicates, self.custom) if self.predicates else (True, [])
             if ok:
                 filtered.append(ni)
             else:
@@ -956,12 +1001,12 @@ class GenericScheduler:
 # scheduleOne loop's Schedule + assume (S/scheduler.go:188-204, 366-397)
 # --------------------------------------------------------------------------
 class SchedulerCache:
-    def __init__(self, predicate_keys, priority_configs):
+    def __init__(self, predicate_keys, priority_configs, custom_predicates=None):
         self.nodes = {}          # name -> NodeInfo (cache.nodes)
         self.listed = []         # names the node lister returns (added, not removed)
         self.pod_states = {}     # key -> pod
         self.assumed = set()
-        self.sched = GenericScheduler(predicate_keys, priority_configs)
+        self.sched = GenericScheduler(predicate_keys, priority_configs, custom_predicates)
 
     def _info(self, name):
         n = self.nodes.get(name)
@@ -1069,7 +1114,7 @@ def expand_simulation_pods(spec_list):
     return out
 
 
-def simulate(nodes, running_pods, sim_pods, predicate_keys, priority_configs):
+def simulate(nodes, running_pods, sim_pods, predicate_keys, priority_configs, custom_predicates=None):
     """Runs the ClusterCapacity loop: pods are popped LIFO (store.go:223-233),
     each is scheduled, bound pods are assumed into the node cache (scheduler.go:366
     → cache.go:125 → node_info.go:318), unschedulable pods are recorded and the
@@ -1081,7 +1126,7 @@ def simulate(nodes, running_pods, sim_pods, predicate_keys, priority_configs):
         nn = (p.get("spec") or {}).get("nodeName", "")
         if nn in by_name:
             by_name[nn].add_pod(p)
-    sched = GenericScheduler(predicate_keys, priority_configs)
+    sched = GenericScheduler(predicate_keys, priority_configs, custom_predicates)
     queue = list(sim_pods)
     out = []
     while queue:

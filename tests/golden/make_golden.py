@@ -585,6 +585,69 @@ for s, milli, val in [("1", 1000, 1), ("100m", 100, 1), ("1000m", 1000, 1), ("20
     add("quantity", {"source": "vendor/k8s.io/apimachinery/pkg/api/resource/quantity.go:695", "q": s,
                      "milli": milli, "value": val})
 
+# ------------------------------------------------ Policy decoding (algorithmprovider/defaults/compatibility_test.go)
+CT = "vendor/k8s.io/kubernetes/pkg/scheduler/algorithmprovider/defaults/compatibility_test.go"
+SA = {"serviceAffinity": {"labels": ["region"]}}
+LP = {"labelsPresence": {"labels": ["foo"], "presence": True}}
+SAA = {"serviceAntiAffinity": {"label": "zone"}}
+LPR = {"labelPreference": {"label": "bar", "presence": True}}
+for ver, ln, preds, prios in [
+        ("1.0", 49, [["MatchNodeSelector", None], ["PodFitsResources", None], ["PodFitsPorts", None],
+                     ["NoDiskConflict", None], ["TestServiceAffinity", SA], ["TestLabelsPresence", LP]],
+         [["LeastRequestedPriority", 1, None], ["ServiceSpreadingPriority", 2, None],
+          ["TestServiceAntiAffinity", 3, SAA], ["TestLabelPreference", 4, LPR]]),
+        ("1.1", 87, [["MatchNodeSelector", None], ["PodFitsHostPorts", None], ["PodFitsResources", None],
+                     ["NoDiskConflict", None], ["HostName", None], ["TestServiceAffinity", SA],
+                     ["TestLabelsPresence", LP]],
+         [["EqualPriority", 2, None], ["LeastRequestedPriority", 2, None], ["BalancedResourceAllocation", 2, None],
+          ["SelectorSpreadPriority", 2, None], ["TestServiceAntiAffinity", 3, SAA], ["TestLabelPreference", 4, LPR]]),
+        ("1.9", 460, [[n, None] for n in ["MatchNodeSelector", "PodFitsResources", "PodFitsHostPorts", "HostName",
+                                          "NoDiskConflict", "NoVolumeZoneConflict", "PodToleratesNodeTaints",
+                                          "CheckNodeMemoryPressure", "CheckNodeDiskPressure", "CheckNodeCondition",
+                                          "MaxEBSVolumeCount", "MaxGCEPDVolumeCount", "MaxAzureDiskVolumeCount",
+                                          "MatchInterPodAffinity", "GeneralPredicates", "CheckVolumeBinding"]]
+         + [["TestServiceAffinity", SA], ["TestLabelsPresence", LP]],
+         [[n, 2, None] for n in ["EqualPriority", "ImageLocalityPriority", "LeastRequestedPriority",
+                                 "BalancedResourceAllocation", "SelectorSpreadPriority", "NodePreferAvoidPodsPriority",
+                                 "NodeAffinityPriority", "TaintTolerationPriority", "InterPodAffinityPriority",
+                                 "MostRequestedPriority"]])]:
+    doc = {"kind": "Policy", "apiVersion": "v1",
+           "predicates": [dict({"name": n}, **({"argument": a} if a else {})) for n, a in preds],
+           "priorities": [dict({"name": n, "weight": w}, **({"argument": a} if a else {})) for n, w, a in prios]}
+    add("policy", {"source": CT + ":%d" % ln, "version": ver, "json": json.dumps(doc),
+                   "predicates": preds, "priorities": prios})
+
+# ------------------------------------------------ ValidatePolicy (api/validation/validation_test.go:27-86)
+VT = "vendor/k8s.io/kubernetes/pkg/scheduler/api/validation/validation_test.go"
+MAXW = ((1 << 63) - 1) // 10
+for ln, pol, err in [
+        (33, {"priorities": [{"name": "NoWeightPriority"}]},
+         "Priority NoWeightPriority should have a positive weight applied to it or it has overflown"),
+        (37, {"priorities": [{"name": "NoWeightPriority", "weight": 0}]},
+         "Priority NoWeightPriority should have a positive weight applied to it or it has overflown"),
+        (41, {"priorities": [{"name": "WeightPriority", "weight": 2}]}, None),
+        (45, {"priorities": [{"name": "WeightPriority", "weight": -2}]},
+         "Priority WeightPriority should have a positive weight applied to it or it has overflown"),
+        (49, {"priorities": [{"name": "WeightPriority", "weight": MAXW}]},
+         "Priority WeightPriority should have a positive weight applied to it or it has overflown"),
+        (53, {"extenders": [{"urlPrefix": "http://127.0.0.1:8081/extender", "prioritizeVerb": "prioritize",
+                             "weight": 2}]}, None),
+        (57, {"extenders": [{"urlPrefix": "http://127.0.0.1:8081/extender", "prioritizeVerb": "prioritize",
+                             "weight": -2}]},
+         "Priority for extender http://127.0.0.1:8081/extender should have a positive weight applied to it"),
+        (61, {"extenders": [{"urlPrefix": "http://127.0.0.1:8081/extender", "filterVerb": "filter"}]}, None),
+        (65, {"extenders": [{"urlPrefix": "http://127.0.0.1:8081/extender", "bindVerb": "bind"},
+                            {"urlPrefix": "http://127.0.0.1:8082/extender", "bindVerb": "bind"}]},
+         "Only one extender can implement bind, found 2"),
+        (72, {"extenders": [{"urlPrefix": "http://127.0.0.1:8081/extender", "managedResources": [{"name": "foo.com/bar"}]},
+                            {"urlPrefix": "http://127.0.0.1:8082/extender", "bindVerb": "bind",
+                             "managedResources": [{"name": "foo.com/bar"}]}]},
+         "Duplicate extender managed resource name foo.com/bar"),
+        (80, {"extenders": [{"urlPrefix": "http://127.0.0.1:8081/extender",
+                             "managedResources": [{"name": "kubernetes.io/foo"}]}]},
+         "kubernetes.io/foo is an invalid extended resource name")]:
+    add("policy_validation", {"source": VT + ":%d" % ln, "policy": pol, "error": err})
+
 if __name__ == "__main__":
     for group, lst in cases.items():
         with open(os.path.join(HERE, group + ".json"), "w") as f:

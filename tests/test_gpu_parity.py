@@ -587,11 +587,17 @@ def test_node_sharded_stream_form_matches_c_oracle(world, monkeypatch):
 def test_no_nodes_is_err_no_nodes_available():
     """genericScheduler.Schedule with an empty node list returns ErrNoNodesAvailable
     (core/generic_scheduler.go:63-64,125): the empty table loads, scheduling on it returns
-    KSIM_E_NO_NODES with that text."""
-    pods = [{"metadata": {"name": "p"}, "spec": {"containers": [{}]}}]
+    KSIM_E_NO_NODES with that text; the simulator's Update records every pod as failed with it
+    (simulator.go:163-185) and the last failure writes the capital-F stop reason."""
+    pods = [{"metadata": {"name": "p%d" % i}, "spec": {"containers": [{}]}} for i in range(2)]
+    cc = scheduler.ClusterCapacity([], [], pods)
     with pytest.raises(abi.NoNodesAvailable) as ei:
-        scheduler.ClusterCapacity([], [], pods).run()
+        cc.scheduler.schedule()
     assert "no nodes available to schedule pods" in str(ei.value)
+    rep = cc.run()
+    assert rep.successful == [] and [m for _, m in rep.failed] == ["no nodes available to schedule pods"] * 2
+    assert rep.stop_reason == "Fail to get next pod: No pods left\n"
+    assert rep.review["review"]["failed"][0]["status"]["reason"] == "Unschedulable"
 
 
 @pytest.mark.parametrize("mode", MODES)

@@ -120,7 +120,8 @@ def test_policy_mapping():
     with pytest.raises(abi.KsimUnsupported):
         scheduler.make_config(["CheckServiceAffinity"], [])
     with pytest.raises(abi.KsimUnsupported):
-        scheduler.make_config([], [("ImageLocalityPriority", 1)])
+        scheduler.make_config([], [("NoSuchPriority", 1)])
+    assert scheduler.make_config([], [("ImageLocalityPriority", 1)]).const_score == 0   # no node images
     assert scheduler.make_config([], []).no_priorities == 1
 
 

@@ -1,0 +1,123 @@
+"""Policy files → key sets (the simulator's Policy path, pkg/scheduler/simulator.go:382-421;
+factory.CreateFromConfig, factory/factory.go:932-1001), pinned by the reference's own goldens:
+algorithmprovider/defaults/compatibility_test.go (decoding of the 1.0 / 1.1 / 1.9 policies) and
+api/validation/validation_test.go (ValidatePolicy's errors).  CPU only."""
+import pytest
+
+from golden_util import case_id, load
+from ksim import abi, policy, scheduler
+
+
+@pytest.mark.parametrize("c", load("policy"), ids=case_id)
+def test_policy_decoding_golden(c):
+    p = policy.decode(c["json"])
+    assert [[n, a] for n, a in p.predicates] == c["predicates"]
+    assert [[n, w, a] for n, w, a in p.priorities] == c["priorities"]
+
+
+@pytest.mark.parametrize("c", load("policy_validation"), ids=case_id)
+def test_policy_validation_golden(c):
+    p = policy.decode(dict(c["policy"], kind="Policy"))
+    if c["error"] is None:
+        policy.validate(p)
+    else:
+        with pytest.raises(policy.PolicyError) as ei:
+            policy.validate(p)
+        assert str(ei.value) == c["error"]
+
+
+def test_policy_errors_are_aggregated():
+    p = policy.decode({"priorities": [{"name": "A", "weight": 0}, {"name": "B", "weight": -1}]})
+    with pytest.raises(policy.PolicyError) as ei:
+        policy.validate(p)
+    assert str(ei.value) == ("[Priority A should have a positive weight applied to it or it has overflown, "
+                             "Priority B should have a positive weight applied to it or it has overflown]")
+
+
+def test_1_9_policy_key_sets():
+    """The 1.9 compatibility policy: every built-in key runs (the custom-named TestServiceAffinity /
+    TestLabelsPresence are registered but outside predicatesOrdering, so never evaluated)."""
+    (c,) = [c for c in load("policy") if c["version"] == "1.9"]
+    preds, prios, lp = policy.key_sets(policy.decode(c["json"]))
+    assert lp is None
+    assert "TestServiceAffinity" not in preds and "GeneralPredicates" in preds
+    cfg = scheduler.make_config(preds, prios)
+    assert cfg.weights[abi.W_LEAST] == 2 and cfg.weights[abi.W_MOST] == 2 and cfg.weights[abi.W_BALANCED] == 2
+    assert cfg.weights[abi.W_TAINT_TOL] == 2 and cfg.weights[abi.W_NODE_AFF] == 2
+    # EqualPriority 1 + ImageLocality 0 + SelectorSpread 10 + NodePreferAvoid 10 + InterPodAffinity 0, x 2
+    assert cfg.const_score == 2 * (1 + 0 + 10 + 10 + 0)
+
+
+def test_1_0_policy_custom_priority_unsupported():
+    (c,) = [c for c in load("policy") if c["version"] == "1.0"]
+    with pytest.raises(abi.KsimUnsupported):
+        policy.key_sets(policy.decode(c["json"]))
+
+
+def test_missing_sections_use_default_provider_and_mandatory_predicate():
+    preds, prios, _ = policy.key_sets(policy.decode({"kind": "Policy"}))
+    d_preds, d_prios = scheduler.provider("DefaultProvider")
+    assert sorted(preds) == sorted(d_preds) and prios == d_prios
+    preds, prios, _ = policy.key_sets(policy.decode({"predicates": [{"name": "PodFitsResources"}],
+                                                      "priorities": [{"name": "MostRequestedPriority", "weight": 3}]}))
+    assert "CheckNodeCondition" in preds  # plugins.go:401-406 mandatory predicate
+    assert scheduler.make_config(["PodFitsResources"], []).predicates & abi.P_CHECK_NODE_CONDITION
+
+
+def test_label_presence_predicate_and_flags():
+    preds, _, lp = policy.key_sets(policy.decode({"predicates": [
+        {"name": "CheckNodeLabelPresence", "argument": {"labelsPresence": {"labels": ["retiring"], "presence": False}}}],
+        "priorities": [{"name": "LeastRequestedPriority", "weight": 1}]}))
+    assert lp == (["retiring"], False) and "CheckNodeLabelPresence" in preds
+    fl = scheduler.label_presence_flags([{}, {"retiring": "2026"}, {"zone": "a"}], [0, 1, 2, 1], lp)
+    assert list(fl) == [0, abi.N_LABEL_PRESENCE, 0, abi.N_LABEL_PRESENCE]
+    assert scheduler.make_config(preds, []).predicates & abi.P_LABEL_PRESENCE
+
+
+def test_extenders_and_always_check_all_unsupported():
+    with pytest.raises(abi.KsimUnsupported):
+        policy.key_sets(policy.decode({"extenders": [{"urlPrefix": "http://x", "filterVerb": "filter"}]}))
+    with pytest.raises(abi.KsimUnsupported):
+        policy.key_sets(policy.decode({"alwaysCheckAllPredicates": True}))
+
+
+# ----------------------------------------------------------------------------- GPU: policy runs
+GPU_POLICIES = {
+    "absent_rank": {"predicates": [{"name": "GeneralPredicates"}, {"name": "PodToleratesNodeTaints"},
+                                   {"name": "CheckNodeLabelPresence",
+                                    "argument": {"labelsPresence": {"labels": ["rank"], "presence": False}}}],
+                    "priorities": [{"name": "LeastRequestedPriority", "weight": 1},
+                                   {"name": "ImageLocalityPriority", "weight": 2}]},
+    "present_tier_disk": {"predicates": [{"name": "PodFitsResources"}, {"name": "MatchNodeSelector"},
+                                         {"name": "CheckNodeLabelPresence",
+                                          "argument": {"labelsPresence": {"labels": ["tier", "disk"], "presence": True}}}],
+                          "priorities": [{"name": "MostRequestedPriority", "weight": 3},
+                                         {"name": "BalancedResourceAllocation", "weight": 1},
+                                         {"name": "EqualPriority", "weight": 1}]},
+    "defaults_1_9_like": {"kind": "Policy"},
+}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [abi.MODE_LAUNCH, abi.MODE_AUTO, abi.MODE_TREE])
+@pytest.mark.parametrize("name", sorted(GPU_POLICIES))
+def test_gpu_policy_run_matches_oracle(name, mode):
+    """A Policy file through ClusterCapacity(policy_obj=...) vs the oracle run with the same key
+    sets and the CheckNodeLabelPresence closure (predicates.go:875-910)."""
+    import ksim_ref as R
+    from workloads import rnd_workload
+    pol = policy.decode(GPU_POLICIES[name])
+    preds, prios, lp = policy.key_sets(pol)
+    custom = {"CheckNodeLabelPresence": R.new_node_label_predicate(*lp)} if lp else None
+    for seed in (3, 11):
+        nodes, running, pods = rnd_workload(seed, n_nodes=31 + seed, n_pods=140)
+        want, lni = R.simulate(nodes, running, pods, set(preds), list(prios), custom)
+        rep = scheduler.ClusterCapacity(nodes, running, pods, policy_obj=pol, mode=mode).run()
+        got = {n: (h, None) for n, h in rep.successful}
+        got.update({n: (None, m) for n, m in rep.failed})
+        assert [n for n, _ in rep.successful] == [n for n, h, _ in want if h is not None]
+        for pod, host, msg in want:
+            assert got[pod] == (host, msg), pod
+        assert rep.last_node_index == lni
+        if lp and not lp[1]:
+            assert any("didn't have the requested labels" in (m or "") for _, _, m in want)
