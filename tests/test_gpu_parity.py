@@ -597,7 +597,7 @@ def test_no_nodes_is_err_no_nodes_available():
     rep = cc.run()
     assert rep.successful == [] and [m for _, m in rep.failed] == ["no nodes available to schedule pods"] * 2
     assert rep.stop_reason == "Fail to get next pod: No pods left\n"
-    assert rep.review["review"]["failed"][0]["status"]["reason"] == "Unschedulable"
+    assert [p["reason"] for p in rep.review["review"]["failed"]["status"]["pods"]] == ["Unschedulable"] * 2
 
 
 @pytest.mark.parametrize("mode", MODES)
