@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 2
+#define KSIM_ABI_VERSION 3
 
 /* ---- status codes ---- */
 #define KSIM_OK 0
@@ -39,14 +39,14 @@ extern "C" {
 
 #define KSIM_MAX_SCALAR 8   /* extended / hugepage resource columns */
 #define KSIM_MAX_RCLASS 16  /* reduce classes per pod (TaintToleration x NodeAffinity) */
-#define KSIM_NREASONS 24    /* failure-reason histogram slots */
+#define KSIM_NREASONS 28    /* failure-reason histogram slots */
 #define KSIM_MAX_RANKS 8    /* devices of one node-sharded cluster */
 
 /* ---- predicate key bits: the FitPredicate keys of predicates.go:129-138 that carry
- *      logic for supported pods.  The volume / inter-pod-affinity keys (NoDiskConflict,
- *      MaxEBS/GCEPD/AzureDiskVolumeCount, CheckVolumeBinding, NoVolumeZoneConflict,
- *      MatchInterPodAffinity) are true for pods without volumes or affinity terms and
- *      need no bit: the host rejects pods that would make them non-trivial. ---- */
+ *      logic for supported pods.  The volume keys (NoDiskConflict, MaxEBS/GCEPD/
+ *      AzureDiskVolumeCount, CheckVolumeBinding, NoVolumeZoneConflict) are true for pods
+ *      without volumes and need no bit: the host rejects pods that would make them
+ *      non-trivial. ---- */
 #define KSIM_P_CHECK_NODE_CONDITION (1u << 0)     /* predicates.go:1534 */
 #define KSIM_P_CHECK_NODE_UNSCHEDULABLE (1u << 1) /* CheckNodeUnschedulablePredicate */
 #define KSIM_P_GENERAL (1u << 2)                  /* predicates.go:1059 */
@@ -61,18 +61,22 @@ extern "C" {
 #define KSIM_P_LABEL_PRESENCE (1u << 11)          /* CheckNodeLabelPresence with a labelsPresence
                                                      argument (predicates.go:875-910); the node's
                                                      verdict is the KSIM_N_LABEL_PRESENCE bit */
+#define KSIM_P_INTERPOD_AFFINITY (1u << 12)       /* MatchInterPodAffinity (predicates.go:1143-1450),
+                                                     over the tables of ksim_load_affinity */
 
 /* ---- priority weight slots (0 = not configured).  Priorities that evaluate to the
  *      same value on every node under supported inputs (SelectorSpread /
  *      ServiceSpreading with no selectors, NodePreferAvoidPods for pods without an
- *      RC/RS owner, InterPodAffinity without affinity terms, EqualPriority) do not
- *      change placements; their sum goes in ksim_config.const_score. ---- */
+ *      RC/RS owner, EqualPriority) do not change placements; their sum goes in
+ *      ksim_config.const_score. ---- */
 #define KSIM_W_LEAST_REQUESTED 0     /* least_requested.go:36 */
 #define KSIM_W_MOST_REQUESTED 1      /* most_requested.go:34 */
 #define KSIM_W_BALANCED 2            /* balanced_resource_allocation.go:39 */
 #define KSIM_W_TAINT_TOLERATION 3    /* taint_toleration.go:55 + NormalizeReduce(10,true) */
 #define KSIM_W_NODE_AFFINITY 4       /* node_affinity.go:34 + NormalizeReduce(10,false) */
-#define KSIM_NW 5
+#define KSIM_W_INTERPOD_AFFINITY 5   /* interpod_affinity.go:118-240 (0 everywhere without
+                                        affinity tables or terms) */
+#define KSIM_NW 6
 
 /* ---- node condition / dynamic flags (ksim_node_table.flags) ---- */
 #define KSIM_N_NOT_READY (1u << 0)      /* Ready condition present, status != True */
@@ -109,6 +113,12 @@ extern "C" {
 #define KSIM_R_DISK_PRESSURE 14
 #define KSIM_R_LABEL_PRESENCE 15
 #define KSIM_R_INSUFFICIENT_SCALAR0 16 /* +column, up to KSIM_MAX_SCALAR */
+/* MatchInterPodAffinity fails with two reasons (predicates.go:1149-1160): the generic one
+ * plus the rule that failed (algorithm/predicates/error.go:40-47) */
+#define KSIM_R_POD_AFFINITY 24            /* node(s) didn't match pod affinity/anti-affinity */
+#define KSIM_R_EXISTING_ANTI_AFFINITY 25  /* node(s) didn't satisfy existing pods anti-affinity rules */
+#define KSIM_R_AFFINITY_RULES 26          /* node(s) didn't match pod affinity rules */
+#define KSIM_R_ANTI_AFFINITY_RULES 27     /* node(s) didn't match pod anti-affinity rules */
 
 /* ---- execution modes ---- */
 #define KSIM_MODE_AUTO 0        /* library picks (persistent when it fits) */
@@ -195,7 +205,9 @@ typedef struct {
   int32_t port_cnt;
   int32_t scalar_off;  /* into the scalar-request array */
   int32_t scalar_cnt;
-  int32_t reserved[5]; /* library-owned scratch (callers pass anything; never read back) */
+  int32_t aff_ident;   /* 1 + identity in the affinity tables (ksim_load_affinity); 0: none */
+  int32_t aff_class;   /* 1 + affinity class (own and carried terms); 0: none */
+  int32_t reserved[3]; /* library-owned scratch (callers pass anything; never read back) */
 } ksim_pod;
 
 typedef struct {
@@ -360,6 +372,83 @@ int ksim_node_count(ksim_handle* h, int64_t* out);
  * reloaded first (ksim_load_classes may be called again with a superset). */
 int ksim_append_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const uint64_t* ports, int64_t n_ports,
                      const ksim_scalar_req* scalars, int64_t n_scalars);
+
+/* ==== Inter-pod affinity (MatchInterPodAffinity, InterPodAffinityPriority) ==================
+ * Reference: algorithm/predicates/predicates.go:1143-1450 (+ metadata.go:102-123),
+ * algorithm/priorities/interpod_affinity.go:118-240, priorities/util/topologies.go:28-71.
+ * The host interns every string test (ksim/affinity.py):
+ *  - topology keys k: dom[k][n] = node n's domain under key k (its value of label k, interned),
+ *    -1 when the node lacks the label.  Keys 0 and 1 are pseudo keys: 0 puts every node in
+ *    domain 0 ("a matching pod exists anywhere"), 1 puts node n in domain n (hostname terms,
+ *    which look only at the node's own pods, predicates.go:1176-1179);
+ *  - selectors s: a term's (namespaces, label selector) as its defining pod resolves them;
+ *  - identities (namespace, labels) of pods: bit s of ident_sel[i][.] (sel_words 64-bit words per
+ *    identity) = the identity matches selector s; bit e of ident_anti / ident_prio[i][.]
+ *    (carry_words words) = it matches carried term e (required anti-affinity / priority terms);
+ *  - counted pairs (s, k): per domain of k, the number of placed pods matching s;
+ *  - carried terms e: terms of placed pods acting on later pods: per domain of the term's
+ *    key, the number (required anti-affinity) or summed signed weight (priority terms) of placed
+ *    pods carrying it;
+ *  - affinity classes: a pod's own terms (required affinity, then required anti-affinity, then
+ *    preferred) and the carried amounts it brings; ac[a] = {req_off, req_cnt, pref_off, pref_cnt,
+ *    carry_off, carry_cnt}.
+ * ksim_pod.aff_ident / aff_class hold 1 + the id (0 = none, so zero-initialised descriptors
+ * take no part).  A pod with either set is scheduled by the launch-mode kernels, which apply
+ * its counts on commit; the node events (ksim_node_add / update / remove) make the tables stale
+ * until they are loaded again. */
+#define KSIM_AFF_REQ_AFFINITY 0  /* required pod affinity term */
+#define KSIM_AFF_REQ_ANTI 1      /* required pod anti-affinity term */
+#define KSIM_AFF_PREFERRED 2     /* preferred term (affinity: +weight, anti-affinity: -weight) */
+#define KSIM_AFF_CARRY_ANTI 0    /* carried: an existing pod's required anti-affinity */
+#define KSIM_AFF_CARRY_PRIO 1    /* carried: symmetric priority term (hard weight or +-weight) */
+#define KSIM_AFF_MAX_SEL 65536
+#define KSIM_AFF_MAX_CARRY 65536
+
+typedef struct {
+  int32_t kind;        /* KSIM_AFF_REQ_AFFINITY / _REQ_ANTI / _PREFERRED */
+  int32_t pair;        /* counted pair read at the node's domain */
+  int32_t gate_key;    /* required terms: key the node must carry */
+  int32_t exist_pair;  /* required affinity: a count > 0 at the node's domain = a matching pod exists */
+  int32_t self_ok;     /* required affinity: the pod matches its own term */
+  int32_t pad;
+  int64_t weight;      /* preferred: signed weight */
+} ksim_aff_term;
+
+typedef struct {
+  int32_t term;        /* carried term */
+  int32_t pad;
+  int64_t amount;      /* 1 (required anti-affinity) or the signed priority weight */
+} ksim_aff_carry;
+
+typedef struct {
+  int32_t n_keys, n_sel, n_ident, n_pair, n_carry, n_aclass;
+  int32_t n_terms, n_carries;
+  int64_t n_nodes;                 /* must equal the loaded node table's */
+  int64_t cnt_len, carried_len;
+  int32_t hard_weight;             /* hardPodAffinitySymmetricWeight the carried amounts use */
+  int32_t sel_words;               /* ceil(n_sel / 64) */
+  int32_t carry_words;             /* ceil(n_carry / 64) */
+  int32_t pad;
+  const int32_t* dom;              /* [n_keys][n_nodes] */
+  const int32_t* n_dom;            /* [n_keys] */
+  const uint64_t* ident_sel;       /* [n_ident][sel_words] */
+  const uint64_t* ident_anti;      /* [n_ident][carry_words] */
+  const uint64_t* ident_prio;      /* [n_ident][carry_words] */
+  const int32_t* pair_sel;         /* [n_pair] */
+  const int32_t* pair_key;         /* [n_pair] */
+  const int64_t* pair_off;         /* [n_pair] into cnt (n_dom[pair_key] entries) */
+  const int32_t* carry_key;        /* [n_carry] */
+  const int32_t* carry_kind;       /* [n_carry] KSIM_AFF_CARRY_* */
+  const int64_t* carry_off;        /* [n_carry] into carried */
+  const int32_t* ac;               /* [n_aclass][6] */
+  const ksim_aff_term* terms;      /* [n_terms] */
+  const ksim_aff_carry* carries;   /* [n_carries] */
+  const int32_t* cnt;              /* [cnt_len] counts of the pods already placed */
+  const int64_t* carried;          /* [carried_len] */
+} ksim_affinity_tables;
+
+/* Load (or replace) the affinity tables; the counts describe the pods already placed. */
+int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t);
 
 int ksim_read_nodes(ksim_handle* h, ksim_node_state* out);
 int ksim_get_counter(ksim_handle* h, uint64_t* out);

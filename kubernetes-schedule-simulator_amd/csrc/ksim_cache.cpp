@@ -176,6 +176,11 @@ int check_ready(ksim_handle* h, const char* where) {
   return KSIM_OK;
 }
 
+// A node event: the affinity tables' per-node domains no longer describe the table.
+void node_event(ksim_handle* h) {
+  if (h->have_aff) h->aff_stale = true;
+}
+
 int check_pod_args(ksim_handle* h, const ksim_pod* pod, int32_t n_ports, int32_t n_scalars, const uint64_t* ports,
                    const ksim_scalar_req* scalars, const char* where) {
   if (!pod) return ksim_fail(h, KSIM_E_INVAL, "%s: null pod", where);
@@ -184,6 +189,10 @@ int check_pod_args(ksim_handle* h, const ksim_pod* pod, int32_t n_ports, int32_t
   if (pod->port_cnt < 0 || pod->port_off < 0 || (int64_t)pod->port_off + pod->port_cnt > n_ports)
     return ksim_fail(h, KSIM_E_INVAL, "%s: port range out of bounds", where);
   return KSIM_OK;
+}
+
+bool ksim_is_aff_host(const ksim_handle* h, const ksim_pod& p) {
+  return h->have_aff && (p.aff_ident || p.aff_class);
 }
 
 int after_commit(ksim_handle* h, int32_t port_cnt) {
@@ -298,6 +307,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   if ((rc = check_pod_args(h, pod, n_ports, n_scalars, ports, scalars, "ksim_schedule_one"))) return rc;
   KsimCtx& c = h->ctx;
   if (c.n == 0) return ksim_fail(h, KSIM_E_NO_NODES, "no nodes available to schedule pods");
+  if ((rc = ksim_rt_check_aff(h, "ksim_schedule_one"))) return rc;
   // room for the pod's ports if it is assumed (and at least one slot column to test against)
   if ((assume || c.port_slots == 0) && (rc = ensure_port_room(h, pod->port_cnt))) return rc;
   if ((rc = ksim_rt_check_pod(h, *pod, n_ports, n_scalars, scalars, "ksim_schedule_one"))) return rc;
@@ -310,7 +320,10 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   const int grid = (int)((c.n + cs.chunk - 1) / cs.chunk);
   if ((rc = ksim_rt_ensure_partials(h, grid))) return rc;
   cs.partials = c.partials;
-  hipError_t e = ksim_launch_scan(&cs, npt, 1, grid, h->stream);
+  hipError_t e = hipSuccess;
+  if (ksim_is_aff_host(h, *pod) && c.w[KSIM_W_INTERPOD_AFFINITY] && !c.no_prio)
+    e = ksim_launch_ipa_pass(&cs, npt, grid, h->stream);  // InterPodAffinityPriority's min / max first
+  if (e == hipSuccess) e = ksim_launch_scan(&cs, npt, 1, grid, h->stream);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "scan launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipMemcpyAsync(h->res_host, h->res_dev, KSIM_RES_WORDS * 4, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipMemcpyAsync(h->ctr_host, c.counter, 8, hipMemcpyDeviceToHost, h->stream));
@@ -334,6 +347,7 @@ static int pod_delta(ksim_handle* h, int64_t node, const ksim_pod* pod, const ui
   if (rc) return rc;
   if ((rc = check_pod_args(h, pod, n_ports, n_scalars, ports, scalars, where))) return rc;
   if (node < 0 || node >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "%s: node %lld out of range", where, (long long)node);
+  if ((rc = ksim_rt_check_aff(h, where))) return rc;
   if (add && (rc = ensure_port_room(h, pod->port_cnt))) return rc;
   ksim_pod p = *pod;
   p.host = -1;  // spec.nodeName plays no part in a resource delta (the node is given)
@@ -367,7 +381,9 @@ int ksim_assume(ksim_handle* h, int64_t pod, int64_t node) {
   if (!h->have_pods) return ksim_fail(h, KSIM_E_STATE, "ksim_assume: nothing loaded");
   if (pod < 0 || pod >= h->n_pods || node < 0 || node >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "ksim_assume: out of range");
   HIPCHK(h, hipSetDevice(h->device));
-  int rc = ensure_staging(h, 0, 0);
+  int rc = ksim_rt_check_aff(h, "ksim_assume");
+  if (rc) return rc;
+  rc = ensure_staging(h, 0, 0);
   if (rc) return rc;
   HIPCHK(h, hipMemsetAsync(h->res_dev, 0, KSIM_RES_WORDS * 4, h->stream));
   hipError_t e = ksim_launch_assume(&h->ctx, pod, node, h->res_dev + KSIM_RES_STATUS, h->stream);
@@ -387,6 +403,7 @@ int ksim_node_add(ksim_handle* h, int64_t index, const ksim_node_row* row) {
       (rc = grow_port_slots(h, std::max({row->port_count, 2 * h->ctx.port_slots, 4}))))
     return rc;
   if ((rc = node_shift(h, KSIM_RELAY_INSERT, index))) return rc;
+  node_event(h);
   if ((rc = set_row(h, index, row, true))) return rc;
   h->port_bound = std::max<int64_t>(h->port_bound, row->port_count);
   h->max_label_set = std::max(h->max_label_set, row->label_set);
@@ -400,6 +417,7 @@ int ksim_node_update(ksim_handle* h, int64_t index, const ksim_node_row* row) {
   if (index < 0 || index >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "ksim_node_update: rank %lld out of range", (long long)index);
   if ((rc = check_row(h, row, false, "ksim_node_update"))) return rc;
   if ((rc = set_row(h, index, row, false))) return rc;
+  node_event(h);                 // labels may have changed: topology domains
   ksim_rt_invalidate_layout(h);  // allocatable feeds the trees' and sweeps' derived columns
   h->max_label_set = std::max(h->max_label_set, row->label_set);
   h->max_taint_set = std::max(h->max_taint_set, row->taint_set);
@@ -410,6 +428,7 @@ int ksim_node_remove(ksim_handle* h, int64_t index) {
   int rc = check_ready(h, "ksim_node_remove");
   if (rc) return rc;
   if (index < 0 || index >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "ksim_node_remove: rank %lld out of range", (long long)index);
+  node_event(h);
   return node_shift(h, KSIM_RELAY_REMOVE, index);
 }
 

@@ -28,6 +28,31 @@ struct __attribute__((aligned(16))) KsimPartial {
   int32_t hist[KSIM_NREASONS];   // failure reasons (only when collecting)
 };
 
+// Inter-pod affinity tables on the device (ksim_load_affinity; layout in include/ksim.h).
+struct KsimAff {
+  int64_t n;                       // nodes (the dom stride)
+  const int32_t* __restrict__ dom; // [n_keys][n]
+  const uint64_t* __restrict__ ident_sel;
+  const uint64_t* __restrict__ ident_anti;
+  const uint64_t* __restrict__ ident_prio;
+  const int32_t* __restrict__ pair_sel;
+  const int32_t* __restrict__ pair_key;
+  const int64_t* __restrict__ pair_off;
+  const int32_t* __restrict__ carry_key;
+  const int64_t* __restrict__ carry_off;
+  const int32_t* __restrict__ ac;  // [n_aclass][6]
+  const ksim_aff_term* __restrict__ terms;
+  const ksim_aff_carry* __restrict__ carries;
+  int32_t* cnt;                    // counted pairs, per domain
+  int64_t* carried;                // carried terms, per domain
+  int64_t* mm;                     // [2] min / max of the raw priority over the fit nodes (pass A)
+  int64_t* part;                   // [grid][2] pass A block partials
+  uint32_t* ticket;                // pass A arrival counter
+  int32_t n_pair;
+  int32_t sel_words, carry_words;
+  int32_t pad;
+};
+
 struct KsimCtx {
   // ---- node table (name-rank order) ----
   int64_t n;
@@ -87,6 +112,7 @@ struct KsimCtx {
   int64_t chunk;          // nodes per block
   uint64_t* dbg;          // diagnostic stamp sums (KSIM_STAMPS builds only), else null
   int32_t* out_fit;       // optional (per-pod drop-in): [0] = len(filtered), [1] |= ksim_row_status
+  const KsimAff* aff;     // inter-pod affinity tables (device), null when none are loaded
 };
 
 // Node-sharded mode (ksim_shard_*): this rank's place in the world and every rank's exchange
@@ -249,6 +275,122 @@ __device__ __forceinline__ uint32_t ksim_selector(const ksim_pod& P, int64_t i, 
   return a.sel_ok(P, i) ? 0u : (1u << KSIM_R_NODE_SELECTOR);
 }
 
+// ---- inter-pod affinity (tables: include/ksim.h, ksim/affinity.py) ----
+__device__ __forceinline__ int32_t ksim_dom(const KsimAff& A, int32_t key, int64_t i) {
+  return A.dom[(int64_t)key * A.n + i];
+}
+
+// A count > 0 of counted pair `pair` at node i's domain of the pair's key.
+__device__ __forceinline__ bool ksim_pair_hit(const KsimAff& A, int32_t pair, int64_t i) {
+  const int32_t d = ksim_dom(A, A.pair_key[pair], i);
+  return d >= 0 && A.cnt[A.pair_off[pair] + d] > 0;
+}
+
+// InterPodAffinityMatches (predicates.go:1143-1160) for pod P on node i: existing pods'
+// required anti-affinity terms that P matches (satisfiesExistingPodsAntiAffinity, :1340-1379),
+// then P's required affinity terms (anyPodMatchesPodAffinityTerm, :1161-1194; a term nobody
+// matches is waived when P matches it itself, :1405-1424), then its required anti-affinity
+// terms (:1430-1441).  Reason mask, 0 = fits.  Out of line: only affinity pods call it.
+__device__ __noinline__ uint32_t ksim_interpod_pred(const KsimAff& A, const ksim_pod& P, int64_t i) {
+  const uint32_t base = 1u << KSIM_R_POD_AFFINITY;
+  if (P.aff_ident > 0) {
+    const uint64_t* mw = A.ident_anti + (int64_t)(P.aff_ident - 1) * A.carry_words;
+    for (int32_t w = 0; w < A.carry_words; ++w) {
+      uint64_t m = mw[w];
+      while (m) {
+        const int e = 64 * w + __builtin_ctzll(m);
+        m &= m - 1;
+        const int32_t d = ksim_dom(A, A.carry_key[e], i);
+        if (d >= 0 && A.carried[A.carry_off[e] + d] > 0) return base | (1u << KSIM_R_EXISTING_ANTI_AFFINITY);
+      }
+    }
+  }
+  if (P.aff_class <= 0) return 0;
+  const int32_t* ac = A.ac + 6 * (int64_t)(P.aff_class - 1);
+  for (int32_t j = ac[0], e = ac[0] + ac[1]; j < e; ++j) {
+    const ksim_aff_term t = A.terms[j];
+    const bool match = ksim_dom(A, t.gate_key, i) >= 0 && ksim_pair_hit(A, t.pair, i);
+    if (t.kind == KSIM_AFF_REQ_AFFINITY) {
+      if (!match && (!t.self_ok || ksim_pair_hit(A, t.exist_pair, i))) return base | (1u << KSIM_R_AFFINITY_RULES);
+    } else if (match) {
+      return base | (1u << KSIM_R_ANTI_AFFINITY_RULES);
+    }
+  }
+  return 0;
+}
+
+// Does pod P read the InterPodAffinity priority (own preferred terms, or carried priority
+// terms its identity matches)?
+__device__ __forceinline__ bool ksim_interpod_prio_work(const KsimAff& A, const ksim_pod& P) {
+  if (P.aff_class > 0 && A.ac[6 * (int64_t)(P.aff_class - 1) + 3] > 0) return true;
+  if (P.aff_ident <= 0) return false;
+  const uint64_t* mw = A.ident_prio + (int64_t)(P.aff_ident - 1) * A.carry_words;
+  for (int32_t w = 0; w < A.carry_words; ++w)
+    if (mw[w]) return true;
+  return false;
+}
+
+// CalculateInterPodAffinityPriority's per-node sum (interpod_affinity.go:124-214) before
+// normalisation: P's preferred terms weight the placed pods they match in the node's domain,
+// the carried terms of placed pods P matches add their per-domain amounts.
+__device__ __noinline__ int64_t ksim_interpod_raw(const KsimAff& A, const ksim_pod& P, int64_t i) {
+  int64_t s = 0;
+  if (P.aff_class > 0) {
+    const int32_t* ac = A.ac + 6 * (int64_t)(P.aff_class - 1);
+    for (int32_t j = ac[2], e = ac[2] + ac[3]; j < e; ++j) {
+      const ksim_aff_term t = A.terms[j];
+      const int32_t d = ksim_dom(A, A.pair_key[t.pair], i);
+      if (d >= 0) s += t.weight * (int64_t)A.cnt[A.pair_off[t.pair] + d];
+    }
+  }
+  if (P.aff_ident > 0) {
+    const uint64_t* mw = A.ident_prio + (int64_t)(P.aff_ident - 1) * A.carry_words;
+    for (int32_t w = 0; w < A.carry_words; ++w) {
+      uint64_t m = mw[w];
+      while (m) {
+        const int e = 64 * w + __builtin_ctzll(m);
+        m &= m - 1;
+        const int32_t d = ksim_dom(A, A.carry_key[e], i);
+        if (d >= 0) s += A.carried[A.carry_off[e] + d];
+      }
+    }
+  }
+  return s;
+}
+
+// fScore = MaxPriority * ((count - min) / (max - min)) in float64, truncated (:228-236); the
+// counts are integers below 2^53, so the float64 operands are exact as in Go.
+__device__ __forceinline__ int64_t ksim_interpod_score(int64_t raw, int64_t mn, int64_t mx) {
+  if (mx - mn <= 0) return 0;
+  return (int64_t)(10.0 * ((double)(raw - mn) / (double)(mx - mn)));
+}
+
+// NodeInfo.AddPod / RemovePod of an affinity pod on node w (sign +1 / -1): every counted pair
+// whose selector its identity matches, and the amounts of the terms it carries.  Single thread.
+__device__ __noinline__ void ksim_aff_commit(const KsimAff& A, const ksim_pod& P, int64_t w, int32_t sign) {
+  if (P.aff_ident > 0) {
+    const uint64_t* sm = A.ident_sel + (int64_t)(P.aff_ident - 1) * A.sel_words;
+    for (int32_t c = 0; c < A.n_pair; ++c) {
+      const int32_t s = A.pair_sel[c];
+      if (!((sm[s >> 6] >> (s & 63)) & 1ull)) continue;
+      const int32_t d = ksim_dom(A, A.pair_key[c], w);
+      if (d >= 0) A.cnt[A.pair_off[c] + d] += sign;
+    }
+  }
+  if (P.aff_class > 0) {
+    const int32_t* ac = A.ac + 6 * (int64_t)(P.aff_class - 1);
+    for (int32_t j = ac[4], e = ac[4] + ac[5]; j < e; ++j) {
+      const ksim_aff_carry k = A.carries[j];
+      const int32_t d = ksim_dom(A, A.carry_key[k.term], w);
+      if (d >= 0) A.carried[A.carry_off[k.term] + d] += (int64_t)sign * k.amount;
+    }
+  }
+}
+
+__device__ __forceinline__ bool ksim_is_aff_pod(const KsimCtx& c, const ksim_pod& P) {
+  return c.aff && (P.aff_ident > 0 || P.aff_class > 0);
+}
+
 // Reason mask of the first failing predicate in predicatesOrdering (predicates.go:129-138,
 // core/generic_scheduler.go:467-528); 0 = fits.
 template <class A>
@@ -293,6 +435,8 @@ __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ks
   if ((pr & KSIM_P_MEM_PRESSURE) && (P.flags & KSIM_POD_BEST_EFFORT) && (r.fl & KSIM_N_MEM_PRESSURE))
     return 1u << KSIM_R_MEM_PRESSURE;
   if ((pr & KSIM_P_DISK_PRESSURE) && (r.fl & KSIM_N_DISK_PRESSURE)) return 1u << KSIM_R_DISK_PRESSURE;
+  if ((pr & KSIM_P_INTERPOD_AFFINITY) && c.aff && (P.aff_ident > 0 || P.aff_class > 0))
+    return ksim_interpod_pred(*c.aff, P, i);
   return 0;
 }
 

@@ -23,6 +23,7 @@
 extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* fit, uint32_t* reasons, int64_t* score,
                                        uint8_t* rcls, hipStream_t s);
+extern "C" hipError_t ksim_launch_ipa_pass(const KsimCtx* c, int npt, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, int32_t* status, hipStream_t s);
 extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
                                              int lds_rows, hipStream_t s);
@@ -91,7 +92,7 @@ struct ksim_handle {
   // launch-mode graph
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
-  int g_batch = 0, g_npt = 0, g_collect = -1, part_cap = 0;
+  int g_batch = 0, g_npt = 0, g_collect = -1, g_ipa = -1, part_cap = 0;
   uint64_t* granules = nullptr;
   KsimCtx* ctx_dev = nullptr;  // device copy of ctx for non-inlined device functions
   size_t gran_bytes = 0;
@@ -142,6 +143,15 @@ struct ksim_handle {
   int32_t* res_host = nullptr;  // pinned
   uint64_t* ctr_host = nullptr; // pinned copy of lastNodeIndex after a call
   int64_t port_bound = 0;       // upper bound of max(port_count) over the nodes
+  // inter-pod affinity (ksim_load_affinity): the device tables, their sizes for validation, and
+  // per queued pod its identity / class (an affinity pod takes the launch-mode kernels)
+  bool have_aff = false;
+  bool aff_stale = false;       // a node event changed the table the domains describe
+  int32_t aff_n_ident = 0, aff_n_aclass = 0;
+  KsimAff* aff_dev = nullptr;
+  std::vector<void*> aff_bufs;
+  std::vector<int32_t> q_ident, q_aclass;
+  std::vector<int64_t> aff_pre;  // aff_pre[i] = affinity pods among the first i queued
 };
 
 int ksim_fail(ksim_handle* h, int code, const char* fmt, ...);
@@ -212,4 +222,8 @@ void ksim_rt_invalidate_layout(ksim_handle* h);
 int ksim_rt_check_pod(ksim_handle* h, const ksim_pod& p, int64_t n_ports, int64_t n_scalars,
                       const ksim_scalar_req* scalars, const char* where);
 int ksim_rt_ensure_partials(ksim_handle* h, int grid);
+// Affinity pods among queued pods [first, first+count).
+int64_t ksim_rt_aff_count(const ksim_handle* h, int64_t first, int64_t count);
+// KSIM_E_STATE when the affinity tables are stale (a node event since they were loaded).
+int ksim_rt_check_aff(ksim_handle* h, const char* where);
 int ksim_rt_pick_npt(int64_t n);

@@ -60,10 +60,28 @@ struct Decision {
 
 }  // namespace
 
-// Evaluate one node for the scan: fit, map score, reduce class, reason mask.
+// InterPodAffinityPriority inputs of one pod: whether it reads the priority and the min / max
+// of its raw per-node sums over the fit nodes (written by ksim_ipa_pass_kernel just before).
+struct IpaNorm {
+  bool on;
+  int64_t mn, mx, w;
+};
+
+__device__ __forceinline__ IpaNorm ipa_norm(const KsimCtx& c, const ksim_pod& P) {
+  IpaNorm z{false, 0, 0, 0};
+  if (!c.aff || c.no_prio || c.w[KSIM_W_INTERPOD_AFFINITY] == 0 || !ksim_interpod_prio_work(*c.aff, P)) return z;
+  z.on = true;
+  z.mn = c.aff->mm[0];
+  z.mx = c.aff->mm[1];
+  z.w = c.w[KSIM_W_INTERPOD_AFFINITY];
+  return z;
+}
+
+// Evaluate one node for the scan: fit, map score (+ the normalised InterPodAffinity score),
+// reduce class, reason mask.
 template <bool COLLECT>
 __device__ __forceinline__ void eval_one(const KsimCtx& c, const ksim_pod& P, int64_t i, int k1, int k2,
-                                         bool& fit, int64_t& score, int& cls, uint32_t& rmask) {
+                                         const IpaNorm& ipa, bool& fit, int64_t& score, int& cls, uint32_t& rmask) {
   fit = false; score = 0; cls = 0; rmask = 0;
   if (i >= c.n) return;
   const KsimRow r = ksim_load_row(c, i);
@@ -71,6 +89,9 @@ __device__ __forceinline__ void eval_one(const KsimCtx& c, const ksim_pod& P, in
   fit = (m == 0);
   if (COLLECT) rmask = m;
   score = ksim_map_score(c, P, r);
+  if (ipa.on && fit)
+    score = (int64_t)((uint64_t)score +
+                      (uint64_t)ipa.w * (uint64_t)ksim_interpod_score(ksim_interpod_raw(*c.aff, P, i), ipa.mn, ipa.mx));
   cls = (k1 * k2 > 1) ? ksim_rclass(c, P, i, k1, k2) : 0;
 }
 
@@ -93,6 +114,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
   const int K = k1 * k2;
   const int64_t base = (int64_t)blockIdx.x * c.chunk;
+  const IpaNorm ipa = ipa_norm(c, P);
 
   if (COLLECT && tid < KSIM_NREASONS) s_hist[tid] = 0;
 
@@ -102,7 +124,8 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   int cl[NPT];
   uint32_t rm[NPT];
 #pragma unroll
-  for (int k = 0; k < NPT; ++k) eval_one<COLLECT>(c, P, base + k * KSIM_BLOCK + tid, k1, k2, fit[k], sc[k], cl[k], rm[k]);
+  for (int k = 0; k < NPT; ++k)
+    eval_one<COLLECT>(c, P, base + k * KSIM_BLOCK + tid, k1, k2, ipa, fit[k], sc[k], cl[k], rm[k]);
 
   int32_t nfit = 0;
 #pragma unroll
@@ -321,7 +344,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       bool f; int64_t sc1; int cl1; uint32_t rm1;
-      eval_one<false>(c, P, bb + k * KSIM_BLOCK + tid, k1, k2, f, sc1, cl1, rm1);
+      eval_one<false>(c, P, bb + k * KSIM_BLOCK + tid, k1, k2, ipa, f, sc1, cl1, rm1);
       bool match = f;
       if (D.mode == 2) match = f && ((D.winners >> cl1) & 1u) && sc1 == D.M[cl1];
       const uint64_t bal = __ballot(match);
@@ -345,6 +368,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       D.node = node;
       if (node >= 0 && !c.no_commit) {
         ksim_commit(c, P, node);
+        if (ksim_is_aff_pod(c, P)) ksim_aff_commit(*c.aff, P, node, 1);
         if (c.out_fit) c.out_fit[1] |= ksim_row_status(c, node);
       }
     }
@@ -354,6 +378,84 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     if (c.out_fit) c.out_fit[0] = D.fitTotal;
     *c.cursor = pod + 1;
     *c.ticket = 0;
+  }
+}
+
+// Pass A of an InterPodAffinityPriority pod (one launch before its scan): min / max of the raw
+// per-node sums over the fit nodes, with 0 folded in as the reference's accumulators start
+// there (interpod_affinity.go:129-131, 218-226).  Every block reduces its chunk to a partial;
+// the last block to arrive combines them into aff->mm and re-arms the ticket.  Pods that do
+// not read the priority exit at once (uniformly, so the launch costs only its dispatch).
+template <int NPT>
+__global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
+  __shared__ int64_t s_mn[KSIM_WAVES], s_mx[KSIM_WAVES];
+  __shared__ int s_last;
+  const int64_t pod = *c.cursor;
+  if (pod >= c.end || !c.aff || c.no_prio || c.w[KSIM_W_INTERPOD_AFFINITY] == 0) return;
+  const ksim_pod P = c.pods[pod];
+  const KsimAff& A = *c.aff;
+  if (!ksim_interpod_prio_work(A, P)) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t base = (int64_t)blockIdx.x * c.chunk;
+  int64_t mn = 0, mx = 0;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int64_t i = base + k * KSIM_BLOCK + tid;
+    if (i >= c.n) continue;
+    const KsimRow r = ksim_load_row(c, i);
+    if (ksim_predicates(c, P, i, r) != 0) continue;
+    const int64_t v = ksim_interpod_raw(A, P, i);
+    mn = v < mn ? v : mn;
+    mx = v > mx ? v : mx;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (lane == 0) { s_mn[wv] = mn; s_mx[wv] = mx; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < KSIM_WAVES; ++w) {
+      mn = s_mn[w] < mn ? s_mn[w] : mn;
+      mx = s_mx[w] > mx ? s_mx[w] : mx;
+    }
+    A.part[2 * blockIdx.x] = mn;
+    A.part[2 * blockIdx.x + 1] = mx;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(A.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (old == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  mn = 0;
+  mx = 0;
+  for (int b = tid; b < (int)gridDim.x; b += KSIM_BLOCK) {
+    const int64_t a = A.part[2 * b], z = A.part[2 * b + 1];
+    mn = a < mn ? a : mn;
+    mx = z > mx ? z : mx;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+  }
+  if (lane == 0) { s_mn[wv] = mn; s_mx[wv] = mx; }
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < KSIM_WAVES; ++w) {
+      mn = s_mn[w] < mn ? s_mn[w] : mn;
+      mx = s_mx[w] > mx ? s_mx[w] : mx;
+    }
+    A.mm[0] = mn;
+    A.mm[1] = mx;
+    *A.ticket = 0;
   }
 }
 
@@ -377,6 +479,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_
 __global__ void ksim_assume_kernel(KsimCtx c, int64_t pod, int64_t node, int32_t* status) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     ksim_commit(c, c.pods[pod], node);
+    if (ksim_is_aff_pod(c, c.pods[pod])) ksim_aff_commit(*c.aff, c.pods[pod], node, 1);
     *status |= ksim_row_status(c, node);
   }
 }
@@ -400,6 +503,16 @@ extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, i
     }
   }
 #undef KSIM_L
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ksim_launch_ipa_pass(const KsimCtx* c, int npt, int grid, hipStream_t s) {
+  switch (npt) {
+    case 1: hipLaunchKernelGGL((ksim_ipa_pass_kernel<1>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
+    case 2: hipLaunchKernelGGL((ksim_ipa_pass_kernel<2>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
+    case 4: hipLaunchKernelGGL((ksim_ipa_pass_kernel<4>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
+    default: hipLaunchKernelGGL((ksim_ipa_pass_kernel<8>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
+  }
   return hipGetLastError();
 }
 

@@ -39,7 +39,7 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
     if (cfg->weights[k] < 0) return ksim_fail(nullptr, KSIM_E_INVAL, "ksim_create: negative weight in slot %d", k);
   if (cfg->mode < KSIM_MODE_AUTO || cfg->mode > KSIM_MODE_TREE)
     return ksim_fail(nullptr, KSIM_E_INVAL, "ksim_create: unknown mode %d", cfg->mode);
-  const uint32_t known = (1u << 12) - 1;
+  const uint32_t known = (1u << 13) - 1;
   if (cfg->predicates & ~known) return ksim_fail(nullptr, KSIM_E_UNSUPPORTED, "ksim_create: unknown predicate bits");
   ksim_handle* h = new ksim_handle();
   h->device = cfg->device;
@@ -249,6 +249,21 @@ int ksim_rt_check_pod(ksim_handle* h, const ksim_pod& p, int64_t n_ports, int64_
   for (int32_t s = 0; s < p.scalar_cnt; ++s)
     if (scalars[p.scalar_off + s].col < 0 || scalars[p.scalar_off + s].col >= c.n_scalar)
       return ksim_fail(h, KSIM_E_INVAL, "%s: scalar request column out of range", where);
+  if ((p.aff_ident || p.aff_class) && !h->have_aff)
+    return ksim_fail(h, KSIM_E_STATE, "%s: affinity identity / class set but no affinity tables are loaded", where);
+  if (p.aff_ident < 0 || p.aff_ident > h->aff_n_ident || p.aff_class < 0 || p.aff_class > h->aff_n_aclass)
+    return ksim_fail(h, KSIM_E_INVAL, "%s: affinity identity / class out of range", where);
+  return KSIM_OK;
+}
+
+int64_t ksim_rt_aff_count(const ksim_handle* h, int64_t first, int64_t count) {
+  if (!h->have_aff || count <= 0) return 0;
+  return h->aff_pre[first + count] - h->aff_pre[first];
+}
+
+int ksim_rt_check_aff(ksim_handle* h, const char* where) {
+  if (h->have_aff && h->aff_stale)
+    return ksim_fail(h, KSIM_E_STATE, "%s: the affinity tables predate a node event; load them again", where);
   return KSIM_OK;
 }
 
@@ -258,7 +273,7 @@ static bool fast_base(const ksim_pod& p) {
   bool in_range = true;
   for (int64_t v : {p.req_cpu, p.req_mem, p.add_cpu, p.add_mem, p.nz_cpu, p.nz_mem}) in_range &= v >= 0 && v < lim;
   return in_range && p.host == -1 && p.port_cnt == 0 && p.scalar_cnt == 0 && p.req_gpu == 0 && p.req_eph == 0 &&
-         !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS));
+         !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS)) && p.aff_ident == 0 && p.aff_class == 0;
 }
 
 static bool fast_k(const ksim_handle* h, int32_t cls) {
@@ -339,6 +354,9 @@ int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
   // host bookkeeping: fast-kernel eligibility, tree classes, float64 bounds
   h->q_cls.resize((size_t)np);
   h->q_base.resize((size_t)np);
+  h->q_ident.resize((size_t)np);
+  h->q_aclass.resize((size_t)np);
+  h->aff_pre.resize((size_t)np + 1);
   h->fast_pre.resize((size_t)np + 1);
   h->pod_qmax.resize((size_t)np);
   std::vector<int32_t> tc((size_t)n_pods, -1);
@@ -348,6 +366,9 @@ int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
     const int64_t q = P0 + i;
     h->q_cls[q] = p.cls;
     h->q_base[q] = fast_base(p) ? 1 : 0;
+    h->q_ident[q] = p.aff_ident;
+    h->q_aclass[q] = p.aff_class;
+    h->aff_pre[q + 1] = h->aff_pre[q] + ((p.aff_ident || p.aff_class) ? 1 : 0);
     const bool fast = h->q_base[q] && fast_k(h, p.cls);
     h->fast_pre[q + 1] = h->fast_pre[q] + (fast ? 1 : 0);
     int64_t m = 0;
@@ -433,14 +454,16 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
   HIPCHK(h, hipMemcpyAsync(c.cursor, &first, 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemsetAsync(c.ticket, 0, 16, h->stream));
   const int batch = (int)std::min<int64_t>(count, 256);
+  const int ipa = ksim_rt_aff_count(h, first, count) > 0 && c.w[KSIM_W_INTERPOD_AFFINITY] != 0 && !c.no_prio ? 1 : 0;
   if (!h->gexec || h->g_batch != batch || h->g_npt != npt || h->g_collect != c.collect || h->g_first != first ||
-      h->g_end != c.end) {
+      h->g_end != c.end || h->g_ipa != ipa) {
     if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
     if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
     for (int k = 0; k < batch; ++k) {
-      hipError_t e = ksim_launch_scan(&c, npt, c.collect, grid, h->stream);
+      hipError_t e = ipa ? ksim_launch_ipa_pass(&c, npt, grid, h->stream) : hipSuccess;
+      if (e == hipSuccess) e = ksim_launch_scan(&c, npt, c.collect, grid, h->stream);
       if (e != hipSuccess) {
         hipGraph_t g = nullptr;
         (void)hipStreamEndCapture(h->stream, &g);
@@ -450,7 +473,7 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
     }
     HIPCHK(h, hipStreamEndCapture(h->stream, &h->graph));
     HIPCHK(h, hipGraphInstantiate(&h->gexec, h->graph, nullptr, nullptr, 0));
-    h->g_batch = batch; h->g_npt = npt; h->g_collect = c.collect; h->g_first = first; h->g_end = c.end;
+    h->g_batch = batch; h->g_npt = npt; h->g_collect = c.collect; h->g_first = first; h->g_end = c.end; h->g_ipa = ipa;
   }
   const int64_t reps = (count + batch - 1) / batch;
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
@@ -550,6 +573,8 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
 
 static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   KsimCtx& c = h->ctx;
+  // inter-pod affinity pods are evaluated and committed by the launch-mode kernels only
+  if (ksim_rt_aff_count(h, first, count)) return run_launch_mode(h, first, count, st);
   int grid = 0, lds_rows = 0;
   if (const int form = pfast_form(h, first, count, &grid, &lds_rows)) {
     int rc = run_pfast_mode(h, first, count, grid, lds_rows, form == 2, st);
@@ -637,6 +662,10 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
 // kernel can take the range), else the launch form.
 static int run_auto_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   int g, l;
+  if (ksim_rt_aff_count(h, first, count)) {
+    h->tree_valid = false;
+    return run_launch_mode(h, first, count, st);
+  }
   const bool pers = (ksim_persistent_config(h->ctx.n, &g, &l) && persistent_weights_ok(h->ctx)) ||
                     pfast_form(h, first, count, &g, &l);
   h->tree_valid = false;  // these paths commit without maintaining the trees
@@ -773,6 +802,7 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
   if (count == 0) return KSIM_OK;
   KsimCtx& c = h->ctx;
   if (c.n == 0) return ksim_fail(h, KSIM_E_NO_NODES, "no nodes available to schedule pods");
+  if (int rc = ksim_rt_check_aff(h, "ksim_schedule")) return rc;
   if (h->shard.world > 1) {  // node-sharded: the fast persistent kernel on every rank, in lockstep
     for (int r = 0; r < h->shard.world; ++r)
       if (!h->shard.peers[r]) return ksim_fail(h, KSIM_E_STATE, "ksim_schedule: rank %d is not connected", r);
@@ -828,6 +858,7 @@ int ksim_evaluate(ksim_handle* h, int64_t pod, uint8_t* out_fit, uint32_t* out_r
   KsimCtx& c = h->ctx;
   const int64_t n = c.n;
   if (n == 0) return ksim_fail(h, KSIM_E_NO_NODES, "no nodes available to schedule pods");
+  if (int rc0 = ksim_rt_check_aff(h, "ksim_evaluate")) return rc0;
   uint8_t *f, *rcl;
   uint32_t* r;
   int64_t* s;
@@ -857,6 +888,7 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
   KsimCtx& c = h->ctx;
   const int64_t n = c.n;
   if (n == 0) return ksim_fail(h, KSIM_E_NO_NODES, "no nodes available to schedule pods");
+  if (int rc0 = ksim_rt_check_aff(h, "ksim_sweep")) return rc0;
   if (n > KSIM_SWEEP_MAX_NODES)
     return ksim_fail(h, KSIM_E_UNSUPPORTED, "ksim_sweep: %lld nodes exceed the %d-node scenario layout", (long long)n,
                 KSIM_SWEEP_MAX_NODES);

@@ -14,10 +14,10 @@ LIB_PATH = os.environ.get("KSIM_LIB") or os.path.join(PKG_DIR, "lib", "libksim.s
 
 KSIM_OK = 0
 E_INVAL, E_DEVICE, E_NOMEM, E_UNSUPPORTED, E_STATE, E_OVERFLOW, E_NO_NODES = -1, -2, -3, -4, -5, -6, -7
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_SCALAR = 8
 MAX_RCLASS = 16
-NREASONS = 24
+NREASONS = 28
 
 # predicate bits
 P_CHECK_NODE_CONDITION = 1 << 0
@@ -32,9 +32,10 @@ P_NOEXEC_TAINTS = 1 << 8
 P_MEM_PRESSURE = 1 << 9
 P_DISK_PRESSURE = 1 << 10
 P_LABEL_PRESENCE = 1 << 11
+P_INTERPOD_AFFINITY = 1 << 12
 
-W_LEAST, W_MOST, W_BALANCED, W_TAINT_TOL, W_NODE_AFF = range(5)
-NW = 5
+W_LEAST, W_MOST, W_BALANCED, W_TAINT_TOL, W_NODE_AFF, W_INTERPOD = range(6)
+NW = 6
 
 N_NOT_READY, N_OUT_OF_DISK, N_NET_UNAVAIL, N_UNSCHEDULABLE = 1, 2, 4, 8
 N_MEM_PRESSURE, N_DISK_PRESSURE, N_LABEL_PRESENCE = 16, 32, 64
@@ -48,6 +49,11 @@ R_PODS, R_CPU, R_MEMORY, R_GPU, R_EPHEMERAL = 4, 5, 6, 7, 8
 R_HOSTNAME, R_HOST_PORTS, R_NODE_SELECTOR, R_TAINTS = 9, 10, 11, 12
 R_MEM_PRESSURE, R_DISK_PRESSURE, R_LABEL_PRESENCE = 13, 14, 15
 R_SCALAR0 = 16
+R_POD_AFFINITY, R_EXISTING_ANTI, R_AFFINITY_RULES, R_ANTI_AFFINITY_RULES = 24, 25, 26, 27
+
+# inter-pod affinity tables (ksim_affinity_tables)
+AFF_REQ_AFFINITY, AFF_REQ_ANTI, AFF_PREFERRED = 0, 1, 2
+AFF_CARRY_ANTI, AFF_CARRY_PRIO = 0, 1
 
 _i64p = C.POINTER(C.c_int64)
 _i32p = C.POINTER(C.c_int32)
@@ -82,7 +88,8 @@ class Pod(C.Structure):
                 ("add_cpu", C.c_int64), ("add_mem", C.c_int64), ("add_gpu", C.c_int64), ("add_eph", C.c_int64),
                 ("nz_cpu", C.c_int64), ("nz_mem", C.c_int64), ("cls", C.c_int32), ("host", C.c_int32),
                 ("flags", C.c_uint32), ("port_off", C.c_int32), ("port_cnt", C.c_int32),
-                ("scalar_off", C.c_int32), ("scalar_cnt", C.c_int32), ("reserved", C.c_int32 * 5)]
+                ("scalar_off", C.c_int32), ("scalar_cnt", C.c_int32), ("aff_ident", C.c_int32),
+                ("aff_class", C.c_int32), ("reserved", C.c_int32 * 3)]
 
 
 class ScalarReq(C.Structure):
@@ -111,6 +118,17 @@ class NodeRow(C.Structure):
 SCHEDULE_ONLY, SCHEDULE_ASSUME = 0, 1
 
 
+class AffinityTables(C.Structure):
+    _fields_ = [("n_keys", C.c_int32), ("n_sel", C.c_int32), ("n_ident", C.c_int32), ("n_pair", C.c_int32),
+                ("n_carry", C.c_int32), ("n_aclass", C.c_int32), ("n_terms", C.c_int32), ("n_carries", C.c_int32),
+                ("n_nodes", C.c_int64), ("cnt_len", C.c_int64), ("carried_len", C.c_int64),
+                ("hard_weight", C.c_int32), ("sel_words", C.c_int32), ("carry_words", C.c_int32), ("pad", C.c_int32),
+                ("dom", _i32p), ("n_dom", _i32p), ("ident_sel", _u64p), ("ident_anti", _u64p), ("ident_prio", _u64p),
+                ("pair_sel", _i32p), ("pair_key", _i32p), ("pair_off", _i64p), ("carry_key", _i32p),
+                ("carry_kind", _i32p), ("carry_off", _i64p), ("ac", _i32p), ("terms", C.c_void_p),
+                ("carries", C.c_void_p), ("cnt", _i32p), ("carried", _i64p)]
+
+
 class NodeState(C.Structure):
     _fields_ = [("req_cpu", _i64p), ("req_mem", _i64p), ("req_gpu", _i64p), ("req_eph", _i64p),
                 ("nz_cpu", _i64p), ("nz_mem", _i64p), ("pod_count", _i32p), ("req_scalar", _i64p),
@@ -122,7 +140,7 @@ POD_DTYPE = np.dtype([("req_cpu", "<i8"), ("req_mem", "<i8"), ("req_gpu", "<i8")
                       ("add_cpu", "<i8"), ("add_mem", "<i8"), ("add_gpu", "<i8"), ("add_eph", "<i8"),
                       ("nz_cpu", "<i8"), ("nz_mem", "<i8"), ("cls", "<i4"), ("host", "<i4"), ("flags", "<u4"),
                       ("port_off", "<i4"), ("port_cnt", "<i4"), ("scalar_off", "<i4"), ("scalar_cnt", "<i4"),
-                      ("reserved", "<i4", (5,))])
+                      ("aff_ident", "<i4"), ("aff_class", "<i4"), ("reserved", "<i4", (3,))])
 SCALAR_DTYPE = np.dtype([("col", "<i4"), ("pad", "<i4"), ("req", "<i8"), ("add", "<i8")])
 assert POD_DTYPE.itemsize == C.sizeof(Pod) == 128
 assert SCALAR_DTYPE.itemsize == C.sizeof(ScalarReq)
@@ -132,7 +150,7 @@ EXPORTS = ["ksim_abi_version", "ksim_last_error", "ksim_create", "ksim_destroy",
            "ksim_read_nodes", "ksim_get_counter", "ksim_set_counter", "ksim_selftest", "ksim_sweep",
            "ksim_shard_setup", "ksim_shard_export", "ksim_shard_connect", "ksim_shard_connect_local",
            "ksim_schedule_one", "ksim_pod_add", "ksim_pod_remove", "ksim_node_add", "ksim_node_update",
-           "ksim_node_remove", "ksim_node_count", "ksim_append_pods"]
+           "ksim_node_remove", "ksim_node_count", "ksim_append_pods", "ksim_load_affinity"]
 IPC_HANDLE_BYTES = 64
 MAX_RANKS = 8
 
@@ -193,6 +211,7 @@ def lib():
     L.ksim_node_remove.argtypes = [C.c_void_p, C.c_int64]
     L.ksim_node_count.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     L.ksim_append_pods.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
+    L.ksim_load_affinity.argtypes = [C.c_void_p, C.POINTER(AffinityTables)]
     if L.ksim_abi_version() != ABI_VERSION:
         raise ImportError("libksim.so ABI version mismatch")
     _lib = L

@@ -1,0 +1,313 @@
+"""Inter-pod affinity → the device tables of ksim_load_affinity (include/ksim.h).
+
+Reference semantics (paths under vendor/k8s.io/kubernetes/pkg/scheduler/):
+- MatchInterPodAffinity: algorithm/predicates/predicates.go:1143-1450 with its metadata
+  (getMatchingAntiAffinityTerms, :1235-1293; GetMetadata, predicates/metadata.go:102-123);
+- InterPodAffinityPriority: algorithm/priorities/interpod_affinity.go:118-240;
+- GetNamespacesFromPodAffinityTerm / PodMatchesTermsNamespaceAndSelector /
+  NodesHaveSameTopologyKey: algorithm/priorities/util/topologies.go:28-71.
+
+Every string test is resolved here, once per distinct object:
+- a *selector* s is (namespaces, label selector) of one term as its defining pod resolves it;
+  an *identity* is (namespace, labels) of a pod; ident_sel[i] has bit s when identity i matches s;
+- a *topology key* k maps every node to a domain id (the node's value of label k interned, -1
+  without it); two pseudo keys: ALL (every node in domain 0, for "a matching pod exists
+  anywhere") and NODE (node i in domain i, for kubernetes.io/hostname terms, which only look at
+  the node's own pods, predicates.go:1176-1179);
+- a *counted pair* (s, k) keeps, per domain of k, the number of placed pods matching s: the
+  pod-side terms read it (required affinity / anti-affinity, preferred terms);
+- a *carried term* e is a term of a placed pod acting on later pods (existing pods'
+  anti-affinity, the symmetric priority terms): per domain of its key, the summed weight (or,
+  for required anti-affinity, the number) of placed pods carrying it.
+Placing a pod adds one to every pair whose selector its identity matches and its carried
+amounts to its node's domains (ksim_commit); removing subtracts.
+
+Inputs whose reference behaviour is an error rather than a placement are rejected (Unsupported):
+unparsable label selectors, required terms with an empty topologyKey, and running pods bound to
+a node that is not in the snapshot while affinity terms exist (the reference then errors or
+falls back to a metadata-less path).
+"""
+from __future__ import annotations
+
+import json
+
+import numpy as np
+
+from . import abi, labels
+
+HOSTNAME = "kubernetes.io/hostname"   # kubeletapis.LabelHostname
+KEY_ALL, KEY_NODE = 0, 1              # pseudo keys
+MAX_SEL = 65536
+MAX_CARRY = 65536
+
+TERM_DTYPE = np.dtype([("kind", "<i4"), ("pair", "<i4"), ("gate_key", "<i4"), ("exist_pair", "<i4"),
+                       ("self_ok", "<i4"), ("pad", "<i4"), ("weight", "<i8")])
+CARRY_DTYPE = np.dtype([("term", "<i4"), ("pad", "<i4"), ("amount", "<i8")])
+
+
+class Unsupported(abi.KsimUnsupported):
+    def __init__(self, msg):
+        super().__init__(abi.E_UNSUPPORTED, msg)
+
+
+def _canon(x):
+    return json.dumps(x, sort_keys=True, separators=(",", ":"))
+
+
+def _meta(o):
+    return o.get("metadata") or {}
+
+
+def _aff(p):
+    return (p.get("spec") or {}).get("affinity") or {}
+
+
+def has_pod_affinity(p):
+    a = _aff(p)
+    return a.get("podAffinity") is not None or a.get("podAntiAffinity") is not None
+
+
+def _required(section):
+    return list((section or {}).get("requiredDuringSchedulingIgnoredDuringExecution") or [])
+
+
+def _preferred(section):
+    return list((section or {}).get("preferredDuringSchedulingIgnoredDuringExecution") or [])
+
+
+class _Interner:
+    def __init__(self):
+        self.ids, self.items = {}, []
+
+    def get(self, key, item=None):
+        i = self.ids.get(key)
+        if i is None:
+            i = self.ids[key] = len(self.items)
+            self.items.append(key if item is None else item)
+        return i
+
+
+class AffinityIndex:
+    """Collects the terms of every pod (running and queued), then builds the tables."""
+
+    def __init__(self, node_labels, hard_weight=10):
+        self.node_labels = node_labels            # per node (name-rank order): dict or None
+        self.hard_weight = int(hard_weight)
+        self.keys = _Interner()
+        self.keys.get("\x00all")
+        self.keys.get("\x00node")
+        self.sels = _Interner()                   # (namespaces, selector) → (set, requirements)
+        self.pairs = _Interner()                  # (sel, key)
+        self.carry = _Interner()                  # (sel, key, kind)
+        self.idents = _Interner()                 # (namespace, labels)
+        self.aclasses = _Interner()               # → (required terms, preferred terms, carries)
+
+    # ---------------------------------------------------------------- interning
+    def _sel(self, defining_pod, term):
+        nss = term.get("namespaces") or []
+        ns = frozenset(nss) if nss else frozenset([_meta(defining_pod).get("namespace", "")])
+        ps = term.get("labelSelector")
+        try:
+            sel = labels.from_label_selector(ps)
+        except labels.SelectorError as e:
+            raise Unsupported("pod %r: affinity label selector: %s" % (_meta(defining_pod).get("name"), e))
+        key = (tuple(sorted(ns)), None if sel is labels.NOTHING else tuple(sel))
+        return self.sels.get(key, (ns, sel)), sel
+
+    def ident(self, pod):
+        md = _meta(pod)
+        return self.idents.get((md.get("namespace", ""), _canon(md.get("labels") or {})),
+                               (md.get("namespace", ""), dict(md.get("labels") or {})))
+
+    def _matches(self, ident_item, sel_item):
+        ns, lab = ident_item
+        nss, sel = sel_item
+        return ns in nss and labels.matches(sel, lab)
+
+    def aclass(self, pod):
+        """The pod's own terms and carried terms, interned; -1 when it has neither."""
+        if not has_pod_affinity(pod):
+            return -1
+        a = _aff(pod)
+        name = _meta(pod).get("name")
+        req, pref, carries = [], [], {}
+        my_ident = self.idents.items[self.ident(pod)]
+        for kind, section in ((abi.AFF_REQ_AFFINITY, a.get("podAffinity")), (abi.AFF_REQ_ANTI, a.get("podAntiAffinity"))):
+            for t in _required(section):
+                key = t.get("topologyKey") or ""
+                if not key:
+                    raise Unsupported("pod %r: required pod (anti-)affinity term without topologyKey" % name)
+                s, sel = self._sel(pod, t)
+                if key == HOSTNAME:
+                    mp = self.pairs.get((s, KEY_NODE))
+                    gate, ep = self.keys.get(key), mp
+                else:
+                    k = self.keys.get(key)
+                    mp, gate, ep = self.pairs.get((s, k)), k, self.pairs.get((s, KEY_ALL))
+                self_ok = int(self._matches(my_ident, self.sels.items[s]))
+                req.append((kind, mp, gate, ep, self_ok, 0))
+        for sign, section in ((1, a.get("podAffinity")), (-1, a.get("podAntiAffinity"))):
+            if section is None:
+                continue
+            for wt in _preferred(section):
+                t = wt.get("podAffinityTerm") or {}
+                s, sel = self._sel(pod, t)
+                key = t.get("topologyKey") or ""
+                if not key or sel is labels.NOTHING:
+                    continue                              # matches no node / no pod: adds nothing
+                pref.append((abi.AFF_PREFERRED, self.pairs.get((s, self.keys.get(key))), 0, 0, 0,
+                             sign * int(wt.get("weight", 0))))
+
+        def carry(t, kind, amount):
+            s, sel = self._sel(pod, t)
+            key = t.get("topologyKey") or ""
+            if not key:
+                if kind == abi.AFF_CARRY_ANTI:
+                    raise Unsupported("pod %r: required anti-affinity term without topologyKey" % name)
+                return                                    # NodesHaveSameTopologyKey is false
+            if sel is labels.NOTHING:
+                return
+            e = self.carry.get((s, self.keys.get(key), kind))
+            carries[e] = carries.get(e, 0) + amount
+
+        for t in _required(a.get("podAntiAffinity")):
+            carry(t, abi.AFF_CARRY_ANTI, 1)
+        if a.get("podAffinity") is not None:
+            if self.hard_weight > 0:
+                for t in _required(a.get("podAffinity")):
+                    carry(t, abi.AFF_CARRY_PRIO, self.hard_weight)
+            for wt in _preferred(a.get("podAffinity")):
+                carry(wt.get("podAffinityTerm") or {}, abi.AFF_CARRY_PRIO, int(wt.get("weight", 0)))
+        if a.get("podAntiAffinity") is not None:
+            for wt in _preferred(a.get("podAntiAffinity")):
+                carry(wt.get("podAffinityTerm") or {}, abi.AFF_CARRY_PRIO, -int(wt.get("weight", 0)))
+        carries = tuple(sorted((e, v) for e, v in carries.items() if v != 0 or self.carry.items[e][2] == abi.AFF_CARRY_ANTI))
+        req.sort(key=lambda r: r[0] != abi.AFF_REQ_AFFINITY)   # affinity terms are checked before anti-affinity
+        if not req and not pref and not carries:
+            return -1
+        return self.aclasses.get((tuple(req), tuple(pref), carries))
+
+    # ------------------------------------------------------------------ tables
+    def build(self, running_nodes, idents, aclasses):
+        """(tables, remap): remap[interned identity] = ksim_pod.aff_ident (1 + table id, 0 when
+        the identity matches no selector).  running_nodes: node ranks of the placed pods, whose
+        interned identities / classes (-1: none) lead `idents` / `aclasses`."""
+        if len(self.sels.items) > MAX_SEL:
+            raise Unsupported("more than %d distinct inter-pod affinity selectors" % MAX_SEL)
+        if len(self.carry.items) > MAX_CARRY:
+            raise Unsupported("more than %d distinct carried inter-pod affinity terms" % MAX_CARRY)
+        n = len(self.node_labels)
+        K = len(self.keys.items)
+        dom = np.full((K, n), -1, np.int32)
+        n_dom = np.zeros(K, np.int32)
+        dom[KEY_ALL, :] = 0
+        n_dom[KEY_ALL] = 1
+        dom[KEY_NODE, :] = np.arange(n, dtype=np.int32)
+        n_dom[KEY_NODE] = n
+        for k in range(2, K):
+            name = self.keys.items[k]
+            vals = {}
+            for i, lab in enumerate(self.node_labels):
+                if lab is not None and name in lab:
+                    dom[k, i] = vals.setdefault(lab[name], len(vals))
+            n_dom[k] = len(vals)
+        # identity masks (identities matching nothing become -1)
+        I = len(self.idents.items)
+        SW, CW = (len(self.sels.items) + 63) // 64, (len(self.carry.items) + 63) // 64
+        isel = np.zeros((I, SW), np.uint64)
+        ianti = np.zeros((I, CW), np.uint64)
+        iprio = np.zeros((I, CW), np.uint64)
+        for i, it in enumerate(self.idents.items):
+            hit = [self._matches(it, si) for si in self.sels.items]
+            for s, h in enumerate(hit):
+                if h:
+                    isel[i, s >> 6] |= np.uint64(1 << (s & 63))
+            for e, (s, _, kind) in enumerate(self.carry.items):
+                if hit[s]:
+                    tgt = ianti if kind == abi.AFF_CARRY_ANTI else iprio
+                    tgt[i, e >> 6] |= np.uint64(1 << (e & 63))
+        live = (isel.any(axis=1) | ianti.any(axis=1) | iprio.any(axis=1)) if I else np.zeros(0, bool)
+        remap = np.zeros(I, np.int32)     # ksim_pod.aff_ident: 1 + the table id, 0 = none
+        remap[live] = np.arange(1, int(live.sum()) + 1, dtype=np.int32)
+        # counted pairs / carried terms: offsets into the count arrays
+        P = len(self.pairs.items)
+        pair_sel = np.array([s for s, _ in self.pairs.items], np.int32)
+        pair_key = np.array([k for _, k in self.pairs.items], np.int32)
+        pair_off = np.zeros(P, np.int64)
+        off = 0
+        for c in range(P):
+            pair_off[c] = off
+            off += int(n_dom[pair_key[c]])
+        cnt = np.zeros(max(off, 1), np.int32)
+        E = len(self.carry.items)
+        carry_key = np.array([k for _, k, _ in self.carry.items], np.int32)
+        carry_kind = np.array([kd for _, _, kd in self.carry.items], np.int32)
+        carry_sel = np.array([s for s, _, _ in self.carry.items], np.int32)
+        carry_off = np.zeros(E, np.int64)
+        off = 0
+        for e in range(E):
+            carry_off[e] = off
+            off += int(n_dom[carry_key[e]])
+        carried = np.zeros(max(off, 1), np.int64)
+        # affinity classes
+        A = len(self.aclasses.items)
+        terms, carries = [], []
+        ac = np.zeros((A, 6), np.int32)   # req_off, req_cnt, pref_off, pref_cnt, carry_off, carry_cnt
+        for a, (req, pref, car) in enumerate(self.aclasses.items):
+            ac[a, 0], ac[a, 1] = len(terms), len(req)
+            terms.extend(req)
+            ac[a, 2], ac[a, 3] = len(terms), len(pref)
+            terms.extend(pref)
+            ac[a, 4], ac[a, 5] = len(carries), len(car)
+            carries.extend(car)
+        terms_a = np.zeros(max(len(terms), 1), TERM_DTYPE)
+        for j, t in enumerate(terms):
+            terms_a[j] = t[:5] + (0, t[5])
+        carries_a = np.zeros(max(len(carries), 1), CARRY_DTYPE)
+        for j, (e, v) in enumerate(carries):
+            carries_a[j] = (e, 0, v)
+        # the running pods' contribution (NodeInfo.AddPod of every cached pod)
+        for w, i_id, a_id in zip(running_nodes, idents[:len(running_nodes)], aclasses[:len(running_nodes)]):
+            for c in range(P):
+                s = int(pair_sel[c])
+                if (int(isel[i_id, s >> 6]) >> (s & 63)) & 1:
+                    d = dom[pair_key[c], w]
+                    if d >= 0:
+                        cnt[pair_off[c] + d] += 1
+            if a_id >= 0:
+                for j in range(ac[a_id, 4], ac[a_id, 4] + ac[a_id, 5]):
+                    e, v = int(carries_a[j]["term"]), int(carries_a[j]["amount"])
+                    d = dom[carry_key[e], w]
+                    if d >= 0:
+                        carried[carry_off[e] + d] += v
+        return dict(n_keys=K, n_sel=len(self.sels.items), n_ident=int(live.sum()), n_pair=P, n_carry=E, n_aclass=A,
+                    sel_words=SW, carry_words=CW,
+                    n_nodes=n, hard_weight=self.hard_weight, dom=np.ascontiguousarray(dom), n_dom=n_dom,
+                    ident_sel=isel[live].copy(), ident_anti=ianti[live].copy(), ident_prio=iprio[live].copy(),
+                    pair_sel=pair_sel, pair_key=pair_key, pair_off=pair_off, carry_key=carry_key,
+                    carry_kind=carry_kind, carry_sel=carry_sel, carry_off=carry_off,
+                    ac=np.ascontiguousarray(ac), terms=terms_a, carries=carries_a, cnt=cnt, carried=carried), remap
+
+
+def tables_struct(d):
+    """ksim_affinity_tables over a tables dict (the dict keeps the arrays alive)."""
+    t = abi.AffinityTables()
+    for k in ("n_keys", "n_sel", "n_ident", "n_pair", "n_carry", "n_aclass", "hard_weight", "sel_words", "carry_words"):
+        setattr(t, k, int(d[k]))
+    t.n_nodes = int(d["n_nodes"])
+    for name, ct in (("dom", abi.C.c_int32), ("n_dom", abi.C.c_int32), ("ident_sel", abi.C.c_uint64),
+                     ("ident_anti", abi.C.c_uint64), ("ident_prio", abi.C.c_uint64), ("pair_sel", abi.C.c_int32),
+                     ("pair_key", abi.C.c_int32), ("pair_off", abi.C.c_int64), ("carry_key", abi.C.c_int32),
+                     ("carry_kind", abi.C.c_int32), ("carry_off", abi.C.c_int64), ("ac", abi.C.c_int32),
+                     ("cnt", abi.C.c_int32), ("carried", abi.C.c_int64)):
+        d[name] = np.ascontiguousarray(d[name])
+        setattr(t, name, abi.ptr(d[name], ct))
+    d["terms"] = np.ascontiguousarray(d["terms"])
+    d["carries"] = np.ascontiguousarray(d["carries"])
+    t.terms = d["terms"].ctypes.data_as(abi.C.c_void_p)
+    t.carries = d["carries"].ctypes.data_as(abi.C.c_void_p)
+    t.n_terms = len(d["terms"])
+    t.n_carries = len(d["carries"])
+    t.cnt_len = len(d["cnt"])
+    t.carried_len = len(d["carried"])
+    return t

@@ -150,11 +150,13 @@ def tolerates(tol, taint) -> bool:
     return op == "Exists"
 
 
+def has_pod_affinity(pod):
+    aff = _spec(pod).get("affinity") or {}
+    return aff.get("podAffinity") is not None or aff.get("podAntiAffinity") is not None
+
+
 def check_pod_supported(pod, where="pod"):
     spec = _spec(pod)
-    aff = spec.get("affinity") or {}
-    if aff.get("podAffinity") or aff.get("podAntiAffinity"):
-        raise Unsupported("%s %r: inter-pod affinity is outside the supported key set" % (where, _meta(pod).get("name")))
     for v in spec.get("volumes") or []:
         for k in _UNSUPPORTED_VOLUMES:
             if v.get(k) is not None:
@@ -202,13 +204,17 @@ class Cluster:
         self.prefer_avoid_nodes = False
         self.node_images = False   # some node lists status.images (ImageLocalityPriority not constant)
         self.bad_affinity_classes = set()   # preferred terms that fail to parse
+        self.affinity = None     # inter-pod affinity tables (ksim/affinity.py), None without terms
+        self.hard_weight = 10
 
     # ------------------------------------------------------------------ nodes
     @classmethod
-    def from_objects(cls, nodes, running_pods=(), pods=(), port_slots=None):
+    def from_objects(cls, nodes, running_pods=(), pods=(), port_slots=None, hard_weight=10):
         """nodes / running_pods / pods: Kubernetes-shaped dicts; pods are in SCHEDULING
-        order (the caller resolves the simulator's LIFO queue)."""
+        order (the caller resolves the simulator's LIFO queue).  hard_weight:
+        hardPodAffinitySymmetricWeight (the simulator's 10, or a Policy's)."""
         self = cls()
+        self.hard_weight = int(hard_weight)
         self.ips.get("0.0.0.0")     # id 0 = wildcard
         self.protos.get("TCP")      # id 0 = default protocol
         nodes = sorted(nodes, key=lambda n: _meta(n).get("name", "").encode())
@@ -220,6 +226,11 @@ class Cluster:
         running = [p for p in running_pods if _spec(p).get("nodeName") in self.index]
         for p in running:
             check_pod_supported(p, "running pod")
+        with_affinity = any(has_pod_affinity(p) for p in list(running_pods) + list(pods))
+        if with_affinity and len(running) != len([p for p in running_pods if _spec(p).get("nodeName")]):
+            # the reference caches them under a node-less NodeInfo: its affinity metadata then
+            # errors and the predicate takes another path (metadata.go:106-109)
+            raise Unsupported("running pods bound to nodes outside the snapshot, with inter-pod affinity terms")
         # scalar columns: every scalar name any node or pod mentions
         for x in nodes:
             for name in ((x.get("status") or {}).get("allocatable") or {}):
@@ -271,7 +282,10 @@ class Cluster:
                 used_ports[i][abi_port_key(self.ips.get(ip), self.protos.get(proto), port)] = True
         self.cols = c
         # pod queue
+        self._affinity_ok = with_affinity
         self._compile_pods(list(pods), compiled[len(running):])
+        if with_affinity:
+            self._build_affinity(nodes, running, list(pods))
         # port slots: enough for everything that could land on one node
         need = max([len(u) for u in used_ports] + [0])
         if self.pods is not None and len(self.pods):
@@ -313,6 +327,9 @@ class Cluster:
         `index` maps spec.nodeName to a name rank (default: the cluster's own index)."""
         pred, add, nzc, nzm = compiled
         check_pod_supported(p)
+        if has_pod_affinity(p) and not getattr(self, "_affinity_ok", False):
+            raise Unsupported("pod %r: inter-pod affinity needs the cluster's affinity tables (ClusterCapacity / "
+                              "GenericScheduler)" % _meta(p).get("name"))
         spec, md = _spec(p), _meta(p)
         if self.prefer_avoid_nodes:
             for o in md.get("ownerReferences") or []:
@@ -338,6 +355,21 @@ class Cluster:
         row["scalar_off"], row["scalar_cnt"] = len(scalars), len(pred.scalar)
         for name, v in pred.scalar.items():
             scalars.append((self.scalar_names.ids[name], 0, v, add.scalar.get(name, 0)))
+
+    def _build_affinity(self, nodes, running, pods):
+        """Inter-pod affinity tables over every pod's identity and terms (ksim/affinity.py); the
+        queued descriptors get their aff_ident / aff_class."""
+        from .affinity import AffinityIndex
+        idx = AffinityIndex([_meta(x).get("labels") for x in nodes], self.hard_weight)
+        allp = list(running) + list(pods)
+        idents = [idx.ident(p) for p in allp]
+        aclasses = [idx.aclass(p) for p in allp]
+        run_nodes = [self.index[_spec(p)["nodeName"]] for p in running]
+        self.affinity, remap = idx.build(run_nodes, idents, aclasses)
+        k = len(running)
+        if len(pods):
+            self.pods["aff_ident"] = remap[np.asarray(idents[k:], np.int64)]
+            self.pods["aff_class"] = np.asarray(aclasses[k:], np.int32) + 1
 
     # ----------------------------------------------------------------- tables
     def _build_tables(self):
@@ -383,6 +415,8 @@ class Cluster:
         """The name-rank range [lo, hi) of the node table with the same pods and interned
         tables (node-sharded mode: rank r loads its contiguous shard, ksim_shard_setup)."""
         import copy
+        if self.affinity is not None:
+            raise Unsupported("node-sharded scheduling of pods with inter-pod affinity terms")
         sub = copy.copy(self)
         sub.cols = {k: (np.ascontiguousarray(v[..., lo:hi]) if isinstance(v, np.ndarray) else v)
                     for k, v in self.cols.items()}

@@ -125,6 +125,24 @@ def from_node_selector_requirements(exprs):
     return out
 
 
+def from_label_selector(ps):
+    """metav1.LabelSelectorAsSelector (apimachinery/pkg/apis/meta/v1/helpers.go): nil → NOTHING,
+    empty → Everything ([]), matchLabels as equality requirements, matchExpressions with the
+    In / NotIn / Exists / DoesNotExist operators; raises SelectorError like the Go error path."""
+    if ps is None:
+        return NOTHING
+    ml, me = ps.get("matchLabels") or {}, ps.get("matchExpressions") or []
+    if not ml and not me:
+        return []
+    out = [requirement(k, "=", [ml[k]]) for k in sorted(ml)]
+    for e in me:
+        op = e.get("operator")
+        if op not in ("In", "NotIn", "Exists", "DoesNotExist"):
+            raise SelectorError("%r is not a valid pod selector operator" % op)
+        out.append(requirement(e.get("key", ""), op, e.get("values")))
+    return out
+
+
 def matches(sel, labels: dict) -> bool:
     if sel is NOTHING:
         return False

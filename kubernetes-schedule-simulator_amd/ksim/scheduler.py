@@ -37,21 +37,22 @@ PREDICATE_BITS = {
     "CheckNodeMemoryPressure": abi.P_MEM_PRESSURE,
     "CheckNodeDiskPressure": abi.P_DISK_PRESSURE,
     "CheckNodeLabelPresence": abi.P_LABEL_PRESENCE,   # with a Policy labelsPresence argument
+    "MatchInterPodAffinity": abi.P_INTERPOD_AFFINITY,  # over the cluster's affinity tables
 }
 # factory/plugins.go:401-406 + defaults.go:165: part of every predicate map
 MANDATORY_PREDICATES = ("CheckNodeCondition",)
-# keys that are true for every pod ingest accepts (no volumes of those kinds, no inter-pod
-# affinity); "PodFitsPorts" is registered but absent from predicatesOrdering, so it never runs
+# keys that are true for every pod ingest accepts (no volumes of those kinds); "PodFitsPorts"
+# is registered but absent from predicatesOrdering, so it never runs
 TRIVIAL_PREDICATES = {"NoDiskConflict", "MaxEBSVolumeCount", "MaxGCEPDVolumeCount", "MaxAzureDiskVolumeCount",
-                      "CheckVolumeBinding", "NoVolumeZoneConflict", "MatchInterPodAffinity", "PodFitsPorts"}
+                      "CheckVolumeBinding", "NoVolumeZoneConflict", "PodFitsPorts"}
 
 PRIORITY_SLOTS = {"LeastRequestedPriority": abi.W_LEAST, "MostRequestedPriority": abi.W_MOST,
                   "BalancedResourceAllocation": abi.W_BALANCED, "TaintTolerationPriority": abi.W_TAINT_TOL,
-                  "NodeAffinityPriority": abi.W_NODE_AFF}
+                  "NodeAffinityPriority": abi.W_NODE_AFF, "InterPodAffinityPriority": abi.W_INTERPOD}
 # value on every node under supported inputs (no services/controllers in the simulator's store,
-# no RC/RS-owned pods next to preferAvoidPods annotations, no affinity terms)
+# no RC/RS-owned pods next to preferAvoidPods annotations)
 CONST_PRIORITIES = {"SelectorSpreadPriority": 10, "ServiceSpreadingPriority": 10, "NodePreferAvoidPodsPriority": 10,
-                    "InterPodAffinityPriority": 0, "EqualPriority": 1,
+                    "EqualPriority": 1,
                     # image_locality.go:39-69: 0 on every node when no node lists status.images
                     "ImageLocalityPriority": 0}
 
@@ -125,6 +126,10 @@ REASON_TEXT = {
     abi.R_MEM_PRESSURE: "node(s) had memory pressure",
     abi.R_DISK_PRESSURE: "node(s) had disk pressure",
     abi.R_LABEL_PRESENCE: "node(s) didn't have the requested labels",
+    abi.R_POD_AFFINITY: "node(s) didn't match pod affinity/anti-affinity",
+    abi.R_EXISTING_ANTI: "node(s) didn't satisfy existing pods anti-affinity rules",
+    abi.R_AFFINITY_RULES: "node(s) didn't match pod affinity rules",
+    abi.R_ANTI_AFFINITY_RULES: "node(s) didn't match pod anti-affinity rules",
 }
 
 
@@ -137,7 +142,7 @@ def reason_strings(mask: int, scalar_names=()):
 
 
 def reason_text(r, scalar_names=()):
-    if r >= abi.R_SCALAR0:
+    if abi.R_SCALAR0 <= r < abi.R_SCALAR0 + abi.MAX_SCALAR:
         return "Insufficient " + scalar_names[r - abi.R_SCALAR0]
     return REASON_TEXT[r]
 
@@ -183,6 +188,16 @@ class GenericScheduler:
         self.h.call("ksim_load_nodes", C.byref(table))
         self.h.call("ksim_load_classes", C.byref(cluster.class_tables()))
         pods = np.ascontiguousarray(cluster.pods)
+        self.affinity = None
+        if cluster.affinity is not None:
+            if self.cfg.predicates & abi.P_INTERPOD_AFFINITY or (self.cfg.weights[abi.W_INTERPOD] and not self.cfg.no_priorities):
+                from .affinity import tables_struct
+                self.affinity = cluster.affinity
+                self.h.call("ksim_load_affinity", C.byref(tables_struct(self.affinity)))
+            elif len(pods):  # neither MatchInterPodAffinity nor its priority: the terms change nothing
+                pods = pods.copy()
+                pods["aff_ident"] = 0
+                pods["aff_class"] = 0
         self._pods = pods
         self.h.call("ksim_load_pods", abi.vptr(pods), len(pods), abi.vptr(cluster.pod_ports), len(cluster.pod_ports),
                     abi.vptr(cluster.pod_scalars), len(cluster.pod_scalars))

@@ -414,6 +414,7 @@ class NodeInfo:
     def __init__(self, node=None):
         self.node = None
         self.pods = []
+        self.pods_with_affinity = []     # PodsWithAffinity (node_info.go:326-328)
         self.requested = Resource()
         self.nonzero_cpu = 0
         self.nonzero_mem = 0
@@ -453,6 +454,8 @@ class NodeInfo:
         self.nonzero_cpu += nzc
         self.nonzero_mem += nzm
         self.pods.append(pod)
+        if has_pod_affinity_constraints(pod):
+            self.pods_with_affinity.append(pod)
         for ip, proto, port in pod_ports(pod):
             if port > 0:
                 self.used_ports.add(_sanitize(ip, proto) + (port,))
@@ -466,6 +469,10 @@ class NodeInfo:
                 continue
             self.pods[i] = self.pods[-1]
             self.pods.pop()
+            for j, q in enumerate(self.pods_with_affinity):
+                if pod_key(q) == key:
+                    del self.pods_with_affinity[j]
+                    break
             res, nzc, nzm = calculate_resource(pod)
             self.requested.cpu -= res.cpu
             self.requested.mem -= res.mem
@@ -655,7 +662,7 @@ PREDICATES = {
     "NoVolumeZoneConflict": pred_true,
     "CheckNodeMemoryPressure": pred_memory_pressure,
     "CheckNodeDiskPressure": pred_disk_pressure,
-    "MatchInterPodAffinity": pred_true,
+    "MatchInterPodAffinity": pred_true,   # replaced per scheduling cycle (GenericScheduler.schedule)
 }
 
 # predicates.go:129-138 (PodFitsPorts is registered under its own key but is not
@@ -681,6 +688,228 @@ def new_node_label_predicate(labels, presence):
                 return False, [R_LABEL_PRESENCE]
         return True, []
     return pred
+
+
+# --------------------------------------------------------------------------
+# Inter-pod affinity: the MatchInterPodAffinity predicate (S/algorithm/predicates/
+# predicates.go:1143-1450, metadata S/algorithm/predicates/metadata.go:102-123) and
+# InterPodAffinityPriority (S/algorithm/priorities/interpod_affinity.go:118-240), with the
+# helpers of S/algorithm/priorities/util/topologies.go:28-71 and
+# AM/pkg/apis/meta/v1/helpers.go LabelSelectorAsSelector.
+# --------------------------------------------------------------------------
+HOSTNAME_LABEL = "kubernetes.io/hostname"     # kubeletapis.LabelHostname
+R_AFFINITY = "node(s) didn't match pod affinity/anti-affinity"
+R_AFFINITY_RULES = "node(s) didn't match pod affinity rules"
+R_ANTI_AFFINITY_RULES = "node(s) didn't match pod anti-affinity rules"
+R_EXISTING_ANTI = "node(s) didn't satisfy existing pods anti-affinity rules"
+NOTHING = None                                 # labels.Nothing(): matches no pod
+
+
+class AffinityError(Exception):
+    """An error the reference returns (not a FitError): bad selector, empty topologyKey on a
+    required term, an existing pod's node missing from the node lister."""
+
+
+def label_selector_as_selector(ps):
+    """metav1.LabelSelectorAsSelector: nil → Nothing, empty → Everything ([]), else the
+    requirements (matchLabels as Equals, matchExpressions In/NotIn/Exists/DoesNotExist)."""
+    if ps is None:
+        return NOTHING
+    ml, me = ps.get("matchLabels") or {}, ps.get("matchExpressions") or []
+    if not ml and not me:
+        return []
+    reqs = []
+    try:
+        for k in sorted(ml):
+            reqs.append(new_requirement(k, "=", [ml[k]]))
+        for e in me:
+            op = e.get("operator")
+            if op not in ("In", "NotIn", "Exists", "DoesNotExist"):
+                raise AffinityError("%r is not a valid pod selector operator" % op)
+            reqs.append(new_requirement(e.get("key", ""), op, list(e.get("values") or [])))
+    except ValueError as err:
+        raise AffinityError(str(err))
+    return reqs
+
+
+def _meta(obj):
+    return obj.get("metadata") or {}
+
+
+def term_namespaces(pod, term):
+    """GetNamespacesFromPodAffinityTerm: the term's namespaces, or the defining pod's."""
+    ns = term.get("namespaces") or []
+    return set(ns) if ns else {_meta(pod).get("namespace", "")}
+
+
+def pod_matches_term(pod, namespaces, sel):
+    """PodMatchesTermsNamespaceAndSelector."""
+    if _meta(pod).get("namespace", "") not in namespaces:
+        return False
+    if sel is NOTHING:
+        return False
+    return selector_matches(sel, _meta(pod).get("labels") or {})
+
+
+def same_topology(node_a, node_b, key):
+    """NodesHaveSameTopologyKey: both nodes carry label `key` with equal values."""
+    if not key:
+        return False
+    la, lb = _meta(node_a).get("labels"), _meta(node_b).get("labels")
+    if la is None or lb is None:
+        return False
+    return key in la and key in lb and la[key] == lb[key]
+
+
+def _affinity(pod):
+    return (pod.get("spec") or {}).get("affinity") or {}
+
+
+def has_pod_affinity_constraints(pod):
+    """hasPodAffinityConstraints (node_info.go): PodAffinity or PodAntiAffinity set."""
+    a = _affinity(pod)
+    return a.get("podAffinity") is not None or a.get("podAntiAffinity") is not None
+
+
+def required_terms(section):
+    """GetPodAffinityTerms / GetPodAntiAffinityTerms."""
+    return list((section or {}).get("requiredDuringSchedulingIgnoredDuringExecution") or [])
+
+
+def preferred_terms(section):
+    return list((section or {}).get("preferredDuringSchedulingIgnoredDuringExecution") or [])
+
+
+def matching_anti_affinity_terms(pod, pods_with_nodes):
+    """getMatchingAntiAffinityTerms (predicates.go:1235-1293 over a nodeInfoMap's
+    PodsWithAffinity, or the metadata-less :1313-1338 over the pod lister): every required
+    anti-affinity term of an existing pod that `pod` matches, with the existing pod's node.
+    pods_with_nodes: [(existing pod, its v1.Node)]."""
+    out = []
+    for e, enode in pods_with_nodes:
+        if not has_pod_affinity_constraints(e):
+            continue
+        for t in required_terms(_affinity(e).get("podAntiAffinity")):
+            sel = label_selector_as_selector(t.get("labelSelector"))
+            if pod_matches_term(pod, term_namespaces(e, t), sel):
+                out.append((t, enode))
+    return out
+
+
+def _any_pod_matches(pod, all_pods, node_pods, node, term):
+    """anyPodMatchesPodAffinityTerm (predicates.go:1161-1194): (a matching pod on a node in the
+    same topology, a matching pod anywhere); hostname terms only look at the node's own pods."""
+    key = term.get("topologyKey", "")
+    if not key:
+        raise AffinityError("empty topologyKey is not allowed except for PreferredDuringScheduling pod anti-affinity")
+    ns = term_namespaces(pod, term)
+    sel = label_selector_as_selector(term.get("labelSelector"))
+    pods = node_pods if key == HOSTNAME_LABEL else all_pods
+    exists = False
+    for e, enode in pods:
+        if pod_matches_term(e, ns, sel):
+            exists = True
+            if same_topology(node, enode, key):
+                return True, True
+    return False, exists
+
+
+def interpod_affinity_matches(pod, node, meta_terms, all_pods, node_pods):
+    """PodAffinityChecker.InterPodAffinityMatches (predicates.go:1143-1156) → (fits, reasons,
+    error) as Go returns them (an error comes with failure reasons; the scheduler turns it into
+    a scheduling error, podFitsOnNode generic_scheduler.go:505-508).  node: the candidate
+    v1.Node; meta_terms: matching_anti_affinity_terms of the predicate metadata; all_pods:
+    podLister.FilteredList as [(pod, node)]; node_pods: nodeInfo.Pods() likewise."""
+    for t, enode in meta_terms:          # satisfiesExistingPodsAntiAffinity (:1340-1379)
+        if not t.get("topologyKey"):
+            return False, [R_AFFINITY, R_EXISTING_ANTI], AffinityError("empty topologyKey")
+        if same_topology(node, enode, t["topologyKey"]):
+            return False, [R_AFFINITY, R_EXISTING_ANTI], None
+    a = _affinity(pod)
+    if a.get("podAffinity") is None and a.get("podAntiAffinity") is None:
+        return True, [], None
+    # satisfiesPodsAffinityAntiAffinity (:1382-1450)
+    for t in required_terms(a.get("podAffinity")):
+        try:
+            matches, exists = _any_pod_matches(pod, all_pods, node_pods, node, t)
+        except AffinityError as err:
+            return False, [R_AFFINITY, R_AFFINITY_RULES], err
+        if not matches:
+            if exists:
+                return False, [R_AFFINITY, R_AFFINITY_RULES], None
+            try:
+                sel = label_selector_as_selector(t.get("labelSelector"))
+            except AffinityError as err:
+                return False, [R_AFFINITY, R_AFFINITY_RULES], err
+            if not pod_matches_term(pod, term_namespaces(pod, t), sel):
+                return False, [R_AFFINITY, R_AFFINITY_RULES], None
+    for t in required_terms(a.get("podAntiAffinity")):
+        try:
+            matches, _ = _any_pod_matches(pod, all_pods, node_pods, node, t)
+        except AffinityError:
+            matches = True               # the error is swallowed: the term fails (:1436-1441)
+        if matches:
+            return False, [R_AFFINITY, R_ANTI_AFFINITY_RULES], None
+    return True, [], None
+
+
+def _interpod_predicate(meta, all_pods):
+    def pred(pod, ni):
+        fits, reasons, err = interpod_affinity_matches(pod, ni.node, meta, all_pods, [(q, ni.node) for q in ni.pods])
+        if err is not None:
+            raise err
+        return fits, reasons
+    return pred
+
+
+def interpod_affinity_priority(pod, infos, filtered_nodes, hard_weight):
+    """CalculateInterPodAffinityPriority (interpod_affinity.go:118-240).  infos: the node infos
+    of nodeNameToInfo (their pods; a pod's node is its info's node); filtered_nodes: the v1.Node
+    list being prioritised.  Returns the 0..10 scores in filtered_nodes' order."""
+    a = _affinity(pod)
+    has_aff, has_anti = a.get("podAffinity") is not None, a.get("podAntiAffinity") is not None
+    counts = [0.0] * len(filtered_nodes)
+
+    def process_term(term, defining, to_check, fixed_node, weight):
+        sel = label_selector_as_selector(term.get("labelSelector"))
+        if pod_matches_term(to_check, term_namespaces(defining, term), sel):
+            for k, n in enumerate(filtered_nodes):
+                if same_topology(n, fixed_node, term.get("topologyKey", "")):
+                    counts[k] += weight
+
+    for info in infos:
+        if info.node is None:
+            continue
+        pods = info.pods if (has_aff or has_anti) else info.pods_with_affinity
+        if not pods:
+            continue
+        for e in pods:
+            enode = info.node
+            ea = _affinity(e)
+            if has_aff:
+                for wt in preferred_terms(a.get("podAffinity")):
+                    process_term(wt.get("podAffinityTerm") or {}, pod, e, enode, float(wt.get("weight", 0)))
+            if has_anti:
+                for wt in preferred_terms(a.get("podAntiAffinity")):
+                    process_term(wt.get("podAffinityTerm") or {}, pod, e, enode, float(-wt.get("weight", 0)))
+            if ea.get("podAffinity") is not None:
+                if hard_weight > 0:
+                    for t in required_terms(ea.get("podAffinity")):
+                        process_term(t, e, pod, enode, float(hard_weight))
+                for wt in preferred_terms(ea.get("podAffinity")):
+                    process_term(wt.get("podAffinityTerm") or {}, e, pod, enode, float(wt.get("weight", 0)))
+            if ea.get("podAntiAffinity") is not None:
+                for wt in preferred_terms(ea.get("podAntiAffinity")):
+                    process_term(wt.get("podAffinityTerm") or {}, e, pod, enode, float(-wt.get("weight", 0)))
+    mx = max([0.0] + counts)
+    mn = min([0.0] + counts)
+    out = []
+    for c in counts:
+        f = 0.0
+        if mx - mn > 0:
+            f = float(MAX_PRIORITY) * ((c - mn) / (mx - mn))
+        out.append(int(f))
+    return out
 
 
 # factory/plugins.go:401-406 + defaults.go:165: always part of the predicate map
@@ -870,7 +1099,7 @@ PRIORITIES = {
     "NodePreferAvoidPodsPriority": ("map", _prio_prefer_avoid),
     "SelectorSpreadPriority": ("spread", _prio_zero),
     "ServiceSpreadingPriority": ("spread", _prio_zero),
-    "InterPodAffinityPriority": ("map", _prio_zero),
+    "InterPodAffinityPriority": ("ipa", None),
     "EqualPriority": ("map", _prio_equal),
     "ImageLocalityPriority": ("map", None),  # set below
 }
@@ -898,14 +1127,19 @@ def prio_image_locality(pod, ni):
 PRIORITIES["ImageLocalityPriority"] = ("map", prio_image_locality)
 
 
-def prioritize_nodes(pod, infos, configs):
-    """S/core/generic_scheduler.go:542-676.  configs: list of (name, weight)."""
+def prioritize_nodes(pod, infos, configs, all_infos=None, hard_weight=10):
+    """S/core/generic_scheduler.go:542-676.  configs: list of (name, weight); infos: the
+    filtered nodes; all_infos: nodeNameToInfo (InterPodAffinityPriority reads every pod)."""
     if not configs:
         return [1 for _ in infos]          # EqualPriorityMap
     total = [0] * len(infos)
     for name, weight in configs:
         kind, fn = PRIORITIES[name]
-        scores = [fn(pod, ni) for ni in infos]
+        if kind == "ipa":
+            scores = interpod_affinity_priority(pod, all_infos if all_infos is not None else infos,
+                                                [ni.node for ni in infos], hard_weight)
+        else:
+            scores = [fn(pod, ni) for ni in infos]
         if kind == "reduce-rev":
             scores = normalize_reduce(scores, True)
         elif kind == "reduce-fwd":
@@ -961,19 +1195,30 @@ class FitError(Exception):
 
 
 class GenericScheduler:
-    def __init__(self, predicate_keys, priority_configs, custom_predicates=None):
+    def __init__(self, predicate_keys, priority_configs, custom_predicates=None, hard_weight=10):
         self.predicates = set(predicate_keys) | set(MANDATORY_PREDICATES)
         self.custom = dict(custom_predicates or {})
         self.prioritizers = list(priority_configs)
+        self.hard_weight = hard_weight    # hardPodAffinitySymmetricWeight (simulator: 10)
         self.last_node_index = 0          # uint64 (generic_scheduler.go:102)
 
     def schedule(self, pod, infos):
-        """Schedule (generic_scheduler.go:112-167). infos: list of NodeInfo in any order."""
+        """Schedule (generic_scheduler.go:112-167). infos: list of NodeInfo in any order (the
+        listed nodes; every cached pod sits on one of them)."""
         if not infos:
             raise RuntimeError("no nodes available to schedule pods")
+        custom = self.custom
+        if "MatchInterPodAffinity" in self.predicates and "MatchInterPodAffinity" not in custom:
+            # the predicate metadata (GetMetadata, metadata.go:102-123: existing pods' anti-affinity
+            # terms, from PodsWithAffinity) once per pod, then the checker per node with the
+            # cache's pods as the pod lister; trivially true without terms on either side
+            meta = matching_anti_affinity_terms(pod, [(p, ni.node) for ni in infos for p in ni.pods_with_affinity])
+            if meta or has_pod_affinity_constraints(pod):
+                all_pods = [(p, ni.node) for ni in infos for p in ni.pods]
+                custom = dict(custom, MatchInterPodAffinity=_interpod_predicate(meta, all_pods))
         filtered, failed = [], {}
         for ni in infos:
-            ok, rs = pod_fits_on_node(pod, ni, self.predicates, self.custom) if self.predicates else (True, [])
+            ok, rs = pod_fits_on_node(pod, ni, self.predicates, custom) if self.predicates else (True, [])
             if ok:
                 filtered.append(ni)
             else:
@@ -982,7 +1227,7 @@ class GenericScheduler:
             raise FitError(len(infos), failed)
         if len(filtered) == 1:
             return filtered[0].name
-        scores = prioritize_nodes(pod, filtered, self.prioritizers)
+        scores = prioritize_nodes(pod, filtered, self.prioritizers, infos, self.hard_weight)
         return self.select_host([(ni.name, s) for ni, s in zip(filtered, scores)])
 
     def select_host(self, plist):

@@ -9,6 +9,9 @@ Run:  python tests/golden/make_golden.py      (rewrites the JSON files)
 """
 import json
 import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 S = "vendor/k8s.io/kubernetes/pkg/scheduler/"
@@ -647,6 +650,77 @@ for ln, pol, err in [
                              "managedResources": [{"name": "kubernetes.io/foo"}]}]},
          "kubernetes.io/foo is an invalid extended resource name")]:
     add("policy_validation", {"source": VT + ":%d" % ln, "policy": pol, "error": err})
+
+
+# ------------------------------------------------ inter-pod affinity (predicate + priority)
+# The cases of TestInterPodAffinity / TestInterPodAffinityWithMultipleNodes
+# (S/algorithm/predicates/predicates_test.go:2168-3146) and TestInterPodAffinityPriority /
+# TestHardPodAffinitySymmetricWeight (S/algorithm/priorities/interpod_affinity_test.go:42-615)
+# are long struct literals: they are read from the reference test files by go_literal.py (data
+# only) rather than retyped.  Each case keeps its harness semantics:
+#  - predicate, single node: every test pod is listed by the pod lister, and FakeNodeInfo maps
+#    any node name to the test node; the metadata sees only the pods on that node;
+#  - predicate, multiple nodes: pods resolve to their own node (FakeNodeListInfo); the metadata
+#    sees the pods of the node under test, or is absent ("nometa": computed from every pod);
+#  - priority: every node's pods (CreateNodeNameToInfoMap), hard weight 1 (the Go default) or
+#    the case's hardPodAffinityWeight.
+REF = "/root/reference/"
+IPA_REASONS = {"ErrPodAffinityNotMatch": "node(s) didn't match pod affinity/anti-affinity",
+               "ErrPodAffinityRulesNotMatch": "node(s) didn't match pod affinity rules",
+               "ErrPodAntiAffinityRulesNotMatch": "node(s) didn't match pod anti-affinity rules",
+               "ErrExistingPodsAntiAffinityRulesNotMatch": "node(s) didn't satisfy existing pods anti-affinity rules"}
+
+
+def _line_of(src, text, start):
+    i = src.find('"%s' % text[:40].replace('"', '\\"'), start)
+    return src.count("\n", 0, i) + 1 if i >= 0 else 0
+
+
+def _reasons(lst):
+    return [IPA_REASONS[r["__ident__"]] for r in (lst or [])]
+
+
+def interpod_cases():
+    import go_literal as g
+    pf = S + "algorithm/predicates/predicates_test.go"
+    with open(REF + pf) as f:
+        src = f.read()
+    start = src.index("func TestInterPodAffinity(")
+    _, cs = g.parse_test(src, "TestInterPodAffinity")
+    for c in cs:
+        add("interpod_predicates", {"source": "%s:%d" % (pf, _line_of(src, c["test"], start)), "test": c["test"],
+                                    "pod": c["pod"], "pods": c.get("pods") or [], "nodes": [c["node"]],
+                                    "single_node": True, "nometa": False,
+                                    "fits": {c["node"]["metadata"]["name"]: c["fits"]},
+                                    "reasons": {c["node"]["metadata"]["name"]: _reasons(c.get("expectFailureReasons"))}})
+    start = src.index("func TestInterPodAffinityWithMultipleNodes(")
+    _, cs = g.parse_test(src, "TestInterPodAffinityWithMultipleNodes")
+    for c in cs:
+        names = [n["metadata"]["name"] for n in c["nodes"]]
+        exp = c.get("nodesExpectAffinityFailureReasons") or [None] * len(names)
+        add("interpod_predicates", {"source": "%s:%d" % (pf, _line_of(src, c["test"], start)), "test": c["test"],
+                                    "pod": c["pod"], "pods": c.get("pods") or [], "nodes": c["nodes"],
+                                    "single_node": False, "nometa": bool(c.get("nometa")), "fits": c["fits"],
+                                    "reasons": {n: _reasons(r) for n, r in zip(names, exp)}})
+    qf = S + "algorithm/priorities/interpod_affinity_test.go"
+    with open(REF + qf) as f:
+        src = f.read()
+    for fn, hw in (("TestInterPodAffinityPriority", 1), ("TestHardPodAffinitySymmetricWeight", None)):
+        start = src.index("func %s(" % fn)
+        _, cs = g.parse_test(src, fn)
+        for c in cs:
+            add("interpod_priorities", {"source": "%s:%d" % (qf, _line_of(src, c["test"], start)), "test": c["test"],
+                                        "pod": c["pod"], "pods": c.get("pods") or [], "nodes": c["nodes"],
+                                        "hard_weight": c["hardPodAffinityWeight"] if hw is None else hw,
+                                        "expect": {h["host"]: h["score"] for h in c["expectedList"]}})
+
+
+if os.path.isdir(REF):
+    interpod_cases()
+else:  # keep the committed fixtures when the reference checkout is absent
+    for group in ("interpod_predicates", "interpod_priorities"):
+        with open(os.path.join(HERE, group + ".json")) as f:
+            cases[group] = json.load(f)
 
 if __name__ == "__main__":
     for group, lst in cases.items():

@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     for f in fns:
         assert hasattr(L, f), f
     assert sorted(fns) == sorted(abi.EXPORTS)
-    assert L.ksim_abi_version() == abi.ABI_VERSION == 2
+    assert L.ksim_abi_version() == abi.ABI_VERSION == 3
 
 
 def test_create_without_device_fails_loudly():
@@ -127,9 +127,24 @@ def test_policy_mapping():
 
 def test_unsupported_pods_rejected():
     n = [{"metadata": {"name": "n"}, "status": {"allocatable": {"cpu": "1", "pods": "10"}}}]
-    p = {"metadata": {"name": "p"}, "spec": {"affinity": {"podAntiAffinity": {"x": 1}}}}
+    # inter-pod affinity inputs on which the reference errors instead of placing
+    term = {"labelSelector": {"matchLabels": {"a": "b"}}}
+    p = {"metadata": {"name": "p"}, "spec": {"affinity": {"podAntiAffinity": {
+        "requiredDuringSchedulingIgnoredDuringExecution": [term]}}}}                 # no topologyKey
     with pytest.raises(abi.KsimUnsupported):
         ingest.Cluster.from_objects(n, [], [p])
+    bad = {"labelSelector": {"matchExpressions": [{"key": "a", "operator": "Gt", "values": ["1"]}]}, "topologyKey": "z"}
+    p = {"metadata": {"name": "p"}, "spec": {"affinity": {"podAffinity": {
+        "requiredDuringSchedulingIgnoredDuringExecution": [bad]}}}}                  # not a pod selector operator
+    with pytest.raises(abi.KsimUnsupported):
+        ingest.Cluster.from_objects(n, [], [p])
+    ok = dict(term, topologyKey="zone")
+    p = {"metadata": {"name": "p"}, "spec": {"affinity": {"podAffinity": {
+        "requiredDuringSchedulingIgnoredDuringExecution": [ok]}}}}
+    assert ingest.Cluster.from_objects(n, [], [p]).affinity is not None
+    r = {"metadata": {"name": "r"}, "spec": {"nodeName": "gone"}}                      # bound to an unknown node
+    with pytest.raises(abi.KsimUnsupported):
+        ingest.Cluster.from_objects(n, [r], [p])
     p = {"metadata": {"name": "p"}, "spec": {"volumes": [{"persistentVolumeClaim": {"claimName": "c"}}]}}
     with pytest.raises(abi.KsimUnsupported):
         ingest.Cluster.from_objects(n, [], [p])

@@ -94,3 +94,98 @@ def rnd_workload(seed, n_nodes=24, n_pods=120, n_running=10, features=True):
         running.append(p)
     pods = [rnd_pod(rng, "sim-%d" % k, features) for k in range(n_pods)]
     return nodes, running, pods
+
+
+# ----------------------------------------------------------------------------- inter-pod affinity
+AFF_KEYS = ["kubernetes.io/hostname", "zone", "region", "rack"]
+APPS = ["web", "db", "cache", "batch"]
+
+
+def rnd_affinity_nodes(rng, n, name_fmt="node-{i}"):
+    """Nodes with topology labels: hostname (missing on a few), zone / region (missing on
+    some), a sparse rack label, and two nodes sharing one hostname value."""
+    nodes = rnd_nodes(rng, n, features=False, name_fmt=name_fmt)
+    for k, x in enumerate(nodes):
+        lab = x["metadata"].setdefault("labels", {})
+        name = x["metadata"]["name"]
+        if rng.random() < 0.9:
+            lab["kubernetes.io/hostname"] = name if k != 1 else nodes[0]["metadata"]["name"]
+        if rng.random() < 0.85:
+            lab["zone"] = "z%d" % rng.randint(0, 3)
+        if rng.random() < 0.8:
+            lab["region"] = "r%d" % rng.randint(0, 1)
+        if rng.random() < 0.25:
+            lab["rack"] = "k%d" % rng.randint(0, 5)
+        if rng.random() < 0.05:
+            x["metadata"]["labels"] = None
+        x["status"]["allocatable"]["pods"] = "110"
+    return nodes
+
+
+def _rnd_selector(rng):
+    r = rng.random()
+    if r < 0.45:
+        return {"matchLabels": {"app": rng.choice(APPS)}}
+    if r < 0.6:
+        return {"matchExpressions": [{"key": "app", "operator": "In", "values": rng.sample(APPS, 2)}]}
+    if r < 0.7:
+        return {"matchExpressions": [{"key": "app", "operator": "NotIn", "values": [rng.choice(APPS)]}]}
+    if r < 0.8:
+        return {"matchExpressions": [{"key": "tier", "operator": "Exists"}]}
+    if r < 0.85:
+        return {"matchExpressions": [{"key": "tier", "operator": "DoesNotExist"}]}
+    if r < 0.92:
+        return {"matchLabels": {"app": rng.choice(APPS), "tier": rng.choice(["fe", "be"])}}
+    return {}
+
+
+def _rnd_term(rng, required):
+    t = {"labelSelector": _rnd_selector(rng), "topologyKey": rng.choice(AFF_KEYS)}
+    if rng.random() < 0.15:
+        t["namespaces"] = rng.sample(["", "ns1", "ns2"], rng.randint(1, 2))
+    if not required and rng.random() < 0.05:
+        t["topologyKey"] = ""                       # allowed on preferred terms: contributes nothing
+    return t
+
+
+def rnd_affinity_pod(rng, name, p_aff=0.6, resources=True):
+    """A pod with labels / namespace drawn from small sets and, with probability p_aff, pod
+    (anti-)affinity terms of every kind."""
+    pod = rnd_pod(rng, name, features=False) if resources else {"metadata": {"name": name}, "spec": {"containers": [{}]}}
+    md = pod["metadata"]
+    md["namespace"] = rng.choice(["", "", "ns1", "ns2"])
+    md["labels"] = {"app": rng.choice(APPS)}
+    if rng.random() < 0.5:
+        md["labels"]["tier"] = rng.choice(["fe", "be"])
+    if rng.random() < 0.1:
+        md["labels"] = {}
+    if rng.random() >= p_aff:
+        return pod
+    aff = {}
+    for sec in ("podAffinity", "podAntiAffinity"):
+        if rng.random() < 0.6:
+            s = {}
+            if rng.random() < 0.5:
+                s["requiredDuringSchedulingIgnoredDuringExecution"] = [_rnd_term(rng, True)
+                                                                        for _ in range(rng.randint(1, 2))]
+            if rng.random() < 0.6:
+                s["preferredDuringSchedulingIgnoredDuringExecution"] = [
+                    {"weight": rng.randint(1, 100), "podAffinityTerm": _rnd_term(rng, False)}
+                    for _ in range(rng.randint(1, 2))]
+            aff[sec] = s
+    if aff:
+        pod["spec"]["affinity"] = aff
+    return pod
+
+
+def rnd_affinity_workload(seed, n_nodes=20, n_pods=80, n_running=12, p_aff=0.6, resources=True):
+    rng = random.Random(seed)
+    nodes = rnd_affinity_nodes(rng, n_nodes)
+    running = []
+    for k in range(n_running):
+        p = rnd_affinity_pod(rng, "run-%d" % k, p_aff, resources)
+        p["metadata"]["uid"] = "run-%d" % k
+        p["spec"]["nodeName"] = rng.choice(nodes)["metadata"]["name"]
+        running.append(p)
+    pods = [rnd_affinity_pod(rng, "sim-%d" % k, p_aff, resources) for k in range(n_pods)]
+    return nodes, running, pods
