@@ -254,6 +254,8 @@ struct KsimGlobalAcc {
     return ksim_bit(c.noexec_ok, P.cls, c.twords, c.taint_set[i]);
   }
   __device__ __forceinline__ bool port_conflict(int64_t i, uint64_t want) const { return ksim_port_conflict(c, i, want); }
+  // k-th host-port key the pod wants
+  __device__ __forceinline__ uint64_t want(const ksim_pod& P, int32_t k) const { return c.pod_ports[P.port_off + k]; }
   __device__ __forceinline__ int tt_class(const ksim_pod& P, int64_t i) const {
     return c.tt_class[(int64_t)P.cls * c.n_taint_sets + c.taint_set[i]];
   }
@@ -265,7 +267,7 @@ struct KsimGlobalAcc {
 template <class A>
 __device__ __forceinline__ uint32_t ksim_hostports(const KsimCtx& c, const ksim_pod& P, int64_t i, const A& a) {
   for (int32_t k = 0; k < P.port_cnt; ++k)
-    if (a.port_conflict(i, c.pod_ports[P.port_off + k])) return 1u << KSIM_R_HOST_PORTS;
+    if (a.port_conflict(i, a.want(P, k))) return 1u << KSIM_R_HOST_PORTS;
   return 0;
 }
 
@@ -476,7 +478,16 @@ __device__ __forceinline__ int ksim_rclass(const KsimCtx& c, const ksim_pod& P, 
 __device__ __forceinline__ int64_t ksim_norm(int64_t v, int64_t mx, bool reverse) {
   if (mx == 0) return reverse ? 10 : v;
   int64_t s;
-  if (v >= 0 && v < (int64_t(1) << 40) && mx > 0 && mx < (int64_t(1) << 40)) {
+  if (v >= 0 && v < (int64_t(1) << 20) && mx > 0 && mx < (int64_t(1) << 24)) {
+    // the common case (taint counts, preference weights): both operands exact in float32 and
+    // the quotient <= 10 for v <= mx, so an approximate reciprocal is within one of the
+    // truncated quotient and one integer correction makes it exact
+    const int32_t x = 10 * (int32_t)v, m = (int32_t)mx;
+    int32_t q = (int32_t)((float)x * __builtin_amdgcn_rcpf((float)m));
+    if (q * m > x) q -= 1;
+    else if ((q + 1) * m <= x) q += 1;
+    s = q;
+  } else if (v >= 0 && v < (int64_t(1) << 40) && mx > 0 && mx < (int64_t(1) << 40)) {
     // map values are small: a correctly rounded float64 quotient plus one integer correction
     // is Go's truncating int64 division (ksim_mul10_div), without the emulated 64-bit divide
     const int64_t x = 10 * v;

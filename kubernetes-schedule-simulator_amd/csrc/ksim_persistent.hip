@@ -12,13 +12,15 @@
 //      decide (findNodesThatFit →                 but one); wave-level (max, count) into LDS
 //      PrioritizeNodes → selectHost,
 //      core/generic_scheduler.go:112-198)
+//   d. owner of p's winner only: pick the exact row from p's entries in LDS, commit it
+//      (NodeInfo.AddPod) and publish the correction of its p+1 partial — O(1): the row waves
+//      evaluated p+1 on every row twice (ev: as is; ev2: with p committed to that row, the
+//      "dual hypothesis") and kept each reduce class's top two (value, count), so replacing
+//      one row's entry needs no re-evaluation and no re-reduction.
 //   ------------------------------- barrier -------------------------------
-//   d. owner of p's winner only: pick the exact node from the p scores in registers, commit
-//      it into LDS (NodeInfo.AddPod), re-evaluate that one row for p+1 and redo its wave's
-//      partial.  Then the control wave combines the row waves' partials of p+1.
 //
 // so the full-table evaluation of the next pod runs concurrently with the exchange, and the
-// critical path per pod is publish → sweep → decide → (owner) one-row fix-up.
+// critical path per pod is sweep → decide → (owner) select + commit + O(1) correction.
 // lastNodeIndex is replicated in every workgroup's control wave.  Granules are
 // double-buffered by pod parity with an 8-bit pod tag: a workgroup that publishes pod p has
 // seen every workgroup's pod p-1 partial, so nobody still reads the p-2 slot it overwrites.
@@ -35,7 +37,7 @@
 namespace {
 
 constexpr int GR = KSIM_MAX_RCLASS;                  // granules per workgroup per slot
-constexpr int MAXB = 4;                              // workgroups per sweep lane (grid <= 256)
+constexpr int MAXB = 4;                              // most workgroups per sweep lane (grid <= 256)
 constexpr int RING = 16;                             // pod-descriptor ring slots in LDS
 constexpr int RING_FILL = 8;                         // descriptors fetched per refill
 constexpr uint64_t SPIN_LIMIT_TICKS = 200000000ull;  // s_memrealtime ticks at 100 MHz = 2 s
@@ -55,14 +57,17 @@ __device__ __forceinline__ uint64_t load_granule(const uint64_t* g) {
 // Dense layout [slot][q][pos(b)]: one poll of class 0 touches 2 KiB (16 lines) instead of a
 // line per workgroup.  pos(b) = (b % MAXB) * 64 + b / MAXB, so the sweep's j-th load of lane l
 // (position j * 64 + l, coalesced across the wave) is workgroup l * MAXB + j.
+// MB: workgroups per sweep lane of the kernel instance (1 for grids of <= 64, else MAXB)
+template <int MB>
 __device__ __forceinline__ uint64_t* spec_at(uint64_t* gr, int slot, int b, int q) {
-  return gr + ((int64_t)slot * GR + q) * MAXG + (b % MAXB) * 64 + b / MAXB;
+  return gr + ((int64_t)slot * GR + q) * MAXG + (b % MB) * 64 + b / MB;
 }
 __device__ __forceinline__ uint64_t* fix_at(uint64_t* gr, int slot, int q) {
   return gr + (int64_t)NSLOT * MAXG * GR + (int64_t)slot * GR + q;
 }
+template <int MB>
 __device__ __forceinline__ uint64_t* gran_at(uint64_t* gr, int slot, int b, int q, int X) {
-  return b == X ? fix_at(gr, slot, q) : spec_at(gr, slot, b, q);
+  return b == X ? fix_at(gr, slot, q) : spec_at<MB>(gr, slot, b, q);
 }
 __device__ __forceinline__ uint32_t gtag(uint64_t v) { return (uint32_t)(v >> 56); }
 __device__ __forceinline__ int32_t gfit(uint64_t v) { return (int32_t)((v >> 44) & 0xFFF); }
@@ -105,12 +110,16 @@ struct Rows {  // LDS image of the owned rows (SoA)
   double *dac, *dam;  // alloc as float64 (derived, for the fast path)
   int32_t *allowed, *count;
   uint32_t* fl;
-  int32_t* ev;  // [2][rows] per pod parity: packed evaluation of the row (ev_pack)
+  int32_t* ev;   // [2][rows] per pod parity: packed evaluation of the row (ev_pack)
   int32_t *ls, *ts;  // label-set / taint-set id of the row
+  int32_t* ev2;  // [2][rows] per pod parity: the evaluation with the previous pod committed to the row
+  uint32_t* rm2; // [2][rows] ... and its reason mask
+  uint32_t* rm1; // [2][rows] reason mask of ev
 };
 
-// 6 x i64 + 2 x f64 + 3 x i32 + 2 x i32 evaluations + 2 x i32 set ids, padded
-constexpr int LDS_ROW_BYTES = 8 * 8 + 3 * 4 + 2 * 4 + 2 * 4 + 4;  // 96
+// 6 x i64 + 2 x f64 + 3 x i32 + 2 x i32 evaluations + 2 x i32 set ids + 2 x 2 x i32 dual
+// hypothesis + 2 x i32 reason masks
+constexpr int LDS_ROW_BYTES = 8 * 8 + 3 * 4 + 2 * 4 + 2 * 4 + 4 * 4 + 2 * 4;  // 116
 
 extern __shared__ __attribute__((aligned(16))) char ksim_smem[];  // dynamic LDS: the row image
 
@@ -126,6 +135,9 @@ __device__ __forceinline__ Rows carve(char* smem, int rows) {
   r.ev = q + 3 * rows;
   r.ls = q + 5 * rows;
   r.ts = q + 6 * rows;
+  r.ev2 = q + 7 * rows;
+  r.rm2 = reinterpret_cast<uint32_t*>(q + 9 * rows);
+  r.rm1 = reinterpret_cast<uint32_t*>(q + 11 * rows);
   return r;
 }
 
@@ -143,53 +155,6 @@ struct PLayout {
 };
 
 namespace {
-
-// The general evaluation's reads beyond the row, from LDS (KsimGlobalAcc's LDS twin).
-struct LdsAcc {
-  const KsimCtx& c;
-  const PLayout& L;
-  int64_t lo;
-  int rows;
-  const int32_t* ls;
-  const int32_t* ts;
-  __device__ __forceinline__ const uint32_t* sel() const {
-    return L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_sel) : c.sel_ok;
-  }
-  __device__ __forceinline__ bool sel_ok(const ksim_pod& P, int64_t i) const {
-    return ksim_bit(sel(), P.cls, c.lwords, ls[i - lo]);
-  }
-  __device__ __forceinline__ bool taint_ok(const ksim_pod& P, int64_t i) const {
-    const uint32_t* t = L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_tok) : c.taint_ok;
-    return ksim_bit(t, P.cls, c.twords, ts[i - lo]);
-  }
-  __device__ __forceinline__ bool noexec_ok(const ksim_pod& P, int64_t i) const {
-    const uint32_t* t = L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_nok) : c.noexec_ok;
-    return ksim_bit(t, P.cls, c.twords, ts[i - lo]);
-  }
-  __device__ __forceinline__ bool port_conflict(int64_t i, uint64_t want) const {
-    if (!L.ps) return ksim_port_conflict(c, i, want);
-    const int j = (int)(i - lo);
-    const int32_t cnt = reinterpret_cast<const int32_t*>(ksim_smem + L.off_pc)[j];
-    const uint64_t* pk = reinterpret_cast<const uint64_t*>(ksim_smem + L.off_pk);
-    const uint32_t wip = (uint32_t)(want >> 40);
-    const uint64_t wpp = want & 0xFFFFFFFFFFull;  // HostPortInfo.CheckConflict (utils.go:101-130)
-    for (int32_t s = 0; s < cnt; ++s) {
-      const uint64_t e = pk[s * rows + j];
-      if ((e & 0xFFFFFFFFFFull) != wpp) continue;
-      const uint32_t eip = (uint32_t)(e >> 40);
-      if (wip == 0 || eip == 0 || eip == wip) return true;
-    }
-    return false;
-  }
-  __device__ __forceinline__ int tt_class(const ksim_pod& P, int64_t i) const {
-    const uint8_t* t = L.tables ? reinterpret_cast<const uint8_t*>(ksim_smem + L.off_ttc) : c.tt_class;
-    return t[(int64_t)P.cls * c.n_taint_sets + ts[i - lo]];
-  }
-  __device__ __forceinline__ int na_class(const ksim_pod& P, int64_t i) const {
-    const uint8_t* t = L.tables ? reinterpret_cast<const uint8_t*>(ksim_smem + L.off_nac) : c.na_class;
-    return t[(int64_t)P.cls * c.n_label_sets + ls[i - lo]];
-  }
-};
 
 // Commit of the columns that stay in HBM (gpu, ephemeral, scalars, ports) and of the
 // over-commit bits (node_info.go:318-341, utils.go:45-60).  Single thread of the owner.
@@ -275,69 +240,78 @@ __device__ __forceinline__ int64_t readlane64(int64_t v, int q) {
                    (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)v, q));
 }
 
-// General per-row evaluation (any supported pod), everything it reads in LDS (LdsAcc) except
-// the gpu / ephemeral / scalar columns of pods requesting them.  Reads the context through a
-// pointer to its device-memory copy, so no kernel-argument copy goes to scratch.
-struct RowEval {
-  int32_t sc;
-  uint32_t rm;
-  int32_t cl;
-  int32_t fit;
+// A committed pod's change to a row (NodeInfo.AddPod of the resource-only part): the dual
+// hypothesis evaluates the next pod on row + delta.  pp: the two pods' host ports conflict.
+struct RowDelta {
+  int64_t c, m, zc, zm;
+  int32_t n, pp;
+  int64_t g, e;  // gpu / ephemeral adds (the over-commit bits are re-derived from HBM)
 };
-
-typedef __attribute__((address_space(3))) const KsimCtx lds_ctx;
-typedef __attribute__((address_space(3))) const PLayout lds_layout;
-typedef __attribute__((address_space(3))) const ksim_pod lds_pod;
-
-// One out-of-line copy shared by the row waves, the owner's pre-evaluation and its fix-up: its
-// context, layout and pod are LDS copies, so nothing it reads for a plain pod leaves the CU.
-__device__ __noinline__ RowEval eval_row_general(lds_ctx* cl, lds_layout* Ll, lds_pod* Pl, int chunk, int64_t i,
-                                                 int64_t j) {
-  const KsimCtx& c = *(const KsimCtx*)cl;
-  const PLayout& Lp = *(const PLayout*)Ll;
-  const ksim_pod& P = *(const ksim_pod*)Pl;
-  const int k1 = P.reserved[0], k2 = P.reserved[1];
-  const Rows R = carve(ksim_smem, chunk);
-  const LdsAcc acc{c, Lp, i - j, chunk, R.ls, R.ts};
-  KsimRow r;
-  r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j]; r.rm = R.rm[j]; r.zc = R.zc[j]; r.zm = R.zm[j];
-  r.allowed = R.allowed[j]; r.count = R.count[j]; r.fl = R.fl[j];
-  const uint32_t m = ksim_predicates_a(c, P, i, r, acc);
-  RowEval e;
-  e.fit = (m == 0);
-  e.rm = m;
-  // ksim_map_score through ksim_fast.h's float64 form (bit-identical; out-of-line beyond 2^49)
-  e.sc = c.no_prio ? 0
-                   : (int32_t)ksim_fast_score(P.nz_cpu + r.zc, r.ac, R.dac[j], P.nz_mem + r.zm, r.am, R.dam[j],
-                                              c.w[KSIM_W_LEAST_REQUESTED], c.w[KSIM_W_MOST_REQUESTED], c.w[KSIM_W_BALANCED]);
-  e.cl = (k1 * k2 > 1) ? ksim_rclass_a(P, i, k1, k2, acc) : 0;
-  return e;
-}
 
 }  // namespace
 
-template <int BS, int NPT>
+// The uniform inputs of one pod's evaluation, read once per pod from the LDS ring into
+// registers (the per-row evaluation then touches LDS only for the row and its table bits).
+struct PodView {
+  int64_t rq_c, rq_m, rq_g, rq_e, nz_c, nz_m;
+  uint32_t flags;
+  int32_t host, cls, k1, k2;
+  int32_t port_cnt, port_off, scalar_off, scalar_cnt;
+  bool fast;  // resource-only (ksim_is_fast_pod)
+};
+
+// The descriptor in LDS → PodView with eight 16-byte reads issued together.
+__device__ __forceinline__ PodView pod_view_lds(const ksim_pod* Pl);
+
+__device__ __forceinline__ PodView pod_view(const ksim_pod& P) {
+  PodView V;
+  V.rq_c = P.req_cpu; V.rq_m = P.req_mem; V.rq_g = P.req_gpu; V.rq_e = P.req_eph;
+  V.nz_c = P.nz_cpu; V.nz_m = P.nz_mem;
+  V.flags = P.flags; V.host = P.host; V.cls = P.cls; V.k1 = P.reserved[0]; V.k2 = P.reserved[1];
+  V.port_cnt = P.port_cnt; V.port_off = P.port_off; V.scalar_off = P.scalar_off; V.scalar_cnt = P.scalar_cnt;
+  V.fast = ksim_is_fast_pod(P, V.k1 * V.k2);
+  return V;
+}
+
+__device__ __forceinline__ PodView pod_view_lds(const ksim_pod* Pl) {
+  const uint4* w = reinterpret_cast<const uint4*>(Pl);
+  uint4 a[sizeof(ksim_pod) / 16];
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(ksim_pod) / 16); ++k) a[k] = w[k];
+  ksim_pod P;
+  __builtin_memcpy(&P, a, sizeof P);
+  return pod_view(P);
+}
+
+template <int BS, int NPT, int MB>
 __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const KsimCtx* __restrict__ cg,
                                                              uint64_t* granules, PLayout L) {
   constexpr int NW = BS / 64;
-  constexpr int RT = BS - 64;  // row threads
-  __shared__ int32_t s_mx[2][NW][KSIM_MAX_RCLASS];   // per row wave, double-buffered by pod parity
-  __shared__ int32_t s_cnt[2][NW][KSIM_MAX_RCLASS];
+  constexpr int RT = BS - 64;          // row threads
+  constexpr int SPLIT_ROWS = 192;       // dual-hypothesis split: ev on the first waves, ev2 on the next
+  constexpr int PPK = 4;                 // host-port keys staged per pod descriptor
+  __shared__ int32_t s_mx[2][NW][KSIM_MAX_RCLASS];   // per row wave, double-buffered by pod parity:
+  __shared__ int32_t s_cnt[2][NW][KSIM_MAX_RCLASS];  // per reduce class the top value and its count,
+  __shared__ int32_t s_mx2[2][NW][KSIM_MAX_RCLASS];  // the second value and its count
+  __shared__ int32_t s_cnt2[2][NW][KSIM_MAX_RCLASS];
   __shared__ int32_t s_fit[2][NW];
-  __shared__ uint64_t s_fm[2][NPT][NW];  // single-class pods: per 64-row segment, fit rows
-  __shared__ uint64_t s_bm[2][NPT][NW];  // ... and rows at the wave maximum
-  __shared__ int32_t s_fix[2][2];  // per pod parity: {row the owner re-evaluated (-1 none), its reason mask}
+  __shared__ int4 s_top[2][KSIM_MAX_RCLASS];  // the workgroup's (top, count, second, count) per class
+  __shared__ int32_t s_F[2];                  // ... its fit rows
+  __shared__ int32_t s_done[2];               // tag of the pod whose workgroup stats are complete
+  __shared__ int32_t s_ev2[2];                // 1: ev2 was evaluated for that pod
   __shared__ int32_t s_hist[KSIM_NREASONS];
   __shared__ int32_t s_M[KSIM_MAX_RCLASS];
   __shared__ uint64_t s_gq[KSIM_MAX_RCLASS - 1][MAXG];  // control wave: granules of classes >= 1 (by b)
   __shared__ int32_t s_C[KSIM_MAX_RCLASS];
-  __shared__ int32_t s_mode;
-  __shared__ int32_t s_arr;  // row-wave arrivals (the last one of a pod publishes)
+  __shared__ int32_t s_dec;    // pods decided and committed (control wave → row waves)
+  __shared__ int32_t s_abort;  // the control wave stopped on an error
+  __shared__ int32_t s_arr[2];  // row-wave arrivals per pod parity (the last one of a pod publishes)
   __shared__ __attribute__((aligned(16))) ksim_pod s_pod[RING];
-  __shared__ PLayout s_L;
-  __shared__ KsimCtx s_ctx;  // the evaluation's copy of the context (LDS reads, no K$ misses)
+  __shared__ uint64_t s_ppk[RING][PPK];  // the ring's pods' host-port keys (pods with <= PPK ports)
 #ifdef KSIM_STAMPS
   uint64_t st_acc[16] = {};
+  uint64_t ev_acc[4] = {};  // row wave 1: pod view, evaluation, read-back (tid 64 of block 0)
+  uint64_t wait_acc = 0;    // row wave 1: waiting for the control wave (s_dec)
 #endif
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -351,6 +325,8 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   const uint32_t preds = c.preds;
   const int64_t wl = c.w[KSIM_W_LEAST_REQUESTED], wmr = c.w[KSIM_W_MOST_REQUESTED], wb = c.w[KSIM_W_BALANCED];
   const bool no_prio = c.no_prio != 0;
+  // dual hypothesis layout: split (ev and ev2 on disjoint waves) when the rows fit both halves
+  const bool split = NPT == 1 && nrows <= SPLIT_ROWS;
 
   for (int32_t j = tid; j < nrows; j += BS) {  // stage the owned rows into LDS
     const int64_t i = lo + j;
@@ -382,107 +358,294 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       reinterpret_cast<int64_t*>(ksim_smem + L.off_nav)[k] = c.na_val[k];
     }
   }
-  if (tid == 0) { s_L = L; s_ctx = c; }
-  // pod ring: RING_FILL descriptors (1 KiB) per refill, one 16-byte load per lane of wave 1
-  // pod ring: RING_FILL descriptors (1 KiB) per refill, one 16-byte load per lane of wave 1.
-  // The reduce-class counts k1 (TaintToleration) / k2 (NodeAffinity) ride in each queued
-  // descriptor's reserved[0..1] (written by the library, ksim_launch_pod_k).
-  auto ring_load = [&](int64_t p0, uint4& v) {
+  // pod ring: RING_FILL descriptors (1 KiB) per refill, one 16-byte load per lane of wave 1, then
+  // their host-port keys (lane 4s+k: key k of the refill's pod s).  The reduce-class counts k1
+  // (TaintToleration) / k2 (NodeAffinity) ride in each queued descriptor's reserved[0..1]
+  // (written by the library, ksim_launch_pod_k).
+  auto ring_load = [&](int64_t p0, uint4& v, uint64_t& key) {
     const int64_t p = p0 + lane / 8;
     if (p < c.end) v = reinterpret_cast<const uint4*>(&c.pods[p])[lane % 8];
+    // port_off (bytes 92..95) sits in part 5's .w, port_cnt (96..99) in part 6's .x
+    const int s = lane / PPK, k = lane % PPK;
+    const int32_t off = __shfl((int32_t)v.w, s * 8 + 5, 64), cnt = __shfl((int32_t)v.x, s * 8 + 6, 64);
+    key = 0;
+    if (lane < RING_FILL * PPK && p0 + s < c.end && k < cnt && cnt <= PPK) key = c.pod_ports[off + k];
   };
-  auto ring_store = [&](int64_t p0, const uint4& v) {
+  auto ring_store = [&](int64_t p0, const uint4& v, uint64_t key) {
     const int64_t p = p0 + lane / 8;
     if (p < c.end) reinterpret_cast<uint4*>(&s_pod[p % RING])[lane % 8] = v;
+    if (lane < RING_FILL * PPK && p0 + lane / PPK < c.end) s_ppk[(p0 + lane / PPK) % RING][lane % PPK] = key;
   };
   if (wv == 1) {
-    uint4 v;
-    ring_load(c.first, v);
-    ring_store(c.first, v);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    uint64_t key;
+    ring_load(c.first, v, key);
+    ring_store(c.first, v, key);
   }
-  if (tid == 0) { s_fix[c.first & 1][0] = -1; s_arr = 0; }
+  if (tid == 0) {
+    s_arr[0] = s_arr[1] = 0;
+    s_done[0] = s_done[1] = -1;
+    s_dec = 0;
+    s_abort = 0;
+    s_ev2[0] = s_ev2[1] = 0;
+  }
   uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex (control wave)
   __syncthreads();
 
   auto pod_K = [&](const ksim_pod& P) -> int { return P.reserved[0] * P.reserved[1]; };
-  // one row against pod P → packed entry + reason mask (fast path when the pod qualifies)
-  auto load_row = [&](int32_t j) -> KsimFastRow {
+  // One row against pod V (the pod at ring slot p) → packed entry (ev_pack, -1 = does not fit)
+  // and reason mask: ksim_predicates_a's predicatesOrdering chain (predicates.go:129-138)
+  // evaluated branch-free on the LDS row, the map score in ksim_fast.h's float64 form
+  // (bit-identical), the reduce class from the staged class tables.  d: the previous pod
+  // committed to the row (dual hypothesis), or zero.
+  auto eval_row = [&](const PodView& V, int64_t p, int32_t j, const RowDelta& d, uint32_t& rm) -> int32_t {
     KsimFastRow r;
-    r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j]; r.rm = R.rm[j]; r.zc = R.zc[j]; r.zm = R.zm[j];
-    r.dac = R.dac[j]; r.dam = R.dam[j];
-    r.allowed = R.allowed[j]; r.count = R.count[j]; r.fl = R.fl[j];
-    return r;
-  };
-  auto eval_one = [&](const ksim_pod& P, bool fast, int32_t j, uint32_t& rm) -> int32_t {
-    if (fast) {
-      const KsimFastPod F{P.req_cpu, P.req_mem, P.nz_cpu, P.nz_mem, P.flags};
-      return ksim_fast_eval(preds, F, load_row(j), no_prio, wl, wmr, wb, rm);
+    r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j] + d.c; r.rm = R.rm[j] + d.m; r.zc = R.zc[j] + d.zc;
+    r.zm = R.zm[j] + d.zm; r.dac = R.dac[j]; r.dam = R.dam[j];
+    r.allowed = R.allowed[j]; r.count = R.count[j] + d.n; r.fl = R.fl[j];
+    if (d.g | d.e) {  // the previous pod's gpu / ephemeral request re-derives the over-commit bits
+      const int64_t i = lo + j;
+      r.fl &= ~(KSIM_N_GPU_OVER | KSIM_N_EPH_OVER);
+      if (c.alloc_gpu[i] < c.req_gpu[i] + d.g) r.fl |= KSIM_N_GPU_OVER;
+      if (c.alloc_eph[i] < c.req_eph[i] + d.e) r.fl |= KSIM_N_EPH_OVER;
     }
-    const RowEval e = eval_row_general((lds_ctx*)&s_ctx, (lds_layout*)&s_L, (lds_pod*)&P, (int)chunk, lo + j, j);
-    rm = e.rm;
-    return ev_pack(e.fit != 0, e.cl, e.sc);
+    if (V.fast) {
+      const KsimFastPod F{V.rq_c, V.rq_m, V.nz_c, V.nz_m, V.flags};
+      return ksim_fast_eval(preds, F, r, no_prio, wl, wmr, wb, rm);
+    }
+    const int64_t i = lo + j;
+    const int32_t ls = R.ls[j], ts = R.ts[j];
+    const uint32_t fl = r.fl;
+    // PodFitsResources (predicates.go:706-778)
+    uint32_t res = (r.count + 1 > r.allowed) ? (1u << KSIM_R_INSUFFICIENT_PODS) : 0u;
+    if (V.flags & KSIM_POD_ANY_REQUEST) {
+      res |= (r.ac < V.rq_c + r.rc) ? (1u << KSIM_R_INSUFFICIENT_CPU) : 0u;
+      res |= (r.am < V.rq_m + r.rm) ? (1u << KSIM_R_INSUFFICIENT_MEMORY) : 0u;
+      if (V.rq_g == 0) res |= (fl & KSIM_N_GPU_OVER) ? (1u << KSIM_R_INSUFFICIENT_GPU) : 0u;
+      else if (c.alloc_gpu[i] < V.rq_g + c.req_gpu[i] + d.g) res |= 1u << KSIM_R_INSUFFICIENT_GPU;
+      if (V.rq_e == 0) res |= (fl & KSIM_N_EPH_OVER) ? (1u << KSIM_R_INSUFFICIENT_EPHEMERAL) : 0u;
+      else if (c.alloc_eph[i] < V.rq_e + c.req_eph[i] + d.e) res |= 1u << KSIM_R_INSUFFICIENT_EPHEMERAL;
+      for (int32_t s = 0; s < V.scalar_cnt; ++s) {
+        const ksim_scalar_req q = c.pod_scalars[V.scalar_off + s];
+        const int64_t off = (int64_t)q.col * c.n + i;
+        if (c.alloc_scalar[off] < q.req + c.req_scalar[off]) res |= 1u << (KSIM_R_INSUFFICIENT_SCALAR0 + q.col);
+      }
+    }
+    const uint32_t host = (V.host == -1 || V.host == i) ? 0u : (1u << KSIM_R_HOSTNAME);
+    // PodFitsHostPorts (predicates.go:1019-1039, HostPortInfo.CheckConflict utils.go:101-130)
+    uint32_t ports = 0;
+    if (V.port_cnt) {
+      const bool lk = V.port_cnt <= PPK;
+      const int32_t pc = L.ps ? reinterpret_cast<const int32_t*>(ksim_smem + L.off_pc)[j] : c.port_count[i];
+      for (int32_t k = 0; k < V.port_cnt && !ports; ++k) {
+        const uint64_t want = lk ? s_ppk[p % RING][k] : c.pod_ports[V.port_off + k];
+        const uint32_t wip = (uint32_t)(want >> 40);
+        const uint64_t wpp = want & 0xFFFFFFFFFFull;
+        bool hit = d.pp != 0;
+        for (int32_t sl = 0; sl < pc && !hit; ++sl) {
+          const uint64_t e = L.ps ? reinterpret_cast<const uint64_t*>(ksim_smem + L.off_pk)[sl * chunk + j]
+                                  : c.ports[(int64_t)sl * c.n + i];
+          if ((e & 0xFFFFFFFFFFull) != wpp) continue;
+          const uint32_t eip = (uint32_t)(e >> 40);
+          hit = wip == 0 || eip == 0 || eip == wip;
+        }
+        if (hit) ports = 1u << KSIM_R_HOST_PORTS;
+      }
+    }
+    // podMatchesNodeLabels / tolerations: bits of the staged class tables
+    uint32_t sel = 0, taint = 0, noexec = 0;
+    if (V.flags & KSIM_POD_NEED_SELECTOR) {
+      const int64_t w = (int64_t)V.cls * c.lwords + (ls >> 5);
+      const uint32_t word = L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_sel)[w] : c.sel_ok[w];
+      sel = ((word >> (ls & 31)) & 1u) ? 0u : (1u << KSIM_R_NODE_SELECTOR);
+    }
+    if (V.flags & KSIM_POD_NEED_TAINTS) {
+      const int64_t w = (int64_t)V.cls * c.twords + (ts >> 5);
+      const uint32_t wt = L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_tok)[w] : c.taint_ok[w];
+      const uint32_t wn = L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_nok)[w] : c.noexec_ok[w];
+      taint = ((wt >> (ts & 31)) & 1u) ? 0u : (1u << KSIM_R_TAINTS);
+      noexec = ((wn >> (ts & 31)) & 1u) ? 0u : (1u << KSIM_R_TAINTS);
+    }
+    // the first failing predicate in order (ksim_predicates_a)
+    const uint32_t pr = preds;
+    const uint32_t m_cond = (pr & KSIM_P_CHECK_NODE_CONDITION) ? (fl & KSIM_COND_REASON_MASK) : 0u;
+    const uint32_t m_uns = ((pr & KSIM_P_CHECK_NODE_UNSCHEDULABLE) && (fl & KSIM_N_UNSCHEDULABLE)) ? (1u << KSIM_R_UNSCHEDULABLE) : 0u;
+    const uint32_t m_gen = (pr & KSIM_P_GENERAL) ? (res | host | ports | sel) : 0u;
+    const uint32_t m_host = (pr & KSIM_P_HOSTNAME) ? host : 0u;
+    const uint32_t m_ports = (pr & KSIM_P_HOST_PORTS) ? ports : 0u;
+    const uint32_t m_sel = (pr & KSIM_P_NODE_SELECTOR) ? sel : 0u;
+    const uint32_t m_res = (pr & KSIM_P_RESOURCES) ? res : 0u;
+    const uint32_t m_t = (pr & KSIM_P_TAINTS) ? taint : 0u;
+    const uint32_t m_nt = (pr & KSIM_P_NOEXEC_TAINTS) ? noexec : 0u;
+    const uint32_t m_lp = ((pr & KSIM_P_LABEL_PRESENCE) && (fl & KSIM_N_LABEL_PRESENCE)) ? (1u << KSIM_R_LABEL_PRESENCE) : 0u;
+    const uint32_t m_mp = ((pr & KSIM_P_MEM_PRESSURE) && (V.flags & KSIM_POD_BEST_EFFORT) && (fl & KSIM_N_MEM_PRESSURE))
+                              ? (1u << KSIM_R_MEM_PRESSURE) : 0u;
+    const uint32_t m_dp = ((pr & KSIM_P_DISK_PRESSURE) && (fl & KSIM_N_DISK_PRESSURE)) ? (1u << KSIM_R_DISK_PRESSURE) : 0u;
+    const uint32_t m = m_cond ? m_cond : m_uns ? m_uns : m_gen ? m_gen : m_host ? m_host : m_ports ? m_ports
+                     : m_sel ? m_sel : m_res ? m_res : m_t ? m_t : m_nt ? m_nt : m_lp ? m_lp : m_mp ? m_mp : m_dp;
+    rm = m;
+    if (m) return -1;
+    const int32_t sc = no_prio ? 0 : (int32_t)ksim_fast_score(V.nz_c + r.zc, r.ac, r.dac, V.nz_m + r.zm, r.am, r.dam, wl, wmr, wb);
+    int32_t cl = 0;
+    if (V.k1 * V.k2 > 1) {
+      int a = 0, b = 0;
+      if (V.k1 > 1) {
+        const int64_t x = (int64_t)V.cls * c.n_taint_sets + ts;
+        a = L.tables ? (uint8_t)(ksim_smem + L.off_ttc)[x] : c.tt_class[x];
+      }
+      if (V.k2 > 1) {
+        const int64_t x = (int64_t)V.cls * c.n_label_sets + ls;
+        b = L.tables ? (uint8_t)(ksim_smem + L.off_nac)[x] : c.na_class[x];
+      }
+      cl = a * V.k2 + b;
+    }
+    return ev_pack(true, cl, sc);
   };
-  // row wave: all rows of this lane for pod p → LDS entries + reason masks
-  auto eval_rows = [&](int64_t p, int32_t (&e)[NPT], uint32_t (&rm)[NPT], int32_t* ev) {
+  // The delta pod `p` makes to a row when committed, if the dual hypothesis can express it: not
+  // when both pods carry scalar resources, nor beyond PPK host ports (host ports go through the
+  // pair-conflict flag against pod q; gpu / ephemeral through re-derived over-commit bits).
+  auto delta_of = [&](int64_t p, int64_t q, RowDelta& d) -> bool {
     const ksim_pod& P = s_pod[p % RING];
-    const bool fast = ksim_is_fast_pod(P, pod_K(P));
+    const ksim_pod& Q = s_pod[q % RING];
+    if (P.scalar_cnt && Q.scalar_cnt) return false;
+    if (P.port_cnt > PPK || Q.port_cnt > PPK) return false;
+    d.c = P.add_cpu; d.m = P.add_mem; d.zc = P.nz_cpu; d.zm = P.nz_mem; d.n = 1; d.pp = 0;
+    d.g = P.add_gpu; d.e = P.add_eph;
+    // HostPortInfo.CheckConflict of Q's wanted keys against P's (utils.go:101-130)
+    for (int32_t a = 0; a < Q.port_cnt; ++a) {
+      const uint64_t want = s_ppk[q % RING][a];
+      const uint32_t wip = (uint32_t)(want >> 40);
+      for (int32_t b = 0; b < P.port_cnt; ++b) {
+        const uint64_t e = s_ppk[p % RING][b];
+        if ((e & 0xFFFFFFFFFFull) != (want & 0xFFFFFFFFFFull)) continue;
+        const uint32_t eip = (uint32_t)(e >> 40);
+        if (wip == 0 || eip == 0 || eip == wip) d.pp = 1;
+      }
+    }
+    return true;
+  };
+  // row wave: pod p's entries (ev) for this lane's rows → LDS ev / rm1; with `hyp`, also the
+  // entries with pod p-1 committed to each row (ev2 / rm2) — on the next waves up when the rows
+  // fit one wave set each (split), else after ev on the same lane.  One evaluation call site,
+  // so one inlined copy; the partial reads the entries back from LDS.
+  auto eval_rows = [&](int64_t p, bool hyp, const RowDelta& d, int32_t (&e)[NPT], int buf) {
+#ifdef KSIM_STAMPS
+    const uint64_t q0 = __builtin_amdgcn_s_memtime();
+#endif
+    const PodView V = pod_view_lds(&s_pod[p % RING]);
+#ifdef KSIM_STAMPS
+    const uint64_t q1 = __builtin_amdgcn_s_memtime();
+#endif
+    const RowDelta z{0, 0, 0, 0, 0, 0, 0, 0};
+    int32_t* ev = R.ev + buf * chunk;
+    uint32_t* rm1 = R.rm1 + buf * chunk;
+    int32_t* ev2 = R.ev2 + buf * chunk;
+    uint32_t* rm2 = R.rm2 + buf * chunk;
+    const int32_t half = split ? 64 * ((nrows + 63) / 64) : 0;  // split: ev2 threads start here
+    const int ntask = split ? 1 : NPT * (hyp ? 2 : 1);
+#pragma unroll 1
+    for (int t = 0; t < ntask; ++t) {
+      int32_t j;
+      bool h;
+      if (split) {
+        h = rt >= half;
+        j = h ? rt - half : rt;
+        if (h && !hyp) j = nrows;  // nothing to do
+      } else {
+        h = hyp && (t & 1);
+        j = (hyp ? t >> 1 : t) * RT + rt;
+      }
+      if (j < nrows) {
+        uint32_t m;
+        const int32_t x = eval_row(V, p, j, h ? d : z, m);
+        if (h) { ev2[j] = x; rm2[j] = m; }
+        else { ev[j] = x; rm1[j] = m; }
+      }
+    }
+#ifdef KSIM_STAMPS
+    const uint64_t q2 = __builtin_amdgcn_s_memtime();
+#endif
+    // this lane's entries for the partial (split: the ev threads' only)
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int32_t j = k * RT + rt;
-      e[k] = -1;
-      rm[k] = 0;
-      if (j < nrows) {
-        e[k] = eval_one(P, fast, j, rm[k]);
-        ev[j] = e[k];
-      }
+      e[k] = (j < nrows && !(split && rt >= half)) ? ev[j] : -1;
     }
+#ifdef KSIM_STAMPS
+    const uint64_t q3 = __builtin_amdgcn_s_memtime();
+    ev_acc[0] += q1 - q0; ev_acc[1] += q2 - q1; ev_acc[2] += q3 - q2; ev_acc[3] += 1;
+#endif
   };
-  // (fit count, per-class max, count at max) of one row wave's entries → LDS slot w
+  // (fit count, per class: top value / count, second value / count) of one row wave → LDS slot w.
+  // Four classes at a time: their DPP reductions are independent chains that interleave.
   auto partial = [&](const int32_t (&e)[NPT], int K, int buf, int w) {
-    uint64_t fm[NPT];
     int32_t nf = 0;
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      fm[k] = __ballot(e[k] >= 0);
-      nf += __popcll(fm[k]);
-    }
-    if (K == 1) {  // class 0: the entry is the score
-      int32_t v = -1;
-#pragma unroll
-      for (int k = 0; k < NPT; ++k) v = e[k] > v ? e[k] : v;
-      const int32_t wm = ksimw::max_i32(v);
-      int32_t n = 0;
-#pragma unroll
-      for (int k = 0; k < NPT; ++k) {
-        const uint64_t bm = wm < 0 ? 0ull : __ballot(e[k] == wm);
-        n += __popcll(bm);
-        if (lane == 0) { s_fm[buf][k][w] = fm[k]; s_bm[buf][k][w] = bm; }
-      }
-      if (lane == 0) { s_fit[buf][w] = nf; s_mx[buf][w][0] = wm; s_cnt[buf][w][0] = n; }
-      return;
-    }
+    for (int k = 0; k < NPT; ++k) nf += __popcll(__ballot(e[k] >= 0));
     if (lane == 0) s_fit[buf][w] = nf;
-    for (int q = 0; q < K; ++q) {
-      int32_t v = -1;
+    for (int q0 = 0; q0 < K; q0 += 4) {
+      int32_t v[4], wm[4], n[4], v2[4], wm2[4], n2[4];
 #pragma unroll
-      for (int k = 0; k < NPT; ++k)
-        if (e[k] >= 0 && ev_cls(e[k]) == q && ev_score(e[k]) > v) v = ev_score(e[k]);
-      const int32_t wm = ksimw::max_i32(v);
-      int32_t n = 0;
+      for (int u = 0; u < 4; ++u) {
+        v[u] = -1;
 #pragma unroll
-      for (int k = 0; k < NPT; ++k) n += __popcll(__ballot(e[k] >= 0 && ev_cls(e[k]) == q && ev_score(e[k]) == wm));
-      if (lane == 0) { s_mx[buf][w][q] = wm; s_cnt[buf][w][q] = (wm < 0) ? 0 : n; }
+        for (int k = 0; k < NPT; ++k) {
+          const bool in = e[k] >= 0 && (K == 1 || ev_cls(e[k]) == q0 + u);
+          const int32_t sc = K == 1 ? e[k] : ev_score(e[k]);
+          v[u] = (in && sc > v[u]) ? sc : v[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wm[u] = ksimw::max_i32(v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        n[u] = 0;
+        v2[u] = -1;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          const bool in = e[k] >= 0 && (K == 1 || ev_cls(e[k]) == q0 + u);
+          const int32_t sc = K == 1 ? e[k] : ev_score(e[k]);
+          n[u] += __popcll(__ballot(in && sc == wm[u]));
+          v2[u] = (in && sc < wm[u] && sc > v2[u]) ? sc : v2[u];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) wm2[u] = ksimw::max_i32(v2[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        n2[u] = 0;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          const bool in = e[k] >= 0 && (K == 1 || ev_cls(e[k]) == q0 + u);
+          const int32_t sc = K == 1 ? e[k] : ev_score(e[k]);
+          n2[u] += __popcll(__ballot(in && wm2[u] >= 0 && sc == wm2[u]));
+        }
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (q0 + u >= K) break;
+          s_mx[buf][w][q0 + u] = wm[u]; s_cnt[buf][w][q0 + u] = wm[u] < 0 ? 0 : n[u];
+          s_mx2[buf][w][q0 + u] = wm2[u]; s_cnt2[buf][w][q0 + u] = wm2[u] < 0 ? 0 : n2[u];
+        }
+      }
     }
   };
-  // control wave: combine the row waves' partials → granule payloads (lane q = class q)
+  // the last row wave of a pod: combine the row waves' partials (lane q = class q) into the
+  // workgroup's top two per class → LDS (the owner's correction) and the granule payloads
   auto combine = [&](int K, int buf) -> uint64_t {
     const int q = lane < K ? lane : 0;
-    int32_t f = 0, mx[NW], cn[NW];
+    int32_t f = 0, mx[NW], cn[NW], mx2[NW], cn2[NW];
 #pragma unroll
     for (int w = 1; w < NW; ++w) {  // all loads first: one LDS round trip
       f += s_fit[buf][w];
       mx[w] = s_mx[buf][w][q];
       cn[w] = s_cnt[buf][w][q];
+      mx2[w] = s_mx2[buf][w][q];
+      cn2[w] = s_cnt2[buf][w][q];
     }
     int32_t m = -1, n = 0;
 #pragma unroll
@@ -491,6 +654,21 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       n = up ? cn[w] : (eq ? n + cn[w] : n);
       m = up ? mx[w] : m;
     }
+    // second value: the best below m among the waves' tops and seconds
+    int32_t m2 = -1, n2 = 0;
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      const int32_t a = (cn[w] != 0 && mx[w] < m) ? mx[w] : (cn2[w] != 0 ? mx2[w] : -1);
+      m2 = a > m2 ? a : m2;
+    }
+#pragma unroll
+    for (int w = 1; w < NW; ++w) {
+      if (m2 < 0) break;
+      n2 += (cn[w] != 0 && mx[w] == m2) ? cn[w] : 0;
+      n2 += (cn2[w] != 0 && mx2[w] == m2) ? cn2[w] : 0;
+    }
+    if (lane < K) s_top[buf][lane] = make_int4(m, n, m2, n2);
+    if (lane == 0) s_F[buf] = f;
     if (lane >= K) return 0;
     return (lane == 0 ? ((uint64_t)f << 44) : 0) | ((uint64_t)n << 32) | (uint64_t)(uint32_t)m;
   };
@@ -498,22 +676,27 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   // row waves: the last one to finish pod p's partial combines and publishes it
   auto arrive_publish = [&](int64_t p, int K, int buf) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    // per-parity counter: a row wave can run a pod ahead of its slower siblings (the waves are
+    // decoupled), never two, so pods of one parity never mix; the last arriver re-arms it
     int32_t old = 0;
-    if (lane == 0) old = atomicAdd(&s_arr, 1);
+    if (lane == 0) old = atomicAdd(&s_arr[buf], 1);
     old = __builtin_amdgcn_readfirstlane(old);
-    if ((old + 1) % (NW - 1) == 0) {
+    if (old + 1 == NW - 1) {
+      if (lane == 0) s_arr[buf] = 0;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       const uint64_t v = combine(K, buf);
-      if (lane < K) store_granule(spec_at(granules, (int)(p % NSLOT), blockIdx.x, lane), (ptag(p) << 56) | v);
+      if (lane < K) store_granule(spec_at<MB>(granules, (int)(p % NSLOT), blockIdx.x, lane), (ptag(p) << 56) | v);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&s_done[buf], (int32_t)ptag(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   };
 
   // ---- prologue: partial of the first pod ----
-  uint32_t A_rm[NPT], B_rm[NPT];
   if (wv > 0) {
     int32_t e[NPT];
     const int K0 = pod_K(s_pod[c.first % RING]);
-    eval_rows(c.first, e, A_rm, R.ev + (c.first & 1) * chunk);
+    const RowDelta z{0, 0, 0, 0, 0, 0, 0, 0};
+    eval_rows(c.first, false, z, e, (int)(c.first & 1));
     partial(e, K0, c.first & 1, wv);
     arrive_publish(c.first, K0, c.first & 1);
   }
@@ -523,19 +706,18 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   uint64_t t_prev = __builtin_amdgcn_s_memtime();
 #endif
 
+  // The two roles run decoupled, synchronised through LDS only: the row waves evaluate pod + 1
+  // once the control wave has committed every pod up to pod - 1 (s_dec), the control wave's
+  // owner correction waits for the row waves' pod + 1 statistics (s_done).
+  if (wv == 0) {
   for (int64_t pod = c.first; pod < c.end; ++pod) {
     const bool has_next = pod + 1 < c.end;
     const int pb = (int)(pod & 1);        // LDS buffers of pod
     const int nb = (int)((pod + 1) & 1);  // LDS buffers of pod + 1
-    int32_t jsel = -1;                    // control wave: row committed by this workgroup
-    bool have_pre = false;                // ... and its pod + 1 evaluation, when computed early
-    int32_t ej_pre = -1;
-    uint32_t rm_pre = 0;
 #ifdef KSIM_STAMPS
     uint64_t o_prev = 0;
 #endif
 
-    if (wv == 0) {
       const ksim_pod& P = s_pod[pod % RING];
       const int K = pod_K(P);
       const int k2 = P.reserved[1];
@@ -551,7 +733,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       const uint64_t tag = ptag(pod);
       const int slot = (int)(pod % NSLOT);
       STAMP(1);
-      uint64_t g[MAXB];
+      uint64_t g[MB];
       bool ok = false;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef KSIM_STAMPS
@@ -561,28 +743,28 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         // unconditional loads (slots are sized for MAXG workgroups): one fabric round trip for
         // class 0, the owner's correction and (KF at a time) the further reduce classes
 #pragma unroll
-        for (int j = 0; j < MAXB; ++j) g[j] = load_granule(spec_at(granules, slot, lane * MAXB + j, 0));
+        for (int j = 0; j < MB; ++j) g[j] = load_granule(spec_at<MB>(granules, slot, lane * MB + j, 0));
         const uint64_t fx = load_granule(fix_at(granules, slot, 0));
         bool mine = X < 0 || gtag(fx) == tag;
 #pragma unroll
-        for (int j = 0; j < MAXB; ++j) {
-          const int b = lane * MAXB + j;
+        for (int j = 0; j < MB; ++j) {
+          const int b = lane * MB + j;
           mine &= (b >= G) || b == X || gtag(g[j]) == tag;
         }
         for (int q0 = 1; q0 < K; q0 += KF) {  // classes >= 1 were published with class 0
-          uint64_t v[KF][MAXB];
+          uint64_t v[KF][MB];
 #pragma unroll
           for (int u = 0; u < KF; ++u)
 #pragma unroll
-            for (int j = 0; j < MAXB; ++j) {
-              const int b = lane * MAXB + j;
-              v[u][j] = (q0 + u < K && b < G) ? load_granule(gran_at(granules, slot, b, q0 + u, X)) : 0;
+            for (int j = 0; j < MB; ++j) {
+              const int b = lane * MB + j;
+              v[u][j] = (q0 + u < K && b < G) ? load_granule(gran_at<MB>(granules, slot, b, q0 + u, X)) : 0;
             }
 #pragma unroll
           for (int u = 0; u < KF; ++u)
 #pragma unroll
-            for (int j = 0; j < MAXB; ++j) {
-              const int b = lane * MAXB + j;
+            for (int j = 0; j < MB; ++j) {
+              const int b = lane * MB + j;
               if (q0 + u < K && b < G) {
                 mine &= gtag(v[u][j]) == tag;
                 s_gq[q0 + u - 1][b] = v[u][j];
@@ -594,7 +776,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         {
           bool sp = true;
 #pragma unroll
-          for (int j = 0; j < MAXB; ++j) sp &= (lane * MAXB + j >= G) || lane * MAXB + j == X || gtag(g[j]) == tag;
+          for (int j = 0; j < MB; ++j) sp &= (lane * MB + j >= G) || lane * MB + j == X || gtag(g[j]) == tag;
           const uint64_t tn = __builtin_amdgcn_s_memtime();
           if (!seen_spec && __all(sp)) { seen_spec = true; st_acc[12] += tn - t_prev; }
           if (!seen_fix && (X < 0 || gtag(fx) == tag)) { seen_fix = true; st_acc[13] += tn - t_prev; }
@@ -603,7 +785,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         if (__all(mine)) {
           ok = true;
 #pragma unroll
-          for (int j = 0; j < MAXB; ++j) g[j] = (lane * MAXB + j == X) ? fx : g[j];
+          for (int j = 0; j < MB; ++j) g[j] = (lane * MB + j == X) ? fx : g[j];
           break;
         }
         if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_LIMIT_TICKS) break;
@@ -611,13 +793,13 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       }
       STAMP(2);
 #pragma unroll
-      for (int j = 0; j < MAXB; ++j) g[j] = (lane * MAXB + j < G) ? g[j] : 0;
+      for (int j = 0; j < MB; ++j) g[j] = (lane * MB + j < G) ? g[j] : 0;
       ok = __all(ok);
       int32_t F = 0, M0 = -1, C0 = 0;
       if (ok) {
         int32_t f = 0, m = -1, n = 0;
 #pragma unroll
-        for (int j = 0; j < MAXB; ++j) {
+        for (int j = 0; j < MB; ++j) {
           f += gfit(g[j]);
           const int32_t cnt = gcnt(g[j]), s = gscore(g[j]);
           if (cnt == 0) continue;
@@ -634,8 +816,8 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         for (int q = 1; q < K; ++q) {
           int32_t mm = -1, nn = 0;
 #pragma unroll
-          for (int j = 0; j < MAXB; ++j) {
-            const int b = lane * MAXB + j;
+          for (int j = 0; j < MB; ++j) {
+            const int b = lane * MB + j;
             if (b >= G) continue;
             const uint64_t v = s_gq[q - 1][b];
             const int32_t cnt = gcnt(v), s = gscore(v);
@@ -651,6 +833,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       STAMP(11);
       int mode = 0, blk = -1, rank = 0;
       uint32_t win = 1;
+      int32_t tgt = -2;  // lane q: the packed entry a winning row of class q has (select), -2 none
       if (!ok) {
         mode = -1;
         if (lane == 0) atomicOr(c.err, 4);
@@ -670,20 +853,23 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
             const int64_t mxT = wave_max_i64(live ? tv_l : 0), mxA = wave_max_i64(live ? av_l : 0);
             const int64_t t = live ? class_total(c, tv_l, av_l, mq, mxT, mxA) : -1;  // totals are >= 0
             const int64_t best = wave_max_i64(t);
-            const uint64_t wb = __ballot(live && t == best);
-            win = (uint32_t)wb;
-            C = ksimw::sum_i32((wb >> lane) & 1ull ? cq : 0);
+            const uint64_t wbm = __ballot(live && t == best);
+            win = (uint32_t)wbm;
+            C = ksimw::sum_i32((wbm >> lane) & 1ull ? cq : 0);
+            tgt = ((wbm >> lane) & 1ull) ? ((lane << EV_SHIFT) | (int32_t)mq) : -2;
+          } else {
+            tgt = lane == 0 ? M0 : -2;
           }
           ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)C) : (int64_t)((uint32_t)counter % (uint32_t)C);
           counter += 1;  // generic_scheduler.go:192-195
         }
         STAMP(10);
         // ---- locate the workgroup holding the ix-th match counted from the top ----
-        int32_t bm[MAXB];
+        int32_t bm[MB];
         int32_t tot = 0;
 #pragma unroll
-        for (int j = 0; j < MAXB; ++j) {
-          const int b = lane * MAXB + j;
+        for (int j = 0; j < MB; ++j) {
+          const int b = lane * MB + j;
           int32_t m = 0;
           if (b < G) {
             if (mode == 1) {
@@ -708,9 +894,9 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         if (hit) {
           int64_t rr = ix - above;
 #pragma unroll
-          for (int j = MAXB - 1; j >= 0; --j) {
+          for (int j = MB - 1; j >= 0; --j) {
             if (found < 0) {
-              if (rr < bm[j]) found = lane * MAXB + j;
+              if (rr < bm[j]) found = lane * MB + j;
               else rr -= bm[j];
             }
           }
@@ -732,32 +918,10 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       o_prev = __builtin_amdgcn_s_memtime();
 #endif
       if (mode > 0 && blk == (int)blockIdx.x) {
-        // ---------------- d. owner: exact row (rank from the top), commit ----------------
-        if (K == 1) {
-          // lane t = t-th 64-row segment from the top (k descending, then wave descending)
-          constexpr int S = NPT * (NW - 1);
-          uint64_t m = 0;
-          if (lane < S) {
-            const int k = NPT - 1 - lane / (NW - 1), w = NW - 1 - lane % (NW - 1);
-            m = (mode == 1) ? s_fm[pb][k][w] : (s_mx[pb][w][0] == M0 ? s_bm[pb][k][w] : 0ull);
-          }
-          const int32_t cnt = __popcll(m);
-          const int32_t pre = ksimw::prefix_incl_i32(cnt);
-          const uint64_t hm = __ballot(pre > rank);
-          if (hm) {
-            const int ts = __builtin_ffsll((long long)hm) - 1;
-            const int32_t r2 = rank - (__builtin_amdgcn_readlane(pre, ts) - __builtin_amdgcn_readlane(cnt, ts));
-            const uint64_t ms = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(m >> 32), ts) << 32) |
-                                (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)m, ts);
-            // the r2-th set bit counted from the top: set, with exactly r2 set bits above it
-            const bool is = ((ms >> lane) & 1ull) && __popcll((ms >> lane) >> 1) == r2;
-            const uint64_t bb = __ballot(is);
-            if (bb) {
-              const int ks = NPT - 1 - ts / (NW - 1), ws = NW - 1 - ts % (NW - 1);
-              jsel = ks * RT + (ws - 1) * 64 + (__builtin_ffsll((long long)bb) - 1);
-            }
-          }
-        } else {  // several reduce classes: scan the packed entries from the top
+        // ---------------- d. owner: exact row (rank from the top), commit, correction ----------
+        // scan pod's entries from the top: 64-row segments, four per LDS round trip
+        int32_t jsel = -1;
+        {
           const int32_t* ev = R.ev + pb * chunk;
           int32_t rr = rank;
           const int nseg = (nrows + 63) / 64;
@@ -768,9 +932,10 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
               const int32_t j = (s0 - u) * 64 + lane;
               const int32_t e = (s0 - u >= 0 && j < nrows) ? ev[j] : -1;
               bool mt = e >= 0;
-              if (mode == 2 && mt) {
-                const int q = ev_cls(e);
-                mt = ((win >> q) & 1u) && ev_score(e) == (q == 0 ? M0 : s_M[q]);
+              if (mode == 2) {  // one compare per winning class (usually one)
+                mt = false;
+                for (uint32_t wq = win; wq; wq &= wq - 1)
+                  mt |= e == __builtin_amdgcn_readlane(tgt, __builtin_ctz(wq));
               }
               bl[u] = __ballot(mt);
             }
@@ -780,8 +945,10 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
               uint64_t m = bl[u];
               const int nbits = __popcll(m);
               if (rr >= nbits) { rr -= nbits; continue; }
-              for (int t = 0; t < rr; ++t) m &= ~(1ull << (63 - __clzll(m)));
-              jsel = (s0 - u) * 64 + (63 - __clzll(m));
+              // the rr-th set bit from the top: set, with exactly rr set bits above it
+              const bool is = ((m >> lane) & 1ull) && __popcll((m >> lane) >> 1) == rr;
+              const uint64_t bb = __ballot(is);
+              jsel = (s0 - u) * 64 + (__builtin_ffsll((long long)bb) - 1);
             }
           }
         }
@@ -790,60 +957,157 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
           mode = -1;
           if (lane == 0) atomicOr(c.err, 2);
         } else {
-          // commit (NodeInfo.AddPod); the committed row stays in registers for the fix-up
-          KsimFastRow r = load_row(jsel);
-          r.rc += P.add_cpu; r.rm += P.add_mem; r.zc += P.nz_cpu; r.zm += P.nz_mem; r.count += 1;
+          // commit the LDS row (NodeInfo.AddPod); the HBM side columns come after the correction
           const bool side = (P.add_gpu | P.add_eph | P.scalar_cnt | P.port_cnt) != 0;
           if (lane == 0) {
-            R.rc[jsel] = r.rc; R.rm[jsel] = r.rm; R.zc[jsel] = r.zc; R.zm[jsel] = r.zm; R.count[jsel] = r.count;
-            if (side) {
+            R.rc[jsel] += P.add_cpu; R.rm[jsel] += P.add_mem; R.zc[jsel] += P.nz_cpu; R.zm[jsel] += P.nz_mem;
+            R.count[jsel] += 1;
+          }
+          bool side_done = false;
+          OSTAMP(23);
+          if (has_next) {
+            // the row waves' pod + 1 stats (and ev2) must be complete
+            const int32_t want = (int32_t)ptag(pod + 1);
+            while (__hip_atomic_load(&s_done[nb], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != want)
+              __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            const ksim_pod& Q = s_pod[(pod + 1) % RING];
+            const int Kn = pod_K(Q);
+            const int32_t e1 = R.ev[nb * chunk + jsel];
+            int32_t e2;
+            uint32_t rm2;
+            if (s_ev2[nb]) {  // the dual hypothesis already evaluated pod + 1 on the committed row
+              e2 = R.ev2[nb * chunk + jsel];
+              rm2 = R.rm2[nb * chunk + jsel];
+            } else {          // commit everything, then evaluate the one row here
+              if (side) {
+                if (lane == 0) {
+                  const bool lds_ports = P.port_cnt && L.ps;
+                  uint32_t fl = R.fl[jsel];
+                  if (P.add_gpu | P.add_eph | P.scalar_cnt | (P.port_cnt && !L.ps)) {
+                    fl = commit_side(cg, &P, lo + jsel, fl, lds_ports ? 0 : 1);
+                    R.fl[jsel] = fl;
+                  }
+                  if (lds_ports) commit_ports_lds(cg, &P, lo + jsel, jsel, (int32_t)chunk, L.off_pc, L.off_pk);
+                }
+                side_done = true;
+              }
+              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+              __builtin_amdgcn_wave_barrier();
+              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+              const RowDelta z{0, 0, 0, 0, 0, 0, 0, 0};
+              e2 = eval_row(pod_view(Q), pod + 1, jsel, z, rm2);
+            }
+            OSTAMP(16);
+            // O(1) correction of this workgroup's pod + 1 partial: e1 leaves its class, e2 joins
+            // (the reduce class is the row's, the same for both when both fit)
+            const int q = lane < Kn ? lane : 0;
+            const int4 t = s_top[nb][q];
+            int32_t f = s_F[nb] - (e1 >= 0) + (e2 >= 0);
+            int32_t m = t.x, n = t.y;
+            const int q1 = e1 < 0 ? -1 : (Kn == 1 ? 0 : ev_cls(e1));
+            const int32_t s1 = Kn == 1 ? e1 : ev_score(e1);
+            if (q1 == q && s1 == m) {
+              if (n > 1) n -= 1;
+              else { m = t.z; n = t.w; }
+            }
+            const int q2 = e2 < 0 ? -1 : (Kn == 1 ? 0 : ev_cls(e2));
+            const int32_t s2 = Kn == 1 ? e2 : ev_score(e2);
+            if (q2 == q) {
+              if (n == 0 || s2 > m) { m = s2; n = 1; }
+              else if (s2 == m) n += 1;
+            }
+            if (n == 0) m = -1;
+            const uint64_t v = (lane == 0 ? ((uint64_t)f << 44) : 0) | ((uint64_t)n << 32) | (uint64_t)(uint32_t)m;
+            if (lane < Kn) store_granule(fix_at(granules, (int)((pod + 1) % NSLOT), lane), (ptag(pod + 1) << 56) | v);
+            if (lane == 0) {
+              R.ev[nb * chunk + jsel] = e2;
+              R.rm1[nb * chunk + jsel] = rm2;
+            }
+            OSTAMP(19);
+#ifdef KSIM_STAMPS
+            if (lane == 0) atomicAdd((unsigned long long*)&c.dbg[21], 1ull);
+#endif
+          }
+          if (lane == 0) {
+            if (side && !side_done) {
               const bool lds_ports = P.port_cnt && L.ps;
+              uint32_t fl = R.fl[jsel];
               if (P.add_gpu | P.add_eph | P.scalar_cnt | (P.port_cnt && !L.ps)) {
-                r.fl = commit_side(cg, &P, lo + jsel, r.fl, lds_ports ? 0 : 1);
-                R.fl[jsel] = r.fl;
+                fl = commit_side(cg, &P, lo + jsel, fl, lds_ports ? 0 : 1);
+                R.fl[jsel] = fl;
               }
               if (lds_ports) commit_ports_lds(cg, &P, lo + jsel, jsel, (int32_t)chunk, L.off_pc, L.off_pk);
             }
             c.out_node[pod] = (int32_t)(lo + jsel);
           }
-          OSTAMP(23);
-          if (has_next) {  // pod + 1 against the committed row, before the barrier
-            const ksim_pod& Q = s_pod[(pod + 1) % RING];
-            const int Kq = pod_K(Q);
-            if (ksim_is_fast_pod(Q, Kq) && !side) {
-              const KsimFastPod F{Q.req_cpu, Q.req_mem, Q.nz_cpu, Q.nz_mem, Q.flags};
-              ej_pre = ksim_fast_eval(preds, F, r, no_prio, wl, wmr, wb, rm_pre);
-              have_pre = true;
-            } else if (!ksim_is_fast_pod(Q, Kq)) {
-              // general pod: everything it reads is in LDS; lane 0's commit stores first
-              __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-              __builtin_amdgcn_wave_barrier();
-              __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-              ej_pre = eval_one(Q, false, jsel, rm_pre);
-              have_pre = true;
-            }
-          }
+          OSTAMP(20);
         }
-        OSTAMP(16);
       }
       if (mode == 0 && blockIdx.x == 0 && lane == 0) c.out_node[pod] = -1;
-      if (lane == 0) s_mode = mode;
       X = mode > 0 ? blk : -1;
       STAMP(6);
-    } else {
+      if (mode < 0) {  // uniform: every workgroup reaches the same verdict
+        if (lane == 0) __hip_atomic_store(&s_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        break;
+      }
+      if (mode == 0 && c.collect && c.out_reasons) {  // FitError: every workgroup adds its rows' reasons
+        int32_t acc = 0;
+        for (int32_t j0 = 0; j0 < nrows; j0 += 64) {
+          const int32_t j = j0 + lane;
+          const uint32_t rm = j < nrows ? R.rm1[pb * chunk + j] : 0u;
+#pragma unroll
+          for (int r = 0; r < KSIM_NREASONS; ++r) {
+            const int32_t n = __popcll(__ballot((rm >> r) & 1u));
+            acc += lane == r ? n : 0;
+          }
+        }
+        if (lane < KSIM_NREASONS && acc) atomicAdd(&c.out_reasons[pod * KSIM_NREASONS + lane], acc);
+      }
+      // pods through `pod` are decided and committed: the row waves may evaluate pod + 2
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      if (lane == 0) __hip_atomic_store(&s_dec, (int32_t)(pod - c.first + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      STAMP(4);
+    }
+  } else {
+  for (int64_t pod = c.first; pod < c.end; ++pod) {
+    const bool has_next = pod + 1 < c.end;
+    const int pb = (int)(pod & 1);        // LDS buffers of pod
+    const int nb = (int)((pod + 1) & 1);  // LDS buffers of pod + 1
+#ifdef KSIM_STAMPS
+    uint64_t o_prev = 0;
+#endif
+
       // ---------------- b. speculative evaluation of pod + 1 (row waves) ----------------
       // wave 1 refills the descriptor ring every RING_FILL pods; the load's latency hides
-      // under the evaluation, the LDS store lands before the next barrier
+      // under the evaluation (the control wave is at most one pod behind the row waves)
       const bool refill = wv == 1 && ((pod - c.first) % RING_FILL) == 0;
-      uint4 rv;
-      if (refill) ring_load(pod + RING_FILL, rv);
+      uint4 rv = make_uint4(0, 0, 0, 0);
+      uint64_t rkey = 0;
+      if (refill) ring_load(pod + RING_FILL, rv, rkey);
 #ifdef KSIM_STAMPS
       const uint64_t te0 = __builtin_amdgcn_s_memtime();
 #endif
       if (has_next) {
+        // pod + 1 is evaluated on the rows as committed through pod - 1 (the hypothesis covers pod)
+        const int32_t need = (int32_t)(pod - c.first);
+#ifdef KSIM_STAMPS
+        const uint64_t tw0 = __builtin_amdgcn_s_memtime();
+#endif
+        while (__hip_atomic_load(&s_dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < need &&
+               !__hip_atomic_load(&s_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+          __builtin_amdgcn_s_sleep(1);
+#ifdef KSIM_STAMPS
+        if (tid == 64) wait_acc += __builtin_amdgcn_s_memtime() - tw0;
+#endif
+        if (__hip_atomic_load(&s_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
         int32_t e[NPT];
         const int Kn = pod_K(s_pod[(pod + 1) % RING]);
-        eval_rows(pod + 1, e, B_rm, R.ev + nb * chunk);
+        RowDelta d{0, 0, 0, 0, 0, 0, 0, 0};
+        const bool hyp = delta_of(pod, pod + 1, d);
+        if (tid == 64) s_ev2[nb] = hyp ? 1 : 0;
+        eval_rows(pod + 1, hyp, d, e, nb);
 #ifdef KSIM_STAMPS
         const uint64_t te1 = __builtin_amdgcn_s_memtime();
         if (tid == 64) st_acc[14] += te1 - te0;
@@ -858,67 +1122,9 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
 #ifdef KSIM_STAMPS
       if (tid == 64) st_acc[5] += __builtin_amdgcn_s_memtime() - te0;
 #endif
-      if (refill) ring_store(pod + RING_FILL, rv);
-    }
-    __syncthreads();
-    STAMP(7);
-    const int mode = s_mode;
-    if (mode < 0) break;  // uniform: every workgroup reaches the same verdict
-
-    if (mode == 0 && c.collect && c.out_reasons) {  // FitError: every workgroup adds its reasons
-      if (tid < KSIM_NREASONS) s_hist[tid] = 0;
-      __syncthreads();
-      if (wv > 0) {
-        const int32_t fr = s_fix[pb][0];
-        const uint32_t fm = (uint32_t)s_fix[pb][1];
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-          const uint32_t rm = (k * RT + rt == fr) ? fm : A_rm[k];
-          for (int r = 0; r < KSIM_NREASONS; ++r) {
-            const int32_t n = __popcll(__ballot((rm >> r) & 1u));
-            if (lane == 0 && n) atomicAdd(&s_hist[r], n);
-          }
-        }
-      }
-      __syncthreads();
-      if (tid < KSIM_NREASONS && s_hist[tid]) atomicAdd(&c.out_reasons[pod * KSIM_NREASONS + tid], s_hist[tid]);
-    }
-    if (wv == 0 && has_next) {
-      // ---------------- e. owner: fix-up of pod + 1, publish the correction ----------------
-      if (jsel >= 0) {  // only row jsel changed: re-evaluate it and redo its row wave's partial
-        OSTAMP(17);
-        const ksim_pod& Q = s_pod[(pod + 1) % RING];
-        const int Kn = pod_K(Q);
-        uint32_t rmj = rm_pre;
-        const int32_t ej = have_pre ? ej_pre : eval_one(Q, ksim_is_fast_pod(Q, Kn), jsel, rmj);
-        OSTAMP(18);
-        const int w = 1 + (jsel % RT) / 64;
-        int32_t e[NPT];
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-          const int32_t j = k * RT + (w - 1) * 64 + lane;
-          e[k] = (j == jsel) ? ej : (j < nrows ? R.ev[nb * chunk + j] : -1);
-        }
-        partial(e, Kn, nb, w);
-        if (lane == 0) { R.ev[nb * chunk + jsel] = ej; s_fix[nb][0] = jsel; s_fix[nb][1] = (int32_t)rmj; }
-        OSTAMP(19);
-        const uint64_t v = combine(Kn, nb);
-        if (lane < Kn) store_granule(fix_at(granules, (int)((pod + 1) % NSLOT), lane), (ptag(pod + 1) << 56) | v);
-        OSTAMP(20);
-#ifdef KSIM_STAMPS
-        if (lane == 0) atomicAdd((unsigned long long*)&c.dbg[21], 1ull);
-#endif
-      } else if (lane == 0) {
-        s_fix[nb][0] = -1;
-      }
-    }
-    STAMP(4);
-    if (wv > 0) {
-#pragma unroll
-      for (int k = 0; k < NPT; ++k) A_rm[k] = B_rm[k];
+      if (refill) ring_store(pod + RING_FILL, rv, rkey);
     }
   }
-
   // the table is authoritative in HBM between calls: write the owned rows back
   __syncthreads();
   for (int32_t j = tid; j < nrows; j += BS) {
@@ -934,7 +1140,11 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
 #ifdef KSIM_STAMPS
   if (blockIdx.x == 0 && tid == 0)
     for (int k = 0; k < 16; ++k) c.dbg[k] += (k == 5) ? 0 : st_acc[k];
-  if (blockIdx.x == 0 && tid == 64) { c.dbg[5] += st_acc[5]; c.dbg[24] += st_acc[14]; c.dbg[25] += st_acc[15]; }
+  if (blockIdx.x == 0 && tid == 64) {
+    c.dbg[5] += st_acc[5]; c.dbg[24] += st_acc[14]; c.dbg[25] += st_acc[15];
+    for (int k = 0; k < 4; ++k) c.dbg[26 + k] += ev_acc[k];
+    c.dbg[30] += wait_acc;
+  }
 #endif
 }
 
@@ -964,6 +1174,9 @@ extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows) {
   if (g <= 0 || n <= 0) return 0;
   if (g > 64 * MAXB) g = 64 * MAXB;
   if (n < (int64_t)g * 64) g = (int)((n + 63) / 64);  // >= 64 rows per workgroup
+  // tables the dual-hypothesis split covers in 64 workgroups (<= 192 rows each) take 64: one
+  // workgroup per sweep lane (fewer granules per lane on the decision's critical path)
+  if (g > 64 && n <= 64 * 192) g = 64;
   if (g < 1) g = 1;
   const int64_t chunk = (n + g - 1) / g;
   if (chunk * LDS_ROW_BYTES > LDS_BUDGET || chunk > 4095 || chunk > 8 * 448) return 0;  // launch mode
@@ -977,17 +1190,17 @@ extern "C" size_t ksim_persistent_granule_bytes(int) {
 }
 
 // Static LDS of the kernel instance (granule stash, rings, partials), for the dynamic budget.
-template <int BS, int NPT>
+template <int BS, int NPT, int MB>
 static size_t static_lds() {
   hipFuncAttributes fa;
-  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&ksim_persistent_kernel<BS, NPT>)) != hipSuccess) return 48 * 1024;
+  if (hipFuncGetAttributes(&fa, reinterpret_cast<const void*>(&ksim_persistent_kernel<BS, NPT, MB>)) != hipSuccess) return 48 * 1024;
   return fa.sharedSizeBytes;
 }
 
-template <int BS, int NPT>
+template <int BS, int NPT, int MB>
 static hipError_t launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid, int lds_rows,
                                     hipStream_t s) {
-  const size_t lds_max = 160 * 1024 - static_lds<BS, NPT>();
+  const size_t lds_max = 160 * 1024 - static_lds<BS, NPT, MB>();
   auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
   size_t off = al((size_t)lds_rows * LDS_ROW_BYTES);
   if (off > lds_max) return hipErrorInvalidValue;  // ksim_persistent_config keeps rows within budget
@@ -1014,16 +1227,17 @@ static hipError_t launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint6
     L.off_ttv = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
     L.off_nav = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
   }
-  hipLaunchKernelGGL((ksim_persistent_kernel<BS, NPT>), dim3(grid), dim3(BS), off, s, *c, cdev, granules, L);
+  hipLaunchKernelGGL((ksim_persistent_kernel<BS, NPT, MB>), dim3(grid), dim3(BS), off, s, *c, cdev, granules, L);
   return hipGetLastError();
 }
 
 extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
                                              int lds_rows, hipStream_t s) {
-  if (lds_rows <= 448) return launch_persistent<512, 1>(c, cdev, granules, grid, lds_rows, s);
-  if (lds_rows <= 896) return launch_persistent<512, 2>(c, cdev, granules, grid, lds_rows, s);
-  if (lds_rows <= 1792) return launch_persistent<512, 4>(c, cdev, granules, grid, lds_rows, s);
-  return launch_persistent<512, 8>(c, cdev, granules, grid, lds_rows, s);
+  if (grid <= 64 && lds_rows <= 448) return launch_persistent<512, 1, 1>(c, cdev, granules, grid, lds_rows, s);
+  if (lds_rows <= 448) return launch_persistent<512, 1, MAXB>(c, cdev, granules, grid, lds_rows, s);
+  if (lds_rows <= 896) return launch_persistent<512, 2, MAXB>(c, cdev, granules, grid, lds_rows, s);
+  if (lds_rows <= 1792) return launch_persistent<512, 4, MAXB>(c, cdev, granules, grid, lds_rows, s);
+  return launch_persistent<512, 8, MAXB>(c, cdev, granules, grid, lds_rows, s);
 }
 
 extern "C" int ksim_selftest(void) {

@@ -641,6 +641,9 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
     fprintf(stderr, "[ksim stamps] pods=%lld (%.3f ms) cycles/pod:", (long long)count, ms);
     for (int k : {1, 2, 12, 13, 9, 11, 10, 3, 6, 7, 4, 5, 8}) fprintf(stderr, " %s %.0f", names[k], d[k] / (double)count);
     fprintf(stderr, "\n[ksim stamps] row wave 1: eval %.0f partial %.0f", d[24] / (double)count, d[25] / (double)count);
+    fprintf(stderr, " (per call: view %.0f rows %.0f read-back %.0f)", d[26] / (double)(d[29] ? d[29] : 1),
+            d[27] / (double)(d[29] ? d[29] : 1), d[28] / (double)(d[29] ? d[29] : 1));
+    fprintf(stderr, " wait for control %.0f", d[30] / (double)count);
     fprintf(stderr, "\n[ksim stamps] owner select %.0f commit %.0f", d[22] / (double)(d[21] ? d[21] : 1),
             d[23] / (double)(d[21] ? d[21] : 1));
     fprintf(stderr, "\n[ksim stamps] owner (%llu fix-ups) cycles/fix-up: pre-eval %.0f barrier %.0f eval-row %.0f partial %.0f combine+publish %.0f\n",
