@@ -31,6 +31,8 @@
 // -1 = no fit node of that class).  Scores < 2^31 and chunks <= 4095 rows (host checks).
 // Sweep lane l reads workgroups [l*MAXB, l*MAXB+MAXB): name-rank order is lane-major, so the
 // matches above a workgroup are one DPP prefix sum away.
+#include <type_traits>
+
 #include "ksim_fast.h"
 #include "ksim_wave.h"
 
@@ -73,6 +75,16 @@ __device__ __forceinline__ uint32_t gtag(uint64_t v) { return (uint32_t)(v >> 56
 __device__ __forceinline__ int32_t gfit(uint64_t v) { return (int32_t)((v >> 44) & 0xFFF); }
 __device__ __forceinline__ int32_t gcnt(uint64_t v) { return (int32_t)((v >> 32) & 0xFFF); }
 __device__ __forceinline__ int32_t gscore(uint64_t v) { return (int32_t)(uint32_t)v; }
+
+// critical-path probe (diagnostic builds, -DKSIM_PROBE=k): a 512-cycle delay at point k; the
+// per-pod time grows by the delay only where k sits on the critical path
+#ifdef KSIM_PROBE
+#define PROBE(k) do { if (KSIM_PROBE == (k)) __builtin_amdgcn_s_sleep(8); } while (0)
+#define PROBE_IF(k, cond) do { if (KSIM_PROBE == (k) && (cond)) __builtin_amdgcn_s_sleep(8); } while (0)
+#else
+#define PROBE(k) do { } while (0)
+#define PROBE_IF(k, cond) do { } while (0)
+#endif
 
 #ifdef KSIM_STAMPS
 // phase cycle sums kept in registers of block 0's control wave, written once at the end
@@ -260,6 +272,21 @@ struct PodView {
   bool fast;  // resource-only (ksim_is_fast_pod)
 };
 
+// Pin a wave-uniform value into VGPRs: the kernel's scalar file is full (both roles share one
+// allocation), so uniform per-pod inputs held in SGPRs get spilled to VGPR lanes and reloaded
+// with a v_readlane at every use inside the row evaluation; an asm operand the compiler must
+// treat as divergent keeps them in vector registers instead.
+template <class T>
+__device__ __forceinline__ void to_vgpr(T& x) {
+  asm volatile("" : "+v"(x));
+}
+
+__device__ __forceinline__ void to_vgpr(bool& x) {
+  int32_t t = x;
+  asm volatile("" : "+v"(t));
+  x = t != 0;
+}
+
 // The descriptor in LDS → PodView with eight 16-byte reads issued together.
 __device__ __forceinline__ PodView pod_view_lds(const ksim_pod* Pl);
 
@@ -299,10 +326,13 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   __shared__ int32_t s_F[2];                  // ... its fit rows
   __shared__ int32_t s_done[2];               // tag of the pod whose workgroup stats are complete
   __shared__ int32_t s_ev2[2];                // 1: ev2 was evaluated for that pod
-  __shared__ int32_t s_hist[KSIM_NREASONS];
-  __shared__ int32_t s_M[KSIM_MAX_RCLASS];
-  __shared__ uint64_t s_gq[KSIM_MAX_RCLASS - 1][MAXG];  // control wave: granules of classes >= 1 (by b)
-  __shared__ int32_t s_C[KSIM_MAX_RCLASS];
+  // one row per row thread (NPT == 1): per row wave and class, the rows at the wave's top value
+  // (bit l = row (w-1)*64 + l), so the owner's selectHost pick needs no scan of the entries;
+  // s_mok: the masks are exact for that pod (an owner correction that empties a wave's top
+  // clears it, and the owner then scans)
+  __shared__ uint64_t s_msk[2][NW][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_mok[2];
+  __shared__ uint64_t s_gq[KSIM_MAX_RCLASS - 1 - KF][MAXG];  // control wave: granules of classes > KF (by b)
   __shared__ int32_t s_dec;    // pods decided and committed (control wave → row waves)
   __shared__ int32_t s_abort;  // the control wave stopped on an error
   __shared__ int32_t s_arr[2];  // row-wave arrivals per pod parity (the last one of a pod publishes)
@@ -388,6 +418,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     s_dec = 0;
     s_abort = 0;
     s_ev2[0] = s_ev2[1] = 0;
+    s_mok[0] = s_mok[1] = 1;
   }
   uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex (control wave)
   __syncthreads();
@@ -399,6 +430,10 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   // (bit-identical), the reduce class from the staged class tables.  d: the previous pod
   // committed to the row (dual hypothesis), or zero.
   auto eval_row = [&](const PodView& V, int64_t p, int32_t j, const RowDelta& d, uint32_t& rm) -> int32_t {
+    // rare-path columns and tables through a laundered context pointer: loaded (scalar cache)
+    // where a branch needs them instead of held in scalar registers across the pod loop
+    const KsimCtx* cx = cg;
+    asm volatile("" : "+s"(cx));
     KsimFastRow r;
     r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j] + d.c; r.rm = R.rm[j] + d.m; r.zc = R.zc[j] + d.zc;
     r.zm = R.zm[j] + d.zm; r.dac = R.dac[j]; r.dam = R.dam[j];
@@ -406,8 +441,8 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     if (d.g | d.e) {  // the previous pod's gpu / ephemeral request re-derives the over-commit bits
       const int64_t i = lo + j;
       r.fl &= ~(KSIM_N_GPU_OVER | KSIM_N_EPH_OVER);
-      if (c.alloc_gpu[i] < c.req_gpu[i] + d.g) r.fl |= KSIM_N_GPU_OVER;
-      if (c.alloc_eph[i] < c.req_eph[i] + d.e) r.fl |= KSIM_N_EPH_OVER;
+      if (cx->alloc_gpu[i] < cx->req_gpu[i] + d.g) r.fl |= KSIM_N_GPU_OVER;
+      if (cx->alloc_eph[i] < cx->req_eph[i] + d.e) r.fl |= KSIM_N_EPH_OVER;
     }
     if (V.fast) {
       const KsimFastPod F{V.rq_c, V.rq_m, V.nz_c, V.nz_m, V.flags};
@@ -422,13 +457,13 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       res |= (r.ac < V.rq_c + r.rc) ? (1u << KSIM_R_INSUFFICIENT_CPU) : 0u;
       res |= (r.am < V.rq_m + r.rm) ? (1u << KSIM_R_INSUFFICIENT_MEMORY) : 0u;
       if (V.rq_g == 0) res |= (fl & KSIM_N_GPU_OVER) ? (1u << KSIM_R_INSUFFICIENT_GPU) : 0u;
-      else if (c.alloc_gpu[i] < V.rq_g + c.req_gpu[i] + d.g) res |= 1u << KSIM_R_INSUFFICIENT_GPU;
+      else if (cx->alloc_gpu[i] < V.rq_g + cx->req_gpu[i] + d.g) res |= 1u << KSIM_R_INSUFFICIENT_GPU;
       if (V.rq_e == 0) res |= (fl & KSIM_N_EPH_OVER) ? (1u << KSIM_R_INSUFFICIENT_EPHEMERAL) : 0u;
-      else if (c.alloc_eph[i] < V.rq_e + c.req_eph[i] + d.e) res |= 1u << KSIM_R_INSUFFICIENT_EPHEMERAL;
+      else if (cx->alloc_eph[i] < V.rq_e + cx->req_eph[i] + d.e) res |= 1u << KSIM_R_INSUFFICIENT_EPHEMERAL;
       for (int32_t s = 0; s < V.scalar_cnt; ++s) {
-        const ksim_scalar_req q = c.pod_scalars[V.scalar_off + s];
-        const int64_t off = (int64_t)q.col * c.n + i;
-        if (c.alloc_scalar[off] < q.req + c.req_scalar[off]) res |= 1u << (KSIM_R_INSUFFICIENT_SCALAR0 + q.col);
+        const ksim_scalar_req q = cx->pod_scalars[V.scalar_off + s];
+        const int64_t off = (int64_t)q.col * cx->n + i;
+        if (cx->alloc_scalar[off] < q.req + cx->req_scalar[off]) res |= 1u << (KSIM_R_INSUFFICIENT_SCALAR0 + q.col);
       }
     }
     const uint32_t host = (V.host == -1 || V.host == i) ? 0u : (1u << KSIM_R_HOSTNAME);
@@ -436,15 +471,20 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     uint32_t ports = 0;
     if (V.port_cnt) {
       const bool lk = V.port_cnt <= PPK;
-      const int32_t pc = L.ps ? reinterpret_cast<const int32_t*>(ksim_smem + L.off_pc)[j] : c.port_count[i];
+      int32_t pc;
+      if (L.ps) pc = reinterpret_cast<const int32_t*>(ksim_smem + L.off_pc)[j];
+      else pc = cx->port_count[i];
       for (int32_t k = 0; k < V.port_cnt && !ports; ++k) {
-        const uint64_t want = lk ? s_ppk[p % RING][k] : c.pod_ports[V.port_off + k];
+        uint64_t want;
+        if (lk) want = s_ppk[p % RING][k];
+        else want = cx->pod_ports[V.port_off + k];
         const uint32_t wip = (uint32_t)(want >> 40);
         const uint64_t wpp = want & 0xFFFFFFFFFFull;
         bool hit = d.pp != 0;
         for (int32_t sl = 0; sl < pc && !hit; ++sl) {
-          const uint64_t e = L.ps ? reinterpret_cast<const uint64_t*>(ksim_smem + L.off_pk)[sl * chunk + j]
-                                  : c.ports[(int64_t)sl * c.n + i];
+          uint64_t e;
+          if (L.ps) e = reinterpret_cast<const uint64_t*>(ksim_smem + L.off_pk)[sl * chunk + j];
+          else e = cx->ports[(int64_t)sl * cx->n + i];
           if ((e & 0xFFFFFFFFFFull) != wpp) continue;
           const uint32_t eip = (uint32_t)(e >> 40);
           hit = wip == 0 || eip == 0 || eip == wip;
@@ -455,34 +495,47 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     // podMatchesNodeLabels / tolerations: bits of the staged class tables
     uint32_t sel = 0, taint = 0, noexec = 0;
     if (V.flags & KSIM_POD_NEED_SELECTOR) {
-      const int64_t w = (int64_t)V.cls * c.lwords + (ls >> 5);
-      const uint32_t word = L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_sel)[w] : c.sel_ok[w];
+      const int64_t w = (int64_t)V.cls * cx->lwords + (ls >> 5);
+      uint32_t word;
+      if (L.tables) word = reinterpret_cast<const uint32_t*>(ksim_smem + L.off_sel)[w];
+      else word = cx->sel_ok[w];
       sel = ((word >> (ls & 31)) & 1u) ? 0u : (1u << KSIM_R_NODE_SELECTOR);
     }
     if (V.flags & KSIM_POD_NEED_TAINTS) {
-      const int64_t w = (int64_t)V.cls * c.twords + (ts >> 5);
-      const uint32_t wt = L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_tok)[w] : c.taint_ok[w];
-      const uint32_t wn = L.tables ? reinterpret_cast<const uint32_t*>(ksim_smem + L.off_nok)[w] : c.noexec_ok[w];
+      const int64_t w = (int64_t)V.cls * cx->twords + (ts >> 5);
+      uint32_t wt, wn;
+      if (L.tables) {
+        wt = reinterpret_cast<const uint32_t*>(ksim_smem + L.off_tok)[w];
+        wn = reinterpret_cast<const uint32_t*>(ksim_smem + L.off_nok)[w];
+      } else {
+        wt = cx->taint_ok[w];
+        wn = cx->noexec_ok[w];
+      }
       taint = ((wt >> (ts & 31)) & 1u) ? 0u : (1u << KSIM_R_TAINTS);
       noexec = ((wn >> (ts & 31)) & 1u) ? 0u : (1u << KSIM_R_TAINTS);
     }
     // the first failing predicate in order (ksim_predicates_a)
+    // Predicate enables as 32-bit integer masks (uniform, one scalar register each), node
+    // conditions as per-lane bit moves: boolean selects on uniform conditions become 64-bit lane
+    // masks the compiler hoists out of the pod loop and then spills
     const uint32_t pr = preds;
-    const uint32_t m_cond = (pr & KSIM_P_CHECK_NODE_CONDITION) ? (fl & KSIM_COND_REASON_MASK) : 0u;
-    const uint32_t m_uns = ((pr & KSIM_P_CHECK_NODE_UNSCHEDULABLE) && (fl & KSIM_N_UNSCHEDULABLE)) ? (1u << KSIM_R_UNSCHEDULABLE) : 0u;
-    const uint32_t m_gen = (pr & KSIM_P_GENERAL) ? (res | host | ports | sel) : 0u;
-    const uint32_t m_host = (pr & KSIM_P_HOSTNAME) ? host : 0u;
-    const uint32_t m_ports = (pr & KSIM_P_HOST_PORTS) ? ports : 0u;
-    const uint32_t m_sel = (pr & KSIM_P_NODE_SELECTOR) ? sel : 0u;
-    const uint32_t m_res = (pr & KSIM_P_RESOURCES) ? res : 0u;
-    const uint32_t m_t = (pr & KSIM_P_TAINTS) ? taint : 0u;
-    const uint32_t m_nt = (pr & KSIM_P_NOEXEC_TAINTS) ? noexec : 0u;
-    const uint32_t m_lp = ((pr & KSIM_P_LABEL_PRESENCE) && (fl & KSIM_N_LABEL_PRESENCE)) ? (1u << KSIM_R_LABEL_PRESENCE) : 0u;
-    const uint32_t m_mp = ((pr & KSIM_P_MEM_PRESSURE) && (V.flags & KSIM_POD_BEST_EFFORT) && (fl & KSIM_N_MEM_PRESSURE))
-                              ? (1u << KSIM_R_MEM_PRESSURE) : 0u;
-    const uint32_t m_dp = ((pr & KSIM_P_DISK_PRESSURE) && (fl & KSIM_N_DISK_PRESSURE)) ? (1u << KSIM_R_DISK_PRESSURE) : 0u;
-    const uint32_t m = m_cond ? m_cond : m_uns ? m_uns : m_gen ? m_gen : m_host ? m_host : m_ports ? m_ports
-                     : m_sel ? m_sel : m_res ? m_res : m_t ? m_t : m_nt ? m_nt : m_lp ? m_lp : m_mp ? m_mp : m_dp;
+    auto en = [&](uint32_t f) -> uint32_t { return 0u - (uint32_t)((pr & f) != 0u); };
+    auto on = [](uint32_t v, uint32_t f, int r) -> uint32_t { return (uint32_t)((v & f) != 0u) << r; };
+    const uint32_t be = 0u - (uint32_t)((V.flags & KSIM_POD_BEST_EFFORT) != 0u);
+    const uint32_t m_cond = en(KSIM_P_CHECK_NODE_CONDITION) & (fl & KSIM_COND_REASON_MASK);
+    const uint32_t m_uns = en(KSIM_P_CHECK_NODE_UNSCHEDULABLE) & on(fl, KSIM_N_UNSCHEDULABLE, KSIM_R_UNSCHEDULABLE);
+    const uint32_t m_gen = en(KSIM_P_GENERAL) & (res | host | ports | sel);
+    const uint32_t m_host = en(KSIM_P_HOSTNAME) & host;
+    const uint32_t m_ports = en(KSIM_P_HOST_PORTS) & ports;
+    const uint32_t m_sel = en(KSIM_P_NODE_SELECTOR) & sel;
+    const uint32_t m_res = en(KSIM_P_RESOURCES) & res;
+    const uint32_t m_t = en(KSIM_P_TAINTS) & taint;
+    const uint32_t m_nt = en(KSIM_P_NOEXEC_TAINTS) & noexec;
+    const uint32_t m_lp = en(KSIM_P_LABEL_PRESENCE) & on(fl, KSIM_N_LABEL_PRESENCE, KSIM_R_LABEL_PRESENCE);
+    const uint32_t m_mp = en(KSIM_P_MEM_PRESSURE) & be & on(fl, KSIM_N_MEM_PRESSURE, KSIM_R_MEM_PRESSURE);
+    const uint32_t m_dp = en(KSIM_P_DISK_PRESSURE) & on(fl, KSIM_N_DISK_PRESSURE, KSIM_R_DISK_PRESSURE);
+    uint32_t m = m_cond;
+    for (const uint32_t x : {m_uns, m_gen, m_host, m_ports, m_sel, m_res, m_t, m_nt, m_lp, m_mp, m_dp}) m = m ? m : x;
     rm = m;
     if (m) return -1;
     const int32_t sc = no_prio ? 0 : (int32_t)ksim_fast_score(V.nz_c + r.zc, r.ac, r.dac, V.nz_m + r.zm, r.am, r.dam, wl, wmr, wb);
@@ -490,12 +543,14 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     if (V.k1 * V.k2 > 1) {
       int a = 0, b = 0;
       if (V.k1 > 1) {
-        const int64_t x = (int64_t)V.cls * c.n_taint_sets + ts;
-        a = L.tables ? (uint8_t)(ksim_smem + L.off_ttc)[x] : c.tt_class[x];
+        const int64_t x = (int64_t)V.cls * cx->n_taint_sets + ts;
+        if (L.tables) a = (uint8_t)(ksim_smem + L.off_ttc)[x];
+        else a = cx->tt_class[x];
       }
       if (V.k2 > 1) {
-        const int64_t x = (int64_t)V.cls * c.n_label_sets + ls;
-        b = L.tables ? (uint8_t)(ksim_smem + L.off_nac)[x] : c.na_class[x];
+        const int64_t x = (int64_t)V.cls * cx->n_label_sets + ls;
+        if (L.tables) b = (uint8_t)(ksim_smem + L.off_nac)[x];
+        else b = cx->na_class[x];
       }
       cl = a * V.k2 + b;
     }
@@ -528,13 +583,10 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   // entries with pod p-1 committed to each row (ev2 / rm2) — on the next waves up when the rows
   // fit one wave set each (split), else after ev on the same lane.  One evaluation call site,
   // so one inlined copy; the partial reads the entries back from LDS.
-  auto eval_rows = [&](int64_t p, bool hyp, const RowDelta& d, int32_t (&e)[NPT], int buf) {
+  auto eval_rows = [&](const PodView& V, int64_t p, bool hyp, const RowDelta& d, int32_t (&e)[NPT], int buf) {
 #ifdef KSIM_STAMPS
     const uint64_t q0 = __builtin_amdgcn_s_memtime();
-#endif
-    const PodView V = pod_view_lds(&s_pod[p % RING]);
-#ifdef KSIM_STAMPS
-    const uint64_t q1 = __builtin_amdgcn_s_memtime();
+    const uint64_t q1 = q0;
 #endif
     const RowDelta z{0, 0, 0, 0, 0, 0, 0, 0};
     int32_t* ev = R.ev + buf * chunk;
@@ -586,10 +638,14 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
 #pragma unroll
     for (int k = 0; k < NPT; ++k) nf += __popcll(__ballot(e[k] >= 0));
     if (lane == 0) s_fit[buf][w] = nf;
-    for (int q0 = 0; q0 < K; q0 += 4) {
-      int32_t v[4], wm[4], n[4], v2[4], wm2[4], n2[4];
+    // U classes per group (their DPP chains are independent and interleave); the group width
+    // follows K so a one- or two-class pod runs one or two chains, not four
+    auto group = [&](int q0, auto UU) {
+      constexpr int U = decltype(UU)::value;
+      int32_t v[U], wm[U], n[U], v2[U], wm2[U], n2[U];
+      uint64_t mk[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         v[u] = -1;
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
@@ -599,23 +655,26 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) wm[u] = ksimw::max_i32(v[u]);
+      for (int u = 0; u < U; ++u) wm[u] = ksimw::max_i32(v[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         n[u] = 0;
         v2[u] = -1;
+        mk[u] = 0;
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
           const bool in = e[k] >= 0 && (K == 1 || ev_cls(e[k]) == q0 + u);
           const int32_t sc = K == 1 ? e[k] : ev_score(e[k]);
-          n[u] += __popcll(__ballot(in && sc == wm[u]));
+          const uint64_t b = __ballot(in && sc == wm[u]);
+          mk[u] = b;
+          n[u] += __popcll(b);
           v2[u] = (in && sc < wm[u] && sc > v2[u]) ? sc : v2[u];
         }
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) wm2[u] = ksimw::max_i32(v2[u]);
+      for (int u = 0; u < U; ++u) wm2[u] = ksimw::max_i32(v2[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < U; ++u) {
         n2[u] = 0;
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
@@ -626,13 +685,18 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       }
       if (lane == 0) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
+        for (int u = 0; u < U; ++u) {
           if (q0 + u >= K) break;
           s_mx[buf][w][q0 + u] = wm[u]; s_cnt[buf][w][q0 + u] = wm[u] < 0 ? 0 : n[u];
           s_mx2[buf][w][q0 + u] = wm2[u]; s_cnt2[buf][w][q0 + u] = wm2[u] < 0 ? 0 : n2[u];
+          if (NPT == 1) s_msk[buf][w][q0 + u] = wm[u] < 0 ? 0ull : mk[u];
         }
       }
-    }
+    };
+    if (K == 1) group(0, std::integral_constant<int, 1>{});
+    else if (K == 2) group(0, std::integral_constant<int, 2>{});
+    else
+      for (int q0 = 0; q0 < K; q0 += 4) group(q0, std::integral_constant<int, 4>{});
   };
   // the last row wave of a pod: combine the row waves' partials (lane q = class q) into the
   // workgroup's top two per class → LDS (the owner's correction) and the granule payloads
@@ -682,6 +746,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     if (lane == 0) old = atomicAdd(&s_arr[buf], 1);
     old = __builtin_amdgcn_readfirstlane(old);
     if (old + 1 == NW - 1) {
+      PROBE(10);
       if (lane == 0) s_arr[buf] = 0;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
       const uint64_t v = combine(K, buf);
@@ -696,7 +761,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     int32_t e[NPT];
     const int K0 = pod_K(s_pod[c.first % RING]);
     const RowDelta z{0, 0, 0, 0, 0, 0, 0, 0};
-    eval_rows(c.first, false, z, e, (int)(c.first & 1));
+    eval_rows(pod_view_lds(&s_pod[c.first % RING]), c.first, false, z, e, (int)(c.first & 1));
     partial(e, K0, c.first & 1, wv);
     arrive_publish(c.first, K0, c.first & 1);
   }
@@ -734,6 +799,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       const int slot = (int)(pod % NSLOT);
       STAMP(1);
       uint64_t g[MB];
+      uint64_t gq[KF][MB];  // granules of classes 1..KF, kept in registers (LDS beyond)
       bool ok = false;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
 #ifdef KSIM_STAMPS
@@ -765,10 +831,9 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
 #pragma unroll
             for (int j = 0; j < MB; ++j) {
               const int b = lane * MB + j;
-              if (q0 + u < K && b < G) {
-                mine &= gtag(v[u][j]) == tag;
-                s_gq[q0 + u - 1][b] = v[u][j];
-              }
+              if (q0 + u < K && b < G) mine &= gtag(v[u][j]) == tag;
+              if (q0 == 1) gq[u][j] = v[u][j];
+              else if (q0 + u < K && b < G) s_gq[q0 + u - 1 - KF][b] = v[u][j];
             }
         }
 #ifdef KSIM_STAMPS
@@ -792,6 +857,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         __builtin_amdgcn_s_sleep(1);
       }
       STAMP(2);
+      PROBE(2);
 #pragma unroll
       for (int j = 0; j < MB; ++j) g[j] = (lane * MB + j < G) ? g[j] : 0;
       ok = __all(ok);
@@ -811,23 +877,33 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         C0 = ksimw::sum_i32((n && m == M0) ? n : 0);
       }
       STAMP(9);
+      // lane q: reduce class q's global maximum and its count (registers: the control wave's
+      // LDS round trips queue behind the row waves' evaluation traffic)
+      int32_t mq_l = lane == 0 ? M0 : -1, cq_l = lane == 0 ? C0 : 0;
       if (ok && K > 1) {  // further reduce classes (TaintToleration x NodeAffinity), swept above
-        if (lane == 0) { s_M[0] = M0; s_C[0] = C0; }
-        for (int q = 1; q < K; ++q) {
+        auto class_stat = [&](int q, const uint64_t (&v)[MB]) {
           int32_t mm = -1, nn = 0;
 #pragma unroll
           for (int j = 0; j < MB; ++j) {
             const int b = lane * MB + j;
-            if (b >= G) continue;
-            const uint64_t v = s_gq[q - 1][b];
-            const int32_t cnt = gcnt(v), s = gscore(v);
+            const int32_t cnt = b < G ? gcnt(v[j]) : 0, s = gscore(v[j]);
             if (cnt == 0) continue;
             if (s > mm) { mm = s; nn = cnt; }
             else if (s == mm) nn += cnt;
           }
           const int32_t Mq = ksimw::max_i32(nn ? mm : -1);
           const int32_t Cq = ksimw::sum_i32((nn && mm == Mq) ? nn : 0);
-          if (lane == 0) { s_M[q] = Mq; s_C[q] = Cq; }
+          mq_l = lane == q ? Mq : mq_l;
+          cq_l = lane == q ? Cq : cq_l;
+        };
+#pragma unroll
+        for (int u = 0; u < KF; ++u)
+          if (1 + u < K) class_stat(1 + u, gq[u]);
+        for (int q = 1 + KF; q < K; ++q) {
+          uint64_t v[MB];
+#pragma unroll
+          for (int j = 0; j < MB; ++j) v[j] = lane * MB + j < G ? s_gq[q - 1 - KF][lane * MB + j] : 0;
+          class_stat(q, v);
         }
       }
       STAMP(11);
@@ -847,9 +923,9 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
             // lane q = reduce class q, all at once: NormalizeReduce's maxima over the filtered
             // set (classes with fit nodes), each class's weighted total, the best total and the
             // classes that reach it (reduce.go:29-64, generic_scheduler.go:632-639)
-            const bool live = lane < K && s_C[lane < K ? lane : 0] != 0;
-            const int32_t cq = live ? s_C[lane] : 0;
-            const int64_t mq = live ? s_M[lane] : 0;
+            const bool live = lane < K && cq_l != 0;
+            const int32_t cq = live ? cq_l : 0;
+            const int64_t mq = live ? mq_l : 0;
             const int64_t mxT = wave_max_i64(live ? tv_l : 0), mxA = wave_max_i64(live ? av_l : 0);
             const int64_t t = live ? class_total(c, tv_l, av_l, mq, mxT, mxA) : -1;  // totals are >= 0
             const int64_t best = wave_max_i64(t);
@@ -876,10 +952,17 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
               m = gfit(g[j]);
             } else {
               if ((win & 1u) && gcnt(g[j]) && gscore(g[j]) == M0) m += gcnt(g[j]);
-              for (int q = 1; q < K; ++q) {
+#pragma unroll
+              for (int u = 0; u < KF; ++u) {
+                const int q = 1 + u;
+                if (q >= K || !((win >> q) & 1u)) continue;
+                const uint64_t v = gq[u][j];
+                if (gcnt(v) && gscore(v) == __builtin_amdgcn_readlane(mq_l, q)) m += gcnt(v);
+              }
+              for (int q = 1 + KF; q < K; ++q) {
                 if (!((win >> q) & 1u)) continue;
-                const uint64_t v = s_gq[q - 1][b];
-                if (gcnt(v) && gscore(v) == s_M[q]) m += gcnt(v);
+                const uint64_t v = s_gq[q - 1 - KF][b];
+                if (gcnt(v) && gscore(v) == __builtin_amdgcn_readlane(mq_l, q)) m += gcnt(v);
               }
             }
           }
@@ -918,10 +1001,31 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       o_prev = __builtin_amdgcn_s_memtime();
 #endif
       if (mode > 0 && blk == (int)blockIdx.x) {
-        // ---------------- d. owner: exact row (rank from the top), commit, correction ----------
-        // scan pod's entries from the top: 64-row segments, four per LDS round trip
+        // ---------------- d. owner: exact row (rank from the top), correction, commit ----------
         int32_t jsel = -1;
-        {
+        if (NPT == 1 && mode == 2 && s_mok[pb]) {
+          // from the row waves' top masks: lane w = row wave w's rows at a winning class's
+          // maximum (a wave whose top is below the class maximum holds none of them)
+          uint64_t cm = 0;
+          for (uint32_t wq = win; wq; wq &= wq - 1) {
+            const int q = __builtin_ctz(wq);
+            const int32_t t = __builtin_amdgcn_readlane(tgt, q);
+            const int32_t ts = K == 1 ? t : ev_score(t);
+            if (lane >= 1 && lane < NW && s_cnt[pb][lane][q] && s_mx[pb][lane][q] == ts) cm |= s_msk[pb][lane][q];
+          }
+          int32_t rr = rank;
+#pragma unroll
+          for (int w = NW - 1; w >= 1; --w) {  // rows of wave w: (w-1)*64 + lane; the top first
+            if (jsel >= 0) break;
+            const uint64_t m = (uint64_t)readlane64((int64_t)cm, w);
+            const int nbits = __popcll(m);
+            if (rr >= nbits) { rr -= nbits; continue; }
+            const bool is = ((m >> lane) & 1ull) && __popcll((m >> lane) >> 1) == rr;
+            jsel = (w - 1) * 64 + (__builtin_ffsll((long long)__ballot(is)) - 1);
+          }
+        }
+        if (jsel < 0) {
+          // scan pod's entries from the top: 64-row segments, four per LDS round trip
           const int32_t* ev = R.ev + pb * chunk;
           int32_t rr = rank;
           const int nseg = (nrows + 63) / 64;
@@ -953,17 +1057,35 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
           }
         }
         OSTAMP(22);
+        PROBE(3);
         if (jsel < 0) {
           mode = -1;
           if (lane == 0) atomicOr(c.err, 2);
         } else {
-          // commit the LDS row (NodeInfo.AddPod); the HBM side columns come after the correction
           const bool side = (P.add_gpu | P.add_eph | P.scalar_cnt | P.port_cnt) != 0;
-          if (lane == 0) {
-            R.rc[jsel] += P.add_cpu; R.rm[jsel] += P.add_mem; R.zc[jsel] += P.nz_cpu; R.zm[jsel] += P.nz_mem;
-            R.count[jsel] += 1;
-          }
-          bool side_done = false;
+          // NodeInfo.AddPod on the row: LDS columns, then the side columns (HBM / LDS ports).
+          // Only after the row waves' pod + 1 evaluation is complete: they read this row.
+          auto commit_row = [&]() {
+            if (lane == 0) {
+              R.rc[jsel] += P.add_cpu; R.rm[jsel] += P.add_mem; R.zc[jsel] += P.nz_cpu; R.zm[jsel] += P.nz_mem;
+              R.count[jsel] += 1;
+              if (side) {
+                const bool lds_ports = P.port_cnt && L.ps;
+                uint32_t fl = R.fl[jsel];
+                if (P.add_gpu | P.add_eph | P.scalar_cnt | (P.port_cnt && !L.ps)) {
+                  fl = commit_side(cg, &P, lo + jsel, fl, lds_ports ? 0 : 1);
+                  R.fl[jsel] = fl;
+                }
+                if (lds_ports) commit_ports_lds(cg, &P, lo + jsel, jsel, (int32_t)chunk, L.off_pc, L.off_pk);
+              }
+            }
+          };
+          // pods through `pod` committed: the row waves may evaluate pod + 2 (their chain to the
+          // next-but-one decision starts here, so the owner releases them before its bookkeeping)
+          auto release_dec = [&]() {
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+            if (lane == 0) __hip_atomic_store(&s_dec, (int32_t)(pod - c.first + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          };
           OSTAMP(23);
           if (has_next) {
             // the row waves' pod + 1 stats (and ev2) must be complete
@@ -973,25 +1095,18 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
             const ksim_pod& Q = s_pod[(pod + 1) % RING];
             const int Kn = pod_K(Q);
+            const int q = lane < Kn ? lane : 0;
+            // one LDS round trip: the workgroup's top two, the row's two entries, the flags
+            const int4 t = s_top[nb][q];
+            const int32_t fN = s_F[nb];
             const int32_t e1 = R.ev[nb * chunk + jsel];
-            int32_t e2;
-            uint32_t rm2;
-            if (s_ev2[nb]) {  // the dual hypothesis already evaluated pod + 1 on the committed row
-              e2 = R.ev2[nb * chunk + jsel];
-              rm2 = R.rm2[nb * chunk + jsel];
-            } else {          // commit everything, then evaluate the one row here
-              if (side) {
-                if (lane == 0) {
-                  const bool lds_ports = P.port_cnt && L.ps;
-                  uint32_t fl = R.fl[jsel];
-                  if (P.add_gpu | P.add_eph | P.scalar_cnt | (P.port_cnt && !L.ps)) {
-                    fl = commit_side(cg, &P, lo + jsel, fl, lds_ports ? 0 : 1);
-                    R.fl[jsel] = fl;
-                  }
-                  if (lds_ports) commit_ports_lds(cg, &P, lo + jsel, jsel, (int32_t)chunk, L.off_pc, L.off_pk);
-                }
-                side_done = true;
-              }
+            const bool dual = s_ev2[nb] != 0;
+            const int32_t mok = s_mok[nb];
+            int32_t e2 = R.ev2[nb * chunk + jsel];
+            uint32_t rm2 = R.rm2[nb * chunk + jsel];
+            if (!dual) {  // commit everything, then evaluate the one row here
+              commit_row();
+              release_dec();
               __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
               __builtin_amdgcn_wave_barrier();
               __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1001,9 +1116,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
             OSTAMP(16);
             // O(1) correction of this workgroup's pod + 1 partial: e1 leaves its class, e2 joins
             // (the reduce class is the row's, the same for both when both fit)
-            const int q = lane < Kn ? lane : 0;
-            const int4 t = s_top[nb][q];
-            int32_t f = s_F[nb] - (e1 >= 0) + (e2 >= 0);
+            int32_t f = fN - (e1 >= 0) + (e2 >= 0);
             int32_t m = t.x, n = t.y;
             const int q1 = e1 < 0 ? -1 : (Kn == 1 ? 0 : ev_cls(e1));
             const int32_t s1 = Kn == 1 ? e1 : ev_score(e1);
@@ -1020,27 +1133,41 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
             if (n == 0) m = -1;
             const uint64_t v = (lane == 0 ? ((uint64_t)f << 44) : 0) | ((uint64_t)n << 32) | (uint64_t)(uint32_t)m;
             if (lane < Kn) store_granule(fix_at(granules, (int)((pod + 1) % NSLOT), lane), (ptag(pod + 1) << 56) | v);
+            OSTAMP(19);
+            PROBE(4);
+            if (dual) {
+              commit_row();
+              release_dec();
+            }
             if (lane == 0) {
               R.ev[nb * chunk + jsel] = e2;
               R.rm1[nb * chunk + jsel] = rm2;
+              // the same replacement in row wave wj's top masks (one row per row thread)
+              if (NPT == 1 && mok) {
+                const int wj = 1 + jsel / 64;
+                const uint64_t bit = 1ull << (jsel % 64);
+                bool keep = true;
+                if (q1 >= 0 && s_cnt[nb][wj][q1] && s_mx[nb][wj][q1] == s1) {
+                  s_msk[nb][wj][q1] &= ~bit;
+                  const int32_t cn = s_cnt[nb][wj][q1] - 1;
+                  s_cnt[nb][wj][q1] = cn;
+                  keep = cn > 0;  // the wave's next value's rows are not recorded: scan
+                }
+                if (keep && q2 >= 0) {
+                  const int32_t cn = s_cnt[nb][wj][q2], tv = s_mx[nb][wj][q2];
+                  if (cn == 0 || s2 > tv) { s_mx[nb][wj][q2] = s2; s_cnt[nb][wj][q2] = 1; s_msk[nb][wj][q2] = bit; }
+                  else if (s2 == tv) { s_cnt[nb][wj][q2] = cn + 1; s_msk[nb][wj][q2] |= bit; }
+                }
+                if (!keep) s_mok[nb] = 0;
+              }
             }
-            OSTAMP(19);
 #ifdef KSIM_STAMPS
             if (lane == 0) atomicAdd((unsigned long long*)&c.dbg[21], 1ull);
 #endif
+          } else {
+            commit_row();
           }
-          if (lane == 0) {
-            if (side && !side_done) {
-              const bool lds_ports = P.port_cnt && L.ps;
-              uint32_t fl = R.fl[jsel];
-              if (P.add_gpu | P.add_eph | P.scalar_cnt | (P.port_cnt && !L.ps)) {
-                fl = commit_side(cg, &P, lo + jsel, fl, lds_ports ? 0 : 1);
-                R.fl[jsel] = fl;
-              }
-              if (lds_ports) commit_ports_lds(cg, &P, lo + jsel, jsel, (int32_t)chunk, L.off_pc, L.off_pk);
-            }
-            c.out_node[pod] = (int32_t)(lo + jsel);
-          }
+          if (lane == 0) c.out_node[pod] = (int32_t)(lo + jsel);
           OSTAMP(20);
         }
       }
@@ -1065,6 +1192,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         if (lane < KSIM_NREASONS && acc) atomicAdd(&c.out_reasons[pod * KSIM_NREASONS + lane], acc);
       }
       // pods through `pod` are decided and committed: the row waves may evaluate pod + 2
+      PROBE(5);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       if (lane == 0) __hip_atomic_store(&s_dec, (int32_t)(pod - c.first + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       STAMP(4);
@@ -1072,7 +1200,6 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   } else {
   for (int64_t pod = c.first; pod < c.end; ++pod) {
     const bool has_next = pod + 1 < c.end;
-    const int pb = (int)(pod & 1);        // LDS buffers of pod
     const int nb = (int)((pod + 1) & 1);  // LDS buffers of pod + 1
 #ifdef KSIM_STAMPS
     uint64_t o_prev = 0;
@@ -1089,7 +1216,12 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       const uint64_t te0 = __builtin_amdgcn_s_memtime();
 #endif
       if (has_next) {
-        // pod + 1 is evaluated on the rows as committed through pod - 1 (the hypothesis covers pod)
+        // pod + 1 is evaluated on the rows as committed through pod - 1 (the hypothesis covers pod).
+        // The pod view and the commit delta need only the ring: before the wait, off the chain.
+        PodView V = pod_view_lds(&s_pod[(pod + 1) % RING]);
+        const int Kn = pod_K(s_pod[(pod + 1) % RING]);
+        RowDelta d{0, 0, 0, 0, 0, 0, 0, 0};
+        const bool hyp = delta_of(pod, pod + 1, d);
         const int32_t need = (int32_t)(pod - c.first);
 #ifdef KSIM_STAMPS
         const uint64_t tw0 = __builtin_amdgcn_s_memtime();
@@ -1102,12 +1234,17 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
 #endif
         if (__hip_atomic_load(&s_abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) break;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        PROBE(1);
+        PROBE_IF(7, wv == 1);
+        PROBE_IF(8, wv == 3);
+        PROBE_IF(9, wv >= 5);
+        PROBE_IF(11, wv == 2);
         int32_t e[NPT];
-        const int Kn = pod_K(s_pod[(pod + 1) % RING]);
-        RowDelta d{0, 0, 0, 0, 0, 0, 0, 0};
-        const bool hyp = delta_of(pod, pod + 1, d);
-        if (tid == 64) s_ev2[nb] = hyp ? 1 : 0;
-        eval_rows(pod + 1, hyp, d, e, nb);
+        if (tid == 64) {
+          s_ev2[nb] = hyp ? 1 : 0;
+          s_mok[nb] = 1;
+        }
+        eval_rows(V, pod + 1, hyp, d, e, nb);
 #ifdef KSIM_STAMPS
         const uint64_t te1 = __builtin_amdgcn_s_memtime();
         if (tid == 64) st_acc[14] += te1 - te0;
@@ -1117,6 +1254,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         const uint64_t te2 = __builtin_amdgcn_s_memtime();
         if (tid == 64) st_acc[15] += te2 - te1;
 #endif
+        PROBE(6);
         arrive_publish(pod + 1, Kn, nb);
       }
 #ifdef KSIM_STAMPS

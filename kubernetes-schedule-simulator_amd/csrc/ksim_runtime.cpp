@@ -939,13 +939,17 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
       const size_t N = (size_t)n, P = (size_t)count, K = (size_t)g.K;
       const size_t per = al(4 * N * 8) + al(N * 4) + al(K * g.st[0] * 4) + al(g.level_entries * 8) + al(K * 4) + al(8) +
                          al(P * 4) + al(sizeof(kf64::EvCfg));
-      const size_t budget = (size_t)24 << 30;  // all 4,096 C5 scenarios (~3.7 MB each) in one launch
+      // scratch budget: at most 24 GiB (all 4,096 C5 scenarios, ~3.7 MB each, in one launch) and
+      // at most half of the device memory free now (a shared or smaller device gets smaller chunks)
+      size_t budget = (size_t)24 << 30, mfree = 0, mtotal = 0;
+      if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree / 2 < budget) budget = mfree / 2;
       int32_t chunk = (int32_t)std::max<size_t>(1, std::min<size_t>((size_t)n_scen, budget / per));
       if (const char* ch = getenv("KSIM_SWEEP_CHUNK")) chunk = std::max(1, std::min(chunk, atoi(ch)));  // tests
-      const size_t C = (size_t)chunk;
-      const size_t need = C * (al(4 * N * 8) + al(N * 4)) + al(C * K * g.st[0] * 4) + al(C * g.level_entries * 8) +
-                          al(C * K * 4) + al(C * 8) + al(C * P * 4) + al(C * sizeof(kf64::EvCfg)) + 4096;
-      if (h->swt_bytes < need) {
+      auto need_of = [&](size_t C) {
+        return C * (al(4 * N * 8) + al(N * 4)) + al(C * K * g.st[0] * 4) + al(C * g.level_entries * 8) + al(C * K * 4) +
+               al(C * 8) + al(C * P * 4) + al(C * sizeof(kf64::EvCfg)) + 4096;
+      };
+      if (h->swt_bytes < need_of((size_t)chunk)) {
         if (h->swt_scratch) {
           for (auto& b : h->bufs)
             if (b.p == h->swt_scratch) b.p = nullptr;
@@ -953,11 +957,22 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
           h->swt_scratch = nullptr;
           h->swt_bytes = 0;
         }
+        // an allocation that fails halves the scenario chunk until one fits (one scenario at least)
         char* p = nullptr;
-        if ((rc = dev_alloc(h, &p, need))) return rc;
-        h->swt_scratch = p;
-        h->swt_bytes = need;
+        for (;;) {
+          const size_t need = need_of((size_t)chunk);
+          if (hipMalloc((void**)&p, need) == hipSuccess) {
+            h->bufs.push_back({p, need});
+            h->swt_scratch = p;
+            h->swt_bytes = need;
+            break;
+          }
+          (void)hipGetLastError();
+          if (chunk == 1) return ksim_fail(h, KSIM_E_NOMEM, "ksim_sweep: no device memory for one scenario (%zu bytes)", need);
+          chunk = (chunk + 1) / 2;
+        }
       }
+      const size_t C = (size_t)chunk;
       char* q = (char*)h->swt_scratch;
       auto take = [&](size_t b) { char* r = q; q += al(b); return r; };
       KsimTreeSweep sw{};

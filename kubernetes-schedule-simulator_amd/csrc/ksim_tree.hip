@@ -380,7 +380,10 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
   // reads them with readlane instead of two dependent LDS loads; LDS keeps the root level too
   uint64_t rootv = lane < K ? root[lane] : 0ull;
   int32_t fitv = lane < K ? s_fit[lane] : 0;
-  int hist_cls = -1;
+  // lane k: the last pod of class k whose FitError histogram (in out_reasons) still holds — a
+  // failing pod commits nothing, so until the next commit every class's histogram stays valid
+  // (past saturation, where nearly every pod fails, each class is scanned once per commit)
+  int64_t hist_pod = -1;
   int64_t p = a.first;
   int64_t ready = a.first;  // pods below this are in the ring
   bool stop = false;
@@ -404,7 +407,11 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
     if (F == 0) {  // FitError: no commit, lastNodeIndex unchanged
       if (lane == 0) a.out_node[p] = -1;
       if (a.collect) {
-        if (hist_cls != k) {  // histogram of first-failing-predicate reasons over every node
+        const int64_t pk = (int64_t)(((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)((uint64_t)hist_pod >> 32), k) << 32) |
+                                     (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)hist_pod, k));
+        if (pk >= 0) {  // same wave wrote it: program order makes the load see the store
+          if (lane < KSIM_NREASONS) a.out_reasons[p * KSIM_NREASONS + lane] = a.out_reasons[pk * KSIM_NREASONS + lane];
+        } else {  // histogram of first-failing-predicate reasons over every node
           if (lane < KSIM_NREASONS) s_hist[lane] = 0;
           const kf64::FPod P = class_pod(s_cls[k]);
           for (int i0 = 0; i0 < n; i0 += 64) {
@@ -417,9 +424,9 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
                 if (lane == 0 && nr) s_hist[r] += nr;
               }
           }
-          hist_cls = k;
+          hist_pod = lane == k ? p : hist_pod;
+          if (lane < KSIM_NREASONS) a.out_reasons[p * KSIM_NREASONS + lane] = s_hist[lane];
         }
-        if (lane < KSIM_NREASONS) a.out_reasons[p * KSIM_NREASONS + lane] = s_hist[lane];
       }
       ++p;
       if (lane == 0) __hip_atomic_store(&s_done, p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -593,7 +600,7 @@ __global__ __launch_bounds__(128) void ksim_tree_kernel(TreeArgs a0) {
     ts_acc[6] += __popcll(__ballot(chg));
     ts_acc[7] += __popcll(__ballot(resc_h != 0));
 #endif
-    hist_cls = -1;
+    hist_pod = -1;
     // quantities must stay exact in float64 (ksim_f64.h): stop after this pod otherwise
     stop = nrc >= LIM48 || nrm >= LIM48 || nzc >= LIM48 || nzm >= LIM48;
     ++p;

@@ -298,6 +298,10 @@ class ShardedScheduler(GenericScheduler):
 
     def __init__(self, cluster: Cluster, predicates, priorities, rank, world, device=0, collect_reasons=False,
                  last_node_index=0):
+        if collect_reasons:
+            # a rank's FitError histogram covers its own shard only ("0/n_shard nodes"), and the
+            # ranks' histograms are not summed: refuse rather than build a wrong FitError text
+            raise abi.KsimUnsupported(abi.E_UNSUPPORTED, "node-sharded scheduling does not collect FitError reasons")
         n = cluster.n_nodes
         self.lo, self.hi = rank * n // world, (rank + 1) * n // world
         self.rank, self.world = rank, world

@@ -29,6 +29,29 @@ def test_golden_priorities_on_gpu(c):
     assert [[h, got[h]] for h, _ in c["expect"]] == c["expect"]
 
 
+REDUCE_PRIORITIES = ("TaintTolerationPriority", "NodeAffinityPriority")
+
+
+@pytest.mark.parametrize("mode", [abi.MODE_LAUNCH, abi.MODE_PERSISTENT])
+@pytest.mark.parametrize("c", [c for c in load("priorities") if c["priority"] in REDUCE_PRIORITIES], ids=case_id)
+def test_golden_reduce_priorities_select_on_gpu(c, mode):
+    """The reference's TaintToleration / NodeAffinity golden vectors through the scheduling
+    kernels' own NormalizeReduce (reduce classes, per-class maxima, class totals — not the host
+    numpy path priority_scores uses): with lastNodeIndex = k, the pod must land on the k-th host
+    of the golden maximum in descending bytewise name order (selectHost,
+    generic_scheduler.go:183-198), for every k over two periods."""
+    expect = dict((h, s) for h, s in c["expect"])
+    best = max(expect.values())
+    tied = sorted((h for h, s in expect.items() if s == best), key=lambda h: h.encode(), reverse=True)
+    for k in range(2 * len(tied)):
+        cl, g = _sched(c["nodes"], c["pods"], [c["pod"]], [], [(c["priority"], 1)], mode=mode, last_node_index=k)
+        assert cl.n_nodes == len(expect)
+        out, _, _ = g.schedule(0, 1)
+        assert cl.names[int(out[0])] == tied[k % len(tied)], (k, tied)
+        assert g.last_node_index == (k + 1 if len(expect) > 1 else k)
+        g.close()
+
+
 @pytest.mark.parametrize("c", load("predicates"), ids=case_id)
 def test_golden_predicates_on_gpu(c):
     cl, g = _sched([c["node"]], c["pods"], [c["pod"]], [c["predicate"]], [("EqualPriority", 1)])
