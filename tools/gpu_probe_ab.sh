@@ -1,6 +1,6 @@
 #!/bin/bash
 # Critical-path probe A/B for one workload on one box: the C2 parity subset, then the base
-# library and each probe build (tools/build_probes.sh) timed twice, then the stamps split.
+# library and each probe build (tools/probe_libs.sh) timed twice, then the stamps split.
 # Usage: tools/gpu_probe_ab.sh <tag> <pytest -k expr> <workload> k1 k2 ...
 set -o pipefail
 TAG=$1; K=$2; W=$3; shift 3
