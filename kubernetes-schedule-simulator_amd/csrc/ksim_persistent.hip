@@ -31,6 +31,7 @@
 // -1 = no fit node of that class).  Scores < 2^31 and chunks <= 4095 rows (host checks).
 // Sweep lane l reads workgroups [l*MAXB, l*MAXB+MAXB): name-rank order is lane-major, so the
 // matches above a workgroup are one DPP prefix sum away.
+#include <cstdlib>
 #include <type_traits>
 
 #include "ksim_fast.h"
@@ -117,41 +118,25 @@ __device__ __forceinline__ int32_t ev_pack(bool fit, int32_t cl, int32_t sc) { r
 __device__ __forceinline__ int32_t ev_cls(int32_t e) { return e >> EV_SHIFT; }
 __device__ __forceinline__ int32_t ev_score(int32_t e) { return e & ((1 << EV_SHIFT) - 1); }
 
-struct Rows {  // LDS image of the owned rows (SoA)
-  int64_t *ac, *am, *rc, *rm, *zc, *zm;
-  double *dac, *dam;  // alloc as float64 (derived, for the fast path)
-  int32_t *allowed, *count;
-  uint32_t* fl;
-  int32_t* ev;   // [2][rows] per pod parity: packed evaluation of the row (ev_pack)
-  int32_t *ls, *ts;  // label-set / taint-set id of the row
-  int32_t* ev2;  // [2][rows] per pod parity: the evaluation with the previous pod committed to the row
-  uint32_t* rm2; // [2][rows] ... and its reason mask
-  uint32_t* rm1; // [2][rows] reason mask of ev
+// LDS image of one owned row, array-of-structs: every field is an immediate offset from one
+// per-lane address (row * 116 B), so the evaluation holds no per-column base addresses in
+// scalar registers; the 29-dword stride keeps a wave's same-field accesses on distinct banks.
+struct __attribute__((packed, aligned(4))) LRow {
+  int64_t ac, am, rc, rm, zc, zm;
+  double dac, dam;  // alloc as float64 (derived, for the fast path)
+  int32_t allowed, count;
+  uint32_t fl;
+  int32_t ls, ts;    // label-set / taint-set id of the row
+  int32_t ev[2];     // per pod parity: packed evaluation of the row (ev_pack)
+  int32_t ev2[2];    // per pod parity: the evaluation with the previous pod committed to the row
+  uint32_t rm1[2];   // reason mask of ev
+  uint32_t rm2[2];   // ... and of ev2
 };
 
-// 6 x i64 + 2 x f64 + 3 x i32 + 2 x i32 evaluations + 2 x i32 set ids + 2 x 2 x i32 dual
-// hypothesis + 2 x i32 reason masks
-constexpr int LDS_ROW_BYTES = 8 * 8 + 3 * 4 + 2 * 4 + 2 * 4 + 4 * 4 + 2 * 4;  // 116
+constexpr int LDS_ROW_BYTES = (int)sizeof(LRow);  // 116
+static_assert(sizeof(LRow) == 116, "LRow layout");
 
 extern __shared__ __attribute__((aligned(16))) char ksim_smem[];  // dynamic LDS: the row image
-
-__device__ __forceinline__ Rows carve(char* smem, int rows) {
-  Rows r;
-  int64_t* p = reinterpret_cast<int64_t*>(smem);
-  r.ac = p; r.am = p + rows; r.rc = p + 2 * rows; r.rm = p + 3 * rows; r.zc = p + 4 * rows; r.zm = p + 5 * rows;
-  double* d = reinterpret_cast<double*>(p + 6 * rows);
-  r.dac = d; r.dam = d + rows;
-  int32_t* q = reinterpret_cast<int32_t*>(d + 2 * rows);
-  r.allowed = q; r.count = q + rows;
-  r.fl = reinterpret_cast<uint32_t*>(q + 2 * rows);
-  r.ev = q + 3 * rows;
-  r.ls = q + 5 * rows;
-  r.ts = q + 6 * rows;
-  r.ev2 = q + 7 * rows;
-  r.rm2 = reinterpret_cast<uint32_t*>(q + 9 * rows);
-  r.rm1 = reinterpret_cast<uint32_t*>(q + 11 * rows);
-  return r;
-}
 
 }  // namespace
 
@@ -164,6 +149,11 @@ struct PLayout {
   int32_t tables;      // 1: sel_ok / taint_ok / noexec_ok / tt_class / na_class staged
   int32_t off_pc, off_pk, off_sel, off_tok, off_nok, off_ttc, off_nac;  // byte offsets in ksim_smem
   int32_t off_ttv, off_nav;  // [C][KSIM_MAX_RCLASS] reduce-class map values (int64)
+  // [C][rows] uint16 per (pod class, owned row), built at launch from the class tables: bit 0 the
+  // selector does not match, bit 1 / 2 a NoSchedule+NoExecute / NoExecute taint is not
+  // tolerated, bits 4-7 / 8-11 the TaintToleration / NodeAffinity reduce class — one LDS load
+  // beside the row's own instead of two dependent table lookups per evaluation (0: not staged)
+  int32_t off_st;
 };
 
 namespace {
@@ -351,23 +341,33 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   const int64_t lo = (int64_t)blockIdx.x * chunk;
   const int64_t hi = (lo + chunk < c.n) ? lo + chunk : c.n;
   const int32_t nrows = (int32_t)(hi - lo);
-  Rows R = carve(ksim_smem, (int)chunk);
+  LRow* const RW = reinterpret_cast<LRow*>(ksim_smem);
   const uint32_t preds = c.preds;
   const int64_t wl = c.w[KSIM_W_LEAST_REQUESTED], wmr = c.w[KSIM_W_MOST_REQUESTED], wb = c.w[KSIM_W_BALANCED];
   const bool no_prio = c.no_prio != 0;
   // dual hypothesis layout: split (ev and ev2 on disjoint waves) when the rows fit both halves
   const bool split = NPT == 1 && nrows <= SPLIT_ROWS;
+  // row waves with rows to evaluate (split: the ev waves from row thread 0, the ev2 waves from
+  // `half`); the others sit the pod loop out — they would only add arrivals and LDS traffic
+  auto active = [&](int w) -> bool {
+    const int r0 = (w - 1) * 64;
+    if (!split) return r0 < nrows || NPT > 1;
+    const int hf = 64 * ((nrows + 63) / 64);
+    return r0 < nrows || (r0 >= hf && r0 - hf < nrows);
+  };
+  int nact = 0;
+  for (int w = 1; w < NW; ++w) nact += active(w) ? 1 : 0;
 
   for (int32_t j = tid; j < nrows; j += BS) {  // stage the owned rows into LDS
     const int64_t i = lo + j;
     const int64_t ac = c.alloc_cpu[i], am = c.alloc_mem[i];
-    R.ac[j] = ac; R.am[j] = am;
-    R.dac[j] = (double)ac;
-    R.dam[j] = (double)am;
-    R.rc[j] = c.req_cpu[i]; R.rm[j] = c.req_mem[i];
-    R.zc[j] = c.nz_cpu[i]; R.zm[j] = c.nz_mem[i];
-    R.allowed[j] = c.allowed_pods[i]; R.count[j] = c.pod_count[i]; R.fl[j] = c.flags[i];
-    R.ls[j] = c.label_set[i]; R.ts[j] = c.taint_set[i];
+    RW[j].ac = ac; RW[j].am = am;
+    RW[j].dac = (double)ac;
+    RW[j].dam = (double)am;
+    RW[j].rc = c.req_cpu[i]; RW[j].rm = c.req_mem[i];
+    RW[j].zc = c.nz_cpu[i]; RW[j].zm = c.nz_mem[i];
+    RW[j].allowed = c.allowed_pods[i]; RW[j].count = c.pod_count[i]; RW[j].fl = c.flags[i];
+    RW[j].ls = c.label_set[i]; RW[j].ts = c.taint_set[i];
     if (L.ps) {  // the rows' host ports (HostPortInfo), slot-major like the HBM column
       reinterpret_cast<int32_t*>(ksim_smem + L.off_pc)[j] = c.port_count[i];
       for (int32_t q = 0; q < L.ps; ++q)
@@ -386,6 +386,22 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     for (int32_t k = tid; k < C * KSIM_MAX_RCLASS; k += BS) {
       reinterpret_cast<int64_t*>(ksim_smem + L.off_ttv)[k] = c.tt_val[k];
       reinterpret_cast<int64_t*>(ksim_smem + L.off_nav)[k] = c.na_val[k];
+    }
+  }
+  if (L.off_st) {  // static per-(class, row) bits; the staged tables are read back after the barrier
+    __syncthreads();
+    const int32_t C = c.n_classes_dev;
+    uint16_t* st = reinterpret_cast<uint16_t*>(ksim_smem + L.off_st);
+    for (int32_t k = tid; k < C * nrows; k += BS) {
+      const int32_t cls = k / nrows, j = k - cls * nrows;
+      const int32_t ls = RW[j].ls, ts = RW[j].ts;
+      const uint32_t ws = reinterpret_cast<const uint32_t*>(ksim_smem + L.off_sel)[(int64_t)cls * c.lwords + (ls >> 5)];
+      const uint32_t wt = reinterpret_cast<const uint32_t*>(ksim_smem + L.off_tok)[(int64_t)cls * c.twords + (ts >> 5)];
+      const uint32_t wn = reinterpret_cast<const uint32_t*>(ksim_smem + L.off_nok)[(int64_t)cls * c.twords + (ts >> 5)];
+      const uint32_t a = (uint8_t)(ksim_smem + L.off_ttc)[(int64_t)cls * c.n_taint_sets + ts];
+      const uint32_t b = (uint8_t)(ksim_smem + L.off_nac)[(int64_t)cls * c.n_label_sets + ls];
+      st[(int64_t)cls * chunk + j] = (uint16_t)((((ws >> (ls & 31)) & 1u) ^ 1u) | ((((wt >> (ts & 31)) & 1u) ^ 1u) << 1) |
+                                                ((((wn >> (ts & 31)) & 1u) ^ 1u) << 2) | ((a & 15u) << 4) | ((b & 15u) << 8));
     }
   }
   // pod ring: RING_FILL descriptors (1 KiB) per refill, one 16-byte load per lane of wave 1, then
@@ -419,6 +435,15 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     s_abort = 0;
     s_ev2[0] = s_ev2[1] = 0;
     s_mok[0] = s_mok[1] = 1;
+    for (int w = 1; w < NW; ++w) {  // idle waves' partials: empty, for the combine and the masks
+      if (active(w)) continue;
+      for (int b = 0; b < 2; ++b) {
+        s_fit[b][w] = 0;
+        for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
+          s_mx[b][w][q] = -1; s_cnt[b][w][q] = 0; s_mx2[b][w][q] = -1; s_cnt2[b][w][q] = 0; s_msk[b][w][q] = 0;
+        }
+      }
+    }
   }
   uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex (control wave)
   __syncthreads();
@@ -435,9 +460,9 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     const KsimCtx* cx = cg;
     asm volatile("" : "+s"(cx));
     KsimFastRow r;
-    r.ac = R.ac[j]; r.am = R.am[j]; r.rc = R.rc[j] + d.c; r.rm = R.rm[j] + d.m; r.zc = R.zc[j] + d.zc;
-    r.zm = R.zm[j] + d.zm; r.dac = R.dac[j]; r.dam = R.dam[j];
-    r.allowed = R.allowed[j]; r.count = R.count[j] + d.n; r.fl = R.fl[j];
+    r.ac = RW[j].ac; r.am = RW[j].am; r.rc = RW[j].rc + d.c; r.rm = RW[j].rm + d.m; r.zc = RW[j].zc + d.zc;
+    r.zm = RW[j].zm + d.zm; r.dac = RW[j].dac; r.dam = RW[j].dam;
+    r.allowed = RW[j].allowed; r.count = RW[j].count + d.n; r.fl = RW[j].fl;
     if (d.g | d.e) {  // the previous pod's gpu / ephemeral request re-derives the over-commit bits
       const int64_t i = lo + j;
       r.fl &= ~(KSIM_N_GPU_OVER | KSIM_N_EPH_OVER);
@@ -449,7 +474,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       return ksim_fast_eval(preds, F, r, no_prio, wl, wmr, wb, rm);
     }
     const int64_t i = lo + j;
-    const int32_t ls = R.ls[j], ts = R.ts[j];
+    const int32_t ls = RW[j].ls, ts = RW[j].ts;
     const uint32_t fl = r.fl;
     // PodFitsResources (predicates.go:706-778)
     uint32_t res = (r.count + 1 > r.allowed) ? (1u << KSIM_R_INSUFFICIENT_PODS) : 0u;
@@ -494,14 +519,22 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     }
     // podMatchesNodeLabels / tolerations: bits of the staged class tables
     uint32_t sel = 0, taint = 0, noexec = 0;
-    if (V.flags & KSIM_POD_NEED_SELECTOR) {
+    uint32_t sv = 0;  // the (class, row) static bits when staged
+    if (L.off_st) {
+      sv = reinterpret_cast<const uint16_t*>(ksim_smem + L.off_st)[V.cls * chunk + j];
+      if (V.flags & KSIM_POD_NEED_SELECTOR) sel = (sv & 1u) << KSIM_R_NODE_SELECTOR;
+      if (V.flags & KSIM_POD_NEED_TAINTS) {
+        taint = ((sv >> 1) & 1u) << KSIM_R_TAINTS;
+        noexec = ((sv >> 2) & 1u) << KSIM_R_TAINTS;
+      }
+    } else if (V.flags & KSIM_POD_NEED_SELECTOR) {
       const int64_t w = (int64_t)V.cls * cx->lwords + (ls >> 5);
       uint32_t word;
       if (L.tables) word = reinterpret_cast<const uint32_t*>(ksim_smem + L.off_sel)[w];
       else word = cx->sel_ok[w];
       sel = ((word >> (ls & 31)) & 1u) ? 0u : (1u << KSIM_R_NODE_SELECTOR);
     }
-    if (V.flags & KSIM_POD_NEED_TAINTS) {
+    if (!L.off_st && (V.flags & KSIM_POD_NEED_TAINTS)) {
       const int64_t w = (int64_t)V.cls * cx->twords + (ts >> 5);
       uint32_t wt, wn;
       if (L.tables) {
@@ -518,10 +551,14 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     // Predicate enables as 32-bit integer masks (uniform, one scalar register each), node
     // conditions as per-lane bit moves: boolean selects on uniform conditions become 64-bit lane
     // masks the compiler hoists out of the pod loop and then spills
-    const uint32_t pr = preds;
-    auto en = [&](uint32_t f) -> uint32_t { return 0u - (uint32_t)((pr & f) != 0u); };
+    // preds through a VGPR: a uniform condition would come back as a hoisted 64-bit lane mask
+    uint32_t pr = preds;
+    asm volatile("" : "+v"(pr));
+    auto en = [&](uint32_t f) -> uint32_t { return 0u - ((pr / f) & 1u); };
     auto on = [](uint32_t v, uint32_t f, int r) -> uint32_t { return (uint32_t)((v & f) != 0u) << r; };
-    const uint32_t be = 0u - (uint32_t)((V.flags & KSIM_POD_BEST_EFFORT) != 0u);
+    uint32_t vf = V.flags;
+    asm volatile("" : "+v"(vf));
+    const uint32_t be = 0u - ((vf / KSIM_POD_BEST_EFFORT) & 1u);
     const uint32_t m_cond = en(KSIM_P_CHECK_NODE_CONDITION) & (fl & KSIM_COND_REASON_MASK);
     const uint32_t m_uns = en(KSIM_P_CHECK_NODE_UNSCHEDULABLE) & on(fl, KSIM_N_UNSCHEDULABLE, KSIM_R_UNSCHEDULABLE);
     const uint32_t m_gen = en(KSIM_P_GENERAL) & (res | host | ports | sel);
@@ -542,12 +579,15 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     int32_t cl = 0;
     if (V.k1 * V.k2 > 1) {
       int a = 0, b = 0;
-      if (V.k1 > 1) {
+      if (L.off_st) {
+        a = V.k1 > 1 ? (int)((sv >> 4) & 15u) : 0;
+        b = V.k2 > 1 ? (int)((sv >> 8) & 15u) : 0;
+      } else if (V.k1 > 1) {
         const int64_t x = (int64_t)V.cls * cx->n_taint_sets + ts;
         if (L.tables) a = (uint8_t)(ksim_smem + L.off_ttc)[x];
         else a = cx->tt_class[x];
       }
-      if (V.k2 > 1) {
+      if (!L.off_st && V.k2 > 1) {
         const int64_t x = (int64_t)V.cls * cx->n_label_sets + ls;
         if (L.tables) b = (uint8_t)(ksim_smem + L.off_nac)[x];
         else b = cx->na_class[x];
@@ -589,10 +629,6 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     const uint64_t q1 = q0;
 #endif
     const RowDelta z{0, 0, 0, 0, 0, 0, 0, 0};
-    int32_t* ev = R.ev + buf * chunk;
-    uint32_t* rm1 = R.rm1 + buf * chunk;
-    int32_t* ev2 = R.ev2 + buf * chunk;
-    uint32_t* rm2 = R.rm2 + buf * chunk;
     const int32_t half = split ? 64 * ((nrows + 63) / 64) : 0;  // split: ev2 threads start here
     const int ntask = split ? 1 : NPT * (hyp ? 2 : 1);
 #pragma unroll 1
@@ -610,8 +646,8 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       if (j < nrows) {
         uint32_t m;
         const int32_t x = eval_row(V, p, j, h ? d : z, m);
-        if (h) { ev2[j] = x; rm2[j] = m; }
-        else { ev[j] = x; rm1[j] = m; }
+        if (h) { RW[j].ev2[buf] = x; RW[j].rm2[buf] = m; }
+        else { RW[j].ev[buf] = x; RW[j].rm1[buf] = m; }
       }
     }
 #ifdef KSIM_STAMPS
@@ -624,7 +660,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int32_t j = k * RT + rt;
-      e[k] = (j < nrows && !(split && rt >= half)) ? ev[j] : -1;
+      e[k] = (j < nrows && !(split && rt >= half)) ? RW[j].ev[buf] : -1;
     }
 #ifdef KSIM_STAMPS
     const uint64_t q3 = __builtin_amdgcn_s_memtime();
@@ -745,7 +781,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     int32_t old = 0;
     if (lane == 0) old = atomicAdd(&s_arr[buf], 1);
     old = __builtin_amdgcn_readfirstlane(old);
-    if (old + 1 == NW - 1) {
+    if (old + 1 == nact) {
       PROBE(10);
       if (lane == 0) s_arr[buf] = 0;
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -757,7 +793,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   };
 
   // ---- prologue: partial of the first pod ----
-  if (wv > 0) {
+  if (wv > 0 && active(wv)) {
     int32_t e[NPT];
     const int K0 = pod_K(s_pod[c.first % RING]);
     const RowDelta z{0, 0, 0, 0, 0, 0, 0, 0};
@@ -1026,7 +1062,6 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         }
         if (jsel < 0) {
           // scan pod's entries from the top: 64-row segments, four per LDS round trip
-          const int32_t* ev = R.ev + pb * chunk;
           int32_t rr = rank;
           const int nseg = (nrows + 63) / 64;
           for (int s0 = nseg - 1; s0 >= 0 && jsel < 0; s0 -= 4) {
@@ -1034,7 +1069,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
 #pragma unroll
             for (int u = 0; u < 4; ++u) {
               const int32_t j = (s0 - u) * 64 + lane;
-              const int32_t e = (s0 - u >= 0 && j < nrows) ? ev[j] : -1;
+              const int32_t e = (s0 - u >= 0 && j < nrows) ? RW[j].ev[pb] : -1;
               bool mt = e >= 0;
               if (mode == 2) {  // one compare per winning class (usually one)
                 mt = false;
@@ -1067,14 +1102,14 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
           // Only after the row waves' pod + 1 evaluation is complete: they read this row.
           auto commit_row = [&]() {
             if (lane == 0) {
-              R.rc[jsel] += P.add_cpu; R.rm[jsel] += P.add_mem; R.zc[jsel] += P.nz_cpu; R.zm[jsel] += P.nz_mem;
-              R.count[jsel] += 1;
+              RW[jsel].rc += P.add_cpu; RW[jsel].rm += P.add_mem; RW[jsel].zc += P.nz_cpu; RW[jsel].zm += P.nz_mem;
+              RW[jsel].count += 1;
               if (side) {
                 const bool lds_ports = P.port_cnt && L.ps;
-                uint32_t fl = R.fl[jsel];
+                uint32_t fl = RW[jsel].fl;
                 if (P.add_gpu | P.add_eph | P.scalar_cnt | (P.port_cnt && !L.ps)) {
                   fl = commit_side(cg, &P, lo + jsel, fl, lds_ports ? 0 : 1);
-                  R.fl[jsel] = fl;
+                  RW[jsel].fl = fl;
                 }
                 if (lds_ports) commit_ports_lds(cg, &P, lo + jsel, jsel, (int32_t)chunk, L.off_pc, L.off_pk);
               }
@@ -1099,11 +1134,11 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
             // one LDS round trip: the workgroup's top two, the row's two entries, the flags
             const int4 t = s_top[nb][q];
             const int32_t fN = s_F[nb];
-            const int32_t e1 = R.ev[nb * chunk + jsel];
+            const int32_t e1 = RW[jsel].ev[nb];
             const bool dual = s_ev2[nb] != 0;
             const int32_t mok = s_mok[nb];
-            int32_t e2 = R.ev2[nb * chunk + jsel];
-            uint32_t rm2 = R.rm2[nb * chunk + jsel];
+            int32_t e2 = RW[jsel].ev2[nb];
+            uint32_t rm2 = RW[jsel].rm2[nb];
             if (!dual) {  // commit everything, then evaluate the one row here
               commit_row();
               release_dec();
@@ -1140,8 +1175,8 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
               release_dec();
             }
             if (lane == 0) {
-              R.ev[nb * chunk + jsel] = e2;
-              R.rm1[nb * chunk + jsel] = rm2;
+              RW[jsel].ev[nb] = e2;
+              RW[jsel].rm1[nb] = rm2;
               // the same replacement in row wave wj's top masks (one row per row thread)
               if (NPT == 1 && mok) {
                 const int wj = 1 + jsel / 64;
@@ -1182,7 +1217,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
         int32_t acc = 0;
         for (int32_t j0 = 0; j0 < nrows; j0 += 64) {
           const int32_t j = j0 + lane;
-          const uint32_t rm = j < nrows ? R.rm1[pb * chunk + j] : 0u;
+          const uint32_t rm = j < nrows ? RW[j].rm1[pb] : 0u;
 #pragma unroll
           for (int r = 0; r < KSIM_NREASONS; ++r) {
             const int32_t n = __popcll(__ballot((rm >> r) & 1u));
@@ -1197,7 +1232,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       if (lane == 0) __hip_atomic_store(&s_dec, (int32_t)(pod - c.first + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       STAMP(4);
     }
-  } else {
+  } else if (active(wv)) {
   for (int64_t pod = c.first; pod < c.end; ++pod) {
     const bool has_next = pod + 1 < c.end;
     const int nb = (int)((pod + 1) & 1);  // LDS buffers of pod + 1
@@ -1267,9 +1302,9 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   __syncthreads();
   for (int32_t j = tid; j < nrows; j += BS) {
     const int64_t i = lo + j;
-    c.req_cpu[i] = R.rc[j]; c.req_mem[i] = R.rm[j];
-    c.nz_cpu[i] = R.zc[j]; c.nz_mem[i] = R.zm[j];
-    c.pod_count[i] = R.count[j]; c.flags[i] = R.fl[j];
+    c.req_cpu[i] = RW[j].rc; c.req_mem[i] = RW[j].rm;
+    c.nz_cpu[i] = RW[j].zc; c.nz_mem[i] = RW[j].zm;
+    c.pod_count[i] = RW[j].count; c.flags[i] = RW[j].fl;
   }
   if (blockIdx.x == 0 && tid == 0) {
     *c.counter = counter;
@@ -1315,6 +1350,10 @@ extern "C" int ksim_persistent_config(int64_t n, int* grid, int* lds_rows) {
   // tables the dual-hypothesis split covers in 64 workgroups (<= 192 rows each) take 64: one
   // workgroup per sweep lane (fewer granules per lane on the decision's critical path)
   if (g > 64 && n <= 64 * 192) g = 64;
+  if (const char* e = getenv("KSIM_PERSIST_GRID")) {  // diagnostic cap (grid A/B)
+    const int cap = atoi(e);
+    if (cap > 0 && cap < g) g = cap;
+  }
   if (g < 1) g = 1;
   const int64_t chunk = (n + g - 1) / g;
   if (chunk * LDS_ROW_BYTES > LDS_BUDGET || chunk > 4095 || chunk > 8 * 448) return 0;  // launch mode
@@ -1364,6 +1403,11 @@ static hipError_t launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint6
     L.off_nac = (int32_t)off; off += al(C * c->n_label_sets);
     L.off_ttv = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
     L.off_nav = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
+    const size_t sb = al(C * (size_t)lds_rows * 2);
+    if (off + sb <= lds_max && !getenv("KSIM_NO_STATIC_TABLE")) {
+      L.off_st = (int32_t)off;
+      off += sb;
+    }
   }
   hipLaunchKernelGGL((ksim_persistent_kernel<BS, NPT, MB>), dim3(grid), dim3(BS), off, s, *c, cdev, granules, L);
   return hipGetLastError();
