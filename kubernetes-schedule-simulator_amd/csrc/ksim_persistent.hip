@@ -350,6 +350,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
   // row waves with rows to evaluate (split: the ev waves from row thread 0, the ev2 waves from
   // `half`); the others sit the pod loop out — they would only add arrivals and LDS traffic
   auto active = [&](int w) -> bool {
+    if (w == 1) return true;  // refills the pod ring; publishes (empty) partials of a range with no rows
     const int r0 = (w - 1) * 64;
     if (!split) return r0 < nrows || NPT > 1;
     const int hf = 64 * ((nrows + 63) / 64);
