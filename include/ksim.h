@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 3
+#define KSIM_ABI_VERSION 4
 
 /* ---- status codes ---- */
 #define KSIM_OK 0
@@ -188,6 +188,12 @@ typedef struct {
   const int32_t* n_na;         /* [n_classes] number of NodeAffinity classes K2 (K1*K2 <= 16) */
   const int64_t* tt_val;       /* [n_classes][KSIM_MAX_RCLASS] map value of each class */
   const int64_t* na_val;       /* [n_classes][KSIM_MAX_RCLASS] */
+  /* Optional (NULL = none): a weighted constant added to the total of every node of NodeAffinity
+   * class b, [n_classes][KSIM_MAX_RCLASS] — NodePreferAvoidPodsPriority's map score x weight
+   * (node_prefer_avoid_pods.go:32-68), which is a function of (pod class, label set) like the
+   * NodeAffinity value.  When set, the NodeAffinity class dimension is used whatever
+   * NodeAffinityPriority's weight (n_na then counts (preferred weight, avoid score) pairs). */
+  const int64_t* na_add;
 } ksim_class_tables;
 
 /* Pod descriptor, 128 bytes.  The three request vectors follow the reference exactly:

@@ -59,7 +59,7 @@ int stage_pod(ksim_handle* h, const ksim_pod& pod, const uint64_t* ports, const 
   p.port_off = 0;
   p.scalar_off = 0;
   p.reserved[0] = h->ctx.w[KSIM_W_TAINT_TOLERATION] ? h->h_n_tt[p.cls] : 1;  // ksim_launch_pod_k
-  p.reserved[1] = h->ctx.w[KSIM_W_NODE_AFFINITY] ? h->h_n_na[p.cls] : 1;
+  p.reserved[1] = h->ctx.use_na ? h->h_n_na[p.cls] : 1;
   memcpy(hs + STG_POD, &p, sizeof p);
   const size_t pb = (size_t)pod.port_cnt * 8, sb = (size_t)pod.scalar_cnt * sizeof(ksim_scalar_req);
   if (pb) memcpy(hs + STG_PORTS, ports + pod.port_off, pb);

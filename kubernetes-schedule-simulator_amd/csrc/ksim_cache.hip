@@ -153,6 +153,6 @@ extern "C" hipError_t ksim_launch_port_max(const int32_t* port_count, int64_t n,
 extern "C" hipError_t ksim_launch_pod_k(ksim_pod* pods, int64_t n_pods, const KsimCtx* c, hipStream_t s) {
   if (n_pods <= 0) return hipSuccess;
   hipLaunchKernelGGL(ksim_pod_k_kernel, dim3(grid_for(n_pods)), dim3(256), 0, s, pods, n_pods, c->n_tt, c->n_na,
-                     c->w[KSIM_W_TAINT_TOLERATION] != 0 ? 1 : 0, c->w[KSIM_W_NODE_AFFINITY] != 0 ? 1 : 0);
+                     c->w[KSIM_W_TAINT_TOLERATION] != 0 ? 1 : 0, c->use_na);
   return hipGetLastError();
 }

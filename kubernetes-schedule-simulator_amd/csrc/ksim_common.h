@@ -87,6 +87,8 @@ struct KsimCtx {
   const int32_t* __restrict__ n_na;
   const int64_t* __restrict__ tt_val;
   const int64_t* __restrict__ na_val;
+  const int64_t* __restrict__ na_add;  // [C][KSIM_MAX_RCLASS] weighted per-NA-class addend, or null
+  int32_t use_na;                      // NA class dimension in use: NodeAffinity weight or na_add
   int32_t lwords, twords, n_label_sets, n_taint_sets;
   int32_t n_classes_dev;  // pod classes in the tables
   int32_t pad1;

@@ -111,7 +111,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   if (pod >= c.end) return;  // uniform: graph replay past the end of the queue
   const ksim_pod P = c.pods[pod];
   const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
-  const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
+  const int k2 = c.use_na ? c.n_na[P.cls] : 1;
   const int K = k1 * k2;
   const int64_t base = (int64_t)blockIdx.x * c.chunk;
   const IpaNorm ipa = ipa_norm(c, P);
@@ -274,6 +274,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
           const int64_t av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];
           t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(av, mxA, false);
         }
+        if (c.na_add) t += (uint64_t)c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];  // NodePreferAvoidPods
         tot[q] = (int64_t)t;
         if (tot[q] > best) best = tot[q];
       }
@@ -466,7 +467,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_
   if (i >= c.n) return;
   const ksim_pod P = c.pods[pod];
   const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
-  const int k2 = (c.w[KSIM_W_NODE_AFFINITY] != 0) ? c.n_na[P.cls] : 1;
+  const int k2 = c.use_na ? c.n_na[P.cls] : 1;
   const KsimRow r = ksim_load_row(c, i);
   const uint32_t m = ksim_predicates(c, P, i, r);
   fit[i] = m == 0;

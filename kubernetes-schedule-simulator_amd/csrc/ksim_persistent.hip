@@ -149,6 +149,7 @@ struct PLayout {
   int32_t tables;      // 1: sel_ok / taint_ok / noexec_ok / tt_class / na_class staged
   int32_t off_pc, off_pk, off_sel, off_tok, off_nok, off_ttc, off_nac;  // byte offsets in ksim_smem
   int32_t off_ttv, off_nav;  // [C][KSIM_MAX_RCLASS] reduce-class map values (int64)
+  int32_t off_nad;           // [C][KSIM_MAX_RCLASS] NodePreferAvoidPods addends (int64), staged when present
   // [C][rows] uint16 per (pod class, owned row), built at launch from the class tables: bit 0 the
   // selector does not match, bit 1 / 2 a NoSchedule+NoExecute / NoExecute taint is not
   // tolerated, bits 4-7 / 8-11 the TaintToleration / NodeAffinity reduce class — one LDS load
@@ -216,9 +217,9 @@ __device__ __noinline__ void commit_ports_lds(const KsimCtx* __restrict__ cg, co
 // Total score of reduce class q once the per-class maxima over the filtered set are known
 // (NormalizeReduce, priorities/reduce.go:29-64; weighted sum generic_scheduler.go:632-639).
 // tv / av: the class's TaintToleration / NodeAffinity map values (prefetched per pod).
-__device__ __forceinline__ int64_t class_total(const KsimCtx& c, int64_t tv, int64_t av, int64_t base, int64_t mxT,
-                                               int64_t mxA) {
-  uint64_t t = (uint64_t)base;
+__device__ __forceinline__ int64_t class_total(const KsimCtx& c, int64_t tv, int64_t av, int64_t ad, int64_t base,
+                                               int64_t mxT, int64_t mxA) {
+  uint64_t t = (uint64_t)base + (uint64_t)ad;  // ad: NodePreferAvoidPods' weighted score of the class
   if (c.w[KSIM_W_TAINT_TOLERATION]) t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(tv, mxT, true);
   if (c.w[KSIM_W_NODE_AFFINITY]) t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(av, mxA, false);
   return (int64_t)t;
@@ -387,6 +388,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     for (int32_t k = tid; k < C * KSIM_MAX_RCLASS; k += BS) {
       reinterpret_cast<int64_t*>(ksim_smem + L.off_ttv)[k] = c.tt_val[k];
       reinterpret_cast<int64_t*>(ksim_smem + L.off_nav)[k] = c.na_val[k];
+      if (c.na_add) reinterpret_cast<int64_t*>(ksim_smem + L.off_nad)[k] = c.na_add[k];
     }
   }
   if (L.off_st) {  // static per-(class, row) bits; the staged tables are read back after the barrier
@@ -824,12 +826,16 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       const int K = pod_K(P);
       const int k2 = P.reserved[1];
       // the reduce classes' map values (lane q = class q), loaded now, used after the sweep
-      int64_t tv_l = 0, av_l = 0;
+      int64_t tv_l = 0, av_l = 0, ad_l = 0;
       if (K > 1 && lane < K) {
         const int64_t* ttv = L.tables ? reinterpret_cast<const int64_t*>(ksim_smem + L.off_ttv) : c.tt_val;
         const int64_t* nav = L.tables ? reinterpret_cast<const int64_t*>(ksim_smem + L.off_nav) : c.na_val;
         tv_l = ttv[(int64_t)P.cls * KSIM_MAX_RCLASS + lane / k2];
         av_l = nav[(int64_t)P.cls * KSIM_MAX_RCLASS + lane % k2];
+        if (c.na_add) {
+          const int64_t* nad = L.tables ? reinterpret_cast<const int64_t*>(ksim_smem + L.off_nad) : c.na_add;
+          ad_l = nad[(int64_t)P.cls * KSIM_MAX_RCLASS + lane % k2];
+        }
       }
       // ---------------- a. sweep: every speculative partial of pod + the owner's correction ----
       const uint64_t tag = ptag(pod);
@@ -964,7 +970,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
             const int32_t cq = live ? cq_l : 0;
             const int64_t mq = live ? mq_l : 0;
             const int64_t mxT = wave_max_i64(live ? tv_l : 0), mxA = wave_max_i64(live ? av_l : 0);
-            const int64_t t = live ? class_total(c, tv_l, av_l, mq, mxT, mxA) : -1;  // totals are >= 0
+            const int64_t t = live ? class_total(c, tv_l, av_l, ad_l, mq, mxT, mxA) : -1;  // totals are >= 0
             const int64_t best = wave_max_i64(t);
             const uint64_t wbm = __ballot(live && t == best);
             win = (uint32_t)wbm;
@@ -1394,7 +1400,7 @@ static hipError_t launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint6
   // the pod-class tables, when they fit
   const size_t C = (size_t)c->n_classes_dev;
   const size_t tb = al(C * c->lwords * 4) + 2 * al(C * c->twords * 4) + al(C * c->n_taint_sets) + al(C * c->n_label_sets) +
-                    2 * al(C * KSIM_MAX_RCLASS * 8);
+                    3 * al(C * KSIM_MAX_RCLASS * 8);
   if (C > 0 && off + tb <= lds_max) {
     L.tables = 1;
     L.off_sel = (int32_t)off; off += al(C * c->lwords * 4);
@@ -1404,6 +1410,7 @@ static hipError_t launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint6
     L.off_nac = (int32_t)off; off += al(C * c->n_label_sets);
     L.off_ttv = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
     L.off_nav = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
+    L.off_nad = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
     const size_t sb = al(C * (size_t)lds_rows * 2);
     if (off + sb <= lds_max && !getenv("KSIM_NO_STATIC_TABLE")) {
       L.off_st = (int32_t)off;

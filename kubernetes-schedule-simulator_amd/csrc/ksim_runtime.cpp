@@ -181,7 +181,7 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
   uint32_t *so, *to, *no;
   uint8_t *tc, *nc;
   int32_t *ntt, *nna;
-  int64_t *tv, *nv;
+  int64_t *tv, *nv, *na = nullptr;
   std::vector<int32_t> ones(C, 1);
   const size_t nb0 = h->bufs.size();
   if ((rc = dev_upload(h, &so, t->sel_ok, C * lw)) || (rc = dev_upload(h, &to, t->taint_ok, C * tw)) ||
@@ -189,14 +189,16 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
       (rc = dev_upload(h, &nc, t->na_class, C * L)) ||
       (rc = dev_upload(h, &ntt, t->n_tt ? t->n_tt : ones.data(), C)) ||
       (rc = dev_upload(h, &nna, t->n_na ? t->n_na : ones.data(), C)) ||
-      (rc = dev_upload(h, &tv, t->tt_val, C * KSIM_MAX_RCLASS)) || (rc = dev_upload(h, &nv, t->na_val, C * KSIM_MAX_RCLASS)))
+      (rc = dev_upload(h, &tv, t->tt_val, C * KSIM_MAX_RCLASS)) || (rc = dev_upload(h, &nv, t->na_val, C * KSIM_MAX_RCLASS)) ||
+      (t->na_add && (rc = dev_upload(h, &na, t->na_add, C * KSIM_MAX_RCLASS))))
     return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   for (void* q : h->class_bufs) dev_free(h, q);  // the previous tables (reload)
   h->class_bufs.clear();
   for (size_t k = nb0; k < h->bufs.size(); ++k) h->class_bufs.push_back(h->bufs[k].p);
   c.sel_ok = so; c.taint_ok = to; c.noexec_ok = no; c.tt_class = tc; c.na_class = nc;
-  c.n_tt = ntt; c.n_na = nna; c.tt_val = tv; c.na_val = nv;
+  c.n_tt = ntt; c.n_na = nna; c.tt_val = tv; c.na_val = nv; c.na_add = na;
+  c.use_na = (c.w[KSIM_W_NODE_AFFINITY] != 0 || na) ? 1 : 0;
   c.lwords = (int32_t)lw; c.twords = (int32_t)tw;
   c.n_label_sets = (int32_t)L; c.n_taint_sets = (int32_t)T;
   c.n_classes_dev = t->n_classes;
@@ -278,7 +280,7 @@ static bool fast_base(const ksim_pod& p) {
 
 static bool fast_k(const ksim_handle* h, int32_t cls) {
   const int k1 = h->ctx.w[KSIM_W_TAINT_TOLERATION] ? h->h_n_tt[cls] : 1;
-  const int k2 = h->ctx.w[KSIM_W_NODE_AFFINITY] ? h->h_n_na[cls] : 1;
+  const int k2 = h->ctx.use_na ? h->h_n_na[cls] : 1;
   return k1 * k2 == 1;
 }
 

@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("KSIM_LIB") or os.path.join(PKG_DIR, "lib", "libksim.s
 
 KSIM_OK = 0
 E_INVAL, E_DEVICE, E_NOMEM, E_UNSUPPORTED, E_STATE, E_OVERFLOW, E_NO_NODES = -1, -2, -3, -4, -5, -6, -7
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_SCALAR = 8
 MAX_RCLASS = 16
 NREASONS = 28
@@ -80,7 +80,8 @@ class NodeTable(C.Structure):
 class ClassTables(C.Structure):
     _fields_ = [("n_classes", C.c_int32), ("n_label_sets", C.c_int32), ("n_taint_sets", C.c_int32),
                 ("sel_ok", _u32p), ("taint_ok", _u32p), ("noexec_ok", _u32p), ("tt_class", _u8p),
-                ("na_class", _u8p), ("n_tt", _i32p), ("n_na", _i32p), ("tt_val", _i64p), ("na_val", _i64p)]
+                ("na_class", _u8p), ("n_tt", _i32p), ("n_na", _i32p), ("tt_val", _i64p), ("na_val", _i64p),
+                ("na_add", _i64p)]
 
 
 class Pod(C.Structure):

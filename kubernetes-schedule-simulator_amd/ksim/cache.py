@@ -93,7 +93,8 @@ class SchedulerCache:
         self.tables, self.need, bad = ingest.build_class_tables(cl.label_sets.items, cl.taint_sets.items,
                                                                 cl.classes.items)
         cl.bad_affinity_classes = set(bad)
-        self.h.call("ksim_load_classes", C.byref(ingest.class_tables_struct(self.tables)))
+        tables, na_add = scheduler.class_tables_for(self.tables, self.prioritizers)
+        self.h.call("ksim_load_classes", C.byref(ingest.class_tables_struct(tables, na_add)))
         self._tables_for = key
 
     def _scalar_id(self, name):
@@ -132,9 +133,9 @@ class SchedulerCache:
     # ------------------------------------------------------------------ node rows
     def _node_row(self, name, info, ns):
         cl = self.cl
-        lid = cl.label_sets.get(_canon(ns.labels), dict(ns.labels))
+        lid = cl.label_sets.get(ingest.label_set_key(ns.labels, ns.prefer_avoid), ingest.LabelSet(ns.labels, ns.prefer_avoid))
         tid = cl.taint_sets.get(_canon(ns.taints), ns.taints)
-        cl.prefer_avoid_nodes |= ns.prefer_avoid
+        cl.prefer_avoid_nodes |= bool(ns.prefer_avoid)
         alloc_s = np.zeros(abi.MAX_SCALAR, np.int64)
         for k, v in ns.scalar.items():
             alloc_s[self._scalar_id(k)] = v

@@ -181,6 +181,117 @@ def _canon(x):
     return json.dumps(x, sort_keys=True, separators=(",", ":"))
 
 
+class LabelSet(dict):
+    """A node label set (a plain dict of labels for every label test) that also carries the
+    node's preferAvoidPods controller signatures: nodes with equal labels but different
+    annotations are different sets, so NodePreferAvoidPods is a function of (pod class, set)."""
+
+    def __init__(self, labels, avoid=()):
+        super().__init__(labels)
+        self.avoid = tuple(avoid)
+
+
+def label_set_key(labels, avoid):
+    """Interning key of a label set: the labels' canonical form, plus the avoided controller
+    signatures when there are any (so annotation-free sets keep their plain key)."""
+    k = _canon(labels)
+    return k if not avoid else k + "|avoid:" + _canon([list(e) if e is not None else None for e in avoid])
+
+
+def _go_field(obj, name):
+    """encoding/json's field lookup: the exact key, else a case-insensitive match; the last
+    matching key in document order wins (obj: list of (key, value) pairs)."""
+    found, val = False, None
+    for k, v in obj:
+        if k == name or k.lower() == name.lower():
+            found, val = True, v
+    return found, val
+
+
+class _JsonObj(list):
+    """A decoded JSON object as its ordered (key, value) pairs."""
+
+
+def avoid_signatures(annotations):
+    """v1helper.GetAvoidPodsFromNodeAnnotations (pkg/apis/core/v1/helper/helpers.go:338-347):
+    the preferAvoidPods entries' controller signatures (kind, uid) in order, or None for an entry
+    whose podSignature / podController is absent or null.  Any decoding error → no entries (the
+    priority then scores the node MaxPriority, node_prefer_avoid_pods.go:53-56); encoding/json
+    matches field names exactly or case-insensitively, and a type error anywhere fails the whole
+    decode.  evictionTime is only checked to be a string."""
+    raw = (annotations or {}).get(PREFER_AVOID_ANNOTATION) or ""
+    if not raw:
+        return ()
+    try:
+        doc = json.loads(raw, object_pairs_hook=_JsonObj)
+    except ValueError:
+        return ()
+    if not isinstance(doc, _JsonObj):
+        return ()
+    ok, lst = _go_field(doc, "preferAvoidPods")
+    if not ok or lst is None:
+        return ()
+    if not isinstance(lst, list) or isinstance(lst, _JsonObj):
+        return ()
+
+    def strings_ok(o, names):
+        return all((lambda v: v is None or isinstance(v, str))(_go_field(o, n)[1]) for n in names)
+
+    entries, err = [], False
+    for e in lst:
+        if e is None:
+            entries.append(None)
+            continue
+        if not isinstance(e, _JsonObj) or not strings_ok(e, ("reason", "message", "evictionTime")):
+            err = True
+            continue
+        ok, sig = _go_field(e, "podSignature")
+        if not ok or sig is None:
+            entries.append(None)
+            continue
+        if not isinstance(sig, _JsonObj):
+            err = True
+            continue
+        ok, ctl = _go_field(sig, "podController")
+        if not ok or ctl is None:
+            entries.append(None)
+            continue
+        if not isinstance(ctl, _JsonObj) or not strings_ok(ctl, ("kind", "uid", "name", "apiVersion")):
+            err = True
+            continue
+        if any(_go_field(ctl, n)[1] is not None and not isinstance(_go_field(ctl, n)[1], bool)
+               for n in ("controller", "blockOwnerDeletion")):
+            err = True
+            continue
+        entries.append((_go_field(ctl, "kind")[1] or "", _go_field(ctl, "uid")[1] or ""))
+    return () if err else tuple(entries)
+
+
+def avoid_score(entries, ctrl):
+    """CalculateNodePreferAvoidPodsPriorityMap's loop (node_prefer_avoid_pods.go:57-63) for a pod
+    whose RC / RS controllerRef is ctrl: 0 at the first entry with the same (kind, uid), else
+    MaxPriority.  The reference dereferences a nil podController before reaching later entries:
+    Unsupported."""
+    for e in entries:
+        if e is None:
+            raise Unsupported("preferAvoidPods entry without a podController (the reference dereferences nil)")
+        if e == tuple(ctrl):
+            return 0
+    return 10
+
+
+def avoid_controller(md):
+    """The pod's controllerRef as CalculateNodePreferAvoidPodsPriorityMap uses it
+    (node_prefer_avoid_pods.go:38-50, priorities/util/util.go:25-36): the first ownerReference with
+    controller=true, kept only for ReplicationController / ReplicaSet → (kind, uid), else None."""
+    for o in md.get("ownerReferences") or []:
+        if o.get("controller") is True:
+            if o.get("kind") in ("ReplicationController", "ReplicaSet"):
+                return (o.get("kind"), o.get("uid") or "")
+            return None
+    return None
+
+
 class Cluster:
     """Node table + pod queue in device layout.  Build with from_objects() or from arrays."""
 
@@ -260,9 +371,10 @@ class Cluster:
             for name, v in ns.scalar.items():
                 c["alloc_scalar"][self.scalar_names.ids[name], i] = v
             c["flags"][i] = ns.flags
-            c["label_set"][i] = self.label_sets.get(_canon(ns.labels), dict(ns.labels))
+            c["label_set"][i] = self.label_sets.get(label_set_key(ns.labels, ns.prefer_avoid),
+                                                    LabelSet(ns.labels, ns.prefer_avoid))
             c["taint_set"][i] = self.taint_sets.get(_canon(ns.taints), ns.taints)
-            self.prefer_avoid_nodes |= ns.prefer_avoid
+            self.prefer_avoid_nodes |= bool(ns.prefer_avoid)
             self.node_images |= bool((x.get("status") or {}).get("images"))
             node_taints.append(ns.taints)
         # running pods: NodeInfo.AddPod
@@ -331,10 +443,6 @@ class Cluster:
             raise Unsupported("pod %r: inter-pod affinity needs the cluster's affinity tables (ClusterCapacity / "
                               "GenericScheduler)" % _meta(p).get("name"))
         spec, md = _spec(p), _meta(p)
-        if self.prefer_avoid_nodes:
-            for o in md.get("ownerReferences") or []:
-                if o.get("controller") and o.get("kind") in ("ReplicationController", "ReplicaSet"):
-                    raise Unsupported("NodePreferAvoidPods with RC/RS-owned pods and preferAvoidPods annotations")
         row["req_cpu"], row["req_mem"], row["req_gpu"], row["req_eph"] = pred.cpu, pred.mem, pred.gpu, pred.eph
         row["add_cpu"], row["add_mem"], row["add_gpu"], row["add_eph"] = add.cpu, add.mem, add.gpu, add.eph
         row["nz_cpu"], row["nz_mem"] = nzc, nzm
@@ -346,7 +454,8 @@ class Cluster:
         nn = spec.get("nodeName") or ""
         idx = self.index if index is None else index
         row["host"] = -1 if not nn else idx.get(nn, -2)
-        row["cls"] = self.classes.get(pod_class_key(spec), spec)
+        ctrl = avoid_controller(md)
+        row["cls"] = self.classes.get(pod_class_key(spec, ctrl), spec if ctrl is None else dict(spec, __ctrl=ctrl))
         row["flags"] = flags
         hp = host_ports(p)
         row["port_off"], row["port_cnt"] = len(ports), len(hp)
@@ -404,8 +513,8 @@ class Cluster:
                 setattr(t, name, abi.ptr(a, ct))
         return t
 
-    def class_tables(self):
-        return class_tables_struct(self.tables)
+    def class_tables(self, na_add=None):
+        return class_tables_struct(self.tables, na_add)
 
     @property
     def n_nodes(self):
@@ -433,7 +542,7 @@ class NodeStatic:
     flags: int            # KSIM_N_* condition bits
     labels: dict
     taints: list
-    prefer_avoid: bool
+    prefer_avoid: tuple  # preferAvoidPods controller signatures (avoid_signatures)
     mem_pressure: object  # status of the last MemoryPressure condition (None: absent)
     disk_pressure: object
 
@@ -477,13 +586,17 @@ def node_static(x, prev_mem=None, prev_disk=None):
     taints = [{"key": t.get("key") or "", "value": t.get("value") or "", "effect": t.get("effect") or ""}
               for t in (sp.get("taints") or [])]
     return NodeStatic((r.cpu, r.mem, r.gpu, r.eph), r.pods, dict(r.scalar), f, dict(md.get("labels") or {}), taints,
-                      PREFER_AVOID_ANNOTATION in (md.get("annotations") or {}), mem, disk)
+                      avoid_signatures(md.get("annotations")), mem, disk)
 
 
-def pod_class_key(spec):
-    """Pods whose nodeSelector, node affinity and tolerations are equal share a class."""
-    return _canon({"ns": spec.get("nodeSelector") or {}, "na": (spec.get("affinity") or {}).get("nodeAffinity"),
-                   "tol": spec.get("tolerations") or []})
+def pod_class_key(spec, ctrl=None):
+    """Pods whose nodeSelector, node affinity and tolerations are equal share a class; an RC / RS
+    controllerRef (NodePreferAvoidPods' input) is part of the class when present."""
+    k = {"ns": spec.get("nodeSelector") or {}, "na": (spec.get("affinity") or {}).get("nodeAffinity"),
+         "tol": spec.get("tolerations") or []}
+    if ctrl is not None:
+        k["ctrl"] = list(ctrl)
+    return _canon(k)
 
 
 def build_class_tables(label_items, taint_items, specs):
@@ -505,14 +618,21 @@ def build_class_tables(label_items, taint_items, specs):
     nna = np.ones(Cn, np.int32)
     ttv = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
     nav = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
+    na_w = np.zeros((Cn, L), np.int64)   # preferred node-affinity weight per (class, label set)
+    na_p = np.full((Cn, L), 10, np.int64)  # NodePreferAvoidPods map score per (class, label set)
     need = np.zeros(Cn, np.uint32)
+    pa_split = False
     bad = set()
     for k, spec in enumerate(specs):
         tols = spec.get("tolerations") or []
         prefer_tols = [t for t in tols if (t.get("effect") or "") in ("", "PreferNoSchedule")]
         all_sel = all_taint = True
         weights = []
+        ctrl = spec.get("__ctrl")
+        pas = []
         for li, lab in enumerate(label_items):
+            # CalculateNodePreferAvoidPodsPriorityMap (node_prefer_avoid_pods.go:32-68)
+            pas.append(10 if ctrl is None else avoid_score(getattr(lab, "avoid", ()), ctrl))
             ok = labels.pod_matches_node_labels(spec, lab)
             if ok:
                 sel[k, li >> 5] |= np.uint32(1 << (li & 31))
@@ -545,6 +665,11 @@ def build_class_tables(label_items, taint_items, specs):
         nav[k, :len(av)] = av
         ttc[k, :] = [tv.index(x) for x in counts]
         nac[k, :] = [av.index(x) for x in weights]
+        # raw per-label-set inputs of the NodeAffinity class dimension, for a scheduler whose
+        # policy also weighs NodePreferAvoidPods (scheduler.class_tables_for re-keys the classes)
+        na_w[k, :] = weights
+        na_p[k, :] = pas
+        pa_split |= len(set(pas)) > 1
         f = 0
         if not all_sel:
             f |= abi.POD_NEED_SELECTOR
@@ -552,12 +677,14 @@ def build_class_tables(label_items, taint_items, specs):
             f |= abi.POD_NEED_TAINTS
         need[k] = f
     tables = dict(n_classes=Cn, n_label_sets=L, n_taint_sets=T, sel_ok=sel, taint_ok=tok, noexec_ok=nok,
-                  tt_class=ttc, na_class=nac, n_tt=ntt, n_na=nna, tt_val=ttv, na_val=nav)
+                  tt_class=ttc, na_class=nac, n_tt=ntt, n_na=nna, tt_val=ttv, na_val=nav, na_w=na_w, na_p=na_p,
+                  pa_split=pa_split)
     return tables, need, bad
 
 
-def class_tables_struct(d):
-    """ksim_class_tables over the arrays of a tables dict (kept alive by the dict)."""
+def class_tables_struct(d, na_add=None):
+    """ksim_class_tables over the arrays of a tables dict (kept alive by the dict); na_add: the
+    weighted NodePreferAvoidPods addends per NodeAffinity class (scheduler.prefer_avoid_add)."""
     t = abi.ClassTables()
     t.n_classes, t.n_label_sets, t.n_taint_sets = d["n_classes"], d["n_label_sets"], d["n_taint_sets"]
     for name, ct in (("sel_ok", abi.C.c_uint32), ("taint_ok", abi.C.c_uint32), ("noexec_ok", abi.C.c_uint32),
@@ -565,6 +692,9 @@ def class_tables_struct(d):
                      ("n_na", abi.C.c_int32), ("tt_val", abi.C.c_int64), ("na_val", abi.C.c_int64)):
         d[name] = np.ascontiguousarray(d[name])
         setattr(t, name, abi.ptr(d[name], ct))
+    if na_add is not None:
+        d["na_add"] = np.ascontiguousarray(na_add, np.int64)
+        t.na_add = abi.ptr(d["na_add"], abi.C.c_int64)
     return t
 
 

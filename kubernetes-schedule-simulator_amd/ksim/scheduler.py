@@ -21,7 +21,7 @@ from dataclasses import dataclass, field
 import numpy as np
 
 from . import abi
-from .ingest import Cluster, Unsupported
+from .ingest import Cluster, Unsupported, class_tables_struct
 
 # predicates.go:129-138 keys → kernel bits
 PREDICATE_BITS = {
@@ -153,6 +153,41 @@ def fit_error_message(num_nodes, hist, scalar_names=()):
     return "0/%d nodes are available: %s." % (num_nodes, ", ".join(parts))
 
 
+def class_tables_for(tables, priorities):
+    """The class tables a scheduler with these priorities loads, and NodePreferAvoidPods' weighted
+    per-NodeAffinity-class addends (ksim_class_tables.na_add) or None.
+
+    NodePreferAvoidPodsPriority (node_prefer_avoid_pods.go:32-68) is a function of (pod class,
+    label set) — the label set carries the node's preferAvoidPods annotation — so when the policy
+    weighs it and some pod class sees nodes that differ in it (an RC / RS controller a node's
+    annotation names), the NodeAffinity class dimension is re-keyed by (preferred weight, avoid
+    score) — by the avoid score alone if NodeAffinityPriority is not configured — and each class
+    adds its weighted score.  Otherwise it is the constant MaxPriority x weight of const_score."""
+    w_pa = sum(int(x) for n, x in priorities if n == "NodePreferAvoidPodsPriority")
+    if not w_pa or not tables.get("pa_split"):
+        return tables, None
+    use_w = any(n == "NodeAffinityPriority" for n, _ in priorities)
+    d = dict(tables)
+    Cn = d["n_classes"]
+    nac = np.zeros_like(tables["na_class"])
+    nna = np.ones(Cn, np.int32)
+    nav = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
+    add = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
+    for k in range(Cn):
+        keys = list(zip((int(x) if use_w else 0 for x in tables["na_w"][k]), (int(x) for x in tables["na_p"][k])))
+        av = sorted(set(keys))
+        if int(tables["n_tt"][k]) * len(av) > abi.MAX_RCLASS:
+            raise Unsupported("pod class needs %d x %d reduce classes (> %d)" % (int(tables["n_tt"][k]), len(av),
+                                                                                abi.MAX_RCLASS))
+        nna[k] = len(av)
+        nav[k, :len(av)] = [w for w, _ in av]
+        add[k, :len(av)] = [p * w_pa for _, p in av]
+        pos = {x: i for i, x in enumerate(av)}
+        nac[k, :] = [pos[x] for x in keys]
+    d.update(na_class=nac, n_na=nna, na_val=nav)
+    return d, add
+
+
 def label_presence_flags(label_sets, label_set_ids, label_presence):
     """KSIM_N_LABEL_PRESENCE per node: CheckNodeLabelPresence (predicates.go:875-910) fails when
     a listed label's presence differs from `presence`; a function of the node's label set."""
@@ -186,7 +221,12 @@ class GenericScheduler:
             self._flags = np.ascontiguousarray(fl, np.uint32)
             table.flags = abi.ptr(self._flags, C.c_uint32)
         self.h.call("ksim_load_nodes", C.byref(table))
-        self.h.call("ksim_load_classes", C.byref(cluster.class_tables()))
+        self.tables, self.na_add = class_tables_for(cluster.tables, self.prioritizers)
+        # const_score without NodePreferAvoidPods when its per-class addends carry it
+        self.const_score = self.cfg.const_score - (10 * sum(int(x) for n, x in self.prioritizers
+                                                            if n == "NodePreferAvoidPodsPriority")
+                                                   if self.na_add is not None else 0)
+        self.h.call("ksim_load_classes", C.byref(class_tables_struct(self.tables, self.na_add)))
         pods = np.ascontiguousarray(cluster.pods)
         self.affinity = None
         if cluster.affinity is not None:
@@ -252,9 +292,10 @@ class GenericScheduler:
         fit, _, sc, rc = self.evaluate(pod)
         idx = np.nonzero(fit)[0] if over is None else np.asarray(over)
         p = self.cluster.pods[pod]
-        t = self.cluster.tables
+        t = self.tables
         cls = int(p["cls"])
-        k2 = int(t["n_na"][cls]) if self.cfg.weights[abi.W_NODE_AFF] else 1
+        use_na = bool(self.cfg.weights[abi.W_NODE_AFF]) or self.na_add is not None
+        k2 = int(t["n_na"][cls]) if use_na else 1
         tv = t["tt_val"][cls][rc[idx] // k2]
         av = t["na_val"][cls][rc[idx] % k2]
         total = sc[idx].copy()
@@ -262,7 +303,9 @@ class GenericScheduler:
             total += self.cfg.weights[abi.W_TAINT_TOL] * _normalize(tv, True)
         if self.cfg.weights[abi.W_NODE_AFF]:
             total += self.cfg.weights[abi.W_NODE_AFF] * _normalize(av, False)
-        return idx, total + self.cfg.const_score
+        if self.na_add is not None:
+            total += self.na_add[cls][rc[idx] % k2]
+        return idx, total + self.const_score
 
     def node_state(self):
         n = self.cluster.n_nodes

@@ -247,6 +247,10 @@ int ksim_ref_run(const ksim_config* cfg, const ksim_node_table* tab, ksim_node_s
         if (cfg->no_priorities) t = 0;
         if (wt) t += (uint64_t)wt * (uint64_t)normalize(ttv[i], mxT, 1);
         if (wa) t += (uint64_t)wa * (uint64_t)normalize(nav[i], mxA, 0);
+        /* NodePreferAvoidPods (node_prefer_avoid_pods.go:32-68): its weighted map score rides the
+           node's NodeAffinity class (ksim_class_tables.na_add) */
+        if (ct->na_add)
+          t += (uint64_t)ct->na_add[cls * KSIM_MAX_RCLASS + ct->na_class[cls * ct->n_label_sets + N.label_set[i]]];
         score[i] = (int64_t)t;
         if (score[i] > M) M = score[i];
       }

@@ -21,9 +21,11 @@ def lib():
     return _lib
 
 
-def run(cluster, cfg, first=0, count=None, threads=1, state=None, counter=0):
+def run(cluster, cfg, first=0, count=None, threads=1, state=None, counter=0, tables=None, na_add=None):
     """Schedule cluster pods [first, first+count) on the CPU.  `state` (dict of dynamic
     columns, updated in place) defaults to a fresh copy of the cluster's initial state.
+    tables / na_add: a scheduler's class tables and NodePreferAvoidPods addends
+    (scheduler.class_tables_for), default the cluster's own tables.
     Returns (out_node, reasons, state, counter)."""
     from ksim import abi  # ABI struct layouts (include/ksim.h)
 
@@ -41,7 +43,8 @@ def run(cluster, cfg, first=0, count=None, threads=1, state=None, counter=0):
                   ("ports", C.c_uint64), ("port_count", C.c_int32)):
         setattr(st, k, abi.ptr(state[k], ct))
     tab = cluster.node_table()
-    ct = cluster.class_tables()
+    from ksim.ingest import class_tables_struct
+    ct = class_tables_struct(cluster.tables if tables is None else tables, na_add)
     out = np.zeros(count, np.int32)
     reasons = np.zeros((count, abi.NREASONS), np.int32)
     ctr = C.c_uint64(counter)

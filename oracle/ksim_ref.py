@@ -1078,11 +1078,105 @@ def _prio_zero(pod, ni):
     return 0
 
 
+PREFER_AVOID_KEY = "scheduler.alpha.kubernetes.io/preferAvoidPods"  # core/v1 annotation_key_constants.go
+
+
+class _GoDecodeError(Exception):
+    pass
+
+
+def _go_obj(v):
+    """encoding/json into a struct: a JSON object (kept as ordered pairs) or null."""
+    if v is None or (isinstance(v, tuple) and v[0] == "obj"):
+        return v
+    raise _GoDecodeError("not an object")
+
+
+def _go_get(o, name):
+    """Field lookup of encoding/json: exact or case-insensitive key, later keys overwrite."""
+    hit = None
+    for k, v in o[1]:
+        if k.lower() == name.lower():
+            hit = (v,)
+    return hit
+
+
+def _go_str(o, name):
+    h = _go_get(o, name)
+    if h is None or h[0] is None:
+        return ""
+    if not isinstance(h[0], str):
+        raise _GoDecodeError("not a string")
+    return h[0]
+
+
+def get_avoid_pods(annotations):
+    """v1helper.GetAvoidPodsFromNodeAnnotations (pkg/apis/core/v1/helper/helpers.go:338-347):
+    v1.AvoidPods from the node's annotation, or an error.  Entries are (kind, uid) of
+    podSignature.podController, or None where that pointer stays nil (types.go AvoidPods /
+    PreferAvoidPodsEntry / PodSignature)."""
+    import json
+    raw = (annotations or {}).get(PREFER_AVOID_KEY, "")
+    if raw == "":
+        return [], None
+    try:
+        doc = json.loads(raw, object_pairs_hook=lambda pairs: ("obj", pairs))
+        top = _go_obj(doc)
+        if top is None:
+            return [], None
+        h = _go_get(top, "preferAvoidPods")
+        lst = None if h is None else h[0]
+        if lst is None:
+            return [], None
+        if not isinstance(lst, list):
+            raise _GoDecodeError("not an array")
+        out = []
+        for e in lst:
+            e = _go_obj(e)
+            ctl = None
+            if e is not None:
+                for f in ("reason", "message", "evictionTime"):
+                    _go_str(e, f)
+                hs = _go_get(e, "podSignature")
+                sig = _go_obj(hs[0]) if hs is not None else None
+                if sig is not None:
+                    hc = _go_get(sig, "podController")
+                    ctl = _go_obj(hc[0]) if hc is not None else None
+            if ctl is None:
+                out.append(None)
+                continue
+            for f in ("name", "apiVersion"):
+                _go_str(ctl, f)
+            for f in ("controller", "blockOwnerDeletion"):
+                hb = _go_get(ctl, f)
+                if hb is not None and hb[0] is not None and not isinstance(hb[0], bool):
+                    raise _GoDecodeError("not a bool")
+            out.append((_go_str(ctl, "kind"), _go_str(ctl, "uid")))
+        return out, None
+    except (ValueError, _GoDecodeError) as err:
+        return [], err
+
+
 def _prio_prefer_avoid(pod, ni):
-    """node_prefer_avoid_pods.go:32-68: pods without an RC/RS controllerRef → 10."""
+    """CalculateNodePreferAvoidPodsPriorityMap (node_prefer_avoid_pods.go:32-68): the controllerRef
+    (priorities/util/util.go:25-36, first ownerReference with controller=true) counts only for a
+    ReplicationController / ReplicaSet; the node scores 0 when an annotation entry names the same
+    (kind, uid), else MaxPriority (also when the annotation does not decode)."""
+    ref = None
     for o in ((pod.get("metadata") or {}).get("ownerReferences") or []):
-        if o.get("controller") and o.get("kind") in ("ReplicationController", "ReplicaSet"):
-            raise NotImplementedError("NodePreferAvoidPods with controller refs")
+        if o.get("controller") is True:
+            ref = o
+            break
+    if ref is None or ref.get("kind") not in ("ReplicationController", "ReplicaSet"):
+        return MAX_PRIORITY
+    avoids, err = get_avoid_pods((_meta(ni.node).get("annotations") or {}))
+    if err is not None:
+        return MAX_PRIORITY
+    for sig in avoids:
+        if sig is None:
+            raise NotImplementedError("nil podController: the reference panics")
+        if sig == (ref.get("kind"), ref.get("uid") or ""):
+            return 0
     return MAX_PRIORITY
 
 

@@ -257,6 +257,50 @@ prio_case(NAsrc + ":169", "NodeAffinityPriority",
           pod(affinity=aff2), [node("machine1", labels=L1), node("machine5", labels=L5), node("machine2", labels=L2)],
           [["machine1", 1], ["machine5", 10], ["machine2", 3]])
 
+# ------------------------------------------------ NodePreferAvoidPods
+PAsrc = S + "algorithm/priorities/node_prefer_avoid_pods_test.go"
+PA_KEY = "scheduler.alpha.kubernetes.io/preferAvoidPods"   # v1.PreferAvoidPodsAnnotationKey
+
+
+def pa_annotation(kind, uid):   # node_prefer_avoid_pods_test.go:31-70 (whitespace dropped)
+    return {PA_KEY: json.dumps({"preferAvoidPods": [{
+        "podSignature": {"podController": {"apiVersion": "v1", "kind": kind, "name": "foo", "uid": uid,
+                                           "controller": True}},
+        "reason": "some reason", "message": "some message"}]})}
+
+
+def pa_node(name, ann=None):
+    n = node(name)
+    if ann:
+        n["metadata"]["annotations"] = ann
+    return n
+
+
+def owned(kind, uid, controller=True):
+    p = pod()
+    ref = {"kind": kind, "name": "foo", "uid": uid}
+    if controller:
+        ref["controller"] = True
+    p["metadata"]["namespace"] = "default"
+    p["metadata"]["ownerReferences"] = [ref]
+    return p
+
+
+PA_NODES = [pa_node("machine1", pa_annotation("ReplicationController", "abcdef123456")),
+            pa_node("machine2", pa_annotation("ReplicaSet", "qwert12345")), pa_node("machine3")]
+prio_case(PAsrc + ":89", "NodePreferAvoidPodsPriority",
+          "pod managed by ReplicationController should avoid a node, this node get lowest priority score",
+          owned("ReplicationController", "abcdef123456"), PA_NODES, [["machine1", 0], ["machine2", 10], ["machine3", 10]])
+prio_case(PAsrc + ":102", "NodePreferAvoidPodsPriority", "ownership by random controller should be ignored",
+          owned("RandomController", "abcdef123456"), PA_NODES, [["machine1", 10], ["machine2", 10], ["machine3", 10]])
+prio_case(PAsrc + ":115", "NodePreferAvoidPodsPriority", "owner without Controller field set should be ignored",
+          owned("ReplicationController", "abcdef123456", controller=False), PA_NODES,
+          [["machine1", 10], ["machine2", 10], ["machine3", 10]])
+prio_case(PAsrc + ":128", "NodePreferAvoidPodsPriority",
+          "pod managed by ReplicaSet should avoid a node, this node get lowest priority score",
+          owned("ReplicaSet", "qwert12345"), PA_NODES, [["machine1", 10], ["machine2", 0], ["machine3", 10]])
+
+
 # ------------------------------------------------ PodFitsResources
 PFsrc = S + "algorithm/predicates/predicates_test.go"
 EXT_A, EXT_B, HUGE_A = "example.com/aaa", "example.com/bbb", "hugepages-2Mi"

@@ -9,7 +9,7 @@ import pytest
 import ksim_ref as R
 from golden_util import case_id, load
 from ksim import abi, ingest, scheduler
-from workloads import rnd_workload
+from workloads import add_prefer_avoid, rnd_workload
 
 pytestmark = pytest.mark.gpu
 
@@ -29,14 +29,14 @@ def test_golden_priorities_on_gpu(c):
     assert [[h, got[h]] for h, _ in c["expect"]] == c["expect"]
 
 
-REDUCE_PRIORITIES = ("TaintTolerationPriority", "NodeAffinityPriority")
+REDUCE_PRIORITIES = ("TaintTolerationPriority", "NodeAffinityPriority", "NodePreferAvoidPodsPriority")
 
 
 @pytest.mark.parametrize("mode", [abi.MODE_LAUNCH, abi.MODE_PERSISTENT])
 @pytest.mark.parametrize("c", [c for c in load("priorities") if c["priority"] in REDUCE_PRIORITIES], ids=case_id)
 def test_golden_reduce_priorities_select_on_gpu(c, mode):
-    """The reference's TaintToleration / NodeAffinity golden vectors through the scheduling
-    kernels' own NormalizeReduce (reduce classes, per-class maxima, class totals — not the host
+    """The reference's TaintToleration / NodeAffinity / NodePreferAvoidPods golden vectors through
+    the scheduling kernels' own reduce classes (per-class maxima, class totals — not the host
     numpy path priority_scores uses): with lastNodeIndex = k, the pod must land on the k-th host
     of the golden maximum in descending bytewise name order (selectHost,
     generic_scheduler.go:183-198), for every k over two periods."""
@@ -110,6 +110,33 @@ def test_simulation_matches_oracle(seed, policy, mode):
     got, rep = _gpu_run(nodes, running, pods, preds, prios, mode)
     order = [name for name, _, _ in want]
     assert [n for n, _ in rep.successful] == [n for n, h, _ in want if h is not None]  # bind order
+    for name, host, msg in want:
+        assert got[name] == (host, msg), name
+    assert rep.last_node_index == want_lni
+
+
+PA_POLICIES = {
+    "default": scheduler.provider("DefaultProvider"),
+    "pa_only": (["GeneralPredicates"], [("NodePreferAvoidPodsPriority", 3)]),
+    "pa_affinity": (["GeneralPredicates", "PodToleratesNodeTaints"],
+                    [("NodePreferAvoidPodsPriority", 2), ("NodeAffinityPriority", 3), ("TaintTolerationPriority", 1),
+                     ("LeastRequestedPriority", 1)]),
+}
+
+
+@pytest.mark.parametrize("mode", [abi.MODE_LAUNCH, abi.MODE_PERSISTENT, abi.MODE_AUTO])
+@pytest.mark.parametrize("policy", sorted(PA_POLICIES))
+@pytest.mark.parametrize("seed", range(3))
+def test_prefer_avoid_matches_oracle(seed, policy, mode):
+    """NodePreferAvoidPods with RC / RS-owned pods and preferAvoidPods node annotations (its
+    weighted score rides the kernels' NodeAffinity reduce classes, ksim_class_tables.na_add)
+    against the object oracle's CalculateNodePreferAvoidPodsPriorityMap."""
+    nodes, running, pods = rnd_workload(300 + seed, n_nodes=21 + seed * 11, n_pods=140)
+    nodes, pods = add_prefer_avoid(seed, nodes, pods)
+    preds, prios = PA_POLICIES[policy]
+    want, want_lni = _oracle_run(nodes, running, pods, preds, prios)
+    got, rep = _gpu_run(nodes, running, pods, preds, prios, mode)
+    assert [n for n, _ in rep.successful] == [n for n, h, _ in want if h is not None]
     for name, host, msg in want:
         assert got[name] == (host, msg), name
     assert rep.last_node_index == want_lni

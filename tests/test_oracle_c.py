@@ -9,7 +9,7 @@ import pytest
 import cpu_ref
 import ksim_ref as R
 from ksim import ingest, scheduler, synth
-from workloads import rnd_workload
+from workloads import add_prefer_avoid, rnd_workload
 
 POLICIES = {
     "default": scheduler.provider("DefaultProvider"),
@@ -26,7 +26,9 @@ POLICIES = {
 def c_oracle(nodes, running, pods, preds, prios, threads=2):
     """The simulator's loop on the C oracle: pods popped LIFO (store.go:223-233)."""
     cl = ingest.Cluster.from_objects(nodes, running, list(reversed(pods)))
-    out, reasons, _, ctr = cpu_ref.run(cl, scheduler.make_config(preds, prios), threads=threads)
+    tables, na_add = scheduler.class_tables_for(cl.tables, prios)
+    out, reasons, _, ctr = cpu_ref.run(cl, scheduler.make_config(preds, prios), threads=threads, tables=tables,
+                                       na_add=na_add)
     res = []
     for k, w in enumerate(out):
         if w >= 0:
@@ -42,6 +44,30 @@ def c_oracle(nodes, running, pods, preds, prios, threads=2):
 def test_c_oracle_matches_object_oracle(seed, policy):
     nodes, running, pods = rnd_workload(100 + seed, n_nodes=19 + seed * 13, n_pods=160)
     preds, prios = POLICIES[policy]
+    want, want_lni = R.simulate(nodes, running, pods, set(preds), list(prios))
+    got, ctr = c_oracle(nodes, running, pods, preds, prios)
+    assert got == want
+    assert ctr == want_lni
+
+
+PA_POLICIES = {
+    "default": scheduler.provider("DefaultProvider"),
+    "pa_only": (["GeneralPredicates"], [("NodePreferAvoidPodsPriority", 3)]),
+    "pa_affinity": (["GeneralPredicates", "PodToleratesNodeTaints"],
+                    [("NodePreferAvoidPodsPriority", 2), ("NodeAffinityPriority", 3), ("TaintTolerationPriority", 1),
+                     ("LeastRequestedPriority", 1)]),
+}
+
+
+@pytest.mark.parametrize("policy", sorted(PA_POLICIES))
+@pytest.mark.parametrize("seed", range(4))
+def test_c_oracle_matches_object_oracle_prefer_avoid(seed, policy):
+    """NodePreferAvoidPods with RC / RS-owned pods and preferAvoidPods annotations (case-varied
+    field names, malformed JSON): the table-level oracle's per-class addends against the object
+    oracle's CalculateNodePreferAvoidPodsPriorityMap."""
+    nodes, running, pods = rnd_workload(300 + seed, n_nodes=21 + seed * 11, n_pods=140)
+    nodes, pods = add_prefer_avoid(seed, nodes, pods)
+    preds, prios = PA_POLICIES[policy]
     want, want_lni = R.simulate(nodes, running, pods, set(preds), list(prios))
     got, ctr = c_oracle(nodes, running, pods, preds, prios)
     assert got == want

@@ -96,6 +96,43 @@ def rnd_workload(seed, n_nodes=24, n_pods=120, n_running=10, features=True):
     return nodes, running, pods
 
 
+PREFER_AVOID = "scheduler.alpha.kubernetes.io/preferAvoidPods"
+CONTROLLERS = [("ReplicationController", "rc-uid-1"), ("ReplicationController", "rc-uid-2"),
+               ("ReplicaSet", "rs-uid-1"), ("ReplicaSet", "rs-uid-2"), ("StatefulSet", "ss-uid-1")]
+
+
+def add_prefer_avoid(seed, nodes, pods):
+    """NodePreferAvoidPods inputs on a workload (own stream, the base workload unchanged): ~35 %
+    of nodes carry a preferAvoidPods annotation naming one or two controllers (some with a
+    case-varied field name, a few malformed), ~50 % of pods an ownerReference (controller or not,
+    RC / RS / other kinds) — those pods drop preferred node-affinity terms, so a pod class never
+    needs more than the kernels' 16 reduce classes."""
+    import json
+    rng = random.Random(seed * 7919 + 13)
+    for x in nodes:
+        r = rng.random()
+        if r < 0.35:
+            ents = [{"podSignature": {"podController": {"apiVersion": "v1", "kind": k, "name": "c", "uid": u,
+                                                        "controller": True}}, "reason": "r"}
+                    for k, u in rng.sample(CONTROLLERS, rng.choice([1, 1, 2]))]
+            doc = {"preferAvoidPods": ents} if rng.random() < 0.8 else {"PreferAvoidPods": ents}
+            x["metadata"].setdefault("annotations", {})[PREFER_AVOID] = json.dumps(doc)
+        elif r < 0.38:
+            x["metadata"].setdefault("annotations", {})[PREFER_AVOID] = "{not json"
+    for p in pods:
+        if rng.random() < 0.5:
+            k, u = rng.choice(CONTROLLERS)
+            ref = {"kind": k, "name": "c", "uid": u}
+            if rng.random() < 0.85:
+                ref["controller"] = True
+            p["metadata"]["ownerReferences"] = [ref]
+            # (TaintToleration x NodeAffinity weight x avoid) classes must stay <= 16 per pod class:
+            # an owned pod keeps its required node affinity, not its preferred terms
+            na = ((p["spec"].get("affinity") or {}).get("nodeAffinity") or {})
+            na.pop("preferredDuringSchedulingIgnoredDuringExecution", None)
+    return nodes, pods
+
+
 # ----------------------------------------------------------------------------- inter-pod affinity
 AFF_KEYS = ["kubernetes.io/hostname", "zone", "region", "rack"]
 APPS = ["web", "db", "cache", "batch"]
