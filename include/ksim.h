@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 4
+#define KSIM_ABI_VERSION 5
 
 /* ---- status codes ---- */
 #define KSIM_OK 0
@@ -34,19 +34,18 @@ extern "C" {
 #define KSIM_E_NOMEM (-3)       /* device allocation failed */
 #define KSIM_E_UNSUPPORTED (-4) /* configuration outside the supported key set */
 #define KSIM_E_STATE (-5)       /* call order (e.g. schedule before load) */
-#define KSIM_E_OVERFLOW (-6)    /* a node's host-port slots overflowed on commit */
+#define KSIM_E_OVERFLOW (-6)    /* a node's host-port or volume slots overflowed on commit */
 #define KSIM_E_NO_NODES (-7)    /* core.ErrNoNodesAvailable (generic_scheduler.go:64,124-125) */
 
 #define KSIM_MAX_SCALAR 8   /* extended / hugepage resource columns */
 #define KSIM_MAX_RCLASS 16  /* reduce classes per pod (TaintToleration x NodeAffinity) */
-#define KSIM_NREASONS 28    /* failure-reason histogram slots */
+#define KSIM_NREASONS 31    /* failure-reason histogram slots */
 #define KSIM_MAX_RANKS 8    /* devices of one node-sharded cluster */
 
 /* ---- predicate key bits: the FitPredicate keys of predicates.go:129-138 that carry
- *      logic for supported pods.  The volume keys (NoDiskConflict, MaxEBS/GCEPD/
- *      AzureDiskVolumeCount, CheckVolumeBinding, NoVolumeZoneConflict) are true for pods
- *      without volumes and need no bit: the host rejects pods that would make them
- *      non-trivial. ---- */
+ *      logic for supported pods.  The volume keys read the tables of ksim_load_volumes and are
+ *      true for pods without a volume class.  CheckVolumeBinding needs no bit: it is true for
+ *      every pod the host accepts (no PVC, or PVCs bound to PVs without node affinity). ---- */
 #define KSIM_P_CHECK_NODE_CONDITION (1u << 0)     /* predicates.go:1534 */
 #define KSIM_P_CHECK_NODE_UNSCHEDULABLE (1u << 1) /* CheckNodeUnschedulablePredicate */
 #define KSIM_P_GENERAL (1u << 2)                  /* predicates.go:1059 */
@@ -63,6 +62,12 @@ extern "C" {
                                                      verdict is the KSIM_N_LABEL_PRESENCE bit */
 #define KSIM_P_INTERPOD_AFFINITY (1u << 12)       /* MatchInterPodAffinity (predicates.go:1143-1450),
                                                      over the tables of ksim_load_affinity */
+#define KSIM_P_DISK_CONFLICT (1u << 13)           /* NoDiskConflict (predicates.go:220-285) */
+#define KSIM_P_MAX_EBS (1u << 14)                 /* MaxEBSVolumeCount (predicates.go:313-456) */
+#define KSIM_P_MAX_GCE_PD (1u << 15)              /* MaxGCEPDVolumeCount */
+#define KSIM_P_MAX_AZURE_DISK (1u << 16)          /* MaxAzureDiskVolumeCount */
+#define KSIM_P_VOLUME_ZONE (1u << 17)             /* NoVolumeZoneConflict (predicates.go:539-633), as the
+                                                     per (volume class, label set) verdict zone_ok */
 
 /* ---- priority weight slots (0 = not configured).  Priorities that evaluate to the
  *      same value on every node under supported inputs (SelectorSpread /
@@ -119,6 +124,9 @@ extern "C" {
 #define KSIM_R_EXISTING_ANTI_AFFINITY 25  /* node(s) didn't satisfy existing pods anti-affinity rules */
 #define KSIM_R_AFFINITY_RULES 26          /* node(s) didn't match pod affinity rules */
 #define KSIM_R_ANTI_AFFINITY_RULES 27     /* node(s) didn't match pod anti-affinity rules */
+#define KSIM_R_DISK_CONFLICT 28           /* node(s) had no available disk (ErrDiskConflict) */
+#define KSIM_R_MAX_VOLUME_COUNT 29        /* node(s) exceed max volume count (ErrMaxVolumeCountExceeded) */
+#define KSIM_R_VOLUME_ZONE 30             /* node(s) had no available volume zone (ErrVolumeZoneConflict) */
 
 /* ---- execution modes ---- */
 #define KSIM_MODE_AUTO 0        /* library picks (persistent when it fits) */
@@ -213,7 +221,8 @@ typedef struct {
   int32_t scalar_cnt;
   int32_t aff_ident;   /* 1 + identity in the affinity tables (ksim_load_affinity); 0: none */
   int32_t aff_class;   /* 1 + affinity class (own and carried terms); 0: none */
-  int32_t reserved[3]; /* library-owned scratch (callers pass anything; never read back) */
+  int32_t vol_class;   /* 1 + volume class in the tables of ksim_load_volumes; 0: no relevant volume */
+  int32_t reserved[2]; /* library-owned scratch (callers pass anything; never read back) */
 } ksim_pod;
 
 typedef struct {
@@ -455,6 +464,67 @@ typedef struct {
 
 /* Load (or replace) the affinity tables; the counts describe the pods already placed. */
 int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t);
+
+/* ==== Volumes (NoDiskConflict, MaxEBS / GCEPD / AzureDiskVolumeCount, NoVolumeZoneConflict) ====
+ * Reference: algorithm/predicates/predicates.go:220-285 (isVolumeConflict, NoDiskConflict),
+ * :313-507 (MaxPDVolumeCountChecker, the EBS / GCE PD / Azure Disk filters), :539-633
+ * (VolumeZoneChecker).  The host interns every volume identity into a key (ksim/volumes.py):
+ *  - GCE PD by PDName, AWS EBS by VolumeID, Azure Disk by DiskName, ISCSI by IQN, RBD once per
+ *    Ceph monitor as (monitor, pool, image) — isVolumeConflict's haveOverlap becomes "some key
+ *    of the volume is mounted" — and a PVC the PV / PVC listers cannot resolve as
+ *    "<namespace>/<claim>" (counted by every MaxPD filter, :376-403).  A PVC bound to a known PV
+ *    is the PV's GCE PD / EBS / Azure Disk key, or nothing;
+ *  - key_filter[k]: the MaxPD filters (KSIM_VOL_EBS / _GCE_PD / _AZURE_DISK) that count key k;
+ *  - volume classes (pods with identical volume lists): refs[vc[c][0] .. + vc[c][1]] with the
+ *    flags below, vc_filter[c] = the filters with a relevant volume in the pod (MaxPD's
+ *    len(newVolumes) == 0 quick return, :427-430);
+ *  - node state: per node the mounted keys with three mount counts — read-write and read-only
+ *    mounts by inline volumes (what isVolumeConflict sees) and mounts through a PVC (seen only by
+ *    the MaxPD counts) — slot-major [vol_slots][n_nodes] KSIM_VOL_SLOT words (0 = empty) and a
+ *    used-slot count; each commit adds the pod's refs, ksim_pod_remove subtracts them (a slot whose
+ *    counts reach 0 goes; a count at its field's maximum is a KSIM_E_OVERFLOW);
+ *  - zone_ok (optional): [n_vclass][zone_words] bit per label set, NoVolumeZoneConflict's verdict
+ *    (a function of the node's zone / region labels and the class's PV labels).
+ * A pod with vol_class set is scheduled by the launch-mode kernels; node events (ksim_node_add /
+ * update / remove) make the tables stale until they are loaded again. */
+#define KSIM_VOL_EBS 1u
+#define KSIM_VOL_GCE_PD 2u
+#define KSIM_VOL_AZURE_DISK 4u
+#define KSIM_VOL_CONFLICT_ANY (1u << 0) /* NoDiskConflict: any mount of the key conflicts (EBS; read-write
+                                           GCE PD / ISCSI / RBD) */
+#define KSIM_VOL_CONFLICT_RW (1u << 1)  /* NoDiskConflict: read-write mounts conflict (read-only GCE PD /
+                                           ISCSI / RBD) */
+#define KSIM_VOL_READ_ONLY (1u << 2)    /* the mount counts as read-only */
+#define KSIM_VOL_NEW (1u << 3)          /* first ref of the key in the class: one of MaxPD's newVolumes */
+#define KSIM_VOL_VIA_PVC (1u << 4)      /* mounted through a PVC: counted by MaxPD, invisible to NoDiskConflict */
+/* slot word: key | pvc mounts (10 bits) | read-only inline mounts (11) | read-write inline mounts (11) */
+#define KSIM_VOL_SLOT(key, rw, ro, pvc)                                                                   \
+  ((((uint64_t)(uint32_t)(key)) << 32) | (((uint64_t)(pvc) & 0x3FFu) << 22) | (((uint64_t)(ro) & 0x7FFu) << 11) | \
+   ((uint64_t)(rw) & 0x7FFu))
+
+typedef struct {
+  int32_t key;
+  uint32_t flags; /* KSIM_VOL_CONFLICT_* | KSIM_VOL_READ_ONLY | KSIM_VOL_NEW | KSIM_VOL_VIA_PVC */
+} ksim_vol_ref;
+
+typedef struct {
+  int32_t n_keys, n_vclass, n_refs, vol_slots;
+  int64_t n_nodes;             /* must equal the loaded node table's */
+  int32_t max_vols[3];         /* MaxPD limits: EBS, GCE PD, Azure Disk (getMaxVols, :347-359) */
+  int32_t zone_words;          /* ceil(n_label_sets / 32) of the loaded class tables, or 0 without zone_ok */
+  const uint32_t* key_filter;  /* [n_keys] */
+  const int32_t* vc;           /* [n_vclass][2] (offset, count) into refs */
+  const uint32_t* vc_filter;   /* [n_vclass] */
+  const ksim_vol_ref* refs;    /* [n_refs] */
+  const uint32_t* zone_ok;     /* [n_vclass][zone_words] or NULL (every node passes) */
+  const uint64_t* slots;       /* [vol_slots][n_nodes] mounts of the pods already placed */
+  const int32_t* slot_count;   /* [n_nodes] */
+} ksim_volume_tables;
+
+/* Load (or replace) the volume tables; the slots describe the pods already placed. */
+int ksim_load_volumes(ksim_handle* h, const ksim_volume_tables* t);
+/* Read back the volume slots ([vol_slots][n_nodes]) and counts ([n_nodes]); either may be NULL. */
+int ksim_read_volumes(ksim_handle* h, uint64_t* slots, int32_t* slot_count);
 
 int ksim_read_nodes(ksim_handle* h, ksim_node_state* out);
 int ksim_get_counter(ksim_handle* h, uint64_t* out);

@@ -179,6 +179,7 @@ int check_ready(ksim_handle* h, const char* where) {
 // A node event: the affinity tables' per-node domains no longer describe the table.
 void node_event(ksim_handle* h) {
   if (h->have_aff) h->aff_stale = true;
+  if (h->have_vol) h->vol_stale = true;
 }
 
 int check_pod_args(ksim_handle* h, const ksim_pod* pod, int32_t n_ports, int32_t n_scalars, const uint64_t* ports,
@@ -201,7 +202,7 @@ int after_commit(ksim_handle* h, int32_t port_cnt) {
   if (h->res_host[KSIM_RES_STATUS] & 1) h->pfast_off = true;  // keep the fast kernels' float64 range
   int32_t err = 0;
   HIPCHK(h, hipMemcpy(&err, h->ctx.err, 4, hipMemcpyDeviceToHost));
-  if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port slots overflowed (raise port_slots)");
+  if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port or volume slots overflowed (raise port_slots / vol_slots)");
   if (err & ~1) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
   return KSIM_OK;
 }

@@ -73,6 +73,7 @@ __global__ void ksim_release_kernel(KsimCtx c, int64_t pod, int64_t node) {
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     ksim_uncommit(c, c.pods[pod], node);
     if (ksim_is_aff_pod(c, c.pods[pod])) ksim_aff_commit(*c.aff, c.pods[pod], node, -1);
+    if (ksim_is_vol_pod(c, c.pods[pod])) ksim_vol_commit(*c.vol, c.pods[pod], node, -1, c.err);
   }
 }
 

@@ -53,6 +53,22 @@ struct KsimAff {
   int32_t pad;
 };
 
+// Volume tables on the device (ksim_load_volumes; layout in include/ksim.h).
+struct KsimVol {
+  int64_t n;                            // nodes (the slot stride)
+  uint64_t* slots;                      // [vol_slots][n] KSIM_VOL_SLOT words
+  int32_t* slot_count;                  // [n]
+  const uint32_t* __restrict__ key_filter;
+  const int32_t* __restrict__ vc;       // [n_vclass][2]
+  const uint32_t* __restrict__ vc_filter;
+  const ksim_vol_ref* __restrict__ refs;
+  const uint32_t* __restrict__ zone_ok; // [n_vclass][zone_words] or null
+  int32_t max_vols[3];
+  int32_t vol_slots;
+  int32_t zone_words;
+  int32_t pad;
+};
+
 struct KsimCtx {
   // ---- node table (name-rank order) ----
   int64_t n;
@@ -115,6 +131,7 @@ struct KsimCtx {
   uint64_t* dbg;          // diagnostic stamp sums (KSIM_STAMPS builds only), else null
   int32_t* out_fit;       // optional (per-pod drop-in): [0] = len(filtered), [1] |= ksim_row_status
   const KsimAff* aff;     // inter-pod affinity tables (device), null when none are loaded
+  const KsimVol* vol;     // volume tables (device), null when none are loaded
 };
 
 // Node-sharded mode (ksim_shard_*): this rank's place in the world and every rank's exchange
@@ -395,6 +412,101 @@ __device__ __forceinline__ bool ksim_is_aff_pod(const KsimCtx& c, const ksim_pod
   return c.aff && (P.aff_ident > 0 || P.aff_class > 0);
 }
 
+// ---- volumes (tables: include/ksim.h, ksim/volumes.py) ----
+__device__ __forceinline__ bool ksim_is_vol_pod(const KsimCtx& c, const ksim_pod& P) {
+  return c.vol && P.vol_class > 0;
+}
+
+// Mount counts of key k on node i: slot index or -1.
+__device__ __forceinline__ int32_t ksim_vol_find(const KsimVol& V, int64_t i, int32_t cnt, int32_t key) {
+  for (int32_t s = 0; s < cnt; ++s)
+    if ((int32_t)(V.slots[(int64_t)s * V.n + i] >> 32) == key) return s;
+  return -1;
+}
+
+// NoDiskConflict (predicates.go:276-285 over isVolumeConflict :220-265): some volume of the pod
+// is mounted on the node by a placed pod in a conflicting mode.
+__device__ __noinline__ uint32_t ksim_disk_conflict(const KsimVol& V, int32_t vclass, int64_t i) {
+  const int32_t* vc = V.vc + 2 * (int64_t)(vclass - 1);
+  const int32_t cnt = V.slot_count[i];
+  for (int32_t j = vc[0], e = vc[0] + vc[1]; j < e; ++j) {
+    const ksim_vol_ref r = V.refs[j];
+    if (!(r.flags & (KSIM_VOL_CONFLICT_ANY | KSIM_VOL_CONFLICT_RW))) continue;
+    const int32_t s = ksim_vol_find(V, i, cnt, r.key);
+    if (s < 0) continue;
+    const uint64_t w = V.slots[(int64_t)s * V.n + i];
+    const uint32_t rw = (uint32_t)(w & 0x7FFu), ro = (uint32_t)((w >> 11) & 0x7FFu);
+    if ((r.flags & KSIM_VOL_CONFLICT_ANY) ? (rw + ro > 0) : (rw > 0)) return 1u << KSIM_R_DISK_CONFLICT;
+  }
+  return 0;
+}
+
+// MaxEBS / MaxGCEPD / MaxAzureDiskVolumeCount (predicates.go:415-456) for the filters in `which`,
+// in that order: the node's distinct mounted keys the filter counts plus the pod's keys it counts
+// that the node does not mount yet, against the filter's limit.
+__device__ __noinline__ uint32_t ksim_max_volumes(const KsimVol& V, int32_t vclass, int64_t i, uint32_t which) {
+  const int32_t* vc = V.vc + 2 * (int64_t)(vclass - 1);
+  const uint32_t want = V.vc_filter[vclass - 1] & which;
+  if (!want) return 0;
+  const int32_t cnt = V.slot_count[i];
+  for (int t = 0; t < 3; ++t) {
+    const uint32_t f = 1u << t;
+    if (!(want & f)) continue;
+    int32_t have = 0;
+    for (int32_t s = 0; s < cnt; ++s)
+      if (V.key_filter[(int32_t)(V.slots[(int64_t)s * V.n + i] >> 32)] & f) ++have;
+    int32_t add = 0;
+    for (int32_t j = vc[0], e = vc[0] + vc[1]; j < e; ++j) {
+      const ksim_vol_ref r = V.refs[j];
+      if ((r.flags & KSIM_VOL_NEW) && (V.key_filter[r.key] & f) && ksim_vol_find(V, i, cnt, r.key) < 0) ++add;
+    }
+    if (have + add > V.max_vols[t]) return 1u << KSIM_R_MAX_VOLUME_COUNT;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ bool ksim_vol_zone_ok(const KsimVol& V, int32_t vclass, int32_t label_set) {
+  if (!V.zone_ok) return true;
+  return (V.zone_ok[(int64_t)(vclass - 1) * V.zone_words + (label_set >> 5)] >> (label_set & 31)) & 1u;
+}
+
+// NodeInfo.AddPod / RemovePod of a pod with volumes on node w (sign +1 / -1): each ref adds or
+// takes one mount of its key (read-write, read-only or through a PVC).  Single thread; a full node
+// or a saturated count sets err bit 1.
+__device__ __noinline__ void ksim_vol_commit(const KsimVol& V, const ksim_pod& P, int64_t w, int32_t sign,
+                                             int32_t* err) {
+  const int32_t* vc = V.vc + 2 * (int64_t)(P.vol_class - 1);
+  for (int32_t j = vc[0], e = vc[0] + vc[1]; j < e; ++j) {
+    const ksim_vol_ref r = V.refs[j];
+    const int sh = (r.flags & KSIM_VOL_VIA_PVC) ? 22 : (r.flags & KSIM_VOL_READ_ONLY) ? 11 : 0;
+    const uint64_t fmask = (sh == 22 ? 0x3FFull : 0x7FFull) << sh;
+    const uint64_t one = 1ull << sh;
+    const int32_t cnt = V.slot_count[w];
+    const int32_t s = ksim_vol_find(V, w, cnt, r.key);
+    uint64_t* slot = s >= 0 ? &V.slots[(int64_t)s * V.n + w] : nullptr;
+    if (sign > 0) {
+      if (slot) {
+        if ((*slot & fmask) == fmask) atomicOr(err, 1);
+        else *slot += one;
+      } else if (cnt >= V.vol_slots) {
+        atomicOr(err, 1);
+      } else {
+        V.slots[(int64_t)cnt * V.n + w] = ((uint64_t)(uint32_t)r.key << 32) | one;
+        V.slot_count[w] = cnt + 1;
+      }
+    } else if (slot && (*slot & fmask)) {
+      const uint64_t v = *slot - one;
+      if ((v & 0xFFFFFFFFull) == 0) {  // no mount left: the slot goes (slot order is irrelevant)
+        *slot = V.slots[(int64_t)(cnt - 1) * V.n + w];
+        V.slots[(int64_t)(cnt - 1) * V.n + w] = 0;
+        V.slot_count[w] = cnt - 1;
+      } else {
+        *slot = v;
+      }
+    }
+  }
+}
+
 // Reason mask of the first failing predicate in predicatesOrdering (predicates.go:129-138,
 // core/generic_scheduler.go:467-528); 0 = fits.
 template <class A>
@@ -429,6 +541,11 @@ __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ks
     m = ksim_resources(c, P, i, r);
     if (m) return m;
   }
+  const bool vol = ksim_is_vol_pod(c, P);
+  if ((pr & KSIM_P_DISK_CONFLICT) && vol) {
+    m = ksim_disk_conflict(*c.vol, P.vol_class, i);
+    if (m) return m;
+  }
   if ((pr & KSIM_P_TAINTS) && (P.flags & KSIM_POD_NEED_TAINTS)) {
     if (!a.taint_ok(P, i)) return 1u << KSIM_R_TAINTS;
   }
@@ -436,6 +553,15 @@ __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ks
     if (!a.noexec_ok(P, i)) return 1u << KSIM_R_TAINTS;
   }
   if ((pr & KSIM_P_LABEL_PRESENCE) && (r.fl & KSIM_N_LABEL_PRESENCE)) return 1u << KSIM_R_LABEL_PRESENCE;
+  if (vol) {
+    const uint32_t which = ((pr & KSIM_P_MAX_EBS) ? KSIM_VOL_EBS : 0u) | ((pr & KSIM_P_MAX_GCE_PD) ? KSIM_VOL_GCE_PD : 0u) |
+                           ((pr & KSIM_P_MAX_AZURE_DISK) ? KSIM_VOL_AZURE_DISK : 0u);
+    if (which) {
+      m = ksim_max_volumes(*c.vol, P.vol_class, i, which);
+      if (m) return m;
+    }
+    if ((pr & KSIM_P_VOLUME_ZONE) && !ksim_vol_zone_ok(*c.vol, P.vol_class, c.label_set[i])) return 1u << KSIM_R_VOLUME_ZONE;
+  }
   if ((pr & KSIM_P_MEM_PRESSURE) && (P.flags & KSIM_POD_BEST_EFFORT) && (r.fl & KSIM_N_MEM_PRESSURE))
     return 1u << KSIM_R_MEM_PRESSURE;
   if ((pr & KSIM_P_DISK_PRESSURE) && (r.fl & KSIM_N_DISK_PRESSURE)) return 1u << KSIM_R_DISK_PRESSURE;

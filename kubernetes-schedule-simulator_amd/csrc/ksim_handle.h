@@ -152,6 +152,17 @@ struct ksim_handle {
   std::vector<void*> aff_bufs;
   std::vector<int32_t> q_ident, q_aclass;
   std::vector<int64_t> aff_pre;  // aff_pre[i] = affinity pods among the first i queued
+  // volumes (ksim_load_volumes): the device tables, the host copy of their descriptor (slot
+  // pointers for ksim_read_volumes) and per queued pod its volume class (a volume pod takes the
+  // launch-mode kernels)
+  bool have_vol = false;
+  bool vol_stale = false;       // a node event changed the table the slots describe
+  int32_t vol_n_class = 0;
+  KsimVol vol_h{};
+  KsimVol* vol_dev = nullptr;
+  std::vector<void*> vol_bufs;
+  std::vector<int32_t> q_vclass;
+  std::vector<int64_t> vol_pre;  // vol_pre[i] = volume pods among the first i queued
 };
 
 int ksim_fail(ksim_handle* h, int code, const char* fmt, ...);
@@ -224,6 +235,8 @@ int ksim_rt_check_pod(ksim_handle* h, const ksim_pod& p, int64_t n_ports, int64_
 int ksim_rt_ensure_partials(ksim_handle* h, int grid);
 // Affinity pods among queued pods [first, first+count).
 int64_t ksim_rt_aff_count(const ksim_handle* h, int64_t first, int64_t count);
-// KSIM_E_STATE when the affinity tables are stale (a node event since they were loaded).
+// Pods among [first, first+count) that only the launch-mode kernels schedule (affinity, volumes).
+int64_t ksim_rt_launch_only_count(const ksim_handle* h, int64_t first, int64_t count);
+// KSIM_E_STATE when the affinity or volume tables are stale (a node event since they were loaded).
 int ksim_rt_check_aff(ksim_handle* h, const char* where);
 int ksim_rt_pick_npt(int64_t n);

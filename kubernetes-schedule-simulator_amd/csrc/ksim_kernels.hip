@@ -370,6 +370,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       if (node >= 0 && !c.no_commit) {
         ksim_commit(c, P, node);
         if (ksim_is_aff_pod(c, P)) ksim_aff_commit(*c.aff, P, node, 1);
+        if (ksim_is_vol_pod(c, P)) ksim_vol_commit(*c.vol, P, node, 1, c.err);
         if (c.out_fit) c.out_fit[1] |= ksim_row_status(c, node);
       }
     }
@@ -481,6 +482,7 @@ __global__ void ksim_assume_kernel(KsimCtx c, int64_t pod, int64_t node, int32_t
   if (threadIdx.x == 0 && blockIdx.x == 0) {
     ksim_commit(c, c.pods[pod], node);
     if (ksim_is_aff_pod(c, c.pods[pod])) ksim_aff_commit(*c.aff, c.pods[pod], node, 1);
+    if (ksim_is_vol_pod(c, c.pods[pod])) ksim_vol_commit(*c.vol, c.pods[pod], node, 1, c.err);
     *status |= ksim_row_status(c, node);
   }
 }

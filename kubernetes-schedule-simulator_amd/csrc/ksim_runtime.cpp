@@ -255,6 +255,10 @@ int ksim_rt_check_pod(ksim_handle* h, const ksim_pod& p, int64_t n_ports, int64_
     return ksim_fail(h, KSIM_E_STATE, "%s: affinity identity / class set but no affinity tables are loaded", where);
   if (p.aff_ident < 0 || p.aff_ident > h->aff_n_ident || p.aff_class < 0 || p.aff_class > h->aff_n_aclass)
     return ksim_fail(h, KSIM_E_INVAL, "%s: affinity identity / class out of range", where);
+  if (p.vol_class && !h->have_vol)
+    return ksim_fail(h, KSIM_E_STATE, "%s: volume class set but no volume tables are loaded", where);
+  if (p.vol_class < 0 || p.vol_class > h->vol_n_class)
+    return ksim_fail(h, KSIM_E_INVAL, "%s: volume class out of range", where);
   return KSIM_OK;
 }
 
@@ -263,9 +267,17 @@ int64_t ksim_rt_aff_count(const ksim_handle* h, int64_t first, int64_t count) {
   return h->aff_pre[first + count] - h->aff_pre[first];
 }
 
+int64_t ksim_rt_launch_only_count(const ksim_handle* h, int64_t first, int64_t count) {
+  int64_t k = ksim_rt_aff_count(h, first, count);
+  if (h->have_vol && count > 0) k += h->vol_pre[first + count] - h->vol_pre[first];
+  return k;
+}
+
 int ksim_rt_check_aff(ksim_handle* h, const char* where) {
   if (h->have_aff && h->aff_stale)
     return ksim_fail(h, KSIM_E_STATE, "%s: the affinity tables predate a node event; load them again", where);
+  if (h->have_vol && h->vol_stale)
+    return ksim_fail(h, KSIM_E_STATE, "%s: the volume tables predate a node event; load them again", where);
   return KSIM_OK;
 }
 
@@ -275,7 +287,8 @@ static bool fast_base(const ksim_pod& p) {
   bool in_range = true;
   for (int64_t v : {p.req_cpu, p.req_mem, p.add_cpu, p.add_mem, p.nz_cpu, p.nz_mem}) in_range &= v >= 0 && v < lim;
   return in_range && p.host == -1 && p.port_cnt == 0 && p.scalar_cnt == 0 && p.req_gpu == 0 && p.req_eph == 0 &&
-         !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS)) && p.aff_ident == 0 && p.aff_class == 0;
+         !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS)) && p.aff_ident == 0 && p.aff_class == 0 &&
+         p.vol_class == 0;
 }
 
 static bool fast_k(const ksim_handle* h, int32_t cls) {
@@ -359,6 +372,8 @@ int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
   h->q_ident.resize((size_t)np);
   h->q_aclass.resize((size_t)np);
   h->aff_pre.resize((size_t)np + 1);
+  h->q_vclass.resize((size_t)np);
+  h->vol_pre.resize((size_t)np + 1);
   h->fast_pre.resize((size_t)np + 1);
   h->pod_qmax.resize((size_t)np);
   std::vector<int32_t> tc((size_t)n_pods, -1);
@@ -371,6 +386,8 @@ int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
     h->q_ident[q] = p.aff_ident;
     h->q_aclass[q] = p.aff_class;
     h->aff_pre[q + 1] = h->aff_pre[q] + ((p.aff_ident || p.aff_class) ? 1 : 0);
+    h->q_vclass[q] = p.vol_class;
+    h->vol_pre[q + 1] = h->vol_pre[q] + (p.vol_class ? 1 : 0);
     const bool fast = h->q_base[q] && fast_k(h, p.cls);
     h->fast_pre[q + 1] = h->fast_pre[q] + (fast ? 1 : 0);
     int64_t m = 0;
@@ -575,8 +592,8 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
 
 static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   KsimCtx& c = h->ctx;
-  // inter-pod affinity pods are evaluated and committed by the launch-mode kernels only
-  if (ksim_rt_aff_count(h, first, count)) return run_launch_mode(h, first, count, st);
+  // inter-pod affinity and volume pods are evaluated and committed by the launch-mode kernels only
+  if (ksim_rt_launch_only_count(h, first, count)) return run_launch_mode(h, first, count, st);
   int grid = 0, lds_rows = 0;
   if (const int form = pfast_form(h, first, count, &grid, &lds_rows)) {
     int rc = run_pfast_mode(h, first, count, grid, lds_rows, form == 2, st);
@@ -667,7 +684,7 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
 // kernel can take the range), else the launch form.
 static int run_auto_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   int g, l;
-  if (ksim_rt_aff_count(h, first, count)) {
+  if (ksim_rt_launch_only_count(h, first, count)) {
     h->tree_valid = false;
     return run_launch_mode(h, first, count, st);
   }
@@ -849,7 +866,7 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
       st->scheduled = s;
     }
   }
-  if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port slots overflowed (raise port_slots)");
+  if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port or volume slots overflowed (raise port_slots / vol_slots)");
   if (err & ~1) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
   return KSIM_OK;
 }

@@ -14,10 +14,10 @@ LIB_PATH = os.environ.get("KSIM_LIB") or os.path.join(PKG_DIR, "lib", "libksim.s
 
 KSIM_OK = 0
 E_INVAL, E_DEVICE, E_NOMEM, E_UNSUPPORTED, E_STATE, E_OVERFLOW, E_NO_NODES = -1, -2, -3, -4, -5, -6, -7
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_SCALAR = 8
 MAX_RCLASS = 16
-NREASONS = 28
+NREASONS = 31
 
 # predicate bits
 P_CHECK_NODE_CONDITION = 1 << 0
@@ -33,6 +33,11 @@ P_MEM_PRESSURE = 1 << 9
 P_DISK_PRESSURE = 1 << 10
 P_LABEL_PRESENCE = 1 << 11
 P_INTERPOD_AFFINITY = 1 << 12
+P_DISK_CONFLICT = 1 << 13
+P_MAX_EBS = 1 << 14
+P_MAX_GCE_PD = 1 << 15
+P_MAX_AZURE_DISK = 1 << 16
+P_VOLUME_ZONE = 1 << 17
 
 W_LEAST, W_MOST, W_BALANCED, W_TAINT_TOL, W_NODE_AFF, W_INTERPOD = range(6)
 NW = 6
@@ -50,10 +55,15 @@ R_HOSTNAME, R_HOST_PORTS, R_NODE_SELECTOR, R_TAINTS = 9, 10, 11, 12
 R_MEM_PRESSURE, R_DISK_PRESSURE, R_LABEL_PRESENCE = 13, 14, 15
 R_SCALAR0 = 16
 R_POD_AFFINITY, R_EXISTING_ANTI, R_AFFINITY_RULES, R_ANTI_AFFINITY_RULES = 24, 25, 26, 27
+R_DISK_CONFLICT, R_MAX_VOLUME_COUNT, R_VOLUME_ZONE = 28, 29, 30
 
 # inter-pod affinity tables (ksim_affinity_tables)
 AFF_REQ_AFFINITY, AFF_REQ_ANTI, AFF_PREFERRED = 0, 1, 2
 AFF_CARRY_ANTI, AFF_CARRY_PRIO = 0, 1
+
+# volume tables (ksim_volume_tables)
+VOL_EBS, VOL_GCE_PD, VOL_AZURE_DISK = 1, 2, 4
+VOL_CONFLICT_ANY, VOL_CONFLICT_RW, VOL_READ_ONLY, VOL_NEW, VOL_VIA_PVC = 1, 2, 4, 8, 16
 
 _i64p = C.POINTER(C.c_int64)
 _i32p = C.POINTER(C.c_int32)
@@ -90,7 +100,7 @@ class Pod(C.Structure):
                 ("nz_cpu", C.c_int64), ("nz_mem", C.c_int64), ("cls", C.c_int32), ("host", C.c_int32),
                 ("flags", C.c_uint32), ("port_off", C.c_int32), ("port_cnt", C.c_int32),
                 ("scalar_off", C.c_int32), ("scalar_cnt", C.c_int32), ("aff_ident", C.c_int32),
-                ("aff_class", C.c_int32), ("reserved", C.c_int32 * 3)]
+                ("aff_class", C.c_int32), ("vol_class", C.c_int32), ("reserved", C.c_int32 * 2)]
 
 
 class ScalarReq(C.Structure):
@@ -130,6 +140,16 @@ class AffinityTables(C.Structure):
                 ("carries", C.c_void_p), ("cnt", _i32p), ("carried", _i64p)]
 
 
+class VolumeTables(C.Structure):
+    _fields_ = [("n_keys", C.c_int32), ("n_vclass", C.c_int32), ("n_refs", C.c_int32), ("vol_slots", C.c_int32),
+                ("n_nodes", C.c_int64), ("max_vols", C.c_int32 * 3), ("zone_words", C.c_int32),
+                ("key_filter", _u32p), ("vc", _i32p), ("vc_filter", _u32p), ("refs", C.c_void_p),
+                ("zone_ok", _u32p), ("slots", _u64p), ("slot_count", _i32p)]
+
+
+VOL_REF_DTYPE = np.dtype([("key", "<i4"), ("flags", "<u4")])
+
+
 class NodeState(C.Structure):
     _fields_ = [("req_cpu", _i64p), ("req_mem", _i64p), ("req_gpu", _i64p), ("req_eph", _i64p),
                 ("nz_cpu", _i64p), ("nz_mem", _i64p), ("pod_count", _i32p), ("req_scalar", _i64p),
@@ -141,7 +161,8 @@ POD_DTYPE = np.dtype([("req_cpu", "<i8"), ("req_mem", "<i8"), ("req_gpu", "<i8")
                       ("add_cpu", "<i8"), ("add_mem", "<i8"), ("add_gpu", "<i8"), ("add_eph", "<i8"),
                       ("nz_cpu", "<i8"), ("nz_mem", "<i8"), ("cls", "<i4"), ("host", "<i4"), ("flags", "<u4"),
                       ("port_off", "<i4"), ("port_cnt", "<i4"), ("scalar_off", "<i4"), ("scalar_cnt", "<i4"),
-                      ("aff_ident", "<i4"), ("aff_class", "<i4"), ("reserved", "<i4", (3,))])
+                      ("aff_ident", "<i4"), ("aff_class", "<i4"), ("vol_class", "<i4"),
+                      ("reserved", "<i4", (2,))])
 SCALAR_DTYPE = np.dtype([("col", "<i4"), ("pad", "<i4"), ("req", "<i8"), ("add", "<i8")])
 assert POD_DTYPE.itemsize == C.sizeof(Pod) == 128
 assert SCALAR_DTYPE.itemsize == C.sizeof(ScalarReq)
@@ -151,7 +172,8 @@ EXPORTS = ["ksim_abi_version", "ksim_last_error", "ksim_create", "ksim_destroy",
            "ksim_read_nodes", "ksim_get_counter", "ksim_set_counter", "ksim_selftest", "ksim_sweep",
            "ksim_shard_setup", "ksim_shard_export", "ksim_shard_connect", "ksim_shard_connect_local",
            "ksim_schedule_one", "ksim_pod_add", "ksim_pod_remove", "ksim_node_add", "ksim_node_update",
-           "ksim_node_remove", "ksim_node_count", "ksim_append_pods", "ksim_load_affinity"]
+           "ksim_node_remove", "ksim_node_count", "ksim_append_pods", "ksim_load_affinity", "ksim_load_volumes",
+           "ksim_read_volumes"]
 IPC_HANDLE_BYTES = 64
 MAX_RANKS = 8
 
@@ -213,6 +235,8 @@ def lib():
     L.ksim_node_count.argtypes = [C.c_void_p, C.POINTER(C.c_int64)]
     L.ksim_append_pods.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
     L.ksim_load_affinity.argtypes = [C.c_void_p, C.POINTER(AffinityTables)]
+    L.ksim_load_volumes.argtypes = [C.c_void_p, C.POINTER(VolumeTables)]
+    L.ksim_read_volumes.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     if L.ksim_abi_version() != ABI_VERSION:
         raise ImportError("libksim.so ABI version mismatch")
     _lib = L

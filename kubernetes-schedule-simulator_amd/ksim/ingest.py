@@ -32,8 +32,9 @@ CPU, MEM, GPU, EPH, PODS = "cpu", "memory", "alpha.kubernetes.io/nvidia-gpu", "e
 DEFAULT_MILLI_CPU = 100
 DEFAULT_MEMORY = 200 * 1024 * 1024
 PREFER_AVOID_ANNOTATION = "scheduler.alpha.kubernetes.io/preferAvoidPods"
-_UNSUPPORTED_VOLUMES = ("gcePersistentDisk", "awsElasticBlockStore", "rbd", "iscsi", "azureDisk",
-                        "persistentVolumeClaim")
+# volume sources the volume predicates read (ksim/volumes.py); others never change a verdict
+_PREDICATE_VOLUMES = ("gcePersistentDisk", "awsElasticBlockStore", "rbd", "iscsi", "azureDisk",
+                      "persistentVolumeClaim")
 
 
 class Unsupported(abi.KsimUnsupported):
@@ -155,12 +156,14 @@ def has_pod_affinity(pod):
     return aff.get("podAffinity") is not None or aff.get("podAntiAffinity") is not None
 
 
+def has_predicate_volumes(pod):
+    return any(v.get(k) is not None for v in _spec(pod).get("volumes") or [] for k in _PREDICATE_VOLUMES)
+
+
 def check_pod_supported(pod, where="pod"):
-    spec = _spec(pod)
-    for v in spec.get("volumes") or []:
-        for k in _UNSUPPORTED_VOLUMES:
-            if v.get(k) is not None:
-                raise Unsupported("%s %r: %s volumes are outside the supported key set" % (where, _meta(pod).get("name"), k))
+    for v in _spec(pod).get("volumes") or []:
+        if sum(v.get(k) is not None for k in _PREDICATE_VOLUMES) > 1:
+            raise Unsupported("%s %r: a volume with more than one source" % (where, _meta(pod).get("name")))
 
 
 @dataclass
@@ -317,13 +320,18 @@ class Cluster:
         self.bad_affinity_classes = set()   # preferred terms that fail to parse
         self.affinity = None     # inter-pod affinity tables (ksim/affinity.py), None without terms
         self.hard_weight = 10
+        self.volume_index = None  # ksim/volumes.py VolumeIndex when a pod has predicate volumes
+        self.volumes = None       # its device tables (volumes.build_tables)
 
     # ------------------------------------------------------------------ nodes
     @classmethod
-    def from_objects(cls, nodes, running_pods=(), pods=(), port_slots=None, hard_weight=10):
+    def from_objects(cls, nodes, running_pods=(), pods=(), port_slots=None, hard_weight=10, pvs=(), pvcs=(),
+                     storage_classes=(), max_vols=None, vol_slots=None):
         """nodes / running_pods / pods: Kubernetes-shaped dicts; pods are in SCHEDULING
         order (the caller resolves the simulator's LIFO queue).  hard_weight:
-        hardPodAffinitySymmetricWeight (the simulator's 10, or a Policy's)."""
+        hardPodAffinitySymmetricWeight (the simulator's 10, or a Policy's).  pvs / pvcs /
+        storage_classes: what the PV / PVC / StorageClass listers hold (the simulator's are empty);
+        max_vols: the MaxPD limits (EBS, GCE PD, Azure Disk), default KUBE_MAX_PD_VOLS / getMaxVols."""
         self = cls()
         self.hard_weight = int(hard_weight)
         self.ips.get("0.0.0.0")     # id 0 = wildcard
@@ -395,6 +403,9 @@ class Cluster:
         self.cols = c
         # pod queue
         self._affinity_ok = with_affinity
+        if any(has_predicate_volumes(p) for p in list(running) + list(pods)):
+            from .volumes import VolumeIndex
+            self.volume_index = VolumeIndex(pvs, pvcs, storage_classes)
         self._compile_pods(list(pods), compiled[len(running):])
         if with_affinity:
             self._build_affinity(nodes, running, list(pods))
@@ -417,6 +428,11 @@ class Cluster:
             pc[i] = len(u)
         c["ports"], c["port_count"] = ports, pc
         self._build_tables()
+        if self.volume_index is not None:
+            from .volumes import build_tables
+            mounts = self.volume_index.node_slots(n, [(self.index[_spec(p)["nodeName"]], p) for p in running])
+            self.volumes = build_tables(self.volume_index, n, mounts, self.pods["vol_class"] if self.pods is not None else (),
+                                        self.label_sets.items, max_vols, vol_slots)
         return self
 
     # ------------------------------------------------------------------- pods
@@ -464,6 +480,11 @@ class Cluster:
         row["scalar_off"], row["scalar_cnt"] = len(scalars), len(pred.scalar)
         for name, v in pred.scalar.items():
             scalars.append((self.scalar_names.ids[name], 0, v, add.scalar.get(name, 0)))
+        if has_predicate_volumes(p):
+            if self.volume_index is None:
+                raise Unsupported("pod %r: volumes need the cluster's volume tables (ClusterCapacity / "
+                                  "GenericScheduler)" % md.get("name"))
+            row["vol_class"] = self.volume_index.vclass(p)
 
     def _build_affinity(self, nodes, running, pods):
         """Inter-pod affinity tables over every pod's identity and terms (ksim/affinity.py); the
@@ -526,6 +547,8 @@ class Cluster:
         import copy
         if self.affinity is not None:
             raise Unsupported("node-sharded scheduling of pods with inter-pod affinity terms")
+        if self.volumes is not None:
+            raise Unsupported("node-sharded scheduling of pods with volumes")
         sub = copy.copy(self)
         sub.cols = {k: (np.ascontiguousarray(v[..., lo:hi]) if isinstance(v, np.ndarray) else v)
                     for k, v in self.cols.items()}

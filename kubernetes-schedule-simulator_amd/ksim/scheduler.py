@@ -38,13 +38,19 @@ PREDICATE_BITS = {
     "CheckNodeDiskPressure": abi.P_DISK_PRESSURE,
     "CheckNodeLabelPresence": abi.P_LABEL_PRESENCE,   # with a Policy labelsPresence argument
     "MatchInterPodAffinity": abi.P_INTERPOD_AFFINITY,  # over the cluster's affinity tables
+    "NoDiskConflict": abi.P_DISK_CONFLICT,              # over the cluster's volume tables
+    "MaxEBSVolumeCount": abi.P_MAX_EBS,
+    "MaxGCEPDVolumeCount": abi.P_MAX_GCE_PD,
+    "MaxAzureDiskVolumeCount": abi.P_MAX_AZURE_DISK,
+    "NoVolumeZoneConflict": abi.P_VOLUME_ZONE,
 }
+VOLUME_PREDICATE_BITS = abi.P_DISK_CONFLICT | abi.P_MAX_EBS | abi.P_MAX_GCE_PD | abi.P_MAX_AZURE_DISK | abi.P_VOLUME_ZONE
 # factory/plugins.go:401-406 + defaults.go:165: part of every predicate map
 MANDATORY_PREDICATES = ("CheckNodeCondition",)
-# keys that are true for every pod ingest accepts (no volumes of those kinds); "PodFitsPorts"
-# is registered but absent from predicatesOrdering, so it never runs
-TRIVIAL_PREDICATES = {"NoDiskConflict", "MaxEBSVolumeCount", "MaxGCEPDVolumeCount", "MaxAzureDiskVolumeCount",
-                      "CheckVolumeBinding", "NoVolumeZoneConflict", "PodFitsPorts"}
+# keys that are true for every pod the scheduler accepts: CheckVolumeBinding (PVCs only when
+# bound to a PV without node affinity, ksim/volumes.py); "PodFitsPorts" is registered but absent
+# from predicatesOrdering, so it never runs
+TRIVIAL_PREDICATES = {"CheckVolumeBinding", "PodFitsPorts"}
 
 PRIORITY_SLOTS = {"LeastRequestedPriority": abi.W_LEAST, "MostRequestedPriority": abi.W_MOST,
                   "BalancedResourceAllocation": abi.W_BALANCED, "TaintTolerationPriority": abi.W_TAINT_TOL,
@@ -130,6 +136,9 @@ REASON_TEXT = {
     abi.R_EXISTING_ANTI: "node(s) didn't satisfy existing pods anti-affinity rules",
     abi.R_AFFINITY_RULES: "node(s) didn't match pod affinity rules",
     abi.R_ANTI_AFFINITY_RULES: "node(s) didn't match pod anti-affinity rules",
+    abi.R_DISK_CONFLICT: "node(s) had no available disk",
+    abi.R_MAX_VOLUME_COUNT: "node(s) exceed max volume count",
+    abi.R_VOLUME_ZONE: "node(s) had no available volume zone",
 }
 
 
@@ -188,6 +197,24 @@ def class_tables_for(tables, priorities):
     return d, add
 
 
+def check_volume_support(cluster, predicates):
+    """Refuse inputs on which a configured volume predicate returns an error instead of a verdict
+    (ksim/volumes.py): findNodesThatFit then aborts the pod's cycle (core/generic_scheduler.go:351-353)
+    and the simulator's requeue path takes over, which this batch form does not restate."""
+    if cluster.volume_index is None:
+        return
+    errs = cluster.volume_index.errors
+    keys = set(predicates)
+    maxpd = keys & {"MaxEBSVolumeCount", "MaxGCEPDVolumeCount", "MaxAzureDiskVolumeCount"}
+    if "claim_name" in errs and (maxpd or "NoVolumeZoneConflict" in keys):
+        raise Unsupported("a PersistentVolumeClaim volume without a claim name (the volume predicates err)")
+    if "binding" in errs and "CheckVolumeBinding" in keys:
+        raise Unsupported("CheckVolumeBinding with a PVC that is not bound to a PV without node affinity "
+                          "(FindPodVolumes errs or needs the volume binder)")
+    if cluster.volumes is not None and cluster.volumes["zone_err"] and "NoVolumeZoneConflict" in keys:
+        raise Unsupported("NoVolumeZoneConflict with a PVC the PV / PVC listers cannot resolve on a zone-labelled node")
+
+
 def label_presence_flags(label_sets, label_set_ids, label_presence):
     """KSIM_N_LABEL_PRESENCE per node: CheckNodeLabelPresence (predicates.go:875-910) fails when
     a listed label's presence differs from `presence`; a function of the node's label set."""
@@ -213,6 +240,7 @@ class GenericScheduler:
             raise Unsupported("CheckNodeLabelPresence needs its labelsPresence argument")
         self.cfg = make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence], priorities,
                                device, mode, collect_reasons, last_node_index)
+        check_volume_support(cluster, self.predicates)
         self.h = abi.Handle(self.cfg)
         table = cluster.node_table()
         if label_presence is not None and "CheckNodeLabelPresence" in self.predicates:
@@ -238,10 +266,34 @@ class GenericScheduler:
                 pods = pods.copy()
                 pods["aff_ident"] = 0
                 pods["aff_class"] = 0
+        self.volumes = None
+        if cluster.volumes is not None:
+            pods = self._load_volumes(cluster, pods)
         self._pods = pods
         self.h.call("ksim_load_pods", abi.vptr(pods), len(pods), abi.vptr(cluster.pod_ports), len(cluster.pod_ports),
                     abi.vptr(cluster.pod_scalars), len(cluster.pod_scalars))
         self.last_stats = None
+
+    def _load_volumes(self, cluster, pods):
+        """Load the volume tables when a volume predicate is configured (else the pods' volumes change
+        nothing: their classes are cleared)."""
+        if not (self.cfg.predicates & VOLUME_PREDICATE_BITS):
+            if len(pods):
+                pods = pods.copy()
+                pods["vol_class"] = 0
+            return pods
+        from .volumes import tables_struct
+        self.volumes = cluster.volumes
+        self.h.call("ksim_load_volumes", C.byref(tables_struct(self.volumes, "NoVolumeZoneConflict" in self.predicates)))
+        return pods
+
+    def volume_state(self):
+        """The device's volume slots ([vol_slots][n]) and per-node slot counts."""
+        d = self.volumes
+        slots = np.zeros_like(d["slots"])
+        cnt = np.zeros_like(d["slot_count"])
+        self.h.call("ksim_read_volumes", abi.vptr(slots), abi.vptr(cnt))
+        return slots, cnt
 
     def schedule(self, first=0, count=None):
         """Schedule + assume pods [first, first+count) in order.
@@ -472,7 +524,7 @@ class ClusterCapacity:
 
     def __init__(self, nodes, running_pods, simulation_pods, provider_name="DefaultProvider",
                  predicates=None, priorities=None, device=0, mode=abi.MODE_AUTO, collect_reasons=True,
-                 policy_obj=None):
+                 policy_obj=None, pvs=(), pvcs=(), storage_classes=()):
         label_presence = None
         if policy_obj is not None:
             from .policy import key_sets
@@ -483,7 +535,9 @@ class ClusterCapacity:
             priorities = q if priorities is None else priorities
         self.order = list(reversed(simulation_pods))   # PodQueue.Pop takes the last element
         self.running = list(running_pods)
-        self.cluster = Cluster.from_objects(nodes, running_pods, self.order)
+        # pvs / pvcs / storage_classes: the simulator's listers are empty; other callers may fill them
+        self.cluster = Cluster.from_objects(nodes, running_pods, self.order, pvs=pvs, pvcs=pvcs,
+                                            storage_classes=storage_classes)
         self.scheduler = GenericScheduler(self.cluster, predicates, priorities, device=device, mode=mode,
                                           collect_reasons=collect_reasons, label_presence=label_presence)
 

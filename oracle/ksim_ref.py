@@ -24,6 +24,7 @@ from __future__ import annotations
 import math
 import functools
 import re
+import os
 from fractions import Fraction
 
 # --------------------------------------------------------------------------
@@ -643,6 +644,285 @@ def pred_true(pod, ni):
     return True, []
 
 
+# --------------------------------------------------------------------------
+# Volume predicates (predicates.go:205-633)
+# --------------------------------------------------------------------------
+R_DISK_CONFLICT = "node(s) had no available disk"                  # error.go:35
+R_MAX_VOLUME_COUNT = "node(s) exceed max volume count"             # error.go:59
+R_VOLUME_ZONE = "node(s) had no available volume zone"             # error.go:37
+ZONE_LABEL = "failure-domain.beta.kubernetes.io/zone"              # kubelet/apis/well_known_labels.go:21
+REGION_LABEL = "failure-domain.beta.kubernetes.io/region"          # :23
+DEFAULT_MAX_VOLS = {"EBS": 39, "GCE": 16, "AzureDisk": 16}          # predicates.go:93-103
+
+
+class PredicateError(Exception):
+    """A predicate's error return (not a failure reason): findNodesThatFit aborts the pod's
+    scheduling cycle with it (core/generic_scheduler.go:351-353)."""
+
+
+def _src(vol, kind):
+    """The VolumeSource member `kind` (nil when absent, generic_scheduler's != nil tests)."""
+    return vol.get(kind)
+
+
+def _volumes(pod):
+    return (pod.get("spec") or {}).get("volumes") or []
+
+
+def have_overlap(a1, a2):
+    """predicates.go:1042-1055."""
+    m = set(a1 or [])
+    return any(v in m for v in a2 or [])
+
+
+def is_volume_conflict(volume, pod):
+    """isVolumeConflict (predicates.go:220-265): `volume` of the incoming pod against every
+    volume of an existing pod."""
+    gce, ebs = _src(volume, "gcePersistentDisk"), _src(volume, "awsElasticBlockStore")
+    rbd, iscsi = _src(volume, "rbd"), _src(volume, "iscsi")
+    if gce is None and ebs is None and rbd is None and iscsi is None:
+        return False
+    for ev in _volumes(pod):
+        egce = _src(ev, "gcePersistentDisk")
+        if gce is not None and egce is not None:
+            if gce.get("pdName", "") == egce.get("pdName", "") and not (gce.get("readOnly") and egce.get("readOnly")):
+                return True
+        eebs = _src(ev, "awsElasticBlockStore")
+        if ebs is not None and eebs is not None:
+            if ebs.get("volumeID", "") == eebs.get("volumeID", ""):
+                return True
+        eis = _src(ev, "iscsi")
+        if iscsi is not None and eis is not None:
+            if iscsi.get("iqn", "") == eis.get("iqn", "") and not (iscsi.get("readOnly") and eis.get("readOnly")):
+                return True
+        erbd = _src(ev, "rbd")
+        if rbd is not None and erbd is not None:
+            if (have_overlap(rbd.get("monitors"), erbd.get("monitors")) and rbd.get("pool", "") == erbd.get("pool", "")
+                    and rbd.get("image", "") == erbd.get("image", "")
+                    and not (rbd.get("readOnly") and erbd.get("readOnly"))):
+                return True
+    return False
+
+
+def pred_no_disk_conflict(pod, ni):
+    """NoDiskConflict (predicates.go:276-285)."""
+    for v in _volumes(pod):
+        for ev in ni.pods:
+            if is_volume_conflict(v, ev):
+                return False, [R_DISK_CONFLICT]
+    return True, []
+
+
+def go_atoi(s):
+    """strconv.Atoi: optional sign, decimal digits, int64 range; None on error."""
+    import re as _re
+    if not _re.fullmatch(r"[+-]?[0-9]+", s or ""):
+        return None
+    v = int(s)
+    return v if -(1 << 63) <= v < (1 << 63) else None
+
+
+def get_max_vols(default, raw=None):
+    """getMaxVols (predicates.go:347-359): KUBE_MAX_PD_VOLS when it parses to a positive int."""
+    if raw is None:
+        raw = os.environ.get("KUBE_MAX_PD_VOLS", "")
+    if raw != "":
+        v = go_atoi(raw)
+        if v is not None and v > 0:
+            return v
+    return default
+
+
+# VolumeFilter.FilterVolume / FilterPersistentVolume (predicates.go:458-507): (source key, id field)
+VOLUME_FILTERS = {"EBS": ("awsElasticBlockStore", "volumeID"), "GCE": ("gcePersistentDisk", "pdName"),
+                  "AzureDisk": ("azureDisk", "diskName")}
+
+
+class VolumeListers:
+    """PersistentVolumeInfo / PersistentVolumeClaimInfo: the simulator's PV / PVC informers are
+    empty (its store only ever holds nodes and pods, pkg/main.go:147-179), so by default every
+    lookup misses; tests pass the reference tests' fake listers (testing_helper.go:30-72)."""
+
+    def __init__(self, pvs=(), pvcs=(), classes=()):
+        self.pvs = {(x.get("metadata") or {}).get("name", ""): x for x in pvs}
+        self.pvcs = {((x.get("metadata") or {}).get("namespace", ""), (x.get("metadata") or {}).get("name", "")): x
+                     for x in pvcs}
+        self.classes = {(x.get("metadata") or {}).get("name", ""): x for x in classes}
+
+    def pvc(self, ns, name):
+        return self.pvcs.get((ns, name))
+
+    def pv(self, name):
+        return self.pvs.get(name)
+
+
+PV_ID_PREFIX = "ksim-random-prefix"   # rand.String(32) in the reference; any value no real id uses
+
+
+class MaxPDVolumeCountChecker:
+    """MaxPDVolumeCountChecker (predicates.go:287-456)."""
+
+    def __init__(self, filter_name, listers=None, max_vols=None):
+        self.kind, self.field = VOLUME_FILTERS[filter_name]
+        self.max_vols = get_max_vols(DEFAULT_MAX_VOLS[filter_name]) if max_vols is None else max_vols
+        self.listers = listers or VolumeListers()
+
+    def _filter(self, src):
+        s = src.get(self.kind)
+        return (s.get(self.field, ""), True) if s is not None else ("", False)
+
+    def filter_volumes(self, volumes, namespace, out):
+        """filterVolumes (:361-413)."""
+        for vol in volumes:
+            vid, ok = self._filter(vol)
+            if ok:
+                out.add(vid)
+                continue
+            claim = vol.get("persistentVolumeClaim")
+            if claim is None:
+                continue
+            name = claim.get("claimName", "")
+            if name == "":
+                raise PredicateError("PersistentVolumeClaim had no name")
+            pv_id = "%s-%s/%s" % (PV_ID_PREFIX, namespace, name)
+            pvc = self.listers.pvc(namespace, name)
+            if pvc is None:
+                out.add(pv_id)
+                continue
+            pv_name = (pvc.get("spec") or {}).get("volumeName", "")
+            if pv_name == "":
+                out.add(pv_id)
+                continue
+            pv = self.listers.pv(pv_name)
+            if pv is None:
+                out.add(pv_id)
+                continue
+            vid, ok = self._filter(pv.get("spec") or {})
+            if ok:
+                out.add(vid)
+
+    def predicate(self, pod, ni):
+        """predicate (:415-456)."""
+        vols = _volumes(pod)
+        if not vols:
+            return True, []
+        new = set()
+        self.filter_volumes(vols, (pod.get("metadata") or {}).get("namespace", ""), new)
+        if not new:
+            return True, []
+        existing = set()
+        for ep in ni.pods:
+            self.filter_volumes(_volumes(ep), (ep.get("metadata") or {}).get("namespace", ""), existing)
+        if len(existing) + len(new - existing) > self.max_vols:
+            return False, [R_MAX_VOLUME_COUNT]
+        return True, []
+
+
+def label_zones_to_set(v):
+    """volumeutil.LabelZonesToSet (pkg/volume/util/util.go:357-376); None on a parse error."""
+    out = set()
+    for z in v.split("__"):
+        t = z.strip(" \t\n\r\v\f")
+        if t == "":
+            return None
+        out.add(t)
+    return out
+
+
+def new_volume_zone_predicate(listers=None, volume_scheduling=True):
+    """VolumeZoneChecker.predicate (predicates.go:539-633).  volume_scheduling: the
+    VolumeScheduling feature gate (beta, on by default in v1.10: kube_features.go:309)."""
+    listers = listers or VolumeListers()
+
+    def pred(pod, ni):
+        vols = _volumes(pod)
+        if not vols:
+            return True, []
+        node = ni.node
+        if node is None:
+            raise PredicateError("node not found")
+        cons = {k: v for k, v in ((node.get("metadata") or {}).get("labels") or {}).items()
+                if k in (ZONE_LABEL, REGION_LABEL)}
+        if not cons:
+            return True, []
+        ns = (pod.get("metadata") or {}).get("namespace", "")
+        for vol in vols:
+            claim = vol.get("persistentVolumeClaim")
+            if claim is None:
+                continue
+            name = claim.get("claimName", "")
+            if name == "":
+                raise PredicateError("PersistentVolumeClaim had no name")
+            pvc = listers.pvc(ns, name)
+            if pvc is None:
+                raise PredicateError("persistentvolumeclaim %r not found" % name)
+            pv_name = (pvc.get("spec") or {}).get("volumeName", "")
+            if pv_name == "":
+                if volume_scheduling:
+                    sc = (pvc.get("spec") or {}).get("storageClassName")
+                    if sc:
+                        cls = listers.classes.get(sc)
+                        if cls is not None:
+                            mode = cls.get("volumeBindingMode")
+                            if mode is None:
+                                raise PredicateError("VolumeBindingMode not set for StorageClass %r" % sc)
+                            if mode == "WaitForFirstConsumer":
+                                continue
+                raise PredicateError("PersistentVolumeClaim is not bound: %r" % name)
+            pv = listers.pv(pv_name)
+            if pv is None:
+                raise PredicateError("PersistentVolume not found: %r" % pv_name)
+            for k, v in ((pv.get("metadata") or {}).get("labels") or {}).items():
+                if k not in (ZONE_LABEL, REGION_LABEL):
+                    continue
+                zones = label_zones_to_set(v)
+                if zones is None:
+                    continue   # unparsable label: ignored (:619-622)
+                if cons.get(k, "") not in zones:
+                    return False, [R_VOLUME_ZONE]
+        return True, []
+    return pred
+
+
+def new_volume_binding_predicate(listers=None):
+    """VolumeBindingChecker.predicate (predicates.go:1586-1618) with the VolumeScheduling gate on:
+    FindPodVolumes (scheduler_binder.go:127-167, getPodVolumes :290-320).  A PVC the listers do not
+    hold, or an unbound one without a WaitForFirstConsumer class, is an error; a bound PVC checks
+    its PV's node affinity, which only PVs without one satisfy here (others: PredicateError, the
+    outside-the-supported-set marker)."""
+    listers = listers or VolumeListers()
+
+    def pred(pod, ni):
+        if ni.node is None:
+            raise PredicateError("node not found")
+        ns = (pod.get("metadata") or {}).get("namespace", "")
+        for vol in _volumes(pod):
+            claim = vol.get("persistentVolumeClaim")
+            if claim is None:
+                continue
+            pvc = listers.pvc(ns, claim.get("claimName", ""))
+            if pvc is None:
+                raise PredicateError("error getting PVC %r" % claim.get("claimName", ""))
+            pv = listers.pv((pvc.get("spec") or {}).get("volumeName", ""))
+            if pv is None or (pv.get("spec") or {}).get("nodeAffinity") is not None:
+                raise PredicateError("volume binding outside the restated cases")
+        return True, []
+    return pred
+
+
+def volume_predicates(listers=None, max_vols=None):
+    """The volume predicates over `listers`, by key (custom_predicates form); max_vols: a
+    KUBE_MAX_PD_VOLS value (None: the environment's)."""
+    out = {"NoDiskConflict": pred_no_disk_conflict,
+           "NoVolumeZoneConflict": new_volume_zone_predicate(listers),
+           "CheckVolumeBinding": new_volume_binding_predicate(listers)}
+    for key, f in (("MaxEBSVolumeCount", "EBS"), ("MaxGCEPDVolumeCount", "GCE"),
+                   ("MaxAzureDiskVolumeCount", "AzureDisk")):
+        mv = None if max_vols is None else get_max_vols(DEFAULT_MAX_VOLS[f], str(max_vols))
+        out[key] = MaxPDVolumeCountChecker(f, listers, mv).predicate
+    return out
+
+
 PREDICATES = {
     "CheckNodeCondition": pred_check_node_condition,
     "CheckNodeUnschedulable": pred_check_node_unschedulable,
@@ -652,14 +932,15 @@ PREDICATES = {
     "PodFitsPorts": pred_pod_fits_host_ports,
     "MatchNodeSelector": pred_match_node_selector,
     "PodFitsResources": pred_pod_fits_resources,
-    "NoDiskConflict": pred_true,
+    "NoDiskConflict": pred_no_disk_conflict,
     "PodToleratesNodeTaints": pred_tolerates_taints,
     "PodToleratesNodeNoExecuteTaints": pred_tolerates_noexec_taints,
-    "MaxEBSVolumeCount": pred_true,
-    "MaxGCEPDVolumeCount": pred_true,
-    "MaxAzureDiskVolumeCount": pred_true,
-    "CheckVolumeBinding": pred_true,
-    "NoVolumeZoneConflict": pred_true,
+    # the simulator's (empty) PV / PVC listers; volume_predicates() builds them over others
+    "MaxEBSVolumeCount": MaxPDVolumeCountChecker("EBS").predicate,
+    "MaxGCEPDVolumeCount": MaxPDVolumeCountChecker("GCE").predicate,
+    "MaxAzureDiskVolumeCount": MaxPDVolumeCountChecker("AzureDisk").predicate,
+    "CheckVolumeBinding": new_volume_binding_predicate(),
+    "NoVolumeZoneConflict": new_volume_zone_predicate(),
     "CheckNodeMemoryPressure": pred_memory_pressure,
     "CheckNodeDiskPressure": pred_disk_pressure,
     "MatchInterPodAffinity": pred_true,   # replaced per scheduling cycle (GenericScheduler.schedule)

@@ -759,6 +759,133 @@ def interpod_cases():
                                         "expect": {h["host"]: h["score"] for h in c["expectedList"]}})
 
 
+
+# ------------------------------------------------ volumes (predicates_test.go:669-891, 1622-2039, 3676-3913)
+def vpod(vols, ns=None, name=None):
+    md = {}
+    if ns is not None:
+        md["namespace"] = ns
+    if name is not None:
+        md["name"] = name
+    return {"metadata": md, "spec": {"volumes": vols}}
+
+
+def vol_case(pred, src, test, p, existing, fits, reasons, node=None, pvs=(), pvcs=(), max_vols=None):
+    n = node if node is not None else {"metadata": {"name": "node"}}
+    ex = []
+    for k, e in enumerate(existing):
+        e = json.loads(json.dumps(e))
+        e["metadata"].setdefault("name", "existing-%d" % k)
+        e["spec"]["nodeName"] = n["metadata"].get("name", "")
+        ex.append(e)
+    add("volumes", {"source": src, "test": test, "predicate": pred, "pod": p, "node": n, "pods": ex,
+                    "pvs": list(pvs), "pvcs": list(pvcs), "max_vols": max_vols, "fits": fits,
+                    "reasons": list(reasons) if not fits else []})
+
+
+PT = S + "algorithm/predicates/predicates_test.go"
+DC = "node(s) had no available disk"
+for fn, line, k, field, a, b in (
+        ("TestGCEDiskConflicts", 669, "gcePersistentDisk", "pdName", "foo", "bar"),
+        ("TestAWSDiskConflicts", 722, "awsElasticBlockStore", "volumeID", "foo", "bar"),
+        ("TestISCSIDiskConflicts", 834, "iscsi", "iqn", "iqn.2016-12.server:storage.target01",
+         "iqn.2017-12.server:storage.target01")):
+    extra = {"targetPortal": "127.0.0.1:3260", "fsType": "ext4", "lun": 0} if k == "iscsi" else {}
+    vs1 = [{k: dict(extra, **{field: a})}]
+    vs2 = [{k: dict(extra, **{field: b})}]
+    base = line + 29 if k != "iscsi" else line + 35
+    vol_case("NoDiskConflict", "%s:%d" % (PT, base), fn + " nothing", vpod([]), [], True, [])
+    vol_case("NoDiskConflict", "%s:%d" % (PT, base + 1), fn + " one state", vpod([]), [vpod(vs1)], True, [])
+    vol_case("NoDiskConflict", "%s:%d" % (PT, base + 2), fn + " same state", vpod(vs1), [vpod(vs1)], False, [DC])
+    vol_case("NoDiskConflict", "%s:%d" % (PT, base + 3), fn + " different state", vpod(vs2), [vpod(vs1)], True, [])
+rbd1 = [{"rbd": {"monitors": ["a", "b"], "pool": "foo", "image": "bar", "fsType": "ext4"}}]
+rbd2 = [{"rbd": {"monitors": ["c", "d"], "pool": "foo", "image": "bar", "fsType": "ext4"}}]
+vol_case("NoDiskConflict", PT + ":810", "TestRBDDiskConflicts nothing", vpod([]), [], True, [])
+vol_case("NoDiskConflict", PT + ":811", "TestRBDDiskConflicts one state", vpod([]), [vpod(rbd1)], True, [])
+vol_case("NoDiskConflict", PT + ":812", "TestRBDDiskConflicts same state", vpod(rbd1), [vpod(rbd1)], False, [DC])
+vol_case("NoDiskConflict", PT + ":813", "TestRBDDiskConflicts different state", vpod(rbd2), [vpod(rbd1)], True, [])
+
+# TestEBSVolumeCountConflicts (:1622-2039): pods :1623-1828, fake listers :1979-2021
+ebs = lambda i: {"awsElasticBlockStore": {"volumeID": i}}
+pvc = lambda c: {"persistentVolumeClaim": {"claimName": c}}
+hostpath = {"hostPath": {}}
+EV = {"oneVolPod": vpod([ebs("ovp")]), "ebsPVCPod": vpod([pvc("someEBSVol")]),
+      "splitPVCPod": vpod([pvc("someNonEBSVol"), pvc("someEBSVol")]), "twoVolPod": vpod([ebs("tvp1"), ebs("tvp2")]),
+      "splitVolsPod": vpod([hostpath, ebs("svp")]), "nonApplicablePod": vpod([hostpath]),
+      "deletedPVCPod": vpod([pvc("deletedPVC")]), "twoDeletedPVCPod": vpod([pvc("deletedPVC"), pvc("anotherDeletedPVC")]),
+      "deletedPVPod": vpod([pvc("pvcWithDeletedPV")]), "deletedPVPod2": vpod([pvc("pvcWithDeletedPV")]),
+      "anotherDeletedPVPod": vpod([pvc("anotherPVCWithDeletedPV")]), "emptyPod": vpod([]),
+      "unboundPVCPod": vpod([pvc("unboundPVC")]), "unboundPVCPod2": vpod([pvc("unboundPVC")]),
+      "anotherUnboundPVCPod": vpod([pvc("anotherUnboundPVC")])}
+EBS_PVS = [{"metadata": {"name": "someEBSVol"}, "spec": {"awsElasticBlockStore": {"volumeID": "ebsVol"}}},
+           {"metadata": {"name": "someNonEBSVol"}, "spec": {}}]
+EBS_PVCS = [{"metadata": {"name": n}, "spec": {"volumeName": v}} for n, v in (
+    ("someEBSVol", "someEBSVol"), ("someNonEBSVol", "someNonEBSVol"), ("pvcWithDeletedPV", "pvcWithDeletedPV"),
+    ("anotherPVCWithDeletedPV", "anotherPVCWithDeletedPV"), ("unboundPVC", ""), ("anotherUnboundPVC", ""))]
+MV = "node(s) exceed max volume count"
+for line, new, existing, mv, fits, test in (
+        (1837, "oneVolPod", ["twoVolPod", "oneVolPod"], 4, True, "fits when node capacity >= new pod's EBS volumes"),
+        (1844, "twoVolPod", ["oneVolPod"], 2, False, "doesn't fit when node capacity < new pod's EBS volumes"),
+        (1851, "splitVolsPod", ["twoVolPod"], 3, True, "new pod's count ignores non-EBS volumes"),
+        (1858, "twoVolPod", ["splitVolsPod", "nonApplicablePod", "emptyPod"], 3, True,
+         "existing pods' counts ignore non-EBS volumes"),
+        (1865, "ebsPVCPod", ["splitVolsPod", "nonApplicablePod", "emptyPod"], 3, True,
+         "new pod's count considers PVCs backed by EBS volumes"),
+        (1872, "splitPVCPod", ["splitVolsPod", "oneVolPod"], 3, True, "new pod's count ignores PVCs not backed by EBS volumes"),
+        (1879, "twoVolPod", ["oneVolPod", "ebsPVCPod"], 3, False, "existing pods' counts considers PVCs backed by EBS volumes"),
+        (1886, "twoVolPod", ["oneVolPod", "twoVolPod", "ebsPVCPod"], 4, True, "already-mounted EBS volumes are always ok to allow"),
+        (1893, "splitVolsPod", ["oneVolPod", "oneVolPod", "ebsPVCPod"], 3, True, "the same EBS volumes are not counted multiple times"),
+        (1900, "ebsPVCPod", ["oneVolPod", "deletedPVCPod"], 2, False, "pod with missing PVC is counted towards the PV limit"),
+        (1907, "ebsPVCPod", ["oneVolPod", "deletedPVCPod"], 3, True, "pod with missing PVC is counted towards the PV limit"),
+        (1914, "ebsPVCPod", ["oneVolPod", "twoDeletedPVCPod"], 3, False, "pod with missing two PVCs is counted towards the PV limit twice"),
+        (1921, "ebsPVCPod", ["oneVolPod", "deletedPVPod"], 2, False, "pod with missing PV is counted towards the PV limit"),
+        (1928, "ebsPVCPod", ["oneVolPod", "deletedPVPod"], 3, True, "pod with missing PV is counted towards the PV limit"),
+        (1935, "deletedPVPod2", ["oneVolPod", "deletedPVPod"], 2, True,
+         "two pods missing the same PV are counted towards the PV limit only once"),
+        (1942, "anotherDeletedPVPod", ["oneVolPod", "deletedPVPod"], 2, False,
+         "two pods missing different PVs are counted towards the PV limit twice"),
+        (1949, "ebsPVCPod", ["oneVolPod", "unboundPVCPod"], 2, False, "pod with unbound PVC is counted towards the PV limit"),
+        (1956, "ebsPVCPod", ["oneVolPod", "unboundPVCPod"], 3, True, "pod with unbound PVC is counted towards the PV limit"),
+        (1963, "unboundPVCPod2", ["oneVolPod", "unboundPVCPod"], 2, True,
+         "the same unbound PVC in multiple pods is counted towards the PV limit only once"),
+        (1970, "anotherUnboundPVCPod", ["oneVolPod", "unboundPVCPod"], 2, False,
+         "two different unbound PVCs are counted towards the PV limit as two volumes")):
+    vol_case("MaxEBSVolumeCount", "%s:%d" % (PT, line), test, EV[new], [EV[e] for e in existing], fits, [MV],
+             pvs=EBS_PVS, pvcs=EBS_PVCS, max_vols=mv)
+
+# TestVolumeZonePredicate / ...MultiZone (:3694-3913); createPodWithVolume :3676-3692
+ZK, RK = "failure-domain.beta.kubernetes.io/zone", "failure-domain.beta.kubernetes.io/region"
+VZ = "node(s) had no available volume zone"
+zpvcs = [{"metadata": {"name": "PVC_%d" % i, "namespace": "default"}, "spec": {"volumeName": v}}
+         for i, v in ((1, "Vol_1"), (2, "Vol_2"), (3, "Vol_3"), (4, "Vol_not_exist"))]
+cpv = lambda pod_name, pv, c: {"metadata": {"name": pod_name, "namespace": "default"},
+                               "spec": {"volumes": [{"name": pv, "persistentVolumeClaim": {"claimName": c}}]}}
+znode = lambda labels: {"metadata": dict({"name": "host1"}, **({"labels": labels} if labels else {}))}
+zpvs1 = [{"metadata": {"name": "Vol_1", "labels": {ZK: "us-west1-a"}}},
+         {"metadata": {"name": "Vol_2", "labels": {RK: "us-west1-b", "uselessLabel": "none"}}},
+         {"metadata": {"name": "Vol_3", "labels": {RK: "us-west1-c"}}}]
+for line, test, p, labels, fits in (
+        (3732, "pod without volume", {"metadata": {"name": "pod_1", "namespace": "default"}, "spec": {}}, {ZK: "us-west1-a"}, True),
+        (3745, "node without labels", cpv("pod_1", "vol_1", "PVC_1"), None, True),
+        (3755, "label zone failure domain matched", cpv("pod_1", "vol_1", "PVC_1"), {ZK: "us-west1-a", "uselessLabel": "none"}, True),
+        (3766, "label zone region matched", cpv("pod_1", "vol_1", "PVC_2"), {RK: "us-west1-b", "uselessLabel": "none"}, True),
+        (3777, "label zone region failed match", cpv("pod_1", "vol_1", "PVC_2"), {RK: "no_us-west1-b", "uselessLabel": "none"}, False),
+        (3788, "label zone failure domain failed match", cpv("pod_1", "vol_1", "PVC_1"),
+         {ZK: "no_us-west1-a", "uselessLabel": "none"}, False)):
+    vol_case("NoVolumeZoneConflict", "%s:%d" % (PT, line), test, p, [], fits, [VZ], node=znode(labels), pvs=zpvs1,
+             pvcs=zpvcs)
+zpvs2 = [{"metadata": {"name": "Vol_1", "labels": {ZK: "us-west1-a"}}},
+         {"metadata": {"name": "Vol_2", "labels": {ZK: "us-west1-b", "uselessLabel": "none"}}},
+         {"metadata": {"name": "Vol_3", "labels": {ZK: "us-west1-c__us-west1-a"}}}]
+for line, test, p, labels, fits in (
+        (3860, "multi-zone node without labels", cpv("pod_1", "Vol_3", "PVC_3"), None, True),
+        (3870, "multi-zone label zone failure domain matched", cpv("pod_1", "Vol_3", "PVC_3"),
+         {ZK: "us-west1-a", "uselessLabel": "none"}, True),
+        (3881, "multi-zone label zone failure domain failed match", cpv("pod_1", "vol_1", "PVC_1"),
+         {ZK: "us-west1-b", "uselessLabel": "none"}, False)):
+    vol_case("NoVolumeZoneConflict", "%s:%d" % (PT, line), test, p, [], fits, [VZ], node=znode(labels), pvs=zpvs2,
+             pvcs=zpvcs)
+
 if os.path.isdir(REF):
     interpod_cases()
 else:  # keep the committed fixtures when the reference checkout is absent

@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     for f in fns:
         assert hasattr(L, f), f
     assert sorted(fns) == sorted(abi.EXPORTS)
-    assert L.ksim_abi_version() == abi.ABI_VERSION == 4
+    assert L.ksim_abi_version() == abi.ABI_VERSION == 5
 
 
 def test_create_without_device_fails_loudly():
@@ -145,9 +145,20 @@ def test_unsupported_pods_rejected():
     r = {"metadata": {"name": "r"}, "spec": {"nodeName": "gone"}}                      # bound to an unknown node
     with pytest.raises(abi.KsimUnsupported):
         ingest.Cluster.from_objects(n, [r], [p])
+    # a PVC the simulator's empty listers cannot resolve: MaxPD counts it, but CheckVolumeBinding
+    # errs (scheduler_binder.go:290-320) and so does VolumeZone on a zone-labelled node
     p = {"metadata": {"name": "p"}, "spec": {"volumes": [{"persistentVolumeClaim": {"claimName": "c"}}]}}
+    cl = ingest.Cluster.from_objects(n, [], [p])
+    assert cl.pods["vol_class"][0] == 1
     with pytest.raises(abi.KsimUnsupported):
-        ingest.Cluster.from_objects(n, [], [p])
+        scheduler.check_volume_support(cl, scheduler.provider("DefaultProvider")[0])
+    scheduler.check_volume_support(cl, ["NoDiskConflict", "MaxEBSVolumeCount", "NoVolumeZoneConflict"])
+    zn = [dict(n[0], metadata={"name": "n", "labels": {"failure-domain.beta.kubernetes.io/zone": "z"}})]
+    with pytest.raises(abi.KsimUnsupported):
+        scheduler.check_volume_support(ingest.Cluster.from_objects(zn, [], [p]), ["NoVolumeZoneConflict"])
+    two = {"metadata": {"name": "p"}, "spec": {"volumes": [{"rbd": {}, "iscsi": {}}]}}
+    with pytest.raises(abi.KsimUnsupported):
+        ingest.Cluster.from_objects(n, [], [two])
 
 
 def test_fit_error_message_format():

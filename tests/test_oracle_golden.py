@@ -77,3 +77,44 @@ def test_fit_error_message():
     msg = str(R.FitError(c["num_nodes"], c["failed"]))
     for s in c["contains"]:
         assert s in msg
+
+
+@pytest.mark.parametrize("c", load("volumes"), ids=case_id)
+def test_volume_predicate(c):
+    """NoDiskConflict / MaxEBSVolumeCount / NoVolumeZoneConflict over the Go tests' fake PV / PVC
+    listers (predicates_test.go:669-891, 1622-2039, 3694-3913)."""
+    ni = R.NodeInfo(c["node"])
+    for p in c["pods"]:
+        ni.add_pod(p)
+    preds = R.volume_predicates(R.VolumeListers(c["pvs"], c["pvcs"]), c["max_vols"])
+    ok, reasons = preds[c["predicate"]](c["pod"], ni)
+    assert ok == c["fits"]
+    assert reasons == c["reasons"]
+
+
+def test_get_max_vols():
+    """TestGetMaxVols (predicates_test.go:4039-4083): the env value when it parses to a positive
+    int, else the default."""
+    assert R.get_max_vols(39, "") == 39
+    assert R.get_max_vols(39, "2") == 2
+    assert R.get_max_vols(39, "invalid") == 39
+    assert R.get_max_vols(39, "-2") == 39
+    assert R.get_max_vols(39, "0") == 39
+    assert R.get_max_vols(39, "40") == 40
+
+
+def test_volume_error_paths():
+    """A PVC the simulator's (empty) listers cannot resolve: MaxPD counts it, VolumeZone errors on a
+    zone-labelled node, VolumeBinding errors everywhere (predicates.go:376-383, 575-578, 1597-1600)."""
+    p = {"metadata": {"name": "p", "namespace": "ns"}, "spec": {"volumes": [{"persistentVolumeClaim": {"claimName": "c"}}]}}
+    plain = R.NodeInfo({"metadata": {"name": "a"}})
+    zoned = R.NodeInfo({"metadata": {"name": "b", "labels": {R.ZONE_LABEL: "z1"}}})
+    assert R.PREDICATES["MaxEBSVolumeCount"](p, plain) == (True, [])
+    assert R.PREDICATES["NoVolumeZoneConflict"](p, plain) == (True, [])
+    with pytest.raises(R.PredicateError):
+        R.PREDICATES["NoVolumeZoneConflict"](p, zoned)
+    with pytest.raises(R.PredicateError):
+        R.PREDICATES["CheckVolumeBinding"](p, plain)
+    noname = {"metadata": {}, "spec": {"volumes": [{"persistentVolumeClaim": {"claimName": ""}}]}}
+    with pytest.raises(R.PredicateError):
+        R.PREDICATES["MaxGCEPDVolumeCount"](noname, plain)

@@ -226,3 +226,68 @@ def rnd_affinity_workload(seed, n_nodes=20, n_pods=80, n_running=12, p_aff=0.6, 
         running.append(p)
     pods = [rnd_affinity_pod(rng, "sim-%d" % k, p_aff, resources) for k in range(n_pods)]
     return nodes, running, pods
+
+
+ZONE = "failure-domain.beta.kubernetes.io/zone"
+
+
+def volume_listers(resolvable_only=False):
+    """PVs / PVCs in namespace "ns": c1 → EBS PV, c2 → GCE PV (zones a, b), c6 → Azure PV,
+    c7 → NFS-like PV (counted by no filter, zone c); unless resolvable_only: c3 unbound, c4 bound to
+    a missing PV, c5 absent (MaxPD counts all three as their own ids)."""
+    pvs = [{"metadata": {"name": "pv-ebs"}, "spec": {"awsElasticBlockStore": {"volumeID": "e1"}}},
+           {"metadata": {"name": "pv-gce", "labels": {ZONE: "a__b"}}, "spec": {"gcePersistentDisk": {"pdName": "g1"}}},
+           {"metadata": {"name": "pv-az"}, "spec": {"azureDisk": {"diskName": "a1"}}},
+           {"metadata": {"name": "pv-nfs", "labels": {ZONE: "c"}}, "spec": {"nfs": {"server": "s"}}}]
+    pvcs = [{"metadata": {"name": n, "namespace": "ns"}, "spec": {"volumeName": v}}
+            for n, v in (("c1", "pv-ebs"), ("c2", "pv-gce"), ("c6", "pv-az"), ("c7", "pv-nfs"))]
+    claims = ["c1", "c2", "c6", "c7"]
+    if not resolvable_only:
+        pvcs += [{"metadata": {"name": "c3", "namespace": "ns"}, "spec": {"volumeName": ""}},
+                 {"metadata": {"name": "c4", "namespace": "ns"}, "spec": {"volumeName": "gone"}}]
+        claims += ["c3", "c4", "c5"]
+    return pvs, pvcs, claims
+
+
+def rnd_volume(rng, claims, ids=("d1", "d2", "d3", "d4", "d5", "d6", "e1", "g1")):
+    k = rng.random()
+    ro = rng.random() < 0.4
+    nm = rng.choice(ids)
+    if k < 0.2:
+        return {"gcePersistentDisk": {"pdName": nm, "readOnly": ro}}
+    if k < 0.4:
+        return {"awsElasticBlockStore": {"volumeID": nm, "readOnly": ro}}
+    if k < 0.5:
+        return {"iscsi": {"iqn": nm, "readOnly": ro, "targetPortal": "10.0.0.1:3260"}}
+    if k < 0.6:
+        return {"rbd": {"monitors": rng.sample(["m1", "m2", "m3"], rng.randint(1, 2)), "pool": "rbd", "image": nm,
+                        "readOnly": ro}}
+    if k < 0.7:
+        return {"azureDisk": {"diskName": nm, "diskURI": "uri"}}
+    if k < 0.9:
+        return {"persistentVolumeClaim": {"claimName": rng.choice(claims)}}
+    return {"emptyDir": {}}
+
+
+def rnd_volume_workload(seed, n_nodes=16, n_pods=120, n_running=14, zones=False, resolvable_only=False, p_vol=0.7):
+    """Nodes (optionally zone-labelled), running and queued pods in namespace "ns" mixing every
+    volume kind the volume predicates read, with the listers they resolve through."""
+    rng = random.Random(1000 + seed)
+    nodes = rnd_nodes(rng, n_nodes, features=False)
+    for x in nodes:
+        x["status"]["allocatable"]["pods"] = "110"
+        if zones and rng.random() < 0.7:
+            x["metadata"]["labels"][ZONE] = rng.choice(["a", "b", "c"])
+    pvs, pvcs, claims = volume_listers(resolvable_only)
+
+    def pod(name, nn=None):
+        p = rnd_pod(rng, name, features=False)
+        p["metadata"]["namespace"] = "ns"
+        if rng.random() < p_vol:
+            p["spec"]["volumes"] = [rnd_volume(rng, claims) for _ in range(rng.randint(1, 3))]
+        if nn:
+            p["spec"]["nodeName"] = nn
+        return p
+    running = [pod("run-%d" % k, rng.choice(nodes)["metadata"]["name"]) for k in range(n_running)]
+    pods = [pod("pod-%d" % k) for k in range(n_pods)]
+    return nodes, running, pods, pvs, pvcs
