@@ -39,7 +39,7 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
     if (cfg->weights[k] < 0) return ksim_fail(nullptr, KSIM_E_INVAL, "ksim_create: negative weight in slot %d", k);
   if (cfg->mode < KSIM_MODE_AUTO || cfg->mode > KSIM_MODE_TREE)
     return ksim_fail(nullptr, KSIM_E_INVAL, "ksim_create: unknown mode %d", cfg->mode);
-  const uint32_t known = (1u << 13) - 1;
+  const uint32_t known = (1u << 18) - 1;  // KSIM_P_CHECK_NODE_CONDITION .. KSIM_P_VOLUME_ZONE
   if (cfg->predicates & ~known) return ksim_fail(nullptr, KSIM_E_UNSUPPORTED, "ksim_create: unknown predicate bits");
   ksim_handle* h = new ksim_handle();
   h->device = cfg->device;
