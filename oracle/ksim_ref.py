@@ -1341,6 +1341,72 @@ def spread_reduce(scores, zones):
     return out
 
 
+class SpreadListers:
+    """ServiceLister / ControllerLister / ReplicaSetLister / StatefulSetLister as the scheduler's
+    informer-backed listers answer (client-go listers core/v1/service_expansion.go:36-56,
+    replicationcontroller_expansion.go:39-66, extensions/v1beta1/replicaset_expansion.go:41-73,
+    apps/v1beta1/statefulset_expansion.go:41-80).  The simulator's are empty: its store holds no
+    services and its controller informers are fake (pkg/scheduler/simulator.go:352-367)."""
+
+    def __init__(self, services=(), rcs=(), rss=(), sss=()):
+        self.services, self.rcs, self.rss, self.sss = list(services), list(rcs), list(rss), list(sss)
+
+    @staticmethod
+    def _set_matches(sel, lab):
+        """labels.Set(sel).AsSelectorPreValidated().Matches."""
+        return all(k in lab and lab[k] == v for k, v in sel.items())
+
+    def selectors(self, pod, services_only=False):
+        """getSelectors (priorities/metadata.go:82-114): the selectors of the services, RCs, RSs and
+        StatefulSets selecting the pod (a lister error contributes nothing)."""
+        md = pod.get("metadata") or {}
+        ns, lab = md.get("namespace", ""), md.get("labels") or {}
+        out = []
+        for svc in self.services:
+            sel = (svc.get("spec") or {}).get("selector")
+            if (svc.get("metadata") or {}).get("namespace", "") != ns or sel is None:
+                continue
+            if self._set_matches(sel, lab):
+                out.append(selector_from_set(sel))
+        if services_only or not lab:
+            return out            # the controller listers err for a pod without labels
+        for rc in self.rcs:
+            sel = (rc.get("spec") or {}).get("selector") or {}
+            if (rc.get("metadata") or {}).get("namespace", "") == ns and sel and self._set_matches(sel, lab):
+                out.append(selector_from_set(sel))
+        for objs in (self.rss, self.sss):
+            found = []
+            try:
+                for o in objs:
+                    if (o.get("metadata") or {}).get("namespace", "") != ns:
+                        continue
+                    sel = label_selector_as_selector((o.get("spec") or {}).get("selector"))
+                    if sel is NOTHING or sel == [] or not selector_matches(sel, lab):
+                        continue      # nil / empty selectors match nothing here
+                    found.append(sel)
+            except AffinityError:
+                found = []            # an invalid selector fails the whole lookup
+            out.extend(found)
+        return out
+
+
+def selector_spread_map(pod, ni, selectors):
+    """CalculateSpreadPriorityMap (selector_spreading.go:66-114): placed pods of the node in the
+    pod's namespace, not being deleted, matching any of the selectors."""
+    if not selectors:
+        return 0
+    ns = (pod.get("metadata") or {}).get("namespace", "")
+    count = 0
+    for q in ni.pods:
+        md = q.get("metadata") or {}
+        if md.get("namespace", "") != ns or md.get("deletionTimestamp") is not None:
+            continue
+        lab = md.get("labels") or {}
+        if any(selector_matches(sel, lab) for sel in selectors):
+            count += 1
+    return count
+
+
 def zone_key(node):
     """K/pkg/util/node GetZoneKey: region:\\x00:zone from failure-domain labels."""
     labels = (node.get("metadata") or {}).get("labels") or {}
@@ -1502,9 +1568,10 @@ def prio_image_locality(pod, ni):
 PRIORITIES["ImageLocalityPriority"] = ("map", prio_image_locality)
 
 
-def prioritize_nodes(pod, infos, configs, all_infos=None, hard_weight=10):
+def prioritize_nodes(pod, infos, configs, all_infos=None, hard_weight=10, spread=None):
     """S/core/generic_scheduler.go:542-676.  configs: list of (name, weight); infos: the
-    filtered nodes; all_infos: nodeNameToInfo (InterPodAffinityPriority reads every pod)."""
+    filtered nodes; all_infos: nodeNameToInfo (InterPodAffinityPriority reads every pod);
+    spread: SpreadListers for SelectorSpread / ServiceSpreading (None: the simulator's empty ones)."""
     if not configs:
         return [1 for _ in infos]          # EqualPriorityMap
     total = [0] * len(infos)
@@ -1513,6 +1580,11 @@ def prioritize_nodes(pod, infos, configs, all_infos=None, hard_weight=10):
         if kind == "ipa":
             scores = interpod_affinity_priority(pod, all_infos if all_infos is not None else infos,
                                                 [ni.node for ni in infos], hard_weight)
+        elif kind == "spread":
+            # ServiceSpreadingPriority: services only (factory/plugins.go registers it with empty
+            # controller listers, defaults.go:68-74)
+            sels = spread.selectors(pod, name == "ServiceSpreadingPriority") if spread is not None else []
+            scores = [selector_spread_map(pod, ni, sels) for ni in infos]
         else:
             scores = [fn(pod, ni) for ni in infos]
         if kind == "reduce-rev":
@@ -1570,8 +1642,9 @@ class FitError(Exception):
 
 
 class GenericScheduler:
-    def __init__(self, predicate_keys, priority_configs, custom_predicates=None, hard_weight=10):
+    def __init__(self, predicate_keys, priority_configs, custom_predicates=None, hard_weight=10, spread=None):
         self.predicates = set(predicate_keys) | set(MANDATORY_PREDICATES)
+        self.spread = spread              # SpreadListers (None: the simulator's empty listers)
         self.custom = dict(custom_predicates or {})
         self.prioritizers = list(priority_configs)
         self.hard_weight = hard_weight    # hardPodAffinitySymmetricWeight (simulator: 10)
@@ -1602,7 +1675,7 @@ class GenericScheduler:
             raise FitError(len(infos), failed)
         if len(filtered) == 1:
             return filtered[0].name
-        scores = prioritize_nodes(pod, filtered, self.prioritizers, infos, self.hard_weight)
+        scores = prioritize_nodes(pod, filtered, self.prioritizers, infos, self.hard_weight, self.spread)
         return self.select_host([(ni.name, s) for ni, s in zip(filtered, scores)])
 
     def select_host(self, plist):
@@ -1734,7 +1807,7 @@ def expand_simulation_pods(spec_list):
     return out
 
 
-def simulate(nodes, running_pods, sim_pods, predicate_keys, priority_configs, custom_predicates=None):
+def simulate(nodes, running_pods, sim_pods, predicate_keys, priority_configs, custom_predicates=None, spread=None):
     """Runs the ClusterCapacity loop: pods are popped LIFO (store.go:223-233),
     each is scheduled, bound pods are assumed into the node cache (scheduler.go:366
     → cache.go:125 → node_info.go:318), unschedulable pods are recorded and the
@@ -1746,7 +1819,7 @@ def simulate(nodes, running_pods, sim_pods, predicate_keys, priority_configs, cu
         nn = (p.get("spec") or {}).get("nodeName", "")
         if nn in by_name:
             by_name[nn].add_pod(p)
-    sched = GenericScheduler(predicate_keys, priority_configs, custom_predicates)
+    sched = GenericScheduler(predicate_keys, priority_configs, custom_predicates, spread=spread)
     queue = list(sim_pods)
     out = []
     while queue:

@@ -886,10 +886,63 @@ for line, test, p, labels, fits in (
     vol_case("NoVolumeZoneConflict", "%s:%d" % (PT, line), test, p, [], fits, [VZ], node=znode(labels), pvs=zpvs2,
              pvcs=zpvcs)
 
+
+def spread_cases():
+    """TestSelectorSpreadPriority / TestZoneSelectorSpreadPriority (selector_spreading_test.go:43-366,
+    375-812): services / RCs / RSs / StatefulSets selecting the pod, placed pods, expected scores."""
+    import go_literal as g
+    sf = S + "algorithm/priorities/selector_spreading_test.go"
+    with open(REF + sf) as f:
+        src = f.read()
+    zone_nodes = {"nodeMachine1Zone1": ("machine1.zone1", "zone1"), "nodeMachine1Zone2": ("machine1.zone2", "zone2"),
+                  "nodeMachine2Zone2": ("machine2.zone2", "zone2"), "nodeMachine1Zone3": ("machine1.zone3", "zone3"),
+                  "nodeMachine2Zone3": ("machine2.zone3", "zone3"), "nodeMachine3Zone3": ("machine3.zone3", "zone3")}
+    consts = {"metav1.NamespaceDefault": "default"}
+    consts.update({k: v[0] for k, v in zone_nodes.items()})
+
+    def res(x):
+        if isinstance(x, dict):
+            if "__ident__" in x:
+                return consts[x["__ident__"]]
+            if x.get("__call__") == "buildPod":
+                nn, lab, _ = (res(a) for a in x["args"])
+                pod = {"metadata": {"labels": lab or {}}, "spec": {}}
+                if nn:
+                    pod["spec"]["nodeName"] = nn
+                return pod
+            if x.get("__call__") == "new":
+                return {}
+            if x.get("__call__") == "controllerRef":
+                return None      # owner references play no part in getSelectors
+            if "__call__" in x:
+                raise ValueError(x)
+            return {k: res(v) for k, v in x.items()}
+        if isinstance(x, list):
+            return [res(v) for v in x]
+        return x
+    for fn in ("TestSelectorSpreadPriority", "TestZoneSelectorSpreadPriority"):
+        start = src.index("func %s(" % fn)
+        _, cs = g.parse_test(src, fn)
+        for c in cs:
+            c = res(c)
+            pod = c.get("pod") or {}
+            pod.setdefault("metadata", {})
+            if fn == "TestZoneSelectorSpreadPriority":
+                nodes = [{"metadata": {"name": nm, "labels": {"failure-domain.beta.kubernetes.io/zone": z}}}
+                         for nm, z in zone_nodes.values()]
+            else:
+                nodes = [{"metadata": {"name": nm}} for nm in c["nodes"]]
+            add("spread", {"source": "%s:%d" % (sf, _line_of(src, c["test"], start)), "test": c["test"],
+                           "pod": pod, "pods": c.get("pods") or [], "nodes": nodes,
+                           "services": c.get("services") or [], "rcs": c.get("rcs") or [], "rss": c.get("rss") or [],
+                           "sss": c.get("sss") or [],
+                           "expect": {h["host"]: h["score"] for h in c["expectedList"]}})
+
 if os.path.isdir(REF):
     interpod_cases()
+    spread_cases()
 else:  # keep the committed fixtures when the reference checkout is absent
-    for group in ("interpod_predicates", "interpod_priorities"):
+    for group in ("interpod_predicates", "interpod_priorities", "spread"):
         with open(os.path.join(HERE, group + ".json")) as f:
             cases[group] = json.load(f)
 

@@ -118,3 +118,13 @@ def test_volume_error_paths():
     noname = {"metadata": {}, "spec": {"volumes": [{"persistentVolumeClaim": {"claimName": ""}}]}}
     with pytest.raises(R.PredicateError):
         R.PREDICATES["MaxGCEPDVolumeCount"](noname, plain)
+
+
+@pytest.mark.parametrize("c", load("spread"), ids=case_id)
+def test_selector_spread(c):
+    """SelectorSpreadPriority over services / RCs / RSs / StatefulSets (selector_spreading_test.go:43-812),
+    every node listed (no predicates)."""
+    infos = _infos(c["nodes"], c["pods"])
+    listers = R.SpreadListers(c["services"], c["rcs"], c["rss"], c["sss"])
+    scores = R.prioritize_nodes(c["pod"], infos, [("SelectorSpreadPriority", 1)], spread=listers)
+    assert {ni.name: s for ni, s in zip(infos, scores)} == c["expect"]
