@@ -81,7 +81,10 @@ extern "C" {
 #define KSIM_W_NODE_AFFINITY 4       /* node_affinity.go:34 + NormalizeReduce(10,false) */
 #define KSIM_W_INTERPOD_AFFINITY 5   /* interpod_affinity.go:118-240 (0 everywhere without
                                         affinity tables or terms) */
-#define KSIM_NW 6
+#define KSIM_W_SELECTOR_SPREAD 6     /* SelectorSpreadPriority / ServiceSpreadingPriority
+                                        (selector_spreading.go:66-174) for pods whose affinity class
+                                        carries a spread pair; other pods score MaxPriority (constant) */
+#define KSIM_NW 7
 
 /* ---- node condition / dynamic flags (ksim_node_table.flags) ---- */
 #define KSIM_N_NOT_READY (1u << 0)      /* Ready condition present, status != True */
@@ -406,7 +409,7 @@ int ksim_append_pods(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const
  *    pods carrying it;
  *  - affinity classes: a pod's own terms (required affinity, then required anti-affinity, then
  *    preferred) and the carried amounts it brings; ac[a] = {req_off, req_cnt, pref_off, pref_cnt,
- *    carry_off, carry_cnt}.
+ *    carry_off, carry_cnt}; and its SelectorSpread pair (spread_pair[a]).
  * ksim_pod.aff_ident / aff_class hold 1 + the id (0 = none, so zero-initialised descriptors
  * take no part).  A pod with either set is scheduled by the launch-mode kernels, which apply
  * its counts on commit; the node events (ksim_node_add / update / remove) make the tables stale
@@ -443,7 +446,8 @@ typedef struct {
   int32_t hard_weight;             /* hardPodAffinitySymmetricWeight the carried amounts use */
   int32_t sel_words;               /* ceil(n_sel / 64) */
   int32_t carry_words;             /* ceil(n_carry / 64) */
-  int32_t pad;
+  int32_t zone_key;                /* key whose domains are the nodes' zones (utilnode.GetZoneKey), the
+                                      SelectorSpread reduce's countsByZone; -1: none */
   const int32_t* dom;              /* [n_keys][n_nodes] */
   const int32_t* n_dom;            /* [n_keys] */
   const uint64_t* ident_sel;       /* [n_ident][sel_words] */
@@ -460,6 +464,11 @@ typedef struct {
   const ksim_aff_carry* carries;   /* [n_carries] */
   const int32_t* cnt;              /* [cnt_len] counts of the pods already placed */
   const int64_t* carried;          /* [carried_len] */
+  /* SelectorSpread (selector_spreading.go:66-174): per affinity class the counted pair (s, key 1) of
+   * the class's spread selector — s matches the identities, in the pod's namespace and not being
+   * deleted, that any of the pod's service / RC / RS / StatefulSet selectors selects — or -1;
+   * NULL: no class spreads. */
+  const int32_t* spread_pair;      /* [n_aclass] */
 } ksim_affinity_tables;
 
 /* Load (or replace) the affinity tables; the counts describe the pods already placed. */

@@ -86,6 +86,15 @@ int validate(ksim_handle* h, const ksim_affinity_tables* t) {
       if (t->terms[j].kind != KSIM_AFF_PREFERRED)
         return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: class %d lists a required term among its preferred ones", a);
   }
+  if (t->zone_key < -1 || t->zone_key >= t->n_keys)
+    return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: zone key out of range");
+  if (t->spread_pair)
+    for (int32_t a = 0; a < t->n_aclass; ++a) {
+      const int32_t c = t->spread_pair[a];
+      // the scan reads the pair's count at the node's own index: it must be on the node pseudo key
+      if (c < -1 || c >= t->n_pair || (c >= 0 && t->pair_key[c] != 1))
+        return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: class %d spread pair out of range", a);
+    }
   for (size_t q = 0; q < h->q_ident.size(); ++q)
     if (h->q_ident[q] > t->n_ident || h->q_aclass[q] > t->n_aclass)
       return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: queued pod %zu uses an identity / class beyond the tables", q);
@@ -106,7 +115,8 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
   KsimAff A{};
   int32_t *dom, *ps, *pk, *ck, *ac, *cnt;
   uint64_t *is, *ia, *ip;
-  int64_t *po, *co, *carried, *mm, *part;
+  int64_t *po, *co, *carried, *mm, *part, *zsum, *zread;
+  int32_t* spair = nullptr;
   ksim_aff_term* terms;
   ksim_aff_carry* carries;
   uint32_t* ticket;
@@ -119,10 +129,15 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
       (rc = dev_upload(h, &co, t->carry_off, t->n_carry)) || (rc = dev_upload(h, &ac, t->ac, 6 * (size_t)t->n_aclass)) ||
       (rc = dev_upload(h, &terms, t->terms, t->n_terms)) || (rc = dev_upload(h, &carries, t->carries, t->n_carries)) ||
       (rc = dev_upload(h, &cnt, t->cnt, t->cnt_len)) || (rc = dev_upload(h, &carried, t->carried, t->carried_len)) ||
-      (rc = dev_upload<int64_t>(h, &mm, nullptr, 2)) || (rc = dev_upload<int64_t>(h, &part, nullptr, 2 * (size_t)grid_max)) ||
+      (rc = dev_upload<int64_t>(h, &mm, nullptr, 5)) || (rc = dev_upload<int64_t>(h, &part, nullptr, 4 * (size_t)grid_max)) ||
       (rc = dev_upload<uint32_t>(h, &ticket, nullptr, 4)))
     return rc;
+  const int32_t n_zone = t->zone_key >= 0 ? t->n_dom[t->zone_key] : 0;
+  if ((rc = dev_upload<int64_t>(h, &zsum, nullptr, n_zone)) || (rc = dev_upload<int64_t>(h, &zread, nullptr, n_zone)))
+    return rc;
+  if (t->spread_pair && (rc = dev_upload(h, &spair, t->spread_pair, t->n_aclass))) return rc;
   A.n = n;
+  A.spread_pair = spair; A.zsum = zsum; A.zread = zread; A.zone_key = t->zone_key; A.n_zone = n_zone;
   A.dom = dom; A.ident_sel = is; A.ident_anti = ia; A.ident_prio = ip;
   A.pair_sel = ps; A.pair_key = pk; A.pair_off = po; A.carry_key = ck; A.carry_off = co;
   A.ac = ac; A.terms = terms; A.carries = carries; A.cnt = cnt; A.carried = carried;

@@ -322,8 +322,8 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   if ((rc = ksim_rt_ensure_partials(h, grid))) return rc;
   cs.partials = c.partials;
   hipError_t e = hipSuccess;
-  if (ksim_is_aff_host(h, *pod) && c.w[KSIM_W_INTERPOD_AFFINITY] && !c.no_prio)
-    e = ksim_launch_ipa_pass(&cs, npt, grid, h->stream);  // InterPodAffinityPriority's min / max first
+  if (ksim_is_aff_host(h, *pod) && (c.w[KSIM_W_INTERPOD_AFFINITY] || c.w[KSIM_W_SELECTOR_SPREAD]) && !c.no_prio)
+    e = ksim_launch_ipa_pass(&cs, npt, grid, h->stream);  // InterPodAffinity / SelectorSpread reductions first
   if (e == hipSuccess) e = ksim_launch_scan(&cs, npt, 1, grid, h->stream);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "scan launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipMemcpyAsync(h->res_host, h->res_dev, KSIM_RES_WORDS * 4, hipMemcpyDeviceToHost, h->stream));

@@ -45,11 +45,17 @@ struct KsimAff {
   const ksim_aff_carry* __restrict__ carries;
   int32_t* cnt;                    // counted pairs, per domain
   int64_t* carried;                // carried terms, per domain
-  int64_t* mm;                     // [2] min / max of the raw priority over the fit nodes (pass A)
-  int64_t* part;                   // [grid][2] pass A block partials
+  int64_t* mm;                     // pass A results: [0..1] min / max of the raw InterPodAffinity sums,
+                                   // [2] SelectorSpread maxCountByNodeName, [3] haveZones, [4] maxCountByZone
+  int64_t* part;                   // [grid][4] pass A block partials
   uint32_t* ticket;                // pass A arrival counter
+  const int32_t* __restrict__ spread_pair;  // [n_aclass] or null
+  int64_t* zsum;                   // [n_zone] SelectorSpread countsByZone being summed (pass A, zeroed by it)
+  int64_t* zread;                  // [n_zone] countsByZone of the current pod (read by the scan)
   int32_t n_pair;
   int32_t sel_words, carry_words;
+  int32_t zone_key;                // -1: no zone key
+  int32_t n_zone;
   int32_t pad;
 };
 
@@ -406,6 +412,26 @@ __device__ __noinline__ void ksim_aff_commit(const KsimAff& A, const ksim_pod& P
       if (d >= 0) A.carried[A.carry_off[k.term] + d] += (int64_t)sign * k.amount;
     }
   }
+}
+
+// The counted pair of pod P's SelectorSpread selectors, or -1.
+__device__ __forceinline__ int32_t ksim_spread_pair(const KsimAff& A, const ksim_pod& P) {
+  return (A.spread_pair && P.aff_class > 0) ? A.spread_pair[P.aff_class - 1] : -1;
+}
+
+// CalculateSpreadPriorityReduce's score of one fit node (selector_spreading.go:121-174) from its
+// count, the pass-A maxima and the zone's summed count; float64 without contraction as in Go.
+__device__ __forceinline__ int64_t ksim_spread_score(int64_t cnt, int64_t max_node, bool have_zones, int32_t zone,
+                                                     int64_t zone_cnt, int64_t max_zone) {
+  const double zw = 2.0 / 3.0;  // zoneWeighting (selector_spreading.go:33)
+  double f = 10.0;
+  if (max_node > 0) f = 10.0 * ((double)(max_node - cnt) / (double)max_node);
+  if (have_zones && zone >= 0) {
+    double zs = 10.0;
+    if (max_zone > 0) zs = 10.0 * ((double)(max_zone - zone_cnt) / (double)max_zone);
+    f = (f * (1.0 - zw)) + (zw * zs);
+  }
+  return (int64_t)f;
 }
 
 __device__ __forceinline__ bool ksim_is_aff_pod(const KsimCtx& c, const ksim_pod& P) {

@@ -62,18 +62,30 @@ struct Decision {
 
 // InterPodAffinityPriority inputs of one pod: whether it reads the priority and the min / max
 // of its raw per-node sums over the fit nodes (written by ksim_ipa_pass_kernel just before).
+// Same for SelectorSpread: the pod's counted pair and the pass-A maxima.
 struct IpaNorm {
   bool on;
   int64_t mn, mx, w;
+  int32_t sp;          // SelectorSpread counted pair, -1: off
+  bool hz;             // haveZones
+  int64_t sw, smx, szmx;
 };
 
 __device__ __forceinline__ IpaNorm ipa_norm(const KsimCtx& c, const ksim_pod& P) {
-  IpaNorm z{false, 0, 0, 0};
-  if (!c.aff || c.no_prio || c.w[KSIM_W_INTERPOD_AFFINITY] == 0 || !ksim_interpod_prio_work(*c.aff, P)) return z;
-  z.on = true;
-  z.mn = c.aff->mm[0];
-  z.mx = c.aff->mm[1];
-  z.w = c.w[KSIM_W_INTERPOD_AFFINITY];
+  IpaNorm z{false, 0, 0, 0, -1, false, 0, 0, 0};
+  if (!c.aff || c.no_prio) return z;
+  if (c.w[KSIM_W_INTERPOD_AFFINITY] != 0 && ksim_interpod_prio_work(*c.aff, P)) {
+    z.on = true;
+    z.mn = c.aff->mm[0];
+    z.mx = c.aff->mm[1];
+    z.w = c.w[KSIM_W_INTERPOD_AFFINITY];
+  }
+  if (c.w[KSIM_W_SELECTOR_SPREAD] != 0 && (z.sp = ksim_spread_pair(*c.aff, P)) >= 0) {
+    z.sw = c.w[KSIM_W_SELECTOR_SPREAD];
+    z.smx = c.aff->mm[2];
+    z.hz = c.aff->mm[3] != 0;
+    z.szmx = c.aff->mm[4];
+  }
   return z;
 }
 
@@ -92,6 +104,12 @@ __device__ __forceinline__ void eval_one(const KsimCtx& c, const ksim_pod& P, in
   if (ipa.on && fit)
     score = (int64_t)((uint64_t)score +
                       (uint64_t)ipa.w * (uint64_t)ksim_interpod_score(ksim_interpod_raw(*c.aff, P, i), ipa.mn, ipa.mx));
+  if (ipa.sp >= 0 && fit) {
+    const KsimAff& A = *c.aff;
+    const int32_t z = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
+    const int64_t v = ksim_spread_score(A.cnt[A.pair_off[ipa.sp] + i], ipa.smx, ipa.hz, z, z >= 0 ? A.zread[z] : 0, ipa.szmx);
+    score = (int64_t)((uint64_t)score + (uint64_t)ipa.sw * (uint64_t)v);
+  }
   cls = (k1 * k2 > 1) ? ksim_rclass(c, P, i, k1, k2) : 0;
 }
 
@@ -383,48 +401,73 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   }
 }
 
-// Pass A of an InterPodAffinityPriority pod (one launch before its scan): min / max of the raw
-// per-node sums over the fit nodes, with 0 folded in as the reference's accumulators start
-// there (interpod_affinity.go:129-131, 218-226).  Every block reduces its chunk to a partial;
-// the last block to arrive combines them into aff->mm and re-arms the ticket.  Pods that do
-// not read the priority exit at once (uniformly, so the launch costs only its dispatch).
+// Pass A of an InterPodAffinityPriority / SelectorSpread pod (one launch before its scan), over
+// the fit nodes: min / max of the raw InterPodAffinity sums with 0 folded in as the reference's
+// accumulators start there (interpod_affinity.go:129-131, 218-226); SelectorSpread's
+// maxCountByNodeName, haveZones and countsByZone (selector_spreading.go:125-145, zone sums by
+// atomics).  Every block reduces its chunk to a partial; the last block to arrive combines them
+// into aff->mm, publishes the zone sums (zread) with their maximum, zeroes zsum for the next pod
+// and re-arms the ticket.  Pods that read neither priority exit at once (uniformly).
 template <int NPT>
 __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
-  __shared__ int64_t s_mn[KSIM_WAVES], s_mx[KSIM_WAVES];
+  __shared__ int64_t s_v[4][KSIM_WAVES];
   __shared__ int s_last;
   const int64_t pod = *c.cursor;
-  if (pod >= c.end || !c.aff || c.no_prio || c.w[KSIM_W_INTERPOD_AFFINITY] == 0) return;
+  if (pod >= c.end || !c.aff || c.no_prio) return;
   const ksim_pod P = c.pods[pod];
   const KsimAff& A = *c.aff;
-  if (!ksim_interpod_prio_work(A, P)) return;
+  const bool ipa = c.w[KSIM_W_INTERPOD_AFFINITY] != 0 && ksim_interpod_prio_work(A, P);
+  const int32_t sp = c.w[KSIM_W_SELECTOR_SPREAD] != 0 ? ksim_spread_pair(A, P) : -1;
+  if (!ipa && sp < 0) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * c.chunk;
-  int64_t mn = 0, mx = 0;
+  int64_t mn = 0, mx = 0, smx = 0, hz = 0;
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     const int64_t i = base + k * KSIM_BLOCK + tid;
     if (i >= c.n) continue;
     const KsimRow r = ksim_load_row(c, i);
     if (ksim_predicates(c, P, i, r) != 0) continue;
-    const int64_t v = ksim_interpod_raw(A, P, i);
-    mn = v < mn ? v : mn;
-    mx = v > mx ? v : mx;
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const int64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
-    mn = a < mn ? a : mn;
-    mx = b > mx ? b : mx;
-  }
-  if (lane == 0) { s_mn[wv] = mn; s_mx[wv] = mx; }
-  __syncthreads();
-  if (tid == 0) {
-    for (int w = 1; w < KSIM_WAVES; ++w) {
-      mn = s_mn[w] < mn ? s_mn[w] : mn;
-      mx = s_mx[w] > mx ? s_mx[w] : mx;
+    if (ipa) {
+      const int64_t v = ksim_interpod_raw(A, P, i);
+      mn = v < mn ? v : mn;
+      mx = v > mx ? v : mx;
     }
-    A.part[2 * blockIdx.x] = mn;
-    A.part[2 * blockIdx.x + 1] = mx;
+    if (sp >= 0) {
+      const int64_t v = A.cnt[A.pair_off[sp] + i];
+      smx = v > smx ? v : smx;
+      const int32_t z = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
+      if (z >= 0) {
+        hz = 1;
+        if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&A.zsum[z]), (unsigned long long)v);
+      }
+    }
+  }
+  auto combine = [&]() {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+      const int64_t d = __shfl_xor(smx, o, 64), e = __shfl_xor(hz, o, 64);
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+      smx = d > smx ? d : smx;
+      hz = e > hz ? e : hz;
+    }
+    if (lane == 0) { s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < KSIM_WAVES; ++w) {
+        mn = s_v[0][w] < mn ? s_v[0][w] : mn;
+        mx = s_v[1][w] > mx ? s_v[1][w] : mx;
+        smx = s_v[2][w] > smx ? s_v[2][w] : smx;
+        hz = s_v[3][w] > hz ? s_v[3][w] : hz;
+      }
+    }
+  };
+  combine();
+  if (tid == 0) {
+    int64_t* pp = A.part + 4 * (int64_t)blockIdx.x;
+    pp[0] = mn; pp[1] = mx; pp[2] = smx; pp[3] = hz;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t old = __hip_atomic_fetch_add(A.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -435,28 +478,41 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
   if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  mn = 0;
-  mx = 0;
+  mn = 0; mx = 0; smx = 0; hz = 0;
   for (int b = tid; b < (int)gridDim.x; b += KSIM_BLOCK) {
-    const int64_t a = A.part[2 * b], z = A.part[2 * b + 1];
-    mn = a < mn ? a : mn;
-    mx = z > mx ? z : mx;
+    const int64_t* pp = A.part + 4 * (int64_t)b;
+    mn = pp[0] < mn ? pp[0] : mn;
+    mx = pp[1] > mx ? pp[1] : mx;
+    smx = pp[2] > smx ? pp[2] : smx;
+    hz = pp[3] > hz ? pp[3] : hz;
   }
+  __syncthreads();
+  combine();
+  __syncthreads();
+  const int64_t r0 = mn, r1 = mx, r2 = smx, r3 = hz;  // valid in thread 0
+  // zone sums: publish for the scan, zero for the next pod, maximum (countsByZone, :139-143)
+  int64_t zmx = 0;
+  if (sp >= 0)
+    for (int z = tid; z < A.n_zone; z += KSIM_BLOCK) {
+      const int64_t v = __hip_atomic_load(&A.zsum[z], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      A.zread[z] = v;
+      A.zsum[z] = 0;
+      zmx = v > zmx ? v : zmx;
+    }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const int64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
-    mn = a < mn ? a : mn;
-    mx = b > mx ? b : mx;
+    const int64_t a = __shfl_xor(zmx, o, 64);
+    zmx = a > zmx ? a : zmx;
   }
-  if (lane == 0) { s_mn[wv] = mn; s_mx[wv] = mx; }
+  if (lane == 0) s_v[0][wv] = zmx;
   __syncthreads();
   if (tid == 0) {
-    for (int w = 1; w < KSIM_WAVES; ++w) {
-      mn = s_mn[w] < mn ? s_mn[w] : mn;
-      mx = s_mx[w] > mx ? s_mx[w] : mx;
-    }
-    A.mm[0] = mn;
-    A.mm[1] = mx;
+    for (int w = 1; w < KSIM_WAVES; ++w) zmx = s_v[0][w] > zmx ? s_v[0][w] : zmx;
+    A.mm[0] = r0;
+    A.mm[1] = r1;
+    A.mm[2] = r2;
+    A.mm[3] = r3;
+    A.mm[4] = zmx;
     *A.ticket = 0;
   }
 }

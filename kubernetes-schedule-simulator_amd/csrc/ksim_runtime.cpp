@@ -473,7 +473,8 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
   HIPCHK(h, hipMemcpyAsync(c.cursor, &first, 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipMemsetAsync(c.ticket, 0, 16, h->stream));
   const int batch = (int)std::min<int64_t>(count, 256);
-  const int ipa = ksim_rt_aff_count(h, first, count) > 0 && c.w[KSIM_W_INTERPOD_AFFINITY] != 0 && !c.no_prio ? 1 : 0;
+  const int ipa = ksim_rt_aff_count(h, first, count) > 0 &&
+                  (c.w[KSIM_W_INTERPOD_AFFINITY] != 0 || c.w[KSIM_W_SELECTOR_SPREAD] != 0) && !c.no_prio ? 1 : 0;
   if (!h->gexec || h->g_batch != batch || h->g_npt != npt || h->g_collect != c.collect || h->g_first != first ||
       h->g_end != c.end || h->g_ipa != ipa) {
     if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }

@@ -39,8 +39,8 @@ P_MAX_GCE_PD = 1 << 15
 P_MAX_AZURE_DISK = 1 << 16
 P_VOLUME_ZONE = 1 << 17
 
-W_LEAST, W_MOST, W_BALANCED, W_TAINT_TOL, W_NODE_AFF, W_INTERPOD = range(6)
-NW = 6
+W_LEAST, W_MOST, W_BALANCED, W_TAINT_TOL, W_NODE_AFF, W_INTERPOD, W_SPREAD = range(7)
+NW = 7
 
 N_NOT_READY, N_OUT_OF_DISK, N_NET_UNAVAIL, N_UNSCHEDULABLE = 1, 2, 4, 8
 N_MEM_PRESSURE, N_DISK_PRESSURE, N_LABEL_PRESENCE = 16, 32, 64
@@ -133,11 +133,11 @@ class AffinityTables(C.Structure):
     _fields_ = [("n_keys", C.c_int32), ("n_sel", C.c_int32), ("n_ident", C.c_int32), ("n_pair", C.c_int32),
                 ("n_carry", C.c_int32), ("n_aclass", C.c_int32), ("n_terms", C.c_int32), ("n_carries", C.c_int32),
                 ("n_nodes", C.c_int64), ("cnt_len", C.c_int64), ("carried_len", C.c_int64),
-                ("hard_weight", C.c_int32), ("sel_words", C.c_int32), ("carry_words", C.c_int32), ("pad", C.c_int32),
+                ("hard_weight", C.c_int32), ("sel_words", C.c_int32), ("carry_words", C.c_int32), ("zone_key", C.c_int32),
                 ("dom", _i32p), ("n_dom", _i32p), ("ident_sel", _u64p), ("ident_anti", _u64p), ("ident_prio", _u64p),
                 ("pair_sel", _i32p), ("pair_key", _i32p), ("pair_off", _i64p), ("carry_key", _i32p),
                 ("carry_kind", _i32p), ("carry_off", _i64p), ("ac", _i32p), ("terms", C.c_void_p),
-                ("carries", C.c_void_p), ("cnt", _i32p), ("carried", _i64p)]
+                ("carries", C.c_void_p), ("cnt", _i32p), ("carried", _i64p), ("spread_pair", _i32p)]
 
 
 class VolumeTables(C.Structure):

@@ -87,6 +87,27 @@ class _Interner:
         return i
 
 
+class _AnyOf:
+    """A SelectorSpread selector: the pod's service / controller selectors, any of which counts a
+    placed pod of its namespace that is not being deleted (selector_spreading.go:85-107)."""
+
+    def __init__(self, sels):
+        self.sels = tuple(sels)
+
+
+ZONE_KEY = "\x00zone"   # pseudo key: utilnode.GetZoneKey (K/pkg/util/node/node.go), SelectorSpread's zones
+
+
+def zone_key_of(lab):
+    """GetZoneKey: "" without both failure-domain labels, else region + ":\\x00:" + zone."""
+    lab = lab or {}
+    region = lab.get("failure-domain.beta.kubernetes.io/region", "")
+    zone = lab.get("failure-domain.beta.kubernetes.io/zone", "")
+    if region == "" and zone == "":
+        return ""
+    return region + ":\x00:" + zone
+
+
 class AffinityIndex:
     """Collects the terms of every pod (running and queued), then builds the tables."""
 
@@ -116,18 +137,33 @@ class AffinityIndex:
 
     def ident(self, pod):
         md = _meta(pod)
-        return self.idents.get((md.get("namespace", ""), _canon(md.get("labels") or {})),
-                               (md.get("namespace", ""), dict(md.get("labels") or {})))
+        deleting = md.get("deletionTimestamp") is not None
+        return self.idents.get((md.get("namespace", ""), _canon(md.get("labels") or {}), deleting),
+                               (md.get("namespace", ""), dict(md.get("labels") or {}), deleting))
 
     def _matches(self, ident_item, sel_item):
-        ns, lab = ident_item
+        ns, lab, deleting = ident_item
         nss, sel = sel_item
+        if isinstance(sel, _AnyOf):
+            return ns in nss and not deleting and any(labels.matches(x, lab) for x in sel.sels)
         return ns in nss and labels.matches(sel, lab)
 
-    def aclass(self, pod):
-        """The pod's own terms and carried terms, interned; -1 when it has neither."""
-        if not has_pod_affinity(pod):
+    def spread_pair(self, pod, sels):
+        """The counted pair (spread selector, node key) of a pod with SelectorSpread selectors."""
+        if not sels:
             return -1
+        ns = _meta(pod).get("namespace", "")
+        key = ("\x00spread", ns, repr(list(sels)))
+        s = self.sels.get(key, (frozenset([ns]), _AnyOf(sels)))
+        self.keys.get(ZONE_KEY)
+        return self.pairs.get((s, KEY_NODE))
+
+    def aclass(self, pod, spread_sels=()):
+        """The pod's own terms, carried terms and SelectorSpread pair, interned; -1 when it has
+        none of them."""
+        sp = self.spread_pair(pod, spread_sels)
+        if not has_pod_affinity(pod):
+            return -1 if sp < 0 else self.aclasses.get(((), (), (), sp))
         a = _aff(pod)
         name = _meta(pod).get("name")
         req, pref, carries = [], [], {}
@@ -183,9 +219,9 @@ class AffinityIndex:
                 carry(wt.get("podAffinityTerm") or {}, abi.AFF_CARRY_PRIO, -int(wt.get("weight", 0)))
         carries = tuple(sorted((e, v) for e, v in carries.items() if v != 0 or self.carry.items[e][2] == abi.AFF_CARRY_ANTI))
         req.sort(key=lambda r: r[0] != abi.AFF_REQ_AFFINITY)   # affinity terms are checked before anti-affinity
-        if not req and not pref and not carries:
+        if not req and not pref and not carries and sp < 0:
             return -1
-        return self.aclasses.get((tuple(req), tuple(pref), carries))
+        return self.aclasses.get((tuple(req), tuple(pref), carries, sp))
 
     # ------------------------------------------------------------------ tables
     def build(self, running_nodes, idents, aclasses):
@@ -208,7 +244,11 @@ class AffinityIndex:
             name = self.keys.items[k]
             vals = {}
             for i, lab in enumerate(self.node_labels):
-                if lab is not None and name in lab:
+                if name == ZONE_KEY:
+                    z = zone_key_of(lab)
+                    if z != "":
+                        dom[k, i] = vals.setdefault(z, len(vals))
+                elif lab is not None and name in lab:
                     dom[k, i] = vals.setdefault(lab[name], len(vals))
             n_dom[k] = len(vals)
         # identity masks (identities matching nothing become -1)
@@ -253,7 +293,8 @@ class AffinityIndex:
         A = len(self.aclasses.items)
         terms, carries = [], []
         ac = np.zeros((A, 6), np.int32)   # req_off, req_cnt, pref_off, pref_cnt, carry_off, carry_cnt
-        for a, (req, pref, car) in enumerate(self.aclasses.items):
+        spread_pair = np.array([x[3] for x in self.aclasses.items], np.int32) if A else np.zeros(0, np.int32)
+        for a, (req, pref, car, _) in enumerate(self.aclasses.items):
             ac[a, 0], ac[a, 1] = len(terms), len(req)
             terms.extend(req)
             ac[a, 2], ac[a, 3] = len(terms), len(pref)
@@ -286,20 +327,22 @@ class AffinityIndex:
                     ident_sel=isel[live].copy(), ident_anti=ianti[live].copy(), ident_prio=iprio[live].copy(),
                     pair_sel=pair_sel, pair_key=pair_key, pair_off=pair_off, carry_key=carry_key,
                     carry_kind=carry_kind, carry_sel=carry_sel, carry_off=carry_off,
-                    ac=np.ascontiguousarray(ac), terms=terms_a, carries=carries_a, cnt=cnt, carried=carried), remap
+                    ac=np.ascontiguousarray(ac), terms=terms_a, carries=carries_a, cnt=cnt, carried=carried,
+                    zone_key=self.keys.ids.get(ZONE_KEY, -1), spread_pair=spread_pair), remap
 
 
 def tables_struct(d):
     """ksim_affinity_tables over a tables dict (the dict keeps the arrays alive)."""
     t = abi.AffinityTables()
-    for k in ("n_keys", "n_sel", "n_ident", "n_pair", "n_carry", "n_aclass", "hard_weight", "sel_words", "carry_words"):
+    for k in ("n_keys", "n_sel", "n_ident", "n_pair", "n_carry", "n_aclass", "hard_weight", "sel_words", "carry_words",
+              "zone_key"):
         setattr(t, k, int(d[k]))
     t.n_nodes = int(d["n_nodes"])
     for name, ct in (("dom", abi.C.c_int32), ("n_dom", abi.C.c_int32), ("ident_sel", abi.C.c_uint64),
                      ("ident_anti", abi.C.c_uint64), ("ident_prio", abi.C.c_uint64), ("pair_sel", abi.C.c_int32),
                      ("pair_key", abi.C.c_int32), ("pair_off", abi.C.c_int64), ("carry_key", abi.C.c_int32),
                      ("carry_kind", abi.C.c_int32), ("carry_off", abi.C.c_int64), ("ac", abi.C.c_int32),
-                     ("cnt", abi.C.c_int32), ("carried", abi.C.c_int64)):
+                     ("cnt", abi.C.c_int32), ("carried", abi.C.c_int64), ("spread_pair", abi.C.c_int32)):
         d[name] = np.ascontiguousarray(d[name])
         setattr(t, name, abi.ptr(d[name], ct))
     d["terms"] = np.ascontiguousarray(d["terms"])

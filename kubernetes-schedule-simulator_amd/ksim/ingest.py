@@ -326,12 +326,15 @@ class Cluster:
     # ------------------------------------------------------------------ nodes
     @classmethod
     def from_objects(cls, nodes, running_pods=(), pods=(), port_slots=None, hard_weight=10, pvs=(), pvcs=(),
-                     storage_classes=(), max_vols=None, vol_slots=None):
+                     storage_classes=(), max_vols=None, vol_slots=None, spread=None, spread_services_only=False):
         """nodes / running_pods / pods: Kubernetes-shaped dicts; pods are in SCHEDULING
         order (the caller resolves the simulator's LIFO queue).  hard_weight:
         hardPodAffinitySymmetricWeight (the simulator's 10, or a Policy's).  pvs / pvcs /
         storage_classes: what the PV / PVC / StorageClass listers hold (the simulator's are empty);
-        max_vols: the MaxPD limits (EBS, GCE PD, Azure Disk), default KUBE_MAX_PD_VOLS / getMaxVols."""
+        max_vols: the MaxPD limits (EBS, GCE PD, Azure Disk), default KUBE_MAX_PD_VOLS / getMaxVols.
+        spread: ksim.spread.SpreadListers (services / RCs / RSs / StatefulSets) for SelectorSpread
+        (spread_services_only: ServiceSpreadingPriority's services-only form); None: the simulator's
+        empty listers."""
         self = cls()
         self.hard_weight = int(hard_weight)
         self.ips.get("0.0.0.0")     # id 0 = wildcard
@@ -345,8 +348,11 @@ class Cluster:
         running = [p for p in running_pods if _spec(p).get("nodeName") in self.index]
         for p in running:
             check_pod_supported(p, "running pod")
-        with_affinity = any(has_pod_affinity(p) for p in list(running_pods) + list(pods))
-        if with_affinity and len(running) != len([p for p in running_pods if _spec(p).get("nodeName")]):
+        with_pod_affinity = any(has_pod_affinity(p) for p in list(running_pods) + list(pods))
+        self.spread_sels = [spread.selectors(p, spread_services_only) if spread else [] for p in pods]
+        self.spread_active = any(self.spread_sels)
+        with_affinity = with_pod_affinity or self.spread_active
+        if with_pod_affinity and len(running) != len([p for p in running_pods if _spec(p).get("nodeName")]):
             # the reference caches them under a node-less NodeInfo: its affinity metadata then
             # errors and the predicate takes another path (metadata.go:106-109)
             raise Unsupported("running pods bound to nodes outside the snapshot, with inter-pod affinity terms")
@@ -493,7 +499,8 @@ class Cluster:
         idx = AffinityIndex([_meta(x).get("labels") for x in nodes], self.hard_weight)
         allp = list(running) + list(pods)
         idents = [idx.ident(p) for p in allp]
-        aclasses = [idx.aclass(p) for p in allp]
+        sels = [()] * len(running) + list(self.spread_sels)
+        aclasses = [idx.aclass(p, s) for p, s in zip(allp, sels)]
         run_nodes = [self.index[_spec(p)["nodeName"]] for p in running]
         self.affinity, remap = idx.build(run_nodes, idents, aclasses)
         k = len(running)
@@ -546,7 +553,7 @@ class Cluster:
         tables (node-sharded mode: rank r loads its contiguous shard, ksim_shard_setup)."""
         import copy
         if self.affinity is not None:
-            raise Unsupported("node-sharded scheduling of pods with inter-pod affinity terms")
+            raise Unsupported("node-sharded scheduling of pods with inter-pod affinity terms or spread selectors")
         if self.volumes is not None:
             raise Unsupported("node-sharded scheduling of pods with volumes")
         sub = copy.copy(self)

@@ -55,8 +55,10 @@ TRIVIAL_PREDICATES = {"CheckVolumeBinding", "PodFitsPorts"}
 PRIORITY_SLOTS = {"LeastRequestedPriority": abi.W_LEAST, "MostRequestedPriority": abi.W_MOST,
                   "BalancedResourceAllocation": abi.W_BALANCED, "TaintTolerationPriority": abi.W_TAINT_TOL,
                   "NodeAffinityPriority": abi.W_NODE_AFF, "InterPodAffinityPriority": abi.W_INTERPOD}
-# value on every node under supported inputs (no services/controllers in the simulator's store,
-# no RC/RS-owned pods next to preferAvoidPods annotations)
+SPREAD_PRIORITIES = ("SelectorSpreadPriority", "ServiceSpreadingPriority")
+# value on every node under supported inputs (no services/controllers in the simulator's store —
+# with SpreadListers the spread priorities take the W_SPREAD slot —, no RC/RS-owned pods next to
+# preferAvoidPods annotations)
 CONST_PRIORITIES = {"SelectorSpreadPriority": 10, "ServiceSpreadingPriority": 10, "NodePreferAvoidPodsPriority": 10,
                     "EqualPriority": 1,
                     # image_locality.go:39-69: 0 on every node when no node lists status.images
@@ -81,7 +83,10 @@ def provider(name: str):
     return list(DEFAULT_PREDICATES), pri
 
 
-def make_config(predicates, priorities, device=0, mode=abi.MODE_AUTO, collect_reasons=True, last_node_index=0):
+def make_config(predicates, priorities, device=0, mode=abi.MODE_AUTO, collect_reasons=True, last_node_index=0,
+                spread=False):
+    """spread: the cluster has SelectorSpread selectors (Cluster.spread_active): the spread priority
+    scores per node (KSIM_W_SELECTOR_SPREAD) instead of being the constant MaxPriority."""
     cfg = abi.Config()
     cfg.device = device
     cfg.mode = mode
@@ -102,6 +107,10 @@ def make_config(predicates, priorities, device=0, mode=abi.MODE_AUTO, collect_re
             raise abi.KsimError(abi.E_INVAL, "priority %r: weight must be positive" % name)
         if name in PRIORITY_SLOTS:
             cfg.weights[PRIORITY_SLOTS[name]] = w
+        elif spread and name in SPREAD_PRIORITIES:
+            if cfg.weights[abi.W_SPREAD]:
+                raise Unsupported("SelectorSpreadPriority and ServiceSpreadingPriority together with spread selectors")
+            cfg.weights[abi.W_SPREAD] = w
         elif name in CONST_PRIORITIES:
             const += CONST_PRIORITIES[name] * w
         else:
@@ -239,7 +248,8 @@ class GenericScheduler:
         if "CheckNodeLabelPresence" in self.predicates and label_presence is None:
             raise Unsupported("CheckNodeLabelPresence needs its labelsPresence argument")
         self.cfg = make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence], priorities,
-                               device, mode, collect_reasons, last_node_index)
+                               device, mode, collect_reasons, last_node_index,
+                               spread=bool(getattr(cluster, "spread_active", False)))
         check_volume_support(cluster, self.predicates)
         self.h = abi.Handle(self.cfg)
         table = cluster.node_table()
@@ -258,7 +268,8 @@ class GenericScheduler:
         pods = np.ascontiguousarray(cluster.pods)
         self.affinity = None
         if cluster.affinity is not None:
-            if self.cfg.predicates & abi.P_INTERPOD_AFFINITY or (self.cfg.weights[abi.W_INTERPOD] and not self.cfg.no_priorities):
+            if self.cfg.predicates & abi.P_INTERPOD_AFFINITY or ((self.cfg.weights[abi.W_INTERPOD] or
+                                                                  self.cfg.weights[abi.W_SPREAD]) and not self.cfg.no_priorities):
                 from .affinity import tables_struct
                 self.affinity = cluster.affinity
                 self.h.call("ksim_load_affinity", C.byref(tables_struct(self.affinity)))
@@ -524,7 +535,7 @@ class ClusterCapacity:
 
     def __init__(self, nodes, running_pods, simulation_pods, provider_name="DefaultProvider",
                  predicates=None, priorities=None, device=0, mode=abi.MODE_AUTO, collect_reasons=True,
-                 policy_obj=None, pvs=(), pvcs=(), storage_classes=()):
+                 policy_obj=None, pvs=(), pvcs=(), storage_classes=(), spread=None):
         label_presence = None
         if policy_obj is not None:
             from .policy import key_sets
@@ -536,8 +547,12 @@ class ClusterCapacity:
         self.order = list(reversed(simulation_pods))   # PodQueue.Pop takes the last element
         self.running = list(running_pods)
         # pvs / pvcs / storage_classes: the simulator's listers are empty; other callers may fill them
+        names = {n for n, _ in priorities}
+        if spread and {"SelectorSpreadPriority", "ServiceSpreadingPriority"} <= names:
+            raise Unsupported("SelectorSpreadPriority and ServiceSpreadingPriority together with spread listers")
         self.cluster = Cluster.from_objects(nodes, running_pods, self.order, pvs=pvs, pvcs=pvcs,
-                                            storage_classes=storage_classes)
+                                            storage_classes=storage_classes, spread=spread,
+                                            spread_services_only="ServiceSpreadingPriority" in names)
         self.scheduler = GenericScheduler(self.cluster, predicates, priorities, device=device, mode=mode,
                                           collect_reasons=collect_reasons, label_presence=label_presence)
 

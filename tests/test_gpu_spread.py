@@ -1,0 +1,53 @@
+"""GPU parity of SelectorSpreadPriority / ServiceSpreadingPriority with services, RCs, RSs and
+StatefulSets (selector_spreading.go:66-174): the reference's golden cases through the kernels'
+pass-A reductions (maxCountByNodeName, countsByZone) and the scan's float64 reduce — checked by
+where selectHost puts the pod for every lastNodeIndex over two periods — and random simulations
+against the object oracle (placements, FitError texts, lastNodeIndex)."""
+import pytest
+
+import ksim_ref as R
+from golden_util import case_id, load
+from ksim import abi, ingest, scheduler, spread
+from workloads import rnd_spread_workload
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("c", load("spread"), ids=case_id)
+def test_golden_spread_selects_on_gpu(c):
+    expect = c["expect"]
+    best = max(expect.values())
+    tied = sorted((h for h, s in expect.items() if s == best), key=lambda h: h.encode(), reverse=True)
+    lst = spread.SpreadListers(c["services"], c["rcs"], c["rss"], c["sss"])
+    for k in range(2 * len(tied)):
+        cl = ingest.Cluster.from_objects(c["nodes"], c["pods"], [c["pod"]], spread=lst)
+        g = scheduler.GenericScheduler(cl, [], [("SelectorSpreadPriority", 1)], mode=abi.MODE_AUTO, last_node_index=k)
+        out, _, _ = g.schedule(0, 1)
+        assert cl.names[int(out[0])] == tied[k % len(tied)], (k, tied)
+        g.close()
+
+
+POLICIES = {
+    "default": scheduler.provider("DefaultProvider"),
+    "service_spreading": (["GeneralPredicates"], [("ServiceSpreadingPriority", 2), ("LeastRequestedPriority", 1)]),
+    "spread_heavy": (["GeneralPredicates", "PodToleratesNodeTaints"],
+                     [("SelectorSpreadPriority", 5), ("BalancedResourceAllocation", 1)]),
+}
+
+
+@pytest.mark.parametrize("policy", sorted(POLICIES))
+@pytest.mark.parametrize("seed", range(4))
+def test_spread_simulation_matches_oracle(seed, policy):
+    nodes, running, pods, objs = rnd_spread_workload(seed, zones=seed != 3)
+    preds, prios = POLICIES[policy]
+    want, want_lni = R.simulate(nodes, running, pods, set(preds), list(prios), spread=R.SpreadListers(**objs))
+    cc = scheduler.ClusterCapacity(nodes, running, pods, predicates=preds, priorities=prios,
+                                   spread=spread.SpreadListers(**objs))
+    assert cc.cluster.spread_active
+    rep = cc.run()
+    got = {name: (host, None) for name, host in rep.successful}
+    got.update({name: (None, msg) for name, msg in rep.failed})
+    assert [n for n, _ in rep.successful] == [n for n, h, _ in want if h is not None]
+    for name, host, msg in want:
+        assert got[name] == (host, msg), name
+    assert rep.last_node_index == want_lni

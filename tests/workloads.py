@@ -291,3 +291,42 @@ def rnd_volume_workload(seed, n_nodes=16, n_pods=120, n_running=14, zones=False,
     running = [pod("run-%d" % k, rng.choice(nodes)["metadata"]["name"]) for k in range(n_running)]
     pods = [pod("pod-%d" % k) for k in range(n_pods)]
     return nodes, running, pods, pvs, pvcs
+
+
+def rnd_spread_workload(seed, n_nodes=18, n_pods=120, n_running=16, zones=True):
+    """Pods labelled app=a|b|c, tier=x|y in namespaces ns1 / ns2 (a few being deleted among the
+    running ones), services / RCs / RSs / StatefulSets selecting subsets, nodes in zones."""
+    rng = random.Random(2000 + seed)
+    nodes = rnd_nodes(rng, n_nodes, features=False)
+    for x in nodes:
+        x["status"]["allocatable"]["pods"] = "110"
+        if zones and rng.random() < 0.8:
+            x["metadata"]["labels"]["failure-domain.beta.kubernetes.io/zone"] = rng.choice(["z1", "z2", "z3"])
+            if rng.random() < 0.3:
+                x["metadata"]["labels"]["failure-domain.beta.kubernetes.io/region"] = "r1"
+
+    def pod(name, nn=None):
+        p = rnd_pod(rng, name, features=False)
+        p["metadata"]["namespace"] = rng.choice(["ns1", "ns1", "ns2"])
+        lab = {}
+        if rng.random() < 0.9:
+            lab["app"] = rng.choice("abc")
+        if rng.random() < 0.5:
+            lab["tier"] = rng.choice("xy")
+        p["metadata"]["labels"] = lab
+        if nn:
+            p["spec"]["nodeName"] = nn
+            if rng.random() < 0.1:
+                p["metadata"]["deletionTimestamp"] = "2018-01-01T00:00:00Z"
+        return p
+    running = [pod("run-%d" % k, rng.choice(nodes)["metadata"]["name"]) for k in range(n_running)]
+    pods = [pod("pod-%d" % k) for k in range(n_pods)]
+    md = lambda ns: {"namespace": ns, "name": "o%d" % rng.randrange(1000)}
+    services = [{"metadata": md("ns1"), "spec": {"selector": {"app": "a"}}},
+                {"metadata": md("ns2"), "spec": {"selector": {"app": "b", "tier": "x"}}},
+                {"metadata": md("ns1"), "spec": {}}]                                    # nil selector
+    rcs = [{"metadata": md("ns1"), "spec": {"selector": {"tier": "y"}}}]
+    rss = [{"metadata": md("ns2"), "spec": {"selector": {"matchExpressions": [
+        {"key": "app", "operator": "In", "values": ["a", "c"]}]}}}]
+    sss = [{"metadata": md("ns1"), "spec": {"selector": {"matchLabels": {"app": "c"}}}}]
+    return nodes, running, pods, dict(services=services, rcs=rcs, rss=rss, sss=sss)
