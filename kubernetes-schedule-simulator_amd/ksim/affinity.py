@@ -328,7 +328,8 @@ class AffinityIndex:
                     pair_sel=pair_sel, pair_key=pair_key, pair_off=pair_off, carry_key=carry_key,
                     carry_kind=carry_kind, carry_sel=carry_sel, carry_off=carry_off,
                     ac=np.ascontiguousarray(ac), terms=terms_a, carries=carries_a, cnt=cnt, carried=carried,
-                    zone_key=self.keys.ids.get(ZONE_KEY, -1), spread_pair=spread_pair), remap
+                    zone_key=self.keys.ids.get(ZONE_KEY, -1), spread_pair=spread_pair,
+                    n_terms=len(terms), n_carries=len(carries)), remap
 
 
 def tables_struct(d):
@@ -349,8 +350,8 @@ def tables_struct(d):
     d["carries"] = np.ascontiguousarray(d["carries"])
     t.terms = d["terms"].ctypes.data_as(abi.C.c_void_p)
     t.carries = d["carries"].ctypes.data_as(abi.C.c_void_p)
-    t.n_terms = len(d["terms"])
-    t.n_carries = len(d["carries"])
+    t.n_terms = int(d.get("n_terms", len(d["terms"])))       # the arrays are padded to one entry
+    t.n_carries = int(d.get("n_carries", len(d["carries"])))
     t.cnt_len = len(d["cnt"])
     t.carried_len = len(d["carried"])
     return t
