@@ -17,7 +17,8 @@ Reference semantics (paths under vendor/k8s.io/kubernetes/pkg/scheduler/):
   evaluated.
 
 Unsupported pieces raise Unsupported (never a silently different result): HTTP extenders,
-alwaysCheckAllPredicates, CheckServiceAffinity, custom priorities with arguments
+alwaysCheckAllPredicates, CheckServiceAffinity, custom priorities with arguments other than
+labelPreference / serviceAntiAffinity
 (ServiceAntiAffinity / NodeLabelPriority) and priority keys outside the supported set.
 """
 from __future__ import annotations
@@ -160,11 +161,36 @@ def key_sets(policy: Policy):
     else:
         prios = {}
         for name, weight, arg in policy.priorities:
-            if arg:
+            if arg and _priority_argument(name, arg) is None:
                 raise Unsupported("policy: priority %r with argument %r is outside the supported key set" % (name, arg))
             prios[name] = weight  # a repeated name re-registers it: the last weight wins (plugins.go:343)
         prios = list(prios.items())
     return preds, prios, label_presence
+
+
+def _priority_argument(name, arg):
+    """RegisterCustomPriorityFunction (factory/plugins.go:271-323): a labelPreference argument
+    registers NodeLabelPriority (priorities/node_label.go), a serviceAntiAffinity argument the
+    ServiceAntiAffinity priority (selector_spreading.go:180-275) under the policy's name."""
+    if arg.get("labelPreference") is not None:
+        lp = arg["labelPreference"]
+        return ("labelPreference", lp.get("label", ""), bool(lp.get("presence", False)))
+    if arg.get("serviceAntiAffinity") is not None:
+        return ("serviceAntiAffinity", arg["serviceAntiAffinity"].get("label", ""))
+    return None
+
+
+def priority_arguments(policy: Policy):
+    """{priority name: ("labelPreference", label, presence) | ("serviceAntiAffinity", label)} of the
+    policy's custom priorities (the last registration of a name wins)."""
+    out = {}
+    for name, _, arg in policy.priorities or []:
+        spec = _priority_argument(name, arg) if arg else None
+        if spec is not None:
+            out[name] = spec
+        else:
+            out.pop(name, None)
+    return out
 
 
 def load(path):

@@ -171,18 +171,36 @@ def fit_error_message(num_nodes, hist, scalar_names=()):
     return "0/%d nodes are available: %s." % (num_nodes, ", ".join(parts))
 
 
-def class_tables_for(tables, priorities):
-    """The class tables a scheduler with these priorities loads, and NodePreferAvoidPods' weighted
-    per-NodeAffinity-class addends (ksim_class_tables.na_add) or None.
+def label_set_priority(spec, label_set):
+    """Map score of a Policy custom priority that is a function of the node's labels alone:
+    NodeLabelPriority (priorities/node_label.go:42-58) and, with no services selecting the pod, the
+    ServiceAntiAffinity priority (selector_spreading.go:221-275: no first service selector, so every
+    count is 0 and a node scores MaxPriority when it has the label, 0 otherwise)."""
+    if spec[0] == "labelPreference":
+        return 10 if (spec[1] in label_set) == spec[2] else 0
+    return 10 if spec[1] in label_set else 0
+
+
+def class_tables_for(tables, priorities, label_sets=(), custom=None):
+    """The class tables a scheduler with these priorities loads, and the weighted per-NodeAffinity-
+    class addends (ksim_class_tables.na_add) or None.
 
     NodePreferAvoidPodsPriority (node_prefer_avoid_pods.go:32-68) is a function of (pod class,
-    label set) — the label set carries the node's preferAvoidPods annotation — so when the policy
-    weighs it and some pod class sees nodes that differ in it (an RC / RS controller a node's
-    annotation names), the NodeAffinity class dimension is re-keyed by (preferred weight, avoid
-    score) — by the avoid score alone if NodeAffinityPriority is not configured — and each class
-    adds its weighted score.  Otherwise it is the constant MaxPriority x weight of const_score."""
+    label set) — the label set carries the node's preferAvoidPods annotation — and the Policy's
+    labelPreference / serviceAntiAffinity priorities (label_set_priority) of the label set alone.
+    When the policy weighs them and they differ across the nodes some pod class sees, the
+    NodeAffinity class dimension is re-keyed by (preferred weight, summed addend) — by the addend
+    alone if NodeAffinityPriority is not configured — and each class adds its weighted score.
+    Otherwise NodePreferAvoidPods is the constant MaxPriority x weight of const_score."""
+    custom = custom or {}
     w_pa = sum(int(x) for n, x in priorities if n == "NodePreferAvoidPodsPriority")
-    if not w_pa or not tables.get("pa_split"):
+    w_custom = [(custom[n], int(x)) for n, x in priorities if n in custom]
+    L = tables["na_class"].shape[1] if tables["na_class"].ndim == 2 else len(label_sets)
+    lab_add = np.zeros(L, np.int64)
+    for spec, w in w_custom:
+        lab_add += np.array([w * label_set_priority(spec, ls) for ls in label_sets], np.int64)
+    pa_on = bool(w_pa and tables.get("pa_split"))
+    if not pa_on and not lab_add.any():
         return tables, None
     use_w = any(n == "NodeAffinityPriority" for n, _ in priorities)
     d = dict(tables)
@@ -192,17 +210,18 @@ def class_tables_for(tables, priorities):
     nav = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
     add = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
     for k in range(Cn):
-        keys = list(zip((int(x) if use_w else 0 for x in tables["na_w"][k]), (int(x) for x in tables["na_p"][k])))
+        pa = [int(p) * w_pa if pa_on else 0 for p in tables["na_p"][k]]
+        keys = list(zip((int(x) if use_w else 0 for x in tables["na_w"][k]), (a + int(b) for a, b in zip(pa, lab_add))))
         av = sorted(set(keys))
         if int(tables["n_tt"][k]) * len(av) > abi.MAX_RCLASS:
             raise Unsupported("pod class needs %d x %d reduce classes (> %d)" % (int(tables["n_tt"][k]), len(av),
                                                                                 abi.MAX_RCLASS))
         nna[k] = len(av)
         nav[k, :len(av)] = [w for w, _ in av]
-        add[k, :len(av)] = [p * w_pa for _, p in av]
+        add[k, :len(av)] = [p for _, p in av]
         pos = {x: i for i, x in enumerate(av)}
         nac[k, :] = [pos[x] for x in keys]
-    d.update(na_class=nac, n_na=nna, na_val=nav)
+    d.update(na_class=nac, n_na=nna, na_val=nav, pa_in_add=pa_on)
     return d, add
 
 
@@ -237,17 +256,23 @@ class GenericScheduler:
     (labels, presence) of a Policy's CheckNodeLabelPresence predicate (policy.key_sets)."""
 
     def __init__(self, cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO,
-                 collect_reasons=True, last_node_index=0, label_presence=None):
+                 collect_reasons=True, last_node_index=0, label_presence=None, custom_priorities=None):
         self.cluster = cluster
         self.predicates = list(predicates)
         self.prioritizers = list(priorities)
+        # Policy priorities registered with a labelPreference / serviceAntiAffinity argument, by name
+        self.custom_priorities = dict(custom_priorities or {})
+        if any(s[0] == "serviceAntiAffinity" for s in self.custom_priorities.values()) and \
+                getattr(cluster, "spread_active", False):
+            raise Unsupported("a serviceAntiAffinity priority with services selecting the pods")
         if any(n == "NodeAffinityPriority" for n, _ in self.prioritizers) and cluster.bad_affinity_classes:
             raise Unsupported("NodeAffinityPriority: a preferred node-affinity term does not parse")
         if any(n == "ImageLocalityPriority" for n, _ in self.prioritizers) and cluster.node_images:
             raise Unsupported("ImageLocalityPriority with nodes that list status.images")
         if "CheckNodeLabelPresence" in self.predicates and label_presence is None:
             raise Unsupported("CheckNodeLabelPresence needs its labelsPresence argument")
-        self.cfg = make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence], priorities,
+        self.cfg = make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence],
+                               [(n, w) for n, w in priorities if n not in self.custom_priorities],
                                device, mode, collect_reasons, last_node_index,
                                spread=bool(getattr(cluster, "spread_active", False)))
         check_volume_support(cluster, self.predicates)
@@ -259,11 +284,12 @@ class GenericScheduler:
             self._flags = np.ascontiguousarray(fl, np.uint32)
             table.flags = abi.ptr(self._flags, C.c_uint32)
         self.h.call("ksim_load_nodes", C.byref(table))
-        self.tables, self.na_add = class_tables_for(cluster.tables, self.prioritizers)
+        self.tables, self.na_add = class_tables_for(cluster.tables, self.prioritizers, cluster.label_sets.items,
+                                                    self.custom_priorities)
         # const_score without NodePreferAvoidPods when its per-class addends carry it
         self.const_score = self.cfg.const_score - (10 * sum(int(x) for n, x in self.prioritizers
                                                             if n == "NodePreferAvoidPodsPriority")
-                                                   if self.na_add is not None else 0)
+                                                   if self.tables.get("pa_in_add") else 0)
         self.h.call("ksim_load_classes", C.byref(class_tables_struct(self.tables, self.na_add)))
         pods = np.ascontiguousarray(cluster.pods)
         self.affinity = None
@@ -537,9 +563,11 @@ class ClusterCapacity:
                  predicates=None, priorities=None, device=0, mode=abi.MODE_AUTO, collect_reasons=True,
                  policy_obj=None, pvs=(), pvcs=(), storage_classes=(), spread=None):
         label_presence = None
+        custom = None
         if policy_obj is not None:
-            from .policy import key_sets
+            from .policy import key_sets, priority_arguments
             predicates, priorities, label_presence = key_sets(policy_obj)
+            custom = priority_arguments(policy_obj)
         if predicates is None or priorities is None:
             p, q = provider(provider_name)
             predicates = p if predicates is None else predicates
@@ -554,7 +582,8 @@ class ClusterCapacity:
                                             storage_classes=storage_classes, spread=spread,
                                             spread_services_only="ServiceSpreadingPriority" in names)
         self.scheduler = GenericScheduler(self.cluster, predicates, priorities, device=device, mode=mode,
-                                          collect_reasons=collect_reasons, label_presence=label_presence)
+                                          collect_reasons=collect_reasons, label_presence=label_presence,
+                                          custom_priorities=custom)
 
     def run(self) -> Report:
         from .report import ERR_NO_NODES, get_report, simulation_status

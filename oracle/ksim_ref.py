@@ -1568,16 +1568,75 @@ def prio_image_locality(pod, ni):
 PRIORITIES["ImageLocalityPriority"] = ("map", prio_image_locality)
 
 
-def prioritize_nodes(pod, infos, configs, all_infos=None, hard_weight=10, spread=None):
+def node_label_priority(label, presence):
+    """NodeLabelPrioritizer.CalculateNodeLabelPriorityMap (priorities/node_label.go:42-58): a Policy
+    priority with a labelPreference argument."""
+    def fn(pod, ni):
+        exists = label in ((ni.node.get("metadata") or {}).get("labels") or {})
+        return MAX_PRIORITY if exists == presence else 0
+    return ("map", fn)
+
+
+def service_anti_affinity_priority(label, spread=None):
+    """ServiceAntiAffinity (selector_spreading.go:180-275, a Policy priority with a
+    serviceAntiAffinity argument): per node the placed pods of the pod's first service
+    (getFirstServiceSelector), reduced over the filtered nodes by the node's value of `label`."""
+    def fn(pod, infos):
+        sel = None
+        if spread is not None:
+            md = pod.get("metadata") or {}
+            ns, lab = md.get("namespace", ""), md.get("labels") or {}
+            for svc in spread.services:
+                s = (svc.get("spec") or {}).get("selector")
+                if (svc.get("metadata") or {}).get("namespace", "") == ns and s is not None and \
+                        SpreadListers._set_matches(s, lab):
+                    sel = selector_from_set(s)
+                    break
+        ns = (pod.get("metadata") or {}).get("namespace", "")
+        counts = []
+        for ni in infos:
+            c = 0
+            if sel is not None:
+                for q in ni.pods:
+                    qm = q.get("metadata") or {}
+                    if qm.get("namespace", "") == ns and selector_matches(sel, qm.get("labels") or {}):
+                        c += 1
+            counts.append(c)
+        total = sum(counts)
+        per_label = {}
+        vals = []
+        for ni, c in zip(infos, counts):
+            lab = (ni.node.get("metadata") or {}).get("labels") or {}
+            v = lab.get(label) if label in lab else None
+            vals.append(v)
+            if v is not None:
+                per_label[v] = per_label.get(v, 0) + c
+        out = []
+        for v in vals:
+            if v is None:
+                out.append(0)
+                continue
+            f = float(MAX_PRIORITY)
+            if total > 0:
+                f = float(MAX_PRIORITY) * (float(total - per_label[v]) / float(total))
+            out.append(int(f))
+        return out
+    return ("function", fn)
+
+
+def prioritize_nodes(pod, infos, configs, all_infos=None, hard_weight=10, spread=None, custom=None):
     """S/core/generic_scheduler.go:542-676.  configs: list of (name, weight); infos: the
     filtered nodes; all_infos: nodeNameToInfo (InterPodAffinityPriority reads every pod);
-    spread: SpreadListers for SelectorSpread / ServiceSpreading (None: the simulator's empty ones)."""
+    spread: SpreadListers for SelectorSpread / ServiceSpreading (None: the simulator's empty ones);
+    custom: Policy priorities registered with an argument, by name (node_label_priority, ...)."""
     if not configs:
         return [1 for _ in infos]          # EqualPriorityMap
     total = [0] * len(infos)
     for name, weight in configs:
-        kind, fn = PRIORITIES[name]
-        if kind == "ipa":
+        kind, fn = custom[name] if custom and name in custom else PRIORITIES[name]
+        if kind == "function":
+            scores = fn(pod, infos)
+        elif kind == "ipa":
             scores = interpod_affinity_priority(pod, all_infos if all_infos is not None else infos,
                                                 [ni.node for ni in infos], hard_weight)
         elif kind == "spread":
@@ -1642,9 +1701,11 @@ class FitError(Exception):
 
 
 class GenericScheduler:
-    def __init__(self, predicate_keys, priority_configs, custom_predicates=None, hard_weight=10, spread=None):
+    def __init__(self, predicate_keys, priority_configs, custom_predicates=None, hard_weight=10, spread=None,
+                 custom_priorities=None):
         self.predicates = set(predicate_keys) | set(MANDATORY_PREDICATES)
         self.spread = spread              # SpreadListers (None: the simulator's empty listers)
+        self.custom_priorities = custom_priorities
         self.custom = dict(custom_predicates or {})
         self.prioritizers = list(priority_configs)
         self.hard_weight = hard_weight    # hardPodAffinitySymmetricWeight (simulator: 10)
@@ -1675,7 +1736,8 @@ class GenericScheduler:
             raise FitError(len(infos), failed)
         if len(filtered) == 1:
             return filtered[0].name
-        scores = prioritize_nodes(pod, filtered, self.prioritizers, infos, self.hard_weight, self.spread)
+        scores = prioritize_nodes(pod, filtered, self.prioritizers, infos, self.hard_weight, self.spread,
+                                  self.custom_priorities)
         return self.select_host([(ni.name, s) for ni, s in zip(filtered, scores)])
 
     def select_host(self, plist):
@@ -1807,7 +1869,8 @@ def expand_simulation_pods(spec_list):
     return out
 
 
-def simulate(nodes, running_pods, sim_pods, predicate_keys, priority_configs, custom_predicates=None, spread=None):
+def simulate(nodes, running_pods, sim_pods, predicate_keys, priority_configs, custom_predicates=None, spread=None,
+             custom_priorities=None):
     """Runs the ClusterCapacity loop: pods are popped LIFO (store.go:223-233),
     each is scheduled, bound pods are assumed into the node cache (scheduler.go:366
     → cache.go:125 → node_info.go:318), unschedulable pods are recorded and the
@@ -1819,7 +1882,8 @@ def simulate(nodes, running_pods, sim_pods, predicate_keys, priority_configs, cu
         nn = (p.get("spec") or {}).get("nodeName", "")
         if nn in by_name:
             by_name[nn].add_pod(p)
-    sched = GenericScheduler(predicate_keys, priority_configs, custom_predicates, spread=spread)
+    sched = GenericScheduler(predicate_keys, priority_configs, custom_predicates, spread=spread,
+                             custom_priorities=custom_priorities)
     queue = list(sim_pods)
     out = []
     while queue:

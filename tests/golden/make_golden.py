@@ -938,11 +938,43 @@ def spread_cases():
                            "sss": c.get("sss") or [],
                            "expect": {h["host"]: h["score"] for h in c["expectedList"]}})
 
+def label_priority_cases():
+    """TestNewNodeLabelPriority (node_label_test.go:30-128) and TestZoneSpreadPriority — the
+    ServiceAntiAffinity priority with label "zone" (selector_spreading_test.go:605-760)."""
+    import go_literal as g
+    nf = S + "algorithm/priorities/node_label_test.go"
+    with open(REF + nf) as f:
+        src = f.read()
+    start = src.index("func TestNewNodeLabelPriority(")
+    _, cs = g.parse_test(src, "TestNewNodeLabelPriority")
+    for c in cs:
+        add("label_priorities", {"source": "%s:%d" % (nf, _line_of(src, c["test"], start)), "test": c["test"],
+                                 "kind": "labelPreference", "label": c["label"], "presence": c["presence"],
+                                 "pod": {"metadata": {}}, "pods": [], "nodes": c["nodes"], "services": [],
+                                 "expect": {h["host"]: h["score"] for h in c["expectedList"]}})
+    sf = S + "algorithm/priorities/selector_spreading_test.go"
+    with open(REF + sf) as f:
+        src = f.read()
+    start = src.index("func TestZoneSpreadPriority(")
+    _, cs = g.parse_test(src, "TestZoneSpreadPriority")
+    for c in cs:
+        pod = c.get("pod") or {}
+        if pod.get("__call__") == "new":
+            pod = {}
+        pod.setdefault("metadata", {})
+        nodes = [{"metadata": {"name": nm, "labels": lab}} for nm, lab in c["nodes"].items()]
+        add("label_priorities", {"source": "%s:%d" % (sf, _line_of(src, c["test"], start)), "test": c["test"],
+                                 "kind": "serviceAntiAffinity", "label": "zone", "pod": pod,
+                                 "pods": c.get("pods") or [], "nodes": nodes, "services": c.get("services") or [],
+                                 "expect": {h["host"]: h["score"] for h in c["expectedList"]}})
+
+
 if os.path.isdir(REF):
     interpod_cases()
     spread_cases()
+    label_priority_cases()
 else:  # keep the committed fixtures when the reference checkout is absent
-    for group in ("interpod_predicates", "interpod_priorities", "spread"):
+    for group in ("interpod_predicates", "interpod_priorities", "spread", "label_priorities"):
         with open(os.path.join(HERE, group + ".json")) as f:
             cases[group] = json.load(f)
 

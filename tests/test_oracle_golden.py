@@ -128,3 +128,16 @@ def test_selector_spread(c):
     listers = R.SpreadListers(c["services"], c["rcs"], c["rss"], c["sss"])
     scores = R.prioritize_nodes(c["pod"], infos, [("SelectorSpreadPriority", 1)], spread=listers)
     assert {ni.name: s for ni, s in zip(infos, scores)} == c["expect"]
+
+
+@pytest.mark.parametrize("c", load("label_priorities"), ids=case_id)
+def test_label_priorities(c):
+    """Policy priorities with arguments: labelPreference (node_label_test.go:30-128) and
+    serviceAntiAffinity (TestZoneSpreadPriority, selector_spreading_test.go:605-760)."""
+    infos = _infos(c["nodes"], c["pods"])
+    if c["kind"] == "labelPreference":
+        custom = {"P": R.node_label_priority(c["label"], c["presence"])}
+    else:
+        custom = {"P": R.service_anti_affinity_priority(c["label"], R.SpreadListers(c["services"]))}
+    scores = R.prioritize_nodes(c["pod"], infos, [("P", 1)], custom=custom)
+    assert {ni.name: s for ni, s in zip(infos, scores)} == c["expect"]

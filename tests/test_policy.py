@@ -48,10 +48,36 @@ def test_1_9_policy_key_sets():
     assert cfg.const_score == 2 * (1 + 0 + 10 + 10 + 0)
 
 
-def test_1_0_policy_custom_priority_unsupported():
+def test_1_0_policy_custom_priorities():
+    """The 1.0 compatibility policy's serviceAntiAffinity / labelPreference priorities register under
+    their policy names (factory/plugins.go:271-323)."""
     (c,) = [c for c in load("policy") if c["version"] == "1.0"]
+    pol = policy.decode(c["json"])
+    _, prios, _ = policy.key_sets(pol)
+    args = policy.priority_arguments(pol)
+    assert args == {"TestServiceAntiAffinity": ("serviceAntiAffinity", "zone"),
+                    "TestLabelPreference": ("labelPreference", "bar", True)}
+    assert ("TestServiceAntiAffinity", 3) in prios and ("TestLabelPreference", 4) in prios
     with pytest.raises(abi.KsimUnsupported):
-        policy.key_sets(policy.decode(c["json"]))
+        policy.key_sets(policy.decode({"priorities": [{"name": "X", "weight": 1, "argument": {"bogus": {}}}]}))
+
+
+def test_label_set_priorities_as_addends():
+    """NodeLabel / ServiceAntiAffinity (no services) scores are functions of the label set: carried
+    as per-NodeAffinity-class addends."""
+    import ksim_ref as R
+    from ksim import ingest
+    nodes = [{"metadata": {"name": "n%d" % i, "labels": lab}, "status": {"allocatable": {"cpu": "1", "pods": "9"}}}
+             for i, lab in enumerate([{}, {"bar": "1"}, {"zone": "a"}, {"bar": "2", "zone": "b"}])]
+    cl = ingest.Cluster.from_objects(nodes, [], [{"metadata": {"name": "p"}, "spec": {}}])
+    custom = {"LP": ("labelPreference", "bar", True), "SAA": ("serviceAntiAffinity", "zone")}
+    t, add = scheduler.class_tables_for(cl.tables, [("LP", 4), ("SAA", 3)], cl.label_sets.items, custom)
+    got = [int(add[0][t["na_class"][0][int(cl.cols["label_set"][i])]]) for i in range(4)]
+    infos = [R.NodeInfo(x) for x in sorted(nodes, key=lambda x: x["metadata"]["name"].encode())]
+    want = R.prioritize_nodes({"metadata": {}}, infos, [("LP", 4), ("SAA", 3)],
+                              custom={"LP": R.node_label_priority("bar", True),
+                                      "SAA": R.service_anti_affinity_priority("zone")})
+    assert got == want
 
 
 def test_missing_sections_use_default_provider_and_mandatory_predicate():
@@ -95,6 +121,13 @@ GPU_POLICIES = {
                                          {"name": "BalancedResourceAllocation", "weight": 1},
                                          {"name": "EqualPriority", "weight": 1}]},
     "defaults_1_9_like": {"kind": "Policy"},
+    "label_priorities": {"predicates": [{"name": "GeneralPredicates"}, {"name": "PodToleratesNodeTaints"}],
+                         "priorities": [{"name": "LeastRequestedPriority", "weight": 1},
+                                        {"name": "PreferSsd", "weight": 3,
+                                         "argument": {"labelPreference": {"label": "rank", "presence": True}}},
+                                        {"name": "SpreadByTier", "weight": 2,
+                                         "argument": {"serviceAntiAffinity": {"label": "tier"}}},
+                                        {"name": "NodePreferAvoidPodsPriority", "weight": 10000}]},
 }
 
 
@@ -109,9 +142,11 @@ def test_gpu_policy_run_matches_oracle(name, mode):
     pol = policy.decode(GPU_POLICIES[name])
     preds, prios, lp = policy.key_sets(pol)
     custom = {"CheckNodeLabelPresence": R.new_node_label_predicate(*lp)} if lp else None
+    cprios = {n: (R.node_label_priority(a[1], a[2]) if a[0] == "labelPreference" else R.service_anti_affinity_priority(a[1]))
+              for n, a in policy.priority_arguments(pol).items()}
     for seed in (3, 11):
         nodes, running, pods = rnd_workload(seed, n_nodes=31 + seed, n_pods=140)
-        want, lni = R.simulate(nodes, running, pods, set(preds), list(prios), custom)
+        want, lni = R.simulate(nodes, running, pods, set(preds), list(prios), custom, custom_priorities=cprios)
         rep = scheduler.ClusterCapacity(nodes, running, pods, policy_obj=pol, mode=mode).run()
         got = {n: (h, None) for n, h in rep.successful}
         got.update({n: (None, m) for n, m in rep.failed})
