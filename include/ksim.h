@@ -39,7 +39,7 @@ extern "C" {
 
 #define KSIM_MAX_SCALAR 8   /* extended / hugepage resource columns */
 #define KSIM_MAX_RCLASS 16  /* reduce classes per pod (TaintToleration x NodeAffinity) */
-#define KSIM_NREASONS 31    /* failure-reason histogram slots */
+#define KSIM_NREASONS 32    /* failure-reason histogram slots */
 #define KSIM_MAX_RANKS 8    /* devices of one node-sharded cluster */
 
 /* ---- predicate key bits: the FitPredicate keys of predicates.go:129-138 that carry
@@ -68,6 +68,9 @@ extern "C" {
 #define KSIM_P_MAX_AZURE_DISK (1u << 16)          /* MaxAzureDiskVolumeCount */
 #define KSIM_P_VOLUME_ZONE (1u << 17)             /* NoVolumeZoneConflict (predicates.go:539-633), as the
                                                      per (volume class, label set) verdict zone_ok */
+#define KSIM_P_SERVICE_AFFINITY (1u << 18)        /* CheckServiceAffinity with a serviceAffinity argument
+                                                     (predicates.go:940-1016), as the per (pod class, label
+                                                     set) verdict ksim_class_tables.svc_ok */
 
 /* ---- priority weight slots (0 = not configured).  Priorities that evaluate to the
  *      same value on every node under supported inputs (SelectorSpread /
@@ -102,6 +105,7 @@ extern "C" {
 #define KSIM_POD_BEST_EFFORT (1u << 1)  /* qos.go:39 BestEffort */
 #define KSIM_POD_NEED_SELECTOR (1u << 2)/* nodeSelector/required affinity not matching every label set */
 #define KSIM_POD_NEED_TAINTS (1u << 3)  /* some taint set is not tolerated */
+#define KSIM_POD_NEED_SVC_AFFINITY (1u << 4) /* CheckServiceAffinity fails on some label set (launch kernels) */
 
 /* ---- failure reasons: bit r of a node's reason mask / slot r of a histogram ---- */
 #define KSIM_R_NOT_READY 0
@@ -130,6 +134,7 @@ extern "C" {
 #define KSIM_R_DISK_CONFLICT 28           /* node(s) had no available disk (ErrDiskConflict) */
 #define KSIM_R_MAX_VOLUME_COUNT 29        /* node(s) exceed max volume count (ErrMaxVolumeCountExceeded) */
 #define KSIM_R_VOLUME_ZONE 30             /* node(s) had no available volume zone (ErrVolumeZoneConflict) */
+#define KSIM_R_SERVICE_AFFINITY 31        /* node(s) didn't match service affinity (ErrServiceAffinityViolated) */
 
 /* ---- execution modes ---- */
 #define KSIM_MODE_AUTO 0        /* library picks (persistent when it fits) */
@@ -205,6 +210,10 @@ typedef struct {
    * NodeAffinity value.  When set, the NodeAffinity class dimension is used whatever
    * NodeAffinityPriority's weight (n_na then counts (preferred weight, avoid score) pairs). */
   const int64_t* na_add;
+  /* Optional (NULL = every node passes): CheckServiceAffinity's verdict per label set,
+   * [n_classes][words] like sel_ok — the pod's nodeSelector values of the predicate's labels must
+   * be the node's (FindLabelsInSet, CreateSelectorFromLabels; no service selects the pod). */
+  const uint32_t* svc_ok;
 } ksim_class_tables;
 
 /* Pod descriptor, 128 bytes.  The three request vectors follow the reference exactly:

@@ -110,6 +110,7 @@ struct KsimCtx {
   const int64_t* __restrict__ tt_val;
   const int64_t* __restrict__ na_val;
   const int64_t* __restrict__ na_add;  // [C][KSIM_MAX_RCLASS] weighted per-NA-class addend, or null
+  const uint32_t* __restrict__ svc_ok; // [C][lwords] CheckServiceAffinity per label set, or null
   int32_t use_na;                      // NA class dimension in use: NodeAffinity weight or na_add
   int32_t lwords, twords, n_label_sets, n_taint_sets;
   int32_t n_classes_dev;  // pod classes in the tables
@@ -579,6 +580,9 @@ __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ks
     if (!a.noexec_ok(P, i)) return 1u << KSIM_R_TAINTS;
   }
   if ((pr & KSIM_P_LABEL_PRESENCE) && (r.fl & KSIM_N_LABEL_PRESENCE)) return 1u << KSIM_R_LABEL_PRESENCE;
+  if ((pr & KSIM_P_SERVICE_AFFINITY) && (P.flags & KSIM_POD_NEED_SVC_AFFINITY) && c.svc_ok &&
+      !ksim_bit(c.svc_ok, P.cls, c.lwords, c.label_set[i]))
+    return 1u << KSIM_R_SERVICE_AFFINITY;
   if (vol) {
     const uint32_t which = ((pr & KSIM_P_MAX_EBS) ? KSIM_VOL_EBS : 0u) | ((pr & KSIM_P_MAX_GCE_PD) ? KSIM_VOL_GCE_PD : 0u) |
                            ((pr & KSIM_P_MAX_AZURE_DISK) ? KSIM_VOL_AZURE_DISK : 0u);

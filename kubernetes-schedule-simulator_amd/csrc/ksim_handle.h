@@ -162,7 +162,7 @@ struct ksim_handle {
   KsimVol* vol_dev = nullptr;
   std::vector<void*> vol_bufs;
   std::vector<int32_t> q_vclass;
-  std::vector<int64_t> vol_pre;  // vol_pre[i] = volume pods among the first i queued
+  std::vector<int64_t> vol_pre;  // vol_pre[i] = volume / service-affinity pods among the first i queued
 };
 
 int ksim_fail(ksim_handle* h, int code, const char* fmt, ...);

@@ -39,7 +39,7 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
     if (cfg->weights[k] < 0) return ksim_fail(nullptr, KSIM_E_INVAL, "ksim_create: negative weight in slot %d", k);
   if (cfg->mode < KSIM_MODE_AUTO || cfg->mode > KSIM_MODE_TREE)
     return ksim_fail(nullptr, KSIM_E_INVAL, "ksim_create: unknown mode %d", cfg->mode);
-  const uint32_t known = (1u << 18) - 1;  // KSIM_P_CHECK_NODE_CONDITION .. KSIM_P_VOLUME_ZONE
+  const uint32_t known = (1u << 19) - 1;  // KSIM_P_CHECK_NODE_CONDITION .. KSIM_P_SERVICE_AFFINITY
   if (cfg->predicates & ~known) return ksim_fail(nullptr, KSIM_E_UNSUPPORTED, "ksim_create: unknown predicate bits");
   ksim_handle* h = new ksim_handle();
   h->device = cfg->device;
@@ -178,7 +178,7 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
   }
   KsimCtx& c = h->ctx;
   int rc;
-  uint32_t *so, *to, *no;
+  uint32_t *so, *to, *no, *sv = nullptr;
   uint8_t *tc, *nc;
   int32_t *ntt, *nna;
   int64_t *tv, *nv, *na = nullptr;
@@ -190,14 +190,15 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
       (rc = dev_upload(h, &ntt, t->n_tt ? t->n_tt : ones.data(), C)) ||
       (rc = dev_upload(h, &nna, t->n_na ? t->n_na : ones.data(), C)) ||
       (rc = dev_upload(h, &tv, t->tt_val, C * KSIM_MAX_RCLASS)) || (rc = dev_upload(h, &nv, t->na_val, C * KSIM_MAX_RCLASS)) ||
-      (t->na_add && (rc = dev_upload(h, &na, t->na_add, C * KSIM_MAX_RCLASS))))
+      (t->na_add && (rc = dev_upload(h, &na, t->na_add, C * KSIM_MAX_RCLASS))) ||
+      (t->svc_ok && (rc = dev_upload(h, &sv, t->svc_ok, C * lw))))
     return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   for (void* q : h->class_bufs) dev_free(h, q);  // the previous tables (reload)
   h->class_bufs.clear();
   for (size_t k = nb0; k < h->bufs.size(); ++k) h->class_bufs.push_back(h->bufs[k].p);
   c.sel_ok = so; c.taint_ok = to; c.noexec_ok = no; c.tt_class = tc; c.na_class = nc;
-  c.n_tt = ntt; c.n_na = nna; c.tt_val = tv; c.na_val = nv; c.na_add = na;
+  c.n_tt = ntt; c.n_na = nna; c.tt_val = tv; c.na_val = nv; c.na_add = na; c.svc_ok = sv;
   c.use_na = (c.w[KSIM_W_NODE_AFFINITY] != 0 || na) ? 1 : 0;
   c.lwords = (int32_t)lw; c.twords = (int32_t)tw;
   c.n_label_sets = (int32_t)L; c.n_taint_sets = (int32_t)T;
@@ -269,7 +270,7 @@ int64_t ksim_rt_aff_count(const ksim_handle* h, int64_t first, int64_t count) {
 
 int64_t ksim_rt_launch_only_count(const ksim_handle* h, int64_t first, int64_t count) {
   int64_t k = ksim_rt_aff_count(h, first, count);
-  if (h->have_vol && count > 0) k += h->vol_pre[first + count] - h->vol_pre[first];
+  if (count > 0) k += h->vol_pre[first + count] - h->vol_pre[first];  // volume and service-affinity pods
   return k;
 }
 
@@ -287,8 +288,8 @@ static bool fast_base(const ksim_pod& p) {
   bool in_range = true;
   for (int64_t v : {p.req_cpu, p.req_mem, p.add_cpu, p.add_mem, p.nz_cpu, p.nz_mem}) in_range &= v >= 0 && v < lim;
   return in_range && p.host == -1 && p.port_cnt == 0 && p.scalar_cnt == 0 && p.req_gpu == 0 && p.req_eph == 0 &&
-         !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS)) && p.aff_ident == 0 && p.aff_class == 0 &&
-         p.vol_class == 0;
+         !(p.flags & (KSIM_POD_NEED_SELECTOR | KSIM_POD_NEED_TAINTS | KSIM_POD_NEED_SVC_AFFINITY)) && p.aff_ident == 0 &&
+         p.aff_class == 0 && p.vol_class == 0;
 }
 
 static bool fast_k(const ksim_handle* h, int32_t cls) {
@@ -387,7 +388,7 @@ int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
     h->q_aclass[q] = p.aff_class;
     h->aff_pre[q + 1] = h->aff_pre[q] + ((p.aff_ident || p.aff_class) ? 1 : 0);
     h->q_vclass[q] = p.vol_class;
-    h->vol_pre[q + 1] = h->vol_pre[q] + (p.vol_class ? 1 : 0);
+    h->vol_pre[q + 1] = h->vol_pre[q] + ((p.vol_class || (p.flags & KSIM_POD_NEED_SVC_AFFINITY)) ? 1 : 0);
     const bool fast = h->q_base[q] && fast_k(h, p.cls);
     h->fast_pre[q + 1] = h->fast_pre[q] + (fast ? 1 : 0);
     int64_t m = 0;

@@ -17,7 +17,7 @@ E_INVAL, E_DEVICE, E_NOMEM, E_UNSUPPORTED, E_STATE, E_OVERFLOW, E_NO_NODES = -1,
 ABI_VERSION = 5
 MAX_SCALAR = 8
 MAX_RCLASS = 16
-NREASONS = 31
+NREASONS = 32
 
 # predicate bits
 P_CHECK_NODE_CONDITION = 1 << 0
@@ -38,6 +38,7 @@ P_MAX_EBS = 1 << 14
 P_MAX_GCE_PD = 1 << 15
 P_MAX_AZURE_DISK = 1 << 16
 P_VOLUME_ZONE = 1 << 17
+P_SERVICE_AFFINITY = 1 << 18
 
 W_LEAST, W_MOST, W_BALANCED, W_TAINT_TOL, W_NODE_AFF, W_INTERPOD, W_SPREAD = range(7)
 NW = 7
@@ -45,7 +46,7 @@ NW = 7
 N_NOT_READY, N_OUT_OF_DISK, N_NET_UNAVAIL, N_UNSCHEDULABLE = 1, 2, 4, 8
 N_MEM_PRESSURE, N_DISK_PRESSURE, N_LABEL_PRESENCE = 16, 32, 64
 
-POD_ANY_REQUEST, POD_BEST_EFFORT, POD_NEED_SELECTOR, POD_NEED_TAINTS = 1, 2, 4, 8
+POD_ANY_REQUEST, POD_BEST_EFFORT, POD_NEED_SELECTOR, POD_NEED_TAINTS, POD_NEED_SVC_AFFINITY = 1, 2, 4, 8, 16
 
 MODE_AUTO, MODE_LAUNCH, MODE_PERSISTENT, MODE_TREE = 0, 1, 2, 3
 
@@ -55,7 +56,7 @@ R_HOSTNAME, R_HOST_PORTS, R_NODE_SELECTOR, R_TAINTS = 9, 10, 11, 12
 R_MEM_PRESSURE, R_DISK_PRESSURE, R_LABEL_PRESENCE = 13, 14, 15
 R_SCALAR0 = 16
 R_POD_AFFINITY, R_EXISTING_ANTI, R_AFFINITY_RULES, R_ANTI_AFFINITY_RULES = 24, 25, 26, 27
-R_DISK_CONFLICT, R_MAX_VOLUME_COUNT, R_VOLUME_ZONE = 28, 29, 30
+R_DISK_CONFLICT, R_MAX_VOLUME_COUNT, R_VOLUME_ZONE, R_SERVICE_AFFINITY = 28, 29, 30, 31
 
 # inter-pod affinity tables (ksim_affinity_tables)
 AFF_REQ_AFFINITY, AFF_REQ_ANTI, AFF_PREFERRED = 0, 1, 2
@@ -91,7 +92,7 @@ class ClassTables(C.Structure):
     _fields_ = [("n_classes", C.c_int32), ("n_label_sets", C.c_int32), ("n_taint_sets", C.c_int32),
                 ("sel_ok", _u32p), ("taint_ok", _u32p), ("noexec_ok", _u32p), ("tt_class", _u8p),
                 ("na_class", _u8p), ("n_tt", _i32p), ("n_na", _i32p), ("tt_val", _i64p), ("na_val", _i64p),
-                ("na_add", _i64p)]
+                ("na_add", _i64p), ("svc_ok", _u32p)]
 
 
 class Pod(C.Structure):

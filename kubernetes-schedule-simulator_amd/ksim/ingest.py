@@ -725,6 +725,9 @@ def class_tables_struct(d, na_add=None):
     if na_add is not None:
         d["na_add"] = np.ascontiguousarray(na_add, np.int64)
         t.na_add = abi.ptr(d["na_add"], abi.C.c_int64)
+    if d.get("svc_ok") is not None:
+        d["svc_ok"] = np.ascontiguousarray(d["svc_ok"], np.uint32)
+        t.svc_ok = abi.ptr(d["svc_ok"], abi.C.c_uint32)
     return t
 
 

@@ -17,7 +17,7 @@ Reference semantics (paths under vendor/k8s.io/kubernetes/pkg/scheduler/):
   evaluated.
 
 Unsupported pieces raise Unsupported (never a silently different result): HTTP extenders,
-alwaysCheckAllPredicates, CheckServiceAffinity, custom priorities with arguments other than
+alwaysCheckAllPredicates, CheckServiceAffinity without a serviceAffinity argument, custom priorities with arguments other than
 labelPreference / serviceAntiAffinity
 (ServiceAntiAffinity / NodeLabelPriority) and priority keys outside the supported set.
 """
@@ -147,6 +147,9 @@ def key_sets(policy: Policy):
                     label_presence = (list(lp.get("labels") or []), bool(lp.get("presence", False)))
                     preds.append(name)
                     continue
+                if name == "CheckServiceAffinity" and arg.get("serviceAffinity") is not None:
+                    preds.append(name)   # its labels: service_affinity_labels(policy)
+                    continue
                 raise Unsupported("policy: predicate %r with argument %r is outside the supported key set" % (name, arg))
             if name == "CheckNodeLabelPresence":
                 raise Unsupported("policy: CheckNodeLabelPresence needs a labelsPresence argument")
@@ -166,6 +169,16 @@ def key_sets(policy: Policy):
             prios[name] = weight  # a repeated name re-registers it: the last weight wins (plugins.go:343)
         prios = list(prios.items())
     return preds, prios, label_presence
+
+
+def service_affinity_labels(policy: Policy):
+    """The labels of a CheckServiceAffinity predicate registered with a serviceAffinity argument
+    (factory/plugins.go:199-239), or None."""
+    out = None
+    for name, arg in policy.predicates or []:
+        if name == "CheckServiceAffinity" and arg and arg.get("serviceAffinity") is not None:
+            out = list(arg["serviceAffinity"].get("labels") or [])
+    return out
 
 
 def _priority_argument(name, arg):

@@ -43,6 +43,7 @@ PREDICATE_BITS = {
     "MaxGCEPDVolumeCount": abi.P_MAX_GCE_PD,
     "MaxAzureDiskVolumeCount": abi.P_MAX_AZURE_DISK,
     "NoVolumeZoneConflict": abi.P_VOLUME_ZONE,
+    "CheckServiceAffinity": abi.P_SERVICE_AFFINITY,     # with a Policy serviceAffinity argument
 }
 VOLUME_PREDICATE_BITS = abi.P_DISK_CONFLICT | abi.P_MAX_EBS | abi.P_MAX_GCE_PD | abi.P_MAX_AZURE_DISK | abi.P_VOLUME_ZONE
 # factory/plugins.go:401-406 + defaults.go:165: part of every predicate map
@@ -148,6 +149,7 @@ REASON_TEXT = {
     abi.R_DISK_CONFLICT: "node(s) had no available disk",
     abi.R_MAX_VOLUME_COUNT: "node(s) exceed max volume count",
     abi.R_VOLUME_ZONE: "node(s) had no available volume zone",
+    abi.R_SERVICE_AFFINITY: "node(s) didn't match service affinity",
 }
 
 
@@ -225,6 +227,28 @@ def class_tables_for(tables, priorities, label_sets=(), custom=None):
     return d, add
 
 
+def service_affinity_table(class_specs, label_sets, affinity_labels):
+    """CheckServiceAffinity (predicates.go:980-1016) with no service selecting the pod: per pod
+    class the label sets carrying the class's nodeSelector values of `affinity_labels`
+    (FindLabelsInSet, CreateSelectorFromLabels — labels.Set.AsSelector, Everything when empty or
+    invalid).  Returns ([n_classes][words] bits, per-class "fails somewhere")."""
+    from . import labels as L
+    C, S = len(class_specs), len(label_sets)
+    words = max((S + 31) // 32, 1)
+    ok = np.zeros((C, words), np.uint32)
+    need = np.zeros(C, bool)
+    for k, spec in enumerate(class_specs):
+        sel = (spec or {}).get("nodeSelector") or {}
+        al = {x: sel[x] for x in affinity_labels if x in sel}
+        req = L.from_set(al)
+        for j, ls in enumerate(label_sets):
+            if L.matches(req, dict(ls)):
+                ok[k, j >> 5] |= np.uint32(1 << (j & 31))
+            else:
+                need[k] = True
+    return ok, need
+
+
 def check_volume_support(cluster, predicates):
     """Refuse inputs on which a configured volume predicate returns an error instead of a verdict
     (ksim/volumes.py): findNodesThatFit then aborts the pod's cycle (core/generic_scheduler.go:351-353)
@@ -256,7 +280,8 @@ class GenericScheduler:
     (labels, presence) of a Policy's CheckNodeLabelPresence predicate (policy.key_sets)."""
 
     def __init__(self, cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO,
-                 collect_reasons=True, last_node_index=0, label_presence=None, custom_priorities=None):
+                 collect_reasons=True, last_node_index=0, label_presence=None, custom_priorities=None,
+                 service_affinity=None):
         self.cluster = cluster
         self.predicates = list(predicates)
         self.prioritizers = list(priorities)
@@ -271,6 +296,11 @@ class GenericScheduler:
             raise Unsupported("ImageLocalityPriority with nodes that list status.images")
         if "CheckNodeLabelPresence" in self.predicates and label_presence is None:
             raise Unsupported("CheckNodeLabelPresence needs its labelsPresence argument")
+        if "CheckServiceAffinity" in self.predicates:
+            if service_affinity is None:
+                raise Unsupported("CheckServiceAffinity needs its serviceAffinity argument")
+            if getattr(cluster, "spread_active", False):
+                raise Unsupported("CheckServiceAffinity with services selecting the pods (the pod lister's order decides)")
         self.cfg = make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence],
                                [(n, w) for n, w in priorities if n not in self.custom_priorities],
                                device, mode, collect_reasons, last_node_index,
@@ -290,8 +320,15 @@ class GenericScheduler:
         self.const_score = self.cfg.const_score - (10 * sum(int(x) for n, x in self.prioritizers
                                                             if n == "NodePreferAvoidPodsPriority")
                                                    if self.tables.get("pa_in_add") else 0)
-        self.h.call("ksim_load_classes", C.byref(class_tables_struct(self.tables, self.na_add)))
         pods = np.ascontiguousarray(cluster.pods)
+        if "CheckServiceAffinity" in self.predicates:
+            ok, need = service_affinity_table(cluster.classes.items or [{}],
+                                              cluster.label_sets.items, service_affinity)
+            self.tables = dict(self.tables, svc_ok=ok)
+            if len(pods):
+                pods = pods.copy()
+                pods["flags"] |= np.where(need[pods["cls"]], abi.POD_NEED_SVC_AFFINITY, 0).astype(np.uint32)
+        self.h.call("ksim_load_classes", C.byref(class_tables_struct(self.tables, self.na_add)))
         self.affinity = None
         if cluster.affinity is not None:
             if self.cfg.predicates & abi.P_INTERPOD_AFFINITY or ((self.cfg.weights[abi.W_INTERPOD] or
@@ -564,10 +601,12 @@ class ClusterCapacity:
                  policy_obj=None, pvs=(), pvcs=(), storage_classes=(), spread=None):
         label_presence = None
         custom = None
+        svc_aff = None
         if policy_obj is not None:
-            from .policy import key_sets, priority_arguments
+            from .policy import key_sets, priority_arguments, service_affinity_labels
             predicates, priorities, label_presence = key_sets(policy_obj)
             custom = priority_arguments(policy_obj)
+            svc_aff = service_affinity_labels(policy_obj)
         if predicates is None or priorities is None:
             p, q = provider(provider_name)
             predicates = p if predicates is None else predicates
@@ -583,7 +622,7 @@ class ClusterCapacity:
                                             spread_services_only="ServiceSpreadingPriority" in names)
         self.scheduler = GenericScheduler(self.cluster, predicates, priorities, device=device, mode=mode,
                                           collect_reasons=collect_reasons, label_presence=label_presence,
-                                          custom_priorities=custom)
+                                          custom_priorities=custom, service_affinity=svc_aff)
 
     def run(self) -> Report:
         from .report import ERR_NO_NODES, get_report, simulation_status

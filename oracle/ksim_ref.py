@@ -956,6 +956,46 @@ ORDERING = ["CheckNodeCondition", "CheckNodeUnschedulable", "GeneralPredicates",
             "CheckNodeMemoryPressure", "CheckNodeDiskPressure", "MatchInterPodAffinity"]
 
 
+R_SERVICE_AFFINITY = "node(s) didn't match service affinity"   # error.go:57
+
+
+def new_service_affinity_predicate(affinity_labels, services=(), pods=(), nodes=()):
+    """ServiceAffinity.checkServiceAffinity (predicates.go:940-1016) with its metadata producer
+    (:958-978): `services` what the ServiceLister holds, `pods` the PodLister's pods (in its order),
+    `nodes` the NodeLister's nodes.  The node must carry the pod's nodeSelector values of the listed
+    labels; when some are missing and a service selects the pod, the first pod with the pod's
+    labels (FilterOutPods, node_info.go:466-488) lends its node's values."""
+    by_name = {(n.get("metadata") or {}).get("name", ""): n for n in nodes}
+
+    def pred(pod, ni):
+        md = pod.get("metadata") or {}
+        ns, lab = md.get("namespace", ""), md.get("labels") or {}
+        svcs = [x for x in services if (x.get("metadata") or {}).get("namespace", "") == ns and
+                (x.get("spec") or {}).get("selector") is not None and
+                SpreadListers._set_matches((x.get("spec") or {}).get("selector"), lab)]
+        own = selector_from_set(lab)
+        matching = [q for q in pods if (q.get("metadata") or {}).get("namespace", "") == ns and
+                    selector_matches(own, (q.get("metadata") or {}).get("labels") or {})]
+        keys = {pod_key(q) for q in ni.pods}
+        filtered = [q for q in matching
+                    if (q.get("spec") or {}).get("nodeName", "") != ni.name or pod_key(q) in keys]
+        sel = (pod.get("spec") or {}).get("nodeSelector") or {}
+        al = {k: sel[k] for k in affinity_labels if k in sel}
+        if len(affinity_labels) > len(al) and svcs and filtered:
+            nn = (filtered[0].get("spec") or {}).get("nodeName", "")
+            if nn not in by_name:
+                raise PredicateError("node %r not found" % nn)
+            nl = (by_name[nn].get("metadata") or {}).get("labels") or {}
+            for k in affinity_labels:
+                if k not in al and k in nl:
+                    al[k] = nl[k]
+        node_labels = (ni.node.get("metadata") or {}).get("labels") or {}
+        if selector_matches(selector_from_set(al), node_labels):
+            return True, []
+        return False, [R_SERVICE_AFFINITY]
+    return pred
+
+
 R_LABEL_PRESENCE = "node(s) didn't have the requested labels"
 
 

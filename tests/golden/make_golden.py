@@ -969,12 +969,31 @@ def label_priority_cases():
                                  "expect": {h["host"]: h["score"] for h in c["expectedList"]}})
 
 
+def service_affinity_cases():
+    """TestServiceAffinity (predicates_test.go:1460-1620): the pod lister's pods, the service
+    lister's services, the node list of the five machines; the predicate's NodeInfo holds the test
+    node and no pods."""
+    import go_literal as g
+    pf = S + "algorithm/predicates/predicates_test.go"
+    with open(REF + pf) as f:
+        src = f.read()
+    start = src.index("func TestServiceAffinity(")
+    loc, cs = g.parse_test(src, "TestServiceAffinity")
+    nodes = [loc["node%d" % i] for i in range(1, 6)]
+    for c in cs:
+        add("service_affinity", {"source": "%s:%d" % (pf, _line_of(src, c["test"], start)), "test": c["test"],
+                                 "pod": c.get("pod") or {"metadata": {}}, "pods": c.get("pods") or [],
+                                 "node": c["node"], "nodes": nodes, "services": c.get("services") or [],
+                                 "labels": c["labels"], "fits": c["fits"]})
+
+
 if os.path.isdir(REF):
     interpod_cases()
     spread_cases()
     label_priority_cases()
+    service_affinity_cases()
 else:  # keep the committed fixtures when the reference checkout is absent
-    for group in ("interpod_predicates", "interpod_priorities", "spread", "label_priorities"):
+    for group in ("interpod_predicates", "interpod_priorities", "spread", "label_priorities", "service_affinity"):
         with open(os.path.join(HERE, group + ".json")) as f:
             cases[group] = json.load(f)
 

@@ -118,7 +118,7 @@ def test_policy_mapping():
     assert cfg.const_score == 10 + 0 + 10 * 10000
     assert cfg.predicates & abi.P_GENERAL and cfg.predicates & abi.P_CHECK_NODE_CONDITION
     with pytest.raises(abi.KsimUnsupported):
-        scheduler.make_config(["CheckServiceAffinity"], [])
+        scheduler.make_config(["NoSuchPredicate"], [])
     with pytest.raises(abi.KsimUnsupported):
         scheduler.make_config([], [("NoSuchPriority", 1)])
     assert scheduler.make_config([], [("ImageLocalityPriority", 1)]).const_score == 0   # no node images

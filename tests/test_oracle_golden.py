@@ -141,3 +141,13 @@ def test_label_priorities(c):
         custom = {"P": R.service_anti_affinity_priority(c["label"], R.SpreadListers(c["services"]))}
     scores = R.prioritize_nodes(c["pod"], infos, [("P", 1)], custom=custom)
     assert {ni.name: s for ni, s in zip(infos, scores)} == c["expect"]
+
+
+@pytest.mark.parametrize("c", load("service_affinity"), ids=case_id)
+def test_service_affinity(c):
+    """CheckServiceAffinity (TestServiceAffinity, predicates_test.go:1460-1620)."""
+    ni = R.NodeInfo(c["node"])
+    pred = R.new_service_affinity_predicate(c["labels"], c["services"], c["pods"], c["nodes"])
+    ok, reasons = pred(c["pod"], ni)
+    assert ok == c["fits"]
+    assert reasons == ([] if ok else [R.R_SERVICE_AFFINITY])

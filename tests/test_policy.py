@@ -121,6 +121,11 @@ GPU_POLICIES = {
                                          {"name": "BalancedResourceAllocation", "weight": 1},
                                          {"name": "EqualPriority", "weight": 1}]},
     "defaults_1_9_like": {"kind": "Policy"},
+    "service_affinity": {"predicates": [{"name": "PodFitsResources"}, {"name": "PodToleratesNodeTaints"},
+                                        {"name": "CheckServiceAffinity",
+                                         "argument": {"serviceAffinity": {"labels": ["tier", "disk"]}}}],
+                         "priorities": [{"name": "BalancedResourceAllocation", "weight": 1},
+                                        {"name": "NodeAffinityPriority", "weight": 2}]},
     "label_priorities": {"predicates": [{"name": "GeneralPredicates"}, {"name": "PodToleratesNodeTaints"}],
                          "priorities": [{"name": "LeastRequestedPriority", "weight": 1},
                                         {"name": "PreferSsd", "weight": 3,
@@ -141,7 +146,9 @@ def test_gpu_policy_run_matches_oracle(name, mode):
     from workloads import rnd_workload
     pol = policy.decode(GPU_POLICIES[name])
     preds, prios, lp = policy.key_sets(pol)
-    custom = {"CheckNodeLabelPresence": R.new_node_label_predicate(*lp)} if lp else None
+    custom = {"CheckNodeLabelPresence": R.new_node_label_predicate(*lp)} if lp else {}
+    if policy.service_affinity_labels(pol) is not None:
+        custom["CheckServiceAffinity"] = R.new_service_affinity_predicate(policy.service_affinity_labels(pol))
     cprios = {n: (R.node_label_priority(a[1], a[2]) if a[0] == "labelPreference" else R.service_anti_affinity_priority(a[1]))
               for n, a in policy.priority_arguments(pol).items()}
     for seed in (3, 11):
@@ -156,3 +163,29 @@ def test_gpu_policy_run_matches_oracle(name, mode):
         assert rep.last_node_index == lni
         if lp and not lp[1]:
             assert any("didn't have the requested labels" in (m or "") for _, _, m in want)
+
+
+def test_service_affinity_table_matches_oracle():
+    """CheckServiceAffinity without services: the per (pod class, label set) table against the
+    oracle's checkServiceAffinity on every node."""
+    import ksim_ref as R
+    from ksim import ingest
+    from workloads import rnd_workload
+    nodes, running, pods = rnd_workload(5, n_nodes=20, n_pods=60)
+    for p in pods[::3]:
+        p["spec"]["nodeSelector"] = {"tier": "a", "disk": "ssd"}
+    cl = ingest.Cluster.from_objects(nodes, running, pods)
+    ok, need = scheduler.service_affinity_table(cl.classes.items, cl.label_sets.items, ["disk", "region"])
+    pred = R.new_service_affinity_predicate(["disk", "region"])
+    infos = [R.NodeInfo(x) for x in sorted(nodes, key=lambda x: x["metadata"]["name"].encode())]
+    assert need.any()
+    for k, p in enumerate(pods):
+        c = int(cl.pods["cls"][k])
+        for i, ni in enumerate(infos):
+            s = int(cl.cols["label_set"][i])
+            assert bool((int(ok[c, s >> 5]) >> (s & 31)) & 1) == pred(p, ni)[0]
+    pol = policy.decode({"predicates": [{"name": "CheckServiceAffinity", "argument": {"serviceAffinity": {"labels": ["disk"]}}},
+                                        {"name": "PodFitsResources"}]})
+    preds, _, _ = policy.key_sets(pol)
+    assert "CheckServiceAffinity" in preds and policy.service_affinity_labels(pol) == ["disk"]
+    assert scheduler.make_config(preds, []).predicates & abi.P_SERVICE_AFFINITY
