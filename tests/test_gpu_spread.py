@@ -51,3 +51,27 @@ def test_spread_simulation_matches_oracle(seed, policy):
     for name, host, msg in want:
         assert got[name] == (host, msg), name
     assert rep.last_node_index == want_lni
+
+
+def test_schedule_one_with_spread_matches_batch():
+    """ksim_schedule_one (+ assume) pod by pod == ksim_schedule: pass A and the zone sums run for
+    the single-pod launch as well (the accumulators are zeroed by each pass)."""
+    import ctypes as C
+    nodes, running, pods, objs = rnd_spread_workload(1, n_pods=50)
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order, spread=spread.SpreadListers(**objs))
+    preds, prios = POLICIES["default"]
+    batch = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH)
+    one = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH)
+    try:
+        out, reasons, _ = batch.schedule()
+        for k in range(len(order)):
+            pod = abi.Pod.from_buffer_copy(cl.pods[k].tobytes())
+            res = abi.Result()
+            one.h.call("ksim_schedule_one", C.byref(pod), abi.vptr(cl.pod_ports), len(cl.pod_ports),
+                       abi.vptr(cl.pod_scalars), len(cl.pod_scalars), abi.SCHEDULE_ASSUME, C.byref(res))
+            assert res.node == out[k], k
+        assert one.last_node_index == batch.last_node_index
+    finally:
+        batch.close()
+        one.close()

@@ -136,3 +136,31 @@ def test_volume_release_restores_state():
              abi.vptr(cl.pod_scalars), len(cl.pod_scalars))
     assert _device_mounts(g, cl.n_nodes) == before
     g.close()
+
+
+def test_schedule_one_with_volumes_matches_batch():
+    """ksim_schedule_one (+ assume) pod by pod == ksim_schedule on another handle: the per-pod
+    entry point evaluates and commits volume pods through the same tables."""
+    import ctypes as C
+    nodes, running, pods, pvs, pvcs = rnd_volume_workload(5, n_pods=60)
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order, pvs=pvs, pvcs=pvcs, max_vols=(3, 3, 3))
+    preds, prios = POLICIES["volumes_lr_bra"]
+    batch = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH)
+    one = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH)
+    try:
+        out, reasons, _ = batch.schedule()
+        assert (out < 0).any() and (out >= 0).any()
+        for k in range(len(order)):
+            pod = abi.Pod.from_buffer_copy(cl.pods[k].tobytes())
+            res = abi.Result()
+            one.h.call("ksim_schedule_one", C.byref(pod), abi.vptr(cl.pod_ports), len(cl.pod_ports),
+                       abi.vptr(cl.pod_scalars), len(cl.pod_scalars), abi.SCHEDULE_ASSUME, C.byref(res))
+            assert res.node == out[k], k
+            if res.node < 0:
+                assert list(res.reasons) == list(reasons[k]), k
+        assert one.last_node_index == batch.last_node_index
+        assert _device_mounts(one, cl.n_nodes) == _device_mounts(batch, cl.n_nodes)
+    finally:
+        batch.close()
+        one.close()
