@@ -58,7 +58,11 @@ class SchedulerCache:
     """schedulercache.Cache + genericScheduler of one device.  `predicates` / `priorities` are
     key sets and weights as a provider or Policy lists them (scheduler.provider / policy)."""
 
-    def __init__(self, predicates, priorities, device=0, mode=abi.MODE_AUTO, last_node_index=0, port_slots=4):
+    def __init__(self, predicates, priorities, device=0, mode=abi.MODE_AUTO, last_node_index=0, port_slots=4,
+                 pvs=(), pvcs=(), storage_classes=()):
+        """pvs / pvcs / storage_classes: what the PV / PVC / StorageClass listers hold (the volume
+        predicates resolve PVCs through them)."""
+        from .volumes import VolumeIndex
         self.predicates = list(predicates)
         self.prioritizers = list(priorities)
         self.cfg = scheduler.make_config(predicates, priorities, device, mode, True, last_node_index)
@@ -70,6 +74,10 @@ class SchedulerCache:
         cl.label_sets.get(_canon({}), {})
         cl.taint_sets.get(_canon([]), [])
         cl.classes.get(ingest.pod_class_key({}), {})
+        cl.volume_index = VolumeIndex(pvs, pvcs, storage_classes)
+        self._vol_on = bool(self.cfg.predicates & scheduler.VOLUME_PREDICATE_BITS)
+        self._vol_key = None     # what the loaded volume tables were built for (None: not loaded)
+        self._vol_dirty = False  # a node event since: the library refuses calls until a reload
         self.names = []          # listed node names, ascending bytewise (= name rank)
         self._keys = []          # the same as bytes
         self._rank = None        # name -> rank (rebuilt lazily after node events)
@@ -130,6 +138,52 @@ class SchedulerCache:
         row, p, s = enc
         return (abi.vptr(row), abi.vptr(p) if len(p) else None, len(p), abi.vptr(s) if len(s) else None, len(s))
 
+    # ------------------------------------------------------------------ volume tables
+    def _mounts(self):
+        """Per listed node (name-rank order) the mounts of its cached pods: {key: [rw, ro, pvc]}."""
+        idx = self.cl.volume_index
+        out = []
+        for name in self.names:
+            m = {}
+            info = self.infos.get(name)
+            for _, enc in (info.pods.values() if info else ()):
+                vc = int(enc[0][0]["vol_class"])
+                if vc:
+                    for k, j in idx.mounts_of(vc):
+                        m.setdefault(k, [0, 0, 0])[j] += 1
+            out.append(m)
+        return out
+
+    def _sync_volumes(self, need):
+        """(Re)load the volume tables from the host's view of the cache when a volume pod needs
+        them and they are missing or out of date (new keys / classes / label sets), and after
+        every node event once loaded (the library marks them stale)."""
+        if not self._vol_on:
+            return
+        idx = self.cl.volume_index
+        key = (len(idx.key_filter), len(idx.class_refs), len(self.cl.label_sets.items))
+        if not self._vol_dirty and (self._vol_key == key or (self._vol_key is None and not need)):
+            return
+        from .volumes import build_tables, tables_struct
+        n = len(self.names)
+        self.vol_tables = build_tables(idx, n, self._mounts(), range(1, len(idx.class_refs) + 1),
+                                       self.cl.label_sets.items)
+        self.h.call("ksim_load_volumes", C.byref(tables_struct(self.vol_tables, "NoVolumeZoneConflict" in self.predicates)))
+        self._vol_key = key
+        self._vol_dirty = False
+
+    def _check_volume_errors(self, pod):
+        """The scheduler refuses a pod on which a configured volume predicate errs (ksim/volumes.py)."""
+        errs = self.cl.volume_index.pod_errors(pod, self.cl.label_sets.items)
+        keys = set(self.predicates)
+        maxpd = keys & {"MaxEBSVolumeCount", "MaxGCEPDVolumeCount", "MaxAzureDiskVolumeCount"}
+        if "claim_name" in errs and (maxpd or "NoVolumeZoneConflict" in keys):
+            raise Unsupported("a PersistentVolumeClaim volume without a claim name (the volume predicates err)")
+        if "binding" in errs and "CheckVolumeBinding" in keys:
+            raise Unsupported("CheckVolumeBinding with a PVC that is not bound to a PV without node affinity")
+        if "zone" in errs and "NoVolumeZoneConflict" in keys:
+            raise Unsupported("NoVolumeZoneConflict with a PVC the listers cannot resolve on a zone-labelled cluster")
+
     # ------------------------------------------------------------------ node rows
     def _node_row(self, name, info, ns):
         cl = self.cl
@@ -189,6 +243,7 @@ class SchedulerCache:
             self.names.insert(rank, name)
             self._rank = None
         info.node, info.mem, info.disk = node, ns.mem_pressure, ns.disk_pressure
+        self._vol_dirty = self._vol_key is not None
 
     def update_node(self, old, new):
         """cache.UpdateNode (cache.go:366-375) → SetNode on the (possibly new) NodeInfo."""
@@ -209,12 +264,14 @@ class SchedulerCache:
         info.node, info.mem, info.disk = None, "Unknown", "Unknown"
         if not info.pods:
             del self.infos[name]
+        self._vol_dirty = self._vol_key is not None
 
     # ------------------------------------------------------------------ pods
     def _add(self, pod, enc=None):                          # cache.go:200-207
         name = _spec(pod).get("nodeName", "")
         enc = enc if enc is not None else self._encode(pod)
         if name in self._ranks():
+            self._sync_volumes(bool(enc[0][0]["vol_class"]))
             self.h.call("ksim_pod_add", self._ranks()[name], *self._pod_args(enc))
         self._info(name).pods[pod_key(pod)] = (pod, enc)
 
@@ -224,9 +281,11 @@ class SchedulerCache:
         key = pod_key(pod)
         if info is None or key not in info.pods:
             raise KeyError("no corresponding pod %s in pods of node %s" % (_meta(pod).get("name"), name))
-        _, enc = info.pods.pop(key)
+        _, enc = info.pods[key]
         if name in self._ranks():
+            self._sync_volumes(bool(enc[0][0]["vol_class"]))
             self.h.call("ksim_pod_remove", self._ranks()[name], *self._pod_args(enc))
+        info.pods.pop(key)
         if not info.pods and info.node is None:
             del self.infos[name]
 
@@ -280,6 +339,9 @@ class SchedulerCache:
         FitError / abi.NoNodesAvailable.  assume=True also runs Scheduler.assume
         (scheduler.go:366): the pod enters the cache on that host, as an assumed pod."""
         enc = self._encode(pod)
+        if enc[0][0]["vol_class"]:
+            self._check_volume_errors(pod)
+        self._sync_volumes(bool(enc[0][0]["vol_class"]))
         res = abi.Result()
         self.h.call("ksim_schedule_one", *self._pod_args(enc), abi.SCHEDULE_ASSUME if assume else abi.SCHEDULE_ONLY,
                     C.byref(res))

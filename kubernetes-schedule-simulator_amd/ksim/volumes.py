@@ -185,6 +185,33 @@ class VolumeIndex:
         if pv is None or (pv.get("spec") or {}).get("nodeAffinity") is not None:
             self.errors.add("binding")
 
+    def pod_errors(self, pod, label_sets):
+        """The error paths one pod to be scheduled would take (module doc), without interning:
+        "claim_name", "binding", "zone" (an unresolvable PVC while some label set is zoned)."""
+        errs = set()
+        ns = _ns(pod)
+        zoned = any(k in dict(ls) for ls in label_sets for k in (ZONE_LABEL, REGION_LABEL))
+        for vol in (pod.get("spec") or {}).get("volumes") or []:
+            claim = vol.get("persistentVolumeClaim")
+            if claim is None:
+                continue
+            name = claim.get("claimName", "")
+            if name == "":
+                errs.add("claim_name")
+                continue
+            if zoned and self._zone_entry(ns, name) == "error":
+                errs.add("zone")
+            pvc = self.pvcs.get((ns, name))
+            pv = self.pvs.get(((pvc or {}).get("spec") or {}).get("volumeName", "")) if pvc is not None else None
+            if pv is None or (pv.get("spec") or {}).get("nodeAffinity") is not None:
+                errs.add("binding")
+        return errs
+
+    def mounts_of(self, vclass):
+        """(key, slot field) of every ref of a volume class: 0 read-write, 1 read-only, 2 via PVC."""
+        return [(k, 2 if f & abi.VOL_VIA_PVC else 1 if f & abi.VOL_READ_ONLY else 0)
+                for k, f in self.class_refs[vclass - 1]]
+
     def vclass(self, pod):
         """1 + the pod's volume class, 0 when no volume matters to the predicates."""
         refs, zone, has_pvc = self.refs(pod)

@@ -89,3 +89,45 @@ def test_schedule_only_leaves_cache_unchanged():
         assert list(dut.node_state()["req_cpu"]) == [0, 0, 1000]
     finally:
         dut.close()
+
+
+def _volume_stream(seed, ref, n_events, n_nodes, claims):
+    """event_stream with volumes on the scheduled and bound pods (namespace "ns")."""
+    import random
+    from events import event_stream
+    from workloads import rnd_volume
+    rng = random.Random(7000 + seed)
+    for kind, x in event_stream(seed, ref, n_events, n_nodes, features=False):
+        if kind in ("schedule", "add_pod") and "uid" not in x["metadata"] and x["metadata"].get("namespace") != "ns":
+            x["metadata"]["namespace"] = "ns"
+            if rng.random() < 0.6:
+                x["spec"]["volumes"] = [rnd_volume(rng, claims) for _ in range(rng.randint(1, 3))]
+        yield kind, x
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_event_stream_with_volumes(seed, monkeypatch):
+    """Volume pods through the per-pod mirror: its volume tables are rebuilt from the cache's pods
+    after node events and when new keys appear, and every decision matches the oracle's."""
+    from workloads import volume_listers
+    monkeypatch.setenv("KUBE_MAX_PD_VOLS", "3")
+    pvs, pvcs, claims = volume_listers()
+    preds = ["GeneralPredicates", "CheckNodeCondition", "NoDiskConflict", "MaxEBSVolumeCount",
+             "MaxGCEPDVolumeCount", "MaxAzureDiskVolumeCount"]
+    prios = [("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
+    custom = {k: v for k, v in R.volume_predicates(R.VolumeListers(pvs, pvcs), 3).items() if k in preds}
+    ref = R.SchedulerCache(set(preds), prios, custom)
+    dut = SchedulerCache(preds, prios, device=0, pvs=pvs, pvcs=pvcs)
+    decisions = fails = 0
+    try:
+        for ev in _volume_stream(seed, ref, 300, 10, claims):
+            want = apply(ref, ev)
+            got = apply(dut, ev)
+            if ev[0] == "schedule":
+                decisions += 1
+                fails += want[0] is None
+                assert got == want, (ev[1]["metadata"]["name"], want, got)
+        assert dut.last_node_index == ref.sched.last_node_index
+    finally:
+        dut.close()
+    assert decisions > 100
