@@ -60,7 +60,8 @@ def parse():
     ap.add_argument("--mode", default="auto", choices=["auto", "launch", "persistent", "tree"])
     ap.add_argument("--no-tree", dest="tree", action="store_false",
                     help="skip the tree-mode line measured beside the scan (c3/c4)")
-    ap.add_argument("--cpu-sample", type=int, default=3000, help="pods in the 16-thread CPU-baseline prefix (0 = skip)")
+    ap.add_argument("--cpu-sample", type=int, default=30000,
+                    help="most pods in a CPU-baseline prefix (0 = skip); each leg is sized to ~10 s of CPU work")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"],
                     help="c3: the headline metric (default); c2: 5k heterogeneous nodes with selectors, "
@@ -268,7 +269,9 @@ def cpu_baseline(a, cl, preds, prios, placements, unit="pods/s"):
     cfg = scheduler.make_config(preds, prios)
     avail = len(os.sched_getaffinity(0))
     legs = []
-    for t, budget in ((1, 3e7), (min(a.cpu_threads, avail), 3e8), (min(avail, 64), 3e8)):
+    # node-eval budgets: ~10 s per leg at the measured C3 rates (1 thread ~0.09e9, 16 threads
+    # ~0.28e9 node-evals/s); the all-cores leg oversubscribes the box's CPU share, so it gets less
+    for t, budget in ((1, 9e8), (min(a.cpu_threads, avail), 2.8e9), (min(avail, 64), 3e8)):
         if any(t == x[0] for x in legs):
             continue
         S = int(min(a.cpu_sample, len(placements), max(20, budget // n)))
