@@ -698,3 +698,27 @@ def test_single_node_fit_error_message():
     pods = [{"metadata": {"name": "big"}, "spec": {"containers": [{"resources": {"requests": {"cpu": "2", "memory": "2Gi"}}}]}}]
     rep = scheduler.ClusterCapacity(nodes, [], pods).run()
     assert rep.failed == [("big", "0/1 nodes are available: 1 Insufficient cpu, 1 Insufficient memory.")]
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_mixed_features_at_scale(seed, monkeypatch):
+    """Every launch-kernel feature in one run — volumes (all kinds, PVCs through the listers, zones),
+    SelectorSpread over services / RCs / RSs / StatefulSets, selectors, taints, host ports, extended
+    resources, node conditions — 160 nodes × 1,500 pods against the object oracle."""
+    from ksim import spread
+    from workloads import rnd_mixed_workload
+    monkeypatch.setenv("KUBE_MAX_PD_VOLS", "4")
+    nodes, running, pods, pvs, pvcs, objs = rnd_mixed_workload(seed, n_nodes=160, n_pods=1500)
+    preds = [k for k in scheduler.DEFAULT_PREDICATES if k != "MatchInterPodAffinity"]
+    prios = [(n, w) for n, w in scheduler.DEFAULT_PRIORITIES if n != "InterPodAffinityPriority"]
+    custom = {k: v for k, v in R.volume_predicates(R.VolumeListers(pvs, pvcs), 4).items() if k in preds}
+    want, want_lni = R.simulate(nodes, running, pods, set(preds), list(prios), custom, spread=R.SpreadListers(**objs))
+    cc = scheduler.ClusterCapacity(nodes, running, pods, predicates=preds, priorities=prios, pvs=pvs, pvcs=pvcs,
+                                   spread=spread.SpreadListers(**objs))
+    rep = cc.run()
+    got = {n: (h, None) for n, h in rep.successful}
+    got.update({n: (None, m) for n, m in rep.failed})
+    assert [n for n, _ in rep.successful] == [n for n, h, _ in want if h is not None]
+    for name, host, msg in want:
+        assert got[name] == (host, msg), name
+    assert rep.last_node_index == want_lni

@@ -330,3 +330,30 @@ def rnd_spread_workload(seed, n_nodes=18, n_pods=120, n_running=16, zones=True):
         {"key": "app", "operator": "In", "values": ["a", "c"]}]}}}]
     sss = [{"metadata": md("ns1"), "spec": {"selector": {"matchLabels": {"app": "c"}}}}]
     return nodes, running, pods, dict(services=services, rcs=rcs, rss=rss, sss=sss)
+
+
+def rnd_mixed_workload(seed, n_nodes=120, n_pods=900):
+    """Every feature at once: volumes (all kinds, PVCs through the listers), spread selectors,
+    zones, labels, taints, selectors, host ports — the launch kernels' full predicate chain."""
+    rng = random.Random(3000 + seed)
+    nodes = rnd_nodes(rng, n_nodes, features=True)
+    for x in nodes:
+        x["status"]["allocatable"]["pods"] = "110"
+        if rng.random() < 0.8:
+            x["metadata"]["labels"]["failure-domain.beta.kubernetes.io/zone"] = rng.choice(["z1", "z2", "z3", "z4"])
+    pvs, pvcs, claims = volume_listers(resolvable_only=True)
+    _, _, _, objs = rnd_spread_workload(seed, n_nodes=1, n_pods=0, n_running=0)
+
+    def pod(name, nn=None):
+        p = rnd_pod(rng, name, features=True)
+        p["metadata"]["namespace"] = rng.choice(["ns", "ns1", "ns2"])
+        p["metadata"]["labels"] = {"app": rng.choice("abc"), "tier": rng.choice("xy")}
+        if rng.random() < 0.5:
+            p["spec"]["volumes"] = [rnd_volume(rng, claims) for _ in range(rng.randint(1, 2))]
+            p["metadata"]["namespace"] = "ns"   # where the listers' PVCs live
+        if nn:
+            p["spec"]["nodeName"] = nn
+        return p
+    running = [pod("run-%d" % k, rng.choice(nodes)["metadata"]["name"]) for k in range(n_nodes // 3)]
+    pods = [pod("pod-%d" % k) for k in range(n_pods)]
+    return nodes, running, pods, pvs, pvcs, objs
