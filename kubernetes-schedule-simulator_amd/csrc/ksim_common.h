@@ -155,6 +155,20 @@ struct KsimShard {
   uint64_t start_ticks;
 };
 
+// The persistent kernels spin on each other's progress, so every workgroup of the grid must be
+// resident at once: check the occupancy of this kernel at this block size and dynamic LDS on the
+// current device before launching.  hipErrorCooperativeLaunchTooLarge when the grid cannot be
+// co-resident (the runtime then takes the launch form, or fails in KSIM_MODE_PERSISTENT).
+template <class K>
+static hipError_t ksim_check_coresident(K kernel, int grid, int block, size_t lds) {
+  int dev = 0, cus = 0, per_cu = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e == hipSuccess) e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, block, lds);
+  if (e != hipSuccess) return e;
+  return (int64_t)per_cu * cus >= grid ? hipSuccess : hipErrorCooperativeLaunchTooLarge;
+}
+
 // ((a*10)/b) with Go int64 semantics (wrapping multiply, truncating divide), b > 0.
 // Quotients here are 0..10, so for a < 2^49 a correctly rounded double divide plus one
 // integer correction is exact; larger values take the native (slow) 64-bit divide.

@@ -1417,6 +1417,8 @@ static hipError_t launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint6
       off += sb;
     }
   }
+  hipError_t e = ksim_check_coresident(ksim_persistent_kernel<BS, NPT, MB>, grid, BS, off);
+  if (e != hipSuccess) return e;
   hipLaunchKernelGGL((ksim_persistent_kernel<BS, NPT, MB>), dim3(grid), dim3(BS), off, s, *c, cdev, granules, L);
   return hipGetLastError();
 }

@@ -961,17 +961,25 @@ extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, in
   a.wl = (int32_t)c->w[KSIM_W_LEAST_REQUESTED]; a.wm = (int32_t)c->w[KSIM_W_MOST_REQUESTED];
   a.wb = (int32_t)c->w[KSIM_W_BALANCED];
   a.mirror = mirror;
+  // every workgroup resident at once (the kernel spins on its peers), then the launch
+#define KSIM_PF(R, S, L)                                                             \
+  do {                                                                               \
+    hipError_t e_ = ksim_check_coresident(ksim_pfast_kernel<R, S>, grid, BS, L);     \
+    if (e_ != hipSuccess) return e_;                                                 \
+    hipLaunchKernelGGL((ksim_pfast_kernel<R, S>), dim3(grid), dim3(BS), L, s, a);    \
+  } while (0)
   if (mirror) {  // streaming form (image prepared by ksim_pstream_prepare on the same stream)
     const size_t lds = (size_t)lds_rows * LDS_ROW_BYTES_STREAM;
-    if (lds_rows <= RT) hipLaunchKernelGGL((ksim_pfast_kernel<1, true>), dim3(grid), dim3(BS), lds, s, a);
-    else if (lds_rows <= 2 * RT) hipLaunchKernelGGL((ksim_pfast_kernel<2, true>), dim3(grid), dim3(BS), lds, s, a);
-    else if (lds_rows <= 4 * RT) hipLaunchKernelGGL((ksim_pfast_kernel<4, true>), dim3(grid), dim3(BS), lds, s, a);
-    else hipLaunchKernelGGL((ksim_pfast_kernel<9, true>), dim3(grid), dim3(BS), lds, s, a);
+    if (lds_rows <= RT) KSIM_PF(1, true, lds);
+    else if (lds_rows <= 2 * RT) KSIM_PF(2, true, lds);
+    else if (lds_rows <= 4 * RT) KSIM_PF(4, true, lds);
+    else KSIM_PF(9, true, lds);
     return hipGetLastError();
   }
   const size_t lds = (size_t)lds_rows * LDS_ROW_BYTES;
-  if (lds_rows <= RT) hipLaunchKernelGGL((ksim_pfast_kernel<1, false>), dim3(grid), dim3(BS), lds, s, a);
-  else if (lds_rows <= 2 * RT) hipLaunchKernelGGL((ksim_pfast_kernel<2, false>), dim3(grid), dim3(BS), lds, s, a);
-  else hipLaunchKernelGGL((ksim_pfast_kernel<4, false>), dim3(grid), dim3(BS), lds, s, a);
+  if (lds_rows <= RT) KSIM_PF(1, false, lds);
+  else if (lds_rows <= 2 * RT) KSIM_PF(2, false, lds);
+  else KSIM_PF(4, false, lds);
+#undef KSIM_PF
   return hipGetLastError();
 }

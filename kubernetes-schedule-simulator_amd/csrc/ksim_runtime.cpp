@@ -538,6 +538,8 @@ static int pfast_form(ksim_handle* h, int64_t first, int64_t count, int* grid, i
   return 0;
 }
 
+static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st);
+
 // All pods of [first, first+count) resource-only: the specialised kernel (ksim_pfast.hip).
 static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid, int lds_rows, bool stream,
                           ksim_stats* st) {
@@ -562,6 +564,14 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
   HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
   hipError_t e = ksim_launch_pfast(&c, h->granules, grid, lds_rows, stream ? h->mirror : nullptr, &h->shard, h->stream);
+  if (e == hipErrorCooperativeLaunchTooLarge) {
+    // the grid cannot be co-resident here (a smaller or shared device): the general kernels instead
+    if (h->cfg.mode != KSIM_MODE_PERSISTENT && h->shard.world == 1) {
+      h->pfast_off = true;
+      return run_persistent_mode(h, first, count, st);
+    }
+    return ksim_fail(h, KSIM_E_UNSUPPORTED, "persistent launch: %d workgroups cannot be co-resident on this device", grid);
+  }
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   HIPCHK(h, hipEventSynchronize(h->ev1));
@@ -645,6 +655,11 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
   HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
   hipError_t e = ksim_launch_persistent(&c, h->ctx_dev, h->granules, grid, lds_rows, h->stream);
+  if (e == hipErrorCooperativeLaunchTooLarge) {
+    // the grid cannot be co-resident here (a smaller or shared device): the launch form instead
+    if (h->cfg.mode != KSIM_MODE_PERSISTENT && h->shard.world == 1) return run_launch_mode(h, first, count, st);
+    return ksim_fail(h, KSIM_E_UNSUPPORTED, "persistent launch: %d workgroups cannot be co-resident on this device", grid);
+  }
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
   HIPCHK(h, hipEventSynchronize(h->ev1));
