@@ -59,13 +59,25 @@ class SchedulerCache:
     key sets and weights as a provider or Policy lists them (scheduler.provider / policy)."""
 
     def __init__(self, predicates, priorities, device=0, mode=abi.MODE_AUTO, last_node_index=0, port_slots=4,
-                 pvs=(), pvcs=(), storage_classes=()):
+                 pvs=(), pvcs=(), storage_classes=(), hard_weight=10, spread=None):
         """pvs / pvcs / storage_classes: what the PV / PVC / StorageClass listers hold (the volume
-        predicates resolve PVCs through them)."""
+        predicates resolve PVCs through them); hard_weight: hardPodAffinitySymmetricWeight; spread:
+        ksim.spread.SpreadListers for SelectorSpread (None: the simulator's empty listers)."""
         from .volumes import VolumeIndex
         self.predicates = list(predicates)
         self.prioritizers = list(priorities)
-        self.cfg = scheduler.make_config(predicates, priorities, device, mode, True, last_node_index)
+        self.spread = spread if spread else None
+        self.cfg = scheduler.make_config(predicates, priorities, device, mode, True, last_node_index,
+                                         spread=self.spread is not None)
+        self.hard_weight = int(hard_weight)
+        names = {n for n, _ in priorities}
+        self._spread_services_only = "ServiceSpreadingPriority" in names and "SelectorSpreadPriority" not in names
+        # inter-pod affinity / SelectorSpread tables are needed once any cached or scheduled pod has
+        # terms or spread selectors; then every call reloads them over the cached pods
+        self._aff_on = False
+        self._aff_wanted = bool(self.cfg.predicates & abi.P_INTERPOD_AFFINITY or
+                                ((self.cfg.weights[abi.W_INTERPOD] or self.cfg.weights[abi.W_SPREAD])
+                                 and not self.cfg.no_priorities))
         self._need_na = any(n == "NodeAffinityPriority" for n, _ in self.prioritizers)
         self.h = abi.Handle(self.cfg)
         cl = self.cl = ingest.Cluster()
@@ -75,6 +87,7 @@ class SchedulerCache:
         cl.taint_sets.get(_canon([]), [])
         cl.classes.get(ingest.pod_class_key({}), {})
         cl.volume_index = VolumeIndex(pvs, pvcs, storage_classes)
+        cl._affinity_ok = True   # affinity pods: their tables are built here per call (_sync_affinity)
         self._vol_on = bool(self.cfg.predicates & scheduler.VOLUME_PREDICATE_BITS)
         self._vol_key = None     # what the loaded volume tables were built for (None: not loaded)
         self._vol_dirty = False  # a node event since: the library refuses calls until a reload
@@ -171,6 +184,46 @@ class SchedulerCache:
         self.h.call("ksim_load_volumes", C.byref(tables_struct(self.vol_tables, "NoVolumeZoneConflict" in self.predicates)))
         self._vol_key = key
         self._vol_dirty = False
+
+    def _spread_sels(self, pod):
+        return self.spread.selectors(pod, self._spread_services_only) if self.spread is not None else []
+
+    def _sync_affinity(self, enc, pod, extra):
+        """Inter-pod affinity and SelectorSpread through the affinity tables (ksim/affinity.py),
+        rebuilt over the pods this cache holds on listed nodes plus `pod` when `extra` (a pod not
+        cached yet), loaded, and the descriptor's identity / class set from them.  The tables are
+        needed once any pod has terms or spread selectors; before that identities change nothing."""
+        from .affinity import AffinityIndex, has_pod_affinity, tables_struct
+        if not self._aff_wanted:
+            return
+        sels = self._spread_sels(pod)
+        if not self._aff_on:
+            if not has_pod_affinity(pod) and not sels:
+                return
+            self._aff_on = True
+        ranks = self._ranks()
+        cached = []
+        for name, info in self.infos.items():
+            for p, _ in info.pods.values():
+                if name in ranks:
+                    cached.append((ranks[name], p))
+                elif has_pod_affinity(p):
+                    # the reference's metadata then errors on the node-less NodeInfo (metadata.go:106-109)
+                    raise Unsupported("a pod with inter-pod affinity terms cached on a node that is not listed")
+        idx = AffinityIndex([_meta(self.infos[n].node).get("labels") for n in self.names], self.hard_weight)
+        allp = [p for _, p in cached]
+        if extra:
+            allp.append(pod)
+            me = len(allp) - 1
+        else:
+            me = next(i for i, p in enumerate(allp) if pod_key(p) == pod_key(pod))
+        idents = [idx.ident(p) for p in allp]
+        aclasses = [idx.aclass(p, sels if i == me else ()) for i, p in enumerate(allp)]
+        tables, remap = idx.build([w for w, _ in cached], idents, aclasses)
+        self._aff_tables = tables
+        self.h.call("ksim_load_affinity", C.byref(tables_struct(tables)))
+        enc[0][0]["aff_ident"] = remap[idents[me]]
+        enc[0][0]["aff_class"] = aclasses[me] + 1
 
     def _check_volume_errors(self, pod):
         """The scheduler refuses a pod on which a configured volume predicate errs (ksim/volumes.py)."""
@@ -272,6 +325,7 @@ class SchedulerCache:
         enc = enc if enc is not None else self._encode(pod)
         if name in self._ranks():
             self._sync_volumes(bool(enc[0][0]["vol_class"]))
+            self._sync_affinity(enc, pod, True)
             self.h.call("ksim_pod_add", self._ranks()[name], *self._pod_args(enc))
         self._info(name).pods[pod_key(pod)] = (pod, enc)
 
@@ -281,9 +335,10 @@ class SchedulerCache:
         key = pod_key(pod)
         if info is None or key not in info.pods:
             raise KeyError("no corresponding pod %s in pods of node %s" % (_meta(pod).get("name"), name))
-        _, enc = info.pods[key]
+        cur, enc = info.pods[key]
         if name in self._ranks():
             self._sync_volumes(bool(enc[0][0]["vol_class"]))
+            self._sync_affinity(enc, cur, False)
             self.h.call("ksim_pod_remove", self._ranks()[name], *self._pod_args(enc))
         info.pods.pop(key)
         if not info.pods and info.node is None:
@@ -342,6 +397,7 @@ class SchedulerCache:
         if enc[0][0]["vol_class"]:
             self._check_volume_errors(pod)
         self._sync_volumes(bool(enc[0][0]["vol_class"]))
+        self._sync_affinity(enc, pod, True)
         res = abi.Result()
         self.h.call("ksim_schedule_one", *self._pod_args(enc), abi.SCHEDULE_ASSUME if assume else abi.SCHEDULE_ONLY,
                     C.byref(res))

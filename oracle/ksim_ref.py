@@ -1796,12 +1796,12 @@ class GenericScheduler:
 # scheduleOne loop's Schedule + assume (S/scheduler.go:188-204, 366-397)
 # --------------------------------------------------------------------------
 class SchedulerCache:
-    def __init__(self, predicate_keys, priority_configs, custom_predicates=None):
+    def __init__(self, predicate_keys, priority_configs, custom_predicates=None, spread=None):
         self.nodes = {}          # name -> NodeInfo (cache.nodes)
         self.listed = []         # names the node lister returns (added, not removed)
         self.pod_states = {}     # key -> pod
         self.assumed = set()
-        self.sched = GenericScheduler(predicate_keys, priority_configs, custom_predicates)
+        self.sched = GenericScheduler(predicate_keys, priority_configs, custom_predicates, spread=spread)
 
     def _info(self, name):
         n = self.nodes.get(name)

@@ -131,3 +131,62 @@ def test_event_stream_with_volumes(seed, monkeypatch):
     finally:
         dut.close()
     assert decisions > 100
+
+
+def _affinity_stream(seed, ref, n_events, n_nodes):
+    """scheduleOne calls of pods with inter-pod (anti-)affinity terms and spread labels, pods bound
+    elsewhere on listed nodes, confirmations, removals and node updates (no node removal: the
+    reference errs on affinity pods cached under a node-less NodeInfo)."""
+    import copy
+    import random
+    from workloads import rnd_affinity_nodes, rnd_affinity_pod
+    rng = random.Random(9000 + seed)
+    for node in rnd_affinity_nodes(rng, n_nodes):
+        yield "add_node", node
+    for k in range(n_events):
+        names = list(ref.listed)
+        added = sorted(key for key in ref.pod_states if key not in ref.assumed)
+        assumed = sorted(ref.assumed)
+        r = rng.random()
+        if r < 0.6:
+            yield "schedule", rnd_affinity_pod(rng, "p-%d" % k, p_aff=0.5)
+        elif r < 0.7:
+            p = rnd_affinity_pod(rng, "bound-%d" % k, p_aff=0.3)
+            p["spec"]["nodeName"] = rng.choice(names)
+            yield "add_pod", p
+        elif r < 0.8 and assumed:
+            yield "add_pod", copy.deepcopy(ref.pod_states[rng.choice(assumed)])
+        elif r < 0.9 and added:
+            yield "remove_pod", copy.deepcopy(ref.pod_states[rng.choice(added)])
+        else:
+            name = rng.choice(names)
+            old = ref.nodes[name].node
+            new = copy.deepcopy(old)
+            lab = new["metadata"].get("labels") or {}
+            lab["zone"] = "z%d" % rng.randint(0, 3)
+            new["metadata"]["labels"] = lab
+            yield "update_node", (old, new)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_event_stream_with_affinity_and_spread(seed):
+    """Inter-pod affinity and SelectorSpread pods through the per-pod mirror: the affinity tables
+    are rebuilt over the cached pods for every call; every decision matches the oracle's cache."""
+    from ksim.spread import SpreadListers
+    svc = [{"metadata": {"namespace": ns}, "spec": {"selector": {"app": a}}} for ns, a in (("", "web"), ("ns1", "db"))]
+    rss = [{"metadata": {"namespace": ""}, "spec": {"selector": {"matchLabels": {"tier": "fe"}}}}]
+    preds, prios = POLICIES["default"]
+    ref = R.SchedulerCache(set(preds), prios, spread=R.SpreadListers(services=svc, rss=rss))
+    dut = SchedulerCache(preds, prios, device=0, spread=SpreadListers(services=svc, rss=rss))
+    decisions = 0
+    try:
+        for ev in _affinity_stream(seed, ref, 200, 12):
+            want = apply(ref, ev)
+            got = apply(dut, ev)
+            if ev[0] == "schedule":
+                decisions += 1
+                assert got == want, (ev[1]["metadata"]["name"], want, got)
+        assert dut.last_node_index == ref.sched.last_node_index
+    finally:
+        dut.close()
+    assert decisions > 80
