@@ -63,7 +63,7 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=30000,
                     help="most pods in a CPU-baseline prefix (0 = skip); each leg is sized to ~10 s of CPU work")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c4", "c5"],
+    ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c2x", "c4", "c5"],
                     help="c3: the headline metric (default); c2: 5k heterogeneous nodes with selectors, "
                          "ports and taints; c4: 1M nodes; c5: the 4,096-scenario policy sweep")
     ap.add_argument("--scenarios", type=int, default=4096, help="c5: total scenarios (split across ranks)")
@@ -94,6 +94,9 @@ def parse():
 WORKLOADS = {
     "c3": dict(steps=20, warmup=2, batch=None, nodes=100_000, pods=1_000_000, bytes=60),
     "c2": dict(steps=9, warmup=2, batch=None, nodes=5000, pods=50_000, bytes=68),
+    # C2 + the launch-kernel features (volumes, SelectorSpread, pod anti-affinity): 68 B per node-eval
+    # of the row and its label / taint ids; the volume slots and counted pairs a pod reads come on top
+    "c2x": dict(steps=5, warmup=1, batch=None, nodes=5000, pods=20_000, bytes=68),
     "c4": dict(steps=10, warmup=1, batch=512, nodes=1_000_000, pods=None, bytes=60),
     "c5": dict(steps=3, warmup=1, batch=0, nodes=20_000, pods=0, bytes=60),
 }
@@ -292,6 +295,35 @@ def cpu_baseline(a, cl, preds, prios, placements, unit="pods/s"):
     return cpu, parity
 
 
+def cpu_baseline_objects(a, objs, preds, prios, placements, cl, budget_s=10.0):
+    """C2x: the C port does not restate volumes / spread / affinity, so the CPU leg is the object
+    oracle (oracle/ksim_ref.py, one thread, pure Python) on a prefix sized to ~budget_s; parity =
+    its placements equal the GPU's over that prefix."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ksim_ref as R
+    listers = R.VolumeListers(objs["pvs"], objs["pvcs"])
+    custom = {k: v for k, v in R.volume_predicates(listers).items() if k in preds}
+    queue = objs["pods"]                            # scheduling order (the cluster's queue)
+    S, s = 8, 0.0
+    while True:
+        t1 = time.perf_counter()
+        want, _ = R.simulate(objs["nodes"], [], list(reversed(queue[:S])), set(preds), list(prios), custom,
+                             spread=R.SpreadListers(services=objs["services"]))
+        s = time.perf_counter() - t1
+        if s >= budget_s / 4 or S >= min(a.cpu_sample, len(placements)):
+            break
+        S = min(int(S * max(2.0, budget_s / max(s, 1e-3))), min(a.cpu_sample, len(placements)))
+    idx = {nm: i for i, nm in enumerate(cl.names)}
+    ref = np.array([idx[h] if h is not None else -1 for _, h, _ in want], np.int32)
+    cpu = {"value": round(S / s, 2), "unit": "pods/s", "cores": 1, "kind": "port",
+           "sample": "first %d pods of the same C2x queue on the same %d-node cluster (oracle/ksim_ref.py, the "
+                     "object-level restatement in pure Python: the C port does not cover volumes / spread / "
+                     "affinity), %.2f s" % (S, cl.n_nodes, s),
+           "node_evals_per_s": round(S * cl.n_nodes / s, 1)}
+    return cpu, {"prefix_pods": S, "match": bool(np.array_equal(ref, placements[:S]))}
+
+
 def main():
     a = parse()
     if a.workload == "c5":
@@ -310,6 +342,11 @@ def main():
         cl, preds, prios = synth.config_c4(a.nodes, a.pods)
         desc = "C4: %d nodes, %d-pod queue, default predicates + LeastRequested(1) + BalancedResourceAllocation(1)"
         data = "synthetic (splitmix64 seed 4, SURVEY.md §8d C4)"
+    elif a.workload == "c2x":
+        cl, preds, prios, objs = synth.config_c2x(a.nodes, a.pods)
+        desc = ("C2x: %d C2 nodes in zones, %d pods: C2's plus volumes (GCE PD / EBS / zoned PVCs), services "
+                "(SelectorSpread), hostname anti-affinity; DefaultProvider")
+        data = "synthetic (random.Random seed 6 objects through ingest; C2 extended with the launch-kernel features)"
     else:
         cl, preds, prios = synth.config_c2(a.nodes, a.pods)
         desc = ("C2: %d heterogeneous nodes (labels, taints, NotReady), %d pods with nodeSelector, host ports, "
@@ -317,7 +354,7 @@ def main():
         data = "synthetic (random.Random seed 2 objects through ingest, SURVEY.md §8d C2)"
     n = cl.n_nodes
     mode = {"auto": abi.MODE_AUTO, "launch": abi.MODE_LAUNCH, "persistent": abi.MODE_PERSISTENT, "tree": abi.MODE_TREE}[a.mode]
-    sharded_head = world > 1 and a.shard == "nodes" and a.workload != "c2"  # sharding takes resource-only pods
+    sharded_head = world > 1 and a.shard == "nodes" and a.workload not in ("c2", "c2x")  # sharding: resource-only pods
 
     # ---- the one cluster: single GPU (N = 1), or node-sharded across the N ranks ----
     single = None
@@ -331,7 +368,7 @@ def main():
         sharded = node_sharded(a, D, cl, preds, prios)
         head = sharded
     replicas = None
-    if world > 1 and a.shard != "none" and not (a.shard == "replicas" or a.workload == "c2"):
+    if world > 1 and a.shard != "none" and not (a.shard == "replicas" or a.workload in ("c2", "c2x")):
         # side line: each rank its own cluster under its own LeastRequested weight (weak scaling)
         prios_r = [(k, w + rank) if k == "LeastRequestedPriority" else (k, w) for k, w in prios]
         r_args = argparse.Namespace(**vars(a))
@@ -352,7 +389,10 @@ def main():
         tree = tree_mode(a, cl, preds, prios, local, single["out"])
     cpu = parity = None
     if rank == 0 and a.cpu_sample > 0 and single is not None:
-        cpu, parity = cpu_baseline(a, cl, preds, prios, single["out"])
+        if a.workload == "c2x":
+            cpu, parity = cpu_baseline_objects(a, objs, preds, prios, single["out"], cl)
+        else:
+            cpu, parity = cpu_baseline(a, cl, preds, prios, single["out"])
 
     if rank == 0:
         if "error" in head:

@@ -23,6 +23,7 @@ from . import labels
 class SpreadListers:
     def __init__(self, services=(), rcs=(), rss=(), sss=()):
         self.services, self.rcs, self.rss, self.sss = list(services), list(rcs), list(rss), list(sss)
+        self._memo = {}   # (namespace, labels, services_only) -> selectors: pods share few label sets
 
     def __bool__(self):
         return bool(self.services or self.rcs or self.rss or self.sss)
@@ -36,6 +37,13 @@ class SpreadListers:
         """getSelectors: a list of selectors (ksim.labels form), in lister order."""
         md = pod.get("metadata") or {}
         ns, lab = md.get("namespace", ""), md.get("labels") or {}
+        key = (ns, tuple(sorted(lab.items())), services_only)
+        hit = self._memo.get(key)
+        if hit is None:
+            hit = self._memo[key] = self._selectors(ns, lab, services_only)
+        return hit
+
+    def _selectors(self, ns, lab, services_only):
         out = []
         for svc in self.services:
             sel = (svc.get("spec") or {}).get("selector")

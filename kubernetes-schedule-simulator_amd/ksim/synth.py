@@ -191,6 +191,55 @@ def config_c2(n_nodes=5000, n_pods=50_000, seed=2):
     return cl, p, q
 
 
+ZONE = "failure-domain.beta.kubernetes.io/zone"
+
+
+def c2x_objects(n_nodes=5000, n_pods=50_000, seed=6):
+    """C2 extended with the launch-kernel features: the C2 nodes (70 % in one of four zones) and
+    pods, of which 25 % mount volumes (inline GCE PD / EBS from a pool of 2,000 disks, read-only
+    now and then, or a PVC bound to a zoned GCE PV), 10 % carry a required pod anti-affinity term on
+    kubernetes.io/hostname, every pod labelled app=<one of 20> and selected by that app's service
+    (SelectorSpread).  Returns (nodes, pods, pvs, pvcs, services), pods in SCHEDULING order."""
+    import random
+    rng = random.Random(seed)
+    nodes, pods = c2_objects(n_nodes, n_pods, seed)
+    for x in nodes:
+        if rng.random() < 0.7:
+            x["metadata"]["labels"][ZONE] = "z%d" % rng.randrange(4)
+        x["metadata"]["labels"]["kubernetes.io/hostname"] = x["metadata"]["name"]
+    pvs = [{"metadata": {"name": "pv-%d" % i, "labels": {ZONE: "z%d" % (i % 4)}},
+            "spec": {"gcePersistentDisk": {"pdName": "pv-disk-%d" % i}}} for i in range(400)]
+    pvcs = [{"metadata": {"name": "claim-%d" % i, "namespace": "default"}, "spec": {"volumeName": "pv-%d" % i}}
+            for i in range(400)]
+    services = [{"metadata": {"name": "svc-%d" % a, "namespace": "default"}, "spec": {"selector": {"app": "a%d" % a}}}
+                for a in range(20)]
+    for p in pods:
+        app = "a%d" % rng.randrange(20)
+        p["metadata"]["labels"] = {"app": app}
+        r = rng.random()
+        if r < 0.10:
+            disk = "d%d" % rng.randrange(2000)
+            p["spec"]["volumes"] = [{"name": "v", "gcePersistentDisk": {"pdName": disk, "readOnly": rng.random() < 0.3}}]
+        elif r < 0.20:
+            p["spec"]["volumes"] = [{"name": "v", "awsElasticBlockStore": {"volumeID": "e%d" % rng.randrange(2000)}}]
+        elif r < 0.25:
+            p["spec"]["volumes"] = [{"name": "v", "persistentVolumeClaim": {"claimName": "claim-%d" % rng.randrange(400)}}]
+        if rng.random() < 0.10:
+            p["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": {"matchLabels": {"app": app}}, "topologyKey": "kubernetes.io/hostname"}]}}
+    return nodes, pods, pvs, pvcs, services
+
+
+def config_c2x(n_nodes=5000, n_pods=50_000, seed=6):
+    """C2x through the object path with its listers: (cluster, predicates, priorities, objects) of
+    the DefaultProvider; objects = dict(nodes, pods, pvs, pvcs, services) for the oracle."""
+    from .spread import SpreadListers
+    nodes, pods, pvs, pvcs, services = c2x_objects(n_nodes, n_pods, seed)
+    cl = Cluster.from_objects(nodes, (), pods, pvs=pvs, pvcs=pvcs, spread=SpreadListers(services=services))
+    p, q = scheduler.provider("DefaultProvider")
+    return cl, p, q, dict(nodes=nodes, pods=pods, pvs=pvs, pvcs=pvcs, services=services)
+
+
 def c5_scenarios():
     """4,096 (wLR, wBRA, wMR) policy points; wMR = 0 means MostRequested absent."""
     out = []

@@ -236,14 +236,26 @@ class VolumeIndex:
 
     def zone_verdicts(self, label_sets):
         """NoVolumeZoneConflict per (class, label set): bit table [n_class][words], and whether
-        some (class, label set) errs (predicates.go:559-628)."""
+        some (class, label set) errs (predicates.go:559-628).  Evaluated once per distinct
+        (zone, region) constraint of the label sets; classes without PVCs pass everywhere."""
         L = len(label_sets)
         words = (L + 31) // 32
         ok = np.zeros((len(self.class_zone), max(words, 1)), np.uint32)
+        cons_of = [tuple(sorted((k, v) for k, v in dict(ls).items() if k in (ZONE_LABEL, REGION_LABEL)))
+                   for ls in label_sets]
+        groups = {}
+        for s, c in enumerate(cons_of):
+            groups.setdefault(c, []).append(s)
+        full = np.zeros(max(words, 1), np.uint32)
+        for s in range(L):
+            full[s >> 5] |= np.uint32(1 << (s & 31))
         err = False
         for c, zone in enumerate(self.class_zone):
-            for s, labels in enumerate(label_sets):
-                cons = {k: v for k, v in dict(labels).items() if k in (ZONE_LABEL, REGION_LABEL)}
+            if not zone:
+                ok[c] = full
+                continue
+            for cons_t, members in groups.items():
+                cons = dict(cons_t)
                 fits = True
                 if cons:
                     for z in zone:
@@ -263,7 +275,8 @@ class VolumeIndex:
                             fits = False
                             break
                 if fits:
-                    ok[c, s >> 5] |= np.uint32(1 << (s & 31))
+                    for s in members:
+                        ok[c, s >> 5] |= np.uint32(1 << (s & 31))
         return ok[:, :words] if words else ok[:, :0], err
 
     def node_slots(self, n, running):
