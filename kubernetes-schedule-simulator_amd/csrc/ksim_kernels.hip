@@ -408,9 +408,11 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
 // atomics).  Every block reduces its chunk to a partial; the last block to arrive combines them
 // into aff->mm, publishes the zone sums (zread) with their maximum, zeroes zsum for the next pod
 // and re-arms the ticket.  Pods that read neither priority exit at once (uniformly).
+#define KSIM_PASS_ZONES 512
 template <int NPT>
 __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
   __shared__ int64_t s_v[4][KSIM_WAVES];
+  __shared__ unsigned long long s_z[KSIM_PASS_ZONES];  // block-local zone sums (few zones: no global contention)
   __shared__ int s_last;
   const int64_t pod = *c.cursor;
   if (pod >= c.end || !c.aff || c.no_prio) return;
@@ -421,6 +423,11 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
   if (!ipa && sp < 0) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t base = (int64_t)blockIdx.x * c.chunk;
+  const bool zlocal = A.n_zone <= KSIM_PASS_ZONES;
+  if (sp >= 0 && zlocal) {
+    for (int z = tid; z < A.n_zone; z += KSIM_BLOCK) s_z[z] = 0;
+    __syncthreads();
+  }
   int64_t mn = 0, mx = 0, smx = 0, hz = 0;
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
@@ -439,9 +446,17 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
       const int32_t z = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
       if (z >= 0) {
         hz = 1;
-        if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&A.zsum[z]), (unsigned long long)v);
+        if (v) {
+          if (zlocal) atomicAdd(&s_z[z], (unsigned long long)v);
+          else atomicAdd(reinterpret_cast<unsigned long long*>(&A.zsum[z]), (unsigned long long)v);
+        }
       }
     }
+  }
+  if (sp >= 0 && zlocal) {  // one global add per (block, zone) with a count
+    __syncthreads();
+    for (int z = tid; z < A.n_zone; z += KSIM_BLOCK)
+      if (s_z[z]) atomicAdd(reinterpret_cast<unsigned long long*>(&A.zsum[z]), s_z[z]);
   }
   auto combine = [&]() {
 #pragma unroll
