@@ -28,6 +28,15 @@ struct __attribute__((aligned(16))) KsimPartial {
   int32_t hist[KSIM_NREASONS];   // failure reasons (only when collecting)
 };
 
+// Per-block candidate masks of the launch-form scan, beside the partials: for every reduce class q
+// and node slot k of the chunk, each wave's ballot of its nodes at the wave's maximum of class q
+// ([q][k][wave], q = KSIM_MAX_RCLASS: the fit ballot), then each wave's maximum per class.  The
+// last block picks the node from the chosen block's masks instead of re-evaluating that block.
+#define KSIM_PM_NPT 8
+#define KSIM_PM_MASK(q, k, w) ((((q) * KSIM_PM_NPT) + (k)) * KSIM_WAVES + (w))
+#define KSIM_PM_MX(q, w) ((KSIM_MAX_RCLASS + 1) * KSIM_PM_NPT * KSIM_WAVES + (q) * KSIM_WAVES + (w))
+#define KSIM_PM_STRIDE ((KSIM_MAX_RCLASS + 1) * KSIM_PM_NPT * KSIM_WAVES + KSIM_MAX_RCLASS * KSIM_WAVES)
+
 // Inter-pod affinity tables on the device (ksim_load_affinity; layout in include/ksim.h).
 struct KsimAff {
   int64_t n;                       // nodes (the dom stride)
@@ -131,6 +140,7 @@ struct KsimCtx {
   uint64_t* counter;      // genericScheduler.lastNodeIndex
   uint32_t* ticket;       // last-block arrival counter
   KsimPartial* partials;  // [grid]
+  uint64_t* pmask;        // [grid][KSIM_PM_STRIDE] candidate masks (KSIM_PM_*)
   int32_t* out_node;      // [end-first]
   int32_t* out_reasons;   // [end-first][KSIM_NREASONS]
   int32_t* err;           // sticky error word

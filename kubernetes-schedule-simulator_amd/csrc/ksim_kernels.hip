@@ -6,8 +6,9 @@
 // histogram) partial, publishes it, and takes an arrival ticket.  The last block to
 // arrive acquires, combines all partials into the global decision (findNodesThatFit
 // → PrioritizeNodes → selectHost, core/generic_scheduler.go:112-198), locates the
-// selected node by walking block counts from the highest name rank down, re-evaluates
-// only that block to pick the exact node, commits the pod (NodeInfo.AddPod) and advances
+// selected node by walking block counts from the highest name rank down, picks the exact
+// node from that block's published candidate masks (KSIM_PM_*: per wave and reduce class, the
+// ballot of nodes at the wave's maximum), commits the pod (NodeInfo.AddPod) and advances
 // the device-side pod cursor.  Launches are replayed from a hipGraph, so per-pod host
 // work is zero and no PCIe traffic happens between pods.
 #include "ksim_common.h"
@@ -123,6 +124,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   __shared__ uint64_t s_ball[NPT][KSIM_WAVES];
   __shared__ int s_last;
   __shared__ Decision D;
+  static_assert(NPT <= KSIM_PM_NPT, "candidate masks hold KSIM_PM_NPT node slots per thread");
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int64_t pod = *c.cursor;
@@ -145,9 +147,16 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   for (int k = 0; k < NPT; ++k)
     eval_one<COLLECT>(c, P, base + k * KSIM_BLOCK + tid, k1, k2, ipa, fit[k], sc[k], cl[k], rm[k]);
 
+  // candidate masks: write-through (sc1) stores, drained by every storing wave before the barrier
+  // that precedes the ticket, read back with sc1 loads by the last block
+  uint64_t* pm = c.pmask + (int64_t)blockIdx.x * KSIM_PM_STRIDE;
   int32_t nfit = 0;
 #pragma unroll
-  for (int k = 0; k < NPT; ++k) nfit += __popcll(__ballot(fit[k]));
+  for (int k = 0; k < NPT; ++k) {
+    const uint64_t b = __ballot(fit[k]);
+    nfit += __popcll(b);
+    if (lane == 0) __hip_atomic_store(&pm[KSIM_PM_MASK(KSIM_MAX_RCLASS, k, wv)], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   if (lane == 0) s_fit[wv] = nfit;
 
 #pragma unroll
@@ -160,8 +169,16 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     const int64_t wm = wave_max_i64(v);
     int32_t n = 0;
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) n += __popcll(__ballot(fit[k] && cl[k] == q && sc[k] == wm));
-    if (lane == 0) { s_mx[wv][q] = wm; s_cnt[wv][q] = (wm == INT64_MIN) ? 0 : n; }
+    for (int k = 0; k < NPT; ++k) {
+      const uint64_t b = __ballot(fit[k] && cl[k] == q && sc[k] == wm);
+      n += __popcll(b);
+      if (lane == 0) __hip_atomic_store(&pm[KSIM_PM_MASK(q, k, wv)], b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (lane == 0) {
+      s_mx[wv][q] = wm;
+      s_cnt[wv][q] = (wm == INT64_MIN) ? 0 : n;
+      __hip_atomic_store(reinterpret_cast<int64_t*>(&pm[KSIM_PM_MX(q, wv)]), wm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   if (COLLECT) {
     __syncthreads();
@@ -175,6 +192,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       }
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   // ---------------- publish the partial, take a ticket ----------------
@@ -358,16 +376,24 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       if (tid == 0) { atomicOr(c.err, 2); c.out_node[pod] = -1; *c.cursor = pod + 1; *c.ticket = 0; }
       return;
     }
-    // ---- re-evaluate the selected block, pick the exact node ----
+    // ---- the selected block's candidate masks (no re-evaluation), pick the exact node ----
     const int64_t bb = D.blk * c.chunk;
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      bool f; int64_t sc1; int cl1; uint32_t rm1;
-      eval_one<false>(c, P, bb + k * KSIM_BLOCK + tid, k1, k2, ipa, f, sc1, cl1, rm1);
-      bool match = f;
-      if (D.mode == 2) match = f && ((D.winners >> cl1) & 1u) && sc1 == D.M[cl1];
-      const uint64_t bal = __ballot(match);
-      if (lane == 0) s_ball[k][wv] = bal;
+    if (tid < NPT * KSIM_WAVES) {
+      const int k = tid / KSIM_WAVES, w = tid % KSIM_WAVES;
+      uint64_t* pb = c.pmask + D.blk * KSIM_PM_STRIDE;
+      uint64_t m = 0;
+      if (D.mode == 1) {
+        m = __hip_atomic_load(&pb[KSIM_PM_MASK(KSIM_MAX_RCLASS, k, w)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        for (int q = 0; q < K; ++q) {
+          if (!((D.winners >> q) & 1u)) continue;
+          const int64_t wm = __hip_atomic_load(reinterpret_cast<int64_t*>(&pb[KSIM_PM_MX(q, w)]), __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+          if (wm == D.M[q])
+            m |= __hip_atomic_load(&pb[KSIM_PM_MASK(q, k, w)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      s_ball[k][w] = m;
     }
     __syncthreads();
     if (tid == 0) {

@@ -452,10 +452,14 @@ int ksim_rt_ensure_partials(ksim_handle* h, int grid) {
   KsimCtx& c = h->ctx;
   if (c.partials && h->part_cap >= grid) return KSIM_OK;
   KsimPartial* p;
+  uint64_t* pm;
   int rc = dev_alloc(h, &p, (size_t)std::max(grid, 1024));
   if (rc) return rc;
+  if ((rc = dev_alloc(h, &pm, (size_t)std::max(grid, 1024) * KSIM_PM_STRIDE))) { dev_free(h, p); return rc; }
   dev_free(h, c.partials);
+  dev_free(h, c.pmask);
   c.partials = p;
+  c.pmask = pm;
   h->part_cap = std::max(grid, 1024);
   if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
   if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
