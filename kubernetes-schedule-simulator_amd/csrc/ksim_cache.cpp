@@ -322,6 +322,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   if ((rc = ksim_rt_ensure_partials(h, grid))) return rc;
   cs.partials = c.partials;
   cs.pmask = c.pmask;
+  cs.fuse_a = 0;  // pass A as its own launch below
   hipError_t e = hipSuccess;
   if (ksim_is_aff_host(h, *pod) && (c.w[KSIM_W_INTERPOD_AFFINITY] || c.w[KSIM_W_SELECTOR_SPREAD]) && !c.no_prio)
     e = ksim_launch_ipa_pass(&cs, npt, grid, h->stream);  // InterPodAffinity / SelectorSpread reductions first

@@ -123,7 +123,7 @@ struct KsimCtx {
   int32_t use_na;                      // NA class dimension in use: NodeAffinity weight or na_add
   int32_t lwords, twords, n_label_sets, n_taint_sets;
   int32_t n_classes_dev;  // pod classes in the tables
-  int32_t pad1;
+  int32_t fuse_a;         // launch form: pass A fused into the scan (grid barrier; co-resident grid)
   // ---- pod queue ----
   const ksim_pod* __restrict__ pods;
   const uint64_t* __restrict__ pod_ports;

@@ -114,6 +114,162 @@ __device__ __forceinline__ void eval_one(const KsimCtx& c, const ksim_pod& P, in
   cls = (k1 * k2 > 1) ? ksim_rclass(c, P, i, k1, k2) : 0;
 }
 
+// Pass A of an InterPodAffinityPriority / SelectorSpread pod, over the fit nodes: min / max of the
+// raw InterPodAffinity sums with 0 folded in as the reference's accumulators start there
+// (interpod_affinity.go:129-131, 218-226); SelectorSpread's maxCountByNodeName, haveZones and
+// countsByZone (selector_spreading.go:125-145, zone sums by atomics).  Every block reduces its
+// chunk to a partial; the last block to arrive combines them into aff->mm, publishes the zone sums
+// (zread) with their maximum, zeroes zsum for the next pod and re-arms the ticket.  Returns true
+// in that block.  Run either as its own launch before the scan (ksim_ipa_pass_kernel) or fused
+// into the scan behind a grid barrier (KsimCtx::fuse_a).
+#define KSIM_PASS_ZONES 512
+template <int NPT>
+__device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t sp, const bool (&fit)[NPT],
+                                             const int64_t (&raw)[NPT], const int64_t (&cnt)[NPT],
+                                             const int32_t (&zz)[NPT], int64_t (*s_v)[KSIM_WAVES],
+                                             unsigned long long* s_z, int* s_last) {
+  const KsimAff& A = *c.aff;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const bool zlocal = A.n_zone <= KSIM_PASS_ZONES;
+  if (sp >= 0 && zlocal) {
+    for (int z = tid; z < A.n_zone; z += KSIM_BLOCK) s_z[z] = 0;
+    __syncthreads();
+  }
+  int64_t mn = 0, mx = 0, smx = 0, hz = 0;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    if (!fit[k]) continue;
+    if (ipa) {
+      mn = raw[k] < mn ? raw[k] : mn;
+      mx = raw[k] > mx ? raw[k] : mx;
+    }
+    if (sp >= 0) {
+      const int64_t v = cnt[k];
+      smx = v > smx ? v : smx;
+      const int32_t z = zz[k];
+      if (z >= 0) {
+        hz = 1;
+        if (v) {
+          if (zlocal) atomicAdd(&s_z[z], (unsigned long long)v);
+          else atomicAdd(reinterpret_cast<unsigned long long*>(&A.zsum[z]), (unsigned long long)v);
+        }
+      }
+    }
+  }
+  if (sp >= 0 && zlocal) {  // one global add per (block, zone) with a count
+    __syncthreads();
+    for (int z = tid; z < A.n_zone; z += KSIM_BLOCK)
+      if (s_z[z]) atomicAdd(reinterpret_cast<unsigned long long*>(&A.zsum[z]), s_z[z]);
+  }
+  auto combine = [&]() {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+      const int64_t d = __shfl_xor(smx, o, 64), e = __shfl_xor(hz, o, 64);
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+      smx = d > smx ? d : smx;
+      hz = e > hz ? e : hz;
+    }
+    if (lane == 0) { s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < KSIM_WAVES; ++w) {
+        mn = s_v[0][w] < mn ? s_v[0][w] : mn;
+        mx = s_v[1][w] > mx ? s_v[1][w] : mx;
+        smx = s_v[2][w] > smx ? s_v[2][w] : smx;
+        hz = s_v[3][w] > hz ? s_v[3][w] : hz;
+      }
+    }
+  };
+  combine();
+  if (tid == 0) {
+    int64_t* pp = A.part + 4 * (int64_t)blockIdx.x;
+    pp[0] = mn; pp[1] = mx; pp[2] = smx; pp[3] = hz;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const uint32_t old = __hip_atomic_fetch_add(A.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *s_last = (old == gridDim.x - 1);
+  }
+  __syncthreads();
+  if (!*s_last) return false;
+  if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  mn = 0; mx = 0; smx = 0; hz = 0;
+  for (int b = tid; b < (int)gridDim.x; b += KSIM_BLOCK) {
+    const int64_t* pp = A.part + 4 * (int64_t)b;
+    mn = pp[0] < mn ? pp[0] : mn;
+    mx = pp[1] > mx ? pp[1] : mx;
+    smx = pp[2] > smx ? pp[2] : smx;
+    hz = pp[3] > hz ? pp[3] : hz;
+  }
+  __syncthreads();
+  combine();
+  __syncthreads();
+  const int64_t r0 = mn, r1 = mx, r2 = smx, r3 = hz;  // valid in thread 0
+  // zone sums: publish for the scan, zero for the next pod, maximum (countsByZone, :139-143)
+  int64_t zmx = 0;
+  if (sp >= 0)
+    for (int z = tid; z < A.n_zone; z += KSIM_BLOCK) {
+      const int64_t v = __hip_atomic_load(&A.zsum[z], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      A.zread[z] = v;
+      A.zsum[z] = 0;
+      zmx = v > zmx ? v : zmx;
+    }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int64_t a = __shfl_xor(zmx, o, 64);
+    zmx = a > zmx ? a : zmx;
+  }
+  if (lane == 0) s_v[0][wv] = zmx;
+  __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < KSIM_WAVES; ++w) zmx = s_v[0][w] > zmx ? s_v[0][w] : zmx;
+    A.mm[0] = r0;
+    A.mm[1] = r1;
+    A.mm[2] = r2;
+    A.mm[3] = r3;
+    A.mm[4] = zmx;
+    *A.ticket = 0;
+  }
+  return true;
+}
+
+// Pass A as its own launch (pods that read neither priority exit at once, uniformly).
+template <int NPT>
+__global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
+  __shared__ int64_t s_v[4][KSIM_WAVES];
+  __shared__ unsigned long long s_z[KSIM_PASS_ZONES];  // block-local zone sums (few zones: no global contention)
+  __shared__ int s_last;
+  const int64_t pod = *c.cursor;
+  if (pod >= c.end || !c.aff || c.no_prio) return;
+  const ksim_pod P = c.pods[pod];
+  const KsimAff& A = *c.aff;
+  const bool ipa = c.w[KSIM_W_INTERPOD_AFFINITY] != 0 && ksim_interpod_prio_work(A, P);
+  const int32_t sp = c.w[KSIM_W_SELECTOR_SPREAD] != 0 ? ksim_spread_pair(A, P) : -1;
+  if (!ipa && sp < 0) return;
+  const int64_t base = (int64_t)blockIdx.x * c.chunk;
+  bool fit[NPT];
+  int64_t raw[NPT], cnt[NPT];
+  int32_t zz[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int64_t i = base + k * KSIM_BLOCK + threadIdx.x;
+    fit[k] = false; raw[k] = 0; cnt[k] = 0; zz[k] = -1;
+    if (i >= c.n) continue;
+    const KsimRow r = ksim_load_row(c, i);
+    if (ksim_predicates(c, P, i, r) != 0) continue;
+    fit[k] = true;
+    if (ipa) raw[k] = ksim_interpod_raw(A, P, i);
+    if (sp >= 0) {
+      cnt[k] = A.cnt[A.pair_off[sp] + i];
+      zz[k] = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
+    }
+  }
+  (void)passa_reduce<NPT>(c, ipa, sp, fit, raw, cnt, zz, s_v, s_z, &s_last);
+}
+
 template <int NPT, bool COLLECT>
 __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   __shared__ int64_t s_mx[KSIM_WAVES][KSIM_MAX_RCLASS];
@@ -124,6 +280,10 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   __shared__ uint64_t s_ball[NPT][KSIM_WAVES];
   __shared__ int s_last;
   __shared__ Decision D;
+  __shared__ int64_t s_v[4][KSIM_WAVES];               // fused pass A
+  __shared__ unsigned long long s_z[KSIM_PASS_ZONES];
+  __shared__ uint32_t s_gen;
+  __shared__ int s_bail;
   static_assert(NPT <= KSIM_PM_NPT, "candidate masks hold KSIM_PM_NPT node slots per thread");
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -134,7 +294,21 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   const int k2 = c.use_na ? c.n_na[P.cls] : 1;
   const int K = k1 * k2;
   const int64_t base = (int64_t)blockIdx.x * c.chunk;
-  const IpaNorm ipa = ipa_norm(c, P);
+  IpaNorm ipa = ipa_norm(c, P);
+  // fused pass A (KsimCtx::fuse_a, grid co-resident): this pod's pass-A reductions run over the
+  // fit nodes evaluated here, behind one grid barrier (generation word ticket[1], read before
+  // this block's pass-A ticket), and the normalised scores are added afterwards
+  const bool fuse = c.fuse_a && (ipa.on || ipa.sp >= 0);
+  IpaNorm ipa0 = ipa;
+  if (fuse) {
+    ipa0.on = false;
+    ipa0.sp = -1;
+    if (tid == 0) {
+      s_bail = 0;
+      s_gen = __hip_atomic_load(c.ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
 
   if (COLLECT && tid < KSIM_NREASONS) s_hist[tid] = 0;
 
@@ -145,7 +319,60 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   uint32_t rm[NPT];
 #pragma unroll
   for (int k = 0; k < NPT; ++k)
-    eval_one<COLLECT>(c, P, base + k * KSIM_BLOCK + tid, k1, k2, ipa, fit[k], sc[k], cl[k], rm[k]);
+    eval_one<COLLECT>(c, P, base + k * KSIM_BLOCK + tid, k1, k2, ipa0, fit[k], sc[k], cl[k], rm[k]);
+
+  if (fuse) {
+    const KsimAff& A = *c.aff;
+    int64_t raw[NPT], cnt[NPT];
+    int32_t zz[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int64_t i = base + k * KSIM_BLOCK + tid;
+      raw[k] = 0; cnt[k] = 0; zz[k] = -1;
+      if (!fit[k]) continue;
+      if (ipa.on) raw[k] = ksim_interpod_raw(A, P, i);
+      if (ipa.sp >= 0) {
+        cnt[k] = A.cnt[A.pair_off[ipa.sp] + i];
+        zz[k] = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
+      }
+    }
+    if (passa_reduce<NPT>(c, ipa.on, ipa.sp, fit, raw, cnt, zz, s_v, s_z, &s_last)) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's zread stores
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(c.ticket + 1, s_gen + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    } else {
+      if (tid == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(c.ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == s_gen) {
+          __builtin_amdgcn_s_sleep(1);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: blocks not co-resident
+            atomicOr(c.err, 8);
+            s_bail = 1;
+            break;
+          }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (s_bail) return;
+    }
+    ipa = ipa_norm(c, P);  // the combined maxima
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {  // eval_one's additions, same order
+      if (!fit[k]) continue;
+      if (ipa.on)
+        sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)ipa.w * (uint64_t)ksim_interpod_score(raw[k], ipa.mn, ipa.mx));
+      if (ipa.sp >= 0) {
+        const int64_t v = ksim_spread_score(cnt[k], ipa.smx, ipa.hz, zz[k], zz[k] >= 0 ? A.zread[zz[k]] : 0, ipa.szmx);
+        sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)ipa.sw * (uint64_t)v);
+      }
+    }
+  }
 
   // candidate masks: write-through (sc1) stores, drained by every storing wave before the barrier
   // that precedes the ticket, read back with sc1 loads by the last block
@@ -427,137 +654,6 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   }
 }
 
-// Pass A of an InterPodAffinityPriority / SelectorSpread pod (one launch before its scan), over
-// the fit nodes: min / max of the raw InterPodAffinity sums with 0 folded in as the reference's
-// accumulators start there (interpod_affinity.go:129-131, 218-226); SelectorSpread's
-// maxCountByNodeName, haveZones and countsByZone (selector_spreading.go:125-145, zone sums by
-// atomics).  Every block reduces its chunk to a partial; the last block to arrive combines them
-// into aff->mm, publishes the zone sums (zread) with their maximum, zeroes zsum for the next pod
-// and re-arms the ticket.  Pods that read neither priority exit at once (uniformly).
-#define KSIM_PASS_ZONES 512
-template <int NPT>
-__global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
-  __shared__ int64_t s_v[4][KSIM_WAVES];
-  __shared__ unsigned long long s_z[KSIM_PASS_ZONES];  // block-local zone sums (few zones: no global contention)
-  __shared__ int s_last;
-  const int64_t pod = *c.cursor;
-  if (pod >= c.end || !c.aff || c.no_prio) return;
-  const ksim_pod P = c.pods[pod];
-  const KsimAff& A = *c.aff;
-  const bool ipa = c.w[KSIM_W_INTERPOD_AFFINITY] != 0 && ksim_interpod_prio_work(A, P);
-  const int32_t sp = c.w[KSIM_W_SELECTOR_SPREAD] != 0 ? ksim_spread_pair(A, P) : -1;
-  if (!ipa && sp < 0) return;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int64_t base = (int64_t)blockIdx.x * c.chunk;
-  const bool zlocal = A.n_zone <= KSIM_PASS_ZONES;
-  if (sp >= 0 && zlocal) {
-    for (int z = tid; z < A.n_zone; z += KSIM_BLOCK) s_z[z] = 0;
-    __syncthreads();
-  }
-  int64_t mn = 0, mx = 0, smx = 0, hz = 0;
-#pragma unroll
-  for (int k = 0; k < NPT; ++k) {
-    const int64_t i = base + k * KSIM_BLOCK + tid;
-    if (i >= c.n) continue;
-    const KsimRow r = ksim_load_row(c, i);
-    if (ksim_predicates(c, P, i, r) != 0) continue;
-    if (ipa) {
-      const int64_t v = ksim_interpod_raw(A, P, i);
-      mn = v < mn ? v : mn;
-      mx = v > mx ? v : mx;
-    }
-    if (sp >= 0) {
-      const int64_t v = A.cnt[A.pair_off[sp] + i];
-      smx = v > smx ? v : smx;
-      const int32_t z = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
-      if (z >= 0) {
-        hz = 1;
-        if (v) {
-          if (zlocal) atomicAdd(&s_z[z], (unsigned long long)v);
-          else atomicAdd(reinterpret_cast<unsigned long long*>(&A.zsum[z]), (unsigned long long)v);
-        }
-      }
-    }
-  }
-  if (sp >= 0 && zlocal) {  // one global add per (block, zone) with a count
-    __syncthreads();
-    for (int z = tid; z < A.n_zone; z += KSIM_BLOCK)
-      if (s_z[z]) atomicAdd(reinterpret_cast<unsigned long long*>(&A.zsum[z]), s_z[z]);
-  }
-  auto combine = [&]() {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const int64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
-      const int64_t d = __shfl_xor(smx, o, 64), e = __shfl_xor(hz, o, 64);
-      mn = a < mn ? a : mn;
-      mx = b > mx ? b : mx;
-      smx = d > smx ? d : smx;
-      hz = e > hz ? e : hz;
-    }
-    if (lane == 0) { s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz; }
-    __syncthreads();
-    if (tid == 0) {
-      for (int w = 1; w < KSIM_WAVES; ++w) {
-        mn = s_v[0][w] < mn ? s_v[0][w] : mn;
-        mx = s_v[1][w] > mx ? s_v[1][w] : mx;
-        smx = s_v[2][w] > smx ? s_v[2][w] : smx;
-        hz = s_v[3][w] > hz ? s_v[3][w] : hz;
-      }
-    }
-  };
-  combine();
-  if (tid == 0) {
-    int64_t* pp = A.part + 4 * (int64_t)blockIdx.x;
-    pp[0] = mn; pp[1] = mx; pp[2] = smx; pp[3] = hz;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const uint32_t old = __hip_atomic_fetch_add(A.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (old == gridDim.x - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  mn = 0; mx = 0; smx = 0; hz = 0;
-  for (int b = tid; b < (int)gridDim.x; b += KSIM_BLOCK) {
-    const int64_t* pp = A.part + 4 * (int64_t)b;
-    mn = pp[0] < mn ? pp[0] : mn;
-    mx = pp[1] > mx ? pp[1] : mx;
-    smx = pp[2] > smx ? pp[2] : smx;
-    hz = pp[3] > hz ? pp[3] : hz;
-  }
-  __syncthreads();
-  combine();
-  __syncthreads();
-  const int64_t r0 = mn, r1 = mx, r2 = smx, r3 = hz;  // valid in thread 0
-  // zone sums: publish for the scan, zero for the next pod, maximum (countsByZone, :139-143)
-  int64_t zmx = 0;
-  if (sp >= 0)
-    for (int z = tid; z < A.n_zone; z += KSIM_BLOCK) {
-      const int64_t v = __hip_atomic_load(&A.zsum[z], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      A.zread[z] = v;
-      A.zsum[z] = 0;
-      zmx = v > zmx ? v : zmx;
-    }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const int64_t a = __shfl_xor(zmx, o, 64);
-    zmx = a > zmx ? a : zmx;
-  }
-  if (lane == 0) s_v[0][wv] = zmx;
-  __syncthreads();
-  if (tid == 0) {
-    for (int w = 1; w < KSIM_WAVES; ++w) zmx = s_v[0][w] > zmx ? s_v[0][w] : zmx;
-    A.mm[0] = r0;
-    A.mm[1] = r1;
-    A.mm[2] = r2;
-    A.mm[3] = r3;
-    A.mm[4] = zmx;
-    *A.ticket = 0;
-  }
-}
-
 // Per-node evaluation of one pod without commit (ksim_evaluate).
 __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_t pod, uint8_t* fit, uint32_t* reasons,
                                                              int64_t* score, uint8_t* rcls) {
@@ -604,6 +700,18 @@ extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, i
   }
 #undef KSIM_L
   return hipGetLastError();
+}
+
+// Whether the scan grid is co-resident (the fused pass A's grid barrier needs it).
+extern "C" int ksim_scan_coresident(int npt, int collect, int grid) {
+#define KSIM_C(N, C) (ksim_check_coresident(ksim_scan_kernel<N, C>, grid, KSIM_BLOCK, 0) == hipSuccess)
+  switch (npt) {
+    case 1: return collect ? KSIM_C(1, true) : KSIM_C(1, false);
+    case 2: return collect ? KSIM_C(2, true) : KSIM_C(2, false);
+    case 4: return collect ? KSIM_C(4, true) : KSIM_C(4, false);
+    default: return collect ? KSIM_C(8, true) : KSIM_C(8, false);
+  }
+#undef KSIM_C
 }
 
 extern "C" hipError_t ksim_launch_ipa_pass(const KsimCtx* c, int npt, int grid, hipStream_t s) {

@@ -480,14 +480,18 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
   const int batch = (int)std::min<int64_t>(count, 256);
   const int ipa = ksim_rt_aff_count(h, first, count) > 0 &&
                   (c.w[KSIM_W_INTERPOD_AFFINITY] != 0 || c.w[KSIM_W_SELECTOR_SPREAD] != 0) && !c.no_prio ? 1 : 0;
+  // pass A fused into the scan behind a grid barrier when the grid is co-resident (KSIM_FUSE_A=0: two launches)
+  const char* fz = getenv("KSIM_FUSE_A");
+  c.fuse_a = ipa && !(fz && fz[0] == '0') && ksim_scan_coresident(npt, c.collect, grid) ? 1 : 0;
+  const int gkey = ipa | c.fuse_a << 1;
   if (!h->gexec || h->g_batch != batch || h->g_npt != npt || h->g_collect != c.collect || h->g_first != first ||
-      h->g_end != c.end || h->g_ipa != ipa) {
+      h->g_end != c.end || h->g_ipa != gkey) {
     if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
     if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
     for (int k = 0; k < batch; ++k) {
-      hipError_t e = ipa ? ksim_launch_ipa_pass(&c, npt, grid, h->stream) : hipSuccess;
+      hipError_t e = ipa && !c.fuse_a ? ksim_launch_ipa_pass(&c, npt, grid, h->stream) : hipSuccess;
       if (e == hipSuccess) e = ksim_launch_scan(&c, npt, c.collect, grid, h->stream);
       if (e != hipSuccess) {
         hipGraph_t g = nullptr;
@@ -498,7 +502,7 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
     }
     HIPCHK(h, hipStreamEndCapture(h->stream, &h->graph));
     HIPCHK(h, hipGraphInstantiate(&h->gexec, h->graph, nullptr, nullptr, 0));
-    h->g_batch = batch; h->g_npt = npt; h->g_collect = c.collect; h->g_first = first; h->g_end = c.end; h->g_ipa = ipa;
+    h->g_batch = batch; h->g_npt = npt; h->g_collect = c.collect; h->g_first = first; h->g_end = c.end; h->g_ipa = gkey;
   }
   const int64_t reps = (count + batch - 1) / batch;
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
