@@ -52,6 +52,16 @@ def test_affinity_simulation_matches_oracle(seed, policy, mode):
         assert any(m and "affinity" in m for _, _, m in want)   # the predicate decided something
 
 
+@pytest.mark.parametrize("policy", sorted(POLICIES))
+@pytest.mark.parametrize("seed", range(3))
+def test_affinity_two_launch_form_matches_oracle(seed, policy, monkeypatch):
+    """Launch form with pass A as its own launch (KSIM_FUSE_A=0) instead of fused into the scan."""
+    monkeypatch.setenv("KSIM_FUSE_A", "0")
+    preds, prios = POLICIES[policy]
+    nodes, running, pods = rnd_affinity_workload(seed, n_nodes=18 + 7 * seed, n_pods=90, n_running=12)
+    _check(nodes, running, pods, preds, prios, abi.MODE_LAUNCH)
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_mixed_affinity_and_resource_only_pods(seed):
     """Mostly term-free pods (tree / fast kernels) interleaved with affinity pods (launch kernels):

@@ -35,9 +35,13 @@ POLICIES = {
 }
 
 
+@pytest.mark.parametrize("fuse", ["fused", "two_launch"])
 @pytest.mark.parametrize("policy", sorted(POLICIES))
 @pytest.mark.parametrize("seed", range(4))
-def test_spread_simulation_matches_oracle(seed, policy):
+def test_spread_simulation_matches_oracle(seed, policy, fuse, monkeypatch):
+    """Both launch forms: pass A fused into the scan (grid barrier) and as its own launch."""
+    if fuse == "two_launch":
+        monkeypatch.setenv("KSIM_FUSE_A", "0")
     nodes, running, pods, objs = rnd_spread_workload(seed, zones=seed != 3)
     preds, prios = POLICIES[policy]
     want, want_lni = R.simulate(nodes, running, pods, set(preds), list(prios), spread=R.SpreadListers(**objs))
