@@ -419,22 +419,26 @@ __device__ __forceinline__ int64_t ksim_interpod_score(int64_t raw, int64_t mn, 
 
 // NodeInfo.AddPod / RemovePod of an affinity pod on node w (sign +1 / -1): every counted pair
 // whose selector its identity matches, and the amounts of the terms it carries.  Single thread.
-__device__ __noinline__ void ksim_aff_commit(const KsimAff& A, const ksim_pod& P, int64_t w, int32_t sign) {
+__device__ __noinline__ void ksim_aff_commit(const KsimAff& A, const ksim_pod& P, int64_t w, int32_t sign,
+                                             int32_t lane = 0, int32_t stride = 1) {
+  // lanes [lane, stride) split the pairs and carries; the updates are atomic adds (order-free sums)
   if (P.aff_ident > 0) {
     const uint64_t* sm = A.ident_sel + (int64_t)(P.aff_ident - 1) * A.sel_words;
-    for (int32_t c = 0; c < A.n_pair; ++c) {
+    for (int32_t c = lane; c < A.n_pair; c += stride) {
       const int32_t s = A.pair_sel[c];
       if (!((sm[s >> 6] >> (s & 63)) & 1ull)) continue;
       const int32_t d = ksim_dom(A, A.pair_key[c], w);
-      if (d >= 0) A.cnt[A.pair_off[c] + d] += sign;
+      if (d >= 0) atomicAdd(&A.cnt[A.pair_off[c] + d], sign);
     }
   }
   if (P.aff_class > 0) {
     const int32_t* ac = A.ac + 6 * (int64_t)(P.aff_class - 1);
-    for (int32_t j = ac[4], e = ac[4] + ac[5]; j < e; ++j) {
+    for (int32_t j = ac[4] + lane, e = ac[4] + ac[5]; j < e; j += stride) {
       const ksim_aff_carry k = A.carries[j];
       const int32_t d = ksim_dom(A, A.carry_key[k.term], w);
-      if (d >= 0) A.carried[A.carry_off[k.term] + d] += (int64_t)sign * k.amount;
+      if (d >= 0)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&A.carried[A.carry_off[k.term] + d]),
+                  (unsigned long long)((int64_t)sign * k.amount));
     }
   }
 }

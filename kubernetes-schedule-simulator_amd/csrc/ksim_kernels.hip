@@ -638,11 +638,16 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       }
       if (node < 0) atomicOr(c.err, 2);  // inconsistent partials: must never happen
       D.node = node;
-      if (node >= 0 && !c.no_commit) {
-        ksim_commit(c, P, node);
-        if (ksim_is_aff_pod(c, P)) ksim_aff_commit(*c.aff, P, node, 1);
-        if (ksim_is_vol_pod(c, P)) ksim_vol_commit(*c.vol, P, node, 1, c.err);
-        if (c.out_fit) c.out_fit[1] |= ksim_row_status(c, node);
+    }
+    __syncthreads();
+    // commit: the row and volumes in thread 0, the affinity counts across wave 1 meanwhile
+    if (D.node >= 0 && !c.no_commit) {
+      if (tid == 0) {
+        ksim_commit(c, P, D.node);
+        if (ksim_is_vol_pod(c, P)) ksim_vol_commit(*c.vol, P, D.node, 1, c.err);
+        if (c.out_fit) c.out_fit[1] |= ksim_row_status(c, D.node);
+      } else if (wv == 1 && ksim_is_aff_pod(c, P)) {
+        ksim_aff_commit(*c.aff, P, D.node, 1, lane, 64);
       }
     }
   }
