@@ -677,12 +677,13 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_
 
 // Commit one pod to one node (ksim_assume, ksim_pod_add); status |= ksim_row_status.
 __global__ void ksim_assume_kernel(KsimCtx c, int64_t pod, int64_t node, int32_t* status) {
-  if (threadIdx.x == 0 && blockIdx.x == 0) {
+  if (blockIdx.x != 0 || threadIdx.x >= 64) return;
+  if (threadIdx.x == 0) {
     ksim_commit(c, c.pods[pod], node);
-    if (ksim_is_aff_pod(c, c.pods[pod])) ksim_aff_commit(*c.aff, c.pods[pod], node, 1);
     if (ksim_is_vol_pod(c, c.pods[pod])) ksim_vol_commit(*c.vol, c.pods[pod], node, 1, c.err);
     *status |= ksim_row_status(c, node);
   }
+  if (ksim_is_aff_pod(c, c.pods[pod])) ksim_aff_commit(*c.aff, c.pods[pod], node, 1, threadIdx.x, 64);
 }
 
 // Launch-mode entry points used by the host runtime (ksim_runtime.cpp).
