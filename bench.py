@@ -38,14 +38,49 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
 def pmc_traffic(workload, evals_per_launch):
-    """HBM bytes per launch of the dominant kernel from the committed PMC profile
-    (profiles/pmc_<workload>.json: FETCH_SIZE x2 + WRITE_SIZE per node-eval, collected with
-    tools/gpu_pmc.sh / tools/gpu_c5.sh as MI355X_MICROARCH.md prescribes), or None."""
+    """HBM traffic of the dominant kernel from the PMC profile collected at this round's code
+    (profiles/r3/pmc_<workload>.json: FETCH_SIZE (x2, the gfx950 correction) + WRITE_SIZE per
+    dispatch in separate rocprofv3 --pmc passes of the bench command, tools/gpu_pmc.sh +
+    tools/pmc_summary.py, as MI355X_MICROARCH.md prescribes), scaled to this launch's node-evals;
+    None when no such profile exists.  Returns {"gb_per_launch", "bytes_per_node_eval", "source"}."""
+    path = os.path.join(ROOT, "profiles", "r3", "pmc_%s.json" % workload)
     try:
-        d = json.load(open(os.path.join(ROOT, "profiles", "pmc_%s.json" % workload)))
-        return round(d["hbm_bytes_per_node_eval"] * evals_per_launch / 1e9, 6)  # GB per launch
+        d = json.load(open(path))
+        per_eval = float(d["hbm_bytes_per_node_eval"])
     except (OSError, KeyError, ValueError):
         return None
+    return {"gb_per_launch": round(per_eval * evals_per_launch / 1e9, 6), "bytes_per_node_eval": round(per_eval, 4),
+            "source": os.path.relpath(path, ROOT), "profiled": d.get("profiled")}
+
+
+def roofline_bound(alg_bytes, traffic):
+    """"hbm" when the kernel moves about the algorithmic bytes through HBM; "latency" when the PMC
+    bytes per node-eval are far below them (the table is on chip: the per-pod exchange bounds it)."""
+    if traffic is None:
+        return "hbm"
+    return "latency" if traffic["bytes_per_node_eval"] < 0.1 * alg_bytes else "hbm"
+
+
+def effective_cpus():
+    """Host cores this process may use: the affinity mask, capped by a cgroup CPU quota and by the
+    box's thread budget (OMP_NUM_THREADS / MAX_JOBS, 16 on the GPU box)."""
+    n = len(os.sched_getaffinity(0))
+    for path in ("/sys/fs/cgroup/cpu.max", "/sys/fs/cgroup/cpu/cpu.cfs_quota_us"):
+        try:
+            f = open(path).read().split()
+            if path.endswith("cpu.max"):
+                if f[0] != "max":
+                    n = min(n, max(1, int(f[0]) // int(f[1])))
+            elif int(f[0]) > 0:
+                per = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+                n = min(n, max(1, int(f[0]) // per))
+        except (OSError, ValueError, IndexError):
+            pass
+    for k in ("OMP_NUM_THREADS", "MAX_JOBS"):
+        v = os.environ.get(k, "")
+        if v.isdigit() and int(v) > 0:
+            n = min(n, int(v))
+    return n
 
 
 def parse():
@@ -61,7 +96,9 @@ def parse():
     ap.add_argument("--no-tree", dest="tree", action="store_false",
                     help="skip the tree-mode line measured beside the scan (c3/c4)")
     ap.add_argument("--cpu-sample", type=int, default=30000,
-                    help="most pods in a CPU-baseline prefix (0 = skip); each leg is sized to ~10 s of CPU work")
+                    help="most pods in a CPU-baseline prefix (0 = skip); each leg is sized to ~8 s of CPU work")
+    ap.add_argument("--c4-pods", type=int, default=20000,
+                    help="c3 line: pods of the 1M-node C4 streaming side measurement (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c2x", "c4", "c5"],
                     help="c3: the headline metric (default); c2: 5k heterogeneous nodes with selectors, "
@@ -260,68 +297,94 @@ def tree_mode(a, cl, preds, prios, device, ref):
                     "node-evals/s metric is defined on the full scan, so this is reported beside it"}
 
 
-def cpu_baseline(a, cl, preds, prios, placements, unit="pods/s"):
-    """The C port of the Go path (oracle/cpu_ref.c, OpenMP node-parallel like
-    workqueue.Parallelize) on bounded prefixes of the same queue, at 1, 16 and all host threads;
-    parity = its placements equal the GPU's over the largest prefix."""
+def cpu_baseline(a, cl, preds, prios, placements, unit="pods/s", leg_s=8.0, full_parity=False):
+    """The C port of the Go path (oracle/cpu_ref.c: one OpenMP team per call splitting every pod's
+    node loop, like workqueue.Parallelize(16)) over the same tables the device loads
+    (scheduler.plan: class tables, affinity / spread / volume tables), on prefixes of the same
+    queue at 1 and 16 threads (and every usable core when the box has more than 16), each leg
+    sized to ~leg_s seconds from a short calibration run; parity = its placements equal the GPU's
+    over every prefix.  full_parity: also run the whole queue at 16 threads when that fits ~30 s."""
     import numpy as np
     from ksim import scheduler
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import cpu_ref
     n = cl.n_nodes
-    cfg = scheduler.make_config(preds, prios)
-    avail = len(os.sched_getaffinity(0))
-    legs = []
-    # node-eval budgets: ~10 s per leg at the measured C3 rates (1 thread ~0.09e9, 16 threads
-    # ~0.28e9 node-evals/s); the all-cores leg oversubscribes the box's CPU share, so it gets less
-    for t, budget in ((1, 9e8), (min(a.cpu_threads, avail), 2.8e9), (min(avail, 64), 3e8)):
-        if any(t == x[0] for x in legs):
-            continue
-        S = int(min(a.cpu_sample, len(placements), max(20, budget // n)))
+    plan = scheduler.plan(cl, preds, prios)
+    cores = effective_cpus()
+    total = len(placements)
+
+    def run(S, t):
         t1 = time.perf_counter()
-        ref, _, _, _ = cpu_ref.run(cl, cfg, 0, S, threads=t)
-        s = time.perf_counter() - t1
-        legs.append((t, S, s, bool(np.array_equal(ref, placements[:S]))))
-    main = max(legs, key=lambda x: (x[0] == min(a.cpu_threads, avail), x[1]))
+        ref = cpu_ref.run(cl, None, 0, S, threads=t, plan=plan)[0]
+        return time.perf_counter() - t1, bool(np.array_equal(ref, placements[:S]))
+
+    legs = []
+    for t in sorted({1, min(a.cpu_threads, cores), cores}):
+        S0 = int(min(total, a.cpu_sample, max(8, 4e7 // n)))  # calibration: ~40M node-evals
+        s0, ok0 = run(S0, t)
+        S = int(min(total, a.cpu_sample, max(S0, S0 * leg_s / max(s0, 1e-3))))
+        s, ok = run(S, t) if S > S0 else (s0, ok0)
+        legs.append((t, S, s, ok and ok0))
+    main = max(legs, key=lambda x: (x[0] == min(a.cpu_threads, cores), x[1]))
     t, S, s, match = main
     cpu = {"value": round(S / s, 1), "unit": unit, "cores": t, "kind": "port",
-           "sample": "first %d pods of the same %s queue on the same %d-node cluster (oracle/cpu_ref.c, "
-                     "OpenMP node-parallel like workqueue.Parallelize), %.2f s" % (S, a.workload.upper(), n, s),
+           "sample": "first %d pods of the same %s queue on the same %d-node cluster (oracle/cpu_ref.c over the "
+                     "tables the device loads, one OpenMP team per call like workqueue.Parallelize), %.2f s"
+                     % (S, a.workload.upper(), n, s),
            "node_evals_per_s": round(S * n / s, 1),
            "by_threads": [{"cores": x[0], "pods": x[1], "seconds": round(x[2], 3), "value": round(x[1] / x[2], 1)}
                           for x in legs],
-           "host_cpus_visible": avail}
+           "host_cpus_visible": len(os.sched_getaffinity(0)), "host_cpus_usable": cores}
     parity = {"prefix_pods": max(x[1] for x in legs), "match": all(x[3] for x in legs)}
+    if full_parity and parity["prefix_pods"] < total:
+        t16 = min(a.cpu_threads, cores)
+        rate = max(x[1] / x[2] for x in legs if x[0] == t16)
+        if total / rate <= 30.0:
+            s, ok = run(total, t16)
+            parity = {"prefix_pods": total, "match": ok and parity["match"], "full_queue": True,
+                      "seconds": round(s, 2), "cores": t16}
     return cpu, parity
 
 
-def cpu_baseline_objects(a, objs, preds, prios, placements, cl, budget_s=10.0):
-    """C2x: the C port does not restate volumes / spread / affinity, so the CPU leg is the object
-    oracle (oracle/ksim_ref.py, one thread, pure Python) on a prefix sized to ~budget_s; parity =
-    its placements equal the GPU's over that prefix."""
+def c4_stream_side(a):
+    """BASELINE configs[3]'s node count on ONE GPU (1,000,000 nodes: 60 MB of table, beyond the
+    per-CU LDS budget, so the fast kernel streams the rows from HBM): --c4-pods pods of the C4
+    distributions, timed like the headline (warmup on a separate copy), with its own HBM roofline,
+    PMC traffic and a parity prefix against the C port (16 threads)."""
     import numpy as np
+    from ksim import abi, scheduler, synth
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import ksim_ref as R
-    listers = R.VolumeListers(objs["pvs"], objs["pvcs"])
-    custom = {k: v for k, v in R.volume_predicates(listers).items() if k in preds}
-    queue = objs["pods"]                            # scheduling order (the cluster's queue)
-    S, s = 8, 0.0
-    while True:
-        t1 = time.perf_counter()
-        want, _ = R.simulate(objs["nodes"], [], list(reversed(queue[:S])), set(preds), list(prios), custom,
-                             spread=R.SpreadListers(services=objs["services"]))
-        s = time.perf_counter() - t1
-        if s >= budget_s / 4 or S >= min(a.cpu_sample, len(placements)):
-            break
-        S = min(int(S * max(2.0, budget_s / max(s, 1e-3))), min(a.cpu_sample, len(placements)))
-    idx = {nm: i for i, nm in enumerate(cl.names)}
-    ref = np.array([idx[h] if h is not None else -1 for _, h, _ in want], np.int32)
-    cpu = {"value": round(S / s, 2), "unit": "pods/s", "cores": 1, "kind": "port",
-           "sample": "first %d pods of the same C2x queue on the same %d-node cluster (oracle/ksim_ref.py, the "
-                     "object-level restatement in pure Python: the C port does not cover volumes / spread / "
-                     "affinity), %.2f s" % (S, cl.n_nodes, s),
-           "node_evals_per_s": round(S * cl.n_nodes / s, 1)}
-    return cpu, {"prefix_pods": S, "match": bool(np.array_equal(ref, placements[:S]))}
+    import cpu_ref
+    n, P = 1_000_000, a.c4_pods
+    cl, preds, prios = synth.config_c4(n, P)
+    steps = 10
+    batch = -(-P // steps)
+    a4 = argparse.Namespace(**vars(a))
+    a4.warmup = 1
+    make = lambda: scheduler.GenericScheduler(cl, preds, prios, device=0, collect_reasons=False)
+    g, out, el, kms, launches, st, pods = timed_queue(a4, Local, make, steps, batch, P)
+    g.close()
+    avg = kms / 1e3 / max(launches, 1)
+    achieved = 60 * n * batch / avg / 1e9
+    traffic = pmc_traffic("c4", n * batch)
+    S = min(P, 1500)
+    t1 = time.perf_counter()
+    ref = cpu_ref.run(cl, scheduler.make_config(preds, prios), 0, S, threads=min(a.cpu_threads, effective_cpus()))[0]
+    cs = time.perf_counter() - t1
+    return {"value": round(pods / el, 1), "unit": "pods/s", "node_evals_per_s": round(pods * n / el, 1),
+            "config": "C4 node count on one GPU: %d nodes, %d pods of the C4 distributions, default predicates + "
+                      "LeastRequested(1) + BalancedResourceAllocation(1), %d steps of %d pods" % (n, P, steps, batch),
+            "mode": {1: "launch", 2: "persistent", 3: "tree"}.get(st.mode, str(st.mode)),
+            "form": "streaming (rows from HBM)" if st.mode == abi.MODE_PERSISTENT else "other",
+            "ms_per_step": round(el * 1e3 / steps, 4),
+            "roofline": {"bound": roofline_bound(60, traffic), "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic and traffic["gb_per_launch"], "traffic_unit": "GB per launch (PMC)",
+                         "traffic_source": traffic and traffic["source"], "bytes_per_node_eval": 60,
+                         "avg_launch_us": round(avg * 1e6, 3), "pods_per_launch": batch},
+            "cpu_baseline": {"value": round(S / cs, 1), "unit": "pods/s", "cores": min(a.cpu_threads, effective_cpus()),
+                             "kind": "port", "sample": "first %d pods, oracle/cpu_ref.c, %.2f s" % (S, cs)},
+            "parity": {"prefix_pods": S, "match": bool(np.array_equal(ref, out[:S]))}}
 
 
 def main():
@@ -387,12 +450,12 @@ def main():
     tree = None
     if rank == 0 and a.tree and a.mode != "tree" and a.workload in ("c3", "c4") and single is not None:
         tree = tree_mode(a, cl, preds, prios, local, single["out"])
+    c4 = None
+    if world == 1 and a.workload == "c3" and a.c4_pods > 0 and a.mode == "auto":
+        c4 = c4_stream_side(a)
     cpu = parity = None
     if rank == 0 and a.cpu_sample > 0 and single is not None:
-        if a.workload == "c2x":
-            cpu, parity = cpu_baseline_objects(a, objs, preds, prios, single["out"], cl)
-        else:
-            cpu, parity = cpu_baseline(a, cl, preds, prios, single["out"])
+        cpu, parity = cpu_baseline(a, cl, preds, prios, single["out"], full_parity=a.workload in ("c2", "c2x"))
 
     if rank == 0:
         if "error" in head:
@@ -417,6 +480,9 @@ def main():
         achieved = W["bytes"] * n_local * min(pods_per_launch, pods_timed) / avg_launch_s / 1e9
         tree_kernel = mode_used == abi.MODE_TREE
         bound = int((head.get("merged", head["out"]) >= 0).sum())
+        traffic = None if (tree_kernel or world > 1) else \
+            pmc_traffic(a.workload + ("" if mode_used == abi.MODE_PERSISTENT else "_launch"),
+                        n * min(pods_per_launch, pods_timed))
         line = {
             "metric": ("pods scheduled/sec + node-evals/sec at 100k nodes, 1/2/4/8 MI355X" if a.workload == "c3" else
                        "pods scheduled/sec + node-evals/sec, %s (%d nodes)" % (a.workload.upper(), n)),
@@ -441,22 +507,29 @@ def main():
                        "blocks": head["blocks"],
                        "parallelism": ("node-sharded x%d" % world if sharded_head else
                                        "scenario-replicas x%d" % world if world > 1 else "single-gpu")},
-            "roofline": {"bound": "hbm", "achieved": None if tree_kernel else round(achieved, 1), "peak": HBM_PEAK_GBS,
+            "roofline": {"bound": "latency" if tree_kernel else roofline_bound(W["bytes"], traffic),
+                         "achieved": None if tree_kernel else round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": None if tree_kernel else round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None if (tree_kernel or world > 1) else
-                         pmc_traffic(a.workload + ("" if mode_used == abi.MODE_PERSISTENT else "_launch"),
-                                     n * pods_per_launch),
-                         "traffic_unit": "GB per launch (PMC)", "bytes_per_node_eval": W["bytes"],
+                         "traffic": traffic and traffic["gb_per_launch"],
+                         "traffic_unit": "GB per launch (PMC)",
+                         "traffic_bytes_per_node_eval": traffic and traffic["bytes_per_node_eval"],
+                         "traffic_source": traffic and traffic["source"],
+                         "bytes_per_node_eval": W["bytes"],
                          "nodes_per_gpu": n_local,
                          "avg_launch_us": round(avg_launch_s * 1e6, 3), "pods_per_launch": pods_per_launch,
                          **({"note": "tree mode reads O(classes x log N) bytes per pod, not the table: no HBM "
-                                     "roofline applies"} if tree_kernel else {})},
+                                     "roofline applies"} if tree_kernel else
+                            {"note": "achieved = algorithmic bytes / launch time; the PMC traffic shows the table "
+                                     "stays on chip (LDS), so the per-pod cross-CU exchange, not HBM, bounds it"}
+                            if roofline_bound(W["bytes"], traffic) == "latency" else {})},
             "cpu_baseline": cpu,
             "parity": parity,
             "pods_bound": bound,
         }
         if tree is not None:
             line["tree_mode"] = tree
+        if c4 is not None:
+            line["c4_stream"] = c4
         if sharded is not None:
             ns = {"ranks": world, "nodes_per_rank": n_local, "scaling": "strong",
                   "exchange": "device-initiated system-scope stores into every rank's fine-grained exchange buffer "
@@ -515,7 +588,7 @@ def main_c5(a):
     if rank == 0 and a.cpu_sample > 0:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import cpu_ref
-        threads = max(1, min(a.cpu_threads, len(os.sched_getaffinity(0))))
+        threads = max(1, min(a.cpu_threads, effective_cpus()))
         S = min(a.cpu_sample, a.sweep_pods)
         t1 = time.perf_counter()
         ref, _, _, _ = cpu_ref.run(cl, scheduler.make_config(preds, mine[0]), 0, S, threads=threads)
@@ -544,10 +617,10 @@ def main_c5(a):
                        "nodes": n, "scenarios": len(scen), "scenarios_per_rank": len(mine),
                        "pods_per_scenario": a.sweep_pods, "parallelism": "scenario-parallel x%d" % world,
                        "form": "tree (one tree-mode wave per scenario)" if tree else "scan (one workgroup per scenario)"},
-            "roofline": {"bound": "hbm", "achieved": None if tree else round(achieved, 1), "peak": HBM_PEAK_GBS,
-                         "unit": "GB/s",
+            "roofline": {"bound": "latency" if tree else "hbm", "achieved": None if tree else round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": None if tree else round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": None if tree else pmc_traffic("c5", evals_per_launch),
+                         "traffic": None if tree else (pmc_traffic("c5", evals_per_launch) or {}).get("gb_per_launch"),
                          "traffic_unit": "GB per launch (PMC)",
                          "bytes_per_node_eval": BYTES_PER_NODE_EVAL, "avg_launch_us": round(avg_launch_s * 1e6, 3),
                          "node_evals_per_launch": evals_per_launch,

@@ -152,6 +152,7 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
   h->aff_bufs.clear();
   for (size_t k = nb0; k < h->bufs.size(); ++k) h->aff_bufs.push_back(h->bufs[k].p);
   h->aff_dev = dev;
+  h->aff_h = A;
   h->ctx.aff = dev;
   h->aff_n_ident = t->n_ident;
   h->aff_n_aclass = t->n_aclass;

@@ -124,6 +124,7 @@ struct KsimCtx {
   int32_t lwords, twords, n_label_sets, n_taint_sets;
   int32_t n_classes_dev;  // pod classes in the tables
   int32_t fuse_a;         // launch form: pass A fused into the scan (grid barrier; co-resident grid)
+  uint64_t barrier_ticks; // fused pass A: bound of the grid-barrier wait (s_memrealtime ticks, 100 MHz)
   // ---- pod queue ----
   const ksim_pod* __restrict__ pods;
   const uint64_t* __restrict__ pod_ports;

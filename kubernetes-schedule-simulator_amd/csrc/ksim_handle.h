@@ -150,6 +150,8 @@ struct ksim_handle {
   bool aff_stale = false;       // a node event changed the table the domains describe
   int32_t aff_n_ident = 0, aff_n_aclass = 0;
   KsimAff* aff_dev = nullptr;
+  KsimAff aff_h{};              // host copy of the device descriptor (pass-A scratch pointers)
+  bool fuse_off = false;        // a fused pass-A barrier timed out once: pass A as its own launch
   std::vector<void*> aff_bufs;
   std::vector<int32_t> q_ident, q_aclass;
   std::vector<int64_t> aff_pre;  // aff_pre[i] = affinity pods among the first i queued

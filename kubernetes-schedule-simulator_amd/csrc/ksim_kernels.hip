@@ -161,6 +161,9 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t
     for (int z = tid; z < A.n_zone; z += KSIM_BLOCK)
       if (s_z[z]) atomicAdd(reinterpret_cast<unsigned long long*>(&A.zsum[z]), s_z[z]);
   }
+  // every wave's zone atomics have landed before the barrier that precedes this block's ticket
+  // (thread 0's release fence covers its own wave only)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   auto combine = [&]() {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -287,6 +290,13 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   static_assert(NPT <= KSIM_PM_NPT, "candidate masks hold KSIM_PM_NPT node slots per thread");
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (c.fuse_a) {
+    // a fused barrier that timed out (err bit 64) left this run's tickets mid-pod: every later
+    // launch of the graph exits at once (uniformly per block) and the host resumes unfused
+    if (tid == 0) s_bail = (int)__hip_atomic_load(c.ticket + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (s_bail) return;
+  }
   const int64_t pod = *c.cursor;
   if (pod >= c.end) return;  // uniform: graph replay past the end of the queue
   const ksim_pod P = c.pods[pod];
@@ -349,8 +359,9 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         while (__hip_atomic_load(c.ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == s_gen) {
           __builtin_amdgcn_s_sleep(1);
-          if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {  // 2 s: blocks not co-resident
-            atomicOr(c.err, 8);
+          if (__builtin_amdgcn_s_memrealtime() - t0 > c.barrier_ticks) {  // 2 s: blocks not co-resident
+            atomicOr(c.err, 64);
+            __hip_atomic_store(c.ticket + 2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_bail = 1;
             break;
           }

@@ -69,6 +69,9 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
     return ksim_fail(nullptr, KSIM_E_DEVICE, "ksim_create: initial copies failed");
   }
   if (const char* g = getenv("KSIM_MAX_GRID")) h->max_grid = atoi(g);
+  // fused pass A's grid-barrier bound: 2 s (KSIM_BARRIER_TICKS, 100 MHz ticks: tests force the bail path)
+  c.barrier_ticks = 200000000ull;
+  if (const char* b = getenv("KSIM_BARRIER_TICKS")) c.barrier_ticks = strtoull(b, nullptr, 10);
   *out = h;
   return KSIM_OK;
 }
@@ -482,7 +485,7 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
                   (c.w[KSIM_W_INTERPOD_AFFINITY] != 0 || c.w[KSIM_W_SELECTOR_SPREAD] != 0) && !c.no_prio ? 1 : 0;
   // pass A fused into the scan behind a grid barrier when the grid is co-resident (KSIM_FUSE_A=0: two launches)
   const char* fz = getenv("KSIM_FUSE_A");
-  c.fuse_a = ipa && !(fz && fz[0] == '0') && ksim_scan_coresident(npt, c.collect, grid) ? 1 : 0;
+  c.fuse_a = ipa && !h->fuse_off && !(fz && fz[0] == '0') && ksim_scan_coresident(npt, c.collect, grid) ? 1 : 0;
   const int gkey = ipa | c.fuse_a << 1;
   if (!h->gexec || h->g_batch != batch || h->g_npt != npt || h->g_collect != c.collect || h->g_first != first ||
       h->g_end != c.end || h->g_ipa != gkey) {
@@ -517,6 +520,33 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
     st->kernel_launches = reps * batch;
     st->mode = KSIM_MODE_LAUNCH;
     st->blocks = grid;
+  }
+  if (c.fuse_a) {
+    int32_t err = 0;
+    HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
+    if (err & 64) {
+      // the fused pass-A barrier timed out (blocks not co-resident after all, e.g. another handle's
+      // kernels on the device): the pod at the cursor was not committed, later launches exited at
+      // once.  Re-arm the tickets and pass-A scratch, and finish the range with pass A as its own launch.
+      int64_t cur = 0;
+      HIPCHK(h, hipMemcpy(&cur, c.cursor, 8, hipMemcpyDeviceToHost));
+      err &= ~64;
+      HIPCHK(h, hipMemcpy(c.err, &err, 4, hipMemcpyHostToDevice));
+      HIPCHK(h, hipMemset(c.ticket, 0, 16));
+      HIPCHK(h, hipMemset(h->aff_h.ticket, 0, 16));
+      if (h->aff_h.n_zone) HIPCHK(h, hipMemset(h->aff_h.zsum, 0, (size_t)h->aff_h.n_zone * 8));
+      h->fuse_off = true;
+      if (cur < first + count) {
+        ksim_stats s2{};
+        const int rc2 = run_launch_mode(h, cur, first + count - cur, &s2);
+        if (rc2) return rc2;
+        if (st) {
+          st->device_ms += s2.device_ms;
+          st->kernel_ms += s2.kernel_ms;
+          st->kernel_launches += s2.kernel_launches;
+        }
+      }
+    }
   }
   return KSIM_OK;
 }
@@ -779,6 +809,11 @@ static int run_tree_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stat
       ksim_stats s2{};
       if ((rc = run_auto_mode(h, i, j - i, &s2))) return rc;
       add_stats(st, s2);
+      // a failure of that segment (overflow, inconsistency) ends the call here: ksim_schedule reports
+      // it before any later segment could read or clear the error word
+      int32_t err = 0;
+      HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
+      if (err) return KSIM_OK;
       i = j;
       continue;
     }

@@ -275,6 +275,84 @@ def label_presence_flags(label_sets, label_set_ids, label_presence):
     return np.where(bad[np.asarray(label_set_ids)], abi.N_LABEL_PRESENCE, 0).astype(np.uint32)
 
 
+@dataclass
+class Plan:
+    """What a scheduler over `cluster` loads, derived on the host alone (no device): the config,
+    the node flags, the class tables with their NodePreferAvoidPods addends, the pod queue as
+    loaded (affinity / volume / service-affinity fields adjusted to the configured keys), and the
+    affinity / volume tables when a configured key reads them (else None)."""
+    cfg: object
+    flags: object          # node flags with the CheckNodeLabelPresence verdicts, or None (the cluster's)
+    tables: dict
+    na_add: object
+    const_score: int
+    pods: object
+    affinity: object
+    volumes: object
+    use_zone: bool
+
+
+def plan(cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO, collect_reasons=True,
+         last_node_index=0, label_presence=None, custom_priorities=None, service_affinity=None) -> Plan:
+    """The host half of GenericScheduler's construction (also what the table-level C oracle runs
+    on): validates the key sets against the cluster's inputs (Unsupported where the reference errs
+    or where this restatement stops) and builds every table the library loads."""
+    predicates = list(predicates)
+    prioritizers = list(priorities)
+    custom_priorities = dict(custom_priorities or {})
+    if any(s[0] == "serviceAntiAffinity" for s in custom_priorities.values()) and getattr(cluster, "spread_active", False):
+        raise Unsupported("a serviceAntiAffinity priority with services selecting the pods")
+    if any(n == "NodeAffinityPriority" for n, _ in prioritizers) and cluster.bad_affinity_classes:
+        raise Unsupported("NodeAffinityPriority: a preferred node-affinity term does not parse")
+    if any(n == "ImageLocalityPriority" for n, _ in prioritizers) and cluster.node_images:
+        raise Unsupported("ImageLocalityPriority with nodes that list status.images")
+    if "CheckNodeLabelPresence" in predicates and label_presence is None:
+        raise Unsupported("CheckNodeLabelPresence needs its labelsPresence argument")
+    if "CheckServiceAffinity" in predicates:
+        if service_affinity is None:
+            raise Unsupported("CheckServiceAffinity needs its serviceAffinity argument")
+        if getattr(cluster, "spread_active", False):
+            raise Unsupported("CheckServiceAffinity with services selecting the pods (the pod lister's order decides)")
+    cfg = make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence],
+                      [(n, w) for n, w in prioritizers if n not in custom_priorities],
+                      device, mode, collect_reasons, last_node_index,
+                      spread=bool(getattr(cluster, "spread_active", False)))
+    check_volume_support(cluster, predicates)
+    flags = None
+    if label_presence is not None and "CheckNodeLabelPresence" in predicates:
+        fl = cluster.cols["flags"] | label_presence_flags(cluster.label_sets.items, cluster.cols["label_set"],
+                                                            label_presence)
+        flags = np.ascontiguousarray(fl, np.uint32)
+    tables, na_add = class_tables_for(cluster.tables, prioritizers, cluster.label_sets.items, custom_priorities)
+    # const_score without NodePreferAvoidPods when its per-class addends carry it
+    const_score = cfg.const_score - (10 * sum(int(x) for n, x in prioritizers if n == "NodePreferAvoidPodsPriority")
+                                     if tables.get("pa_in_add") else 0)
+    pods = np.ascontiguousarray(cluster.pods)
+    if "CheckServiceAffinity" in predicates:
+        ok, need = service_affinity_table(cluster.classes.items or [{}], cluster.label_sets.items, service_affinity)
+        tables = dict(tables, svc_ok=ok)
+        if len(pods):
+            pods = pods.copy()
+            pods["flags"] |= np.where(need[pods["cls"]], abi.POD_NEED_SVC_AFFINITY, 0).astype(np.uint32)
+    affinity = None
+    if cluster.affinity is not None:
+        if cfg.predicates & abi.P_INTERPOD_AFFINITY or ((cfg.weights[abi.W_INTERPOD] or cfg.weights[abi.W_SPREAD])
+                                                        and not cfg.no_priorities):
+            affinity = cluster.affinity
+        elif len(pods):  # neither MatchInterPodAffinity nor its priority: the terms change nothing
+            pods = pods.copy()
+            pods["aff_ident"] = 0
+            pods["aff_class"] = 0
+    volumes = None
+    if cluster.volumes is not None:
+        if cfg.predicates & VOLUME_PREDICATE_BITS:
+            volumes = cluster.volumes
+        elif len(pods):  # no volume predicate: the pods' volumes change nothing
+            pods = pods.copy()
+            pods["vol_class"] = 0
+    return Plan(cfg, flags, tables, na_add, const_score, pods, affinity, volumes, "NoVolumeZoneConflict" in predicates)
+
+
 class GenericScheduler:
     """Batch drop-in for genericScheduler + Scheduler.assume on one MI355X.  label_presence:
     (labels, presence) of a Policy's CheckNodeLabelPresence predicate (policy.key_sets)."""
@@ -287,79 +365,29 @@ class GenericScheduler:
         self.prioritizers = list(priorities)
         # Policy priorities registered with a labelPreference / serviceAntiAffinity argument, by name
         self.custom_priorities = dict(custom_priorities or {})
-        if any(s[0] == "serviceAntiAffinity" for s in self.custom_priorities.values()) and \
-                getattr(cluster, "spread_active", False):
-            raise Unsupported("a serviceAntiAffinity priority with services selecting the pods")
-        if any(n == "NodeAffinityPriority" for n, _ in self.prioritizers) and cluster.bad_affinity_classes:
-            raise Unsupported("NodeAffinityPriority: a preferred node-affinity term does not parse")
-        if any(n == "ImageLocalityPriority" for n, _ in self.prioritizers) and cluster.node_images:
-            raise Unsupported("ImageLocalityPriority with nodes that list status.images")
-        if "CheckNodeLabelPresence" in self.predicates and label_presence is None:
-            raise Unsupported("CheckNodeLabelPresence needs its labelsPresence argument")
-        if "CheckServiceAffinity" in self.predicates:
-            if service_affinity is None:
-                raise Unsupported("CheckServiceAffinity needs its serviceAffinity argument")
-            if getattr(cluster, "spread_active", False):
-                raise Unsupported("CheckServiceAffinity with services selecting the pods (the pod lister's order decides)")
-        self.cfg = make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence],
-                               [(n, w) for n, w in priorities if n not in self.custom_priorities],
-                               device, mode, collect_reasons, last_node_index,
-                               spread=bool(getattr(cluster, "spread_active", False)))
-        check_volume_support(cluster, self.predicates)
+        p = self.plan = plan(cluster, predicates, priorities, device, mode, collect_reasons, last_node_index,
+                             label_presence, custom_priorities, service_affinity)
+        self.cfg = p.cfg
         self.h = abi.Handle(self.cfg)
         table = cluster.node_table()
-        if label_presence is not None and "CheckNodeLabelPresence" in self.predicates:
-            fl = cluster.cols["flags"] | label_presence_flags(cluster.label_sets.items, cluster.cols["label_set"],
-                                                                label_presence)
-            self._flags = np.ascontiguousarray(fl, np.uint32)
+        if p.flags is not None:
+            self._flags = p.flags
             table.flags = abi.ptr(self._flags, C.c_uint32)
         self.h.call("ksim_load_nodes", C.byref(table))
-        self.tables, self.na_add = class_tables_for(cluster.tables, self.prioritizers, cluster.label_sets.items,
-                                                    self.custom_priorities)
-        # const_score without NodePreferAvoidPods when its per-class addends carry it
-        self.const_score = self.cfg.const_score - (10 * sum(int(x) for n, x in self.prioritizers
-                                                            if n == "NodePreferAvoidPodsPriority")
-                                                   if self.tables.get("pa_in_add") else 0)
-        pods = np.ascontiguousarray(cluster.pods)
-        if "CheckServiceAffinity" in self.predicates:
-            ok, need = service_affinity_table(cluster.classes.items or [{}],
-                                              cluster.label_sets.items, service_affinity)
-            self.tables = dict(self.tables, svc_ok=ok)
-            if len(pods):
-                pods = pods.copy()
-                pods["flags"] |= np.where(need[pods["cls"]], abi.POD_NEED_SVC_AFFINITY, 0).astype(np.uint32)
+        self.tables, self.na_add, self.const_score = p.tables, p.na_add, p.const_score
         self.h.call("ksim_load_classes", C.byref(class_tables_struct(self.tables, self.na_add)))
-        self.affinity = None
-        if cluster.affinity is not None:
-            if self.cfg.predicates & abi.P_INTERPOD_AFFINITY or ((self.cfg.weights[abi.W_INTERPOD] or
-                                                                  self.cfg.weights[abi.W_SPREAD]) and not self.cfg.no_priorities):
-                from .affinity import tables_struct
-                self.affinity = cluster.affinity
-                self.h.call("ksim_load_affinity", C.byref(tables_struct(self.affinity)))
-            elif len(pods):  # neither MatchInterPodAffinity nor its priority: the terms change nothing
-                pods = pods.copy()
-                pods["aff_ident"] = 0
-                pods["aff_class"] = 0
-        self.volumes = None
-        if cluster.volumes is not None:
-            pods = self._load_volumes(cluster, pods)
-        self._pods = pods
+        self.affinity = p.affinity
+        if self.affinity is not None:
+            from .affinity import tables_struct
+            self.h.call("ksim_load_affinity", C.byref(tables_struct(self.affinity)))
+        self.volumes = p.volumes
+        if self.volumes is not None:
+            from .volumes import tables_struct as vol_struct
+            self.h.call("ksim_load_volumes", C.byref(vol_struct(self.volumes, p.use_zone)))
+        pods = self._pods = p.pods
         self.h.call("ksim_load_pods", abi.vptr(pods), len(pods), abi.vptr(cluster.pod_ports), len(cluster.pod_ports),
                     abi.vptr(cluster.pod_scalars), len(cluster.pod_scalars))
         self.last_stats = None
-
-    def _load_volumes(self, cluster, pods):
-        """Load the volume tables when a volume predicate is configured (else the pods' volumes change
-        nothing: their classes are cleared)."""
-        if not (self.cfg.predicates & VOLUME_PREDICATE_BITS):
-            if len(pods):
-                pods = pods.copy()
-                pods["vol_class"] = 0
-            return pods
-        from .volumes import tables_struct
-        self.volumes = cluster.volumes
-        self.h.call("ksim_load_volumes", C.byref(tables_struct(self.volumes, "NoVolumeZoneConflict" in self.predicates)))
-        return pods
 
     def volume_state(self):
         """The device's volume slots ([vol_slots][n]) and per-node slot counts."""

@@ -62,6 +62,18 @@ def test_affinity_two_launch_form_matches_oracle(seed, policy, monkeypatch):
     _check(nodes, running, pods, preds, prios, abi.MODE_LAUNCH)
 
 
+@pytest.mark.parametrize("policy", ["default", "ipa_heavy"])
+def test_fused_barrier_timeout_recovers(policy, monkeypatch):
+    """The fused pass-A grid barrier bailing out (KSIM_BARRIER_TICKS=0: every block that has to wait
+    gives up at once, as when the grid is not co-resident after all): the launch at the cursor
+    commits nothing, the rest of the graph exits at its entry check, and the runtime re-arms the
+    tickets and finishes with pass A as its own launch — placements still identical to the oracle."""
+    monkeypatch.setenv("KSIM_BARRIER_TICKS", "0")
+    preds, prios = POLICIES[policy]
+    nodes, running, pods = rnd_affinity_workload(4, n_nodes=600, n_pods=60, n_running=12, p_aff=0.6)
+    _check(nodes, running, pods, preds, prios, abi.MODE_LAUNCH)
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_mixed_affinity_and_resource_only_pods(seed):
     """Mostly term-free pods (tree / fast kernels) interleaved with affinity pods (launch kernels):

@@ -1,0 +1,126 @@
+"""The table-level C oracle (oracle/cpu_ref.c, ksim_ref_run_ex) over the inter-pod affinity,
+SelectorSpread and volume tables, pinned to the object-level oracle (oracle/ksim_ref.py, itself
+pinned by the reference's golden vectors: test_oracle_interpod.py, test_oracle_golden.py).  Both are
+driven from the same Kubernetes-shaped objects — the C oracle through the product's ingest
+(ksim/affinity.py, ksim/volumes.py, ksim/spread.py) and scheduler.plan, the object oracle straight
+from the objects — so that GPU parity at C2x scale can use the C oracle without trusting the
+ingest.  Placements, bind order, FitError texts and lastNodeIndex must be identical.  CPU only."""
+import numpy as np
+import pytest
+
+import cpu_ref
+import ksim_ref as R
+from ksim import ingest, scheduler, spread as ksp, synth
+from workloads import (rnd_affinity_workload, rnd_mixed_workload, rnd_spread_workload, rnd_volume_workload)
+
+AFF_POLICIES = {
+    "default": scheduler.provider("DefaultProvider"),
+    "ipa_heavy": (list(scheduler.DEFAULT_PREDICATES), [("InterPodAffinityPriority", 7), ("LeastRequestedPriority", 1),
+                                                       ("TaintTolerationPriority", 2)]),
+    "predicate_only": (["MatchInterPodAffinity", "GeneralPredicates"], [("MostRequestedPriority", 1)]),
+}
+
+
+def c_oracle_objects(nodes, running, pods, preds, prios, pvs=(), pvcs=(), spread=None, threads=4,
+                     spread_services_only=False):
+    """The simulator's loop on the C oracle over the tables scheduler.plan builds: pods popped
+    LIFO (store.go:223-233).  Returns ([(pod, node or None, FitError text or None)], lastNodeIndex)."""
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order, pvs=pvs, pvcs=pvcs, spread=spread,
+                                     spread_services_only=spread_services_only)
+    p = scheduler.plan(cl, preds, prios)
+    out, reasons, _, ctr, _ = cpu_ref.run(cl, None, threads=threads, plan=p)
+    res = []
+    for k, w in enumerate(out):
+        if w >= 0:
+            res.append((cl.pod_names[k], cl.names[w], None))
+        else:
+            res.append((cl.pod_names[k], None, scheduler.fit_error_message(cl.n_nodes, reasons[k], cl.scalar_names.items)))
+    return res, ctr
+
+
+def _same(want, got):
+    assert len(got) == len(want)
+    bad = [(w, g) for w, g in zip(want, got) if w != g]
+    assert not bad, bad[:3]
+
+
+@pytest.mark.parametrize("policy", sorted(AFF_POLICIES))
+@pytest.mark.parametrize("seed", range(4))
+def test_affinity_matches_object_oracle(seed, policy):
+    preds, prios = AFF_POLICIES[policy]
+    nodes, running, pods = rnd_affinity_workload(seed, n_nodes=18 + 7 * seed, n_pods=90, n_running=12)
+    want, lni = R.simulate(nodes, running, pods, set(preds), list(prios))
+    got, ctr = c_oracle_objects(nodes, running, pods, preds, prios)
+    _same(want, got)
+    assert ctr == lni
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_volumes_match_object_oracle(seed, monkeypatch):
+    monkeypatch.setenv("KUBE_MAX_PD_VOLS", "3")
+    nodes, running, pods, pvs, pvcs = rnd_volume_workload(seed, zones=seed % 2 == 1, resolvable_only=seed % 2 == 1)
+    preds = ["GeneralPredicates", "NoDiskConflict", "MaxEBSVolumeCount", "MaxGCEPDVolumeCount",
+             "MaxAzureDiskVolumeCount"] + (["NoVolumeZoneConflict"] if seed % 2 else [])
+    prios = [("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
+    custom = {k: v for k, v in R.volume_predicates(R.VolumeListers(pvs, pvcs), 3).items() if k in preds}
+    want, lni = R.simulate(nodes, running, pods, set(preds), list(prios), custom)
+    got, ctr = c_oracle_objects(nodes, running, pods, preds, prios, pvs=pvs, pvcs=pvcs)
+    _same(want, got)
+    assert ctr == lni
+    assert any(m and ("disk" in m or "volume" in m) for _, _, m in want)   # the volume predicates decided something
+
+
+@pytest.mark.parametrize("policy", ["default", "service"])
+@pytest.mark.parametrize("seed", range(4))
+def test_spread_matches_object_oracle(seed, policy):
+    nodes, running, pods, objs = rnd_spread_workload(seed, zones=seed != 3)
+    preds, prios = scheduler.provider("DefaultProvider")
+    if policy == "service":
+        prios = [("ServiceSpreadingPriority", 2), ("LeastRequestedPriority", 1)]
+    want, lni = R.simulate(nodes, running, pods, set(preds), list(prios), spread=R.SpreadListers(**objs))
+    got, ctr = c_oracle_objects(nodes, running, pods, preds, prios, spread=ksp.SpreadListers(**objs),
+                                spread_services_only=policy == "service")
+    _same(want, got)
+    assert ctr == lni
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_mixed_features_match_object_oracle(seed, monkeypatch):
+    monkeypatch.setenv("KUBE_MAX_PD_VOLS", "4")
+    nodes, running, pods, pvs, pvcs, objs = rnd_mixed_workload(seed, n_nodes=60, n_pods=500)
+    preds = [k for k in scheduler.DEFAULT_PREDICATES if k != "MatchInterPodAffinity"]
+    prios = [(n, w) for n, w in scheduler.DEFAULT_PRIORITIES if n != "InterPodAffinityPriority"]
+    custom = {k: v for k, v in R.volume_predicates(R.VolumeListers(pvs, pvcs), 4).items() if k in preds}
+    want, lni = R.simulate(nodes, running, pods, set(preds), list(prios), custom, spread=R.SpreadListers(**objs))
+    got, ctr = c_oracle_objects(nodes, running, pods, preds, prios, pvs=pvs, pvcs=pvcs, spread=ksp.SpreadListers(**objs))
+    _same(want, got)
+    assert ctr == lni
+
+
+def _c2x(n_nodes, n_pods, seed, threads):
+    nodes, pods, pvs, pvcs, services = synth.c2x_objects(n_nodes, n_pods, seed)
+    preds, prios = scheduler.provider("DefaultProvider")
+    queue = list(reversed(pods))                    # c2x_objects is in scheduling order
+    custom = {k: v for k, v in R.volume_predicates(R.VolumeListers(pvs, pvcs)).items() if k in preds}
+    want, lni = R.simulate(nodes, [], queue, set(preds), list(prios), custom, spread=R.SpreadListers(services=services))
+    got, ctr = c_oracle_objects(nodes, [], queue, preds, prios, pvs=pvs, pvcs=pvcs,
+                                spread=ksp.SpreadListers(services=services), threads=threads)
+    _same(want, got)
+    assert ctr == lni
+    return want
+
+
+def test_c2x_objects_at_scale():
+    """C2x (zones, GCE PD / EBS / zoned-PVC volumes, services → SelectorSpread, hostname
+    anti-affinity) at 400 nodes x 4,000 pods, C oracle on 8 threads against the object oracle."""
+    want = _c2x(400, 4000, 61, threads=8)
+    assert len({h for _, h, _ in want if h}) > 300
+
+
+def test_c2x_objects_saturated():
+    """C2x scaled down until the cluster overflows: 40 nodes x 3,000 pods — FitErrors from
+    resources, disk conflicts, volume counts and anti-affinity dominate the tail."""
+    want = _c2x(40, 3000, 62, threads=3)
+    fails = [m for _, h, m in want if h is None]
+    assert len(fails) > 500
