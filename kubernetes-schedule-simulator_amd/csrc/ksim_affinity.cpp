@@ -136,6 +136,29 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
   if ((rc = dev_upload<int64_t>(h, &zsum, nullptr, n_zone)) || (rc = dev_upload<int64_t>(h, &zread, nullptr, n_zone)))
     return rc;
   if (t->spread_pair && (rc = dev_upload(h, &spair, t->spread_pair, t->n_aclass))) return rc;
+  // node-like keys: every domain holds at most one node (the node pseudo key, a unique hostname
+  // label), so a commit changes one row's counts; other keys' domains are shared by several nodes
+  std::vector<uint8_t> nodelike(t->n_keys, 1);
+  for (int32_t k = 0; k < t->n_keys; ++k) {
+    std::vector<int32_t> per(t->n_dom[k], 0);
+    const int32_t* row = t->dom + (int64_t)k * n;
+    for (int64_t i = 0; i < n && nodelike[k]; ++i)
+      if (row[i] >= 0 && ++per[row[i]] > 1) nodelike[k] = 0;
+  }
+  std::vector<uint8_t> ishared(t->n_ident, 0), ashared(t->n_aclass, 0);
+  for (int64_t i = 0; i < t->n_ident; ++i)
+    for (int32_t cp = 0; cp < t->n_pair && !ishared[i]; ++cp) {
+      const int32_t s = t->pair_sel[cp];
+      if (((t->ident_sel[i * t->sel_words + (s >> 6)] >> (s & 63)) & 1ull) && !nodelike[t->pair_key[cp]]) ishared[i] = 1;
+    }
+  for (int32_t a = 0; a < t->n_aclass; ++a) {
+    const int32_t* r = t->ac + 6 * (int64_t)a;
+    for (int32_t j = r[4]; j < r[4] + r[5]; ++j)
+      if (!nodelike[t->carry_key[t->carries[j].term]]) ashared[a] = 1;
+  }
+  uint8_t *ish, *ash;
+  if ((rc = dev_upload(h, &ish, ishared.data(), ishared.size())) || (rc = dev_upload(h, &ash, ashared.data(), ashared.size())))
+    return rc;
   A.n = n;
   A.spread_pair = spair; A.zsum = zsum; A.zread = zread; A.zone_key = t->zone_key; A.n_zone = n_zone;
   A.dom = dom; A.ident_sel = is; A.ident_anti = ia; A.ident_prio = ip;
@@ -153,6 +176,14 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
   for (size_t k = nb0; k < h->bufs.size(); ++k) h->aff_bufs.push_back(h->bufs[k].p);
   h->aff_dev = dev;
   h->aff_h = A;
+  h->aff_ident_shared = ish;
+  h->aff_aclass_shared = ash;
+  h->aff_n_pair = t->n_pair;
+  h->aff_n_carry = t->n_carry;
+  h->aff_n_zone = n_zone;
+  h->pg_rows_bytes = 0;  // the row-form arrays are sized by the new tables
+  if (h->pg_cnt_row) { dev_free(h, h->pg_cnt_row); h->pg_cnt_row = nullptr; }
+  if (h->pg_car_row) { dev_free(h, h->pg_car_row); h->pg_car_row = nullptr; }
   h->ctx.aff = dev;
   h->aff_n_ident = t->n_ident;
   h->aff_n_aclass = t->n_aclass;

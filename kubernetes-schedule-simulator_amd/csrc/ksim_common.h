@@ -564,8 +564,9 @@ __device__ __noinline__ void ksim_vol_commit(const KsimVol& V, const ksim_pod& P
 }
 
 // Reason mask of the first failing predicate in predicatesOrdering (predicates.go:129-138,
-// core/generic_scheduler.go:467-528); 0 = fits.
-template <class A>
+// core/generic_scheduler.go:467-528); 0 = fits.  IPA = false stops before MatchInterPodAffinity (the
+// last key), for a kernel that evaluates it over its own count layout (ksim_pgen.hip).
+template <class A, bool IPA = true>
 __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ksim_pod& P, int64_t i, const KsimRow& r,
                                                       const A& a) {
   const uint32_t pr = c.preds;
@@ -624,7 +625,7 @@ __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ks
   if ((pr & KSIM_P_MEM_PRESSURE) && (P.flags & KSIM_POD_BEST_EFFORT) && (r.fl & KSIM_N_MEM_PRESSURE))
     return 1u << KSIM_R_MEM_PRESSURE;
   if ((pr & KSIM_P_DISK_PRESSURE) && (r.fl & KSIM_N_DISK_PRESSURE)) return 1u << KSIM_R_DISK_PRESSURE;
-  if ((pr & KSIM_P_INTERPOD_AFFINITY) && c.aff && (P.aff_ident > 0 || P.aff_class > 0))
+  if (IPA && (pr & KSIM_P_INTERPOD_AFFINITY) && c.aff && (P.aff_ident > 0 || P.aff_class > 0))
     return ksim_interpod_pred(*c.aff, P, i);
   return 0;
 }

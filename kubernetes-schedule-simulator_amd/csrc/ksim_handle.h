@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "ksim_common.h"
+#include "ksim_pgen.h"
 #include "ksim_sweep.h"
 #include "ksim_tree.h"
 #include "ksim_f64.h"
@@ -151,6 +152,15 @@ struct ksim_handle {
   int32_t aff_n_ident = 0, aff_n_aclass = 0;
   KsimAff* aff_dev = nullptr;
   KsimAff aff_h{};              // host copy of the device descriptor (pass-A scratch pointers)
+  // general persistent kernel (ksim_pgen.hip): per identity / affinity class "its counts live in a
+  // shared topology domain" flags, the tables' sizes, and the row-form count arrays + exchange buffer
+  uint8_t* aff_ident_shared = nullptr;
+  uint8_t* aff_aclass_shared = nullptr;
+  int32_t aff_n_pair = 0, aff_n_carry = 0, aff_n_zone = 0;
+  int32_t* pg_cnt_row = nullptr;
+  int64_t* pg_car_row = nullptr;
+  size_t pg_rows_bytes = 0;
+  uint64_t* pg_gran = nullptr;
   bool fuse_off = false;        // a fused pass-A barrier timed out once: pass A as its own launch
   std::vector<void*> aff_bufs;
   std::vector<int32_t> q_ident, q_aclass;

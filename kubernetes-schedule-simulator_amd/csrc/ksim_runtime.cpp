@@ -640,10 +640,116 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
   return KSIM_OK;
 }
 
+// Can the general persistent kernel (ksim_pgen.hip) take a range with affinity / spread / volume /
+// service-affinity pods?  One workgroup per <= 1,024 rows, <= 256 workgroups, co-resident (checked
+// at launch), scores within the granule's 31 bits, the spread reduce's zones within one record.
+static bool pgen_ok(ksim_handle* h, int* grid, int* npt) {
+  const KsimCtx& c = h->ctx;
+  if (getenv("KSIM_NO_PGEN") || h->shard.world > 1) return false;
+  if (!ksim_pgen_config(c.n, h->max_grid, grid, npt)) return false;
+  int64_t s = 0;
+  for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED, KSIM_W_INTERPOD_AFFINITY,
+                KSIM_W_SELECTOR_SPREAD}) {
+    if (c.w[k] > ((int64_t)1 << 30)) return false;
+    s += c.w[k] * 10;
+  }
+  if (s >= ((int64_t)1 << 31)) return false;
+  if (h->have_aff) {
+    if (c.w[KSIM_W_SELECTOR_SPREAD] && h->aff_n_zone > ksim_pgen_max_zones()) return false;
+    const double bytes = ((double)h->aff_n_pair * 4 + (double)h->aff_n_carry * 8) * (double)c.n;
+    if (bytes > 8.0 * (1ull << 30)) return false;
+  }
+  return true;
+}
+
+// The general persistent kernel over [first, first+count): the affinity counts go to their row form
+// before the launch and back to the canonical per-domain form after (the launch kernels and the
+// per-pod entry points read that one).
+static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, int grid, int npt, ksim_stats* st) {
+  KsimCtx& c = h->ctx;
+  int rc;
+  const size_t gb = ksim_pgen_gran_bytes();
+  if (!h->pg_gran && (rc = dev_alloc(h, &h->pg_gran, gb / sizeof(uint64_t)))) return rc;
+  PGenArgs g{};
+  g.gran = h->pg_gran;
+  g.spin_ticks = 200000000ull;
+  g.has_vol = h->have_vol ? 1 : 0;
+  if (h->have_vol) g.V = h->vol_h;
+  if (h->have_aff) {
+    const size_t want = (size_t)h->aff_n_pair * c.n * 4 + (size_t)h->aff_n_carry * c.n * 8;
+    if (h->pg_rows_bytes < want || !h->pg_cnt_row) {
+      if (h->pg_cnt_row) dev_free(h, h->pg_cnt_row);
+      if (h->pg_car_row) dev_free(h, h->pg_car_row);
+      h->pg_cnt_row = nullptr;
+      h->pg_car_row = nullptr;
+      if ((rc = dev_alloc(h, &h->pg_cnt_row, (size_t)h->aff_n_pair * c.n)) ||
+          (rc = dev_alloc(h, &h->pg_car_row, (size_t)h->aff_n_carry * c.n)))
+        return rc;
+      h->pg_rows_bytes = want;
+    }
+    g.cnt_row = h->pg_cnt_row;
+    g.car_row = h->pg_car_row;
+    g.ident_shared = h->aff_ident_shared;
+    g.aclass_shared = h->aff_aclass_shared;
+    g.n_zone = h->aff_n_zone;
+    g.has_aff = 1;
+    g.A = h->aff_h;
+    hipError_t e = ksim_pgen_rows(h->aff_dev, g.cnt_row, g.car_row, h->aff_n_pair, h->aff_n_carry, c.n, 1, h->stream);
+    if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pgen rows: %s", hipGetErrorString(e));
+  }
+  c.first = first;
+  c.end = first + count;
+  c.chunk = (c.n + grid - 1) / grid;
+  (void)ksim_pgen_plan(c.chunk, c.n_classes_dev, g.has_vol ? g.V.vol_slots : 0, &g.vs, &g.st_classes);
+  HIPCHK(h, hipMemsetAsync(h->pg_gran, 0, gb, h->stream));
+  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+  hipError_t e = ksim_launch_pgen(&c, &g, grid, npt, h->stream);
+  if (e == hipErrorCooperativeLaunchTooLarge) {
+    if (h->cfg.mode != KSIM_MODE_PERSISTENT) return run_launch_mode(h, first, count, st);
+    return ksim_fail(h, KSIM_E_UNSUPPORTED, "persistent launch: %d workgroups cannot be co-resident on this device", grid);
+  }
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pgen launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+  if (h->have_aff) {
+    e = ksim_pgen_rows(h->aff_dev, g.cnt_row, g.car_row, h->aff_n_pair, h->aff_n_carry, c.n, 0, h->stream);
+    if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pgen rows: %s", hipGetErrorString(e));
+  }
+  HIPCHK(h, hipStreamSynchronize(h->stream));
+  float ms = 0.f;
+  HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
+#ifdef KSIM_STAMPS
+  {
+    uint64_t d[32];
+    HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
+    fprintf(stderr, "[ksim stamps] pgen pods=%lld (%.3f ms, grid %d, vs %d, st %d) cycles/pod: eval %.0f passA-local %.0f "
+            "passA-xchg %.0f classes %.0f class-sweep %.0f decide %.0f pick+commit %.0f aff-rows %.0f\n", (long long)count,
+            ms, grid, g.vs, g.st_classes, d[0] / (double)count, d[6] / (double)count, d[1] / (double)count,
+            d[2] / (double)count, d[7] / (double)count, d[3] / (double)count, d[4] / (double)count, d[5] / (double)count);
+  }
+#endif
+  if (st) {
+    st->device_ms = ms;
+    st->kernel_ms = ms;
+    st->kernel_launches = 1;
+    st->mode = KSIM_MODE_PERSISTENT;
+    st->blocks = grid;
+  }
+  return KSIM_OK;
+}
+
+// Pods only the launch kernels or the general persistent kernel schedule (affinity, volumes,
+// service affinity): the persistent one when it can take the range.
+static int run_f3_range(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
+  int grid = 0, npt = 0;
+  if (h->cfg.mode != KSIM_MODE_LAUNCH && pgen_ok(h, &grid, &npt)) return run_pgen_mode(h, first, count, grid, npt, st);
+  return run_launch_mode(h, first, count, st);
+}
+
 static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   KsimCtx& c = h->ctx;
-  // inter-pod affinity and volume pods are evaluated and committed by the launch-mode kernels only
-  if (ksim_rt_launch_only_count(h, first, count)) return run_launch_mode(h, first, count, st);
+  // inter-pod affinity, volume and service-affinity pods: the general persistent kernel (or the launch form)
+  if (ksim_rt_launch_only_count(h, first, count)) return run_f3_range(h, first, count, st);
   int grid = 0, lds_rows = 0;
   if (const int form = pfast_form(h, first, count, &grid, &lds_rows)) {
     int rc = run_pfast_mode(h, first, count, grid, lds_rows, form == 2, st);
@@ -741,7 +847,7 @@ static int run_auto_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stat
   int g, l;
   if (ksim_rt_launch_only_count(h, first, count)) {
     h->tree_valid = false;
-    return run_launch_mode(h, first, count, st);
+    return run_f3_range(h, first, count, st);
   }
   const bool pers = (ksim_persistent_config(h->ctx.n, &g, &l) && persistent_weights_ok(h->ctx)) ||
                     pfast_form(h, first, count, &g, &l);

@@ -527,13 +527,15 @@ def test_node_sharded_fills_cluster_with_fit_errors(monkeypatch):
     assert all(s.last_node_index == ref_ctr for s in scheds)
 
 
-@pytest.mark.parametrize("skew", [0.0, 3.5])
-def test_node_sharded_multi_process(tmp_path, skew):
-    """Two ranks in two processes (the one-process-per-device layout: rank r on device
-    r % device_count, so both on device 0 of a one-GPU box), exchange buffers shared through
-    hipIpcGetMemHandle / hipIpcOpenMemHandle over a gloo group: merged placements, counters and
-    node state equal the C oracle's.  skew: the last rank starts its first call 3.5 s late —
-    beyond the 2 s per-pod spin bound — which the first pod's start handshake must absorb."""
+@pytest.mark.parametrize("world,skew", [(2, 0.0), (2, 3.5), (4, 0.0), (8, 0.0)])
+def test_node_sharded_multi_process(tmp_path, world, skew):
+    """`world` ranks in as many processes (the one-process-per-device layout: rank r on device
+    r % device_count — all on device 0 of a one-GPU box, each process with its own hardware
+    queues), exchange buffers shared through hipIpcGetMemHandle / hipIpcOpenMemHandle over a gloo
+    group: merged placements, counters and node state equal the C oracle's.  world = 8 is
+    KSIM_MAX_RANKS: every exchange slot and the decision's rank walk at full width.  skew: the
+    last rank starts its first call 3.5 s late — beyond the 2 s per-pod spin bound — which the
+    first pod's start handshake must absorb."""
     import socket
     import subprocess
     import sys
@@ -543,14 +545,13 @@ def test_node_sharded_multi_process(tmp_path, skew):
     with socket.socket() as so:
         so.bind(("127.0.0.1", 0))
         port = so.getsockname()[1]
-    world = 2
     env = dict(os.environ)
     if torch.cuda.device_count() < world:  # ranks share a device: their persistent grids must co-reside
-        env["KSIM_MAX_GRID"] = "64"
+        env["KSIM_MAX_GRID"] = str(256 // world // 2)
     worker = os.path.join(os.path.dirname(__file__), "shard_worker.py")
     procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(port), str(tmp_path / ("r%d.npz" % r)),
                                str(skew)], env=env) for r in range(world)]
-    rcs = [pr.wait(timeout=100) for pr in procs]
+    rcs = [pr.wait(timeout=150) for pr in procs]
     assert rcs == [0] * world
     res = [np.load(tmp_path / ("r%d.npz" % r)) for r in range(world)]
     cl, p, q = synth.config_c3(40_000, 2500, seed=9)
