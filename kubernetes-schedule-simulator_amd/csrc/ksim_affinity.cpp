@@ -159,6 +159,37 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
   uint8_t *ish, *ash;
   if ((rc = dev_upload(h, &ish, ishared.data(), ishared.size())) || (rc = dev_upload(h, &ash, ashared.data(), ashared.size())))
     return rc;
+  // per identity, as lists (the general persistent kernel's pod-context records): the carried
+  // anti-affinity / priority terms it matches and the counted pairs (with their key) it matches
+  std::vector<int32_t> anti_off(1, 0), prio_off(1, 0), mp_off(1, 0), anti, prio, mp;
+  int32_t mx_anti = 0, mx_prio = 0, mx_mp = 0;
+  for (int64_t i = 0; i < t->n_ident; ++i) {
+    for (int32_t w = 0; w < t->carry_words; ++w) {
+      for (uint64_t m = t->ident_anti[i * t->carry_words + w]; m; m &= m - 1) anti.push_back(64 * w + __builtin_ctzll(m));
+      for (uint64_t m = t->ident_prio[i * t->carry_words + w]; m; m &= m - 1) prio.push_back(64 * w + __builtin_ctzll(m));
+    }
+    for (int32_t cp = 0; cp < t->n_pair; ++cp) {
+      const int32_t s = t->pair_sel[cp];
+      if ((t->ident_sel[i * t->sel_words + (s >> 6)] >> (s & 63)) & 1ull) { mp.push_back(cp); mp.push_back(t->pair_key[cp]); }
+    }
+    mx_anti = std::max<int32_t>(mx_anti, (int32_t)anti.size() - anti_off.back());
+    mx_prio = std::max<int32_t>(mx_prio, (int32_t)prio.size() - prio_off.back());
+    mx_mp = std::max<int32_t>(mx_mp, ((int32_t)mp.size() - mp_off.back()) / 2);
+    anti_off.push_back((int32_t)anti.size());
+    prio_off.push_back((int32_t)prio.size());
+    mp_off.push_back((int32_t)mp.size() / 2);
+  }
+  int32_t mx_req = 0, mx_pref = 0, mx_car = 0;
+  for (int32_t a = 0; a < t->n_aclass; ++a) {
+    mx_req = std::max(mx_req, t->ac[6 * (int64_t)a + 1]);
+    mx_pref = std::max(mx_pref, t->ac[6 * (int64_t)a + 3]);
+    mx_car = std::max(mx_car, t->ac[6 * (int64_t)a + 5]);
+  }
+  int32_t *dao, *da, *dpo, *dp, *dmo, *dm;
+  if ((rc = dev_upload(h, &dao, anti_off.data(), anti_off.size())) || (rc = dev_upload(h, &da, anti.data(), anti.size())) ||
+      (rc = dev_upload(h, &dpo, prio_off.data(), prio_off.size())) || (rc = dev_upload(h, &dp, prio.data(), prio.size())) ||
+      (rc = dev_upload(h, &dmo, mp_off.data(), mp_off.size())) || (rc = dev_upload(h, &dm, mp.data(), mp.size())))
+    return rc;
   A.n = n;
   A.spread_pair = spair; A.zsum = zsum; A.zread = zread; A.zone_key = t->zone_key; A.n_zone = n_zone;
   A.dom = dom; A.ident_sel = is; A.ident_anti = ia; A.ident_prio = ip;
@@ -181,9 +212,11 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
   h->aff_n_pair = t->n_pair;
   h->aff_n_carry = t->n_carry;
   h->aff_n_zone = n_zone;
-  h->pg_rows_bytes = 0;  // the row-form arrays are sized by the new tables
-  if (h->pg_cnt_row) { dev_free(h, h->pg_cnt_row); h->pg_cnt_row = nullptr; }
-  if (h->pg_car_row) { dev_free(h, h->pg_car_row); h->pg_car_row = nullptr; }
+  h->aff_n_keys = t->n_keys;
+  h->pg_id_anti_off = dao; h->pg_id_anti = da; h->pg_id_prio_off = dpo; h->pg_id_prio = dp;
+  h->pg_id_mp_off = dmo; h->pg_id_mp = dm;
+  h->pg_max_anti = mx_anti; h->pg_max_prio = mx_prio; h->pg_max_mp = mx_mp;
+  h->pg_max_req = mx_req; h->pg_max_pref = mx_pref; h->pg_max_car = mx_car;
   h->ctx.aff = dev;
   h->aff_n_ident = t->n_ident;
   h->aff_n_aclass = t->n_aclass;

@@ -156,11 +156,18 @@ struct ksim_handle {
   // shared topology domain" flags, the tables' sizes, and the row-form count arrays + exchange buffer
   uint8_t* aff_ident_shared = nullptr;
   uint8_t* aff_aclass_shared = nullptr;
-  int32_t aff_n_pair = 0, aff_n_carry = 0, aff_n_zone = 0;
-  int32_t* pg_cnt_row = nullptr;
-  int64_t* pg_car_row = nullptr;
-  size_t pg_rows_bytes = 0;
+  int32_t aff_n_pair = 0, aff_n_carry = 0, aff_n_zone = 0, aff_n_keys = 0;
+  // identity lists for the pod-context records (CSR, device): carried anti / priority terms the
+  // identity matches, counted pairs it matches as (pair, key); and the longest list of each kind
+  // over identities / affinity classes (the record-size bound)
+  int32_t *pg_id_anti_off = nullptr, *pg_id_anti = nullptr, *pg_id_prio_off = nullptr, *pg_id_prio = nullptr;
+  int32_t *pg_id_mp_off = nullptr, *pg_id_mp = nullptr;
+  int32_t pg_max_anti = 0, pg_max_prio = 0, pg_max_mp = 0, pg_max_req = 0, pg_max_pref = 0, pg_max_car = 0;
+  int32_t vol_max_ref = 0;                 // longest volume class
+  int32_t q_max_port = 0, q_max_scal = 0;  // most host ports / scalar requests of a queued pod
   uint64_t* pg_gran = nullptr;
+  char* pg_rec = nullptr;                  // pod-context records of the current call
+  size_t pg_rec_bytes = 0;
   bool fuse_off = false;        // a fused pass-A barrier timed out once: pass A as its own launch
   std::vector<void*> aff_bufs;
   std::vector<int32_t> q_ident, q_aclass;

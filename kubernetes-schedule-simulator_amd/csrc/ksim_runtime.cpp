@@ -391,6 +391,8 @@ int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
     h->q_aclass[q] = p.aff_class;
     h->aff_pre[q + 1] = h->aff_pre[q] + ((p.aff_ident || p.aff_class) ? 1 : 0);
     h->q_vclass[q] = p.vol_class;
+    h->q_max_port = std::max(h->q_max_port, p.port_cnt);
+    h->q_max_scal = std::max(h->q_max_scal, p.scalar_cnt);
     h->vol_pre[q + 1] = h->vol_pre[q] + ((p.vol_class || (p.flags & KSIM_POD_NEED_SVC_AFFINITY)) ? 1 : 0);
     const bool fast = h->q_base[q] && fast_k(h, p.cls);
     h->fast_pre[q + 1] = h->fast_pre[q] + (fast ? 1 : 0);
@@ -640,13 +642,22 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
   return KSIM_OK;
 }
 
-// Can the general persistent kernel (ksim_pgen.hip) take a range with affinity / spread / volume /
-// service-affinity pods?  One workgroup per <= 1,024 rows, <= 256 workgroups, co-resident (checked
-// at launch), scores within the granule's 31 bits, the spread reduce's zones within one record.
-static bool pgen_ok(ksim_handle* h, int* grid, int* npt) {
+// The general persistent kernel (ksim_pgen.hip) for a range with affinity / spread / volume /
+// service-affinity pods: its launch plan, or false when it cannot take the range (the launch form
+// then does).  Everything the cycle touches must fit one workgroup's LDS for <= 1,024 rows and
+// <= 256 workgroups (co-resident, checked at launch); scores within the granule's 31 bits; the
+// spread reduce's zones within one record; every pod-context record within PG_REC_MAX.
+struct PgPlan {
+  int grid = 0, npt = 0;
+  int64_t chunk = 0;
+  size_t lds = 0;
+  PgDims d{};
+  uint32_t off[PGO_N] = {};
+};
+
+static bool pgen_plan(ksim_handle* h, PgPlan* pl) {
   const KsimCtx& c = h->ctx;
-  if (getenv("KSIM_NO_PGEN") || h->shard.world > 1) return false;
-  if (!ksim_pgen_config(c.n, h->max_grid, grid, npt)) return false;
+  if (getenv("KSIM_NO_PGEN") || h->shard.world > 1 || c.n <= 0) return false;
   int64_t s = 0;
   for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED, KSIM_W_INTERPOD_AFFINITY,
                 KSIM_W_SELECTOR_SPREAD}) {
@@ -656,76 +667,121 @@ static bool pgen_ok(ksim_handle* h, int* grid, int* npt) {
   if (s >= ((int64_t)1 << 31)) return false;
   if (h->have_aff) {
     if (c.w[KSIM_W_SELECTOR_SPREAD] && h->aff_n_zone > ksim_pgen_max_zones()) return false;
-    const double bytes = ((double)h->aff_n_pair * 4 + (double)h->aff_n_carry * 8) * (double)c.n;
-    if (bytes > 8.0 * (1ull << 30)) return false;
+    if (h->pg_max_mp + h->pg_max_car > 512) return false;  // the shared-domain commit's list
   }
+  // the pod-context record bound (ksim_pgen.h): the longest list of every kind
+  PgHdr b{};
+  if (h->have_aff) {
+    b.n_anti = h->pg_max_anti; b.n_prio = h->pg_max_prio; b.n_mp = h->pg_max_mp;
+    b.n_req = h->pg_max_req; b.n_pref = h->pg_max_pref; b.n_car = h->pg_max_car;
+  }
+  if (h->have_vol) {
+    b.n_ref = h->vol_max_ref;
+    b.n_zw = h->vol_h.zone_ok ? h->vol_h.zone_words : 0;
+  }
+  b.n_port = h->q_max_port;
+  b.n_scal = h->q_max_scal;
+  uint32_t so[PGS_END + 1];
+  pg_sections(b, so);
+  if (so[PGS_END] > PG_REC_MAX) return false;
+  PgDims d{};
+  d.rec_stride = (int32_t)so[PGS_END];
+  d.vcap = h->have_vol ? h->vol_h.vol_slots : 0;
+  d.vslots = std::min(d.vcap, PG_VS_LDS);
+  d.pslots = c.port_slots;
+  if (h->have_aff) { d.n_keys = h->aff_n_keys; d.n_pair = h->aff_n_pair; d.n_carry = h->aff_n_carry; }
+  const size_t budget = ksim_pgen_lds_budget();
+  const int64_t gcap = (h->max_grid > 0 && h->max_grid < 256) ? h->max_grid : 256;
+  const int64_t cmin = (c.n + gcap - 1) / gcap;  // at most 256 workgroups (KSIM_MAX_GRID)
+  if (cmin > 1024) return false;
+  int64_t chunk = std::min<int64_t>(std::max<int64_t>(cmin, 256), c.n);
+  if (const char* e = getenv("KSIM_PGEN_CHUNK")) chunk = std::max<int64_t>(cmin, std::min<int64_t>(atoll(e), 1024));
+  for (;;) {
+    d.n_st = c.n_classes_dev;  // the static (pod class, row) words, when they fit
+    size_t lds = ksim_pgen_plan(chunk, &d, pl->off);
+    if (lds > budget) {
+      d.n_st = 0;
+      lds = ksim_pgen_plan(chunk, &d, pl->off);
+    }
+    if (lds <= budget) {
+      pl->lds = lds;
+      break;
+    }
+    if (chunk <= cmin) return false;
+    chunk = std::max<int64_t>(cmin, chunk * 7 / 8);
+  }
+  pl->chunk = chunk;
+  pl->grid = (int)((c.n + chunk - 1) / chunk);
+  pl->npt = chunk <= 256 ? 1 : chunk <= 512 ? 2 : 4;
+  pl->d = d;
   return true;
 }
 
-// The general persistent kernel over [first, first+count): the affinity counts go to their row form
-// before the launch and back to the canonical per-domain form after (the launch kernels and the
-// per-pod entry points read that one).
-static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, int grid, int npt, ksim_stats* st) {
+// The general persistent kernel over [first, first+count): the pod-context records are packed,
+// then one launch schedules the range; the kernel writes the node rows, volume slots, host ports
+// and canonical affinity counts back to HBM at its end.
+static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, const PgPlan& pl, ksim_stats* st) {
   KsimCtx& c = h->ctx;
   int rc;
   const size_t gb = ksim_pgen_gran_bytes();
   if (!h->pg_gran && (rc = dev_alloc(h, &h->pg_gran, gb / sizeof(uint64_t)))) return rc;
+  const size_t rb = (size_t)count * pl.d.rec_stride;
+  if (h->pg_rec_bytes < rb) {
+    if (h->pg_rec) dev_free(h, h->pg_rec);
+    h->pg_rec = nullptr;
+    h->pg_rec_bytes = 0;
+    if ((rc = dev_alloc(h, &h->pg_rec, std::max<size_t>(rb, 1 << 20)))) return rc;
+    h->pg_rec_bytes = std::max<size_t>(rb, 1 << 20);
+  }
   PGenArgs g{};
   g.gran = h->pg_gran;
+  g.rec = h->pg_rec;
   g.spin_ticks = 200000000ull;
+  g.d = pl.d;
+  memcpy(g.off, pl.off, sizeof g.off);
   g.has_vol = h->have_vol ? 1 : 0;
   if (h->have_vol) g.V = h->vol_h;
   if (h->have_aff) {
-    const size_t want = (size_t)h->aff_n_pair * c.n * 4 + (size_t)h->aff_n_carry * c.n * 8;
-    if (h->pg_rows_bytes < want || !h->pg_cnt_row) {
-      if (h->pg_cnt_row) dev_free(h, h->pg_cnt_row);
-      if (h->pg_car_row) dev_free(h, h->pg_car_row);
-      h->pg_cnt_row = nullptr;
-      h->pg_car_row = nullptr;
-      if ((rc = dev_alloc(h, &h->pg_cnt_row, (size_t)h->aff_n_pair * c.n)) ||
-          (rc = dev_alloc(h, &h->pg_car_row, (size_t)h->aff_n_carry * c.n)))
-        return rc;
-      h->pg_rows_bytes = want;
-    }
-    g.cnt_row = h->pg_cnt_row;
-    g.car_row = h->pg_car_row;
     g.ident_shared = h->aff_ident_shared;
     g.aclass_shared = h->aff_aclass_shared;
+    g.id_anti_off = h->pg_id_anti_off; g.id_anti = h->pg_id_anti;
+    g.id_prio_off = h->pg_id_prio_off; g.id_prio = h->pg_id_prio;
+    g.id_mp_off = h->pg_id_mp_off; g.id_mp = h->pg_id_mp;
     g.n_zone = h->aff_n_zone;
     g.has_aff = 1;
     g.A = h->aff_h;
-    hipError_t e = ksim_pgen_rows(h->aff_dev, g.cnt_row, g.car_row, h->aff_n_pair, h->aff_n_carry, c.n, 1, h->stream);
-    if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pgen rows: %s", hipGetErrorString(e));
   }
   c.first = first;
   c.end = first + count;
-  c.chunk = (c.n + grid - 1) / grid;
-  (void)ksim_pgen_plan(c.chunk, c.n_classes_dev, g.has_vol ? g.V.vol_slots : 0, &g.vs, &g.st_classes);
+  c.chunk = pl.chunk;
   HIPCHK(h, hipMemsetAsync(h->pg_gran, 0, gb, h->stream));
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipError_t e = ksim_launch_pgen(&c, &g, grid, npt, h->stream);
+  hipError_t e = ksim_pgen_pack(&c, &g, h->stream);
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pgen pack: %s", hipGetErrorString(e));
+  e = ksim_launch_pgen(&c, &g, pl.grid, pl.npt, pl.lds, h->stream);
   if (e == hipErrorCooperativeLaunchTooLarge) {
     if (h->cfg.mode != KSIM_MODE_PERSISTENT) return run_launch_mode(h, first, count, st);
-    return ksim_fail(h, KSIM_E_UNSUPPORTED, "persistent launch: %d workgroups cannot be co-resident on this device", grid);
+    return ksim_fail(h, KSIM_E_UNSUPPORTED, "persistent launch: %d workgroups cannot be co-resident on this device", pl.grid);
   }
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pgen launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipEventRecord(h->ev1, h->stream));
-  if (h->have_aff) {
-    e = ksim_pgen_rows(h->aff_dev, g.cnt_row, g.car_row, h->aff_n_pair, h->aff_n_carry, c.n, 0, h->stream);
-    if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pgen rows: %s", hipGetErrorString(e));
-  }
   HIPCHK(h, hipStreamSynchronize(h->stream));
   float ms = 0.f;
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
 #ifdef KSIM_STAMPS
   {
-    uint64_t d[32];
-    HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
-    HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
-    fprintf(stderr, "[ksim stamps] pgen pods=%lld (%.3f ms, grid %d, vs %d, st %d) cycles/pod: eval %.0f passA-local %.0f "
-            "passA-xchg %.0f classes %.0f class-sweep %.0f decide %.0f pick+commit %.0f aff-rows %.0f\n", (long long)count,
-            ms, grid, g.vs, g.st_classes, d[0] / (double)count, d[6] / (double)count, d[1] / (double)count,
-            d[2] / (double)count, d[7] / (double)count, d[3] / (double)count, d[4] / (double)count, d[5] / (double)count);
+    uint64_t dd[32];
+    HIPCHK(h, hipMemcpy(dd, c.dbg, sizeof dd, hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemset(c.dbg, 0, sizeof dd));
+    fprintf(stderr, "[ksim stamps] pgen pods=%lld (%.3f ms, grid %d, chunk %lld, st %d, rec %d B, lds %zu) cycles/pod: eval %.0f "
+            "passA-local %.0f passA-xchg %.0f classes %.0f class-sweep %.0f decide %.0f pick+commit %.0f aff-shared %.0f\n",
+            (long long)count, ms, pl.grid, (long long)pl.chunk, pl.d.n_st, pl.d.rec_stride, pl.lds, dd[0] / (double)count,
+            dd[6] / (double)count, dd[1] / (double)count, dd[2] / (double)count, dd[7] / (double)count, dd[3] / (double)count,
+            dd[4] / (double)count, dd[5] / (double)count);
+    fprintf(stderr, "[ksim stamps] pgen eval split (thread 0's row) cycles/pod: top+row %.0f predicates %.0f map %.0f\n",
+            dd[8] / (double)count, dd[9] / (double)count, dd[10] / (double)count);
+    fprintf(stderr, "[ksim stamps] pgen decide split (wave 0 of workgroup 0) cycles/pod: per-class %.0f rest %.0f barrier %.0f\n",
+            dd[11] / (double)count, dd[12] / (double)count, dd[3] / (double)count);
   }
 #endif
   if (st) {
@@ -733,7 +789,7 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, int grid,
     st->kernel_ms = ms;
     st->kernel_launches = 1;
     st->mode = KSIM_MODE_PERSISTENT;
-    st->blocks = grid;
+    st->blocks = pl.grid;
   }
   return KSIM_OK;
 }
@@ -741,8 +797,8 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, int grid,
 // Pods only the launch kernels or the general persistent kernel schedule (affinity, volumes,
 // service affinity): the persistent one when it can take the range.
 static int run_f3_range(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
-  int grid = 0, npt = 0;
-  if (h->cfg.mode != KSIM_MODE_LAUNCH && pgen_ok(h, &grid, &npt)) return run_pgen_mode(h, first, count, grid, npt, st);
+  PgPlan pl;
+  if (h->cfg.mode != KSIM_MODE_LAUNCH && pgen_plan(h, &pl)) return run_pgen_mode(h, first, count, pl, st);
   return run_launch_mode(h, first, count, st);
 }
 

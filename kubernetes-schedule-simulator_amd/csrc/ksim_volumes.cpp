@@ -94,6 +94,8 @@ extern "C" int ksim_load_volumes(ksim_handle* h, const ksim_volume_tables* t) {
   h->vol_h = V;
   h->ctx.vol = dev;
   h->vol_n_class = t->n_vclass;
+  h->vol_max_ref = 0;
+  for (int32_t c = 0; c < t->n_vclass; ++c) h->vol_max_ref = std::max(h->vol_max_ref, t->vc[2 * (int64_t)c + 1]);
   h->have_vol = true;
   h->vol_stale = false;
   // the table pointer is baked into the launch graph's kernel arguments

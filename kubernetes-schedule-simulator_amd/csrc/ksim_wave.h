@@ -61,4 +61,52 @@ __device__ __forceinline__ int32_t prefix_incl_i32(int32_t v) {
   return x;
 }
 
+// 64-bit forms: the two halves move through the same DPP control, the compare / add is 64-bit.
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF, bool BOUND_ZERO = false>
+__device__ __forceinline__ int64_t dpp64(int64_t old, int64_t v) {
+  const int lo = dpp<CTRL, ROW_MASK, BANK_MASK, BOUND_ZERO>((int)(uint32_t)old, (int)(uint32_t)v);
+  const int hi = dpp<CTRL, ROW_MASK, BANK_MASK, BOUND_ZERO>((int)(old >> 32), (int)(v >> 32));
+  return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+__device__ __forceinline__ int64_t readlane64(int64_t v, int l) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, l);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(v >> 32), l);
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
+
+__device__ __forceinline__ int64_t max_i64(int64_t v) {
+  constexpr int64_t ID = INT64_MIN;
+  int64_t t;
+  t = dpp64<QP_1032>(ID, v); v = t > v ? t : v;
+  t = dpp64<QP_2301>(ID, v); v = t > v ? t : v;
+  t = dpp64<ROW_HALF_MIRROR>(ID, v); v = t > v ? t : v;
+  t = dpp64<ROW_MIRROR>(ID, v); v = t > v ? t : v;
+  t = dpp64<ROW_BCAST15, 0xA>(ID, v); v = t > v ? t : v;
+  t = dpp64<ROW_BCAST31, 0xC>(ID, v); v = t > v ? t : v;
+  return readlane64(v, 63);
+}
+
+__device__ __forceinline__ int64_t min_i64(int64_t v) {
+  constexpr int64_t ID = INT64_MAX;
+  int64_t t;
+  t = dpp64<QP_1032>(ID, v); v = t < v ? t : v;
+  t = dpp64<QP_2301>(ID, v); v = t < v ? t : v;
+  t = dpp64<ROW_HALF_MIRROR>(ID, v); v = t < v ? t : v;
+  t = dpp64<ROW_MIRROR>(ID, v); v = t < v ? t : v;
+  t = dpp64<ROW_BCAST15, 0xA>(ID, v); v = t < v ? t : v;
+  t = dpp64<ROW_BCAST31, 0xC>(ID, v); v = t < v ? t : v;
+  return readlane64(v, 63);
+}
+
+__device__ __forceinline__ int64_t sum_i64(int64_t v) {
+  v += dpp64<QP_1032>(0, v);
+  v += dpp64<QP_2301>(0, v);
+  v += dpp64<ROW_HALF_MIRROR>(0, v);
+  v += dpp64<ROW_MIRROR>(0, v);
+  v += dpp64<ROW_BCAST15, 0xA>(0, v);
+  v += dpp64<ROW_BCAST31, 0xC>(0, v);
+  return readlane64(v, 63);
+}
+
 }  // namespace ksimw
