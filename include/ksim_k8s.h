@@ -1,0 +1,286 @@
+/* ksim_k8s.h — the Kubernetes-field front end of libksim: v1.Node / v1.Pod / PV / PVC fields in,
+ * device tables out.  Everything the scheduler decides by comparing strings — label selectors
+ * (apimachinery labels/selector.go:193-215, 837-853), node selectors and node affinity
+ * (algorithm/predicates/predicates.go:780-838), tolerations (core/v1/toleration.go:37-56, predicates
+ * .go:1465-1494), inter-pod affinity terms with their namespaces and topology keys
+ * (predicates.go:1143-1450, priorities/interpod_affinity.go:118-240, priorities/util/topologies.go),
+ * SelectorSpread selectors and zones (priorities/selector_spreading.go:66-174), volume identities
+ * and their listers (predicates.go:220-633), NodePreferAvoidPods signatures
+ * (priorities/node_prefer_avoid_pods.go:32-68) — is interned and evaluated here, in C++, into the
+ * tables of include/ksim.h.  A cgo adapter flattens the Go objects into these structs and never
+ * re-implements a scheduling rule.
+ *
+ * Conventions: strings are NUL-terminated UTF-8 and may be NULL where "absent" and "" mean the same
+ * to the reference; arrays are (count, pointer) pairs; every input is copied, no pointer is kept.
+ * Quantities arrive canonical: cpu as MilliValue(), everything else as Value() (resource.Quantity
+ * rounding, pkg/api/resource/quantity.go). */
+#ifndef KSIM_K8S_H
+#define KSIM_K8S_H
+
+#include "ksim.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+  const char* key;
+  const char* value;
+} ksim_k8s_kv;
+
+/* A selector requirement: operator as the API spells it ("In", "NotIn", "Exists",
+ * "DoesNotExist", "Gt", "Lt"; "=", "==", "!=" in resolved label selectors). */
+typedef struct {
+  const char* key;
+  const char* op;
+  int32_t n_values;
+  const char* const* values;
+} ksim_k8s_req;
+
+/* v1.NodeSelectorTerm (its matchExpressions). */
+typedef struct {
+  int32_t n_reqs;
+  const ksim_k8s_req* reqs;
+} ksim_k8s_node_term;
+
+/* v1.PreferredSchedulingTerm. */
+typedef struct {
+  int32_t weight;
+  ksim_k8s_node_term preference;
+} ksim_k8s_pref_node_term;
+
+/* metav1.LabelSelector; present = 0 is a nil selector. */
+typedef struct {
+  int32_t present;
+  int32_t n_match_labels;
+  const ksim_k8s_kv* match_labels;
+  int32_t n_exprs;
+  const ksim_k8s_req* exprs;
+} ksim_k8s_label_selector;
+
+/* v1.PodAffinityTerm (weight: WeightedPodAffinityTerm.weight for preferred terms, else 0). */
+typedef struct {
+  ksim_k8s_label_selector selector;
+  int32_t n_namespaces;
+  const char* const* namespaces;
+  const char* topology_key;
+  int32_t weight;
+} ksim_k8s_pod_term;
+
+typedef struct {
+  const char* key;
+  const char* value;
+  const char* effect;
+} ksim_k8s_taint;
+
+typedef struct {
+  const char* key;
+  const char* op;     /* "", "Equal" or "Exists" */
+  const char* value;
+  const char* effect;
+} ksim_k8s_toleration;
+
+typedef struct {
+  const char* name;
+  int64_t value;      /* Quantity.Value() */
+} ksim_k8s_resource;
+
+typedef struct {
+  const char* host_ip;   /* "" / NULL: 0.0.0.0 */
+  const char* protocol;  /* "" / NULL: TCP */
+  int32_t host_port;     /* <= 0: not a host port */
+} ksim_k8s_port;
+
+/* One container's requests (and whether a cpu / memory request or limit is positive, for the
+ * QoS class, K/pkg/apis/core/v1/helper/qos/qos.go:39-85). */
+typedef struct {
+  int32_t has_cpu, has_mem;          /* the requests map names cpu / memory */
+  int64_t cpu_milli, mem, gpu, eph;  /* requests (0 when absent) */
+  int32_t n_other;                   /* other requested resources (scalar ones are kept) */
+  const ksim_k8s_resource* other;
+  int32_t qos_positive;              /* some cpu / memory request or limit is > 0 */
+  int32_t n_ports;
+  const ksim_k8s_port* ports;
+} ksim_k8s_container;
+
+#define KSIM_K8S_VOL_GCE_PD 1
+#define KSIM_K8S_VOL_EBS 2
+#define KSIM_K8S_VOL_AZURE_DISK 3
+#define KSIM_K8S_VOL_ISCSI 4
+#define KSIM_K8S_VOL_RBD 5
+#define KSIM_K8S_VOL_PVC 6
+#define KSIM_K8S_VOL_OTHER 7
+
+/* One volume: id = pdName / volumeID / diskName / iqn / claimName; RBD: monitors, pool, image. */
+typedef struct {
+  int32_t kind;
+  int32_t read_only;
+  const char* id;
+  const char* pool;
+  const char* image;
+  int32_t n_monitors;
+  const char* const* monitors;
+} ksim_k8s_volume;
+
+typedef struct {
+  const char* name;
+  const char* namespace_;
+  int32_t n_labels;
+  const ksim_k8s_kv* labels;
+  int32_t deleting;                     /* metadata.deletionTimestamp is set */
+  const char* node_name;                /* spec.nodeName, NULL / "": none */
+  int32_t n_containers;
+  const ksim_k8s_container* containers;
+  int32_t n_init_containers;
+  const ksim_k8s_container* init_containers;
+  int32_t n_node_selector;
+  const ksim_k8s_kv* node_selector;
+  /* spec.affinity.nodeAffinity */
+  int32_t has_node_affinity;
+  int32_t has_required;                 /* requiredDuringSchedulingIgnoredDuringExecution is set */
+  int32_t n_required_terms;
+  const ksim_k8s_node_term* required_terms;
+  int32_t n_preferred;
+  const ksim_k8s_pref_node_term* preferred;
+  int32_t n_tolerations;
+  const ksim_k8s_toleration* tolerations;
+  /* spec.affinity.podAffinity / podAntiAffinity */
+  int32_t has_pod_affinity, has_pod_anti_affinity;
+  int32_t n_affinity_required, n_affinity_preferred, n_anti_required, n_anti_preferred;
+  const ksim_k8s_pod_term* affinity_required;
+  const ksim_k8s_pod_term* affinity_preferred;
+  const ksim_k8s_pod_term* anti_required;
+  const ksim_k8s_pod_term* anti_preferred;
+  int32_t n_volumes;
+  const ksim_k8s_volume* volumes;
+  /* getSelectors (priorities/metadata.go:82-114) as the caller's listers resolve it: the
+   * selectors of the services / RCs (set_selector = 1: labels.SelectorFromSet over matchLabels)
+   * and ReplicaSets / StatefulSets (0: LabelSelectorAsSelector) selecting the pod, in lister order */
+  int32_t n_spread;
+  const ksim_k8s_label_selector* spread;
+  const int32_t* spread_set_selector;
+  /* the RC / RS controllerRef NodePreferAvoidPods compares (kind, uid), NULL kind: none */
+  const char* avoid_ctrl_kind;
+  const char* avoid_ctrl_uid;
+} ksim_k8s_pod;
+
+typedef struct {
+  const char* type;
+  const char* status;
+} ksim_k8s_condition;
+
+/* preferAvoidPods entry as v1helper.GetAvoidPodsFromNodeAnnotations decodes it; has_controller = 0
+ * for an entry whose podSignature.podController is nil. */
+typedef struct {
+  int32_t has_controller;
+  const char* kind;
+  const char* uid;
+} ksim_k8s_avoid;
+
+typedef struct {
+  const char* name;
+  int32_t n_labels;
+  const ksim_k8s_kv* labels;
+  int32_t n_taints;
+  const ksim_k8s_taint* taints;
+  int32_t unschedulable;
+  int32_t n_conditions;
+  const ksim_k8s_condition* conditions;
+  int64_t alloc_cpu_milli, alloc_mem, alloc_gpu, alloc_eph, alloc_pods;
+  int32_t n_alloc_other;                /* other allocatable resources (scalar ones are kept) */
+  const ksim_k8s_resource* alloc_other;
+  int32_t n_avoid;
+  const ksim_k8s_avoid* avoid;
+  int32_t has_images;                   /* status.images is non-empty (ImageLocalityPriority) */
+} ksim_k8s_node;
+
+typedef struct {
+  const char* name;
+  int32_t n_labels;
+  const ksim_k8s_kv* labels;
+  int32_t kind;                         /* KSIM_K8S_VOL_GCE_PD / _EBS / _AZURE_DISK / _OTHER */
+  const char* id;
+  int32_t has_node_affinity;
+} ksim_k8s_pv;
+
+typedef struct {
+  const char* namespace_;
+  const char* name;
+  const char* volume_name;              /* spec.volumeName, "" / NULL: unbound */
+  const char* storage_class;            /* spec.storageClassName, NULL: unset */
+} ksim_k8s_pvc;
+
+typedef struct {
+  const char* name;
+  const char* binding_mode;             /* volumeBindingMode, NULL: unset */
+} ksim_k8s_storage_class;
+
+typedef struct {
+  int32_t hard_weight;                  /* hardPodAffinitySymmetricWeight (the simulator's 10) */
+  int32_t max_vols[3];                  /* MaxPD limits (EBS, GCE PD, Azure Disk); 0: getMaxVols */
+  int32_t port_slots;                   /* host-port slots per node, < 0: enough for the queue */
+  int32_t vol_slots;                    /* volume slots per node, < 0: enough for the queue */
+} ksim_k8s_options;
+
+typedef struct ksim_k8s_cluster ksim_k8s_cluster;
+
+/* A snapshot under construction: nodes, PVs / PVCs / storage classes, running pods (spec.nodeName
+ * set) and the queue in scheduling order. */
+int ksim_k8s_create(const ksim_k8s_options* opt, ksim_k8s_cluster** out);
+void ksim_k8s_destroy(ksim_k8s_cluster* c);
+const char* ksim_k8s_last_error(const ksim_k8s_cluster* c);
+int ksim_k8s_add_node(ksim_k8s_cluster* c, const ksim_k8s_node* n);
+int ksim_k8s_add_pv(ksim_k8s_cluster* c, const ksim_k8s_pv* pv);
+int ksim_k8s_add_pvc(ksim_k8s_cluster* c, const ksim_k8s_pvc* pvc);
+int ksim_k8s_add_storage_class(ksim_k8s_cluster* c, const ksim_k8s_storage_class* sc);
+int ksim_k8s_add_running_pod(ksim_k8s_cluster* c, const ksim_k8s_pod* p);
+int ksim_k8s_add_queued_pod(ksim_k8s_cluster* c, const ksim_k8s_pod* p);
+
+/* Intern everything and build the tables (NodeInfo.SetNode / AddPod for the running pods, the
+ * class, affinity and volume tables, the pod descriptors).  KSIM_E_UNSUPPORTED where the reference
+ * errs instead of placing (ksim_k8s_last_error says which input). */
+int ksim_k8s_build(ksim_k8s_cluster* c);
+
+/* The configured scheduler on the built snapshot: cfg as for ksim_create (predicate bits and
+ * priority weights; KSIM_W_SELECTOR_SPREAD carries SelectorSpread / ServiceSpreading's weight when
+ * some pod has spread selectors), prefer_avoid_weight: NodePreferAvoidPodsPriority's weight (0: not
+ * configured; it is the constant 10 x weight of cfg->const_score unless the nodes' preferAvoidPods
+ * annotations tell some pod class apart).  Creates the handle and loads the node table, class /
+ * affinity / volume tables and the queue. */
+int ksim_k8s_open(ksim_k8s_cluster* c, const ksim_config* cfg, int64_t prefer_avoid_weight, ksim_handle** out);
+
+/* Name-rank order and sizes of the built snapshot. */
+int64_t ksim_k8s_node_count(const ksim_k8s_cluster* c);
+const char* ksim_k8s_node_name(const ksim_k8s_cluster* c, int64_t rank);
+int64_t ksim_k8s_queue_length(const ksim_k8s_cluster* c);
+
+/* Built tables, read back (the parity tests compare them with the Python host's): the queued
+ * pods' descriptors and their port / scalar arrays, a node's label-set / taint-set ids, a class
+ * verdict: kind 0 = podMatchesNodeLabels bit of (class, label set), 1 = NoSchedule+NoExecute
+ * tolerated (class, taint set), 2 = NoExecute tolerated, 3 = intolerable PreferNoSchedule count
+ * (class, taint set), 4 = preferred node-affinity weight (class, label set). */
+int ksim_k8s_pods(const ksim_k8s_cluster* c, const ksim_pod** pods, const uint64_t** ports, int64_t* n_ports,
+                  const ksim_scalar_req** scalars, int64_t* n_scalars);
+int ksim_k8s_node_sets(const ksim_k8s_cluster* c, int64_t rank, int32_t* label_set, int32_t* taint_set, uint32_t* flags);
+int64_t ksim_k8s_class_value(const ksim_k8s_cluster* c, int32_t kind, int32_t cls, int32_t set);
+
+/* The built tables as the structs ksim_load_nodes / _classes / _affinity / _volumes take (views
+ * into the cluster, valid until the next call that changes it; absent tables are zeroed). */
+int ksim_k8s_tables(ksim_k8s_cluster* c, ksim_node_table* nodes, ksim_class_tables* classes, ksim_affinity_tables* aff,
+                    ksim_volume_tables* vol);
+
+/* Per-pod drop-in (scheduler.go:188-204 scheduleOne): describe one more pod against an open
+ * handle — its class, identity, affinity and volume classes interned, and the tables reloaded when
+ * it brings new ones — ready for ksim_schedule_one; ports / scalars receive its arrays (capacity
+ * given, counts returned).  ksim_k8s_bind records a placed pod (Scheduler.assume / cache.AddPod) so
+ * later reloads keep its affinity counts and volume mounts. */
+int ksim_k8s_describe(ksim_k8s_cluster* c, ksim_handle* h, const ksim_k8s_pod* p, ksim_pod* out, uint64_t* ports,
+                      int32_t port_cap, int32_t* n_ports, ksim_scalar_req* scalars, int32_t scalar_cap,
+                      int32_t* n_scalars, int64_t* pod_id);
+int ksim_k8s_bind(ksim_k8s_cluster* c, int64_t pod_id, int64_t node);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* KSIM_K8S_H */

@@ -839,11 +839,12 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
           mode = -1;
           if (lane == 0) atomicOr(c.err, 4);
         } else {
+          int32_t F = 0;
+          int32_t mq_l = -1, cq_l = 0;  // lane q: class q's global maximum and its count
           int32_t f = 0;
 #pragma unroll
           for (int m = 0; m < MB; ++m) f += (lane + 64 * m < G) ? gfit(gv[0][m]) : 0;
-          const int32_t F = ksimw::sum_i32(f);
-          int32_t mq_l = -1, cq_l = 0;  // lane q: class q's global maximum and its count
+          F = ksimw::sum_i32(f);
 #pragma unroll
           for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
             if (q < K) {
@@ -874,16 +875,17 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
               // (reduce.go:29-64, generic_scheduler.go:632-639), the best total and its classes
               const bool live = lane < K && cq_l != 0;
               int64_t mxT = 0, mxA = 0;
-              if (k1 > 1 || c.w[KSIM_W_TAINT_TOLERATION]) mxT = ksimw::max_i64(live ? tv_l : 0);
-              if (k2 > 1 || c.w[KSIM_W_NODE_AFFINITY]) mxA = ksimw::max_i64(live ? av_l : 0);
+              // K <= 16: the class lanes are one DPP row
+              if (k1 > 1 || c.w[KSIM_W_TAINT_TOLERATION]) mxT = ksimw::max16_i64(live ? tv_l : 0);
+              if (k2 > 1 || c.w[KSIM_W_NODE_AFFINITY]) mxA = ksimw::max16_i64(live ? av_l : 0);
               uint64_t t = (uint64_t)(int64_t)mq_l + (uint64_t)ad_l;
               if (c.w[KSIM_W_TAINT_TOLERATION]) t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(tv_l, mxT, true);
               if (c.w[KSIM_W_NODE_AFFINITY]) t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(av_l, mxA, false);
               const int64_t tot = live ? (int64_t)t : INT64_MIN;
-              const int64_t best = ksimw::max_i64(tot);
+              const int64_t best = ksimw::max16_i64(tot);
               const uint64_t wbm = __ballot(live && tot == best);
               win = (uint32_t)wbm;
-              const int32_t C = ksimw::sum_i32(((wbm >> lane) & 1ull) ? cq_l : 0);
+              const int32_t C = ksimw::sum16_i32(((wbm >> lane) & 1ull) ? cq_l : 0);
               tgt_l = ((wbm >> lane) & 1ull) ? mq_l : -2;
               ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)C) : (int64_t)((uint32_t)counter % (uint32_t)C);
               counter += 1;  // generic_scheduler.go:192-195

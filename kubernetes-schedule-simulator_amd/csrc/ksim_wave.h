@@ -109,4 +109,23 @@ __device__ __forceinline__ int64_t sum_i64(int64_t v) {
   return readlane64(v, 63);
 }
 
+// Over the first 16 lanes only (one DPP row: four steps, no row broadcasts), result from lane 0.
+__device__ __forceinline__ int64_t max16_i64(int64_t v) {
+  constexpr int64_t ID = INT64_MIN;
+  int64_t t;
+  t = dpp64<QP_1032>(ID, v); v = t > v ? t : v;
+  t = dpp64<QP_2301>(ID, v); v = t > v ? t : v;
+  t = dpp64<ROW_HALF_MIRROR>(ID, v); v = t > v ? t : v;
+  t = dpp64<ROW_MIRROR>(ID, v); v = t > v ? t : v;
+  return readlane64(v, 0);
+}
+
+__device__ __forceinline__ int32_t sum16_i32(int32_t v) {
+  v += dpp<QP_1032>(0, v);
+  v += dpp<QP_2301>(0, v);
+  v += dpp<ROW_HALF_MIRROR>(0, v);
+  v += dpp<ROW_MIRROR>(0, v);
+  return __builtin_amdgcn_readlane(v, 0);
+}
+
 }  // namespace ksimw

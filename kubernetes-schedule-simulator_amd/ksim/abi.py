@@ -264,6 +264,15 @@ class Handle:
         self.h = h
         self._keep = []
 
+    @classmethod
+    def adopt(cls, h, cfg=None):
+        """Wrap a handle another entry point created (ksim_k8s_open); it is destroyed with this."""
+        self = cls.__new__(cls)
+        self._L = lib()
+        self.h = h
+        self._keep = []
+        return self
+
     def _check(self, rc, h):
         if rc != KSIM_OK:
             msg = self._L.ksim_last_error(h).decode(errors="replace")

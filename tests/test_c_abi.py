@@ -40,3 +40,38 @@ def test_c_schedule_one_loop():
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS" in r.stdout
+
+
+K8S_BIN = os.path.join(CDIR, "build", "ksim_k8s_loop")
+
+
+@pytest.mark.parametrize("std", ["c99", "c11"])
+def test_k8s_header_compiles_as_plain_c(tmp_path, std):
+    src = tmp_path / "t.c"
+    src.write_text('#include "ksim_k8s.h"\nint main(void) { ksim_k8s_pod p; ksim_k8s_node n; ksim_k8s_cluster* c = 0;\n'
+                   '  (void)p; (void)n; return ksim_k8s_create(0, &c); }\n')
+    subprocess.run(["gcc", "-std=" + std, "-pedantic", "-Wall", "-Werror", "-fsyntax-only",
+                    "-I" + os.path.join(ROOT, "include"), str(src)], check=True)
+
+
+def test_k8s_front_end_runs_without_a_device(tmp_path):
+    """The front end is host code: a snapshot builds from raw fields on a machine without a GPU
+    (only ksim_k8s_open needs the device)."""
+    from ksim import frontend
+    from workloads import rnd_affinity_workload
+    nodes, running, pods = rnd_affinity_workload(3, n_nodes=10, n_pods=30)
+    fe = frontend.K8sCluster(nodes, running, pods)
+    assert len(fe.names) == 10 and len(fe.pods()[0]) == 30
+
+
+@pytest.mark.gpu
+def test_c_k8s_loop():
+    """Raw Kubernetes fields in plain C: the queue through ksim_k8s_open + ksim_schedule vs the C
+    oracle on the front end's tables, then scheduleOne (describe → schedule_one → bind) per pod vs
+    the queue run (exit 0 and PASS)."""
+    assert os.path.exists(K8S_BIN), "tests/c/build/ksim_k8s_loop not built (__graft_entry__.build())"
+    for n_nodes, n_pods in (("240", "1500"), ("30", "1500")):   # the second saturates: FitErrors
+        r = subprocess.run([K8S_BIN, n_nodes, n_pods], capture_output=True, text=True, timeout=300)
+        print(r.stdout, r.stderr)
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert "PASS" in r.stdout
