@@ -27,6 +27,7 @@
 #define PGF_IPA 2     // reads the InterPodAffinity priority (pass A min / max)
 #define PGF_SHARED 4  // its commit changes counts in a topology domain several nodes share
 #define PGF_VOL 8     // has a volume class
+#define PGF_NOHYP 16  // its commit leaves the rows' LDS image (gpu / ephemeral / scalar requests, shared domains)
 
 struct PgHdr {
   int32_t K, k1, k2, sp;  // reduce classes (K = k1 * k2), SelectorSpread pair or -1
@@ -71,7 +72,8 @@ enum {
   PGO_DOM,                                         // i32 [n_keys][chunk] topology domains
   PGO_CNT,                                         // i32 [n_pair][chunk] counted pairs, row form
   PGO_CAR,                                         // i64 [n_carry][chunk] carried terms, row form
-  PGO_X0, PGO_X1,                                  // two pod-context records
+  PGO_X0, PGO_X1, PGO_X2, PGO_X3,                  // four pod-context records (ring)
+  PGO_E1,                                          // PgEv [chunk] the rows' E1 evaluations (dual form)
   PGO_N
 };
 
@@ -82,9 +84,10 @@ struct PgDims {
   int32_t pslots;   // host-port slots per row (0: none)
   int32_t n_keys, n_pair, n_carry;
   int32_t rec_stride;
-  int32_t pad;
+  int32_t hyp;      // 1: the dual-hypothesis kernel's layout (PGO_E1 and four records)
 };
 #define PG_VS_LDS 8
+#define PG_EV_BYTES 40  // sizeof(PgEv) (ksim_pgen.hip)
 
 // Arguments beyond the context.  The affinity / volume descriptors travel by value (kernel
 // arguments stay in scalar registers instead of being re-read from HBM after every barrier).
@@ -108,6 +111,7 @@ struct PGenArgs {
   uint64_t spin_ticks;
 };
 
+extern "C" hipError_t ksim_launch_pgen2(const KsimCtx* c, const PGenArgs* g, int grid, int npt, size_t lds, hipStream_t s);
 extern "C" hipError_t ksim_launch_pgen(const KsimCtx* c, const PGenArgs* g, int grid, int npt, size_t lds, hipStream_t s);
 extern "C" hipError_t ksim_pgen_pack(const KsimCtx* c, const PGenArgs* g, hipStream_t s);
 // LDS plan for `chunk` rows per workgroup: fills off[], returns the dynamic LDS bytes.

@@ -180,13 +180,83 @@ __device__ __forceinline__ int32_t pg_vol_find(const PGenArgs& g, const PgL& L, 
   return -1;
 }
 
+// The previous pod p as a hypothesis on the evaluated row (the dual-hypothesis kernel): pod p+1
+// is evaluated both on the row as it stands and as it would stand with p committed to it, so the
+// owner of p's node needs no re-evaluation after the decision.  Only pods whose commit touches the
+// row alone and the LDS image (no gpu / ephemeral / scalar requests, no shared-domain affinity
+// counts) are hypotheses; the others take the re-evaluation path.
+struct PgHyp {
+  const PgX* X;    // pod p's record
+  const PgHdr* H;  // its uniform header
+};
+
+__device__ __forceinline__ bool pg_port_hit(uint64_t wk, uint64_t e) {
+  if ((e & 0xFFFFFFFFFFull) != (wk & 0xFFFFFFFFFFull)) return false;
+  const uint32_t wip = (uint32_t)(wk >> 40), eip = (uint32_t)(e >> 40);
+  return wip == 0 || eip == 0 || eip == wip;
+}
+
+// counted pair `pair` on row j (+1 when the hypothesis's identity matches it and j has its key)
+template <bool HYP>
+__device__ __forceinline__ int32_t pg_cnt(const PgL& L, const PgHyp& y, int32_t pair, int32_t j) {
+  int32_t v = L.cnt[(int64_t)pair * L.chunk + j];
+  if (HYP) {
+    const int2* mp = y.X->sec<int2>(PGS_MP);
+    for (int32_t x = 0; x < y.H->n_mp; ++x)
+      if (mp[x].x == pair && L.dom[(int64_t)mp[x].y * L.chunk + j] >= 0) v += 1;
+  }
+  return v;
+}
+
+// carried term e on row j (+ the hypothesis's carried amounts of e)
+template <bool HYP>
+__device__ __forceinline__ int64_t pg_car(const PgL& L, const PgHyp& y, int32_t e, int32_t j) {
+  int64_t v = L.car[(int64_t)e * L.chunk + j];
+  if (HYP) {
+    const PgCar* cr = y.X->sec<PgCar>(PGS_CAR);
+    for (int32_t x = 0; x < y.H->n_car; ++x)
+      if (cr[x].term == e && L.dom[(int64_t)cr[x].key * L.chunk + j] >= 0) v += cr[x].amount;
+  }
+  return v;
+}
+
+// the hypothesis's mounts of volume key k: read-write / read-only inline mounts, any mount
+template <bool HYP>
+__device__ __forceinline__ void pg_hyp_mounts(const PgHyp& y, int32_t key, uint32_t* rw, uint32_t* ro, bool* any) {
+  if (!HYP || !(y.H->fl & PGF_VOL)) return;
+  const int4* r = y.X->sec<int4>(PGS_REF);
+  for (int32_t x = 0; x < y.H->n_ref; ++x) {
+    if (r[x].x != key) continue;
+    const uint32_t f = (uint32_t)r[x].y;
+    *any = true;
+    if (f & KSIM_VOL_VIA_PVC) continue;
+    if (f & KSIM_VOL_READ_ONLY) *ro += 1;
+    else *rw += 1;
+  }
+}
+
 // The first failing predicate of predicatesOrdering (predicates.go:129-138) on row j (node i),
-// exactly the chain of ksim_predicates_a, over the LDS image and the pod's record.  0 = fits.
+// exactly the chain of ksim_predicates_a, over the LDS image and the pod's record (HYP: with the
+// hypothesis pod committed to the row: r carries its resources).  0 = fits.
+template <bool HYP>
 __device__ __forceinline__ uint32_t pg_predicates(const KsimCtx& c, const PGenArgs& g, const PgL& L, const PgX& X,
                                                   const ksim_pod& P, const PgHdr& H, int32_t j, int64_t i,
-                                                  const KsimRow& r, uint32_t st) {
+                                                  const KsimRow& r, uint32_t st, const PgHyp& y, uint64_t* sa = nullptr) {
   const uint32_t pr = c.preds;
   uint32_t m;
+#ifdef KSIM_STAMPS
+  uint64_t ts_ = __builtin_amdgcn_s_memtime();
+#define EV_T(k)                                          \
+  do {                                                   \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+    if (sa) sa[k] += t_ - ts_;                           \
+    ts_ = t_;                                            \
+  } while (0)
+#else
+#define EV_T(k) \
+  do {          \
+  } while (0)
+#endif
   if (pr & KSIM_P_CHECK_NODE_CONDITION) {
     m = r.fl & KSIM_COND_REASON_MASK;  // bit positions coincide with KSIM_R_*
     if (m) return m;
@@ -200,13 +270,12 @@ __device__ __forceinline__ uint32_t pg_predicates(const KsimCtx& c, const PGenAr
     const int32_t pcn = g.d.pslots ? L.pc[j] : 0;
     for (int32_t k = 0; k < H.n_port && !ports; ++k) {
       const uint64_t wk = want[k];
-      const uint32_t wip = (uint32_t)(wk >> 40);
-      const uint64_t wpp = wk & 0xFFFFFFFFFFull;
-      for (int32_t s = 0; s < pcn; ++s) {
-        const uint64_t e = L.pk[(int64_t)s * L.chunk + j];
-        if ((e & 0xFFFFFFFFFFull) != wpp) continue;
-        const uint32_t eip = (uint32_t)(e >> 40);
-        if (wip == 0 || eip == 0 || eip == wip) { ports = 1u << KSIM_R_HOST_PORTS; break; }
+      for (int32_t s = 0; s < pcn; ++s)
+        if (pg_port_hit(wk, L.pk[(int64_t)s * L.chunk + j])) { ports = 1u << KSIM_R_HOST_PORTS; break; }
+      if (HYP && !ports) {
+        const uint64_t* hp = y.X->sec<uint64_t>(PGS_PORT);
+        for (int32_t s = 0; s < y.H->n_port; ++s)
+          if (pg_port_hit(wk, hp[s])) { ports = 1u << KSIM_R_HOST_PORTS; break; }
       }
     }
   }
@@ -224,22 +293,29 @@ __device__ __forceinline__ uint32_t pg_predicates(const KsimCtx& c, const PGenAr
     m = ksim_resources(c, P, i, r);
     if (m) return m;
   }
+  EV_T(1);
   const bool vol = (H.fl & PGF_VOL) != 0;
   const int4* refs = X.sec<int4>(PGS_REF);
   const int32_t vcn = (vol && g.d.vcap) ? L.vc[j] : 0;
-  if ((pr & KSIM_P_DISK_CONFLICT) && vol && vcn) {
+  if ((pr & KSIM_P_DISK_CONFLICT) && vol && (vcn || (HYP && (y.H->fl & PGF_VOL)))) {
     // NoDiskConflict (predicates.go:276-285 over isVolumeConflict :220-265)
     for (int32_t x = 0; x < H.n_ref; ++x) {
       const int4 ref = refs[x];
       const uint32_t f = (uint32_t)ref.y;
       if (!(f & (KSIM_VOL_CONFLICT_ANY | KSIM_VOL_CONFLICT_RW))) continue;
       const int32_t s = pg_vol_find(g, L, j, i, vcn, ref.x);
-      if (s < 0) continue;
-      const uint64_t w = pg_slot_get(g, L, j, i, s);
-      const uint32_t rw = (uint32_t)(w & 0x7FFu), ro = (uint32_t)((w >> 11) & 0x7FFu);
+      uint32_t rw = 0, ro = 0;
+      bool any = false;
+      if (s >= 0) {
+        const uint64_t w = pg_slot_get(g, L, j, i, s);
+        rw = (uint32_t)(w & 0x7FFu);
+        ro = (uint32_t)((w >> 11) & 0x7FFu);
+      }
+      pg_hyp_mounts<HYP>(y, ref.x, &rw, &ro, &any);
       if ((f & KSIM_VOL_CONFLICT_ANY) ? (rw + ro > 0) : (rw > 0)) return 1u << KSIM_R_DISK_CONFLICT;
     }
   }
+  EV_T(2);
   if ((pr & KSIM_P_TAINTS) && (P.flags & KSIM_POD_NEED_TAINTS) && (st & PG_ST_TAINT)) return 1u << KSIM_R_TAINTS;
   if ((pr & KSIM_P_NOEXEC_TAINTS) && (P.flags & KSIM_POD_NEED_TAINTS) && (st & PG_ST_NOEXEC)) return 1u << KSIM_R_TAINTS;
   if ((pr & KSIM_P_LABEL_PRESENCE) && (r.fl & KSIM_N_LABEL_PRESENCE)) return 1u << KSIM_R_LABEL_PRESENCE;
@@ -258,9 +334,18 @@ __device__ __forceinline__ uint32_t pg_predicates(const KsimCtx& c, const PGenAr
         int32_t add = 0;
         for (int32_t x = 0; x < H.n_ref; ++x) {
           const int4 ref = refs[x];
-          if (((uint32_t)ref.y & KSIM_VOL_NEW) && ((uint32_t)ref.z & f) && pg_vol_find(g, L, j, i, vcn, ref.x) < 0) ++add;
+          if (!(((uint32_t)ref.y & KSIM_VOL_NEW) && ((uint32_t)ref.z & f)) || pg_vol_find(g, L, j, i, vcn, ref.x) >= 0) continue;
+          uint32_t rw = 0, ro = 0;
+          bool any = false;
+          pg_hyp_mounts<HYP>(y, ref.x, &rw, &ro, &any);
+          if (!any) ++add;
         }
-        const int32_t have = g.d.vcap ? (int32_t)L.vh[(int64_t)t * L.chunk + j] : 0;
+        int32_t have = g.d.vcap ? (int32_t)L.vh[(int64_t)t * L.chunk + j] : 0;
+        if (HYP && (y.H->fl & PGF_VOL)) {  // the hypothesis's keys this filter counts, not mounted yet
+          const int4* hr = y.X->sec<int4>(PGS_REF);
+          for (int32_t x = 0; x < y.H->n_ref; ++x)
+            if (((uint32_t)hr[x].y & KSIM_VOL_NEW) && ((uint32_t)hr[x].z & f) && pg_vol_find(g, L, j, i, vcn, hr[x].x) < 0) ++have;
+        }
         if (have + add > g.V.max_vols[t]) return 1u << KSIM_R_MAX_VOLUME_COUNT;
       }
     }
@@ -270,6 +355,7 @@ __device__ __forceinline__ uint32_t pg_predicates(const KsimCtx& c, const PGenAr
       if (!((X.sec<uint32_t>(PGS_ZOK)[ls >> 5] >> (ls & 31)) & 1u)) return 1u << KSIM_R_VOLUME_ZONE;
     }
   }
+  EV_T(3);
   if ((pr & KSIM_P_MEM_PRESSURE) && (P.flags & KSIM_POD_BEST_EFFORT) && (r.fl & KSIM_N_MEM_PRESSURE))
     return 1u << KSIM_R_MEM_PRESSURE;
   if ((pr & KSIM_P_DISK_PRESSURE) && (r.fl & KSIM_N_DISK_PRESSURE)) return 1u << KSIM_R_DISK_PRESSURE;
@@ -281,29 +367,32 @@ __device__ __forceinline__ uint32_t pg_predicates(const KsimCtx& c, const PGenAr
     const uint32_t base = 1u << KSIM_R_POD_AFFINITY;
     const int32_t* anti = X.sec<int32_t>(PGS_ANTI);
     for (int32_t x = 0; x < H.n_anti; ++x)
-      if (L.car[(int64_t)anti[x] * L.chunk + j] > 0) return base | (1u << KSIM_R_EXISTING_ANTI_AFFINITY);
+      if (pg_car<HYP>(L, y, anti[x], j) > 0) return base | (1u << KSIM_R_EXISTING_ANTI_AFFINITY);
     const int4* req = X.sec<int4>(PGS_REQ);
     for (int32_t x = 0; x < H.n_req; ++x) {
       const int4 t = req[x];
-      const bool match = L.dom[(int64_t)t.y * L.chunk + j] >= 0 && L.cnt[(int64_t)t.x * L.chunk + j] > 0;
+      const bool match = L.dom[(int64_t)t.y * L.chunk + j] >= 0 && pg_cnt<HYP>(L, y, t.x, j) > 0;
       if ((t.w & 0xFF) == KSIM_AFF_REQ_AFFINITY) {
-        if (!match && (!(t.w >> 8) || L.cnt[(int64_t)t.z * L.chunk + j] > 0)) return base | (1u << KSIM_R_AFFINITY_RULES);
+        if (!match && (!(t.w >> 8) || pg_cnt<HYP>(L, y, t.z, j) > 0)) return base | (1u << KSIM_R_AFFINITY_RULES);
       } else if (match) {
         return base | (1u << KSIM_R_ANTI_AFFINITY_RULES);
       }
     }
   }
+  EV_T(4);
   return 0;
 }
+#undef EV_T
 
 // CalculateInterPodAffinityPriority's per-node sum (interpod_affinity.go:124-214) before the
 // normalisation, over the row-form counts (0 on rows without the term's key, as in Go).
-__device__ __forceinline__ int64_t pg_interpod_raw(const PgL& L, const PgX& X, const PgHdr& H, int32_t j) {
+template <bool HYP>
+__device__ __forceinline__ int64_t pg_interpod_raw(const PgL& L, const PgX& X, const PgHdr& H, int32_t j, const PgHyp& y) {
   int64_t s = 0;
   const PgPref* pref = X.sec<PgPref>(PGS_PREF);
-  for (int32_t x = 0; x < H.n_pref; ++x) s += pref[x].weight * (int64_t)L.cnt[(int64_t)pref[x].pair * L.chunk + j];
+  for (int32_t x = 0; x < H.n_pref; ++x) s += pref[x].weight * (int64_t)pg_cnt<HYP>(L, y, pref[x].pair, j);
   const int32_t* prio = X.sec<int32_t>(PGS_PRIO);
-  for (int32_t x = 0; x < H.n_prio; ++x) s += L.car[(int64_t)prio[x] * L.chunk + j];
+  for (int32_t x = 0; x < H.n_prio; ++x) s += pg_car<HYP>(L, y, prio[x], j);
   return s;
 }
 
@@ -330,6 +419,96 @@ __device__ __forceinline__ char* pg_xrec(char* sm, const PGenArgs& g, int64_t r)
 }
 
 }  // namespace
+
+
+// ---- staging and write-back shared by both persistent forms ----
+__device__ __forceinline__ void pg_stage_rows(const KsimCtx& c, const PGenArgs& g, const PgL& L, int64_t lo, int32_t nrows,
+                                              int64_t chunk, int tid, int nthr) {
+  const int64_t n = c.n;
+  const int32_t vsl = g.d.vslots, vcap = g.d.vcap, psl = g.d.pslots;
+  for (int32_t j = tid; j < nrows; j += nthr) {
+    const int64_t i = lo + j;
+    L.ac[j] = c.alloc_cpu[i]; L.am[j] = c.alloc_mem[i];
+    L.rc[j] = c.req_cpu[i]; L.rm[j] = c.req_mem[i]; L.zc[j] = c.nz_cpu[i]; L.zm[j] = c.nz_mem[i];
+    L.al[j] = c.allowed_pods[i]; L.ct[j] = c.pod_count[i]; L.fl[j] = c.flags[i];
+    L.ls[j] = c.label_set[i]; L.ts[j] = c.taint_set[i];
+    if (psl) {
+      const int32_t pc = c.port_count[i];
+      L.pc[j] = pc;
+      for (int32_t s = 0; s < pc; ++s) L.pk[(int64_t)s * chunk + j] = c.ports[(int64_t)s * n + i];
+    }
+    if (vcap) {
+      const int32_t vc = g.V.slot_count[i];
+      L.vc[j] = vc;
+      uint32_t h0 = 0, h1 = 0, h2 = 0;
+      for (int32_t s = 0; s < vc; ++s) {
+        const uint64_t w = g.V.slots[(int64_t)s * n + i];
+        if (s < vsl) L.vs[(int64_t)s * chunk + j] = w;
+        const uint32_t f = g.V.key_filter[(int32_t)(w >> 32)];
+        h0 += f & 1u; h1 += (f >> 1) & 1u; h2 += (f >> 2) & 1u;
+      }
+      L.vh[j] = (uint16_t)h0; L.vh[chunk + j] = (uint16_t)h1; L.vh[2 * chunk + j] = (uint16_t)h2;
+    }
+  }
+  for (int32_t x = tid; x < g.d.n_keys * nrows; x += nthr) {
+    const int32_t k = x / nrows, j = x - k * nrows;
+    L.dom[(int64_t)k * chunk + j] = g.A.dom[(int64_t)k * n + lo + j];
+  }
+}
+
+__device__ __forceinline__ void pg_stage_counts(const KsimCtx& c, const PGenArgs& g, const PgL& L, int32_t nrows,
+                                                int64_t chunk, int tid, int nthr) {
+  // affinity counts in row form, from the canonical per-domain counts
+  for (int32_t x = tid; x < g.d.n_pair * nrows; x += nthr) {
+    const int32_t cp = x / nrows, j = x - cp * nrows;
+    const int32_t d = L.dom[(int64_t)g.A.pair_key[cp] * chunk + j];
+    L.cnt[(int64_t)cp * chunk + j] = d >= 0 ? g.A.cnt[g.A.pair_off[cp] + d] : 0;
+  }
+  for (int32_t x = tid; x < g.d.n_carry * nrows; x += nthr) {
+    const int32_t e = x / nrows, j = x - e * nrows;
+    const int32_t d = L.dom[(int64_t)g.A.carry_key[e] * chunk + j];
+    L.car[(int64_t)e * chunk + j] = d >= 0 ? g.A.carried[g.A.carry_off[e] + d] : 0;
+  }
+  if (g.d.n_st)  // static (pod class, row) words from the class tables
+    for (int32_t k = tid; k < g.d.n_st * nrows; k += nthr) {
+      const int32_t cls = k / nrows, j = k - cls * nrows;
+      L.st[(int64_t)cls * chunk + j] = (uint16_t)pg_static_word(c, cls, L.ls[j], L.ts[j]);
+    }
+}
+
+__device__ __forceinline__ void pg_write_back(const KsimCtx& c, const PGenArgs& g, const PgL& L, int64_t lo, int32_t nrows,
+                                              int64_t chunk, int tid, int nthr) {
+  const int64_t n = c.n;
+  const int32_t vsl = g.d.vslots, vcap = g.d.vcap, psl = g.d.pslots;
+  __syncthreads();
+  for (int32_t j = tid; j < nrows; j += nthr) {
+    const int64_t i = lo + j;
+    c.req_cpu[i] = L.rc[j]; c.req_mem[i] = L.rm[j]; c.nz_cpu[i] = L.zc[j]; c.nz_mem[i] = L.zm[j];
+    c.pod_count[i] = L.ct[j]; c.flags[i] = L.fl[j];
+    if (psl) {
+      const int32_t pc = L.pc[j];
+      c.port_count[i] = pc;
+      for (int32_t s = 0; s < pc; ++s) c.ports[(int64_t)s * n + i] = L.pk[(int64_t)s * chunk + j];
+    }
+    if (vcap) {
+      const int32_t vc = L.vc[j];
+      g.V.slot_count[i] = vc;
+      for (int32_t s = 0; s < vc && s < vsl; ++s) g.V.slots[(int64_t)s * n + i] = L.vs[(int64_t)s * chunk + j];
+    }
+  }
+  // canonical per-domain counts: every row of a domain holds the same value, so concurrent
+  // identical stores from several workgroups are benign
+  for (int32_t x = tid; x < g.d.n_pair * nrows; x += nthr) {
+    const int32_t cp = x / nrows, j = x - cp * nrows;
+    const int32_t d = L.dom[(int64_t)g.A.pair_key[cp] * chunk + j];
+    if (d >= 0) g.A.cnt[g.A.pair_off[cp] + d] = L.cnt[(int64_t)cp * chunk + j];
+  }
+  for (int32_t x = tid; x < g.d.n_carry * nrows; x += nthr) {
+    const int32_t e = x / nrows, j = x - e * nrows;
+    const int32_t d = L.dom[(int64_t)g.A.carry_key[e] * chunk + j];
+    if (d >= 0) g.A.carried[g.A.carry_off[e] + d] = L.car[(int64_t)e * chunk + j];
+  }
+}
 
 #ifdef KSIM_STAMPS
 // per-phase cycle sums of workgroup 0's thread 0 (s_memtime), written to c.dbg at the end
@@ -386,6 +565,7 @@ __global__ __launch_bounds__(64) void ksim_pgen_pack_kernel(KsimCtx c, PGenArgs 
     }
     H.n_port = P.port_cnt;
     H.n_scal = P.scalar_cnt;
+    if ((H.fl & PGF_SHARED) || P.add_gpu || P.add_eph || H.n_scal) H.fl |= PGF_NOHYP;
     uint32_t so[PGS_END + 1];
     pg_sections(H, so);
     if (so[PGS_END] > (uint32_t)g.d.rec_stride) {  // the host's bound is wrong: never write past the record
@@ -461,37 +641,9 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
   const int64_t n = c.n;
   PgL L = pg_lds(pg_smem, g, chunk);
   auto xrec = [&](int64_t r) { return pg_xrec(pg_smem, g, r); };
-  const int32_t vsl = g.d.vslots, vcap = g.d.vcap, psl = g.d.pslots;
+  const int32_t vcap = g.d.vcap, psl = g.d.pslots;
 
-  // ---- the workgroup's rows into LDS ----
-  for (int32_t j = tid; j < nrows; j += PG_BS) {
-    const int64_t i = lo + j;
-    L.ac[j] = c.alloc_cpu[i]; L.am[j] = c.alloc_mem[i];
-    L.rc[j] = c.req_cpu[i]; L.rm[j] = c.req_mem[i]; L.zc[j] = c.nz_cpu[i]; L.zm[j] = c.nz_mem[i];
-    L.al[j] = c.allowed_pods[i]; L.ct[j] = c.pod_count[i]; L.fl[j] = c.flags[i];
-    L.ls[j] = c.label_set[i]; L.ts[j] = c.taint_set[i];
-    if (psl) {
-      const int32_t pc = c.port_count[i];
-      L.pc[j] = pc;
-      for (int32_t s = 0; s < pc; ++s) L.pk[(int64_t)s * chunk + j] = c.ports[(int64_t)s * n + i];
-    }
-    if (vcap) {
-      const int32_t vc = g.V.slot_count[i];
-      L.vc[j] = vc;
-      uint32_t h0 = 0, h1 = 0, h2 = 0;
-      for (int32_t s = 0; s < vc; ++s) {
-        const uint64_t w = g.V.slots[(int64_t)s * n + i];
-        if (s < vsl) L.vs[(int64_t)s * chunk + j] = w;
-        const uint32_t f = g.V.key_filter[(int32_t)(w >> 32)];
-        h0 += f & 1u; h1 += (f >> 1) & 1u; h2 += (f >> 2) & 1u;
-      }
-      L.vh[j] = (uint16_t)h0; L.vh[chunk + j] = (uint16_t)h1; L.vh[2 * chunk + j] = (uint16_t)h2;
-    }
-  }
-  for (int32_t x = tid; x < g.d.n_keys * nrows; x += PG_BS) {
-    const int32_t k = x / nrows, j = x - k * nrows;
-    L.dom[(int64_t)k * chunk + j] = g.A.dom[(int64_t)k * n + lo + j];
-  }
+  pg_stage_rows(c, g, L, lo, nrows, chunk, tid, blockDim.x);
   // the pod-context record of the first pod
   {
     const uint4* src = reinterpret_cast<const uint4*>(g.rec);
@@ -502,22 +654,7 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
   if (tid < PG_MAXZ) s_z[tid] = 0;
   uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex (wave 0)
   __syncthreads();
-  // affinity counts in row form, from the canonical per-domain counts
-  for (int32_t x = tid; x < g.d.n_pair * nrows; x += PG_BS) {
-    const int32_t cp = x / nrows, j = x - cp * nrows;
-    const int32_t d = L.dom[(int64_t)g.A.pair_key[cp] * chunk + j];
-    L.cnt[(int64_t)cp * chunk + j] = d >= 0 ? g.A.cnt[g.A.pair_off[cp] + d] : 0;
-  }
-  for (int32_t x = tid; x < g.d.n_carry * nrows; x += PG_BS) {
-    const int32_t e = x / nrows, j = x - e * nrows;
-    const int32_t d = L.dom[(int64_t)g.A.carry_key[e] * chunk + j];
-    L.car[(int64_t)e * chunk + j] = d >= 0 ? g.A.carried[g.A.carry_off[e] + d] : 0;
-  }
-  if (g.d.n_st)  // static (pod class, row) words from the class tables
-    for (int32_t k = tid; k < g.d.n_st * nrows; k += PG_BS) {
-      const int32_t cls = k / nrows, j = k - cls * nrows;
-      L.st[(int64_t)cls * chunk + j] = (uint16_t)pg_static_word(c, cls, L.ls[j], L.ts[j]);
-    }
+  pg_stage_counts(c, g, L, nrows, chunk, tid, blockDim.x);
   __syncthreads();
 
   for (int64_t pod = c.first; pod < c.end; ++pod) {
@@ -559,7 +696,7 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
       r.allowed = L.al[j]; r.count = L.ct[j]; r.fl = L.fl[j];
       const uint32_t st = g.d.n_st ? (uint32_t)L.st[(int64_t)P.cls * chunk + j] : pg_static_word(c, P.cls, L.ls[j], L.ts[j]);
       if (k == 0) PG_STAMP(8);
-      const uint32_t m = pg_predicates(c, g, L, X, P, H, j, i, r, st);
+      const uint32_t m = pg_predicates<false>(c, g, L, X, P, H, j, i, r, st, PgHyp{});
       if (k == 0) PG_STAMP(9);
       rmk[k] = m;
       if (m) continue;
@@ -567,7 +704,7 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
       sc[k] = ksim_map_score(c, P, r);
       if (k == 0) PG_STAMP(10);
       cl[k] = (k1 > 1 ? (int32_t)((st >> 4) & 15u) : 0) * k2 + (k2 > 1 ? (int32_t)((st >> 8) & 15u) : 0);
-      if (ipa) raw[k] = pg_interpod_raw(L, X, H, j);
+      if (ipa) raw[k] = pg_interpod_raw<false>(L, X, H, j, PgHyp{});
       if (sp >= 0) {
         cnt[k] = L.cnt[(int64_t)sp * chunk + j];
         zz[k] = g.A.zone_key >= 0 ? L.dom[(int64_t)g.A.zone_key * chunk + j] : -1;
@@ -1102,34 +1239,846 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
     PG_STAMP(5);
   }
   // ---- the table is authoritative in HBM between calls: write the owned rows back ----
+  pg_write_back(c, g, L, lo, nrows, chunk, tid, blockDim.x);
+  if (blockIdx.x == 0 && tid == 0) {
+    *c.counter = counter;
+    *c.cursor = c.end;
+#ifdef KSIM_STAMPS
+    for (int k = 0; k < 16; ++k) c.dbg[k] += st_acc[k];
+#endif
+  }
+}
+
+// ===================================================================================================
+// The dual-hypothesis form (the default): wave 0 is the control wave (exchange, decision), waves 1-3
+// own the rows (row j = k * 192 + thread - 64).  While wave 0 sweeps pod p's class granules and
+// decides, the row threads evaluate pod p+1 on every row twice — as the row stands (E0) and with
+// pod p committed to it (E1, PgHyp) — so after the decision the owner's selected row swaps in its E1
+// entry and every other row keeps E0: no evaluation sits between one decision and the next pass-A
+// reduction.  The commit itself is deferred into the next exchange window.  Pods whose commit
+// leaves the row's LDS image (gpu / ephemeral / scalar requests, shared-domain affinity counts) are
+// no hypotheses (PGF_NOHYP): their node is committed at once and pod p+1 re-evaluated.
+#define PG2_BS 512
+#define PG2_NW (PG2_BS / 64)
+#define PG_RT 192  // rows per thread slot: waves 1-3 (E0, the row state), waves 5-7 (E1)
+#define PG_RW 3
+
+struct PgEv {
+  int64_t sc, raw;
+  int32_t cnt, cl, zz;
+  uint32_t rmk;
+  bool fit;
+};
+static_assert(sizeof(PgEv) == PG_EV_BYTES, "PgEv layout");
+
+namespace {
+
+template <bool HYP>
+__device__ __forceinline__ PgEv pg_eval(const KsimCtx& c, const PGenArgs& g, const PgL& L, const PgX& X, const ksim_pod& P,
+                                        const PgHdr& H, int32_t j, int64_t i, const PgHyp& y, const ksim_pod& Py,
+                                        uint64_t* sa = nullptr) {
+  PgEv e{0, 0, 0, 0, -1, 0, false};
+#ifdef KSIM_STAMPS
+  uint64_t t0_ = __builtin_amdgcn_s_memtime();
+#endif
+  KsimRow r;
+  r.ac = L.ac[j]; r.am = L.am[j]; r.rc = L.rc[j]; r.rm = L.rm[j]; r.zc = L.zc[j]; r.zm = L.zm[j];
+  r.allowed = L.al[j]; r.count = L.ct[j]; r.fl = L.fl[j];
+  if (HYP) {  // NodeInfo.AddPod of the hypothesis (node_info.go:318-341): requests, non-zero requests, count
+    const ksim_pod& Pr = y.X->pod();  // add_* are not in the uniform copy
+    r.rc += Pr.add_cpu; r.rm += Pr.add_mem; r.zc += Py.nz_cpu; r.zm += Py.nz_mem; r.count += 1;
+  }
+  const uint32_t st = g.d.n_st ? (uint32_t)L.st[(int64_t)P.cls * L.chunk + j] : pg_static_word(c, P.cls, L.ls[j], L.ts[j]);
+#ifdef KSIM_STAMPS
+  if (sa) sa[0] += __builtin_amdgcn_s_memtime() - t0_;
+#endif
+  const uint32_t m = pg_predicates<HYP>(c, g, L, X, P, H, j, i, r, st, y, sa);
+#ifdef KSIM_STAMPS
+  t0_ = __builtin_amdgcn_s_memtime();
+#endif
+  e.rmk = m;
+  if (m) return e;
+  e.fit = true;
+  e.sc = ksim_map_score(c, P, r);
+  e.cl = (H.k1 > 1 ? (int32_t)((st >> 4) & 15u) : 0) * H.k2 + (H.k2 > 1 ? (int32_t)((st >> 8) & 15u) : 0);
+  if (H.fl & PGF_IPA) e.raw = pg_interpod_raw<HYP>(L, X, H, j, y);
+  if (H.sp >= 0) {
+    e.cnt = pg_cnt<HYP>(L, y, H.sp, j);
+    e.zz = g.A.zone_key >= 0 ? L.dom[(int64_t)g.A.zone_key * L.chunk + j] : -1;
+  }
+#ifdef KSIM_STAMPS
+  if (sa) sa[5] += __builtin_amdgcn_s_memtime() - t0_;
+#endif
+  return e;
+}
+
+// NodeInfo.AddPod of pod (X, P, H) on row jsel = node w, on the LDS image (+ HBM side columns):
+// resources, gpu / ephemeral / scalar requests, host ports, volume mounts and — unless the counts
+// live in shared domains (applied by every workgroup) — the pod's affinity counts on its row.
+__device__ __forceinline__ void pg_commit_row(const KsimCtx& c, const PGenArgs& g, const PgL& L, const PgX& X,
+                                              const PgHdr& H, int32_t jsel, int64_t w) {
+  const ksim_pod& Pr = X.pod();
+  const int64_t n = c.n, chunk = L.chunk;
+  L.rc[jsel] += Pr.add_cpu; L.rm[jsel] += Pr.add_mem; L.zc[jsel] += Pr.nz_cpu; L.zm[jsel] += Pr.nz_mem;
+  L.ct[jsel] += 1;
+  const int64_t agpu = Pr.add_gpu, aeph = Pr.add_eph;
+  if (agpu | aeph) {
+    const int64_t gg = c.req_gpu[w] + agpu, ge = c.req_eph[w] + aeph;
+    c.req_gpu[w] = gg;
+    c.req_eph[w] = ge;
+    uint32_t fl = L.fl[jsel] & ~(KSIM_N_GPU_OVER | KSIM_N_EPH_OVER);
+    if (c.alloc_gpu[w] < gg) fl |= KSIM_N_GPU_OVER;
+    if (c.alloc_eph[w] < ge) fl |= KSIM_N_EPH_OVER;
+    L.fl[jsel] = fl;
+  }
+  const ksim_scalar_req* sr = X.sec<ksim_scalar_req>(PGS_SCAL);
+  for (int32_t s = 0; s < H.n_scal; ++s) c.req_scalar[(int64_t)sr[s].col * n + w] += sr[s].add;
+  // HostPortInfo.Add (utils.go:45-60)
+  const int32_t psl = g.d.pslots, vcap = g.d.vcap;
+  const uint64_t* pk = X.sec<uint64_t>(PGS_PORT);
+  for (int32_t k = 0; k < H.n_port; ++k) {
+    const uint64_t key = pk[k];
+    const int32_t cnt0 = psl ? L.pc[jsel] : 0;
+    bool dup = false;
+    for (int32_t s = 0; s < cnt0; ++s)
+      if (L.pk[(int64_t)s * chunk + jsel] == key) { dup = true; break; }
+    if (dup) continue;
+    if (cnt0 >= psl) { atomicOr(c.err, 1); continue; }
+    L.pk[(int64_t)cnt0 * chunk + jsel] = key;
+    L.pc[jsel] = cnt0 + 1;
+  }
+  if (H.fl & PGF_VOL) {  // ksim_vol_commit with sign +1
+    const int4* refs = X.sec<int4>(PGS_REF);
+    for (int32_t x = 0; x < H.n_ref; ++x) {
+      const int4 ref = refs[x];
+      const uint32_t f = (uint32_t)ref.y;
+      const int sh = (f & KSIM_VOL_VIA_PVC) ? 22 : (f & KSIM_VOL_READ_ONLY) ? 11 : 0;
+      const uint64_t fmask = (sh == 22 ? 0x3FFull : 0x7FFull) << sh;
+      const uint64_t one = 1ull << sh;
+      const int32_t cnt0 = vcap ? L.vc[jsel] : 0;
+      const int32_t s = pg_vol_find(g, L, jsel, w, cnt0, ref.x);
+      if (s >= 0) {
+        uint64_t& sw = *pg_slot(g, L, jsel, w, s);
+        if ((sw & fmask) == fmask) atomicOr(c.err, 1);
+        else sw += one;
+      } else if (cnt0 >= vcap) {
+        atomicOr(c.err, 1);
+      } else {
+        *pg_slot(g, L, jsel, w, cnt0) = ((uint64_t)(uint32_t)ref.x << 32) | one;
+        L.vc[jsel] = cnt0 + 1;
+        const uint32_t kf = (uint32_t)ref.z;
+        for (int t = 0; t < 3; ++t)
+          if ((kf >> t) & 1u) L.vh[(int64_t)t * chunk + jsel] += 1;
+      }
+    }
+  }
+  if ((H.fl & PGF_AFF) && !(H.fl & PGF_SHARED)) {  // node-like keys: only this row's counts change
+    const int2* mp = X.sec<int2>(PGS_MP);
+    for (int32_t x = 0; x < H.n_mp; ++x)
+      if (L.dom[(int64_t)mp[x].y * chunk + jsel] >= 0) L.cnt[(int64_t)mp[x].x * chunk + jsel] += 1;
+    const PgCar* cr = X.sec<PgCar>(PGS_CAR);
+    for (int32_t x = 0; x < H.n_car; ++x)
+      if (L.dom[(int64_t)cr[x].key * chunk + jsel] >= 0) L.car[(int64_t)cr[x].term * chunk + jsel] += cr[x].amount;
+  }
+}
+
+// Reduce within each group of 8 lanes (every lane of the group gets the group's result): op 0 min,
+// 1 max, 2 sum, per lane.
+__device__ __forceinline__ int64_t pg_red8_step(int64_t acc, int64_t t, int op) {
+  return op == 0 ? (t < acc ? t : acc) : (op == 1 ? (t > acc ? t : acc) : acc + t);
+}
+__device__ __forceinline__ int64_t pg_red8(int64_t acc, int op) {
+  acc = pg_red8_step(acc, ksimw::dpp64<ksimw::QP_1032>(acc, acc), op);
+  acc = pg_red8_step(acc, ksimw::dpp64<ksimw::QP_2301>(acc, acc), op);
+  acc = pg_red8_step(acc, ksimw::dpp64<ksimw::ROW_HALF_MIRROR>(acc, acc), op);
+  return acc;
+}
+
+__device__ __forceinline__ char* pg_xrec4(char* sm, const PGenArgs& g, int64_t r) {
+  return sm + g.off[PGO_X0] + (uint32_t)(r & 3) * (g.off[PGO_X1] - g.off[PGO_X0]);
+}
+
+}  // namespace
+
+template <int NPT, int MB>
+__global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenArgs g_arg) {
+  extern __shared__ __attribute__((aligned(16))) char pg_smem[];
+  __shared__ int64_t s_a[4][PG2_NW];                  // pass A per wave: min, max, max count, haveZones
+  __shared__ unsigned long long s_z[PG_MAXZ];        // pass A zone sums of this workgroup
+  __shared__ int64_t s_g[5];                         // pass A over the grid
+  __shared__ int64_t s_gz[PG_MAXZ];                  // countsByZone over the grid
+  __shared__ int32_t s_mx[PG2_NW][KSIM_MAX_RCLASS];  // class partials per wave (only waves 1-3 hold rows)
+  __shared__ int32_t s_cn[PG2_NW][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_fit[PG2_NW];
+  __shared__ int32_t s_mode, s_blk, s_rank, s_abort;
+  __shared__ uint32_t s_win;
+  __shared__ int32_t s_tgt[KSIM_MAX_RCLASS];
+  __shared__ int64_t s_node;
+  __shared__ int32_t s_dw[PG_MAXL * 2];
+  __shared__ uint64_t s_bal[NPT][PG_RW];             // owner: each row wave's ballot of its rows at the chosen score
+#ifdef KSIM_STAMPS
+  uint64_t st_acc[16] = {};
+  uint64_t t_prev = __builtin_amdgcn_s_memtime();
+  uint64_t ev_acc = 0, ev_acc1 = 0;  // threads 64 / 320: their rows' E0 / E1 evaluations
+  uint64_t ev_sa[6] = {};
+  uint64_t cm_acc = 0, cm_n = 0, ps_acc = 0, pr_acc = 0, cs_acc = 0, t_pub = 0;
+#endif
+  const KsimCtx& c = c_arg;
+  const PGenArgs& g = g_arg;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const bool rowt = wv >= 1 && wv <= 3;  // E0: the row state
+  const bool hypt = wv >= 5;             // E1: the same rows under the hypothesis
+  const int rt = rowt ? tid - 64 : tid - 320;
+  const int G = gridDim.x;
+  const int64_t chunk = c.chunk;
+  const int64_t lo = (int64_t)blockIdx.x * chunk;
+  const int64_t hi = (lo + chunk < c.n) ? lo + chunk : c.n;
+  const int32_t nrows = (int32_t)(hi - lo);
+  const int64_t n = c.n;
+  const PgL L = pg_lds(pg_smem, g, chunk);
+  auto xrec = [&](int64_t r) { return pg_xrec4(pg_smem, g, r); };
+  PgEv* ev1 = reinterpret_cast<PgEv*>(pg_smem + g.off[PGO_E1]);
+
+  pg_stage_rows(c, g, L, lo, nrows, chunk, tid, blockDim.x);
+  for (int64_t q = c.first; q < c.end && q < c.first + 2; ++q) {  // the records of the first two pods
+    const uint4* src = reinterpret_cast<const uint4*>(g.rec + (q - c.first) * (int64_t)g.d.rec_stride);
+    uint4* dst = reinterpret_cast<uint4*>(xrec(q));
+    for (int32_t x = tid; x < g.d.rec_stride / 16; x += PG2_BS) dst[x] = src[x];
+  }
+  if (tid == 0) s_abort = 0;
+  if (tid < PG_MAXZ) s_z[tid] = 0;
+  uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex (wave 0)
   __syncthreads();
-  for (int32_t j = tid; j < nrows; j += PG_BS) {
-    const int64_t i = lo + j;
-    c.req_cpu[i] = L.rc[j]; c.req_mem[i] = L.rm[j]; c.nz_cpu[i] = L.zc[j]; c.nz_mem[i] = L.zm[j];
-    c.pod_count[i] = L.ct[j]; c.flags[i] = L.fl[j];
-    if (psl) {
-      const int32_t pc = L.pc[j];
-      c.port_count[i] = pc;
-      for (int32_t s = 0; s < pc; ++s) c.ports[(int64_t)s * n + i] = L.pk[(int64_t)s * chunk + j];
+  pg_stage_counts(c, g, L, nrows, chunk, tid, blockDim.x);
+  __syncthreads();
+
+  // pod `first` on every row, as the rows stand
+  PgEv cur[NPT];
+  {
+    PgX X0;
+    X0.base = xrec(c.first);
+    const PgHdr H0 = pg_hdr_u(X0.hdr());
+    pg_sections(H0, X0.so);
+    const ksim_pod P0 = pg_pod_u(X0.pod());
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int32_t j = k * PG_RT + rt;
+      cur[k] = PgEv{0, 0, 0, 0, -1, 0, false};
+      if (rowt && j < nrows) cur[k] = pg_eval<false>(c, g, L, X0, P0, H0, j, lo + j, PgHyp{}, P0);
     }
-    if (vcap) {
-      const int32_t vc = L.vc[j];
-      g.V.slot_count[i] = vc;
-      for (int32_t s = 0; s < vc && s < vsl; ++s) g.V.slots[(int64_t)s * n + i] = L.vs[(int64_t)s * chunk + j];
+  }
+  int32_t pend_j = -1;   // deferred commit of pod pend_pod on row pend_j (its row thread)
+  int64_t pend_pod = -1;
+
+  for (int64_t pod = c.first; pod < c.end; ++pod) {
+    PgX X;
+    X.base = xrec(pod);
+    const PgHdr H = pg_hdr_u(X.hdr());
+    pg_sections(H, X.so);
+    const ksim_pod P = pg_pod_u(X.pod());
+    const int K = H.K, k1 = H.k1, k2 = H.k2;
+    const bool ipa = (H.fl & PGF_IPA) != 0;
+    const int32_t sp = H.sp;
+    const uint32_t tag = (uint32_t)((pod - c.first + 1) & 0xFF);
+    const int slot = (int)(pod % PG_NSLOT);
+    const bool has_next = pod + 1 < c.end;
+    // wave 4 copies pod p+2's record into LDS in the decision window (its buffer held pod p-2's)
+    const bool pf = wv == 4 && pod + 2 < c.end;
+
+    // ---- pass A over the grid (pods that read InterPodAffinity / SelectorSpread) ----
+    if (ipa || sp >= 0) {
+      int64_t mn = 0, mx = 0, smx = 0, hz = 0;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        if (!cur[k].fit) continue;
+        mn = cur[k].raw < mn ? cur[k].raw : mn;
+        mx = cur[k].raw > mx ? cur[k].raw : mx;
+        smx = cur[k].cnt > smx ? cur[k].cnt : smx;
+        if (cur[k].zz >= 0) {
+          hz = 1;
+          if (cur[k].cnt) atomicAdd(&s_z[cur[k].zz], (unsigned long long)cur[k].cnt);
+        }
+      }
+      if (ipa) { mn = ksimw::min_i64(mn); mx = ksimw::max_i64(mx); }
+      if (sp >= 0) { smx = ksimw::max_i32((int32_t)smx); hz = __ballot(hz != 0) ? 1 : 0; }
+      if (lane == 0) { s_a[0][wv] = mn; s_a[1][wv] = mx; s_a[2][wv] = smx; s_a[3][wv] = hz; }
+      __syncthreads();
+      PG_STAMP(6);
+      if (wv == 0) {
+        const int nz = sp >= 0 ? g.n_zone : 0;
+        const int RA = 4 + nz;
+        if (lane < RA) {
+          int64_t v;
+          if (lane < 4) {
+            v = s_a[lane][0];
+#pragma unroll
+            for (int w = 1; w < PG2_NW; ++w) v = lane == 0 ? (s_a[0][w] < v ? s_a[0][w] : v) : (s_a[lane][w] > v ? s_a[lane][w] : v);
+          } else {
+            v = (int64_t)s_z[lane - 4];
+            s_z[lane - 4] = 0;
+          }
+          pg_store(rec_at(g.gran, slot, lane, blockIdx.x), ((uint64_t)tag << 56) | ((uint64_t)(v + B55) & M56));
+        }
+#ifdef KSIM_STAMPS
+        t_pub = __builtin_amdgcn_s_memtime();
+#endif
+        // transposed sweep: lane l reads word w0 + l / 8 of workgroups l % 8, l % 8 + 8, ... (G <= 64),
+        // folds them, and one 3-step DPP chain within each group of 8 lanes reduces every word at once
+        int64_t r0 = 0, zmax = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool ok = true;
+        for (int w0 = 0; w0 < RA && ok; w0 += 8) {
+          const int word = w0 + (lane >> 3);
+          const bool wl = word < RA;
+          uint64_t v[8];
+          for (;;) {
+            bool mine = true;
+#pragma unroll
+            for (int m = 0; m < 8; ++m) {
+              const int b = (lane & 7) + 8 * m;
+              v[m] = (wl && b < G) ? pg_load(rec_at(g.gran, slot, word, b)) : ((uint64_t)tag << 56);
+              mine &= gtag(v[m]) == tag;
+            }
+            if (__all(mine)) break;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > g.spin_ticks) { ok = false; break; }
+            __builtin_amdgcn_s_sleep(1);
+          }
+          if (!ok) break;
+#ifdef KSIM_STAMPS
+          {
+            const uint64_t t_ = __builtin_amdgcn_s_memtime();
+            ps_acc += t_ - t_pub;
+            t_pub = t_;
+          }
+#endif
+          const int op = word == 0 ? 0 : (word < 4 ? 1 : 2);  // min, max, sum
+          int64_t acc = op == 0 ? INT64_MAX : (op == 1 ? INT64_MIN : 0);
+#pragma unroll
+          for (int m = 0; m < 8; ++m) {
+            if (!wl || (lane & 7) + 8 * m >= G) continue;
+            const int64_t x = (int64_t)(v[m] & M56) - B55;
+            acc = op == 0 ? (x < acc ? x : acc) : (op == 1 ? (x > acc ? x : acc) : acc + x);
+          }
+          acc = pg_red8(acc, op);
+          if (w0 == 0) r0 = acc;
+          if (wl && word >= 4) {
+            zmax = acc > zmax ? acc : zmax;
+            if ((lane & 7) == 0) s_gz[word - 4] = acc;
+          }
+        }
+        if (nz) zmax = ksimw::max_i64(zmax);
+        const int64_t a_mn = ipa ? ksimw::readlane64(r0, 0) : 0, a_mx = ipa ? ksimw::readlane64(r0, 8) : 0;
+        const int64_t a_smx = sp >= 0 ? ksimw::readlane64(r0, 16) : 0, a_hz = sp >= 0 ? ksimw::readlane64(r0, 24) : 0;
+#ifdef KSIM_STAMPS
+        pr_acc += __builtin_amdgcn_s_memtime() - t_pub;
+#endif
+        if (!ok) {
+          if (lane == 0) { atomicOr(c.err, 4); s_abort = 1; }
+        } else if (lane == 0) {
+          s_g[0] = a_mn < 0 ? a_mn : 0;  // the accumulators start at 0 (interpod_affinity.go:129-131)
+          s_g[1] = a_mx > 0 ? a_mx : 0;
+          s_g[2] = a_smx; s_g[3] = a_hz;
+          s_g[4] = zmax;
+        }
+      } else if (pend_j >= 0) {
+        // the previous pod's deferred commit, inside this exchange window
+        PgX Xp;
+        Xp.base = xrec(pend_pod);
+        const PgHdr Hp = pg_hdr_u(Xp.hdr());
+        pg_sections(Hp, Xp.so);
+#ifdef KSIM_STAMPS
+        const uint64_t tc0 = __builtin_amdgcn_s_memtime();
+#endif
+        pg_commit_row(c, g, L, Xp, Hp, pend_j, lo + pend_j);
+#ifdef KSIM_STAMPS
+        cm_acc += __builtin_amdgcn_s_memtime() - tc0;
+        cm_n += 1;
+#endif
+        pend_j = -1;
+      }
+      __syncthreads();
+      if (s_abort) break;
+      const int64_t gmn = s_g[0], gmx = s_g[1], gsmx = s_g[2], ghz = s_g[3], gzm = s_g[4];
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        if (!cur[k].fit) continue;
+        if (ipa)
+          cur[k].sc = (int64_t)((uint64_t)cur[k].sc +
+                                (uint64_t)c.w[KSIM_W_INTERPOD_AFFINITY] * (uint64_t)ksim_interpod_score(cur[k].raw, gmn, gmx));
+        if (sp >= 0)
+          cur[k].sc = (int64_t)((uint64_t)cur[k].sc +
+                                (uint64_t)c.w[KSIM_W_SELECTOR_SPREAD] *
+                                    (uint64_t)ksim_spread_score(cur[k].cnt, gsmx, ghz != 0, cur[k].zz,
+                                                                cur[k].zz >= 0 ? s_gz[cur[k].zz] : 0, gzm));
+      }
+    }
+    if (pend_j >= 0) {  // the previous pod's deferred commit, when no pass-A window took it
+      PgX Xp;
+      Xp.base = xrec(pend_pod);
+      const PgHdr Hp = pg_hdr_u(Xp.hdr());
+      pg_sections(Hp, Xp.so);
+#ifdef KSIM_STAMPS
+      const uint64_t tc0 = __builtin_amdgcn_s_memtime();
+#endif
+      pg_commit_row(c, g, L, Xp, Hp, pend_j, lo + pend_j);
+#ifdef KSIM_STAMPS
+      cm_acc += __builtin_amdgcn_s_memtime() - tc0;
+      cm_n += 1;
+#endif
+      pend_j = -1;
+    }
+    PG_STAMP(1);
+
+    // ---- per reduce class (max, count) and fit count of this workgroup's rows ----
+    int32_t nf = 0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) nf += __popcll(__ballot(cur[k].fit));
+    if (lane == 0) s_fit[wv] = nf;
+    for (int q = 0; q < K; ++q) {
+      int32_t v = -1;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k)
+        if (cur[k].fit && cur[k].cl == q && (int32_t)cur[k].sc > v) v = (int32_t)cur[k].sc;
+      const int32_t wm = ksimw::max_i32(v);
+      int32_t cn = 0;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) cn += __popcll(__ballot(cur[k].fit && cur[k].cl == q && (int32_t)cur[k].sc == wm));
+      if (lane == 0) { s_mx[wv][q] = wm; s_cn[wv][q] = wm < 0 ? 0 : cn; }
+    }
+    __syncthreads();
+    PG_STAMP(2);
+
+    // ---- wave 0: publish, sweep, decide; row threads: pod p+1 on every row, E0 and E1 ----
+    PgEv n0[NPT];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) n0[k] = PgEv{0, 0, 0, 0, -1, 0, false};
+    if (wv == 0) {
+      if (lane < K) {
+        int32_t m = -1, nn = 0, f = 0;
+#pragma unroll
+        for (int w = 0; w < PG2_NW; ++w) {
+          f += s_fit[w];
+          if (!s_cn[w][lane]) continue;
+          if (s_mx[w][lane] > m) { m = s_mx[w][lane]; nn = s_cn[w][lane]; }
+          else if (s_mx[w][lane] == m) nn += s_cn[w][lane];
+        }
+        const uint64_t v = ((uint64_t)tag << 56) | (lane == 0 ? ((uint64_t)f << 44) : 0) | ((uint64_t)nn << 32) |
+                           (uint64_t)(uint32_t)m;
+        pg_store(cls_at(g.gran, slot, lane, blockIdx.x), v);
+      }
+#ifdef KSIM_STAMPS
+      t_pub = __builtin_amdgcn_s_memtime();
+#endif
+      // the decision's per-class map values (lane q = reduce class q)
+      int64_t tv_l = 0, av_l = 0, ad_l = 0;
+      if (lane < K) {
+        tv_l = X.tv(K > 1 ? lane / k2 : 0);
+        av_l = X.av(K > 1 ? lane % k2 : 0);
+        ad_l = X.ad(K > 1 ? lane % k2 : 0);
+      }
+      int mode = 0, blk = -1, rank = 0;
+      uint32_t win = 0;
+      int32_t tgt_l = -2;  // lane q: class q's maximum if q wins
+      // the workgroup holding the ix-th match from the top (lane-major workgroup order: lane l
+      // holds l, l + 64, ...; name rank grows with the workgroup index), bm = matches per workgroup
+      auto locate = [&](const int32_t (&bm)[MB], int64_t ix) {
+        // matches in workgroups above b = (lanes above, same m) + (every lane, higher m)
+        int64_t above = 0;
+        int found = -1, rk = 0;
+#pragma unroll
+        for (int m = MB - 1; m >= 0; --m) {
+        if (found < 0 && 64 * m < G) {
+          const int32_t pre = ksimw::prefix_incl_i32(bm[m]);
+          const int32_t tot = __builtin_amdgcn_readlane(pre, 63);
+          const int64_t ab = above + (int64_t)(tot - pre);
+          const bool hit = bm[m] > 0 && ix >= ab && ix < ab + bm[m];
+          const uint64_t hb = __ballot(hit);
+          if (hb) {
+            const int src = __builtin_ffsll((long long)hb) - 1;
+            found = src + 64 * m;
+            rk = (int)__builtin_amdgcn_readlane((int32_t)(ix - ab), src);
+          }
+          above += tot;
+        }
+        }
+        if (found < 0) { mode = -1; if (lane == 0) atomicOr(c.err, 2); }
+        blk = found;
+        rank = rk;
+      };
+      if (K == 1) {
+        // one reduce class (no TaintToleration / NodeAffinity spread among the fit nodes): the
+        // class maximum is the best total, and only granule 0 of each workgroup is read
+        uint64_t gv0[MB];
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool ok = false;
+        for (;;) {
+          bool mine = true;
+#pragma unroll
+          for (int m = 0; m < MB; ++m) {
+            const int b = lane + 64 * m;
+            gv0[m] = b < G ? pg_load(cls_at(g.gran, slot, 0, b)) : ((uint64_t)tag << 56);
+            mine &= gtag(gv0[m]) == tag;
+          }
+          if (__all(mine)) { ok = true; break; }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > g.spin_ticks) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+#ifdef KSIM_STAMPS
+        cs_acc += __builtin_amdgcn_s_memtime() - t_pub;
+        if (blockIdx.x == 0 && tid == 0) PG_STAMP(7);
+#endif
+        if (!ok) {
+          mode = -1;
+          if (lane == 0) atomicOr(c.err, 4);
+        } else {
+          int32_t f = 0, mm = -1, cc = 0;
+#pragma unroll
+          for (int m = 0; m < MB; ++m) {
+            if (lane + 64 * m >= G) continue;
+            f += gfit(gv0[m]);
+            const int32_t cn = gcnt(gv0[m]), sc0 = gscore(gv0[m]);
+            if (!cn) continue;
+            if (sc0 > mm) { mm = sc0; cc = cn; }
+            else if (sc0 == mm) cc += cn;
+          }
+          const int32_t F = ksimw::sum_i32(f);
+          if (F > 0) {
+            mode = 1;
+            int64_t ix = 0;
+            int32_t M0 = -1;
+            if (F > 1) {  // generic_scheduler.go:153-156: a single fit skips selectHost
+              mode = 2;
+              M0 = ksimw::max_i32(cc ? mm : -1);
+              const int32_t C = ksimw::sum_i32((cc && mm == M0) ? cc : 0);
+              win = 1;
+              tgt_l = lane == 0 ? M0 : -2;
+              ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)C) : (int64_t)((uint32_t)counter % (uint32_t)C);
+              counter += 1;  // generic_scheduler.go:192-195
+            }
+            int32_t bm[MB];
+#pragma unroll
+            for (int m = 0; m < MB; ++m) {
+              int32_t sb = 0;
+              if (lane + 64 * m < G)
+                sb = mode == 1 ? gfit(gv0[m]) : ((gcnt(gv0[m]) && gscore(gv0[m]) == M0) ? gcnt(gv0[m]) : 0);
+              bm[m] = sb;
+            }
+            locate(bm, ix);
+          }
+        }
+      } else {
+        uint64_t gv[KSIM_MAX_RCLASS][MB];
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        bool ok = false;
+        for (;;) {
+          bool mine = true;
+#pragma unroll
+          for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
+#pragma unroll
+            for (int m = 0; m < MB; ++m) {
+              const int b = lane + 64 * m;
+              gv[q][m] = (q < K && b < G) ? pg_load(cls_at(g.gran, slot, q, b)) : ((uint64_t)tag << 56);
+              mine &= gtag(gv[q][m]) == tag;
+            }
+          }
+          if (__all(mine)) { ok = true; break; }
+          if (__builtin_amdgcn_s_memrealtime() - t0 > g.spin_ticks) break;
+          __builtin_amdgcn_s_sleep(1);
+        }
+#ifdef KSIM_STAMPS
+        cs_acc += __builtin_amdgcn_s_memtime() - t_pub;
+        if (blockIdx.x == 0 && tid == 0) PG_STAMP(7);
+#endif
+        if (!ok) {
+          mode = -1;
+          if (lane == 0) atomicOr(c.err, 4);
+        } else {
+          int32_t F = 0;
+          int32_t mq_l = -1, cq_l = 0;  // lane q: class q's global maximum and its count
+          int32_t f = 0;
+#pragma unroll
+          for (int m = 0; m < MB; ++m) f += (lane + 64 * m < G) ? gfit(gv[0][m]) : 0;
+          F = ksimw::sum_i32(f);
+#pragma unroll
+          for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
+            if (q < K) {
+              int32_t mm = -1, cc = 0;
+#pragma unroll
+              for (int m = 0; m < MB; ++m) {
+                if (lane + 64 * m >= G) continue;
+                const int32_t cn = gcnt(gv[q][m]), s = gscore(gv[q][m]);
+                if (!cn) continue;
+                if (s > mm) { mm = s; cc = cn; }
+                else if (s == mm) cc += cn;
+              }
+              const int32_t Mq = ksimw::max_i32(cc ? mm : -1);
+              const int32_t Cq = ksimw::sum_i32((cc && mm == Mq) ? cc : 0);
+              mq_l = lane == q ? Mq : mq_l;
+              cq_l = lane == q ? Cq : cq_l;
+            }
+          }
+#ifdef KSIM_STAMPS
+          if (blockIdx.x == 0 && tid == 0) PG_STAMP(11);
+#endif
+          if (F > 0) {
+            mode = 1;
+            int64_t ix = 0;
+            if (F > 1) {  // generic_scheduler.go:153-156: a single fit skips selectHost
+              mode = 2;
+              // lane q = reduce class q: NormalizeReduce over the filtered set, weighted totals
+              // (reduce.go:29-64, generic_scheduler.go:632-639), the best total and its classes
+              const bool live = lane < K && cq_l != 0;
+              int64_t mxT = 0, mxA = 0;
+              // K <= 16: the class lanes are one DPP row
+              if (k1 > 1 || c.w[KSIM_W_TAINT_TOLERATION]) mxT = ksimw::max16_i64(live ? tv_l : 0);
+              if (k2 > 1 || c.w[KSIM_W_NODE_AFFINITY]) mxA = ksimw::max16_i64(live ? av_l : 0);
+              uint64_t t = (uint64_t)(int64_t)mq_l + (uint64_t)ad_l;
+              if (c.w[KSIM_W_TAINT_TOLERATION]) t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(tv_l, mxT, true);
+              if (c.w[KSIM_W_NODE_AFFINITY]) t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(av_l, mxA, false);
+              const int64_t tot = live ? (int64_t)t : INT64_MIN;
+              const int64_t best = ksimw::max16_i64(tot);
+              const uint64_t wbm = __ballot(live && tot == best);
+              win = (uint32_t)wbm;
+              const int32_t C = ksimw::sum16_i32(((wbm >> lane) & 1ull) ? cq_l : 0);
+              tgt_l = ((wbm >> lane) & 1ull) ? mq_l : -2;
+              ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)C) : (int64_t)((uint32_t)counter % (uint32_t)C);
+              counter += 1;  // generic_scheduler.go:192-195
+            }
+            // locate the workgroup holding the ix-th match from the top (lane-major workgroup order:
+            // lane l holds l, l + 64, ...; name rank grows with the workgroup index)
+            int32_t bm[MB];
+#pragma unroll
+            for (int m = 0; m < MB; ++m) {
+              const int b = lane + 64 * m;
+              int32_t s = 0;
+              if (b < G) {
+                if (mode == 1) {
+                  s = gfit(gv[0][m]);
+                } else {
+#pragma unroll
+                  for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
+                    if (q < K && ((win >> q) & 1u)) {
+                      const int32_t Mq = __builtin_amdgcn_readlane(mq_l, q);
+                      if (gcnt(gv[q][m]) && gscore(gv[q][m]) == Mq) s += gcnt(gv[q][m]);
+                    }
+                  }
+                }
+              }
+              bm[m] = s;
+            }
+            locate(bm, ix);
+          }
+        }
+      }
+#ifdef KSIM_STAMPS
+      if (blockIdx.x == 0 && tid == 0) PG_STAMP(12);
+#endif
+      if (lane < KSIM_MAX_RCLASS) s_tgt[lane] = tgt_l;
+      if (lane == 0) { s_mode = mode; s_blk = blk; s_rank = rank; s_win = win; s_node = -1; }
+    } else if (pf) {
+      const uint4* src = reinterpret_cast<const uint4*>(g.rec + (pod + 2 - c.first) * (int64_t)g.d.rec_stride);
+      uint4* dst = reinterpret_cast<uint4*>(xrec(pod + 2));
+      for (int32_t x = lane; x < g.d.rec_stride / 16; x += 64) dst[x] = src[x];
+    } else if ((rowt || hypt) && has_next) {
+#ifdef KSIM_STAMPS
+      const uint64_t te0 = __builtin_amdgcn_s_memtime();
+      uint64_t* sa = (tid == 64 || tid == 320) ? ev_sa : nullptr;
+#else
+      uint64_t* sa = nullptr;
+#endif
+      PgX X1;
+      X1.base = xrec(pod + 1);
+      const PgHdr H1 = pg_hdr_u(X1.hdr());
+      pg_sections(H1, X1.so);
+      const ksim_pod P1 = pg_pod_u(X1.pod());
+      const PgHyp y{&X, &H};
+      if (rowt) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          const int32_t j = k * PG_RT + rt;
+          if (j < nrows) n0[k] = pg_eval<false>(c, g, L, X1, P1, H1, j, lo + j, y, P, k == 0 ? sa : nullptr);
+        }
+      } else if (!(H.fl & PGF_NOHYP) && !c.no_commit) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          const int32_t j = k * PG_RT + rt;
+          if (j < nrows) ev1[j] = pg_eval<true>(c, g, L, X1, P1, H1, j, lo + j, y, P, k == 0 ? sa : nullptr);
+        }
+      }
+#ifdef KSIM_STAMPS
+      if (tid == 64) ev_acc += __builtin_amdgcn_s_memtime() - te0;
+      if (tid == 320) ev_acc1 += __builtin_amdgcn_s_memtime() - te0;
+#endif
+    }
+    __syncthreads();
+    PG_STAMP(3);
+    const int mode = s_mode;
+    if (mode < 0) break;  // uniform: every workgroup reached the same verdict
+
+    // ---- FitError: every workgroup adds its rows' reasons; nothing committed ----
+    if (mode == 0) {
+      if (c.collect && c.out_reasons && rowt) {
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          if (!__ballot(cur[k].rmk != 0)) continue;
+          for (int r = 0; r < KSIM_NREASONS; ++r) {
+            const int32_t nr = __popcll(__ballot((cur[k].rmk >> r) & 1u));
+            if (lane == 0 && nr) atomicAdd(&c.out_reasons[pod * KSIM_NREASONS + r], nr);
+          }
+        }
+      }
+      if (blockIdx.x == 0 && tid == 0) c.out_node[pod] = -1;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) cur[k] = n0[k];
+      continue;
+    }
+
+    // ---- the owner picks the row (the rank-th match from the top, selectHost's order) ----
+    const bool owner = s_blk == (int)blockIdx.x;
+    const bool shared = (H.fl & PGF_SHARED) != 0;
+    const bool aff_commit = (H.fl & PGF_AFF) && !c.no_commit;
+    int ksel = -1;
+    if (owner) {
+      const uint32_t win = s_win;
+      const int32_t rr = s_rank;
+      bool mt[NPT];
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        mt[k] = rowt && cur[k].fit && (mode == 1 || (((win >> cur[k].cl) & 1u) && (int32_t)cur[k].sc == s_tgt[cur[k].cl]));
+        const uint64_t bl = __ballot(mt[k]);
+        if (lane == 0 && rowt) s_bal[k][wv - 1] = bl;
+      }
+      __syncthreads();
+      int32_t above = 0;
+#pragma unroll
+      for (int k = NPT - 1; k >= 0; --k) {
+        int32_t up = 0;
+#pragma unroll
+        for (int w = PG_RW - 1; w >= 0; --w)
+          if (rowt && w > wv - 1) up += __popcll(s_bal[k][w]);
+        const int32_t mine = rowt ? __popcll((s_bal[k][wv - 1] >> lane) >> 1) : 0;
+        if (mt[k] && above + up + mine == rr) ksel = k;
+#pragma unroll
+        for (int w = 0; w < PG_RW; ++w) above += __popcll(s_bal[k][w]);
+      }
+      if (rr >= above) {  // uniform in the owner workgroup
+        if (tid == 0) atomicOr(c.err, 2);
+        break;
+      }
+    }
+    int32_t jsel = -1;
+    if (ksel >= 0) {
+      jsel = ksel * PG_RT + rt;
+      const int64_t w = lo + jsel;
+      c.out_node[pod] = (int32_t)w;
+      if (shared) {
+        s_node = w;
+        pg_store(g.gran + PG_COMMIT_OFF + slot, ((uint64_t)tag << 56) | (uint64_t)w);
+      }
+    }
+    PG_STAMP(4);
+    if (!(H.fl & PGF_NOHYP) || c.no_commit) {
+      // the hypothesis holds: every row takes E0, the chosen row E1, its commit is deferred
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) cur[k] = (k == ksel && !c.no_commit) ? ev1[k * PG_RT + rt] : n0[k];
+      if (jsel >= 0 && !c.no_commit) {
+        pend_j = jsel;
+        pend_pod = pod;
+      }
+      PG_STAMP(5);
+      continue;
+    }
+    // ---- no hypothesis: commit now, shared domains in every workgroup, re-evaluate pod p+1 ----
+    if (jsel >= 0) pg_commit_row(c, g, L, X, H, jsel, lo + jsel);
+    if (shared && aff_commit) {
+      if (!owner && tid == 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint64_t v;
+        while (gtag(v = pg_load(g.gran + PG_COMMIT_OFF + slot)) != tag) {
+          if (__builtin_amdgcn_s_memrealtime() - t0 > g.spin_ticks) { atomicOr(c.err, 4); s_abort = 1; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        s_node = (int64_t)(v & M56);
+      }
+      __syncthreads();
+      if (s_abort) break;
+      const int64_t w = s_node;
+      const int2* mp = X.sec<int2>(PGS_MP);
+      const PgCar* cr = X.sec<PgCar>(PGS_CAR);
+      const int32_t nm = H.n_mp, ncr = H.n_car;
+      for (int32_t x = tid; x < nm + ncr; x += PG2_BS) {
+        const int32_t key = x < nm ? mp[x].y : cr[x - nm].key;
+        s_dw[x] = g.A.dom[(int64_t)key * n + w];
+      }
+      __syncthreads();
+      for (int32_t yy = tid; yy < (nm + ncr) * nrows; yy += PG2_BS) {
+        const int32_t x = yy / nrows, j = yy - x * nrows;
+        const int32_t dw = s_dw[x];
+        if (dw < 0) continue;
+        if (x < nm) {
+          if (L.dom[(int64_t)mp[x].y * chunk + j] == dw) L.cnt[(int64_t)mp[x].x * chunk + j] += 1;
+        } else {
+          const PgCar& k = cr[x - nm];
+          if (L.dom[(int64_t)k.key * chunk + j] == dw)
+            atomicAdd(reinterpret_cast<unsigned long long*>(&L.car[(int64_t)k.term * chunk + j]), (unsigned long long)k.amount);
+        }
+      }
+    }
+    __syncthreads();
+    if (has_next && rowt) {
+      PgX X1;
+      X1.base = xrec(pod + 1);
+      const PgHdr H1 = pg_hdr_u(X1.hdr());
+      pg_sections(H1, X1.so);
+      const ksim_pod P1 = pg_pod_u(X1.pod());
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int32_t j = k * PG_RT + rt;
+        // shared domains may have changed any row; otherwise only the chosen one
+        if (j < nrows && (shared || k == ksel)) cur[k] = pg_eval<false>(c, g, L, X1, P1, H1, j, lo + j, PgHyp{}, P1);
+        else cur[k] = n0[k];
+      }
+    }
+    PG_STAMP(5);
+  }
+  if (pend_j >= 0) {  // the last deferred commit
+    PgX Xp;
+    Xp.base = xrec(pend_pod);
+    const PgHdr Hp = pg_hdr_u(Xp.hdr());
+    pg_sections(Hp, Xp.so);
+    pg_commit_row(c, g, L, Xp, Hp, pend_j, lo + pend_j);
+  }
+  pg_write_back(c, g, L, lo, nrows, chunk, tid, blockDim.x);
+#ifdef KSIM_STAMPS
+  // the spread over workgroups: max and (as ~max of ~) min of pass-A exchange, classes, decide
+  // window, pass-A local, and of the row evaluations
+  if (tid == 0) {
+    const int ks[4] = {1, 2, 3, 6};
+    for (int x = 0; x < 4; ++x) {
+      atomicMax((unsigned long long*)&c.dbg[16 + 2 * x], (unsigned long long)st_acc[ks[x]]);
+      atomicMax((unsigned long long*)&c.dbg[17 + 2 * x], (unsigned long long)~st_acc[ks[x]]);
     }
   }
-  // canonical per-domain counts: every row of a domain holds the same value, so concurrent
-  // identical stores from several workgroups are benign
-  for (int32_t x = tid; x < g.d.n_pair * nrows; x += PG_BS) {
-    const int32_t cp = x / nrows, j = x - cp * nrows;
-    const int32_t d = L.dom[(int64_t)g.A.pair_key[cp] * chunk + j];
-    if (d >= 0) g.A.cnt[g.A.pair_off[cp] + d] = L.cnt[(int64_t)cp * chunk + j];
+  if (cm_n) {
+    atomicAdd((unsigned long long*)&c.dbg[32], (unsigned long long)cm_acc);
+    atomicAdd((unsigned long long*)&c.dbg[36], (unsigned long long)cm_n);
   }
-  for (int32_t x = tid; x < g.d.n_carry * nrows; x += PG_BS) {
-    const int32_t e = x / nrows, j = x - e * nrows;
-    const int32_t d = L.dom[(int64_t)g.A.carry_key[e] * chunk + j];
-    if (d >= 0) g.A.carried[g.A.carry_off[e] + d] = L.car[(int64_t)e * chunk + j];
+  if (tid == 0) {
+    atomicAdd((unsigned long long*)&c.dbg[33], (unsigned long long)ps_acc);
+    atomicAdd((unsigned long long*)&c.dbg[34], (unsigned long long)pr_acc);
+    atomicAdd((unsigned long long*)&c.dbg[35], (unsigned long long)cs_acc);
   }
+  if (tid == 64 || tid == 320)
+    for (int x = 0; x < 6; ++x) atomicAdd((unsigned long long*)&c.dbg[26 + x], (unsigned long long)ev_sa[x]);
+  if (tid == 64) {
+    atomicMax((unsigned long long*)&c.dbg[24], (unsigned long long)ev_acc);
+    atomicMax((unsigned long long*)&c.dbg[25], (unsigned long long)~ev_acc);
+  }
+  if (tid == 320) {
+    atomicMax((unsigned long long*)&c.dbg[14], (unsigned long long)ev_acc1);
+    atomicMax((unsigned long long*)&c.dbg[15], (unsigned long long)~ev_acc1);
+  }
+#endif
   if (blockIdx.x == 0 && tid == 0) {
     *c.counter = counter;
     *c.cursor = c.end;
@@ -1157,6 +2106,8 @@ extern "C" size_t ksim_pgen_plan(int64_t chunk, const PgDims* d, uint32_t* off) 
   put(PGO_PC, d->pslots ? C * 4 : 0); put(PGO_PK, (size_t)d->pslots * C * 8);
   put(PGO_DOM, (size_t)d->n_keys * C * 4); put(PGO_CNT, (size_t)d->n_pair * C * 4); put(PGO_CAR, (size_t)d->n_carry * C * 8);
   put(PGO_X0, (size_t)d->rec_stride); put(PGO_X1, (size_t)d->rec_stride);
+  put(PGO_X2, d->hyp ? (size_t)d->rec_stride : 0); put(PGO_X3, d->hyp ? (size_t)d->rec_stride : 0);
+  put(PGO_E1, d->hyp ? C * PG_EV_BYTES : 0);
   return o;
 }
 
@@ -1183,6 +2134,26 @@ extern "C" hipError_t ksim_launch_pgen(const KsimCtx* c, const PGenArgs* g, int 
     case 1: return launch_pgen<1, 4>(c, g, grid, lds, s);
     case 2: return launch_pgen<2, 4>(c, g, grid, lds, s);
     default: return launch_pgen<4, 4>(c, g, grid, lds, s);
+  }
+}
+
+template <int NPT, int MB>
+static hipError_t launch_pgen2(const KsimCtx* c, const PGenArgs* g, int grid, size_t lds, hipStream_t s) {
+  hipError_t e = ksim_check_coresident(ksim_pgen2_kernel<NPT, MB>, grid, PG2_BS, lds);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((ksim_pgen2_kernel<NPT, MB>), dim3(grid), dim3(PG2_BS), lds, s, *c, *g);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ksim_launch_pgen2(const KsimCtx* c, const PGenArgs* g, int grid, int npt, size_t lds, hipStream_t s) {
+  if (grid <= 0 || grid > PG_MAXG || g->d.rec_stride % 16 || g->d.rec_stride > PG_REC_MAX || lds > PG_LDS_BUDGET ||
+      (int64_t)grid * c->chunk < c->n || c->chunk > (int64_t)npt * PG_RT || (npt != 1 && npt != 2 && npt != 4) || !g->d.hyp ||
+      grid > 64)
+    return hipErrorInvalidValue;
+  switch (npt) {  // one granule per lane in the sweeps (grid <= 64; larger grids take the single form)
+    case 1: return launch_pgen2<1, 1>(c, g, grid, lds, s);
+    case 2: return launch_pgen2<2, 1>(c, g, grid, lds, s);
+    default: return launch_pgen2<4, 1>(c, g, grid, lds, s);
   }
 }
 

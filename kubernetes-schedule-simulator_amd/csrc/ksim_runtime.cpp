@@ -56,13 +56,13 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
   for (int k = 0; k < KSIM_NW; ++k) c.w[k] = cfg->weights[k];
   int rc;
   if ((rc = dev_alloc(h, &c.cursor, 1)) || (rc = dev_alloc(h, &c.counter, 1)) || (rc = dev_alloc(h, &c.ticket, 4)) ||
-      (rc = dev_alloc(h, &c.err, 4)) || (rc = dev_alloc(h, &c.dbg, 32))) {
+      (rc = dev_alloc(h, &c.err, 4)) || (rc = dev_alloc(h, &c.dbg, 64))) {
     ksim_destroy(h);
     return rc;
   }
   (void)hipMemsetAsync(c.ticket, 0, 16, h->stream);
   (void)hipMemsetAsync(c.err, 0, 16, h->stream);
-  (void)hipMemsetAsync(c.dbg, 0, 32 * sizeof(uint64_t), h->stream);
+  (void)hipMemsetAsync(c.dbg, 0, 64 * sizeof(uint64_t), h->stream);
   (void)hipMemcpyAsync(c.counter, &cfg->last_node_index, 8, hipMemcpyHostToDevice, h->stream);
   if (hipStreamSynchronize(h->stream) != hipSuccess) {
     ksim_destroy(h);
@@ -649,13 +649,14 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
 // spread reduce's zones within one record; every pod-context record within PG_REC_MAX.
 struct PgPlan {
   int grid = 0, npt = 0;
+  bool v2 = true;  // the dual-hypothesis kernel (192 rows per thread slot); KSIM_PGEN_V1 selects the single one
   int64_t chunk = 0;
   size_t lds = 0;
   PgDims d{};
   uint32_t off[PGO_N] = {};
 };
 
-static bool pgen_plan(ksim_handle* h, PgPlan* pl) {
+static bool pgen_plan(ksim_handle* h, PgPlan* pl, bool allow_v2 = true) {
   const KsimCtx& c = h->ctx;
   if (getenv("KSIM_NO_PGEN") || h->shard.world > 1 || c.n <= 0) return false;
   int64_t s = 0;
@@ -692,10 +693,15 @@ static bool pgen_plan(ksim_handle* h, PgPlan* pl) {
   if (h->have_aff) { d.n_keys = h->aff_n_keys; d.n_pair = h->aff_n_pair; d.n_carry = h->aff_n_carry; }
   const size_t budget = ksim_pgen_lds_budget();
   const int64_t gcap = (h->max_grid > 0 && h->max_grid < 256) ? h->max_grid : 256;
-  const int64_t cmin = (c.n + gcap - 1) / gcap;  // at most 256 workgroups (KSIM_MAX_GRID)
+  int64_t cmin = (c.n + gcap - 1) / gcap;  // at most 256 workgroups (KSIM_MAX_GRID)
   if (cmin > 1024) return false;
-  int64_t chunk = std::min<int64_t>(std::max<int64_t>(cmin, 256), c.n);
-  if (const char* e = getenv("KSIM_PGEN_CHUNK")) chunk = std::max<int64_t>(cmin, std::min<int64_t>(atoll(e), 1024));
+  // the dual form: at most 64 workgroups (one granule per lane in its sweeps), 768 rows each
+  pl->v2 = allow_v2 && !getenv("KSIM_PGEN_V1") && c.n <= 64 * 768;
+  if (pl->v2) cmin = std::max<int64_t>(cmin, (c.n + 63) / 64);
+  const int64_t rt = pl->v2 ? 192 : 256;  // rows per thread slot
+  d.hyp = pl->v2 ? 1 : 0;
+  int64_t chunk = std::min<int64_t>(std::max<int64_t>(cmin, rt), c.n);
+  if (const char* e = getenv("KSIM_PGEN_CHUNK")) chunk = std::max<int64_t>(cmin, std::min<int64_t>(atoll(e), 4 * rt));
   for (;;) {
     d.n_st = c.n_classes_dev;  // the static (pod class, row) words, when they fit
     size_t lds = ksim_pgen_plan(chunk, &d, pl->off);
@@ -707,12 +713,13 @@ static bool pgen_plan(ksim_handle* h, PgPlan* pl) {
       pl->lds = lds;
       break;
     }
-    if (chunk <= cmin) return false;
+    if (chunk <= cmin) return pl->v2 ? pgen_plan(h, pl, false) : false;
     chunk = std::max<int64_t>(cmin, chunk * 7 / 8);
   }
   pl->chunk = chunk;
   pl->grid = (int)((c.n + chunk - 1) / chunk);
-  pl->npt = chunk <= 256 ? 1 : chunk <= 512 ? 2 : 4;
+  if (pl->v2 && pl->grid > 64) return pgen_plan(h, pl, false);
+  pl->npt = chunk <= rt ? 1 : chunk <= 2 * rt ? 2 : 4;
   pl->d = d;
   return true;
 }
@@ -758,7 +765,8 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, const PgP
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
   hipError_t e = ksim_pgen_pack(&c, &g, h->stream);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pgen pack: %s", hipGetErrorString(e));
-  e = ksim_launch_pgen(&c, &g, pl.grid, pl.npt, pl.lds, h->stream);
+  e = pl.v2 ? ksim_launch_pgen2(&c, &g, pl.grid, pl.npt, pl.lds, h->stream)
+            : ksim_launch_pgen(&c, &g, pl.grid, pl.npt, pl.lds, h->stream);
   if (e == hipErrorCooperativeLaunchTooLarge) {
     if (h->cfg.mode != KSIM_MODE_PERSISTENT) return run_launch_mode(h, first, count, st);
     return ksim_fail(h, KSIM_E_UNSUPPORTED, "persistent launch: %d workgroups cannot be co-resident on this device", pl.grid);
@@ -770,7 +778,7 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, const PgP
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
 #ifdef KSIM_STAMPS
   {
-    uint64_t dd[32];
+    uint64_t dd[64];
     HIPCHK(h, hipMemcpy(dd, c.dbg, sizeof dd, hipMemcpyDeviceToHost));
     HIPCHK(h, hipMemset(c.dbg, 0, sizeof dd));
     fprintf(stderr, "[ksim stamps] pgen pods=%lld (%.3f ms, grid %d, chunk %lld, st %d, rec %d B, lds %zu) cycles/pod: eval %.0f "
@@ -782,6 +790,25 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, const PgP
             dd[8] / (double)count, dd[9] / (double)count, dd[10] / (double)count);
     fprintf(stderr, "[ksim stamps] pgen decide split (wave 0 of workgroup 0) cycles/pod: per-class %.0f rest %.0f barrier %.0f\n",
             dd[11] / (double)count, dd[12] / (double)count, dd[3] / (double)count);
+    if (pl.v2)
+      fprintf(stderr, "[ksim stamps] pgen2 over workgroups cycles/pod max/min: passA-xchg %.0f/%.0f classes %.0f/%.0f decide-window "
+              "%.0f/%.0f passA-local %.0f/%.0f row-eval %.0f/%.0f\n",
+              dd[16] / (double)count, ~dd[17] / (double)count, dd[18] / (double)count, ~dd[19] / (double)count,
+              dd[20] / (double)count, ~dd[21] / (double)count, dd[22] / (double)count, ~dd[23] / (double)count,
+              dd[24] / (double)count, ~dd[25] / (double)count);
+    if (pl.v2)
+      fprintf(stderr, "[ksim stamps] pgen2 mean over workgroups cycles/pod: passA spin %.0f passA reduce %.0f class spin %.0f; "
+              "deferred commit %.0f cycles each (%.0f commits)\n",
+              dd[33] / (double)count / pl.grid, dd[34] / (double)count / pl.grid, dd[35] / (double)count / pl.grid,
+              dd[36] ? dd[32] / (double)dd[36] : 0.0, (double)dd[36]);
+    if (pl.v2)
+      fprintf(stderr, "[ksim stamps] pgen2 E1 waves (thread 320) cycles/pod max/min: %.0f/%.0f\n", dd[14] / (double)count,
+              ~dd[15] / (double)count);
+    if (pl.v2)
+      fprintf(stderr, "[ksim stamps] pgen2 row eval split (threads 64 + 320, mean over workgroups, E0+E1) cycles/pod: row+static %.0f "
+              "ports+resources %.0f disk-conflict %.0f taints..max-volumes %.0f pressure+interpod %.0f map+ipa+spread %.0f\n",
+              dd[26] / (double)count / pl.grid, dd[27] / (double)count / pl.grid, dd[28] / (double)count / pl.grid,
+              dd[29] / (double)count / pl.grid, dd[30] / (double)count / pl.grid, dd[31] / (double)count / pl.grid);
   }
 #endif
   if (st) {
