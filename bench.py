@@ -53,12 +53,18 @@ def pmc_traffic(workload, evals_per_launch):
             "source": os.path.relpath(path, ROOT), "profiled": d.get("profiled")}
 
 
-def roofline_bound(alg_bytes, traffic):
+def roofline_bound(alg_bytes, traffic, launch_s=None):
     """"hbm" when the kernel moves about the algorithmic bytes through HBM; "latency" when the PMC
-    bytes per node-eval are far below them (the table is on chip: the per-pod exchange bounds it)."""
+    bytes per node-eval are far below them (the table is on chip: the per-pod exchange bounds it),
+    or when the measured HBM traffic runs at under a tenth of the peak rate (what it moves is the
+    exchange's polling, not the table)."""
     if traffic is None:
         return "hbm"
-    return "latency" if traffic["bytes_per_node_eval"] < 0.1 * alg_bytes else "hbm"
+    if traffic["bytes_per_node_eval"] < 0.1 * alg_bytes:
+        return "latency"
+    if launch_s and traffic["gb_per_launch"] / launch_s < 0.1 * HBM_PEAK_GBS:
+        return "latency"
+    return "hbm"
 
 
 def effective_cpus():
@@ -507,7 +513,7 @@ def main():
                        "blocks": head["blocks"],
                        "parallelism": ("node-sharded x%d" % world if sharded_head else
                                        "scenario-replicas x%d" % world if world > 1 else "single-gpu")},
-            "roofline": {"bound": "latency" if tree_kernel else roofline_bound(W["bytes"], traffic),
+            "roofline": {"bound": "latency" if tree_kernel else roofline_bound(W["bytes"], traffic, avg_launch_s),
                          "achieved": None if tree_kernel else round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": None if tree_kernel else round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic and traffic["gb_per_launch"],
@@ -521,7 +527,7 @@ def main():
                                      "roofline applies"} if tree_kernel else
                             {"note": "achieved = algorithmic bytes / launch time; the PMC traffic shows the table "
                                      "stays on chip (LDS), so the per-pod cross-CU exchange, not HBM, bounds it"}
-                            if roofline_bound(W["bytes"], traffic) == "latency" else {})},
+                            if roofline_bound(W["bytes"], traffic, avg_launch_s) == "latency" else {})},
             "cpu_baseline": cpu,
             "parity": parity,
             "pods_bound": bound,
