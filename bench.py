@@ -106,6 +106,9 @@ def parse():
     ap.add_argument("--c4-pods", type=int, default=20000,
                     help="c3 line: pods of the 1M-node C4 streaming side measurement (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--per-pod-calls", type=int, default=0,
+                    help="c2 / c2x: timed ksim_schedule_one calls through the per-pod mirror at each "
+                         "cached-pod mark (0 = skip the per_pod side line)")
     ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c2x", "c4", "c5"],
                     help="c3: the headline metric (default); c2: 5k heterogeneous nodes with selectors, "
                          "ports and taints; c4: 1M nodes; c5: the 4,096-scenario policy sweep")
@@ -459,6 +462,9 @@ def main():
     c4 = None
     if world == 1 and a.workload == "c3" and a.c4_pods > 0 and a.mode == "auto":
         c4 = c4_stream_side(a)
+    per_pod = None
+    if world == 1 and a.workload in ("c2", "c2x") and a.per_pod_calls > 0:
+        per_pod = per_pod_side(a)
     cpu = parity = None
     if rank == 0 and a.cpu_sample > 0 and single is not None:
         cpu, parity = cpu_baseline(a, cl, preds, prios, single["out"], full_parity=a.workload in ("c2", "c2x"))
@@ -536,6 +542,8 @@ def main():
             line["tree_mode"] = tree
         if c4 is not None:
             line["c4_stream"] = c4
+        if per_pod is not None:
+            line["per_pod"] = per_pod
         if sharded is not None:
             ns = {"ranks": world, "nodes_per_rank": n_local, "scaling": "strong",
                   "exchange": "device-initiated system-scope stores into every rank's fine-grained exchange buffer "
@@ -550,6 +558,54 @@ def main():
             line["replicas"] = replicas
         print(json.dumps(line))
     D.close()
+
+
+def per_pod_side(a, marks=(1000, 20000)):
+    """The per-pod drop-in's latency: genericScheduler.Schedule + assume as
+    scheduleOne drives them (scheduler.go:431-484), through ksim.cache.SchedulerCache — host
+    encode, incremental affinity / volume sync, one ksim_schedule_one call — timed over
+    `a.per_pod_calls` consecutive pods of the workload's queue once `m` pods are cached, for each
+    mark m (the calls before a mark are the untimed fill).  The cluster is the workload's nodes
+    (and, for C2x, its PV / PVC listers and services)."""
+    from ksim import synth
+    from ksim.cache import SchedulerCache
+    from ksim.spread import SpreadListers
+    calls = a.per_pod_calls
+    total = max(marks) + calls
+    if a.workload == "c2x":
+        nodes, pods, pvs, pvcs, services = synth.c2x_objects(a.nodes, total)
+        kw = dict(pvs=pvs, pvcs=pvcs, spread=SpreadListers(services=services))
+    else:
+        nodes, pods = synth.c2_objects(a.nodes, total)
+        kw = {}
+    preds, prios = scheduler_provider()
+    sc = SchedulerCache(preds, prios, **kw)
+    try:
+        for nd in nodes:
+            sc.add_node(nd)
+        out, i, bound = [], 0, 0
+        for m in marks:
+            while i < m:
+                bound += sc.schedule_one(pods[i])[0] is not None
+                i += 1
+            r0 = sc.aff_reloads
+            t0 = time.perf_counter()
+            for _ in range(calls):
+                bound += sc.schedule_one(pods[i])[0] is not None
+                i += 1
+            dt = time.perf_counter() - t0
+            out.append({"cached_pods": m, "calls": calls, "us_per_call": round(dt / calls * 1e6, 1),
+                        "affinity_table_loads": sc.aff_reloads - r0})
+        return {"marks": out, "pods_bound": bound, "nodes": len(nodes),
+                "note": "wall time per scheduleOne-equivalent call (host encode + table sync + one "
+                        "ksim_schedule_one with assume), pods of the same workload queue in order"}
+    finally:
+        sc.close()
+
+
+def scheduler_provider():
+    from ksim import scheduler
+    return scheduler.provider("DefaultProvider")
 
 
 def main_c5(a):

@@ -74,6 +74,9 @@ enum {
   PGO_CAR,                                         // i64 [n_carry][chunk] carried terms, row form
   PGO_X0, PGO_X1, PGO_X2, PGO_X3,                  // four pod-context records (ring)
   PGO_E1,                                          // PgEv [chunk] the rows' E1 evaluations (dual form)
+  PGO_HD, PGO_HC, PGO_HK,                          // dense hypothesis deltas (dual form, when they fit):
+                                                   //   i32 [n_pair] key + 1 of pod p's count on pair c,
+                                                   //   i64 [n_carry] its carried amount of term e, i32 key + 1
   PGO_N
 };
 
@@ -85,6 +88,7 @@ struct PgDims {
   int32_t n_keys, n_pair, n_carry;
   int32_t rec_stride;
   int32_t hyp;      // 1: the dual-hypothesis kernel's layout (PGO_E1 and four records)
+  int32_t hdense;   // 1: the dense hypothesis deltas are staged (PGO_HD / HC / HK)
 };
 #define PG_VS_LDS 8
 #define PG_EV_BYTES 40  // sizeof(PgEv) (ksim_pgen.hip)

@@ -98,6 +98,9 @@ struct PgL {
   int32_t* dom;
   int32_t* cnt;
   int64_t* car;
+  int32_t* hd;   // dense hypothesis deltas (null when not staged)
+  int64_t* hc;
+  int32_t* hk;
   int32_t chunk;
 };
 
@@ -200,7 +203,10 @@ __device__ __forceinline__ bool pg_port_hit(uint64_t wk, uint64_t e) {
 template <bool HYP>
 __device__ __forceinline__ int32_t pg_cnt(const PgL& L, const PgHyp& y, int32_t pair, int32_t j) {
   int32_t v = L.cnt[(int64_t)pair * L.chunk + j];
-  if (HYP) {
+  if (HYP && L.hd) {  // the staged dense delta: one lookup
+    const int32_t k1 = L.hd[pair];
+    if (k1 && L.dom[(int64_t)(k1 - 1) * L.chunk + j] >= 0) v += 1;
+  } else if (HYP) {
     const int2* mp = y.X->sec<int2>(PGS_MP);
     for (int32_t x = 0; x < y.H->n_mp; ++x)
       if (mp[x].x == pair && L.dom[(int64_t)mp[x].y * L.chunk + j] >= 0) v += 1;
@@ -212,7 +218,10 @@ __device__ __forceinline__ int32_t pg_cnt(const PgL& L, const PgHyp& y, int32_t 
 template <bool HYP>
 __device__ __forceinline__ int64_t pg_car(const PgL& L, const PgHyp& y, int32_t e, int32_t j) {
   int64_t v = L.car[(int64_t)e * L.chunk + j];
-  if (HYP) {
+  if (HYP && L.hk) {
+    const int32_t k1 = L.hk[e];
+    if (k1 && L.dom[(int64_t)(k1 - 1) * L.chunk + j] >= 0) v += L.hc[e];
+  } else if (HYP) {
     const PgCar* cr = y.X->sec<PgCar>(PGS_CAR);
     for (int32_t x = 0; x < y.H->n_car; ++x)
       if (cr[x].term == e && L.dom[(int64_t)cr[x].key * L.chunk + j] >= 0) v += cr[x].amount;
@@ -411,6 +420,9 @@ __device__ __forceinline__ PgL pg_lds(char* sm, const PGenArgs& g, int64_t chunk
   L.vs = (uint64_t*)(sm + g.off[PGO_VS]); L.pc = (int32_t*)(sm + g.off[PGO_PC]);
   L.pk = (uint64_t*)(sm + g.off[PGO_PK]); L.dom = (int32_t*)(sm + g.off[PGO_DOM]);
   L.cnt = (int32_t*)(sm + g.off[PGO_CNT]); L.car = (int64_t*)(sm + g.off[PGO_CAR]);
+  L.hd = g.d.hdense ? (int32_t*)(sm + g.off[PGO_HD]) : nullptr;
+  L.hc = g.d.hdense ? (int64_t*)(sm + g.off[PGO_HC]) : nullptr;
+  L.hk = g.d.hdense ? (int32_t*)(sm + g.off[PGO_HK]) : nullptr;
   return L;
 }
 // pod-context record r & 1 (offset arithmetic on the LDS base keeps the accesses ds_*)
@@ -1450,6 +1462,10 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
   uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex (wave 0)
   __syncthreads();
   pg_stage_counts(c, g, L, nrows, chunk, tid, blockDim.x);
+  if (L.hd) {
+    for (int32_t x = tid; x < g.d.n_pair; x += PG2_BS) L.hd[x] = 0;
+    for (int32_t x = tid; x < g.d.n_carry; x += PG2_BS) { L.hc[x] = 0; L.hk[x] = 0; }
+  }
   __syncthreads();
 
   // pod `first` on every row, as the rows stand
@@ -1626,6 +1642,24 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
       cm_n += 1;
 #endif
       pend_j = -1;
+    }
+    if (wv == 4 && L.hd) {
+      // the dense hypothesis deltas: pod p-1's entries out, pod p's in (read by the E1 waves in this
+      // pod's decision window; pod p-1's readers finished before its decision barrier)
+      if (pod > c.first) {
+        PgX Xq;
+        Xq.base = xrec(pod - 1);
+        const PgHdr Hq = pg_hdr_u(Xq.hdr());
+        pg_sections(Hq, Xq.so);
+        const int2* mp = Xq.sec<int2>(PGS_MP);
+        for (int32_t x = lane; x < Hq.n_mp; x += 64) L.hd[mp[x].x] = 0;
+        const PgCar* cr = Xq.sec<PgCar>(PGS_CAR);
+        for (int32_t x = lane; x < Hq.n_car; x += 64) { L.hc[cr[x].term] = 0; L.hk[cr[x].term] = 0; }
+      }
+      const int2* mp = X.sec<int2>(PGS_MP);
+      for (int32_t x = lane; x < H.n_mp; x += 64) L.hd[mp[x].x] = mp[x].y + 1;
+      const PgCar* cr = X.sec<PgCar>(PGS_CAR);
+      for (int32_t x = lane; x < H.n_car; x += 64) { L.hc[cr[x].term] = cr[x].amount; L.hk[cr[x].term] = cr[x].key + 1; }
     }
     PG_STAMP(1);
 
@@ -2108,6 +2142,9 @@ extern "C" size_t ksim_pgen_plan(int64_t chunk, const PgDims* d, uint32_t* off) 
   put(PGO_X0, (size_t)d->rec_stride); put(PGO_X1, (size_t)d->rec_stride);
   put(PGO_X2, d->hyp ? (size_t)d->rec_stride : 0); put(PGO_X3, d->hyp ? (size_t)d->rec_stride : 0);
   put(PGO_E1, d->hyp ? C * PG_EV_BYTES : 0);
+  put(PGO_HD, d->hdense ? (size_t)d->n_pair * 4 : 0);
+  put(PGO_HC, d->hdense ? (size_t)d->n_carry * 8 : 0);
+  put(PGO_HK, d->hdense ? (size_t)d->n_carry * 4 : 0);
   return o;
 }
 

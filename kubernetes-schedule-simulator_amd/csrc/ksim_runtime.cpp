@@ -700,13 +700,21 @@ static bool pgen_plan(ksim_handle* h, PgPlan* pl, bool allow_v2 = true) {
   if (pl->v2) cmin = std::max<int64_t>(cmin, (c.n + 63) / 64);
   const int64_t rt = pl->v2 ? 192 : 256;  // rows per thread slot
   d.hyp = pl->v2 ? 1 : 0;
+  // the dense hypothesis deltas (E1's count lookups in one step), when small
+  const int32_t hdense = (pl->v2 && h->have_aff && !getenv("KSIM_PGEN_NO_HDENSE") &&
+                          (int64_t)d.n_pair * 4 + (int64_t)d.n_carry * 12 <= 16384) ? 1 : 0;
   int64_t chunk = std::min<int64_t>(std::max<int64_t>(cmin, rt), c.n);
   if (const char* e = getenv("KSIM_PGEN_CHUNK")) chunk = std::max<int64_t>(cmin, std::min<int64_t>(atoll(e), 4 * rt));
   for (;;) {
     d.n_st = c.n_classes_dev;  // the static (pod class, row) words, when they fit
+    d.hdense = hdense;
     size_t lds = ksim_pgen_plan(chunk, &d, pl->off);
     if (lds > budget) {
       d.n_st = 0;
+      lds = ksim_pgen_plan(chunk, &d, pl->off);
+    }
+    if (lds > budget && d.hdense) {
+      d.hdense = 0;
       lds = ksim_pgen_plan(chunk, &d, pl->off);
     }
     if (lds <= budget) {
@@ -781,9 +789,9 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, const PgP
     uint64_t dd[64];
     HIPCHK(h, hipMemcpy(dd, c.dbg, sizeof dd, hipMemcpyDeviceToHost));
     HIPCHK(h, hipMemset(c.dbg, 0, sizeof dd));
-    fprintf(stderr, "[ksim stamps] pgen pods=%lld (%.3f ms, grid %d, chunk %lld, st %d, rec %d B, lds %zu) cycles/pod: eval %.0f "
+    fprintf(stderr, "[ksim stamps] pgen pods=%lld (%.3f ms, grid %d, chunk %lld, st %d, hdense %d, rec %d B, lds %zu) cycles/pod: eval %.0f "
             "passA-local %.0f passA-xchg %.0f classes %.0f class-sweep %.0f decide %.0f pick+commit %.0f aff-shared %.0f\n",
-            (long long)count, ms, pl.grid, (long long)pl.chunk, pl.d.n_st, pl.d.rec_stride, pl.lds, dd[0] / (double)count,
+            (long long)count, ms, pl.grid, (long long)pl.chunk, pl.d.n_st, pl.d.hdense, pl.d.rec_stride, pl.lds, dd[0] / (double)count,
             dd[6] / (double)count, dd[1] / (double)count, dd[2] / (double)count, dd[7] / (double)count, dd[3] / (double)count,
             dd[4] / (double)count, dd[5] / (double)count);
     fprintf(stderr, "[ksim stamps] pgen eval split (thread 0's row) cycles/pod: top+row %.0f predicates %.0f map %.0f\n",

@@ -75,12 +75,19 @@ class SchedulerCache:
         # inter-pod affinity / SelectorSpread tables are needed once any cached or scheduled pod has
         # terms or spread selectors; then every call reloads them over the cached pods
         self._aff_on = False
+        self._aidx = None        # the persistent AffinityIndex (None: rebuild it; node events reset it)
+        self._aff_sig = None     # its sizes at the last table load
+        self._aff_remap = None
+        self._aff_check = False  # an affinity pod was cached on an unlisted node: re-check on the next call
+        self.aff_reloads = 0     # affinity table loads so far (the per-pod path's amortised cost)
         self._aff_wanted = bool(self.cfg.predicates & abi.P_INTERPOD_AFFINITY or
                                 ((self.cfg.weights[abi.W_INTERPOD] or self.cfg.weights[abi.W_SPREAD])
                                  and not self.cfg.no_priorities))
         self._need_na = any(n == "NodeAffinityPriority" for n, _ in self.prioritizers)
         self.h = abi.Handle(self.cfg)
         cl = self.cl = ingest.Cluster()
+        # ImageLocalityPriority reads node / pod images: intern them into label sets / classes
+        cl.image_locality = any(n == "ImageLocalityPriority" for n, _ in self.prioritizers)
         cl.ips.get("0.0.0.0")
         cl.protos.get("TCP")
         cl.label_sets.get(_canon({}), {})
@@ -190,10 +197,16 @@ class SchedulerCache:
 
     def _sync_affinity(self, enc, pod, extra):
         """Inter-pod affinity and SelectorSpread through the affinity tables (ksim/affinity.py),
-        rebuilt over the pods this cache holds on listed nodes plus `pod` when `extra` (a pod not
-        cached yet), loaded, and the descriptor's identity / class set from them.  The tables are
-        needed once any pod has terms or spread selectors; before that identities change nothing."""
-        from .affinity import AffinityIndex, has_pod_affinity, tables_struct
+        kept incrementally like predicateMetadata.AddPod / RemovePod (predicates/metadata.go:127-190)
+        and the cache's NodeInfo updates (schedulercache/cache.go:200-318): the index of selectors,
+        counted pairs, carried terms, identities and term classes persists across calls, the
+        device keeps the counts (every ksim_pod_add / _remove / assume updates them), and the tables
+        are rebuilt over the cached pods and reloaded only when the index grew by something the
+        device tables must hold (a new selector, pair, carried term, term class, or an identity
+        that some selector matches) or after a node event.  A call that interns nothing new costs
+        O(the pod's terms), not O(cached pods).  The tables are needed once any pod has terms or
+        spread selectors; before that identities change nothing."""
+        from .affinity import AffinityIndex, has_pod_affinity
         if not self._aff_wanted:
             return
         sels = self._spread_sels(pod)
@@ -201,6 +214,50 @@ class SchedulerCache:
             if not has_pod_affinity(pod) and not sels:
                 return
             self._aff_on = True
+        for attempt in (0, 1):
+            fresh = self._aidx is None
+            if fresh:
+                self._aidx = AffinityIndex([_meta(self.infos[n].node).get("labels") for n in self.names], self.hard_weight)
+                self._aff_sig = None
+            idx = self._aidx
+            me_ident = idx.ident(pod)
+            me_class = idx.aclass(pod, sels)
+            if self._aff_sig is not None and not self._aff_check and self._aff_grew_only_dead(idx):
+                grown = len(idx.idents.items) - len(self._aff_remap)
+                self._aff_remap = np.concatenate([self._aff_remap, np.zeros(grown, np.int32)])
+                self._aff_sig = self._aff_signature(idx)
+                break
+            try:
+                self._aff_rebuild(idx)
+                break
+            except Unsupported:
+                if fresh or attempt:
+                    raise
+                # a long-lived index keeps every selector / term it has seen: retry from the live pods
+                self._aidx = None
+        enc[0][0]["aff_ident"] = self._aff_remap[me_ident]
+        enc[0][0]["aff_class"] = me_class + 1
+
+    @staticmethod
+    def _aff_signature(idx):
+        return (len(idx.sels.items), len(idx.pairs.items), len(idx.carry.items), len(idx.keys.items),
+                len(idx.aclasses.items), len(idx.idents.items))
+
+    def _aff_grew_only_dead(self, idx):
+        """Nothing the device tables hold changed since the last load, except new identities that
+        no selector matches (their ksim_pod.aff_ident is 0: they count toward nothing)."""
+        sig = self._aff_signature(idx)
+        if sig[:5] != self._aff_sig[:5]:
+            return False
+        for it in idx.idents.items[self._aff_sig[5]:]:
+            if any(idx._matches(it, si) for si in idx.sels.items):
+                return False
+        return True
+
+    def _aff_rebuild(self, idx):
+        """Rebuild the tables over the pods cached on listed nodes and load them (counts from the
+        host's view of the cache)."""
+        from .affinity import has_pod_affinity, tables_struct
         ranks = self._ranks()
         cached = []
         for name, info in self.infos.items():
@@ -210,20 +267,15 @@ class SchedulerCache:
                 elif has_pod_affinity(p):
                     # the reference's metadata then errors on the node-less NodeInfo (metadata.go:106-109)
                     raise Unsupported("a pod with inter-pod affinity terms cached on a node that is not listed")
-        idx = AffinityIndex([_meta(self.infos[n].node).get("labels") for n in self.names], self.hard_weight)
-        allp = [p for _, p in cached]
-        if extra:
-            allp.append(pod)
-            me = len(allp) - 1
-        else:
-            me = next(i for i, p in enumerate(allp) if pod_key(p) == pod_key(pod))
-        idents = [idx.ident(p) for p in allp]
-        aclasses = [idx.aclass(p, sels if i == me else ()) for i, p in enumerate(allp)]
+        idents = [idx.ident(p) for _, p in cached]
+        aclasses = [idx.aclass(p) for _, p in cached]
         tables, remap = idx.build([w for w, _ in cached], idents, aclasses)
         self._aff_tables = tables
         self.h.call("ksim_load_affinity", C.byref(tables_struct(tables)))
-        enc[0][0]["aff_ident"] = remap[idents[me]]
-        enc[0][0]["aff_class"] = aclasses[me] + 1
+        self._aff_remap = remap
+        self._aff_sig = self._aff_signature(idx)
+        self._aff_check = False
+        self.aff_reloads += 1
 
     def _check_volume_errors(self, pod):
         """The scheduler refuses a pod on which a configured volume predicate errs (ksim/volumes.py)."""
@@ -240,7 +292,9 @@ class SchedulerCache:
     # ------------------------------------------------------------------ node rows
     def _node_row(self, name, info, ns):
         cl = self.cl
-        lid = cl.label_sets.get(ingest.label_set_key(ns.labels, ns.prefer_avoid), ingest.LabelSet(ns.labels, ns.prefer_avoid))
+        imgs = ns.images if cl.image_locality else None
+        lid = cl.label_sets.get(ingest.label_set_key(ns.labels, ns.prefer_avoid, imgs),
+                                ingest.LabelSet(ns.labels, ns.prefer_avoid, imgs))
         tid = cl.taint_sets.get(_canon(ns.taints), ns.taints)
         cl.prefer_avoid_nodes |= bool(ns.prefer_avoid)
         alloc_s = np.zeros(abi.MAX_SCALAR, np.int64)
@@ -297,6 +351,7 @@ class SchedulerCache:
             self._rank = None
         info.node, info.mem, info.disk = node, ns.mem_pressure, ns.disk_pressure
         self._vol_dirty = self._vol_key is not None
+        self._aidx = None
 
     def update_node(self, old, new):
         """cache.UpdateNode (cache.go:366-375) → SetNode on the (possibly new) NodeInfo."""
@@ -318,6 +373,7 @@ class SchedulerCache:
         if not info.pods:
             del self.infos[name]
         self._vol_dirty = self._vol_key is not None
+        self._aidx = None
 
     # ------------------------------------------------------------------ pods
     def _add(self, pod, enc=None):                          # cache.go:200-207
@@ -327,6 +383,8 @@ class SchedulerCache:
             self._sync_volumes(bool(enc[0][0]["vol_class"]))
             self._sync_affinity(enc, pod, True)
             self.h.call("ksim_pod_add", self._ranks()[name], *self._pod_args(enc))
+        elif self._aff_on:
+            self._aff_check = True
         self._info(name).pods[pod_key(pod)] = (pod, enc)
 
     def _remove(self, pod):                                 # cache.go:219-228

@@ -186,19 +186,57 @@ def _canon(x):
 
 class LabelSet(dict):
     """A node label set (a plain dict of labels for every label test) that also carries the
-    node's preferAvoidPods controller signatures: nodes with equal labels but different
-    annotations are different sets, so NodePreferAvoidPods is a function of (pod class, set)."""
+    node's preferAvoidPods controller signatures and — when the cluster interns them
+    (Cluster.image_locality) — its image sizes by name: nodes with equal labels but different
+    annotations / images are different sets, so NodePreferAvoidPods and ImageLocality are
+    functions of (pod class, set)."""
 
-    def __init__(self, labels, avoid=()):
+    def __init__(self, labels, avoid=(), images=None):
         super().__init__(labels)
         self.avoid = tuple(avoid)
+        self.images = dict(images or {})
 
 
-def label_set_key(labels, avoid):
+def label_set_key(labels, avoid, images=None):
     """Interning key of a label set: the labels' canonical form, plus the avoided controller
-    signatures when there are any (so annotation-free sets keep their plain key)."""
+    signatures and the image sizes when there are any (so plain sets keep their plain key)."""
     k = _canon(labels)
-    return k if not avoid else k + "|avoid:" + _canon([list(e) if e is not None else None for e in avoid])
+    if avoid:
+        k += "|avoid:" + _canon([list(e) if e is not None else None for e in avoid])
+    if images:
+        k += "|img:" + _canon(sorted(images.items()))
+    return k
+
+
+MB = 1024 * 1024
+MIN_IMG_SIZE, MAX_IMG_SIZE = 23 * MB, 1000 * MB   # image_locality.go:29-33
+
+
+def node_images(status):
+    """totalImageSize's map (image_locality.go:78-84): every name of every listed image → its
+    size; a name listed twice keeps the later image's size."""
+    out = {}
+    for img in (status or {}).get("images") or []:
+        for name in img.get("names") or []:
+            out[name] = int(img.get("sizeBytes") or 0)
+    return out
+
+
+def image_score(images, node_imgs):
+    """ImageLocalityPriorityMap (image_locality.go:39-88): the summed size of the pod's container
+    images (spec.containers only) the node lists, bucketed by calculateScoreFromSize."""
+    total = sum(node_imgs.get(i, 0) for i in images)
+    if total == 0 or total < MIN_IMG_SIZE:
+        return 0
+    if total >= MAX_IMG_SIZE:
+        return 10
+    return 10 * (total - MIN_IMG_SIZE) // (MAX_IMG_SIZE - MIN_IMG_SIZE) + 1
+
+
+def pod_images(spec):
+    """The images ImageLocality sums over: spec.containers[*].image, in order (init containers
+    are not looked at)."""
+    return [c.get("image") or "" for c in spec.get("containers") or []]
 
 
 def _go_field(obj, name):
@@ -317,6 +355,9 @@ class Cluster:
         self.tables = None
         self.prefer_avoid_nodes = False
         self.node_images = False   # some node lists status.images (ImageLocalityPriority not constant)
+        # node images are interned into the label sets and pod images into the classes (what
+        # ImageLocalityPriority reads); from_objects turns it on when some node lists images
+        self.image_locality = False
         self.bad_affinity_classes = set()   # preferred terms that fail to parse
         self.affinity = None     # inter-pod affinity tables (ksim/affinity.py), None without terms
         self.hard_weight = 10
@@ -326,7 +367,8 @@ class Cluster:
     # ------------------------------------------------------------------ nodes
     @classmethod
     def from_objects(cls, nodes, running_pods=(), pods=(), port_slots=None, hard_weight=10, pvs=(), pvcs=(),
-                     storage_classes=(), max_vols=None, vol_slots=None, spread=None, spread_services_only=False):
+                     storage_classes=(), max_vols=None, vol_slots=None, spread=None, spread_services_only=False,
+                     image_locality=None):
         """nodes / running_pods / pods: Kubernetes-shaped dicts; pods are in SCHEDULING
         order (the caller resolves the simulator's LIFO queue).  hard_weight:
         hardPodAffinitySymmetricWeight (the simulator's 10, or a Policy's).  pvs / pvcs /
@@ -334,9 +376,12 @@ class Cluster:
         max_vols: the MaxPD limits (EBS, GCE PD, Azure Disk), default KUBE_MAX_PD_VOLS / getMaxVols.
         spread: ksim.spread.SpreadListers (services / RCs / RSs / StatefulSets) for SelectorSpread
         (spread_services_only: ServiceSpreadingPriority's services-only form); None: the simulator's
-        empty listers."""
+        empty listers.  image_locality: intern node / pod images (what ImageLocalityPriority reads;
+        default: when some node lists status.images)."""
         self = cls()
         self.hard_weight = int(hard_weight)
+        self.image_locality = (any((x.get("status") or {}).get("images") for x in nodes) if image_locality is None
+                               else bool(image_locality))
         self.ips.get("0.0.0.0")     # id 0 = wildcard
         self.protos.get("TCP")      # id 0 = default protocol
         nodes = sorted(nodes, key=lambda n: _meta(n).get("name", "").encode())
@@ -385,8 +430,9 @@ class Cluster:
             for name, v in ns.scalar.items():
                 c["alloc_scalar"][self.scalar_names.ids[name], i] = v
             c["flags"][i] = ns.flags
-            c["label_set"][i] = self.label_sets.get(label_set_key(ns.labels, ns.prefer_avoid),
-                                                    LabelSet(ns.labels, ns.prefer_avoid))
+            imgs = ns.images if self.image_locality else None
+            c["label_set"][i] = self.label_sets.get(label_set_key(ns.labels, ns.prefer_avoid, imgs),
+                                                    LabelSet(ns.labels, ns.prefer_avoid, imgs))
             c["taint_set"][i] = self.taint_sets.get(_canon(ns.taints), ns.taints)
             self.prefer_avoid_nodes |= bool(ns.prefer_avoid)
             self.node_images |= bool((x.get("status") or {}).get("images"))
@@ -477,7 +523,11 @@ class Cluster:
         idx = self.index if index is None else index
         row["host"] = -1 if not nn else idx.get(nn, -2)
         ctrl = avoid_controller(md)
-        row["cls"] = self.classes.get(pod_class_key(spec, ctrl), spec if ctrl is None else dict(spec, __ctrl=ctrl))
+        imgs = pod_images(spec) if self.image_locality else None
+        cspec = spec if ctrl is None else dict(spec, __ctrl=ctrl)
+        if imgs and any(imgs):
+            cspec = dict(cspec, __img=imgs)
+        row["cls"] = self.classes.get(pod_class_key(spec, ctrl, imgs), cspec)
         row["flags"] = flags
         hp = host_ports(p)
         row["port_off"], row["port_cnt"] = len(ports), len(hp)
@@ -575,6 +625,7 @@ class NodeStatic:
     prefer_avoid: tuple  # preferAvoidPods controller signatures (avoid_signatures)
     mem_pressure: object  # status of the last MemoryPressure condition (None: absent)
     disk_pressure: object
+    images: dict = None   # status.images sizes by name (node_images)
 
 
 def node_static(x, prev_mem=None, prev_disk=None):
@@ -616,16 +667,19 @@ def node_static(x, prev_mem=None, prev_disk=None):
     taints = [{"key": t.get("key") or "", "value": t.get("value") or "", "effect": t.get("effect") or ""}
               for t in (sp.get("taints") or [])]
     return NodeStatic((r.cpu, r.mem, r.gpu, r.eph), r.pods, dict(r.scalar), f, dict(md.get("labels") or {}), taints,
-                      avoid_signatures(md.get("annotations")), mem, disk)
+                      avoid_signatures(md.get("annotations")), mem, disk, node_images(st))
 
 
-def pod_class_key(spec, ctrl=None):
+def pod_class_key(spec, ctrl=None, images=None):
     """Pods whose nodeSelector, node affinity and tolerations are equal share a class; an RC / RS
-    controllerRef (NodePreferAvoidPods' input) is part of the class when present."""
+    controllerRef (NodePreferAvoidPods' input) and the container images (ImageLocality's, when
+    the cluster interns them) are part of the class when present."""
     k = {"ns": spec.get("nodeSelector") or {}, "na": (spec.get("affinity") or {}).get("nodeAffinity"),
          "tol": spec.get("tolerations") or []}
     if ctrl is not None:
         k["ctrl"] = list(ctrl)
+    if images and any(images):
+        k["img"] = list(images)
     return _canon(k)
 
 
@@ -650,6 +704,7 @@ def build_class_tables(label_items, taint_items, specs):
     nav = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
     na_w = np.zeros((Cn, L), np.int64)   # preferred node-affinity weight per (class, label set)
     na_p = np.full((Cn, L), 10, np.int64)  # NodePreferAvoidPods map score per (class, label set)
+    im_s = np.zeros((Cn, L), np.int64)     # ImageLocality map score per (class, label set)
     need = np.zeros(Cn, np.uint32)
     pa_split = False
     bad = set()
@@ -659,10 +714,13 @@ def build_class_tables(label_items, taint_items, specs):
         all_sel = all_taint = True
         weights = []
         ctrl = spec.get("__ctrl")
+        imgs = spec.get("__img")
         pas = []
         for li, lab in enumerate(label_items):
             # CalculateNodePreferAvoidPodsPriorityMap (node_prefer_avoid_pods.go:32-68)
             pas.append(10 if ctrl is None else avoid_score(getattr(lab, "avoid", ()), ctrl))
+            if imgs:
+                im_s[k, li] = image_score(imgs, getattr(lab, "images", None) or {})
             ok = labels.pod_matches_node_labels(spec, lab)
             if ok:
                 sel[k, li >> 5] |= np.uint32(1 << (li & 31))
@@ -708,7 +766,7 @@ def build_class_tables(label_items, taint_items, specs):
         need[k] = f
     tables = dict(n_classes=Cn, n_label_sets=L, n_taint_sets=T, sel_ok=sel, taint_ok=tok, noexec_ok=nok,
                   tt_class=ttc, na_class=nac, n_tt=ntt, n_na=nna, tt_val=ttv, na_val=nav, na_w=na_w, na_p=na_p,
-                  pa_split=pa_split)
+                  pa_split=pa_split, im_s=im_s)
     return tables, need, bad
 
 

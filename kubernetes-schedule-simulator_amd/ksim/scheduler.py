@@ -187,22 +187,27 @@ def class_tables_for(tables, priorities, label_sets=(), custom=None):
     """The class tables a scheduler with these priorities loads, and the weighted per-NodeAffinity-
     class addends (ksim_class_tables.na_add) or None.
 
-    NodePreferAvoidPodsPriority (node_prefer_avoid_pods.go:32-68) is a function of (pod class,
-    label set) — the label set carries the node's preferAvoidPods annotation — and the Policy's
-    labelPreference / serviceAntiAffinity priorities (label_set_priority) of the label set alone.
+    NodePreferAvoidPodsPriority (node_prefer_avoid_pods.go:32-68) and ImageLocalityPriority
+    (image_locality.go:39-88) are functions of (pod class, label set) — the label set carries the
+    node's preferAvoidPods annotation and its images, the class the pod's controller and container
+    images — and the Policy's labelPreference / serviceAntiAffinity priorities
+    (label_set_priority) of the label set alone.
     When the policy weighs them and they differ across the nodes some pod class sees, the
     NodeAffinity class dimension is re-keyed by (preferred weight, summed addend) — by the addend
     alone if NodeAffinityPriority is not configured — and each class adds its weighted score.
     Otherwise NodePreferAvoidPods is the constant MaxPriority x weight of const_score."""
     custom = custom or {}
     w_pa = sum(int(x) for n, x in priorities if n == "NodePreferAvoidPodsPriority")
+    w_im = sum(int(x) for n, x in priorities if n == "ImageLocalityPriority")
+    im_s = tables.get("im_s")
+    im_on = bool(w_im and im_s is not None and im_s.any())
     w_custom = [(custom[n], int(x)) for n, x in priorities if n in custom]
     L = tables["na_class"].shape[1] if tables["na_class"].ndim == 2 else len(label_sets)
     lab_add = np.zeros(L, np.int64)
     for spec, w in w_custom:
         lab_add += np.array([w * label_set_priority(spec, ls) for ls in label_sets], np.int64)
     pa_on = bool(w_pa and tables.get("pa_split"))
-    if not pa_on and not lab_add.any():
+    if not pa_on and not im_on and not lab_add.any():
         return tables, None
     use_w = any(n == "NodeAffinityPriority" for n, _ in priorities)
     d = dict(tables)
@@ -213,6 +218,8 @@ def class_tables_for(tables, priorities, label_sets=(), custom=None):
     add = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
     for k in range(Cn):
         pa = [int(p) * w_pa if pa_on else 0 for p in tables["na_p"][k]]
+        if im_on:
+            pa = [a + w_im * int(x) for a, x in zip(pa, im_s[k])]
         keys = list(zip((int(x) if use_w else 0 for x in tables["na_w"][k]), (a + int(b) for a, b in zip(pa, lab_add))))
         av = sorted(set(keys))
         if int(tables["n_tt"][k]) * len(av) > abi.MAX_RCLASS:
@@ -304,8 +311,10 @@ def plan(cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO,
         raise Unsupported("a serviceAntiAffinity priority with services selecting the pods")
     if any(n == "NodeAffinityPriority" for n, _ in prioritizers) and cluster.bad_affinity_classes:
         raise Unsupported("NodeAffinityPriority: a preferred node-affinity term does not parse")
-    if any(n == "ImageLocalityPriority" for n, _ in prioritizers) and cluster.node_images:
-        raise Unsupported("ImageLocalityPriority with nodes that list status.images")
+    if (any(n == "ImageLocalityPriority" for n, _ in prioritizers) and cluster.node_images
+            and not getattr(cluster, "image_locality", False)):
+        raise Unsupported("ImageLocalityPriority with nodes that list status.images, on a cluster built "
+                          "without image interning (Cluster.from_objects(image_locality=True))")
     if "CheckNodeLabelPresence" in predicates and label_presence is None:
         raise Unsupported("CheckNodeLabelPresence needs its labelsPresence argument")
     if "CheckServiceAffinity" in predicates:

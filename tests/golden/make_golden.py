@@ -301,6 +301,32 @@ prio_case(PAsrc + ":128", "NodePreferAvoidPodsPriority",
           owned("ReplicaSet", "qwert12345"), PA_NODES, [["machine1", 10], ["machine2", 0], ["machine3", 10]])
 
 
+# ------------------------------------------------ ImageLocality
+ILsrc = S + "algorithm/priorities/image_locality_test.go"
+MiB = 1024 * 1024
+
+
+def img_node(name, images):   # makeImageNode (image_locality_test.go:203-208)
+    n = node(name)
+    n["status"]["images"] = [{"names": names, "sizeBytes": size} for names, size in images]
+    return n
+
+
+def img_pod(*images):
+    return pod(containers=[{"image": i} for i in images])
+
+
+IL_N1 = [(["gcr.io/40", "gcr.io/40:v1", "gcr.io/40:v1"], 40 * MiB), (["gcr.io/140", "gcr.io/140:v1"], 140 * MiB),
+         (["gcr.io/2000"], 2000 * MiB)]                                   # node401402000 (:68-92)
+IL_N2 = [(["gcr.io/250"], 250 * MiB), (["gcr.io/10", "gcr.io/10:v1"], 10 * MiB)]   # node25010 (:94-109)
+IL_NODES = [img_node("machine1", IL_N1), img_node("machine2", IL_N2)]
+prio_case(ILsrc + ":130", "ImageLocalityPriority", "two images spread on two nodes, prefer the larger image one",
+          img_pod("gcr.io/40", "gcr.io/250"), IL_NODES, [["machine1", 1], ["machine2", 3]])
+prio_case(ILsrc + ":145", "ImageLocalityPriority", "two images on one node, prefer this node",
+          img_pod("gcr.io/40", "gcr.io/140"), IL_NODES, [["machine1", 2], ["machine2", 0]])
+prio_case(ILsrc + ":160", "ImageLocalityPriority", "if exceed limit, use limit",
+          img_pod("gcr.io/10", "gcr.io/2000"), IL_NODES, [["machine1", 10], ["machine2", 0]])
+
 # ------------------------------------------------ PodFitsResources
 PFsrc = S + "algorithm/predicates/predicates_test.go"
 EXT_A, EXT_B, HUGE_A = "example.com/aaa", "example.com/bbb", "hugepages-2Mi"

@@ -170,8 +170,9 @@ def _affinity_stream(seed, ref, n_events, n_nodes):
 
 @pytest.mark.parametrize("seed", range(4))
 def test_event_stream_with_affinity_and_spread(seed):
-    """Inter-pod affinity and SelectorSpread pods through the per-pod mirror: the affinity tables
-    are rebuilt over the cached pods for every call; every decision matches the oracle's cache."""
+    """Inter-pod affinity and SelectorSpread pods through the per-pod mirror (incremental affinity
+    index, tables reloaded only when it grows or after node events): every decision matches the
+    oracle's cache."""
     from ksim.spread import SpreadListers
     svc = [{"metadata": {"namespace": ns}, "spec": {"selector": {"app": a}}} for ns, a in (("", "web"), ("ns1", "db"))]
     rss = [{"metadata": {"namespace": ""}, "spec": {"selector": {"matchLabels": {"tier": "fe"}}}}]
@@ -190,3 +191,56 @@ def test_event_stream_with_affinity_and_spread(seed):
     finally:
         dut.close()
     assert decisions > 80
+
+
+def test_affinity_tables_load_only_on_growth():
+    """The per-pod path keeps the inter-pod affinity / SelectorSpread state incrementally
+    (predicates/metadata.go:127-190): on a replicated workload — four pod templates, hostname
+    anti-affinity on two of them, services selecting all — the tables load a handful of times while
+    the index learns the templates, then never again over hundreds of Schedule + assume calls and
+    removals; every decision still matches the oracle's cache."""
+    import copy
+    import random
+    from ksim.spread import SpreadListers
+    rng = random.Random(77)
+    svc = [{"metadata": {"namespace": ""}, "spec": {"selector": {"app": a}}} for a in ("web", "db")]
+    preds, prios = POLICIES["default"]
+    ref = R.SchedulerCache(set(preds), prios, spread=R.SpreadListers(services=svc))
+    dut = SchedulerCache(preds, prios, device=0, spread=SpreadListers(services=svc))
+
+    def template(k, name):
+        app = ("web", "db", "web", "cache")[k]
+        pod = {"metadata": {"name": name, "namespace": "", "uid": name, "labels": {"app": app, "tier": str(k)}},
+               "spec": {"containers": [{"resources": {"requests": {"cpu": "100m", "memory": "64Mi"}}}]}}
+        if k in (0, 1):
+            pod["spec"]["affinity"] = {"podAntiAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": [
+                {"labelSelector": {"matchLabels": {"app": app}}, "topologyKey": "kubernetes.io/hostname"}]}}
+        return pod
+
+    try:
+        for i in range(40):
+            node = {"metadata": {"name": "n-%02d" % i, "labels": {"kubernetes.io/hostname": "n-%02d" % i,
+                                                                   "failure-domain.beta.kubernetes.io/zone": "z%d" % (i % 3)}},
+                    "status": {"allocatable": {"cpu": "8", "memory": "16Gi", "pods": "110"}}}
+            apply(ref, ("add_node", node))
+            apply(dut, ("add_node", node))
+        loads_after_warmup = None
+        for k in range(400):
+            if k == 40:
+                loads_after_warmup = dut.aff_reloads
+            added = sorted(key for key in ref.pod_states if key not in ref.assumed)
+            if k % 10 == 9 and added:
+                ev = ("remove_pod", copy.deepcopy(ref.pod_states[rng.choice(added)]))
+            elif k % 10 == 8 and ref.assumed:
+                ev = ("add_pod", copy.deepcopy(ref.pod_states[sorted(ref.assumed)[0]]))
+            else:
+                ev = ("schedule", template(rng.randrange(4), "p-%d" % k))
+            want = apply(ref, ev)
+            got = apply(dut, ev)
+            if ev[0] == "schedule":
+                assert got == want, (ev[1]["metadata"]["name"], want, got)
+        assert dut.last_node_index == ref.sched.last_node_index
+        assert dut.aff_reloads <= 8
+        assert dut.aff_reloads == loads_after_warmup
+    finally:
+        dut.close()

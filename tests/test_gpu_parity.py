@@ -29,14 +29,16 @@ def test_golden_priorities_on_gpu(c):
     assert [[h, got[h]] for h, _ in c["expect"]] == c["expect"]
 
 
-REDUCE_PRIORITIES = ("TaintTolerationPriority", "NodeAffinityPriority", "NodePreferAvoidPodsPriority")
+REDUCE_PRIORITIES = ("TaintTolerationPriority", "NodeAffinityPriority", "NodePreferAvoidPodsPriority",
+                     "ImageLocalityPriority")
 
 
 @pytest.mark.parametrize("mode", [abi.MODE_LAUNCH, abi.MODE_PERSISTENT])
 @pytest.mark.parametrize("c", [c for c in load("priorities") if c["priority"] in REDUCE_PRIORITIES], ids=case_id)
 def test_golden_reduce_priorities_select_on_gpu(c, mode):
-    """The reference's TaintToleration / NodeAffinity / NodePreferAvoidPods golden vectors through
-    the scheduling kernels' own reduce classes (per-class maxima, class totals — not the host
+    """The reference's TaintToleration / NodeAffinity / NodePreferAvoidPods / ImageLocality golden
+    vectors through the scheduling kernels' own reduce classes (ImageLocality and NodePreferAvoidPods
+    as per-class addends) (per-class maxima, class totals — not the host
     numpy path priority_scores uses): with lastNodeIndex = k, the pod must land on the k-th host
     of the golden maximum in descending bytewise name order (selectHost,
     generic_scheduler.go:183-198), for every k over two periods."""

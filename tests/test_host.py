@@ -170,3 +170,29 @@ def test_fit_error_message_format():
     for s in c["contains"]:
         assert s in msg
     assert msg == "0/3 nodes are available: 1 node(s) had memory pressure, 2 node(s) had disk pressure."
+
+
+def test_image_locality_addends_match_goldens():
+    """ImageLocalityPriority (image_locality.go:39-88) with node images: node image sizes are
+    interned into the label sets, the pod's container images into its class, and the per-(class,
+    label set) score becomes a NodeAffinity-class addend (scheduler.class_tables_for).  On the
+    reference's TestImageLocalityPriority cases the addend of each node's class is the golden score;
+    a cluster built without image interning refuses the priority."""
+    import json
+    import os
+    from ksim import ingest, scheduler
+    cases = [c for c in json.load(open(os.path.join(os.path.dirname(__file__), "golden", "priorities.json")))
+             if c["priority"] == "ImageLocalityPriority"]
+    assert len(cases) == 3
+    for c in cases:
+        cl = ingest.Cluster.from_objects(c["nodes"], c["pods"], [c["pod"]])
+        assert cl.image_locality
+        plan = scheduler.plan(cl, [], [("ImageLocalityPriority", 1)])
+        cls = int(cl.pods[0]["cls"])
+        t = plan.tables
+        got = {cl.names[i]: int(plan.na_add[cls][t["na_class"][cls][cl.cols["label_set"][i]]]) + plan.const_score
+               for i in range(cl.n_nodes)}
+        assert [[h, got[h]] for h, _ in c["expect"]] == c["expect"], c["test"]
+        bare = ingest.Cluster.from_objects(c["nodes"], c["pods"], [c["pod"]], image_locality=False)
+        with pytest.raises(abi.KsimUnsupported):
+            scheduler.plan(bare, [], [("ImageLocalityPriority", 1)])
