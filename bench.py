@@ -580,6 +580,7 @@ def per_pod_side(a, marks=(1000, 20000)):
         kw = {}
     preds, prios = scheduler_provider()
     sc = SchedulerCache(preds, prios, **kw)
+    t_start = time.perf_counter()
     try:
         for nd in nodes:
             sc.add_node(nd)
@@ -588,6 +589,9 @@ def per_pod_side(a, marks=(1000, 20000)):
             while i < m:
                 bound += sc.schedule_one(pods[i])[0] is not None
                 i += 1
+                if i % 1000 == 0:
+                    print("per_pod: %d pods cached (%.1f s)" % (i, time.perf_counter() - t_start), file=sys.stderr,
+                          flush=True)
             r0 = sc.aff_reloads
             t0 = time.perf_counter()
             for _ in range(calls):
@@ -596,7 +600,8 @@ def per_pod_side(a, marks=(1000, 20000)):
             dt = time.perf_counter() - t0
             out.append({"cached_pods": m, "calls": calls, "us_per_call": round(dt / calls * 1e6, 1),
                         "affinity_table_loads": sc.aff_reloads - r0})
-        return {"marks": out, "pods_bound": bound, "nodes": len(nodes),
+        return {"marks": out, "pods_bound": bound, "nodes": len(nodes), "volume_table_loads": sc.vol_loads,
+                "volume_table_grows": sc.vol_grows, "affinity_table_loads": sc.aff_reloads,
                 "note": "wall time per scheduleOne-equivalent call (host encode + table sync + one "
                         "ksim_schedule_one with assume), pods of the same workload queue in order"}
     finally:

@@ -541,6 +541,14 @@ typedef struct {
 
 /* Load (or replace) the volume tables; the slots describe the pods already placed. */
 int ksim_load_volumes(ksim_handle* h, const ksim_volume_tables* t);
+/* Grow the loaded volume tables for a pod that brings new volume keys / classes (the per-pod
+ * path; predicates.go:287-507 read them): key_filter, vc, vc_filter, refs and zone_ok are replaced
+ * (each at least as large as before, existing entries unchanged), vol_slots may grow, and slots /
+ * slot_count are ignored (may be NULL) — the device keeps every node's mounts, so the cost is the
+ * small tables, not the cached pods.  KSIM_E_STATE after a node event (reload with
+ * ksim_load_volumes).  Replaces the rebuild the reference never needs: its NodeInfo holds the
+ * pods and predicateMetadata grows with them (schedulercache/cache.go:200-318). */
+int ksim_grow_volumes(ksim_handle* h, const ksim_volume_tables* t);
 /* Read back the volume slots ([vol_slots][n_nodes]) and counts ([n_nodes]); either may be NULL. */
 int ksim_read_volumes(ksim_handle* h, uint64_t* slots, int32_t* slot_count);
 

@@ -178,6 +178,7 @@ struct ksim_handle {
   bool have_vol = false;
   bool vol_stale = false;       // a node event changed the table the slots describe
   int32_t vol_n_class = 0;
+  int32_t vol_n_keys = 0;
   KsimVol vol_h{};
   KsimVol* vol_dev = nullptr;
   std::vector<void*> vol_bufs;

@@ -10,7 +10,7 @@
 
 namespace {
 
-int validate(ksim_handle* h, const ksim_volume_tables* t) {
+int validate(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
   const int64_t n = h->ctx.n;
   if (t->n_nodes != n)
     return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: tables for %lld nodes, table has %lld", (long long)t->n_nodes,
@@ -23,8 +23,12 @@ int validate(ksim_handle* h, const ksim_volume_tables* t) {
     if (t->max_vols[k] < 0) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: negative volume limit");
   auto need = [&](const void* p, int64_t cnt) { return cnt == 0 || p != nullptr; };
   if (!need(t->key_filter, t->n_keys) || !need(t->vc, 2 * (int64_t)t->n_vclass) || !need(t->vc_filter, t->n_vclass) ||
-      !need(t->refs, t->n_refs) || !need(t->slots, (int64_t)t->vol_slots * n) || !t->slot_count)
+      !need(t->refs, t->n_refs) || (!keep && (!need(t->slots, (int64_t)t->vol_slots * n) || !t->slot_count)))
     return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: missing array");
+  if (keep && (t->n_keys < h->vol_n_keys || t->n_vclass < h->vol_n_class || t->vol_slots < h->vol_h.vol_slots))
+    return ksim_fail(h, KSIM_E_INVAL, "ksim_grow_volumes: the tables may only grow (keys %d < %d, classes %d < %d or "
+                     "slots %d < %d)", t->n_keys, h->vol_n_keys, t->n_vclass, h->vol_n_class, t->vol_slots,
+                     h->vol_h.vol_slots);
   if (t->zone_ok && t->zone_words != (h->n_label_sets + 31) / 32)
     return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: zone_words does not match the %d loaded label sets",
                      h->n_label_sets);
@@ -40,7 +44,7 @@ int validate(ksim_handle* h, const ksim_volume_tables* t) {
     if (off < 0 || cnt < 0 || off + cnt > t->n_refs)
       return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: class %d refs out of bounds", c);
   }
-  for (int64_t i = 0; i < n; ++i) {
+  for (int64_t i = 0; !keep && i < n; ++i) {
     const int32_t cnt = t->slot_count[i];
     if (cnt < 0 || cnt > t->vol_slots)
       return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: node %lld slot count out of range", (long long)i);
@@ -60,12 +64,15 @@ int validate(ksim_handle* h, const ksim_volume_tables* t) {
 
 }  // namespace
 
-extern "C" int ksim_load_volumes(ksim_handle* h, const ksim_volume_tables* t) {
+// keep: ksim_grow_volumes — the device's mounts stay (re-laid out when vol_slots grew).
+static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
   if (!h || !t) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: null argument");
   if (!h->have_nodes || !h->have_classes) return ksim_fail(h, KSIM_E_STATE, "ksim_load_volumes: load nodes and classes first");
   if (h->shard.world > 1) return ksim_fail(h, KSIM_E_UNSUPPORTED, "ksim_load_volumes: not available on a node-sharded handle");
+  if (keep && (!h->have_vol || h->vol_stale))
+    return ksim_fail(h, KSIM_E_STATE, "ksim_grow_volumes: no current volume tables (load them after a node event)");
   HIPCHK(h, hipSetDevice(h->device));
-  int rc = validate(h, t);
+  int rc = validate(h, t, keep);
   if (rc) return rc;
   const int64_t n = h->ctx.n;
   const size_t nb0 = h->bufs.size();
@@ -75,9 +82,20 @@ extern "C" int ksim_load_volumes(ksim_handle* h, const ksim_volume_tables* t) {
   ksim_vol_ref* refs;
   uint64_t* slots;
   if ((rc = dev_upload(h, &kf, t->key_filter, t->n_keys)) || (rc = dev_upload(h, &vc, t->vc, 2 * (size_t)t->n_vclass)) ||
-      (rc = dev_upload(h, &vf, t->vc_filter, t->n_vclass)) || (rc = dev_upload(h, &refs, t->refs, t->n_refs)) ||
-      (rc = dev_upload(h, &slots, t->slots, (size_t)t->vol_slots * n)) || (rc = dev_upload(h, &sc, t->slot_count, n)))
+      (rc = dev_upload(h, &vf, t->vc_filter, t->n_vclass)) || (rc = dev_upload(h, &refs, t->refs, t->n_refs)))
     return rc;
+  if (!keep) {
+    if ((rc = dev_upload(h, &slots, t->slots, (size_t)t->vol_slots * n)) || (rc = dev_upload(h, &sc, t->slot_count, n)))
+      return rc;
+  } else if (t->vol_slots == h->vol_h.vol_slots) {
+    slots = h->vol_h.slots;  // the same buffers: carried over below
+    sc = h->vol_h.slot_count;
+  } else {  // [S][n] → [S'][n]: the first S rows are one contiguous block
+    if ((rc = dev_alloc(h, &slots, (size_t)t->vol_slots * n)) || (rc = dev_alloc(h, &sc, (size_t)n))) return rc;
+    HIPCHK(h, hipMemsetAsync(slots, 0, (size_t)t->vol_slots * n * 8, h->stream));
+    HIPCHK(h, hipMemcpyAsync(slots, h->vol_h.slots, (size_t)h->vol_h.vol_slots * n * 8, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(sc, h->vol_h.slot_count, (size_t)n * 4, hipMemcpyDeviceToDevice, h->stream));
+  }
   if (t->zone_ok && (rc = dev_upload(h, &zo, t->zone_ok, (size_t)t->n_vclass * t->zone_words))) return rc;
   V.n = n;
   V.slots = slots; V.slot_count = sc; V.key_filter = kf; V.vc = vc; V.vc_filter = vf; V.refs = refs; V.zone_ok = zo;
@@ -87,13 +105,17 @@ extern "C" int ksim_load_volumes(ksim_handle* h, const ksim_volume_tables* t) {
   KsimVol* dev;
   if ((rc = dev_upload(h, &dev, &V, 1))) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
-  for (void* q : h->vol_bufs) dev_free(h, q);  // the previous tables (reload)
+  const bool carry = keep && t->vol_slots == h->vol_h.vol_slots;
+  for (void* q : h->vol_bufs)  // the previous tables (reload), except the mounts carried over
+    if (!(carry && (q == (void*)h->vol_h.slots || q == (void*)h->vol_h.slot_count))) dev_free(h, q);
   h->vol_bufs.clear();
+  if (carry) { h->vol_bufs.push_back(slots); h->vol_bufs.push_back(sc); }
   for (size_t k = nb0; k < h->bufs.size(); ++k) h->vol_bufs.push_back(h->bufs[k].p);
   h->vol_dev = dev;
   h->vol_h = V;
   h->ctx.vol = dev;
   h->vol_n_class = t->n_vclass;
+  h->vol_n_keys = t->n_keys;
   h->vol_max_ref = 0;
   for (int32_t c = 0; c < t->n_vclass; ++c) h->vol_max_ref = std::max(h->vol_max_ref, t->vc[2 * (int64_t)c + 1]);
   h->have_vol = true;
@@ -103,6 +125,13 @@ extern "C" int ksim_load_volumes(ksim_handle* h, const ksim_volume_tables* t) {
   if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
   return KSIM_OK;
 }
+
+extern "C" int ksim_load_volumes(ksim_handle* h, const ksim_volume_tables* t) { return load(h, t, false); }
+
+// Grow the tables the pod-side lookups index (keys, volume classes, refs, zone verdicts, more
+// slots per node) while the device keeps every node's mounts: the per-pod path's answer to a pod
+// that brings new volumes (its cost is the small tables, not O(cached pods)).
+extern "C" int ksim_grow_volumes(ksim_handle* h, const ksim_volume_tables* t) { return load(h, t, true); }
 
 extern "C" int ksim_read_volumes(ksim_handle* h, uint64_t* slots, int32_t* slot_count) {
   if (!h) return ksim_fail(h, KSIM_E_INVAL, "ksim_read_volumes: null handle");

@@ -174,7 +174,7 @@ EXPORTS = ["ksim_abi_version", "ksim_last_error", "ksim_create", "ksim_destroy",
            "ksim_shard_setup", "ksim_shard_export", "ksim_shard_connect", "ksim_shard_connect_local",
            "ksim_schedule_one", "ksim_pod_add", "ksim_pod_remove", "ksim_node_add", "ksim_node_update",
            "ksim_node_remove", "ksim_node_count", "ksim_append_pods", "ksim_load_affinity", "ksim_load_volumes",
-           "ksim_read_volumes"]
+           "ksim_read_volumes", "ksim_grow_volumes"]
 IPC_HANDLE_BYTES = 64
 MAX_RANKS = 8
 
@@ -237,6 +237,7 @@ def lib():
     L.ksim_append_pods.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_void_p, C.c_int64]
     L.ksim_load_affinity.argtypes = [C.c_void_p, C.POINTER(AffinityTables)]
     L.ksim_load_volumes.argtypes = [C.c_void_p, C.POINTER(VolumeTables)]
+    L.ksim_grow_volumes.argtypes = [C.c_void_p, C.POINTER(VolumeTables)]
     L.ksim_read_volumes.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     if L.ksim_abi_version() != ABI_VERSION:
         raise ImportError("libksim.so ABI version mismatch")

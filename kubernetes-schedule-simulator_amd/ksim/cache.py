@@ -97,6 +97,11 @@ class SchedulerCache:
         cl._affinity_ok = True   # affinity pods: their tables are built here per call (_sync_affinity)
         self._vol_on = bool(self.cfg.predicates & scheduler.VOLUME_PREDICATE_BITS)
         self._vol_key = None     # what the loaded volume tables were built for (None: not loaded)
+        self._vol_mounts = {}    # node name -> {key: [rw, ro, pvc]} of its cached pods (incremental)
+        self._vol_max = 0        # an upper bound of the mounted keys on any node
+        self._vol_S = 0          # vol_slots of the loaded tables
+        self._vol_zone = None    # NoVolumeZoneConflict verdicts of the loaded classes
+        self.vol_loads = self.vol_grows = 0
         self._vol_dirty = False  # a node event since: the library refuses calls until a reload
         self.names = []          # listed node names, ascending bytewise (= name rank)
         self._keys = []          # the same as bytes
@@ -160,37 +165,64 @@ class SchedulerCache:
 
     # ------------------------------------------------------------------ volume tables
     def _mounts(self):
-        """Per listed node (name-rank order) the mounts of its cached pods: {key: [rw, ro, pvc]}."""
-        idx = self.cl.volume_index
-        out = []
-        for name in self.names:
-            m = {}
-            info = self.infos.get(name)
-            for _, enc in (info.pods.values() if info else ()):
-                vc = int(enc[0][0]["vol_class"])
-                if vc:
-                    for k, j in idx.mounts_of(vc):
-                        m.setdefault(k, [0, 0, 0])[j] += 1
-            out.append(m)
-        return out
+        """Per listed node (name-rank order) the mounts of its cached pods: {key: [rw, ro, pvc]}
+        (kept incrementally by _mount)."""
+        return [self._vol_mounts.get(name, {}) for name in self.names]
 
-    def _sync_volumes(self, need):
-        """(Re)load the volume tables from the host's view of the cache when a volume pod needs
-        them and they are missing or out of date (new keys / classes / label sets), and after
-        every node event once loaded (the library marks them stale)."""
+    def _mount(self, name, enc, sign):
+        """NodeInfo.AddPod / RemovePod of a volume pod's mounts on node `name` (host view)."""
+        vc = int(enc[0][0]["vol_class"])
+        if not vc or not self._vol_on:
+            return
+        m = self._vol_mounts.setdefault(name, {})
+        for k, j in self.cl.volume_index.mounts_of(vc):
+            e = m.setdefault(k, [0, 0, 0])
+            e[j] += sign
+            if not any(e):
+                del m[k]
+        self._vol_max = max(self._vol_max, len(m))
+
+    def _sync_volumes(self, need, enc=None):
+        """Keep the device's volume tables current for a call.  First load (when a volume pod needs
+        them) and after every node event (the library marks them stale): the full tables with the
+        cached pods' mounts.  Otherwise, when a pod brings new volume keys / classes or needs more
+        slots per node than loaded: ksim_grow_volumes with the small tables only — the device keeps
+        every node's mounts (its commits and releases maintain them), so the call costs
+        O(keys + classes), not O(cached pods) (schedulercache/cache.go:200-318)."""
         if not self._vol_on:
             return
         idx = self.cl.volume_index
         key = (len(idx.key_filter), len(idx.class_refs), len(self.cl.label_sets.items))
-        if not self._vol_dirty and (self._vol_key == key or (self._vol_key is None and not need)):
+        vc = int(enc[0][0]["vol_class"]) if enc is not None else 0
+        want = self._vol_max + (len(idx.class_refs[vc - 1]) if vc else 0)
+        if not self._vol_dirty and self._vol_key is None and not need:
             return
+        if not self._vol_dirty and self._vol_key is not None:
+            if self._vol_key == key and want <= self._vol_S:
+                return
+            if self._vol_key[2] == key[2]:
+                from .volumes import build_tables, tables_struct
+                old_n = len(self._vol_zone[0])
+                if key[1] > old_n:
+                    ok, err = idx.zone_verdicts(self.cl.label_sets.items, first=old_n)
+                    self._vol_zone = (np.concatenate([self._vol_zone[0], ok]), self._vol_zone[1] or err)
+                S = max(self._vol_S, 2 * want)
+                t = build_tables(idx, len(self.names), None, (), self.cl.label_sets.items, vol_slots=S, zone=self._vol_zone)
+                self.vol_tables = t
+                self.h.call("ksim_grow_volumes", C.byref(tables_struct(t, "NoVolumeZoneConflict" in self.predicates)))
+                self._vol_key, self._vol_S = key, S
+                self.vol_grows += 1
+                return
         from .volumes import build_tables, tables_struct
         n = len(self.names)
-        self.vol_tables = build_tables(idx, n, self._mounts(), range(1, len(idx.class_refs) + 1),
-                                       self.cl.label_sets.items)
+        self._vol_zone = idx.zone_verdicts(self.cl.label_sets.items)
+        S = max(2 * want, 8)
+        self.vol_tables = build_tables(idx, n, self._mounts(), (), self.cl.label_sets.items, vol_slots=S,
+                                       zone=self._vol_zone)
         self.h.call("ksim_load_volumes", C.byref(tables_struct(self.vol_tables, "NoVolumeZoneConflict" in self.predicates)))
-        self._vol_key = key
+        self._vol_key, self._vol_S = key, S
         self._vol_dirty = False
+        self.vol_loads += 1
 
     def _spread_sels(self, pod):
         return self.spread.selectors(pod, self._spread_services_only) if self.spread is not None else []
@@ -380,12 +412,13 @@ class SchedulerCache:
         name = _spec(pod).get("nodeName", "")
         enc = enc if enc is not None else self._encode(pod)
         if name in self._ranks():
-            self._sync_volumes(bool(enc[0][0]["vol_class"]))
+            self._sync_volumes(bool(enc[0][0]["vol_class"]), enc)
             self._sync_affinity(enc, pod, True)
             self.h.call("ksim_pod_add", self._ranks()[name], *self._pod_args(enc))
         elif self._aff_on:
             self._aff_check = True
         self._info(name).pods[pod_key(pod)] = (pod, enc)
+        self._mount(name, enc, 1)
 
     def _remove(self, pod):                                 # cache.go:219-228
         name = _spec(pod).get("nodeName", "")
@@ -399,6 +432,7 @@ class SchedulerCache:
             self._sync_affinity(enc, cur, False)
             self.h.call("ksim_pod_remove", self._ranks()[name], *self._pod_args(enc))
         info.pods.pop(key)
+        self._mount(name, enc, -1)
         if not info.pods and info.node is None:
             del self.infos[name]
 
@@ -454,7 +488,7 @@ class SchedulerCache:
         enc = self._encode(pod)
         if enc[0][0]["vol_class"]:
             self._check_volume_errors(pod)
-        self._sync_volumes(bool(enc[0][0]["vol_class"]))
+        self._sync_volumes(bool(enc[0][0]["vol_class"]), enc)
         self._sync_affinity(enc, pod, True)
         res = abi.Result()
         self.h.call("ksim_schedule_one", *self._pod_args(enc), abi.SCHEDULE_ASSUME if assume else abi.SCHEDULE_ONLY,
@@ -473,6 +507,7 @@ class SchedulerCache:
             enc2 = (enc[0].copy(), enc[1], enc[2])
             enc2[0][0]["host"] = res.node
             self._info(host).pods[key] = (assumed, enc2)
+            self._mount(host, enc2, 1)
             self.pod_states[key] = assumed
             self.assumed.add(key)
         return host

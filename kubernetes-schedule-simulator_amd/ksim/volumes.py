@@ -234,13 +234,14 @@ class VolumeIndex:
             self.class_zone.append(zone)
         return c + 1
 
-    def zone_verdicts(self, label_sets):
-        """NoVolumeZoneConflict per (class, label set): bit table [n_class][words], and whether
-        some (class, label set) errs (predicates.go:559-628).  Evaluated once per distinct
-        (zone, region) constraint of the label sets; classes without PVCs pass everywhere."""
+    def zone_verdicts(self, label_sets, first=0):
+        """NoVolumeZoneConflict per (class, label set): bit table [n_class - first][words] for the
+        classes from `first` on, and whether one of them errs somewhere (predicates.go:559-628).
+        Evaluated once per distinct (zone, region) constraint of the label sets; classes without
+        PVCs pass everywhere."""
         L = len(label_sets)
         words = (L + 31) // 32
-        ok = np.zeros((len(self.class_zone), max(words, 1)), np.uint32)
+        ok = np.zeros((len(self.class_zone) - first, max(words, 1)), np.uint32)
         cons_of = [tuple(sorted((k, v) for k, v in dict(ls).items() if k in (ZONE_LABEL, REGION_LABEL)))
                    for ls in label_sets]
         groups = {}
@@ -250,7 +251,7 @@ class VolumeIndex:
         for s in range(L):
             full[s >> 5] |= np.uint32(1 << (s & 31))
         err = False
-        for c, zone in enumerate(self.class_zone):
+        for c, zone in enumerate(self.class_zone[first:]):
             if not zone:
                 ok[c] = full
                 continue
@@ -290,8 +291,10 @@ class VolumeIndex:
         return mounts
 
 
-def build_tables(index: VolumeIndex, n, mounts, queued_classes, label_sets, max_limits=None, vol_slots=None):
-    """The ksim_volume_tables arrays (a dict of numpy arrays and sizes)."""
+def build_tables(index: VolumeIndex, n, mounts, queued_classes, label_sets, max_limits=None, vol_slots=None,
+                 zone=None):
+    """The ksim_volume_tables arrays (a dict of numpy arrays and sizes).  mounts=None: no slot
+    arrays (ksim_grow_volumes keeps the device's); zone: precomputed (zone_ok, zone_err)."""
     key_filter = np.asarray(index.key_filter, np.uint32)
     refs = [r for c in index.class_refs for r in c]
     vc = np.zeros((len(index.class_refs), 2), np.int32)
@@ -308,11 +311,11 @@ def build_tables(index: VolumeIndex, n, mounts, queued_classes, label_sets, max_
     for c in set(queued_classes):
         if c > 0:
             qkeys.update(k for k, _ in index.class_refs[c - 1])
-    need = max([len(m) for m in mounts] + [0]) + len(qkeys)
+    need = max([len(m) for m in (mounts or ())] + [0]) + len(qkeys)
     S = int(need if vol_slots is None else vol_slots)
-    slots = np.zeros((S, n), np.uint64)
-    count = np.zeros(n, np.int32)
-    for i, m in enumerate(mounts):
+    slots = np.zeros((S, n) if mounts is not None else (0, 0), np.uint64)
+    count = np.zeros(n if mounts is not None else 0, np.int32)
+    for i, m in enumerate(mounts or ()):
         if len(m) > S:
             raise abi.KsimError(abi.E_INVAL, "vol_slots too small for running pods")
         for s, (k, (rw, ro, pv)) in enumerate(m.items()):
@@ -320,7 +323,7 @@ def build_tables(index: VolumeIndex, n, mounts, queued_classes, label_sets, max_
                 raise abi.KsimUnsupported(abi.E_UNSUPPORTED, "more mounts of one volume on a node than a slot counts")
             slots[s, i] = (k << 32) | (pv << 22) | (ro << 11) | rw
         count[i] = len(m)
-    zone_ok, zone_err = index.zone_verdicts(label_sets)
+    zone_ok, zone_err = index.zone_verdicts(label_sets) if zone is None else zone
     return dict(key_filter=key_filter, vc=vc, vc_filter=np.asarray(index.class_filter, np.uint32), refs=ref_arr,
                 zone_ok=np.ascontiguousarray(zone_ok), zone_words=int(zone_ok.shape[1]), zone_err=zone_err,
                 slots=slots, slot_count=count, vol_slots=S, n_nodes=n,
@@ -344,6 +347,7 @@ def tables_struct(d, use_zone=True):
     if use_zone and d["zone_words"]:
         t.zone_words = d["zone_words"]
         t.zone_ok = abi.ptr(d["zone_ok"], abi.C.c_uint32)
-    t.slots = abi.ptr(d["slots"], abi.C.c_uint64)
-    t.slot_count = abi.ptr(d["slot_count"], abi.C.c_int32)
+    if d["slots"].size:
+        t.slots = abi.ptr(d["slots"], abi.C.c_uint64)
+        t.slot_count = abi.ptr(d["slot_count"], abi.C.c_int32)
     return t

@@ -244,3 +244,47 @@ def test_affinity_tables_load_only_on_growth():
         assert dut.aff_reloads == loads_after_warmup
     finally:
         dut.close()
+
+
+def test_volume_tables_grow_without_reload():
+    """Volume pods through the per-pod mirror: a pod that brings a new disk grows the device's
+    volume tables (ksim_grow_volumes: keys, classes, refs, zone verdicts, more slots) while the
+    device keeps every node's mounts, so the full reload happens once (no node events here) over
+    hundreds of Schedule + assume calls and removals; every decision matches the oracle's cache."""
+    import copy
+    import random
+    preds, prios = POLICIES["default"]
+    ref = R.SchedulerCache(set(preds), prios)
+    dut = SchedulerCache(preds, prios, device=0)
+    rng = random.Random(5)
+    try:
+        for i in range(24):
+            node = {"metadata": {"name": "v-%02d" % i, "labels": {"kubernetes.io/hostname": "v-%02d" % i}},
+                    "status": {"allocatable": {"cpu": "16", "memory": "32Gi", "pods": "110"}}}
+            apply(ref, ("add_node", node))
+            apply(dut, ("add_node", node))
+        for k in range(360):
+            added = sorted(key for key in ref.pod_states if key not in ref.assumed)
+            if k % 9 == 8 and added:
+                ev = ("remove_pod", copy.deepcopy(ref.pod_states[rng.choice(added)]))
+            elif k % 9 == 7 and ref.assumed:
+                ev = ("add_pod", copy.deepcopy(ref.pod_states[sorted(ref.assumed)[0]]))
+            else:
+                vols = []
+                for v in range(rng.choice([1, 1, 2, 3])):
+                    if rng.random() < 0.5:
+                        vols.append({"name": "g%d" % v, "gcePersistentDisk": {"pdName": "pd-%d" % rng.randrange(150),
+                                                                              "readOnly": rng.random() < 0.4}})
+                    else:
+                        vols.append({"name": "e%d" % v, "awsElasticBlockStore": {"volumeID": "vol-%d" % rng.randrange(150)}})
+                name = "vp-%d" % k
+                ev = ("schedule", {"metadata": {"name": name, "namespace": "", "uid": name},
+                                   "spec": {"containers": [{"resources": {"requests": {"cpu": "100m"}}}], "volumes": vols}})
+            want = apply(ref, ev)
+            got = apply(dut, ev)
+            if ev[0] == "schedule":
+                assert got == want, (ev[1]["metadata"]["name"], want, got)
+        assert dut.last_node_index == ref.sched.last_node_index
+        assert dut.vol_loads == 1 and dut.vol_grows > 20
+    finally:
+        dut.close()

@@ -11,7 +11,7 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_cache.py -m gpu -x -v --tim
 tail -3 $OUT/pytest_cache.log
 timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "golden_priorities or golden_reduce" > $OUT/pytest_golden.log 2>&1 || { echo "golden tests failed"; grep -E "^E |FAILED" $OUT/pytest_golden.log | head -20; exit 1; }
 tail -2 $OUT/pytest_golden.log
-timeout -k 10 400 python3 -u bench.py --workload c2x --cpu-sample 0 > $OUT/bench_c2x.json 2> $OUT/bench_c2x.err || { echo "c2x bench failed"; tail -20 $OUT/bench_c2x.err; exit 1; }
+timeout -k 10 400 python3 -u bench.py --workload c2x --cpu-sample 0 --per-pod-calls 200 > $OUT/bench_c2x.json 2> $OUT/bench_c2x.err || { echo "c2x bench failed"; tail -20 $OUT/bench_c2x.err; exit 1; }
 python3 -c "import json,sys; d=json.load(open('$OUT/bench_c2x.json')); print(d['value'], json.dumps(d.get('per_pod')))"
-timeout -k 10 400 python3 -u bench.py --workload c2 --cpu-sample 0 > $OUT/bench_c2.json 2> $OUT/bench_c2.err || { echo "c2 bench failed"; tail -20 $OUT/bench_c2.err; exit 1; }
+timeout -k 10 400 python3 -u bench.py --workload c2 --cpu-sample 0 --per-pod-calls 200 > $OUT/bench_c2.json 2> $OUT/bench_c2.err || { echo "c2 bench failed"; tail -20 $OUT/bench_c2.err; exit 1; }
 python3 -c "import json,sys; d=json.load(open('$OUT/bench_c2.json')); print(d['value'], json.dumps(d.get('per_pod')))"
