@@ -106,11 +106,12 @@ static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
   if ((rc = dev_upload(h, &dev, &V, 1))) return rc;
   HIPCHK(h, hipStreamSynchronize(h->stream));
   const bool carry = keep && t->vol_slots == h->vol_h.vol_slots;
+  std::vector<void*> fresh;  // this load's buffers (taken before any free shifts h->bufs)
+  for (size_t k = nb0; k < h->bufs.size(); ++k) fresh.push_back(h->bufs[k].p);
+  if (carry) { fresh.push_back(slots); fresh.push_back(sc); }
   for (void* q : h->vol_bufs)  // the previous tables (reload), except the mounts carried over
-    if (!(carry && (q == (void*)h->vol_h.slots || q == (void*)h->vol_h.slot_count))) dev_free(h, q);
-  h->vol_bufs.clear();
-  if (carry) { h->vol_bufs.push_back(slots); h->vol_bufs.push_back(sc); }
-  for (size_t k = nb0; k < h->bufs.size(); ++k) h->vol_bufs.push_back(h->bufs[k].p);
+    if (!(carry && (q == (void*)slots || q == (void*)sc))) dev_free(h, q);
+  h->vol_bufs = fresh;
   h->vol_dev = dev;
   h->vol_h = V;
   h->ctx.vol = dev;
