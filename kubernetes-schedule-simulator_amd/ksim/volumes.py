@@ -326,7 +326,7 @@ def build_tables(index: VolumeIndex, n, mounts, queued_classes, label_sets, max_
     zone_ok, zone_err = index.zone_verdicts(label_sets) if zone is None else zone
     return dict(key_filter=key_filter, vc=vc, vc_filter=np.asarray(index.class_filter, np.uint32), refs=ref_arr,
                 zone_ok=np.ascontiguousarray(zone_ok), zone_words=int(zone_ok.shape[1]), zone_err=zone_err,
-                slots=slots, slot_count=count, vol_slots=S, n_nodes=n,
+                slots=slots, slot_count=count, vol_slots=S, n_nodes=n, grow_only=mounts is None,
                 max_vols=tuple(max_vols() if max_limits is None else max_limits))
 
 
@@ -347,7 +347,7 @@ def tables_struct(d, use_zone=True):
     if use_zone and d["zone_words"]:
         t.zone_words = d["zone_words"]
         t.zone_ok = abi.ptr(d["zone_ok"], abi.C.c_uint32)
-    if d["slots"].size:
+    if not d.get("grow_only"):
         t.slots = abi.ptr(d["slots"], abi.C.c_uint64)
         t.slot_count = abi.ptr(d["slot_count"], abi.C.c_int32)
     return t
