@@ -106,7 +106,7 @@ def parse():
     ap.add_argument("--c4-pods", type=int, default=20000,
                     help="c3 line: pods of the 1M-node C4 streaming side measurement (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
-    ap.add_argument("--per-pod-calls", type=int, default=0,
+    ap.add_argument("--per-pod-calls", type=int, default=200,
                     help="c2 / c2x: timed ksim_schedule_one calls through the per-pod mirror at each "
                          "cached-pod mark (0 = skip the per_pod side line)")
     ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c2x", "c4", "c5"],
