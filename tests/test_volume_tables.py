@@ -145,3 +145,41 @@ def test_random_verdicts_and_commits(seed):
         for i, ni in enumerate(infos):
             ok, _ = preds["NoDiskConflict"](p, ni)
             assert _model_fits(cl, "NoDiskConflict", q, i, mounts[i]) == ok
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_grown_tables_match_full_build(seed):
+    """What the per-pod path hands ksim_grow_volumes (build_tables without mounts, zone verdicts
+    of the new classes appended to the old ones) equals the full build's class-side arrays, and
+    carries no slot arrays."""
+    import numpy as np
+    from ksim.volumes import build_tables, tables_struct
+    rng = random.Random(100 + seed)
+    names = ["v1", "v2", "v3", "v4", "v5", "v6"]
+    nodes = []
+    for i in range(5):
+        labels = {R.ZONE_LABEL: rng.choice(["a", "b", "c"])} if rng.random() < 0.6 else {}
+        nodes.append({"metadata": {"name": "n%d" % i, "labels": labels},
+                      "status": {"allocatable": {"cpu": "64", "memory": "64Gi", "pods": "200"}}})
+    queued = [{"metadata": {"name": "q%d" % k, "namespace": "ns"},
+               "spec": {"volumes": [_rand_volume(rng, names) for _ in range(rng.randint(1, 3))],
+                        "containers": [{"name": "c"}]}} for k in range(16)]
+    pvs, pvcs = _listers(rng)
+    cl = ingest.Cluster.from_objects(nodes, (), queued, pvs=pvs, pvcs=pvcs)
+    if cl.volumes is None:
+        return
+    idx, ls = cl.volume_index, cl.label_sets.items
+    full_ok, full_err = idx.zone_verdicts(ls)
+    k = len(idx.class_refs) // 2
+    head_ok, head_err = idx.zone_verdicts(ls, first=0)
+    tail_ok, tail_err = idx.zone_verdicts(ls, first=k)
+    assert np.array_equal(np.concatenate([head_ok[:k], tail_ok]), full_ok)
+    full = build_tables(idx, cl.n_nodes, [{} for _ in range(cl.n_nodes)], (), ls, vol_slots=8)
+    grow = build_tables(idx, cl.n_nodes, None, (), ls, vol_slots=8, zone=(full_ok, full_err))
+    for name in ("key_filter", "vc", "vc_filter", "zone_ok"):
+        assert np.array_equal(full[name], grow[name]), name
+    assert np.array_equal(full["refs"], grow["refs"])
+    t = tables_struct(grow)
+    assert not t.slots and not t.slot_count and t.vol_slots == 8
+    t_full = tables_struct(full)
+    assert t_full.slots and t_full.slot_count
