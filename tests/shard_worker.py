@@ -11,6 +11,10 @@ sys.path[:0] = [os.path.join(ROOT, "kubernetes-schedule-simulator_amd")]
 def main():
     rank, world, port, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4]
     skew = float(sys.argv[5]) if len(sys.argv) > 5 else 0.0
+    # cluster shape (default: the 40k-node rehearsal) and the call split of the pod range
+    n_nodes = int(sys.argv[6]) if len(sys.argv) > 6 else 40_000
+    n_pods = int(sys.argv[7]) if len(sys.argv) > 7 else 2500
+    split = int(sys.argv[8]) if len(sys.argv) > 8 else 1200
     import time
     import numpy as np
     import torch
@@ -19,15 +23,15 @@ def main():
     device = rank % max(1, torch.cuda.device_count())
     from ksim import scheduler, synth
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%s" % port, rank=rank, world_size=world)
-    cl, p, q = synth.config_c3(40_000, 2500, seed=9)
+    cl, p, q = synth.config_c3(n_nodes, n_pods, seed=9)
     s = scheduler.ShardedScheduler(cl, p, q, rank, world, device=device)
     s.connect_torch(dist)
     dist.barrier()
     if skew and rank == world - 1:
         time.sleep(skew)  # launch skew beyond the 2 s per-pod bound: the start handshake absorbs it
-    o1, _, _ = s.schedule(0, 1200)
+    o1, _, _ = s.schedule(0, split)
     dist.barrier()
-    o2, _, _ = s.schedule(1200, 1300)
+    o2, _, _ = s.schedule(split, n_pods - split)
     st = s.node_state()
     np.savez(out, out=np.concatenate([o1, o2]), ctr=np.uint64(s.last_node_index), lo=s.lo, hi=s.hi,
              **{k: st[k] for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count")})

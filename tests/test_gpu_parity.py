@@ -529,6 +529,43 @@ def test_node_sharded_fills_cluster_with_fit_errors(monkeypatch):
     assert all(s.last_node_index == ref_ctr for s in scheds)
 
 
+def _sharded_processes(tmp_path, world, skew, n_nodes, n_pods, split, env_extra=None, wait=150):
+    """`world` shard_worker.py processes over a gloo group; returns their .npz results."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ)
+    env.update(env_extra or {})
+    worker = os.path.join(os.path.dirname(__file__), "shard_worker.py")
+    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(port), str(tmp_path / ("r%d.npz" % r)),
+                               str(skew), str(n_nodes), str(n_pods), str(split)], env=env) for r in range(world)]
+    try:
+        rcs = [pr.wait(timeout=wait) for pr in procs]
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    assert rcs == [0] * world
+    return [np.load(tmp_path / ("r%d.npz" % r)) for r in range(world)]
+
+
+def _check_sharded(res, n_nodes, n_pods, threads=8):
+    import cpu_ref
+    from ksim import synth
+    cl, p, q = synth.config_c3(n_nodes, n_pods, seed=9)
+    ref, _, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, n_pods, threads=threads)
+    assert np.array_equal(scheduler.merge_sharded([r["out"] for r in res]), ref)
+    assert sum(int(r["hi"]) - int(r["lo"]) for r in res) == n_nodes
+    for r in res:
+        assert int(r["ctr"]) == ref_ctr
+        lo, hi = int(r["lo"]), int(r["hi"])
+        for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+            assert np.array_equal(r[k], ref_state[k][lo:hi]), k
+
+
 @pytest.mark.parametrize("world,skew", [(2, 0.0), (2, 3.5), (4, 0.0), (8, 0.0)])
 def test_node_sharded_multi_process(tmp_path, world, skew):
     """`world` ranks in as many processes (the one-process-per-device layout: rank r on device
@@ -538,32 +575,27 @@ def test_node_sharded_multi_process(tmp_path, world, skew):
     KSIM_MAX_RANKS: every exchange slot and the decision's rank walk at full width.  skew: the
     last rank starts its first call 3.5 s late — beyond the 2 s per-pod spin bound — which the
     first pod's start handshake must absorb."""
-    import socket
-    import subprocess
-    import sys
     import torch
-    import cpu_ref
-    from ksim import synth
-    with socket.socket() as so:
-        so.bind(("127.0.0.1", 0))
-        port = so.getsockname()[1]
-    env = dict(os.environ)
+    env = {}
     if torch.cuda.device_count() < world:  # ranks share a device: their persistent grids must co-reside
         env["KSIM_MAX_GRID"] = str(256 // world // 2)
-    worker = os.path.join(os.path.dirname(__file__), "shard_worker.py")
-    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(port), str(tmp_path / ("r%d.npz" % r)),
-                               str(skew)], env=env) for r in range(world)]
-    rcs = [pr.wait(timeout=150) for pr in procs]
-    assert rcs == [0] * world
-    res = [np.load(tmp_path / ("r%d.npz" % r)) for r in range(world)]
-    cl, p, q = synth.config_c3(40_000, 2500, seed=9)
-    ref, _, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, 2500, threads=8)
-    assert np.array_equal(scheduler.merge_sharded([r["out"] for r in res]), ref)
-    for r in res:
-        assert int(r["ctr"]) == ref_ctr
-        lo, hi = int(r["lo"]), int(r["hi"])
-        for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
-            assert np.array_equal(r[k], ref_state[k][lo:hi]), k
+    res = _sharded_processes(tmp_path, world, skew, 40_000, 2500, 1200, env)
+    _check_sharded(res, 40_000, 2500)
+
+
+@pytest.mark.timeout(600)
+def test_node_sharded_c4_shape_world8(tmp_path):
+    """C4's real shard shape (BASELINE configs[3]: 1,000,000 nodes over 8 ranks = 125,000 name-rank
+    rows per shard), 3,000 pods in two calls, 8 processes.  On a one-GPU box all ranks share device
+    0: each rank's grid is capped at 32 workgroups (8 x 32 = every CU, one 512-thread workgroup per
+    CU), so every shard takes the streaming form at 3,907 rows per workgroup; on an 8-GPU node each
+    rank owns a device.  Placements, counters and every shard's node state equal the C oracle's."""
+    import torch
+    env = {"KSIM_SHARD_START_S": "60"}
+    if torch.cuda.device_count() < 8:
+        env["KSIM_MAX_GRID"] = "32"
+    res = _sharded_processes(tmp_path, 8, 0.0, 1_000_000, 3000, 1700, env, wait=300)
+    _check_sharded(res, 1_000_000, 3000, threads=16)
 
 
 @pytest.mark.parametrize("max_grid", [0, 128, 64, 28])  # rows per row thread: 1, 2, 4, 9

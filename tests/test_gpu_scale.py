@@ -24,6 +24,32 @@ def _invariants(cl, out, s):
     assert (s["req_cpu"] <= cl.cols["alloc_cpu"]).all() and (s["req_mem"] <= cl.cols["alloc_mem"]).all()
 
 
+@pytest.mark.timeout(900)
+def test_c3_full_queue_matches_c_oracle():
+    """BASELINE configs[2] exactly as bench.py times it: 100,000 nodes, the whole 1,000,000-pod
+    queue from the empty cluster in ONE ksim_schedule call (the persistent fast kernel), against the
+    C oracle over the same queue on 16 host threads (~100 s): every placement, the counter and the
+    final node state."""
+    cl, p, q = synth.config_c3(100_000, 1_000_000)
+    g = scheduler.GenericScheduler(cl, p, q, collect_reasons=True)
+    try:
+        out, reasons, st = g.schedule()
+        assert st.mode == abi.MODE_PERSISTENT and st.blocks > 1
+        s = g.node_state()
+        ctr = g.last_node_index
+    finally:
+        g.close()
+    ref, ref_reasons, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, 1_000_000, threads=16)
+    mism = np.flatnonzero(out != ref)
+    assert mism.size == 0, ("first mismatch at pod", int(mism[0]), int(out[mism[0]]), int(ref[mism[0]]), mism.size)
+    failed = out < 0
+    assert np.array_equal(reasons[failed], ref_reasons[failed])
+    assert ctr == ref_ctr
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+        assert np.array_equal(s[k], ref_state[k]), k
+    _invariants(cl, out, s)
+
+
 @pytest.mark.parametrize("mode", [abi.MODE_AUTO, abi.MODE_TREE], ids=["scan", "tree"])
 def test_c3_saturated_tail_matches_c_oracle(mode):
     """C3 (100k nodes): 2,950,000 pods on the GPU (past cpu saturation), then the next 3,000 on
