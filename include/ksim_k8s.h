@@ -101,6 +101,7 @@ typedef struct {
   int32_t qos_positive;              /* some cpu / memory request or limit is > 0 */
   int32_t n_ports;
   const ksim_k8s_port* ports;
+  const char* image;                 /* container.image (ImageLocalityPriority), NULL / "": none */
 } ksim_k8s_container;
 
 #define KSIM_K8S_VOL_GCE_PD 1
@@ -162,6 +163,8 @@ typedef struct {
   /* the RC / RS controllerRef NodePreferAvoidPods compares (kind, uid), NULL kind: none */
   const char* avoid_ctrl_kind;
   const char* avoid_ctrl_uid;
+  const char* uid;                      /* metadata.uid: the cache's pod key (getPodKey, node_info.go:497-503);
+                                           NULL / "": namespace/name */
 } ksim_k8s_pod;
 
 typedef struct {
@@ -177,6 +180,13 @@ typedef struct {
   const char* uid;
 } ksim_k8s_avoid;
 
+/* v1.ContainerImage of status.images. */
+typedef struct {
+  int32_t n_names;
+  const char* const* names;
+  int64_t size_bytes;
+} ksim_k8s_image;
+
 typedef struct {
   const char* name;
   int32_t n_labels;
@@ -191,7 +201,9 @@ typedef struct {
   const ksim_k8s_resource* alloc_other;
   int32_t n_avoid;
   const ksim_k8s_avoid* avoid;
-  int32_t has_images;                   /* status.images is non-empty (ImageLocalityPriority) */
+  int32_t has_images;                   /* status.images is non-empty (implied by n_images > 0) */
+  int32_t n_images;                     /* status.images (ImageLocalityPriority, image_locality.go:39-88) */
+  const ksim_k8s_image* images;
 } ksim_k8s_node;
 
 typedef struct {
@@ -220,6 +232,8 @@ typedef struct {
   int32_t max_vols[3];                  /* MaxPD limits (EBS, GCE PD, Azure Disk); 0: getMaxVols */
   int32_t port_slots;                   /* host-port slots per node, < 0: enough for the queue */
   int32_t vol_slots;                    /* volume slots per node, < 0: enough for the queue */
+  int32_t image_locality;               /* intern node / pod images (what ImageLocalityPriority reads):
+                                           0 = when some node lists status.images, 1 = always, -1 = never */
 } ksim_k8s_options;
 
 typedef struct ksim_k8s_cluster ksim_k8s_cluster;
@@ -248,6 +262,19 @@ int ksim_k8s_build(ksim_k8s_cluster* c);
  * annotations tell some pod class apart).  Creates the handle and loads the node table, class /
  * affinity / volume tables and the queue. */
 int ksim_k8s_open(ksim_k8s_cluster* c, const ksim_config* cfg, int64_t prefer_avoid_weight, ksim_handle** out);
+
+/* Weights of the priorities the front end evaluates per (pod class, label set) on the host — they
+ * have no ksim_config weight slot; 0 = not configured. */
+typedef struct {
+  int64_t prefer_avoid;   /* NodePreferAvoidPodsPriority (node_prefer_avoid_pods.go:32-68) */
+  int64_t image_locality; /* ImageLocalityPriority (image_locality.go:39-88): with images interned
+                             (ksim_k8s_options.image_locality), node images x pod container images;
+                             KSIM_E_UNSUPPORTED when some node lists images the snapshot did not intern */
+} ksim_k8s_weights;
+
+/* ksim_k8s_open for a policy that may weigh ImageLocalityPriority; ksim_k8s_open(c, cfg, w_pa, out) is
+ * ksim_k8s_open_ex with {w_pa, 0}: a policy without ImageLocalityPriority. */
+int ksim_k8s_open_ex(ksim_k8s_cluster* c, const ksim_config* cfg, const ksim_k8s_weights* w, ksim_handle** out);
 
 /* Name-rank order and sizes of the built snapshot. */
 int64_t ksim_k8s_node_count(const ksim_k8s_cluster* c);
@@ -278,6 +305,64 @@ int ksim_k8s_describe(ksim_k8s_cluster* c, ksim_handle* h, const ksim_k8s_pod* p
                       int32_t port_cap, int32_t* n_ports, ksim_scalar_req* scalars, int32_t scalar_cap,
                       int32_t* n_scalars, int64_t* pod_id);
 int ksim_k8s_bind(ksim_k8s_cluster* c, int64_t pod_id, int64_t node);
+/* The snapshot's per-pod path follows bindings only: once a node or pod event has reached the handle
+ * directly (ksim_node_* / ksim_pod_*), describe refuses with KSIM_E_STATE rather than reload tables
+ * from a stale view.  Event-driven callers use the scheduler cache below. */
+
+/* ==== The scheduler cache: the complete per-pod drop-in ===================================
+ * schedulercache.Cache (schedulercache/cache.go:125-393) + genericScheduler.Schedule
+ * (core/generic_scheduler.go:112-198) over the device-resident table, driven by the informer events
+ * the reference's config factory wires (factory/factory.go:596 addPodToCache, :613 updatePodInCache,
+ * :695 deletePodFromCache, :740 addNodeToCache, :755 updateNodeInCache, :841 deleteNodeFromCache)
+ * and by scheduleOne (scheduler.go:431-484: Schedule, assume = AssumePod, ForgetPod on a failed
+ * bind, :412).  Every string rule is evaluated in the library; node rows, class / affinity / volume
+ * tables grow or are reloaded as the events require.  The errors are cache.go's (KSIM_E_STATE, the
+ * reference's message in ksim_k8s_cache_last_error); inputs the reference errs on are
+ * KSIM_E_UNSUPPORTED, never a silently different placement. */
+typedef struct ksim_k8s_cache ksim_k8s_cache;
+
+typedef struct {
+  ksim_config cfg;          /* device, mode, predicate bits, priority weights (ksim_create) */
+  ksim_k8s_weights extra;   /* NodePreferAvoidPods / ImageLocality weights */
+  int32_t hard_weight;      /* hardPodAffinitySymmetricWeight */
+  int32_t max_vols[3];      /* MaxPD limits (EBS, GCE PD, Azure Disk); 0: getMaxVols */
+  int32_t port_slots;       /* host-port slots per node row (<= 0: 8) */
+  int32_t check_volume_binding; /* CheckVolumeBinding is configured (no kernel bit: refusals only) */
+} ksim_k8s_cache_options;
+
+int ksim_k8s_cache_create(const ksim_k8s_cache_options* opt, ksim_k8s_cache** out);
+void ksim_k8s_cache_destroy(ksim_k8s_cache* c);
+const char* ksim_k8s_cache_last_error(const ksim_k8s_cache* c);
+/* the PV / PVC / StorageClass listers the volume predicates resolve PVCs through */
+int ksim_k8s_cache_add_pv(ksim_k8s_cache* c, const ksim_k8s_pv* pv);
+int ksim_k8s_cache_add_pvc(ksim_k8s_cache* c, const ksim_k8s_pvc* pvc);
+int ksim_k8s_cache_add_storage_class(ksim_k8s_cache* c, const ksim_k8s_storage_class* sc);
+/* node events: AddNode / UpdateNode → NodeInfo.SetNode (cache.go:354-375); RemoveNode (:378-393): the
+ * node leaves the listed set, its NodeInfo stays while pods remain on it */
+int ksim_k8s_cache_add_node(ksim_k8s_cache* c, const ksim_k8s_node* node);
+int ksim_k8s_cache_update_node(ksim_k8s_cache* c, const ksim_k8s_node* old_node, const ksim_k8s_node* new_node);
+int ksim_k8s_cache_remove_node(ksim_k8s_cache* c, const ksim_k8s_node* node);
+/* pod events (pod->node_name = the node it is bound / assumed to): AssumePod (:125-143), ForgetPod
+ * (:170-197), AddPod (:230-262, confirms an assumed pod), UpdatePod (:265-289), RemovePod (:292-318) */
+int ksim_k8s_cache_assume_pod(ksim_k8s_cache* c, const ksim_k8s_pod* pod);
+int ksim_k8s_cache_forget_pod(ksim_k8s_cache* c, const ksim_k8s_pod* pod);
+int ksim_k8s_cache_add_pod(ksim_k8s_cache* c, const ksim_k8s_pod* pod);
+int ksim_k8s_cache_update_pod(ksim_k8s_cache* c, const ksim_k8s_pod* old_pod, const ksim_k8s_pod* new_pod);
+int ksim_k8s_cache_remove_pod(ksim_k8s_cache* c, const ksim_k8s_pod* pod);
+/* genericScheduler.Schedule over the listed nodes; assume = KSIM_SCHEDULE_ASSUME also runs
+ * Scheduler.assume (the pod enters the cache on the chosen node as an assumed pod).  KSIM_OK with
+ * out->node = the host's name rank (ksim_k8s_cache_node_name), or -1 for a FitError
+ * (ksim_k8s_cache_fit_error gives its text); KSIM_E_NO_NODES when no node is listed. */
+int ksim_k8s_cache_schedule(ksim_k8s_cache* c, const ksim_k8s_pod* pod, int32_t assume, ksim_result* out);
+/* FitError.Error of a result (generic_scheduler.go:72-90) into buf (NUL-terminated, truncated to cap);
+ * returns the full length. */
+int32_t ksim_k8s_cache_fit_error(const ksim_k8s_cache* c, const ksim_result* res, char* buf, int32_t cap);
+int64_t ksim_k8s_cache_node_count(const ksim_k8s_cache* c);
+const char* ksim_k8s_cache_node_name(const ksim_k8s_cache* c, int64_t rank);
+/* the cache's scheduling handle (ksim_get_counter, ksim_read_nodes, ...); owned by the cache */
+ksim_handle* ksim_k8s_cache_handle(ksim_k8s_cache* c);
+/* counters of table work: [0] affinity loads, [1] volume loads, [2] volume grows, [3] class loads */
+int ksim_k8s_cache_stats(const ksim_k8s_cache* c, int64_t* out4);
 
 #ifdef __cplusplus
 }

@@ -1,978 +1,11 @@
-// ksim_k8s.cpp — the Kubernetes-field front end (include/ksim_k8s.h): interns the string-valued
-// scheduling inputs of v1 objects and evaluates every string comparison the scheduler makes, once
-// per (pod class, node label set / taint set), into the device tables of include/ksim.h.
-//
-// Reference semantics (paths under vendor/k8s.io/; S/ = kubernetes/pkg/scheduler/):
-//  - label selectors: apimachinery/pkg/labels/selector.go:193-235 (Requirement.Matches), :837-853
-//    (SelectorFromSet), NewRequirement's validation (:124-170), validation.IsQualifiedName /
-//    IsValidLabelValue (apimachinery/pkg/util/validation/validation.go:34-112);
-//    metav1.LabelSelectorAsSelector (apimachinery/pkg/apis/meta/v1/helpers.go:31-70);
-//    NodeSelectorRequirementsAsSelector (kubernetes/pkg/apis/core/v1/helper/helpers.go:215-245);
-//  - podMatchesNodeLabels / nodeMatchesNodeSelectorTerms: S/algorithm/predicates/predicates.go:780-838;
-//  - PodToleratesNodeTaints / ToleratesTaint: predicates.go:1465-1494, api/core/v1/toleration.go:37-56;
-//  - TaintToleration / NodeAffinity map values: S/algorithm/priorities/taint_toleration.go:29-73,
-//    node_affinity.go:34-75; NodePreferAvoidPods: node_prefer_avoid_pods.go:32-68;
-//  - NodeInfo.SetNode / AddPod, calculateResource: S/schedulercache/node_info.go:318-448;
-//    GetResourceRequest: predicates.go:659-697; GetNonzeroRequests: priorities/util/non_zero.go:38-53;
-//    CheckNodeConditionPredicate: predicates.go:1534-1568; HostPortInfo: S/util/utils.go:31-155;
-//  - inter-pod affinity: predicates.go:1143-1450, priorities/interpod_affinity.go:118-240,
-//    priorities/util/topologies.go:28-71; SelectorSpread zones: utilnode.GetZoneKey;
-//  - volumes: predicates.go:220-285 (NoDiskConflict), :287-507 (MaxPD), :539-633 (VolumeZone).
-// The table layouts and the interning rules are the Python host's (ksim/ingest.py, labels.py,
-// affinity.py, volumes.py, scheduler.py), which tests/test_k8s_frontend.py compares this with.
-#include <algorithm>
-#include <array>
-#include <cerrno>
-#include <cstdarg>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <functional>
-#include <map>
-#include <set>
-#include <string>
-#include <tuple>
-#include <vector>
-
-#include "../../include/ksim_k8s.h"
-
-namespace {
-
-using Str = std::string;
-using Labels = std::map<Str, Str>;
-
-Str S(const char* p) { return p ? Str(p) : Str(); }
-
-struct Fail {
-  int code;
-  Str msg;
-};
-
-[[noreturn]] void fail(int code, const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof buf, fmt, ap);
-  va_end(ap);
-  throw Fail{code, buf};
-}
-
-// ---------------------------------------------------------------- labels (ksim/labels.py)
-bool alnum(char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9'); }
-
-// (?:[A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9]
-bool name_re(const Str& s) {
-  if (s.empty() || !alnum(s.front()) || !alnum(s.back())) return false;
-  for (char c : s)
-    if (!alnum(c) && c != '-' && c != '_' && c != '.') return false;
-  return true;
-}
-
-// DNS-1123 subdomain: [a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*
-bool dns_subdomain(const Str& s) {
-  if (s.empty()) return false;
-  size_t i = 0;
-  for (;;) {
-    size_t j = s.find('.', i);
-    const Str part = s.substr(i, j == Str::npos ? Str::npos : j - i);
-    if (part.empty()) return false;
-    auto lo = [](char c) { return (c >= 'a' && c <= 'z') || (c >= '0' && c <= '9'); };
-    if (!lo(part.front()) || !lo(part.back())) return false;
-    for (char c : part)
-      if (!lo(c) && c != '-') return false;
-    if (j == Str::npos) return true;
-    i = j + 1;
-  }
-}
-
-bool qualified_name(const Str& k) {
-  const size_t n = std::count(k.begin(), k.end(), '/');
-  if (n > 1) return false;
-  Str name = k;
-  if (n == 1) {
-    const size_t p = k.find('/');
-    const Str prefix = k.substr(0, p);
-    name = k.substr(p + 1);
-    if (prefix.empty() || prefix.size() > 253 || !dns_subdomain(prefix)) return false;
-  }
-  return !name.empty() && name.size() <= 63 && name_re(name);
-}
-
-bool label_value_ok(const Str& v) { return v.size() <= 63 && (v.empty() || name_re(v)); }
-
-bool parse_i64(const Str& s, int64_t* out) {
-  size_t i = 0;
-  if (i < s.size() && (s[i] == '+' || s[i] == '-')) ++i;
-  if (i == s.size()) return false;
-  for (size_t k = i; k < s.size(); ++k)
-    if (s[k] < '0' || s[k] > '9') return false;
-  errno = 0;
-  char* end = nullptr;
-  const long long v = strtoll(s.c_str(), &end, 10);
-  if (errno == ERANGE) return false;
-  *out = v;
-  return true;
-}
-
-enum Op { OP_IN, OP_NOTIN, OP_EXISTS, OP_DNE, OP_GT, OP_LT };
-
-struct Req {
-  Str key;
-  Str op;  // as spelled (validation and the interning key)
-  Op o;
-  std::vector<Str> vals;  // sorted
-  bool operator<(const Req& r) const { return std::tie(key, op, vals) < std::tie(r.key, r.op, r.vals); }
-  bool operator==(const Req& r) const { return key == r.key && op == r.op && vals == r.vals; }
-};
-
-// A selector: nothing = matches no label set (labels.Nothing()); otherwise an AND of requirements.
-struct Sel {
-  bool nothing = false;
-  std::vector<Req> reqs;
-  bool operator<(const Sel& s) const { return std::tie(nothing, reqs) < std::tie(s.nothing, s.reqs); }
-  bool operator==(const Sel& s) const { return nothing == s.nothing && reqs == s.reqs; }
-};
-
-// labels.NewRequirement with its validation; false on an error.
-bool requirement(const Str& key, const Str& op, std::vector<Str> vals, Req* out) {
-  if (!qualified_name(key)) return false;
-  Op o;
-  if (op == "In" || op == "NotIn") {
-    if (vals.empty()) return false;
-    o = op == "In" ? OP_IN : OP_NOTIN;
-  } else if (op == "=" || op == "==" || op == "!=") {
-    if (vals.size() != 1) return false;
-    o = op == "!=" ? OP_NOTIN : OP_IN;
-  } else if (op == "Exists" || op == "DoesNotExist") {
-    if (!vals.empty()) return false;
-    o = op == "Exists" ? OP_EXISTS : OP_DNE;
-  } else if (op == "Gt" || op == "Lt") {
-    int64_t x;
-    if (vals.size() != 1 || !parse_i64(vals[0], &x)) return false;
-    o = op == "Gt" ? OP_GT : OP_LT;
-  } else {
-    return false;
-  }
-  for (const Str& v : vals)
-    if (!label_value_ok(v)) return false;
-  std::sort(vals.begin(), vals.end());
-  *out = Req{key, op, o, vals};
-  return true;
-}
-
-bool req_matches(const Req& r, const Labels& lab) {
-  auto it = lab.find(r.key);
-  const bool has = it != lab.end();
-  switch (r.o) {
-    case OP_IN: return has && std::binary_search(r.vals.begin(), r.vals.end(), it->second);
-    case OP_NOTIN: return !has || !std::binary_search(r.vals.begin(), r.vals.end(), it->second);
-    case OP_EXISTS: return has;
-    case OP_DNE: return !has;
-    case OP_GT:
-    case OP_LT: {
-      if (!has || r.vals.size() != 1) return false;
-      int64_t lv, rv;
-      if (!parse_i64(it->second, &lv) || !parse_i64(r.vals[0], &rv)) return false;
-      return r.o == OP_GT ? lv > rv : lv < rv;
-    }
-  }
-  return false;
-}
-
-bool matches(const Sel& s, const Labels& lab) {
-  if (s.nothing) return false;
-  for (const Req& r : s.reqs)
-    if (!req_matches(r, lab)) return false;
-  return true;
-}
-
-// SelectorFromSet: an invalid key / value makes the selector Everything().
-Sel from_set(const std::vector<std::pair<Str, Str>>& kv) {
-  Sel s;
-  for (const auto& e : kv) {
-    Req r;
-    if (!requirement(e.first, "=", {e.second}, &r)) return Sel{};
-    s.reqs.push_back(r);
-  }
-  return s;
-}
-
-std::vector<Str> strs(int32_t n, const char* const* p) {
-  std::vector<Str> v;
-  for (int32_t i = 0; i < n; ++i) v.push_back(S(p[i]));
-  return v;
-}
-
-// NodeSelectorRequirementsAsSelector: Nothing for an empty list; false on an error.
-bool from_node_reqs(const std::vector<Req>& raw, Sel* out) {
-  if (raw.empty()) {
-    *out = Sel{true, {}};
-    return true;
-  }
-  Sel s;
-  for (const Req& e : raw) {
-    if (e.op != "In" && e.op != "NotIn" && e.op != "Exists" && e.op != "DoesNotExist" && e.op != "Gt" && e.op != "Lt")
-      return false;
-    Req r;
-    if (!requirement(e.key, e.op, e.vals, &r)) return false;
-    s.reqs.push_back(r);
-  }
-  *out = s;
-  return true;
-}
-
-// Raw requirement lists as passed (unvalidated, values unsorted).
-std::vector<Req> raw_reqs(int32_t n, const ksim_k8s_req* r) {
-  std::vector<Req> v;
-  for (int32_t i = 0; i < n; ++i) v.push_back(Req{S(r[i].key), S(r[i].op), OP_IN, strs(r[i].n_values, r[i].values)});
-  return v;
-}
-
-struct LabelSel {  // a metav1.LabelSelector as passed
-  bool present = false;
-  std::vector<std::pair<Str, Str>> ml;
-  std::vector<Req> exprs;
-};
-
-LabelSel copy_ls(const ksim_k8s_label_selector& x) {
-  LabelSel s;
-  s.present = x.present != 0;
-  for (int32_t i = 0; i < x.n_match_labels; ++i) s.ml.push_back({S(x.match_labels[i].key), S(x.match_labels[i].value)});
-  s.exprs = raw_reqs(x.n_exprs, x.exprs);
-  return s;
-}
-
-// LabelSelectorAsSelector: nil → Nothing, empty → Everything; false on an error.
-bool from_label_selector(const LabelSel& ls, Sel* out) {
-  if (!ls.present) {
-    *out = Sel{true, {}};
-    return true;
-  }
-  Sel s;
-  if (ls.ml.empty() && ls.exprs.empty()) {
-    *out = s;
-    return true;
-  }
-  std::map<Str, Str> ml;
-  for (const auto& e : ls.ml) ml[e.first] = e.second;  // a Go map: the last duplicate wins
-  for (const auto& e : ml) {
-    Req r;
-    if (!requirement(e.first, "=", {e.second}, &r)) return false;
-    s.reqs.push_back(r);
-  }
-  for (const Req& e : ls.exprs) {
-    if (e.op != "In" && e.op != "NotIn" && e.op != "Exists" && e.op != "DoesNotExist") return false;
-    Req r;
-    if (!requirement(e.key, e.op, e.vals, &r)) return false;
-    s.reqs.push_back(r);
-  }
-  *out = s;
-  return true;
-}
-
-// ---------------------------------------------------------------- object copies
-struct Taint {
-  Str key, value, effect;
-  bool operator<(const Taint& t) const { return std::tie(key, value, effect) < std::tie(t.key, t.value, t.effect); }
-  bool operator==(const Taint& t) const { return key == t.key && value == t.value && effect == t.effect; }
-};
-struct Tol {
-  Str key, op, value, effect;
-  bool operator<(const Tol& t) const { return std::tie(key, op, value, effect) < std::tie(t.key, t.op, t.value, t.effect); }
-};
-
-bool tolerates(const Tol& t, const Taint& x) {
-  if (!t.effect.empty() && t.effect != x.effect) return false;
-  if (!t.key.empty() && t.key != x.key) return false;
-  if (t.op.empty() || t.op == "Equal") return t.value == x.value;
-  return t.op == "Exists";
-}
-
-struct Avoid {
-  bool has = false;
-  Str kind, uid;
-  bool operator<(const Avoid& a) const { return std::tie(has, kind, uid) < std::tie(a.has, a.kind, a.uid); }
-};
-
-struct NodeObj {
-  Str name;
-  Labels labels;
-  std::vector<Taint> taints;
-  bool unschedulable = false;
-  std::vector<std::pair<Str, Str>> conds;
-  int64_t alloc[4] = {0, 0, 0, 0};
-  int64_t pods = 0;
-  std::vector<std::pair<Str, int64_t>> other;
-  std::vector<Avoid> avoid;
-  bool images = false;
-};
-
-struct Container {
-  bool has_cpu = false, has_mem = false;
-  int64_t cpu = 0, mem = 0, gpu = 0, eph = 0;
-  std::vector<std::pair<Str, int64_t>> other;
-  bool qos = false;
-  std::vector<std::tuple<Str, Str, int32_t>> ports;
-};
-
-struct PodTerm {
-  LabelSel sel;
-  std::vector<Str> nss;
-  Str key;
-  int32_t weight = 0;
-};
-
-struct Volume {
-  int32_t kind = 0;
-  bool ro = false;
-  Str id, pool, image;
-  std::vector<Str> monitors;
-};
-
-struct NodeAff {
-  bool has = false, has_required = false;
-  std::vector<std::vector<Req>> required;              // raw terms
-  std::vector<std::pair<int32_t, std::vector<Req>>> preferred;
-};
-
-struct PodObj {
-  Str name, ns;
-  Labels labels;
-  bool deleting = false;
-  Str node_name;
-  std::vector<Container> cs, init;
-  std::vector<std::pair<Str, Str>> node_selector;
-  NodeAff na;
-  std::vector<Tol> tols;
-  bool has_pa = false, has_anti = false;
-  std::vector<PodTerm> a_req, a_pref, n_req, n_pref;
-  std::vector<Volume> vols;
-  std::vector<Sel> spread;  // resolved SelectorSpread selectors
-  bool has_ctrl = false;
-  Str ctrl_kind, ctrl_uid;
-};
-
-std::vector<PodTerm> copy_terms(int32_t n, const ksim_k8s_pod_term* t) {
-  std::vector<PodTerm> v;
-  for (int32_t i = 0; i < n; ++i) {
-    PodTerm x;
-    x.sel = copy_ls(t[i].selector);
-    x.nss = strs(t[i].n_namespaces, t[i].namespaces);
-    x.key = S(t[i].topology_key);
-    x.weight = t[i].weight;
-    v.push_back(x);
-  }
-  return v;
-}
-
-Container copy_container(const ksim_k8s_container& c) {
-  Container x;
-  x.has_cpu = c.has_cpu != 0;
-  x.has_mem = c.has_mem != 0;
-  x.cpu = c.cpu_milli; x.mem = c.mem; x.gpu = c.gpu; x.eph = c.eph;
-  for (int32_t i = 0; i < c.n_other; ++i) x.other.push_back({S(c.other[i].name), c.other[i].value});
-  x.qos = c.qos_positive != 0;
-  for (int32_t i = 0; i < c.n_ports; ++i)
-    x.ports.emplace_back(S(c.ports[i].host_ip), S(c.ports[i].protocol), c.ports[i].host_port);
-  return x;
-}
-
-PodObj copy_pod(const ksim_k8s_pod& p) {
-  PodObj o;
-  o.name = S(p.name);
-  o.ns = S(p.namespace_);
-  for (int32_t i = 0; i < p.n_labels; ++i) o.labels[S(p.labels[i].key)] = S(p.labels[i].value);
-  o.deleting = p.deleting != 0;
-  o.node_name = S(p.node_name);
-  for (int32_t i = 0; i < p.n_containers; ++i) o.cs.push_back(copy_container(p.containers[i]));
-  for (int32_t i = 0; i < p.n_init_containers; ++i) o.init.push_back(copy_container(p.init_containers[i]));
-  {
-    std::map<Str, Str> ns;  // a Go map
-    for (int32_t i = 0; i < p.n_node_selector; ++i) ns[S(p.node_selector[i].key)] = S(p.node_selector[i].value);
-    o.node_selector.assign(ns.begin(), ns.end());
-  }
-  o.na.has = p.has_node_affinity != 0;
-  o.na.has_required = p.has_required != 0;
-  for (int32_t i = 0; i < p.n_required_terms; ++i)
-    o.na.required.push_back(raw_reqs(p.required_terms[i].n_reqs, p.required_terms[i].reqs));
-  for (int32_t i = 0; i < p.n_preferred; ++i)
-    o.na.preferred.push_back({p.preferred[i].weight, raw_reqs(p.preferred[i].preference.n_reqs, p.preferred[i].preference.reqs)});
-  for (int32_t i = 0; i < p.n_tolerations; ++i)
-    o.tols.push_back(Tol{S(p.tolerations[i].key), S(p.tolerations[i].op), S(p.tolerations[i].value), S(p.tolerations[i].effect)});
-  o.has_pa = p.has_pod_affinity != 0;
-  o.has_anti = p.has_pod_anti_affinity != 0;
-  o.a_req = copy_terms(p.n_affinity_required, p.affinity_required);
-  o.a_pref = copy_terms(p.n_affinity_preferred, p.affinity_preferred);
-  o.n_req = copy_terms(p.n_anti_required, p.anti_required);
-  o.n_pref = copy_terms(p.n_anti_preferred, p.anti_preferred);
-  for (int32_t i = 0; i < p.n_volumes; ++i) {
-    const ksim_k8s_volume& v = p.volumes[i];
-    o.vols.push_back(Volume{v.kind, v.read_only != 0, S(v.id), S(v.pool), S(v.image), strs(v.n_monitors, v.monitors)});
-  }
-  for (int32_t i = 0; i < p.n_spread; ++i) {
-    const LabelSel ls = copy_ls(p.spread[i]);
-    Sel s;
-    if (p.spread_set_selector && p.spread_set_selector[i]) {
-      s = from_set(ls.ml);
-    } else if (!from_label_selector(ls, &s)) {
-      continue;  // the caller's lister resolution keeps only parsable selectors
-    }
-    o.spread.push_back(s);
-  }
-  if (p.avoid_ctrl_kind) {
-    o.has_ctrl = true;
-    o.ctrl_kind = S(p.avoid_ctrl_kind);
-    o.ctrl_uid = S(p.avoid_ctrl_uid);
-  }
-  return o;
-}
-
-// ---------------------------------------------------------------- scheduling semantics
-bool pod_matches_node_labels(const PodObj& p, const Labels& lab) {
-  if (!p.node_selector.empty() && !matches(from_set(p.node_selector), lab)) return false;
-  if (p.na.has) {
-    if (!p.na.has_required) return true;
-    for (const auto& t : p.na.required) {
-      Sel s;
-      if (!from_node_reqs(t, &s)) return false;
-      if (matches(s, lab)) return true;
-    }
-    return false;
-  }
-  return true;
-}
-
-// CalculateNodeAffinityPriorityMap's count; false when a preferred term does not parse.
-bool preferred_weight(const PodObj& p, const Labels& lab, int64_t* out) {
-  int64_t count = 0;
-  for (const auto& t : p.na.preferred) {
-    if (t.first == 0) continue;
-    Sel s;
-    if (!from_node_reqs(t.second, &s)) return false;
-    if (matches(s, lab)) count += t.first;
-  }
-  *out = count;
-  return true;
-}
-
-bool is_scalar_resource(const Str& name) {
-  if (name.rfind("hugepages-", 0) == 0) return true;
-  if (name.find('/') == Str::npos || name.find("kubernetes.io/") != Str::npos || name.rfind("requests.", 0) == 0)
-    return false;
-  return qualified_name("requests." + name);
-}
-
-struct Res {
-  int64_t cpu = 0, mem = 0, gpu = 0, eph = 0;
-  std::vector<std::pair<Str, int64_t>> scalar;  // insertion order, presence kept
-  int64_t* find(const Str& n) {
-    for (auto& e : scalar)
-      if (e.first == n) return &e.second;
-    return nullptr;
-  }
-};
-
-struct Compiled {
-  Res pred, add;
-  int64_t nzc = 0, nzm = 0;
-};
-
-// GetResourceRequest / calculateResource / GetNonzeroRequests of one pod.
-Compiled container_requests(const PodObj& p) {
-  Compiled c;
-  for (const Container& x : p.cs) {
-    for (Res* r : {&c.pred, &c.add}) {
-      r->cpu += x.cpu; r->mem += x.mem; r->gpu += x.gpu; r->eph += x.eph;
-      for (const auto& o : x.other) {
-        if (!is_scalar_resource(o.first)) continue;
-        if (int64_t* v = r->find(o.first)) *v += o.second;
-        else r->scalar.push_back(o);
-      }
-    }
-    c.nzc += x.has_cpu ? x.cpu : 100;
-    c.nzm += x.has_mem ? x.mem : 200ll * 1024 * 1024;
-  }
-  for (const Container& x : p.init) {
-    c.pred.mem = std::max(c.pred.mem, x.mem);
-    c.pred.eph = std::max(c.pred.eph, x.eph);
-    c.pred.cpu = std::max(c.pred.cpu, x.cpu);
-    c.pred.gpu = std::max(c.pred.gpu, x.gpu);
-    for (const auto& o : x.other) {
-      if (!is_scalar_resource(o.first)) continue;
-      int64_t* v = c.pred.find(o.first);
-      if (!v) {
-        if (o.second > 0) c.pred.scalar.push_back(o);
-      } else if (o.second > *v) {
-        *v = o.second;
-      }
-    }
-  }
-  return c;
-}
-
-bool best_effort(const PodObj& p) {
-  for (const Container& x : p.cs)
-    if (x.qos) return false;
-  return true;
-}
-
-std::vector<std::tuple<Str, Str, int32_t>> host_ports(const PodObj& p) {
-  std::vector<std::tuple<Str, Str, int32_t>> out;
-  for (const Container& x : p.cs)
-    for (const auto& e : x.ports) {
-      if (std::get<2>(e) <= 0) continue;
-      const Str ip = std::get<0>(e).empty() ? "0.0.0.0" : std::get<0>(e);
-      const Str proto = std::get<1>(e).empty() ? "TCP" : std::get<1>(e);
-      out.emplace_back(ip, proto, std::get<2>(e));
-    }
-  return out;
-}
-
-bool has_pod_affinity(const PodObj& p) { return p.has_pa || p.has_anti; }
-
-bool is_pred_volume(const Volume& v) { return v.kind >= KSIM_K8S_VOL_GCE_PD && v.kind <= KSIM_K8S_VOL_PVC; }
-
-bool has_pred_volumes(const PodObj& p) {
-  for (const Volume& v : p.vols)
-    if (is_pred_volume(v)) return true;
-  return false;
-}
-
-// ---------------------------------------------------------------- interning
-template <class K>
-struct Interner {
-  std::map<K, int32_t> ids;
-  std::vector<K> items;
-  int32_t get(const K& k) {
-    auto it = ids.find(k);
-    if (it != ids.end()) return it->second;
-    const int32_t i = (int32_t)items.size();
-    ids.emplace(k, i);
-    items.push_back(k);
-    return i;
-  }
-  int32_t find(const K& k) const {
-    auto it = ids.find(k);
-    return it == ids.end() ? -1 : it->second;
-  }
-};
-
-struct LabelSetKey {
-  Labels labels;
-  std::vector<Avoid> avoid;
-  bool operator<(const LabelSetKey& o) const { return std::tie(labels, avoid) < std::tie(o.labels, o.avoid); }
-};
-
-// The part of a pod a class stands for: nodeSelector, node affinity, tolerations, RC / RS owner.
-struct ClassKey {
-  std::vector<std::pair<Str, Str>> ns;
-  bool na_has = false, na_req = false;
-  std::vector<std::vector<Req>> na_required;
-  std::vector<std::pair<int32_t, std::vector<Req>>> na_pref;
-  std::vector<Tol> tols;
-  bool has_ctrl = false;
-  Str kind, uid;
-  bool operator<(const ClassKey& o) const {
-    return std::tie(ns, na_has, na_req, na_required, na_pref, tols, has_ctrl, kind, uid) <
-           std::tie(o.ns, o.na_has, o.na_req, o.na_required, o.na_pref, o.tols, o.has_ctrl, o.kind, o.uid);
-  }
-};
-
-ClassKey class_key(const PodObj& p) {
-  ClassKey k;
-  k.ns = p.node_selector;
-  k.na_has = p.na.has;
-  k.na_req = p.na.has_required;
-  k.na_required = p.na.required;
-  k.na_pref = p.na.preferred;
-  k.tols = p.tols;
-  k.has_ctrl = p.has_ctrl;
-  k.kind = p.ctrl_kind;
-  k.uid = p.ctrl_uid;
-  return k;
-}
-
-PodObj class_pod(const ClassKey& k) {  // the class's pod-side inputs as a pod
-  PodObj p;
-  p.node_selector = k.ns;
-  p.na.has = k.na_has;
-  p.na.has_required = k.na_req;
-  p.na.required = k.na_required;
-  p.na.preferred = k.na_pref;
-  p.tols = k.tols;
-  p.has_ctrl = k.has_ctrl;
-  p.ctrl_kind = k.kind;
-  p.ctrl_uid = k.uid;
-  return p;
-}
-
-constexpr int KEY_ALL = 0, KEY_NODE = 1;
-const char* const HOSTNAME = "kubernetes.io/hostname";
-const char* const ZONE_KEY = "\x01zone";  // utilnode.GetZoneKey's domains (a pseudo key)
-
-Str zone_key_of(const Labels& lab) {
-  auto g = [&](const char* k) {
-    auto it = lab.find(k);
-    return it == lab.end() ? Str() : it->second;
-  };
-  const Str region = g("failure-domain.beta.kubernetes.io/region"), zone = g("failure-domain.beta.kubernetes.io/zone");
-  if (region.empty() && zone.empty()) return "";
-  return region + Str(":\0:", 3) + zone;
-}
-
-// ---------------------------------------------------------------- inter-pod affinity (affinity.py)
-struct SelItem {  // (namespaces, selector); any_of: a SelectorSpread OR-selector
-  std::vector<Str> nss;
-  bool any_of = false;
-  Sel sel;
-  std::vector<Sel> sels;
-  bool operator<(const SelItem& o) const { return std::tie(nss, any_of, sel, sels) < std::tie(o.nss, o.any_of, o.sel, o.sels); }
-};
-
-struct Ident {
-  Str ns;
-  Labels labels;
-  bool deleting = false;
-  bool operator<(const Ident& o) const { return std::tie(ns, labels, deleting) < std::tie(o.ns, o.labels, o.deleting); }
-};
-
-struct Term {  // ksim_aff_term
-  int32_t kind, pair, gate, exist, self_ok;
-  int64_t weight;
-  bool operator<(const Term& o) const {
-    return std::tie(kind, pair, gate, exist, self_ok, weight) < std::tie(o.kind, o.pair, o.gate, o.exist, o.self_ok, o.weight);
-  }
-};
-
-struct AClass {
-  std::vector<Term> req, pref;
-  std::vector<std::pair<int32_t, int64_t>> carries;
-  int32_t sp = -1;
-  bool operator<(const AClass& o) const { return std::tie(req, pref, carries, sp) < std::tie(o.req, o.pref, o.carries, o.sp); }
-};
-
-struct AffinityIndex {
-  std::vector<const Labels*> node_labels;
-  int32_t hard_weight = 10;
-  Interner<Str> keys;
-  Interner<SelItem> sels;
-  Interner<std::pair<int32_t, int32_t>> pairs;
-  Interner<std::tuple<int32_t, int32_t, int32_t>> carry;
-  Interner<Ident> idents;
-  Interner<AClass> aclasses;
-
-  AffinityIndex() {
-    keys.get(Str("\x01" "all"));
-    keys.get(Str("\x01" "node"));
-  }
-
-  std::pair<int32_t, Sel> sel_of(const PodObj& p, const PodTerm& t) {
-    std::vector<Str> nss = t.nss;
-    if (nss.empty()) nss.push_back(p.ns);
-    std::sort(nss.begin(), nss.end());
-    nss.erase(std::unique(nss.begin(), nss.end()), nss.end());
-    Sel s;
-    if (!from_label_selector(t.sel, &s)) fail(KSIM_E_UNSUPPORTED, "pod %s: affinity label selector does not parse", p.name.c_str());
-    SelItem it;
-    it.nss = nss;
-    it.sel = s;
-    return {sels.get(it), s};
-  }
-
-  int32_t ident(const PodObj& p) { return idents.get(Ident{p.ns, p.labels, p.deleting}); }
-
-  static bool in(const std::vector<Str>& v, const Str& x) { return std::binary_search(v.begin(), v.end(), x); }
-
-  static bool sel_matches(const Ident& id, const SelItem& s) {
-    if (!in(s.nss, id.ns)) return false;
-    if (s.any_of) {
-      if (id.deleting) return false;
-      for (const Sel& x : s.sels)
-        if (matches(x, id.labels)) return true;
-      return false;
-    }
-    return matches(s.sel, id.labels);
-  }
-
-  int32_t spread_pair(const PodObj& p) {
-    if (p.spread.empty()) return -1;
-    SelItem it;
-    it.nss = {p.ns};
-    it.any_of = true;
-    it.sels = p.spread;
-    const int32_t s = sels.get(it);
-    keys.get(ZONE_KEY);
-    return pairs.get({s, KEY_NODE});
-  }
-
-  int32_t aclass(const PodObj& p, bool with_spread) {
-    const int32_t sp = with_spread ? spread_pair(p) : -1;
-    if (!has_pod_affinity(p)) return sp < 0 ? -1 : aclasses.get(AClass{{}, {}, {}, sp});
-    AClass ac;
-    ac.sp = sp;
-    const Ident me{p.ns, p.labels, p.deleting};
-    for (int kind : {KSIM_AFF_REQ_AFFINITY, KSIM_AFF_REQ_ANTI}) {
-      const std::vector<PodTerm>& ts = kind == KSIM_AFF_REQ_AFFINITY ? p.a_req : p.n_req;
-      for (const PodTerm& t : ts) {
-        if (t.key.empty()) fail(KSIM_E_UNSUPPORTED, "pod %s: required pod (anti-)affinity term without topologyKey", p.name.c_str());
-        const int32_t s = sel_of(p, t).first;
-        int32_t mp, gate, ep;
-        if (t.key == HOSTNAME) {
-          mp = pairs.get({s, KEY_NODE});
-          gate = keys.get(t.key);
-          ep = mp;
-        } else {
-          const int32_t k = keys.get(t.key);
-          mp = pairs.get({s, k});
-          gate = k;
-          ep = pairs.get({s, KEY_ALL});
-        }
-        const int32_t self_ok = sel_matches(me, sels.items[s]) ? 1 : 0;
-        ac.req.push_back(Term{kind, mp, gate, ep, self_ok, 0});
-      }
-    }
-    for (int sign : {1, -1}) {
-      if (sign > 0 ? !p.has_pa : !p.has_anti) continue;
-      for (const PodTerm& t : sign > 0 ? p.a_pref : p.n_pref) {
-        const auto sv = sel_of(p, t);
-        if (t.key.empty() || sv.second.nothing) continue;
-        ac.pref.push_back(Term{KSIM_AFF_PREFERRED, pairs.get({sv.first, keys.get(t.key)}), 0, 0, 0, (int64_t)sign * t.weight});
-      }
-    }
-    std::map<int32_t, int64_t> carries;
-    auto add_carry = [&](const PodTerm& t, int32_t kind, int64_t amount) {
-      const auto sv = sel_of(p, t);
-      if (t.key.empty()) {
-        if (kind == KSIM_AFF_CARRY_ANTI) fail(KSIM_E_UNSUPPORTED, "pod %s: required anti-affinity term without topologyKey", p.name.c_str());
-        return;
-      }
-      if (sv.second.nothing) return;
-      const int32_t e = carry.get(std::make_tuple(sv.first, keys.get(t.key), kind));
-      carries[e] += amount;
-    };
-    for (const PodTerm& t : p.n_req) add_carry(t, KSIM_AFF_CARRY_ANTI, 1);
-    if (p.has_pa) {
-      if (hard_weight > 0)
-        for (const PodTerm& t : p.a_req) add_carry(t, KSIM_AFF_CARRY_PRIO, hard_weight);
-      for (const PodTerm& t : p.a_pref) add_carry(t, KSIM_AFF_CARRY_PRIO, t.weight);
-    }
-    if (p.has_anti)
-      for (const PodTerm& t : p.n_pref) add_carry(t, KSIM_AFF_CARRY_PRIO, -(int64_t)t.weight);
-    for (const auto& e : carries)
-      if (e.second != 0 || std::get<2>(carry.items[e.first]) == KSIM_AFF_CARRY_ANTI) ac.carries.push_back(e);
-    std::stable_sort(ac.req.begin(), ac.req.end(),
-                     [](const Term& a, const Term& b) { return (a.kind != KSIM_AFF_REQ_AFFINITY) < (b.kind != KSIM_AFF_REQ_AFFINITY); });
-    if (ac.req.empty() && ac.pref.empty() && ac.carries.empty() && sp < 0) return -1;
-    return aclasses.get(ac);
-  }
-};
-
-struct AffTables {
-  int32_t n_keys = 0, n_sel = 0, n_ident = 0, n_pair = 0, n_carry = 0, n_aclass = 0, sw = 0, cw = 0, zone_key = -1;
-  std::vector<int32_t> dom, n_dom, pair_sel, pair_key, carry_key, carry_kind, ac, spread_pair, cnt;
-  std::vector<int64_t> pair_off, carry_off, carried;
-  std::vector<uint64_t> isel, ianti, iprio;
-  std::vector<ksim_aff_term> terms;
-  std::vector<ksim_aff_carry> carries;
-  std::vector<int32_t> remap;  // interned identity -> aff_ident
-};
-
-// ---------------------------------------------------------------- volumes (volumes.py)
-struct VolKey {
-  Str tag, a, b, c;
-  bool operator<(const VolKey& o) const { return std::tie(tag, a, b, c) < std::tie(o.tag, o.a, o.b, o.c); }
-};
-
-struct ZoneEntry {  // one PVC's VolumeZone input: error / skip / the PV's zone labels
-  int kind = 0;     // 0 labels, 1 error, 2 skip
-  std::vector<std::pair<Str, Str>> labels;
-  bool operator<(const ZoneEntry& o) const { return std::tie(kind, labels) < std::tie(o.kind, o.labels); }
-};
-
-struct PV {
-  Labels labels;
-  int32_t kind = 0;
-  Str id;
-  bool node_affinity = false;
-};
-struct PVC {
-  Str volume_name;
-  bool has_sc = false;
-  Str sc;
-};
-
-const uint32_t ALL_FILTERS = KSIM_VOL_EBS | KSIM_VOL_GCE_PD | KSIM_VOL_AZURE_DISK;
-const char* const ZONE_LABEL = "failure-domain.beta.kubernetes.io/zone";
-const char* const REGION_LABEL = "failure-domain.beta.kubernetes.io/region";
-
-struct VolumeIndex {
-  std::map<Str, PV> pvs;
-  std::map<std::pair<Str, Str>, PVC> pvcs;
-  std::map<Str, std::pair<bool, Str>> scs;  // name -> (binding mode set, mode)
-  Interner<VolKey> keys;
-  std::vector<uint32_t> key_filter;
-  std::map<std::pair<std::vector<std::pair<int32_t, uint32_t>>, std::vector<ZoneEntry>>, int32_t> classes;
-  std::vector<std::vector<std::pair<int32_t, uint32_t>>> class_refs;
-  std::vector<uint32_t> class_filter;
-  std::vector<std::vector<ZoneEntry>> class_zone;
-  bool err_claim = false, err_binding = false;
-
-  int32_t key(const VolKey& k, uint32_t filt) {
-    const int32_t n = (int32_t)keys.items.size();
-    const int32_t i = keys.get(k);
-    if (i == n) key_filter.push_back(filt);
-    return i;
-  }
-
-  // the PV behind a PVC as MaxPD resolves it; false when the PV is not of a counted kind
-  bool pvc_target(const Str& ns, const Str& claim, VolKey* k, uint32_t* f) {
-    auto pc = pvcs.find({ns, claim});
-    const PV* pv = nullptr;
-    if (pc != pvcs.end() && !pc->second.volume_name.empty()) {
-      auto it = pvs.find(pc->second.volume_name);
-      if (it != pvs.end()) pv = &it->second;
-    }
-    if (!pv) {
-      *k = VolKey{"PVC", ns, claim, ""};
-      *f = ALL_FILTERS;
-      return true;
-    }
-    switch (pv->kind) {
-      case KSIM_K8S_VOL_EBS: *k = VolKey{"EBS", pv->id, "", ""}; *f = KSIM_VOL_EBS; return true;
-      case KSIM_K8S_VOL_GCE_PD: *k = VolKey{"GCE", pv->id, "", ""}; *f = KSIM_VOL_GCE_PD; return true;
-      case KSIM_K8S_VOL_AZURE_DISK: *k = VolKey{"AZ", pv->id, "", ""}; *f = KSIM_VOL_AZURE_DISK; return true;
-      default: return false;
-    }
-  }
-
-  ZoneEntry zone_entry(const Str& ns, const Str& claim) {
-    ZoneEntry z;
-    auto pc = pvcs.find({ns, claim});
-    if (pc == pvcs.end()) { z.kind = 1; return z; }
-    if (pc->second.volume_name.empty()) {
-      if (pc->second.has_sc && !pc->second.sc.empty()) {
-        auto s = scs.find(pc->second.sc);
-        if (s != scs.end()) {
-          if (!s->second.first) { z.kind = 1; return z; }
-          if (s->second.second == "WaitForFirstConsumer") { z.kind = 2; return z; }
-        }
-      }
-      z.kind = 1;
-      return z;
-    }
-    auto it = pvs.find(pc->second.volume_name);
-    if (it == pvs.end()) { z.kind = 1; return z; }
-    for (const auto& l : it->second.labels)
-      if (l.first == ZONE_LABEL || l.first == REGION_LABEL) z.labels.push_back(l);
-    return z;
-  }
-
-  void binding_check(const Str& ns, const Str& claim) {
-    auto pc = pvcs.find({ns, claim});
-    const PV* pv = nullptr;
-    if (pc != pvcs.end()) {
-      auto it = pvs.find(pc->second.volume_name);
-      if (it != pvs.end()) pv = &it->second;
-    }
-    if (!pv || pv->node_affinity) err_binding = true;
-  }
-
-  // (refs, zone list, has a PVC) of one pod's volumes
-  void refs(const PodObj& p, bool queued, std::vector<std::pair<int32_t, uint32_t>>* out, std::vector<ZoneEntry>* zone,
-            bool* has_pvc) {
-    *has_pvc = false;
-    for (const Volume& v : p.vols) {
-      const uint32_t ro_rw = KSIM_VOL_CONFLICT_RW | KSIM_VOL_READ_ONLY;
-      switch (v.kind) {
-        case KSIM_K8S_VOL_GCE_PD:
-          out->push_back({key(VolKey{"GCE", v.id, "", ""}, KSIM_VOL_GCE_PD), v.ro ? ro_rw : KSIM_VOL_CONFLICT_ANY});
-          break;
-        case KSIM_K8S_VOL_EBS:
-          out->push_back({key(VolKey{"EBS", v.id, "", ""}, KSIM_VOL_EBS), KSIM_VOL_CONFLICT_ANY | (v.ro ? KSIM_VOL_READ_ONLY : 0u)});
-          break;
-        case KSIM_K8S_VOL_ISCSI:
-          out->push_back({key(VolKey{"ISCSI", v.id, "", ""}, 0), v.ro ? ro_rw : KSIM_VOL_CONFLICT_ANY});
-          break;
-        case KSIM_K8S_VOL_RBD: {
-          std::vector<Str> seen;
-          for (const Str& m : v.monitors) {  // haveOverlap: some monitor shared
-            if (std::find(seen.begin(), seen.end(), m) != seen.end()) continue;
-            seen.push_back(m);
-            out->push_back({key(VolKey{"RBD", m, v.pool, v.image}, 0), v.ro ? ro_rw : KSIM_VOL_CONFLICT_ANY});
-          }
-          break;
-        }
-        case KSIM_K8S_VOL_AZURE_DISK:
-          out->push_back({key(VolKey{"AZ", v.id, "", ""}, KSIM_VOL_AZURE_DISK), 0u});
-          break;
-        case KSIM_K8S_VOL_PVC: {
-          *has_pvc = true;
-          if (v.id.empty()) {
-            err_claim = true;
-            ZoneEntry e;
-            e.kind = 1;
-            zone->push_back(e);
-            continue;
-          }
-          VolKey k;
-          uint32_t f;
-          if (pvc_target(p.ns, v.id, &k, &f)) out->push_back({key(k, f), KSIM_VOL_VIA_PVC});
-          if (queued) {
-            zone->push_back(zone_entry(p.ns, v.id));
-            binding_check(p.ns, v.id);
-          }
-          break;
-        }
-        default:
-          break;
-      }
-    }
-  }
-
-  int32_t vclass(const PodObj& p) {
-    std::vector<std::pair<int32_t, uint32_t>> refs_;
-    std::vector<ZoneEntry> zone;
-    bool has_pvc;
-    refs(p, true, &refs_, &zone, &has_pvc);
-    if (refs_.empty() && !has_pvc) return 0;
-    std::set<int32_t> seen;
-    uint32_t filt = 0;
-    std::vector<std::pair<int32_t, uint32_t>> flagged;
-    for (auto r : refs_) {
-      const uint32_t kf = key_filter[r.first];
-      if (kf && !seen.count(r.first)) r.second |= KSIM_VOL_NEW;
-      seen.insert(r.first);
-      filt |= kf;
-      flagged.push_back(r);
-    }
-    auto k = std::make_pair(flagged, zone);
-    auto it = classes.find(k);
-    if (it != classes.end()) return it->second + 1;
-    const int32_t c = (int32_t)class_refs.size();
-    classes.emplace(k, c);
-    class_refs.push_back(flagged);
-    class_filter.push_back(filt);
-    class_zone.push_back(zone);
-    return c + 1;
-  }
-};
-
-// volumeutil.LabelZonesToSet; false on a parse error
-bool zones_of(const Str& v, std::set<Str>* out) {
-  size_t i = 0;
-  for (;;) {
-    const size_t j = v.find("__", i);
-    Str t = v.substr(i, j == Str::npos ? Str::npos : j - i);
-    const size_t a = t.find_first_not_of(" \t\n\r\f\v"), b = t.find_last_not_of(" \t\n\r\f\v");
-    t = a == Str::npos ? Str() : t.substr(a, b - a + 1);
-    if (t.empty()) return false;
-    out->insert(t);
-    if (j == Str::npos) return true;
-    i = j + 2;
-  }
-}
-
-}  // namespace
+// ksim_k8s.cpp — the snapshot form of the Kubernetes-field front end (include/ksim_k8s.h): nodes,
+// running pods and a queue are added, then interned at once (ksim_k8s_build) into the device tables
+// of include/ksim.h, every string comparison the scheduler makes evaluated once per (pod class,
+// node label set / taint set).  The semantics (selectors, tolerations, requests, affinity and volume
+// identities, table builders) live in ksim_k8s_sem.h, shared with the event-driven scheduler cache
+// (ksim_k8s_cache.cpp).  The table layouts and interning rules are the Python host's
+// (ksim/ingest.py), which tests/test_k8s_frontend.py compares this with array for array.
+#include "ksim_k8s_sem.h"
 
 // ---------------------------------------------------------------- the cluster
 struct ksim_k8s_cluster {
@@ -985,10 +18,7 @@ struct ksim_k8s_cluster {
   // ---- built ----
   std::vector<NodeObj> nodes;  // name-rank order
   std::map<Str, int64_t> index;
-  Interner<LabelSetKey> label_sets;
-  Interner<std::vector<Taint>> taint_sets;
-  Interner<Str> scalar_names, ips, protos;
-  Interner<ClassKey> classes;
+  Interns in;
   int32_t port_slots = 0;
   std::vector<int64_t> col_i64[12];  // alloc cpu, mem, gpu, eph, req cpu, mem, gpu, eph, nz cpu, nz mem, (unused)
   std::vector<int32_t> allowed, label_set, taint_set, pod_count, port_count;
@@ -996,20 +26,11 @@ struct ksim_k8s_cluster {
   std::vector<int64_t> alloc_scalar, req_scalar;
   std::vector<uint64_t> ports;
   bool prefer_avoid_nodes = false, node_images = false;
-  // class tables
-  int32_t Cn = 0, L = 0, T = 0, lw = 0, tw = 0;
-  std::vector<uint32_t> sel_ok, taint_ok, noexec_ok;
-  std::vector<uint8_t> tt_class, na_class;
-  std::vector<int32_t> n_tt, n_na;
-  std::vector<int64_t> tt_val, na_val, na_w, na_p;
-  std::vector<uint32_t> need;
-  std::set<int32_t> bad_classes;
-  bool pa_split = false;
+  ClassTab ct;
   // pods
   std::vector<ksim_pod> pods;
   std::vector<uint64_t> pod_ports;
   std::vector<ksim_scalar_req> pod_scalars;
-  std::vector<std::vector<std::pair<Str, int64_t>>> pod_scalar_pred;
   // affinity
   bool with_affinity = false, spread_active = false;
   AffinityIndex aidx;
@@ -1019,9 +40,9 @@ struct ksim_k8s_cluster {
   // volumes
   bool with_volumes = false;
   VolumeIndex vidx;
-  std::vector<uint32_t> vol_key_filter, vol_vc_filter, vol_zone_ok;
-  std::vector<int32_t> vol_vc, vol_slot_count;
-  std::vector<ksim_vol_ref> vol_refs;
+  VolSmall vsmall;
+  std::vector<uint32_t> vol_zone_ok;
+  std::vector<int32_t> vol_slot_count;
   std::vector<uint64_t> vol_slots;
   int32_t vol_S = 0, vol_zone_words = 0;
   bool vol_zone_err = false;
@@ -1037,292 +58,25 @@ struct ksim_k8s_cluster {
   };
   std::vector<Described> described;
   bool dropin = false;        // the affinity tables keep every identity (ksim_k8s_describe)
-  int64_t pa_weight = 0;      // the open handle's NodePreferAvoidPods weight and NodeAffinity use
+  ksim_k8s_weights w{};       // the open handle's NodePreferAvoidPods / ImageLocality weights
   bool pa_use_w = false, opened_aff = false, opened_vol = false, opened_zone = false;
   bool aff_cfg = false, vol_cfg = false;  // the open handle's configuration reads the tables
+  int32_t vol_grown_classes = 0;          // volume classes whose zone verdicts the handle holds
 };
 
 namespace {
 
-int guard(ksim_k8s_cluster* c, const std::function<void()>& f) {
-  try {
-    f();
-    return KSIM_OK;
-  } catch (const Fail& e) {
-    if (c) c->err = e.msg;
-    return e.code;
-  } catch (const std::exception& e) {
-    if (c) c->err = e.what();
-    return KSIM_E_INVAL;
-  }
-}
-
-}  // namespace
-
-namespace {
-
 // ---------------------------------------------------------------- build
-uint64_t port_key(int32_t ip, int32_t proto, int32_t port) { return KSIM_PORT_KEY(ip, proto, port); }
-
-// NodeInfo.SetNode + CheckNodeConditionPredicate's condition bits (ingest.node_static).
-uint32_t node_flags(const NodeObj& x) {
-  uint32_t f = 0;
-  Str mem, disk;
-  bool seen[3] = {false, false, false};
-  for (const auto& cd : x.conds) {
-    const Str& t = cd.first;
-    const Str& s = cd.second;
-    int b = -1;
-    if (t == "Ready" && s != "True") b = 0;
-    else if (t == "OutOfDisk" && s != "False") b = 1;
-    else if (t == "NetworkUnavailable" && s != "False") b = 2;
-    if (b >= 0) {
-      if (seen[b]) fail(KSIM_E_UNSUPPORTED, "node %s: repeated failing %s condition", x.name.c_str(), t.c_str());
-      seen[b] = true;
-      f |= b == 0 ? KSIM_N_NOT_READY : b == 1 ? KSIM_N_OUT_OF_DISK : KSIM_N_NET_UNAVAIL;
-    }
-    if (t == "MemoryPressure") mem = s;
-    else if (t == "DiskPressure") disk = s;
-  }
-  if (mem == "True") f |= KSIM_N_MEM_PRESSURE;
-  if (disk == "True") f |= KSIM_N_DISK_PRESSURE;
-  if (x.unschedulable) f |= KSIM_N_UNSCHEDULABLE;
-  return f;
+std::vector<const Labels*> node_labels(const ksim_k8s_cluster* c) {
+  std::vector<const Labels*> v;
+  for (const NodeObj& x : c->nodes) v.push_back(&x.labels);
+  return v;
 }
 
-// CalculateNodePreferAvoidPodsPriorityMap for a pod whose RC / RS controllerRef is (kind, uid).
-int64_t avoid_score(const std::vector<Avoid>& entries, const Str& kind, const Str& uid) {
-  for (const Avoid& e : entries) {
-    if (!e.has) fail(KSIM_E_UNSUPPORTED, "preferAvoidPods entry without a podController (the reference dereferences nil)");
-    if (e.kind == kind && e.uid == uid) return 0;
-  }
-  return 10;
-}
-
-void build_class_tables(ksim_k8s_cluster* c) {
-  const int32_t L = (int32_t)c->label_sets.items.size(), T = (int32_t)c->taint_sets.items.size();
-  const int32_t Cn = std::max<int32_t>((int32_t)c->classes.items.size(), 1);
-  const int32_t lw = (L + 31) / 32, tw = (T + 31) / 32;
-  c->Cn = Cn; c->L = L; c->T = T; c->lw = lw; c->tw = tw;
-  c->sel_ok.assign((size_t)Cn * lw, 0);
-  c->taint_ok.assign((size_t)Cn * tw, 0);
-  c->noexec_ok.assign((size_t)Cn * tw, 0);
-  c->tt_class.assign((size_t)Cn * T, 0);
-  c->na_class.assign((size_t)Cn * L, 0);
-  c->n_tt.assign(Cn, 1);
-  c->n_na.assign(Cn, 1);
-  c->tt_val.assign((size_t)Cn * KSIM_MAX_RCLASS, 0);
-  c->na_val.assign((size_t)Cn * KSIM_MAX_RCLASS, 0);
-  c->na_w.assign((size_t)Cn * L, 0);
-  c->na_p.assign((size_t)Cn * L, 10);
-  c->need.assign(Cn, 0);
-  c->bad_classes.clear();
-  c->pa_split = false;
-  for (int32_t k = 0; k < Cn; ++k) {
-    const PodObj spec = k < (int32_t)c->classes.items.size() ? class_pod(c->classes.items[k]) : PodObj{};
-    std::vector<Tol> prefer;
-    for (const Tol& t : spec.tols)
-      if (t.effect.empty() || t.effect == "PreferNoSchedule") prefer.push_back(t);
-    bool all_sel = true, all_taint = true;
-    std::vector<int64_t> weights, pas, counts;
-    for (int32_t li = 0; li < L; ++li) {
-      const LabelSetKey& ls = c->label_sets.items[li];
-      pas.push_back(spec.has_ctrl ? avoid_score(ls.avoid, spec.ctrl_kind, spec.ctrl_uid) : 10);
-      const bool ok = pod_matches_node_labels(spec, ls.labels);
-      if (ok) c->sel_ok[(size_t)k * lw + (li >> 5)] |= 1u << (li & 31);
-      all_sel &= ok;
-      int64_t w = 0;
-      if (!preferred_weight(spec, ls.labels, &w)) {
-        c->bad_classes.insert(k);
-        w = 0;
-      }
-      weights.push_back(w);
-    }
-    for (int32_t ti = 0; ti < T; ++ti) {
-      const std::vector<Taint>& ts = c->taint_sets.items[ti];
-      auto tolerated = [&](const Taint& x, const std::vector<Tol>& tols) {
-        for (const Tol& t : tols)
-          if (tolerates(t, x)) return true;
-        return false;
-      };
-      bool ok = true, ok2 = true;
-      int64_t cnt = 0;
-      for (const Taint& x : ts) {
-        if ((x.effect == "NoSchedule" || x.effect == "NoExecute") && !tolerated(x, spec.tols)) ok = false;
-        if (x.effect == "NoExecute" && !tolerated(x, spec.tols)) ok2 = false;
-        if (x.effect == "PreferNoSchedule" && !tolerated(x, prefer)) ++cnt;
-      }
-      if (ok) c->taint_ok[(size_t)k * tw + (ti >> 5)] |= 1u << (ti & 31);
-      if (ok2) c->noexec_ok[(size_t)k * tw + (ti >> 5)] |= 1u << (ti & 31);
-      all_taint &= ok && ok2;
-      counts.push_back(cnt);
-    }
-    std::vector<int64_t> tv(counts), av(weights);
-    std::sort(tv.begin(), tv.end()); tv.erase(std::unique(tv.begin(), tv.end()), tv.end());
-    std::sort(av.begin(), av.end()); av.erase(std::unique(av.begin(), av.end()), av.end());
-    if (tv.empty()) tv.push_back(0);  // an empty taint-set list still has one class
-    if (av.empty()) av.push_back(0);
-    if (tv.size() * av.size() > KSIM_MAX_RCLASS)
-      fail(KSIM_E_UNSUPPORTED, "pod class needs %zu x %zu reduce classes (> %d)", tv.size(), av.size(), KSIM_MAX_RCLASS);
-    c->n_tt[k] = (int32_t)tv.size();
-    c->n_na[k] = (int32_t)av.size();
-    for (size_t q = 0; q < tv.size(); ++q) c->tt_val[(size_t)k * KSIM_MAX_RCLASS + q] = tv[q];
-    for (size_t q = 0; q < av.size(); ++q) c->na_val[(size_t)k * KSIM_MAX_RCLASS + q] = av[q];
-    for (int32_t ti = 0; ti < T; ++ti)
-      c->tt_class[(size_t)k * T + ti] = (uint8_t)(std::lower_bound(tv.begin(), tv.end(), counts[ti]) - tv.begin());
-    for (int32_t li = 0; li < L; ++li) {
-      c->na_class[(size_t)k * L + li] = (uint8_t)(std::lower_bound(av.begin(), av.end(), weights[li]) - av.begin());
-      c->na_w[(size_t)k * L + li] = weights[li];
-      c->na_p[(size_t)k * L + li] = pas[li];
-    }
-    for (int32_t li = 1; li < L; ++li) c->pa_split |= pas[li] != pas[0];
-    c->need[k] = (all_sel ? 0u : KSIM_POD_NEED_SELECTOR) | (all_taint ? 0u : KSIM_POD_NEED_TAINTS);
-  }
-}
-
-// One pod → its descriptor (ingest.Cluster.encode_pod); affinity / volume ids are set later.
-void encode_pod(ksim_k8s_cluster* c, const PodObj& p, const Compiled& cr, ksim_pod* row) {
-  memset(row, 0, sizeof *row);
-  row->req_cpu = cr.pred.cpu; row->req_mem = cr.pred.mem; row->req_gpu = cr.pred.gpu; row->req_eph = cr.pred.eph;
-  row->add_cpu = cr.add.cpu; row->add_mem = cr.add.mem; row->add_gpu = cr.add.gpu; row->add_eph = cr.add.eph;
-  row->nz_cpu = cr.nzc; row->nz_mem = cr.nzm;
-  uint32_t fl = 0;
-  if (cr.pred.cpu || cr.pred.mem || cr.pred.gpu || cr.pred.eph || !cr.pred.scalar.empty()) fl |= KSIM_POD_ANY_REQUEST;
-  if (best_effort(p)) fl |= KSIM_POD_BEST_EFFORT;
-  if (p.node_name.empty()) row->host = -1;
-  else {
-    auto it = c->index.find(p.node_name);
-    row->host = it == c->index.end() ? -2 : (int32_t)it->second;
-  }
-  row->cls = c->classes.get(class_key(p));
-  row->flags = fl;
-  const auto hp = host_ports(p);
-  row->port_off = (int32_t)c->pod_ports.size();
-  row->port_cnt = (int32_t)hp.size();
-  for (const auto& e : hp) c->pod_ports.push_back(port_key(c->ips.get(std::get<0>(e)), c->protos.get(std::get<1>(e)), std::get<2>(e)));
-  row->scalar_off = (int32_t)c->pod_scalars.size();
-  row->scalar_cnt = (int32_t)cr.pred.scalar.size();
-  Res add = cr.add;
-  for (const auto& e : cr.pred.scalar) {
-    const int32_t col = c->scalar_names.find(e.first);
-    if (col < 0) fail(KSIM_E_UNSUPPORTED, "pod %s: scalar resource %s is not a column of the node table", p.name.c_str(), e.first.c_str());
-    const int64_t* a = add.find(e.first);
-    c->pod_scalars.push_back(ksim_scalar_req{col, 0, e.second, a ? *a : 0});
-  }
-}
-
-// The affinity tables from the interned index and the placed pods (identity, class, node);
-// keep_all: every interned identity keeps its id (1 + index) instead of dropping the ones that
-// match nothing (the per-pod path: ids described earlier stay valid across reloads).
-void affinity_tables(ksim_k8s_cluster* c, bool keep_all) {
-  AffinityIndex& idx = c->aidx;
-  if (idx.sels.items.size() > KSIM_AFF_MAX_SEL) fail(KSIM_E_UNSUPPORTED, "more than %d distinct inter-pod affinity selectors", KSIM_AFF_MAX_SEL);
-  if (idx.carry.items.size() > KSIM_AFF_MAX_CARRY) fail(KSIM_E_UNSUPPORTED, "more than %d distinct carried inter-pod affinity terms", KSIM_AFF_MAX_CARRY);
-  AffTables& t = c->aff;
-  t = AffTables();
-  const int64_t n = (int64_t)c->nodes.size();
-  const int32_t K = (int32_t)idx.keys.items.size();
-  t.n_keys = K;
-  t.dom.assign((size_t)K * n, -1);
-  t.n_dom.assign(K, 0);
-  for (int64_t i = 0; i < n; ++i) { t.dom[KEY_ALL * n + i] = 0; t.dom[KEY_NODE * n + i] = (int32_t)i; }
-  t.n_dom[KEY_ALL] = 1;
-  t.n_dom[KEY_NODE] = (int32_t)n;
-  for (int32_t k = 2; k < K; ++k) {
-    const Str& name = idx.keys.items[k];
-    std::map<Str, int32_t> vals;
-    for (int64_t i = 0; i < n; ++i) {
-      const Labels& lab = c->nodes[i].labels;
-      Str v;
-      if (name == ZONE_KEY) {
-        v = zone_key_of(lab);
-        if (v.empty()) continue;
-      } else {
-        auto it = lab.find(name);
-        if (it == lab.end()) continue;
-        v = it->second;
-      }
-      auto ins = vals.emplace(v, (int32_t)vals.size());
-      t.dom[(size_t)k * n + i] = ins.first->second;
-    }
-    t.n_dom[k] = (int32_t)vals.size();
-  }
-  const int32_t I = (int32_t)idx.idents.items.size(), NS = (int32_t)idx.sels.items.size();
-  const int32_t E = (int32_t)idx.carry.items.size(), P = (int32_t)idx.pairs.items.size();
-  const int32_t SW = (NS + 63) / 64, CW = (E + 63) / 64;
-  std::vector<uint64_t> isel((size_t)I * SW, 0), ianti((size_t)I * CW, 0), iprio((size_t)I * CW, 0);
-  std::vector<uint8_t> live(I, 0);
-  for (int32_t i = 0; i < I; ++i) {
-    std::vector<uint8_t> hit(NS, 0);
-    for (int32_t s = 0; s < NS; ++s) {
-      hit[s] = AffinityIndex::sel_matches(idx.idents.items[i], idx.sels.items[s]) ? 1 : 0;
-      if (hit[s]) isel[(size_t)i * SW + (s >> 6)] |= 1ull << (s & 63);
-    }
-    for (int32_t e = 0; e < E; ++e) {
-      if (!hit[std::get<0>(idx.carry.items[e])]) continue;
-      std::vector<uint64_t>& tgt = std::get<2>(idx.carry.items[e]) == KSIM_AFF_CARRY_ANTI ? ianti : iprio;
-      tgt[(size_t)i * CW + (e >> 6)] |= 1ull << (e & 63);
-    }
-    for (int32_t w = 0; w < SW; ++w) live[i] |= isel[(size_t)i * SW + w] != 0;
-    for (int32_t w = 0; w < CW; ++w) live[i] |= (ianti[(size_t)i * CW + w] | iprio[(size_t)i * CW + w]) != 0;
-    if (keep_all) live[i] = 1;
-  }
-  t.remap.assign(I, 0);
-  int32_t nl = 0;
-  for (int32_t i = 0; i < I; ++i)
-    if (live[i]) {
-      t.remap[i] = ++nl;
-      for (int32_t w = 0; w < SW; ++w) t.isel.push_back(isel[(size_t)i * SW + w]);
-      for (int32_t w = 0; w < CW; ++w) { t.ianti.push_back(ianti[(size_t)i * CW + w]); t.iprio.push_back(iprio[(size_t)i * CW + w]); }
-    }
-  t.n_sel = NS; t.n_ident = nl; t.n_pair = P; t.n_carry = E; t.sw = SW; t.cw = CW;
-  int64_t off = 0;
-  for (const auto& pr : idx.pairs.items) {
-    t.pair_sel.push_back(pr.first);
-    t.pair_key.push_back(pr.second);
-    t.pair_off.push_back(off);
-    off += t.n_dom[pr.second];
-  }
-  t.cnt.assign(std::max<int64_t>(off, 1), 0);
-  off = 0;
-  for (const auto& e : idx.carry.items) {
-    t.carry_key.push_back(std::get<1>(e));
-    t.carry_kind.push_back(std::get<2>(e));
-    t.carry_off.push_back(off);
-    off += t.n_dom[std::get<1>(e)];
-  }
-  t.carried.assign(std::max<int64_t>(off, 1), 0);
-  const int32_t A = (int32_t)idx.aclasses.items.size();
-  t.n_aclass = A;
-  t.ac.assign((size_t)A * 6, 0);
-  for (int32_t a = 0; a < A; ++a) {
-    const AClass& x = idx.aclasses.items[a];
-    t.ac[a * 6 + 0] = (int32_t)t.terms.size(); t.ac[a * 6 + 1] = (int32_t)x.req.size();
-    for (const Term& y : x.req) t.terms.push_back(ksim_aff_term{y.kind, y.pair, y.gate, y.exist, y.self_ok, 0, y.weight});
-    t.ac[a * 6 + 2] = (int32_t)t.terms.size(); t.ac[a * 6 + 3] = (int32_t)x.pref.size();
-    for (const Term& y : x.pref) t.terms.push_back(ksim_aff_term{y.kind, y.pair, y.gate, y.exist, y.self_ok, 0, y.weight});
-    t.ac[a * 6 + 4] = (int32_t)t.carries.size(); t.ac[a * 6 + 5] = (int32_t)x.carries.size();
-    for (const auto& y : x.carries) t.carries.push_back(ksim_aff_carry{y.first, 0, y.second});
-    t.spread_pair.push_back(x.sp);
-  }
-  t.zone_key = idx.keys.find(ZONE_KEY);
-  // the placed pods' contribution (NodeInfo.AddPod of every cached pod)
-  for (size_t r = 0; r < c->placed_ident.size(); ++r) {
-    const int64_t w = c->placed_nodes[r];
-    const int32_t i_id = c->placed_ident[r], a_id = c->placed_aclass[r];
-    for (int32_t cp = 0; cp < P; ++cp) {
-      const int32_t s = t.pair_sel[cp];
-      if (!((isel[(size_t)i_id * SW + (s >> 6)] >> (s & 63)) & 1ull)) continue;
-      const int32_t d = t.dom[(size_t)t.pair_key[cp] * n + w];
-      if (d >= 0) t.cnt[t.pair_off[cp] + d] += 1;
-    }
-    if (a_id >= 0)
-      for (int32_t j = t.ac[a_id * 6 + 4]; j < t.ac[a_id * 6 + 4] + t.ac[a_id * 6 + 5]; ++j) {
-        const int32_t e = t.carries[j].term;
-        const int32_t d = t.dom[(size_t)t.carry_key[e] * n + w];
-        if (d >= 0) t.carried[t.carry_off[e] + d] += t.carries[j].amount;
-      }
-  }
+std::vector<Placed> placed_pods(const ksim_k8s_cluster* c) {
+  std::vector<Placed> v;
+  for (size_t r = 0; r < c->placed_ident.size(); ++r) v.push_back(Placed{c->placed_nodes[r], c->placed_ident[r], c->placed_aclass[r]});
+  return v;
 }
 
 void build_affinity(ksim_k8s_cluster* c, const std::vector<const PodObj*>& running, const std::vector<const PodObj*>& queued) {
@@ -1336,7 +90,7 @@ void build_affinity(ksim_k8s_cluster* c, const std::vector<const PodObj*>& runni
   for (size_t k = 0; k < all.size(); ++k) aclasses.push_back(idx.aclass(*all[k], k >= running.size()));
   c->placed_ident.assign(idents.begin(), idents.begin() + running.size());
   c->placed_aclass.assign(aclasses.begin(), aclasses.begin() + running.size());
-  affinity_tables(c, false);
+  build_aff_tables(c->aidx, node_labels(c), placed_pods(c), false, &c->aff);
   for (size_t q = 0; q < queued.size(); ++q) {
     ksim_pod& row = c->pods[q];
     row.aff_ident = c->aff.remap[idents[running.size() + q]];
@@ -1353,37 +107,11 @@ void add_mounts(ksim_k8s_cluster* c, int64_t node, const std::vector<std::pair<i
   }
 }
 
-void volume_tables(ksim_k8s_cluster* c);
-
-void build_volumes(ksim_k8s_cluster* c, const std::vector<const PodObj*>& running) {
-  VolumeIndex& vi = c->vidx;
-  const int64_t n = (int64_t)c->nodes.size();
-  // initial mounts of the running pods
-  c->mounts.assign(n, {});
-  c->mount_order.assign(n, {});
-  for (size_t r = 0; r < running.size(); ++r) {
-    std::vector<std::pair<int32_t, uint32_t>> refs;
-    std::vector<ZoneEntry> zone;
-    bool has_pvc;
-    vi.refs(*running[r], false, &refs, &zone, &has_pvc);
-    add_mounts(c, c->placed_nodes[r], refs);
-  }
-  volume_tables(c);
-}
-
 void volume_tables(ksim_k8s_cluster* c) {
   VolumeIndex& vi = c->vidx;
   const int64_t n = (int64_t)c->nodes.size();
   const auto& order = c->mount_order;
-  c->vol_key_filter = vi.key_filter;
-  c->vol_vc.clear();
-  c->vol_refs.clear();
-  for (const auto& cr : vi.class_refs) {
-    c->vol_vc.push_back((int32_t)c->vol_refs.size());
-    c->vol_vc.push_back((int32_t)cr.size());
-    for (const auto& e : cr) c->vol_refs.push_back(ksim_vol_ref{e.first, e.second});
-  }
-  c->vol_vc_filter = vi.class_filter;
+  vol_small(vi, &c->vsmall);
   std::set<int32_t> qkeys;
   for (const ksim_pod& p : c->pods)
     if (p.vol_class > 0)
@@ -1408,55 +136,42 @@ void volume_tables(ksim_k8s_cluster* c) {
     c->vol_slot_count[i] = (int32_t)order[i].size();
   }
   // NoVolumeZoneConflict per (class, label set), once per distinct (zone, region) constraint
-  const int32_t L = (int32_t)c->label_sets.items.size();
-  const int32_t words = (L + 31) / 32;
-  c->vol_zone_words = words;
-  c->vol_zone_ok.assign(std::max<size_t>((size_t)vi.class_zone.size() * words, 1), 0);
+  c->vol_zone_words = ((int32_t)c->in.label_sets.items.size() + 31) / 32;
+  c->vol_zone_ok.clear();
   c->vol_zone_err = false;
-  std::map<std::vector<std::pair<Str, Str>>, std::vector<int32_t>> groups;
-  for (int32_t s = 0; s < L; ++s) {
-    std::vector<std::pair<Str, Str>> cons;
-    for (const auto& l : c->label_sets.items[s].labels)
-      if (l.first == ZONE_LABEL || l.first == REGION_LABEL) cons.push_back(l);
-    groups[cons].push_back(s);
+  vol_zone_verdicts(vi, c->in.label_sets, 0, &c->vol_zone_ok, &c->vol_zone_err);
+  if (c->vol_zone_ok.empty()) c->vol_zone_ok.push_back(0);
+  c->vol_grown_classes = (int32_t)vi.class_zone.size();
+}
+
+void build_volumes(ksim_k8s_cluster* c, const std::vector<const PodObj*>& running) {
+  VolumeIndex& vi = c->vidx;
+  const int64_t n = (int64_t)c->nodes.size();
+  // initial mounts of the running pods
+  c->mounts.assign(n, {});
+  c->mount_order.assign(n, {});
+  for (size_t r = 0; r < running.size(); ++r) {
+    std::vector<std::pair<int32_t, uint32_t>> refs;
+    std::vector<ZoneEntry> zone;
+    bool has_pvc;
+    vi.refs(*running[r], false, &refs, &zone, &has_pvc);
+    add_mounts(c, c->placed_nodes[r], refs);
   }
-  for (size_t k = 0; k < vi.class_zone.size(); ++k) {
-    const auto& zone = vi.class_zone[k];
-    for (const auto& g : groups) {
-      bool fits = true;
-      if (!zone.empty() && !g.first.empty()) {
-        std::map<Str, Str> cons(g.first.begin(), g.first.end());
-        for (const ZoneEntry& z : zone) {
-          if (z.kind == 2) continue;
-          if (z.kind == 1) { c->vol_zone_err = true; fits = false; break; }
-          bool bad = false;
-          for (const auto& kv : z.labels) {
-            std::set<Str> zs;
-            if (!zones_of(kv.second, &zs)) continue;
-            auto it = cons.find(kv.first);
-            if (!zs.count(it == cons.end() ? Str() : it->second)) { bad = true; break; }
-          }
-          if (bad) { fits = false; break; }
-        }
-      }
-      if (fits)
-        for (int32_t s : g.second) c->vol_zone_ok[k * words + (s >> 5)] |= 1u << (s & 31);
-    }
-  }
+  volume_tables(c);
 }
 
 void build(ksim_k8s_cluster* c) {
   if (c->built) fail(KSIM_E_STATE, "ksim_k8s_build: already built");
-  c->ips = Interner<Str>();
-  c->protos = Interner<Str>();
-  c->ips.get("0.0.0.0");  // id 0 = wildcard
-  c->protos.get("TCP");   // id 0 = default protocol
+  c->in = Interns();
   c->nodes = c->nodes_in;
   std::stable_sort(c->nodes.begin(), c->nodes.end(), [](const NodeObj& a, const NodeObj& b) { return a.name < b.name; });
   const int64_t n = (int64_t)c->nodes.size();
   for (int64_t i = 0; i < n; ++i) {
     if (!c->index.emplace(c->nodes[i].name, i).second) fail(KSIM_E_INVAL, "duplicate node names");
   }
+  for (const NodeObj& x : c->nodes) c->node_images |= x.has_images;
+  // ImageLocality's inputs are interned when some node lists images (ingest.Cluster.from_objects)
+  c->in.images = c->opt.image_locality > 0 || (c->opt.image_locality == 0 && c->node_images);
   std::vector<const PodObj*> running, queued;
   size_t with_node = 0;
   bool with_pod_affinity = false;
@@ -1475,16 +190,16 @@ void build(ksim_k8s_cluster* c) {
     fail(KSIM_E_UNSUPPORTED, "running pods bound to nodes outside the snapshot, with inter-pod affinity terms");
   for (const NodeObj& x : c->nodes)
     for (const auto& o : x.other)
-      if (is_scalar_resource(o.first)) c->scalar_names.get(o.first);
+      if (is_scalar_resource(o.first)) c->in.scalar_names.get(o.first);
   std::vector<Compiled> compiled;
   for (const PodObj* p : running) compiled.push_back(container_requests(*p));
   for (const PodObj* p : queued) compiled.push_back(container_requests(*p));
   for (const Compiled& cr : compiled) {
-    for (const auto& e : cr.pred.scalar) c->scalar_names.get(e.first);
-    for (const auto& e : cr.add.scalar) c->scalar_names.get(e.first);
+    for (const auto& e : cr.pred.scalar) c->in.scalar_names.get(e.first);
+    for (const auto& e : cr.add.scalar) c->in.scalar_names.get(e.first);
   }
-  if (c->scalar_names.items.size() > KSIM_MAX_SCALAR) fail(KSIM_E_UNSUPPORTED, "more than %d scalar resources", KSIM_MAX_SCALAR);
-  const int32_t S = (int32_t)c->scalar_names.items.size();
+  if (c->in.scalar_names.items.size() > KSIM_MAX_SCALAR) fail(KSIM_E_UNSUPPORTED, "more than %d scalar resources", KSIM_MAX_SCALAR);
+  const int32_t S = (int32_t)c->in.scalar_names.items.size();
   for (auto& v : c->col_i64) v.assign(n, 0);
   c->allowed.assign(n, 0); c->label_set.assign(n, 0); c->taint_set.assign(n, 0); c->pod_count.assign(n, 0);
   c->flags.assign(n, 0);
@@ -1494,12 +209,11 @@ void build(ksim_k8s_cluster* c) {
     for (int k = 0; k < 4; ++k) c->col_i64[k][i] = x.alloc[k];
     c->allowed[i] = (int32_t)x.pods;
     for (const auto& o : x.other)
-      if (is_scalar_resource(o.first)) c->alloc_scalar[(size_t)c->scalar_names.find(o.first) * n + i] += o.second;
+      if (is_scalar_resource(o.first)) c->alloc_scalar[(size_t)c->in.scalar_names.find(o.first) * n + i] += o.second;
     c->flags[i] = node_flags(x);
-    c->label_set[i] = c->label_sets.get(LabelSetKey{x.labels, x.avoid});
-    c->taint_set[i] = c->taint_sets.get(x.taints);
+    c->label_set[i] = c->in.label_set(x);
+    c->taint_set[i] = c->in.taint_sets.get(x.taints);
     c->prefer_avoid_nodes |= !x.avoid.empty();
-    c->node_images |= x.images;
   }
   // running pods: NodeInfo.AddPod
   std::vector<std::vector<uint64_t>> used(n);
@@ -1510,11 +224,11 @@ void build(ksim_k8s_cluster* c) {
     const int64_t i = c->index[p.node_name];
     c->placed_nodes.push_back(i);
     c->col_i64[4][i] += cr.add.cpu; c->col_i64[5][i] += cr.add.mem; c->col_i64[6][i] += cr.add.gpu; c->col_i64[7][i] += cr.add.eph;
-    for (const auto& e : cr.add.scalar) c->req_scalar[(size_t)c->scalar_names.find(e.first) * n + i] += e.second;
+    for (const auto& e : cr.add.scalar) c->req_scalar[(size_t)c->in.scalar_names.find(e.first) * n + i] += e.second;
     c->col_i64[8][i] += cr.nzc; c->col_i64[9][i] += cr.nzm;
     c->pod_count[i] += 1;
     for (const auto& e : host_ports(p)) {
-      const uint64_t k = port_key(c->ips.get(std::get<0>(e)), c->protos.get(std::get<1>(e)), std::get<2>(e));
+      const uint64_t k = port_key(c->in.ips.get(std::get<0>(e)), c->in.protos.get(std::get<1>(e)), std::get<2>(e));
       if (std::find(used[i].begin(), used[i].end(), k) == used[i].end()) used[i].push_back(k);
     }
   }
@@ -1531,7 +245,7 @@ void build(ksim_k8s_cluster* c) {
   }
   c->pods.assign(queued.size(), ksim_pod{});
   for (size_t q = 0; q < queued.size(); ++q) {
-    encode_pod(c, *queued[q], compiled[running.size() + q], &c->pods[q]);
+    encode_pod_row(c->in, c->index, *queued[q], compiled[running.size() + q], &c->pods[q], &c->pod_ports, &c->pod_scalars);
     if (has_pred_volumes(*queued[q])) c->pods[q].vol_class = c->vidx.vclass(*queued[q]);
   }
   if (c->with_affinity) build_affinity(c, running, queued);
@@ -1551,115 +265,17 @@ void build(ksim_k8s_cluster* c) {
     for (size_t s = 0; s < used[i].size(); ++s) c->ports[s * n + i] = used[i][s];
     c->port_count[i] = (int32_t)used[i].size();
   }
-  if (c->label_sets.items.empty()) c->label_sets.get(LabelSetKey{});  // an empty cluster still has tables
-  if (c->taint_sets.items.empty()) c->taint_sets.get({});
-  build_class_tables(c);
-  for (ksim_pod& p : c->pods) p.flags |= c->need[p.cls];
+  if (c->in.label_sets.items.empty()) c->in.label_sets.get(LabelSetKey{});  // an empty cluster still has tables
+  if (c->in.taint_sets.items.empty()) c->in.taint_sets.get({});
+  build_class_tab(c->in, &c->ct);
+  for (ksim_pod& p : c->pods) p.flags |= c->ct.need[p.cls];
   if (any_vol) build_volumes(c, running);
   c->built = true;
 }
 
-// class_tables_for: NodePreferAvoidPods' per-class addends when its weight and the annotations
-// tell some class's nodes apart (the NodeAffinity class dimension re-keyed by (preferred weight,
-// addend)); returns whether it applies.
-bool prefer_avoid_tables(const ksim_k8s_cluster* c, int64_t w_pa, bool use_w, std::vector<uint8_t>* nac,
-                         std::vector<int32_t>* nna, std::vector<int64_t>* nav, std::vector<int64_t>* add) {
-  if (!w_pa || !c->pa_split) return false;
-  const int32_t Cn = c->Cn, L = c->L;
-  nac->assign((size_t)Cn * L, 0);
-  nna->assign(Cn, 1);
-  nav->assign((size_t)Cn * KSIM_MAX_RCLASS, 0);
-  add->assign((size_t)Cn * KSIM_MAX_RCLASS, 0);
-  for (int32_t k = 0; k < Cn; ++k) {
-    std::vector<std::pair<int64_t, int64_t>> keys;
-    for (int32_t li = 0; li < L; ++li)
-      keys.push_back({use_w ? c->na_w[(size_t)k * L + li] : 0, c->na_p[(size_t)k * L + li] * w_pa});
-    std::vector<std::pair<int64_t, int64_t>> av(keys);
-    std::sort(av.begin(), av.end());
-    av.erase(std::unique(av.begin(), av.end()), av.end());
-    if ((size_t)c->n_tt[k] * av.size() > KSIM_MAX_RCLASS)
-      fail(KSIM_E_UNSUPPORTED, "pod class needs %d x %zu reduce classes (> %d)", c->n_tt[k], av.size(), KSIM_MAX_RCLASS);
-    (*nna)[k] = (int32_t)av.size();
-    for (size_t q = 0; q < av.size(); ++q) {
-      (*nav)[(size_t)k * KSIM_MAX_RCLASS + q] = av[q].first;
-      (*add)[(size_t)k * KSIM_MAX_RCLASS + q] = av[q].second;
-    }
-    for (int32_t li = 0; li < L; ++li)
-      (*nac)[(size_t)k * L + li] = (uint8_t)(std::lower_bound(av.begin(), av.end(), keys[li]) - av.begin());
-  }
-  return true;
-}
-
-int load_classes(ksim_k8s_cluster* c, ksim_handle* h, int64_t w_pa, bool use_w) {
-  std::vector<uint8_t> nac;
-  std::vector<int32_t> nna;
-  std::vector<int64_t> nav, add;
-  const bool pa = prefer_avoid_tables(c, w_pa, use_w, &nac, &nna, &nav, &add);
-  ksim_class_tables t{};
-  t.n_classes = c->Cn;
-  t.n_label_sets = c->L;
-  t.n_taint_sets = c->T;
-  t.sel_ok = c->sel_ok.data();
-  t.taint_ok = c->taint_ok.data();
-  t.noexec_ok = c->noexec_ok.data();
-  t.tt_class = c->tt_class.data();
-  t.na_class = pa ? nac.data() : c->na_class.data();
-  t.n_tt = c->n_tt.data();
-  t.n_na = pa ? nna.data() : c->n_na.data();
-  t.tt_val = c->tt_val.data();
-  t.na_val = pa ? nav.data() : c->na_val.data();
-  t.na_add = pa ? add.data() : nullptr;
-  return ksim_load_classes(h, &t);
-}
-
-int load_affinity(ksim_k8s_cluster* c, ksim_handle* h) {
-  const AffTables& a = c->aff;
-  ksim_affinity_tables t{};
-  t.n_keys = a.n_keys; t.n_sel = a.n_sel; t.n_ident = a.n_ident; t.n_pair = a.n_pair; t.n_carry = a.n_carry;
-  t.n_aclass = a.n_aclass; t.n_terms = (int32_t)a.terms.size(); t.n_carries = (int32_t)a.carries.size();
-  t.n_nodes = (int64_t)c->nodes.size();
-  t.cnt_len = (int64_t)a.cnt.size(); t.carried_len = (int64_t)a.carried.size();
-  t.hard_weight = c->opt.hard_weight;
-  t.sel_words = a.sw; t.carry_words = a.cw; t.zone_key = a.zone_key;
-  t.dom = a.dom.data(); t.n_dom = a.n_dom.data();
-  t.ident_sel = a.isel.data(); t.ident_anti = a.ianti.data(); t.ident_prio = a.iprio.data();
-  t.pair_sel = a.pair_sel.data(); t.pair_key = a.pair_key.data(); t.pair_off = a.pair_off.data();
-  t.carry_key = a.carry_key.data(); t.carry_kind = a.carry_kind.data(); t.carry_off = a.carry_off.data();
-  t.ac = a.ac.data(); t.terms = a.terms.data(); t.carries = a.carries.data();
-  t.cnt = a.cnt.data(); t.carried = a.carried.data();
-  t.spread_pair = a.spread_pair.data();
-  return ksim_load_affinity(h, &t);
-}
-
 int load_volumes(ksim_k8s_cluster* c, ksim_handle* h, bool use_zone) {
-  ksim_volume_tables t{};
-  t.n_keys = (int32_t)c->vol_key_filter.size();
-  t.n_vclass = (int32_t)c->vol_vc_filter.size();
-  t.n_refs = (int32_t)c->vol_refs.size();
-  t.vol_slots = c->vol_S;
-  t.n_nodes = (int64_t)c->nodes.size();
-  for (int k = 0; k < 3; ++k) t.max_vols[k] = c->opt.max_vols[k];
-  t.key_filter = c->vol_key_filter.data();
-  t.vc = c->vol_vc.data();
-  t.vc_filter = c->vol_vc_filter.data();
-  t.refs = c->vol_refs.data();
-  if (use_zone && c->vol_zone_words) {
-    t.zone_words = c->vol_zone_words;
-    t.zone_ok = c->vol_zone_ok.data();
-  }
-  t.slots = c->vol_slots.data();
-  t.slot_count = c->vol_slot_count.data();
-  return ksim_load_volumes(h, &t);
-}
-
-// getMaxVols (predicates.go:347-359): KUBE_MAX_PD_VOLS when it parses to a positive int
-void default_max_vols(int32_t* mv) {
-  const int32_t def[3] = {39, 16, 16};
-  const char* e = getenv("KUBE_MAX_PD_VOLS");
-  int64_t v = 0;
-  const bool ok = e && *e && parse_i64(e, &v) && v > 0 && v <= INT32_MAX;
-  for (int k = 0; k < 3; ++k)
-    if (mv[k] <= 0) mv[k] = ok ? (int32_t)v : def[k];
+  return load_vol_tab(c->vsmall, (int64_t)c->nodes.size(), c->vol_S, c->opt.max_vols, use_zone ? &c->vol_zone_ok : nullptr,
+                      c->vol_zone_words, c->vol_slots.data(), c->vol_slot_count.data(), h);
 }
 
 }  // namespace
@@ -1686,48 +302,24 @@ extern "C" const char* ksim_k8s_last_error(const ksim_k8s_cluster* c) { return c
 extern "C" int ksim_k8s_add_node(ksim_k8s_cluster* c, const ksim_k8s_node* x) {
   if (!c || !x) return KSIM_E_INVAL;
   return guard(c, [&] {
-    if (c->built) fail(KSIM_E_STATE, "ksim_k8s_add_node: the snapshot is built");
-    NodeObj o;
-    o.name = S(x->name);
-    for (int32_t i = 0; i < x->n_labels; ++i) o.labels[S(x->labels[i].key)] = S(x->labels[i].value);
-    for (int32_t i = 0; i < x->n_taints; ++i) o.taints.push_back(Taint{S(x->taints[i].key), S(x->taints[i].value), S(x->taints[i].effect)});
-    o.unschedulable = x->unschedulable != 0;
-    for (int32_t i = 0; i < x->n_conditions; ++i) o.conds.push_back({S(x->conditions[i].type), S(x->conditions[i].status)});
-    o.alloc[0] = x->alloc_cpu_milli; o.alloc[1] = x->alloc_mem; o.alloc[2] = x->alloc_gpu; o.alloc[3] = x->alloc_eph;
-    o.pods = x->alloc_pods;
-    for (int32_t i = 0; i < x->n_alloc_other; ++i) o.other.push_back({S(x->alloc_other[i].name), x->alloc_other[i].value});
-    for (int32_t i = 0; i < x->n_avoid; ++i) o.avoid.push_back(Avoid{x->avoid[i].has_controller != 0, S(x->avoid[i].kind), S(x->avoid[i].uid)});
-    o.images = x->has_images != 0;
-    c->nodes_in.push_back(o);
+    if (c->built) fail(KSIM_E_STATE, "ksim_k8s_add_node: the snapshot is built (node events go to ksim_k8s_cache)");
+    c->nodes_in.push_back(copy_node(*x));
   });
 }
 
 extern "C" int ksim_k8s_add_pv(ksim_k8s_cluster* c, const ksim_k8s_pv* x) {
   if (!c || !x) return KSIM_E_INVAL;
-  return guard(c, [&] {
-    PV pv;
-    for (int32_t i = 0; i < x->n_labels; ++i) pv.labels[S(x->labels[i].key)] = S(x->labels[i].value);
-    pv.kind = x->kind;
-    pv.id = S(x->id);
-    pv.node_affinity = x->has_node_affinity != 0;
-    c->vidx_in.pvs[S(x->name)] = pv;
-  });
+  return guard(c, [&] { add_pv(&c->vidx_in, *x); });
 }
 
 extern "C" int ksim_k8s_add_pvc(ksim_k8s_cluster* c, const ksim_k8s_pvc* x) {
   if (!c || !x) return KSIM_E_INVAL;
-  return guard(c, [&] {
-    PVC pvc;
-    pvc.volume_name = S(x->volume_name);
-    pvc.has_sc = x->storage_class != nullptr;
-    pvc.sc = S(x->storage_class);
-    c->vidx_in.pvcs[{S(x->namespace_), S(x->name)}] = pvc;
-  });
+  return guard(c, [&] { add_pvc(&c->vidx_in, *x); });
 }
 
 extern "C" int ksim_k8s_add_storage_class(ksim_k8s_cluster* c, const ksim_k8s_storage_class* x) {
   if (!c || !x) return KSIM_E_INVAL;
-  return guard(c, [&] { c->vidx_in.scs[S(x->name)] = {x->binding_mode != nullptr, S(x->binding_mode)}; });
+  return guard(c, [&] { add_storage_class(&c->vidx_in, *x); });
 }
 
 extern "C" int ksim_k8s_add_running_pod(ksim_k8s_cluster* c, const ksim_k8s_pod* p) {
@@ -1751,18 +343,22 @@ extern "C" int ksim_k8s_build(ksim_k8s_cluster* c) {
   return guard(c, [&] { build(c); });
 }
 
-extern "C" int ksim_k8s_open(ksim_k8s_cluster* c, const ksim_config* cfg_in, int64_t prefer_avoid_weight, ksim_handle** out) {
+extern "C" int ksim_k8s_open_ex(ksim_k8s_cluster* c, const ksim_config* cfg_in, const ksim_k8s_weights* w_in, ksim_handle** out) {
   if (!c || !cfg_in || !out) return KSIM_E_INVAL;
   *out = nullptr;
   ksim_handle* h = nullptr;
+  const ksim_k8s_weights w = w_in ? *w_in : ksim_k8s_weights{};
   const int rc = guard(c, [&] {
     if (!c->built) fail(KSIM_E_STATE, "ksim_k8s_open: build the snapshot first");
     ksim_config cfg = *cfg_in;
     const uint32_t pr = cfg.predicates;
     if (pr & (KSIM_P_LABEL_PRESENCE | KSIM_P_SERVICE_AFFINITY))
       fail(KSIM_E_UNSUPPORTED, "CheckNodeLabelPresence / CheckServiceAffinity need their Policy arguments (the Python host)");
-    if (cfg.weights[KSIM_W_NODE_AFFINITY] && !c->bad_classes.empty())
+    if (cfg.weights[KSIM_W_NODE_AFFINITY] && !c->ct.bad_classes.empty())
       fail(KSIM_E_UNSUPPORTED, "NodeAffinityPriority: a preferred node-affinity term does not parse");
+    if (w.image_locality && c->node_images && !c->in.images)
+      fail(KSIM_E_UNSUPPORTED, "ImageLocalityPriority with nodes that list status.images, on a snapshot built without "
+                               "image interning (ksim_k8s_options.image_locality = -1)");
     // SelectorSpread's weight stays in its slot even when no queued pod has spread selectors: pods
     // without a spread pair score nothing there (the constant MaxPriority changes no placement), and
     // pods described later (ksim_k8s_describe) may bring selectors
@@ -1777,7 +373,9 @@ extern "C" int ksim_k8s_open(ksim_k8s_cluster* c, const ksim_config* cfg_in, int
     std::vector<int32_t> nna;
     std::vector<int64_t> nav, add;
     const bool use_w = cfg.weights[KSIM_W_NODE_AFFINITY] != 0;
-    if (prefer_avoid_tables(c, prefer_avoid_weight, use_w, &nac, &nna, &nav, &add)) cfg.const_score -= 10 * prefer_avoid_weight;
+    bool pa_on = false;
+    class_addends(c->ct, w.prefer_avoid, w.image_locality, use_w, &nac, &nna, &nav, &add, &pa_on);
+    if (pa_on) cfg.const_score -= 10 * w.prefer_avoid;
     const bool aff = c->with_affinity &&
                      ((pr & KSIM_P_INTERPOD_AFFINITY) ||
                       ((cfg.weights[KSIM_W_INTERPOD_AFFINITY] || cfg.weights[KSIM_W_SELECTOR_SPREAD]) && !cfg.no_priorities));
@@ -1787,7 +385,7 @@ extern "C" int ksim_k8s_open(ksim_k8s_cluster* c, const ksim_config* cfg_in, int
     const int64_t n = (int64_t)c->nodes.size();
     ksim_node_table t{};
     t.n_nodes = n;
-    t.n_scalar = (int32_t)c->scalar_names.items.size();
+    t.n_scalar = (int32_t)c->in.scalar_names.items.size();
     t.port_slots = c->port_slots;
     t.alloc_cpu = c->col_i64[0].data(); t.alloc_mem = c->col_i64[1].data(); t.alloc_gpu = c->col_i64[2].data();
     t.alloc_eph = c->col_i64[3].data();
@@ -1798,10 +396,10 @@ extern "C" int ksim_k8s_open(ksim_k8s_cluster* c, const ksim_config* cfg_in, int
     t.pod_count = c->pod_count.data(); t.req_scalar = c->req_scalar.data(); t.ports = c->ports.data();
     t.port_count = c->port_count.data();
     if ((e = ksim_load_nodes(h, &t))) fail(e, "ksim_load_nodes: %s", ksim_last_error(h));
-    if ((e = load_classes(c, h, prefer_avoid_weight, use_w))) fail(e, "ksim_load_classes: %s", ksim_last_error(h));
-    if (aff && (e = load_affinity(c, h))) fail(e, "ksim_load_affinity: %s", ksim_last_error(h));
+    if ((e = load_class_tab(c->ct, h, w.prefer_avoid, w.image_locality, use_w))) fail(e, "ksim_load_classes: %s", ksim_last_error(h));
+    if (aff && (e = load_aff_tab(c->aff, n, c->opt.hard_weight, h))) fail(e, "ksim_load_affinity: %s", ksim_last_error(h));
     if (vol && (e = load_volumes(c, h, (pr & KSIM_P_VOLUME_ZONE) != 0))) fail(e, "ksim_load_volumes: %s", ksim_last_error(h));
-    c->pa_weight = prefer_avoid_weight;
+    c->w = w;
     c->pa_use_w = use_w;
     c->opened_aff = aff;
     c->opened_vol = vol;
@@ -1824,6 +422,11 @@ extern "C" int ksim_k8s_open(ksim_k8s_cluster* c, const ksim_config* cfg_in, int
   }
   *out = h;
   return KSIM_OK;
+}
+
+extern "C" int ksim_k8s_open(ksim_k8s_cluster* c, const ksim_config* cfg, int64_t prefer_avoid_weight, ksim_handle** out) {
+  const ksim_k8s_weights w{prefer_avoid_weight, 0};
+  return ksim_k8s_open_ex(c, cfg, &w, out);
 }
 
 extern "C" int64_t ksim_k8s_node_count(const ksim_k8s_cluster* c) { return c && c->built ? (int64_t)c->nodes.size() : -1; }
@@ -1855,13 +458,15 @@ extern "C" int ksim_k8s_node_sets(const ksim_k8s_cluster* c, int64_t rank, int32
 }
 
 extern "C" int64_t ksim_k8s_class_value(const ksim_k8s_cluster* c, int32_t kind, int32_t cls, int32_t set) {
-  if (!c || !c->built || cls < 0 || cls >= c->Cn) return -1;
+  if (!c || !c->built || cls < 0 || cls >= c->ct.Cn) return -1;
+  const ClassTab& t = c->ct;
   switch (kind) {
-    case 0: return set < c->L ? (c->sel_ok[(size_t)cls * c->lw + (set >> 5)] >> (set & 31)) & 1u : -1;
-    case 1: return set < c->T ? (c->taint_ok[(size_t)cls * c->tw + (set >> 5)] >> (set & 31)) & 1u : -1;
-    case 2: return set < c->T ? (c->noexec_ok[(size_t)cls * c->tw + (set >> 5)] >> (set & 31)) & 1u : -1;
-    case 3: return set < c->T ? c->tt_val[(size_t)cls * KSIM_MAX_RCLASS + c->tt_class[(size_t)cls * c->T + set]] : -1;
-    case 4: return set < c->L ? c->na_w[(size_t)cls * c->L + set] : -1;
+    case 0: return set < t.L ? (t.sel_ok[(size_t)cls * t.lw + (set >> 5)] >> (set & 31)) & 1u : -1;
+    case 1: return set < t.T ? (t.taint_ok[(size_t)cls * t.tw + (set >> 5)] >> (set & 31)) & 1u : -1;
+    case 2: return set < t.T ? (t.noexec_ok[(size_t)cls * t.tw + (set >> 5)] >> (set & 31)) & 1u : -1;
+    case 3: return set < t.T ? t.tt_val[(size_t)cls * KSIM_MAX_RCLASS + t.tt_class[(size_t)cls * t.T + set]] : -1;
+    case 4: return set < t.L ? t.na_w[(size_t)cls * t.L + set] : -1;
+    case 5: return set < t.L ? t.im_s[(size_t)cls * t.L + set] : -1;
     default: return -1;
   }
 }
@@ -1872,31 +477,33 @@ extern "C" int ksim_k8s_describe(ksim_k8s_cluster* c, ksim_handle* h, const ksim
   if (!c || !h || !pod || !out) return KSIM_E_INVAL;
   return guard(c, [&] {
     if (!c->built) fail(KSIM_E_STATE, "ksim_k8s_describe: build and open the snapshot first");
+    int64_t hn = -1;
+    if (ksim_node_count(h, &hn) != KSIM_OK || hn != (int64_t)c->nodes.size())
+      fail(KSIM_E_STATE, "ksim_k8s_describe: the handle has seen node events the snapshot has not (use ksim_k8s_cache)");
     const PodObj p = copy_pod(*pod);
     const Compiled cr = container_requests(p);
     for (const Res* r : {&cr.pred, &cr.add})
       for (const auto& e : r->scalar)
-        if (c->scalar_names.find(e.first) < 0)
+        if (c->in.scalar_names.find(e.first) < 0)
           fail(KSIM_E_UNSUPPORTED, "pod %s: scalar resource %s is not a column of the node table", p.name.c_str(), e.first.c_str());
-    const size_t c0 = c->classes.items.size(), np0 = c->pod_ports.size(), ns0 = c->pod_scalars.size();
+    const size_t c0 = c->in.classes.items.size();
     ksim_pod row;
-    encode_pod(c, p, cr, &row);
+    std::vector<uint64_t> pp;
+    std::vector<ksim_scalar_req> ps;
+    encode_pod_row(c->in, c->index, p, cr, &row, &pp, &ps);
     const int32_t np = row.port_cnt, nsc = row.scalar_cnt;
     if (np > port_cap || nsc > scalar_cap) fail(KSIM_E_INVAL, "pod %s: %d ports / %d scalar requests exceed the arrays", p.name.c_str(), np, nsc);
-    for (int32_t k = 0; k < np; ++k) ports[k] = c->pod_ports[np0 + k];
-    for (int32_t k = 0; k < nsc; ++k) scalars[k] = c->pod_scalars[ns0 + k];
-    c->pod_ports.resize(np0);
-    c->pod_scalars.resize(ns0);
-    row.port_off = 0;
-    row.scalar_off = 0;
+    for (int32_t k = 0; k < np; ++k) ports[k] = pp[k];
+    for (int32_t k = 0; k < nsc; ++k) scalars[k] = ps[k];
     if (n_ports) *n_ports = np;
     if (n_scalars) *n_scalars = nsc;
     int e;
-    if (c->classes.items.size() != c0) {  // a new pod class: the class tables grow (a superset)
-      build_class_tables(c);
-      if ((e = load_classes(c, h, c->pa_weight, c->pa_use_w))) fail(e, "ksim_load_classes: %s", ksim_last_error(h));
+    if (c->in.classes.items.size() != c0) {  // a new pod class: the class tables grow (a superset)
+      build_class_tab(c->in, &c->ct);
+      if ((e = load_class_tab(c->ct, h, c->w.prefer_avoid, c->w.image_locality, c->pa_use_w)))
+        fail(e, "ksim_load_classes: %s", ksim_last_error(h));
     }
-    row.flags |= c->need[row.cls];
+    row.flags |= c->ct.need[row.cls];
     ksim_k8s_cluster::Described d;
     // inter-pod affinity / SelectorSpread: identities keep their ids from here on (keep_all)
     const bool takes_part = has_pod_affinity(p) || !p.spread.empty() || c->with_affinity;
@@ -1915,13 +522,13 @@ extern "C" int ksim_k8s_describe(ksim_k8s_cluster* c, ksim_handle* h, const ksim
             }
           // pods described and bound before any affinity term appeared count as placed pods
           c->placed_nodes.resize(c->placed_ident.size());
-          for (auto& e : c->described)
-            if (e.node >= 0) {
-              e.ident = idx.ident(e.pod);
-              e.aclass = idx.aclass(e.pod, true);
-              c->placed_nodes.push_back(e.node);
-              c->placed_ident.push_back(e.ident);
-              c->placed_aclass.push_back(e.aclass);
+          for (auto& x : c->described)
+            if (x.node >= 0) {
+              x.ident = idx.ident(x.pod);
+              x.aclass = idx.aclass(x.pod, true);
+              c->placed_nodes.push_back(x.node);
+              c->placed_ident.push_back(x.ident);
+              c->placed_aclass.push_back(x.aclass);
             }
           c->with_affinity = true;
         }
@@ -1934,8 +541,8 @@ extern "C" int ksim_k8s_describe(ksim_k8s_cluster* c, ksim_handle* h, const ksim
       const size_t s1[6] = {idx.keys.items.size(), idx.sels.items.size(), idx.pairs.items.size(), idx.carry.items.size(),
                             idx.idents.items.size(), idx.aclasses.items.size()};
       if (!std::equal(s0, s0 + 6, s1) || !c->opened_aff || c->aff.remap.size() != idx.idents.items.size()) {
-        affinity_tables(c, true);
-        if ((e = load_affinity(c, h))) fail(e, "ksim_load_affinity: %s", ksim_last_error(h));
+        build_aff_tables(c->aidx, node_labels(c), placed_pods(c), true, &c->aff);
+        if ((e = load_aff_tab(c->aff, (int64_t)c->nodes.size(), c->opt.hard_weight, h))) fail(e, "ksim_load_affinity: %s", ksim_last_error(h));
         c->opened_aff = true;
       }
       row.aff_ident = c->aff.remap[d.ident];
@@ -1943,7 +550,8 @@ extern "C" int ksim_k8s_describe(ksim_k8s_cluster* c, ksim_handle* h, const ksim
     } else {
       row.aff_ident = row.aff_class = 0;
     }
-    // volumes
+    // volumes: the first volume pod loads the tables with the bound pods' mounts; later ones grow
+    // the small tables in place (ksim_grow_volumes) — the device keeps every node's mounts
     row.vol_class = 0;
     if (c->vol_cfg && has_pred_volumes(p)) {
       if (!c->with_volumes) {
@@ -1966,16 +574,34 @@ extern "C" int ksim_k8s_describe(ksim_k8s_cluster* c, ksim_handle* h, const ksim
       bool has_pvc;
       std::vector<ZoneEntry> zone;
       vi.refs(p, false, &d.refs, &zone, &has_pvc);
-      const size_t slots_before = c->vol_S;
       for (const auto& r : d.refs) c->extra_vol_keys.insert(r.first);
-      if (vi.keys.items.size() != k0 || vi.class_refs.size() != v0 || !c->opened_vol) {
+      if (!c->opened_vol) {
         volume_tables(c);
         if (c->vol_zone_err && c->opened_zone)
           fail(KSIM_E_UNSUPPORTED, "NoVolumeZoneConflict with a PVC the PV / PVC listers cannot resolve on a zone-labelled node");
         if ((e = load_volumes(c, h, c->opened_zone))) fail(e, "ksim_load_volumes: %s", ksim_last_error(h));
         c->opened_vol = true;
+      } else if (vi.keys.items.size() != k0 || vi.class_refs.size() != v0) {
+        // a new key or class: the small tables and the new classes' zone verdicts, more slots when
+        // a node could now hold more keys than the loaded tables have
+        vol_small(vi, &c->vsmall);
+        bool zerr = false;
+        std::vector<uint32_t> zk;
+        vol_zone_verdicts(vi, c->in.label_sets, (size_t)c->vol_grown_classes, &zk, &zerr);
+        if (c->vol_grown_classes == 0) c->vol_zone_ok.clear();
+        c->vol_zone_ok.insert(c->vol_zone_ok.end(), zk.begin(), zk.end());
+        if (c->vol_zone_ok.empty()) c->vol_zone_ok.push_back(0);
+        c->vol_grown_classes = (int32_t)vi.class_zone.size();
+        if (zerr && c->opened_zone)
+          fail(KSIM_E_UNSUPPORTED, "NoVolumeZoneConflict with a PVC the PV / PVC listers cannot resolve on a zone-labelled node");
+        size_t most = 0;
+        for (const auto& m : c->mounts) most = std::max(most, m.size());
+        const int32_t want = (int32_t)(most + c->extra_vol_keys.size());
+        if (c->opt.vol_slots < 0 && want > c->vol_S) c->vol_S = std::max(want, 2 * c->vol_S);
+        if ((e = load_vol_tab(c->vsmall, (int64_t)c->nodes.size(), c->vol_S, c->opt.max_vols,
+                              c->opened_zone ? &c->vol_zone_ok : nullptr, c->vol_zone_words, nullptr, nullptr, h)))
+          fail(e, "ksim_grow_volumes: %s", ksim_last_error(h));
       }
-      (void)slots_before;
     }
     d.pod = p;
     c->described.push_back(d);
@@ -2009,7 +635,7 @@ extern "C" int ksim_k8s_tables(ksim_k8s_cluster* c, ksim_node_table* nodes, ksim
     ksim_node_table& t = *nodes;
     t = ksim_node_table{};
     t.n_nodes = n;
-    t.n_scalar = (int32_t)c->scalar_names.items.size();
+    t.n_scalar = (int32_t)c->in.scalar_names.items.size();
     t.port_slots = c->port_slots;
     t.alloc_cpu = c->col_i64[0].data(); t.alloc_mem = c->col_i64[1].data(); t.alloc_gpu = c->col_i64[2].data();
     t.alloc_eph = c->col_i64[3].data();
@@ -2022,39 +648,27 @@ extern "C" int ksim_k8s_tables(ksim_k8s_cluster* c, ksim_node_table* nodes, ksim
   }
   if (classes) {
     ksim_class_tables& t = *classes;
+    const ClassTab& x = c->ct;
     t = ksim_class_tables{};
-    t.n_classes = c->Cn; t.n_label_sets = c->L; t.n_taint_sets = c->T;
-    t.sel_ok = c->sel_ok.data(); t.taint_ok = c->taint_ok.data(); t.noexec_ok = c->noexec_ok.data();
-    t.tt_class = c->tt_class.data(); t.na_class = c->na_class.data(); t.n_tt = c->n_tt.data(); t.n_na = c->n_na.data();
-    t.tt_val = c->tt_val.data(); t.na_val = c->na_val.data();
+    t.n_classes = x.Cn; t.n_label_sets = x.L; t.n_taint_sets = x.T;
+    t.sel_ok = x.sel_ok.data(); t.taint_ok = x.taint_ok.data(); t.noexec_ok = x.noexec_ok.data();
+    t.tt_class = x.tt_class.data(); t.na_class = x.na_class.data(); t.n_tt = x.n_tt.data(); t.n_na = x.n_na.data();
+    t.tt_val = x.tt_val.data(); t.na_val = x.na_val.data();
   }
   if (aff) {
     *aff = ksim_affinity_tables{};
-    if (c->with_affinity) {
-      const AffTables& a = c->aff;
-      ksim_affinity_tables& t = *aff;
-      t.n_keys = a.n_keys; t.n_sel = a.n_sel; t.n_ident = a.n_ident; t.n_pair = a.n_pair; t.n_carry = a.n_carry;
-      t.n_aclass = a.n_aclass; t.n_terms = (int32_t)a.terms.size(); t.n_carries = (int32_t)a.carries.size();
-      t.n_nodes = n; t.cnt_len = (int64_t)a.cnt.size(); t.carried_len = (int64_t)a.carried.size();
-      t.hard_weight = c->opt.hard_weight; t.sel_words = a.sw; t.carry_words = a.cw; t.zone_key = a.zone_key;
-      t.dom = a.dom.data(); t.n_dom = a.n_dom.data();
-      t.ident_sel = a.isel.data(); t.ident_anti = a.ianti.data(); t.ident_prio = a.iprio.data();
-      t.pair_sel = a.pair_sel.data(); t.pair_key = a.pair_key.data(); t.pair_off = a.pair_off.data();
-      t.carry_key = a.carry_key.data(); t.carry_kind = a.carry_kind.data(); t.carry_off = a.carry_off.data();
-      t.ac = a.ac.data(); t.terms = a.terms.data(); t.carries = a.carries.data();
-      t.cnt = a.cnt.data(); t.carried = a.carried.data(); t.spread_pair = a.spread_pair.data();
-    }
+    if (c->with_affinity) aff_struct(c->aff, n, c->opt.hard_weight, aff);
   }
   if (vol) {
     *vol = ksim_volume_tables{};
     if (c->with_volumes) {
       ksim_volume_tables& t = *vol;
-      t.n_keys = (int32_t)c->vol_key_filter.size(); t.n_vclass = (int32_t)c->vol_vc_filter.size();
-      t.n_refs = (int32_t)c->vol_refs.size(); t.vol_slots = c->vol_S; t.n_nodes = n;
+      t.n_keys = (int32_t)c->vsmall.key_filter.size(); t.n_vclass = (int32_t)c->vsmall.vc_filter.size();
+      t.n_refs = (int32_t)c->vsmall.refs.size(); t.vol_slots = c->vol_S; t.n_nodes = n;
       for (int k = 0; k < 3; ++k) t.max_vols[k] = c->opt.max_vols[k];
       t.zone_words = c->vol_zone_words;
-      t.key_filter = c->vol_key_filter.data(); t.vc = c->vol_vc.data(); t.vc_filter = c->vol_vc_filter.data();
-      t.refs = c->vol_refs.data(); t.zone_ok = c->vol_zone_ok.data(); t.slots = c->vol_slots.data();
+      t.key_filter = c->vsmall.key_filter.data(); t.vc = c->vsmall.vc.data(); t.vc_filter = c->vsmall.vc_filter.data();
+      t.refs = c->vsmall.refs.data(); t.zone_ok = c->vol_zone_ok.data(); t.slots = c->vol_slots.data();
       t.slot_count = c->vol_slot_count.data();
     }
   }

@@ -480,6 +480,20 @@ class SchedulerCache:
         self._remove(cur)
         del self.pod_states[key]
 
+    def forget_pod(self, pod):
+        """cache.ForgetPod (cache.go:170-197): an assumed pod whose binding failed (scheduler.go:412)
+        leaves the cache."""
+        key = pod_key(pod)
+        cur = self.pod_states.get(key)
+        if cur is not None and _spec(cur).get("nodeName") != _spec(pod).get("nodeName"):
+            raise KeyError("pod %s was assumed on %s but assigned to %s" % (key, _spec(pod).get("nodeName"),
+                                                                          _spec(cur).get("nodeName")))
+        if cur is None or key not in self.assumed:
+            raise KeyError("pod %s wasn't assumed so cannot be forgotten" % key)
+        self._remove(pod)
+        self.assumed.discard(key)
+        del self.pod_states[key]
+
     # ------------------------------------------------------------------ Schedule
     def schedule(self, pod, assume=False):
         """genericScheduler.Schedule (generic_scheduler.go:112-167): the host name, or raises

@@ -64,7 +64,7 @@ class Port(C.Structure):
 class Container(C.Structure):
     _fields_ = [("has_cpu", C.c_int32), ("has_mem", C.c_int32), ("cpu_milli", C.c_int64), ("mem", C.c_int64),
                 ("gpu", C.c_int64), ("eph", C.c_int64), ("n_other", C.c_int32), ("other", C.POINTER(Resource)),
-                ("qos_positive", C.c_int32), ("n_ports", C.c_int32), ("ports", C.POINTER(Port))]
+                ("qos_positive", C.c_int32), ("n_ports", C.c_int32), ("ports", C.POINTER(Port)), ("image", _CSTR)]
 
 
 class Volume(C.Structure):
@@ -89,7 +89,7 @@ class Pod(C.Structure):
                 ("anti_required", C.POINTER(PodTerm)), ("anti_preferred", C.POINTER(PodTerm)),
                 ("n_volumes", C.c_int32), ("volumes", C.POINTER(Volume)),
                 ("n_spread", C.c_int32), ("spread", C.POINTER(LabelSelector)), ("spread_set_selector", C.POINTER(C.c_int32)),
-                ("avoid_ctrl_kind", _CSTR), ("avoid_ctrl_uid", _CSTR)]
+                ("avoid_ctrl_kind", _CSTR), ("avoid_ctrl_uid", _CSTR), ("uid", _CSTR)]
 
 
 class Condition(C.Structure):
@@ -100,13 +100,18 @@ class Avoid(C.Structure):
     _fields_ = [("has_controller", C.c_int32), ("kind", _CSTR), ("uid", _CSTR)]
 
 
+class Image(C.Structure):
+    _fields_ = [("n_names", C.c_int32), ("names", C.POINTER(_CSTR)), ("size_bytes", C.c_int64)]
+
+
 class Node(C.Structure):
     _fields_ = [("name", _CSTR), ("n_labels", C.c_int32), ("labels", C.POINTER(KV)), ("n_taints", C.c_int32),
                 ("taints", C.POINTER(Taint)), ("unschedulable", C.c_int32), ("n_conditions", C.c_int32),
                 ("conditions", C.POINTER(Condition)), ("alloc_cpu_milli", C.c_int64), ("alloc_mem", C.c_int64),
                 ("alloc_gpu", C.c_int64), ("alloc_eph", C.c_int64), ("alloc_pods", C.c_int64),
                 ("n_alloc_other", C.c_int32), ("alloc_other", C.POINTER(Resource)),
-                ("n_avoid", C.c_int32), ("avoid", C.POINTER(Avoid)), ("has_images", C.c_int32)]
+                ("n_avoid", C.c_int32), ("avoid", C.POINTER(Avoid)), ("has_images", C.c_int32),
+                ("n_images", C.c_int32), ("images", C.POINTER(Image))]
 
 
 class PV(C.Structure):
@@ -122,9 +127,18 @@ class StorageClass(C.Structure):
     _fields_ = [("name", _CSTR), ("binding_mode", _CSTR)]
 
 
+class Weights(C.Structure):
+    _fields_ = [("prefer_avoid", C.c_int64), ("image_locality", C.c_int64)]
+
+
+class CacheOptions(C.Structure):
+    _fields_ = [("cfg", abi.Config), ("extra", Weights), ("hard_weight", C.c_int32), ("max_vols", C.c_int32 * 3),
+                ("port_slots", C.c_int32), ("check_volume_binding", C.c_int32)]
+
+
 class Options(C.Structure):
     _fields_ = [("hard_weight", C.c_int32), ("max_vols", C.c_int32 * 3), ("port_slots", C.c_int32),
-                ("vol_slots", C.c_int32)]
+                ("vol_slots", C.c_int32), ("image_locality", C.c_int32)]
 
 
 class _Keep(list):
@@ -188,7 +202,8 @@ def _container(k, c):
     n_ports, p_ports = k.arr(Port, ports)
     g = lambda n, milli=False: (quantity.milli_value(req[n]) if milli else quantity.value(req[n])) if n in req else 0
     return Container(int("cpu" in req), int("memory" in req), g("cpu", True), g("memory"),
-                     g("alpha.kubernetes.io/nvidia-gpu"), g("ephemeral-storage"), n_other, p_other, int(qos), n_ports, p_ports)
+                     g("alpha.kubernetes.io/nvidia-gpu"), g("ephemeral-storage"), n_other, p_other, int(qos), n_ports, p_ports,
+                     k.s(c.get("image") or ""))
 
 
 def _volume(k, v):
@@ -272,7 +287,8 @@ def flatten_pod(k, p, spread=()):
     return Pod(k.s(md.get("name", "")), k.s(md.get("namespace", "")), n_lab, labs, int(md.get("deletionTimestamp") is not None),
                k.s(spec.get("nodeName") or ""), n_c, cs, n_i, ics, n_ns, nsel, int(na is not None), int(req is not None),
                n_rt, rts, n_pf, pfs, n_t, ts, int(pa is not None), int(pn is not None), n_ar, n_ap, n_nr, n_np, ar, ap, nr, npf,
-               n_v, vs, n_sp, sps, spf, k.s(ctrl[0]) if ctrl else None, k.s(ctrl[1]) if ctrl else None)
+               n_v, vs, n_sp, sps, spf, k.s(ctrl[0]) if ctrl else None, k.s(ctrl[1]) if ctrl else None,
+               k.s(md.get("uid") or ""))
 
 
 def flatten_node(k, x):
@@ -291,9 +307,11 @@ def flatten_node(k, x):
     n_o, os_ = k.arr(Resource, other)
     av = [Avoid(0, None, None) if e is None else Avoid(1, k.s(e[0]), k.s(e[1])) for e in avoid_signatures(md.get("annotations"))]
     n_a, avs = k.arr(Avoid, av)
+    imgs = [Image(*k.strs(img.get("names")), int(img.get("sizeBytes") or 0)) for img in st.get("images") or []]
+    n_im, ims = k.arr(Image, imgs)
     return Node(k.s(md.get("name", "")), n_lab, labs, n_t, ts, int(bool(spec.get("unschedulable"))), n_c, cs,
                 g("cpu", True), g("memory"), g("alpha.kubernetes.io/nvidia-gpu"), g("ephemeral-storage"), g("pods"),
-                n_o, os_, n_a, avs, int(bool(st.get("images"))))
+                n_o, os_, n_a, avs, int(bool(st.get("images"))), n_im, ims)
 
 
 def _pv_kind(spec):
@@ -321,7 +339,23 @@ def lib():
                 "ksim_k8s_pods": [P, P, P, P, P, P], "ksim_k8s_tables": [P, P, P, P, P],
                 "ksim_k8s_describe": [P, P, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int32, C.POINTER(C.c_int32),
                                       C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int64)],
-                "ksim_k8s_bind": [P, C.c_int64, C.c_int64]}
+                "ksim_k8s_bind": [P, C.c_int64, C.c_int64],
+                "ksim_k8s_open_ex": [P, C.POINTER(abi.Config), C.POINTER(Weights), C.POINTER(P)],
+                "ksim_k8s_cache_create": [C.POINTER(CacheOptions), C.POINTER(P)], "ksim_k8s_cache_destroy": [P],
+                "ksim_k8s_cache_last_error": [P], "ksim_k8s_cache_add_pv": [P, C.POINTER(PV)],
+                "ksim_k8s_cache_add_pvc": [P, C.POINTER(PVC)],
+                "ksim_k8s_cache_add_storage_class": [P, C.POINTER(StorageClass)],
+                "ksim_k8s_cache_add_node": [P, C.POINTER(Node)],
+                "ksim_k8s_cache_update_node": [P, C.POINTER(Node), C.POINTER(Node)],
+                "ksim_k8s_cache_remove_node": [P, C.POINTER(Node)],
+                "ksim_k8s_cache_assume_pod": [P, C.POINTER(Pod)], "ksim_k8s_cache_forget_pod": [P, C.POINTER(Pod)],
+                "ksim_k8s_cache_add_pod": [P, C.POINTER(Pod)],
+                "ksim_k8s_cache_update_pod": [P, C.POINTER(Pod), C.POINTER(Pod)],
+                "ksim_k8s_cache_remove_pod": [P, C.POINTER(Pod)],
+                "ksim_k8s_cache_schedule": [P, C.POINTER(Pod), C.c_int32, C.POINTER(abi.Result)],
+                "ksim_k8s_cache_fit_error": [P, C.POINTER(abi.Result), C.c_char_p, C.c_int32],
+                "ksim_k8s_cache_node_count": [P], "ksim_k8s_cache_node_name": [P, C.c_int64],
+                "ksim_k8s_cache_handle": [P], "ksim_k8s_cache_stats": [P, C.POINTER(C.c_int64)]}
         for name, args in sigs.items():
             f = getattr(L, name)
             f.argtypes = args
@@ -331,6 +365,12 @@ def lib():
         L.ksim_k8s_node_name.restype = C.c_char_p
         L.ksim_k8s_node_count.restype = C.c_int64
         L.ksim_k8s_queue_length.restype = C.c_int64
+        L.ksim_k8s_cache_destroy.restype = None
+        L.ksim_k8s_cache_last_error.restype = C.c_char_p
+        L.ksim_k8s_cache_node_count.restype = C.c_int64
+        L.ksim_k8s_cache_node_name.restype = C.c_char_p
+        L.ksim_k8s_cache_handle.restype = C.c_void_p
+        L.ksim_k8s_cache_fit_error.restype = C.c_int32
         _lib = L
     return _lib
 
@@ -340,10 +380,12 @@ class K8sCluster:
     ingest.Cluster.from_objects)."""
 
     def __init__(self, nodes, running_pods=(), pods=(), hard_weight=10, pvs=(), pvcs=(), storage_classes=(),
-                 max_vols=None, port_slots=None, vol_slots=None, spread=None, spread_services_only=False):
+                 max_vols=None, port_slots=None, vol_slots=None, spread=None, spread_services_only=False,
+                 image_locality=None):
         L = lib()
         opt = Options(int(hard_weight), (C.c_int32 * 3)(*(max_vols or (0, 0, 0))),
-                      -1 if port_slots is None else int(port_slots), -1 if vol_slots is None else int(vol_slots))
+                      -1 if port_slots is None else int(port_slots), -1 if vol_slots is None else int(vol_slots),
+                      0 if image_locality is None else (1 if image_locality else -1))
         h = C.c_void_p()
         self._check(L.ksim_k8s_create(C.byref(opt), C.byref(h)), None)
         self.h = h
@@ -414,8 +456,200 @@ class K8sCluster:
         self._check(lib().ksim_k8s_tables(self.h, *[C.byref(x) for x in t]))
         return t
 
+    def open_ex(self, cfg, prefer_avoid_weight=0, image_locality_weight=0):
+        """ksim_k8s_open_ex: a policy that may weigh ImageLocalityPriority."""
+        hh = C.c_void_p()
+        w = Weights(int(prefer_avoid_weight), int(image_locality_weight))
+        self._check(lib().ksim_k8s_open_ex(self.h, C.byref(cfg), C.byref(w), C.byref(hh)))
+        return abi.Handle.adopt(hh, cfg)
+
     def open(self, cfg, prefer_avoid_weight=0):
         """A ksim_handle with everything loaded (abi.Handle-compatible wrapper)."""
         hh = C.c_void_p()
         self._check(lib().ksim_k8s_open(self.h, C.byref(cfg), int(prefer_avoid_weight), C.byref(hh)))
         return abi.Handle.adopt(hh, cfg)
+
+
+def _pv_struct(k, x):
+    kind, vid = _pv_kind(x.get("spec") or {})
+    md = x.get("metadata") or {}
+    n_l, labs = _kvs(k, md.get("labels"))
+    return PV(k.s(md.get("name", "")), n_l, labs, kind, k.s(vid), int((x.get("spec") or {}).get("nodeAffinity") is not None))
+
+
+def _pvc_struct(k, x):
+    md, sp = x.get("metadata") or {}, x.get("spec") or {}
+    sc = sp.get("storageClassName")
+    return PVC(k.s(md.get("namespace", "")), k.s(md.get("name", "")), k.s(sp.get("volumeName", "")),
+               k.s(sc) if sc is not None else None)
+
+
+class K8sCache:
+    """The C++ scheduler cache (ksim_k8s_cache_*): the per-pod drop-in a cgo adapter drives, with the
+    method surface of ksim.cache.SchedulerCache / the reference's schedulercache.Cache (add_node,
+    update_node, remove_node, assume_pod, forget_pod, add_pod, update_pod, remove_pod, schedule,
+    schedule_one).  Objects are flattened exactly as a Go adapter would flatten v1 objects; every
+    scheduling rule runs in the library.  Errors: KeyError with cache.go's message for cache-state
+    errors (as SchedulerCache raises), KsimUnsupported / NoNodesAvailable / KsimError otherwise."""
+
+    def __init__(self, predicates, priorities, device=0, mode=abi.MODE_AUTO, last_node_index=0, port_slots=8,
+                 pvs=(), pvcs=(), storage_classes=(), hard_weight=10, spread=None, max_vols=None):
+        from . import scheduler
+        self.predicates = list(predicates)
+        self.prioritizers = list(priorities)
+        self.spread = spread if spread else None
+        names = {n for n, _ in priorities}
+        self._services_only = "ServiceSpreadingPriority" in names and "SelectorSpreadPriority" not in names
+        cfg = scheduler.make_config(predicates, priorities, device, mode, True, last_node_index, spread=self.spread is not None)
+        w = lambda key: sum(int(x) for n, x in priorities if n == key)
+        opt = CacheOptions(cfg, Weights(w("NodePreferAvoidPodsPriority"), w("ImageLocalityPriority")), int(hard_weight),
+                           (C.c_int32 * 3)(*(max_vols or (0, 0, 0))), int(port_slots),
+                           int("CheckVolumeBinding" in self.predicates))
+        L = lib()
+        h = C.c_void_p()
+        rc = L.ksim_k8s_cache_create(C.byref(opt), C.byref(h))
+        if rc:
+            self.h = None
+            raise self._err(rc, L.ksim_k8s_cache_last_error(None))
+        self.h = h
+        for x in pvs:
+            k = _Keep()
+            self._call("ksim_k8s_cache_add_pv", C.byref(_pv_struct(k, x)))
+        for x in pvcs:
+            k = _Keep()
+            self._call("ksim_k8s_cache_add_pvc", C.byref(_pvc_struct(k, x)))
+        for x in storage_classes:
+            k = _Keep()
+            mode_ = x.get("volumeBindingMode")
+            sc = StorageClass(k.s((x.get("metadata") or {}).get("name", "")), k.s(mode_) if mode_ is not None else None)
+            self._call("ksim_k8s_cache_add_storage_class", C.byref(sc))
+
+    @staticmethod
+    def _err(rc, msg):
+        msg = (msg or b"").decode()
+        if rc == abi.E_STATE:
+            return KeyError(msg)
+        if rc == abi.E_NO_NODES:
+            return abi.NoNodesAvailable(rc, msg)
+        return (abi.KsimUnsupported if rc == abi.E_UNSUPPORTED else abi.KsimError)(rc, msg)
+
+    def _call(self, fn, *args):
+        L = lib()
+        rc = getattr(L, fn)(self.h, *args)
+        if rc:
+            raise self._err(rc, L.ksim_k8s_cache_last_error(self.h))
+
+    def _pod(self, k, p):
+        return C.byref(flatten_pod(k, p, spread_raw(self.spread, p, self._services_only)))
+
+    def add_node(self, node):
+        k = _Keep()
+        self._call("ksim_k8s_cache_add_node", C.byref(flatten_node(k, node)))
+
+    def update_node(self, old, new):
+        k = _Keep()
+        self._call("ksim_k8s_cache_update_node", C.byref(flatten_node(k, old)), C.byref(flatten_node(k, new)))
+
+    def remove_node(self, node):
+        k = _Keep()
+        self._call("ksim_k8s_cache_remove_node", C.byref(flatten_node(k, node)))
+
+    def assume_pod(self, pod):
+        k = _Keep()
+        self._call("ksim_k8s_cache_assume_pod", self._pod(k, pod))
+
+    def forget_pod(self, pod):
+        k = _Keep()
+        self._call("ksim_k8s_cache_forget_pod", self._pod(k, pod))
+
+    def add_pod(self, pod):
+        k = _Keep()
+        self._call("ksim_k8s_cache_add_pod", self._pod(k, pod))
+
+    def update_pod(self, old, new):
+        k = _Keep()
+        self._call("ksim_k8s_cache_update_pod", self._pod(k, old), self._pod(k, new))
+
+    def remove_pod(self, pod):
+        k = _Keep()
+        self._call("ksim_k8s_cache_remove_pod", self._pod(k, pod))
+
+    def schedule(self, pod, assume=False):
+        """genericScheduler.Schedule: the host name, or raises FitError (ksim.cache.FitError, message
+        from the library) / abi.NoNodesAvailable; assume=True also runs Scheduler.assume."""
+        from .cache import FitError
+        k = _Keep()
+        res = abi.Result()
+        self._call("ksim_k8s_cache_schedule", self._pod(k, pod), abi.SCHEDULE_ASSUME if assume else abi.SCHEDULE_ONLY,
+                   C.byref(res))
+        self.last_fit_nodes = res.fit_nodes
+        if res.node < 0:
+            buf = C.create_string_buffer(4096)
+            lib().ksim_k8s_cache_fit_error(self.h, C.byref(res), buf, 4096)
+            err = FitError(self.node_count(), list(res.reasons))
+            err.args = (buf.value.decode(),)
+            raise err
+        return lib().ksim_k8s_cache_node_name(self.h, res.node).decode()
+
+    def schedule_one(self, pod):
+        from .cache import FitError
+        try:
+            return self.schedule(pod, assume=True), None
+        except FitError as e:
+            return None, str(e)
+
+    @property
+    def names(self):
+        L = lib()
+        return [L.ksim_k8s_cache_node_name(self.h, i).decode() for i in range(L.ksim_k8s_cache_node_count(self.h))]
+
+    def node_count(self):
+        return lib().ksim_k8s_cache_node_count(self.h)
+
+    def _hcall(self, fn, *args):
+        """A ksim_* call on the cache's own handle (borrowed: the cache destroys it)."""
+        L = abi.lib()
+        hh = C.c_void_p(lib().ksim_k8s_cache_handle(self.h))
+        rc = getattr(L, fn)(hh, *args)
+        if rc:
+            raise abi.KsimError(rc, L.ksim_last_error(hh).decode(errors="replace"))
+
+    @property
+    def last_node_index(self):
+        v = C.c_uint64()
+        self._hcall("ksim_get_counter", C.byref(v))
+        return v.value
+
+    def stats(self):
+        """(affinity loads, volume loads, volume grows, class loads)."""
+        out = (C.c_int64 * 4)()
+        self._call("ksim_k8s_cache_stats", out)
+        return tuple(out)
+
+    aff_reloads = property(lambda self: self.stats()[0])  # SchedulerCache's counters, same meaning
+    vol_loads = property(lambda self: self.stats()[1])
+    vol_grows = property(lambda self: self.stats()[2])
+
+    def node_state(self):
+        """Dynamic columns read back from the device, in name-rank order."""
+        import numpy as np
+        n = self.node_count()
+        S = abi.MAX_SCALAR
+        out = dict(req_cpu=np.zeros(n, np.int64), req_mem=np.zeros(n, np.int64), req_gpu=np.zeros(n, np.int64),
+                   req_eph=np.zeros(n, np.int64), nz_cpu=np.zeros(n, np.int64), nz_mem=np.zeros(n, np.int64),
+                   pod_count=np.zeros(n, np.int32), req_scalar=np.zeros((S, n), np.int64),
+                   port_count=np.zeros(n, np.int32))
+        st = abi.NodeState()
+        for key, ct in (("req_cpu", C.c_int64), ("req_mem", C.c_int64), ("req_gpu", C.c_int64), ("req_eph", C.c_int64),
+                        ("nz_cpu", C.c_int64), ("nz_mem", C.c_int64), ("pod_count", C.c_int32),
+                        ("req_scalar", C.c_int64), ("port_count", C.c_int32)):
+            setattr(st, key, abi.ptr(out[key], ct))
+        self._hcall("ksim_read_nodes", C.byref(st))
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().ksim_k8s_cache_destroy(self.h)
+            self.h = None
+
+    __del__ = close

@@ -1858,6 +1858,18 @@ class SchedulerCache:
         self._remove(cur)
         del self.pod_states[key]
 
+    def forget_pod(self, pod):                             # cache.go:170-197 (scheduler.go:412: the bind failed)
+        key = pod_key(pod)
+        cur = self.pod_states.get(key)
+        if cur is not None and (cur.get("spec") or {}).get("nodeName") != (pod.get("spec") or {}).get("nodeName"):
+            raise KeyError("pod %s was assumed on %s but assigned to %s" % (key, (pod.get("spec") or {}).get("nodeName"),
+                                                                          (cur.get("spec") or {}).get("nodeName")))
+        if cur is None or key not in self.assumed:
+            raise KeyError("pod %s wasn't assumed so cannot be forgotten" % key)
+        self._remove(pod)
+        self.assumed.discard(key)
+        del self.pod_states[key]
+
     def add_node(self, node):                              # cache.go:354-363
         name = (node.get("metadata") or {}).get("name", "")
         self._info(name).set_node(node)

@@ -188,7 +188,7 @@ static void make_pod(PodObj* o, int k, const char* node_name) {
 }
 
 static ksim_k8s_cluster* snapshot(const NodeObj* nodes, int n, const PodObj* running, int nr, const PodObj* queue, int nq) {
-  ksim_k8s_options opt = {10, {0, 0, 0}, -1, -1};
+  ksim_k8s_options opt = {10, {0, 0, 0}, -1, -1, 0};
   ksim_k8s_cluster* c = NULL;
   OK(ksim_k8s_create(&opt, &c));
   for (int i = 0; i < n; ++i) OK(ksim_k8s_add_node(c, &nodes[i].n));

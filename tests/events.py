@@ -8,7 +8,7 @@ import random
 from workloads import rnd_nodes, rnd_pod
 
 
-def event_stream(seed, ref, n_events=400, n_nodes=16, features=True):
+def event_stream(seed, ref, n_events=400, n_nodes=16, features=True, forget=0.0):
     """Yields (kind, payload) with kind in: add_node, update_node, remove_node, add_pod,
     update_pod, remove_pod, schedule.  The consumer applies each event to the oracle cache
     `ref` (ksim_ref.SchedulerCache) before pulling the next one; the generator reads it to pick
@@ -23,6 +23,9 @@ def event_stream(seed, ref, n_events=400, n_nodes=16, features=True):
         names = list(ref.listed)
         added = [key for key in ref.pod_states if key not in ref.assumed]
         assumed = sorted(ref.assumed)
+        if forget and assumed and rng.random() < forget:
+            yield "forget_pod", copy.deepcopy(ref.pod_states[rng.choice(assumed)])
+            continue
         r = rng.random()
         k += 1
         if r < 0.55 or not names:

@@ -75,3 +75,65 @@ def test_c_k8s_loop():
         print(r.stdout, r.stderr)
         assert r.returncode == 0, r.stdout + r.stderr
         assert "PASS" in r.stdout
+
+
+EVENTS_BIN = os.path.join(CDIR, "build", "ksim_k8s_events")
+
+
+def test_event_script_round_trips_node_and_pod_fields():
+    """The event-script tokens carry every field of the flattened structs (CPU-only: the writer)."""
+    import c_events
+    from ksim import frontend
+    from workloads import rnd_affinity_workload
+    nodes, _, pods = rnd_affinity_workload(4, n_nodes=6, n_pods=12)
+    k = frontend._Keep()
+    for x in nodes:
+        t = c_events.node_tokens(frontend.flatten_node(k, x))
+        assert t[0] == c_events._s(x["metadata"]["name"].encode())
+    for p in pods:
+        t = c_events.pod_tokens(frontend.flatten_pod(k, p))
+        assert all(" " not in s and s for s in t)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("stream", ["features_forget", "affinity_spread"])
+def test_c_k8s_event_loop(tmp_path, stream):
+    """The scheduler cache driven from plain C (tests/c/ksim_k8s_events.c, include/ksim_k8s.h only):
+    informer events — node add / update / remove, pod add / confirm / update / remove, forget — and
+    Schedule + assume calls, flattened v1 objects in; every decision line (host or FitError text) and
+    the final lastNodeIndex equal the object oracle's cache (ksim_ref.SchedulerCache)."""
+    import c_events
+    import ksim_ref as R
+    from events import apply, event_stream
+    from ksim import scheduler
+    assert os.path.exists(EVENTS_BIN), "tests/c/build/ksim_k8s_events not built (__graft_entry__.build())"
+    preds, prios = scheduler.provider("DefaultProvider")
+    spread = rspread = None
+    if stream == "affinity_spread":
+        from ksim.spread import SpreadListers
+        from test_gpu_cache import _affinity_stream
+        svc = [{"metadata": {"namespace": ns}, "spec": {"selector": {"app": a}}} for ns, a in (("", "web"), ("ns1", "db"))]
+        spread, rspread = SpreadListers(services=svc), R.SpreadListers(services=svc)
+        ref = R.SchedulerCache(set(preds), prios, spread=rspread)
+        events = _affinity_stream(3, ref, 160, 10)
+    else:
+        ref = R.SchedulerCache(set(preds), prios)
+        events = event_stream(17, ref, 300, 12, True, forget=0.06)
+    cfg = scheduler.make_config(preds, prios, 0, spread=spread is not None)
+    lines = [c_events.config_line(cfg, prefer_avoid=10000)]
+    want = []
+    for ev in events:
+        r = apply(ref, ev)
+        lines.append(c_events.event_line(*ev, spread=spread))
+        if ev[0] == "schedule":
+            want.append(r[0] if r[0] is not None else ("NONODES" if "no nodes available" in r[1] else "FIT " + r[1]))
+    want.append("COUNTER %d" % ref.sched.last_node_index)
+    script, out = tmp_path / "events.txt", tmp_path / "out.txt"
+    script.write_text("\n".join(lines) + "\n")
+    r = subprocess.run([EVENTS_BIN, str(script), str(out)], capture_output=True, text=True, timeout=300)
+    print(r.stdout, r.stderr)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = out.read_text().splitlines()
+    assert len(got) == len(want) and len(want) > 60
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert g == w, (i, w, g)

@@ -1,17 +1,21 @@
-"""Per-pod drop-in parity (GPU): the scheduleOne loop through ksim.cache.SchedulerCache
-(ksim_schedule_one + the cache-event entry points of include/ksim.h) against the object-level
-oracle's SchedulerCache (oracle/ksim_ref.py, restating schedulercache/cache.go and
-genericScheduler.Schedule), on seeded streams that interleave Schedule + assume with node add /
-update / remove and pod add / confirm / update / remove events.  Every decision (host or FitError
-text), lastNodeIndex and the final per-node state must be identical."""
+"""Per-pod drop-in parity (GPU): the scheduleOne loop through both cache mirrors —
+ksim.cache.SchedulerCache (Python host over ksim_schedule_one + the cache-event entry points of
+include/ksim.h) and ksim.frontend.K8sCache (the C++ scheduler cache of include/ksim_k8s.h, what a cgo
+adapter drives: every rule in the library) — against the object-level oracle's SchedulerCache
+(oracle/ksim_ref.py, restating schedulercache/cache.go and genericScheduler.Schedule), on seeded
+streams that interleave Schedule + assume with node add / update / remove and pod add / confirm /
+update / remove / forget events.  Every decision (host or FitError text), lastNodeIndex and the
+final per-node state must be identical."""
 import pytest
 
 import ksim_ref as R
 from events import apply, event_stream
 from ksim import abi, scheduler
 from ksim.cache import SchedulerCache
+from ksim.frontend import K8sCache
 
 pytestmark = pytest.mark.gpu
+IMPLS = {"py": SchedulerCache, "cpp": K8sCache}
 
 POLICIES = {
     "default": scheduler.provider("DefaultProvider"),
@@ -22,13 +26,13 @@ POLICIES = {
 }
 
 
-def _drive(seed, policy, n_events, n_nodes, features=True, mode=abi.MODE_AUTO):
+def _drive(seed, policy, n_events, n_nodes, features=True, mode=abi.MODE_AUTO, impl="py", forget=0.0):
     preds, prios = POLICIES[policy]
     ref = R.SchedulerCache(set(preds), prios)
-    dut = SchedulerCache(preds, prios, device=0, mode=mode)
+    dut = IMPLS[impl](preds, prios, device=0, mode=mode)
     decisions = 0
     try:
-        for ev in event_stream(seed, ref, n_events, n_nodes, features):
+        for ev in event_stream(seed, ref, n_events, n_nodes, features, forget=forget):
             want = apply(ref, ev)
             got = apply(dut, ev)
             if ev[0] == "schedule":
@@ -49,21 +53,70 @@ def _drive(seed, policy, n_events, n_nodes, features=True, mode=abi.MODE_AUTO):
     return decisions
 
 
+@pytest.mark.parametrize("impl", sorted(IMPLS))
 @pytest.mark.parametrize("seed", range(6))
 @pytest.mark.parametrize("policy", sorted(POLICIES))
-def test_event_stream_parity(seed, policy):
-    assert _drive(seed, policy, n_events=300, n_nodes=14) > 100
+def test_event_stream_parity(seed, policy, impl):
+    assert _drive(seed, policy, n_events=300, n_nodes=14, impl=impl) > 100
 
 
+@pytest.mark.parametrize("impl", sorted(IMPLS))
 @pytest.mark.parametrize("seed", range(3))
-def test_event_stream_resource_only(seed):
+def test_event_stream_resource_only(seed, impl):
     """Resource-only pods (the fast kernels' pod shape) through the same event mix."""
-    assert _drive(100 + seed, "lr_bra", n_events=400, n_nodes=20, features=False) > 150
+    assert _drive(100 + seed, "lr_bra", n_events=400, n_nodes=20, features=False, impl=impl) > 150
 
 
-def test_empty_cache_is_err_no_nodes():
+@pytest.mark.parametrize("impl", sorted(IMPLS))
+@pytest.mark.parametrize("seed", range(3))
+def test_event_stream_with_forget(seed, impl):
+    """ForgetPod of assumed pods whose binding failed (scheduler.go:412, cache.go:170-197) mixed into
+    the stream: the pod's commit leaves the device row, every later decision matches."""
+    assert _drive(200 + seed, "default", n_events=300, n_nodes=12, impl=impl, forget=0.08) > 80
+
+
+@pytest.mark.parametrize("impl", sorted(IMPLS))
+def test_cache_errors_match_reference_messages(impl):
+    """cache.go's error paths, with its messages: assume of a cached pod, add of an added pod,
+    update / remove of unknown or assumed pods, forget of a pod that was not assumed or was assumed
+    elsewhere, remove of an unknown node."""
+    preds, prios = POLICIES["lr_bra"]
+    dut = IMPLS[impl](preds, prios, device=0)
+    node = {"metadata": {"name": "n1"}, "status": {"allocatable": {"cpu": "4", "memory": "8Gi", "pods": "10"}}}
+    pod = {"metadata": {"name": "p", "namespace": "ns", "uid": "u1"},
+           "spec": {"nodeName": "n1", "containers": [{"resources": {"requests": {"cpu": "1"}}}]}}
+    try:
+        dut.add_node(node)
+        dut.assume_pod(pod)
+        with pytest.raises(KeyError, match="pod u1 is in the cache, so can't be assumed"):
+            dut.assume_pod(pod)
+        with pytest.raises(KeyError, match="pod u1 is not added to scheduler cache, so cannot be updated"):
+            dut.update_pod(pod, pod)
+        with pytest.raises(KeyError, match="pod u1 is not found in scheduler cache, so cannot be removed from it"):
+            dut.remove_pod(pod)
+        moved = {"metadata": pod["metadata"], "spec": dict(pod["spec"], nodeName="n2")}
+        with pytest.raises(KeyError, match="pod u1 was assumed on n2 but assigned to n1"):
+            dut.forget_pod(moved)
+        dut.forget_pod(pod)
+        assert int(dut.node_state()["req_cpu"][0]) == 0
+        with pytest.raises(KeyError, match="pod u1 wasn't assumed so cannot be forgotten"):
+            dut.forget_pod(pod)
+        dut.add_pod(pod)
+        with pytest.raises(KeyError, match="pod u1 was already in added state"):
+            dut.add_pod(pod)
+        with pytest.raises(KeyError, match="wasn't assumed so cannot be forgotten"):
+            dut.forget_pod(pod)
+        assert int(dut.node_state()["req_cpu"][0]) == 1000
+        with pytest.raises(KeyError, match="node gone is not in the cache"):
+            dut.remove_node({"metadata": {"name": "gone"}})
+    finally:
+        dut.close()
+
+
+@pytest.mark.parametrize("impl", sorted(IMPLS))
+def test_empty_cache_is_err_no_nodes(impl):
     preds, prios = POLICIES["default"]
-    dut = SchedulerCache(preds, prios, device=0)
+    dut = IMPLS[impl](preds, prios, device=0)
     try:
         with pytest.raises(abi.NoNodesAvailable):
             dut.schedule({"metadata": {"name": "p"}, "spec": {"containers": [{}]}})
@@ -74,9 +127,10 @@ def test_empty_cache_is_err_no_nodes():
         dut.close()
 
 
-def test_schedule_only_leaves_cache_unchanged():
+@pytest.mark.parametrize("impl", sorted(IMPLS))
+def test_schedule_only_leaves_cache_unchanged(impl):
     preds, prios = POLICIES["lr_bra"]
-    dut = SchedulerCache(preds, prios, device=0)
+    dut = IMPLS[impl](preds, prios, device=0)
     try:
         for i in range(3):
             dut.add_node({"metadata": {"name": "n%d" % i},
@@ -105,8 +159,9 @@ def _volume_stream(seed, ref, n_events, n_nodes, claims):
         yield kind, x
 
 
+@pytest.mark.parametrize("impl", sorted(IMPLS))
 @pytest.mark.parametrize("seed", range(4))
-def test_event_stream_with_volumes(seed, monkeypatch):
+def test_event_stream_with_volumes(seed, monkeypatch, impl):
     """Volume pods through the per-pod mirror: its volume tables are rebuilt from the cache's pods
     after node events and when new keys appear, and every decision matches the oracle's."""
     from workloads import volume_listers
@@ -117,7 +172,7 @@ def test_event_stream_with_volumes(seed, monkeypatch):
     prios = [("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
     custom = {k: v for k, v in R.volume_predicates(R.VolumeListers(pvs, pvcs), 3).items() if k in preds}
     ref = R.SchedulerCache(set(preds), prios, custom)
-    dut = SchedulerCache(preds, prios, device=0, pvs=pvs, pvcs=pvcs)
+    dut = IMPLS[impl](preds, prios, device=0, pvs=pvs, pvcs=pvcs)
     decisions = fails = 0
     try:
         for ev in _volume_stream(seed, ref, 300, 10, claims):
@@ -168,8 +223,9 @@ def _affinity_stream(seed, ref, n_events, n_nodes):
             yield "update_node", (old, new)
 
 
+@pytest.mark.parametrize("impl", sorted(IMPLS))
 @pytest.mark.parametrize("seed", range(4))
-def test_event_stream_with_affinity_and_spread(seed):
+def test_event_stream_with_affinity_and_spread(seed, impl):
     """Inter-pod affinity and SelectorSpread pods through the per-pod mirror (incremental affinity
     index, tables reloaded only when it grows or after node events): every decision matches the
     oracle's cache."""
@@ -178,7 +234,7 @@ def test_event_stream_with_affinity_and_spread(seed):
     rss = [{"metadata": {"namespace": ""}, "spec": {"selector": {"matchLabels": {"tier": "fe"}}}}]
     preds, prios = POLICIES["default"]
     ref = R.SchedulerCache(set(preds), prios, spread=R.SpreadListers(services=svc, rss=rss))
-    dut = SchedulerCache(preds, prios, device=0, spread=SpreadListers(services=svc, rss=rss))
+    dut = IMPLS[impl](preds, prios, device=0, spread=SpreadListers(services=svc, rss=rss))
     decisions = 0
     try:
         for ev in _affinity_stream(seed, ref, 200, 12):
@@ -193,7 +249,8 @@ def test_event_stream_with_affinity_and_spread(seed):
     assert decisions > 80
 
 
-def test_affinity_tables_load_only_on_growth():
+@pytest.mark.parametrize("impl", sorted(IMPLS))
+def test_affinity_tables_load_only_on_growth(impl):
     """The per-pod path keeps the inter-pod affinity / SelectorSpread state incrementally
     (predicates/metadata.go:127-190): on a replicated workload — four pod templates, hostname
     anti-affinity on two of them, services selecting all — the tables load a handful of times while
@@ -206,7 +263,7 @@ def test_affinity_tables_load_only_on_growth():
     svc = [{"metadata": {"namespace": ""}, "spec": {"selector": {"app": a}}} for a in ("web", "db")]
     preds, prios = POLICIES["default"]
     ref = R.SchedulerCache(set(preds), prios, spread=R.SpreadListers(services=svc))
-    dut = SchedulerCache(preds, prios, device=0, spread=SpreadListers(services=svc))
+    dut = IMPLS[impl](preds, prios, device=0, spread=SpreadListers(services=svc))
 
     def template(k, name):
         app = ("web", "db", "web", "cache")[k]
@@ -246,7 +303,8 @@ def test_affinity_tables_load_only_on_growth():
         dut.close()
 
 
-def test_volume_tables_grow_without_reload():
+@pytest.mark.parametrize("impl", sorted(IMPLS))
+def test_volume_tables_grow_without_reload(impl):
     """Volume pods through the per-pod mirror: a pod that brings a new disk grows the device's
     volume tables (ksim_grow_volumes: keys, classes, refs, zone verdicts, more slots) while the
     device keeps every node's mounts, so the full reload happens once (no node events here) over
@@ -255,7 +313,7 @@ def test_volume_tables_grow_without_reload():
     import random
     preds, prios = POLICIES["default"]
     ref = R.SchedulerCache(set(preds), prios)
-    dut = SchedulerCache(preds, prios, device=0)
+    dut = IMPLS[impl](preds, prios, device=0)
     rng = random.Random(5)
     try:
         for i in range(24):
@@ -288,3 +346,51 @@ def test_volume_tables_grow_without_reload():
         assert dut.vol_loads == 1 and dut.vol_grows > 20
     finally:
         dut.close()
+
+
+def _image_stream(seed, ref, n_events, n_nodes):
+    """event_stream with status.images on the nodes (sizes across calculateScoreFromSize's buckets)
+    and container images on the scheduled / bound pods."""
+    import random
+    from events import event_stream
+    rng = random.Random(4000 + seed)
+    catalog = [("reg/app:%d" % i, size) for i, size in enumerate([5, 30, 120, 400, 800, 1200])]
+
+    def images(node):
+        picks = rng.sample(catalog, rng.randint(0, 4))
+        node.setdefault("status", {})["images"] = [{"names": [n, n + "@sha"], "sizeBytes": s * 1024 * 1024} for n, s in picks]
+
+    for kind, x in event_stream(seed, ref, n_events, n_nodes, features=False):
+        if kind == "add_node":
+            images(x)
+        elif kind == "update_node":
+            images(x[1])
+        elif kind in ("schedule", "add_pod") and "uid" not in x["metadata"]:
+            for c in x["spec"]["containers"]:
+                if rng.random() < 0.8:
+                    c["image"] = rng.choice(catalog)[0]
+        yield kind, x
+
+
+@pytest.mark.parametrize("impl", sorted(IMPLS))
+@pytest.mark.parametrize("seed", range(3))
+def test_event_stream_with_image_locality(seed, impl):
+    """ImageLocalityPriority (image_locality.go:39-88) weighted in the policy, nodes listing images
+    that change on node updates: node images interned into label sets, pod images into classes, the
+    bucketed score a per-(class, label set) addend; every decision matches the oracle's cache."""
+    preds = ["GeneralPredicates", "CheckNodeCondition", "PodToleratesNodeTaints"]
+    prios = [("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1), ("ImageLocalityPriority", 2)]
+    ref = R.SchedulerCache(set(preds), prios)
+    dut = IMPLS[impl](preds, prios, device=0)
+    decisions = 0
+    try:
+        for ev in _image_stream(seed, ref, 250, 10):
+            want = apply(ref, ev)
+            got = apply(dut, ev)
+            if ev[0] == "schedule":
+                decisions += 1
+                assert got == want, (ev[1]["metadata"]["name"], want, got)
+        assert dut.last_node_index == ref.sched.last_node_index
+    finally:
+        dut.close()
+    assert decisions > 80
