@@ -107,7 +107,7 @@ def parse():
                     help="c3 line: pods of the 1M-node C4 streaming side measurement (0 = skip)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--per-pod-calls", type=int, default=200,
-                    help="c2 / c2x: timed ksim_schedule_one calls through the per-pod mirror at each "
+                    help="c2 / c2x: timed ksim_k8s_cache_schedule calls through the C++ scheduler cache at each "
                          "cached-pod mark (0 = skip the per_pod side line)")
     ap.add_argument("--workload", default="c3", choices=["c3", "c2", "c2x", "c4", "c5"],
                     help="c3: the headline metric (default); c2: 5k heterogeneous nodes with selectors, "
@@ -561,14 +561,18 @@ def main():
 
 
 def per_pod_side(a, marks=(1000, 20000)):
-    """The per-pod drop-in's latency: genericScheduler.Schedule + assume as
-    scheduleOne drives them (scheduler.go:431-484), through ksim.cache.SchedulerCache — host
-    encode, incremental affinity / volume sync, one ksim_schedule_one call — timed over
+    """The per-pod drop-in's latency: genericScheduler.Schedule +
+    assume as scheduleOne drives them (scheduler.go:431-484), through the C++ scheduler cache
+    (ksim_k8s_cache_schedule, the call a cgo adapter makes: encode, incremental affinity / volume
+    sync, one launch, one stream sync, results in host-mapped memory) — timed over
     `a.per_pod_calls` consecutive pods of the workload's queue once `m` pods are cached, for each
-    mark m (the calls before a mark are the untimed fill).  The cluster is the workload's nodes
-    (and, for C2x, its PV / PVC listers and services)."""
-    from ksim import synth
-    from ksim.cache import SchedulerCache
+    mark m (the calls before a mark are the untimed fill).  The pods of a timed window are
+    flattened to their C structs beforehand (a Go adapter's cost, not the library's); each call is
+    timed on its own for the percentiles.  The cluster is the workload's nodes (and, for C2x, its
+    PV / PVC listers and services)."""
+    import ctypes as C
+    from ksim import abi, synth
+    from ksim.frontend import K8sCache, _Keep, lib as k8s_lib
     from ksim.spread import SpreadListers
     calls = a.per_pod_calls
     total = max(marks) + calls
@@ -579,7 +583,8 @@ def per_pod_side(a, marks=(1000, 20000)):
         nodes, pods = synth.c2_objects(a.nodes, total)
         kw = {}
     preds, prios = scheduler_provider()
-    sc = SchedulerCache(preds, prios, **kw)
+    sc = K8sCache(preds, prios, **kw)
+    L = k8s_lib()
     t_start = time.perf_counter()
     try:
         for nd in nodes:
@@ -592,18 +597,34 @@ def per_pod_side(a, marks=(1000, 20000)):
                 if i % 1000 == 0:
                     print("per_pod: %d pods cached (%.1f s)" % (i, time.perf_counter() - t_start), file=sys.stderr,
                           flush=True)
-            r0 = sc.aff_reloads
+            keep = [_Keep() for _ in range(calls)]
+            flat = [sc._pod(keep[j], pods[i + j]) for j in range(calls)]
+            res = abi.Result()
+            r0 = sc.stats()
+            lat = []
             t0 = time.perf_counter()
-            for _ in range(calls):
-                bound += sc.schedule_one(pods[i])[0] is not None
-                i += 1
+            for j in range(calls):
+                c0 = time.perf_counter()
+                rc = L.ksim_k8s_cache_schedule(sc.h, flat[j], abi.SCHEDULE_ASSUME, C.byref(res))
+                lat.append(time.perf_counter() - c0)
+                if rc:
+                    raise sc._err(rc, L.ksim_k8s_cache_last_error(sc.h))
+                bound += res.node >= 0
             dt = time.perf_counter() - t0
+            i += calls
+            r1 = sc.stats()
+            lat.sort()
+            pct = lambda q: round(lat[min(len(lat) - 1, int(q * len(lat)))] * 1e6, 1)
             out.append({"cached_pods": m, "calls": calls, "us_per_call": round(dt / calls * 1e6, 1),
-                        "affinity_table_loads": sc.aff_reloads - r0})
-        return {"marks": out, "pods_bound": bound, "nodes": len(nodes), "volume_table_loads": sc.vol_loads,
-                "volume_table_grows": sc.vol_grows, "affinity_table_loads": sc.aff_reloads,
-                "note": "wall time per scheduleOne-equivalent call (host encode + table sync + one "
-                        "ksim_schedule_one with assume), pods of the same workload queue in order"}
+                        "p50_us": pct(0.5), "p90_us": pct(0.9), "p99_us": pct(0.99),
+                        "affinity_table_loads": r1[0] - r0[0], "volume_table_loads": r1[1] - r0[1],
+                        "volume_table_grows": r1[2] - r0[2]})
+        st = sc.stats()
+        return {"front_end": "C++ ksim_k8s_cache_schedule (SCHEDULE_ASSUME)", "marks": out, "pods_bound": bound,
+                "nodes": len(nodes), "affinity_table_loads": st[0], "volume_table_loads": st[1],
+                "volume_table_grows": st[2], "class_table_loads": st[3],
+                "note": "wall time per scheduleOne-equivalent native call (encode + table sync + one launch "
+                        "+ one sync + assume), pods of the same workload queue in order"}
     finally:
         sc.close()
 

@@ -10,8 +10,10 @@
 //   NodeInfo.AddPod / RemovePod / SetNode schedulercache/node_info.go:318-341, 343-390, 429-448
 //
 // A Schedule call is one scan launch (ksim_scan_kernel, the launch-mode kernel) over the
-// resident table against a staged pod descriptor: one packed host→device copy {cursor, result
-// block, pod, ports, scalars}, one kernel, one device→host copy of the result block.  Node
+// resident table against a staged pod descriptor: the pod, its ports / scalars and the result
+// block live in one pinned host block mapped into the device's address space, so the kernel reads
+// the pod over the bus and writes node, fit count, FitError histogram, error word and
+// lastNodeIndex back the same way — one launch and one stream sync per call, no copies.  Node
 // events relayout the table in one kernel (rows stay in name-rank order).
 #include "ksim_handle.h"
 #include "ksim_cache.h"
@@ -27,23 +29,22 @@ constexpr size_t STG_PORTS = STG_POD + sizeof(ksim_pod);
 int ensure_staging(ksim_handle* h, int32_t n_ports, int32_t n_scalars) {
   const size_t need = STG_PORTS + (size_t)n_ports * 8 + (size_t)n_scalars * sizeof(ksim_scalar_req) +
                       (size_t)KSIM_PK_WORDS(KSIM_MAX_SCALAR, 0) * 8;
-  if (h->stg_dev && h->stg_cap >= need) return KSIM_OK;
+  if (h->stg_host && h->stg_cap >= need) return KSIM_OK;
   const size_t cap = std::max<size_t>(need * 2, 4096);
-  char* d = nullptr;
-  int rc = dev_alloc(h, &d, cap);
-  if (rc) return rc;
   char* hst = nullptr;
-  HIPCHK(h, hipHostMalloc((void**)&hst, cap, hipHostMallocDefault));
-  dev_free(h, h->stg_dev);
-  if (h->stg_host) (void)hipHostFree(h->stg_host);
+  HIPCHK(h, hipHostMalloc((void**)&hst, cap, hipHostMallocMapped));
+  char* d = nullptr;
+  HIPCHK(h, hipHostGetDevicePointer((void**)&d, hst, 0));
+  if (h->stg_host) {  // every earlier call has synchronised its stream
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    (void)hipHostFree(h->stg_host);
+  }
+  memset(hst, 0, cap);
   h->stg_dev = d;
   h->stg_host = hst;
   h->stg_cap = cap;
-  if (!h->res_host) {
-    HIPCHK(h, hipHostMalloc((void**)&h->res_host, KSIM_RES_WORDS * 4, hipHostMallocDefault));
-    HIPCHK(h, hipHostMalloc((void**)&h->ctr_host, 8, hipHostMallocDefault));
-  }
   h->res_dev = reinterpret_cast<int32_t*>(d + STG_RES);
+  h->res_host = reinterpret_cast<int32_t*>(hst + STG_RES);
   return KSIM_OK;
 }
 
@@ -64,7 +65,6 @@ int stage_pod(ksim_handle* h, const ksim_pod& pod, const uint64_t* ports, const 
   const size_t pb = (size_t)pod.port_cnt * 8, sb = (size_t)pod.scalar_cnt * sizeof(ksim_scalar_req);
   if (pb) memcpy(hs + STG_PORTS, ports + pod.port_off, pb);
   if (sb) memcpy(hs + STG_PORTS + pb, scalars + pod.scalar_off, sb);
-  HIPCHK(h, hipMemcpyAsync(h->stg_dev, hs, STG_PORTS + pb + sb, hipMemcpyHostToDevice, h->stream));
   *cs = h->ctx;
   cs->pods = reinterpret_cast<const ksim_pod*>(h->stg_dev + STG_POD);
   cs->pod_ports = reinterpret_cast<const uint64_t*>(h->stg_dev + STG_PORTS);
@@ -158,7 +158,6 @@ int ensure_port_room(ksim_handle* h, int32_t need) {
     if (rc) return rc;
     hipError_t e = ksim_launch_port_max(c.port_count, c.n, h->res_dev + KSIM_RES_STATUS, h->stream);
     if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "port max: %s", hipGetErrorString(e));
-    HIPCHK(h, hipMemcpyAsync(h->res_host, h->res_dev, KSIM_RES_WORDS * 4, hipMemcpyDeviceToHost, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->port_bound = h->res_host[KSIM_RES_STATUS];
   } else {
@@ -200,8 +199,7 @@ int after_commit(ksim_handle* h, int32_t port_cnt) {
   h->tree_valid = false;  // the trees are maintained by the tree kernel only
   h->port_bound += port_cnt;
   if (h->res_host[KSIM_RES_STATUS] & 1) h->pfast_off = true;  // keep the fast kernels' float64 range
-  int32_t err = 0;
-  HIPCHK(h, hipMemcpy(&err, h->ctx.err, 4, hipMemcpyDeviceToHost));
+  const int32_t err = h->res_host[KSIM_RES_ERR];  // written by the committing kernel
   if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port or volume slots overflowed (raise port_slots / vol_slots)");
   if (err & ~1) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
   return KSIM_OK;
@@ -257,8 +255,7 @@ int set_row(ksim_handle* h, int64_t index, const ksim_node_row* row, bool full) 
   pack_row(h->ctx, row, pk);
   int rc = ensure_staging(h, (int32_t)pk.size(), 0);
   if (rc) return rc;
-  memcpy(h->stg_host + STG_PORTS, pk.data(), pk.size() * 8);
-  HIPCHK(h, hipMemcpyAsync(h->stg_dev + STG_PORTS, h->stg_host + STG_PORTS, pk.size() * 8, hipMemcpyHostToDevice, h->stream));
+  memcpy(h->stg_host + STG_PORTS, pk.data(), pk.size() * 8);  // read by the kernel through the mapping
   hipError_t e = ksim_launch_set_row(&h->ctx, index, reinterpret_cast<const uint64_t*>(h->stg_dev + STG_PORTS), full ? 1 : 0,
                                      h->stream);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "set_row launch: %s", hipGetErrorString(e));
@@ -328,19 +325,15 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
     e = ksim_launch_ipa_pass(&cs, npt, grid, h->stream);  // InterPodAffinity / SelectorSpread reductions first
   if (e == hipSuccess) e = ksim_launch_scan(&cs, npt, 1, grid, h->stream);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "scan launch: %s", hipGetErrorString(e));
-  HIPCHK(h, hipMemcpyAsync(h->res_host, h->res_dev, KSIM_RES_WORDS * 4, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(h, hipMemcpyAsync(h->ctr_host, c.counter, 8, hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(h->stream));  // the result block is host memory: nothing to copy
   const int32_t* r = h->res_host;
   memset(out, 0, sizeof *out);
   out->node = r[KSIM_RES_NODE];
   out->fit_nodes = r[KSIM_RES_FIT];
-  out->last_node_index = *h->ctr_host;
+  memcpy(&out->last_node_index, r + KSIM_RES_CTR, 8);
   if (out->node < 0) memcpy(out->reasons, r + KSIM_RES_REASONS, sizeof out->reasons);
   if (assume && out->node >= 0) return after_commit(h, pod->port_cnt);
-  int32_t err = 0;
-  HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
-  if (err) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
+  if (r[KSIM_RES_ERR]) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", r[KSIM_RES_ERR]);
   return KSIM_OK;
 }
 
@@ -360,7 +353,6 @@ static int pod_delta(ksim_handle* h, int64_t node, const ksim_pod* pod, const ui
   hipError_t e = add ? ksim_launch_assume(&cs, 0, node, h->res_dev + KSIM_RES_STATUS, h->stream)
                      : ksim_launch_release(&cs, 0, node, h->stream);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "%s launch: %s", where, hipGetErrorString(e));
-  HIPCHK(h, hipMemcpyAsync(h->res_host, h->res_dev, KSIM_RES_WORDS * 4, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   if (!add) {  // a release can only shrink quantities, but never below zero in a consistent cache
     h->tree_valid = false;
@@ -388,10 +380,9 @@ int ksim_assume(ksim_handle* h, int64_t pod, int64_t node) {
   if (rc) return rc;
   rc = ensure_staging(h, 0, 0);
   if (rc) return rc;
-  HIPCHK(h, hipMemsetAsync(h->res_dev, 0, KSIM_RES_WORDS * 4, h->stream));
+  memset(h->res_host, 0, KSIM_RES_WORDS * 4);
   hipError_t e = ksim_launch_assume(&h->ctx, pod, node, h->res_dev + KSIM_RES_STATUS, h->stream);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "assume launch: %s", hipGetErrorString(e));
-  HIPCHK(h, hipMemcpyAsync(h->res_host, h->res_dev, KSIM_RES_WORDS * 4, hipMemcpyDeviceToHost, h->stream));
   HIPCHK(h, hipStreamSynchronize(h->stream));
   return after_commit(h, 0);
 }

@@ -84,6 +84,16 @@ struct KsimVol {
   int32_t pad;
 };
 
+// Result block of the per-pod drop-in entry points (int32 words; pinned host memory mapped into the
+// device's address space, written by the scan / assume kernels, read by the host after the sync).
+#define KSIM_RES_NODE 0
+#define KSIM_RES_FIT 1
+#define KSIM_RES_STATUS 2   /* bit 0: a committed quantity left the fast kernels' exact range */
+#define KSIM_RES_ERR 3      /* the sticky device error word after the call */
+#define KSIM_RES_REASONS 4
+#define KSIM_RES_CTR (KSIM_RES_REASONS + KSIM_NREASONS)  /* uint64 lastNodeIndex after the call */
+#define KSIM_RES_WORDS (KSIM_RES_CTR + 2)
+
 struct KsimCtx {
   // ---- node table (name-rank order) ----
   int64_t n;

@@ -64,13 +64,11 @@ struct DevBuf {
   size_t bytes = 0;
 };
 
-// Per-pod staging area of the drop-in entry points (ksim_schedule_one, ksim_pod_add/remove):
-// one packed host->device upload {cursor, pod, ports, scalars} and one result block.
-#define KSIM_RES_NODE 0
-#define KSIM_RES_FIT 1
-#define KSIM_RES_STATUS 2   /* bit 0: a committed quantity left the fast kernels' exact range */
-#define KSIM_RES_REASONS 4
-#define KSIM_RES_WORDS (KSIM_RES_REASONS + KSIM_NREASONS)
+// Per-pod staging area of the drop-in entry points (ksim_schedule_one, ksim_pod_add/remove): one
+// block of pinned host memory mapped into the device's address space — {cursor, result block, pod,
+// ports, scalars} — that the kernels read the pod from and write the result to directly, so a call
+// is one launch and one stream sync, with no copy either way.
+// (the result block layout KSIM_RES_* is in ksim_common.h: the kernels write it)
 
 struct ksim_handle {
   int device = 0;
@@ -138,12 +136,12 @@ struct ksim_handle {
   void* swt_scratch = nullptr;  // tree sweep: per-scenario columns, trees, counters, outputs
   size_t swt_bytes = 0;
   // per-pod drop-in staging (ksim_cache.cpp)
-  char* stg_dev = nullptr;      // device: [int64 cursor][ksim_pod][ports][scalars]
-  char* stg_host = nullptr;     // pinned host mirror of the upload
+  char* stg_dev = nullptr;      // the mapped staging block as the device addresses it
+  char* stg_host = nullptr;     // pinned host memory: [int64 cursor][result block][ksim_pod][ports][scalars]
   size_t stg_cap = 0;
-  int32_t* res_dev = nullptr;   // device result block (KSIM_RES_*)
-  int32_t* res_host = nullptr;  // pinned
-  uint64_t* ctr_host = nullptr; // pinned copy of lastNodeIndex after a call
+  int32_t* res_dev = nullptr;   // result block (KSIM_RES_*), device view
+  int32_t* res_host = nullptr;  // the same words, host view
+  uint64_t* ctr_host = nullptr; // unused (lastNodeIndex comes back in the result block)
   int64_t port_bound = 0;       // upper bound of max(port_count) over the nodes
   // inter-pod affinity (ksim_load_affinity): the device tables, their sizes for validation, and
   // per queued pod its identity / class (an affinity pod takes the launch-mode kernels)
@@ -169,6 +167,7 @@ struct ksim_handle {
   char* pg_rec = nullptr;                  // pod-context records of the current call
   size_t pg_rec_bytes = 0;
   bool fuse_off = false;        // a fused pass-A barrier timed out once: pass A as its own launch
+  bool pgen_off = false;        // a general persistent kernel ran out of a spin bound once: the launch form
   std::vector<void*> aff_bufs;
   std::vector<int32_t> q_ident, q_aclass;
   std::vector<int64_t> aff_pre;  // aff_pre[i] = affinity pods among the first i queued

@@ -275,7 +275,7 @@ void build(ksim_k8s_cluster* c) {
 
 int load_volumes(ksim_k8s_cluster* c, ksim_handle* h, bool use_zone) {
   return load_vol_tab(c->vsmall, (int64_t)c->nodes.size(), c->vol_S, c->opt.max_vols, use_zone ? &c->vol_zone_ok : nullptr,
-                      c->vol_zone_words, c->vol_slots.data(), c->vol_slot_count.data(), h);
+                      c->vol_zone_words, true, c->vol_slots.data(), c->vol_slot_count.data(), h);
 }
 
 }  // namespace
@@ -599,7 +599,7 @@ extern "C" int ksim_k8s_describe(ksim_k8s_cluster* c, ksim_handle* h, const ksim
         const int32_t want = (int32_t)(most + c->extra_vol_keys.size());
         if (c->opt.vol_slots < 0 && want > c->vol_S) c->vol_S = std::max(want, 2 * c->vol_S);
         if ((e = load_vol_tab(c->vsmall, (int64_t)c->nodes.size(), c->vol_S, c->opt.max_vols,
-                              c->opened_zone ? &c->vol_zone_ok : nullptr, c->vol_zone_words, nullptr, nullptr, h)))
+                              c->opened_zone ? &c->vol_zone_ok : nullptr, c->vol_zone_words, false, nullptr, nullptr, h)))
           fail(e, "ksim_grow_volumes: %s", ksim_last_error(h));
       }
     }

@@ -172,7 +172,7 @@ void sync_volumes(Cache* c, bool need, const Enc* e) {
       const int32_t S = std::max<int32_t>(c->vol_S, (int32_t)(2 * want));
       vol_small(vi, &vs);
       check(c, load_vol_tab(vs, (int64_t)c->names.size(), S, c->opt.max_vols, c->use_zone ? &c->vol_zone : nullptr,
-                            c->vol_zone_words, nullptr, nullptr, c->h),
+                            c->vol_zone_words, false, nullptr, nullptr, c->h),
             "ksim_grow_volumes");
       c->vol_key = key;
       c->vol_S = S;
@@ -202,8 +202,8 @@ void sync_volumes(Cache* c, bool need, const Enc* e) {
     count[i] = s;
   }
   vol_small(vi, &vs);
-  check(c, load_vol_tab(vs, n, S, c->opt.max_vols, c->use_zone ? &c->vol_zone : nullptr, c->vol_zone_words, slots.data(),
-                        count.data(), c->h),
+  check(c, load_vol_tab(vs, n, S, c->opt.max_vols, c->use_zone ? &c->vol_zone : nullptr, c->vol_zone_words, true,
+                        slots.data(), count.data(), c->h),
         "ksim_load_volumes");
   c->vol_key = key;
   c->vol_S = S;

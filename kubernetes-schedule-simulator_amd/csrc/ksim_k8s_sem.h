@@ -1505,9 +1505,9 @@ void vol_small(const VolumeIndex& vi, VolSmall* t) {
   t->vc_filter = vi.class_filter;
 }
 
-// ksim_load_volumes (slots given) or ksim_grow_volumes (slots NULL) over the small tables.
+// ksim_load_volumes (full: with the slots) or ksim_grow_volumes (slots ignored) over the small tables.
 int load_vol_tab(const VolSmall& v, int64_t n, int32_t S, const int32_t* max_vols, const std::vector<uint32_t>* zone_ok,
-                 int32_t zone_words, const uint64_t* slots, const int32_t* slot_count, ksim_handle* h) {
+                 int32_t zone_words, bool full, const uint64_t* slots, const int32_t* slot_count, ksim_handle* h) {
   ksim_volume_tables t{};
   t.n_keys = (int32_t)v.key_filter.size();
   t.n_vclass = (int32_t)v.vc_filter.size();
@@ -1525,7 +1525,7 @@ int load_vol_tab(const VolSmall& v, int64_t n, int32_t S, const int32_t* max_vol
   }
   t.slots = slots;
   t.slot_count = slot_count;
-  return slots ? ksim_load_volumes(h, &t) : ksim_grow_volumes(h, &t);
+  return full ? ksim_load_volumes(h, &t) : ksim_grow_volumes(h, &t);
 }
 
 // The listers' objects (what the volume predicates resolve PVCs through).

@@ -662,9 +662,16 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       }
     }
   }
+  if (c.out_fit) __syncthreads();  // (uniform) wave 1's affinity commit is done
   if (tid == 0) {
     c.out_node[pod] = (int32_t)D.node;
-    if (c.out_fit) c.out_fit[0] = D.fitTotal;
+    if (c.out_fit) {  // per-pod drop-in: fit count, error word and lastNodeIndex into the result block
+      c.out_fit[0] = D.fitTotal;
+      c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t ctr = *c.counter;
+      c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT] = (int32_t)(uint32_t)ctr;
+      c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1] = (int32_t)(uint32_t)(ctr >> 32);
+    }
     *c.cursor = pod + 1;
     *c.ticket = 0;
   }
@@ -687,6 +694,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_
 }
 
 // Commit one pod to one node (ksim_assume, ksim_pod_add); status |= ksim_row_status.
+// status[0] |= ksim_row_status, status[1] = the error word afterwards (KSIM_RES_STATUS / _ERR).
 __global__ void ksim_assume_kernel(KsimCtx c, int64_t pod, int64_t node, int32_t* status) {
   if (blockIdx.x != 0 || threadIdx.x >= 64) return;
   if (threadIdx.x == 0) {
@@ -695,6 +703,8 @@ __global__ void ksim_assume_kernel(KsimCtx c, int64_t pod, int64_t node, int32_t
     *status |= ksim_row_status(c, node);
   }
   if (ksim_is_aff_pod(c, c.pods[pod])) ksim_aff_commit(*c.aff, c.pods[pod], node, 1, threadIdx.x, 64);
+  __syncthreads();
+  if (threadIdx.x == 0) status[KSIM_RES_ERR - KSIM_RES_STATUS] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Launch-mode entry points used by the host runtime (ksim_runtime.cpp).

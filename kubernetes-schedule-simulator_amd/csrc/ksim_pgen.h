@@ -113,6 +113,8 @@ struct PGenArgs {
   int32_t n_zone;     // zones of the spread reduce (<= PG_MAXZ)
   int32_t pad;
   uint64_t spin_ticks;
+  int32_t test_stall;  // diagnostic (KSIM_PGEN_TEST_STALL): the last workgroup exits at once, as one
+                       // that never became resident; the others must abort and the host recover
 };
 
 extern "C" hipError_t ksim_launch_pgen2(const KsimCtx* c, const PGenArgs* g, int grid, int npt, size_t lds, hipStream_t s);

@@ -644,6 +644,7 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
 
   const KsimCtx& c = c_arg;
   const PGenArgs& g = g_arg;
+  if (g.test_stall && blockIdx.x == gridDim.x - 1) return;  // diagnostic: a workgroup that never ran
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int G = gridDim.x;
   const int64_t chunk = c.chunk;
@@ -669,6 +670,7 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
   pg_stage_counts(c, g, L, nrows, chunk, tid, blockDim.x);
   __syncthreads();
 
+  int64_t stop_pod = c.end;  // first pod not scheduled (a spin bound ran out: the grid is not co-resident)
   for (int64_t pod = c.first; pod < c.end; ++pod) {
     PgX X;
     X.base = xrec(pod);
@@ -816,7 +818,7 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
         }
       }
       __syncthreads();
-      if (s_abort) break;
+      if (s_abort) { stop_pod = pod; break; }
       const int64_t gmn = s_g[0], gmx = s_g[1], gsmx = s_g[2], ghz = s_g[3], gzm = s_g[4];
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
@@ -1079,7 +1081,7 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
     __syncthreads();
     PG_STAMP(3);
     const int mode = s_mode;
-    if (mode < 0) break;  // uniform: every workgroup reached the same verdict
+    if (mode < 0) { stop_pod = pod; break; }  // uniform: every workgroup reached the same verdict
 
     // ---- 5. FitError: every workgroup adds its rows' reasons ----
     if (mode == 0) {
@@ -1224,7 +1226,7 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
         s_node = (int64_t)(v & M56);
       }
       __syncthreads();
-      if (s_abort) break;
+      if (s_abort) { stop_pod = pod; break; }
       const int64_t w = s_node;
       const int2* mp = X.sec<int2>(PGS_MP);
       const PgCar* cr = X.sec<PgCar>(PGS_CAR);
@@ -1252,9 +1254,10 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
   }
   // ---- the table is authoritative in HBM between calls: write the owned rows back ----
   pg_write_back(c, g, L, lo, nrows, chunk, tid, blockDim.x);
+  if (tid == 0 && stop_pod < c.end) atomicMin((unsigned long long*)c.cursor, (unsigned long long)stop_pod);
   if (blockIdx.x == 0 && tid == 0) {
     *c.counter = counter;
-    *c.cursor = c.end;
+    (void)0;  // the cursor: c.end preset by the host, lowered below by an aborting workgroup
 #ifdef KSIM_STAMPS
     for (int k = 0; k < 16; ++k) c.dbg[k] += st_acc[k];
 #endif
@@ -1437,6 +1440,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
 #endif
   const KsimCtx& c = c_arg;
   const PGenArgs& g = g_arg;
+  if (g.test_stall && blockIdx.x == gridDim.x - 1) return;  // diagnostic: a workgroup that never ran
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const bool rowt = wv >= 1 && wv <= 3;  // E0: the row state
   const bool hypt = wv >= 5;             // E1: the same rows under the hypothesis
@@ -1486,6 +1490,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
   int32_t pend_j = -1;   // deferred commit of pod pend_pod on row pend_j (its row thread)
   int64_t pend_pod = -1;
 
+  int64_t stop_pod = c.end;  // first pod not scheduled (a spin bound ran out: the grid is not co-resident)
   for (int64_t pod = c.first; pod < c.end; ++pod) {
     PgX X;
     X.base = xrec(pod);
@@ -1613,7 +1618,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
         pend_j = -1;
       }
       __syncthreads();
-      if (s_abort) break;
+      if (s_abort) { stop_pod = pod; break; }
       const int64_t gmn = s_g[0], gmx = s_g[1], gsmx = s_g[2], ghz = s_g[3], gzm = s_g[4];
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
@@ -1947,7 +1952,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
     __syncthreads();
     PG_STAMP(3);
     const int mode = s_mode;
-    if (mode < 0) break;  // uniform: every workgroup reached the same verdict
+    if (mode < 0) { stop_pod = pod; break; }  // uniform: every workgroup reached the same verdict
 
     // ---- FitError: every workgroup adds its rows' reasons; nothing committed ----
     if (mode == 0) {
@@ -2035,7 +2040,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
         s_node = (int64_t)(v & M56);
       }
       __syncthreads();
-      if (s_abort) break;
+      if (s_abort) { stop_pod = pod; break; }
       const int64_t w = s_node;
       const int2* mp = X.sec<int2>(PGS_MP);
       const PgCar* cr = X.sec<PgCar>(PGS_CAR);
@@ -2083,6 +2088,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
     pg_commit_row(c, g, L, Xp, Hp, pend_j, lo + pend_j);
   }
   pg_write_back(c, g, L, lo, nrows, chunk, tid, blockDim.x);
+  if (tid == 0 && stop_pod < c.end) atomicMin((unsigned long long*)c.cursor, (unsigned long long)stop_pod);
 #ifdef KSIM_STAMPS
   // the spread over workgroups: max and (as ~max of ~) min of pass-A exchange, classes, decide
   // window, pass-A local, and of the row evaluations
@@ -2115,7 +2121,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
 #endif
   if (blockIdx.x == 0 && tid == 0) {
     *c.counter = counter;
-    *c.cursor = c.end;
+    (void)0;  // the cursor: c.end preset by the host, lowered below by an aborting workgroup
 #ifdef KSIM_STAMPS
     for (int k = 0; k < 16; ++k) c.dbg[k] += st_acc[k];
 #endif

@@ -86,8 +86,7 @@ void ksim_destroy(ksim_handle* h) {
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
   if (h->graph) (void)hipGraphDestroy(h->graph);
   for (auto& b : h->bufs) (void)hipFree(b.p);
-  for (void* q : {(void*)h->stg_host, (void*)h->res_host, (void*)h->ctr_host})
-    if (q) (void)hipHostFree(q);
+  if (h->stg_host) (void)hipHostFree(h->stg_host);  // res_host points into it
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->stream) (void)hipStreamDestroy(h->stream);
@@ -623,9 +622,10 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
     HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
     HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
     const double nf = (double)(d[21] ? d[21] : 1);
-    fprintf(stderr, "[ksim stamps] pfast pods=%lld (%.3f ms) cycles/pod: sweep %.0f decide %.0f owner %.0f barrier %.0f tail %.0f row-eval %.0f\n",
-            (long long)count, ms, d[2] / (double)count, d[3] / (double)count, d[6] / (double)count, d[7] / (double)count,
-            (d[4] + d[1]) / (double)count, d[5] / (double)count);
+    fprintf(stderr, "[ksim stamps] pfast pods=%lld (%.3f ms) cycles/pod: sweep %.0f fix-wait %.0f decide %.0f owner %.0f barrier %.0f "
+            "tail %.0f row-eval %.0f; consecutive owners %.3f\n",
+            (long long)count, ms, d[2] / (double)count, d[12] / (double)count, d[3] / (double)count, d[6] / (double)count,
+            d[7] / (double)count, (d[4] + d[1]) / (double)count, d[5] / (double)count, d[23] / (double)count);
     fprintf(stderr, "[ksim stamps] pfast row wave 1 cycles/pod: pods %.0f eval %.0f wave-stats %.0f publish %.0f\n",
             d[8] / (double)count, d[9] / (double)count, d[10] / (double)count, d[11] / (double)count);
     fprintf(stderr, "[ksim stamps] pfast owner (%llu fixes) cycles: select %.0f barrier %.0f fix-publish %.0f commit+barrier+restat %.0f\n",
@@ -658,7 +658,7 @@ struct PgPlan {
 
 static bool pgen_plan(ksim_handle* h, PgPlan* pl, bool allow_v2 = true) {
   const KsimCtx& c = h->ctx;
-  if (getenv("KSIM_NO_PGEN") || h->shard.world > 1 || c.n <= 0) return false;
+  if (getenv("KSIM_NO_PGEN") || h->pgen_off || h->shard.world > 1 || c.n <= 0) return false;
   int64_t s = 0;
   for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED, KSIM_W_INTERPOD_AFFINITY,
                 KSIM_W_SELECTOR_SPREAD}) {
@@ -751,7 +751,9 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, const PgP
   PGenArgs g{};
   g.gran = h->pg_gran;
   g.rec = h->pg_rec;
-  g.spin_ticks = 200000000ull;
+  g.spin_ticks = 200000000ull;  // 2 s per wait
+  if (const char* e = getenv("KSIM_PGEN_SPIN_TICKS")) g.spin_ticks = strtoull(e, nullptr, 10);
+  g.test_stall = getenv("KSIM_PGEN_TEST_STALL") ? 1 : 0;
   g.d = pl.d;
   memcpy(g.off, pl.off, sizeof g.off);
   g.has_vol = h->have_vol ? 1 : 0;
@@ -770,6 +772,8 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, const PgP
   c.end = first + count;
   c.chunk = pl.chunk;
   HIPCHK(h, hipMemsetAsync(h->pg_gran, 0, gb, h->stream));
+  const int64_t end = first + count;  // the kernel lowers the cursor to the first pod it did not schedule
+  HIPCHK(h, hipMemcpyAsync(c.cursor, &end, 8, hipMemcpyHostToDevice, h->stream));
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
   hipError_t e = ksim_pgen_pack(&c, &g, h->stream);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pgen pack: %s", hipGetErrorString(e));
@@ -826,6 +830,30 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, const PgP
     st->mode = KSIM_MODE_PERSISTENT;
     st->blocks = pl.grid;
   }
+  int32_t err = 0;
+  HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
+  if (err & 4) {
+    // a spin bound ran out (the grid was not co-resident after all, e.g. another process's kernels
+    // held CUs): every workgroup stopped before deciding the pod at the cursor and wrote back what
+    // it had committed.  Clear the bit and finish [cursor, end) with the launch form; the general
+    // persistent kernel stays off for this handle.
+    int64_t cur = end;
+    HIPCHK(h, hipMemcpy(&cur, c.cursor, 8, hipMemcpyDeviceToHost));
+    err &= ~4;
+    HIPCHK(h, hipMemcpy(c.err, &err, 4, hipMemcpyHostToDevice));
+    h->pgen_off = true;
+    if (cur < first || cur > end) return ksim_fail(h, KSIM_E_DEVICE, "pgen abort at an impossible pod %lld", (long long)cur);
+    if (cur < end) {
+      ksim_stats s2{};
+      if ((rc = run_launch_mode(h, cur, end - cur, &s2))) return rc;
+      if (st) {
+        st->device_ms += s2.device_ms;
+        st->kernel_ms += s2.kernel_ms;
+        st->kernel_launches += s2.kernel_launches;
+        st->mode = KSIM_MODE_LAUNCH;
+      }
+    }
+  }
   return KSIM_OK;
 }
 
@@ -833,8 +861,25 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, const PgP
 // service affinity): the persistent one when it can take the range.
 static int run_f3_range(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   PgPlan pl;
-  if (h->cfg.mode != KSIM_MODE_LAUNCH && pgen_plan(h, &pl)) return run_pgen_mode(h, first, count, pl, st);
-  return run_launch_mode(h, first, count, st);
+  if (h->cfg.mode == KSIM_MODE_LAUNCH || !pgen_plan(h, &pl)) return run_launch_mode(h, first, count, st);
+  // the pod-context records (up to PG_REC_MAX bytes per pod) of at most ~256 MB per launch: a long
+  // range goes in sub-ranges (the table, slots and counts persist in HBM between launches)
+  const int64_t per = std::max<int64_t>(1, ((int64_t)256 << 20) / std::max<int64_t>(pl.d.rec_stride, 1));
+  if (st) memset(st, 0, sizeof *st);
+  for (int64_t a = first; a < first + count; a += per) {
+    const int64_t n = std::min<int64_t>(per, first + count - a);
+    ksim_stats s2{};
+    int rc = h->pgen_off ? run_launch_mode(h, a, n, &s2) : run_pgen_mode(h, a, n, pl, &s2);
+    if (rc) return rc;
+    if (st) {
+      st->device_ms += s2.device_ms;
+      st->kernel_ms += s2.kernel_ms;
+      st->kernel_launches += s2.kernel_launches;
+      st->mode = s2.mode;
+      st->blocks = s2.blocks;
+    }
+  }
+  return KSIM_OK;
 }
 
 static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {

@@ -23,7 +23,7 @@ int validate(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
     if (t->max_vols[k] < 0) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: negative volume limit");
   auto need = [&](const void* p, int64_t cnt) { return cnt == 0 || p != nullptr; };
   if (!need(t->key_filter, t->n_keys) || !need(t->vc, 2 * (int64_t)t->n_vclass) || !need(t->vc_filter, t->n_vclass) ||
-      !need(t->refs, t->n_refs) || (!keep && (!need(t->slots, (int64_t)t->vol_slots * n) || !t->slot_count)))
+      !need(t->refs, t->n_refs) || (!keep && (!need(t->slots, (int64_t)t->vol_slots * n) || !need(t->slot_count, n))))
     return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: missing array");
   if (keep && (t->n_keys < h->vol_n_keys || t->n_vclass < h->vol_n_class || t->vol_slots < h->vol_h.vol_slots))
     return ksim_fail(h, KSIM_E_INVAL, "ksim_grow_volumes: the tables may only grow (keys %d < %d, classes %d < %d or "

@@ -586,8 +586,10 @@ class K8sCache:
         if res.node < 0:
             buf = C.create_string_buffer(4096)
             lib().ksim_k8s_cache_fit_error(self.h, C.byref(res), buf, 4096)
-            err = FitError(self.node_count(), list(res.reasons))
-            err.args = (buf.value.decode(),)
+            import numpy as np
+            err = FitError.__new__(FitError)  # the library's FitError text (scalar names are its own)
+            Exception.__init__(err, buf.value.decode())
+            err.num_nodes, err.hist = self.node_count(), np.asarray(list(res.reasons), np.int32)
             raise err
         return lib().ksim_k8s_cache_node_name(self.h, res.node).decode()
 

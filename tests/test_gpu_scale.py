@@ -153,3 +153,28 @@ def test_c2x_matches_c_oracle(n_nodes, n_pods, mode):
         assert _slot_sets(slots, cnt) == _slot_sets(extra["vslots"], extra["vcount"])
     finally:
         g.close()
+
+
+def test_pgen_spin_abort_recovers(monkeypatch):
+    """The general persistent kernel's spin bounds running out (its grid not co-resident after all):
+    KSIM_PGEN_TEST_STALL makes the last workgroup exit at once, as one that never became resident,
+    and a 1 ms bound ends the others' first wait.  Every workgroup stops before deciding the pod at
+    the cursor; the runtime clears the error and finishes the range with the launch form — the whole
+    C2x-shaped queue still equals the C oracle (placements, FitErrors, counter, node state)."""
+    monkeypatch.setenv("KSIM_PGEN_TEST_STALL", "1")
+    monkeypatch.setenv("KSIM_PGEN_SPIN_TICKS", "100000")
+    cl, preds, prios, _ = synth.config_c2x(600, 3000)
+    g = scheduler.GenericScheduler(cl, preds, prios, collect_reasons=True)
+    try:
+        out, reasons, st = g.schedule()
+        assert st.mode == abi.MODE_LAUNCH  # finished by the launch form after the abort
+        ref, ref_reasons, ref_state, ref_ctr, _ = cpu_ref.run(cl, None, threads=16, plan=g.plan)
+        assert np.array_equal(out, ref)
+        failed = out < 0
+        assert np.array_equal(reasons[failed], ref_reasons[failed])
+        assert g.last_node_index == ref_ctr
+        s = g.node_state()
+        for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count", "port_count"):
+            assert np.array_equal(s[k], ref_state[k]), k
+    finally:
+        g.close()
