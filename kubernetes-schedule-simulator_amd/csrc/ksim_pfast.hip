@@ -480,6 +480,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   lds_barrier();
 #ifdef KSIM_STAMPS
   uint64_t t_prev = __builtin_amdgcn_s_memtime();
+  uint64_t tb_prev = t_prev, bw_busy = 0, bw_wait = 0;
 #endif
 
   int64_t last = a.first;  // last pod iterated
@@ -749,7 +750,18 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       // the barrier: from the next pod on the owner may read that row (load_frow_l2)
       if (STREAM && prow >= 0 && wv == 1 + (prow % RT) / 64) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
+#ifdef KSIM_STAMPS
+    const uint64_t tb0 = __builtin_amdgcn_s_memtime();
+#endif
     lds_barrier();
+#ifdef KSIM_STAMPS
+    {  // per wave: time from the last main barrier to this one (busy) and the wait in it
+      const uint64_t tb1 = __builtin_amdgcn_s_memtime();
+      bw_busy += tb0 - tb_prev;
+      bw_wait += tb1 - tb0;
+      tb_prev = tb1;
+    }
+#endif
     STAMP(7);
     const int mode = s_mode[pb];
     if (mode < 0) {  // uniform: every workgroup reaches the same verdict
@@ -881,6 +893,10 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
     *a.cursor = stop_at;
   }
 #ifdef KSIM_STAMPS
+  if (me == 0 && lane == 0) {
+    atomicAdd((unsigned long long*)&a.dbg[32 + wv], bw_busy);
+    atomicAdd((unsigned long long*)&a.dbg[40 + wv], bw_wait);
+  }
   if (me == 0 && tid == 0)
     for (int k = 0; k < 16; ++k) a.dbg[k] += (k == 5 || (k >= 8 && k <= 11)) ? 0 : st_acc[k];
   if (me == 0 && tid == 64)

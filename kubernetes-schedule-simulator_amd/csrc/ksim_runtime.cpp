@@ -618,10 +618,13 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
 #ifdef KSIM_STAMPS
   {
-    uint64_t d[32];
+    uint64_t d[64];
     HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
     HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
     const double nf = (double)(d[21] ? d[21] : 1);
+    fprintf(stderr, "[ksim stamps] pfast workgroup 0, per wave (0 = control) cycles/pod between main barriers busy/wait:");
+    for (int w = 0; w < 8; ++w) fprintf(stderr, " %d:%.0f/%.0f", w, d[32 + w] / (double)count, d[40 + w] / (double)count);
+    fprintf(stderr, "\n");
     fprintf(stderr, "[ksim stamps] pfast pods=%lld (%.3f ms) cycles/pod: sweep %.0f fix-wait %.0f decide %.0f owner %.0f barrier %.0f "
             "tail %.0f row-eval %.0f; consecutive owners %.3f\n",
             (long long)count, ms, d[2] / (double)count, d[12] / (double)count, d[3] / (double)count, d[6] / (double)count,
