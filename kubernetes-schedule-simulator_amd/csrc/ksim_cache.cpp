@@ -15,6 +15,9 @@
 // the pod over the bus and writes node, fit count, FitError histogram, error word and
 // lastNodeIndex back the same way — one launch and one stream sync per call, no copies.  Node
 // events relayout the table in one kernel (rows stay in name-rank order).
+#include <chrono>
+#include <cstdio>
+
 #include "ksim_handle.h"
 #include "ksim_cache.h"
 
@@ -25,6 +28,34 @@ constexpr size_t STG_CURSOR = 0;
 constexpr size_t STG_RES = 16;
 constexpr size_t STG_POD = STG_RES + ((KSIM_RES_WORDS * 4 + 15) / 16) * 16;
 constexpr size_t STG_PORTS = STG_POD + sizeof(ksim_pod);
+
+// KSIM_CACHE_PROFILE=1 (diagnostic): ksim_schedule_one's host checks + staging, launch calls,
+// stream wait, result handling, in ns, printed at exit
+struct OneProfile {
+  int64_t ns[4] = {0, 0, 0, 0};
+  int64_t calls = 0;
+  ~OneProfile() {
+    if (calls)
+      fprintf(stderr, "[ksim schedule_one profile] %lld calls, us/call: checks+staging %.1f launch %.1f wait %.1f result %.1f\n",
+              (long long)calls, ns[0] / 1e3 / calls, ns[1] / 1e3 / calls, ns[2] / 1e3 / calls, ns[3] / 1e3 / calls);
+  }
+};
+OneProfile g_one_prof;
+bool one_profile() {
+  static const bool on = getenv("KSIM_CACHE_PROFILE") && atoi(getenv("KSIM_CACHE_PROFILE")) != 0;
+  return on;
+}
+int64_t g_one_seen = 0;
+struct OneClock {
+  bool on = one_profile() && g_one_seen++ >= (getenv("KSIM_CACHE_PROFILE_SKIP") ? atoll(getenv("KSIM_CACHE_PROFILE_SKIP")) : 0);
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  void lap(int k) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    g_one_prof.ns[k] += std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count();
+    t = now;
+  }
+};
 
 int ensure_staging(ksim_handle* h, int32_t n_ports, int32_t n_scalars) {
   const size_t need = STG_PORTS + (size_t)n_ports * 8 + (size_t)n_scalars * sizeof(ksim_scalar_req) +
@@ -70,6 +101,15 @@ int stage_pod(ksim_handle* h, const ksim_pod& pod, const uint64_t* ports, const 
   cs->pod_ports = reinterpret_cast<const uint64_t*>(h->stg_dev + STG_PORTS);
   cs->pod_scalars = reinterpret_cast<const ksim_scalar_req*>(h->stg_dev + STG_PORTS + pb);
   cs->cursor = reinterpret_cast<int64_t*>(h->stg_dev + STG_CURSOR);
+  // the pod and its arrays in the kernel arguments (the mapped copy above serves pods with more
+  // host ports than KSIM_ONE_PORTS)
+  cs->one = 0;
+  if (pod.port_cnt <= KSIM_ONE_PORTS && pod.scalar_cnt <= KSIM_MAX_SCALAR) {
+    cs->one = 1;
+    cs->one_pod = p;
+    if (pb) memcpy(cs->one_ports, ports + pod.port_off, pb);
+    if (sb) memcpy(cs->one_scalars, scalars + pod.scalar_off, sb);
+  }
   cs->out_node = h->res_dev + KSIM_RES_NODE;
   cs->out_fit = h->res_dev + KSIM_RES_FIT;
   cs->out_reasons = h->res_dev + KSIM_RES_REASONS;
@@ -299,6 +339,8 @@ extern "C" {
 
 int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports, int32_t n_ports,
                       const ksim_scalar_req* scalars, int32_t n_scalars, int32_t assume, ksim_result* out) {
+  OneClock oc;
+  if (oc.on) g_one_prof.calls += 1;
   int rc = check_ready(h, "ksim_schedule_one");
   if (rc) return rc;
   if (!out) return ksim_fail(h, KSIM_E_INVAL, "ksim_schedule_one: null result");
@@ -319,20 +361,51 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   if ((rc = ksim_rt_ensure_partials(h, grid))) return rc;
   cs.partials = c.partials;
   cs.pmask = c.pmask;
-  cs.fuse_a = 0;  // pass A as its own launch below
+  // InterPodAffinity / SelectorSpread reductions (pass A): fused into the scan behind a grid barrier
+  // when the grid is co-resident (one launch), else their own launch first
+  const bool ipa = ksim_is_aff_host(h, *pod) && (c.w[KSIM_W_INTERPOD_AFFINITY] || c.w[KSIM_W_SELECTOR_SPREAD]) && !c.no_prio;
+  cs.fuse_a = 0;
+  if (ipa && !h->fuse_off) {
+    const char* fz = getenv("KSIM_FUSE_A");
+    if (h->one_fuse_grid != grid) {
+      h->one_fuse_ok = !(fz && fz[0] == '0') && ksim_scan_coresident(npt, 1, grid);
+      h->one_fuse_grid = grid;
+    }
+    cs.fuse_a = h->one_fuse_ok ? 1 : 0;
+  }
+  h->res_host[KSIM_RES_NODE] = INT32_MIN;  // still there after the wait: the fused barrier gave up
   hipError_t e = hipSuccess;
-  if (ksim_is_aff_host(h, *pod) && (c.w[KSIM_W_INTERPOD_AFFINITY] || c.w[KSIM_W_SELECTOR_SPREAD]) && !c.no_prio)
-    e = ksim_launch_ipa_pass(&cs, npt, grid, h->stream);  // InterPodAffinity / SelectorSpread reductions first
+  oc.lap(0);
+  if (ipa && !cs.fuse_a) e = ksim_launch_ipa_pass(&cs, npt, grid, h->stream);
   if (e == hipSuccess) e = ksim_launch_scan(&cs, npt, 1, grid, h->stream);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "scan launch: %s", hipGetErrorString(e));
+  oc.lap(1);
   HIPCHK(h, hipStreamSynchronize(h->stream));  // the result block is host memory: nothing to copy
+  oc.lap(2);
   const int32_t* r = h->res_host;
+  if (cs.fuse_a && r[KSIM_RES_NODE] == INT32_MIN) {
+    // the fused pass-A barrier timed out (blocks not co-resident after all): nothing was decided or
+    // committed.  Re-arm the tickets and pass-A scratch and run this pod with pass A as its own launch.
+    int32_t err = 0;
+    HIPCHK(h, hipMemcpy(&err, c.err, 4, hipMemcpyDeviceToHost));
+    err &= ~64;
+    HIPCHK(h, hipMemcpy(c.err, &err, 4, hipMemcpyHostToDevice));
+    HIPCHK(h, hipMemset(c.ticket, 0, 16));
+    HIPCHK(h, hipMemset(h->aff_h.ticket, 0, 16));
+    if (h->aff_h.n_zone) HIPCHK(h, hipMemset(h->aff_h.zsum, 0, (size_t)h->aff_h.n_zone * 8));
+    h->fuse_off = true;
+    return ksim_schedule_one(h, pod, ports, n_ports, scalars, n_scalars, assume, out);
+  }
   memset(out, 0, sizeof *out);
   out->node = r[KSIM_RES_NODE];
   out->fit_nodes = r[KSIM_RES_FIT];
   memcpy(&out->last_node_index, r + KSIM_RES_CTR, 8);
   if (out->node < 0) memcpy(out->reasons, r + KSIM_RES_REASONS, sizeof out->reasons);
-  if (assume && out->node >= 0) return after_commit(h, pod->port_cnt);
+  if (assume && out->node >= 0) {
+    rc = after_commit(h, pod->port_cnt);
+    oc.lap(3);
+    return rc;
+  }
   if (r[KSIM_RES_ERR]) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", r[KSIM_RES_ERR]);
   return KSIM_OK;
 }

@@ -93,6 +93,7 @@ struct KsimVol {
 #define KSIM_RES_REASONS 4
 #define KSIM_RES_CTR (KSIM_RES_REASONS + KSIM_NREASONS)  /* uint64 lastNodeIndex after the call */
 #define KSIM_RES_WORDS (KSIM_RES_CTR + 2)
+#define KSIM_ONE_PORTS 16  // host ports a per-pod launch carries in its kernel arguments
 
 struct KsimCtx {
   // ---- node table (name-rank order) ----
@@ -160,7 +161,22 @@ struct KsimCtx {
   int32_t* out_fit;       // optional (per-pod drop-in): [0] = len(filtered), [1] |= ksim_row_status
   const KsimAff* aff;     // inter-pod affinity tables (device), null when none are loaded
   const KsimVol* vol;     // volume tables (device), null when none are loaded
+  // per-pod launches (ksim_schedule_one): the pod and its arrays travel in the kernel arguments,
+  // so no read of host memory or of a staging copy sits on the kernel's critical path
+  int32_t one;            // 1: the pod is one_pod (index first), its ports / scalars one_ports / one_scalars
+  int32_t one_pad;
+  ksim_pod one_pod;
+  uint64_t one_ports[KSIM_ONE_PORTS];
+  ksim_scalar_req one_scalars[KSIM_MAX_SCALAR];
 };
+
+// The pod of a launch and its arrays (KsimCtx::one: the kernel arguments).
+__device__ __forceinline__ uint64_t ksim_pod_port(const KsimCtx& c, const ksim_pod& P, int32_t k) {
+  return c.one ? c.one_ports[k] : c.pod_ports[P.port_off + k];
+}
+__device__ __forceinline__ ksim_scalar_req ksim_pod_scalar(const KsimCtx& c, const ksim_pod& P, int32_t s) {
+  return c.one ? c.one_scalars[s] : c.pod_scalars[P.scalar_off + s];
+}
 
 // Node-sharded mode (ksim_shard_*): this rank's place in the world and every rank's exchange
 // buffer as mapped on this device.
@@ -288,7 +304,7 @@ __device__ __forceinline__ uint32_t ksim_resources(const KsimCtx& c, const ksim_
     m |= 1u << KSIM_R_INSUFFICIENT_EPHEMERAL;
   }
   for (int32_t s = 0; s < P.scalar_cnt; ++s) {
-    const ksim_scalar_req q = c.pod_scalars[P.scalar_off + s];
+    const ksim_scalar_req q = ksim_pod_scalar(c, P, s);
     const int64_t off = (int64_t)q.col * c.n + i;
     if (c.alloc_scalar[off] < q.req + c.req_scalar[off]) m |= 1u << (KSIM_R_INSUFFICIENT_SCALAR0 + q.col);
   }
@@ -316,7 +332,7 @@ struct KsimGlobalAcc {
   }
   __device__ __forceinline__ bool port_conflict(int64_t i, uint64_t want) const { return ksim_port_conflict(c, i, want); }
   // k-th host-port key the pod wants
-  __device__ __forceinline__ uint64_t want(const ksim_pod& P, int32_t k) const { return c.pod_ports[P.port_off + k]; }
+  __device__ __forceinline__ uint64_t want(const ksim_pod& P, int32_t k) const { return ksim_pod_port(c, P, k); }
   __device__ __forceinline__ int tt_class(const ksim_pod& P, int64_t i) const {
     return c.tt_class[(int64_t)P.cls * c.n_taint_sets + c.taint_set[i]];
   }
@@ -715,11 +731,11 @@ __device__ __forceinline__ void ksim_commit(const KsimCtx& c, const ksim_pod& P,
   if (c.alloc_eph[w] < e) fl |= KSIM_N_EPH_OVER;
   c.flags[w] = fl;
   for (int32_t s = 0; s < P.scalar_cnt; ++s) {
-    const ksim_scalar_req q = c.pod_scalars[P.scalar_off + s];
+    const ksim_scalar_req q = ksim_pod_scalar(c, P, s);
     c.req_scalar[(int64_t)q.col * c.n + w] += q.add;
   }
   for (int32_t k = 0; k < P.port_cnt; ++k) {
-    const uint64_t key = c.pod_ports[P.port_off + k];
+    const uint64_t key = ksim_pod_port(c, P, k);
     int32_t cnt = c.port_count[w];
     bool dup = false;
     for (int32_t s = 0; s < cnt; ++s)
@@ -737,6 +753,63 @@ __device__ __forceinline__ int32_t ksim_row_status(const KsimCtx& c, int64_t w) 
   const int64_t lim = int64_t(1) << 48;
   const int64_t a = c.req_cpu[w], b = c.req_mem[w], d = c.nz_cpu[w], e = c.nz_mem[w];
   return (a < 0 || a >= lim || b < 0 || b >= lim || d < 0 || d >= lim || e < 0 || e >= lim) ? 1 : 0;
+}
+
+// ksim_commit by one wave (lane = 0..63, every lane calls): lane 0 updates the row's columns and
+// returns ksim_row_status of the committed values; the host-port dedup reads the row's port slots
+// in parallel (one lane a slot) instead of one dependent load per slot.
+__device__ __forceinline__ int32_t ksim_commit_wave(const KsimCtx& c, const ksim_pod& P, int64_t w, int lane) {
+  int32_t st = 0;
+  if (lane == 0) {
+    const int64_t rc = c.req_cpu[w] + P.add_cpu, rm = c.req_mem[w] + P.add_mem;
+    const int64_t g = c.req_gpu[w] + P.add_gpu, e = c.req_eph[w] + P.add_eph;
+    const int64_t zc = c.nz_cpu[w] + P.nz_cpu, zm = c.nz_mem[w] + P.nz_mem;
+    const int32_t pc = c.pod_count[w] + 1;
+    uint32_t fl = c.flags[w] & ~(KSIM_N_GPU_OVER | KSIM_N_EPH_OVER);
+    if (c.alloc_gpu[w] < g) fl |= KSIM_N_GPU_OVER;
+    if (c.alloc_eph[w] < e) fl |= KSIM_N_EPH_OVER;
+    c.req_cpu[w] = rc; c.req_mem[w] = rm; c.req_gpu[w] = g; c.req_eph[w] = e;
+    c.nz_cpu[w] = zc; c.nz_mem[w] = zm; c.pod_count[w] = pc; c.flags[w] = fl;
+    for (int32_t s = 0; s < P.scalar_cnt; ++s) {
+      const ksim_scalar_req q = ksim_pod_scalar(c, P, s);
+      c.req_scalar[(int64_t)q.col * c.n + w] += q.add;
+    }
+    const int64_t lim = int64_t(1) << 48;
+    st = (rc < 0 || rc >= lim || rm < 0 || rm >= lim || zc < 0 || zc >= lim || zm < 0 || zm >= lim) ? 1 : 0;
+  }
+  if (P.port_cnt == 0) return st;
+  if (c.port_slots > 64) {  // wider than a wave: the serial form
+    if (lane == 0) {
+      for (int32_t k = 0; k < P.port_cnt; ++k) {
+        const uint64_t key = ksim_pod_port(c, P, k);
+        int32_t cnt = c.port_count[w];
+        bool dup = false;
+        for (int32_t s = 0; s < cnt; ++s)
+          if (c.ports[(int64_t)s * c.n + w] == key) { dup = true; break; }
+        if (dup) continue;
+        if (cnt >= c.port_slots) { atomicOr(c.err, 1); continue; }
+        c.ports[(int64_t)cnt * c.n + w] = key;
+        c.port_count[w] = cnt + 1;
+      }
+    }
+    return st;
+  }
+  const int32_t cnt0 = c.port_count[w];
+  uint64_t mine = lane < cnt0 ? c.ports[(int64_t)lane * c.n + w] : 0ull;
+  int32_t cnt = cnt0;
+  for (int32_t k = 0; k < P.port_cnt; ++k) {  // uniform: the pod's keys in order
+    const uint64_t key = ksim_pod_port(c, P, k);
+    if (__ballot(lane < cnt && mine == key)) continue;
+    if (cnt >= c.port_slots) {
+      if (lane == 0) atomicOr(c.err, 1);
+      continue;
+    }
+    if (lane == cnt) mine = key;
+    if (lane == 0) c.ports[(int64_t)cnt * c.n + w] = key;
+    ++cnt;
+  }
+  if (lane == 0 && cnt != cnt0) c.port_count[w] = cnt;
+  return st;
 }
 
 // Remove pod P from node w: NodeInfo.RemovePod (node_info.go:343-390) — the containers-only
@@ -758,11 +831,11 @@ __device__ __forceinline__ void ksim_uncommit(const KsimCtx& c, const ksim_pod& 
   if (c.alloc_eph[w] < e) fl |= KSIM_N_EPH_OVER;
   c.flags[w] = fl;
   for (int32_t s = 0; s < P.scalar_cnt; ++s) {
-    const ksim_scalar_req q = c.pod_scalars[P.scalar_off + s];
+    const ksim_scalar_req q = ksim_pod_scalar(c, P, s);
     c.req_scalar[(int64_t)q.col * c.n + w] -= q.add;
   }
   for (int32_t k = 0; k < P.port_cnt; ++k) {
-    const uint64_t key = c.pod_ports[P.port_off + k];
+    const uint64_t key = ksim_pod_port(c, P, k);
     const int32_t cnt = c.port_count[w];
     for (int32_t s = 0; s < cnt; ++s) {
       if (c.ports[(int64_t)s * c.n + w] != key) continue;

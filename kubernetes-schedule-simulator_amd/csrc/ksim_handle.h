@@ -167,6 +167,8 @@ struct ksim_handle {
   char* pg_rec = nullptr;                  // pod-context records of the current call
   size_t pg_rec_bytes = 0;
   bool fuse_off = false;        // a fused pass-A barrier timed out once: pass A as its own launch
+  int one_fuse_grid = -1;       // ksim_schedule_one: the grid whose co-residency was checked ...
+  bool one_fuse_ok = false;     // ... and whether the fused pass A may run on it
   bool pgen_off = false;        // a general persistent kernel ran out of a spin bound once: the launch form
   std::vector<void*> aff_bufs;
   std::vector<int32_t> q_ident, q_aclass;
@@ -180,7 +182,12 @@ struct ksim_handle {
   int32_t vol_n_keys = 0;
   KsimVol vol_h{};
   KsimVol* vol_dev = nullptr;
-  std::vector<void*> vol_bufs;
+  std::vector<void*> vol_bufs;  // the mounts (slots, slot_count) of the current tables
+  // the small volume tables (KsimVol at offset 0, then key / class / ref / zone arrays) in one
+  // persistent device buffer grown geometrically, so that ksim_grow_volumes is one upload
+  char* vol_small = nullptr;
+  size_t vol_small_cap = 0;
+  std::vector<char> vol_small_host;
   std::vector<int32_t> q_vclass;
   std::vector<int64_t> vol_pre;  // vol_pre[i] = volume / service-affinity pods among the first i queued
 };

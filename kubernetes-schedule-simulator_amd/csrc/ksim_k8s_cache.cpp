@@ -14,6 +14,8 @@
 //    tables reloaded only when it grows by something the device must hold or after a node event;
 //  - volumes: the device keeps every node's mounts; new keys / classes grow the small tables
 //    (ksim_grow_volumes), a node event reloads them with the host's mount view.
+#include <chrono>
+#include <cstdio>
 #include <memory>
 
 #include "ksim_k8s_sem.h"
@@ -79,6 +81,12 @@ struct ksim_k8s_cache {
   int32_t vol_zone_words = 0;
   bool vol_zone_err = false;
   int64_t stats[4] = {0, 0, 0, 0};   // affinity loads, volume loads, volume grows, class loads
+  // KSIM_CACHE_PROFILE=1 (diagnostic): ns per Schedule phase — encode, volume errors, volume sync,
+  // affinity sync, ksim_schedule_one, bookkeeping; [6] calls — printed by ksim_k8s_cache_destroy
+  int64_t prof[7] = {0, 0, 0, 0, 0, 0, 0};
+  int64_t prof_seen = 0;              // Schedule calls so far (KSIM_CACHE_PROFILE_SKIP: untimed head)
+  size_t zoned_upto = 0;              // label sets scanned for zone / region labels
+  bool zoned = false;
 };
 
 namespace {
@@ -217,9 +225,12 @@ void sync_volumes(Cache* c, bool need, const Enc* e) {
 // return the predicate's error and scheduleOne would requeue the pod.
 void check_volume_errors(Cache* c, const PodObj& p) {
   VolumeIndex& vi = c->vidx;
-  bool zoned = false;
-  for (const LabelSetKey& ls : c->in.label_sets.items)
-    zoned |= ls.labels.count(ZONE_LABEL) || ls.labels.count(REGION_LABEL);
+  // some label set carries a zone / region label (label sets are only ever added: scan the new ones)
+  for (; c->zoned_upto < c->in.label_sets.items.size(); ++c->zoned_upto) {
+    const Labels& l = c->in.label_sets.items[c->zoned_upto].labels;
+    c->zoned |= l.count(ZONE_LABEL) || l.count(REGION_LABEL);
+  }
+  const bool zoned = c->zoned;
   bool claim = false, zone = false, binding = false;
   for (const Volume& v : p.vols) {
     if (v.kind != KSIM_K8S_VOL_PVC) continue;
@@ -449,11 +460,42 @@ void remove(Cache* c, const PodObj& p) {
   if (it->second.pods.empty() && !it->second.has_node) c->infos.erase(it);
 }
 
+bool cache_profile() {
+  static const bool on = getenv("KSIM_CACHE_PROFILE") && atoi(getenv("KSIM_CACHE_PROFILE")) != 0;
+  return on;
+}
+
+int64_t profile_skip() {
+  static const int64_t k = getenv("KSIM_CACHE_PROFILE_SKIP") ? atoll(getenv("KSIM_CACHE_PROFILE_SKIP")) : 0;
+  return k;
+}
+
+struct PhaseClock {
+  Cache* c;
+  bool on;
+  std::chrono::steady_clock::time_point t;
+  explicit PhaseClock(Cache* cc) : c(cc), on(cache_profile() && cc->prof_seen++ >= profile_skip()) {
+    if (on) t = std::chrono::steady_clock::now();
+  }
+  void lap(int k) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    c->prof[k] += std::chrono::duration_cast<std::chrono::nanoseconds>(now - t).count();
+    t = now;
+  }
+};
+
 void schedule(Cache* c, const PodObj& p, int32_t assume, ksim_result* out) {
+  PhaseClock pc(c);
+  if (pc.on) c->prof[6] += 1;
   Enc e = encode(c, p);
+  pc.lap(0);
   if (has_pred_volumes(p)) check_volume_errors(c, p);
+  pc.lap(1);
   sync_volumes(c, e.row.vol_class != 0, &e);
+  pc.lap(2);
   sync_affinity(c, &e, p);
+  pc.lap(3);
   const Str key = pod_key(p);
   // Scheduler.assume runs after Schedule: a pod already in the cache is decided (lastNodeIndex moves)
   // and then refused by AssumePod
@@ -461,6 +503,7 @@ void schedule(Cache* c, const PodObj& p, int32_t assume, ksim_result* out) {
   const uint64_t* pp; const ksim_scalar_req* sp; int32_t np, ns;
   pod_args(e, &pp, &np, &sp, &ns);
   const int rc = ksim_schedule_one(c->h, &e.row, pp, np, sp, ns, assume && !dup ? KSIM_SCHEDULE_ASSUME : KSIM_SCHEDULE_ONLY, out);
+  pc.lap(4);
   if (rc == KSIM_E_NO_NODES) fail(rc, "no nodes available to schedule pods");
   check(c, rc, "ksim_schedule_one");
   if (out->node < 0 || !assume) return;
@@ -475,6 +518,7 @@ void schedule(Cache* c, const PodObj& p, int32_t assume, ksim_result* out) {
   info.pods[key] = PodRec{a, std::move(e)};
   c->pod_states[key] = a;
   c->assumed.insert(key);
+  pc.lap(5);
 }
 
 }  // namespace
@@ -523,6 +567,11 @@ extern "C" int ksim_k8s_cache_create(const ksim_k8s_cache_options* opt, ksim_k8s
 
 extern "C" void ksim_k8s_cache_destroy(ksim_k8s_cache* c) {
   if (!c) return;
+  if (cache_profile() && c->prof[6])
+    fprintf(stderr, "[ksim cache profile] %lld Schedule calls, us/call: encode %.1f volume-errors %.1f volume-sync %.1f "
+            "affinity-sync %.1f schedule_one %.1f bookkeeping %.1f\n", (long long)c->prof[6], c->prof[0] / 1e3 / c->prof[6],
+            c->prof[1] / 1e3 / c->prof[6], c->prof[2] / 1e3 / c->prof[6], c->prof[3] / 1e3 / c->prof[6],
+            c->prof[4] / 1e3 / c->prof[6], c->prof[5] / 1e3 / c->prof[6]);
   if (c->h) ksim_destroy(c->h);
   delete c;
 }

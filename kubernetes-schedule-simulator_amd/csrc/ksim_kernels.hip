@@ -245,9 +245,9 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
   __shared__ int64_t s_v[4][KSIM_WAVES];
   __shared__ unsigned long long s_z[KSIM_PASS_ZONES];  // block-local zone sums (few zones: no global contention)
   __shared__ int s_last;
-  const int64_t pod = *c.cursor;
+  const int64_t pod = c.one ? c.first : *c.cursor;
   if (pod >= c.end || !c.aff || c.no_prio) return;
-  const ksim_pod P = c.pods[pod];
+  const ksim_pod P = c.one ? c.one_pod : c.pods[pod];
   const KsimAff& A = *c.aff;
   const bool ipa = c.w[KSIM_W_INTERPOD_AFFINITY] != 0 && ksim_interpod_prio_work(A, P);
   const int32_t sp = c.w[KSIM_W_SELECTOR_SPREAD] != 0 ? ksim_spread_pair(A, P) : -1;
@@ -273,6 +273,25 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
   (void)passa_reduce<NPT>(c, ipa, sp, fit, raw, cnt, zz, s_v, s_z, &s_last);
 }
 
+// diagnostic builds (make stamps): thread 0's cycles per scan phase, summed over blocks into
+// dbg[48..58] (every block: 48 pod read, 49 evaluation, 50 candidate masks + statistics, 51 partial
+// + ticket; the last block: 52 combine, 53 decide, 54 locate, 55 masks + pick, 56 commit,
+// 57 results), dbg[60] blocks, dbg[61] last blocks; printed by ksim_destroy
+#ifdef KSIM_STAMPS
+#define SSTAMP(k)                                                                          \
+  do {                                                                                     \
+    if (tid == 0) {                                                                        \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();                                   \
+      atomicAdd((unsigned long long*)&c.dbg[48 + (k)], (unsigned long long)(t_ - ts_prev)); \
+      ts_prev = t_;                                                                        \
+    }                                                                                      \
+  } while (0)
+#else
+#define SSTAMP(k) \
+  do {            \
+  } while (0)
+#endif
+
 template <int NPT, bool COLLECT>
 __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   __shared__ int64_t s_mx[KSIM_WAVES][KSIM_MAX_RCLASS];
@@ -287,9 +306,19 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   __shared__ unsigned long long s_z[KSIM_PASS_ZONES];
   __shared__ uint32_t s_gen;
   __shared__ int s_bail;
+  __shared__ uint64_t s_ctr;
+  __shared__ int64_t s_tv[KSIM_MAX_RCLASS], s_av[KSIM_MAX_RCLASS], s_ad[KSIM_MAX_RCLASS];
+  // last block, single reduce class: every block's (fit, max, count) as combined, for the locate step
+  constexpr int LOC_MAX = 1024;
+  __shared__ int64_t s_bmx[LOC_MAX];
+  __shared__ int32_t s_bcnt[LOC_MAX], s_bfit[LOC_MAX];
   static_assert(NPT <= KSIM_PM_NPT, "candidate masks hold KSIM_PM_NPT node slots per thread");
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+#ifdef KSIM_STAMPS
+  uint64_t ts_prev = __builtin_amdgcn_s_memtime();
+  if (tid == 0) atomicAdd((unsigned long long*)&c.dbg[60], 1ull);
+#endif
   if (c.fuse_a) {
     // a fused barrier that timed out (err bit 64) left this run's tickets mid-pod: every later
     // launch of the graph exits at once (uniformly per block) and the host resumes unfused
@@ -297,12 +326,22 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     __syncthreads();
     if (s_bail) return;
   }
-  const int64_t pod = *c.cursor;
+  const int64_t pod = c.one ? c.first : *c.cursor;
   if (pod >= c.end) return;  // uniform: graph replay past the end of the queue
-  const ksim_pod P = c.pods[pod];
-  const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
-  const int k2 = c.use_na ? c.n_na[P.cls] : 1;
+  const ksim_pod P = c.one ? c.one_pod : c.pods[pod];
+  // per-pod launches carry the class's reduce-class counts in the descriptor (stage_pod)
+  const int k1 = c.one ? P.reserved[0] : (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
+  const int k2 = c.one ? P.reserved[1] : c.use_na ? c.n_na[P.cls] : 1;
   const int K = k1 * k2;
+  // what the last block's decision reads, fetched now while the chunk is evaluated: the counter
+  // (kernels of a stream run one after another, so its value is final) and the pod's per-class
+  // TaintToleration / NodeAffinity values and NodePreferAvoidPods addends
+  if (tid == 0) s_ctr = *c.counter;
+  if (tid < K) {
+    s_tv[tid] = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid / k2];
+    s_av[tid] = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2];
+    s_ad[tid] = c.na_add ? c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2] : 0;
+  }
   const int64_t base = (int64_t)blockIdx.x * c.chunk;
   IpaNorm ipa = ipa_norm(c, P);
   // fused pass A (KsimCtx::fuse_a, grid co-resident): this pod's pass-A reductions run over the
@@ -321,6 +360,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   }
 
   if (COLLECT && tid < KSIM_NREASONS) s_hist[tid] = 0;
+  SSTAMP(0);
 
   // ---------------- phase 1: evaluate this block's chunk ----------------
   bool fit[NPT];
@@ -385,6 +425,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     }
   }
 
+  SSTAMP(1);
   // candidate masks: write-through (sc1) stores, drained by every storing wave before the barrier
   // that precedes the ticket, read back with sc1 loads by the last block
   uint64_t* pm = c.pmask + (int64_t)blockIdx.x * KSIM_PM_STRIDE;
@@ -432,6 +473,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  SSTAMP(2);
 
   // ---------------- publish the partial, take a ticket ----------------
   if (tid == 0) {
@@ -458,9 +500,13 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     s_last = (old == gridDim.x - 1);
   }
   __syncthreads();
+  SSTAMP(3);
   if (!s_last) return;
 
   // ---------------- last block: the global decision ----------------
+#ifdef KSIM_STAMPS
+  if (tid == 0) atomicAdd((unsigned long long*)&c.dbg[61], 1ull);
+#endif
   if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -472,9 +518,15 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   int32_t lf = 0;
 #pragma unroll
   for (int q = 0; q < KSIM_MAX_RCLASS; ++q) { lm[q] = INT64_MIN; ln[q] = 0; }
+  const bool loc_lds = K == 1 && G <= LOC_MAX;
   for (int b = tid; b < G; b += KSIM_BLOCK) {
     const KsimPartial* p = &c.partials[b];
     lf += p->fit;
+    if (loc_lds) {
+      s_bfit[b] = p->fit;
+      s_bcnt[b] = p->cnt[0];
+      s_bmx[b] = p->mx[0];
+    }
 #pragma unroll
     for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
       if (q >= K) break;
@@ -495,6 +547,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     if (lane == 0) { s_mx[wv][q] = wm; s_cnt[wv][q] = wn; }
   }
   __syncthreads();
+  SSTAMP(4);
 
   if (tid == 0) {
     D.pod = pod;
@@ -530,8 +583,8 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       int64_t mxT = 0, mxA = 0;
       for (int q = 0; q < K; ++q) {
         if (Cq[q] == 0) continue;
-        const int64_t tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2];
-        const int64_t av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];
+        const int64_t tv = s_tv[q];
+        const int64_t av = s_av[q];
         if (k1 > 1 || c.w[KSIM_W_TAINT_TOLERATION]) mxT = tv > mxT ? tv : mxT;
         if (k2 > 1 || c.w[KSIM_W_NODE_AFFINITY]) mxA = av > mxA ? av : mxA;
       }
@@ -540,15 +593,9 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       for (int q = 0; q < K; ++q) {
         if (Cq[q] == 0) continue;
         uint64_t t = (uint64_t)Mq[q];
-        if (c.w[KSIM_W_TAINT_TOLERATION]) {
-          const int64_t tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q / k2];
-          t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(tv, mxT, true);
-        }
-        if (c.w[KSIM_W_NODE_AFFINITY]) {
-          const int64_t av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];
-          t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(av, mxA, false);
-        }
-        if (c.na_add) t += (uint64_t)c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + q % k2];  // NodePreferAvoidPods
+        if (c.w[KSIM_W_TAINT_TOLERATION]) t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(s_tv[q], mxT, true);
+        if (c.w[KSIM_W_NODE_AFFINITY]) t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(s_av[q], mxA, false);
+        t += (uint64_t)s_ad[q];  // NodePreferAvoidPods (0 without the addends)
         tot[q] = (int64_t)t;
         if (tot[q] > best) best = tot[q];
       }
@@ -558,12 +605,14 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
         if (Cq[q] && tot[q] == best) { win |= 1u << q; C += Cq[q]; }
       D.winners = win;
       for (int q = 0; q < K; ++q) D.M[q] = Mq[q];
-      const uint64_t li = *c.counter;           // generic_scheduler.go:192-195
+      const uint64_t li = s_ctr;                // generic_scheduler.go:192-195
       D.ix = (int64_t)(li % (uint64_t)C);
       *c.counter = li + 1;
+      s_ctr = li + 1;
     }
   }
   __syncthreads();
+  SSTAMP(5);
 
   if (D.mode == 0) {
     if (COLLECT && c.out_reasons) {
@@ -582,34 +631,30 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     const int64_t per = (G + KSIM_BLOCK - 1) / KSIM_BLOCK;
     const int tr = KSIM_BLOCK - 1 - tid;  // reversed: thread 0 owns the highest blocks
     const int64_t b0 = (int64_t)tr * per, b1 = (b0 + per < G) ? b0 + per : G;
-    int64_t s = 0;
-    for (int64_t b = b0; b < b1; ++b) {
+    // matches in block b (the partials kept in LDS by the combine step when K == 1)
+    auto matches = [&](int64_t b) -> int64_t {
+      if (loc_lds) return D.mode == 1 ? s_bfit[b] : ((s_bcnt[b] && s_bmx[b] == D.M[0]) ? s_bcnt[b] : 0);
       const KsimPartial* p = &c.partials[b];
-      if (D.mode == 1) {
-        s += p->fit;
-      } else {
-        for (int q = 0; q < K; ++q)
-          if (((D.winners >> q) & 1u) && p->cnt[q] && p->mx[q] == D.M[q]) s += p->cnt[q];
-      }
-    }
+      if (D.mode == 1) return p->fit;
+      int64_t cb = 0;
+      for (int q = 0; q < K; ++q)
+        if (((D.winners >> q) & 1u) && p->cnt[q] && p->mx[q] == D.M[q]) cb += p->cnt[q];
+      return cb;
+    };
+    int64_t s = 0;
+    for (int64_t b = b0; b < b1; ++b) s += matches(b);
     const int64_t incl = block_incl_scan(s, s_scan);
     const int64_t above = incl - s;
     if (s > 0 && D.ix >= above && D.ix < incl) {
       int64_t r = D.ix - above;
       for (int64_t b = b1 - 1; b >= b0; --b) {
-        const KsimPartial* p = &c.partials[b];
-        int64_t cb = 0;
-        if (D.mode == 1) {
-          cb = p->fit;
-        } else {
-          for (int q = 0; q < K; ++q)
-            if (((D.winners >> q) & 1u) && p->cnt[q] && p->mx[q] == D.M[q]) cb += p->cnt[q];
-        }
+        const int64_t cb = matches(b);
         if (r < cb) { D.blk = b; D.rank = r; break; }
         r -= cb;
       }
     }
     __syncthreads();
+    SSTAMP(6);
     if (D.blk < 0) {  // inconsistent partials: must never happen
       if (tid == 0) { atomicOr(c.err, 2); c.out_node[pod] = -1; *c.cursor = pod + 1; *c.ticket = 0; }
       return;
@@ -651,30 +696,35 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       D.node = node;
     }
     __syncthreads();
+    SSTAMP(7);
     // commit: the row and volumes in thread 0, the affinity counts across wave 1 meanwhile
     if (D.node >= 0 && !c.no_commit) {
-      if (tid == 0) {
-        ksim_commit(c, P, D.node);
-        if (ksim_is_vol_pod(c, P)) ksim_vol_commit(*c.vol, P, D.node, 1, c.err);
-        if (c.out_fit) c.out_fit[1] |= ksim_row_status(c, D.node);
+      if (wv == 0) {
+        const int32_t st = ksim_commit_wave(c, P, D.node, lane);
+        if (tid == 0) {
+          if (ksim_is_vol_pod(c, P)) ksim_vol_commit(*c.vol, P, D.node, 1, c.err);
+          if (c.out_fit) c.out_fit[1] |= st;
+        }
       } else if (wv == 1 && ksim_is_aff_pod(c, P)) {
         ksim_aff_commit(*c.aff, P, D.node, 1, lane, 64);
       }
     }
   }
   if (c.out_fit) __syncthreads();  // (uniform) wave 1's affinity commit is done
+  SSTAMP(8);
   if (tid == 0) {
     c.out_node[pod] = (int32_t)D.node;
     if (c.out_fit) {  // per-pod drop-in: fit count, error word and lastNodeIndex into the result block
       c.out_fit[0] = D.fitTotal;
       c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t ctr = *c.counter;
+      const uint64_t ctr = s_ctr;
       c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT] = (int32_t)(uint32_t)ctr;
       c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1] = (int32_t)(uint32_t)(ctr >> 32);
     }
-    *c.cursor = pod + 1;
+    if (!c.one) *c.cursor = pod + 1;
     *c.ticket = 0;
   }
+  SSTAMP(9);
 }
 
 // Per-node evaluation of one pod without commit (ksim_evaluate).
@@ -682,7 +732,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_
                                                              int64_t* score, uint8_t* rcls) {
   const int64_t i = (int64_t)blockIdx.x * KSIM_BLOCK + threadIdx.x;
   if (i >= c.n) return;
-  const ksim_pod P = c.pods[pod];
+  const ksim_pod P = c.one ? c.one_pod : c.pods[pod];
   const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
   const int k2 = c.use_na ? c.n_na[P.cls] : 1;
   const KsimRow r = ksim_load_row(c, i);
@@ -697,12 +747,13 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_
 // status[0] |= ksim_row_status, status[1] = the error word afterwards (KSIM_RES_STATUS / _ERR).
 __global__ void ksim_assume_kernel(KsimCtx c, int64_t pod, int64_t node, int32_t* status) {
   if (blockIdx.x != 0 || threadIdx.x >= 64) return;
+  const ksim_pod P = c.one ? c.one_pod : c.pods[pod];
+  const int32_t st = ksim_commit_wave(c, P, node, threadIdx.x);
   if (threadIdx.x == 0) {
-    ksim_commit(c, c.pods[pod], node);
-    if (ksim_is_vol_pod(c, c.pods[pod])) ksim_vol_commit(*c.vol, c.pods[pod], node, 1, c.err);
-    *status |= ksim_row_status(c, node);
+    if (ksim_is_vol_pod(c, P)) ksim_vol_commit(*c.vol, P, node, 1, c.err);
+    *status |= st;
   }
-  if (ksim_is_aff_pod(c, c.pods[pod])) ksim_aff_commit(*c.aff, c.pods[pod], node, 1, threadIdx.x, 64);
+  if (ksim_is_aff_pod(c, P)) ksim_aff_commit(*c.aff, P, node, 1, threadIdx.x, 64);
   __syncthreads();
   if (threadIdx.x == 0) status[KSIM_RES_ERR - KSIM_RES_STATUS] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

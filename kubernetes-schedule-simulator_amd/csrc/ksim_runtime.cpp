@@ -80,6 +80,18 @@ void ksim_destroy(ksim_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+#ifdef KSIM_STAMPS
+  if (h->ctx.dbg) {  // the scan kernel's phase stamps (ksim_kernels.hip SSTAMP)
+    uint64_t d[64];
+    if (hipMemcpy(d, h->ctx.dbg, sizeof d, hipMemcpyDeviceToHost) == hipSuccess && d[61]) {
+      const double nb = (double)(d[60] ? d[60] : 1), nl = (double)d[61];
+      fprintf(stderr, "[ksim stamps] scan: %llu launches (%llu blocks), thread-0 cycles per block: pod %.0f eval %.0f "
+              "masks+stats %.0f partial+ticket %.0f; last block: combine %.0f decide %.0f locate %.0f pick %.0f commit %.0f "
+              "results %.0f\n", (unsigned long long)d[61], (unsigned long long)d[60], d[48] / nb, d[49] / nb, d[50] / nb,
+              d[51] / nb, d[52] / nl, d[53] / nl, d[54] / nl, d[55] / nl, d[56] / nl, d[57] / nl);
+    }
+  }
+#endif
   for (void*& m : h->ipc_mapped)
     if (m) { (void)hipIpcCloseMemHandle(m); m = nullptr; }
   if (h->shard.xchg) { (void)hipFree(h->shard.xchg); h->shard.xchg = nullptr; }

@@ -75,20 +75,47 @@ static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
   int rc = validate(h, t, keep);
   if (rc) return rc;
   const int64_t n = h->ctx.n;
-  const size_t nb0 = h->bufs.size();
+  // the small tables, packed: [KsimVol][key_filter][vc][vc_filter][refs][zone_ok], 16-byte aligned
+  size_t off = 0;
+  auto seg = [&](size_t bytes) {
+    const size_t o = off;
+    off = (off + bytes + 15) & ~(size_t)15;
+    return o;
+  };
+  const size_t o_V = seg(sizeof(KsimVol)), o_kf = seg(sizeof(*t->key_filter) * t->n_keys),
+               o_vc = seg(sizeof(*t->vc) * 2 * (size_t)t->n_vclass), o_vf = seg(sizeof(*t->vc_filter) * t->n_vclass),
+               o_refs = seg(sizeof(*t->refs) * t->n_refs),
+               o_zo = seg(t->zone_ok ? sizeof(*t->zone_ok) * (size_t)t->n_vclass * t->zone_words : 0);
+  char* old_small = nullptr;
+  if (off > h->vol_small_cap) {  // grown geometrically: most grows reuse the buffer
+    old_small = h->vol_small;
+    const size_t cap = std::max<size_t>(off * 2, 4096);
+    char* q;
+    if ((rc = dev_alloc(h, &q, cap))) return rc;
+    h->vol_small = q;
+    h->vol_small_cap = cap;
+  }
+  char* base = h->vol_small;
+  std::vector<char>& hb = h->vol_small_host;  // kept until the next load: the upload reads it
+  hb.assign(off, 0);
+  auto put = [&](size_t o, const void* src, size_t bytes) {
+    if (bytes) memcpy(hb.data() + o, src, bytes);
+  };
+  put(o_kf, t->key_filter, sizeof(*t->key_filter) * t->n_keys);
+  put(o_vc, t->vc, sizeof(*t->vc) * 2 * (size_t)t->n_vclass);
+  put(o_vf, t->vc_filter, sizeof(*t->vc_filter) * t->n_vclass);
+  put(o_refs, t->refs, sizeof(*t->refs) * t->n_refs);
+  if (t->zone_ok) put(o_zo, t->zone_ok, sizeof(*t->zone_ok) * (size_t)t->n_vclass * t->zone_words);
   KsimVol V{};
-  uint32_t *kf, *vf, *zo = nullptr;
-  int32_t *vc, *sc;
-  ksim_vol_ref* refs;
   uint64_t* slots;
-  if ((rc = dev_upload(h, &kf, t->key_filter, t->n_keys)) || (rc = dev_upload(h, &vc, t->vc, 2 * (size_t)t->n_vclass)) ||
-      (rc = dev_upload(h, &vf, t->vc_filter, t->n_vclass)) || (rc = dev_upload(h, &refs, t->refs, t->n_refs)))
-    return rc;
+  int32_t* sc;
+  const size_t nb0 = h->bufs.size();
+  const bool carry = keep && t->vol_slots == h->vol_h.vol_slots;  // the mounts stay where they are
   if (!keep) {
     if ((rc = dev_upload(h, &slots, t->slots, (size_t)t->vol_slots * n)) || (rc = dev_upload(h, &sc, t->slot_count, n)))
       return rc;
-  } else if (t->vol_slots == h->vol_h.vol_slots) {
-    slots = h->vol_h.slots;  // the same buffers: carried over below
+  } else if (carry) {
+    slots = h->vol_h.slots;
     sc = h->vol_h.slot_count;
   } else {  // [S][n] → [S'][n]: the first S rows are one contiguous block
     if ((rc = dev_alloc(h, &slots, (size_t)t->vol_slots * n)) || (rc = dev_alloc(h, &sc, (size_t)n))) return rc;
@@ -96,22 +123,29 @@ static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
     HIPCHK(h, hipMemcpyAsync(slots, h->vol_h.slots, (size_t)h->vol_h.vol_slots * n * 8, hipMemcpyDeviceToDevice, h->stream));
     HIPCHK(h, hipMemcpyAsync(sc, h->vol_h.slot_count, (size_t)n * 4, hipMemcpyDeviceToDevice, h->stream));
   }
-  if (t->zone_ok && (rc = dev_upload(h, &zo, t->zone_ok, (size_t)t->n_vclass * t->zone_words))) return rc;
   V.n = n;
-  V.slots = slots; V.slot_count = sc; V.key_filter = kf; V.vc = vc; V.vc_filter = vf; V.refs = refs; V.zone_ok = zo;
+  V.slots = slots; V.slot_count = sc;
+  V.key_filter = reinterpret_cast<const uint32_t*>(base + o_kf);
+  V.vc = reinterpret_cast<const int32_t*>(base + o_vc);
+  V.vc_filter = reinterpret_cast<const uint32_t*>(base + o_vf);
+  V.refs = reinterpret_cast<const ksim_vol_ref*>(base + o_refs);
+  V.zone_ok = t->zone_ok ? reinterpret_cast<const uint32_t*>(base + o_zo) : nullptr;
   for (int k = 0; k < 3; ++k) V.max_vols[k] = t->max_vols[k];
   V.vol_slots = t->vol_slots;
   V.zone_words = t->zone_words;
-  KsimVol* dev;
-  if ((rc = dev_upload(h, &dev, &V, 1))) return rc;
-  HIPCHK(h, hipStreamSynchronize(h->stream));
-  const bool carry = keep && t->vol_slots == h->vol_h.vol_slots;
-  std::vector<void*> fresh;  // this load's buffers (taken before any free shifts h->bufs)
+  put(o_V, &V, sizeof V);
+  HIPCHK(h, hipMemcpyAsync(base, hb.data(), off, hipMemcpyHostToDevice, h->stream));
+  KsimVol* dev = reinterpret_cast<KsimVol*>(base);
+  std::vector<void*> fresh;  // this load's mount buffers (taken before any free shifts h->bufs)
   for (size_t k = nb0; k < h->bufs.size(); ++k) fresh.push_back(h->bufs[k].p);
   if (carry) { fresh.push_back(slots); fresh.push_back(sc); }
-  for (void* q : h->vol_bufs)  // the previous tables (reload), except the mounts carried over
+  const bool frees = old_small || !carry;
+  if (frees) HIPCHK(h, hipStreamSynchronize(h->stream));
+  for (void* q : h->vol_bufs)  // the previous mounts (reload / re-layout), unless carried over
     if (!(carry && (q == (void*)slots || q == (void*)sc))) dev_free(h, q);
+  if (old_small) dev_free(h, old_small);
   h->vol_bufs = fresh;
+  const bool moved = dev != h->vol_dev;
   h->vol_dev = dev;
   h->vol_h = V;
   h->ctx.vol = dev;
@@ -122,8 +156,8 @@ static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
   h->have_vol = true;
   h->vol_stale = false;
   // the table pointer is baked into the launch graph's kernel arguments
-  if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
-  if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
+  if (moved && h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
+  if (moved && h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
   return KSIM_OK;
 }
 
