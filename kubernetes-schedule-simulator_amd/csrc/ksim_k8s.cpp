@@ -62,6 +62,7 @@ struct ksim_k8s_cluster {
   bool pa_use_w = false, opened_aff = false, opened_vol = false, opened_zone = false;
   bool aff_cfg = false, vol_cfg = false;  // the open handle's configuration reads the tables
   int32_t vol_grown_classes = 0;          // volume classes whose zone verdicts the handle holds
+  ZoneGroups zone_groups;                 // label sets by zone / region labels (reset with the interns)
 };
 
 namespace {
@@ -139,7 +140,7 @@ void volume_tables(ksim_k8s_cluster* c) {
   c->vol_zone_words = ((int32_t)c->in.label_sets.items.size() + 31) / 32;
   c->vol_zone_ok.clear();
   c->vol_zone_err = false;
-  vol_zone_verdicts(vi, c->in.label_sets, 0, &c->vol_zone_ok, &c->vol_zone_err);
+  vol_zone_verdicts(vi, c->zone_groups, c->in.label_sets, 0, &c->vol_zone_ok, &c->vol_zone_err);
   if (c->vol_zone_ok.empty()) c->vol_zone_ok.push_back(0);
   c->vol_grown_classes = (int32_t)vi.class_zone.size();
 }
@@ -163,6 +164,7 @@ void build_volumes(ksim_k8s_cluster* c, const std::vector<const PodObj*>& runnin
 void build(ksim_k8s_cluster* c) {
   if (c->built) fail(KSIM_E_STATE, "ksim_k8s_build: already built");
   c->in = Interns();
+  c->zone_groups = ZoneGroups();
   c->nodes = c->nodes_in;
   std::stable_sort(c->nodes.begin(), c->nodes.end(), [](const NodeObj& a, const NodeObj& b) { return a.name < b.name; });
   const int64_t n = (int64_t)c->nodes.size();
@@ -587,7 +589,7 @@ extern "C" int ksim_k8s_describe(ksim_k8s_cluster* c, ksim_handle* h, const ksim
         vol_small(vi, &c->vsmall);
         bool zerr = false;
         std::vector<uint32_t> zk;
-        vol_zone_verdicts(vi, c->in.label_sets, (size_t)c->vol_grown_classes, &zk, &zerr);
+        vol_zone_verdicts(vi, c->zone_groups, c->in.label_sets, (size_t)c->vol_grown_classes, &zk, &zerr);
         if (c->vol_grown_classes == 0) c->vol_zone_ok.clear();
         c->vol_zone_ok.insert(c->vol_zone_ok.end(), zk.begin(), zk.end());
         if (c->vol_zone_ok.empty()) c->vol_zone_ok.push_back(0);

@@ -86,6 +86,7 @@ struct ksim_k8s_cache {
   int64_t prof[7] = {0, 0, 0, 0, 0, 0, 0};
   int64_t prof_seen = 0;              // Schedule calls so far (KSIM_CACHE_PROFILE_SKIP: untimed head)
   size_t zoned_upto = 0;              // label sets scanned for zone / region labels
+  ZoneGroups zone_groups;             // label sets by their zone / region labels (volume zone verdicts)
   bool zoned = false;
 };
 
@@ -174,7 +175,7 @@ void sync_volumes(Cache* c, bool need, const Enc* e) {
     if (c->vol_key == key && (int64_t)want <= c->vol_S) return;
     if (c->vol_key[2] == key[2]) {
       if (key[1] > c->vol_zone_classes) {
-        vol_zone_verdicts(vi, c->in.label_sets, c->vol_zone_classes, &c->vol_zone, &c->vol_zone_err);
+        vol_zone_verdicts(vi, c->zone_groups, c->in.label_sets, c->vol_zone_classes, &c->vol_zone, &c->vol_zone_err);
         c->vol_zone_classes = key[1];
       }
       const int32_t S = std::max<int32_t>(c->vol_S, (int32_t)(2 * want));
@@ -191,7 +192,7 @@ void sync_volumes(Cache* c, bool need, const Enc* e) {
   const int64_t n = (int64_t)c->names.size();
   c->vol_zone.clear();
   c->vol_zone_err = false;
-  vol_zone_verdicts(vi, c->in.label_sets, 0, &c->vol_zone, &c->vol_zone_err);
+  vol_zone_verdicts(vi, c->zone_groups, c->in.label_sets, 0, &c->vol_zone, &c->vol_zone_err);
   c->vol_zone_classes = key[1];
   c->vol_zone_words = ((int32_t)key[2] + 31) / 32;
   const int32_t S = std::max<int32_t>((int32_t)(2 * want), 8);

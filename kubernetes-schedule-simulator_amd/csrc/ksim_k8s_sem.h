@@ -1448,24 +1448,42 @@ int load_aff_tab(const AffTables& a, int64_t n, int32_t hard_weight, ksim_handle
 // NoVolumeZoneConflict per (volume class, label set) for the classes from `first` on, appended to
 // ok[class][words] (words = ceil(L / 32)); *err: a class errs on some zone-labelled set
 // (VolumeIndex.zone_verdicts).  Evaluated once per distinct (zone, region) constraint.
-void vol_zone_verdicts(const VolumeIndex& vi, const Interner<LabelSetKey>& label_sets, size_t first, std::vector<uint32_t>* ok,
-                       bool* err) {
+// Label sets grouped by their zone / region labels (the only labels NoVolumeZoneConflict reads),
+// kept incrementally: label sets are only ever added, so a caller that keeps one ZoneGroups scans
+// each label set once instead of once per volume class.
+struct ZoneGroups {
+  size_t upto = 0;
+  std::map<std::vector<std::pair<Str, Str>>, int32_t> index;
+  std::vector<std::vector<std::pair<Str, Str>>> cons;  // per group: its (key, value) constraints
+  std::vector<std::vector<int32_t>> members;          // per group: its label sets
+  void update(const Interner<LabelSetKey>& label_sets) {
+    for (; upto < label_sets.items.size(); ++upto) {
+      std::vector<std::pair<Str, Str>> c;
+      for (const auto& l : label_sets.items[upto].labels)
+        if (l.first == ZONE_LABEL || l.first == REGION_LABEL) c.push_back(l);
+      auto it = index.find(c);
+      if (it == index.end()) {
+        it = index.emplace(c, (int32_t)cons.size()).first;
+        cons.push_back(c);
+        members.emplace_back();
+      }
+      members[it->second].push_back((int32_t)upto);
+    }
+  }
+};
+
+void vol_zone_verdicts(const VolumeIndex& vi, ZoneGroups& groups, const Interner<LabelSetKey>& label_sets, size_t first,
+                       std::vector<uint32_t>* ok, bool* err) {
+  groups.update(label_sets);
   const int32_t L = (int32_t)label_sets.items.size();
   const int32_t words = (L + 31) / 32;
-  std::map<std::vector<std::pair<Str, Str>>, std::vector<int32_t>> groups;
-  for (int32_t s = 0; s < L; ++s) {
-    std::vector<std::pair<Str, Str>> cons;
-    for (const auto& l : label_sets.items[s].labels)
-      if (l.first == ZONE_LABEL || l.first == REGION_LABEL) cons.push_back(l);
-    groups[cons].push_back(s);
-  }
   for (size_t k = first; k < vi.class_zone.size(); ++k) {
     const auto& zone = vi.class_zone[k];
     std::vector<uint32_t> row(words, 0);
-    for (const auto& g : groups) {
+    for (size_t g = 0; g < groups.cons.size(); ++g) {
       bool fits = true;
-      if (!zone.empty() && !g.first.empty()) {
-        std::map<Str, Str> cons(g.first.begin(), g.first.end());
+      if (!zone.empty() && !groups.cons[g].empty()) {
+        std::map<Str, Str> cons(groups.cons[g].begin(), groups.cons[g].end());
         for (const ZoneEntry& z : zone) {
           if (z.kind == 2) continue;
           if (z.kind == 1) { *err = true; fits = false; break; }
@@ -1480,10 +1498,16 @@ void vol_zone_verdicts(const VolumeIndex& vi, const Interner<LabelSetKey>& label
         }
       }
       if (fits)
-        for (int32_t s : g.second) row[s >> 5] |= 1u << (s & 31);
+        for (int32_t s : groups.members[g]) row[s >> 5] |= 1u << (s & 31);
     }
     ok->insert(ok->end(), row.begin(), row.end());
   }
+}
+
+void vol_zone_verdicts(const VolumeIndex& vi, const Interner<LabelSetKey>& label_sets, size_t first, std::vector<uint32_t>* ok,
+                       bool* err) {
+  ZoneGroups g;
+  vol_zone_verdicts(vi, g, label_sets, first, ok, err);
 }
 
 // The small tables of ksim_volume_tables (keys, classes, refs) from an index.
