@@ -71,12 +71,14 @@ __global__ void ksim_set_row_kernel(KsimCtx c, int64_t i, const uint64_t* __rest
 // NodeInfo.RemovePod of queue pod `pod` from row `node` (ksim_pod_remove).
 __global__ void ksim_release_kernel(KsimCtx c, int64_t pod, int64_t node) {
   if (blockIdx.x != 0 || threadIdx.x >= 64) return;
-  const ksim_pod P = c.one ? c.one_pod : c.pods[pod];
+  ksim_pod P;  // (a branch, not a pointer select: the pod stays in registers)
+  if (c.one) P = c.one_pod;
+  else P = c.pods[pod];
   if (threadIdx.x == 0) {
     ksim_uncommit(c, P, node);
-    if (ksim_is_vol_pod(c, P)) ksim_vol_commit(*c.vol, P, node, -1, c.err);
+    if (ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, node, -1, c.err);
   }
-  if (ksim_is_aff_pod(c, P)) ksim_aff_commit(*c.aff, P, node, -1, threadIdx.x, 64);
+  if (ksim_is_aff_pod(c, P)) ksim_aff_commit_body(*c.aff, P, node, -1, threadIdx.x, 64);
 }
 
 // Queued pods' spec.nodeName name ranks after a node insert (op 1) or removal (op 2).

@@ -370,7 +370,7 @@ __device__ __forceinline__ bool ksim_pair_hit(const KsimAff& A, int32_t pair, in
 // then P's required affinity terms (anyPodMatchesPodAffinityTerm, :1161-1194; a term nobody
 // matches is waived when P matches it itself, :1405-1424), then its required anti-affinity
 // terms (:1430-1441).  Reason mask, 0 = fits.  Out of line: only affinity pods call it.
-__device__ __noinline__ uint32_t ksim_interpod_pred(const KsimAff& A, const ksim_pod& P, int64_t i) {
+__device__ __forceinline__ uint32_t ksim_interpod_pred_body(const KsimAff& A, const ksim_pod& P, int64_t i) {
   const uint32_t base = 1u << KSIM_R_POD_AFFINITY;
   if (P.aff_ident > 0) {
     const uint64_t* mw = A.ident_anti + (int64_t)(P.aff_ident - 1) * A.carry_words;
@@ -397,6 +397,7 @@ __device__ __noinline__ uint32_t ksim_interpod_pred(const KsimAff& A, const ksim
   }
   return 0;
 }
+__device__ __noinline__ uint32_t ksim_interpod_pred(const KsimAff& A, const ksim_pod& P, int64_t i) { return ksim_interpod_pred_body(A, P, i); }
 
 // Does pod P read the InterPodAffinity priority (own preferred terms, or carried priority
 // terms its identity matches)?
@@ -412,7 +413,7 @@ __device__ __forceinline__ bool ksim_interpod_prio_work(const KsimAff& A, const 
 // CalculateInterPodAffinityPriority's per-node sum (interpod_affinity.go:124-214) before
 // normalisation: P's preferred terms weight the placed pods they match in the node's domain,
 // the carried terms of placed pods P matches add their per-domain amounts.
-__device__ __noinline__ int64_t ksim_interpod_raw(const KsimAff& A, const ksim_pod& P, int64_t i) {
+__device__ __forceinline__ int64_t ksim_interpod_raw_body(const KsimAff& A, const ksim_pod& P, int64_t i) {
   int64_t s = 0;
   if (P.aff_class > 0) {
     const int32_t* ac = A.ac + 6 * (int64_t)(P.aff_class - 1);
@@ -436,6 +437,7 @@ __device__ __noinline__ int64_t ksim_interpod_raw(const KsimAff& A, const ksim_p
   }
   return s;
 }
+__device__ __noinline__ int64_t ksim_interpod_raw(const KsimAff& A, const ksim_pod& P, int64_t i) { return ksim_interpod_raw_body(A, P, i); }
 
 // fScore = MaxPriority * ((count - min) / (max - min)) in float64, truncated (:228-236); the
 // counts are integers below 2^53, so the float64 operands are exact as in Go.
@@ -446,7 +448,7 @@ __device__ __forceinline__ int64_t ksim_interpod_score(int64_t raw, int64_t mn, 
 
 // NodeInfo.AddPod / RemovePod of an affinity pod on node w (sign +1 / -1): every counted pair
 // whose selector its identity matches, and the amounts of the terms it carries.  Single thread.
-__device__ __noinline__ void ksim_aff_commit(const KsimAff& A, const ksim_pod& P, int64_t w, int32_t sign,
+__device__ __forceinline__ void ksim_aff_commit_body(const KsimAff& A, const ksim_pod& P, int64_t w, int32_t sign,
                                              int32_t lane = 0, int32_t stride = 1) {
   // lanes [lane, stride) split the pairs and carries; the updates are atomic adds (order-free sums)
   if (P.aff_ident > 0) {
@@ -468,6 +470,10 @@ __device__ __noinline__ void ksim_aff_commit(const KsimAff& A, const ksim_pod& P
                   (unsigned long long)((int64_t)sign * k.amount));
     }
   }
+}
+__device__ __noinline__ void ksim_aff_commit(const KsimAff& A, const ksim_pod& P, int64_t w, int32_t sign,
+                                             int32_t lane = 0, int32_t stride = 1) {
+  ksim_aff_commit_body(A, P, w, sign, lane, stride);
 }
 
 // The counted pair of pod P's SelectorSpread selectors, or -1.
@@ -506,11 +512,42 @@ __device__ __forceinline__ int32_t ksim_vol_find(const KsimVol& V, int64_t i, in
   return -1;
 }
 
+// The node's mount words, all loads in flight at once (nodes with up to KSIM_VOL_REG mounted keys;
+// more take the one-slot-at-a-time form): the lookups below then run on registers instead of one
+// dependent load per slot.
+#define KSIM_VOL_REG 16
+__device__ __forceinline__ void ksim_vol_load_slots(const KsimVol& V, int64_t i, int32_t cnt, uint64_t (&sw)[KSIM_VOL_REG]) {
+#pragma unroll
+  for (int s = 0; s < KSIM_VOL_REG; ++s) sw[s] = s < cnt ? V.slots[(int64_t)s * V.n + i] : 0ull;
+}
+__device__ __forceinline__ int32_t ksim_vol_find_reg(const uint64_t (&sw)[KSIM_VOL_REG], int32_t cnt, int32_t key) {
+  int32_t f = -1;
+#pragma unroll
+  for (int s = KSIM_VOL_REG - 1; s >= 0; --s) f = (s < cnt && (int32_t)(sw[s] >> 32) == key) ? s : f;
+  return f;
+}
+
 // NoDiskConflict (predicates.go:276-285 over isVolumeConflict :220-265): some volume of the pod
 // is mounted on the node by a placed pod in a conflicting mode.
-__device__ __noinline__ uint32_t ksim_disk_conflict(const KsimVol& V, int32_t vclass, int64_t i) {
+__device__ __forceinline__ uint32_t ksim_disk_conflict_body(const KsimVol& V, int32_t vclass, int64_t i) {
   const int32_t* vc = V.vc + 2 * (int64_t)(vclass - 1);
   const int32_t cnt = V.slot_count[i];
+  if (cnt <= KSIM_VOL_REG) {
+    uint64_t sw[KSIM_VOL_REG];
+    ksim_vol_load_slots(V, i, cnt, sw);
+    for (int32_t j = vc[0], e = vc[0] + vc[1]; j < e; ++j) {
+      const ksim_vol_ref r = V.refs[j];
+      if (!(r.flags & (KSIM_VOL_CONFLICT_ANY | KSIM_VOL_CONFLICT_RW))) continue;
+      const int32_t s = ksim_vol_find_reg(sw, cnt, r.key);
+      if (s < 0) continue;
+      uint64_t w = 0;
+#pragma unroll
+      for (int t = 0; t < KSIM_VOL_REG; ++t) w = t == s ? sw[t] : w;
+      const uint32_t rw = (uint32_t)(w & 0x7FFu), ro = (uint32_t)((w >> 11) & 0x7FFu);
+      if ((r.flags & KSIM_VOL_CONFLICT_ANY) ? (rw + ro > 0) : (rw > 0)) return 1u << KSIM_R_DISK_CONFLICT;
+    }
+    return 0;
+  }
   for (int32_t j = vc[0], e = vc[0] + vc[1]; j < e; ++j) {
     const ksim_vol_ref r = V.refs[j];
     if (!(r.flags & (KSIM_VOL_CONFLICT_ANY | KSIM_VOL_CONFLICT_RW))) continue;
@@ -522,15 +559,37 @@ __device__ __noinline__ uint32_t ksim_disk_conflict(const KsimVol& V, int32_t vc
   }
   return 0;
 }
+__device__ __noinline__ uint32_t ksim_disk_conflict(const KsimVol& V, int32_t vclass, int64_t i) { return ksim_disk_conflict_body(V, vclass, i); }
 
 // MaxEBS / MaxGCEPD / MaxAzureDiskVolumeCount (predicates.go:415-456) for the filters in `which`,
 // in that order: the node's distinct mounted keys the filter counts plus the pod's keys it counts
 // that the node does not mount yet, against the filter's limit.
-__device__ __noinline__ uint32_t ksim_max_volumes(const KsimVol& V, int32_t vclass, int64_t i, uint32_t which) {
+__device__ __forceinline__ uint32_t ksim_max_volumes_body(const KsimVol& V, int32_t vclass, int64_t i, uint32_t which) {
   const int32_t* vc = V.vc + 2 * (int64_t)(vclass - 1);
   const uint32_t want = V.vc_filter[vclass - 1] & which;
   if (!want) return 0;
   const int32_t cnt = V.slot_count[i];
+  if (cnt <= KSIM_VOL_REG) {
+    uint64_t sw[KSIM_VOL_REG];
+    ksim_vol_load_slots(V, i, cnt, sw);
+    uint32_t kf[KSIM_VOL_REG];  // the filters of the node's mounted keys, loaded together
+#pragma unroll
+    for (int s = 0; s < KSIM_VOL_REG; ++s) kf[s] = s < cnt ? V.key_filter[(int32_t)(sw[s] >> 32)] : 0u;
+    for (int t = 0; t < 3; ++t) {
+      const uint32_t f = 1u << t;
+      if (!(want & f)) continue;
+      int32_t have = 0;
+#pragma unroll
+      for (int s = 0; s < KSIM_VOL_REG; ++s) have += (kf[s] & f) ? 1 : 0;
+      int32_t add = 0;
+      for (int32_t j = vc[0], e = vc[0] + vc[1]; j < e; ++j) {
+        const ksim_vol_ref r = V.refs[j];
+        if ((r.flags & KSIM_VOL_NEW) && (V.key_filter[r.key] & f) && ksim_vol_find_reg(sw, cnt, r.key) < 0) ++add;
+      }
+      if (have + add > V.max_vols[t]) return 1u << KSIM_R_MAX_VOLUME_COUNT;
+    }
+    return 0;
+  }
   for (int t = 0; t < 3; ++t) {
     const uint32_t f = 1u << t;
     if (!(want & f)) continue;
@@ -546,6 +605,7 @@ __device__ __noinline__ uint32_t ksim_max_volumes(const KsimVol& V, int32_t vcla
   }
   return 0;
 }
+__device__ __noinline__ uint32_t ksim_max_volumes(const KsimVol& V, int32_t vclass, int64_t i, uint32_t which) { return ksim_max_volumes_body(V, vclass, i, which); }
 
 __device__ __forceinline__ bool ksim_vol_zone_ok(const KsimVol& V, int32_t vclass, int32_t label_set) {
   if (!V.zone_ok) return true;
@@ -555,7 +615,7 @@ __device__ __forceinline__ bool ksim_vol_zone_ok(const KsimVol& V, int32_t vclas
 // NodeInfo.AddPod / RemovePod of a pod with volumes on node w (sign +1 / -1): each ref adds or
 // takes one mount of its key (read-write, read-only or through a PVC).  Single thread; a full node
 // or a saturated count sets err bit 1.
-__device__ __noinline__ void ksim_vol_commit(const KsimVol& V, const ksim_pod& P, int64_t w, int32_t sign,
+__device__ __forceinline__ void ksim_vol_commit_body(const KsimVol& V, const ksim_pod& P, int64_t w, int32_t sign,
                                              int32_t* err) {
   const int32_t* vc = V.vc + 2 * (int64_t)(P.vol_class - 1);
   for (int32_t j = vc[0], e = vc[0] + vc[1]; j < e; ++j) {
@@ -588,11 +648,17 @@ __device__ __noinline__ void ksim_vol_commit(const KsimVol& V, const ksim_pod& P
     }
   }
 }
+__device__ __noinline__ void ksim_vol_commit(const KsimVol& V, const ksim_pod& P, int64_t w, int32_t sign,
+                                             int32_t* err) {
+  ksim_vol_commit_body(V, P, w, sign, err);
+}
 
 // Reason mask of the first failing predicate in predicatesOrdering (predicates.go:129-138,
 // core/generic_scheduler.go:467-528); 0 = fits.  IPA = false stops before MatchInterPodAffinity (the
 // last key), for a kernel that evaluates it over its own count layout (ksim_pgen.hip).
-template <class A, bool IPA = true>
+// INL: the volume / affinity predicates inlined (the launch-form kernels) instead of called out of
+// line (the persistent kernels, whose instruction-cache footprint they would grow)
+template <class A, bool IPA = true, bool INL = false>
 __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ksim_pod& P, int64_t i, const KsimRow& r,
                                                       const A& a) {
   const uint32_t pr = c.preds;
@@ -626,7 +692,7 @@ __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ks
   }
   const bool vol = ksim_is_vol_pod(c, P);
   if ((pr & KSIM_P_DISK_CONFLICT) && vol) {
-    m = ksim_disk_conflict(*c.vol, P.vol_class, i);
+    m = INL ? ksim_disk_conflict_body(*c.vol, P.vol_class, i) : ksim_disk_conflict(*c.vol, P.vol_class, i);
     if (m) return m;
   }
   if ((pr & KSIM_P_TAINTS) && (P.flags & KSIM_POD_NEED_TAINTS)) {
@@ -643,7 +709,7 @@ __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ks
     const uint32_t which = ((pr & KSIM_P_MAX_EBS) ? KSIM_VOL_EBS : 0u) | ((pr & KSIM_P_MAX_GCE_PD) ? KSIM_VOL_GCE_PD : 0u) |
                            ((pr & KSIM_P_MAX_AZURE_DISK) ? KSIM_VOL_AZURE_DISK : 0u);
     if (which) {
-      m = ksim_max_volumes(*c.vol, P.vol_class, i, which);
+      m = INL ? ksim_max_volumes_body(*c.vol, P.vol_class, i, which) : ksim_max_volumes(*c.vol, P.vol_class, i, which);
       if (m) return m;
     }
     if ((pr & KSIM_P_VOLUME_ZONE) && !ksim_vol_zone_ok(*c.vol, P.vol_class, c.label_set[i])) return 1u << KSIM_R_VOLUME_ZONE;
@@ -652,12 +718,12 @@ __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ks
     return 1u << KSIM_R_MEM_PRESSURE;
   if ((pr & KSIM_P_DISK_PRESSURE) && (r.fl & KSIM_N_DISK_PRESSURE)) return 1u << KSIM_R_DISK_PRESSURE;
   if (IPA && (pr & KSIM_P_INTERPOD_AFFINITY) && c.aff && (P.aff_ident > 0 || P.aff_class > 0))
-    return ksim_interpod_pred(*c.aff, P, i);
+    return INL ? ksim_interpod_pred_body(*c.aff, P, i) : ksim_interpod_pred(*c.aff, P, i);
   return 0;
 }
 
 __device__ __forceinline__ uint32_t ksim_predicates(const KsimCtx& c, const ksim_pod& P, int64_t i, const KsimRow& r) {
-  return ksim_predicates_a(c, P, i, r, KsimGlobalAcc{c});
+  return ksim_predicates_a<KsimGlobalAcc, true, true>(c, P, i, r, KsimGlobalAcc{c});
 }
 
 // Weighted sum of the map-type priorities (core/generic_scheduler.go:632-639); the reduce

@@ -104,7 +104,7 @@ __device__ __forceinline__ void eval_one(const KsimCtx& c, const ksim_pod& P, in
   score = ksim_map_score(c, P, r);
   if (ipa.on && fit)
     score = (int64_t)((uint64_t)score +
-                      (uint64_t)ipa.w * (uint64_t)ksim_interpod_score(ksim_interpod_raw(*c.aff, P, i), ipa.mn, ipa.mx));
+                      (uint64_t)ipa.w * (uint64_t)ksim_interpod_score(ksim_interpod_raw_body(*c.aff, P, i), ipa.mn, ipa.mx));
   if (ipa.sp >= 0 && fit) {
     const KsimAff& A = *c.aff;
     const int32_t z = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
@@ -247,7 +247,9 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
   __shared__ int s_last;
   const int64_t pod = c.one ? c.first : *c.cursor;
   if (pod >= c.end || !c.aff || c.no_prio) return;
-  const ksim_pod P = c.one ? c.one_pod : c.pods[pod];
+  ksim_pod P;  // (a branch, not a pointer select: the pod stays in registers)
+  if (c.one) P = c.one_pod;
+  else P = c.pods[pod];
   const KsimAff& A = *c.aff;
   const bool ipa = c.w[KSIM_W_INTERPOD_AFFINITY] != 0 && ksim_interpod_prio_work(A, P);
   const int32_t sp = c.w[KSIM_W_SELECTOR_SPREAD] != 0 ? ksim_spread_pair(A, P) : -1;
@@ -264,7 +266,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
     const KsimRow r = ksim_load_row(c, i);
     if (ksim_predicates(c, P, i, r) != 0) continue;
     fit[k] = true;
-    if (ipa) raw[k] = ksim_interpod_raw(A, P, i);
+    if (ipa) raw[k] = ksim_interpod_raw_body(A, P, i);
     if (sp >= 0) {
       cnt[k] = A.cnt[A.pair_off[sp] + i];
       zz[k] = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
@@ -278,17 +280,27 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
 // + ticket; the last block: 52 combine, 53 decide, 54 locate, 55 masks + pick, 56 commit,
 // 57 results), dbg[60] blocks, dbg[61] last blocks; printed by ksim_destroy
 #ifdef KSIM_STAMPS
-#define SSTAMP(k)                                                                          \
-  do {                                                                                     \
-    if (tid == 0) {                                                                        \
-      const uint64_t t_ = __builtin_amdgcn_s_memtime();                                   \
-      atomicAdd((unsigned long long*)&c.dbg[48 + (k)], (unsigned long long)(t_ - ts_prev)); \
-      ts_prev = t_;                                                                        \
-    }                                                                                      \
+#define SSTAMP(k)                                          \
+  do {                                                     \
+    if (tid == 0) {                                        \
+      const uint64_t t_ = __builtin_amdgcn_s_memtime();   \
+      st_acc[k] += t_ - ts_prev;                           \
+      ts_prev = t_;                                        \
+    }                                                      \
+  } while (0)
+// thread 0 adds its sums at the block's exit (no global atomic between the phases it times)
+#define SFLUSH()                                                                                   \
+  do {                                                                                             \
+    if (tid == 0)                                                                                  \
+      for (int k_ = 0; k_ < 10; ++k_)                                                              \
+        if (st_acc[k_]) atomicAdd((unsigned long long*)&c.dbg[48 + k_], (unsigned long long)st_acc[k_]); \
   } while (0)
 #else
 #define SSTAMP(k) \
   do {            \
+  } while (0)
+#define SFLUSH() \
+  do {           \
   } while (0)
 #endif
 
@@ -307,6 +319,8 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   __shared__ uint32_t s_gen;
   __shared__ int s_bail;
   __shared__ uint64_t s_ctr;
+  __shared__ int64_t s_Mq[KSIM_MAX_RCLASS], s_tot[KSIM_MAX_RCLASS];
+  __shared__ int32_t s_Cq[KSIM_MAX_RCLASS];
   __shared__ int64_t s_tv[KSIM_MAX_RCLASS], s_av[KSIM_MAX_RCLASS], s_ad[KSIM_MAX_RCLASS];
   // last block, single reduce class: every block's (fit, max, count) as combined, for the locate step
   constexpr int LOC_MAX = 1024;
@@ -317,6 +331,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
 #ifdef KSIM_STAMPS
   uint64_t ts_prev = __builtin_amdgcn_s_memtime();
+  uint64_t st_acc[10] = {};
   if (tid == 0) atomicAdd((unsigned long long*)&c.dbg[60], 1ull);
 #endif
   if (c.fuse_a) {
@@ -328,7 +343,9 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   }
   const int64_t pod = c.one ? c.first : *c.cursor;
   if (pod >= c.end) return;  // uniform: graph replay past the end of the queue
-  const ksim_pod P = c.one ? c.one_pod : c.pods[pod];
+  ksim_pod P;  // (a branch, not a pointer select: the pod stays in registers)
+  if (c.one) P = c.one_pod;
+  else P = c.pods[pod];
   // per-pod launches carry the class's reduce-class counts in the descriptor (stage_pod)
   const int k1 = c.one ? P.reserved[0] : (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
   const int k2 = c.one ? P.reserved[1] : c.use_na ? c.n_na[P.cls] : 1;
@@ -380,7 +397,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       const int64_t i = base + k * KSIM_BLOCK + tid;
       raw[k] = 0; cnt[k] = 0; zz[k] = -1;
       if (!fit[k]) continue;
-      if (ipa.on) raw[k] = ksim_interpod_raw(A, P, i);
+      if (ipa.on) raw[k] = ksim_interpod_raw_body(A, P, i);
       if (ipa.sp >= 0) {
         cnt[k] = A.cnt[A.pair_off[ipa.sp] + i];
         zz[k] = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
@@ -501,7 +518,10 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   }
   __syncthreads();
   SSTAMP(3);
-  if (!s_last) return;
+  if (!s_last) {
+    SFLUSH();
+    return;
+  }
 
   // ---------------- last block: the global decision ----------------
 #ifdef KSIM_STAMPS
@@ -566,8 +586,9 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       D.ix = 0;
     } else {
       D.mode = 2;
-      int64_t Mq[KSIM_MAX_RCLASS];
-      int32_t Cq[KSIM_MAX_RCLASS];
+      int64_t* const Mq = s_Mq;  // per-class arrays in LDS: private arrays indexed by a run-time
+      int32_t* const Cq = s_Cq;  // class would live in scratch memory
+      int64_t* const tot = s_tot;
       for (int q = 0; q < K; ++q) {
         int64_t m = INT64_MIN;
         int32_t n = 0;
@@ -589,7 +610,6 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
         if (k2 > 1 || c.w[KSIM_W_NODE_AFFINITY]) mxA = av > mxA ? av : mxA;
       }
       int64_t best = INT64_MIN;
-      int64_t tot[KSIM_MAX_RCLASS];
       for (int q = 0; q < K; ++q) {
         if (Cq[q] == 0) continue;
         uint64_t t = (uint64_t)Mq[q];
@@ -606,7 +626,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       D.winners = win;
       for (int q = 0; q < K; ++q) D.M[q] = Mq[q];
       const uint64_t li = s_ctr;                // generic_scheduler.go:192-195
-      D.ix = (int64_t)(li % (uint64_t)C);
+      D.ix = ((li >> 32) == 0 && C < ((int64_t)1 << 32)) ? (int64_t)((uint32_t)li % (uint32_t)C) : (int64_t)(li % (uint64_t)C);
       *c.counter = li + 1;
       s_ctr = li + 1;
     }
@@ -702,11 +722,11 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       if (wv == 0) {
         const int32_t st = ksim_commit_wave(c, P, D.node, lane);
         if (tid == 0) {
-          if (ksim_is_vol_pod(c, P)) ksim_vol_commit(*c.vol, P, D.node, 1, c.err);
+          if (ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, D.node, 1, c.err);
           if (c.out_fit) c.out_fit[1] |= st;
         }
       } else if (wv == 1 && ksim_is_aff_pod(c, P)) {
-        ksim_aff_commit(*c.aff, P, D.node, 1, lane, 64);
+        ksim_aff_commit_body(*c.aff, P, D.node, 1, lane, 64);
       }
     }
   }
@@ -725,6 +745,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     *c.ticket = 0;
   }
   SSTAMP(9);
+  SFLUSH();
 }
 
 // Per-node evaluation of one pod without commit (ksim_evaluate).
@@ -732,7 +753,9 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_
                                                              int64_t* score, uint8_t* rcls) {
   const int64_t i = (int64_t)blockIdx.x * KSIM_BLOCK + threadIdx.x;
   if (i >= c.n) return;
-  const ksim_pod P = c.one ? c.one_pod : c.pods[pod];
+  ksim_pod P;  // (a branch, not a pointer select: the pod stays in registers)
+  if (c.one) P = c.one_pod;
+  else P = c.pods[pod];
   const int k1 = (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
   const int k2 = c.use_na ? c.n_na[P.cls] : 1;
   const KsimRow r = ksim_load_row(c, i);
@@ -747,13 +770,15 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_
 // status[0] |= ksim_row_status, status[1] = the error word afterwards (KSIM_RES_STATUS / _ERR).
 __global__ void ksim_assume_kernel(KsimCtx c, int64_t pod, int64_t node, int32_t* status) {
   if (blockIdx.x != 0 || threadIdx.x >= 64) return;
-  const ksim_pod P = c.one ? c.one_pod : c.pods[pod];
+  ksim_pod P;  // (a branch, not a pointer select: the pod stays in registers)
+  if (c.one) P = c.one_pod;
+  else P = c.pods[pod];
   const int32_t st = ksim_commit_wave(c, P, node, threadIdx.x);
   if (threadIdx.x == 0) {
-    if (ksim_is_vol_pod(c, P)) ksim_vol_commit(*c.vol, P, node, 1, c.err);
+    if (ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, node, 1, c.err);
     *status |= st;
   }
-  if (ksim_is_aff_pod(c, P)) ksim_aff_commit(*c.aff, P, node, 1, threadIdx.x, 64);
+  if (ksim_is_aff_pod(c, P)) ksim_aff_commit_body(*c.aff, P, node, 1, threadIdx.x, 64);
   __syncthreads();
   if (threadIdx.x == 0) status[KSIM_RES_ERR - KSIM_RES_STATUS] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
