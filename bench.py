@@ -53,13 +53,14 @@ def pmc_traffic(workload, evals_per_launch):
             "source": os.path.relpath(path, ROOT), "profiled": d.get("profiled")}
 
 
-def roofline_bound(alg_bytes, traffic, launch_s=None):
+def roofline_bound(alg_bytes, traffic, launch_s=None, on_chip=False):
     """"hbm" when the kernel moves about the algorithmic bytes through HBM; "latency" when the PMC
     bytes per node-eval are far below them (the table is on chip: the per-pod exchange bounds it),
     or when the measured HBM traffic runs at under a tenth of the peak rate (what it moves is the
-    exchange's polling, not the table)."""
+    exchange's polling, not the table).  Without a PMC file: "latency" for a persistent kernel
+    whose rows live in LDS (on_chip), else "hbm"."""
     if traffic is None:
-        return "hbm"
+        return "latency" if on_chip else "hbm"
     if traffic["bytes_per_node_eval"] < 0.1 * alg_bytes:
         return "latency"
     if launch_s and traffic["gb_per_launch"] / launch_s < 0.1 * HBM_PEAK_GBS:
@@ -491,6 +492,9 @@ def main():
             avg_launch_s = head["kernel_ms"] / 1e3 / max(head["launches"], 1)
         achieved = W["bytes"] * n_local * min(pods_per_launch, pods_timed) / avg_launch_s / 1e9
         tree_kernel = mode_used == abi.MODE_TREE
+        # the persistent kernels keep up to ~400k rows per device in LDS (ksim_pfast_config /
+        # the general kernel's plan); beyond that the fast kernel streams rows from HBM
+        on_chip = mode_used == abi.MODE_PERSISTENT and n_local <= 400_000
         bound = int((head.get("merged", head["out"]) >= 0).sum())
         traffic = None if (tree_kernel or world > 1) else \
             pmc_traffic(a.workload + ("" if mode_used == abi.MODE_PERSISTENT else "_launch"),
@@ -519,7 +523,7 @@ def main():
                        "blocks": head["blocks"],
                        "parallelism": ("node-sharded x%d" % world if sharded_head else
                                        "scenario-replicas x%d" % world if world > 1 else "single-gpu")},
-            "roofline": {"bound": "latency" if tree_kernel else roofline_bound(W["bytes"], traffic, avg_launch_s),
+            "roofline": {"bound": "latency" if tree_kernel else roofline_bound(W["bytes"], traffic, avg_launch_s, on_chip),
                          "achieved": None if tree_kernel else round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": None if tree_kernel else round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic and traffic["gb_per_launch"],
@@ -533,7 +537,7 @@ def main():
                                      "roofline applies"} if tree_kernel else
                             {"note": "achieved = algorithmic bytes / launch time; the PMC traffic shows the table "
                                      "stays on chip (LDS), so the per-pod cross-CU exchange, not HBM, bounds it"}
-                            if roofline_bound(W["bytes"], traffic, avg_launch_s) == "latency" else {})},
+                            if roofline_bound(W["bytes"], traffic, avg_launch_s, on_chip) == "latency" else {})},
             "cpu_baseline": cpu,
             "parity": parity,
             "pods_bound": bound,

@@ -237,7 +237,11 @@ bool ksim_is_aff_host(const ksim_handle* h, const ksim_pod& p) {
 
 int after_commit(ksim_handle* h, int32_t port_cnt) {
   h->tree_valid = false;  // the trees are maintained by the tree kernel only
-  h->port_bound += port_cnt;
+  const int32_t status = h->res_host[KSIM_RES_STATUS];
+  if (status & 2)  // the committing kernel reported the row's port count: the bound stays exact
+    h->port_bound = std::max<int64_t>(h->port_bound, (int64_t)(status >> 8));
+  else
+    h->port_bound += port_cnt;
   if (h->res_host[KSIM_RES_STATUS] & 1) h->pfast_off = true;  // keep the fast kernels' float64 range
   const int32_t err = h->res_host[KSIM_RES_ERR];  // written by the committing kernel
   if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port or volume slots overflowed (raise port_slots / vol_slots)");
@@ -355,6 +359,34 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   if ((rc = stage_pod(h, *pod, ports, scalars, &cs))) return rc;
   cs.collect = 1;  // the FitError histogram is part of the answer
   cs.no_commit = assume ? 0 : 1;
+  // a small cluster: the single-workgroup kernel (every reduction in LDS, no cross-block round
+  // trips); measured slower than the multi-block scan at 5,000 nodes (its evaluation has one CU's
+  // load bandwidth), so by default only up to 1,024 nodes.  KSIM_ONE_WG=0: never, =1: whenever it fits.
+  const int one_npt = ksim_one_npt(c.n);
+  const char* ko = getenv("KSIM_ONE_WG");
+  const bool one_wg = ko ? ko[0] != '0' : c.n <= 1024;
+  if (cs.one && one_npt > 0 && one_wg && (!h->have_aff || h->aff_h.n_zone <= 512)) {
+    h->res_host[KSIM_RES_NODE] = INT32_MIN;
+    oc.lap(0);
+    hipError_t e1 = ksim_launch_one(&cs, one_npt, h->stream);
+    if (e1 != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "one-workgroup launch: %s", hipGetErrorString(e1));
+    oc.lap(1);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    oc.lap(2);
+    const int32_t* r = h->res_host;
+    memset(out, 0, sizeof *out);
+    out->node = r[KSIM_RES_NODE];
+    out->fit_nodes = r[KSIM_RES_FIT];
+    memcpy(&out->last_node_index, r + KSIM_RES_CTR, 8);
+    if (out->node < 0) memcpy(out->reasons, r + KSIM_RES_REASONS, sizeof out->reasons);
+    if (assume && out->node >= 0) {
+      rc = after_commit(h, pod->port_cnt);
+      oc.lap(3);
+      return rc;
+    }
+    if (r[KSIM_RES_ERR]) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", r[KSIM_RES_ERR]);
+    return KSIM_OK;
+  }
   const int npt = ksim_rt_pick_npt(c.n);
   cs.chunk = (int64_t)KSIM_BLOCK * npt;
   const int grid = (int)((c.n + cs.chunk - 1) / cs.chunk);

@@ -822,8 +822,9 @@ __device__ __forceinline__ int32_t ksim_row_status(const KsimCtx& c, int64_t w) 
 }
 
 // ksim_commit by one wave (lane = 0..63, every lane calls): lane 0 updates the row's columns and
-// returns ksim_row_status of the committed values; the host-port dedup reads the row's port slots
-// in parallel (one lane a slot) instead of one dependent load per slot.
+// returns ksim_row_status of the committed values (bit 0), and for a pod with host ports bit 1 and
+// the row's port count after the commit in bits 8.. (the host keeps its port-slot bound exact);
+// the host-port dedup reads the row's port slots in parallel (one lane a slot).
 __device__ __forceinline__ int32_t ksim_commit_wave(const KsimCtx& c, const ksim_pod& P, int64_t w, int lane) {
   int32_t st = 0;
   if (lane == 0) {
@@ -846,17 +847,18 @@ __device__ __forceinline__ int32_t ksim_commit_wave(const KsimCtx& c, const ksim
   if (P.port_cnt == 0) return st;
   if (c.port_slots > 64) {  // wider than a wave: the serial form
     if (lane == 0) {
+      int32_t cnt = c.port_count[w];
       for (int32_t k = 0; k < P.port_cnt; ++k) {
         const uint64_t key = ksim_pod_port(c, P, k);
-        int32_t cnt = c.port_count[w];
         bool dup = false;
         for (int32_t s = 0; s < cnt; ++s)
           if (c.ports[(int64_t)s * c.n + w] == key) { dup = true; break; }
         if (dup) continue;
         if (cnt >= c.port_slots) { atomicOr(c.err, 1); continue; }
         c.ports[(int64_t)cnt * c.n + w] = key;
-        c.port_count[w] = cnt + 1;
+        c.port_count[w] = ++cnt;
       }
+      st |= 2 | (cnt << 8);
     }
     return st;
   }
@@ -875,7 +877,7 @@ __device__ __forceinline__ int32_t ksim_commit_wave(const KsimCtx& c, const ksim
     ++cnt;
   }
   if (lane == 0 && cnt != cnt0) c.port_count[w] = cnt;
-  return st;
+  return st | 2 | (cnt << 8);
 }
 
 // Remove pod P from node w: NodeInfo.RemovePod (node_info.go:343-390) — the containers-only

@@ -25,6 +25,8 @@ extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, i
 extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* fit, uint32_t* reasons, int64_t* score,
                                        uint8_t* rcls, hipStream_t s);
 extern "C" int ksim_scan_coresident(int npt, int collect, int grid);
+extern "C" int ksim_one_npt(int64_t n);
+extern "C" hipError_t ksim_launch_one(const KsimCtx* c, int npt, hipStream_t s);
 extern "C" hipError_t ksim_launch_ipa_pass(const KsimCtx* c, int npt, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, int32_t* status, hipStream_t s);
 extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,

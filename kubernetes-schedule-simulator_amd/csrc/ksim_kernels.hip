@@ -353,11 +353,14 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   // what the last block's decision reads, fetched now while the chunk is evaluated: the counter
   // (kernels of a stream run one after another, so its value is final) and the pod's per-class
   // TaintToleration / NodeAffinity values and NodePreferAvoidPods addends
-  if (tid == 0) s_ctr = *c.counter;
+  // (loaded into registers here, stored to LDS after the evaluation: the loads overlap it)
+  uint64_t pre_ctr = 0;
+  int64_t pre_tv = 0, pre_av = 0, pre_ad = 0;
+  if (tid == 0) pre_ctr = *c.counter;
   if (tid < K) {
-    s_tv[tid] = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid / k2];
-    s_av[tid] = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2];
-    s_ad[tid] = c.na_add ? c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2] : 0;
+    pre_tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid / k2];
+    pre_av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2];
+    pre_ad = c.na_add ? c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2] : 0;
   }
   const int64_t base = (int64_t)blockIdx.x * c.chunk;
   IpaNorm ipa = ipa_norm(c, P);
@@ -443,6 +446,12 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   }
 
   SSTAMP(1);
+  if (tid == 0) s_ctr = pre_ctr;
+  if (tid < K) {
+    s_tv[tid] = pre_tv;
+    s_av[tid] = pre_av;
+    s_ad[tid] = pre_ad;
+  }
   // candidate masks: write-through (sc1) stores, drained by every storing wave before the barrier
   // that precedes the ticket, read back with sc1 loads by the last block
   uint64_t* pm = c.pmask + (int64_t)blockIdx.x * KSIM_PM_STRIDE;
@@ -584,6 +593,24 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     } else if (F == 1) {  // generic_scheduler.go:153-156: no selectHost, no counter bump
       D.mode = 1;
       D.ix = 0;
+    } else if (K == 1) {  // one reduce class: it wins, its count at the maximum is C
+      D.mode = 2;
+      int64_t m = INT64_MIN;
+      int32_t n = 0;
+      for (int w = 0; w < KSIM_WAVES; ++w) {
+        const int32_t cw = s_cnt[w][0];
+        const int64_t mw = s_mx[w][0];
+        if (cw == 0) continue;
+        if (mw > m) { m = mw; n = cw; }
+        else if (mw == m) n += cw;
+      }
+      D.winners = 1u;
+      D.M[0] = m;
+      const uint64_t li = s_ctr;  // generic_scheduler.go:192-195
+      const int64_t C = n;
+      D.ix = ((li >> 32) == 0 && C < ((int64_t)1 << 32)) ? (int64_t)((uint32_t)li % (uint32_t)C) : (int64_t)(li % (uint64_t)C);
+      *c.counter = li + 1;
+      s_ctr = li + 1;
     } else {
       D.mode = 2;
       int64_t* const Mq = s_Mq;  // per-class arrays in LDS: private arrays indexed by a run-time
@@ -748,6 +775,303 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   SFLUSH();
 }
 
+// ---------------------------------------------------------------------------------------
+// The per-pod call on a cluster one workgroup covers (ksim_schedule_one, n <= 16 x 512): the
+// same evaluation, pass A, decision and commit as ksim_scan_kernel, with every cross-node
+// reduction in LDS — no partials, arrival ticket, candidate masks or second pass through global
+// memory, so the launch is bounded by the evaluation's own load chains.  Pass A's zone sums stay
+// in LDS (<= KSIM_PASS_ZONES zones, host-checked); the pod comes from the kernel arguments.
+constexpr int ONE_BLOCK = 512;  // 2 waves per SIMD: 256 VGPRs for the NPT evaluations in flight
+constexpr int ONE_WAVES = ONE_BLOCK / 64;
+
+template <int NPT>
+__global__ __launch_bounds__(ONE_BLOCK) void ksim_one_kernel(KsimCtx c) {
+  __shared__ int64_t s_mx[ONE_WAVES][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_cnt[ONE_WAVES][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_fit[ONE_WAVES];
+  __shared__ int32_t s_hist[KSIM_NREASONS];
+  __shared__ int64_t s_v[4][ONE_WAVES];
+  __shared__ unsigned long long s_z[KSIM_PASS_ZONES];
+  __shared__ uint64_t s_bm[NPT][ONE_WAVES];
+  __shared__ Decision D;
+  __shared__ int64_t s_pa[5];  // pass A: min / max raw InterPodAffinity sum, max spread count, haveZones, zone max
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const ksim_pod P = c.one_pod;
+  const int64_t pod = c.first;
+  const int k1 = P.reserved[0], k2 = P.reserved[1];
+  const int K = k1 * k2;
+  // the decision's inputs, loaded while the nodes are evaluated (to LDS afterwards)
+  __shared__ int64_t s_tv[KSIM_MAX_RCLASS], s_av[KSIM_MAX_RCLASS], s_ad[KSIM_MAX_RCLASS];
+  uint64_t pre_ctr = 0;
+  int64_t pre_tv = 0, pre_av = 0, pre_ad = 0;
+  if (tid == 0) pre_ctr = *c.counter;
+  if (tid < K) {
+    pre_tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid / k2];
+    pre_av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2];
+    pre_ad = c.na_add ? c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2] : 0;
+  }
+  IpaNorm ipa = ipa_norm(c, P);  // which of pass A's priorities the pod reads (maxima below)
+  IpaNorm ipa0 = ipa;
+  ipa0.on = false;
+  ipa0.sp = -1;
+  const bool pass_a = ipa.on || ipa.sp >= 0;
+  if (tid < KSIM_NREASONS) s_hist[tid] = 0;
+  if (ipa.sp >= 0)
+    for (int z = tid; z < c.aff->n_zone; z += ONE_BLOCK) s_z[z] = 0;
+  if (ipa.sp >= 0) __syncthreads();  // (uniform) the zone sums are zero before the atomics
+
+  bool fit[NPT];
+  int64_t sc[NPT];
+  int cl[NPT];
+  uint32_t rm[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) eval_one<true>(c, P, (int64_t)k * ONE_BLOCK + tid, k1, k2, ipa0, fit[k], sc[k], cl[k], rm[k]);
+
+  if (pass_a) {  // (uniform) pass A over the fit nodes, reduced in LDS
+    const KsimAff& A = *c.aff;
+    int64_t raw[NPT], cnt[NPT];
+    int32_t zz[NPT];
+    int64_t mn = 0, mx = 0, smx = 0, hz = 0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int64_t i = (int64_t)k * ONE_BLOCK + tid;
+      raw[k] = 0; cnt[k] = 0; zz[k] = -1;
+      if (!fit[k]) continue;
+      if (ipa.on) {
+        raw[k] = ksim_interpod_raw_body(A, P, i);
+        mn = raw[k] < mn ? raw[k] : mn;
+        mx = raw[k] > mx ? raw[k] : mx;
+      }
+      if (ipa.sp >= 0) {
+        cnt[k] = A.cnt[A.pair_off[ipa.sp] + i];
+        zz[k] = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
+        smx = cnt[k] > smx ? cnt[k] : smx;
+        if (zz[k] >= 0) {
+          hz = 1;
+          if (cnt[k]) atomicAdd(&s_z[zz[k]], (unsigned long long)cnt[k]);
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int64_t a = __shfl_xor(mn, o, 64), b = __shfl_xor(mx, o, 64);
+      const int64_t d = __shfl_xor(smx, o, 64), e = __shfl_xor(hz, o, 64);
+      mn = a < mn ? a : mn;
+      mx = b > mx ? b : mx;
+      smx = d > smx ? d : smx;
+      hz = e > hz ? e : hz;
+    }
+    if (lane == 0) { s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz; }
+    __syncthreads();
+    if (wv == 0) {  // wave 0: the waves' values, then the zone maximum
+      const bool in = lane < ONE_WAVES;
+      int64_t a = in ? s_v[0][lane] : 0, b = in ? s_v[1][lane] : 0, d = in ? s_v[2][lane] : 0, e = in ? s_v[3][lane] : 0;
+      int64_t zm = 0;
+      if (ipa.sp >= 0)
+        for (int z = lane; z < A.n_zone; z += 64) zm = (int64_t)s_z[z] > zm ? (int64_t)s_z[z] : zm;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const int64_t a2 = __shfl_xor(a, o, 64), b2 = __shfl_xor(b, o, 64), d2 = __shfl_xor(d, o, 64);
+        const int64_t e2 = __shfl_xor(e, o, 64), z2 = __shfl_xor(zm, o, 64);
+        a = a2 < a ? a2 : a; b = b2 > b ? b2 : b; d = d2 > d ? d2 : d; e = e2 > e ? e2 : e; zm = z2 > zm ? z2 : zm;
+      }
+      if (lane == 0) { s_pa[0] = a; s_pa[1] = b; s_pa[2] = d; s_pa[3] = e; s_pa[4] = zm; }
+    }
+    __syncthreads();
+    ipa.mn = s_pa[0]; ipa.mx = s_pa[1]; ipa.smx = s_pa[2]; ipa.hz = s_pa[3] != 0; ipa.szmx = s_pa[4];
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {  // eval_one's additions, same order
+      if (!fit[k]) continue;
+      if (ipa.on) sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)ipa.w * (uint64_t)ksim_interpod_score(raw[k], ipa.mn, ipa.mx));
+      if (ipa.sp >= 0) {
+        const int64_t v = ksim_spread_score(cnt[k], ipa.smx, ipa.hz, zz[k], zz[k] >= 0 ? (int64_t)s_z[zz[k]] : 0, ipa.szmx);
+        sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)ipa.sw * (uint64_t)v);
+      }
+    }
+  }
+
+  if (tid < K) {
+    s_tv[tid] = pre_tv;
+    s_av[tid] = pre_av;
+    s_ad[tid] = pre_ad;
+  }
+  // ---- per-wave statistics: fit count, per reduce class (max, count at max), reasons ----
+  int32_t nfit = 0;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) nfit += __popcll(__ballot(fit[k]));
+  if (lane == 0) s_fit[wv] = nfit;
+  for (int q = 0; q < K; ++q) {  // (uniform)
+    int64_t v = INT64_MIN;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k)
+      if (fit[k] && cl[k] == q && sc[k] > v) v = sc[k];
+    const int64_t wm = wave_max_i64(v);
+    int32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) n += __popcll(__ballot(fit[k] && cl[k] == q && sc[k] == wm));
+    if (lane == 0) {
+      s_mx[wv][q] = wm;
+      s_cnt[wv][q] = (wm == INT64_MIN) ? 0 : n;
+    }
+  }
+  if (c.collect) {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      if (__ballot(rm[k] != 0)) {
+        for (int r = 0; r < KSIM_NREASONS; ++r) {
+          const int32_t n = __popcll(__ballot((rm[k] >> r) & 1u));
+          if (lane == 0 && n) atomicAdd(&s_hist[r], n);
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- the decision (thread 0): findNodesThatFit count, PrioritizeNodes' reduce step, selectHost ----
+  if (tid == 0) {
+    D.pod = pod;
+    D.K = K;
+    D.K2 = k2;
+    int32_t F = 0;
+    for (int w = 0; w < ONE_WAVES; ++w) F += s_fit[w];
+    D.fitTotal = F;
+    D.node = -1;
+    D.winners = 0;
+    if (F == 0) {
+      D.mode = 0;
+    } else if (F == 1) {  // generic_scheduler.go:153-156: no selectHost, no counter bump
+      D.mode = 1;
+      D.ix = 0;
+    } else {
+      D.mode = 2;
+      int64_t Mq[KSIM_MAX_RCLASS];
+      int32_t Cq[KSIM_MAX_RCLASS];
+#pragma unroll
+      for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
+        int64_t m = INT64_MIN;
+        int32_t n = 0;
+        if (q < K)
+          for (int w = 0; w < ONE_WAVES; ++w) {
+            const int32_t cw = s_cnt[w][q];
+            const int64_t mw = s_mx[w][q];
+            if (cw == 0) continue;
+            if (mw > m) { m = mw; n = cw; }
+            else if (mw == m) n += cw;
+          }
+        Mq[q] = m;
+        Cq[q] = n;
+      }
+      // reduce priorities over the filtered set (NormalizeReduce), as ksim_scan_kernel
+      int64_t mxT = 0, mxA = 0;
+#pragma unroll
+      for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
+        if (q >= K || Cq[q] == 0) continue;
+        if (k1 > 1 || c.w[KSIM_W_TAINT_TOLERATION]) mxT = s_tv[q] > mxT ? s_tv[q] : mxT;
+        if (k2 > 1 || c.w[KSIM_W_NODE_AFFINITY]) mxA = s_av[q] > mxA ? s_av[q] : mxA;
+      }
+      int64_t best = INT64_MIN, tot[KSIM_MAX_RCLASS];
+#pragma unroll
+      for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
+        tot[q] = INT64_MIN;
+        if (q >= K || Cq[q] == 0) continue;
+        uint64_t t = (uint64_t)Mq[q];
+        if (c.w[KSIM_W_TAINT_TOLERATION]) t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(s_tv[q], mxT, true);
+        if (c.w[KSIM_W_NODE_AFFINITY]) t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(s_av[q], mxA, false);
+        t += (uint64_t)s_ad[q];  // NodePreferAvoidPods
+        tot[q] = (int64_t)t;
+        best = tot[q] > best ? tot[q] : best;
+      }
+      uint32_t win = 0;
+      int64_t C = 0;
+#pragma unroll
+      for (int q = 0; q < KSIM_MAX_RCLASS; ++q)
+        if (q < K && Cq[q] && tot[q] == best) { win |= 1u << q; C += Cq[q]; }
+      D.winners = win;
+#pragma unroll
+      for (int q = 0; q < KSIM_MAX_RCLASS; ++q) D.M[q] = Mq[q];
+      const uint64_t li = pre_ctr;  // generic_scheduler.go:192-195
+      D.ix = ((li >> 32) == 0 && C < ((int64_t)1 << 32)) ? (int64_t)((uint32_t)li % (uint32_t)C) : (int64_t)(li % (uint64_t)C);
+      pre_ctr = li + 1;
+      *c.counter = pre_ctr;
+    }
+  }
+  __syncthreads();
+
+  if (D.mode == 0) {
+    if (c.collect && c.out_reasons && tid < KSIM_NREASONS) c.out_reasons[pod * KSIM_NREASONS + tid] = s_hist[tid];
+  } else {
+    // ---- the ix-th match counted from the largest name rank down ----
+    const int mode = D.mode;
+    const uint32_t win = D.winners;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const bool mt = fit[k] && (mode == 1 || (((win >> cl[k]) & 1u) && sc[k] == D.M[cl[k]]));
+      const uint64_t b = __ballot(mt);
+      if (lane == 0) s_bm[k][wv] = b;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      // entries e = 0.. (NPT x 16) from the top: (k, w) = (NPT - 1 - e / 16, 15 - e % 16); lane l holds EPL of them
+      constexpr int E = NPT * ONE_WAVES, EPL = (E + 63) / 64;
+      int32_t n[EPL], tot = 0;
+#pragma unroll
+      for (int j = 0; j < EPL; ++j) {
+        const int e = lane * EPL + j;
+        n[j] = e < E ? __popcll(s_bm[NPT - 1 - e / ONE_WAVES][ONE_WAVES - 1 - e % ONE_WAVES]) : 0;
+        tot += n[j];
+      }
+      int32_t incl = tot;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int32_t t = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += t;
+      }
+      const int64_t ix = D.ix;
+      const int32_t base = incl - tot;
+      const bool hold = tot > 0 && ix >= base && ix < incl;
+      if (hold) {
+        int64_t r = ix - base;
+        for (int j = 0; j < EPL; ++j) {
+          if (r < n[j]) {
+            const int e = lane * EPL + j;
+            const int k = NPT - 1 - e / ONE_WAVES, w = ONE_WAVES - 1 - e % ONE_WAVES;
+            uint64_t m = s_bm[k][w];
+            for (int64_t q = 0; q < r; ++q) m &= ~(1ull << (63 - __clzll(m)));
+            D.node = (int64_t)k * ONE_BLOCK + w * 64 + (63 - __clzll(m));
+            break;
+          }
+          r -= n[j];
+        }
+      }
+      const uint64_t held = __ballot(hold);
+      if (lane == 0 && !held) atomicOr(c.err, 2);  // inconsistent counts: must never happen
+    }
+    __syncthreads();
+    if (D.node >= 0 && !c.no_commit) {
+      if (wv == 0) {
+        const int32_t st = ksim_commit_wave(c, P, D.node, lane);
+        if (tid == 0) {
+          if (ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, D.node, 1, c.err);
+          if (c.out_fit) c.out_fit[1] |= st;
+        }
+      } else if (wv == 1 && ksim_is_aff_pod(c, P)) {
+        ksim_aff_commit_body(*c.aff, P, D.node, 1, lane, 64);
+      }
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    c.out_node[pod] = (int32_t)D.node;
+    if (c.out_fit) {  // fit count, error word and lastNodeIndex into the result block
+      c.out_fit[0] = D.fitTotal;
+      c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT] = (int32_t)(uint32_t)pre_ctr;
+      c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1] = (int32_t)(uint32_t)(pre_ctr >> 32);
+    }
+  }
+}
+
 // Per-node evaluation of one pod without commit (ksim_evaluate).
 __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_t pod, uint8_t* fit, uint32_t* reasons,
                                                              int64_t* score, uint8_t* rcls) {
@@ -806,6 +1130,29 @@ extern "C" hipError_t ksim_launch_scan(const KsimCtx* c, int npt, int collect, i
 }
 
 // Whether the scan grid is co-resident (the fused pass A's grid barrier needs it).
+// ksim_schedule_one on a cluster of n nodes in one workgroup (ksim_one_kernel): nodes per thread
+// (0: more than 16 x 512 nodes), and the launch.
+extern "C" int ksim_one_npt(int64_t n) {
+  for (int npt : {2, 4, 6, 8, 10, 12, 16})
+    if (n <= (int64_t)npt * ONE_BLOCK) return npt;
+  return 0;
+}
+extern "C" hipError_t ksim_launch_one(const KsimCtx* c, int npt, hipStream_t s) {
+#define KSIM_O(N) hipLaunchKernelGGL((ksim_one_kernel<N>), dim3(1), dim3(ONE_BLOCK), 0, s, *c)
+  switch (npt) {
+    case 2: KSIM_O(2); break;
+    case 4: KSIM_O(4); break;
+    case 6: KSIM_O(6); break;
+    case 8: KSIM_O(8); break;
+    case 10: KSIM_O(10); break;
+    case 12: KSIM_O(12); break;
+    case 16: KSIM_O(16); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef KSIM_O
+  return hipGetLastError();
+}
+
 extern "C" int ksim_scan_coresident(int npt, int collect, int grid) {
 #define KSIM_C(N, C) (ksim_check_coresident(ksim_scan_kernel<N, C>, grid, KSIM_BLOCK, 0) == hipSuccess)
   switch (npt) {

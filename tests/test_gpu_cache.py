@@ -17,6 +17,15 @@ from ksim.frontend import K8sCache
 pytestmark = pytest.mark.gpu
 IMPLS = {"py": SchedulerCache, "cpp": K8sCache}
 
+
+@pytest.fixture(autouse=True, params=["one_wg", "scan"])
+def per_pod_form(request, monkeypatch):
+    """Every per-pod call in the single-workgroup kernel (clusters up to 8,192 nodes: every
+    reduction in LDS) or in the multi-block scan kernel the larger clusters take: the same
+    decisions either way."""
+    monkeypatch.setenv("KSIM_ONE_WG", "0" if request.param == "scan" else "1")
+    return request.param
+
 POLICIES = {
     "default": scheduler.provider("DefaultProvider"),
     "talkintdata": scheduler.provider("TalkintDataProvider"),
