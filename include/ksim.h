@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 5
+#define KSIM_ABI_VERSION 6
 
 /* ---- status codes ---- */
 #define KSIM_OK 0
@@ -478,7 +478,24 @@ typedef struct {
    * deleted, that any of the pod's service / RC / RS / StatefulSet selectors selects — or -1;
    * NULL: no class spreads. */
   const int32_t* spread_pair;      /* [n_aclass] */
+  /* One auxiliary counted priority next to the slots of ksim_config.weights (a Policy's second
+   * spreading priority), NULL aux_pair: none.  aux_pair[a]: class a's counted pair (s, key 1) or -1;
+   * aux_key groups the fit nodes' counts by its domains; aux_weight: the priority's weight.
+   *  - KSIM_AUX_SPREAD: SelectorSpread's reduce (selector_spreading.go:121-174) over the pair, zones
+   *    from aux_key (ServiceSpreadingPriority configured next to SelectorSpreadPriority: its
+   *    services-only selectors);
+   *  - KSIM_AUX_SERVICE_ANTI: ServiceAntiAffinity (selector_spreading.go:180-275, a Policy priority
+   *    with a serviceAntiAffinity argument): the pair counts the pods of the pod's single selecting
+   *    service; a fit node without the aux_key label scores 0, one with value v
+   *    MaxPriority x (total - count(v)) / total over the fit nodes (MaxPriority when total = 0, and
+   *    for a class without a pair).  Scheduled by the launch-form kernels only. */
+  const int32_t* aux_pair;         /* [n_aclass] or NULL */
+  int32_t aux_key;                 /* -1 with aux_pair NULL */
+  int32_t aux_kind;                /* KSIM_AUX_* */
+  int64_t aux_weight;
 } ksim_affinity_tables;
+#define KSIM_AUX_SPREAD 0
+#define KSIM_AUX_SERVICE_ANTI 1
 
 /* Load (or replace) the affinity tables; the counts describe the pods already placed. */
 int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t);

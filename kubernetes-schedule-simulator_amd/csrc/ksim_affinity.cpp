@@ -88,6 +88,16 @@ int validate(ksim_handle* h, const ksim_affinity_tables* t) {
   }
   if (t->zone_key < -1 || t->zone_key >= t->n_keys)
     return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: zone key out of range");
+  if (t->aux_pair) {
+    if (t->aux_key < 0 || t->aux_key >= t->n_keys || (t->aux_kind != KSIM_AUX_SPREAD && t->aux_kind != KSIM_AUX_SERVICE_ANTI) ||
+        t->aux_weight < 0)
+      return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: auxiliary priority key / kind / weight out of range");
+    for (int32_t a = 0; a < t->n_aclass; ++a) {
+      const int32_t c = t->aux_pair[a];
+      if (c < -1 || c >= t->n_pair || (c >= 0 && t->pair_key[c] != 1))
+        return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: class %d auxiliary pair out of range", a);
+    }
+  }
   if (t->spread_pair)
     for (int32_t a = 0; a < t->n_aclass; ++a) {
       const int32_t c = t->spread_pair[a];
@@ -117,6 +127,8 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
   uint64_t *is, *ia, *ip;
   int64_t *po, *co, *carried, *mm, *part, *zsum, *zread;
   int32_t* spair = nullptr;
+  int32_t* apair = nullptr;
+  int64_t *asum = nullptr, *aread = nullptr;
   ksim_aff_term* terms;
   ksim_aff_carry* carries;
   uint32_t* ticket;
@@ -129,13 +141,18 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
       (rc = dev_upload(h, &co, t->carry_off, t->n_carry)) || (rc = dev_upload(h, &ac, t->ac, 6 * (size_t)t->n_aclass)) ||
       (rc = dev_upload(h, &terms, t->terms, t->n_terms)) || (rc = dev_upload(h, &carries, t->carries, t->n_carries)) ||
       (rc = dev_upload(h, &cnt, t->cnt, t->cnt_len)) || (rc = dev_upload(h, &carried, t->carried, t->carried_len)) ||
-      (rc = dev_upload<int64_t>(h, &mm, nullptr, 5)) || (rc = dev_upload<int64_t>(h, &part, nullptr, 4 * (size_t)grid_max)) ||
+      (rc = dev_upload<int64_t>(h, &mm, nullptr, KSIM_AFF_MM)) ||
+      (rc = dev_upload<int64_t>(h, &part, nullptr, KSIM_AFF_PART * (size_t)grid_max)) ||
       (rc = dev_upload<uint32_t>(h, &ticket, nullptr, 4)))
     return rc;
   const int32_t n_zone = t->zone_key >= 0 ? t->n_dom[t->zone_key] : 0;
   if ((rc = dev_upload<int64_t>(h, &zsum, nullptr, n_zone)) || (rc = dev_upload<int64_t>(h, &zread, nullptr, n_zone)))
     return rc;
   if (t->spread_pair && (rc = dev_upload(h, &spair, t->spread_pair, t->n_aclass))) return rc;
+  const int32_t n_adom = t->aux_pair ? t->n_dom[t->aux_key] : 0;
+  if (t->aux_pair && ((rc = dev_upload(h, &apair, t->aux_pair, t->n_aclass)) ||
+                      (rc = dev_upload<int64_t>(h, &asum, nullptr, n_adom)) || (rc = dev_upload<int64_t>(h, &aread, nullptr, n_adom))))
+    return rc;
   // node-like keys: every domain holds at most one node (the node pseudo key, a unique hostname
   // label), so a commit changes one row's counts; other keys' domains are shared by several nodes
   std::vector<uint8_t> nodelike(t->n_keys, 1);
@@ -196,6 +213,8 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
   A.pair_sel = ps; A.pair_key = pk; A.pair_off = po; A.carry_key = ck; A.carry_off = co;
   A.ac = ac; A.terms = terms; A.carries = carries; A.cnt = cnt; A.carried = carried;
   A.mm = mm; A.part = part; A.ticket = ticket;
+  A.aux_pair = apair; A.asum = asum; A.aread = aread; A.aux_w = t->aux_pair ? t->aux_weight : 0;
+  A.aux_key = t->aux_pair ? t->aux_key : -1; A.aux_kind = t->aux_kind; A.n_adom = n_adom;
   A.n_pair = t->n_pair;
   A.sel_words = t->sel_words;
   A.carry_words = t->carry_words;

@@ -365,7 +365,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   const int one_npt = ksim_one_npt(c.n);
   const char* ko = getenv("KSIM_ONE_WG");
   const bool one_wg = ko ? ko[0] != '0' : c.n <= 1024;
-  if (cs.one && one_npt > 0 && one_wg && (!h->have_aff || h->aff_h.n_zone <= 512)) {
+  if (cs.one && one_npt > 0 && one_wg && (!h->have_aff || h->aff_h.n_zone <= 512) && !ksim_rt_aux_on(h)) {
     h->res_host[KSIM_RES_NODE] = INT32_MIN;
     oc.lap(0);
     hipError_t e1 = ksim_launch_one(&cs, one_npt, h->stream);
@@ -395,7 +395,8 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   cs.pmask = c.pmask;
   // InterPodAffinity / SelectorSpread reductions (pass A): fused into the scan behind a grid barrier
   // when the grid is co-resident (one launch), else their own launch first
-  const bool ipa = ksim_is_aff_host(h, *pod) && (c.w[KSIM_W_INTERPOD_AFFINITY] || c.w[KSIM_W_SELECTOR_SPREAD]) && !c.no_prio;
+  const bool ipa = ksim_is_aff_host(h, *pod) &&
+                   (c.w[KSIM_W_INTERPOD_AFFINITY] || c.w[KSIM_W_SELECTOR_SPREAD] || ksim_rt_aux_on(h)) && !c.no_prio;
   cs.fuse_a = 0;
   if (ipa && !h->fuse_off) {
     const char* fz = getenv("KSIM_FUSE_A");
@@ -425,6 +426,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
     HIPCHK(h, hipMemset(c.ticket, 0, 16));
     HIPCHK(h, hipMemset(h->aff_h.ticket, 0, 16));
     if (h->aff_h.n_zone) HIPCHK(h, hipMemset(h->aff_h.zsum, 0, (size_t)h->aff_h.n_zone * 8));
+    if (h->aff_h.n_adom) HIPCHK(h, hipMemset(h->aff_h.asum, 0, (size_t)h->aff_h.n_adom * 8));
     h->fuse_off = true;
     return ksim_schedule_one(h, pod, ports, n_ports, scalars, n_scalars, assume, out);
   }

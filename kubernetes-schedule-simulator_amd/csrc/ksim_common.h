@@ -66,7 +66,18 @@ struct KsimAff {
   int32_t zone_key;                // -1: no zone key
   int32_t n_zone;
   int32_t pad;
+  // the auxiliary counted priority (ksim_affinity_tables.aux_*; launch form only), aux_pair null: none.
+  // Pass A adds mm[5] max count, mm[6] summed count, mm[7] haveZones, mm[8] max domain sum over the
+  // fit nodes, and per aux_key domain the fit nodes' summed counts (asum → aread, as zsum / zread)
+  const int32_t* __restrict__ aux_pair;  // [n_aclass]
+  int64_t* asum;
+  int64_t* aread;
+  int64_t aux_w;
+  int32_t aux_key, aux_kind, n_adom, pad2;
 };
+
+#define KSIM_AFF_MM 9      // pass-A result words
+#define KSIM_AFF_PART 8    // pass-A block-partial words
 
 // Volume tables on the device (ksim_load_volumes; layout in include/ksim.h).
 struct KsimVol {
@@ -494,6 +505,23 @@ __device__ __forceinline__ int64_t ksim_spread_score(int64_t cnt, int64_t max_no
     f = (f * (1.0 - zw)) + (zw * zs);
   }
   return (int64_t)f;
+}
+
+// The auxiliary priority's counted pair of pod P, or -1.
+__device__ __forceinline__ int32_t ksim_aux_pair(const KsimAff& A, const ksim_pod& P) {
+  return (A.aux_pair && P.aff_class > 0) ? A.aux_pair[P.aff_class - 1] : -1;
+}
+
+// The auxiliary priority's score of one fit node (ksim_affinity_tables.aux_*): cnt its count, d its
+// aux_key domain (-1: no label), dsum the fit nodes' summed count in d; the pass-A words amx (max
+// count), atot (summed count), ahz (haveZones), azmx (max domain sum).
+__device__ __forceinline__ int64_t ksim_aux_score(int32_t kind, int64_t cnt, int32_t d, int64_t dsum, int64_t amx,
+                                                  int64_t atot, bool ahz, int64_t azmx) {
+  if (kind == KSIM_AUX_SPREAD) return ksim_spread_score(cnt, amx, ahz, d, dsum, azmx);
+  // CalculateAntiAffinityPriorityReduce (selector_spreading.go:248-275): float64 as in Go
+  if (d < 0) return 0;
+  if (atot <= 0) return 10;
+  return (int64_t)(10.0 * ((double)(atot - dsum) / (double)atot));
 }
 
 __device__ __forceinline__ bool ksim_is_aff_pod(const KsimCtx& c, const ksim_pod& P) {

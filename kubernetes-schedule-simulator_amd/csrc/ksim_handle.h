@@ -269,3 +269,8 @@ int64_t ksim_rt_launch_only_count(const ksim_handle* h, int64_t first, int64_t c
 // KSIM_E_STATE when the affinity or volume tables are stale (a node event since they were loaded).
 int ksim_rt_check_aff(ksim_handle* h, const char* where);
 int ksim_rt_pick_npt(int64_t n);
+// The loaded affinity tables carry an auxiliary priority (ksim_affinity_tables.aux_*): only the
+// launch-form kernels read it, so every pod of such a handle takes that form.
+inline bool ksim_rt_aux_on(const ksim_handle* h) {
+  return h->have_aff && h->aff_h.aux_pair != nullptr && h->aff_h.aux_w != 0 && !h->ctx.no_prio;
+}

@@ -70,10 +70,15 @@ struct IpaNorm {
   int32_t sp;          // SelectorSpread counted pair, -1: off
   bool hz;             // haveZones
   int64_t sw, smx, szmx;
+  // the auxiliary priority (KsimAff::aux_*): aon = the pod reads it, ap = its counted pair (-1: no
+  // counts, no pass A), and the pass-A words
+  bool aon, ahz;
+  int32_t ap, akind;
+  int64_t aw, amx, atot, azmx;
 };
 
 __device__ __forceinline__ IpaNorm ipa_norm(const KsimCtx& c, const ksim_pod& P) {
-  IpaNorm z{false, 0, 0, 0, -1, false, 0, 0, 0};
+  IpaNorm z{false, 0, 0, 0, -1, false, 0, 0, 0, false, false, -1, 0, 0, 0, 0, 0};
   if (!c.aff || c.no_prio) return z;
   if (c.w[KSIM_W_INTERPOD_AFFINITY] != 0 && ksim_interpod_prio_work(*c.aff, P)) {
     z.on = true;
@@ -87,7 +92,28 @@ __device__ __forceinline__ IpaNorm ipa_norm(const KsimCtx& c, const ksim_pod& P)
     z.hz = c.aff->mm[3] != 0;
     z.szmx = c.aff->mm[4];
   }
+  const KsimAff& A = *c.aff;
+  if (A.aux_pair && A.aux_w != 0) {
+    z.ap = ksim_aux_pair(A, P);
+    z.akind = A.aux_kind;
+    // a pod without a pair: ServiceAntiAffinity still scores by the node's label (no counts);
+    // the spread reduce of zero counts is MaxPriority everywhere (a constant, left out)
+    z.aon = z.ap >= 0 || z.akind == KSIM_AUX_SERVICE_ANTI;
+    z.aw = A.aux_w;
+    if (z.ap >= 0) {
+      z.amx = A.mm[5];
+      z.atot = A.mm[6];
+      z.ahz = A.mm[7] != 0;
+      z.azmx = A.mm[8];
+    }
+  }
   return z;
+}
+
+// The auxiliary priority's weighted score of fit node i (count cnt, domain d): ap < 0 reads no count.
+__device__ __forceinline__ uint64_t aux_add(const KsimAff& A, const IpaNorm& z, int64_t cnt, int32_t d) {
+  const int64_t ds = (z.ap >= 0 && d >= 0) ? A.aread[d] : 0;
+  return (uint64_t)z.aw * (uint64_t)ksim_aux_score(z.akind, z.ap >= 0 ? cnt : 0, d, ds, z.amx, z.atot, z.ahz, z.azmx);
 }
 
 // Evaluate one node for the scan: fit, map score (+ the normalised InterPodAffinity score),
@@ -111,6 +137,11 @@ __device__ __forceinline__ void eval_one(const KsimCtx& c, const ksim_pod& P, in
     const int64_t v = ksim_spread_score(A.cnt[A.pair_off[ipa.sp] + i], ipa.smx, ipa.hz, z, z >= 0 ? A.zread[z] : 0, ipa.szmx);
     score = (int64_t)((uint64_t)score + (uint64_t)ipa.sw * (uint64_t)v);
   }
+  if (ipa.aon && fit) {
+    const KsimAff& A = *c.aff;
+    const int64_t cnt = ipa.ap >= 0 ? A.cnt[A.pair_off[ipa.ap] + i] : 0;
+    score = (int64_t)((uint64_t)score + aux_add(A, ipa, cnt, ksim_dom(A, A.aux_key, i)));
+  }
   cls = (k1 * k2 > 1) ? ksim_rclass(c, P, i, k1, k2) : 0;
 }
 
@@ -123,10 +154,12 @@ __device__ __forceinline__ void eval_one(const KsimCtx& c, const ksim_pod& P, in
 // in that block.  Run either as its own launch before the scan (ksim_ipa_pass_kernel) or fused
 // into the scan behind a grid barrier (KsimCtx::fuse_a).
 #define KSIM_PASS_ZONES 512
+#define KSIM_PASS_V 7   // pass-A words combined per wave (s_v rows)
 template <int NPT>
-__device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t sp, const bool (&fit)[NPT],
+__device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t sp, int32_t ap, const bool (&fit)[NPT],
                                              const int64_t (&raw)[NPT], const int64_t (&cnt)[NPT],
-                                             const int32_t (&zz)[NPT], int64_t (*s_v)[KSIM_WAVES],
+                                             const int32_t (&zz)[NPT], const int64_t (&acnt)[NPT],
+                                             const int32_t (&azz)[NPT], int64_t (*s_v)[KSIM_WAVES],
                                              unsigned long long* s_z, int* s_last) {
   const KsimAff& A = *c.aff;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -135,7 +168,7 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t
     for (int z = tid; z < A.n_zone; z += KSIM_BLOCK) s_z[z] = 0;
     __syncthreads();
   }
-  int64_t mn = 0, mx = 0, smx = 0, hz = 0;
+  int64_t mn = 0, mx = 0, smx = 0, hz = 0, amx = 0, atot = 0, ahz = 0;
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     if (!fit[k]) continue;
@@ -153,6 +186,15 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t
           if (zlocal) atomicAdd(&s_z[z], (unsigned long long)v);
           else atomicAdd(reinterpret_cast<unsigned long long*>(&A.zsum[z]), (unsigned long long)v);
         }
+      }
+    }
+    if (ap >= 0) {  // the auxiliary priority: max, sum, haveZones and per-domain sums (global adds)
+      const int64_t v = acnt[k];
+      amx = v > amx ? v : amx;
+      atot += v;
+      if (azz[k] >= 0) {
+        ahz = 1;
+        if (v) atomicAdd(reinterpret_cast<unsigned long long*>(&A.asum[azz[k]]), (unsigned long long)v);
       }
     }
   }
@@ -173,8 +215,17 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t
       mx = b > mx ? b : mx;
       smx = d > smx ? d : smx;
       hz = e > hz ? e : hz;
+      if (ap >= 0) {
+        const int64_t f = __shfl_xor(amx, o, 64), g = __shfl_xor(atot, o, 64), q = __shfl_xor(ahz, o, 64);
+        amx = f > amx ? f : amx;
+        atot += g;
+        ahz = q > ahz ? q : ahz;
+      }
     }
-    if (lane == 0) { s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz; }
+    if (lane == 0) {
+      s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz;
+      s_v[4][wv] = amx; s_v[5][wv] = atot; s_v[6][wv] = ahz;
+    }
     __syncthreads();
     if (tid == 0) {
       for (int w = 1; w < KSIM_WAVES; ++w) {
@@ -182,13 +233,17 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t
         mx = s_v[1][w] > mx ? s_v[1][w] : mx;
         smx = s_v[2][w] > smx ? s_v[2][w] : smx;
         hz = s_v[3][w] > hz ? s_v[3][w] : hz;
+        amx = s_v[4][w] > amx ? s_v[4][w] : amx;
+        atot += s_v[5][w];
+        ahz = s_v[6][w] > ahz ? s_v[6][w] : ahz;
       }
     }
   };
   combine();
   if (tid == 0) {
-    int64_t* pp = A.part + 4 * (int64_t)blockIdx.x;
+    int64_t* pp = A.part + KSIM_AFF_PART * (int64_t)blockIdx.x;
     pp[0] = mn; pp[1] = mx; pp[2] = smx; pp[3] = hz;
+    pp[4] = amx; pp[5] = atot; pp[6] = ahz;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const uint32_t old = __hip_atomic_fetch_add(A.ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -199,20 +254,25 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t
   if (tid == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  mn = 0; mx = 0; smx = 0; hz = 0;
+  mn = 0; mx = 0; smx = 0; hz = 0; amx = 0; atot = 0; ahz = 0;
   for (int b = tid; b < (int)gridDim.x; b += KSIM_BLOCK) {
-    const int64_t* pp = A.part + 4 * (int64_t)b;
+    const int64_t* pp = A.part + KSIM_AFF_PART * (int64_t)b;
     mn = pp[0] < mn ? pp[0] : mn;
     mx = pp[1] > mx ? pp[1] : mx;
     smx = pp[2] > smx ? pp[2] : smx;
     hz = pp[3] > hz ? pp[3] : hz;
+    if (ap >= 0) {
+      amx = pp[4] > amx ? pp[4] : amx;
+      atot += pp[5];
+      ahz = pp[6] > ahz ? pp[6] : ahz;
+    }
   }
   __syncthreads();
   combine();
   __syncthreads();
-  const int64_t r0 = mn, r1 = mx, r2 = smx, r3 = hz;  // valid in thread 0
+  const int64_t r0 = mn, r1 = mx, r2 = smx, r3 = hz, r5 = amx, r6 = atot, r7 = ahz;  // valid in thread 0
   // zone sums: publish for the scan, zero for the next pod, maximum (countsByZone, :139-143)
-  int64_t zmx = 0;
+  int64_t zmx = 0, azm = 0;
   if (sp >= 0)
     for (int z = tid; z < A.n_zone; z += KSIM_BLOCK) {
       const int64_t v = __hip_atomic_load(&A.zsum[z], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -220,20 +280,35 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t
       A.zsum[z] = 0;
       zmx = v > zmx ? v : zmx;
     }
+  if (ap >= 0)
+    for (int z = tid; z < A.n_adom; z += KSIM_BLOCK) {
+      const int64_t v = __hip_atomic_load(&A.asum[z], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      A.aread[z] = v;
+      A.asum[z] = 0;
+      azm = v > azm ? v : azm;
+    }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const int64_t a = __shfl_xor(zmx, o, 64);
+    const int64_t a = __shfl_xor(zmx, o, 64), b = __shfl_xor(azm, o, 64);
     zmx = a > zmx ? a : zmx;
+    azm = b > azm ? b : azm;
   }
-  if (lane == 0) s_v[0][wv] = zmx;
+  if (lane == 0) { s_v[0][wv] = zmx; s_v[1][wv] = azm; }
   __syncthreads();
   if (tid == 0) {
-    for (int w = 1; w < KSIM_WAVES; ++w) zmx = s_v[0][w] > zmx ? s_v[0][w] : zmx;
+    for (int w = 1; w < KSIM_WAVES; ++w) {
+      zmx = s_v[0][w] > zmx ? s_v[0][w] : zmx;
+      azm = s_v[1][w] > azm ? s_v[1][w] : azm;
+    }
     A.mm[0] = r0;
     A.mm[1] = r1;
     A.mm[2] = r2;
     A.mm[3] = r3;
     A.mm[4] = zmx;
+    A.mm[5] = r5;
+    A.mm[6] = r6;
+    A.mm[7] = r7;
+    A.mm[8] = azm;
     *A.ticket = 0;
   }
   return true;
@@ -242,7 +317,7 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t
 // Pass A as its own launch (pods that read neither priority exit at once, uniformly).
 template <int NPT>
 __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
-  __shared__ int64_t s_v[4][KSIM_WAVES];
+  __shared__ int64_t s_v[KSIM_PASS_V][KSIM_WAVES];
   __shared__ unsigned long long s_z[KSIM_PASS_ZONES];  // block-local zone sums (few zones: no global contention)
   __shared__ int s_last;
   const int64_t pod = c.one ? c.first : *c.cursor;
@@ -253,15 +328,16 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
   const KsimAff& A = *c.aff;
   const bool ipa = c.w[KSIM_W_INTERPOD_AFFINITY] != 0 && ksim_interpod_prio_work(A, P);
   const int32_t sp = c.w[KSIM_W_SELECTOR_SPREAD] != 0 ? ksim_spread_pair(A, P) : -1;
-  if (!ipa && sp < 0) return;
+  const int32_t ap = A.aux_w != 0 ? ksim_aux_pair(A, P) : -1;
+  if (!ipa && sp < 0 && ap < 0) return;
   const int64_t base = (int64_t)blockIdx.x * c.chunk;
   bool fit[NPT];
-  int64_t raw[NPT], cnt[NPT];
-  int32_t zz[NPT];
+  int64_t raw[NPT], cnt[NPT], acnt[NPT];
+  int32_t zz[NPT], azz[NPT];
 #pragma unroll
   for (int k = 0; k < NPT; ++k) {
     const int64_t i = base + k * KSIM_BLOCK + threadIdx.x;
-    fit[k] = false; raw[k] = 0; cnt[k] = 0; zz[k] = -1;
+    fit[k] = false; raw[k] = 0; cnt[k] = 0; zz[k] = -1; acnt[k] = 0; azz[k] = -1;
     if (i >= c.n) continue;
     const KsimRow r = ksim_load_row(c, i);
     if (ksim_predicates(c, P, i, r) != 0) continue;
@@ -271,8 +347,12 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
       cnt[k] = A.cnt[A.pair_off[sp] + i];
       zz[k] = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
     }
+    if (ap >= 0) {
+      acnt[k] = A.cnt[A.pair_off[ap] + i];
+      azz[k] = ksim_dom(A, A.aux_key, i);
+    }
   }
-  (void)passa_reduce<NPT>(c, ipa, sp, fit, raw, cnt, zz, s_v, s_z, &s_last);
+  (void)passa_reduce<NPT>(c, ipa, sp, ap, fit, raw, cnt, zz, acnt, azz, s_v, s_z, &s_last);
 }
 
 // diagnostic builds (make stamps): thread 0's cycles per scan phase, summed over blocks into
@@ -314,7 +394,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   __shared__ uint64_t s_ball[NPT][KSIM_WAVES];
   __shared__ int s_last;
   __shared__ Decision D;
-  __shared__ int64_t s_v[4][KSIM_WAVES];               // fused pass A
+  __shared__ int64_t s_v[KSIM_PASS_V][KSIM_WAVES];     // fused pass A
   __shared__ unsigned long long s_z[KSIM_PASS_ZONES];
   __shared__ uint32_t s_gen;
   __shared__ int s_bail;
@@ -367,11 +447,12 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   // fused pass A (KsimCtx::fuse_a, grid co-resident): this pod's pass-A reductions run over the
   // fit nodes evaluated here, behind one grid barrier (generation word ticket[1], read before
   // this block's pass-A ticket), and the normalised scores are added afterwards
-  const bool fuse = c.fuse_a && (ipa.on || ipa.sp >= 0);
+  const bool fuse = c.fuse_a && (ipa.on || ipa.sp >= 0 || ipa.ap >= 0);
   IpaNorm ipa0 = ipa;
   if (fuse) {
     ipa0.on = false;
     ipa0.sp = -1;
+    if (ipa.ap >= 0) ipa0.aon = false;
     if (tid == 0) {
       s_bail = 0;
       s_gen = __hip_atomic_load(c.ticket + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -393,20 +474,24 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
 
   if (fuse) {
     const KsimAff& A = *c.aff;
-    int64_t raw[NPT], cnt[NPT];
-    int32_t zz[NPT];
+    int64_t raw[NPT], cnt[NPT], acnt[NPT];
+    int32_t zz[NPT], azz[NPT];
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int64_t i = base + k * KSIM_BLOCK + tid;
-      raw[k] = 0; cnt[k] = 0; zz[k] = -1;
+      raw[k] = 0; cnt[k] = 0; zz[k] = -1; acnt[k] = 0; azz[k] = -1;
       if (!fit[k]) continue;
       if (ipa.on) raw[k] = ksim_interpod_raw_body(A, P, i);
       if (ipa.sp >= 0) {
         cnt[k] = A.cnt[A.pair_off[ipa.sp] + i];
         zz[k] = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
       }
+      if (ipa.ap >= 0) {
+        acnt[k] = A.cnt[A.pair_off[ipa.ap] + i];
+        azz[k] = ksim_dom(A, A.aux_key, i);
+      }
     }
-    if (passa_reduce<NPT>(c, ipa.on, ipa.sp, fit, raw, cnt, zz, s_v, s_z, &s_last)) {
+    if (passa_reduce<NPT>(c, ipa.on, ipa.sp, ipa.ap, fit, raw, cnt, zz, acnt, azz, s_v, s_z, &s_last)) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's zread stores
       __syncthreads();
       if (tid == 0) {
@@ -434,7 +519,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     }
     ipa = ipa_norm(c, P);  // the combined maxima
 #pragma unroll
-    for (int k = 0; k < NPT; ++k) {  // eval_one's additions, same order
+    for (int k = 0; k < NPT; ++k) {  // eval_one's additions (modular sums: any order)
       if (!fit[k]) continue;
       if (ipa.on)
         sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)ipa.w * (uint64_t)ksim_interpod_score(raw[k], ipa.mn, ipa.mx));
@@ -442,6 +527,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
         const int64_t v = ksim_spread_score(cnt[k], ipa.smx, ipa.hz, zz[k], zz[k] >= 0 ? A.zread[zz[k]] : 0, ipa.szmx);
         sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)ipa.sw * (uint64_t)v);
       }
+      if (ipa.ap >= 0) sc[k] = (int64_t)((uint64_t)sc[k] + aux_add(A, ipa, acnt[k], azz[k]));
     }
   }
 

@@ -495,7 +495,8 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
   HIPCHK(h, hipMemsetAsync(c.ticket, 0, 16, h->stream));
   const int batch = (int)std::min<int64_t>(count, 256);
   const int ipa = ksim_rt_aff_count(h, first, count) > 0 &&
-                  (c.w[KSIM_W_INTERPOD_AFFINITY] != 0 || c.w[KSIM_W_SELECTOR_SPREAD] != 0) && !c.no_prio ? 1 : 0;
+                  (c.w[KSIM_W_INTERPOD_AFFINITY] != 0 || c.w[KSIM_W_SELECTOR_SPREAD] != 0 || ksim_rt_aux_on(h)) &&
+                  !c.no_prio ? 1 : 0;
   // pass A fused into the scan behind a grid barrier when the grid is co-resident (KSIM_FUSE_A=0: two launches)
   const char* fz = getenv("KSIM_FUSE_A");
   c.fuse_a = ipa && !h->fuse_off && !(fz && fz[0] == '0') && ksim_scan_coresident(npt, c.collect, grid) ? 1 : 0;
@@ -548,6 +549,7 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
       HIPCHK(h, hipMemset(c.ticket, 0, 16));
       HIPCHK(h, hipMemset(h->aff_h.ticket, 0, 16));
       if (h->aff_h.n_zone) HIPCHK(h, hipMemset(h->aff_h.zsum, 0, (size_t)h->aff_h.n_zone * 8));
+      if (h->aff_h.n_adom) HIPCHK(h, hipMemset(h->aff_h.asum, 0, (size_t)h->aff_h.n_adom * 8));
       h->fuse_off = true;
       if (cur < first + count) {
         ksim_stats s2{};
@@ -673,7 +675,7 @@ struct PgPlan {
 
 static bool pgen_plan(ksim_handle* h, PgPlan* pl, bool allow_v2 = true) {
   const KsimCtx& c = h->ctx;
-  if (getenv("KSIM_NO_PGEN") || h->pgen_off || h->shard.world > 1 || c.n <= 0) return false;
+  if (getenv("KSIM_NO_PGEN") || h->pgen_off || h->shard.world > 1 || c.n <= 0 || ksim_rt_aux_on(h)) return false;
   int64_t s = 0;
   for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED, KSIM_W_INTERPOD_AFFINITY,
                 KSIM_W_SELECTOR_SPREAD}) {
@@ -1160,7 +1162,8 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
       return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded run stopped: a node's quantities left the exact float64 range");
     }
   } else {
-  const int mode = h->cfg.mode;
+  // the auxiliary priority (ksim_affinity_tables.aux_*) is read by the launch-form kernels alone
+  const int mode = ksim_rt_aux_on(h) ? KSIM_MODE_LAUNCH : h->cfg.mode;
   int rc = mode == KSIM_MODE_TREE         ? run_tree_mode(h, first, count, st)
            : mode == KSIM_MODE_AUTO       ? run_auto_mode(h, first, count, st)
            : mode == KSIM_MODE_PERSISTENT ? run_persistent_mode(h, first, count, st)

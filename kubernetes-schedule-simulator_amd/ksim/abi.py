@@ -14,7 +14,7 @@ LIB_PATH = os.environ.get("KSIM_LIB") or os.path.join(PKG_DIR, "lib", "libksim.s
 
 KSIM_OK = 0
 E_INVAL, E_DEVICE, E_NOMEM, E_UNSUPPORTED, E_STATE, E_OVERFLOW, E_NO_NODES = -1, -2, -3, -4, -5, -6, -7
-ABI_VERSION = 5
+ABI_VERSION = 6
 MAX_SCALAR = 8
 MAX_RCLASS = 16
 NREASONS = 32
@@ -138,7 +138,11 @@ class AffinityTables(C.Structure):
                 ("dom", _i32p), ("n_dom", _i32p), ("ident_sel", _u64p), ("ident_anti", _u64p), ("ident_prio", _u64p),
                 ("pair_sel", _i32p), ("pair_key", _i32p), ("pair_off", _i64p), ("carry_key", _i32p),
                 ("carry_kind", _i32p), ("carry_off", _i64p), ("ac", _i32p), ("terms", C.c_void_p),
-                ("carries", C.c_void_p), ("cnt", _i32p), ("carried", _i64p), ("spread_pair", _i32p)]
+                ("carries", C.c_void_p), ("cnt", _i32p), ("carried", _i64p), ("spread_pair", _i32p),
+                ("aux_pair", _i32p), ("aux_key", C.c_int32), ("aux_kind", C.c_int32), ("aux_weight", C.c_int64)]
+
+
+AUX_SPREAD, AUX_SERVICE_ANTI = 0, 1
 
 
 class VolumeTables(C.Structure):

@@ -121,7 +121,8 @@ class AffinityIndex:
         self.pairs = _Interner()                  # (sel, key)
         self.carry = _Interner()                  # (sel, key, kind)
         self.idents = _Interner()                 # (namespace, labels)
-        self.aclasses = _Interner()               # → (required terms, preferred terms, carries)
+        self.aclasses = _Interner()               # → (required terms, preferred terms, carries, spread, aux)
+        self.aux_key, self.aux_kind = None, abi.AUX_SPREAD   # the auxiliary priority (aux_pair), if any
 
     # ---------------------------------------------------------------- interning
     def _sel(self, defining_pod, term):
@@ -158,12 +159,35 @@ class AffinityIndex:
         self.keys.get(ZONE_KEY)
         return self.pairs.get((s, KEY_NODE))
 
-    def aclass(self, pod, spread_sels=()):
-        """The pod's own terms, carried terms and SelectorSpread pair, interned; -1 when it has
-        none of them."""
+    def set_aux(self, kind, key):
+        """Configure the auxiliary counted priority (include/ksim.h ksim_affinity_tables.aux_*):
+        kind abi.AUX_SPREAD (zones: key ZONE_KEY) or abi.AUX_SERVICE_ANTI (key: the label)."""
+        self.aux_kind, self.aux_key = kind, key
+        self.keys.get(key)
+
+    def aux_pair(self, pod, sels):
+        """The pod's counted pair for the auxiliary priority, or -1: abi.AUX_SPREAD takes the
+        services-only SelectorSpread selectors (any of them, not being deleted); abi.AUX_SERVICE_ANTI
+        the one selecting service's selector as a plain set selector over the pod's namespace
+        (filteredPod, selector_spreading.go:232-245: deleting pods count)."""
+        if self.aux_key is None or not sels:
+            return -1
+        ns = _meta(pod).get("namespace", "")
+        if self.aux_kind == abi.AUX_SPREAD:
+            key = ("\x00spread", ns, repr(list(sels)))
+            s = self.sels.get(key, (frozenset([ns]), _AnyOf(sels)))
+        else:
+            (sel,) = sels          # a ksim.labels selector (SpreadListers.selectors)
+            s = self.sels.get(((ns,), tuple(sel)), (frozenset([ns]), sel))
+        return self.pairs.get((s, KEY_NODE))
+
+    def aclass(self, pod, spread_sels=(), aux_sels=()):
+        """The pod's own terms, carried terms, SelectorSpread pair and auxiliary pair, interned; -1
+        when it has none of them."""
         sp = self.spread_pair(pod, spread_sels)
+        ap = self.aux_pair(pod, aux_sels)
         if not has_pod_affinity(pod):
-            return -1 if sp < 0 else self.aclasses.get(((), (), (), sp))
+            return -1 if sp < 0 and ap < 0 else self.aclasses.get(((), (), (), sp, ap))
         a = _aff(pod)
         name = _meta(pod).get("name")
         req, pref, carries = [], [], {}
@@ -219,9 +243,9 @@ class AffinityIndex:
                 carry(wt.get("podAffinityTerm") or {}, abi.AFF_CARRY_PRIO, -int(wt.get("weight", 0)))
         carries = tuple(sorted((e, v) for e, v in carries.items() if v != 0 or self.carry.items[e][2] == abi.AFF_CARRY_ANTI))
         req.sort(key=lambda r: r[0] != abi.AFF_REQ_AFFINITY)   # affinity terms are checked before anti-affinity
-        if not req and not pref and not carries and sp < 0:
+        if not req and not pref and not carries and sp < 0 and ap < 0:
             return -1
-        return self.aclasses.get((tuple(req), tuple(pref), carries, sp))
+        return self.aclasses.get((tuple(req), tuple(pref), carries, sp, ap))
 
     # ------------------------------------------------------------------ tables
     def build(self, running_nodes, idents, aclasses):
@@ -294,7 +318,8 @@ class AffinityIndex:
         terms, carries = [], []
         ac = np.zeros((A, 6), np.int32)   # req_off, req_cnt, pref_off, pref_cnt, carry_off, carry_cnt
         spread_pair = np.array([x[3] for x in self.aclasses.items], np.int32) if A else np.zeros(0, np.int32)
-        for a, (req, pref, car, _) in enumerate(self.aclasses.items):
+        aux_pair = np.array([x[4] for x in self.aclasses.items], np.int32) if A else np.zeros(0, np.int32)
+        for a, (req, pref, car, _, _) in enumerate(self.aclasses.items):
             ac[a, 0], ac[a, 1] = len(terms), len(req)
             terms.extend(req)
             ac[a, 2], ac[a, 3] = len(terms), len(pref)
@@ -329,7 +354,9 @@ class AffinityIndex:
                     carry_kind=carry_kind, carry_sel=carry_sel, carry_off=carry_off,
                     ac=np.ascontiguousarray(ac), terms=terms_a, carries=carries_a, cnt=cnt, carried=carried,
                     zone_key=self.keys.ids.get(ZONE_KEY, -1), spread_pair=spread_pair,
-                    n_terms=len(terms), n_carries=len(carries)), remap
+                    aux_pair=aux_pair if self.aux_key is not None else None,
+                    aux_key=self.keys.ids[self.aux_key] if self.aux_key is not None else -1, aux_kind=self.aux_kind,
+                    aux_weight=0, n_terms=len(terms), n_carries=len(carries)), remap
 
 
 def tables_struct(d):
@@ -350,6 +377,12 @@ def tables_struct(d):
     d["carries"] = np.ascontiguousarray(d["carries"])
     t.terms = d["terms"].ctypes.data_as(abi.C.c_void_p)
     t.carries = d["carries"].ctypes.data_as(abi.C.c_void_p)
+    if d.get("aux_pair") is not None and int(d.get("aux_weight", 0)):
+        d["aux_pair"] = np.ascontiguousarray(d["aux_pair"], np.int32)
+        t.aux_pair = abi.ptr(d["aux_pair"], abi.C.c_int32)
+        t.aux_key, t.aux_kind, t.aux_weight = int(d["aux_key"]), int(d["aux_kind"]), int(d["aux_weight"])
+    else:
+        t.aux_key = -1
     t.n_terms = int(d.get("n_terms", len(d["terms"])))       # the arrays are padded to one entry
     t.n_carries = int(d.get("n_carries", len(d["carries"])))
     t.cnt_len = len(d["cnt"])

@@ -363,12 +363,16 @@ class Cluster:
         self.hard_weight = 10
         self.volume_index = None  # ksim/volumes.py VolumeIndex when a pod has predicate volumes
         self.volumes = None       # its device tables (volumes.build_tables)
+        self.spread_active = False
+        self.aux = None           # the auxiliary spreading priority (from_objects(aux=...))
+        self.aux_sels = []
+        self.aux_active = False   # some queued pod has a counted auxiliary pair
 
     # ------------------------------------------------------------------ nodes
     @classmethod
     def from_objects(cls, nodes, running_pods=(), pods=(), port_slots=None, hard_weight=10, pvs=(), pvcs=(),
                      storage_classes=(), max_vols=None, vol_slots=None, spread=None, spread_services_only=False,
-                     image_locality=None):
+                     image_locality=None, aux=None):
         """nodes / running_pods / pods: Kubernetes-shaped dicts; pods are in SCHEDULING
         order (the caller resolves the simulator's LIFO queue).  hard_weight:
         hardPodAffinitySymmetricWeight (the simulator's 10, or a Policy's).  pvs / pvcs /
@@ -377,7 +381,10 @@ class Cluster:
         spread: ksim.spread.SpreadListers (services / RCs / RSs / StatefulSets) for SelectorSpread
         (spread_services_only: ServiceSpreadingPriority's services-only form); None: the simulator's
         empty listers.  image_locality: intern node / pod images (what ImageLocalityPriority reads;
-        default: when some node lists status.images)."""
+        default: when some node lists status.images).  aux: a second counted spreading priority over
+        `spread`'s services (include/ksim.h ksim_affinity_tables.aux_*): ("service_spreading",) —
+        ServiceSpreadingPriority next to SelectorSpreadPriority — or ("service_anti_affinity", label),
+        a Policy's serviceAntiAffinity priority; None: neither."""
         self = cls()
         self.hard_weight = int(hard_weight)
         self.image_locality = (any((x.get("status") or {}).get("images") for x in nodes) if image_locality is None
@@ -396,7 +403,17 @@ class Cluster:
         with_pod_affinity = any(has_pod_affinity(p) for p in list(running_pods) + list(pods))
         self.spread_sels = [spread.selectors(p, spread_services_only) if spread else [] for p in pods]
         self.spread_active = any(self.spread_sels)
-        with_affinity = with_pod_affinity or self.spread_active
+        self.aux = aux
+        self.aux_sels = [spread.selectors(p, True) if (spread and aux) else [] for p in pods]
+        if aux and aux[0] == "service_anti_affinity":
+            for p, s in zip(pods, self.aux_sels):
+                if len(s) > 1:
+                    # getFirstServiceSelector takes the ServiceLister's first (selector_spreading.go:
+                    # 232-245), an informer-cache order: ambiguous unless one service selects the pod
+                    raise Unsupported("ServiceAntiAffinity: %d services select pod %r (the service lister's order "
+                                      "decides)" % (len(s), _meta(p).get("name")))
+        self.aux_active = any(self.aux_sels)
+        with_affinity = with_pod_affinity or self.spread_active or self.aux_active
         if with_pod_affinity and len(running) != len([p for p in running_pods if _spec(p).get("nodeName")]):
             # the reference caches them under a node-less NodeInfo: its affinity metadata then
             # errors and the predicate takes another path (metadata.go:106-109)
@@ -545,12 +562,16 @@ class Cluster:
     def _build_affinity(self, nodes, running, pods):
         """Inter-pod affinity tables over every pod's identity and terms (ksim/affinity.py); the
         queued descriptors get their aff_ident / aff_class."""
-        from .affinity import AffinityIndex
+        from .affinity import ZONE_KEY, AffinityIndex
         idx = AffinityIndex([_meta(x).get("labels") for x in nodes], self.hard_weight)
         allp = list(running) + list(pods)
         idents = [idx.ident(p) for p in allp]
         sels = [()] * len(running) + list(self.spread_sels)
-        aclasses = [idx.aclass(p, s) for p, s in zip(allp, sels)]
+        asels = [()] * len(running) + list(self.aux_sels)
+        if self.aux_active:
+            idx.set_aux(abi.AUX_SPREAD, ZONE_KEY) if self.aux[0] == "service_spreading" else \
+                idx.set_aux(abi.AUX_SERVICE_ANTI, self.aux[1])
+        aclasses = [idx.aclass(p, s, a) for p, s, a in zip(allp, sels, asels)]
         run_nodes = [self.index[_spec(p)["nodeName"]] for p in running]
         self.affinity, remap = idx.build(run_nodes, idents, aclasses)
         k = len(running)

@@ -85,9 +85,11 @@ def provider(name: str):
 
 
 def make_config(predicates, priorities, device=0, mode=abi.MODE_AUTO, collect_reasons=True, last_node_index=0,
-                spread=False):
+                spread=False, configured=None):
     """spread: the cluster has SelectorSpread selectors (Cluster.spread_active): the spread priority
-    scores per node (KSIM_W_SELECTOR_SPREAD) instead of being the constant MaxPriority."""
+    scores per node (KSIM_W_SELECTOR_SPREAD) instead of being the constant MaxPriority.
+    configured: the whole prioritizer list when `priorities` leaves some out (Policy priorities
+    with arguments, the auxiliary priority): only an empty one means EqualPriorityMap."""
     cfg = abi.Config()
     cfg.device = device
     cfg.mode = mode
@@ -116,8 +118,9 @@ def make_config(predicates, priorities, device=0, mode=abi.MODE_AUTO, collect_re
             const += CONST_PRIORITIES[name] * w
         else:
             raise Unsupported("priority %r is outside the supported key set" % name)
-    cfg.no_priorities = 1 if not priorities else 0
-    if not priorities:
+    empty = not (priorities if configured is None else configured)
+    cfg.no_priorities = 1 if empty else 0
+    if empty:
         const = 1
     cfg.const_score = const
     cfg.collect_reasons = 1 if collect_reasons else 0
@@ -307,8 +310,31 @@ def plan(cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO,
     predicates = list(predicates)
     prioritizers = list(priorities)
     custom_priorities = dict(custom_priorities or {})
-    if any(s[0] == "serviceAntiAffinity" for s in custom_priorities.values()) and getattr(cluster, "spread_active", False):
-        raise Unsupported("a serviceAntiAffinity priority with services selecting the pods")
+    aux = getattr(cluster, "aux", None)
+    aux_active = bool(getattr(cluster, "aux_active", False))
+    aux_weight, aux_const = 0, 0
+    saa = [(n, int(w)) for n, w in prioritizers if n in custom_priorities and custom_priorities[n][0] == "serviceAntiAffinity"]
+    if saa and aux is not None and aux[0] == "service_anti_affinity" and aux_active:
+        # ServiceAntiAffinity with services: the auxiliary counted priority (the pods' single
+        # selecting service; Cluster.from_objects refused two or more)
+        if len(saa) > 1 or custom_priorities[saa[0][0]][1] != aux[1]:
+            raise Unsupported("serviceAntiAffinity priorities other than the one the cluster was built for (%r)" % (aux[1],))
+        aux_weight = saa[0][1]
+        prioritizers = [(n, w) for n, w in prioritizers if n != saa[0][0]]
+        custom_priorities.pop(saa[0][0])
+    elif saa and getattr(cluster, "spread_active", False) and not (aux is not None and aux[0] == "service_anti_affinity"):
+        raise Unsupported("a serviceAntiAffinity priority with services selecting the pods needs the cluster built "
+                          "with aux=('service_anti_affinity', label)")
+    names = {n for n, _ in prioritizers}
+    if aux is not None and aux[0] == "service_spreading" and {"SelectorSpreadPriority", "ServiceSpreadingPriority"} <= names:
+        # ServiceSpreadingPriority next to SelectorSpreadPriority: the auxiliary counted priority over
+        # the services-only selectors (MaxPriority everywhere, a constant, when none selects a pod)
+        w = sum(int(x) for n, x in prioritizers if n == "ServiceSpreadingPriority")
+        if aux_active:
+            aux_weight = w
+        else:
+            aux_const = 10 * w
+        prioritizers = [(n, x) for n, x in prioritizers if n != "ServiceSpreadingPriority"]
     if any(n == "NodeAffinityPriority" for n, _ in prioritizers) and cluster.bad_affinity_classes:
         raise Unsupported("NodeAffinityPriority: a preferred node-affinity term does not parse")
     if (any(n == "ImageLocalityPriority" for n, _ in prioritizers) and cluster.node_images
@@ -325,7 +351,7 @@ def plan(cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO,
     cfg = make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence],
                       [(n, w) for n, w in prioritizers if n not in custom_priorities],
                       device, mode, collect_reasons, last_node_index,
-                      spread=bool(getattr(cluster, "spread_active", False)))
+                      spread=bool(getattr(cluster, "spread_active", False)), configured=list(priorities))
     check_volume_support(cluster, predicates)
     flags = None
     if label_presence is not None and "CheckNodeLabelPresence" in predicates:
@@ -335,7 +361,7 @@ def plan(cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO,
     tables, na_add = class_tables_for(cluster.tables, prioritizers, cluster.label_sets.items, custom_priorities)
     # const_score without NodePreferAvoidPods when its per-class addends carry it
     const_score = cfg.const_score - (10 * sum(int(x) for n, x in prioritizers if n == "NodePreferAvoidPodsPriority")
-                                     if tables.get("pa_in_add") else 0)
+                                     if tables.get("pa_in_add") else 0) + aux_const
     pods = np.ascontiguousarray(cluster.pods)
     if "CheckServiceAffinity" in predicates:
         ok, need = service_affinity_table(cluster.classes.items or [{}], cluster.label_sets.items, service_affinity)
@@ -345,9 +371,10 @@ def plan(cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO,
             pods["flags"] |= np.where(need[pods["cls"]], abi.POD_NEED_SVC_AFFINITY, 0).astype(np.uint32)
     affinity = None
     if cluster.affinity is not None:
-        if cfg.predicates & abi.P_INTERPOD_AFFINITY or ((cfg.weights[abi.W_INTERPOD] or cfg.weights[abi.W_SPREAD])
+        if cfg.predicates & abi.P_INTERPOD_AFFINITY or ((cfg.weights[abi.W_INTERPOD] or cfg.weights[abi.W_SPREAD] or aux_weight)
                                                         and not cfg.no_priorities):
-            affinity = cluster.affinity
+            affinity = dict(cluster.affinity, aux_weight=aux_weight) if cluster.affinity.get("aux_pair") is not None \
+                else cluster.affinity
         elif len(pods):  # neither MatchInterPodAffinity nor its priority: the terms change nothing
             pods = pods.copy()
             pods["aff_ident"] = 0
@@ -652,11 +679,17 @@ class ClusterCapacity:
         self.running = list(running_pods)
         # pvs / pvcs / storage_classes: the simulator's listers are empty; other callers may fill them
         names = {n for n, _ in priorities}
-        if spread and {"SelectorSpreadPriority", "ServiceSpreadingPriority"} <= names:
-            raise Unsupported("SelectorSpreadPriority and ServiceSpreadingPriority together with spread listers")
+        both = {"SelectorSpreadPriority", "ServiceSpreadingPriority"} <= names
+        saa = [custom[n][1] for n in names if custom and n in custom and custom[n][0] == "serviceAntiAffinity"]
+        if both and saa and spread:
+            raise Unsupported("ServiceSpreadingPriority next to SelectorSpreadPriority and a serviceAntiAffinity "
+                              "priority, with spread listers (one auxiliary spreading priority)")
+        # a second spreading priority over the services (include/ksim.h ksim_affinity_tables.aux_*)
+        aux = ("service_spreading",) if both else (("service_anti_affinity", saa[0]) if len(saa) == 1 else None)
         self.cluster = Cluster.from_objects(nodes, running_pods, self.order, pvs=pvs, pvcs=pvcs,
                                             storage_classes=storage_classes, spread=spread,
-                                            spread_services_only="ServiceSpreadingPriority" in names)
+                                            spread_services_only="ServiceSpreadingPriority" in names and not both,
+                                            aux=aux if spread else None)
         self.scheduler = GenericScheduler(self.cluster, predicates, priorities, device=device, mode=mode,
                                           collect_reasons=collect_reasons, label_presence=label_presence,
                                           custom_priorities=custom, service_affinity=svc_aff)

@@ -388,11 +388,25 @@ static int64_t spread_score(int64_t cnt, int64_t max_node, int have_zones, int32
   return (int64_t)f;
 }
 
+/* The auxiliary priority's score of one fit node (ksim_affinity_tables.aux_*): KSIM_AUX_SPREAD is
+ * spread_score over the aux pair and key; KSIM_AUX_SERVICE_ANTI is
+ * CalculateAntiAffinityPriorityReduce (selector_spreading.go:248-275): 0 without the label, else
+ * MaxPriority x (total - count of the node's label value) / total over the fit nodes (MaxPriority
+ * when total is 0), float64 as in Go. */
+static int64_t aux_score(int kind, int64_t cnt, int32_t d, int64_t dsum, int64_t amx, int64_t atot, int ahz,
+                         int64_t azmx) {
+  if (kind == KSIM_AUX_SPREAD) return spread_score(cnt, amx, ahz, d, dsum, azmx);
+  if (d < 0) return 0;
+  if (atot <= 0) return 10;
+  return (int64_t)(10.0 * ((double)(atot - dsum) / (double)atot));
+}
+
 #define MAXT 256
 
 /* Per-thread partials of one pod (one cache line apart). */
 typedef struct {
   int64_t F, mxT, mxA, mn, mx, smx, hz;
+  int64_t amx, atot, ahz;  /* the auxiliary priority (ksim_affinity_tables.aux_*) */
   int64_t M, C;
   int32_t hist[KSIM_NREASONS];
   char pad[64];
@@ -427,8 +441,12 @@ int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_nod
   int64_t* zsum = (int64_t*)calloc((size_t)threads * (n_zone + 1), sizeof(int64_t));
   int64_t* zall = (int64_t*)calloc((size_t)n_zone + 1, sizeof(int64_t));
   RefPart* part = (RefPart*)calloc((size_t)threads, sizeof(RefPart));
-  if (!mask || !score || !ttv || !nav || !raw || !zsum || !zall || !part) {
-    free(mask); free(score); free(ttv); free(nav); free(raw); free(zsum); free(zall); free(part);
+  const int aux_on = at && at->aux_pair && at->aux_weight && !cfg->no_priorities;
+  const int n_adom = aux_on ? at->n_dom[at->aux_key] : 0;
+  int64_t* asum = (int64_t*)calloc((size_t)threads * (n_adom + 1), sizeof(int64_t));
+  int64_t* aall = (int64_t*)calloc((size_t)n_adom + 1, sizeof(int64_t));
+  if (!mask || !score || !ttv || !nav || !raw || !zsum || !zall || !part || !asum || !aall) {
+    free(mask); free(score); free(ttv); free(nav); free(raw); free(zsum); free(zall); free(part); free(asum); free(aall);
     return KSIM_E_NOMEM;
   }
   uint64_t counter = *io_counter;
@@ -439,7 +457,7 @@ int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_nod
   const int64_t wi = cfg->weights[KSIM_W_INTERPOD_AFFINITY], wsp = cfg->weights[KSIM_W_SELECTOR_SPREAD];
   int rc = KSIM_OK;
   /* the pod's decision, shared between the phases */
-  int64_t winner = -1, M = 0, ixv = 0, G_zmx = 0;
+  int64_t winner = -1, M = 0, ixv = 0, G_zmx = 0, G_azmx = 0;
 
 #pragma omp parallel num_threads(threads)
   {
@@ -447,6 +465,7 @@ int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_nod
     const int64_t lo = n * tn / T_, hi = n * (tn + 1) / T_;
     RefPart* my = &part[tn];
     int64_t* myz = zsum + (size_t)tn * (n_zone + 1);
+    int64_t* mya = asum + (size_t)tn * (n_adom + 1);
     for (int64_t k = first; k < first + count; ++k) {
       if (rc != KSIM_OK) break;  /* uniform: read after the previous pod's last barrier */
       const ksim_pod* P = &pods[k];
@@ -455,9 +474,12 @@ int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_nod
       const int ipa = at && wi && !cfg->no_priorities && interpod_prio_work(at, P);
       const int32_t sp = (at && wsp && !cfg->no_priorities && at->spread_pair && P->aff_class > 0)
                              ? at->spread_pair[P->aff_class - 1] : -1;
+      const int32_t ap = (aux_on && P->aff_class > 0) ? at->aux_pair[P->aff_class - 1] : -1;
+      const int aread = aux_on && (ap >= 0 || at->aux_kind == KSIM_AUX_SERVICE_ANTI);
       /* ---- phase 1: findNodesThatFit + the map priorities over this thread's nodes ---- */
-      int64_t F = 0, mxT = 0, mxA = 0, mn = 0, mx = 0, smx = 0, hz = 0;
+      int64_t F = 0, mxT = 0, mxA = 0, mn = 0, mx = 0, smx = 0, hz = 0, amx = 0, atot = 0, ahz = 0;
       for (int z = 0; z < n_zone; ++z) myz[z] = 0;
+      for (int z = 0; z < n_adom; ++z) mya[z] = 0;
       for (int64_t i = lo; i < hi; ++i) {
         const uint32_t m = pod_fits_on_node(preds, &N, &T, P, pod_ports, pod_scalars, i);
         mask[i] = m;
@@ -491,12 +513,23 @@ int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_nod
           const int32_t z = at->zone_key >= 0 ? aff_dom(at, at->zone_key, i) : -1;
           if (z >= 0) { hz = 1; myz[z] += c; }
         }
+        if (ap >= 0) { /* the auxiliary pair: max, total, haveZones, per-domain sums */
+          const int64_t c = xs->cnt[at->pair_off[ap] + aff_dom(at, at->pair_key[ap], i)];
+          if (c > amx) amx = c;
+          atot += c;
+          const int32_t d = aff_dom(at, at->aux_key, i);
+          if (d >= 0) { ahz = 1; mya[d] += c; }
+        }
       }
       my->F = F; my->mxT = mxT; my->mxA = mxA; my->mn = mn; my->mx = mx; my->smx = smx; my->hz = hz;
+      my->amx = amx; my->atot = atot; my->ahz = ahz;
 #pragma omp barrier
       /* ---- combine (every thread, the same result): fit count and the reduce maxima ---- */
-      int64_t Ft = 0, mT = 0, mA = 0, gmn = 0, gmx = 0, gsmx = 0, ghz = 0;
+      int64_t Ft = 0, mT = 0, mA = 0, gmn = 0, gmx = 0, gsmx = 0, ghz = 0, gamx = 0, gatot = 0, gahz = 0;
       for (int t = 0; t < T_; ++t) {
+        if (part[t].amx > gamx) gamx = part[t].amx;
+        gatot += part[t].atot;
+        if (part[t].ahz) gahz = 1;
         Ft += part[t].F;
         if (part[t].mxT > mT) mT = part[t].mxT;
         if (part[t].mxA > mA) mA = part[t].mxA;
@@ -551,6 +584,18 @@ int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_nod
           }
         }
       }
+      if (ap >= 0) {
+#pragma omp single
+        {
+          G_azmx = 0;
+          for (int z = 0; z < n_adom; ++z) {
+            int64_t v = 0;
+            for (int t = 0; t < T_; ++t) v += asum[(size_t)t * (n_adom + 1) + z];
+            aall[z] = v;
+            if (v > G_azmx) G_azmx = v;
+          }
+        }
+      }
       int64_t lM = INT64_MIN, lC = 0;
       for (int64_t i = lo; i < hi; ++i) {
         if (mask[i]) continue;
@@ -568,6 +613,12 @@ int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_nod
           const int64_t c = xs->cnt[at->pair_off[sp] + aff_dom(at, at->pair_key[sp], i)];
           const int32_t z = at->zone_key >= 0 ? aff_dom(at, at->zone_key, i) : -1;
           t += (uint64_t)wsp * (uint64_t)spread_score(c, gsmx, (int)ghz, z, z >= 0 ? zall[z] : 0, G_zmx);
+        }
+        if (aread) {
+          const int64_t c = ap >= 0 ? xs->cnt[at->pair_off[ap] + aff_dom(at, at->pair_key[ap], i)] : 0;
+          const int32_t d = aff_dom(at, at->aux_key, i);
+          t += (uint64_t)at->aux_weight *
+               (uint64_t)aux_score(at->aux_kind, c, d, (ap >= 0 && d >= 0) ? aall[d] : 0, gamx, gatot, (int)gahz, G_azmx);
         }
         score[i] = (int64_t)t;
         if (score[i] > lM) { lM = score[i]; lC = 1; }
@@ -606,7 +657,7 @@ int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_nod
     }
   }
   *io_counter = counter;
-  free(mask); free(score); free(ttv); free(nav); free(raw); free(zsum); free(zall); free(part);
+  free(mask); free(score); free(ttv); free(nav); free(raw); free(zsum); free(zall); free(part); free(asum); free(aall);
   return rc;
 }
 

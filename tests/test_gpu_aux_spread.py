@@ -1,0 +1,178 @@
+"""GPU parity of the auxiliary counted priority (include/ksim.h ksim_affinity_tables.aux_*), the
+second spreading priority a Policy can configure next to SelectorSpread:
+
+- ServiceAntiAffinity with services selecting the pods (selector_spreading.go:180-275): the
+  reference's TestZoneSpreadPriority cases with services (selector_spreading_test.go:605-760),
+  checked by where selectHost puts the pod for every lastNodeIndex over two periods, and random
+  simulations against the object oracle (placements, FitError texts, lastNodeIndex);
+- ServiceSpreadingPriority configured together with SelectorSpreadPriority (the services-only
+  selectors as the auxiliary pair, zones from utilnode.GetZoneKey), the same way.
+
+Both launch forms (pass A fused into the scan, and as its own launch) and the per-pod call."""
+import copy
+
+import pytest
+
+import ksim_ref as R
+from golden_util import case_id, load
+from ksim import abi, ingest, scheduler, spread
+from workloads import rnd_spread_workload
+
+pytestmark = pytest.mark.gpu
+
+ZONE = "failure-domain.beta.kubernetes.io/zone"
+
+
+def _ns_fix(o):
+    """The golden JSON keeps Go identifiers as {"__ident__": ...}; NamespaceDefault is "default"."""
+    o = copy.deepcopy(o)
+    md = o.setdefault("metadata", {})
+    if isinstance(md.get("namespace"), dict):
+        md["namespace"] = "default"
+    return o
+
+
+SAA_CASES = [c for c in load("label_priorities") if c["kind"] == "serviceAntiAffinity" and c["services"]]
+
+
+@pytest.mark.parametrize("c", SAA_CASES, ids=case_id)
+def test_golden_service_anti_affinity_with_services_on_gpu(c):
+    expect = c["expect"]
+    best = max(expect.values())
+    tied = sorted((h for h, s in expect.items() if s == best), key=lambda h: h.encode(), reverse=True)
+    names = {(n.get("metadata") or {}).get("name", "") for n in c["nodes"]}
+    running = [_ns_fix(p) for p in c["pods"] if (p.get("spec") or {}).get("nodeName", "") in names]
+    for k, p in enumerate(running):
+        p["metadata"].setdefault("name", "golden-%d" % k)
+    pod = _ns_fix(c["pod"])
+    lst = spread.SpreadListers(services=[_ns_fix(s) for s in c["services"]])
+    for k in range(2 * len(tied)):
+        cl = ingest.Cluster.from_objects(c["nodes"], running, [pod], spread=lst, aux=("service_anti_affinity", c["label"]))
+        g = scheduler.GenericScheduler(cl, [], [("P", 1)], mode=abi.MODE_AUTO, last_node_index=k,
+                                       custom_priorities={"P": ("serviceAntiAffinity", c["label"])})
+        try:
+            out, _, _ = g.schedule(0, 1)
+        finally:
+            g.close()
+        assert cl.names[int(out[0])] == tied[k % len(tied)], (k, tied)
+
+
+def _check(rep, want, want_lni):
+    got = {name: (host, None) for name, host in rep.successful}
+    got.update({name: (None, msg) for name, msg in rep.failed})
+    assert [n for n, _ in rep.successful] == [n for n, h, _ in want if h is not None]
+    for name, host, msg in want:
+        assert got[name] == (host, msg), name
+    assert rep.last_node_index == want_lni
+
+
+def _saa_prios(seed):
+    if seed % 2:
+        return [("SAA", 3), ("SelectorSpreadPriority", 1), ("LeastRequestedPriority", 1)]
+    return [("SAA", 2), ("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
+
+
+def _run(nodes, running, pods, preds, prios, lst, aux, custom=None, mode=abi.MODE_AUTO):
+    """The simulator's loop (LIFO queue) through GenericScheduler on a cluster with `aux`."""
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order, spread=lst, aux=aux)
+    assert cl.aux_active
+    g = scheduler.GenericScheduler(cl, preds, prios, mode=mode, custom_priorities=custom)
+    try:
+        out, reasons, st = g.schedule()
+        lni = g.last_node_index
+    finally:
+        g.close()
+    assert st.mode == abi.MODE_LAUNCH   # the auxiliary priority is read by the launch form alone
+    rep = scheduler.Report()
+    for k, w in enumerate(out):
+        if w >= 0:
+            rep.successful.append((cl.pod_names[k], cl.names[w]))
+        else:
+            rep.failed.append((cl.pod_names[k], scheduler.fit_error_message(cl.n_nodes, reasons[k], cl.scalar_names.items)))
+    rep.last_node_index = lni
+    return rep
+
+
+@pytest.mark.parametrize("fuse", ["fused", "two_launch"])
+@pytest.mark.parametrize("seed", range(4))
+def test_service_anti_affinity_simulation_matches_oracle(seed, fuse, monkeypatch):
+    if fuse == "two_launch":
+        monkeypatch.setenv("KSIM_FUSE_A", "0")
+    nodes, running, pods, objs = rnd_spread_workload(seed, zones=seed != 3)
+    preds, _ = scheduler.provider("DefaultProvider")
+    prios = _saa_prios(seed)
+    want, want_lni = R.simulate(nodes, running, pods, set(preds), list(prios), spread=R.SpreadListers(**objs),
+                                custom_priorities={"SAA": R.service_anti_affinity_priority(ZONE, R.SpreadListers(**objs))})
+    rep = _run(nodes, running, pods, preds, prios, spread.SpreadListers(**objs), ("service_anti_affinity", ZONE),
+               custom={"SAA": ("serviceAntiAffinity", ZONE)})
+    _check(rep, want, want_lni)
+
+
+@pytest.mark.parametrize("fuse", ["fused", "two_launch"])
+@pytest.mark.parametrize("seed", range(4))
+def test_both_spreading_priorities_match_oracle(seed, fuse, monkeypatch):
+    """Through ClusterCapacity, which builds the cluster with the auxiliary pair itself."""
+    if fuse == "two_launch":
+        monkeypatch.setenv("KSIM_FUSE_A", "0")
+    nodes, running, pods, objs = rnd_spread_workload(seed, zones=seed != 3)
+    preds = list(scheduler.DEFAULT_PREDICATES)
+    prios = [("SelectorSpreadPriority", 1), ("ServiceSpreadingPriority", 2 + seed), ("LeastRequestedPriority", 1)]
+    want, want_lni = R.simulate(nodes, running, pods, set(preds), list(prios), spread=R.SpreadListers(**objs))
+    cc = scheduler.ClusterCapacity(nodes, running, pods, predicates=preds, priorities=prios,
+                                   spread=spread.SpreadListers(**objs))
+    assert cc.cluster.aux_active
+    _check(cc.run(), want, want_lni)
+
+
+def test_schedule_one_with_aux_matches_batch():
+    """ksim_schedule_one (+ assume) pod by pod == ksim_schedule with the auxiliary priority: the
+    per-pod call takes the scan kernel (not the single-workgroup one) and zeroes its sums per pass."""
+    import ctypes as C
+    nodes, running, pods, objs = rnd_spread_workload(1, n_pods=60)
+    order = list(reversed(pods))
+    lst = spread.SpreadListers(**objs)
+    cl = ingest.Cluster.from_objects(nodes, running, order, spread=lst, aux=("service_anti_affinity", ZONE))
+    preds, _ = scheduler.provider("DefaultProvider")
+    prios = _saa_prios(1)
+    custom = {"SAA": ("serviceAntiAffinity", ZONE)}
+    batch = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH, custom_priorities=custom)
+    one = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH, custom_priorities=custom)
+    try:
+        out, _, _ = batch.schedule()
+        for k in range(len(order)):
+            pod = abi.Pod.from_buffer_copy(cl.pods[k].tobytes())
+            res = abi.Result()
+            one.h.call("ksim_schedule_one", C.byref(pod), abi.vptr(cl.pod_ports), len(cl.pod_ports),
+                       abi.vptr(cl.pod_scalars), len(cl.pod_scalars), abi.SCHEDULE_ASSUME, C.byref(res))
+            assert res.node == out[k], k
+        assert one.last_node_index == batch.last_node_index
+    finally:
+        batch.close()
+        one.close()
+
+
+def test_aux_at_scale_matches_c_oracle():
+    """2,000 nodes x 3,000 pods (8 blocks per pod, zone sums across blocks) against the C oracle."""
+    import cpu_ref
+    import random
+    rng = random.Random(77)
+    nodes, running, pods, objs = rnd_spread_workload(5, n_nodes=2000, n_pods=3000, n_running=400)
+    for x in nodes:
+        if rng.random() < 0.7:
+            x["metadata"]["labels"]["rack"] = "r%d" % rng.randrange(40)
+    order = list(reversed(pods))
+    lst = spread.SpreadListers(**objs)
+    preds, _ = scheduler.provider("DefaultProvider")
+    prios = [("SAA", 4), ("SelectorSpreadPriority", 1), ("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
+    custom = {"SAA": ("serviceAntiAffinity", "rack")}
+    cl = ingest.Cluster.from_objects(nodes, running, order, spread=lst, aux=("service_anti_affinity", "rack"))
+    p = scheduler.plan(cl, preds, prios, custom_priorities=custom)
+    want, _, _, ctr, _ = cpu_ref.run(cl, None, threads=8, plan=p)
+    g = scheduler.GenericScheduler(cl, preds, prios, custom_priorities=custom)
+    try:
+        out, _, _ = g.schedule()
+        assert (out == want).all(), int((out != want).argmax())
+        assert g.last_node_index == ctr
+    finally:
+        g.close()

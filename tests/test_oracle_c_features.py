@@ -10,7 +10,7 @@ import pytest
 
 import cpu_ref
 import ksim_ref as R
-from ksim import ingest, scheduler, spread as ksp, synth
+from ksim import abi, ingest, scheduler, spread as ksp, synth
 from workloads import (rnd_affinity_workload, rnd_mixed_workload, rnd_spread_workload, rnd_volume_workload)
 
 AFF_POLICIES = {
@@ -22,13 +22,13 @@ AFF_POLICIES = {
 
 
 def c_oracle_objects(nodes, running, pods, preds, prios, pvs=(), pvcs=(), spread=None, threads=4,
-                     spread_services_only=False):
+                     spread_services_only=False, aux=None, custom_priorities=None):
     """The simulator's loop on the C oracle over the tables scheduler.plan builds: pods popped
     LIFO (store.go:223-233).  Returns ([(pod, node or None, FitError text or None)], lastNodeIndex)."""
     order = list(reversed(pods))
     cl = ingest.Cluster.from_objects(nodes, running, order, pvs=pvs, pvcs=pvcs, spread=spread,
-                                     spread_services_only=spread_services_only)
-    p = scheduler.plan(cl, preds, prios)
+                                     spread_services_only=spread_services_only, aux=aux)
+    p = scheduler.plan(cl, preds, prios, custom_priorities=custom_priorities)
     out, reasons, _, ctr, _ = cpu_ref.run(cl, None, threads=threads, plan=p)
     res = []
     for k, w in enumerate(out):
@@ -85,6 +85,55 @@ def test_spread_matches_object_oracle(seed, policy):
     assert ctr == lni
 
 
+ZONE = "failure-domain.beta.kubernetes.io/zone"
+
+
+def _saa_prios(seed):
+    if seed % 2:
+        return [("SAA", 3), ("SelectorSpreadPriority", 1), ("LeastRequestedPriority", 1)]
+    return [("SAA", 2), ("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_service_anti_affinity_matches_object_oracle(seed):
+    """A Policy's serviceAntiAffinity priority with services selecting the pods (the auxiliary
+    counted priority, include/ksim.h ksim_affinity_tables.aux_*): the pods of the one selecting
+    service counted per node and summed per zone-label value over the fit nodes
+    (selector_spreading.go:180-275)."""
+    nodes, running, pods, objs = rnd_spread_workload(seed, zones=seed != 3)
+    preds, _ = scheduler.provider("DefaultProvider")
+    prios = _saa_prios(seed)
+    want, lni = R.simulate(nodes, running, pods, set(preds), list(prios), spread=R.SpreadListers(**objs),
+                           custom_priorities={"SAA": R.service_anti_affinity_priority(ZONE, R.SpreadListers(**objs))})
+    got, ctr = c_oracle_objects(nodes, running, pods, preds, prios, spread=ksp.SpreadListers(**objs),
+                                aux=("service_anti_affinity", ZONE), custom_priorities={"SAA": ("serviceAntiAffinity", ZONE)})
+    _same(want, got)
+    assert ctr == lni
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_both_spreading_priorities_match_object_oracle(seed):
+    """SelectorSpreadPriority and ServiceSpreadingPriority configured together with spread listers:
+    the second one is the auxiliary counted priority over the services-only selectors."""
+    nodes, running, pods, objs = rnd_spread_workload(seed, zones=seed != 3)
+    preds, _ = scheduler.provider("DefaultProvider")
+    prios = [("SelectorSpreadPriority", 1), ("ServiceSpreadingPriority", 2 + seed), ("LeastRequestedPriority", 1)]
+    want, lni = R.simulate(nodes, running, pods, set(preds), list(prios), spread=R.SpreadListers(**objs))
+    got, ctr = c_oracle_objects(nodes, running, pods, preds, prios, spread=ksp.SpreadListers(**objs),
+                                aux=("service_spreading",))
+    _same(want, got)
+    assert ctr == lni
+
+
+def test_service_anti_affinity_two_services_refused():
+    """Two services selecting one pod: getFirstServiceSelector's pick is the lister's order."""
+    nodes, running, pods, objs = rnd_spread_workload(0)
+    objs["services"] = objs["services"] + [{"metadata": {"namespace": "ns1", "name": "dup"}, "spec": {"selector": {}}}]
+    with pytest.raises(abi.KsimUnsupported):
+        ingest.Cluster.from_objects(nodes, running, pods, spread=ksp.SpreadListers(**objs),
+                                    aux=("service_anti_affinity", ZONE))
+
+
 @pytest.mark.parametrize("seed", range(2))
 def test_mixed_features_match_object_oracle(seed, monkeypatch):
     monkeypatch.setenv("KUBE_MAX_PD_VOLS", "4")
@@ -124,3 +173,37 @@ def test_c2x_objects_saturated():
     want = _c2x(40, 3000, 62, threads=3)
     fails = [m for _, h, m in want if h is None]
     assert len(fails) > 500
+
+
+def _ns_default(o):
+    """The golden JSON keeps Go identifiers as {"__ident__": ...}; NamespaceDefault is "default"."""
+    import copy
+    o = copy.deepcopy(o)
+    md = o.setdefault("metadata", {})
+    if isinstance(md.get("namespace"), dict):
+        md["namespace"] = "default"
+    return o
+
+
+def test_golden_service_anti_affinity_with_services_c_oracle():
+    """TestZoneSpreadPriority's cases with services (selector_spreading_test.go:605-760) through the
+    product's ingest + scheduler.plan and the C oracle: selectHost over two periods of
+    lastNodeIndex lands on the expected top nodes from the highest name down."""
+    from golden_util import load
+    cases = [c for c in load("label_priorities") if c["kind"] == "serviceAntiAffinity" and c["services"]]
+    assert len(cases) == 7
+    for c in cases:
+        expect = c["expect"]
+        best = max(expect.values())
+        tied = sorted((h for h, s in expect.items() if s == best), key=lambda h: h.encode(), reverse=True)
+        names = {(n.get("metadata") or {}).get("name", "") for n in c["nodes"]}
+        running = [_ns_default(p) for p in c["pods"] if (p.get("spec") or {}).get("nodeName", "") in names]
+        for k, p in enumerate(running):
+            p["metadata"].setdefault("name", "golden-%d" % k)
+        lst = ksp.SpreadListers(services=[_ns_default(s) for s in c["services"]])
+        cl = ingest.Cluster.from_objects(c["nodes"], running, [_ns_default(c["pod"])], spread=lst,
+                                         aux=("service_anti_affinity", c["label"]))
+        p = scheduler.plan(cl, [], [("P", 1)], custom_priorities={"P": ("serviceAntiAffinity", c["label"])})
+        for k in range(2 * len(tied)):
+            out, _, _, _, _ = cpu_ref.run(cl, None, threads=1, plan=p, counter=k)
+            assert cl.names[int(out[0])] == tied[k % len(tied)], (c["test"], k, tied)
