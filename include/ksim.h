@@ -447,6 +447,14 @@ typedef struct {
   int64_t amount;      /* 1 (required anti-affinity) or the signed priority weight */
 } ksim_aff_carry;
 
+#define KSIM_SVC_LABELS 8
+typedef struct {
+  int32_t pair_all;                      /* (s_v, key 0): the matching cached pods */
+  int32_t pad;
+  int32_t pair_present[KSIM_SVC_LABELS]; /* (s_v, presence key of label l) */
+  int32_t pair_value[KSIM_SVC_LABELS];   /* (s_v, key of label l) */
+} ksim_svc_ident;
+
 typedef struct {
   int32_t n_keys, n_sel, n_ident, n_pair, n_carry, n_aclass;
   int32_t n_terms, n_carries;
@@ -493,6 +501,23 @@ typedef struct {
   int32_t aux_key;                 /* -1 with aux_pair NULL */
   int32_t aux_kind;                /* KSIM_AUX_* */
   int64_t aux_weight;
+  /* CheckServiceAffinity for pods a service selects whose nodeSelector lacks some of the
+   * predicate's labels (predicates.go:920-1016): the missing labels take the values of the node
+   * of the first cached pod with the pod's labels in its namespace (serviceAffinityMetadataProducer,
+   * a pod-lister order), so the library checks that every such pod's node agrees on them and
+   * refuses the run (KSIM_E_UNSUPPORTED, the order would decide) when they do not.  Per service-
+   * affinity identity v (namespace + labels of such pods): selector s_v (namespace, the labels as a
+   * set selector) with counted pairs (s_v, key 0) — the matching cached pods — and per predicate
+   * label l (s_v, presence key of l: domain 0 on nodes carrying l) and (s_v, key of l).  NULL
+   * svc_ident: none.  Scheduled by the launch-form kernels only. */
+  int32_t n_svc;                   /* service-affinity identities */
+  int32_t n_svc_labels;            /* the predicate's labels (<= KSIM_SVC_LABELS) */
+  const ksim_svc_ident* svc_ident; /* [n_svc] */
+  const int32_t* svc_class;        /* [n_aclass]: the class's identity v, or -1 */
+  const uint32_t* svc_miss;        /* [n_aclass]: bit l = the class's nodeSelector lacks label l */
+  const uint32_t* svc_conflict;    /* [n_svc]: bit l = the cached pods of v disagree on label l */
+  const int32_t* svc_of_off;       /* [n_ident + 1] offsets into svc_of */
+  const int32_t* svc_of;           /* the identities v whose selector an affinity identity matches */
 } ksim_affinity_tables;
 #define KSIM_AUX_SPREAD 0
 #define KSIM_AUX_SERVICE_ANTI 1

@@ -105,6 +105,31 @@ int validate(ksim_handle* h, const ksim_affinity_tables* t) {
       if (c < -1 || c >= t->n_pair || (c >= 0 && t->pair_key[c] != 1))
         return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: class %d spread pair out of range", a);
     }
+  if (t->svc_class) {
+    if (!t->svc_ident || !t->svc_miss || !t->svc_conflict || !t->svc_of_off || t->n_svc < 0 || t->n_svc_labels < 0 ||
+        t->n_svc_labels > KSIM_SVC_LABELS)
+      return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: service-affinity tables incomplete");
+    for (int32_t a = 0; a < t->n_aclass; ++a)
+      if (t->svc_class[a] < -1 || t->svc_class[a] >= t->n_svc || (t->svc_miss[a] >> t->n_svc_labels) != 0)
+        return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: class %d service-affinity identity out of range", a);
+    auto pair_on = [&](int32_t c, bool node_key) {  // a pair on a real key (the key-0 pair on key 0)
+      return c >= 0 && c < t->n_pair && (node_key ? t->pair_key[c] == 0 : t->pair_key[c] >= 2);
+    };
+    for (int32_t v = 0; v < t->n_svc; ++v) {
+      const ksim_svc_ident& S = t->svc_ident[v];
+      bool ok = pair_on(S.pair_all, true);
+      for (int32_t l = 0; l < t->n_svc_labels && ok; ++l) ok = pair_on(S.pair_present[l], false) && pair_on(S.pair_value[l], false);
+      if (!ok) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: service-affinity identity %d pairs out of range", v);
+    }
+    if (t->svc_of_off[0] != 0)
+      return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: svc_of_off[0] must be 0");
+    for (int32_t i = 0; i < t->n_ident; ++i)
+      if (t->svc_of_off[i + 1] < t->svc_of_off[i] || (t->svc_of_off[i + 1] > t->svc_of_off[i] && !t->svc_of))
+        return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: svc_of_off not ascending");
+    for (int32_t e = 0; e < t->svc_of_off[t->n_ident]; ++e)
+      if (t->svc_of[e] < 0 || t->svc_of[e] >= t->n_svc)
+        return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: svc_of entry %d out of range", e);
+  }
   for (size_t q = 0; q < h->q_ident.size(); ++q)
     if (h->q_ident[q] > t->n_ident || h->q_aclass[q] > t->n_aclass)
       return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: queued pod %zu uses an identity / class beyond the tables", q);
@@ -129,6 +154,9 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
   int32_t* spair = nullptr;
   int32_t* apair = nullptr;
   int64_t *asum = nullptr, *aread = nullptr;
+  int32_t *sv_cls = nullptr, *sv_of_off = nullptr, *sv_of = nullptr;
+  uint32_t *sv_miss = nullptr, *sv_conf = nullptr;
+  ksim_svc_ident* sv = nullptr;
   ksim_aff_term* terms;
   ksim_aff_carry* carries;
   uint32_t* ticket;
@@ -150,6 +178,12 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
     return rc;
   if (t->spread_pair && (rc = dev_upload(h, &spair, t->spread_pair, t->n_aclass))) return rc;
   const int32_t n_adom = t->aux_pair ? t->n_dom[t->aux_key] : 0;
+  if (t->svc_class &&
+      ((rc = dev_upload(h, &sv_cls, t->svc_class, t->n_aclass)) || (rc = dev_upload(h, &sv_miss, t->svc_miss, t->n_aclass)) ||
+       (rc = dev_upload(h, &sv, t->svc_ident, t->n_svc)) || (rc = dev_upload(h, &sv_conf, t->svc_conflict, t->n_svc)) ||
+       (rc = dev_upload(h, &sv_of_off, t->svc_of_off, (size_t)t->n_ident + 1)) ||
+       (rc = dev_upload(h, &sv_of, t->svc_of, (size_t)t->svc_of_off[t->n_ident]))))
+    return rc;
   if (t->aux_pair && ((rc = dev_upload(h, &apair, t->aux_pair, t->n_aclass)) ||
                       (rc = dev_upload<int64_t>(h, &asum, nullptr, n_adom)) || (rc = dev_upload<int64_t>(h, &aread, nullptr, n_adom))))
     return rc;
@@ -215,6 +249,8 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
   A.mm = mm; A.part = part; A.ticket = ticket;
   A.aux_pair = apair; A.asum = asum; A.aread = aread; A.aux_w = t->aux_pair ? t->aux_weight : 0;
   A.aux_key = t->aux_pair ? t->aux_key : -1; A.aux_kind = t->aux_kind; A.n_adom = n_adom;
+  A.svc_class = sv_cls; A.svc_miss = sv_miss; A.svc = sv; A.svc_conflict = sv_conf; A.svc_of_off = sv_of_off;
+  A.svc_of = sv_of; A.n_svc = t->svc_class ? t->n_svc : 0; A.n_svc_labels = t->svc_class ? t->n_svc_labels : 0;
   A.n_pair = t->n_pair;
   A.sel_words = t->sel_words;
   A.carry_words = t->carry_words;

@@ -74,6 +74,16 @@ struct KsimAff {
   int64_t* aread;
   int64_t aux_w;
   int32_t aux_key, aux_kind, n_adom, pad2;
+  // CheckServiceAffinity's lender agreement (ksim_affinity_tables.svc_*; launch form only), svc_class
+  // null: none.  svc_conflict is device-mutable (the commits' disagreement bits); err bit 128 = a pod
+  // read a disagreeing label (the host refuses the run)
+  const int32_t* __restrict__ svc_class;
+  const uint32_t* __restrict__ svc_miss;
+  const ksim_svc_ident* __restrict__ svc;
+  uint32_t* svc_conflict;
+  const int32_t* __restrict__ svc_of_off;
+  const int32_t* __restrict__ svc_of;
+  int32_t n_svc, n_svc_labels;
 };
 
 #define KSIM_AFF_MM 9      // pass-A result words
@@ -681,6 +691,53 @@ __device__ __noinline__ void ksim_vol_commit(const KsimVol& V, const ksim_pod& P
   ksim_vol_commit_body(V, P, w, sign, err);
 }
 
+// CheckServiceAffinity's labels from the lender (predicates.go:986-1011) for affinity class a on
+// node i: the class's nodeSelector lacks the labels of svc_miss[a]; with cached pods matching its
+// identity v (pair_all > 0), label l is constrained to the value their nodes share — unless none of
+// them carries l (the pair at l's presence key is 0).  Disagreeing nodes (svc_conflict) make the
+// reference's answer depend on the pod lister's order: err bit 128, the host refuses the run.
+__device__ __forceinline__ uint32_t ksim_svc_lender(const KsimCtx& c, const KsimAff& A, int32_t a, int64_t i) {
+  const int32_t v = A.svc_class[a];
+  if (v < 0) return 0;
+  const uint32_t miss = A.svc_miss[a];
+  const ksim_svc_ident& S = A.svc[v];
+  const int32_t total = A.cnt[A.pair_off[S.pair_all]];
+  if (total == 0) return 0;  // no cached pod to lend labels
+  if (A.svc_conflict[v] & miss) {
+    atomicOr(c.err, 128);
+    return 1u << KSIM_R_SERVICE_AFFINITY;
+  }
+  for (uint32_t mm = miss; mm; mm &= mm - 1) {
+    const int l = __builtin_ctz(mm);
+    if (A.cnt[A.pair_off[S.pair_present[l]]] == 0) continue;  // the lender lacks l: no constraint
+    const int32_t pv = S.pair_value[l];
+    const int32_t d = ksim_dom(A, A.pair_key[pv], i);
+    if (d < 0 || A.cnt[A.pair_off[pv] + d] != total) return 1u << KSIM_R_SERVICE_AFFINITY;
+  }
+  return 0;
+}
+
+// Before the commit of pod P on node w adds its counts: the service-affinity identities whose
+// selector P matches record the labels on which w disagrees with their earlier cached pods.
+// Single thread.
+__device__ __forceinline__ void ksim_svc_commit(const KsimAff& A, const ksim_pod& P, int64_t w) {
+  if (!A.svc_class || P.aff_ident <= 0) return;
+  for (int32_t e = A.svc_of_off[P.aff_ident - 1], end = A.svc_of_off[P.aff_ident]; e < end; ++e) {
+    const int32_t v = A.svc_of[e];
+    const ksim_svc_ident& S = A.svc[v];
+    const int32_t total = A.cnt[A.pair_off[S.pair_all]];
+    if (total == 0) continue;  // the first one: nothing to disagree with
+    uint32_t bad = 0;
+    for (int l = 0; l < A.n_svc_labels; ++l) {
+      const int32_t pv = S.pair_value[l];
+      const int32_t d = ksim_dom(A, A.pair_key[pv], w);
+      const int32_t here = d >= 0 ? A.cnt[A.pair_off[pv] + d] : total - A.cnt[A.pair_off[S.pair_present[l]]];
+      if (here != total) bad |= 1u << l;
+    }
+    if (bad) atomicOr(&A.svc_conflict[v], bad);
+  }
+}
+
 // Reason mask of the first failing predicate in predicatesOrdering (predicates.go:129-138,
 // core/generic_scheduler.go:467-528); 0 = fits.  IPA = false stops before MatchInterPodAffinity (the
 // last key), for a kernel that evaluates it over its own count layout (ksim_pgen.hip).
@@ -733,6 +790,10 @@ __device__ __forceinline__ uint32_t ksim_predicates_a(const KsimCtx& c, const ks
   if ((pr & KSIM_P_SERVICE_AFFINITY) && (P.flags & KSIM_POD_NEED_SVC_AFFINITY) && c.svc_ok &&
       !ksim_bit(c.svc_ok, P.cls, c.lwords, c.label_set[i]))
     return 1u << KSIM_R_SERVICE_AFFINITY;
+  if (INL && (pr & KSIM_P_SERVICE_AFFINITY) && c.aff && c.aff->svc_class && P.aff_class > 0) {
+    m = ksim_svc_lender(c, *c.aff, P.aff_class - 1, i);
+    if (m) return m;
+  }
   if (vol) {
     const uint32_t which = ((pr & KSIM_P_MAX_EBS) ? KSIM_VOL_EBS : 0u) | ((pr & KSIM_P_MAX_GCE_PD) ? KSIM_VOL_GCE_PD : 0u) |
                            ((pr & KSIM_P_MAX_AZURE_DISK) ? KSIM_VOL_AZURE_DISK : 0u);

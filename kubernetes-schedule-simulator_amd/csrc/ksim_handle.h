@@ -274,3 +274,9 @@ int ksim_rt_pick_npt(int64_t n);
 inline bool ksim_rt_aux_on(const ksim_handle* h) {
   return h->have_aff && h->aff_h.aux_pair != nullptr && h->aff_h.aux_w != 0 && !h->ctx.no_prio;
 }
+// ... and the service-affinity lender check (ksim_affinity_tables.svc_*).
+inline bool ksim_rt_launch_tables(const ksim_handle* h) {
+  return ksim_rt_aux_on(h) || (h->have_aff && h->aff_h.svc_class != nullptr && (h->ctx.preds & KSIM_P_SERVICE_AFFINITY));
+}
+// err bit 128 (a pod read disagreeing service-affinity labels): clear it, KSIM_E_UNSUPPORTED.
+int ksim_rt_svc_refusal(ksim_handle* h);

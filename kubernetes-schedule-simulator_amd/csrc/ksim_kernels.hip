@@ -839,6 +839,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
           if (c.out_fit) c.out_fit[1] |= st;
         }
       } else if (wv == 1 && ksim_is_aff_pod(c, P)) {
+        if (lane == 0) ksim_svc_commit(*c.aff, P, D.node);  // reads the counts before this commit's adds
         ksim_aff_commit_body(*c.aff, P, D.node, 1, lane, 64);
       }
     }
@@ -1142,6 +1143,7 @@ __global__ __launch_bounds__(ONE_BLOCK) void ksim_one_kernel(KsimCtx c) {
           if (c.out_fit) c.out_fit[1] |= st;
         }
       } else if (wv == 1 && ksim_is_aff_pod(c, P)) {
+        if (lane == 0) ksim_svc_commit(*c.aff, P, D.node);  // reads the counts before this commit's adds
         ksim_aff_commit_body(*c.aff, P, D.node, 1, lane, 64);
       }
     }
@@ -1188,7 +1190,10 @@ __global__ void ksim_assume_kernel(KsimCtx c, int64_t pod, int64_t node, int32_t
     if (ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, node, 1, c.err);
     *status |= st;
   }
-  if (ksim_is_aff_pod(c, P)) ksim_aff_commit_body(*c.aff, P, node, 1, threadIdx.x, 64);
+  if (ksim_is_aff_pod(c, P)) {
+    if (threadIdx.x == 0) ksim_svc_commit(*c.aff, P, node);
+    ksim_aff_commit_body(*c.aff, P, node, 1, threadIdx.x, 64);
+  }
   __syncthreads();
   if (threadIdx.x == 0) status[KSIM_RES_ERR - KSIM_RES_STATUS] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

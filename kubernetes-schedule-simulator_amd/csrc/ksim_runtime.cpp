@@ -288,6 +288,16 @@ int64_t ksim_rt_launch_only_count(const ksim_handle* h, int64_t first, int64_t c
   return k;
 }
 
+int ksim_rt_svc_refusal(ksim_handle* h) {
+  int32_t err = 0;
+  HIPCHK(h, hipMemcpy(&err, h->ctx.err, 4, hipMemcpyDeviceToHost));
+  err &= ~128;  // the refusal is this call's: the handle stays usable
+  HIPCHK(h, hipMemcpy(h->ctx.err, &err, 4, hipMemcpyHostToDevice));
+  return ksim_fail(h, KSIM_E_UNSUPPORTED, "CheckServiceAffinity: the cached pods with a pod's labels sit on nodes that disagree "
+                                      "on a service-affinity label the pod's nodeSelector leaves open (the pod lister's "
+                                      "order would decide)");
+}
+
 int ksim_rt_check_aff(ksim_handle* h, const char* where) {
   if (h->have_aff && h->aff_stale)
     return ksim_fail(h, KSIM_E_STATE, "%s: the affinity tables predate a node event; load them again", where);
@@ -675,7 +685,7 @@ struct PgPlan {
 
 static bool pgen_plan(ksim_handle* h, PgPlan* pl, bool allow_v2 = true) {
   const KsimCtx& c = h->ctx;
-  if (getenv("KSIM_NO_PGEN") || h->pgen_off || h->shard.world > 1 || c.n <= 0 || ksim_rt_aux_on(h)) return false;
+  if (getenv("KSIM_NO_PGEN") || h->pgen_off || h->shard.world > 1 || c.n <= 0 || ksim_rt_launch_tables(h)) return false;
   int64_t s = 0;
   for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED, KSIM_W_INTERPOD_AFFINITY,
                 KSIM_W_SELECTOR_SPREAD}) {
@@ -1162,8 +1172,9 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
       return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded run stopped: a node's quantities left the exact float64 range");
     }
   } else {
-  // the auxiliary priority (ksim_affinity_tables.aux_*) is read by the launch-form kernels alone
-  const int mode = ksim_rt_aux_on(h) ? KSIM_MODE_LAUNCH : h->cfg.mode;
+  // the auxiliary priority and the service-affinity lender check (ksim_affinity_tables.aux_* / svc_*)
+  // are read by the launch-form kernels alone
+  const int mode = ksim_rt_launch_tables(h) ? KSIM_MODE_LAUNCH : h->cfg.mode;
   int rc = mode == KSIM_MODE_TREE         ? run_tree_mode(h, first, count, st)
            : mode == KSIM_MODE_AUTO       ? run_auto_mode(h, first, count, st)
            : mode == KSIM_MODE_PERSISTENT ? run_persistent_mode(h, first, count, st)
@@ -1187,6 +1198,7 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
     }
   }
   if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port or volume slots overflowed (raise port_slots / vol_slots)");
+  if (err & 128) return ksim_rt_svc_refusal(h);
   if (err & ~1) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
   return KSIM_OK;
 }

@@ -139,7 +139,15 @@ class AffinityTables(C.Structure):
                 ("pair_sel", _i32p), ("pair_key", _i32p), ("pair_off", _i64p), ("carry_key", _i32p),
                 ("carry_kind", _i32p), ("carry_off", _i64p), ("ac", _i32p), ("terms", C.c_void_p),
                 ("carries", C.c_void_p), ("cnt", _i32p), ("carried", _i64p), ("spread_pair", _i32p),
-                ("aux_pair", _i32p), ("aux_key", C.c_int32), ("aux_kind", C.c_int32), ("aux_weight", C.c_int64)]
+                ("aux_pair", _i32p), ("aux_key", C.c_int32), ("aux_kind", C.c_int32), ("aux_weight", C.c_int64),
+                ("n_svc", C.c_int32), ("n_svc_labels", C.c_int32), ("svc_ident", C.c_void_p), ("svc_class", _i32p),
+                ("svc_miss", C.POINTER(C.c_uint32)), ("svc_conflict", C.POINTER(C.c_uint32)), ("svc_of_off", _i32p),
+                ("svc_of", _i32p)]
+
+
+SVC_LABELS = 8
+SVC_IDENT_DTYPE = np.dtype([("pair_all", np.int32), ("pad", np.int32), ("pair_present", np.int32, SVC_LABELS),
+                            ("pair_value", np.int32, SVC_LABELS)])
 
 
 AUX_SPREAD, AUX_SERVICE_ANTI = 0, 1

@@ -96,6 +96,7 @@ class _AnyOf:
 
 
 ZONE_KEY = "\x00zone"   # pseudo key: utilnode.GetZoneKey (K/pkg/util/node/node.go), SelectorSpread's zones
+PRESENCE = "\x00has:"   # pseudo key prefix: domain 0 on the nodes carrying the label
 
 
 def zone_key_of(lab):
@@ -123,6 +124,8 @@ class AffinityIndex:
         self.idents = _Interner()                 # (namespace, labels)
         self.aclasses = _Interner()               # → (required terms, preferred terms, carries, spread, aux)
         self.aux_key, self.aux_kind = None, abi.AUX_SPREAD   # the auxiliary priority (aux_pair), if any
+        self.svc_labels = None                    # CheckServiceAffinity's labels (set_svc), if any
+        self.svcs = _Interner()                   # service-affinity identities → (sel, pair_all, present, value)
 
     # ---------------------------------------------------------------- interning
     def _sel(self, defining_pod, term):
@@ -165,6 +168,32 @@ class AffinityIndex:
         self.aux_kind, self.aux_key = kind, key
         self.keys.get(key)
 
+    def set_svc(self, affinity_labels):
+        """CheckServiceAffinity's labels (include/ksim.h ksim_affinity_tables.svc_*): a value key and
+        a presence key per label."""
+        self.svc_labels = list(affinity_labels)
+        for l in self.svc_labels:
+            self.keys.get(l)
+            self.keys.get(PRESENCE + l)
+
+    def svc_class(self, pod, miss):
+        """(identity, missing-label mask) of a pod a service selects whose nodeSelector lacks the
+        labels of `miss`: the identity's selector is the pod's labels as a set selector in its
+        namespace (serviceAffinityMetadataProducer, predicates.go:920-940: CreateSelectorFromLabels,
+        FilterPodsByNamespace — deleting pods count), with the counted pairs the lender check reads."""
+        md = _meta(pod)
+        ns, lab = md.get("namespace", ""), md.get("labels") or {}
+        key = (ns, _canon(lab))
+        v = self.svcs.ids.get(key)
+        if v is None:
+            sel = labels.from_set(lab)
+            s = self.sels.get(((ns,), tuple(sel)), (frozenset([ns]), sel))
+            rec = (s, self.pairs.get((s, KEY_ALL)),
+                   tuple(self.pairs.get((s, self.keys.ids[PRESENCE + l])) for l in self.svc_labels),
+                   tuple(self.pairs.get((s, self.keys.ids[l])) for l in self.svc_labels))
+            v = self.svcs.get(key, rec)
+        return (v, int(miss))
+
     def aux_pair(self, pod, sels):
         """The pod's counted pair for the auxiliary priority, or -1: abi.AUX_SPREAD takes the
         services-only SelectorSpread selectors (any of them, not being deleted); abi.AUX_SERVICE_ANTI
@@ -181,13 +210,13 @@ class AffinityIndex:
             s = self.sels.get(((ns,), tuple(sel)), (frozenset([ns]), sel))
         return self.pairs.get((s, KEY_NODE))
 
-    def aclass(self, pod, spread_sels=(), aux_sels=()):
-        """The pod's own terms, carried terms, SelectorSpread pair and auxiliary pair, interned; -1
-        when it has none of them."""
+    def aclass(self, pod, spread_sels=(), aux_sels=(), svc=None):
+        """The pod's own terms, carried terms, SelectorSpread pair, auxiliary pair and
+        service-affinity identity (svc_class), interned; -1 when it has none of them."""
         sp = self.spread_pair(pod, spread_sels)
         ap = self.aux_pair(pod, aux_sels)
         if not has_pod_affinity(pod):
-            return -1 if sp < 0 and ap < 0 else self.aclasses.get(((), (), (), sp, ap))
+            return -1 if sp < 0 and ap < 0 and svc is None else self.aclasses.get(((), (), (), sp, ap, svc))
         a = _aff(pod)
         name = _meta(pod).get("name")
         req, pref, carries = [], [], {}
@@ -243,9 +272,9 @@ class AffinityIndex:
                 carry(wt.get("podAffinityTerm") or {}, abi.AFF_CARRY_PRIO, -int(wt.get("weight", 0)))
         carries = tuple(sorted((e, v) for e, v in carries.items() if v != 0 or self.carry.items[e][2] == abi.AFF_CARRY_ANTI))
         req.sort(key=lambda r: r[0] != abi.AFF_REQ_AFFINITY)   # affinity terms are checked before anti-affinity
-        if not req and not pref and not carries and sp < 0 and ap < 0:
+        if not req and not pref and not carries and sp < 0 and ap < 0 and svc is None:
             return -1
-        return self.aclasses.get((tuple(req), tuple(pref), carries, sp, ap))
+        return self.aclasses.get((tuple(req), tuple(pref), carries, sp, ap, svc))
 
     # ------------------------------------------------------------------ tables
     def build(self, running_nodes, idents, aclasses):
@@ -272,6 +301,9 @@ class AffinityIndex:
                     z = zone_key_of(lab)
                     if z != "":
                         dom[k, i] = vals.setdefault(z, len(vals))
+                elif name.startswith(PRESENCE):
+                    if lab is not None and name[len(PRESENCE):] in lab:
+                        dom[k, i] = vals.setdefault(True, 0)
                 elif lab is not None and name in lab:
                     dom[k, i] = vals.setdefault(lab[name], len(vals))
             n_dom[k] = len(vals)
@@ -319,7 +351,7 @@ class AffinityIndex:
         ac = np.zeros((A, 6), np.int32)   # req_off, req_cnt, pref_off, pref_cnt, carry_off, carry_cnt
         spread_pair = np.array([x[3] for x in self.aclasses.items], np.int32) if A else np.zeros(0, np.int32)
         aux_pair = np.array([x[4] for x in self.aclasses.items], np.int32) if A else np.zeros(0, np.int32)
-        for a, (req, pref, car, _, _) in enumerate(self.aclasses.items):
+        for a, (req, pref, car, _, _, _) in enumerate(self.aclasses.items):
             ac[a, 0], ac[a, 1] = len(terms), len(req)
             terms.extend(req)
             ac[a, 2], ac[a, 3] = len(terms), len(pref)
@@ -356,7 +388,53 @@ class AffinityIndex:
                     zone_key=self.keys.ids.get(ZONE_KEY, -1), spread_pair=spread_pair,
                     aux_pair=aux_pair if self.aux_key is not None else None,
                     aux_key=self.keys.ids[self.aux_key] if self.aux_key is not None else -1, aux_kind=self.aux_kind,
-                    aux_weight=0, n_terms=len(terms), n_carries=len(carries)), remap
+                    aux_weight=0, n_terms=len(terms), n_carries=len(carries),
+                    **self._svc_tables(isel, live, remap, dom, running_nodes, idents)), remap
+
+
+def _svc_tables_impl(self, isel, live, remap, dom, running_nodes, idents):
+    """CheckServiceAffinity's lender tables (include/ksim.h ksim_affinity_tables.svc_*): per identity
+    its pairs, per affinity class its identity and missing labels, per live affinity identity the
+    service-affinity identities whose selector it matches, and the running pods' disagreements."""
+    if self.svc_labels is None:
+        return dict(svc_on=False)
+    V, L = len(self.svcs.items), len(self.svc_labels)
+    rec = np.zeros(V, abi.SVC_IDENT_DTYPE)
+    for v, (_, pall, pres, pval) in enumerate(self.svcs.items):
+        rec[v]["pair_all"] = pall
+        rec[v]["pair_present"][:L] = pres
+        rec[v]["pair_value"][:L] = pval
+    A = len(self.aclasses.items)
+    svc_class = np.full(max(A, 1), -1, np.int32)
+    svc_miss = np.zeros(max(A, 1), np.uint32)
+    for a, it in enumerate(self.aclasses.items):
+        if it[5] is not None:
+            svc_class[a], svc_miss[a] = it[5]
+    sel_of = [s for s, _, _, _ in self.svcs.items]
+    live_ids = np.nonzero(live)[0] if len(live) else np.zeros(0, np.int64)
+    off, lst = [0], []
+    for i in live_ids:
+        for v, s in enumerate(sel_of):
+            if (int(isel[i, s >> 6]) >> (s & 63)) & 1:
+                lst.append(v)
+        off.append(len(lst))
+    # the running pods' nodes: per identity, the (present, value) of every label must agree
+    conflict = np.zeros(max(V, 1), np.uint32)
+    vkeys = [self.keys.ids[l] for l in self.svc_labels]
+    for v, s in enumerate(sel_of):
+        seen = [set() for _ in range(L)]
+        for w, i_id in zip(running_nodes, idents[:len(running_nodes)]):
+            if (int(isel[i_id, s >> 6]) >> (s & 63)) & 1:
+                for l in range(L):
+                    seen[l].add(int(dom[vkeys[l], w]))
+        for l in range(L):
+            if len(seen[l]) > 1:
+                conflict[v] |= np.uint32(1 << l)
+    return dict(svc_on=True, n_svc=V, n_svc_labels=L, svc_ident=rec, svc_class=svc_class, svc_miss=svc_miss,
+                svc_conflict=conflict, svc_of_off=np.array(off, np.int32), svc_of=np.array(lst or [0], np.int32))
+
+
+AffinityIndex._svc_tables = _svc_tables_impl
 
 
 def tables_struct(d):
@@ -377,6 +455,18 @@ def tables_struct(d):
     d["carries"] = np.ascontiguousarray(d["carries"])
     t.terms = d["terms"].ctypes.data_as(abi.C.c_void_p)
     t.carries = d["carries"].ctypes.data_as(abi.C.c_void_p)
+    if d.get("svc_on") and d.get("svc_use", True):
+        for k, dt in (("svc_class", np.int32), ("svc_miss", np.uint32), ("svc_conflict", np.uint32),
+                      ("svc_of_off", np.int32), ("svc_of", np.int32)):
+            d[k] = np.ascontiguousarray(d[k], dt)
+        d["svc_ident"] = np.ascontiguousarray(d["svc_ident"])
+        t.n_svc, t.n_svc_labels = int(d["n_svc"]), int(d["n_svc_labels"])
+        t.svc_ident = d["svc_ident"].ctypes.data_as(abi.C.c_void_p)
+        t.svc_class = abi.ptr(d["svc_class"], abi.C.c_int32)
+        t.svc_miss = abi.ptr(d["svc_miss"], abi.C.c_uint32)
+        t.svc_conflict = abi.ptr(d["svc_conflict"], abi.C.c_uint32)
+        t.svc_of_off = abi.ptr(d["svc_of_off"], abi.C.c_int32)
+        t.svc_of = abi.ptr(d["svc_of"], abi.C.c_int32)
     if d.get("aux_pair") is not None and int(d.get("aux_weight", 0)):
         d["aux_pair"] = np.ascontiguousarray(d["aux_pair"], np.int32)
         t.aux_pair = abi.ptr(d["aux_pair"], abi.C.c_int32)

@@ -367,12 +367,16 @@ class Cluster:
         self.aux = None           # the auxiliary spreading priority (from_objects(aux=...))
         self.aux_sels = []
         self.aux_active = False   # some queued pod has a counted auxiliary pair
+        self.svc_labels = None    # CheckServiceAffinity's labels the cluster was built for
+        self.svc_any = False      # a service selects some queued pod
+        self.svc_miss = []
+        self.svc_active = False   # some queued pod needs the lender check
 
     # ------------------------------------------------------------------ nodes
     @classmethod
     def from_objects(cls, nodes, running_pods=(), pods=(), port_slots=None, hard_weight=10, pvs=(), pvcs=(),
                      storage_classes=(), max_vols=None, vol_slots=None, spread=None, spread_services_only=False,
-                     image_locality=None, aux=None):
+                     image_locality=None, aux=None, service_affinity=None):
         """nodes / running_pods / pods: Kubernetes-shaped dicts; pods are in SCHEDULING
         order (the caller resolves the simulator's LIFO queue).  hard_weight:
         hardPodAffinitySymmetricWeight (the simulator's 10, or a Policy's).  pvs / pvcs /
@@ -384,7 +388,10 @@ class Cluster:
         default: when some node lists status.images).  aux: a second counted spreading priority over
         `spread`'s services (include/ksim.h ksim_affinity_tables.aux_*): ("service_spreading",) —
         ServiceSpreadingPriority next to SelectorSpreadPriority — or ("service_anti_affinity", label),
-        a Policy's serviceAntiAffinity priority; None: neither."""
+        a Policy's serviceAntiAffinity priority; None: neither.  service_affinity: CheckServiceAffinity's
+        labels (a Policy's serviceAffinity argument) — with `spread`'s services, pods a service selects
+        whose nodeSelector lacks some of them get the lender check (include/ksim.h
+        ksim_affinity_tables.svc_*)."""
         self = cls()
         self.hard_weight = int(hard_weight)
         self.image_locality = (any((x.get("status") or {}).get("images") for x in nodes) if image_locality is None
@@ -413,7 +420,33 @@ class Cluster:
                     raise Unsupported("ServiceAntiAffinity: %d services select pod %r (the service lister's order "
                                       "decides)" % (len(s), _meta(p).get("name")))
         self.aux_active = any(self.aux_sels)
-        with_affinity = with_pod_affinity or self.spread_active or self.aux_active
+        # CheckServiceAffinity with services (predicates.go:980-1011): per queued pod the missing
+        # labels when a service selects it, else 0
+        self.svc_labels = list(service_affinity) if service_affinity is not None else None
+        self.svc_any = bool(spread) and any(spread.selectors(p, True) for p in pods)
+        self.svc_miss = [0] * len(pods)
+        if self.svc_labels is not None and spread:
+            if len(self.svc_labels) > abi.SVC_LABELS:
+                raise Unsupported("CheckServiceAffinity with more than %d labels and services" % abi.SVC_LABELS)
+            for k, p in enumerate(pods):
+                sel = _spec(p).get("nodeSelector") or {}
+                miss = sum(1 << l for l, name in enumerate(self.svc_labels) if name not in sel)
+                if miss and spread.selectors(p, True):
+                    self.svc_miss[k] = miss
+            need = {(_meta(p).get("namespace", ""), _canon(_meta(p).get("labels") or {})): p
+                    for p, m in zip(pods, self.svc_miss) if m}
+            for q in running_pods:
+                if not _spec(q).get("nodeName") or _spec(q).get("nodeName") in self.index:
+                    continue
+                qm = _meta(q)
+                for (ns, _), p in need.items():
+                    lab = _meta(p).get("labels") or {}
+                    if qm.get("namespace", "") == ns and all((qm.get("labels") or {}).get(k) == v for k, v in lab.items()):
+                        # GetNodeInfo errs for a lender outside the node lister (predicates.go:1003-1006)
+                        raise Unsupported("CheckServiceAffinity: a cached pod with pod %r's labels is bound to a node "
+                                          "outside the snapshot" % _meta(p).get("name"))
+        self.svc_active = any(self.svc_miss)
+        with_affinity = with_pod_affinity or self.spread_active or self.aux_active or self.svc_active
         if with_pod_affinity and len(running) != len([p for p in running_pods if _spec(p).get("nodeName")]):
             # the reference caches them under a node-less NodeInfo: its affinity metadata then
             # errors and the predicate takes another path (metadata.go:106-109)
@@ -571,7 +604,14 @@ class Cluster:
         if self.aux_active:
             idx.set_aux(abi.AUX_SPREAD, ZONE_KEY) if self.aux[0] == "service_spreading" else \
                 idx.set_aux(abi.AUX_SERVICE_ANTI, self.aux[1])
-        aclasses = [idx.aclass(p, s, a) for p, s, a in zip(allp, sels, asels)]
+        svcs = [None] * len(allp)
+        if self.svc_active:
+            idx.set_svc(self.svc_labels)
+            k0 = len(running)
+            for k, m in enumerate(self.svc_miss):
+                if m:
+                    svcs[k0 + k] = idx.svc_class(allp[k0 + k], m)
+        aclasses = [idx.aclass(p, s, a, v) for p, s, a, v in zip(allp, sels, asels, svcs)]
         run_nodes = [self.index[_spec(p)["nodeName"]] for p in running]
         self.affinity, remap = idx.build(run_nodes, idents, aclasses)
         k = len(running)

@@ -343,11 +343,16 @@ def plan(cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO,
                           "without image interning (Cluster.from_objects(image_locality=True))")
     if "CheckNodeLabelPresence" in predicates and label_presence is None:
         raise Unsupported("CheckNodeLabelPresence needs its labelsPresence argument")
+    svc_dyn = False
     if "CheckServiceAffinity" in predicates:
         if service_affinity is None:
             raise Unsupported("CheckServiceAffinity needs its serviceAffinity argument")
-        if getattr(cluster, "spread_active", False):
-            raise Unsupported("CheckServiceAffinity with services selecting the pods (the pod lister's order decides)")
+        if getattr(cluster, "svc_any", getattr(cluster, "spread_active", False)):
+            # services select queued pods: the lender check needs the cluster built for these labels
+            if getattr(cluster, "svc_labels", None) != list(service_affinity):
+                raise Unsupported("CheckServiceAffinity with services selecting the pods needs the cluster built with "
+                                  "service_affinity=%r" % (list(service_affinity),))
+            svc_dyn = bool(cluster.svc_active)
     cfg = make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence],
                       [(n, w) for n, w in prioritizers if n not in custom_priorities],
                       device, mode, collect_reasons, last_node_index,
@@ -371,10 +376,11 @@ def plan(cluster: Cluster, predicates, priorities, device=0, mode=abi.MODE_AUTO,
             pods["flags"] |= np.where(need[pods["cls"]], abi.POD_NEED_SVC_AFFINITY, 0).astype(np.uint32)
     affinity = None
     if cluster.affinity is not None:
-        if cfg.predicates & abi.P_INTERPOD_AFFINITY or ((cfg.weights[abi.W_INTERPOD] or cfg.weights[abi.W_SPREAD] or aux_weight)
-                                                        and not cfg.no_priorities):
-            affinity = dict(cluster.affinity, aux_weight=aux_weight) if cluster.affinity.get("aux_pair") is not None \
-                else cluster.affinity
+        if cfg.predicates & abi.P_INTERPOD_AFFINITY or svc_dyn or \
+                ((cfg.weights[abi.W_INTERPOD] or cfg.weights[abi.W_SPREAD] or aux_weight) and not cfg.no_priorities):
+            affinity = cluster.affinity
+            if cluster.affinity.get("aux_pair") is not None or cluster.affinity.get("svc_on"):
+                affinity = dict(cluster.affinity, aux_weight=aux_weight, svc_use=svc_dyn)
         elif len(pods):  # neither MatchInterPodAffinity nor its priority: the terms change nothing
             pods = pods.copy()
             pods["aff_ident"] = 0
@@ -689,7 +695,8 @@ class ClusterCapacity:
         self.cluster = Cluster.from_objects(nodes, running_pods, self.order, pvs=pvs, pvcs=pvcs,
                                             storage_classes=storage_classes, spread=spread,
                                             spread_services_only="ServiceSpreadingPriority" in names and not both,
-                                            aux=aux if spread else None)
+                                            aux=aux if spread else None,
+                                            service_affinity=svc_aff if "CheckServiceAffinity" in predicates else None)
         self.scheduler = GenericScheduler(self.cluster, predicates, priorities, device=device, mode=mode,
                                           collect_reasons=collect_reasons, label_presence=label_presence,
                                           custom_priorities=custom, service_affinity=svc_aff)

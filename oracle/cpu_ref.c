@@ -63,6 +63,9 @@ typedef struct {
   int64_t* carried;   /* affinity carried terms [carried_len] */
   uint64_t* vslots;   /* volume slots [vol_slots][n] */
   int32_t* vcount;    /* used volume slots per node [n] */
+  uint32_t* svc_conflict; /* service-affinity disagreement bits [n_svc] */
+  int32_t svc_err;        /* set when a pod read a disagreeing label: the run is refused */
+  int32_t pad;
 } ksim_ref_extra;
 
 /* ---- priorities: least_requested.go:44-53, most_requested.go:45-55,
@@ -262,6 +265,34 @@ static int64_t interpod_raw(const RefTables* T, const ksim_pod* P, int64_t i) {
 }
 
 /* podFitsOnNode: the reasons of the first failing predicate in predicatesOrdering */
+/* CheckServiceAffinity with services (predicates.go:980-1011): the labels the pod's nodeSelector
+ * leaves open take the values of the node of the first cached pod with the pod's labels
+ * (serviceAffinityMetadataProducer :920-940 lists them in pod-lister order).  Over the counted
+ * pairs of the class's service-affinity identity: with matching pods cached, a label some of their
+ * nodes carry must have the value they all share; when their nodes disagree on an open label
+ * (svc_conflict) the answer would depend on the lister's order and the run is refused. */
+static uint32_t pred_svc_lender(const RefTables* T, const ksim_pod* P, int64_t i) {
+  const ksim_affinity_tables* A = T->A;
+  if (!A || !A->svc_class || P->aff_class <= 0) return 0;
+  const int32_t v = A->svc_class[P->aff_class - 1];
+  if (v < 0) return 0;
+  const uint32_t open = A->svc_miss[P->aff_class - 1];
+  const ksim_svc_ident* S = &A->svc_ident[v];
+  const int32_t matching = T->X->cnt[A->pair_off[S->pair_all]];
+  if (matching == 0) return 0;
+  if (T->X->svc_conflict[v] & open) {
+    __atomic_store_n(&T->X->svc_err, 1, __ATOMIC_RELAXED);
+    return 1u << KSIM_R_SERVICE_AFFINITY;
+  }
+  for (int l = 0; l < A->n_svc_labels; ++l) {
+    if (!((open >> l) & 1u) || T->X->cnt[A->pair_off[S->pair_present[l]]] == 0) continue;
+    const int32_t pv = S->pair_value[l];
+    const int32_t d = aff_dom(A, A->pair_key[pv], i);
+    if (d < 0 || T->X->cnt[A->pair_off[pv] + d] != matching) return 1u << KSIM_R_SERVICE_AFFINITY;
+  }
+  return 0;
+}
+
 static uint32_t pod_fits_on_node(uint32_t preds, const RefNodes* N, const RefTables* T, const ksim_pod* P,
                                  const uint64_t* pp, const ksim_scalar_req* sc, int64_t i) {
   uint32_t fl = N->cond[i], m;
@@ -285,6 +316,7 @@ static uint32_t pod_fits_on_node(uint32_t preds, const RefNodes* N, const RefTab
   if ((preds & KSIM_P_LABEL_PRESENCE) && (fl & KSIM_N_LABEL_PRESENCE)) return 1u << KSIM_R_LABEL_PRESENCE;
   if ((preds & KSIM_P_SERVICE_AFFINITY) && T->T->svc_ok && !bit(T->T->svc_ok, P->cls, T->lw, N->label_set[i]))
     return 1u << KSIM_R_SERVICE_AFFINITY;
+  if ((preds & KSIM_P_SERVICE_AFFINITY) && (m = pred_svc_lender(T, P, i))) return m;
   if (vol) {
     static const uint32_t keys[3] = {KSIM_P_MAX_EBS, KSIM_P_MAX_GCE_PD, KSIM_P_MAX_AZURE_DISK};
     for (int t = 0; t < 3; ++t)
@@ -354,6 +386,22 @@ static int assume_volumes(RefTables* T, const ksim_pod* P, int64_t w) {
  * matches (at node w's domain of the pair's key), + its carried amounts at w's domains. */
 static void assume_affinity(RefTables* T, const ksim_pod* P, int64_t w) {
   const ksim_affinity_tables* A = T->A;
+  if (A->svc_class && P->aff_ident > 0) {
+    /* the service-affinity identities this pod's labels match: record the labels on which node w
+       disagrees with their cached pods' nodes (before this pod counts) */
+    for (int32_t e = A->svc_of_off[P->aff_ident - 1]; e < A->svc_of_off[P->aff_ident]; ++e) {
+      const int32_t v = A->svc_of[e];
+      const ksim_svc_ident* S = &A->svc_ident[v];
+      const int32_t matching = T->X->cnt[A->pair_off[S->pair_all]];
+      if (matching == 0) continue;
+      for (int l = 0; l < A->n_svc_labels; ++l) {
+        const int32_t pv = S->pair_value[l];
+        const int32_t d = aff_dom(A, A->pair_key[pv], w);
+        const int32_t same = d >= 0 ? T->X->cnt[A->pair_off[pv] + d] : matching - T->X->cnt[A->pair_off[S->pair_present[l]]];
+        if (same != matching) T->X->svc_conflict[v] |= 1u << l;
+      }
+    }
+  }
   if (P->aff_ident > 0) {
     const uint64_t* sm = A->ident_sel + (int64_t)(P->aff_ident - 1) * A->sel_words;
     for (int32_t c = 0; c < A->n_pair; ++c) {
@@ -658,6 +706,7 @@ int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_nod
   }
   *io_counter = counter;
   free(mask); free(score); free(ttv); free(nav); free(raw); free(zsum); free(zall); free(part); free(asum); free(aall);
+  if (rc == KSIM_OK && xs && xs->svc_err) rc = KSIM_E_UNSUPPORTED;
   return rc;
 }
 

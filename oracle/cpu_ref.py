@@ -14,7 +14,8 @@ _lib = None
 class Extra(C.Structure):
     """ksim_ref_extra (cpu_ref.c): the mutable affinity counts and volume slots."""
     _fields_ = [("cnt", C.POINTER(C.c_int32)), ("carried", C.POINTER(C.c_int64)),
-                ("vslots", C.POINTER(C.c_uint64)), ("vcount", C.POINTER(C.c_int32))]
+                ("vslots", C.POINTER(C.c_uint64)), ("vcount", C.POINTER(C.c_int32)),
+                ("svc_conflict", C.POINTER(C.c_uint32)), ("svc_err", C.c_int32), ("pad", C.c_int32)]
 
 
 def lib():
@@ -80,6 +81,8 @@ def run(cluster, cfg, first=0, count=None, threads=1, state=None, counter=0, tab
         if plan.affinity is not None:
             extra["cnt"] = np.ascontiguousarray(plan.affinity["cnt"]).copy()
             extra["carried"] = np.ascontiguousarray(plan.affinity["carried"]).copy()
+            if plan.affinity.get("svc_on") and plan.affinity.get("svc_use", True):
+                extra["svc_conflict"] = np.ascontiguousarray(plan.affinity["svc_conflict"], np.uint32).copy()
         if plan.volumes is not None:
             extra["vslots"] = np.ascontiguousarray(plan.volumes["slots"]).copy()
             extra["vcount"] = np.ascontiguousarray(plan.volumes["slot_count"]).copy()
@@ -89,6 +92,8 @@ def run(cluster, cfg, first=0, count=None, threads=1, state=None, counter=0, tab
         at = tables_struct(plan.affinity)
         x.cnt = abi.ptr(extra["cnt"], C.c_int32)
         x.carried = abi.ptr(extra["carried"], C.c_int64)
+        if "svc_conflict" in extra:
+            x.svc_conflict = abi.ptr(extra["svc_conflict"], C.c_uint32)
     if plan.volumes is not None:
         from ksim.volumes import tables_struct as vol_struct
         vt = vol_struct(plan.volumes, plan.use_zone)
@@ -99,6 +104,12 @@ def run(cluster, cfg, first=0, count=None, threads=1, state=None, counter=0, tab
                                C.byref(x), abi.vptr(pods), abi.vptr(cluster.pod_ports), abi.vptr(cluster.pod_scalars),
                                C.c_int64(first), C.c_int64(count), C.c_int(threads), abi.vptr(out), abi.vptr(reasons),
                                C.byref(ctr))
+    if rc == -4:
+        raise Unsupported("ksim_ref_run_ex: KSIM_E_UNSUPPORTED (CheckServiceAffinity lenders disagree)")
     if rc != 0:
         raise RuntimeError("ksim_ref_run_ex failed: %d" % rc)
     return out, reasons, state, ctr.value, extra
+
+
+class Unsupported(RuntimeError):
+    """The oracle refuses the run where the library does (KSIM_E_UNSUPPORTED)."""

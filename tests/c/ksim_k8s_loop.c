@@ -29,6 +29,9 @@ typedef struct {
   int64_t* carried;
   uint64_t* vslots;
   int32_t* vcount;
+  uint32_t* svc_conflict;
+  int32_t svc_err;
+  int32_t pad;
 } ksim_ref_extra;
 int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_node_state* st, const ksim_class_tables* ct,
                     const ksim_affinity_tables* at, const ksim_volume_tables* vt, ksim_ref_extra* xs,
@@ -259,6 +262,7 @@ int main(int argc, char** argv) {
   memcpy(ports, nt.ports, P * N * 8);
   ns = (ksim_node_state){rc, rm, rg, re, zc, zm, pc, rs, ports, pcount};
   ksim_ref_extra xs;
+  memset(&xs, 0, sizeof xs);
   xs.cnt = malloc(at.cnt_len * 4 + 4);
   xs.carried = malloc(at.carried_len * 8 + 8);
   memcpy(xs.cnt, at.cnt, at.cnt_len * 4);

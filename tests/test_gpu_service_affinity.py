@@ -1,0 +1,114 @@
+"""GPU parity of CheckServiceAffinity with services selecting the pods (predicates.go:920-1016; the
+lender check of include/ksim.h ksim_affinity_tables.svc_*):
+
+- the reference's TestServiceAffinity cases with services (predicates_test.go:1460-1620): the
+  verdict on the node under test from ksim_evaluate, the case's pods cached on their nodes;
+- random simulations against the object oracle reading the live scheduler cache as its pod lister
+  (tests/test_oracle_c_features.py svc_simulate): identical placements, FitError texts and
+  lastNodeIndex, and KSIM_E_UNSUPPORTED exactly where the oracle meets lenders that disagree on an
+  open label (the reference's answer would depend on the pod lister's map order);
+- the per-pod call (ksim_schedule_one + assume) against the batch."""
+import copy
+
+import pytest
+
+from golden_util import case_id, load
+from ksim import abi, ingest, scheduler, spread
+from test_oracle_c_features import SVC_PREDS, SVC_PRIOS, Ambiguous, svc_simulate
+from workloads import rnd_svc_affinity_workload
+
+pytestmark = pytest.mark.gpu
+
+
+def _ns(o, names):
+    """The golden JSON keeps Go identifiers as {"__ident__": ...}: one string per identifier."""
+    o = copy.deepcopy(o)
+    md = o.setdefault("metadata", {})
+    ns = md.get("namespace")
+    if isinstance(ns, dict):
+        md["namespace"] = names.setdefault(ns.get("__ident__", ""), "ident-%d" % len(names))
+    return o
+
+
+SVC_CASES = [c for c in load("service_affinity") if c["services"]]
+
+
+@pytest.mark.parametrize("c", SVC_CASES, ids=case_id)
+def test_golden_service_affinity_with_services_on_gpu(c):
+    names = {"metav1.NamespaceDefault": "default"}
+    node_names = {(n.get("metadata") or {}).get("name", "") for n in c["nodes"]}
+    running = [_ns(p, names) for p in c["pods"] if (p.get("spec") or {}).get("nodeName", "") in node_names]
+    for k, p in enumerate(running):
+        p["metadata"].setdefault("name", "golden-%d" % k)
+    lst = spread.SpreadListers(services=[_ns(s, names) for s in c["services"]])
+    cl = ingest.Cluster.from_objects(c["nodes"], running, [_ns(c["pod"], names)], spread=lst,
+                                     service_affinity=c["labels"])
+    g = scheduler.GenericScheduler(cl, ["CheckServiceAffinity"], [], mode=abi.MODE_LAUNCH, service_affinity=c["labels"])
+    try:
+        fit, rs, _, _ = g.evaluate(0)
+    finally:
+        g.close()
+    k = cl.names.index(c["node"]["metadata"]["name"])
+    assert bool(fit[k]) == c["fits"]
+    if not c["fits"]:
+        assert set(scheduler.reason_strings(int(rs[k]))) == {"node(s) didn't match service affinity"}
+
+
+def _gpu_run(nodes, running, pods, services, aff_labels, mode=abi.MODE_AUTO):
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order, spread=spread.SpreadListers(services=services),
+                                     service_affinity=aff_labels)
+    g = scheduler.GenericScheduler(cl, SVC_PREDS, SVC_PRIOS, mode=mode, service_affinity=aff_labels)
+    try:
+        out, reasons, st = g.schedule()
+        lni = g.last_node_index
+    finally:
+        g.close()
+    res = [(cl.pod_names[k], cl.names[w] if w >= 0 else None,
+            None if w >= 0 else scheduler.fit_error_message(cl.n_nodes, reasons[k], cl.scalar_names.items))
+           for k, w in enumerate(out)]
+    return res, lni, st
+
+
+@pytest.mark.parametrize("variant", ["consistent", "mixed_labels", "conflicting_running"])
+@pytest.mark.parametrize("seed", range(4))
+def test_service_affinity_simulation_matches_oracle(seed, variant):
+    aff_labels = ["region", "rack"]
+    nodes, running, pods, services = rnd_svc_affinity_workload(seed, mixed_labels=variant == "mixed_labels",
+                                                               conflicting_running=variant == "conflicting_running",
+                                                               full_labels=variant == "consistent")
+    try:
+        want, lni = svc_simulate(nodes, running, pods, SVC_PREDS, SVC_PRIOS, aff_labels, services)
+    except Ambiguous:
+        with pytest.raises(abi.KsimUnsupported):
+            _gpu_run(nodes, running, pods, services, aff_labels)
+        return
+    got, ctr, st = _gpu_run(nodes, running, pods, services, aff_labels)
+    assert st.mode == abi.MODE_LAUNCH
+    assert got == want
+    assert ctr == lni
+
+
+def test_schedule_one_with_service_affinity_matches_batch():
+    """Pod by pod through ksim_schedule_one + assume (the scan kernel's commit records the lenders'
+    disagreements like the batch's) == ksim_schedule."""
+    import ctypes as C
+    aff_labels = ["region", "rack"]
+    nodes, running, pods, services = rnd_svc_affinity_workload(0, n_pods=80, full_labels=True)
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order, spread=spread.SpreadListers(services=services),
+                                     service_affinity=aff_labels)
+    batch = scheduler.GenericScheduler(cl, SVC_PREDS, SVC_PRIOS, mode=abi.MODE_LAUNCH, service_affinity=aff_labels)
+    one = scheduler.GenericScheduler(cl, SVC_PREDS, SVC_PRIOS, mode=abi.MODE_LAUNCH, service_affinity=aff_labels)
+    try:
+        out, _, _ = batch.schedule()
+        for k in range(len(order)):
+            pod = abi.Pod.from_buffer_copy(cl.pods[k].tobytes())
+            res = abi.Result()
+            one.h.call("ksim_schedule_one", C.byref(pod), abi.vptr(cl.pod_ports), len(cl.pod_ports),
+                       abi.vptr(cl.pod_scalars), len(cl.pod_scalars), abi.SCHEDULE_ASSUME, C.byref(res))
+            assert res.node == out[k], k
+        assert one.last_node_index == batch.last_node_index
+    finally:
+        batch.close()
+        one.close()

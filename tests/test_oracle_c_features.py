@@ -11,7 +11,8 @@ import pytest
 import cpu_ref
 import ksim_ref as R
 from ksim import abi, ingest, scheduler, spread as ksp, synth
-from workloads import (rnd_affinity_workload, rnd_mixed_workload, rnd_spread_workload, rnd_volume_workload)
+from workloads import (rnd_affinity_workload, rnd_mixed_workload, rnd_spread_workload, rnd_svc_affinity_workload,
+                       rnd_volume_workload)
 
 AFF_POLICIES = {
     "default": scheduler.provider("DefaultProvider"),
@@ -22,13 +23,13 @@ AFF_POLICIES = {
 
 
 def c_oracle_objects(nodes, running, pods, preds, prios, pvs=(), pvcs=(), spread=None, threads=4,
-                     spread_services_only=False, aux=None, custom_priorities=None):
+                     spread_services_only=False, aux=None, custom_priorities=None, service_affinity=None):
     """The simulator's loop on the C oracle over the tables scheduler.plan builds: pods popped
     LIFO (store.go:223-233).  Returns ([(pod, node or None, FitError text or None)], lastNodeIndex)."""
     order = list(reversed(pods))
     cl = ingest.Cluster.from_objects(nodes, running, order, pvs=pvs, pvcs=pvcs, spread=spread,
-                                     spread_services_only=spread_services_only, aux=aux)
-    p = scheduler.plan(cl, preds, prios, custom_priorities=custom_priorities)
+                                     spread_services_only=spread_services_only, aux=aux, service_affinity=service_affinity)
+    p = scheduler.plan(cl, preds, prios, custom_priorities=custom_priorities, service_affinity=service_affinity)
     out, reasons, _, ctr, _ = cpu_ref.run(cl, None, threads=threads, plan=p)
     res = []
     for k, w in enumerate(out):
@@ -207,3 +208,80 @@ def test_golden_service_anti_affinity_with_services_c_oracle():
         for k in range(2 * len(tied)):
             out, _, _, _, _ = cpu_ref.run(cl, None, threads=1, plan=p, counter=k)
             assert cl.names[int(out[0])] == tied[k % len(tied)], (c["test"], k, tied)
+
+
+class Ambiguous(Exception):
+    """The object oracle met a pod whose service-affinity lenders disagree on an open label."""
+
+
+def svc_simulate(nodes, running, pods, preds, prios, aff_labels, services):
+    """The simulator's loop (LIFO) on the object oracle with CheckServiceAffinity reading the live
+    scheduler cache as its pod lister (factory.go:166 podLister = schedulerCache): every cached pod,
+    the running ones and those bound so far.  Raises Ambiguous where the pods a pod's labels select
+    sit on nodes that disagree on a label its nodeSelector leaves open (filteredPods[0], a map order,
+    would decide: predicates.go:1000-1008)."""
+    infos = [R.NodeInfo(n) for n in nodes]
+    by_name = {ni.name: ni for ni in infos}
+    node_labels = {n["metadata"]["name"]: n["metadata"].get("labels") or {} for n in nodes}
+    for q in running:
+        if q["spec"].get("nodeName", "") in by_name:
+            by_name[q["spec"]["nodeName"]].add_pod(q)
+
+    def pred(pod, ni):
+        cached = [q for x in infos for q in x.pods]
+        md = pod.get("metadata") or {}
+        ns, lab = md.get("namespace", ""), md.get("labels") or {}
+        open_ = [l for l in aff_labels if l not in (pod["spec"].get("nodeSelector") or {})]
+        svcs = [x for x in services if x["metadata"].get("namespace", "") == ns and x["spec"].get("selector") is not None
+                and all(lab.get(k) == v for k, v in x["spec"]["selector"].items())]
+        if open_ and svcs:
+            lenders = {tuple(node_labels[q["spec"]["nodeName"]].get(l) for l in open_) for q in cached
+                       if q["metadata"].get("namespace", "") == ns
+                       and all((q["metadata"].get("labels") or {}).get(k) == v for k, v in lab.items())}
+            if len(lenders) > 1:
+                raise Ambiguous(md.get("name"))
+        return R.new_service_affinity_predicate(aff_labels, services, cached, nodes)(pod, ni)
+
+    sched = R.GenericScheduler(set(preds), list(prios), {"CheckServiceAffinity": pred})
+    queue, out = list(pods), []
+    while queue:
+        pod = queue.pop()
+        name = pod["metadata"]["name"]
+        try:
+            host = sched.schedule(pod, infos)
+        except R.FitError as e:
+            out.append((name, None, str(e)))
+            continue
+        bound = dict(pod, spec=dict(pod["spec"], nodeName=host))   # assume: Spec.NodeName = host (scheduler.go:366)
+        by_name[host].add_pod(bound)
+        out.append((name, host, None))
+    return out, sched.last_node_index
+
+
+SVC_PREDS = ["GeneralPredicates", "PodToleratesNodeTaints", "CheckServiceAffinity"]
+SVC_PRIOS = [("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
+
+
+@pytest.mark.parametrize("variant", ["consistent", "mixed_labels", "conflicting_running"])
+@pytest.mark.parametrize("seed", range(4))
+def test_service_affinity_with_services_matches_object_oracle(seed, variant):
+    """CheckServiceAffinity with services selecting the pods: the lender check over the counted
+    pairs (include/ksim.h ksim_affinity_tables.svc_*) places like the object oracle reading the live
+    cache, and refuses exactly where the oracle meets disagreeing lenders."""
+    aff_labels = ["region", "rack"]
+    nodes, running, pods, services = rnd_svc_affinity_workload(seed, mixed_labels=variant == "mixed_labels",
+                                                               conflicting_running=variant == "conflicting_running",
+                                                               full_labels=variant == "consistent")
+    try:
+        want, lni = svc_simulate(nodes, running, pods, SVC_PREDS, SVC_PRIOS, aff_labels, services)
+    except Ambiguous:
+        with pytest.raises(cpu_ref.Unsupported):
+            c_oracle_objects(nodes, running, pods, SVC_PREDS, SVC_PRIOS, spread=ksp.SpreadListers(services=services),
+                             service_affinity=aff_labels)
+        return
+    got, ctr = c_oracle_objects(nodes, running, pods, SVC_PREDS, SVC_PRIOS, spread=ksp.SpreadListers(services=services),
+                                service_affinity=aff_labels)
+    _same(want, got)
+    assert ctr == lni
+    if variant == "consistent":
+        assert any(m and "service affinity" in m for _, _, m in want)   # the lenders constrained something

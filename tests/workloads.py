@@ -357,3 +357,50 @@ def rnd_mixed_workload(seed, n_nodes=120, n_pods=900):
     running = [pod("run-%d" % k, rng.choice(nodes)["metadata"]["name"]) for k in range(n_nodes // 3)]
     pods = [pod("pod-%d" % k) for k in range(n_pods)]
     return nodes, running, pods, pvs, pvcs, objs
+
+
+def rnd_svc_affinity_workload(seed, n_nodes=24, n_pods=120, mixed_labels=False, conflicting_running=False,
+                              full_labels=False):
+    """CheckServiceAffinity with services (predicates.go:980-1011): nodes labelled region / rack
+    (some without, unless full_labels), services selecting app=a / app=b in ns1 and app=a in ns2, pods with app=a|b|c
+    (mixed_labels: sometimes tier=x too, so lender sets overlap and may disagree) and sometimes a
+    nodeSelector for region shared by the pods of one (namespace, app); running pods of the services
+    placed consistently on one region / rack each, or (conflicting_running) anywhere."""
+    rng = random.Random(4000 + seed)
+    nodes = rnd_nodes(rng, n_nodes, features=False)
+    for x in nodes:
+        x["status"]["allocatable"]["pods"] = "110"
+        lab = x["metadata"]["labels"]
+        if full_labels or rng.random() < 0.85:
+            lab["region"] = rng.choice(["r1", "r2"])
+        if full_labels or rng.random() < 0.7:
+            lab["rack"] = rng.choice(["k1", "k2", "k3", "k4"])
+
+    def pod(name, ns=None, app=None):
+        p = rnd_pod(rng, name, features=False)
+        p["metadata"]["namespace"] = ns or rng.choice(["ns1", "ns1", "ns2"])
+        lab = {"app": app or rng.choice("abc")}
+        if mixed_labels and rng.random() < 0.3:
+            lab["tier"] = "x"
+        p["metadata"]["labels"] = lab
+        sel = group_sel.get((p["metadata"]["namespace"], lab["app"]))   # a deployment's pods share one
+        if sel:
+            p["spec"]["nodeSelector"] = dict(sel)
+        return p
+    group_sel = {(ns, app): ({"region": rng.choice(["r1", "r2"])} if rng.random() < 0.5 else None)
+                 for ns in ("ns1", "ns2") for app in "abc"}
+    running = []
+    for k, (ns, app) in enumerate([("ns1", "a"), ("ns1", "b"), ("ns2", "a")]):
+        home = rng.choice(nodes)["metadata"]["labels"]
+        same = [x for x in nodes if all(x["metadata"]["labels"].get(l) == home.get(l) for l in ("region", "rack"))]
+        for j in range(rng.randrange(0, 3)):
+            q = pod("run-%d-%d" % (k, j), ns, app)
+            q["spec"].pop("nodeSelector", None)
+            q["spec"]["nodeName"] = rng.choice(nodes if conflicting_running else same)["metadata"]["name"]
+            running.append(q)
+    pods = [pod("pod-%d" % k) for k in range(n_pods)]
+    md = lambda ns: {"namespace": ns, "name": "s%d" % rng.randrange(1000)}
+    services = [{"metadata": md("ns1"), "spec": {"selector": {"app": "a"}}},
+                {"metadata": md("ns1"), "spec": {"selector": {"app": "b"}}},
+                {"metadata": md("ns2"), "spec": {"selector": {"app": "a"}}}]
+    return nodes, running, pods, services
