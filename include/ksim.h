@@ -38,7 +38,9 @@ extern "C" {
 #define KSIM_E_NO_NODES (-7)    /* core.ErrNoNodesAvailable (generic_scheduler.go:64,124-125) */
 
 #define KSIM_MAX_SCALAR 8   /* extended / hugepage resource columns */
-#define KSIM_MAX_RCLASS 16  /* reduce classes per pod (TaintToleration x NodeAffinity) */
+#define KSIM_MAX_RCLASS 16  /* TaintToleration / NodeAffinity values per pod class (each dimension); a
+                               product above 16 takes the launch form's wide decision */
+#define KSIM_MAX_WIDE 256   /* reduce classes per pod (TaintToleration x NodeAffinity) */
 #define KSIM_NREASONS 32    /* failure-reason histogram slots */
 #define KSIM_MAX_RANKS 8    /* devices of one node-sharded cluster */
 

@@ -365,7 +365,8 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   const int one_npt = ksim_one_npt(c.n);
   const char* ko = getenv("KSIM_ONE_WG");
   const bool one_wg = ko ? ko[0] != '0' : c.n <= 1024;
-  if (cs.one && one_npt > 0 && one_wg && (!h->have_aff || h->aff_h.n_zone <= 512) && !ksim_rt_launch_tables(h)) {
+  if (cs.one && one_npt > 0 && one_wg && (!h->have_aff || h->aff_h.n_zone <= 512) && !ksim_rt_launch_tables(h) &&
+      cs.one_pod.reserved[0] * cs.one_pod.reserved[1] <= KSIM_MAX_RCLASS) {
     h->res_host[KSIM_RES_NODE] = INT32_MIN;
     oc.lap(0);
     hipError_t e1 = ksim_launch_one(&cs, one_npt, h->stream);
@@ -385,8 +386,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
       return rc;
     }
     if (r[KSIM_RES_ERR] & 128) return ksim_rt_svc_refusal(h);
-    if (r[KSIM_RES_ERR] & 128) return ksim_rt_svc_refusal(h);
-  if (r[KSIM_RES_ERR]) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", r[KSIM_RES_ERR]);
+    if (r[KSIM_RES_ERR]) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", r[KSIM_RES_ERR]);
     return KSIM_OK;
   }
   const int npt = ksim_rt_pick_npt(c.n);
@@ -395,6 +395,8 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   if ((rc = ksim_rt_ensure_partials(h, grid))) return rc;
   cs.partials = c.partials;
   cs.pmask = c.pmask;
+  cs.wmx = c.wmx;
+  cs.wcnt = c.wcnt;
   // InterPodAffinity / SelectorSpread reductions (pass A): fused into the scan behind a grid barrier
   // when the grid is co-resident (one launch), else their own launch first
   const bool ipa = ksim_is_aff_host(h, *pod) &&

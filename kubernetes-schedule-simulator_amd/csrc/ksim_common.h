@@ -173,6 +173,8 @@ struct KsimCtx {
   uint64_t* counter;      // genericScheduler.lastNodeIndex
   uint32_t* ticket;       // last-block arrival counter
   KsimPartial* partials;  // [grid]
+  int64_t* wmx;           // wide reduce classes (K > KSIM_MAX_RCLASS, launch form): per block and class the
+  int32_t* wcnt;          // max map score among its fit nodes and their count, [grid][KSIM_MAX_WIDE]
   uint64_t* pmask;        // [grid][KSIM_PM_STRIDE] candidate masks (KSIM_PM_*)
   int32_t* out_node;      // [end-first]
   int32_t* out_reasons;   // [end-first][KSIM_NREASONS]

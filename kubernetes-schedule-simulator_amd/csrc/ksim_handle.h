@@ -81,6 +81,7 @@ struct ksim_handle {
   std::vector<DevBuf> bufs;
   KsimCtx ctx{};
   bool have_nodes = false, have_classes = false, have_pods = false;
+  bool any_wide = false;  // some pod class has more than KSIM_MAX_RCLASS reduce classes
   int64_t n_pods = 0, pod_cap = 0;
   int64_t n_port_keys = 0, port_key_cap = 0;     // pod-port array (queue)
   int64_t n_scalar_reqs = 0, scalar_req_cap = 0; // pod-scalar array (queue)
@@ -278,5 +279,8 @@ inline bool ksim_rt_aux_on(const ksim_handle* h) {
 inline bool ksim_rt_launch_tables(const ksim_handle* h) {
   return ksim_rt_aux_on(h) || (h->have_aff && h->aff_h.svc_class != nullptr && (h->ctx.preds & KSIM_P_SERVICE_AFFINITY));
 }
+// Pod classes with more than KSIM_MAX_RCLASS reduce classes (the launch form's wide decision).
+bool wide_k(const ksim_handle* h, int32_t cls);
+bool ksim_rt_range_wide(const ksim_handle* h, int64_t first, int64_t count);
 // err bit 128 (a pod read disagreeing service-affinity labels): clear it, KSIM_E_UNSUPPORTED.
 int ksim_rt_svc_refusal(ksim_handle* h);

@@ -1189,8 +1189,9 @@ void build_class_tab(const Interns& in, ClassTab* c) {
     std::sort(av.begin(), av.end()); av.erase(std::unique(av.begin(), av.end()), av.end());
     if (tv.empty()) tv.push_back(0);  // an empty taint-set list still has one class
     if (av.empty()) av.push_back(0);
-    if (tv.size() * av.size() > KSIM_MAX_RCLASS)
-      fail(KSIM_E_UNSUPPORTED, "pod class needs %zu x %zu reduce classes (> %d)", tv.size(), av.size(), KSIM_MAX_RCLASS);
+    if (tv.size() > KSIM_MAX_RCLASS || av.size() > KSIM_MAX_RCLASS)  // (a product above 16: the wide decision)
+      fail(KSIM_E_UNSUPPORTED, "pod class needs %zu x %zu reduce classes (> %d per dimension)", tv.size(), av.size(),
+           KSIM_MAX_RCLASS);
     c->n_tt[k] = (int32_t)tv.size();
     c->n_na[k] = (int32_t)av.size();
     for (size_t q = 0; q < tv.size(); ++q) c->tt_val[(size_t)k * KSIM_MAX_RCLASS + q] = tv[q];
@@ -1230,8 +1231,9 @@ bool class_addends(const ClassTab& c, int64_t w_pa, int64_t w_im, bool use_w, st
     std::vector<std::pair<int64_t, int64_t>> av(keys);
     std::sort(av.begin(), av.end());
     av.erase(std::unique(av.begin(), av.end()), av.end());
-    if ((size_t)c.n_tt[k] * av.size() > KSIM_MAX_RCLASS)
-      fail(KSIM_E_UNSUPPORTED, "pod class needs %d x %zu reduce classes (> %d)", c.n_tt[k], av.size(), KSIM_MAX_RCLASS);
+    if (av.size() > KSIM_MAX_RCLASS)
+      fail(KSIM_E_UNSUPPORTED, "pod class needs %d x %zu reduce classes (> %d per dimension)", c.n_tt[k], av.size(),
+           KSIM_MAX_RCLASS);
     (*nna)[k] = (int32_t)av.size();
     for (size_t q = 0; q < av.size(); ++q) {
       (*nav)[(size_t)k * KSIM_MAX_RCLASS + q] = av[q].first;

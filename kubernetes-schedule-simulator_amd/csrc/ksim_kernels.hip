@@ -401,7 +401,12 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   __shared__ uint64_t s_ctr;
   __shared__ int64_t s_Mq[KSIM_MAX_RCLASS], s_tot[KSIM_MAX_RCLASS];
   __shared__ int32_t s_Cq[KSIM_MAX_RCLASS];
-  __shared__ int64_t s_tv[KSIM_MAX_RCLASS], s_av[KSIM_MAX_RCLASS], s_ad[KSIM_MAX_RCLASS];
+  __shared__ int64_t s_tv[KSIM_MAX_WIDE], s_av[KSIM_MAX_WIDE], s_ad[KSIM_MAX_WIDE];
+  // wide pods (K > KSIM_MAX_RCLASS): per class the block's max and count, then the grid's, and the
+  // winning classes
+  __shared__ int64_t s_wm[KSIM_MAX_WIDE];
+  __shared__ int32_t s_wc[KSIM_MAX_WIDE];
+  __shared__ uint8_t s_ww[KSIM_MAX_WIDE];
   // last block, single reduce class: every block's (fit, max, count) as combined, for the locate step
   constexpr int LOC_MAX = 1024;
   __shared__ int64_t s_bmx[LOC_MAX];
@@ -430,6 +435,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   const int k1 = c.one ? P.reserved[0] : (c.w[KSIM_W_TAINT_TOLERATION] != 0) ? c.n_tt[P.cls] : 1;
   const int k2 = c.one ? P.reserved[1] : c.use_na ? c.n_na[P.cls] : 1;
   const int K = k1 * k2;
+  const bool wide = K > KSIM_MAX_RCLASS;  // uniform: the wide decision (per-class arrays in LDS / global)
   // what the last block's decision reads, fetched now while the chunk is evaluated: the counter
   // (kernels of a stream run one after another, so its value is final) and the pod's per-class
   // TaintToleration / NodeAffinity values and NodePreferAvoidPods addends
@@ -550,9 +556,26 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   }
   if (lane == 0) s_fit[wv] = nfit;
 
+  if (wide) {
+    // per class: the block's max map score among its fit nodes (LDS max), then the count at it
+    for (int q = tid; q < K; q += KSIM_BLOCK) { s_wm[q] = INT64_MIN; s_wc[q] = 0; }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NPT; ++k)
+      if (fit[k]) __hip_atomic_fetch_max(&s_wm[cl[k]], sc[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < NPT; ++k)
+      if (fit[k] && sc[k] == s_wm[cl[k]]) atomicAdd(&s_wc[cl[k]], 1);
+    __syncthreads();
+    for (int q = tid; q < K; q += KSIM_BLOCK) {
+      c.wmx[(int64_t)blockIdx.x * KSIM_MAX_WIDE + q] = s_wm[q];
+      c.wcnt[(int64_t)blockIdx.x * KSIM_MAX_WIDE + q] = s_wc[q];
+    }
+  }
 #pragma unroll
   for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
-    if (q >= K) break;
+    if (q >= K || wide) break;
     int64_t v = INT64_MIN;
 #pragma unroll
     for (int k = 0; k < NPT; ++k)
@@ -593,7 +616,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     int32_t f = 0;
     for (int w = 0; w < KSIM_WAVES; ++w) f += s_fit[w];
     p->fit = f;
-    for (int q = 0; q < K; ++q) {
+    for (int q = 0; q < (wide ? 0 : K); ++q) {
       int64_t m = INT64_MIN;
       int32_t n = 0;
       for (int w = 0; w < KSIM_WAVES; ++w) {
@@ -644,7 +667,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     }
 #pragma unroll
     for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
-      if (q >= K) break;
+      if (q >= K || wide) break;
       const int32_t n = p->cnt[q];
       if (n == 0) continue;
       const int64_t m = p->mx[q];
@@ -656,13 +679,76 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   if (lane == 0) s_fit[wv] = wf;
 #pragma unroll
   for (int q = 0; q < KSIM_MAX_RCLASS; ++q) {
-    if (q >= K) break;
+    if (q >= K || wide) break;
     const int64_t wm = wave_max_i64(ln[q] ? lm[q] : INT64_MIN);
     const int32_t wn = wave_sum_i32((ln[q] && lm[q] == wm) ? ln[q] : 0);
     if (lane == 0) { s_mx[wv][q] = wm; s_cnt[wv][q] = wn; }
   }
   __syncthreads();
   SSTAMP(4);
+
+  if (wide) {
+    // the grid's max and count per class (thread q), the NormalizeReduce maxima over the present
+    // classes, each class's total and the winners (generic_scheduler.go:632-639, reduce.go:29-64)
+    int64_t tq = INT64_MIN, mT = 0, mA = 0;
+    for (int q = tid; q < K; q += KSIM_BLOCK) {
+      int64_t m = INT64_MIN;
+      int32_t n = 0;
+      for (int b = 0; b < G; ++b) {
+        const int32_t cb = c.wcnt[(int64_t)b * KSIM_MAX_WIDE + q];
+        if (!cb) continue;
+        const int64_t mb = c.wmx[(int64_t)b * KSIM_MAX_WIDE + q];
+        if (mb > m) { m = mb; n = cb; }
+        else if (mb == m) n += cb;
+      }
+      s_wm[q] = m;
+      s_wc[q] = n;
+      if (n) {
+        if (k1 > 1 || c.w[KSIM_W_TAINT_TOLERATION]) mT = s_tv[q] > mT ? s_tv[q] : mT;
+        if (k2 > 1 || c.w[KSIM_W_NODE_AFFINITY]) mA = s_av[q] > mA ? s_av[q] : mA;
+      }
+    }
+    mT = wave_max_i64(mT);
+    mA = wave_max_i64(mA);
+    if (lane == 0) { s_v[0][wv] = mT; s_v[1][wv] = mA; }
+    __syncthreads();
+    mT = 0; mA = 0;
+    for (int w = 0; w < KSIM_WAVES; ++w) {
+      mT = s_v[0][w] > mT ? s_v[0][w] : mT;
+      mA = s_v[1][w] > mA ? s_v[1][w] : mA;
+    }
+    for (int q = tid; q < K; q += KSIM_BLOCK) {
+      if (!s_wc[q]) continue;
+      uint64_t t = (uint64_t)s_wm[q];
+      if (c.w[KSIM_W_TAINT_TOLERATION]) t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(s_tv[q], mT, true);
+      if (c.w[KSIM_W_NODE_AFFINITY]) t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(s_av[q], mA, false);
+      t += (uint64_t)s_ad[q];
+      tq = (int64_t)t > tq ? (int64_t)t : tq;
+    }
+    const int64_t best_w = wave_max_i64(tq);
+    __syncthreads();  // s_v reused
+    if (lane == 0) s_v[0][wv] = best_w;
+    __syncthreads();
+    int64_t best = INT64_MIN;
+    for (int w = 0; w < KSIM_WAVES; ++w) best = s_v[0][w] > best ? s_v[0][w] : best;
+    int64_t cw = 0;
+    for (int q = tid; q < K; q += KSIM_BLOCK) {
+      bool win = false;
+      if (s_wc[q]) {
+        uint64_t t = (uint64_t)s_wm[q];
+        if (c.w[KSIM_W_TAINT_TOLERATION]) t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(s_tv[q], mT, true);
+        if (c.w[KSIM_W_NODE_AFFINITY]) t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(s_av[q], mA, false);
+        t += (uint64_t)s_ad[q];
+        win = (int64_t)t == best;
+      }
+      s_ww[q] = win ? 1 : 0;
+      if (win) cw += s_wc[q];
+    }
+    __syncthreads();  // s_v reused
+    const int32_t cws = wave_sum_i32((int32_t)cw);
+    if (lane == 0) s_cnt[wv][0] = cws;
+    __syncthreads();
+  }
 
   if (tid == 0) {
     D.pod = pod;
@@ -679,6 +765,15 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     } else if (F == 1) {  // generic_scheduler.go:153-156: no selectHost, no counter bump
       D.mode = 1;
       D.ix = 0;
+    } else if (wide) {  // the winners and their count from the wide combine above
+      D.mode = 2;
+      int64_t C = 0;
+      for (int w = 0; w < KSIM_WAVES; ++w) C += s_cnt[w][0];
+      D.winners = 0;
+      const uint64_t li = s_ctr;  // generic_scheduler.go:192-195
+      D.ix = ((li >> 32) == 0 && C < ((int64_t)1 << 32)) ? (int64_t)((uint32_t)li % (uint32_t)C) : (int64_t)(li % (uint64_t)C);
+      *c.counter = li + 1;
+      s_ctr = li + 1;
     } else if (K == 1) {  // one reduce class: it wins, its count at the maximum is C
       D.mode = 2;
       int64_t m = INT64_MIN;
@@ -769,6 +864,15 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
       if (loc_lds) return D.mode == 1 ? s_bfit[b] : ((s_bcnt[b] && s_bmx[b] == D.M[0]) ? s_bcnt[b] : 0);
       const KsimPartial* p = &c.partials[b];
       if (D.mode == 1) return p->fit;
+      if (wide) {
+        int64_t cw = 0;
+        for (int q = 0; q < K; ++q) {
+          if (!s_ww[q]) continue;
+          const int32_t n = c.wcnt[b * KSIM_MAX_WIDE + q];
+          if (n && c.wmx[b * KSIM_MAX_WIDE + q] == s_wm[q]) cw += n;
+        }
+        return cw;
+      }
       int64_t cb = 0;
       for (int q = 0; q < K; ++q)
         if (((D.winners >> q) & 1u) && p->cnt[q] && p->mx[q] == D.M[q]) cb += p->cnt[q];
@@ -794,7 +898,19 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
     }
     // ---- the selected block's candidate masks (no re-evaluation), pick the exact node ----
     const int64_t bb = D.blk * c.chunk;
-    if (tid < NPT * KSIM_WAVES) {
+    if (wide && D.mode == 2) {
+      // no per-class masks: the selected block's nodes evaluated again, with the final maxima
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        bool f;
+        int64_t sk;
+        int qk;
+        uint32_t rk;
+        eval_one<false>(c, P, bb + k * KSIM_BLOCK + tid, k1, k2, ipa, f, sk, qk, rk);
+        const uint64_t b = __ballot(f && s_ww[qk] && sk == s_wm[qk]);
+        if (lane == 0) s_ball[k][wv] = b;
+      }
+    } else if (tid < NPT * KSIM_WAVES) {
       const int k = tid / KSIM_WAVES, w = tid % KSIM_WAVES;
       uint64_t* pb = c.pmask + D.blk * KSIM_PM_STRIDE;
       uint64_t m = 0;
@@ -887,7 +1003,7 @@ __global__ __launch_bounds__(ONE_BLOCK) void ksim_one_kernel(KsimCtx c) {
   const ksim_pod P = c.one_pod;
   const int64_t pod = c.first;
   const int k1 = P.reserved[0], k2 = P.reserved[1];
-  const int K = k1 * k2;
+  const int K = k1 * k2 <= KSIM_MAX_RCLASS ? k1 * k2 : KSIM_MAX_RCLASS;  // (the host never sends a wide pod here)
   // the decision's inputs, loaded while the nodes are evaluated (to LDS afterwards)
   __shared__ int64_t s_tv[KSIM_MAX_RCLASS], s_av[KSIM_MAX_RCLASS], s_ad[KSIM_MAX_RCLASS];
   uint64_t pre_ctr = 0;

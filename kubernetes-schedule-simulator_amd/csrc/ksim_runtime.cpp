@@ -187,8 +187,9 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
   const size_t lw = (L + 31) / 32, tw = (T + 31) / 32;
   for (size_t k = 0; k < C; ++k) {
     const int a = t->n_tt ? t->n_tt[k] : 1, b = t->n_na ? t->n_na[k] : 1;
-    if (a < 1 || b < 1 || a * b > KSIM_MAX_RCLASS)
-      return ksim_fail(h, KSIM_E_UNSUPPORTED, "class %zu: %d x %d reduce classes exceed %d", k, a, b, KSIM_MAX_RCLASS);
+    if (a < 1 || b < 1 || a > KSIM_MAX_RCLASS || b > KSIM_MAX_RCLASS)
+      return ksim_fail(h, KSIM_E_UNSUPPORTED, "class %zu: %d x %d reduce classes exceed %d per dimension", k, a, b,
+                       KSIM_MAX_RCLASS);
   }
   KsimCtx& c = h->ctx;
   int rc;
@@ -222,6 +223,8 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
   h->n_taint_sets = t->n_taint_sets;
   h->h_n_tt.assign(t->n_tt ? t->n_tt : ones.data(), (t->n_tt ? t->n_tt : ones.data()) + C);
   h->h_n_na.assign(t->n_na ? t->n_na : ones.data(), (t->n_na ? t->n_na : ones.data()) + C);
+  h->any_wide = false;
+  for (size_t k = 0; k < C; ++k) h->any_wide |= wide_k(h, (int32_t)k);
   // class pointers are baked into the launch graph's kernel arguments
   if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
   if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
@@ -320,6 +323,20 @@ static bool fast_k(const ksim_handle* h, int32_t cls) {
   const int k1 = h->ctx.w[KSIM_W_TAINT_TOLERATION] ? h->h_n_tt[cls] : 1;
   const int k2 = h->ctx.use_na ? h->h_n_na[cls] : 1;
   return k1 * k2 == 1;
+}
+
+// A pod class with more than KSIM_MAX_RCLASS reduce classes: the launch form's wide decision.
+bool wide_k(const ksim_handle* h, int32_t cls) {
+  const int k1 = h->ctx.w[KSIM_W_TAINT_TOLERATION] ? h->h_n_tt[cls] : 1;
+  const int k2 = h->ctx.use_na ? h->h_n_na[cls] : 1;
+  return k1 * k2 > KSIM_MAX_RCLASS;
+}
+
+bool ksim_rt_range_wide(const ksim_handle* h, int64_t first, int64_t count) {
+  if (!h->any_wide) return false;
+  for (int64_t q = first; q < first + count; ++q)
+    if (wide_k(h, h->q_cls[q])) return true;
+  return false;
 }
 
 void ksim_rt_recompute_fast(ksim_handle* h) {
@@ -479,13 +496,21 @@ int ksim_rt_ensure_partials(ksim_handle* h, int grid) {
   if (c.partials && h->part_cap >= grid) return KSIM_OK;
   KsimPartial* p;
   uint64_t* pm;
-  int rc = dev_alloc(h, &p, (size_t)std::max(grid, 1024));
+  int64_t* wm;
+  int32_t* wc;
+  const size_t cap = (size_t)std::max(grid, 1024);
+  int rc = dev_alloc(h, &p, cap);
   if (rc) return rc;
-  if ((rc = dev_alloc(h, &pm, (size_t)std::max(grid, 1024) * KSIM_PM_STRIDE))) { dev_free(h, p); return rc; }
+  if ((rc = dev_alloc(h, &pm, cap * KSIM_PM_STRIDE))) { dev_free(h, p); return rc; }
+  if ((rc = dev_alloc(h, &wm, cap * KSIM_MAX_WIDE)) || (rc = dev_alloc(h, &wc, cap * KSIM_MAX_WIDE))) return rc;
   dev_free(h, c.partials);
   dev_free(h, c.pmask);
+  dev_free(h, c.wmx);
+  dev_free(h, c.wcnt);
   c.partials = p;
   c.pmask = pm;
+  c.wmx = wm;
+  c.wcnt = wc;
   h->part_cap = std::max(grid, 1024);
   if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
   if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
@@ -1174,7 +1199,7 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
   } else {
   // the auxiliary priority and the service-affinity lender check (ksim_affinity_tables.aux_* / svc_*)
   // are read by the launch-form kernels alone
-  const int mode = ksim_rt_launch_tables(h) ? KSIM_MODE_LAUNCH : h->cfg.mode;
+  const int mode = (ksim_rt_launch_tables(h) || ksim_rt_range_wide(h, first, count)) ? KSIM_MODE_LAUNCH : h->cfg.mode;
   int rc = mode == KSIM_MODE_TREE         ? run_tree_mode(h, first, count, st)
            : mode == KSIM_MODE_AUTO       ? run_auto_mode(h, first, count, st)
            : mode == KSIM_MODE_PERSISTENT ? run_persistent_mode(h, first, count, st)

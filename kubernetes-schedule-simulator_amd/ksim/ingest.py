@@ -807,8 +807,10 @@ def build_class_tables(label_items, taint_items, specs):
                               and not any(tolerates(t, x) for t in prefer_tols)))
         tv = sorted(set(counts))
         av = sorted(set(weights))
-        if len(tv) * len(av) > abi.MAX_RCLASS:
-            raise Unsupported("pod class needs %d x %d reduce classes (> %d)" % (len(tv), len(av), abi.MAX_RCLASS))
+        if len(tv) > abi.MAX_RCLASS or len(av) > abi.MAX_RCLASS:
+            # more than 16 values in one dimension (a product above 16 takes the wide decision)
+            raise Unsupported("pod class needs %d x %d reduce classes (> %d per dimension)" % (len(tv), len(av),
+                                                                                          abi.MAX_RCLASS))
         ntt[k], nna[k] = len(tv), len(av)
         ttv[k, :len(tv)] = tv
         nav[k, :len(av)] = av

@@ -225,9 +225,9 @@ def class_tables_for(tables, priorities, label_sets=(), custom=None):
             pa = [a + w_im * int(x) for a, x in zip(pa, im_s[k])]
         keys = list(zip((int(x) if use_w else 0 for x in tables["na_w"][k]), (a + int(b) for a, b in zip(pa, lab_add))))
         av = sorted(set(keys))
-        if int(tables["n_tt"][k]) * len(av) > abi.MAX_RCLASS:
-            raise Unsupported("pod class needs %d x %d reduce classes (> %d)" % (int(tables["n_tt"][k]), len(av),
-                                                                                abi.MAX_RCLASS))
+        if len(av) > abi.MAX_RCLASS:
+            raise Unsupported("pod class needs %d x %d reduce classes (> %d per dimension)" % (int(tables["n_tt"][k]), len(av),
+                                                                                              abi.MAX_RCLASS))
         nna[k] = len(av)
         nav[k, :len(av)] = [w for w, _ in av]
         add[k, :len(av)] = [p for _, p in av]

@@ -285,3 +285,29 @@ def test_service_affinity_with_services_matches_object_oracle(seed, variant):
     assert ctr == lni
     if variant == "consistent":
         assert any(m and "service affinity" in m for _, _, m in want)   # the lenders constrained something
+
+
+def wide_workload(seed, n_nodes=60, n_pods=300):
+    """Taints, node selectors / affinity and preferAvoidPods with owned pods keeping their preferred
+    node-affinity terms: pod classes with more than 16 (TaintToleration x NodeAffinity /
+    NodePreferAvoidPods) reduce classes — the launch form's wide decision."""
+    from workloads import add_prefer_avoid, rnd_workload
+    nodes, running, pods = rnd_workload(seed, n_nodes=n_nodes, n_pods=n_pods)
+    nodes, pods = add_prefer_avoid(seed, nodes, pods, keep_preferred=True)
+    return nodes, running, pods
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_wide_reduce_classes_match_object_oracle(seed):
+    """More than 16 reduce classes per pod class (formerly refused): ingest + plan + the C oracle
+    against the object oracle."""
+    nodes, running, pods = wide_workload(seed)
+    preds, prios = scheduler.provider("DefaultProvider")
+    want, lni = R.simulate(nodes, running, pods, set(preds), list(prios))
+    got, ctr = c_oracle_objects(nodes, running, pods, preds, prios)
+    _same(want, got)
+    assert ctr == lni
+    cl = ingest.Cluster.from_objects(nodes, running, list(reversed(pods)))
+    t = scheduler.plan(cl, preds, prios).tables
+    k = (np.asarray(t["n_tt"]) * np.asarray(t["n_na"]))[np.asarray(cl.pods["cls"])]
+    assert (k > 16).any()

@@ -101,7 +101,7 @@ CONTROLLERS = [("ReplicationController", "rc-uid-1"), ("ReplicationController", 
                ("ReplicaSet", "rs-uid-1"), ("ReplicaSet", "rs-uid-2"), ("StatefulSet", "ss-uid-1")]
 
 
-def add_prefer_avoid(seed, nodes, pods):
+def add_prefer_avoid(seed, nodes, pods, keep_preferred=False):
     """NodePreferAvoidPods inputs on a workload (own stream, the base workload unchanged): ~35 %
     of nodes carry a preferAvoidPods annotation naming one or two controllers (some with a
     case-varied field name, a few malformed), ~50 % of pods an ownerReference (controller or not,
@@ -128,8 +128,9 @@ def add_prefer_avoid(seed, nodes, pods):
             p["metadata"]["ownerReferences"] = [ref]
             # (TaintToleration x NodeAffinity weight x avoid) classes must stay <= 16 per pod class:
             # an owned pod keeps its required node affinity, not its preferred terms
-            na = ((p["spec"].get("affinity") or {}).get("nodeAffinity") or {})
-            na.pop("preferredDuringSchedulingIgnoredDuringExecution", None)
+            if not keep_preferred:  # keep_preferred: pod classes beyond 16 reduce classes (the wide decision)
+                na = ((p["spec"].get("affinity") or {}).get("nodeAffinity") or {})
+                na.pop("preferredDuringSchedulingIgnoredDuringExecution", None)
     return nodes, pods
 
 
