@@ -87,6 +87,11 @@ struct KsimAff {
 };
 
 #define KSIM_AFF_MM 9      // pass-A result words
+// node-sharded launch form: exchange slots (pod mod KSIM_LX_SLOTS) of KSIM_LX_REC words per rank,
+// each word (tag:24 | value:40): the fit count, then per reduce class its max (biased by 2^39) and count
+#define KSIM_LX_SLOTS 4
+#define KSIM_LX_REC (1 + 2 * KSIM_MAX_RCLASS)
+#define KSIM_LX_BIAS (1ll << 39)
 #define KSIM_AFF_PART 8    // pass-A block-partial words
 
 // Volume tables on the device (ksim_load_volumes; layout in include/ksim.h).
@@ -184,6 +189,16 @@ struct KsimCtx {
   int32_t* out_fit;       // optional (per-pod drop-in): [0] = len(filtered), [1] |= ksim_row_status
   const KsimAff* aff;     // inter-pod affinity tables (device), null when none are loaded
   const KsimVol* vol;     // volume tables (device), null when none are loaded
+  // node-sharded launch form (world > 1, pods the fast kernel does not take; SURVEY.md §8e Phase A):
+  // the last block exchanges this rank's fit count and per-class (max, count) with every rank
+  // through the launch region of the exchange buffers, decides on the world's, and the rank that
+  // holds the selected node commits it.  sh_world 0: off
+  int32_t sh_world, sh_rank;
+  int64_t sh_base;                       // global name rank of this shard's first node
+  uint32_t sh_tag0;                      // tag of pod p: 1 + (sh_tag0 + p - first) mod (2^24 - 1)
+  uint32_t sh_pad;
+  uint64_t sh_start_ticks;               // the first pod's wait bound (the start handshake)
+  uint64_t* sh_peers[KSIM_MAX_RANKS];    // every rank's launch region as mapped here (self included)
   // per-pod launches (ksim_schedule_one): the pod and its arrays travel in the kernel arguments,
   // so no read of host memory or of a staging copy sits on the kernel's critical path
   int32_t one;            // 1: the pod is one_pod (index first), its ports / scalars one_ports / one_scalars

@@ -42,6 +42,7 @@ extern "C" int ksim_pfast_config(int64_t n, int max_grid, int stream, int* grid,
 extern "C" hipError_t ksim_pstream_prepare(const KsimCtx* c, double* mirror, hipStream_t s);
 extern "C" size_t ksim_pfast_granule_bytes(void);
 extern "C" size_t ksim_shard_xchg_bytes(void);
+extern "C" size_t ksim_shard_lx_offset(void);
 extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, double* mirror,
                                         const KsimShard* sh, hipStream_t s);
 extern "C" hipError_t ksim_tree_build(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,

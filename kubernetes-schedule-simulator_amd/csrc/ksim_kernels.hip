@@ -46,6 +46,14 @@ __device__ __forceinline__ int64_t block_incl_scan(int64_t v, int64_t* s_w) {
   return v + add;
 }
 
+// cross-device exchange words (fine-grained buffers written by peers over xGMI)
+__device__ __forceinline__ void lx_store(uint64_t* g, uint64_t v) {
+  __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t lx_load(const uint64_t* g) {
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 struct Decision {
   int64_t pod;
   int32_t K, K2;
@@ -407,6 +415,11 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   __shared__ int64_t s_wm[KSIM_MAX_WIDE];
   __shared__ int32_t s_wc[KSIM_MAX_WIDE];
   __shared__ uint8_t s_ww[KSIM_MAX_WIDE];
+  // node-sharded launch form: every rank's fit count and per-class (max, count)
+  __shared__ int64_t s_rM[KSIM_MAX_RANKS][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_rC[KSIM_MAX_RANKS][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_rF[KSIM_MAX_RANKS];
+  __shared__ int s_shok;
   // last block, single reduce class: every block's (fit, max, count) as combined, for the locate step
   constexpr int LOC_MAX = 1024;
   __shared__ int64_t s_bmx[LOC_MAX];
@@ -428,6 +441,8 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   }
   const int64_t pod = c.one ? c.first : *c.cursor;
   if (pod >= c.end) return;  // uniform: graph replay past the end of the queue
+  // node-sharded: a peer that never answered (err bit 4) ends the run for every later launch
+  if (c.sh_world > 1 && (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4)) return;
   ksim_pod P;  // (a branch, not a pointer select: the pod stays in registers)
   if (c.one) P = c.one_pod;
   else P = c.pods[pod];
@@ -687,6 +702,91 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   __syncthreads();
   SSTAMP(4);
 
+  if (c.sh_world > 1) {
+    // ---- node-sharded: the world's decision inputs (SURVEY.md §8e Phase A) ----
+    const int me = c.sh_rank, W = 1 + 2 * K;
+    if (tid == 0) {
+      int32_t F = 0;
+      for (int w = 0; w < KSIM_WAVES; ++w) F += s_fit[w];
+      s_rF[me] = F;
+      for (int q = 0; q < K; ++q) {
+        int64_t m = INT64_MIN;
+        int32_t n = 0;
+        for (int w = 0; w < KSIM_WAVES; ++w) {
+          if (s_cnt[w][q] == 0) continue;
+          if (s_mx[w][q] > m) { m = s_mx[w][q]; n = s_cnt[w][q]; }
+          else if (s_mx[w][q] == m) n += s_cnt[w][q];
+        }
+        s_rM[me][q] = m;
+        s_rC[me][q] = n;
+      }
+      s_shok = 1;
+    }
+    __syncthreads();
+    if (wv == 0) {
+      const uint64_t tag = (uint64_t)(1u + (uint32_t)((c.sh_tag0 + (uint64_t)(pod - c.first)) % 0xFFFFFFull)) << 40;
+      const int slot = (int)(pod % KSIM_LX_SLOTS);
+      const uint64_t vmask = (1ull << 40) - 1;
+      auto word = [&](int j) -> uint64_t {  // this rank's word j: F, then (max + bias, count) per class
+        if (j == 0) return (uint64_t)(uint32_t)s_rF[me];
+        const int q = (j - 1) >> 1;
+        if ((j - 1) & 1) return (uint64_t)(uint32_t)s_rC[me][q];
+        return s_rC[me][q] ? (uint64_t)(s_rM[me][q] + KSIM_LX_BIAS) & vmask : 0ull;
+      };
+      for (int x = lane; x < c.sh_world * W; x += 64) {
+        const int r = x / W, j = x % W;
+        lx_store(c.sh_peers[r] + ((int64_t)slot * KSIM_MAX_RANKS + me) * KSIM_LX_REC + j, tag | word(j));
+      }
+      const uint64_t* mine = c.sh_peers[me] + (int64_t)slot * KSIM_MAX_RANKS * KSIM_LX_REC;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      const uint64_t lim = pod == c.first ? c.sh_start_ticks : 200000000ull;  // 2 s at 100 MHz
+      for (;;) {
+        bool ready = true;
+        for (int x = lane; x < c.sh_world * W; x += 64) {
+          const int r = x / W, j = x % W;
+          if (r == me) continue;
+          const uint64_t v = lx_load(mine + (int64_t)r * KSIM_LX_REC + j);
+          if ((v & ~vmask) != tag) { ready = false; continue; }
+          const uint64_t val = v & vmask;
+          if (j == 0) s_rF[r] = (int32_t)val;
+          else if ((j - 1) & 1) s_rC[r][(j - 1) >> 1] = (int32_t)val;
+          else s_rM[r][(j - 1) >> 1] = (int64_t)val - KSIM_LX_BIAS;
+        }
+        if (__all(ready)) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > lim) {
+          if (lane == 0) { atomicOr(c.err, 4); s_shok = 0; }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+    if (!s_shok) {  // a peer never answered: the run ends here (the host reports it)
+      if (tid == 0) { c.out_node[pod] = -1; *c.ticket = 0; }
+      return;
+    }
+    // the world's inputs in the slots the decision below reads (wave 0's; the other waves' cleared)
+    if (tid == 0) {
+      int32_t F = 0;
+      for (int r = 0; r < c.sh_world; ++r) F += s_rF[r];
+      s_fit[0] = F;
+      for (int w = 1; w < KSIM_WAVES; ++w) s_fit[w] = 0;
+      for (int q = 0; q < K; ++q) {
+        int64_t m = INT64_MIN;
+        int32_t n = 0;
+        for (int r = 0; r < c.sh_world; ++r) {
+          if (s_rC[r][q] == 0) continue;
+          if (s_rM[r][q] > m) { m = s_rM[r][q]; n = s_rC[r][q]; }
+          else if (s_rM[r][q] == m) n += s_rC[r][q];
+        }
+        s_mx[0][q] = m;
+        s_cnt[0][q] = n;
+        for (int w = 1; w < KSIM_WAVES; ++w) s_cnt[w][q] = 0;
+      }
+    }
+    __syncthreads();
+  }
+
   if (wide) {
     // the grid's max and count per class (thread q), the NormalizeReduce maxima over the present
     // classes, each class's total and the winners (generic_scheduler.go:632-639, reduce.go:29-64)
@@ -842,7 +942,32 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   __syncthreads();
   SSTAMP(5);
 
-  if (D.mode == 0) {
+  if (c.sh_world > 1 && D.mode != 0) {
+    // selectHost's ix-th node from the top: ranks hold ascending name-rank shards, so the ranks above
+    // this one come first; this rank holds it when ix falls among its own matches
+    if (tid == 0) {
+      int64_t above = 0, here = 0;
+      for (int r = 0; r < c.sh_world; ++r) {
+        int64_t m = 0;
+        if (D.mode == 1) {
+          m = s_rF[r];
+        } else {
+          for (int q = 0; q < K; ++q)
+            if (((D.winners >> q) & 1u) && s_rC[r][q] && s_rM[r][q] == D.M[q]) m += s_rC[r][q];
+        }
+        if (r > c.sh_rank) above += m;
+        else if (r == c.sh_rank) here = m;
+      }
+      const int64_t ixl = D.ix - above;
+      if (ixl >= 0 && ixl < here) D.ix = ixl;
+      else D.mode = 3;  // another rank holds the node
+    }
+    __syncthreads();
+  }
+
+  if (D.mode == 3) {
+    if (tid == 0) D.node = -2;  // another rank's node (read by thread 0 below)
+  } else if (D.mode == 0) {
     if (COLLECT && c.out_reasons) {
       for (int r = 0; r < KSIM_NREASONS; ++r) {
         int32_t v = 0;
@@ -963,7 +1088,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   if (c.out_fit) __syncthreads();  // (uniform) wave 1's affinity commit is done
   SSTAMP(8);
   if (tid == 0) {
-    c.out_node[pod] = (int32_t)D.node;
+    c.out_node[pod] = (int32_t)(c.sh_world > 1 && D.node >= 0 ? c.sh_base + D.node : D.node);
     if (c.out_fit) {  // per-pod drop-in: fit count, error word and lastNodeIndex into the result block
       c.out_fit[0] = D.fitTotal;
       c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

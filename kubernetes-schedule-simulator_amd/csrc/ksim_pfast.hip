@@ -934,7 +934,11 @@ extern "C" int ksim_pfast_config(int64_t n, int max_grid, int stream, int* grid,
 
 extern "C" size_t ksim_pfast_granule_bytes(void) { return (size_t)NREP * REP_STRIDE * sizeof(uint64_t); }
 
-extern "C" size_t ksim_shard_xchg_bytes(void) { return (size_t)ANSLOT * KSIM_MAX_RANKS * 4 * sizeof(uint64_t); }
+// the fast kernel's aggregate slots, then the launch form's (KSIM_LX_*) at ksim_shard_lx_offset()
+extern "C" size_t ksim_shard_lx_offset(void) { return (size_t)ANSLOT * KSIM_MAX_RANKS * 4; }  // in words
+extern "C" size_t ksim_shard_xchg_bytes(void) {
+  return (ksim_shard_lx_offset() + (size_t)KSIM_LX_SLOTS * KSIM_MAX_RANKS * KSIM_LX_REC) * sizeof(uint64_t);
+}
 
 // float64 image of the node table for the streaming form: one pass over the int64 columns
 // (48 B read, 48 B written per node) before each streaming call.

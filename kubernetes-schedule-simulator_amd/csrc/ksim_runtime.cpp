@@ -1184,10 +1184,33 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
       if (!h->shard.peers[r]) return ksim_fail(h, KSIM_E_STATE, "ksim_schedule: rank %d is not connected", r);
     int grid = 0, lds_rows = 0;
     const int form = pfast_form(h, first, count, &grid, &lds_rows);
-    if (!form)
-      return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling takes resource-only pods on shards of at most ~1M "
-                                         "nodes per device");
-    int rc = run_pfast_mode(h, first, count, grid, lds_rows, form == 2, st);
+    int rc;
+    if (form) {
+      rc = run_pfast_mode(h, first, count, grid, lds_rows, form == 2, st);
+    } else {
+      // pods beyond the fast kernel (selectors, taints, ports, reduce classes): the launch form,
+      // exchanging each pod's decision inputs across the ranks (SURVEY.md §8e Phase A)
+      if (ksim_rt_range_wide(h, first, count))
+        return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling of pods with more than %d reduce classes",
+                         KSIM_MAX_RCLASS);
+      for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED})
+        if (c.w[k] > ((int64_t)1 << 30))
+          return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling: a map-priority weight above 2^30");
+      c.sh_world = h->shard.world;
+      c.sh_rank = h->shard.rank;
+      c.sh_base = h->shard.node_base;
+      c.sh_tag0 = h->shard.xtag_base;
+      c.sh_start_ticks = h->shard.start_ticks;
+      for (int r = 0; r < KSIM_MAX_RANKS; ++r)
+        c.sh_peers[r] = h->shard.peers[r] ? h->shard.peers[r] + ksim_shard_lx_offset() : nullptr;
+      // the tags are baked into the launch graph's arguments: capture it again for this call
+      if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
+      if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
+      rc = run_launch_mode(h, first, count, st);
+      c.sh_world = 0;
+      if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
+      if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
+    }
     h->shard.xtag_base += (uint32_t)count;
     if (rc) return rc;
     int32_t err = 0;

@@ -15,6 +15,7 @@ def main():
     n_nodes = int(sys.argv[6]) if len(sys.argv) > 6 else 40_000
     n_pods = int(sys.argv[7]) if len(sys.argv) > 7 else 2500
     split = int(sys.argv[8]) if len(sys.argv) > 8 else 1200
+    workload = sys.argv[9] if len(sys.argv) > 9 else "c3"   # c2: selectors, taints, reduce classes
     import time
     import numpy as np
     import torch
@@ -23,7 +24,7 @@ def main():
     device = rank % max(1, torch.cuda.device_count())
     from ksim import scheduler, synth
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%s" % port, rank=rank, world_size=world)
-    cl, p, q = synth.config_c3(n_nodes, n_pods, seed=9)
+    cl, p, q = synth.config_c3(n_nodes, n_pods, seed=9) if workload == "c3" else synth.config_c2(n_nodes, n_pods, seed=9)
     s = scheduler.ShardedScheduler(cl, p, q, rank, world, device=device)
     s.connect_torch(dist)
     dist.barrier()

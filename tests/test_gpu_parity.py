@@ -529,7 +529,7 @@ def test_node_sharded_fills_cluster_with_fit_errors(monkeypatch):
     assert all(s.last_node_index == ref_ctr for s in scheds)
 
 
-def _sharded_processes(tmp_path, world, skew, n_nodes, n_pods, split, env_extra=None, wait=150):
+def _sharded_processes(tmp_path, world, skew, n_nodes, n_pods, split, env_extra=None, wait=150, workload="c3"):
     """`world` shard_worker.py processes over a gloo group; returns their .npz results."""
     import socket
     import subprocess
@@ -541,7 +541,8 @@ def _sharded_processes(tmp_path, world, skew, n_nodes, n_pods, split, env_extra=
     env.update(env_extra or {})
     worker = os.path.join(os.path.dirname(__file__), "shard_worker.py")
     procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), str(port), str(tmp_path / ("r%d.npz" % r)),
-                               str(skew), str(n_nodes), str(n_pods), str(split)], env=env) for r in range(world)]
+                               str(skew), str(n_nodes), str(n_pods), str(split), workload], env=env)
+             for r in range(world)]
     try:
         rcs = [pr.wait(timeout=wait) for pr in procs]
     finally:
@@ -552,11 +553,15 @@ def _sharded_processes(tmp_path, world, skew, n_nodes, n_pods, split, env_extra=
     return [np.load(tmp_path / ("r%d.npz" % r)) for r in range(world)]
 
 
-def _check_sharded(res, n_nodes, n_pods, threads=8):
+def _check_sharded(res, n_nodes, n_pods, threads=8, workload="c3"):
     import cpu_ref
     from ksim import synth
-    cl, p, q = synth.config_c3(n_nodes, n_pods, seed=9)
-    ref, _, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, n_pods, threads=threads)
+    if workload == "c3":
+        cl, p, q = synth.config_c3(n_nodes, n_pods, seed=9)
+        ref, _, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, n_pods, threads=threads)
+    else:
+        cl, p, q = synth.config_c2(n_nodes, n_pods, seed=9)
+        ref, _, ref_state, ref_ctr, _ = cpu_ref.run(cl, None, threads=threads, plan=scheduler.plan(cl, p, q))
     assert np.array_equal(scheduler.merge_sharded([r["out"] for r in res]), ref)
     assert sum(int(r["hi"]) - int(r["lo"]) for r in res) == n_nodes
     for r in res:
@@ -581,6 +586,33 @@ def test_node_sharded_multi_process(tmp_path, world, skew):
         env["KSIM_MAX_GRID"] = str(256 // world // 2)
     res = _sharded_processes(tmp_path, world, skew, 40_000, 2500, 1200, env)
     _check_sharded(res, 40_000, 2500)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_node_sharded_c2_multi_process(tmp_path, world):
+    """Node-sharded scheduling of C2-shaped pods (node selectors, required node affinity, taints,
+    TaintToleration / NodeAffinity reduce classes) — SURVEY.md §8e Phase A in the launch form:
+    each rank's last block exchanges its fit count and per-class (max, count) with every rank, all
+    decide on the world's NormalizeReduce maxima and selectHost index, and the rank holding the
+    node commits it.  `world` processes on this box's devices; placements, counters and every
+    shard's node state equal the C oracle's unsharded run (two calls: tags run across calls)."""
+    res = _sharded_processes(tmp_path, world, 0.0, 6000, 800, 300, workload="c2")
+    _check_sharded(res, 6000, 800, workload="c2")
+
+
+def test_node_sharded_c2_in_process_matches_c_oracle():
+    """Two ranks of the C2 shape driven from threads of one process (one stream each)."""
+    import cpu_ref
+    from ksim import synth
+    cl, p, q = synth.config_c2(3000, 400, seed=11)
+    scheds, merged = _run_sharded_threads(cl, p, q, 2, [(0, 150), (150, 250)])
+    ref, _, ref_state, ref_ctr, _ = cpu_ref.run(cl, None, threads=8, plan=scheduler.plan(cl, p, q))
+    assert np.array_equal(merged, ref)
+    for s in scheds:
+        assert s.last_node_index == ref_ctr
+        st = s.node_state()
+        for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+            assert np.array_equal(st[k], ref_state[k][s.lo:s.hi]), k
 
 
 @pytest.mark.timeout(600)
