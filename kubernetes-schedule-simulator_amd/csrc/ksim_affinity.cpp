@@ -141,7 +141,6 @@ int validate(ksim_handle* h, const ksim_affinity_tables* t) {
 extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t) {
   if (!h || !t) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_affinity: null argument");
   if (!h->have_nodes) return ksim_fail(h, KSIM_E_STATE, "ksim_load_affinity: load the node table first");
-  if (h->shard.world > 1) return ksim_fail(h, KSIM_E_UNSUPPORTED, "ksim_load_affinity: not available on a node-sharded handle");
   HIPCHK(h, hipSetDevice(h->device));
   int rc = validate(h, t);
   if (rc) return rc;

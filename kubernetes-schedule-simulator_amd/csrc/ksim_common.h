@@ -92,6 +92,10 @@ struct KsimAff {
 #define KSIM_LX_SLOTS 4
 #define KSIM_LX_REC (1 + 2 * KSIM_MAX_RCLASS)
 #define KSIM_LX_BIAS (1ll << 39)
+// ... and pass A's (after the launch region): min / max raw InterPodAffinity sum, max spread count,
+// haveZones, then the zone sums (<= KSIM_PX_ZONES zones), same word format
+#define KSIM_PX_ZONES 24
+#define KSIM_PX_REC (4 + KSIM_PX_ZONES)
 #define KSIM_AFF_PART 8    // pass-A block-partial words
 
 // Volume tables on the device (ksim_load_volumes; layout in include/ksim.h).

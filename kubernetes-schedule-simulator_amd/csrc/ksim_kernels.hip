@@ -164,7 +164,8 @@ __device__ __forceinline__ void eval_one(const KsimCtx& c, const ksim_pod& P, in
 #define KSIM_PASS_ZONES 512
 #define KSIM_PASS_V 7   // pass-A words combined per wave (s_v rows)
 template <int NPT>
-__device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t sp, int32_t ap, const bool (&fit)[NPT],
+__device__ __forceinline__ bool passa_reduce(const KsimCtx& c, int64_t pod, bool ipa, int32_t sp, int32_t ap,
+                                             const bool (&fit)[NPT],
                                              const int64_t (&raw)[NPT], const int64_t (&cnt)[NPT],
                                              const int32_t (&zz)[NPT], const int64_t (&acnt)[NPT],
                                              const int32_t (&azz)[NPT], int64_t (*s_v)[KSIM_WAVES],
@@ -278,9 +279,76 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, bool ipa, int32_t
   __syncthreads();
   combine();
   __syncthreads();
-  const int64_t r0 = mn, r1 = mx, r2 = smx, r3 = hz, r5 = amx, r6 = atot, r7 = ahz;  // valid in thread 0
+  int64_t r0 = mn, r1 = mx, r2 = smx, r3 = hz;  // valid in thread 0
+  const int64_t r5 = amx, r6 = atot, r7 = ahz;
   // zone sums: publish for the scan, zero for the next pod, maximum (countsByZone, :139-143)
   int64_t zmx = 0, azm = 0;
+  if (c.sh_world > 1) {
+    // node-sharded (SURVEY.md §8e Phase A): this rank's pass-A words to every rank, the world's
+    // min / max / max / haveZones and zone sums back (the aux priority is refused when sharded)
+    const int nz = sp >= 0 ? A.n_zone : 0;  // <= KSIM_PX_ZONES (host-checked)
+    const int W = 4 + nz, me = c.sh_rank;
+    if (tid == 0) { s_v[0][0] = r0; s_v[1][0] = r1; s_v[2][0] = r2; s_v[3][0] = r3; }
+    __syncthreads();
+    int64_t* px = reinterpret_cast<int64_t*>(s_z);  // [KSIM_MAX_RANKS][KSIM_PX_REC] (the zone scratch is free now)
+    if (wv == 0) {
+      const uint64_t tag = (uint64_t)(1u + (uint32_t)((c.sh_tag0 + (uint64_t)(pod - c.first)) % 0xFFFFFFull)) << 40;
+      const uint64_t vmask = (1ull << 40) - 1;
+      const int slot = (int)(pod % KSIM_LX_SLOTS);
+      uint64_t* const base0 = c.sh_peers[me] + (int64_t)KSIM_LX_SLOTS * KSIM_MAX_RANKS * KSIM_LX_REC;
+      if (lane < W) {
+        const int64_t v = lane < 4 ? s_v[lane][0]
+                                   : (int64_t)__hip_atomic_load(&A.zsum[lane - 4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        px[me * KSIM_PX_REC + lane] = v;
+        for (int r = 0; r < c.sh_world; ++r)
+          lx_store(c.sh_peers[r] + (int64_t)KSIM_LX_SLOTS * KSIM_MAX_RANKS * KSIM_LX_REC +
+                       ((int64_t)slot * KSIM_MAX_RANKS + me) * KSIM_PX_REC + lane,
+                   tag | ((uint64_t)(v + KSIM_LX_BIAS) & vmask));
+      }
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      const uint64_t lim = pod == c.first ? c.sh_start_ticks : 200000000ull;  // 2 s at 100 MHz
+      for (;;) {
+        bool ready = true;
+        for (int x = lane; x < c.sh_world * W; x += 64) {
+          const int r = x / W, j = x % W;
+          if (r == me) continue;
+          const uint64_t v = lx_load(base0 + ((int64_t)slot * KSIM_MAX_RANKS + r) * KSIM_PX_REC + j);
+          if ((v & ~vmask) != tag) { ready = false; continue; }
+          px[r * KSIM_PX_REC + j] = (int64_t)(v & vmask) - KSIM_LX_BIAS;
+        }
+        if (__all(ready)) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > lim) {
+          if (lane == 0) atomicOr(c.err, 4);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      // the world's: min, max, max, haveZones, then the zone sums and their maximum
+      int64_t g = 0;
+      if (lane < W) {
+        g = px[lane];
+        for (int r = 1; r < c.sh_world; ++r) {
+          const int64_t v = px[r * KSIM_PX_REC + lane];
+          g = lane == 0 ? (v < g ? v : g) : (lane < 4 ? (v > g ? v : g) : g + v);
+        }
+        if (lane >= 4) {
+          A.zread[lane - 4] = g;
+          A.zsum[lane - 4] = 0;
+        }
+      }
+      const int64_t zm = wave_max_i64(lane >= 4 && lane < W ? g : 0);
+      r0 = __shfl(g, 0, 64); r1 = __shfl(g, 1, 64); r2 = __shfl(g, 2, 64); r3 = __shfl(g, 3, 64);
+      if (lane == 0) {
+        A.mm[0] = r0 < 0 ? r0 : 0;  // (the accumulators start at 0: every rank's are <= 0 / >= 0 already)
+        A.mm[1] = r1;
+        A.mm[2] = r2;
+        A.mm[3] = r3;
+        A.mm[4] = zm;
+        *A.ticket = 0;
+      }
+    }
+    return true;
+  }
   if (sp >= 0)
     for (int z = tid; z < A.n_zone; z += KSIM_BLOCK) {
       const int64_t v = __hip_atomic_load(&A.zsum[z], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -330,6 +398,14 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
   __shared__ int s_last;
   const int64_t pod = c.one ? c.first : *c.cursor;
   if (pod >= c.end || !c.aff || c.no_prio) return;
+  // node-sharded: a peer that never answered (err bit 4) ends the run for every later launch
+  // (one read broadcast through LDS: the exit is uniform across the block's waves)
+  if (c.sh_world > 1) {
+    __shared__ int s_stop;
+    if (threadIdx.x == 0) s_stop = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4;
+    __syncthreads();
+    if (s_stop) return;
+  }
   ksim_pod P;  // (a branch, not a pointer select: the pod stays in registers)
   if (c.one) P = c.one_pod;
   else P = c.pods[pod];
@@ -360,7 +436,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_ipa_pass_kernel(KsimCtx c) {
       azz[k] = ksim_dom(A, A.aux_key, i);
     }
   }
-  (void)passa_reduce<NPT>(c, ipa, sp, ap, fit, raw, cnt, zz, acnt, azz, s_v, s_z, &s_last);
+  (void)passa_reduce<NPT>(c, pod, ipa, sp, ap, fit, raw, cnt, zz, acnt, azz, s_v, s_z, &s_last);
 }
 
 // diagnostic builds (make stamps): thread 0's cycles per scan phase, summed over blocks into
@@ -442,7 +518,12 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   const int64_t pod = c.one ? c.first : *c.cursor;
   if (pod >= c.end) return;  // uniform: graph replay past the end of the queue
   // node-sharded: a peer that never answered (err bit 4) ends the run for every later launch
-  if (c.sh_world > 1 && (__hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4)) return;
+  // (one read broadcast through LDS: the exit is uniform across the block's waves)
+  if (c.sh_world > 1) {
+    if (tid == 0) s_bail = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & 4;
+    __syncthreads();
+    if (s_bail) return;
+  }
   ksim_pod P;  // (a branch, not a pointer select: the pod stays in registers)
   if (c.one) P = c.one_pod;
   else P = c.pods[pod];
@@ -512,7 +593,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
         azz[k] = ksim_dom(A, A.aux_key, i);
       }
     }
-    if (passa_reduce<NPT>(c, ipa.on, ipa.sp, ipa.ap, fit, raw, cnt, zz, acnt, azz, s_v, s_z, &s_last)) {
+    if (passa_reduce<NPT>(c, pod, ipa.on, ipa.sp, ipa.ap, fit, raw, cnt, zz, acnt, azz, s_v, s_z, &s_last)) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's zread stores
       __syncthreads();
       if (tid == 0) {

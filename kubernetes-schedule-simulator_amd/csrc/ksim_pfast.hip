@@ -937,7 +937,8 @@ extern "C" size_t ksim_pfast_granule_bytes(void) { return (size_t)NREP * REP_STR
 // the fast kernel's aggregate slots, then the launch form's (KSIM_LX_*) at ksim_shard_lx_offset()
 extern "C" size_t ksim_shard_lx_offset(void) { return (size_t)ANSLOT * KSIM_MAX_RANKS * 4; }  // in words
 extern "C" size_t ksim_shard_xchg_bytes(void) {
-  return (ksim_shard_lx_offset() + (size_t)KSIM_LX_SLOTS * KSIM_MAX_RANKS * KSIM_LX_REC) * sizeof(uint64_t);
+  return (ksim_shard_lx_offset() + (size_t)KSIM_LX_SLOTS * KSIM_MAX_RANKS * (KSIM_LX_REC + KSIM_PX_REC)) *
+         sizeof(uint64_t);
 }
 
 // float64 image of the node table for the streaming form: one pass over the int64 columns

@@ -534,7 +534,9 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
                   !c.no_prio ? 1 : 0;
   // pass A fused into the scan behind a grid barrier when the grid is co-resident (KSIM_FUSE_A=0: two launches)
   const char* fz = getenv("KSIM_FUSE_A");
-  c.fuse_a = ipa && !h->fuse_off && !(fz && fz[0] == '0') && ksim_scan_coresident(npt, c.collect, grid) ? 1 : 0;
+  // (never node-sharded: pass A's last block waits for the peers, longer than the grid barrier's bound)
+  c.fuse_a = ipa && !h->fuse_off && c.sh_world <= 1 && !(fz && fz[0] == '0') && ksim_scan_coresident(npt, c.collect, grid)
+                 ? 1 : 0;
   const int gkey = ipa | c.fuse_a << 1;
   if (!h->gexec || h->g_batch != batch || h->g_npt != npt || h->g_collect != c.collect || h->g_first != first ||
       h->g_end != c.end || h->g_ipa != gkey) {
@@ -1193,6 +1195,9 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
       if (ksim_rt_range_wide(h, first, count))
         return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling of pods with more than %d reduce classes",
                          KSIM_MAX_RCLASS);
+      if (ksim_rt_launch_tables(h) || (h->have_aff && h->aff_h.n_zone > KSIM_PX_ZONES))
+        return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling with the auxiliary priority, the service-affinity "
+                                           "lender check or more than %d spread zones", KSIM_PX_ZONES);
       for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED})
         if (c.w[k] > ((int64_t)1 << 30))
           return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling: a map-priority weight above 2^30");

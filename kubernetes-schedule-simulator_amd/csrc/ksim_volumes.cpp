@@ -68,7 +68,6 @@ int validate(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
 static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
   if (!h || !t) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: null argument");
   if (!h->have_nodes || !h->have_classes) return ksim_fail(h, KSIM_E_STATE, "ksim_load_volumes: load nodes and classes first");
-  if (h->shard.world > 1) return ksim_fail(h, KSIM_E_UNSUPPORTED, "ksim_load_volumes: not available on a node-sharded handle");
   if (keep && (!h->have_vol || h->vol_stale))
     return ksim_fail(h, KSIM_E_STATE, "ksim_grow_volumes: no current volume tables (load them after a node event)");
   HIPCHK(h, hipSetDevice(h->device));

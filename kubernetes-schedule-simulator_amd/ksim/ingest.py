@@ -663,16 +663,79 @@ class Cluster:
         """The name-rank range [lo, hi) of the node table with the same pods and interned
         tables (node-sharded mode: rank r loads its contiguous shard, ksim_shard_setup)."""
         import copy
-        if self.affinity is not None:
-            raise Unsupported("node-sharded scheduling of pods with inter-pod affinity terms or spread selectors")
-        if self.volumes is not None:
-            raise Unsupported("node-sharded scheduling of pods with volumes")
         sub = copy.copy(self)
+        if self.affinity is not None:
+            sub.affinity = _shard_affinity(self.affinity, lo, hi)
+        if self.volumes is not None:
+            v = dict(self.volumes)
+            if v.get("slots") is not None:
+                v["slots"] = np.ascontiguousarray(v["slots"][:, lo:hi])
+                v["slot_count"] = np.ascontiguousarray(v["slot_count"][lo:hi])
+            v["n_nodes"] = hi - lo
+            sub.volumes = v
         sub.cols = {k: (np.ascontiguousarray(v[..., lo:hi]) if isinstance(v, np.ndarray) else v)
                     for k, v in self.cols.items()}
         sub.names = list(self.names[lo:hi]) if self.names else self.names
         sub.index = {}
         return sub
+
+
+def _shard_affinity(d, lo, hi):
+    """The affinity tables of node-sharded rank [lo, hi) (SURVEY.md §8e Phase A): every counted pair,
+    carried term and term key must be node-like (each domain holds at most one node: the node
+    pseudo key, a unique hostname label), so a commit changes counts on its own rank only: the
+    node pseudo key's domains become the shard's node indices (its count segments sliced), other
+    node-like keys keep their global domain ids and count arrays; the domain columns are sliced.  The zone key
+    only groups the spread reduce's counts (exchanged across ranks in pass A).  Other keys — a
+    domain several ranks share — are refused."""
+    dom = np.asarray(d["dom"])
+    K = dom.shape[0]
+    nodelike = np.zeros(K, bool)
+    for k in range(K):
+        row = dom[k][dom[k] >= 0]
+        nodelike[k] = len(np.unique(row)) == len(row)
+    used = set(int(x) for x in np.asarray(d["pair_key"])[:int(d["n_pair"])]) | \
+        set(int(x) for x in np.asarray(d["carry_key"])[:int(d["n_carry"])])
+    terms = np.asarray(d["terms"])[:int(d.get("n_terms", len(d["terms"])))]
+    for t in terms:
+        if int(t["kind"]) != abi.AFF_PREFERRED:
+            used.add(int(t["gate_key"]))
+    bad = sorted(k for k in used if not nodelike[k])
+    if bad:
+        raise Unsupported("node-sharded scheduling of inter-pod affinity / spread terms over topology domains several "
+                          "nodes share (keys %s)" % bad)
+    if d.get("aux_pair") is not None or d.get("svc_on"):
+        raise Unsupported("node-sharded scheduling with the auxiliary spreading priority or CheckServiceAffinity lenders")
+    if int(d["zone_key"]) >= 0 and int(np.asarray(d["n_dom"])[int(d["zone_key"])]) > abi.SHARD_MAX_ZONES:
+        raise Unsupported("node-sharded scheduling of spread pods over more than %d zones" % abi.SHARD_MAX_ZONES)
+    out = dict(d)
+    n = hi - lo
+    sdom = np.ascontiguousarray(dom[:, lo:hi])
+    # the node pseudo key (1) becomes the shard's own: node i's domain is i (the kernels read a
+    # node-key pair's count at the node's index), its pairs' / carried terms' segments sliced to
+    # [lo, hi); every other key keeps its global domain ids
+    sdom[1] = np.arange(n, dtype=sdom.dtype)
+    n_dom = np.asarray(d["n_dom"]).copy()
+    n_dom[1] = n
+
+    def reslice(keys, offs, arr, m):
+        new_off = np.zeros(m, np.int64)
+        parts, o = [], 0
+        for c in range(m):
+            k, a = int(keys[c]), int(offs[c])
+            seg = arr[a + lo:a + hi] if k == 1 else arr[a:a + int(np.asarray(d["n_dom"])[k])]
+            new_off[c] = o
+            parts.append(seg)
+            o += len(seg)
+        flat = np.concatenate(parts) if parts else arr[:0]
+        return new_off, np.ascontiguousarray(flat if len(flat) else np.zeros(1, arr.dtype))
+
+    P, E = int(d["n_pair"]), int(d["n_carry"])
+    out["pair_off"], out["cnt"] = reslice(np.asarray(d["pair_key"]), np.asarray(d["pair_off"]), np.asarray(d["cnt"]), P)
+    out["carry_off"], out["carried"] = reslice(np.asarray(d["carry_key"]), np.asarray(d["carry_off"]),
+                                               np.asarray(d["carried"]), E)
+    out["dom"], out["n_dom"], out["n_nodes"] = sdom, n_dom.astype(np.int32), n
+    return out
 
 
 @dataclass

@@ -24,7 +24,12 @@ def main():
     device = rank % max(1, torch.cuda.device_count())
     from ksim import scheduler, synth
     dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%s" % port, rank=rank, world_size=world)
-    cl, p, q = synth.config_c3(n_nodes, n_pods, seed=9) if workload == "c3" else synth.config_c2(n_nodes, n_pods, seed=9)
+    if workload == "c3":
+        cl, p, q = synth.config_c3(n_nodes, n_pods, seed=9)
+    elif workload == "c2":
+        cl, p, q = synth.config_c2(n_nodes, n_pods, seed=9)
+    else:
+        cl, p, q, _ = synth.config_c2x(n_nodes, n_pods, seed=9)
     s = scheduler.ShardedScheduler(cl, p, q, rank, world, device=device)
     s.connect_torch(dist)
     dist.barrier()

@@ -560,7 +560,8 @@ def _check_sharded(res, n_nodes, n_pods, threads=8, workload="c3"):
         cl, p, q = synth.config_c3(n_nodes, n_pods, seed=9)
         ref, _, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(p, q), 0, n_pods, threads=threads)
     else:
-        cl, p, q = synth.config_c2(n_nodes, n_pods, seed=9)
+        cl, p, q = synth.config_c2(n_nodes, n_pods, seed=9) if workload == "c2" else \
+            synth.config_c2x(n_nodes, n_pods, seed=9)[:3]
         ref, _, ref_state, ref_ctr, _ = cpu_ref.run(cl, None, threads=threads, plan=scheduler.plan(cl, p, q))
     assert np.array_equal(scheduler.merge_sharded([r["out"] for r in res]), ref)
     assert sum(int(r["hi"]) - int(r["lo"]) for r in res) == n_nodes
@@ -598,6 +599,26 @@ def test_node_sharded_c2_multi_process(tmp_path, world):
     shard's node state equal the C oracle's unsharded run (two calls: tags run across calls)."""
     res = _sharded_processes(tmp_path, world, 0.0, 6000, 800, 300, workload="c2")
     _check_sharded(res, 6000, 800, workload="c2")
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_node_sharded_c2x_multi_process(tmp_path, world):
+    """Node-sharded C2x (zones, volumes, SelectorSpread over services, required anti-affinity on
+    kubernetes.io/hostname): every counted pair and carried term is node-like, so each rank keeps
+    the global count arrays over its own nodes' domains and commits on its own rank only; pass A's
+    InterPodAffinity min / max, SelectorSpread max / haveZones and zone sums are exchanged across
+    the ranks before the scores.  Placements, counters and node state equal the C oracle's."""
+    res = _sharded_processes(tmp_path, world, 0.0, 4000, 600, 250, workload="c2x")
+    _check_sharded(res, 4000, 600, workload="c2x")
+
+
+def test_node_sharded_refuses_shared_domains():
+    """Terms over topology domains several nodes share (a zone-keyed preferred term) are refused."""
+    from workloads import rnd_affinity_workload
+    nodes, running, pods = rnd_affinity_workload(1, n_nodes=20, n_pods=40)
+    cl = ingest.Cluster.from_objects(nodes, running, pods)
+    with pytest.raises(abi.KsimUnsupported):
+        cl.shard(0, 10)
 
 
 def test_node_sharded_c2_in_process_matches_c_oracle():
