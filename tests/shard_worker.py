@@ -37,7 +37,11 @@ def main():
         time.sleep(skew)  # launch skew beyond the 2 s per-pod bound: the start handshake absorbs it
     o1, _, _ = s.schedule(0, split)
     dist.barrier()
+    t2 = time.perf_counter()
     o2, _, _ = s.schedule(split, n_pods - split)
+    t3 = time.perf_counter()
+    print("rank %d %s: %.1f pods/s in the second call (%d pods, %.1f ms)" % (rank, workload, (n_pods - split) / (t3 - t2),
+                                                                      n_pods - split, 1e3 * (t3 - t2)), flush=True)
     st = s.node_state()
     np.savez(out, out=np.concatenate([o1, o2]), ctr=np.uint64(s.last_node_index), lo=s.lo, hi=s.hi,
              **{k: st[k] for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count")})
