@@ -276,6 +276,41 @@ typedef struct {
  * ksim_k8s_open_ex with {w_pa, 0}: a policy without ImageLocalityPriority. */
 int ksim_k8s_open_ex(ksim_k8s_cluster* c, const ksim_config* cfg, const ksim_k8s_weights* w, ksim_handle** out);
 
+/* A Policy's keys with arguments (factory/plugins.go RegisterCustomFitPredicate /
+ * RegisterCustomPriorityFunction over api.PredicateArgument / PriorityArgument):
+ *  - CheckNodeLabelPresence (KSIM_P_LABEL_PRESENCE; predicates.go:875-910): every listed label present
+ *    (presence = 1) or absent (0) on the node;
+ *  - CheckServiceAffinity (KSIM_P_SERVICE_AFFINITY; predicates.go:940-1016) with the ServiceLister
+ *    selecting none of the pods: the node must carry the pod's nodeSelector values of the labels;
+ *  - labelPreference priorities (node_label.go:42-58): MaxPriority x weight when the label's
+ *    presence on the node equals `presence`; a serviceAntiAffinity priority with no service selecting
+ *    the pods (selector_spreading.go:221-275) is {label, presence = 1, weight}.
+ * services_select_pods: the adapter's ServiceLister selects some pod — CheckServiceAffinity and
+ * serviceAntiAffinity then need the service-aware tables the Python host builds (KSIM_E_UNSUPPORTED). */
+typedef struct {
+  const char* label;
+  int32_t presence;
+  int32_t pad;
+  int64_t weight;
+} ksim_k8s_label_priority;
+
+typedef struct {
+  int32_t n_presence_labels;
+  int32_t presence;
+  const char* const* presence_labels;
+  int32_t n_affinity_labels;
+  int32_t services_select_pods;
+  const char* const* affinity_labels;
+  int32_t n_label_priorities;
+  int32_t has_service_anti_affinity;    /* some label priority stands for a serviceAntiAffinity one */
+  const ksim_k8s_label_priority* label_priorities;
+} ksim_k8s_policy_args;
+
+/* ksim_k8s_open_ex with a Policy's arguments (NULL: none — CheckNodeLabelPresence /
+ * CheckServiceAffinity in cfg->predicates are then refused as before). */
+int ksim_k8s_open_policy(ksim_k8s_cluster* c, const ksim_config* cfg, const ksim_k8s_weights* w,
+                         const ksim_k8s_policy_args* args, ksim_handle** out);
+
 /* Name-rank order and sizes of the built snapshot. */
 int64_t ksim_k8s_node_count(const ksim_k8s_cluster* c);
 const char* ksim_k8s_node_name(const ksim_k8s_cluster* c, int64_t rank);

@@ -32,6 +32,7 @@ struct ksim_k8s_cluster {
   std::vector<uint64_t> pod_ports;
   std::vector<ksim_scalar_req> pod_scalars;
   // affinity
+  PolicyArgs pol;  // the open handle's Policy arguments (ksim_k8s_open_policy)
   bool with_affinity = false, spread_active = false;
   AffinityIndex aidx;
   AffTables aff;
@@ -60,6 +61,7 @@ struct ksim_k8s_cluster {
   bool dropin = false;        // the affinity tables keep every identity (ksim_k8s_describe)
   ksim_k8s_weights w{};       // the open handle's NodePreferAvoidPods / ImageLocality weights
   bool pa_use_w = false, opened_aff = false, opened_vol = false, opened_zone = false;
+  bool opened_svc = false;  // CheckServiceAffinity configured with its Policy arguments
   bool aff_cfg = false, vol_cfg = false;  // the open handle's configuration reads the tables
   int32_t vol_grown_classes = 0;          // volume classes whose zone verdicts the handle holds
   ZoneGroups zone_groups;                 // label sets by zone / region labels (reset with the interns)
@@ -346,6 +348,11 @@ extern "C" int ksim_k8s_build(ksim_k8s_cluster* c) {
 }
 
 extern "C" int ksim_k8s_open_ex(ksim_k8s_cluster* c, const ksim_config* cfg_in, const ksim_k8s_weights* w_in, ksim_handle** out) {
+  return ksim_k8s_open_policy(c, cfg_in, w_in, nullptr, out);
+}
+
+extern "C" int ksim_k8s_open_policy(ksim_k8s_cluster* c, const ksim_config* cfg_in, const ksim_k8s_weights* w_in,
+                                    const ksim_k8s_policy_args* args, ksim_handle** out) {
   if (!c || !cfg_in || !out) return KSIM_E_INVAL;
   *out = nullptr;
   ksim_handle* h = nullptr;
@@ -354,8 +361,24 @@ extern "C" int ksim_k8s_open_ex(ksim_k8s_cluster* c, const ksim_config* cfg_in, 
     if (!c->built) fail(KSIM_E_STATE, "ksim_k8s_open: build the snapshot first");
     ksim_config cfg = *cfg_in;
     const uint32_t pr = cfg.predicates;
-    if (pr & (KSIM_P_LABEL_PRESENCE | KSIM_P_SERVICE_AFFINITY))
-      fail(KSIM_E_UNSUPPORTED, "CheckNodeLabelPresence / CheckServiceAffinity need their Policy arguments (the Python host)");
+    PolicyArgs pol;
+    if (args) {
+      pol.on = true;
+      for (int32_t i = 0; i < args->n_presence_labels; ++i) pol.presence_labels.push_back(S(args->presence_labels[i]));
+      pol.presence = args->presence != 0;
+      for (int32_t i = 0; i < args->n_affinity_labels; ++i) pol.affinity_labels.push_back(S(args->affinity_labels[i]));
+      for (int32_t i = 0; i < args->n_label_priorities; ++i) {
+        const ksim_k8s_label_priority& q = args->label_priorities[i];
+        if (q.weight <= 0) fail(KSIM_E_INVAL, "label priority %s: weight must be positive", S(q.label).c_str());
+        pol.label_prios.push_back({S(q.label), {q.presence != 0, q.weight}});
+      }
+      if (args->services_select_pods && ((pr & KSIM_P_SERVICE_AFFINITY) || args->has_service_anti_affinity))
+        fail(KSIM_E_UNSUPPORTED, "CheckServiceAffinity / serviceAntiAffinity with services selecting the pods (the Python "
+                                 "host builds their service-aware tables)");
+    } else if (pr & (KSIM_P_LABEL_PRESENCE | KSIM_P_SERVICE_AFFINITY)) {
+      fail(KSIM_E_UNSUPPORTED, "CheckNodeLabelPresence / CheckServiceAffinity need their Policy arguments (ksim_k8s_open_policy)");
+    }
+    c->pol = pol;
     if (cfg.weights[KSIM_W_NODE_AFFINITY] && !c->ct.bad_classes.empty())
       fail(KSIM_E_UNSUPPORTED, "NodeAffinityPriority: a preferred node-affinity term does not parse");
     if (w.image_locality && c->node_images && !c->in.images)
@@ -376,7 +399,8 @@ extern "C" int ksim_k8s_open_ex(ksim_k8s_cluster* c, const ksim_config* cfg_in, 
     std::vector<int64_t> nav, add;
     const bool use_w = cfg.weights[KSIM_W_NODE_AFFINITY] != 0;
     bool pa_on = false;
-    class_addends(c->ct, w.prefer_avoid, w.image_locality, use_w, &nac, &nna, &nav, &add, &pa_on);
+    const std::vector<int64_t> lab_add = policy_label_add(c->in, pol);
+    class_addends(c->ct, w.prefer_avoid, w.image_locality, use_w, &nac, &nna, &nav, &add, &pa_on, &lab_add);
     if (pa_on) cfg.const_score -= 10 * w.prefer_avoid;
     const bool aff = c->with_affinity &&
                      ((pr & KSIM_P_INTERPOD_AFFINITY) ||
@@ -397,13 +421,26 @@ extern "C" int ksim_k8s_open_ex(ksim_k8s_cluster* c, const ksim_config* cfg_in, 
     t.req_eph = c->col_i64[7].data(); t.nz_cpu = c->col_i64[8].data(); t.nz_mem = c->col_i64[9].data();
     t.pod_count = c->pod_count.data(); t.req_scalar = c->req_scalar.data(); t.ports = c->ports.data();
     t.port_count = c->port_count.data();
+    std::vector<uint32_t> flags = c->flags;  // + CheckNodeLabelPresence's verdicts
+    if ((pr & KSIM_P_LABEL_PRESENCE) && pol.on) {
+      const std::vector<uint8_t> bad = policy_presence_bad(c->in, pol);
+      for (int64_t i = 0; i < n; ++i)
+        if (bad[c->label_set[i]]) flags[i] |= KSIM_N_LABEL_PRESENCE;
+      t.flags = flags.data();
+    }
     if ((e = ksim_load_nodes(h, &t))) fail(e, "ksim_load_nodes: %s", ksim_last_error(h));
-    if ((e = load_class_tab(c->ct, h, w.prefer_avoid, w.image_locality, use_w))) fail(e, "ksim_load_classes: %s", ksim_last_error(h));
+    std::vector<uint32_t> svc_ok;
+    std::vector<uint8_t> svc_need;
+    const bool svc = (pr & KSIM_P_SERVICE_AFFINITY) && pol.on;
+    if (svc) policy_svc_ok(c->in, c->ct, pol, &svc_ok, &svc_need);
+    if ((e = load_class_tab(c->ct, h, w.prefer_avoid, w.image_locality, use_w, svc ? svc_ok.data() : nullptr, &lab_add)))
+      fail(e, "ksim_load_classes: %s", ksim_last_error(h));
     if (aff && (e = load_aff_tab(c->aff, n, c->opt.hard_weight, h))) fail(e, "ksim_load_affinity: %s", ksim_last_error(h));
     if (vol && (e = load_volumes(c, h, (pr & KSIM_P_VOLUME_ZONE) != 0))) fail(e, "ksim_load_volumes: %s", ksim_last_error(h));
     c->w = w;
     c->pa_use_w = use_w;
     c->opened_aff = aff;
+    c->opened_svc = svc;
     c->opened_vol = vol;
     c->opened_zone = (pr & KSIM_P_VOLUME_ZONE) != 0;
     c->aff_cfg = (pr & KSIM_P_INTERPOD_AFFINITY) ||
@@ -413,6 +450,7 @@ extern "C" int ksim_k8s_open_ex(ksim_k8s_cluster* c, const ksim_config* cfg_in, 
     for (ksim_pod& p : pods) {
       if (!aff) p.aff_ident = p.aff_class = 0;
       if (!vol) p.vol_class = 0;
+      if (svc && svc_need[p.cls]) p.flags |= KSIM_POD_NEED_SVC_AFFINITY;
     }
     if ((e = ksim_load_pods(h, pods.data(), (int64_t)pods.size(), c->pod_ports.data(), (int64_t)c->pod_ports.size(),
                             c->pod_scalars.data(), (int64_t)c->pod_scalars.size())))
@@ -500,12 +538,20 @@ extern "C" int ksim_k8s_describe(ksim_k8s_cluster* c, ksim_handle* h, const ksim
     if (n_ports) *n_ports = np;
     if (n_scalars) *n_scalars = nsc;
     int e;
+    std::vector<uint32_t> svc_ok;
+    std::vector<uint8_t> svc_need;
+    const bool svc = c->pol.on && c->opened_svc;
+    if (svc) policy_svc_ok(c->in, c->ct, c->pol, &svc_ok, &svc_need);
     if (c->in.classes.items.size() != c0) {  // a new pod class: the class tables grow (a superset)
       build_class_tab(c->in, &c->ct);
-      if ((e = load_class_tab(c->ct, h, c->w.prefer_avoid, c->w.image_locality, c->pa_use_w)))
+      const std::vector<int64_t> lab_add = policy_label_add(c->in, c->pol);
+      if (svc) policy_svc_ok(c->in, c->ct, c->pol, &svc_ok, &svc_need);
+      if ((e = load_class_tab(c->ct, h, c->w.prefer_avoid, c->w.image_locality, c->pa_use_w, svc ? svc_ok.data() : nullptr,
+                              &lab_add)))
         fail(e, "ksim_load_classes: %s", ksim_last_error(h));
     }
     row.flags |= c->ct.need[row.cls];
+    if (svc && row.cls < (int32_t)svc_need.size() && svc_need[row.cls]) row.flags |= KSIM_POD_NEED_SVC_AFFINITY;
     ksim_k8s_cluster::Described d;
     // inter-pod affinity / SelectorSpread: identities keep their ids from here on (keep_all)
     const bool takes_part = has_pod_affinity(p) || !p.spread.empty() || c->with_affinity;

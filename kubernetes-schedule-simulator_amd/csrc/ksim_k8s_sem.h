@@ -1208,15 +1208,74 @@ void build_class_tab(const Interns& in, ClassTab* c) {
   }
 }
 
+// A Policy's arguments over the interned label sets and classes (scheduler.plan's
+// label_presence_flags, service_affinity_table and label_set_priority, restated).
+struct PolicyArgs {
+  bool on = false;
+  std::vector<Str> presence_labels;
+  bool presence = true;
+  std::vector<Str> affinity_labels;
+  std::vector<std::pair<Str, std::pair<bool, int64_t>>> label_prios;  // label -> (presence, weight)
+};
+
+// CheckNodeLabelPresence (predicates.go:875-910): per label set, whether it fails.
+std::vector<uint8_t> policy_presence_bad(const Interns& in, const PolicyArgs& a) {
+  std::vector<uint8_t> bad(in.label_sets.items.size(), 0);
+  for (size_t li = 0; li < bad.size(); ++li)
+    for (const Str& l : a.presence_labels)
+      if ((in.label_sets.items[li].labels.count(l) != 0) != a.presence) { bad[li] = 1; break; }
+  return bad;
+}
+
+// labelPreference (node_label.go:42-58): per label set, the weighted MaxPriority sum.
+std::vector<int64_t> policy_label_add(const Interns& in, const PolicyArgs& a) {
+  std::vector<int64_t> add(in.label_sets.items.size(), 0);
+  for (size_t li = 0; li < add.size(); ++li)
+    for (const auto& pr : a.label_prios)
+      if ((in.label_sets.items[li].labels.count(pr.first) != 0) == pr.second.first) add[li] += 10 * pr.second.second;
+  return add;
+}
+
+// CheckServiceAffinity with no service selecting the pod (predicates.go:980-1016): per (class, label
+// set) the class's nodeSelector values of the listed labels must be the node's (FindLabelsInSet,
+// CreateSelectorFromLabels); need[class] when it fails somewhere.
+void policy_svc_ok(const Interns& in, const ClassTab& ct, const PolicyArgs& a, std::vector<uint32_t>* ok,
+                   std::vector<uint8_t>* need) {
+  const int32_t Cn = ct.Cn, L = ct.L, lw = std::max<int32_t>((L + 31) / 32, 1);
+  ok->assign((size_t)Cn * lw, 0);
+  need->assign(Cn, 0);
+  for (int32_t k = 0; k < Cn; ++k) {
+    std::vector<std::pair<Str, Str>> al;
+    if (k < (int32_t)in.classes.items.size())
+      for (const auto& kv : in.classes.items[k].ns)
+        if (std::find(a.affinity_labels.begin(), a.affinity_labels.end(), kv.first) != a.affinity_labels.end())
+          al.push_back(kv);
+    for (int32_t li = 0; li < L; ++li) {
+      const Labels& lab = in.label_sets.items[li].labels;
+      bool m = true;
+      for (const auto& kv : al) {
+        auto it = lab.find(kv.first);
+        if (it == lab.end() || it->second != kv.second) { m = false; break; }
+      }
+      if (m) (*ok)[(size_t)k * lw + (li >> 5)] |= 1u << (li & 31);
+      else (*need)[k] = 1;
+    }
+  }
+}
+
 // scheduler.class_tables_for: NodePreferAvoidPods' and ImageLocality's weighted map scores as
 // per-class addends when the policy weighs them and they tell some class's nodes apart — the
 // NodeAffinity class dimension re-keyed by (preferred weight, summed addend).  Returns whether the
 // addends apply; *pa_on: NodePreferAvoidPods rides them (its constant leaves const_score).
 bool class_addends(const ClassTab& c, int64_t w_pa, int64_t w_im, bool use_w, std::vector<uint8_t>* nac,
-                   std::vector<int32_t>* nna, std::vector<int64_t>* nav, std::vector<int64_t>* add, bool* pa_on_out) {
+                   std::vector<int32_t>* nna, std::vector<int64_t>* nav, std::vector<int64_t>* add, bool* pa_on_out,
+                   const std::vector<int64_t>* lab_add = nullptr) {
   const bool pa_on = w_pa && c.pa_split, im_on = w_im && c.im_any;
+  bool lab_on = false;  // a Policy's label priorities (per label set, weighted)
+  if (lab_add)
+    for (int64_t v : *lab_add) lab_on |= v != 0;
   if (pa_on_out) *pa_on_out = pa_on;
-  if (!pa_on && !im_on) return false;
+  if (!pa_on && !im_on && !lab_on) return false;
   const int32_t Cn = c.Cn, L = c.L;
   nac->assign((size_t)Cn * L, 0);
   nna->assign(Cn, 1);
@@ -1226,7 +1285,8 @@ bool class_addends(const ClassTab& c, int64_t w_pa, int64_t w_im, bool use_w, st
     std::vector<std::pair<int64_t, int64_t>> keys;
     for (int32_t li = 0; li < L; ++li) {
       const size_t x = (size_t)k * L + li;
-      keys.push_back({use_w ? c.na_w[x] : 0, (pa_on ? c.na_p[x] * w_pa : 0) + (im_on ? c.im_s[x] * w_im : 0)});
+      keys.push_back({use_w ? c.na_w[x] : 0, (pa_on ? c.na_p[x] * w_pa : 0) + (im_on ? c.im_s[x] * w_im : 0) +
+                                                 (lab_on ? (*lab_add)[li] : 0)});
     }
     std::vector<std::pair<int64_t, int64_t>> av(keys);
     std::sort(av.begin(), av.end());
@@ -1246,11 +1306,12 @@ bool class_addends(const ClassTab& c, int64_t w_pa, int64_t w_im, bool use_w, st
 }
 
 // ksim_load_classes over a ClassTab (with the addends of class_addends when they apply).
-int load_class_tab(const ClassTab& c, ksim_handle* h, int64_t w_pa, int64_t w_im, bool use_w, const uint32_t* svc_ok = nullptr) {
+int load_class_tab(const ClassTab& c, ksim_handle* h, int64_t w_pa, int64_t w_im, bool use_w, const uint32_t* svc_ok = nullptr,
+                   const std::vector<int64_t>* lab_add = nullptr) {
   std::vector<uint8_t> nac;
   std::vector<int32_t> nna;
   std::vector<int64_t> nav, add;
-  const bool pa = class_addends(c, w_pa, w_im, use_w, &nac, &nna, &nav, &add, nullptr);
+  const bool pa = class_addends(c, w_pa, w_im, use_w, &nac, &nna, &nav, &add, nullptr, lab_add);
   ksim_class_tables t{};
   t.n_classes = c.Cn;
   t.n_label_sets = c.L;

@@ -131,6 +131,19 @@ class Weights(C.Structure):
     _fields_ = [("prefer_avoid", C.c_int64), ("image_locality", C.c_int64)]
 
 
+class LabelPriority(C.Structure):
+    _fields_ = [("label", C.c_char_p), ("presence", C.c_int32), ("pad", C.c_int32), ("weight", C.c_int64)]
+
+
+class PolicyArgs(C.Structure):
+    """ksim_k8s_policy_args: a Policy's CheckNodeLabelPresence / CheckServiceAffinity arguments and
+    labelPreference / serviceAntiAffinity (no selecting service) priorities."""
+    _fields_ = [("n_presence_labels", C.c_int32), ("presence", C.c_int32), ("presence_labels", C.POINTER(C.c_char_p)),
+                ("n_affinity_labels", C.c_int32), ("services_select_pods", C.c_int32),
+                ("affinity_labels", C.POINTER(C.c_char_p)), ("n_label_priorities", C.c_int32),
+                ("has_service_anti_affinity", C.c_int32), ("label_priorities", C.POINTER(LabelPriority))]
+
+
 class CacheOptions(C.Structure):
     _fields_ = [("cfg", abi.Config), ("extra", Weights), ("hard_weight", C.c_int32), ("max_vols", C.c_int32 * 3),
                 ("port_slots", C.c_int32), ("check_volume_binding", C.c_int32)]
@@ -341,6 +354,7 @@ def lib():
                                       C.c_void_p, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int64)],
                 "ksim_k8s_bind": [P, C.c_int64, C.c_int64],
                 "ksim_k8s_open_ex": [P, C.POINTER(abi.Config), C.POINTER(Weights), C.POINTER(P)],
+                "ksim_k8s_open_policy": [P, C.POINTER(abi.Config), C.POINTER(Weights), C.POINTER(PolicyArgs), C.POINTER(P)],
                 "ksim_k8s_cache_create": [C.POINTER(CacheOptions), C.POINTER(P)], "ksim_k8s_cache_destroy": [P],
                 "ksim_k8s_cache_last_error": [P], "ksim_k8s_cache_add_pv": [P, C.POINTER(PV)],
                 "ksim_k8s_cache_add_pvc": [P, C.POINTER(PVC)],
@@ -461,6 +475,36 @@ class K8sCluster:
         hh = C.c_void_p()
         w = Weights(int(prefer_avoid_weight), int(image_locality_weight))
         self._check(lib().ksim_k8s_open_ex(self.h, C.byref(cfg), C.byref(w), C.byref(hh)))
+        return abi.Handle.adopt(hh, cfg)
+
+    def open_policy(self, cfg, prefer_avoid_weight=0, image_locality_weight=0, label_presence=None,
+                    service_affinity=None, label_priorities=(), services_select_pods=False):
+        """ksim_k8s_open_policy: label_presence = (labels, presence) of CheckNodeLabelPresence,
+        service_affinity = CheckServiceAffinity's labels, label_priorities = [(label, presence, weight,
+        is_service_anti_affinity)] — a Policy's arguments (policy.key_sets / priority_arguments)."""
+        hh = C.c_void_p()
+        w = Weights(int(prefer_avoid_weight), int(image_locality_weight))
+        keep = []
+
+        def strs(xs):
+            arr = (C.c_char_p * max(len(xs), 1))(*[x.encode() for x in xs])
+            keep.append(arr)
+            return arr
+        a = PolicyArgs()
+        if label_presence is not None:
+            a.n_presence_labels, a.presence = len(label_presence[0]), int(bool(label_presence[1]))
+            a.presence_labels = C.cast(strs(list(label_presence[0])), C.POINTER(C.c_char_p))
+        if service_affinity is not None:
+            a.n_affinity_labels = len(service_affinity)
+            a.affinity_labels = C.cast(strs(list(service_affinity)), C.POINTER(C.c_char_p))
+        a.services_select_pods = int(bool(services_select_pods))
+        lp = (LabelPriority * max(len(label_priorities), 1))(*[LabelPriority(l.encode(), int(bool(pr)), 0, int(wt))
+                                                               for l, pr, wt, _ in label_priorities])
+        keep.append(lp)
+        a.n_label_priorities = len(label_priorities)
+        a.has_service_anti_affinity = int(any(saa for _, _, _, saa in label_priorities))
+        a.label_priorities = C.cast(lp, C.POINTER(LabelPriority))
+        self._check(lib().ksim_k8s_open_policy(self.h, C.byref(cfg), C.byref(w), C.byref(a), C.byref(hh)))
         return abi.Handle.adopt(hh, cfg)
 
     def open(self, cfg, prefer_avoid_weight=0):

@@ -166,3 +166,18 @@ def test_unsupported_inputs_are_refused():
                                                       {"type": "Ready", "status": "Unknown"}])
     with pytest.raises(abi.KsimUnsupported):
         frontend.K8sCluster([node], (), [])
+
+
+def test_policy_arguments_refused_with_services():
+    """CheckServiceAffinity / serviceAntiAffinity through the C++ front end when the adapter's
+    ServiceLister selects pods: refused before any device work (the Python host builds those)."""
+    from ksim import abi, frontend, scheduler
+    from workloads import rnd_workload
+    nodes, running, pods = rnd_workload(2, n_nodes=8, n_pods=10)
+    fe = frontend.K8sCluster(nodes, running, pods)
+    cfg = scheduler.make_config(["GeneralPredicates", "CheckServiceAffinity"], [("LeastRequestedPriority", 1)])
+    with pytest.raises(abi.KsimUnsupported):
+        fe.open_policy(cfg, service_affinity=["tier"], services_select_pods=True)
+    cfg = scheduler.make_config(["GeneralPredicates", "CheckNodeLabelPresence"], [("LeastRequestedPriority", 1)])
+    with pytest.raises(abi.KsimUnsupported):
+        fe.open(cfg)   # the predicate's arguments only come through ksim_k8s_open_policy

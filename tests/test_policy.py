@@ -5,7 +5,7 @@ api/validation/validation_test.go (ValidatePolicy's errors).  CPU only."""
 import pytest
 
 from golden_util import case_id, load
-from ksim import abi, policy, scheduler
+from ksim import abi, ingest, policy, scheduler
 
 
 @pytest.mark.parametrize("c", load("policy"), ids=case_id)
@@ -189,3 +189,57 @@ def test_service_affinity_table_matches_oracle():
     preds, _, _ = policy.key_sets(pol)
     assert "CheckServiceAffinity" in preds and policy.service_affinity_labels(pol) == ["disk"]
     assert scheduler.make_config(preds, []).predicates & abi.P_SERVICE_AFFINITY
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(GPU_POLICIES))
+def test_gpu_policy_arguments_through_cpp_front_end(name):
+    """The Policy's arguments through the C++ front end (ksim_k8s_open_policy): CheckNodeLabelPresence,
+    CheckServiceAffinity (no services), labelPreference / serviceAntiAffinity priorities evaluated in
+    the library from raw fields — placements, FitError histograms' texts and lastNodeIndex equal the
+    object oracle's."""
+    import ctypes as C
+
+    import numpy as np
+
+    import ksim_ref as R
+    from ksim import frontend
+    from workloads import rnd_workload
+    pol = policy.decode(GPU_POLICIES[name])
+    preds, prios, lp = policy.key_sets(pol)
+    sa = policy.service_affinity_labels(pol)
+    args = policy.priority_arguments(pol)
+    custom = {"CheckNodeLabelPresence": R.new_node_label_predicate(*lp)} if lp else {}
+    if sa is not None:
+        custom["CheckServiceAffinity"] = R.new_service_affinity_predicate(sa)
+    cprios = {n: (R.node_label_priority(a[1], a[2]) if a[0] == "labelPreference" else R.service_anti_affinity_priority(a[1]))
+              for n, a in args.items()}
+    weights = dict(prios)
+    label_prios = [(a[1], a[2] if a[0] == "labelPreference" else True, int(weights[n]), a[0] == "serviceAntiAffinity")
+                   for n, a in args.items()]
+    for seed in (3, 11):
+        nodes, running, pods = rnd_workload(seed, n_nodes=31 + seed, n_pods=140)
+        want, lni = R.simulate(nodes, running, pods, set(preds), list(prios), custom, custom_priorities=cprios)
+        order = list(reversed(pods))
+        cl = ingest.Cluster.from_objects(nodes, running, order)
+        p = scheduler.plan(cl, preds, prios, label_presence=lp, custom_priorities=args, service_affinity=sa)
+        fe = frontend.K8sCluster(nodes, running, order)
+        h = fe.open_policy(p.cfg, prefer_avoid_weight=weights.get("NodePreferAvoidPodsPriority", 0),
+                           image_locality_weight=weights.get("ImageLocalityPriority", 0), label_presence=lp,
+                           service_affinity=sa, label_priorities=label_prios)
+        n = len(order)
+        out = np.zeros(n, np.int32)
+        reasons = np.zeros((n, abi.NREASONS), np.int32)
+        st = abi.Stats()
+        try:
+            h.call("ksim_schedule", 0, n, abi.vptr(out), abi.vptr(reasons), C.byref(st))
+            ctr = C.c_uint64()
+            h.call("ksim_get_counter", C.byref(ctr))
+        finally:
+            h.close()
+        names = fe.names
+        got = [(cl.pod_names[k], names[w] if w >= 0 else None,
+                None if w >= 0 else scheduler.fit_error_message(len(names), reasons[k], cl.scalar_names.items))
+               for k, w in enumerate(out)]
+        assert got == want
+        assert ctr.value == lni
