@@ -363,6 +363,8 @@ typedef struct {
   int32_t max_vols[3];      /* MaxPD limits (EBS, GCE PD, Azure Disk); 0: getMaxVols */
   int32_t port_slots;       /* host-port slots per node row (<= 0: 8) */
   int32_t check_volume_binding; /* CheckVolumeBinding is configured (no kernel bit: refusals only) */
+  int32_t pad;
+  const ksim_k8s_policy_args* policy; /* a Policy's arguments (copied at create), NULL: none */
 } ksim_k8s_cache_options;
 
 int ksim_k8s_cache_create(const ksim_k8s_cache_options* opt, ksim_k8s_cache** out);

@@ -56,6 +56,10 @@ struct ksim_k8s_cache {
   ClassTab ct;
   std::array<size_t, 3> tables_for{{SIZE_MAX, SIZE_MAX, SIZE_MAX}};  // (L, T, classes) of the loaded class tables
   bool need_na = false, aff_wanted = false, vol_on = false, use_zone = false;
+  PolicyArgs pol;                    // a Policy's arguments (ksim_k8s_cache_options.policy, copied)
+  bool pol_presence = false, pol_svc = false;
+  std::vector<uint32_t> svc_ok;      // CheckServiceAffinity's (class, label set) table
+  std::vector<uint8_t> svc_need;
   std::vector<Str> names;            // listed nodes, ascending bytewise (= name rank)
   std::map<Str, int64_t> rank;
   bool rank_valid = true;
@@ -118,7 +122,10 @@ void load_tables(Cache* c) {
   const std::array<size_t, 3> key{{c->in.label_sets.items.size(), c->in.taint_sets.items.size(), c->in.classes.items.size()}};
   if (key == c->tables_for) return;
   build_class_tab(c->in, &c->ct);
-  check(c, load_class_tab(c->ct, c->h, c->opt.extra.prefer_avoid, c->opt.extra.image_locality, c->need_na), "ksim_load_classes");
+  const std::vector<int64_t> lab_add = policy_label_add(c->in, c->pol);  // a Policy's label priorities
+  if (c->pol_svc) policy_svc_ok(c->in, c->ct, c->pol, &c->svc_ok, &c->svc_need);
+  check(c, load_class_tab(c->ct, c->h, c->opt.extra.prefer_avoid, c->opt.extra.image_locality, c->need_na,
+                          c->pol_svc ? c->svc_ok.data() : nullptr, &lab_add), "ksim_load_classes");
   c->tables_for = key;
   c->stats[3] += 1;
 }
@@ -142,6 +149,7 @@ Enc encode(Cache* c, const PodObj& p) {
   if (c->need_na && c->ct.bad_classes.count(cls))
     fail(KSIM_E_UNSUPPORTED, "NodeAffinityPriority: a preferred node-affinity term does not parse");
   e.row.flags |= c->ct.need[cls];
+  if (c->pol_svc && cls < (int32_t)c->svc_need.size() && c->svc_need[cls]) e.row.flags |= KSIM_POD_NEED_SVC_AFFINITY;
   if (c->vol_on && has_pred_volumes(p)) e.row.vol_class = c->vidx.vclass(p);
   return e;
 }
@@ -357,6 +365,9 @@ void node_row(Cache* c, const NodeObj& x, const Info& info, Str* mem, Str* disk,
   r.alloc_cpu = x.alloc[0]; r.alloc_mem = x.alloc[1]; r.alloc_gpu = x.alloc[2]; r.alloc_eph = x.alloc[3];
   r.allowed_pods = (int32_t)x.pods;
   r.flags = node_flags(x, mem, disk);
+  if (c->pol_presence)  // CheckNodeLabelPresence (predicates.go:875-910): a function of the label set
+    for (const Str& l : c->pol.presence_labels)
+      if ((x.labels.count(l) != 0) != c->pol.presence) { r.flags |= KSIM_N_LABEL_PRESENCE; break; }
   r.label_set = lid;
   r.taint_set = tid;
   std::set<uint64_t> seen;
@@ -537,8 +548,27 @@ extern "C" int ksim_k8s_cache_create(const ksim_k8s_cache_options* opt, ksim_k8s
   const int rc = guard(c, [&] {
     const ksim_config& cfg = c->opt.cfg;
     const uint32_t pr = cfg.predicates;
-    if (pr & (KSIM_P_LABEL_PRESENCE | KSIM_P_SERVICE_AFFINITY))
-      fail(KSIM_E_UNSUPPORTED, "CheckNodeLabelPresence / CheckServiceAffinity need their Policy arguments (the Python host)");
+    if (const ksim_k8s_policy_args* a = c->opt.policy) {
+      PolicyArgs& pol = c->pol;
+      pol.on = true;
+      for (int32_t i = 0; i < a->n_presence_labels; ++i) pol.presence_labels.push_back(S(a->presence_labels[i]));
+      pol.presence = a->presence != 0;
+      for (int32_t i = 0; i < a->n_affinity_labels; ++i) pol.affinity_labels.push_back(S(a->affinity_labels[i]));
+      for (int32_t i = 0; i < a->n_label_priorities; ++i) {
+        if (a->label_priorities[i].weight <= 0) fail(KSIM_E_INVAL, "label priority: weight must be positive");
+        pol.label_prios.push_back({S(a->label_priorities[i].label),
+                                   {a->label_priorities[i].presence != 0, a->label_priorities[i].weight}});
+      }
+      if (a->services_select_pods && ((pr & KSIM_P_SERVICE_AFFINITY) || a->has_service_anti_affinity))
+        fail(KSIM_E_UNSUPPORTED, "CheckServiceAffinity / serviceAntiAffinity with services selecting the pods (the Python "
+                                 "host builds their service-aware tables)");
+      c->opt.policy = nullptr;  // copied
+      c->pol_presence = (pr & KSIM_P_LABEL_PRESENCE) != 0;
+      c->pol_svc = (pr & KSIM_P_SERVICE_AFFINITY) != 0;
+    } else if (pr & (KSIM_P_LABEL_PRESENCE | KSIM_P_SERVICE_AFFINITY)) {
+      fail(KSIM_E_UNSUPPORTED, "CheckNodeLabelPresence / CheckServiceAffinity need their Policy arguments "
+                               "(ksim_k8s_cache_options.policy)");
+    }
     c->need_na = cfg.weights[KSIM_W_NODE_AFFINITY] != 0;
     c->aff_wanted = (pr & KSIM_P_INTERPOD_AFFINITY) ||
                     ((cfg.weights[KSIM_W_INTERPOD_AFFINITY] || cfg.weights[KSIM_W_SELECTOR_SPREAD]) && !cfg.no_priorities);

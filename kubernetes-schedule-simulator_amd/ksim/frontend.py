@@ -146,7 +146,34 @@ class PolicyArgs(C.Structure):
 
 class CacheOptions(C.Structure):
     _fields_ = [("cfg", abi.Config), ("extra", Weights), ("hard_weight", C.c_int32), ("max_vols", C.c_int32 * 3),
-                ("port_slots", C.c_int32), ("check_volume_binding", C.c_int32)]
+                ("port_slots", C.c_int32), ("check_volume_binding", C.c_int32), ("pad", C.c_int32),
+                ("policy", C.POINTER(PolicyArgs))]
+
+
+def policy_args(keep, label_presence=None, service_affinity=None, label_priorities=(), services_select_pods=False):
+    """ksim_k8s_policy_args from a Policy's arguments (arrays kept alive in `keep`): label_presence =
+    (labels, presence), service_affinity = labels, label_priorities = [(label, presence, weight,
+    is_service_anti_affinity)]."""
+    def strs(xs):
+        arr = (C.c_char_p * max(len(xs), 1))(*[x.encode() for x in xs])
+        keep.append(arr)
+        return C.cast(arr, C.POINTER(C.c_char_p))
+    a = PolicyArgs()
+    if label_presence is not None:
+        a.n_presence_labels, a.presence = len(label_presence[0]), int(bool(label_presence[1]))
+        a.presence_labels = strs(list(label_presence[0]))
+    if service_affinity is not None:
+        a.n_affinity_labels = len(service_affinity)
+        a.affinity_labels = strs(list(service_affinity))
+    a.services_select_pods = int(bool(services_select_pods))
+    lp = (LabelPriority * max(len(label_priorities), 1))(*[LabelPriority(l.encode(), int(bool(pr)), 0, int(wt))
+                                                           for l, pr, wt, _ in label_priorities])
+    keep.append(lp)
+    a.n_label_priorities = len(label_priorities)
+    a.has_service_anti_affinity = int(any(saa for _, _, _, saa in label_priorities))
+    a.label_priorities = C.cast(lp, C.POINTER(LabelPriority))
+    keep.append(a)
+    return a
 
 
 class Options(C.Structure):
@@ -485,25 +512,7 @@ class K8sCluster:
         hh = C.c_void_p()
         w = Weights(int(prefer_avoid_weight), int(image_locality_weight))
         keep = []
-
-        def strs(xs):
-            arr = (C.c_char_p * max(len(xs), 1))(*[x.encode() for x in xs])
-            keep.append(arr)
-            return arr
-        a = PolicyArgs()
-        if label_presence is not None:
-            a.n_presence_labels, a.presence = len(label_presence[0]), int(bool(label_presence[1]))
-            a.presence_labels = C.cast(strs(list(label_presence[0])), C.POINTER(C.c_char_p))
-        if service_affinity is not None:
-            a.n_affinity_labels = len(service_affinity)
-            a.affinity_labels = C.cast(strs(list(service_affinity)), C.POINTER(C.c_char_p))
-        a.services_select_pods = int(bool(services_select_pods))
-        lp = (LabelPriority * max(len(label_priorities), 1))(*[LabelPriority(l.encode(), int(bool(pr)), 0, int(wt))
-                                                               for l, pr, wt, _ in label_priorities])
-        keep.append(lp)
-        a.n_label_priorities = len(label_priorities)
-        a.has_service_anti_affinity = int(any(saa for _, _, _, saa in label_priorities))
-        a.label_priorities = C.cast(lp, C.POINTER(LabelPriority))
+        a = policy_args(keep, label_presence, service_affinity, label_priorities, services_select_pods)
         self._check(lib().ksim_k8s_open_policy(self.h, C.byref(cfg), C.byref(w), C.byref(a), C.byref(hh)))
         return abi.Handle.adopt(hh, cfg)
 
@@ -537,18 +546,33 @@ class K8sCache:
     errors (as SchedulerCache raises), KsimUnsupported / NoNodesAvailable / KsimError otherwise."""
 
     def __init__(self, predicates, priorities, device=0, mode=abi.MODE_AUTO, last_node_index=0, port_slots=8,
-                 pvs=(), pvcs=(), storage_classes=(), hard_weight=10, spread=None, max_vols=None):
+                 pvs=(), pvcs=(), storage_classes=(), hard_weight=10, spread=None, max_vols=None, label_presence=None,
+                 service_affinity=None, custom_priorities=None):
+        """label_presence / service_affinity / custom_priorities: a Policy's arguments (policy.key_sets,
+        service_affinity_labels, priority_arguments) — evaluated in the library (ksim_k8s_policy_args)."""
         from . import scheduler
         self.predicates = list(predicates)
         self.prioritizers = list(priorities)
         self.spread = spread if spread else None
         names = {n for n, _ in priorities}
+        custom = dict(custom_priorities or {})
         self._services_only = "ServiceSpreadingPriority" in names and "SelectorSpreadPriority" not in names
-        cfg = scheduler.make_config(predicates, priorities, device, mode, True, last_node_index, spread=self.spread is not None)
+        cfg = scheduler.make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence],
+                                    [(n, x) for n, x in priorities if n not in custom], device, mode, True,
+                                    last_node_index, spread=self.spread is not None, configured=list(priorities))
         w = lambda key: sum(int(x) for n, x in priorities if n == key)
+        self._keep_policy = []
+        pol = None
+        if label_presence is not None or service_affinity is not None or custom:
+            weights = dict(priorities)
+            pol = policy_args(self._keep_policy, label_presence, service_affinity,
+                              [(a[1], a[2] if a[0] == "labelPreference" else True, int(weights[n]), a[0] == "serviceAntiAffinity")
+                               for n, a in custom.items() if n in weights],
+                              services_select_pods=bool(self.spread and self.spread.services))
         opt = CacheOptions(cfg, Weights(w("NodePreferAvoidPodsPriority"), w("ImageLocalityPriority")), int(hard_weight),
                            (C.c_int32 * 3)(*(max_vols or (0, 0, 0))), int(port_slots),
-                           int("CheckVolumeBinding" in self.predicates))
+                           int("CheckVolumeBinding" in self.predicates), 0,
+                           C.pointer(pol) if pol is not None else None)
         L = lib()
         h = C.c_void_p()
         rc = L.ksim_k8s_cache_create(C.byref(opt), C.byref(h))

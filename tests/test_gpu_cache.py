@@ -403,3 +403,38 @@ def test_event_stream_with_image_locality(seed, impl):
     finally:
         dut.close()
     assert decisions > 80
+
+
+@pytest.mark.parametrize("seed", range(2))
+@pytest.mark.parametrize("name", ["absent_rank", "present_tier_disk", "service_affinity", "label_priorities"])
+def test_event_stream_with_policy_arguments(seed, name):
+    """A Policy's arguments through the C++ scheduler cache (ksim_k8s_cache_options.policy):
+    CheckNodeLabelPresence on node rows as they are added / updated, CheckServiceAffinity's table
+    and the label priorities' addends as label sets and classes are interned — decision by decision
+    against the oracle's cache with the same Policy."""
+    from ksim import policy
+    from test_policy import GPU_POLICIES
+    pol = policy.decode(GPU_POLICIES[name])
+    preds, prios, lp = policy.key_sets(pol)
+    sa = policy.service_affinity_labels(pol)
+    args = policy.priority_arguments(pol)
+    custom = {"CheckNodeLabelPresence": R.new_node_label_predicate(*lp)} if lp else {}
+    if sa is not None:
+        custom["CheckServiceAffinity"] = R.new_service_affinity_predicate(sa)
+    cprios = {n: (R.node_label_priority(a[1], a[2]) if a[0] == "labelPreference" else R.service_anti_affinity_priority(a[1]))
+              for n, a in args.items()}
+    ref = R.SchedulerCache(set(preds), prios, custom)
+    ref.sched = R.GenericScheduler(set(preds), list(prios), custom, custom_priorities=cprios)
+    dut = K8sCache(preds, prios, label_presence=lp, service_affinity=sa, custom_priorities=args)
+    decisions = 0
+    try:
+        for ev in event_stream(seed, ref, 300, 14, True):
+            want = apply(ref, ev)
+            got = apply(dut, ev)
+            if ev[0] == "schedule":
+                decisions += 1
+                assert got == want, (ev[1]["metadata"]["name"], want, got)
+        assert dut.last_node_index == ref.sched.last_node_index
+    finally:
+        dut.close()
+    assert decisions > 100
