@@ -43,8 +43,14 @@ extern "C" hipError_t ksim_pstream_prepare(const KsimCtx* c, double* mirror, hip
 extern "C" size_t ksim_pfast_granule_bytes(void);
 extern "C" size_t ksim_shard_xchg_bytes(void);
 extern "C" size_t ksim_shard_lx_offset(void);
+extern "C" size_t ksim_pfast_cache_bytes(int lds_rows, int ncls);
+extern "C" size_t ksim_pipe_lds_bytes(int lds_rows, int ncls);
+extern "C" size_t ksim_pipe_word_bytes(int grid, int lds_rows);
+extern "C" hipError_t ksim_launch_pipe(const KsimCtx* c, uint64_t* words, int grid, int lds_rows, const int32_t* tcls,
+                                       const KsimTreeClass* tclass, int ncls, hipStream_t s);
 extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, double* mirror,
-                                        const KsimShard* sh, hipStream_t s);
+                                        const KsimShard* sh, const int32_t* tcls, const KsimTreeClass* tclass, int ncls,
+                                        hipStream_t s);
 extern "C" hipError_t ksim_tree_build(const KsimCtx* c, const KsimTreeGeo* g, const KsimTreeClass* cls,
                                       const int32_t* tcls, int32_t* leaves, uint64_t* levels, int32_t* fitc,
                                       double* ty, const KsimTreeSweep* sw, hipStream_t s);
@@ -126,6 +132,10 @@ struct ksim_handle {
   // inputs, the geometry and the device trees; tree_valid = the trees describe the current
   // node table (any other commit path clears it)
   int32_t n_tcls = 0;                      // -1: more classes than the tree supports
+  bool last_pfast_cache = false;           // the last fast-kernel call took the cached form
+  bool last_pfast_pipe = false;            // ... and its two-deep pipelined kernel (ksim_pipe.hip)
+  uint64_t* pipe_words = nullptr;          // the pipelined kernel's published words
+  size_t pipe_bytes = 0;
   int32_t* tcls = nullptr;
   int64_t tcls_cap = 0;
   KsimTreeClass* tclass = nullptr;

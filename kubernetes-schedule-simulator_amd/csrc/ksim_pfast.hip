@@ -31,6 +31,7 @@
 
 #include "ksim_f64.h"
 #include "ksim_fast.h"
+#include "ksim_tree.h"
 #include "ksim_wave.h"
 
 using namespace kf64;
@@ -171,6 +172,11 @@ struct PfArgs {
   // streaming form (tables beyond the LDS budget): float64 image of the table in HBM,
   // [6][n] = alloc cpu, alloc mem, requested cpu, mem, non-zero cpu, mem
   double* mirror;
+  // cached form (LDS rows, map-only policies, ncls > 0): every (tree class, row) evaluation is
+  // kept in LDS and only the committed row is re-evaluated — see "Cached form" below
+  const int32_t* tcls;            // [pods] tree class of each queued pod (resource-only key)
+  const KsimTreeClass* tclass;    // [ncls] the class's predicate / priority inputs
+  int32_t ncls;
 };
 
 namespace {
@@ -183,6 +189,7 @@ struct FRows {  // LDS image of the owned rows (SoA)
   int32_t* ev2;   // [chunk]: evaluation of pod p+1 against row + pod p
   uint32_t* rm2;  // [chunk]: ... its reason mask
   uint32_t* rma;  // STREAM: [2][chunk] reason mask of ev (registers in the LDS form)
+  int16_t* cache; // CACHE: [ncls][chunk] evaluation of tree class k on row j as it stands
 };
 
 constexpr int LDS_ROW_BYTES = 8 * 8 + 8 * 4;  // 96: 8 float64 + allowed, count, flags, ev[2], ev2, rm2, top_list
@@ -208,6 +215,7 @@ __device__ __forceinline__ FRows carve(int rows, const PfArgs& a, int64_t lo) {
     r.ev2 = q + 2 * rows;
     r.rm2 = reinterpret_cast<uint32_t*>(q + 3 * rows);
     r.rma = r.rm2 + 2 * rows;  // after top_list
+    r.cache = nullptr;
     return r;
   }
   double* d = reinterpret_cast<double*>(kf_smem);
@@ -219,6 +227,7 @@ __device__ __forceinline__ FRows carve(int rows, const PfArgs& a, int64_t lo) {
   r.ev = q + 3 * rows;
   r.ev2 = q + 5 * rows;
   r.rm2 = reinterpret_cast<uint32_t*>(q + 6 * rows);
+  r.cache = reinterpret_cast<int16_t*>(q + 8 * rows);  // after top_list (q + 7 rows)
   return r;
 }
 
@@ -266,8 +275,9 @@ struct Top2 {
 
 }  // namespace
 
-template <int NPT, bool STREAM>
+template <int NPT, bool STREAM, bool CACHE>
 __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
+  static_assert(!(STREAM && CACHE), "the cached form keeps the rows in LDS");
   __shared__ int32_t s_wst[2][RW][5];         // per row wave: fit, m1, c1, m2, c2 (by pod parity)
   __shared__ uint64_t s_bm[2][NPT][RW];       // per 64-row segment: rows at the wave maximum
   __shared__ int32_t s_wg[2][5];              // workgroup top-two of the pod
@@ -282,6 +292,8 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   __shared__ double s_pval[4];   // STREAM: the deferred-commit row's dynamic values after applying it
   __shared__ int32_t s_pcnt;
   __shared__ __attribute__((aligned(16))) ksim_pod s_pod[RING];
+  __shared__ int32_t s_pcls[CACHE ? RING : 1];                              // CACHE: tree class of each ring slot
+  __shared__ KsimTreeClass s_tcl[CACHE ? KSIM_TREE_MAX_CLASSES : 1];       // CACHE: the class inputs
 #ifdef KSIM_STAMPS
   uint64_t st_acc[16] = {};
 #endif
@@ -315,24 +327,45 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
   }
   // pod descriptors: RING_FILL (1 KiB) per refill, one 16-byte load per lane of wave 1, loaded
   // a whole refill period before they are stored so the load latency never stalls a pod
-  auto ring_load = [&](int64_t p0, uint4& v) {
+  // (CACHE: lane l < RING_FILL also carries pod p0 + l's tree class)
+  auto ring_load = [&](int64_t p0, uint4& v, int32_t& cl) {
     const int64_t p = p0 + lane / 8;
     if (p < a.end) v = reinterpret_cast<const uint4*>(&a.pods[p])[lane % 8];
+    if (CACHE && lane < RING_FILL && p0 + lane < a.end) cl = a.tcls[p0 + lane];
   };
-  auto ring_store = [&](int64_t p0, const uint4& v) {
+  auto ring_store = [&](int64_t p0, const uint4& v, int32_t cl) {
     const int64_t p = p0 + lane / 8;
     if (p < a.end) reinterpret_cast<uint4*>(&s_pod[p % RING])[lane % 8] = v;
+    if (CACHE && lane < RING_FILL && p0 + lane < a.end) s_pcls[(p0 + lane) % RING] = cl;
   };
   uint4 ring_next = make_uint4(0, 0, 0, 0);  // wave 1: descriptors of the next refill
+  int32_t ring_next_cl = 0;
   if (wv == 1) {
     uint4 v;
-    ring_load(a.first, v);
-    ring_load(a.first + RING_FILL, ring_next);
-    ring_store(a.first, v);
+    int32_t cl = 0;
+    ring_load(a.first, v, cl);
+    ring_load(a.first + RING_FILL, ring_next, ring_next_cl);
+    ring_store(a.first, v, cl);
   }
+  if (CACHE)
+    for (int k = tid; k < a.ncls; k += BS) s_tcl[k] = a.tclass[k];
   if (tid == 0) { s_fix[a.first & 1][0] = -1; s_arr = 0; s_prow[0] = s_prow[1] = -1; }
   uint64_t counter = *a.counter;  // replicated genericScheduler.lastNodeIndex
   __syncthreads();
+  // CACHE: a class's inputs as the evaluation reads them (add_* only matter for a commit)
+  auto cls_fpod = [&](int k) -> FPod {
+    const KsimTreeClass& t = s_tcl[k];
+    return FPod{t.rq_c, t.rq_m, t.nz_c, t.nz_m, 0.0, 0.0, t.anyreq, t.be};
+  };
+  if (CACHE) {  // every (class, owned row) evaluation, once per call
+    const int tot = a.ncls * nrows;
+    for (int idx = tid; idx < tot; idx += BS) {
+      const int k = idx / nrows, j = idx - k * nrows;
+      uint32_t rm;
+      R.cache[k * chunk + j] = (int16_t)feval(EC, cls_fpod(k), load_frow<false>(R, j), rm);
+    }
+    __syncthreads();
+  }
 
   auto ptag = [&](int64_t p) -> uint64_t { return (uint64_t)((p - a.first + 1) & 0xFF); };
   // wave-level statistics of NPT evaluations per lane → LDS slot (buf, w)
@@ -466,7 +499,9 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       e[k] = -1;
       uint32_t& am = A_rm[STREAM ? 0 : k];
       am = 0;
-      if (j < nrows) {
+      if (CACHE) {
+        if (j < nrows) e[k] = R.cache[s_pcls[a.first % RING] * chunk + j];
+      } else if (j < nrows) {
         e[k] = feval(EC, P0, load_frow<STREAM>(R, j), am);
         if (STREAM) R.rma[(a.first & 1) * chunk + j] = am;
         ev[j] = e[k];
@@ -683,9 +718,10 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       if (has_next) {
       // ---------------- row waves: evaluate pod + 1, as the rows stand and after pod -----------
       const bool refill = wv == 1 && ((pod - a.first) % RING_FILL) == 0;
-      if (refill) ring_store(pod + RING_FILL, ring_next);  // loaded a refill period ago
+      if (refill) ring_store(pod + RING_FILL, ring_next, ring_next_cl);  // loaded a refill period ago
       uint4 rv;
-      if (refill) ring_load(pod + 2 * RING_FILL, rv);
+      int32_t rcl = 0;
+      if (refill) ring_load(pod + 2 * RING_FILL, rv, rcl);
 #ifdef KSIM_STAMPS
       const uint64_t te0 = __builtin_amdgcn_s_memtime();
 #endif
@@ -706,6 +742,32 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
       int32_t e[NPT];
       FRow rk[STREAM ? 1 : NPT];
       int32_t* evn = R.ev + nb * chunk;
+      if (CACHE) {
+        // cached form: pod + 1's statistics are its class's cached evaluations (the rows as they
+        // stand), then pod + 1 against "row + pod" only for the rows pod can commit to — the
+        // rows at this workgroup's maximum of pod (its owner picks one of them)
+        const int16_t* c1 = R.cache + s_pcls[(pod + 1) % RING] * chunk;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          const int32_t j = k * RT + rt;
+          e[k] = j < nrows ? (int32_t)c1[j] : -1;
+        }
+        WSTAMP(9);
+        wave_stats(e, nb, wv);
+        WSTAMP(10);
+        arrive_publish(pod + 1, nb);
+        const int32_t M0 = s_wg[pb][1];
+        const int16_t* c0 = R.cache + s_pcls[pod % RING] * chunk;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) {
+          const int32_t j = k * RT + rt;
+          if (M0 >= 0 && j < nrows && (int32_t)c0[j] == M0) {
+            uint32_t m2;
+            R.ev2[j] = feval(EC, Q, plus(load_frow<false>(R, j), P), m2);
+            R.rm2[j] = m2;
+          }
+        }
+      } else {
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
         const int32_t j = k * RT + rt;
@@ -740,11 +802,12 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           }
         }
       }
+      }  // !CACHE
       WSTAMP(11);
 #ifdef KSIM_STAMPS
       if (tid == 64) st_acc[5] += __builtin_amdgcn_s_memtime() - te0;
 #endif
-      if (refill) ring_next = rv;
+      if (refill) { ring_next = rv; ring_next_cl = rcl; }
       }
       // STREAM: the wave that applied pod - 1's deferred commit lets its stores reach L2 before
       // the barrier: from the next pod on the owner may read that row (load_frow_l2)
@@ -785,7 +848,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           if (!STREAM) { e_new = R.ev2[jsel]; m_new = R.rm2[jsel]; }
           // the workgroup's pod + 1 statistics without the committed row's pre-commit
           // evaluation, with its post-commit one (straight-line selects)
-          const int32_t e_old = R.ev[nb * chunk + jsel];
+          const int32_t e_old = CACHE ? (int32_t)R.cache[s_pcls[(pod + 1) % RING] * chunk + jsel] : R.ev[nb * chunk + jsel];
           const int32_t f0 = s_wg[nb][0], m1 = s_wg[nb][1], c1 = s_wg[nb][2], m2 = s_wg[nb][3], c2 = s_wg[nb][4];
           const bool rem = e_old >= 0, add = e_new >= 0;
           const int32_t c1a = c1 - ((rem && e_old == m1) ? 1 : 0);
@@ -804,6 +867,15 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
           }
         }
         OSTAMP(18);
+        if (CACHE) {
+          // the committed row's evaluation for every class (lane k = class k), off the critical
+          // path: the next pods' statistics read them after the barrier below
+          const FRow r2 = plus(load_frow<false>(R, jsel), load_fpod(s_pod[pod % RING]));
+          if (lane < a.ncls) {
+            uint32_t rm;
+            R.cache[lane * chunk + jsel] = (int16_t)feval(EC, cls_fpod(lane), r2, rm);
+          }
+        }
         if (lane == 0) {  // commit: NodeInfo.AddPod into the LDS row (STREAM: deferred, s_prow)
           if (!STREAM) {
             const ksim_pod& Pp = s_pod[pod % RING];
@@ -830,7 +902,7 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
           const int32_t j = k * RT + (w - 1) * 64 + lane;
-          e[k] = j < nrows ? R.ev[nb * chunk + j] : -1;
+          e[k] = j < nrows ? (CACHE ? (int32_t)R.cache[s_pcls[(pod + 1) % RING] * chunk + j] : R.ev[nb * chunk + j]) : -1;
         }
         wave_stats(e, nb, w);
         OSTAMP(19);
@@ -851,7 +923,11 @@ __global__ __launch_bounds__(BS) void ksim_pfast_kernel(PfArgs a) {
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
           const int32_t j = k * RT + rt;
-          const uint32_t rm = (j == fr) ? fmk : !STREAM ? A_rm[STREAM ? 0 : k] : (j < nrows ? R.rma[pb * chunk + j] : 0u);
+          uint32_t rm = (j == fr) ? fmk : !STREAM ? A_rm[STREAM ? 0 : k] : (j < nrows ? R.rma[pb * chunk + j] : 0u);
+          if (CACHE) {  // the cached form keeps no reason masks: pod against the rows as they stand
+            rm = 0;
+            if (j < nrows) (void)feval(EC, load_fpod(s_pod[pod % RING]), load_frow<false>(R, j), rm);
+          }
           for (int r = 0; r < KSIM_NREASONS; ++r) {
             const int32_t n = __popcll(__ballot((rm >> r) & 1u));
             if (lane == 0 && n) atomicAdd(&s_hist[r], n);
@@ -966,9 +1042,19 @@ extern "C" hipError_t ksim_pstream_prepare(const KsimCtx* c, double* mirror, hip
   return hipGetLastError();
 }
 
+// LDS bytes of the cached form's evaluations ([ncls][lds_rows] int16), 0 when it does not fit
+// beside the rows; the cached form needs every map score below 2^15 (host-checked).
+extern "C" size_t ksim_pfast_cache_bytes(int lds_rows, int ncls) {
+  if (ncls <= 0 || ncls > KSIM_TREE_MAX_CLASSES || lds_rows <= 0) return 0;
+  const size_t b = ((size_t)ncls * lds_rows * 2 + 15) & ~(size_t)15;
+  return (size_t)lds_rows * LDS_ROW_BYTES + b <= (size_t)PF_LDS_BUDGET ? b : 0;
+}
+
 extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, double* mirror,
-                                        const KsimShard* sh, hipStream_t s) {
+                                        const KsimShard* sh, const int32_t* tcls, const KsimTreeClass* tclass, int ncls,
+                                        hipStream_t s) {
   PfArgs a;
+  a.tcls = tcls; a.tclass = tclass; a.ncls = ncls;
   a.rank = sh->rank; a.world = sh->world; a.node_base = sh->node_base; a.xtag_base = sh->xtag_base;
   a.xchg = sh->xchg;
   for (int r = 0; r < KSIM_MAX_RANKS; ++r) a.peers[r] = sh->peers[r];
@@ -983,12 +1069,13 @@ extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, in
   a.wb = (int32_t)c->w[KSIM_W_BALANCED];
   a.mirror = mirror;
   // every workgroup resident at once (the kernel spins on its peers), then the launch
-#define KSIM_PF(R, S, L)                                                             \
-  do {                                                                               \
-    hipError_t e_ = ksim_check_coresident(ksim_pfast_kernel<R, S>, grid, BS, L);     \
-    if (e_ != hipSuccess) return e_;                                                 \
-    hipLaunchKernelGGL((ksim_pfast_kernel<R, S>), dim3(grid), dim3(BS), L, s, a);    \
+#define KSIM_PFC(R, S, C, L)                                                           \
+  do {                                                                                 \
+    hipError_t e_ = ksim_check_coresident(ksim_pfast_kernel<R, S, C>, grid, BS, L);    \
+    if (e_ != hipSuccess) return e_;                                                   \
+    hipLaunchKernelGGL((ksim_pfast_kernel<R, S, C>), dim3(grid), dim3(BS), L, s, a);   \
   } while (0)
+#define KSIM_PF(R, S, L) KSIM_PFC(R, S, false, L)
   if (mirror) {  // streaming form (image prepared by ksim_pstream_prepare on the same stream)
     const size_t lds = (size_t)lds_rows * LDS_ROW_BYTES_STREAM;
     if (lds_rows <= RT) KSIM_PF(1, true, lds);
@@ -997,10 +1084,19 @@ extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, in
     else KSIM_PF(9, true, lds);
     return hipGetLastError();
   }
-  const size_t lds = (size_t)lds_rows * LDS_ROW_BYTES;
+  const size_t cb = ncls > 0 ? ksim_pfast_cache_bytes(lds_rows, ncls) : 0;
+  if (ncls > 0 && !cb) return hipErrorInvalidValue;
+  const size_t lds = (size_t)lds_rows * LDS_ROW_BYTES + cb;
+  if (cb) {  // cached form
+    if (lds_rows <= RT) KSIM_PFC(1, false, true, lds);
+    else if (lds_rows <= 2 * RT) KSIM_PFC(2, false, true, lds);
+    else KSIM_PFC(4, false, true, lds);
+    return hipGetLastError();
+  }
   if (lds_rows <= RT) KSIM_PF(1, false, lds);
   else if (lds_rows <= 2 * RT) KSIM_PF(2, false, lds);
   else KSIM_PF(4, false, lds);
 #undef KSIM_PF
+#undef KSIM_PFC
   return hipGetLastError();
 }

@@ -651,9 +651,39 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
   c.first = first;
   c.end = first + count;
   c.chunk = (c.n + grid - 1) / grid;
-  HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
+  // the cached form (every pod of the range has a tree class, <= 64 classes, the classes'
+  // evaluations fit LDS beside the rows, map scores below 2^15): KSIM_NO_PCACHE=1 disables it
+  int ncls = 0;
+  if (!stream && !getenv("KSIM_NO_PCACHE") && h->n_tcls > 0 && h->tcls && h->tclass) {
+    int64_t sw = 0;
+    for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED}) sw += c.no_prio ? 0 : c.w[k] * 10;
+    if (sw < 32767 && ksim_pfast_cache_bytes(lds_rows, h->n_tcls)) ncls = h->n_tcls;
+  }
+  h->last_pfast_cache = ncls > 0;
+  // one device: the two-deep pipelined form of the cached kernel (ksim_pipe.hip), KSIM_PIPE=1 (experimental)
+  const char* pe = getenv("KSIM_PIPE");
+  const bool pipe = ncls > 0 && h->shard.world == 1 && pe && pe[0] == '1' && ksim_pipe_lds_bytes(lds_rows, ncls) &&
+                    (int64_t)grid * lds_rows >= c.n;
+  h->last_pfast_pipe = pipe;
+  if (pipe) {
+    const size_t wb = ksim_pipe_word_bytes(grid, lds_rows);
+    if (h->pipe_bytes < wb) {
+      dev_free(h, h->pipe_words);
+      h->pipe_words = nullptr;
+      h->pipe_bytes = 0;
+      int rc = dev_alloc(h, &h->pipe_words, wb / sizeof(uint64_t));
+      if (rc) return rc;
+      h->pipe_bytes = wb;
+    }
+    HIPCHK(h, hipMemsetAsync(h->pipe_words, 0, wb, h->stream));
+    HIPCHK(h, hipMemsetAsync(c.dbg, 0, 16 * 8, h->stream));
+  } else {
+    HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
+  }
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipError_t e = ksim_launch_pfast(&c, h->granules, grid, lds_rows, stream ? h->mirror : nullptr, &h->shard, h->stream);
+  hipError_t e = pipe ? ksim_launch_pipe(&c, h->pipe_words, grid, lds_rows, h->tcls, h->tclass, ncls, h->stream)
+                      : ksim_launch_pfast(&c, h->granules, grid, lds_rows, stream ? h->mirror : nullptr, &h->shard,
+                                          h->tcls, h->tclass, ncls, h->stream);
   if (e == hipErrorCooperativeLaunchTooLarge) {
     // the grid cannot be co-resident here (a smaller or shared device): the general kernels instead
     if (h->cfg.mode != KSIM_MODE_PERSISTENT && h->shard.world == 1) {
@@ -673,6 +703,14 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
     HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
     HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
     const double nf = (double)(d[21] ? d[21] : 1);
+    if (h->last_pfast_pipe) {
+      const double np = (double)count * grid;
+      fprintf(stderr, "[ksim stamps] pipe pods=%lld (%.3f ms, %.3f us/pod) per pod, mean over workgroups: control sweep %.0f "
+              "decide %.0f retries %.2f prologue %.0f | wave1 wait %.0f commit %.0f spec %.0f rank+fix %.0f | wave7 wait %.0f "
+              "commit %.0f spec %.0f rank+fix %.0f\n",
+              (long long)count, ms, 1000.0 * ms / (double)count, d[16] / np, d[17] / np, d[22] / np, d[23] / (double)grid,
+              d[24] / np, d[25] / np, d[26] / np, d[27] / np, d[32] / np, d[33] / np, d[34] / np, d[35] / np);
+    } else {
     fprintf(stderr, "[ksim stamps] pfast workgroup 0, per wave (0 = control) cycles/pod between main barriers busy/wait:");
     for (int w = 0; w < 8; ++w) fprintf(stderr, " %d:%.0f/%.0f", w, d[32 + w] / (double)count, d[40 + w] / (double)count);
     fprintf(stderr, "\n");
@@ -684,6 +722,7 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
             d[8] / (double)count, d[9] / (double)count, d[10] / (double)count, d[11] / (double)count);
     fprintf(stderr, "[ksim stamps] pfast owner (%llu fixes) cycles: select %.0f barrier %.0f fix-publish %.0f commit+barrier+restat %.0f\n",
             (unsigned long long)d[21], d[22] / nf, d[17] / nf, d[18] / nf, d[19] / nf);
+    }
   }
 #endif
   if (st) {
@@ -1252,7 +1291,21 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
   }
   if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port or volume slots overflowed (raise port_slots / vol_slots)");
   if (err & 128) return ksim_rt_svc_refusal(h);
-  if (err & ~1) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
+  if (err & ~1) {
+    if (h->last_pfast_pipe) {  // the pipelined kernel records its first failed spin in dbg[0]
+      uint64_t d0 = 0, dd[8] = {};
+      (void)hipMemcpy(&d0, c.dbg, 8, hipMemcpyDeviceToHost);
+      (void)hipMemcpy(dd, c.dbg + 8, sizeof dd, hipMemcpyDeviceToHost);
+      if (dd[0] || dd[1]) fprintf(stderr, "[ksim pipe] rel %llu X %llu A %016llx B %016llx F %016llx XR %llu\n",
+                                  (unsigned long long)(dd[0] & 0xffffffff), (unsigned long long)(dd[0] >> 32),
+                                  (unsigned long long)dd[1], (unsigned long long)dd[2], (unsigned long long)dd[3],
+                                  (unsigned long long)dd[4]);
+      return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x (pipe: wg %d wave %d site %d pod %d aux %d)", err,
+                       (int)(d0 >> 52), (int)((d0 >> 48) & 15), (int)((d0 >> 40) & 255), (int)(d0 & 0xFFFFFF),
+                       (int)((d0 >> 24) & 0xFFFF));
+    }
+    return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
+  }
   return KSIM_OK;
 }
 

@@ -810,3 +810,41 @@ def test_mixed_features_at_scale(seed, monkeypatch):
     for name, host, msg in want:
         assert got[name] == (host, msg), name
     assert rep.last_node_index == want_lni
+
+
+@pytest.mark.parametrize("seed", [5, 12])
+def test_cached_fast_form_matches_uncached_and_c_oracle(seed, monkeypatch):
+    """The fast kernel's cached form (per (tree class, row) evaluations kept in LDS, only the
+    committed row re-evaluated) and, with KSIM_NO_PCACHE, the uncached form over the same queue
+    driven past saturation: identical placements, FitError histograms, counter and node state,
+    both equal to the C oracle's (least_requested.go:36-53, balanced_resource_allocation.go:39-61,
+    generic_scheduler.go:183-198)."""
+    import cpu_ref
+    from ksim import synth
+    n, m = 9000, 60000
+    r = synth.splitmix64(seed, 2 * n + 2 * m)
+    cpu = synth._pick(r[0:n], [2000, 4000, 8000]) * 1
+    mem = synth._pick(r[n:2 * n], [4 * synth.GI, 8 * synth.GI, 16 * synth.GI])
+    pcpu = synth._pick(r[2 * n:2 * n + m], [100, 250, 500, 1000, 2000])
+    pmem = synth._pick(r[2 * n + m:], [256 * synth.MI, 512 * synth.MI, synth.GI, 2 * synth.GI])
+    names = ["c-%06d" % i for i in range(n)]
+    preds = list(scheduler.DEFAULT_PREDICATES)
+    prios = [("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
+    res = []
+    for env in (None, "1"):
+        if env:
+            monkeypatch.setenv("KSIM_NO_PCACHE", env)
+        cl = synth.resource_cluster(names, cpu, mem, np.full(n, 30, np.int32), pcpu, pmem)
+        g = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_PERSISTENT)
+        o1, r1, _ = g.schedule(0, 25000)
+        o2, r2, _ = g.schedule(25000, m - 25000)
+        res.append((np.concatenate([o1, o2]), np.concatenate([r1, r2]), g.last_node_index, g.node_state()))
+        monkeypatch.delenv("KSIM_NO_PCACHE", raising=False)
+    (o1, r1, c1, s1), (o2, r2, c2, s2) = res
+    assert (o1 < 0).sum() > 1000 and (o1 >= 0).sum() > 1000  # saturated: FitErrors with reasons
+    assert np.array_equal(o1, o2) and np.array_equal(r1, r2) and c1 == c2
+    ref, ref_reasons, ref_state, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, prios), threads=8)
+    assert np.array_equal(o1, ref) and np.array_equal(r1, ref_reasons) and c1 == ref_ctr
+    for k in ("req_cpu", "req_mem", "nz_cpu", "nz_mem", "pod_count"):
+        assert np.array_equal(s1[k], ref_state[k]), k
+        assert np.array_equal(s2[k], ref_state[k]), k
