@@ -284,7 +284,9 @@ int ksim_k8s_open_ex(ksim_k8s_cluster* c, const ksim_config* cfg, const ksim_k8s
  *    selecting none of the pods: the node must carry the pod's nodeSelector values of the labels;
  *  - labelPreference priorities (node_label.go:42-58): MaxPriority x weight when the label's
  *    presence on the node equals `presence`; a serviceAntiAffinity priority with no service selecting
- *    the pods (selector_spreading.go:221-275) is {label, presence = 1, weight}.
+ *    the pods (selector_spreading.go:221-275) is {label, presence = 1, weight}.  Label priorities
+ *    have no ksim_config weight slot, but they ARE prioritizers: a Policy that configures only them
+ *    must still pass cfg.no_priorities = 0 (the library fails with KSIM_E_INVAL otherwise).
  * services_select_pods: the adapter's ServiceLister selects some pod — CheckServiceAffinity and
  * serviceAntiAffinity then need the service-aware tables the Python host builds (KSIM_E_UNSUPPORTED). */
 typedef struct {

@@ -355,6 +355,12 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   // room for the pod's ports if it is assumed (and at least one slot column to test against)
   if ((assume || c.port_slots == 0) && (rc = ensure_port_room(h, pod->port_cnt))) return rc;
   if ((rc = ksim_rt_check_pod(h, *pod, n_ports, n_scalars, scalars, "ksim_schedule_one"))) return rc;
+  // every scratch buffer the launch forms read is allocated (or re-allocated) BEFORE the per-pod
+  // context is copied from the handle's, so the copy never holds a freed or null pointer (round 4:
+  // an illegal access when the wide decision's wmx / wcnt were re-allocated after the copy)
+  const int npt = ksim_rt_pick_npt(c.n);
+  const int grid = (int)((c.n + (int64_t)KSIM_BLOCK * npt - 1) / ((int64_t)KSIM_BLOCK * npt));
+  if ((rc = ksim_rt_ensure_partials(h, grid))) return rc;
   KsimCtx cs;
   if ((rc = stage_pod(h, *pod, ports, scalars, &cs))) return rc;
   cs.collect = 1;  // the FitError histogram is part of the answer
@@ -368,6 +374,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   if (cs.one && one_npt > 0 && one_wg && (!h->have_aff || h->aff_h.n_zone <= 512) && !ksim_rt_launch_tables(h) &&
       cs.one_pod.reserved[0] * cs.one_pod.reserved[1] <= KSIM_MAX_RCLASS) {
     h->res_host[KSIM_RES_NODE] = INT32_MIN;
+    if ((rc = ksim_rt_check_launch_ctx(h, cs, 1, "ksim_schedule_one"))) return rc;
     oc.lap(0);
     hipError_t e1 = ksim_launch_one(&cs, one_npt, h->stream);
     if (e1 != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "one-workgroup launch: %s", hipGetErrorString(e1));
@@ -389,14 +396,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
     if (r[KSIM_RES_ERR]) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", r[KSIM_RES_ERR]);
     return KSIM_OK;
   }
-  const int npt = ksim_rt_pick_npt(c.n);
   cs.chunk = (int64_t)KSIM_BLOCK * npt;
-  const int grid = (int)((c.n + cs.chunk - 1) / cs.chunk);
-  if ((rc = ksim_rt_ensure_partials(h, grid))) return rc;
-  cs.partials = c.partials;
-  cs.pmask = c.pmask;
-  cs.wmx = c.wmx;
-  cs.wcnt = c.wcnt;
   // InterPodAffinity / SelectorSpread reductions (pass A): fused into the scan behind a grid barrier
   // when the grid is co-resident (one launch), else their own launch first
   const bool ipa = ksim_is_aff_host(h, *pod) &&
@@ -411,6 +411,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
     cs.fuse_a = h->one_fuse_ok ? 1 : 0;
   }
   h->res_host[KSIM_RES_NODE] = INT32_MIN;  // still there after the wait: the fused barrier gave up
+  if ((rc = ksim_rt_check_launch_ctx(h, cs, grid, "ksim_schedule_one"))) return rc;
   hipError_t e = hipSuccess;
   oc.lap(0);
   if (ipa && !cs.fuse_a) e = ksim_launch_ipa_pass(&cs, npt, grid, h->stream);

@@ -211,6 +211,10 @@ struct KsimCtx {
   uint64_t one_ports[KSIM_ONE_PORTS];
   ksim_scalar_req one_scalars[KSIM_MAX_SCALAR];
 };
+// KsimCtx is passed BY VALUE as the launch-form kernels' argument: it must stay within the
+// kernel-argument segment (4 KiB on gfx950; a larger struct makes hipLaunchKernel fail with
+// "invalid argument" — the round-4 r4b failure mode while the per-pod fields were being added).
+static_assert(sizeof(KsimCtx) <= 4096 - 64, "KsimCtx exceeds the kernel-argument limit");
 
 // The pod of a launch and its arrays (KsimCtx::one: the kernel arguments).
 __device__ __forceinline__ uint64_t ksim_pod_port(const KsimCtx& c, const ksim_pod& P, int32_t k) {

@@ -44,10 +44,10 @@ extern "C" size_t ksim_pfast_granule_bytes(void);
 extern "C" size_t ksim_shard_xchg_bytes(void);
 extern "C" size_t ksim_shard_lx_offset(void);
 extern "C" size_t ksim_pfast_cache_bytes(int lds_rows, int ncls);
-extern "C" size_t ksim_pipe_lds_bytes(int lds_rows, int ncls);
+extern "C" size_t ksim_pipe_lds_bytes(int lds_rows, int ncls, int nb);
 extern "C" size_t ksim_pipe_word_bytes(int grid, int lds_rows);
 extern "C" hipError_t ksim_launch_pipe(const KsimCtx* c, uint64_t* words, int grid, int lds_rows, const int32_t* tcls,
-                                       const KsimTreeClass* tclass, int ncls, hipStream_t s);
+                                       const KsimTreeClass* tclass, int ncls, int nb, hipStream_t s);
 extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, double* mirror,
                                         const KsimShard* sh, const int32_t* tcls, const KsimTreeClass* tclass, int ncls,
                                         hipStream_t s);
@@ -292,6 +292,7 @@ inline bool ksim_rt_launch_tables(const ksim_handle* h) {
 }
 // Pod classes with more than KSIM_MAX_RCLASS reduce classes (the launch form's wide decision).
 bool wide_k(const ksim_handle* h, int32_t cls);
+int ksim_rt_check_launch_ctx(ksim_handle* h, const KsimCtx& c, int grid, const char* where);
 bool ksim_rt_range_wide(const ksim_handle* h, int64_t first, int64_t count);
 // err bit 128 (a pod read disagreeing service-affinity labels): clear it, KSIM_E_UNSUPPORTED.
 int ksim_rt_svc_refusal(ksim_handle* h);

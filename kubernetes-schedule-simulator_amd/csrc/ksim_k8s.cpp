@@ -372,6 +372,8 @@ extern "C" int ksim_k8s_open_policy(ksim_k8s_cluster* c, const ksim_config* cfg_
         if (q.weight <= 0) fail(KSIM_E_INVAL, "label priority %s: weight must be positive", S(q.label).c_str());
         pol.label_prios.push_back({S(q.label), {q.presence != 0, q.weight}});
       }
+      if (args->n_label_priorities > 0 && cfg.no_priorities)
+        fail(KSIM_E_INVAL, "label priorities are prioritizers: cfg.no_priorities must be 0 when n_label_priorities > 0");
       if (args->services_select_pods && ((pr & KSIM_P_SERVICE_AFFINITY) || args->has_service_anti_affinity))
         fail(KSIM_E_UNSUPPORTED, "CheckServiceAffinity / serviceAntiAffinity with services selecting the pods (the Python "
                                  "host builds their service-aware tables)");
@@ -541,11 +543,11 @@ extern "C" int ksim_k8s_describe(ksim_k8s_cluster* c, ksim_handle* h, const ksim
     std::vector<uint32_t> svc_ok;
     std::vector<uint8_t> svc_need;
     const bool svc = c->pol.on && c->opened_svc;
-    if (svc) policy_svc_ok(c->in, c->ct, c->pol, &svc_ok, &svc_need);
-    if (c->in.classes.items.size() != c0) {  // a new pod class: the class tables grow (a superset)
-      build_class_tab(c->in, &c->ct);
+    const bool grew = c->in.classes.items.size() != c0;
+    if (grew) build_class_tab(c->in, &c->ct);  // a new pod class: the class tables grow (a superset)
+    if (svc) policy_svc_ok(c->in, c->ct, c->pol, &svc_ok, &svc_need);  // once, over the final class table
+    if (grew) {
       const std::vector<int64_t> lab_add = policy_label_add(c->in, c->pol);
-      if (svc) policy_svc_ok(c->in, c->ct, c->pol, &svc_ok, &svc_need);
       if ((e = load_class_tab(c->ct, h, c->w.prefer_avoid, c->w.image_locality, c->pa_use_w, svc ? svc_ok.data() : nullptr,
                               &lab_add)))
         fail(e, "ksim_load_classes: %s", ksim_last_error(h));

@@ -559,6 +559,8 @@ extern "C" int ksim_k8s_cache_create(const ksim_k8s_cache_options* opt, ksim_k8s
         pol.label_prios.push_back({S(a->label_priorities[i].label),
                                    {a->label_priorities[i].presence != 0, a->label_priorities[i].weight}});
       }
+      if (a->n_label_priorities > 0 && cfg.no_priorities)
+        fail(KSIM_E_INVAL, "label priorities are prioritizers: cfg.no_priorities must be 0 when n_label_priorities > 0");
       if (a->services_select_pods && ((pr & KSIM_P_SERVICE_AFFINITY) || a->has_service_anti_affinity))
         fail(KSIM_E_UNSUPPORTED, "CheckServiceAffinity / serviceAntiAffinity with services selecting the pods (the Python "
                                  "host builds their service-aware tables)");

@@ -38,7 +38,10 @@ using namespace kf64;
 
 namespace {
 
-constexpr int BS = 512;
+#ifndef KSIM_PF_BS
+#define KSIM_PF_BS 512  // threads per workgroup (diagnostic variants: 256 = control + 3 row waves)
+#endif
+constexpr int BS = KSIM_PF_BS;
 constexpr int NW = BS / 64;     // waves per workgroup
 constexpr int RW = NW - 1;      // row waves
 constexpr int RT = RW * 64;     // row threads

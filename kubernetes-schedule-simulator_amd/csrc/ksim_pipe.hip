@@ -20,13 +20,22 @@
 //  * The decision of pod q (made redundantly by every workgroup's control wave) reads A(q) of
 //    every workgroup and, for the owner X and rank r of pod q-1's decision, B_X(q) and
 //    F_X(q)[r], and applies the O(1) correction.  Those were published a whole decision earlier,
-//    so the per-pod critical path is one load of already-visible words plus the decision, not a
-//    publish → observe hand-off: two decisions are in flight at once.
+//    so two decisions are in flight at once: pod q's decision waits for the row work that
+//    followed pod q-2's, not for the one that follows pod q-1's.
+//  * The per-pod row work is O(1) statistics plus the candidates' re-evaluations: every
+//    workgroup keeps, per class, a histogram of its rows' cached scores (workgroup-wide and per
+//    64-row segment; scores are small integers, < 64 bins), so A / B are two ballots over one
+//    histogram, a wave finds the candidates above its segment from the segment histograms, and a
+//    commit moves one row's entry in each class's histograms.
+//  * The control wave's decision splits around the owner's words: the pre-decision over every
+//    workgroup but the owner (sums, maxima, prefix counts) runs while B_X / F_X are loading, the
+//    post-decision that adds the owner back is O(1).
 //
 // Roles in a 512-thread workgroup: wave 0 decides (no barrier, no LDS rows); waves 1-7 own the
-// rows: after decision q they commit pod q (owner only: NodeInfo.AddPod on the LDS row and the
-// row's evaluation for every class), publish A/B(q+2), rank the candidate rows of pod q+1 and
-// publish F(q+2).  Waves synchronise through LDS sequence words only.  Every spin is bounded.
+// rows: after decision q they commit pod q (owner only: NodeInfo.AddPod on the LDS row, the
+// row's evaluation for every class, the histograms), publish A/B(q+2) (wave 7), rank the
+// candidate rows of pod q+1 and publish F(q+2).  Waves synchronise through LDS sequence words
+// only.  Every spin is bounded.
 #include <algorithm>
 
 #include "ksim_f64.h"
@@ -127,6 +136,7 @@ struct PpArgs {
   const int32_t* tcls;
   const KsimTreeClass* tclass;
   int32_t ncls;
+  int32_t nb;  // score bins: every map score is in [0, nb), nb <= 64
   uint64_t* counter;
   int64_t* cursor;
   int32_t* out_node;
@@ -145,13 +155,16 @@ struct PRows {
   double *ac, *am, *rc, *rm, *zc, *zm, *yc, *ym;
   int32_t *allowed, *count;
   uint32_t* fl;
-  int16_t* cache;  // [ncls][chunk]
+  int16_t* cache;  // [ncls][chunk]: class k's evaluation of row j as it stands (-1: does not fit)
+  int32_t* hseg;   // [ncls][nseg][nb]: rows of 64-row segment s whose class-k evaluation is score b
+  int32_t* hwg;    // [ncls][nb]: the same over the workgroup's rows
+  int32_t* fitc;   // [ncls]: rows that fit class k
 };
-constexpr int PP_ROW_BYTES = 8 * 8 + 3 * 4;  // 76 + the cache
+constexpr int PP_ROW_BYTES = 8 * 8 + 3 * 4;  // 76, then the cache and the histograms
 
 extern __shared__ __attribute__((aligned(16))) char kp_smem[];
 
-__device__ __forceinline__ PRows pcarve(int rows) {
+__device__ __forceinline__ PRows pcarve(int rows, int ncls, int nseg, int nb) {
   PRows r;
   double* d = reinterpret_cast<double*>(kp_smem);
   r.ac = d; r.am = d + rows; r.rc = d + 2 * rows; r.rm = d + 3 * rows;
@@ -159,7 +172,11 @@ __device__ __forceinline__ PRows pcarve(int rows) {
   int32_t* q = reinterpret_cast<int32_t*>(d + 8 * rows);
   r.allowed = q; r.count = q + rows;
   r.fl = reinterpret_cast<uint32_t*>(q + 2 * rows);
-  r.cache = reinterpret_cast<int16_t*>(q + 3 * rows + (rows & 1));  // 8-byte aligned
+  int32_t* h = q + 3 * rows;
+  r.hseg = h;
+  r.hwg = h + ncls * nseg * nb;
+  r.fitc = r.hwg + ncls * nb;
+  r.cache = reinterpret_cast<int16_t*>(r.fitc + ncls);
   return r;
 }
 
@@ -175,16 +192,11 @@ __device__ __forceinline__ FRow prow(const PRows& R, int32_t j) {
 
 template <int NPT>
 __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
-  __shared__ int32_t s_wst[SR][RW][5];  // per row wave: fit, m1, c1, m2, c2 (pod mod SR)
-  __shared__ int32_t s_wg[SR][5];       // the workgroup's spec statistics of the pod
-  __shared__ int32_t s_wg_seq[SR];      // relative pod index the slot holds (merged)
-  __shared__ int32_t s_arr[SR];         // row waves arrived at the slot's merge
   __shared__ int32_t s_dec[DR][3];      // decision: mode, owner workgroup, rank
   __shared__ int32_t s_dec_seq;         // last decided relative pod
   __shared__ int32_t s_commit_seq;      // last relative pod committed by this workgroup (or -1)
-  __shared__ int32_t s_m1next;          // the owner's max of the next pod after its commit
   __shared__ int32_t s_iter_done;       // row-wave iterations finished (sum over the waves)
-  __shared__ int32_t s_stop;            // a row wave hit its spin bound
+  __shared__ int32_t s_stop;            // a wave hit its spin bound
   __shared__ __attribute__((aligned(16))) ksim_pod s_pod[RING];
   __shared__ int32_t s_pcls[RING];
   __shared__ KsimTreeClass s_tcl[KSIM_TREE_MAX_CLASSES];
@@ -197,7 +209,8 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
   const int64_t lo = (int64_t)me * chunk;
   const int64_t hi = (lo + chunk < a.n) ? lo + chunk : a.n;
   const int32_t nrows = (int32_t)(hi - lo);
-  const PRows R = pcarve((int)chunk);
+  const int NB = a.nb, NSEG = (int)((chunk + 63) / 64), K = a.ncls;
+  const PRows R = pcarve((int)chunk, K, NSEG, NB);
   const EvCfg EC = make_evcfg(a.preds, a.no_prio != 0, a.wl, a.wm, a.wb);
   uint64_t* const Aw = a.words;
   uint64_t* const Bw = a.words + NREP * REP_STRIDE;
@@ -219,7 +232,7 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
     return Fw + ((int64_t)(rel % NSLOT) * G + b) * chunk + r;
   };
 
-  // ---- stage the rows, the class inputs and the first pods; every class's evaluations ----
+  // ---- stage the rows, the class inputs and the first pods ----
   for (int32_t j = tid; j < nrows; j += BS) {
     const int64_t i = lo + j;
     const double ac = (double)a.alloc_cpu[i], am = (double)a.alloc_mem[i];
@@ -230,120 +243,84 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
     R.zc[j] = (double)a.nz_cpu[i]; R.zm[j] = (double)a.nz_mem[i];
     R.allowed[j] = a.allowed_pods[i]; R.count[j] = a.pod_count[i]; R.fl[j] = a.flags[i];
   }
-  for (int k = tid; k < a.ncls; k += BS) s_tcl[k] = a.tclass[k];
+  for (int k = tid; k < K; k += BS) s_tcl[k] = a.tclass[k];
   for (int x = tid; x < 2 * RING_FILL * 8 && first + x / 8 < end; x += BS) {  // pods [first, first + 16)
     const int64_t p = first + x / 8;
     reinterpret_cast<uint4*>(&s_pod[p % RING])[x % 8] = reinterpret_cast<const uint4*>(&a.pods[p])[x % 8];
   }
   for (int x = tid; x < 2 * RING_FILL && first + x < end; x += BS) s_pcls[(first + x) % RING] = a.tcls[first + x];
-  if (tid < SR) { s_wg_seq[tid] = -1000; s_arr[tid] = 0; }
+  for (int x = tid; x < K * NSEG * NB + K * NB + K; x += BS) R.hseg[x] = 0;  // hseg, hwg, fitc are contiguous
   if (tid == 0) { s_dec_seq = -1; s_commit_seq = -1; s_iter_done = 0; s_stop = 0; }
   __syncthreads();
   auto cls_fpod = [&](int k) -> FPod {
     const KsimTreeClass& t = s_tcl[k];
     return FPod{t.rq_c, t.rq_m, t.nz_c, t.nz_m, 0.0, 0.0, t.anyreq, t.be};
   };
-  {
-    const int tot = a.ncls * nrows;
-    for (int idx = tid; idx < tot; idx += BS) {
-      const int k = idx / nrows, j = idx - k * nrows;
-      uint32_t rm;
-      R.cache[k * chunk + j] = (int16_t)feval(EC, cls_fpod(k), prow(R, j), rm);
+  // every (class, owned row) evaluation, and the score histograms
+  for (int idx = tid; idx < K * nrows; idx += BS) {
+    const int k = idx / nrows, j = idx - k * nrows;
+    uint32_t rm;
+    const int32_t e = feval(EC, cls_fpod(k), prow(R, j), rm);
+    R.cache[(int64_t)k * chunk + j] = (int16_t)e;
+    if (e >= 0) {
+      atomicAdd(&R.hseg[(k * NSEG + (j >> 6)) * NB + e], 1);
+      atomicAdd(&R.hwg[k * NB + e], 1);
+      atomicAdd(&R.fitc[k], 1);
     }
   }
   __syncthreads();
 
+  // the workgroup's (fit, max, count at max, second max, its count) for class c, from the
+  // histogram: lane b holds bin b (one LDS read, two ballots)
+  struct Top2 {
+    int32_t f, m1, c1, m2, c2;
+  };
+  auto top2 = [&](int c) -> Top2 {
+    const int32_t h = lane < NB ? R.hwg[c * NB + lane] : 0;
+    const uint64_t nz = __ballot(h > 0);
+    Top2 t;
+    t.f = R.fitc[c];
+    t.m1 = nz ? 63 - __builtin_clzll(nz) : -1;
+    const uint64_t nz2 = t.m1 >= 0 ? (nz & ~(1ull << t.m1)) : 0ull;
+    t.m2 = nz2 ? 63 - __builtin_clzll(nz2) : -1;
+    t.c1 = t.m1 >= 0 ? __builtin_amdgcn_readlane(h, t.m1) : 0;
+    t.c2 = t.m2 >= 0 ? __builtin_amdgcn_readlane(h, t.m2) : 0;
+    return t;
+  };
+  const int PUB = RW;  // the row wave that publishes A / B (the top rows: the fewest candidates)
+  auto publish_ab = [&](int32_t rel) {
+    const Top2 t = top2(s_pcls[(first + rel) % RING]);
+    const uint64_t tg = ptag(rel);
+    if (lane < NREP) gstore(aslot(Aw + lane * REP_STRIDE, rel, me), apack(tg, t.f, t.c1, t.m1));
+    if (lane == NREP) gstore(Bw + (rel % NSLOT) * MAXG + me, bpack(tg, t.m2, t.c2));
+  };
+
   // ---------------- row-wave work ----------------
   const int w = wv;  // row wave 1..RW
-  // spec statistics of pod rel (class c) over the rows as they stand: wave partials, the last
-  // arriving wave merges, stores the workgroup's top two in s_wg and publishes A and B
-  auto spec_publish = [&](int32_t rel) {
-    const int c = s_pcls[(first + rel) % RING];
-    const int16_t* cc = R.cache + (int64_t)c * chunk;
-    int32_t e[NPT];
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int32_t j = k * RT + rt;
-      e[k] = j < nrows ? (int32_t)cc[j] : -1;
-    }
-    int32_t v = -1, nf = 0;
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      nf += __popcll(__ballot(e[k] >= 0));
-      v = e[k] > v ? e[k] : v;
-    }
-    const int32_t m1 = ksimw::max_i32(v);
-    int32_t v2 = -1;
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) v2 = (e[k] < m1 && e[k] > v2) ? e[k] : v2;
-    const int32_t m2 = ksimw::max_i32(v2);
-    int32_t c1 = 0, c2 = 0;
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      c1 += m1 < 0 ? 0 : __popcll(__ballot(e[k] == m1));
-      c2 += m2 < 0 ? 0 : __popcll(__ballot(e[k] == m2));
-    }
-    const int sl = rel % SR;
-    if (lane == 0) {
-      s_wst[sl][w - 1][0] = nf; s_wst[sl][w - 1][1] = m1; s_wst[sl][w - 1][2] = c1;
-      s_wst[sl][w - 1][3] = m2; s_wst[sl][w - 1][4] = c2;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    int32_t old = 0;
-    if (lane == 0) old = atomicAdd(&s_arr[sl], 1);
-    old = __builtin_amdgcn_readfirstlane(old);
-    if (old + 1 == RW) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-      const bool in = lane < RW;
-      const int x = in ? lane : 0;
-      const int32_t f = in ? s_wst[sl][x][0] : 0;
-      const int32_t a1 = s_wst[sl][x][1], n1 = in ? s_wst[sl][x][2] : 0;
-      const int32_t a2 = s_wst[sl][x][3], n2 = in ? s_wst[sl][x][4] : 0;
-      const int32_t tf = ksimw::sum_i32(f);
-      const int32_t tm1 = ksimw::max_i32(n1 ? a1 : -1);
-      const int32_t tc1 = ksimw::sum_i32((n1 && a1 == tm1) ? n1 : 0);
-      const int32_t tm2 = ksimw::max_i32(n1 && a1 < tm1 ? a1 : (n2 ? a2 : -1));
-      int32_t tc2 = ksimw::sum_i32(((n1 && a1 == tm2) ? n1 : 0) + ((n2 && a2 == tm2) ? n2 : 0));
-      if (tm2 < 0) tc2 = 0;
-      if (lane == 0) s_arr[sl] = 0;  // before the publish: the slot's next use follows it
-      const uint64_t tg = ptag(rel);
-      if (lane < NREP) gstore(aslot(Aw + lane * REP_STRIDE, rel, me), apack(tg, tf, tc1, tm1));
-      if (lane == NREP) gstore(Bw + (rel % NSLOT) * MAXG + me, bpack(tg, tm2, tc2));
-      if (lane == 0) {
-        s_wg[sl][0] = tf; s_wg[sl][1] = tm1; s_wg[sl][2] = tc1; s_wg[sl][3] = tm2; s_wg[sl][4] = tc2;
-        seq_release(&s_wg_seq[sl], rel);
-      }
-    }
-  };
-  // wait until the merged statistics of pod rel are in s_wg (false: spin bound)
-  auto wait_wg = [&](int32_t rel) -> bool {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (seq_acquire(&s_wg_seq[rel % SR]) != rel) {
-      if (past(t0)) { note(1, rel, seq_acquire(&s_wg_seq[rel % SR])); return false; }
-      __builtin_amdgcn_s_sleep(1);
-    }
-    return true;
-  };
-  // candidate rows of pod rel1 (rows at this workgroup's maximum M1, ranked from the top) and,
-  // for each, pod rel1 + 1's evaluation before / after pod rel1 is committed to it → F
+  // candidate rows of pod rel1 (this workgroup's rows at its maximum M1 of the pod's class,
+  // ranked from the top) and, for each, pod rel1 + 1's evaluation before / after pod rel1 is
+  // committed to it → F(rel1 + 1)
   uint64_t tmask[NPT];  // this wave's candidate rows of the pod being decided next, per segment
   int32_t tabove[NPT];  // candidates in the segments above each
-  auto rank_and_fix = [&](int32_t rel1, int32_t M1) {
+  auto rank_and_fix = [&](int32_t rel1) {
     const int c1 = s_pcls[(first + rel1) % RING];
+    const int32_t h = lane < NB ? R.hwg[c1 * NB + lane] : 0;
+    const uint64_t nz = __ballot(h > 0);
+    const int32_t M1 = nz ? 63 - __builtin_clzll(nz) : -1;
     const int16_t* cc = R.cache + (int64_t)c1 * chunk;
+    // candidates per segment (lane = segment), suffix sums give the segments above
+    const int32_t sc = (M1 >= 0 && lane < NSEG) ? R.hseg[(c1 * NSEG + lane) * NB + M1] : 0;
+    const int32_t incl = ksimw::prefix_incl_i32(sc);
+    const int32_t total = __builtin_amdgcn_readlane(incl, 63);
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int32_t j = k * RT + rt;
       tmask[k] = __ballot(M1 >= 0 && j < nrows && (int32_t)cc[j] == M1);
-      int32_t n = 0;
-      if (M1 >= 0)
-        for (int32_t x = k * RT + w * 64 + lane; x < nrows; x += 64) n += ((int32_t)cc[x] == M1) ? 1 : 0;
-      tabove[k] = ksimw::sum_i32(n);
+      tabove[k] = total - __builtin_amdgcn_readlane(incl, k * RW + w - 1);
     }
     const int32_t rel2 = rel1 + 1;
     if (rel2 >= npods) return;
-    const ksim_pod& P1 = s_pod[(first + rel1) % RING];
-    const FPod F1 = load_fpod(P1);
+    const FPod F1 = load_fpod(s_pod[(first + rel1) % RING]);
     const FPod F2 = load_fpod(s_pod[(first + rel2) % RING]);
     const int16_t* c2 = R.cache + (int64_t)s_pcls[(first + rel2) % RING] * chunk;
     const uint64_t tg = ptag(rel2);
@@ -362,26 +339,28 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
   };
 
   int64_t stop_at = end;
+  uint64_t counter = *a.counter;  // replicated genericScheduler.lastNodeIndex (control wave)
 #ifdef KSIM_STAMPS
   uint64_t st[8] = {};  // per wave: phase cycles summed over the pods (flushed at the end)
   uint64_t tp = __builtin_amdgcn_s_memtime();
-#define PSTAMP(k)                                        \
-  do {                                                   \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime();    \
-    st[k] += t_ - tp;                                    \
-    tp = t_;                                             \
+#define PSTAMP(k)                                     \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    st[k] += t_ - tp;                                 \
+    tp = t_;                                          \
   } while (0)
 #else
 #define PSTAMP(k) do { } while (0)
 #endif
-  uint64_t counter = *a.counter;  // replicated genericScheduler.lastNodeIndex (control wave)
 
   if (wv > 0) {
     // ---- prologue: A/B of the first two pods, candidates of the first, F of the second ----
-    spec_publish(0);
-    bool ok = wait_wg(0);
-    if (npods > 1) spec_publish(1);
-    if (ok) rank_and_fix(0, s_wg[0][1]);
+    if (w == PUB) {
+      publish_ab(0);
+      if (npods > 1) publish_ab(1);
+    }
+    rank_and_fix(0);
+    bool ok = true;
     uint4 ring_next = make_uint4(0, 0, 0, 0);  // wave 1: descriptors of the next refill
     int32_t ring_next_cl = 0;
     auto ring_load = [&](int64_t p0, uint4& v, int32_t& cl) {
@@ -396,10 +375,10 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
     };
     if (wv == 1) ring_load(first + 2 * RING_FILL, ring_next, ring_next_cl);
     if (lane == 0) atomicAdd(&s_iter_done, 1);  // the prologue counts as iteration -1
+    PSTAMP(7);
 
     // ---- row iterations: after decision rel ----
-    PSTAMP(7);
-    for (int32_t rel = 0; ok && rel < npods; ++rel) {
+    for (int32_t rel = 0; rel < npods; ++rel) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       while (seq_acquire(&s_dec_seq) < rel) {
         if (past(t0) || seq_acquire(&s_stop)) { note(2, rel, seq_acquire(&s_dec_seq)); ok = false; break; }
@@ -432,8 +411,6 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
           if (lane == 0 && nr) atomicAdd(&a.out_reasons[pod * KSIM_NREASONS + r], nr);
         }
       }
-      const bool has1 = rel + 1 < npods;
-      int32_t M1 = -1;  // this workgroup's maximum of pod rel + 1
       if (mode == 2 && X == me) {
         // ---- owner: the rk-th candidate from the top; commit, re-evaluate its row ----
         int32_t seg = -1, bit = -1;
@@ -456,30 +433,28 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
             __builtin_amdgcn_s_sleep(1);
           }
           const FRow r2 = plus(prow(R, j), load_fpod(s_pod[pod % RING]));
-          int32_t eo = -1, en = -1;
-          if (has1) {
-            const int c1 = s_pcls[(pod + 1) % RING];
-            eo = R.cache[(int64_t)c1 * chunk + j];
-          }
-          if (lane < a.ncls) {
+          if (lane < K) {  // the row's evaluation for every class, and the histograms
             uint32_t m;
-            R.cache[(int64_t)lane * chunk + j] = (int16_t)feval(EC, cls_fpod(lane), r2, m);
-          }
-          if (has1) {
-            const int c1 = s_pcls[(pod + 1) % RING];
-            uint32_t m;
-            en = feval(EC, cls_fpod(c1), r2, m);
-            ok = ok && wait_wg(rel + 1);
-            const int sl = (rel + 1) % SR;
-            const Stat3 s = fix_stats(s_wg[sl][0], s_wg[sl][1], s_wg[sl][2], s_wg[sl][3], s_wg[sl][4], eo, en);
-            if (lane == 0) s_m1next = s.m;
+            const int32_t eo = R.cache[(int64_t)lane * chunk + j];
+            const int32_t en = feval(EC, cls_fpod(lane), r2, m);
+            R.cache[(int64_t)lane * chunk + j] = (int16_t)en;
+            const int sg = j >> 6;
+            if (eo >= 0) {
+              R.hseg[(lane * NSEG + sg) * NB + eo] -= 1;
+              R.hwg[lane * NB + eo] -= 1;
+            }
+            if (en >= 0) {
+              R.hseg[(lane * NSEG + sg) * NB + en] += 1;
+              R.hwg[lane * NB + en] += 1;
+            }
+            R.fitc[lane] += (en >= 0 ? 1 : 0) - (eo >= 0 ? 1 : 0);
           }
           if (lane == 0) {
             R.rc[j] = r2.rc; R.rm[j] = r2.rm; R.zc[j] = r2.zc; R.zm[j] = r2.zm; R.count[j] = r2.count;
             a.out_node[pod] = (int32_t)(lo + j);
             if (r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM) atomicOr(a.err, 8);
-            seq_release(&s_commit_seq, rel);
           }
+          seq_release(&s_commit_seq, rel);
         } else {
           const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
           while (seq_acquire(&s_commit_seq) < rel) {
@@ -487,116 +462,149 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
             __builtin_amdgcn_s_sleep(1);
           }
         }
-        if (has1) M1 = __builtin_amdgcn_readfirstlane(s_m1next);
-      } else if (has1) {
-        ok = ok && wait_wg(rel + 1);
-        M1 = s_wg[(rel + 1) % SR][1];
       }
       if (!ok) break;
       PSTAMP(1);  // reasons, commit / waiting for it
-      if (rel + 2 < npods) spec_publish(rel + 2);
+      if (w == PUB && rel + 2 < npods) publish_ab(rel + 2);
       PSTAMP(2);
-      if (has1) rank_and_fix(rel + 1, M1);
+      if (rel + 1 < npods) rank_and_fix(rel + 1);
       PSTAMP(3);
       if (lane == 0) atomicAdd(&s_iter_done, 1);
     }
     if (!ok && lane == 0) { atomicOr(a.err, 2); atomicExch(&s_stop, 1); }
   } else {
     // ---------------- control wave: decide every pod ----------------
-    int X = -1;       // owner workgroup of the previous pod's node (-1: none)
-    int32_t XR = 0;   // ... and the rank it took
+    // A(rel) of every workgroup is in g[] (lane l: workgroups 4l .. 4l+3); after each decision the
+    // loads of A(rel + 1) and of the owner's B / F words go out together, the pre-decision over
+    // every workgroup but the owner overlaps the owner's words, then an O(1) post-decision.
+    int X = -1;      // owner workgroup of the previous pod's node (-1: none)
+    int32_t XR = 0;  // ... and the rank it took
     const uint64_t* my_rep = Aw + (me % NREP) * REP_STRIDE;
-    PSTAMP(7);
-    uint64_t spins = 0;
-    for (int32_t rel = 0; rel < npods; ++rel) {
+    uint64_t g[MAXB];
+    auto load_a = [&](int32_t rel) -> bool {  // spin until A(rel) of every workgroup is here
       const uint64_t tag = ptag(rel);
-      uint64_t g[MAXB], bx = 0, fx = 0;
-      bool ok = false;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
 #pragma unroll
         for (int j = 0; j < MAXB; ++j) g[j] = gload(my_rep + (rel % NSLOT) * MAXG + j * 64 + lane);
-        if (X >= 0) {
-          bx = gload(Bw + (rel % NSLOT) * MAXG + X);
-          fx = gload(fslot(rel, X, XR));
-        }
-        bool mine = X < 0 || (gtag(bx) == tag && gtag(fx) == tag);
+        bool mine = true;
 #pragma unroll
-        for (int j = 0; j < MAXB; ++j) {
-          const int b = lane * MAXB + j;
-          mine &= (b >= G) || gtag(g[j]) == tag;
-        }
-        if (__all(mine)) { ok = true; break; }
-#ifdef KSIM_STAMPS
-        spins += 1;
-#endif
+        for (int j = 0; j < MAXB; ++j) mine &= (lane * MAXB + j >= G) || gtag(g[j]) == tag;
+        if (__all(mine)) return true;
         if (past(t0) || seq_acquire(&s_stop)) {
           int32_t miss = -1;
 #pragma unroll
           for (int j = 0; j < MAXB; ++j)
             if (lane * MAXB + j < G && gtag(g[j]) != tag) miss = lane * MAXB + j;
           const uint64_t mb = __ballot(miss >= 0);
-          const int32_t m0 = mb ? __builtin_amdgcn_readlane(miss, __builtin_ctzll(mb)) : (X >= 0 ? 1000 + X : 999);
-          note(5, rel, m0);
-          break;
+          note(5, rel, mb ? __builtin_amdgcn_readlane(miss, __builtin_ctzll(mb)) : 999);
+          return false;
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      PSTAMP(0);  // sweep
-      bool stop_any = false;
-      if (ok && X >= 0) {  // the previous owner's statistics with its committed row corrected
-        const int lx = X / MAXB, jx = X % MAXB;
-        const uint64_t ax = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)g[jx], lx) |
-                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(g[jx] >> 32), lx) << 32);
-        const Stat3 s = fix_stats(gfit(ax), gscore(ax), gcnt(ax), bm2(bx), bc2(bx), feo(fx), fen(fx));
-        stop_any = fstop(fx);
-        const int64_t xr = a.n - (int64_t)X * chunk;
-        if (s.c > (xr < chunk ? xr : chunk) && lane == 0 && me == 0) {  // diagnostic: the corrected count exceeds the rows
-          a.dbg[8] = (uint64_t)rel | ((uint64_t)X << 32);
-          a.dbg[9] = ax; a.dbg[10] = bx; a.dbg[11] = fx; a.dbg[12] = (uint64_t)XR;
-        }
-#pragma unroll
-        for (int j = 0; j < MAXB; ++j) g[j] = (lane * MAXB + j == X) ? apack(tag, s.f, s.c, s.m) : g[j];
+    };
+    PSTAMP(7);
+    uint64_t spins = 0;
+    bool ok = load_a(0);
+    for (int32_t rel = 0; rel < npods; ++rel) {
+      const uint64_t tag = ptag(rel);
+      // the owner's words (address known since the last decision), in flight during the pre-decision
+      uint64_t bx = 0, fx = 0;
+      if (ok && X >= 0) {
+        bx = gload(Bw + (rel % NSLOT) * MAXG + X);
+        fx = gload(fslot(rel, X, XR));
       }
-      // findNodesThatFit count, max score, selectHost (generic_scheduler.go:136-198)
+      // ---- pre-decision over every workgroup but X ----
+      int32_t cnt[MAXB];
       int32_t f = 0, lm = -1;
 #pragma unroll
       for (int j = 0; j < MAXB; ++j) {
-        g[j] = (lane * MAXB + j < G) ? g[j] : 0;
-        f += gfit(g[j]);
-        lm = (gcnt(g[j]) && gscore(g[j]) > lm) ? gscore(g[j]) : lm;
+        const int b = lane * MAXB + j;
+        const bool v = b < G && b != X;
+        f += v ? gfit(g[j]) : 0;
+        lm = (v && gcnt(g[j]) && gscore(g[j]) > lm) ? gscore(g[j]) : lm;
       }
-      const int32_t F = ksimw::sum_i32(f);
-      const int32_t M = ksimw::max_i32(lm);
-      int32_t bm[MAXB], tot = 0;
+      const int32_t Fs = ksimw::sum_i32(f);
+      const int32_t Ms = ksimw::max_i32(lm);
+      int32_t tot = 0;
 #pragma unroll
       for (int j = 0; j < MAXB; ++j) {
-        bm[j] = (gcnt(g[j]) && gscore(g[j]) == M) ? gcnt(g[j]) : 0;
-        tot += bm[j];
+        const int b = lane * MAXB + j;
+        cnt[j] = (b < G && b != X && gcnt(g[j]) && gscore(g[j]) == Ms) ? gcnt(g[j]) : 0;
+        tot += cnt[j];
       }
       const int32_t pre = ksimw::prefix_incl_i32(tot);
-      const uint32_t C = (uint32_t)__builtin_amdgcn_readlane(pre, 63);
-      const uint32_t Cs = C ? C : 1u;
-      const int64_t ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)Cs) : (int64_t)((uint32_t)counter % Cs);
-      const int64_t above = (int64_t)C - pre;  // matches in workgroups of higher lanes
-      const bool hit = tot > 0 && ix >= above && ix < above + tot;
-      int32_t found = -1;
-      int64_t rr = ix - above;
+      const int32_t Cs = __builtin_amdgcn_readlane(pre, 63);
+      const int32_t abv = Cs - pre;  // matches in workgroups of higher lanes
+      int32_t aboveX = 0;            // matches (at Ms) in workgroups above X
+      uint64_t ax = 0;
+      if (X >= 0) {
+        const int lx = X / MAXB, jx = X % MAXB;
+        int32_t part = 0;
 #pragma unroll
-      for (int j = MAXB - 1; j >= 0; --j) {
-        const bool here = found < 0 && rr < bm[j];
-        found = here ? lane * MAXB + j : found;
-        rr = (found < 0) ? rr - bm[j] : rr;
+        for (int j = 0; j < MAXB; ++j) part += j > jx ? cnt[j] : 0;
+        aboveX = __builtin_amdgcn_readlane(abv + part, lx);
+        ax = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)g[jx], lx) |
+             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(g[jx] >> 32), lx) << 32);
       }
-      const uint64_t hb = __ballot(hit);
-      const int src = __builtin_ffsll((long long)hb) - 1;
-      const int blk = hb ? __builtin_amdgcn_readlane(found, src) : -1;
-      const int rank = hb ? __builtin_amdgcn_readlane((int32_t)rr, src) : 0;
+      PSTAMP(2);  // pre-decision
+      // ---- the owner's corrected statistics ----
+      bool stop_any = false;
+      int32_t fX = 0, cX = 0, mX = -1;
+      if (ok && X >= 0) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        while (!(gtag(bx) == tag && gtag(fx) == tag)) {
+          if (past(t0) || seq_acquire(&s_stop)) { note(6, rel, X); ok = false; break; }
+#ifdef KSIM_STAMPS
+          spins += 1;
+#endif
+          __builtin_amdgcn_s_sleep(1);
+          bx = gload(Bw + (rel % NSLOT) * MAXG + X);
+          fx = gload(fslot(rel, X, XR));
+        }
+        const Stat3 s = fix_stats(gfit(ax), gscore(ax), gcnt(ax), bm2(bx), bc2(bx), feo(fx), fen(fx));
+        fX = s.f; cX = s.c; mX = s.m;
+        stop_any = fstop(fx);
+      }
+      PSTAMP(0);  // waiting for the owner's words
+      // ---- post-decision: findNodesThatFit count, max score, selectHost (generic_scheduler.go:136-198) ----
+      const int32_t F = Fs + fX;
+      const bool xtop = cX > 0 && (Cs == 0 || mX > Ms);   // X alone holds the maximum
+      const bool xeq = cX > 0 && Cs > 0 && mX == Ms;       // X shares it
+      const uint32_t C = (uint32_t)(xtop ? cX : Cs + (xeq ? cX : 0));
+      const uint32_t Cd = C ? C : 1u;
+      const int64_t ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)Cd) : (int64_t)((uint32_t)counter % Cd);
+      int blk = -1, rank = 0;
+      int64_t t = ix;  // index among the other workgroups' matches, when X does not take it
+      if (xtop) {
+        blk = X; rank = (int)ix;
+      } else if (xeq && ix >= aboveX && ix < aboveX + cX) {
+        blk = X; rank = (int)(ix - aboveX);
+      } else if (xeq && ix >= aboveX + cX) {
+        t = ix - cX;
+      }
+      if (blk < 0 && C > 0) {
+        const bool hit = tot > 0 && t >= abv && t < abv + tot;
+        int32_t found = -1;
+        int64_t rr = t - abv;
+#pragma unroll
+        for (int j = MAXB - 1; j >= 0; --j) {
+          const bool here = found < 0 && rr < cnt[j];
+          found = here ? lane * MAXB + j : found;
+          rr = (found < 0) ? rr - cnt[j] : rr;
+        }
+        const uint64_t hb = __ballot(hit);
+        if (hb) {
+          const int src = __builtin_ctzll(hb);
+          blk = __builtin_amdgcn_readlane(found, src);
+          rank = __builtin_amdgcn_readlane((int32_t)rr, src);
+        }
+      }
       int mode;
       if (!ok) mode = -1;
       else if (stop_any) mode = -2;  // the previous commit left the exact float64 range
       else if (F == 0) mode = 0;
-      else mode = (hb && blk >= 0) ? 2 : -1;
+      else mode = blk >= 0 ? 2 : -1;
       if (mode == 2 && F > 1) counter += 1;  // generic_scheduler.go:192-195
       if (lane == 0) {
         if (mode == -1) atomicOr(a.err, ok ? 2 : 4);
@@ -604,13 +612,15 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
         s_dec[rel % DR][0] = mode; s_dec[rel % DR][1] = blk; s_dec[rel % DR][2] = rank;
         seq_release(&s_dec_seq, rel);
       }
+      PSTAMP(1);  // post-decision
       if (mode < 0) {
         if (mode == -2) stop_at = first + rel;
         break;
       }
-      PSTAMP(1);  // decide
       X = mode == 2 ? blk : -1;
       XR = rank;
+      if (rel + 1 < npods) ok = load_a(rel + 1);
+      PSTAMP(3);  // waiting for the next pod's A words
     }
 #ifdef KSIM_STAMPS
     st[6] = spins;
@@ -622,6 +632,7 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
     for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&a.dbg[base + k], st[k]);
   }
 #endif
+
   // ---- the table is authoritative in HBM between calls: write the owned rows back ----
   __syncthreads();
   for (int32_t j = tid; j < nrows; j += BS) {
@@ -639,10 +650,12 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
 // ---------------------------------------------------------------------------------------
 static constexpr int PP_LDS_BUDGET = 150 * 1024;
 
-// LDS bytes of the pipelined kernel for lds_rows rows and ncls classes (0: does not fit)
-extern "C" size_t ksim_pipe_lds_bytes(int lds_rows, int ncls) {
-  if (ncls <= 0 || ncls > KSIM_TREE_MAX_CLASSES || lds_rows <= 0 || lds_rows > 4 * RT) return 0;
-  const size_t b = (size_t)lds_rows * PP_ROW_BYTES + 8 + (size_t)ncls * lds_rows * 2;
+// LDS bytes of the pipelined kernel for lds_rows rows, ncls classes and nb score bins (0: does not fit)
+extern "C" size_t ksim_pipe_lds_bytes(int lds_rows, int ncls, int nb) {
+  if (ncls <= 0 || ncls > KSIM_TREE_MAX_CLASSES || lds_rows <= 0 || lds_rows > 4 * RT || nb <= 0 || nb > 64) return 0;
+  const size_t nseg = ((size_t)lds_rows + 63) / 64;
+  const size_t b = (size_t)lds_rows * PP_ROW_BYTES + 4 * ((size_t)ncls * nseg * nb + (size_t)ncls * nb + ncls) +
+                   (size_t)ncls * lds_rows * 2;
   return b <= (size_t)PP_LDS_BUDGET ? ((b + 15) & ~(size_t)15) : 0;
 }
 
@@ -652,14 +665,14 @@ extern "C" size_t ksim_pipe_word_bytes(int grid, int lds_rows) {
 }
 
 extern "C" hipError_t ksim_launch_pipe(const KsimCtx* c, uint64_t* words, int grid, int lds_rows, const int32_t* tcls,
-                                       const KsimTreeClass* tclass, int ncls, hipStream_t s) {
-  const size_t lds = ksim_pipe_lds_bytes(lds_rows, ncls);
+                                       const KsimTreeClass* tclass, int ncls, int nb, hipStream_t s) {
+  const size_t lds = ksim_pipe_lds_bytes(lds_rows, ncls, nb);
   if (!lds || grid <= 0 || grid > MAXG || (int64_t)grid * lds_rows < c->n) return hipErrorInvalidValue;
   PpArgs a;
   a.n = c->n; a.chunk = lds_rows; a.first = c->first; a.end = c->end;
   a.alloc_cpu = c->alloc_cpu; a.alloc_mem = c->alloc_mem; a.allowed_pods = c->allowed_pods; a.flags = c->flags;
   a.req_cpu = c->req_cpu; a.req_mem = c->req_mem; a.nz_cpu = c->nz_cpu; a.nz_mem = c->nz_mem;
-  a.pod_count = c->pod_count; a.pods = c->pods; a.tcls = tcls; a.tclass = tclass; a.ncls = ncls;
+  a.pod_count = c->pod_count; a.pods = c->pods; a.tcls = tcls; a.tclass = tclass; a.ncls = ncls; a.nb = nb;
   a.counter = c->counter; a.cursor = c->cursor;
   a.out_node = c->out_node; a.out_reasons = c->out_reasons; a.err = c->err; a.dbg = c->dbg; a.words = words;
   a.preds = c->preds; a.no_prio = c->no_prio; a.collect = c->collect;

@@ -517,6 +517,20 @@ int ksim_rt_ensure_partials(ksim_handle* h, int grid) {
   return KSIM_OK;
 }
 
+// Before a launch-form kernel runs on a context: every scratch pointer it may read or write is
+// set and sized for the grid (a stale copy of the handle's context would fault on the device).
+int ksim_rt_check_launch_ctx(ksim_handle* h, const KsimCtx& c, int grid, const char* where) {
+  const void* need[] = {c.partials, c.pmask, c.wmx, c.wcnt, c.ticket, c.err, c.counter, c.cursor, c.pods, c.out_node,
+                        c.out_reasons, c.alloc_cpu, c.req_cpu, c.pod_count, c.flags};
+  for (const void* p : need)
+    if (!p) return ksim_fail(h, KSIM_E_DEVICE, "%s: launch context has an unset scratch / table pointer", where);
+  if (grid > h->part_cap) return ksim_fail(h, KSIM_E_DEVICE, "%s: grid %d beyond the partials (%lld)", where, grid,
+                                           (long long)h->part_cap);
+  if (c.partials != h->ctx.partials || c.pmask != h->ctx.pmask || c.wmx != h->ctx.wmx || c.wcnt != h->ctx.wcnt)
+    return ksim_fail(h, KSIM_E_DEVICE, "%s: launch context holds stale scratch pointers", where);
+  return KSIM_OK;
+}
+
 static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   KsimCtx& c = h->ctx;
   const int npt = ksim_rt_pick_npt(c.n);
@@ -662,8 +676,11 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
   h->last_pfast_cache = ncls > 0;
   // one device: the two-deep pipelined form of the cached kernel (ksim_pipe.hip), KSIM_PIPE=1 (experimental)
   const char* pe = getenv("KSIM_PIPE");
-  const bool pipe = ncls > 0 && h->shard.world == 1 && pe && pe[0] == '1' && ksim_pipe_lds_bytes(lds_rows, ncls) &&
-                    (int64_t)grid * lds_rows >= c.n;
+  int nb = 1;  // the pipelined kernel's score bins (every map score < 64)
+  if (!c.no_prio)
+    nb = (int)(10 * (c.w[KSIM_W_LEAST_REQUESTED] + c.w[KSIM_W_MOST_REQUESTED] + c.w[KSIM_W_BALANCED])) + 1;
+  const bool pipe = ncls > 0 && h->shard.world == 1 && pe && pe[0] == '1' && nb <= 64 &&
+                    ksim_pipe_lds_bytes(lds_rows, ncls, nb) && (int64_t)grid * lds_rows >= c.n;
   h->last_pfast_pipe = pipe;
   if (pipe) {
     const size_t wb = ksim_pipe_word_bytes(grid, lds_rows);
@@ -681,7 +698,7 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
     HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
   }
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipError_t e = pipe ? ksim_launch_pipe(&c, h->pipe_words, grid, lds_rows, h->tcls, h->tclass, ncls, h->stream)
+  hipError_t e = pipe ? ksim_launch_pipe(&c, h->pipe_words, grid, lds_rows, h->tcls, h->tclass, ncls, nb, h->stream)
                       : ksim_launch_pfast(&c, h->granules, grid, lds_rows, stream ? h->mirror : nullptr, &h->shard,
                                           h->tcls, h->tclass, ncls, h->stream);
   if (e == hipErrorCooperativeLaunchTooLarge) {
@@ -705,10 +722,11 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
     const double nf = (double)(d[21] ? d[21] : 1);
     if (h->last_pfast_pipe) {
       const double np = (double)count * grid;
-      fprintf(stderr, "[ksim stamps] pipe pods=%lld (%.3f ms, %.3f us/pod) per pod, mean over workgroups: control sweep %.0f "
-              "decide %.0f retries %.2f prologue %.0f | wave1 wait %.0f commit %.0f spec %.0f rank+fix %.0f | wave7 wait %.0f "
-              "commit %.0f spec %.0f rank+fix %.0f\n",
-              (long long)count, ms, 1000.0 * ms / (double)count, d[16] / np, d[17] / np, d[22] / np, d[23] / (double)grid,
+      fprintf(stderr, "[ksim stamps] pipe pods=%lld (%.3f ms, %.3f us/pod) per pod, mean over workgroups: control pre %.0f "
+              "owner-wait %.0f post %.0f A-wait %.0f owner-retries %.2f prologue %.0f | wave1 wait %.0f commit %.0f spec %.0f "
+              "rank+fix %.0f | wave7 wait %.0f commit %.0f spec %.0f rank+fix %.0f\n",
+              (long long)count, ms, 1000.0 * ms / (double)count, d[18] / np, d[16] / np, d[17] / np, d[19] / np, d[22] / np,
+              d[23] / (double)grid,
               d[24] / np, d[25] / np, d[26] / np, d[27] / np, d[32] / np, d[33] / np, d[34] / np, d[35] / np);
     } else {
     fprintf(stderr, "[ksim stamps] pfast workgroup 0, per wave (0 = control) cycles/pod between main barriers busy/wait:");
@@ -1237,9 +1255,19 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
       if (ksim_rt_launch_tables(h) || (h->have_aff && h->aff_h.n_zone > KSIM_PX_ZONES))
         return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling with the auxiliary priority, the service-affinity "
                                            "lender check or more than %d spread zones", KSIM_PX_ZONES);
-      for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED})
-        if (c.w[k] > ((int64_t)1 << 30))
-          return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling: a map-priority weight above 2^30");
+      // per-node scores travel as 40-bit biased words (KSIM_LX_BIAS = 2^39): every weight that
+      // reaches a node's score is bounded, and so is their sum x MaxPriority
+      {
+        int64_t sw = 0;
+        for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED, KSIM_W_INTERPOD_AFFINITY,
+                      KSIM_W_SELECTOR_SPREAD}) {
+          if (c.w[k] > ((int64_t)1 << 30))
+            return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling: a priority weight above 2^30");
+          sw += c.w[k] * 10;
+        }
+        if (sw >= ((int64_t)1 << 39))
+          return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling: weighted scores beyond the 40-bit exchange word");
+      }
       c.sh_world = h->shard.world;
       c.sh_rank = h->shard.rank;
       c.sh_base = h->shard.node_base;

@@ -557,7 +557,11 @@ class K8sCache:
         names = {n for n, _ in priorities}
         custom = dict(custom_priorities or {})
         self._services_only = "ServiceSpreadingPriority" in names and "SelectorSpreadPriority" not in names
-        cfg = scheduler.make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence],
+        # the reference fails on CheckNodeLabelPresence without its labelsPresence argument (as plan()
+        # refuses it); with an empty labels list the predicate passes every node and is dropped
+        if "CheckNodeLabelPresence" in self.predicates and label_presence is None:
+            raise abi.KsimUnsupported(abi.E_UNSUPPORTED, "CheckNodeLabelPresence needs its labelsPresence argument")
+        cfg = scheduler.make_config([k for k in predicates if k != "CheckNodeLabelPresence" or label_presence[0]],
                                     [(n, x) for n, x in priorities if n not in custom], device, mode, True,
                                     last_node_index, spread=self.spread is not None, configured=list(priorities))
         w = lambda key: sum(int(x) for n, x in priorities if n == key)

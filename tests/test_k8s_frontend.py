@@ -181,3 +181,13 @@ def test_policy_arguments_refused_with_services():
     cfg = scheduler.make_config(["GeneralPredicates", "CheckNodeLabelPresence"], [("LeastRequestedPriority", 1)])
     with pytest.raises(abi.KsimUnsupported):
         fe.open(cfg)   # the predicate's arguments only come through ksim_k8s_open_policy
+
+
+def test_cache_refuses_label_presence_without_argument():
+    """CheckNodeLabelPresence without its Policy labelsPresence argument: the reference fails on it
+    (predicates/predicates.go NewNodeLabelPredicate needs the labels), so the C++ scheduler cache
+    refuses it as plan() does instead of scheduling without the predicate."""
+    from ksim import scheduler
+    preds = list(scheduler.DEFAULT_PREDICATES) + ["CheckNodeLabelPresence"]
+    with pytest.raises(abi.KsimUnsupported, match="labelsPresence"):
+        frontend.K8sCache(preds, [("LeastRequestedPriority", 1)])
