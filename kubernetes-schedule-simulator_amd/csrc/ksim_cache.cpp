@@ -397,6 +397,53 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
     return KSIM_OK;
   }
   cs.chunk = (int64_t)KSIM_BLOCK * npt;
+  // the pick kernel (<= 64 blocks, co-resident): one tagged-record exchange per reduction and a
+  // redundant decision in every block instead of the scan's last-block round trips.  Not for the
+  // auxiliary priority / service-affinity lender tables, node sharding, > 60 spread zones or scores
+  // beyond its 56-bit record words.  KSIM_NO_PICK=1 disables it.
+  if (cs.one && grid <= KSIM_PICK_MAXG && !getenv("KSIM_NO_PICK") && !ksim_rt_launch_tables(h) && c.sh_world <= 1 &&
+      cs.one_pod.reserved[0] * cs.one_pod.reserved[1] <= KSIM_MAX_RCLASS &&
+      (!h->have_aff || h->aff_h.n_zone <= KSIM_PICK_ZMAX)) {
+    int64_t sw = 0;
+    for (int k = 0; k < KSIM_NW; ++k) sw += (c.w[k] > ((int64_t)1 << 40) ? ((int64_t)1 << 50) : c.w[k] * 10);
+    if (h->pick_grid != grid || h->pick_npt != npt) {
+      h->pick_ok = ksim_pick_coresident(npt, grid) != 0;
+      h->pick_grid = grid;
+      h->pick_npt = npt;
+    }
+    if (sw < ((int64_t)1 << 54) && h->pick_ok) {
+      if (!h->pick_words) {
+        if ((rc = dev_alloc(h, &h->pick_words, (size_t)KSIM_PICK_WORDS))) return rc;
+        HIPCHK(h, hipMemsetAsync(h->pick_words, 0, (size_t)KSIM_PICK_WORDS * 8, h->stream));
+      }
+      h->pick_tag = h->pick_tag % 255u + 1u;  // 1..255: the previous call's words carry another tag
+      cs.pick = h->pick_words;
+      cs.pick_tag = h->pick_tag;
+      h->res_host[KSIM_RES_NODE] = INT32_MIN;
+      if ((rc = ksim_rt_check_launch_ctx(h, cs, grid, "ksim_schedule_one"))) return rc;
+      oc.lap(0);
+      hipError_t ep = ksim_launch_pick(&cs, npt, grid, h->stream);
+      if (ep != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pick launch: %s", hipGetErrorString(ep));
+      oc.lap(1);
+      HIPCHK(h, hipStreamSynchronize(h->stream));
+      oc.lap(2);
+      const int32_t* r = h->res_host;
+      memset(out, 0, sizeof *out);
+      out->node = r[KSIM_RES_NODE];
+      out->fit_nodes = r[KSIM_RES_FIT];
+      memcpy(&out->last_node_index, r + KSIM_RES_CTR, 8);
+      if (out->node < 0) memcpy(out->reasons, r + KSIM_RES_REASONS, sizeof out->reasons);
+      if (r[KSIM_RES_ERR] & 128) return ksim_rt_svc_refusal(h);
+      if (r[KSIM_RES_ERR] || out->node == INT32_MIN)
+        return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x (pick)", r[KSIM_RES_ERR]);
+      if (assume && out->node >= 0) {
+        rc = after_commit(h, pod->port_cnt);
+        oc.lap(3);
+        return rc;
+      }
+      return KSIM_OK;
+    }
+  }
   // InterPodAffinity / SelectorSpread reductions (pass A): fused into the scan behind a grid barrier
   // when the grid is co-resident (one launch), else their own launch first
   const bool ipa = ksim_is_aff_host(h, *pod) &&

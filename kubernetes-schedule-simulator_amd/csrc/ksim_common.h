@@ -124,6 +124,15 @@ struct KsimVol {
 #define KSIM_RES_CTR (KSIM_RES_REASONS + KSIM_NREASONS)  /* uint64 lastNodeIndex after the call */
 #define KSIM_RES_WORDS (KSIM_RES_CTR + 2)
 #define KSIM_ONE_PORTS 16  // host ports a per-pod launch carries in its kernel arguments
+// per-pod pick kernel (ksim_pick_kernel): <= 64 blocks, each publishing a pass-A record (min /
+// max raw InterPodAffinity sum, SelectorSpread max count, haveZones, <= 60 zone sums) and a
+// decision record (fit count, per reduce class max map score and count, reasons when it fits
+// nothing), 8-byte words tag:8 | value:56
+#define KSIM_PICK_MAXG 64
+#define KSIM_PICK_ZMAX 60
+#define KSIM_PICK_RA (4 + KSIM_PICK_ZMAX)
+#define KSIM_PICK_RB (1 + 2 * KSIM_MAX_RCLASS + KSIM_NREASONS)
+#define KSIM_PICK_WORDS (KSIM_PICK_MAXG * (KSIM_PICK_RA + KSIM_PICK_RB))
 
 struct KsimCtx {
   // ---- node table (name-rank order) ----
@@ -185,6 +194,7 @@ struct KsimCtx {
   int64_t* wmx;           // wide reduce classes (K > KSIM_MAX_RCLASS, launch form): per block and class the
   int32_t* wcnt;          // max map score among its fit nodes and their count, [grid][KSIM_MAX_WIDE]
   uint64_t* pmask;        // [grid][KSIM_PM_STRIDE] candidate masks (KSIM_PM_*)
+  uint64_t* pick;         // per-pod pick kernel: the blocks' tagged exchange records (KSIM_PICK_*)
   int32_t* out_node;      // [end-first]
   int32_t* out_reasons;   // [end-first][KSIM_NREASONS]
   int32_t* err;           // sticky error word
@@ -206,7 +216,7 @@ struct KsimCtx {
   // per-pod launches (ksim_schedule_one): the pod and its arrays travel in the kernel arguments,
   // so no read of host memory or of a staging copy sits on the kernel's critical path
   int32_t one;            // 1: the pod is one_pod (index first), its ports / scalars one_ports / one_scalars
-  int32_t one_pad;
+  uint32_t pick_tag;      // per-pod pick kernel: this call's record tag (1..255)
   ksim_pod one_pod;
   uint64_t one_ports[KSIM_ONE_PORTS];
   ksim_scalar_req one_scalars[KSIM_MAX_SCALAR];

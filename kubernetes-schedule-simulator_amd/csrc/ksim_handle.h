@@ -27,6 +27,8 @@ extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* f
 extern "C" int ksim_scan_coresident(int npt, int collect, int grid);
 extern "C" int ksim_one_npt(int64_t n);
 extern "C" hipError_t ksim_launch_one(const KsimCtx* c, int npt, hipStream_t s);
+extern "C" int ksim_pick_coresident(int npt, int grid);
+extern "C" hipError_t ksim_launch_pick(const KsimCtx* c, int npt, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_ipa_pass(const KsimCtx* c, int npt, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, int32_t* status, hipStream_t s);
 extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
@@ -133,7 +135,11 @@ struct ksim_handle {
   // node table (any other commit path clears it)
   int32_t n_tcls = 0;                      // -1: more classes than the tree supports
   bool last_pfast_cache = false;           // the last fast-kernel call took the cached form
-  bool last_pfast_pipe = false;            // ... and its two-deep pipelined kernel (ksim_pipe.hip)
+  bool last_pfast_pipe = false;
+  uint64_t* pick_words = nullptr;          // the per-pod pick kernel's exchange records
+  uint32_t pick_tag = 0;
+  int pick_grid = -1, pick_npt = -1;
+  bool pick_ok = false;            // ... and its two-deep pipelined kernel (ksim_pipe.hip)
   uint64_t* pipe_words = nullptr;          // the pipelined kernel's published words
   size_t pipe_bytes = 0;
   int32_t* tcls = nullptr;

@@ -12,23 +12,13 @@
 // the device-side pod cursor.  Launches are replayed from a hipGraph, so per-pod host
 // work is zero and no PCIe traffic happens between pods.
 #include "ksim_common.h"
+#include "ksim_wave.h"
 
 namespace {
 
-__device__ __forceinline__ int64_t wave_max_i64(int64_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const int64_t t = __shfl_xor(v, o, 64);
-    v = t > v ? t : v;
-  }
-  return v;
-}
-
-__device__ __forceinline__ int32_t wave_sum_i32(int32_t v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
+// wave reductions on the DPP helpers (row shifts / broadcasts, no LDS permute)
+__device__ __forceinline__ int64_t wave_max_i64(int64_t v) { return ksimw::max_i64(v); }
+__device__ __forceinline__ int32_t wave_sum_i32(int32_t v) { return ksimw::sum_i32(v); }
 
 // inclusive prefix sum over the 256-thread block (4 waves)
 __device__ __forceinline__ int64_t block_incl_scan(int64_t v, int64_t* s_w) {
@@ -1482,6 +1472,409 @@ __global__ __launch_bounds__(ONE_BLOCK) void ksim_one_kernel(KsimCtx c) {
   }
 }
 
+// ---------------------------------------------------------------------------------------
+// The per-pod call on a multi-block cluster (ksim_schedule_one, <= 64 blocks): the same
+// evaluation, pass A, decision and commit as ksim_scan_kernel, but with no last block.  Every
+// block publishes one tagged record (write-through 8-byte words tag:8 | value:56) and reads
+// every other block's: pass A's min / max / max count / haveZones / zone sums
+// (interpod_affinity.go:218-236, selector_spreading.go:121-174) in one exchange, the decision
+// inputs — fit count, per reduce class (max map score, count at it), the reasons of a block that
+// fits nothing — in another, and every block then takes the same decision redundantly
+// (generic_scheduler.go:136-198, NormalizeReduce reduce.go:29-64): the block holding the ix-th
+// match from the top picks the node from its own candidate masks in LDS and commits it.  One
+// cross-block hop per exchange instead of the scan's five serial round trips through the last
+// block; the pod travels in the kernel arguments.  All blocks co-resident (host-checked).
+namespace {
+__device__ __forceinline__ uint64_t pk_enc(uint32_t tag, int64_t v) {
+  return ((uint64_t)tag << 56) | ((uint64_t)v & ((1ull << 56) - 1));
+}
+__device__ __forceinline__ int64_t pk_dec(uint64_t w) { return ((int64_t)(w << 8)) >> 8; }
+__device__ __forceinline__ uint32_t pk_tag(uint64_t w) { return (uint32_t)(w >> 56); }
+__device__ __forceinline__ void pk_store(uint64_t* g, uint64_t v) {
+  __hip_atomic_store(g, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t pk_load(const uint64_t* g) {
+  return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr uint64_t PK_SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
+}  // namespace
+
+template <int NPT>
+__global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
+  __shared__ uint64_t s_bm[KSIM_MAX_RCLASS + 1][NPT][KSIM_WAVES];  // per class (and [MAX] = fit) candidate masks
+  __shared__ int64_t s_mx[KSIM_WAVES][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_cnt[KSIM_WAVES][KSIM_MAX_RCLASS];
+  __shared__ int32_t s_fit[KSIM_WAVES];
+  __shared__ int32_t s_hist[KSIM_NREASONS];
+  __shared__ int64_t s_v[4][KSIM_WAVES];
+  __shared__ unsigned long long s_z[KSIM_PICK_ZMAX];
+  __shared__ int64_t s_pa[4];
+  __shared__ int64_t s_tv[KSIM_MAX_RCLASS], s_av[KSIM_MAX_RCLASS], s_ad[KSIM_MAX_RCLASS];
+  __shared__ int64_t s_bmax[KSIM_MAX_RCLASS];  // this block's max per class (after the decision: the winners')
+  __shared__ int32_t s_mode, s_owner, s_rank, s_F, s_ok;
+  __shared__ uint32_t s_win;
+  __shared__ int64_t s_M[KSIM_MAX_RCLASS];
+  __shared__ int32_t s_C[KSIM_MAX_RCLASS];
+  __shared__ int64_t s_rec[KSIM_PICK_MAXG][1 + 2 * KSIM_MAX_RCLASS];  // every block's decision record
+  __shared__ uint64_t s_ctr;
+
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int G = gridDim.x, me = blockIdx.x;
+  const ksim_pod P = c.one_pod;
+  const int64_t pod = c.first;
+  const int k1 = P.reserved[0], k2 = P.reserved[1];
+  const int K = k1 * k2;  // <= KSIM_MAX_RCLASS (host-checked)
+  const uint32_t tag = c.pick_tag;
+  uint64_t* const recA = c.pick;
+  uint64_t* const recB = c.pick + KSIM_PICK_MAXG * KSIM_PICK_RA;
+  // the decision's inputs, loaded while the nodes are evaluated
+  int64_t pre_tv = 0, pre_av = 0, pre_ad = 0;
+  if (tid < K) {
+    pre_tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid / k2];
+    pre_av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2];
+    pre_ad = c.na_add ? c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2] : 0;
+  }
+  uint64_t pre_ctr = 0;
+  if (tid == 0) pre_ctr = *c.counter;
+  IpaNorm ipa = ipa_norm(c, P);  // which of pass A's priorities the pod reads (maxima below)
+  IpaNorm ipa0 = ipa;
+  ipa0.on = false;
+  ipa0.sp = -1;
+  const bool pass_a = ipa.on || ipa.sp >= 0;
+  const int NZ = (ipa.sp >= 0) ? c.aff->n_zone : 0;  // <= KSIM_PICK_ZMAX (host-checked)
+  if (tid < KSIM_NREASONS) s_hist[tid] = 0;
+  if (tid < KSIM_PICK_ZMAX) s_z[tid] = 0;
+  if (tid == 0) s_ok = 1;
+  __syncthreads();
+
+  const int64_t base = (int64_t)me * c.chunk;
+  bool fit[NPT];
+  int64_t sc[NPT];
+  int cl[NPT];
+  uint32_t rm[NPT];
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) eval_one<true>(c, P, base + (int64_t)k * KSIM_BLOCK + tid, k1, k2, ipa0, fit[k], sc[k], cl[k], rm[k]);
+
+  // the first spin that hits its bound: err bit 2 (a consistency error; the grid is co-resident)
+  auto spin_fail = [&]() {
+    if (lane == 0) { atomicOr(c.err, 2); s_ok = 0; }
+  };
+
+  if (pass_a) {  // (uniform) pass A over the fit nodes: the block's partial, then every block's
+    const KsimAff& A = *c.aff;
+    int64_t raw[NPT], cnt[NPT];
+    int32_t zz[NPT];
+    int64_t mn = 0, mx = 0, smx = 0, hz = 0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int64_t i = base + (int64_t)k * KSIM_BLOCK + tid;
+      raw[k] = 0; cnt[k] = 0; zz[k] = -1;
+      if (!fit[k]) continue;
+      if (ipa.on) {
+        raw[k] = ksim_interpod_raw_body(A, P, i);
+        mn = raw[k] < mn ? raw[k] : mn;
+        mx = raw[k] > mx ? raw[k] : mx;
+      }
+      if (ipa.sp >= 0) {
+        cnt[k] = A.cnt[A.pair_off[ipa.sp] + i];
+        zz[k] = A.zone_key >= 0 ? ksim_dom(A, A.zone_key, i) : -1;
+        smx = cnt[k] > smx ? cnt[k] : smx;
+        if (zz[k] >= 0) {
+          hz = 1;
+          if (cnt[k]) atomicAdd(&s_z[zz[k]], (unsigned long long)cnt[k]);
+        }
+      }
+    }
+    mn = ksimw::min_i64(mn);
+    mx = ksimw::max_i64(mx);
+    smx = ksimw::max_i64(smx);
+    hz = ksimw::max_i64(hz);
+    if (lane == 0) { s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz; }
+    __syncthreads();
+    if (wv == 0) {
+      // publish: word x = lane x (0..3 the maxima over this block's waves, 4.. the zone sums)
+      int64_t v = 0;
+      if (lane < 4) {
+        v = s_v[lane][0];
+        for (int w = 1; w < KSIM_WAVES; ++w)
+          v = lane == 0 ? (s_v[0][w] < v ? s_v[0][w] : v) : (s_v[lane][w] > v ? s_v[lane][w] : v);
+      } else if (lane - 4 < NZ) {
+        v = (int64_t)s_z[lane - 4];
+      }
+      const int W = 4 + NZ;
+      if (lane < W) pk_store(recA + (int64_t)me * KSIM_PICK_RA + lane, pk_enc(tag, v));
+      // every block's record: lane x combines word x over the blocks
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      int64_t acc = 0;
+      for (;;) {
+        bool ok = true;
+        acc = 0;  // (0 folded into every combine: the reference's accumulators start there)
+        for (int b = 0; b < G; ++b) {
+          if (lane >= W) break;
+          const uint64_t wd = pk_load(recA + (int64_t)b * KSIM_PICK_RA + lane);
+          ok &= pk_tag(wd) == tag;
+          const int64_t x = pk_dec(wd);
+          acc = lane == 0 ? (x < acc ? x : acc) : (lane < 4 ? (x > acc ? x : acc) : acc + x);
+        }
+        if (__all(ok)) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { spin_fail(); break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (lane < 4) s_pa[lane] = acc;
+      else if (lane < W) s_z[lane - 4] = (unsigned long long)acc;
+    }
+    __syncthreads();
+    ipa.mn = s_pa[0]; ipa.mx = s_pa[1]; ipa.smx = s_pa[2]; ipa.hz = s_pa[3] != 0;
+    int64_t zm = 0;  // the zone maximum (over every zone: zeros included, as the scan's pass A)
+    for (int z = 0; z < NZ; ++z) zm = (int64_t)s_z[z] > zm ? (int64_t)s_z[z] : zm;
+    ipa.szmx = zm;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {  // eval_one's additions, same order
+      if (!fit[k]) continue;
+      if (ipa.on) sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)ipa.w * (uint64_t)ksim_interpod_score(raw[k], ipa.mn, ipa.mx));
+      if (ipa.sp >= 0) {
+        const int64_t v = ksim_spread_score(cnt[k], ipa.smx, ipa.hz, zz[k], zz[k] >= 0 ? (int64_t)s_z[zz[k]] : 0, ipa.szmx);
+        sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)ipa.sw * (uint64_t)v);
+      }
+    }
+  }
+
+  if (tid < K) { s_tv[tid] = pre_tv; s_av[tid] = pre_av; s_ad[tid] = pre_ad; }
+  if (tid == 0) s_ctr = pre_ctr;
+  // ---- per wave: fit count and mask, per reduce class (max, count at max) and masks, reasons ----
+  int32_t nfit = 0;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const uint64_t b = __ballot(fit[k]);
+    nfit += __popcll(b);
+    if (lane == 0) s_bm[KSIM_MAX_RCLASS][k][wv] = b;
+  }
+  if (lane == 0) s_fit[wv] = nfit;
+  for (int q = 0; q < K; ++q) {  // (uniform)
+    int64_t v = INT64_MIN;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k)
+      if (fit[k] && cl[k] == q && sc[k] > v) v = sc[k];
+    const int64_t wm = ksimw::max_i64(v);
+    int32_t n = 0;
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const uint64_t b = __ballot(fit[k] && cl[k] == q && sc[k] == wm);
+      n += __popcll(b);
+      if (lane == 0) s_bm[q][k][wv] = b;
+    }
+    if (lane == 0) { s_mx[wv][q] = wm; s_cnt[wv][q] = wm == INT64_MIN ? 0 : n; }
+  }
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    if (__ballot(rm[k] != 0)) {
+      for (int r = 0; r < KSIM_NREASONS; ++r) {
+        const int32_t n = __popcll(__ballot((rm[k] >> r) & 1u));
+        if (lane == 0 && n) atomicAdd(&s_hist[r], n);
+      }
+    }
+  }
+  __syncthreads();
+
+  if (wv == 0) {
+    // ---- this block's record: fit, per class (max, count), reasons when it fits nothing ----
+    const int32_t F0 = s_fit[0] + s_fit[1] + s_fit[2] + s_fit[3];
+    int64_t bm = INT64_MIN;
+    int32_t bc = 0;
+    if (lane < K) {
+      for (int w = 0; w < KSIM_WAVES; ++w) {
+        if (s_cnt[w][lane] == 0) continue;
+        if (s_mx[w][lane] > bm) { bm = s_mx[w][lane]; bc = s_cnt[w][lane]; }
+        else if (s_mx[w][lane] == bm) bc += s_cnt[w][lane];
+      }
+      s_bmax[lane] = bc ? bm : INT64_MIN;
+    }
+    const int WB = 1 + 2 * K + (F0 == 0 ? KSIM_NREASONS : 0);
+    // word x = lane x: fit, then class q's max (word 1 + q), its count (word 1 + K + q), reasons
+    const int64_t mq = __shfl(bm, (lane - 1) & 63, 64);
+    const int32_t cq = __shfl(bc, (lane - 1) & 63, 64), cq2 = __shfl(bc, (lane - 1 - K) & 63, 64);
+    int64_t v = 0;
+    if (lane == 0) v = F0;
+    else if (lane <= K) v = cq ? mq : 0;  // (a class without fit nodes: count 0, max unread)
+    else if (lane <= 2 * K) v = cq2;
+    else if (lane < WB) v = s_hist[lane - 1 - 2 * K];
+    if (lane < WB) pk_store(recB + (int64_t)me * KSIM_PICK_RB + lane, pk_enc(tag, v));
+    // ---- every block's record (lane b = block b, staged in LDS), then the decision, the same in
+    // every block ----
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      bool ok = true;
+      if (lane < G)
+        for (int x = 0; x <= 2 * K; ++x) {
+          const uint64_t w = pk_load(recB + (int64_t)lane * KSIM_PICK_RB + x);
+          ok &= pk_tag(w) == tag;
+          s_rec[lane][x] = pk_dec(w);
+        }
+      if (__all(ok)) break;
+      if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { spin_fail(); break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    const bool in = lane < G;
+    const int32_t fb = in ? (int32_t)s_rec[lane][0] : 0;
+    const int32_t F = ksimw::sum_i32(fb);
+    int mode = F == 0 ? 0 : (F == 1 ? 1 : 2);
+    uint32_t win = 0;
+    int64_t C = 0;
+    if (mode == 2) {
+      for (int q = 0; q < K; ++q) {  // (uniform) the grid's max and count per class
+        const int32_t cb = in ? (int32_t)s_rec[lane][1 + K + q] : 0;
+        const int64_t mb = cb ? s_rec[lane][1 + q] : INT64_MIN;
+        const int64_t m = ksimw::max_i64(mb);
+        const int32_t n = ksimw::sum_i32((cb && mb == m) ? cb : 0);
+        if (lane == 0) { s_M[q] = m; s_C[q] = n; }
+      }
+      // reduce priorities over the filtered set (NormalizeReduce), as ksim_scan_kernel (every lane
+      // the same values: LDS broadcasts)
+      int64_t mxT = 0, mxA = 0;
+      for (int q = 0; q < K; ++q) {
+        if (s_C[q] == 0) continue;
+        if (k1 > 1 || c.w[KSIM_W_TAINT_TOLERATION]) mxT = s_tv[q] > mxT ? s_tv[q] : mxT;
+        if (k2 > 1 || c.w[KSIM_W_NODE_AFFINITY]) mxA = s_av[q] > mxA ? s_av[q] : mxA;
+      }
+      auto total_of = [&](int q) -> int64_t {
+        uint64_t t = (uint64_t)s_M[q];
+        if (c.w[KSIM_W_TAINT_TOLERATION]) t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(s_tv[q], mxT, true);
+        if (c.w[KSIM_W_NODE_AFFINITY]) t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(s_av[q], mxA, false);
+        t += (uint64_t)s_ad[q];  // NodePreferAvoidPods
+        return (int64_t)t;
+      };
+      int64_t best = INT64_MIN;
+      for (int q = 0; q < K; ++q)
+        if (s_C[q]) { const int64_t t = total_of(q); best = t > best ? t : best; }
+      for (int q = 0; q < K; ++q)
+        if (s_C[q] && total_of(q) == best) { win |= 1u << q; C += s_C[q]; }
+    }
+    // selectHost: the ix-th match counted from the largest name rank down (blocks from the top)
+    const uint64_t li = s_ctr;
+    int64_t ix = 0;
+    if (mode == 2) ix = ((li >> 32) == 0 && C < ((int64_t)1 << 32)) ? (int64_t)((uint32_t)li % (uint32_t)C) : (int64_t)(li % (uint64_t)C);
+    int64_t mt = 0;  // this lane's block: its matches
+    if (in && mode == 1) mt = fb;
+    if (in && mode == 2)
+      for (int q = 0; q < K; ++q) {
+        if (!((win >> q) & 1u)) continue;
+        const int32_t cb = (int32_t)s_rec[lane][1 + K + q];
+        if (cb && s_rec[lane][1 + q] == s_M[q]) mt += cb;
+      }
+    const int32_t incl = ksimw::prefix_incl_i32((int32_t)mt);
+    const int32_t total = __builtin_amdgcn_readlane(incl, 63);
+    // blocks from the top: block b's matches come after those of every block above it
+    const int32_t above = total - incl;
+    const uint64_t hb = __ballot(mode != 0 && mt > 0 && ix >= above && ix < above + mt);
+    const int owner = hb ? 63 - __builtin_clzll(hb) : -1;
+    const int32_t rank = owner >= 0 ? (int32_t)ix - __builtin_amdgcn_readlane(above, owner) : 0;
+    if (lane == 0) {
+      if (mode != 0 && owner < 0) { atomicOr(c.err, 2); mode = 0; }  // inconsistent counts: must never happen
+      s_mode = s_ok ? mode : -1;
+      s_owner = owner;
+      s_rank = rank;
+      s_F = F;
+      s_win = win;
+      s_ctr = (mode == 2) ? li + 1 : li;  // generic_scheduler.go:192-195
+    }
+    if (mode != 2 && lane < KSIM_MAX_RCLASS) s_M[lane] = INT64_MIN;
+  }
+  __syncthreads();
+  const int mode = s_mode;
+  if (mode < 0) return;  // a spin hit its bound (err set): nothing committed
+
+  if (mode == 0) {
+    if (me == 0 && wv == 0) {  // FitError: every block's reasons (each fitted nothing)
+      int32_t v = 0;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {  // (the reason words went out in the same store as the words read above, tagged alike)
+        bool ok = true;
+        v = 0;
+        for (int b = 0; b < G && lane < KSIM_NREASONS; ++b) {
+          const uint64_t wd = pk_load(recB + (int64_t)b * KSIM_PICK_RB + 1 + 2 * K + lane);
+          ok &= pk_tag(wd) == tag;
+          v += (int32_t)pk_dec(wd);
+        }
+        if (__all(ok)) break;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { atomicOr(c.err, 2); break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (lane < KSIM_NREASONS) c.out_reasons[pod * KSIM_NREASONS + lane] = v;
+      if (lane == 0) {
+        c.out_node[pod] = -1;
+        if (c.out_fit) {
+          c.out_fit[0] = 0;
+          c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT] = (int32_t)(uint32_t)s_ctr;
+          c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1] = (int32_t)(uint32_t)(s_ctr >> 32);
+        }
+      }
+    }
+    return;
+  }
+  if (me != s_owner) return;
+
+  // ---- the owner block: its rank-th match from the top, from its own candidate masks ----
+  __shared__ int64_t s_node;
+  if (wv == 0) {
+    // lane t = (k, w) segment from the top: its mask of matches
+    uint64_t m = 0;
+    const int k = NPT - 1 - lane / KSIM_WAVES, w = KSIM_WAVES - 1 - lane % KSIM_WAVES;
+    if (lane < NPT * KSIM_WAVES) {
+      if (mode == 1) {
+        m = s_bm[KSIM_MAX_RCLASS][k][w];
+      } else {
+        for (int q = 0; q < K; ++q)
+          if (((s_win >> q) & 1u) && s_bmax[q] == s_M[q] && s_mx[w][q] == s_M[q]) m |= s_bm[q][k][w];
+      }
+    }
+    const int32_t n = __popcll(m);
+    const int32_t incl = ksimw::prefix_incl_i32(n);
+    const int32_t r = s_rank;
+    const bool here = n > 0 && r >= incl - n && r < incl;
+    const uint64_t hs = __ballot(here);
+    int64_t node = -1;
+    if (hs) {
+      const int t = __builtin_ctzll(hs);
+      const uint64_t ms = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(m >> 32), t) << 32) |
+                          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)m, t);
+      const int32_t rr = r - (__builtin_amdgcn_readlane(incl, t) - __popcll(ms));
+      const uint64_t hb2 = __ballot(((ms >> lane) & 1ull) && __popcll(ms >> lane) - 1 == rr);
+      const int kt = NPT - 1 - t / KSIM_WAVES, wt = KSIM_WAVES - 1 - t % KSIM_WAVES;
+      if (hb2) node = (int64_t)me * c.chunk + (int64_t)kt * KSIM_BLOCK + wt * 64 + __builtin_ctzll(hb2);
+    }
+    if (lane == 0) {
+      if (node < 0) atomicOr(c.err, 2);  // inconsistent masks: must never happen
+      s_node = node;
+    }
+  }
+  __syncthreads();
+  const int64_t node = s_node;
+  if (node >= 0 && !c.no_commit) {
+    if (wv == 0) {
+      const int32_t st = ksim_commit_wave(c, P, node, lane);
+      if (tid == 0) {
+        if (ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, node, 1, c.err);
+        if (c.out_fit) c.out_fit[1] |= st;
+      }
+    } else if (wv == 1 && ksim_is_aff_pod(c, P)) {
+      if (lane == 0) ksim_svc_commit(*c.aff, P, node);  // reads the counts before this commit's adds
+      ksim_aff_commit_body(*c.aff, P, node, 1, lane, 64);
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    if (mode == 2) *c.counter = s_ctr;
+    c.out_node[pod] = (int32_t)node;
+    if (c.out_fit) {
+      c.out_fit[0] = s_F;
+      c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT] = (int32_t)(uint32_t)s_ctr;
+      c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1] = (int32_t)(uint32_t)(s_ctr >> 32);
+    }
+  }
+}
+
 // Per-node evaluation of one pod without commit (ksim_evaluate).
 __global__ __launch_bounds__(KSIM_BLOCK) void ksim_eval_kernel(KsimCtx c, int64_t pod, uint8_t* fit, uint32_t* reasons,
                                                              int64_t* score, uint8_t* rcls) {
@@ -1596,5 +1989,29 @@ extern "C" hipError_t ksim_launch_eval(const KsimCtx* c, int64_t pod, uint8_t* f
 
 extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, int32_t* status, hipStream_t s) {
   hipLaunchKernelGGL(ksim_assume_kernel, dim3(1), dim3(64), 0, s, *c, pod, node, status);
+  return hipGetLastError();
+}
+
+// per-pod pick kernel: <= KSIM_PICK_MAXG blocks of KSIM_BLOCK threads, npt nodes per thread
+extern "C" int ksim_pick_coresident(int npt, int grid) {
+  hipError_t e = hipErrorInvalidValue;
+  switch (npt) {
+    case 1: e = ksim_check_coresident(ksim_pick_kernel<1>, grid, KSIM_BLOCK, 0); break;
+    case 2: e = ksim_check_coresident(ksim_pick_kernel<2>, grid, KSIM_BLOCK, 0); break;
+    case 4: e = ksim_check_coresident(ksim_pick_kernel<4>, grid, KSIM_BLOCK, 0); break;
+    case 8: e = ksim_check_coresident(ksim_pick_kernel<8>, grid, KSIM_BLOCK, 0); break;
+  }
+  return e == hipSuccess ? 1 : 0;
+}
+
+extern "C" hipError_t ksim_launch_pick(const KsimCtx* c, int npt, int grid, hipStream_t s) {
+  if (grid <= 0 || grid > KSIM_PICK_MAXG || !c->pick) return hipErrorInvalidValue;
+  switch (npt) {
+    case 1: hipLaunchKernelGGL(ksim_pick_kernel<1>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
+    case 2: hipLaunchKernelGGL(ksim_pick_kernel<2>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
+    case 4: hipLaunchKernelGGL(ksim_pick_kernel<4>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
+    case 8: hipLaunchKernelGGL(ksim_pick_kernel<8>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }

@@ -190,20 +190,446 @@ __device__ __forceinline__ FRow prow(const PRows& R, int32_t j) {
 
 }  // namespace
 
+// LDS state shared by the two roles (the kernel arguments are copied here once: the role
+// functions are kept out of line, each with its own register allocation)
+struct PipeSh {
+  PpArgs a;
+  int32_t dec[DR][3];      // decision: mode, owner workgroup, rank
+  int32_t dec_seq;         // last decided relative pod
+  int32_t commit_seq;      // last relative pod committed by this workgroup (or -1)
+  int32_t iter_done;       // row-wave iterations finished (sum over the waves)
+  int32_t stop;            // a wave hit its spin bound
+  uint64_t counter;        // the control wave's lastNodeIndex at the end
+  int64_t stop_at;         // first pod not scheduled
+  __attribute__((aligned(16))) ksim_pod pod[RING];
+  int32_t pcls[RING];
+  KsimTreeClass tcl[KSIM_TREE_MAX_CLASSES];
+};
+
+namespace {
+
+__device__ __forceinline__ uint64_t ptag(int32_t rel) { return (uint64_t)((rel + 1) & 0xFF); }
+
+// the first spin that hit its bound: workgroup, wave, site, pod (and a site-specific value)
+__device__ __forceinline__ void note(const PpArgs& a, int site, int32_t rel, int32_t aux) {
+  if ((threadIdx.x & 63) == 0)
+    atomicCAS((unsigned long long*)a.dbg, 0ull,
+              ((unsigned long long)blockIdx.x << 52) | ((unsigned long long)(threadIdx.x >> 6) << 48) |
+                  ((unsigned long long)site << 40) | ((unsigned long long)(aux & 0xFFFF) << 24) |
+                  (unsigned long long)(rel & 0xFFFFFF));
+}
+
+__device__ __forceinline__ uint64_t* aslot(uint64_t* base, int32_t rel, int b) {
+  return base + (rel % NSLOT) * MAXG + (b % MAXB) * 64 + b / MAXB;
+}
+__device__ __forceinline__ uint64_t* bword(const PpArgs& a, int32_t rel, int b) {
+  return a.words + NREP * REP_STRIDE + (rel % NSLOT) * MAXG + b;
+}
+__device__ __forceinline__ uint64_t* fslot(const PpArgs& a, int32_t rel, int b, int32_t r) {
+  return a.words + NREP * REP_STRIDE + NSLOT * MAXG + ((int64_t)(rel % NSLOT) * gridDim.x + b) * a.chunk + r;
+}
+
+__device__ __forceinline__ FPod cls_fpod(const PipeSh& S, int k) {
+  const KsimTreeClass& t = S.tcl[k];
+  return FPod{t.rq_c, t.rq_m, t.nz_c, t.nz_m, 0.0, 0.0, t.anyreq, t.be};
+}
+
+}  // namespace
+
+#ifdef KSIM_STAMPS
+#define PSTAMP(k)                                     \
+  do {                                                \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    st[k] += t_ - tp;                                 \
+    tp = t_;                                          \
+  } while (0)
+#define PFLUSH(base)                                                                                   \
+  do {                                                                                                 \
+    if ((threadIdx.x & 63) == 0)                                                                       \
+      for (int k_ = 0; k_ < 8; ++k_) atomicAdd((unsigned long long*)&a.dbg[(base) + k_], st[k_]);      \
+  } while (0)
+#else
+#define PSTAMP(k) do { } while (0)
+#define PFLUSH(base) do { } while (0)
+#endif
+
+// ---------------- row waves (1..RW) ----------------
+template <int NPT>
+__device__ __noinline__ void pipe_rows(PipeSh* Sp) {
+  PipeSh& S = *Sp;
+  const PpArgs& a = S.a;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int rt = tid - 64;
+  const int me = blockIdx.x;
+  const int64_t chunk = a.chunk;
+  const int64_t lo = (int64_t)me * chunk;
+  const int32_t nrows = (int32_t)(((lo + chunk < a.n) ? lo + chunk : a.n) - lo);
+  const int NB = a.nb, NSEG = (int)((chunk + 63) / 64), K = a.ncls;
+  const PRows R = pcarve((int)chunk, K, NSEG, NB);
+  const EvCfg EC = make_evcfg(a.preds, a.no_prio != 0, a.wl, a.wm, a.wb);
+  const int64_t first = a.first, end = a.end;
+  const int32_t npods = (int32_t)(end - first);
+#ifdef KSIM_STAMPS
+  uint64_t st[8] = {};
+  uint64_t tp = __builtin_amdgcn_s_memtime();
+#endif
+
+  // the workgroup's (fit, max, count at max, second max, its count) for class c from the
+  // histogram (lane b = bin b), published as A / B of pod rel by wave RW
+  auto publish_ab = [&](int32_t rel) {
+    const int c = S.pcls[(first + rel) % RING];
+    const int32_t h = lane < NB ? R.hwg[c * NB + lane] : 0;
+    const uint64_t nz = __ballot(h > 0);
+    const int32_t m1 = nz ? 63 - __builtin_clzll(nz) : -1;
+    const uint64_t nz2 = m1 >= 0 ? (nz & ~(1ull << m1)) : 0ull;
+    const int32_t m2 = nz2 ? 63 - __builtin_clzll(nz2) : -1;
+    const int32_t c1 = m1 >= 0 ? __builtin_amdgcn_readlane(h, m1) : 0;
+    const int32_t c2 = m2 >= 0 ? __builtin_amdgcn_readlane(h, m2) : 0;
+    const uint64_t tg = ptag(rel);
+    if (lane < NREP) gstore(aslot(a.words + lane * REP_STRIDE, rel, me), apack(tg, R.fitc[c], c1, m1));
+    if (lane == NREP) gstore(bword(a, rel, me), bpack(tg, m2, c2));
+  };
+  // candidate rows of pod rel1 (the rows at this workgroup's maximum of the pod's class, ranked
+  // from the top) and, for each, pod rel1 + 1's evaluation before / after pod rel1 is committed
+  // to it → F(rel1 + 1)
+  uint64_t tmask[NPT];  // this wave's candidate rows of the pod being decided next, per segment
+  int32_t tabove[NPT];  // candidates in the segments above each
+  auto rank_and_fix = [&](int32_t rel1) {
+    const int c1 = S.pcls[(first + rel1) % RING];
+    const int32_t h = lane < NB ? R.hwg[c1 * NB + lane] : 0;
+    const uint64_t nz = __ballot(h > 0);
+    const int32_t M1 = nz ? 63 - __builtin_clzll(nz) : -1;
+    const int16_t* cc = R.cache + (int64_t)c1 * chunk;
+    // candidates per segment (lane = segment); suffix sums give the segments above
+    const int32_t sc = (M1 >= 0 && lane < NSEG) ? R.hseg[(c1 * NSEG + lane) * NB + M1] : 0;
+    const int32_t incl = ksimw::prefix_incl_i32(sc);
+    const int32_t total = __builtin_amdgcn_readlane(incl, 63);
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      const int32_t j = k * RT + rt;
+      tmask[k] = __ballot(M1 >= 0 && j < nrows && (int32_t)cc[j] == M1);
+      tabove[k] = total - __builtin_amdgcn_readlane(incl, k * RW + w - 1);
+    }
+    const int32_t rel2 = rel1 + 1;
+    if (rel2 >= npods) return;
+    const FPod F1 = load_fpod(S.pod[(first + rel1) % RING]);
+    const FPod F2 = load_fpod(S.pod[(first + rel2) % RING]);
+    const int16_t* c2 = R.cache + (int64_t)S.pcls[(first + rel2) % RING] * chunk;
+    const uint64_t tg = ptag(rel2);
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) {
+      if ((tmask[k] >> lane) & 1ull) {
+        const int32_t j = k * RT + rt;
+        const int32_t rank = tabove[k] + __popcll((tmask[k] >> lane) >> 1);
+        const FRow r2 = plus(prow(R, j), F1);
+        uint32_t m;
+        const int32_t en = feval(EC, F2, r2, m);
+        const bool stop = r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM;
+        gstore(fslot(a, rel2, me, rank), fpack(tg, stop, (int32_t)c2[j], en));
+      }
+    }
+  };
+  auto ring_load = [&](int64_t p0, uint4& v, int32_t& cl) {
+    const int64_t p = p0 + lane / 8;
+    if (p < end) v = reinterpret_cast<const uint4*>(&a.pods[p])[lane % 8];
+    if (lane < RING_FILL && p0 + lane < end) cl = a.tcls[p0 + lane];
+  };
+  auto ring_store = [&](int64_t p0, const uint4& v, int32_t cl) {
+    const int64_t p = p0 + lane / 8;
+    if (p < end) reinterpret_cast<uint4*>(&S.pod[p % RING])[lane % 8] = v;
+    if (lane < RING_FILL && p0 + lane < end) S.pcls[(p0 + lane) % RING] = cl;
+  };
+
+  // ---- prologue: A/B of the first two pods, candidates of the first, F of the second ----
+  if (w == RW) {
+    publish_ab(0);
+    if (npods > 1) publish_ab(1);
+  }
+  rank_and_fix(0);
+  bool ok = true;
+  uint4 ring_next = make_uint4(0, 0, 0, 0);  // wave 1: descriptors of the next refill
+  int32_t ring_next_cl = 0;
+  if (w == 1) ring_load(first + 2 * RING_FILL, ring_next, ring_next_cl);
+  if (lane == 0) atomicAdd(&S.iter_done, 1);  // the prologue counts as iteration -1
+  PSTAMP(7);
+
+  // ---- row iterations: after decision rel ----
+  for (int32_t rel = 0; rel < npods; ++rel) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (seq_acquire(&S.dec_seq) < rel) {
+      if (past(t0) || seq_acquire(&S.stop)) { note(a, 2, rel, seq_acquire(&S.dec_seq)); ok = false; break; }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (!ok) break;
+    PSTAMP(0);  // waiting for the decision
+    const int32_t mode = S.dec[rel % DR][0], X = S.dec[rel % DR][1], rk = S.dec[rel % DR][2];
+    if (mode < 0) break;
+    const bool own = mode == 2 && X == me;
+    // not the owner: this workgroup's statistics of pod rel + 2 are final already — publish first
+    if (!own && w == RW && rel + 2 < npods) publish_ab(rel + 2);
+    if (w == 1 && (rel % RING_FILL) == 0) {  // pods [rel + 16, rel + 24) into the ring
+      const int64_t p0 = first + rel + 2 * RING_FILL;
+      ring_store(p0, ring_next, ring_next_cl);
+      ring_load(p0 + RING_FILL, ring_next, ring_next_cl);
+    }
+    const int64_t pod = first + rel;
+    if (mode == 0 && a.collect && a.out_reasons) {
+      // FitError: the pod against this wave's rows as they stand
+      const FPod P = load_fpod(S.pod[pod % RING]);
+      uint32_t rms[NPT];
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int32_t j = k * RT + rt;
+        rms[k] = 0;
+        if (j < nrows) (void)feval(EC, P, prow(R, j), rms[k]);
+      }
+      for (int r = 0; r < KSIM_NREASONS; ++r) {
+        int32_t nr = 0;
+#pragma unroll
+        for (int k = 0; k < NPT; ++k) nr += __popcll(__ballot((rms[k] >> r) & 1u));
+        if (lane == 0 && nr) atomicAdd(&a.out_reasons[pod * KSIM_NREASONS + r], nr);
+      }
+    }
+    if (own) {
+      // ---- owner: the rk-th candidate from the top; commit, re-evaluate its row ----
+      int32_t seg = -1, bit = -1;
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        const int32_t cnt = __popcll(tmask[k]);
+        if (rk >= tabove[k] && rk < tabove[k] + cnt) {
+          const int32_t want = rk - tabove[k];
+          const uint64_t hb = __ballot(((tmask[k] >> lane) & 1ull) && __popcll((tmask[k] >> lane) >> 1) == want);
+          seg = k;
+          bit = __builtin_ctzll(hb);
+        }
+      }
+      if (seg >= 0) {
+        const int32_t j = seg * RT + (w - 1) * 64 + bit;
+        // every row wave must have finished the previous iteration (they read this row)
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        while (seq_acquire(&S.iter_done) < RW * (rel + 1)) {
+          if (past(t1)) { note(a, 3, rel, seq_acquire(&S.iter_done)); ok = false; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        const FRow r2 = plus(prow(R, j), load_fpod(S.pod[pod % RING]));
+        if (lane < K) {  // the row's evaluation for every class, and the histograms
+          uint32_t m;
+          const int32_t eo = R.cache[(int64_t)lane * chunk + j];
+          const int32_t en = feval(EC, cls_fpod(S, lane), r2, m);
+          R.cache[(int64_t)lane * chunk + j] = (int16_t)en;
+          const int sg = j >> 6;
+          if (eo >= 0) {
+            R.hseg[(lane * NSEG + sg) * NB + eo] -= 1;
+            R.hwg[lane * NB + eo] -= 1;
+          }
+          if (en >= 0) {
+            R.hseg[(lane * NSEG + sg) * NB + en] += 1;
+            R.hwg[lane * NB + en] += 1;
+          }
+          R.fitc[lane] += (en >= 0 ? 1 : 0) - (eo >= 0 ? 1 : 0);
+        }
+        if (lane == 0) {
+          R.rc[j] = r2.rc; R.rm[j] = r2.rm; R.zc[j] = r2.zc; R.zm[j] = r2.zm; R.count[j] = r2.count;
+          a.out_node[pod] = (int32_t)(lo + j);
+          if (r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM) atomicOr(a.err, 8);
+        }
+        seq_release(&S.commit_seq, rel);
+      } else {
+        const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+        while (seq_acquire(&S.commit_seq) < rel) {
+          if (past(t1)) { note(a, 4, rel, rk); ok = false; break; }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (ok && w == RW && rel + 2 < npods) publish_ab(rel + 2);
+    }
+    if (!ok) break;
+    PSTAMP(1);  // reasons, commit / waiting for it, publish
+    if (rel + 1 < npods) rank_and_fix(rel + 1);
+    PSTAMP(3);
+    if (lane == 0) atomicAdd(&S.iter_done, 1);
+  }
+  if (!ok && lane == 0) { atomicOr(a.err, 2); atomicExch(&S.stop, 1); }
+  if (w == 1) PFLUSH(24);
+  if (w == RW) PFLUSH(32);
+}
+
+// ---------------- control wave: decide every pod ----------------
+// A(rel) of every workgroup is in g[] (lane l: workgroups 4l .. 4l+3); after each decision the
+// loads of A(rel + 1) and of the owner's B / F words go out together, the pre-decision over
+// every workgroup but the owner overlaps the owner's words, then an O(1) post-decision.
+__device__ __noinline__ void pipe_control(PipeSh* Sp) {
+  PipeSh& S = *Sp;
+  const PpArgs& a = S.a;
+  const int lane = threadIdx.x & 63;
+  const int G = gridDim.x;
+  const int me = blockIdx.x;
+  const int64_t first = a.first;
+  const int32_t npods = (int32_t)(a.end - first);
+  uint64_t counter = *a.counter;  // replicated genericScheduler.lastNodeIndex
+  int64_t stop_at = a.end;
+#ifdef KSIM_STAMPS
+  uint64_t st[8] = {};
+  uint64_t tp = __builtin_amdgcn_s_memtime();
+  uint64_t spins = 0;
+#endif
+  __builtin_amdgcn_s_setprio(2);  // the per-pod critical path: ahead of the row wave sharing this SIMD
+  int X = -1;      // owner workgroup of the previous pod's node (-1: none)
+  int32_t XR = 0;  // ... and the rank it took
+  const uint64_t* my_rep = a.words + (me % NREP) * REP_STRIDE;
+  uint64_t g[MAXB];
+  auto load_a = [&](int32_t rel) -> bool {  // spin until A(rel) of every workgroup is here
+    const uint64_t tag = ptag(rel);
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+#pragma unroll
+      for (int j = 0; j < MAXB; ++j) g[j] = gload(my_rep + (rel % NSLOT) * MAXG + j * 64 + lane);
+      bool mine = true;
+#pragma unroll
+      for (int j = 0; j < MAXB; ++j) mine &= (lane * MAXB + j >= G) || gtag(g[j]) == tag;
+      if (__all(mine)) return true;
+      if (past(t0) || seq_acquire(&S.stop)) {
+        int32_t miss = -1;
+#pragma unroll
+        for (int j = 0; j < MAXB; ++j)
+          if (lane * MAXB + j < G && gtag(g[j]) != tag) miss = lane * MAXB + j;
+        const uint64_t mb = __ballot(miss >= 0);
+        note(a, 5, rel, mb ? __builtin_amdgcn_readlane(miss, __builtin_ctzll(mb)) : 999);
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
+  PSTAMP(7);
+  bool ok = load_a(0);
+  for (int32_t rel = 0; rel < npods; ++rel) {
+    const uint64_t tag = ptag(rel);
+    // the owner's words (address known since the last decision), in flight during the pre-decision
+    uint64_t bx = 0, fx = 0;
+    if (ok && X >= 0) {
+      bx = gload(bword(a, rel, X));
+      fx = gload(fslot(a, rel, X, XR));
+    }
+    // ---- pre-decision over every workgroup but X ----
+    int32_t cnt[MAXB];
+    int32_t f = 0, lm = -1;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) {
+      const int b = lane * MAXB + j;
+      const bool v = b < G && b != X;
+      f += v ? gfit(g[j]) : 0;
+      lm = (v && gcnt(g[j]) && gscore(g[j]) > lm) ? gscore(g[j]) : lm;
+    }
+    const int32_t Fs = ksimw::sum_i32(f);
+    const int32_t Ms = ksimw::max_i32(lm);
+    int32_t tot = 0;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) {
+      const int b = lane * MAXB + j;
+      cnt[j] = (b < G && b != X && gcnt(g[j]) && gscore(g[j]) == Ms) ? gcnt(g[j]) : 0;
+      tot += cnt[j];
+    }
+    const int32_t pre = ksimw::prefix_incl_i32(tot);
+    const int32_t Cs = __builtin_amdgcn_readlane(pre, 63);
+    const int32_t abv = Cs - pre;  // matches in workgroups of higher lanes
+    int32_t aboveX = 0;            // matches (at Ms) in workgroups above X
+    uint64_t ax = 0;
+    if (X >= 0) {
+      const int lx = X / MAXB, jx = X % MAXB;
+      int32_t part = 0;
+#pragma unroll
+      for (int j = 0; j < MAXB; ++j) part += j > jx ? cnt[j] : 0;
+      aboveX = __builtin_amdgcn_readlane(abv + part, lx);
+      ax = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)g[jx], lx) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(g[jx] >> 32), lx) << 32);
+    }
+    PSTAMP(2);  // pre-decision
+    // ---- the owner's corrected statistics ----
+    bool stop_any = false;
+    int32_t fX = 0, cX = 0, mX = -1;
+    if (ok && X >= 0) {
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      while (!(gtag(bx) == tag && gtag(fx) == tag)) {
+        if (past(t0) || seq_acquire(&S.stop)) { note(a, 6, rel, X); ok = false; break; }
+#ifdef KSIM_STAMPS
+        spins += 1;
+#endif
+        __builtin_amdgcn_s_sleep(1);
+        bx = gload(bword(a, rel, X));
+        fx = gload(fslot(a, rel, X, XR));
+      }
+      const Stat3 s = fix_stats(gfit(ax), gscore(ax), gcnt(ax), bm2(bx), bc2(bx), feo(fx), fen(fx));
+      fX = s.f; cX = s.c; mX = s.m;
+      stop_any = fstop(fx);
+    }
+    PSTAMP(0);  // waiting for the owner's words
+    // ---- post-decision: findNodesThatFit count, max score, selectHost (generic_scheduler.go:136-198) ----
+    const int32_t F = Fs + fX;
+    const bool xtop = cX > 0 && (Cs == 0 || mX > Ms);  // X alone holds the maximum
+    const bool xeq = cX > 0 && Cs > 0 && mX == Ms;      // X shares it
+    const uint32_t C = (uint32_t)(xtop ? cX : Cs + (xeq ? cX : 0));
+    const uint32_t Cd = C ? C : 1u;
+    const int64_t ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)Cd) : (int64_t)((uint32_t)counter % Cd);
+    int blk = -1, rank = 0;
+    int64_t t = ix;  // index among the other workgroups' matches, when X does not take it
+    if (xtop) {
+      blk = X; rank = (int)ix;
+    } else if (xeq && ix >= aboveX && ix < aboveX + cX) {
+      blk = X; rank = (int)(ix - aboveX);
+    } else if (xeq && ix >= aboveX + cX) {
+      t = ix - cX;
+    }
+    if (blk < 0 && C > 0) {
+      const bool hit = tot > 0 && t >= abv && t < abv + tot;
+      int32_t found = -1;
+      int64_t rr = t - abv;
+#pragma unroll
+      for (int j = MAXB - 1; j >= 0; --j) {
+        const bool here = found < 0 && rr < cnt[j];
+        found = here ? lane * MAXB + j : found;
+        rr = (found < 0) ? rr - cnt[j] : rr;
+      }
+      const uint64_t hb = __ballot(hit);
+      if (hb) {
+        const int src = __builtin_ctzll(hb);
+        blk = __builtin_amdgcn_readlane(found, src);
+        rank = __builtin_amdgcn_readlane((int32_t)rr, src);
+      }
+    }
+    int mode;
+    if (!ok) mode = -1;
+    else if (stop_any) mode = -2;  // the previous commit left the exact float64 range
+    else if (F == 0) mode = 0;
+    else mode = blk >= 0 ? 2 : -1;
+    if (mode == 2 && F > 1) counter += 1;  // generic_scheduler.go:192-195
+    if (lane == 0) {
+      if (mode == -1) atomicOr(a.err, ok ? 2 : 4);
+      if (mode == 0 && me == 0) a.out_node[first + rel] = -1;
+      S.dec[rel % DR][0] = mode; S.dec[rel % DR][1] = blk; S.dec[rel % DR][2] = rank;
+      seq_release(&S.dec_seq, rel);
+    }
+    PSTAMP(1);  // post-decision
+    if (mode < 0) {
+      if (mode == -2) stop_at = first + rel;
+      break;
+    }
+    X = mode == 2 ? blk : -1;
+    XR = rank;
+    if (rel + 1 < npods) ok = load_a(rel + 1);
+    PSTAMP(3);  // waiting for the next pod's A words
+  }
+  __builtin_amdgcn_s_setprio(0);
+#ifdef KSIM_STAMPS
+  st[6] = spins;
+#endif
+  PFLUSH(16);
+  if (lane == 0) { S.counter = counter; S.stop_at = stop_at; }
+}
+
 template <int NPT>
 __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
-  __shared__ int32_t s_dec[DR][3];      // decision: mode, owner workgroup, rank
-  __shared__ int32_t s_dec_seq;         // last decided relative pod
-  __shared__ int32_t s_commit_seq;      // last relative pod committed by this workgroup (or -1)
-  __shared__ int32_t s_iter_done;       // row-wave iterations finished (sum over the waves)
-  __shared__ int32_t s_stop;            // a wave hit its spin bound
-  __shared__ __attribute__((aligned(16))) ksim_pod s_pod[RING];
-  __shared__ int32_t s_pcls[RING];
-  __shared__ KsimTreeClass s_tcl[KSIM_TREE_MAX_CLASSES];
-
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int rt = tid - 64;
-  const int G = gridDim.x;
+  __shared__ PipeSh S;
+  const int tid = threadIdx.x, wv = tid >> 6;
   const int me = blockIdx.x;
   const int64_t chunk = a.chunk;
   const int64_t lo = (int64_t)me * chunk;
@@ -212,25 +638,7 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
   const int NB = a.nb, NSEG = (int)((chunk + 63) / 64), K = a.ncls;
   const PRows R = pcarve((int)chunk, K, NSEG, NB);
   const EvCfg EC = make_evcfg(a.preds, a.no_prio != 0, a.wl, a.wm, a.wb);
-  uint64_t* const Aw = a.words;
-  uint64_t* const Bw = a.words + NREP * REP_STRIDE;
-  uint64_t* const Fw = Bw + NSLOT * MAXG;
   const int64_t first = a.first, end = a.end;
-  const int32_t npods = (int32_t)(end - first);
-  auto ptag = [&](int32_t rel) -> uint64_t { return (uint64_t)((rel + 1) & 0xFF); };
-  // the first spin that hit its bound: workgroup, wave, site, pod (and a site-specific value)
-  auto note = [&](int site, int32_t rel, int32_t aux) {
-    if (lane == 0)
-      atomicCAS((unsigned long long*)a.dbg, 0ull,
-                ((unsigned long long)me << 52) | ((unsigned long long)wv << 48) | ((unsigned long long)site << 40) |
-                    ((unsigned long long)(aux & 0xFFFF) << 24) | (unsigned long long)(rel & 0xFFFFFF));
-  };
-  auto aslot = [&](uint64_t* base, int32_t rel, int b) -> uint64_t* {
-    return base + (rel % NSLOT) * MAXG + (b % MAXB) * 64 + b / MAXB;
-  };
-  auto fslot = [&](int32_t rel, int b, int32_t r) -> uint64_t* {
-    return Fw + ((int64_t)(rel % NSLOT) * G + b) * chunk + r;
-  };
 
   // ---- stage the rows, the class inputs and the first pods ----
   for (int32_t j = tid; j < nrows; j += BS) {
@@ -243,24 +651,24 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
     R.zc[j] = (double)a.nz_cpu[i]; R.zm[j] = (double)a.nz_mem[i];
     R.allowed[j] = a.allowed_pods[i]; R.count[j] = a.pod_count[i]; R.fl[j] = a.flags[i];
   }
-  for (int k = tid; k < K; k += BS) s_tcl[k] = a.tclass[k];
+  for (int k = tid; k < K; k += BS) S.tcl[k] = a.tclass[k];
   for (int x = tid; x < 2 * RING_FILL * 8 && first + x / 8 < end; x += BS) {  // pods [first, first + 16)
     const int64_t p = first + x / 8;
-    reinterpret_cast<uint4*>(&s_pod[p % RING])[x % 8] = reinterpret_cast<const uint4*>(&a.pods[p])[x % 8];
+    reinterpret_cast<uint4*>(&S.pod[p % RING])[x % 8] = reinterpret_cast<const uint4*>(&a.pods[p])[x % 8];
   }
-  for (int x = tid; x < 2 * RING_FILL && first + x < end; x += BS) s_pcls[(first + x) % RING] = a.tcls[first + x];
+  for (int x = tid; x < 2 * RING_FILL && first + x < end; x += BS) S.pcls[(first + x) % RING] = a.tcls[first + x];
   for (int x = tid; x < K * NSEG * NB + K * NB + K; x += BS) R.hseg[x] = 0;  // hseg, hwg, fitc are contiguous
-  if (tid == 0) { s_dec_seq = -1; s_commit_seq = -1; s_iter_done = 0; s_stop = 0; }
+  if (tid == 0) {
+    S.a = a;
+    S.dec_seq = -1; S.commit_seq = -1; S.iter_done = 0; S.stop = 0;
+    S.counter = 0; S.stop_at = end;
+  }
   __syncthreads();
-  auto cls_fpod = [&](int k) -> FPod {
-    const KsimTreeClass& t = s_tcl[k];
-    return FPod{t.rq_c, t.rq_m, t.nz_c, t.nz_m, 0.0, 0.0, t.anyreq, t.be};
-  };
   // every (class, owned row) evaluation, and the score histograms
   for (int idx = tid; idx < K * nrows; idx += BS) {
     const int k = idx / nrows, j = idx - k * nrows;
     uint32_t rm;
-    const int32_t e = feval(EC, cls_fpod(k), prow(R, j), rm);
+    const int32_t e = feval(EC, cls_fpod(S, k), prow(R, j), rm);
     R.cache[(int64_t)k * chunk + j] = (int16_t)e;
     if (e >= 0) {
       atomicAdd(&R.hseg[(k * NSEG + (j >> 6)) * NB + e], 1);
@@ -270,368 +678,8 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
   }
   __syncthreads();
 
-  // the workgroup's (fit, max, count at max, second max, its count) for class c, from the
-  // histogram: lane b holds bin b (one LDS read, two ballots)
-  struct Top2 {
-    int32_t f, m1, c1, m2, c2;
-  };
-  auto top2 = [&](int c) -> Top2 {
-    const int32_t h = lane < NB ? R.hwg[c * NB + lane] : 0;
-    const uint64_t nz = __ballot(h > 0);
-    Top2 t;
-    t.f = R.fitc[c];
-    t.m1 = nz ? 63 - __builtin_clzll(nz) : -1;
-    const uint64_t nz2 = t.m1 >= 0 ? (nz & ~(1ull << t.m1)) : 0ull;
-    t.m2 = nz2 ? 63 - __builtin_clzll(nz2) : -1;
-    t.c1 = t.m1 >= 0 ? __builtin_amdgcn_readlane(h, t.m1) : 0;
-    t.c2 = t.m2 >= 0 ? __builtin_amdgcn_readlane(h, t.m2) : 0;
-    return t;
-  };
-  const int PUB = RW;  // the row wave that publishes A / B (the top rows: the fewest candidates)
-  auto publish_ab = [&](int32_t rel) {
-    const Top2 t = top2(s_pcls[(first + rel) % RING]);
-    const uint64_t tg = ptag(rel);
-    if (lane < NREP) gstore(aslot(Aw + lane * REP_STRIDE, rel, me), apack(tg, t.f, t.c1, t.m1));
-    if (lane == NREP) gstore(Bw + (rel % NSLOT) * MAXG + me, bpack(tg, t.m2, t.c2));
-  };
-
-  // ---------------- row-wave work ----------------
-  const int w = wv;  // row wave 1..RW
-  // candidate rows of pod rel1 (this workgroup's rows at its maximum M1 of the pod's class,
-  // ranked from the top) and, for each, pod rel1 + 1's evaluation before / after pod rel1 is
-  // committed to it → F(rel1 + 1)
-  uint64_t tmask[NPT];  // this wave's candidate rows of the pod being decided next, per segment
-  int32_t tabove[NPT];  // candidates in the segments above each
-  auto rank_and_fix = [&](int32_t rel1) {
-    const int c1 = s_pcls[(first + rel1) % RING];
-    const int32_t h = lane < NB ? R.hwg[c1 * NB + lane] : 0;
-    const uint64_t nz = __ballot(h > 0);
-    const int32_t M1 = nz ? 63 - __builtin_clzll(nz) : -1;
-    const int16_t* cc = R.cache + (int64_t)c1 * chunk;
-    // candidates per segment (lane = segment), suffix sums give the segments above
-    const int32_t sc = (M1 >= 0 && lane < NSEG) ? R.hseg[(c1 * NSEG + lane) * NB + M1] : 0;
-    const int32_t incl = ksimw::prefix_incl_i32(sc);
-    const int32_t total = __builtin_amdgcn_readlane(incl, 63);
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      const int32_t j = k * RT + rt;
-      tmask[k] = __ballot(M1 >= 0 && j < nrows && (int32_t)cc[j] == M1);
-      tabove[k] = total - __builtin_amdgcn_readlane(incl, k * RW + w - 1);
-    }
-    const int32_t rel2 = rel1 + 1;
-    if (rel2 >= npods) return;
-    const FPod F1 = load_fpod(s_pod[(first + rel1) % RING]);
-    const FPod F2 = load_fpod(s_pod[(first + rel2) % RING]);
-    const int16_t* c2 = R.cache + (int64_t)s_pcls[(first + rel2) % RING] * chunk;
-    const uint64_t tg = ptag(rel2);
-#pragma unroll
-    for (int k = 0; k < NPT; ++k) {
-      if ((tmask[k] >> lane) & 1ull) {
-        const int32_t j = k * RT + rt;
-        const int32_t rank = tabove[k] + __popcll((tmask[k] >> lane) >> 1);
-        const FRow r2 = plus(prow(R, j), F1);
-        uint32_t m;
-        const int32_t en = feval(EC, F2, r2, m);
-        const bool stop = r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM;
-        gstore(fslot(rel2, me, rank), fpack(tg, stop, (int32_t)c2[j], en));
-      }
-    }
-  };
-
-  int64_t stop_at = end;
-  uint64_t counter = *a.counter;  // replicated genericScheduler.lastNodeIndex (control wave)
-#ifdef KSIM_STAMPS
-  uint64_t st[8] = {};  // per wave: phase cycles summed over the pods (flushed at the end)
-  uint64_t tp = __builtin_amdgcn_s_memtime();
-#define PSTAMP(k)                                     \
-  do {                                                \
-    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
-    st[k] += t_ - tp;                                 \
-    tp = t_;                                          \
-  } while (0)
-#else
-#define PSTAMP(k) do { } while (0)
-#endif
-
-  if (wv > 0) {
-    // ---- prologue: A/B of the first two pods, candidates of the first, F of the second ----
-    if (w == PUB) {
-      publish_ab(0);
-      if (npods > 1) publish_ab(1);
-    }
-    rank_and_fix(0);
-    bool ok = true;
-    uint4 ring_next = make_uint4(0, 0, 0, 0);  // wave 1: descriptors of the next refill
-    int32_t ring_next_cl = 0;
-    auto ring_load = [&](int64_t p0, uint4& v, int32_t& cl) {
-      const int64_t p = p0 + lane / 8;
-      if (p < end) v = reinterpret_cast<const uint4*>(&a.pods[p])[lane % 8];
-      if (lane < RING_FILL && p0 + lane < end) cl = a.tcls[p0 + lane];
-    };
-    auto ring_store = [&](int64_t p0, const uint4& v, int32_t cl) {
-      const int64_t p = p0 + lane / 8;
-      if (p < end) reinterpret_cast<uint4*>(&s_pod[p % RING])[lane % 8] = v;
-      if (lane < RING_FILL && p0 + lane < end) s_pcls[(p0 + lane) % RING] = cl;
-    };
-    if (wv == 1) ring_load(first + 2 * RING_FILL, ring_next, ring_next_cl);
-    if (lane == 0) atomicAdd(&s_iter_done, 1);  // the prologue counts as iteration -1
-    PSTAMP(7);
-
-    // ---- row iterations: after decision rel ----
-    for (int32_t rel = 0; rel < npods; ++rel) {
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (seq_acquire(&s_dec_seq) < rel) {
-        if (past(t0) || seq_acquire(&s_stop)) { note(2, rel, seq_acquire(&s_dec_seq)); ok = false; break; }
-        __builtin_amdgcn_s_sleep(1);
-      }
-      if (!ok) break;
-      PSTAMP(0);  // waiting for the decision
-      const int32_t mode = s_dec[rel % DR][0], X = s_dec[rel % DR][1], rk = s_dec[rel % DR][2];
-      if (mode < 0) break;
-      if (wv == 1 && (rel % RING_FILL) == 0) {  // pods [rel + 16, rel + 24) into the ring
-        const int64_t p0 = first + rel + 2 * RING_FILL;
-        ring_store(p0, ring_next, ring_next_cl);
-        ring_load(p0 + RING_FILL, ring_next, ring_next_cl);
-      }
-      const int64_t pod = first + rel;
-      if (mode == 0 && a.collect && a.out_reasons) {
-        // FitError: the pod against this wave's rows as they stand
-        const FPod P = load_fpod(s_pod[pod % RING]);
-        uint32_t rms[NPT];
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-          const int32_t j = k * RT + rt;
-          rms[k] = 0;
-          if (j < nrows) (void)feval(EC, P, prow(R, j), rms[k]);
-        }
-        for (int r = 0; r < KSIM_NREASONS; ++r) {
-          int32_t nr = 0;
-#pragma unroll
-          for (int k = 0; k < NPT; ++k) nr += __popcll(__ballot((rms[k] >> r) & 1u));
-          if (lane == 0 && nr) atomicAdd(&a.out_reasons[pod * KSIM_NREASONS + r], nr);
-        }
-      }
-      if (mode == 2 && X == me) {
-        // ---- owner: the rk-th candidate from the top; commit, re-evaluate its row ----
-        int32_t seg = -1, bit = -1;
-#pragma unroll
-        for (int k = 0; k < NPT; ++k) {
-          const int32_t cnt = __popcll(tmask[k]);
-          if (rk >= tabove[k] && rk < tabove[k] + cnt) {
-            const int32_t want = rk - tabove[k];
-            const uint64_t hb = __ballot(((tmask[k] >> lane) & 1ull) && __popcll((tmask[k] >> lane) >> 1) == want);
-            seg = k;
-            bit = __builtin_ctzll(hb);
-          }
-        }
-        if (seg >= 0) {
-          const int32_t j = seg * RT + (w - 1) * 64 + bit;
-          // every row wave must have finished the previous iteration (they read this row)
-          const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-          while (seq_acquire(&s_iter_done) < RW * (rel + 1)) {
-            if (past(t1)) { note(3, rel, seq_acquire(&s_iter_done)); ok = false; break; }
-            __builtin_amdgcn_s_sleep(1);
-          }
-          const FRow r2 = plus(prow(R, j), load_fpod(s_pod[pod % RING]));
-          if (lane < K) {  // the row's evaluation for every class, and the histograms
-            uint32_t m;
-            const int32_t eo = R.cache[(int64_t)lane * chunk + j];
-            const int32_t en = feval(EC, cls_fpod(lane), r2, m);
-            R.cache[(int64_t)lane * chunk + j] = (int16_t)en;
-            const int sg = j >> 6;
-            if (eo >= 0) {
-              R.hseg[(lane * NSEG + sg) * NB + eo] -= 1;
-              R.hwg[lane * NB + eo] -= 1;
-            }
-            if (en >= 0) {
-              R.hseg[(lane * NSEG + sg) * NB + en] += 1;
-              R.hwg[lane * NB + en] += 1;
-            }
-            R.fitc[lane] += (en >= 0 ? 1 : 0) - (eo >= 0 ? 1 : 0);
-          }
-          if (lane == 0) {
-            R.rc[j] = r2.rc; R.rm[j] = r2.rm; R.zc[j] = r2.zc; R.zm[j] = r2.zm; R.count[j] = r2.count;
-            a.out_node[pod] = (int32_t)(lo + j);
-            if (r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM) atomicOr(a.err, 8);
-          }
-          seq_release(&s_commit_seq, rel);
-        } else {
-          const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-          while (seq_acquire(&s_commit_seq) < rel) {
-            if (past(t1)) { note(4, rel, rk); ok = false; break; }
-            __builtin_amdgcn_s_sleep(1);
-          }
-        }
-      }
-      if (!ok) break;
-      PSTAMP(1);  // reasons, commit / waiting for it
-      if (w == PUB && rel + 2 < npods) publish_ab(rel + 2);
-      PSTAMP(2);
-      if (rel + 1 < npods) rank_and_fix(rel + 1);
-      PSTAMP(3);
-      if (lane == 0) atomicAdd(&s_iter_done, 1);
-    }
-    if (!ok && lane == 0) { atomicOr(a.err, 2); atomicExch(&s_stop, 1); }
-  } else {
-    // ---------------- control wave: decide every pod ----------------
-    // A(rel) of every workgroup is in g[] (lane l: workgroups 4l .. 4l+3); after each decision the
-    // loads of A(rel + 1) and of the owner's B / F words go out together, the pre-decision over
-    // every workgroup but the owner overlaps the owner's words, then an O(1) post-decision.
-    int X = -1;      // owner workgroup of the previous pod's node (-1: none)
-    int32_t XR = 0;  // ... and the rank it took
-    const uint64_t* my_rep = Aw + (me % NREP) * REP_STRIDE;
-    uint64_t g[MAXB];
-    auto load_a = [&](int32_t rel) -> bool {  // spin until A(rel) of every workgroup is here
-      const uint64_t tag = ptag(rel);
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      for (;;) {
-#pragma unroll
-        for (int j = 0; j < MAXB; ++j) g[j] = gload(my_rep + (rel % NSLOT) * MAXG + j * 64 + lane);
-        bool mine = true;
-#pragma unroll
-        for (int j = 0; j < MAXB; ++j) mine &= (lane * MAXB + j >= G) || gtag(g[j]) == tag;
-        if (__all(mine)) return true;
-        if (past(t0) || seq_acquire(&s_stop)) {
-          int32_t miss = -1;
-#pragma unroll
-          for (int j = 0; j < MAXB; ++j)
-            if (lane * MAXB + j < G && gtag(g[j]) != tag) miss = lane * MAXB + j;
-          const uint64_t mb = __ballot(miss >= 0);
-          note(5, rel, mb ? __builtin_amdgcn_readlane(miss, __builtin_ctzll(mb)) : 999);
-          return false;
-        }
-        __builtin_amdgcn_s_sleep(1);
-      }
-    };
-    PSTAMP(7);
-    uint64_t spins = 0;
-    bool ok = load_a(0);
-    for (int32_t rel = 0; rel < npods; ++rel) {
-      const uint64_t tag = ptag(rel);
-      // the owner's words (address known since the last decision), in flight during the pre-decision
-      uint64_t bx = 0, fx = 0;
-      if (ok && X >= 0) {
-        bx = gload(Bw + (rel % NSLOT) * MAXG + X);
-        fx = gload(fslot(rel, X, XR));
-      }
-      // ---- pre-decision over every workgroup but X ----
-      int32_t cnt[MAXB];
-      int32_t f = 0, lm = -1;
-#pragma unroll
-      for (int j = 0; j < MAXB; ++j) {
-        const int b = lane * MAXB + j;
-        const bool v = b < G && b != X;
-        f += v ? gfit(g[j]) : 0;
-        lm = (v && gcnt(g[j]) && gscore(g[j]) > lm) ? gscore(g[j]) : lm;
-      }
-      const int32_t Fs = ksimw::sum_i32(f);
-      const int32_t Ms = ksimw::max_i32(lm);
-      int32_t tot = 0;
-#pragma unroll
-      for (int j = 0; j < MAXB; ++j) {
-        const int b = lane * MAXB + j;
-        cnt[j] = (b < G && b != X && gcnt(g[j]) && gscore(g[j]) == Ms) ? gcnt(g[j]) : 0;
-        tot += cnt[j];
-      }
-      const int32_t pre = ksimw::prefix_incl_i32(tot);
-      const int32_t Cs = __builtin_amdgcn_readlane(pre, 63);
-      const int32_t abv = Cs - pre;  // matches in workgroups of higher lanes
-      int32_t aboveX = 0;            // matches (at Ms) in workgroups above X
-      uint64_t ax = 0;
-      if (X >= 0) {
-        const int lx = X / MAXB, jx = X % MAXB;
-        int32_t part = 0;
-#pragma unroll
-        for (int j = 0; j < MAXB; ++j) part += j > jx ? cnt[j] : 0;
-        aboveX = __builtin_amdgcn_readlane(abv + part, lx);
-        ax = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)g[jx], lx) |
-             ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int32_t)(g[jx] >> 32), lx) << 32);
-      }
-      PSTAMP(2);  // pre-decision
-      // ---- the owner's corrected statistics ----
-      bool stop_any = false;
-      int32_t fX = 0, cX = 0, mX = -1;
-      if (ok && X >= 0) {
-        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        while (!(gtag(bx) == tag && gtag(fx) == tag)) {
-          if (past(t0) || seq_acquire(&s_stop)) { note(6, rel, X); ok = false; break; }
-#ifdef KSIM_STAMPS
-          spins += 1;
-#endif
-          __builtin_amdgcn_s_sleep(1);
-          bx = gload(Bw + (rel % NSLOT) * MAXG + X);
-          fx = gload(fslot(rel, X, XR));
-        }
-        const Stat3 s = fix_stats(gfit(ax), gscore(ax), gcnt(ax), bm2(bx), bc2(bx), feo(fx), fen(fx));
-        fX = s.f; cX = s.c; mX = s.m;
-        stop_any = fstop(fx);
-      }
-      PSTAMP(0);  // waiting for the owner's words
-      // ---- post-decision: findNodesThatFit count, max score, selectHost (generic_scheduler.go:136-198) ----
-      const int32_t F = Fs + fX;
-      const bool xtop = cX > 0 && (Cs == 0 || mX > Ms);   // X alone holds the maximum
-      const bool xeq = cX > 0 && Cs > 0 && mX == Ms;       // X shares it
-      const uint32_t C = (uint32_t)(xtop ? cX : Cs + (xeq ? cX : 0));
-      const uint32_t Cd = C ? C : 1u;
-      const int64_t ix = (counter >> 32) ? (int64_t)(counter % (uint64_t)Cd) : (int64_t)((uint32_t)counter % Cd);
-      int blk = -1, rank = 0;
-      int64_t t = ix;  // index among the other workgroups' matches, when X does not take it
-      if (xtop) {
-        blk = X; rank = (int)ix;
-      } else if (xeq && ix >= aboveX && ix < aboveX + cX) {
-        blk = X; rank = (int)(ix - aboveX);
-      } else if (xeq && ix >= aboveX + cX) {
-        t = ix - cX;
-      }
-      if (blk < 0 && C > 0) {
-        const bool hit = tot > 0 && t >= abv && t < abv + tot;
-        int32_t found = -1;
-        int64_t rr = t - abv;
-#pragma unroll
-        for (int j = MAXB - 1; j >= 0; --j) {
-          const bool here = found < 0 && rr < cnt[j];
-          found = here ? lane * MAXB + j : found;
-          rr = (found < 0) ? rr - cnt[j] : rr;
-        }
-        const uint64_t hb = __ballot(hit);
-        if (hb) {
-          const int src = __builtin_ctzll(hb);
-          blk = __builtin_amdgcn_readlane(found, src);
-          rank = __builtin_amdgcn_readlane((int32_t)rr, src);
-        }
-      }
-      int mode;
-      if (!ok) mode = -1;
-      else if (stop_any) mode = -2;  // the previous commit left the exact float64 range
-      else if (F == 0) mode = 0;
-      else mode = blk >= 0 ? 2 : -1;
-      if (mode == 2 && F > 1) counter += 1;  // generic_scheduler.go:192-195
-      if (lane == 0) {
-        if (mode == -1) atomicOr(a.err, ok ? 2 : 4);
-        if (mode == 0 && me == 0) a.out_node[first + rel] = -1;
-        s_dec[rel % DR][0] = mode; s_dec[rel % DR][1] = blk; s_dec[rel % DR][2] = rank;
-        seq_release(&s_dec_seq, rel);
-      }
-      PSTAMP(1);  // post-decision
-      if (mode < 0) {
-        if (mode == -2) stop_at = first + rel;
-        break;
-      }
-      X = mode == 2 ? blk : -1;
-      XR = rank;
-      if (rel + 1 < npods) ok = load_a(rel + 1);
-      PSTAMP(3);  // waiting for the next pod's A words
-    }
-#ifdef KSIM_STAMPS
-    st[6] = spins;
-#endif
-  }
-#ifdef KSIM_STAMPS
-  if (lane == 0 && (wv == 0 || wv == 1 || wv == RW)) {  // summed over the workgroups: control, first and last row wave
-    const int base = 16 + (wv == 0 ? 0 : wv == 1 ? 8 : 16);
-    for (int k = 0; k < 8; ++k) atomicAdd((unsigned long long*)&a.dbg[base + k], st[k]);
-  }
-#endif
+  if (wv > 0) pipe_rows<NPT>(&S);
+  else pipe_control(&S);
 
   // ---- the table is authoritative in HBM between calls: write the owned rows back ----
   __syncthreads();
@@ -642,8 +690,8 @@ __global__ __launch_bounds__(BS) void ksim_pipe_kernel(PpArgs a) {
     a.pod_count[i] = R.count[j];
   }
   if (me == 0 && tid == 0) {
-    *a.counter = counter;
-    *a.cursor = stop_at;
+    *a.counter = S.counter;
+    *a.cursor = S.stop_at;
   }
 }
 
