@@ -537,10 +537,10 @@ class ShardedScheduler(GenericScheduler):
 
     def __init__(self, cluster: Cluster, predicates, priorities, rank, world, device=0, collect_reasons=False,
                  last_node_index=0):
-        if collect_reasons:
-            # a rank's FitError histogram covers its own shard only ("0/n_shard nodes"), and the
-            # ranks' histograms are not summed: refuse rather than build a wrong FitError text
-            raise abi.KsimUnsupported(abi.E_UNSUPPORTED, "node-sharded scheduling does not collect FitError reasons")
+        """collect_reasons: each rank's schedule() returns, for every pod no node of the world fits,
+        the reason histogram of its own shard; merge_sharded_reasons sums the ranks' into the
+        FitError histogram over every node (generic_scheduler.go:51-90 builds FitError from the
+        failedPredicateMap of all nodes, :289-378, and every node lies in exactly one shard)."""
         n = cluster.n_nodes
         self.lo, self.hi = rank * n // world, (rank + 1) * n // world
         self.rank, self.world = rank, world
@@ -581,6 +581,13 @@ def connect_local_world(scheds):
 def merge_sharded(outs):
     """Per-rank ksim_schedule outputs (-2 = another rank's node) → global placements."""
     return np.max(np.stack(outs), axis=0)
+
+
+def merge_sharded_reasons(reasons):
+    """Per-rank FitError histograms ([pods][KSIM_NREASONS], each over its own shard) → the
+    histogram over every node: their sum.  Host-side, once per call (a torch.distributed
+    all_reduce(SUM) of the same arrays between processes)."""
+    return np.sum(np.stack([np.asarray(r, np.int64) for r in reasons]), axis=0).astype(np.int32)
 
 
 def _normalize(vals, reverse):

@@ -43,10 +43,18 @@ def _worker(rank, world, port, out_dir):
     out = np.where((ref >= a) & (ref < b), ref, np.where(ref < 0, -1, -2)).astype(np.int32)  # ksim_schedule's -2
     outs = D.gather(out)
     mx = D.allmax(float(rank + 1))
+    # sharded FitError histograms: each rank's shard histogram, summed across the ranks by an
+    # all_reduce(SUM) between processes equals merge_sharded_reasons of the gathered ones
+    import torch
+    hist = np.random.default_rng(100 + rank).integers(0, 50, size=(7, 16)).astype(np.int32)
+    t = torch.from_numpy(hist.astype(np.int64))
+    dist.all_reduce(t)
+    hists = D.gather(hist)
     D.barrier()
     if rank == 0:
         np.savez(os.path.join(out_dir, "res.npz"), scen=np.concatenate(allv), merged=scheduler.merge_sharded(outs),
-                 ref=ref, mx=mx, sub_n=sub.n_nodes)
+                 ref=ref, mx=mx, sub_n=sub.n_nodes, hsum=t.numpy(),
+                 hmerge=scheduler.merge_sharded_reasons(hists))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -66,3 +74,4 @@ def test_dist_split_and_merge_gloo(world, tmp_path):
     assert np.array_equal(r["scen"], want)
     assert np.array_equal(r["merged"], r["ref"])
     assert float(r["mx"]) == world
+    assert np.array_equal(r["hsum"], r["hmerge"])  # sharded FitError histograms: all_reduce == merge

@@ -465,19 +465,23 @@ def test_sweep_until_unschedulable_and_from_mid_queue(form, monkeypatch):
     assert (out < 0).any()  # the cluster fills up
 
 
-def _run_sharded_threads(cl, preds, prios, world, ranges):
+def _run_sharded_threads(cl, preds, prios, world, ranges, collect_reasons=False, reasons_out=None):
     """world ranks of a node-sharded scheduler on this one device, driven from threads (the
     kernels of all ranks must be co-resident: KSIM_MAX_GRID limits each to 256/world CUs)."""
     import threading
-    scheds = [scheduler.ShardedScheduler(cl, preds, prios, r, world) for r in range(world)]
+    scheds = [scheduler.ShardedScheduler(cl, preds, prios, r, world, collect_reasons=collect_reasons)
+              for r in range(world)]
     scheduler.connect_local_world(scheds)
     outs = [[] for _ in range(world)]
+    rs = [[] for _ in range(world)]
     for first, count in ranges:
         errs = []
 
         def go(r):
             try:
-                outs[r].append(scheds[r].schedule(first, count)[0])
+                o, re, _ = scheds[r].schedule(first, count)
+                outs[r].append(o)
+                rs[r].append(re)
             except Exception as e:  # noqa: BLE001 — surfaced below
                 errs.append(e)
         ts = [threading.Thread(target=go, args=(r,)) for r in range(world)]
@@ -487,6 +491,8 @@ def _run_sharded_threads(cl, preds, prios, world, ranges):
             t.join()
         assert not errs, errs
     merged = scheduler.merge_sharded([np.concatenate(o) for o in outs])
+    if reasons_out is not None:
+        reasons_out.append(scheduler.merge_sharded_reasons([np.concatenate(r) for r in rs]))
     return scheds, merged
 
 
@@ -526,6 +532,36 @@ def test_node_sharded_fills_cluster_with_fit_errors(monkeypatch):
     ref, _, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, prios), 0, 9000, threads=8)
     assert np.array_equal(merged, ref)
     assert (ref < 0).sum() > 1000
+    assert all(s.last_node_index == ref_ctr for s in scheds)
+
+
+@pytest.mark.parametrize("prios", [[("LeastRequestedPriority", 2), ("BalancedResourceAllocation", 1)],
+                                   [("LeastRequestedPriority", 1), ("NodeAffinityPriority", 1), ("TaintTolerationPriority", 1)]],
+                         ids=["fast", "reduce"])
+def test_node_sharded_fit_errors_match_c_oracle(prios, monkeypatch):
+    """FitError when node-sharded: every rank collects the reason histogram of its own shard for
+    the pods no node of the world fits, and their sum is the FitError histogram over all nodes
+    (generic_scheduler.go:51-90, 289-378) — placements, merged histograms and the FitError text
+    ("0/N nodes are available: ...") equal the C oracle's unsharded run, through the fast kernel
+    and the launch form's exchange (reduce priorities)."""
+    import cpu_ref
+    from ksim import synth
+    monkeypatch.setenv("KSIM_MAX_GRID", "40")
+    n = 301
+    cpu, mem = synth.c3_nodes(n, 17)
+    pcpu, pmem = synth.c3_pods(6000, 17)
+    cl = synth.resource_cluster(["s-%04d" % i for i in range(n)], cpu, mem, np.full(n, 12, np.int32), pcpu, pmem)
+    preds = list(scheduler.DEFAULT_PREDICATES)
+    got = []
+    scheds, merged = _run_sharded_threads(cl, preds, prios, 3, [(0, 3500), (3500, 2500)], collect_reasons=True,
+                                          reasons_out=got)
+    ref, ref_reasons, _, ref_ctr = cpu_ref.run(cl, scheduler.make_config(preds, prios), threads=8)
+    assert np.array_equal(merged, ref)
+    assert (ref < 0).sum() > 500
+    fail = ref < 0
+    assert np.array_equal(got[0][fail], ref_reasons[fail])
+    for k in np.nonzero(fail)[0][:50]:
+        assert scheduler.fit_error_message(n, got[0][k]) == scheduler.fit_error_message(n, ref_reasons[k])
     assert all(s.last_node_index == ref_ctr for s in scheds)
 
 
