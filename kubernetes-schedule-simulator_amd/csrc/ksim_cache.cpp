@@ -401,7 +401,8 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   // redundant decision in every block instead of the scan's last-block round trips.  Not for the
   // auxiliary priority / service-affinity lender tables, node sharding, > 60 spread zones or scores
   // beyond its 56-bit record words.  KSIM_NO_PICK=1 disables it.
-  if (cs.one && grid <= KSIM_PICK_MAXG && !getenv("KSIM_NO_PICK") && !ksim_rt_launch_tables(h) && c.sh_world <= 1 &&
+  const char* npk = getenv("KSIM_NO_PICK");
+  if (cs.one && grid <= KSIM_PICK_MAXG && !(npk && npk[0] == '1') && !ksim_rt_launch_tables(h) && c.sh_world <= 1 &&
       cs.one_pod.reserved[0] * cs.one_pod.reserved[1] <= KSIM_MAX_RCLASS &&
       (!h->have_aff || h->aff_h.n_zone <= KSIM_PICK_ZMAX)) {
     int64_t sw = 0;

@@ -48,7 +48,7 @@ extern "C" size_t ksim_shard_lx_offset(void);
 extern "C" size_t ksim_pfast_cache_bytes(int lds_rows, int ncls);
 extern "C" size_t ksim_pipe_lds_bytes(int lds_rows, int ncls, int nb);
 extern "C" size_t ksim_pipe_word_bytes(int grid, int lds_rows);
-extern "C" hipError_t ksim_launch_pipe(const KsimCtx* c, uint64_t* words, int grid, int lds_rows, const int32_t* tcls,
+extern "C" hipError_t ksim_launch_pipe(const KsimCtx* c, uint64_t* words, int grid, int lds_rows, int spec, const int32_t* tcls,
                                        const KsimTreeClass* tclass, int ncls, int nb, hipStream_t s);
 extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, double* mirror,
                                         const KsimShard* sh, const int32_t* tcls, const KsimTreeClass* tclass, int ncls,

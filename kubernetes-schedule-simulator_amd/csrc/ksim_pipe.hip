@@ -95,6 +95,11 @@ __device__ __forceinline__ uint64_t fpack(uint64_t tag, bool stop, int32_t eo, i
   return (tag << 56) | ((uint64_t)stop << 55) | ((uint64_t)(uint16_t)(int16_t)eo << 16) | (uint64_t)(uint16_t)(int16_t)en;
 }
 __device__ __forceinline__ bool fstop(uint64_t v) { return (v >> 55) & 1; }
+// revision bit of A / B (bit 55) and F (bit 54) words: 0 = published speculatively before the
+// decision of pod q-2 (as if this workgroup did not get pod q-2), 1 = republished by the owner of
+// pod q-2 after its commit.  A decider knows pod q-2's owner, so it knows which revision to take.
+__device__ __forceinline__ uint64_t arev(uint64_t v) { return (v >> 55) & 1; }
+__device__ __forceinline__ uint64_t frev(uint64_t v) { return (v >> 54) & 1; }
 __device__ __forceinline__ int32_t feo(uint64_t v) { return (int32_t)(int16_t)(uint16_t)(v >> 16); }
 __device__ __forceinline__ int32_t fen(uint64_t v) { return (int32_t)(int16_t)(uint16_t)v; }
 
@@ -137,6 +142,7 @@ struct PpArgs {
   const KsimTreeClass* tclass;
   int32_t ncls;
   int32_t nb;  // score bins: every map score is in [0, nb), nb <= 64
+  int32_t spec;  // 1: row work for pod rel + 2 is done before decision rel (revision bits); 0: after it
   uint64_t* counter;
   int64_t* cursor;
   int32_t* out_node;
@@ -276,7 +282,7 @@ __device__ __noinline__ void pipe_rows(PipeSh* Sp) {
 
   // the workgroup's (fit, max, count at max, second max, its count) for class c from the
   // histogram (lane b = bin b), published as A / B of pod rel by wave RW
-  auto publish_ab = [&](int32_t rel) {
+  auto publish_ab = [&](int32_t rel, uint64_t rev) {
     const int c = S.pcls[(first + rel) % RING];
     const int32_t h = lane < NB ? R.hwg[c * NB + lane] : 0;
     const uint64_t nz = __ballot(h > 0);
@@ -286,15 +292,17 @@ __device__ __noinline__ void pipe_rows(PipeSh* Sp) {
     const int32_t c1 = m1 >= 0 ? __builtin_amdgcn_readlane(h, m1) : 0;
     const int32_t c2 = m2 >= 0 ? __builtin_amdgcn_readlane(h, m2) : 0;
     const uint64_t tg = ptag(rel);
-    if (lane < NREP) gstore(aslot(a.words + lane * REP_STRIDE, rel, me), apack(tg, R.fitc[c], c1, m1));
-    if (lane == NREP) gstore(bword(a, rel, me), bpack(tg, m2, c2));
+    if (lane < NREP) gstore(aslot(a.words + lane * REP_STRIDE, rel, me), apack(tg, R.fitc[c], c1, m1) | (rev << 55));
+    if (lane == NREP) gstore(bword(a, rel, me), bpack(tg, m2, c2) | (rev << 55));
   };
   // candidate rows of pod rel1 (the rows at this workgroup's maximum of the pod's class, ranked
   // from the top) and, for each, pod rel1 + 1's evaluation before / after pod rel1 is committed
   // to it → F(rel1 + 1)
   uint64_t tmask[NPT];  // this wave's candidate rows of the pod being decided next, per segment
   int32_t tabove[NPT];  // candidates in the segments above each
-  auto rank_and_fix = [&](int32_t rel1) {
+  uint64_t tm_next[NPT];  // ... of the pod after it (the speculative / the owner's redo)
+  int32_t ta_next[NPT];
+  auto rank_and_fix = [&](int32_t rel1, uint64_t rev, uint64_t (&tmask)[NPT], int32_t (&tabove)[NPT]) {
     const int c1 = S.pcls[(first + rel1) % RING];
     const int32_t h = lane < NB ? R.hwg[c1 * NB + lane] : 0;
     const uint64_t nz = __ballot(h > 0);
@@ -325,36 +333,31 @@ __device__ __noinline__ void pipe_rows(PipeSh* Sp) {
         uint32_t m;
         const int32_t en = feval(EC, F2, r2, m);
         const bool stop = r2.rc >= EXACT_LIM || r2.rm >= EXACT_LIM || r2.zc >= EXACT_LIM || r2.zm >= EXACT_LIM;
-        gstore(fslot(a, rel2, me, rank), fpack(tg, stop, (int32_t)c2[j], en));
+        gstore(fslot(a, rel2, me, rank), fpack(tg, stop, (int32_t)c2[j], en) | (rev << 54));
       }
     }
-  };
-  auto ring_load = [&](int64_t p0, uint4& v, int32_t& cl) {
-    const int64_t p = p0 + lane / 8;
-    if (p < end) v = reinterpret_cast<const uint4*>(&a.pods[p])[lane % 8];
-    if (lane < RING_FILL && p0 + lane < end) cl = a.tcls[p0 + lane];
-  };
-  auto ring_store = [&](int64_t p0, const uint4& v, int32_t cl) {
-    const int64_t p = p0 + lane / 8;
-    if (p < end) reinterpret_cast<uint4*>(&S.pod[p % RING])[lane % 8] = v;
-    if (lane < RING_FILL && p0 + lane < end) S.pcls[(p0 + lane) % RING] = cl;
   };
 
   // ---- prologue: A/B of the first two pods, candidates of the first, F of the second ----
   if (w == RW) {
-    publish_ab(0);
-    if (npods > 1) publish_ab(1);
+    publish_ab(0, 0);
+    if (npods > 1) publish_ab(1, 0);
   }
-  rank_and_fix(0);
+  rank_and_fix(0, 0, tmask, tabove);
   bool ok = true;
-  uint4 ring_next = make_uint4(0, 0, 0, 0);  // wave 1: descriptors of the next refill
-  int32_t ring_next_cl = 0;
-  if (w == 1) ring_load(first + 2 * RING_FILL, ring_next, ring_next_cl);
   if (lane == 0) atomicAdd(&S.iter_done, 1);  // the prologue counts as iteration -1
   PSTAMP(7);
 
-  // ---- row iterations: after decision rel ----
+  // ---- row iterations ----
+  // Before decision rel is known, every wave does pod rel + 2's work as if this workgroup does not
+  // get pod rel (A / B(rel + 2), the candidates of pod rel + 1 and F(rel + 2), revision 0): only
+  // pod rel's owner changes, and it redoes that work after its commit (revision 1).  So for every
+  // workgroup but one the per-pod row work is off the critical path.
   for (int32_t rel = 0; rel < npods; ++rel) {
+    if (a.spec && w == RW && rel + 2 < npods) publish_ab(rel + 2, 0);
+    if (a.spec && rel + 1 < npods) rank_and_fix(rel + 1, 0, tm_next, ta_next);
+    if (lane == 0) atomicAdd(&S.iter_done, 1);  // this iteration's speculative reads are done
+    PSTAMP(2);  // the speculative work
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     while (seq_acquire(&S.dec_seq) < rel) {
       if (past(t0) || seq_acquire(&S.stop)) { note(a, 2, rel, seq_acquire(&S.dec_seq)); ok = false; break; }
@@ -365,13 +368,6 @@ __device__ __noinline__ void pipe_rows(PipeSh* Sp) {
     const int32_t mode = S.dec[rel % DR][0], X = S.dec[rel % DR][1], rk = S.dec[rel % DR][2];
     if (mode < 0) break;
     const bool own = mode == 2 && X == me;
-    // not the owner: this workgroup's statistics of pod rel + 2 are final already — publish first
-    if (!own && w == RW && rel + 2 < npods) publish_ab(rel + 2);
-    if (w == 1 && (rel % RING_FILL) == 0) {  // pods [rel + 16, rel + 24) into the ring
-      const int64_t p0 = first + rel + 2 * RING_FILL;
-      ring_store(p0, ring_next, ring_next_cl);
-      ring_load(p0 + RING_FILL, ring_next, ring_next_cl);
-    }
     const int64_t pod = first + rel;
     if (mode == 0 && a.collect && a.out_reasons) {
       // FitError: the pod against this wave's rows as they stand
@@ -405,9 +401,9 @@ __device__ __noinline__ void pipe_rows(PipeSh* Sp) {
       }
       if (seg >= 0) {
         const int32_t j = seg * RT + (w - 1) * 64 + bit;
-        // every row wave must have finished the previous iteration (they read this row)
+        // every row wave must have finished this iteration's speculative reads (they read this row)
         const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
-        while (seq_acquire(&S.iter_done) < RW * (rel + 1)) {
+        while (seq_acquire(&S.iter_done) < RW * (rel + 2)) {
           if (past(t1)) { note(a, 3, rel, seq_acquire(&S.iter_done)); ok = false; break; }
           __builtin_amdgcn_s_sleep(1);
         }
@@ -441,13 +437,17 @@ __device__ __noinline__ void pipe_rows(PipeSh* Sp) {
           __builtin_amdgcn_s_sleep(1);
         }
       }
-      if (ok && w == RW && rel + 2 < npods) publish_ab(rel + 2);
     }
     if (!ok) break;
-    PSTAMP(1);  // reasons, commit / waiting for it, publish
-    if (rel + 1 < npods) rank_and_fix(rel + 1);
-    PSTAMP(3);
-    if (lane == 0) atomicAdd(&S.iter_done, 1);
+    if (own || !a.spec) {
+      // pod rel + 2's work on the committed rows: the owner's redo (revision 1), or everyone's
+      const uint64_t rv = a.spec ? 1ull : 0ull;
+      if (w == RW && rel + 2 < npods) publish_ab(rel + 2, rv);
+      if (rel + 1 < npods) rank_and_fix(rel + 1, rv, tm_next, ta_next);
+    }
+    PSTAMP(1);  // reasons, commit / waiting for it, the owner's redo
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) { tmask[k] = tm_next[k]; tabove[k] = ta_next[k]; }
   }
   if (!ok && lane == 0) { atomicOr(a.err, 2); atomicExch(&S.stop, 1); }
   if (w == 1) PFLUSH(24);
@@ -466,7 +466,14 @@ __device__ __noinline__ void pipe_control(PipeSh* Sp) {
   const int me = blockIdx.x;
   const int64_t first = a.first;
   const int32_t npods = (int32_t)(a.end - first);
-  uint64_t counter = *a.counter;  // replicated genericScheduler.lastNodeIndex
+  // replicated genericScheduler.lastNodeIndex, uniform: read into scalar registers at once (a
+  // vector register still pending from this load would make every later wait conservative)
+  uint64_t counter;
+  {
+    const uint64_t c0 = *a.counter;
+    counter = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(c0 >> 32)) << 32) |
+              (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)c0);
+  }
   int64_t stop_at = a.end;
 #ifdef KSIM_STAMPS
   uint64_t st[8] = {};
@@ -476,40 +483,116 @@ __device__ __noinline__ void pipe_control(PipeSh* Sp) {
   __builtin_amdgcn_s_setprio(2);  // the per-pod critical path: ahead of the row wave sharing this SIMD
   int X = -1;      // owner workgroup of the previous pod's node (-1: none)
   int32_t XR = 0;  // ... and the rank it took
+  int X2 = -1;     // owner workgroup of the pod before that: its words of this pod are revision 1
   const uint64_t* my_rep = a.words + (me % NREP) * REP_STRIDE;
   uint64_t g[MAXB];
-  auto load_a = [&](int32_t rel) -> bool {  // spin until A(rel) of every workgroup is here
+  // The pod-descriptor ring is refilled here, not by the row waves: a row wave that carried
+  // prefetched descriptors across its loop would wait (s_waitcnt vmcnt(0), stores included) for
+  // its own write-through stores at every iteration.  Every RING_FILL pods, pods [rel + 15,
+  // rel + 23) go out with the A loads of pod rel and land in LDS once they are back (the row
+  // waves read pods <= their pod + 2 and lag the decisions by <= 2 pods).
+  // A(rel + 1) is prefetched once pod rel's owner words are in — by then the row work that
+  // publishes it (after decision rel - 1) is normally done — so its load latency overlaps pod
+  // rel's post-decision; a stale prefetch falls back to polling.
+  uint64_t gn[MAXB];
+  uint64_t rv0 = 0, rv1 = 0;  // a 16-byte quarter of a pod descriptor (lane / 8: pod, lane % 8: quarter)
+  int32_t rcl = 0;
+  const uint64_t* rq = reinterpret_cast<const uint64_t*>(a.pods);
+  const int32_t* rt = a.tcls;
+  bool pf_refill = false;
+  int64_t pf_p0 = 0;
+  // the prefetch's address stays live until its data is taken: a VGPR that addresses a load in
+  // flight is not rewritten before the load returns (the compiler would wait for it there)
+  const uint64_t* pf_addr = my_rep + lane;
+  auto prefetch_a = [&](int32_t rel) {
+    pf_refill = ((rel - 1) % RING_FILL) == 0;  // (rel >= 1: the prologue staged pods [first, first + 16))
+    pf_p0 = first + rel + 2 * RING_FILL - 1;
+    if (pf_refill) {  // (asm loads like the A prefetch below, waited for in take_a; clamped addresses)
+      const int64_t pp = pf_p0 + lane / 8 < a.end ? pf_p0 + lane / 8 : a.end - 1;
+      rq = reinterpret_cast<const uint64_t*>(&a.pods[pp]) + 2 * (lane % 8);
+      rt = a.tcls + (pf_p0 + (lane % RING_FILL) < a.end ? pf_p0 + (lane % RING_FILL) : a.end - 1);
+      asm volatile(
+          "global_load_dwordx2 %0, %3, off\n\t"
+          "global_load_dwordx2 %1, %3, off offset:8\n\t"
+          "global_load_dword %2, %4, off"
+          : "=&v"(rv0), "=&v"(rv1), "=&v"(rcl)
+          : "v"(rq), "v"(rt)
+          : "memory");
+    }
+    pf_addr = my_rep + (rel % NSLOT) * MAXG + lane;
+    // the four A loads as one asm block: the compiler does not track them, so its conservative
+    // waits in the post-decision (a 64-bit modulo, joins) do not wait for them; take_a waits
+    // explicitly, with the destinations as in/out operands so nothing reads them earlier
+    static_assert(MAXB == 4, "the prefetch asm loads four granules per lane");
+    asm volatile(
+        "global_load_dwordx2 %0, %4, off sc1\n\t"
+        "global_load_dwordx2 %1, %4, off offset:512 sc1\n\t"
+        "global_load_dwordx2 %2, %4, off offset:1024 sc1\n\t"
+        "global_load_dwordx2 %3, %4, off offset:1536 sc1"
+        : "=&v"(gn[0]), "=&v"(gn[1]), "=&v"(gn[2]), "=&v"(gn[3])
+        : "v"(pf_addr)
+        : "memory");
+  };
+  auto tags_ok = [&](const uint64_t (&v)[MAXB], uint64_t tag) -> bool {
+    bool mine = true;
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) {
+      const int b = lane * MAXB + j;
+      mine &= (b >= G) || (gtag(v[j]) == tag && arev(v[j]) == (b == X2 ? 1ull : 0ull));
+    }
+    return __all(mine);
+  };
+  auto take_a = [&](int32_t rel) -> bool {  // the prefetched A(rel), or poll until every workgroup's is here
     const uint64_t tag = ptag(rel);
+    asm volatile("s_waitcnt vmcnt(0)" : "+v"(gn[0]), "+v"(gn[1]), "+v"(gn[2]), "+v"(gn[3]), "+v"(rv0), "+v"(rv1), "+v"(rcl)
+                 : "v"(pf_addr), "v"(rq), "v"(rt) : "memory");
+    if (pf_refill) {
+      if (pf_p0 + lane / 8 < a.end) {
+        uint64_t* d = reinterpret_cast<uint64_t*>(&S.pod[(pf_p0 + lane / 8) % RING]) + 2 * (lane % 8);
+        d[0] = rv0;
+        d[1] = rv1;
+      }
+      if (lane < RING_FILL && pf_p0 + lane < a.end) S.pcls[(pf_p0 + lane) % RING] = rcl;
+    }
+#pragma unroll
+    for (int j = 0; j < MAXB; ++j) g[j] = gn[j];
+    if (tags_ok(g, tag)) return true;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
+      __builtin_amdgcn_s_sleep(1);
 #pragma unroll
-      for (int j = 0; j < MAXB; ++j) g[j] = gload(my_rep + (rel % NSLOT) * MAXG + j * 64 + lane);
-      bool mine = true;
-#pragma unroll
-      for (int j = 0; j < MAXB; ++j) mine &= (lane * MAXB + j >= G) || gtag(g[j]) == tag;
-      if (__all(mine)) return true;
+      for (int j = 0; j < MAXB; ++j) g[j] = gload(pf_addr + j * 64);
+      if (tags_ok(g, tag)) return true;
       if (past(t0) || seq_acquire(&S.stop)) {
         int32_t miss = -1;
 #pragma unroll
         for (int j = 0; j < MAXB; ++j)
-          if (lane * MAXB + j < G && gtag(g[j]) != tag) miss = lane * MAXB + j;
+          if (lane * MAXB + j < G && (gtag(g[j]) != tag || arev(g[j]) != (lane * MAXB + j == X2 ? 1ull : 0ull)))
+            miss = lane * MAXB + j;
         const uint64_t mb = __ballot(miss >= 0);
         note(a, 5, rel, mb ? __builtin_amdgcn_readlane(miss, __builtin_ctzll(mb)) : 999);
         return false;
       }
-      __builtin_amdgcn_s_sleep(1);
     }
   };
   PSTAMP(7);
-  bool ok = load_a(0);
+  prefetch_a(0);
+  bool ok = take_a(0);
   for (int32_t rel = 0; rel < npods; ++rel) {
     const uint64_t tag = ptag(rel);
     // the owner's words (address known since the last decision), in flight during the pre-decision
     uint64_t bx = 0, fx = 0;
-    if (ok && X >= 0) {
-      bx = gload(bword(a, rel, X));
-      fx = gload(fslot(a, rel, X, XR));
-    }
+    const uint64_t* pbx = bword(a, rel, X >= 0 ? X : 0);
+    const uint64_t* pfx = fslot(a, rel, X >= 0 ? X : 0, XR);
+    // (asm loads like the A prefetch: the compiler's conservative waits never hold them)
+    auto owner_loads = [&]() {
+      asm volatile("global_load_dwordx2 %0, %2, off sc1\n\tglobal_load_dwordx2 %1, %3, off sc1"
+                   : "=&v"(bx), "=&v"(fx) : "v"(pbx), "v"(pfx) : "memory");
+    };
+    auto owner_wait = [&]() {
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(bx), "+v"(fx) : "v"(pbx), "v"(pfx) : "memory");
+    };
+    if (ok && X >= 0) owner_loads();
     // ---- pre-decision over every workgroup but X ----
     int32_t cnt[MAXB];
     int32_t f = 0, lm = -1;
@@ -549,20 +632,23 @@ __device__ __noinline__ void pipe_control(PipeSh* Sp) {
     int32_t fX = 0, cX = 0, mX = -1;
     if (ok && X >= 0) {
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-      while (!(gtag(bx) == tag && gtag(fx) == tag)) {
+      owner_wait();
+      const uint64_t xrev = X == X2 ? 1ull : 0ull;  // (its words of this pod were redone after pod rel-2's commit)
+      while (!(gtag(bx) == tag && gtag(fx) == tag && arev(bx) == xrev && frev(fx) == xrev)) {
         if (past(t0) || seq_acquire(&S.stop)) { note(a, 6, rel, X); ok = false; break; }
 #ifdef KSIM_STAMPS
         spins += 1;
 #endif
         __builtin_amdgcn_s_sleep(1);
-        bx = gload(bword(a, rel, X));
-        fx = gload(fslot(a, rel, X, XR));
+        owner_loads();
+        owner_wait();
       }
       const Stat3 s = fix_stats(gfit(ax), gscore(ax), gcnt(ax), bm2(bx), bc2(bx), feo(fx), fen(fx));
       fX = s.f; cX = s.c; mX = s.m;
       stop_any = fstop(fx);
     }
     PSTAMP(0);  // waiting for the owner's words
+    if (rel + 1 < npods) prefetch_a(rel + 1);
     // ---- post-decision: findNodesThatFit count, max score, selectHost (generic_scheduler.go:136-198) ----
     const int32_t F = Fs + fX;
     const bool xtop = cX > 0 && (Cs == 0 || mX > Ms);  // X alone holds the maximum
@@ -606,16 +692,19 @@ __device__ __noinline__ void pipe_control(PipeSh* Sp) {
       if (mode == -1) atomicOr(a.err, ok ? 2 : 4);
       if (mode == 0 && me == 0) a.out_node[first + rel] = -1;
       S.dec[rel % DR][0] = mode; S.dec[rel % DR][1] = blk; S.dec[rel % DR][2] = rank;
-      seq_release(&S.dec_seq, rel);
+      // release for the LDS words only (a full release would wait for the A prefetch in flight)
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      __hip_atomic_store(&S.dec_seq, rel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
     PSTAMP(1);  // post-decision
     if (mode < 0) {
       if (mode == -2) stop_at = first + rel;
       break;
     }
+    X2 = a.spec ? X : -1;
     X = mode == 2 ? blk : -1;
     XR = rank;
-    if (rel + 1 < npods) ok = load_a(rel + 1);
+    if (rel + 1 < npods) ok = take_a(rel + 1);
     PSTAMP(3);  // waiting for the next pod's A words
   }
   __builtin_amdgcn_s_setprio(0);
@@ -712,7 +801,7 @@ extern "C" size_t ksim_pipe_word_bytes(int grid, int lds_rows) {
   return ((size_t)NREP * REP_STRIDE + (size_t)NSLOT * MAXG + (size_t)NSLOT * grid * lds_rows) * sizeof(uint64_t);
 }
 
-extern "C" hipError_t ksim_launch_pipe(const KsimCtx* c, uint64_t* words, int grid, int lds_rows, const int32_t* tcls,
+extern "C" hipError_t ksim_launch_pipe(const KsimCtx* c, uint64_t* words, int grid, int lds_rows, int spec, const int32_t* tcls,
                                        const KsimTreeClass* tclass, int ncls, int nb, hipStream_t s) {
   const size_t lds = ksim_pipe_lds_bytes(lds_rows, ncls, nb);
   if (!lds || grid <= 0 || grid > MAXG || (int64_t)grid * lds_rows < c->n) return hipErrorInvalidValue;
@@ -720,7 +809,7 @@ extern "C" hipError_t ksim_launch_pipe(const KsimCtx* c, uint64_t* words, int gr
   a.n = c->n; a.chunk = lds_rows; a.first = c->first; a.end = c->end;
   a.alloc_cpu = c->alloc_cpu; a.alloc_mem = c->alloc_mem; a.allowed_pods = c->allowed_pods; a.flags = c->flags;
   a.req_cpu = c->req_cpu; a.req_mem = c->req_mem; a.nz_cpu = c->nz_cpu; a.nz_mem = c->nz_mem;
-  a.pod_count = c->pod_count; a.pods = c->pods; a.tcls = tcls; a.tclass = tclass; a.ncls = ncls; a.nb = nb;
+  a.pod_count = c->pod_count; a.pods = c->pods; a.tcls = tcls; a.tclass = tclass; a.ncls = ncls; a.nb = nb; a.spec = spec;
   a.counter = c->counter; a.cursor = c->cursor;
   a.out_node = c->out_node; a.out_reasons = c->out_reasons; a.err = c->err; a.dbg = c->dbg; a.words = words;
   a.preds = c->preds; a.no_prio = c->no_prio; a.collect = c->collect;

@@ -682,6 +682,8 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
   const bool pipe = ncls > 0 && h->shard.world == 1 && pe && pe[0] == '1' && nb <= 64 &&
                     ksim_pipe_lds_bytes(lds_rows, ncls, nb) && (int64_t)grid * lds_rows >= c.n;
   h->last_pfast_pipe = pipe;
+  const char* pse = getenv("KSIM_PIPE_SPEC");  // speculative row work before each decision (experimental)
+  const int pipe_spec = pse && pse[0] == '1';
   if (pipe) {
     const size_t wb = ksim_pipe_word_bytes(grid, lds_rows);
     if (h->pipe_bytes < wb) {
@@ -698,7 +700,7 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
     HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
   }
   HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipError_t e = pipe ? ksim_launch_pipe(&c, h->pipe_words, grid, lds_rows, h->tcls, h->tclass, ncls, nb, h->stream)
+  hipError_t e = pipe ? ksim_launch_pipe(&c, h->pipe_words, grid, lds_rows, pipe_spec, h->tcls, h->tclass, ncls, nb, h->stream)
                       : ksim_launch_pfast(&c, h->granules, grid, lds_rows, stream ? h->mirror : nullptr, &h->shard,
                                           h->tcls, h->tclass, ncls, h->stream);
   if (e == hipErrorCooperativeLaunchTooLarge) {
@@ -723,8 +725,8 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
     if (h->last_pfast_pipe) {
       const double np = (double)count * grid;
       fprintf(stderr, "[ksim stamps] pipe pods=%lld (%.3f ms, %.3f us/pod) per pod, mean over workgroups: control pre %.0f "
-              "owner-wait %.0f post %.0f A-wait %.0f owner-retries %.2f prologue %.0f | wave1 wait %.0f commit %.0f spec %.0f "
-              "rank+fix %.0f | wave7 wait %.0f commit %.0f spec %.0f rank+fix %.0f\n",
+              "owner-wait %.0f post %.0f A-wait %.0f owner-retries %.2f prologue %.0f | wave1 wait %.0f after-decision %.0f "
+              "speculative %.0f - %.0f | wave7 wait %.0f after-decision %.0f speculative %.0f - %.0f\n",
               (long long)count, ms, 1000.0 * ms / (double)count, d[18] / np, d[16] / np, d[17] / np, d[19] / np, d[22] / np,
               d[23] / (double)grid,
               d[24] / np, d[25] / np, d[26] / np, d[27] / np, d[32] / np, d[33] / np, d[34] / np, d[35] / np);
