@@ -431,7 +431,9 @@ def main():
         data = "synthetic (random.Random seed 2 objects through ingest, SURVEY.md §8d C2)"
     n = cl.n_nodes
     mode = {"auto": abi.MODE_AUTO, "launch": abi.MODE_LAUNCH, "persistent": abi.MODE_PERSISTENT, "tree": abi.MODE_TREE}[a.mode]
-    sharded_head = world > 1 and a.shard == "nodes" and a.workload not in ("c2", "c2x")  # sharding: resource-only pods
+    # node sharding takes every workload's pods: Phase A (reduce-class maxima, inter-pod affinity
+    # min / max, spread maxima and zone sums) is exchanged across the ranks
+    sharded_head = world > 1 and a.shard == "nodes"
 
     # ---- the one cluster: single GPU (N = 1), or node-sharded across the N ranks ----
     single = None
@@ -445,7 +447,7 @@ def main():
         sharded = node_sharded(a, D, cl, preds, prios)
         head = sharded
     replicas = None
-    if world > 1 and a.shard != "none" and not (a.shard == "replicas" or a.workload in ("c2", "c2x")):
+    if world > 1 and a.shard != "none" and a.shard != "replicas":
         # side line: each rank its own cluster under its own LeastRequested weight (weak scaling)
         prios_r = [(k, w + rank) if k == "LeastRequestedPriority" else (k, w) for k, w in prios]
         r_args = argparse.Namespace(**vars(a))

@@ -255,7 +255,7 @@ extern "C" int ksim_load_affinity(ksim_handle* h, const ksim_affinity_tables* t)
   A.carry_words = t->carry_words;
   KsimAff* dev;
   if ((rc = dev_upload(h, &dev, &A, 1))) return rc;
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   for (void* q : h->aff_bufs) dev_free(h, q);  // the previous tables (reload)
   h->aff_bufs.clear();
   for (size_t k = nb0; k < h->bufs.size(); ++k) h->aff_bufs.push_back(h->bufs[k].p);

@@ -67,7 +67,7 @@ int ensure_staging(ksim_handle* h, int32_t n_ports, int32_t n_scalars) {
   char* d = nullptr;
   HIPCHK(h, hipHostGetDevicePointer((void**)&d, hst, 0));
   if (h->stg_host) {  // every earlier call has synchronised its stream
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
     (void)hipHostFree(h->stg_host);
   }
   memset(hst, 0, cap);
@@ -79,6 +79,17 @@ int ensure_staging(ksim_handle* h, int32_t n_ports, int32_t n_scalars) {
   return KSIM_OK;
 }
 
+// The pod as the per-pod kernels take it: offsets rebased to its own arrays, its reduce-class
+// dimensions in reserved[] (as ksim_launch_pod_k does for the queue).
+ksim_pod staged_pod(const ksim_handle* h, const ksim_pod& pod) {
+  ksim_pod p = pod;
+  p.port_off = 0;
+  p.scalar_off = 0;
+  p.reserved[0] = h->ctx.w[KSIM_W_TAINT_TOLERATION] ? h->h_n_tt[p.cls] : 1;
+  p.reserved[1] = h->ctx.use_na ? h->h_n_na[p.cls] : 1;
+  return p;
+}
+
 // Stage one pod: {cursor = 0, zeroed result block, pod (offsets rebased to the staged arrays),
 // ports, scalars} in one copy, and the context that points the scan / commit kernels at it.
 int stage_pod(ksim_handle* h, const ksim_pod& pod, const uint64_t* ports, const ksim_scalar_req* scalars,
@@ -87,11 +98,7 @@ int stage_pod(ksim_handle* h, const ksim_pod& pod, const uint64_t* ports, const 
   if (rc) return rc;
   char* hs = h->stg_host;
   memset(hs, 0, STG_POD);
-  ksim_pod p = pod;
-  p.port_off = 0;
-  p.scalar_off = 0;
-  p.reserved[0] = h->ctx.w[KSIM_W_TAINT_TOLERATION] ? h->h_n_tt[p.cls] : 1;  // ksim_launch_pod_k
-  p.reserved[1] = h->ctx.use_na ? h->h_n_na[p.cls] : 1;
+  const ksim_pod p = staged_pod(h, pod);
   memcpy(hs + STG_POD, &p, sizeof p);
   const size_t pb = (size_t)pod.port_cnt * 8, sb = (size_t)pod.scalar_cnt * sizeof(ksim_scalar_req);
   if (pb) memcpy(hs + STG_PORTS, ports + pod.port_off, pb);
@@ -165,9 +172,9 @@ int relayout(ksim_handle* h, const std::vector<ColRef>& cols, const std::vector<
     }
     r.col[r.ncol++] = KsimRelayCol{*cols[k].p, fresh[k], cols[k].esz, cols[k].slots, ds, 0};
   }
-  hipError_t e = ksim_launch_relayout(&r, h->stream);
+  hipError_t e = ksim_launch_relayout(&r, ksim_stream(h));
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "relayout launch: %s", hipGetErrorString(e));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   for (size_t k = 0; k < cols.size(); ++k) {
     dev_free(h, *cols[k].p);
     *cols[k].p = fresh[k];
@@ -196,9 +203,9 @@ int ensure_port_room(ksim_handle* h, int32_t need) {
   if (c.n > 0) {
     int rc = ensure_staging(h, 0, 0);
     if (rc) return rc;
-    hipError_t e = ksim_launch_port_max(c.port_count, c.n, h->res_dev + KSIM_RES_STATUS, h->stream);
+    hipError_t e = ksim_launch_port_max(c.port_count, c.n, h->res_dev + KSIM_RES_STATUS, ksim_stream(h));
     if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "port max: %s", hipGetErrorString(e));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
     h->port_bound = h->res_host[KSIM_RES_STATUS];
   } else {
     h->port_bound = 0;
@@ -235,17 +242,156 @@ bool ksim_is_aff_host(const ksim_handle* h, const ksim_pod& p) {
   return h->have_aff && (p.aff_ident || p.aff_class);
 }
 
-int after_commit(ksim_handle* h, int32_t port_cnt) {
+int after_commit(ksim_handle* h, int32_t port_cnt, const int32_t* r = nullptr) {
+  if (!r) r = h->res_host;
   h->tree_valid = false;  // the trees are maintained by the tree kernel only
-  const int32_t status = h->res_host[KSIM_RES_STATUS];
+  const int32_t status = r[KSIM_RES_STATUS];
   if (status & 2)  // the committing kernel reported the row's port count: the bound stays exact
     h->port_bound = std::max<int64_t>(h->port_bound, (int64_t)(status >> 8));
   else
     h->port_bound += port_cnt;
-  if (h->res_host[KSIM_RES_STATUS] & 1) h->pfast_off = true;  // keep the fast kernels' float64 range
-  const int32_t err = h->res_host[KSIM_RES_ERR];  // written by the committing kernel
+  if (status & 1) h->pfast_off = true;  // keep the fast kernels' float64 range
+  const int32_t err = r[KSIM_RES_ERR];  // written by the committing kernel
   if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port or volume slots overflowed (raise port_slots / vol_slots)");
   if (err & ~1) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
+  return KSIM_OK;
+}
+
+// ---- the resident per-pod service (ksim_serve_kernel in ksim_kernels.hip) ----
+// The kernel leaves after SERVE_IDLE_TICKS without a message; the host posts a message only within
+// SERVE_POST_NS of its previous post (or of the launch) and otherwise stops and relaunches it, so a
+// message never meets a grid that is on its way out.  KSIM_SERVE=0: per-pod launches only.
+constexpr uint64_t SERVE_IDLE_TICKS = 20000000ull;       // 200 ms of s_memrealtime (100 MHz)
+constexpr int64_t SERVE_POST_NS = 100000000;             // 100 ms
+constexpr int64_t SERVE_WAIT_NS = 10000000000ll;         // an answer's bound (the kernel's spins end in 2 s)
+
+int64_t now_ns() {
+  return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+bool serve_wanted(const ksim_handle* h) {
+  static const bool env_off = getenv("KSIM_SERVE") && getenv("KSIM_SERVE")[0] == '0';
+  return !env_off && !h->serve_off;
+}
+
+size_t serve_stage_bytes(int grid) {
+  return (size_t)grid * (sizeof(ksim_pod) + 8 * KSIM_ONE_PORTS + sizeof(ksim_scalar_req) * KSIM_MAX_SCALAR);
+}
+
+int serve_start(ksim_handle* h, int npt, int grid) {
+  if (!h->serve_box) {
+    KsimServeBox* b = nullptr;
+    HIPCHK(h, hipHostMalloc((void**)&b, sizeof(KsimServeBox), hipHostMallocMapped | hipHostMallocCoherent));
+    memset((void*)b, 0, sizeof *b);
+    KsimServeBox* d = nullptr;
+    HIPCHK(h, hipHostGetDevicePointer((void**)&d, b, 0));
+    h->serve_box = b;
+    h->serve_box_dev = d;
+    b->done = h->serve_seq;
+  }
+  if (h->serve_grid < grid || !h->serve_stage) {
+    dev_free(h, h->serve_stage);
+    h->serve_stage = nullptr;
+    int rc = dev_alloc(h, &h->serve_stage, serve_stage_bytes(grid));
+    if (rc) return rc;
+  }
+  KsimCtx cs = h->ctx;
+  cs.one = 0;  // the pod comes from the mailbox, through each block's staging slot
+  cs.pods = reinterpret_cast<const ksim_pod*>(h->serve_stage);
+  cs.pod_ports = reinterpret_cast<const uint64_t*>(h->serve_stage + (size_t)grid * sizeof(ksim_pod));
+  cs.pod_scalars = reinterpret_cast<const ksim_scalar_req*>(h->serve_stage + (size_t)grid * (sizeof(ksim_pod) + 8 * KSIM_ONE_PORTS));
+  cs.chunk = (int64_t)KSIM_BLOCK * npt;
+  cs.collect = 1;
+  cs.first = 0;
+  cs.end = 1;
+  cs.pick = h->pick_words;
+  KsimServeBox* bd = h->serve_box_dev;
+  cs.out_node = bd->res + KSIM_RES_NODE;
+  cs.out_fit = bd->res + KSIM_RES_FIT;
+  cs.out_reasons = bd->res + KSIM_RES_REASONS;
+  int rc = ksim_rt_check_launch_ctx(h, cs, grid, "ksim_schedule_one (resident)");
+  if (rc) return rc;
+  hipError_t e = ksim_launch_serve(&cs, bd, h->serve_seq, SERVE_IDLE_TICKS, npt, grid, h->stream_raw);
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "resident per-pod kernel launch: %s", hipGetErrorString(e));
+  h->serve_live = true;
+  h->serve_shared = false;  // (the launch itself acquires)
+  h->serve_base = h->ctx;
+  h->serve_npt = npt;
+  h->serve_grid = grid;
+  h->serve_post_ns = now_ns();
+  h->serve_stats[0] += 1;
+  return KSIM_OK;
+}
+
+// Write one message into the mailbox (every word tagged with its number: KSIM_SERVE_MSG_WORDS).
+uint64_t serve_write(ksim_handle* h, int32_t type, const ksim_pod* p, const uint64_t* ports,
+                     const ksim_scalar_req* scalars, int32_t no_commit, int64_t node, uint32_t tag, int32_t sync) {
+  uint32_t w[KSIM_SERVE_MSG_WORDS] = {};
+  w[KSIM_SERVE_W_TYPE] = (uint32_t)type;
+  w[KSIM_SERVE_W_NOCOMMIT] = (uint32_t)no_commit;
+  w[KSIM_SERVE_W_TAG] = tag;
+  w[KSIM_SERVE_W_SYNC] = (uint32_t)sync;
+  w[KSIM_SERVE_W_NODE] = (uint32_t)(uint64_t)node;
+  w[KSIM_SERVE_W_NODE + 1] = (uint32_t)((uint64_t)node >> 32);
+  if (p) {
+    memcpy(w + KSIM_SERVE_W_POD, p, sizeof *p);
+    if (p->port_cnt) memcpy(w + KSIM_SERVE_W_PORTS, ports, (size_t)p->port_cnt * 8);
+    if (p->scalar_cnt) memcpy(w + KSIM_SERVE_W_SCALARS, scalars, (size_t)p->scalar_cnt * sizeof(ksim_scalar_req));
+  }
+  const uint64_t seq = ++h->serve_seq;
+  const uint64_t tg = (uint64_t)(uint32_t)seq << 32;
+  uint64_t* m = h->serve_box->msg;
+  for (int k = 0; k < KSIM_SERVE_MSG_WORDS; ++k) __atomic_store_n(&m[k], tg | w[k], __ATOMIC_RELAXED);
+  return seq;
+}
+
+// Post one message and wait for its answer (the result block of the mailbox).
+int serve_post(ksim_handle* h, int32_t type, const ksim_pod& p, const uint64_t* ports, const ksim_scalar_req* scalars,
+               int32_t no_commit, int64_t node, uint32_t tag) {
+  KsimServeBox* b = h->serve_box;
+  // the system-scope acquire only after commits of state other blocks read (inter-pod affinity /
+  // service counts, volumes); KSIM_SERVE_LIGHT=0: before every message
+  static const bool light_off = getenv("KSIM_SERVE_LIGHT") && getenv("KSIM_SERVE_LIGHT")[0] == '0';
+  const bool shared = ksim_is_aff_host(h, p) || p.vol_class != 0;
+  const int32_t sync = h->serve_shared || light_off ? KSIM_SERVE_SYNC_ACQUIRE : 0;
+  h->serve_shared = shared;
+  memset(b->res, 0, sizeof b->res);
+  b->res[KSIM_RES_NODE] = INT32_MIN;
+  const uint64_t seq = serve_write(h, type, &p, ports, scalars, no_commit, node, tag, sync);
+  h->serve_stats[1] += 1;
+  const int64_t t0 = now_ns();
+  int64_t next_check = t0 + 1000000;  // after 1 ms: is the kernel still there?
+  for (uint64_t spins = 0; __atomic_load_n(&b->done, __ATOMIC_ACQUIRE) != seq; ++spins) {
+    __builtin_ia32_pause();
+    if ((spins & 255) != 255) continue;
+    const int64_t t = now_ns();
+    if (t < next_check) continue;
+    next_check = t + 1000000;
+    const bool gone = hipStreamQuery(h->stream_raw) == hipSuccess;
+    if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) break;
+    if (gone || t - t0 > SERVE_WAIT_NS) {
+      h->serve_off = true;  // per-pod launches from now on
+      if (!gone) (void)ksim_serve_stop(h);
+      h->serve_live = false;
+      return ksim_fail(h, KSIM_E_DEVICE, "resident per-pod kernel %s (message %llu)", gone ? "left before answering" : "did not answer",
+                       (unsigned long long)seq);
+    }
+  }
+  h->serve_post_ns = now_ns();
+  return KSIM_OK;
+}
+
+// The resident kernel serves the current context with this geometry: (re)start it when not.
+int serve_ready(ksim_handle* h, int npt, int grid) {
+  if (h->serve_live) {
+    const bool stale = now_ns() - h->serve_post_ns > SERVE_POST_NS;
+    if (stale || h->serve_npt != npt || h->serve_grid != grid || memcmp(&h->ctx, &h->serve_base, sizeof(KsimCtx)) != 0) {
+      if (stale) h->serve_stats[3] += 1;
+      int rc = ksim_serve_stop(h);
+      if (rc) return rc;
+    }
+  }
+  if (!h->serve_live) return serve_start(h, npt, grid);
   return KSIM_OK;
 }
 
@@ -301,9 +447,9 @@ int set_row(ksim_handle* h, int64_t index, const ksim_node_row* row, bool full) 
   if (rc) return rc;
   memcpy(h->stg_host + STG_PORTS, pk.data(), pk.size() * 8);  // read by the kernel through the mapping
   hipError_t e = ksim_launch_set_row(&h->ctx, index, reinterpret_cast<const uint64_t*>(h->stg_dev + STG_PORTS), full ? 1 : 0,
-                                     h->stream);
+                                     ksim_stream(h));
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "set_row launch: %s", hipGetErrorString(e));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   if (!row_exact(row, full)) h->pfast_off = true;
   return KSIM_OK;
 }
@@ -316,15 +462,39 @@ int node_shift(ksim_handle* h, int32_t op, int64_t index) {
   if (rc) return rc;
   c.n = n_new;
   if (h->have_pods && h->n_pods) {
-    hipError_t e = ksim_launch_remap_hosts(h->d_pods, h->n_pods, index, op, h->stream);
+    hipError_t e = ksim_launch_remap_hosts(h->d_pods, h->n_pods, index, op, ksim_stream(h));
     if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "remap launch: %s", hipGetErrorString(e));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   }
   ksim_rt_invalidate_layout(h);
   return KSIM_OK;
 }
 
 }  // namespace
+
+int ksim_serve_stop(ksim_handle* h) {
+  if (!h->serve_live) return KSIM_OK;
+  h->serve_live = false;  // (first: the drain below goes through the raw stream)
+  h->serve_stats[2] += 1;
+  (void)serve_write(h, KSIM_SERVE_EXIT, nullptr, nullptr, nullptr, 0, -1, 0, 0);
+  HIPCHK(h, hipStreamSynchronize(h->stream_raw));
+#ifdef KSIM_STAMPS
+  uint64_t d[32];
+  HIPCHK(h, hipMemcpy(d, h->ctx.dbg + 64, sizeof d, hipMemcpyDeviceToHost));
+  HIPCHK(h, hipMemset(h->ctx.dbg + 64, 0, sizeof d));
+  if (d[16 + 1])
+    fprintf(stderr, "[ksim stamps] serve: %llu block-messages, us per phase (count): poll %.2f (%llu) copy %.2f (%llu) "
+            "eval %.2f (%llu) passA %.2f (%llu) records+decision %.2f (%llu) owner-select %.2f (%llu) commit %.2f (%llu) "
+            "publish %.2f (%llu)\n", (unsigned long long)d[17],
+            d[0] / 100.0 / std::max<uint64_t>(d[16], 1), (unsigned long long)d[16], d[1] / 100.0 / std::max<uint64_t>(d[17], 1),
+            (unsigned long long)d[17], d[2] / 100.0 / std::max<uint64_t>(d[18], 1), (unsigned long long)d[18],
+            d[3] / 100.0 / std::max<uint64_t>(d[19], 1), (unsigned long long)d[19], d[4] / 100.0 / std::max<uint64_t>(d[20], 1),
+            (unsigned long long)d[20], d[5] / 100.0 / std::max<uint64_t>(d[21], 1), (unsigned long long)d[21],
+            d[6] / 100.0 / std::max<uint64_t>(d[22], 1), (unsigned long long)d[22], d[7] / 100.0 / std::max<uint64_t>(d[23], 1),
+            (unsigned long long)d[23]);
+#endif
+  return KSIM_OK;
+}
 
 void ksim_rt_invalidate_layout(ksim_handle* h) {
   if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
@@ -376,10 +546,10 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
     h->res_host[KSIM_RES_NODE] = INT32_MIN;
     if ((rc = ksim_rt_check_launch_ctx(h, cs, 1, "ksim_schedule_one"))) return rc;
     oc.lap(0);
-    hipError_t e1 = ksim_launch_one(&cs, one_npt, h->stream);
+    hipError_t e1 = ksim_launch_one(&cs, one_npt, ksim_stream(h));
     if (e1 != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "one-workgroup launch: %s", hipGetErrorString(e1));
     oc.lap(1);
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
     oc.lap(2);
     const int32_t* r = h->res_host;
     memset(out, 0, sizeof *out);
@@ -414,19 +584,50 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
     }
     if (sw < ((int64_t)1 << 54) && h->pick_ok) {
       if (!h->pick_words) {
-        if ((rc = dev_alloc(h, &h->pick_words, (size_t)KSIM_PICK_WORDS))) return rc;
-        HIPCHK(h, hipMemsetAsync(h->pick_words, 0, (size_t)KSIM_PICK_WORDS * 8, h->stream));
+        if ((rc = dev_alloc(h, &h->pick_words, (size_t)2 * KSIM_PICK_WORDS))) return rc;
+        HIPCHK(h, hipMemsetAsync(h->pick_words, 0, (size_t)2 * KSIM_PICK_WORDS * 8, ksim_stream(h)));
       }
-      h->pick_tag = h->pick_tag % 255u + 1u;  // 1..255: the previous call's words carry another tag
+      // 1..254, so consecutive calls alternate the record buffer (tag parity) and a buffer's words
+      // always carry the tag of an earlier call
+      h->pick_tag = h->pick_tag % 254u + 1u;
+      if (serve_wanted(h) && pod->port_cnt <= KSIM_ONE_PORTS && pod->scalar_cnt <= KSIM_MAX_SCALAR) {
+        if (h->pick_grid != grid || !h->serve_live) {
+          if (!ksim_serve_coresident(npt, grid)) h->serve_off = true;
+        }
+        if (!h->serve_off) {
+          if ((rc = serve_ready(h, npt, grid))) return rc;
+          oc.lap(0);
+          const ksim_pod sp = staged_pod(h, *pod);
+          if ((rc = serve_post(h, KSIM_SERVE_SCHEDULE, sp, ports + pod->port_off, scalars + pod->scalar_off, assume ? 0 : 1, -1,
+                               h->pick_tag)))
+            return rc;
+          oc.lap(2);
+          const int32_t* r = h->serve_box->res;
+          memset(out, 0, sizeof *out);
+          out->node = r[KSIM_RES_NODE];
+          out->fit_nodes = r[KSIM_RES_FIT];
+          memcpy(&out->last_node_index, r + KSIM_RES_CTR, 8);
+          if (out->node < 0) memcpy(out->reasons, r + KSIM_RES_REASONS, sizeof out->reasons);
+          if (r[KSIM_RES_ERR] & 128) return ksim_rt_svc_refusal(h);
+          if (r[KSIM_RES_ERR] || out->node == INT32_MIN)
+            return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x (resident pick)", r[KSIM_RES_ERR]);
+          if (assume && out->node >= 0) {
+            rc = after_commit(h, pod->port_cnt, r);
+            oc.lap(3);
+            return rc;
+          }
+          return KSIM_OK;
+        }
+      }
       cs.pick = h->pick_words;
       cs.pick_tag = h->pick_tag;
       h->res_host[KSIM_RES_NODE] = INT32_MIN;
       if ((rc = ksim_rt_check_launch_ctx(h, cs, grid, "ksim_schedule_one"))) return rc;
       oc.lap(0);
-      hipError_t ep = ksim_launch_pick(&cs, npt, grid, h->stream);
+      hipError_t ep = ksim_launch_pick(&cs, npt, grid, ksim_stream(h));
       if (ep != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pick launch: %s", hipGetErrorString(ep));
       oc.lap(1);
-      HIPCHK(h, hipStreamSynchronize(h->stream));
+      HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
       oc.lap(2);
       const int32_t* r = h->res_host;
       memset(out, 0, sizeof *out);
@@ -462,11 +663,11 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   if ((rc = ksim_rt_check_launch_ctx(h, cs, grid, "ksim_schedule_one"))) return rc;
   hipError_t e = hipSuccess;
   oc.lap(0);
-  if (ipa && !cs.fuse_a) e = ksim_launch_ipa_pass(&cs, npt, grid, h->stream);
-  if (e == hipSuccess) e = ksim_launch_scan(&cs, npt, 1, grid, h->stream);
+  if (ipa && !cs.fuse_a) e = ksim_launch_ipa_pass(&cs, npt, grid, ksim_stream(h));
+  if (e == hipSuccess) e = ksim_launch_scan(&cs, npt, 1, grid, ksim_stream(h));
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "scan launch: %s", hipGetErrorString(e));
   oc.lap(1);
-  HIPCHK(h, hipStreamSynchronize(h->stream));  // the result block is host memory: nothing to copy
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));  // the result block is host memory: nothing to copy
   oc.lap(2);
   const int32_t* r = h->res_host;
   if (cs.fuse_a && r[KSIM_RES_NODE] == INT32_MIN) {
@@ -509,12 +710,19 @@ static int pod_delta(ksim_handle* h, int64_t node, const ksim_pod* pod, const ui
   ksim_pod p = *pod;
   p.host = -1;  // spec.nodeName plays no part in a resource delta (the node is given)
   if ((rc = ksim_rt_check_pod(h, p, n_ports, n_scalars, scalars, where))) return rc;
+  // the resident per-pod kernel takes an assume as a message (the adapter's Schedule + AssumePod
+  // pattern), when it serves the current context
+  if (add && h->serve_live && p.port_cnt <= KSIM_ONE_PORTS && p.scalar_cnt <= KSIM_MAX_SCALAR &&
+      now_ns() - h->serve_post_ns <= SERVE_POST_NS && memcmp(&h->ctx, &h->serve_base, sizeof(KsimCtx)) == 0) {
+    if ((rc = serve_post(h, KSIM_SERVE_ASSUME, staged_pod(h, p), ports + p.port_off, scalars + p.scalar_off, 0, node, 0))) return rc;
+    return after_commit(h, pod->port_cnt, h->serve_box->res);
+  }
   KsimCtx cs;
   if ((rc = stage_pod(h, p, ports, scalars, &cs))) return rc;
-  hipError_t e = add ? ksim_launch_assume(&cs, 0, node, h->res_dev + KSIM_RES_STATUS, h->stream)
-                     : ksim_launch_release(&cs, 0, node, h->stream);
+  hipError_t e = add ? ksim_launch_assume(&cs, 0, node, h->res_dev + KSIM_RES_STATUS, ksim_stream(h))
+                     : ksim_launch_release(&cs, 0, node, ksim_stream(h));
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "%s launch: %s", where, hipGetErrorString(e));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   if (!add) {  // a release can only shrink quantities, but never below zero in a consistent cache
     h->tree_valid = false;
     return KSIM_OK;
@@ -542,9 +750,9 @@ int ksim_assume(ksim_handle* h, int64_t pod, int64_t node) {
   rc = ensure_staging(h, 0, 0);
   if (rc) return rc;
   memset(h->res_host, 0, KSIM_RES_WORDS * 4);
-  hipError_t e = ksim_launch_assume(&h->ctx, pod, node, h->res_dev + KSIM_RES_STATUS, h->stream);
+  hipError_t e = ksim_launch_assume(&h->ctx, pod, node, h->res_dev + KSIM_RES_STATUS, ksim_stream(h));
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "assume launch: %s", hipGetErrorString(e));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   return after_commit(h, 0);
 }
 

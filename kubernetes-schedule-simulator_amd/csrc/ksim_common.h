@@ -132,7 +132,7 @@ struct KsimVol {
 #define KSIM_PICK_ZMAX 60
 #define KSIM_PICK_RA (4 + KSIM_PICK_ZMAX)
 #define KSIM_PICK_RB (1 + 2 * KSIM_MAX_RCLASS + KSIM_NREASONS)
-#define KSIM_PICK_WORDS (KSIM_PICK_MAXG * (KSIM_PICK_RA + KSIM_PICK_RB))
+#define KSIM_PICK_WORDS (KSIM_PICK_MAXG * (KSIM_PICK_RA + KSIM_PICK_RB))  /* one record buffer (two are allocated) */
 
 struct KsimCtx {
   // ---- node table (name-rank order) ----
@@ -233,6 +233,36 @@ __device__ __forceinline__ uint64_t ksim_pod_port(const KsimCtx& c, const ksim_p
 __device__ __forceinline__ ksim_scalar_req ksim_pod_scalar(const KsimCtx& c, const ksim_pod& P, int32_t s) {
   return c.one ? c.one_scalars[s] : c.pod_scalars[P.scalar_off + s];
 }
+
+// The resident per-pod service's mailbox (ksim_serve_kernel), in coherent host memory mapped
+// into the device.  A message is KSIM_SERVE_MSG_WORDS 32-bit payload words, each stored by the
+// host as one 8-byte word `payload | (uint32)seq << 32`: the device reads the whole message with
+// one 16-byte load per lane (one PCIe round trip) and takes it when every word carries the
+// message's number — no separate sequence word, no second round trip for the body.  The block
+// that answers writes the result block and then the number into `done` (a system-scope release).
+#define KSIM_SERVE_EXIT 0
+#define KSIM_SERVE_SCHEDULE 1
+#define KSIM_SERVE_ASSUME 2
+#define KSIM_SERVE_SYNC_ACQUIRE 1  // the previous message committed state other blocks read: acquire first
+#define KSIM_SERVE_MSG_WORDS 128
+// payload word offsets
+#define KSIM_SERVE_W_TYPE 0      // KSIM_SERVE_*
+#define KSIM_SERVE_W_NOCOMMIT 1  // SCHEDULE: 1 = decide only
+#define KSIM_SERVE_W_TAG 2       // SCHEDULE: the pick records' tag (1..254; its parity picks the record buffer)
+#define KSIM_SERVE_W_SYNC 3      // KSIM_SERVE_SYNC_* (the host knows which pods commit shared counts)
+#define KSIM_SERVE_W_NODE 4      // ASSUME: the node (two words, low first)
+#define KSIM_SERVE_W_POD 6       // ksim_pod (32 words)
+#define KSIM_SERVE_W_PORTS (KSIM_SERVE_W_POD + (int)(sizeof(ksim_pod) / 4))   // KSIM_ONE_PORTS keys
+#define KSIM_SERVE_W_SCALARS (KSIM_SERVE_W_PORTS + 2 * KSIM_ONE_PORTS)       // KSIM_MAX_SCALAR requests
+static_assert(sizeof(ksim_pod) % 4 == 0 && sizeof(ksim_scalar_req) % 4 == 0, "mailbox words");
+static_assert(KSIM_SERVE_W_SCALARS + (int)(KSIM_MAX_SCALAR * sizeof(ksim_scalar_req) / 4) <= KSIM_SERVE_MSG_WORDS,
+              "a mailbox message holds a pod with KSIM_ONE_PORTS ports and KSIM_MAX_SCALAR scalars");
+struct KsimServeBox {
+  uint64_t msg[KSIM_SERVE_MSG_WORDS];  // host: the current message (16-byte aligned)
+  uint64_t done;                       // device: the last message answered
+  uint64_t pad1[7];
+  int32_t res[KSIM_RES_WORDS];         // the result block (KSIM_RES_*)
+};
 
 // Node-sharded mode (ksim_shard_*): this rank's place in the world and every rank's exchange
 // buffer as mapped on this device.

@@ -29,6 +29,9 @@ extern "C" int ksim_one_npt(int64_t n);
 extern "C" hipError_t ksim_launch_one(const KsimCtx* c, int npt, hipStream_t s);
 extern "C" int ksim_pick_coresident(int npt, int grid);
 extern "C" hipError_t ksim_launch_pick(const KsimCtx* c, int npt, int grid, hipStream_t s);
+extern "C" int ksim_serve_coresident(int npt, int grid);
+extern "C" hipError_t ksim_launch_serve(const KsimCtx* c, KsimServeBox* box, uint64_t seq0, uint64_t idle_ticks, int npt,
+                                        int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_ipa_pass(const KsimCtx* c, int npt, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, int32_t* status, hipStream_t s);
 extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
@@ -83,7 +86,9 @@ struct DevBuf {
 
 struct ksim_handle {
   int device = 0;
-  hipStream_t stream = nullptr;
+  // the handle's one stream: every launch and copy goes through ksim_stream(h), which first stops
+  // the resident per-pod kernel when it is running (so nothing ever queues behind it)
+  hipStream_t stream_raw = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   ksim_config cfg{};
   std::string err;
@@ -142,6 +147,19 @@ struct ksim_handle {
   bool pick_ok = false;            // ... and its two-deep pipelined kernel (ksim_pipe.hip)
   uint64_t* pipe_words = nullptr;          // the pipelined kernel's published words
   size_t pipe_bytes = 0;
+  // the resident per-pod service (ksim_serve_kernel, ksim_cache.cpp): mailbox, the context and
+  // geometry it was launched with, per-block pod staging, the last message posted and when
+  bool serve_live = false;
+  bool serve_off = false;                  // KSIM_SERVE=0, or a failure: per-pod launches only
+  KsimServeBox* serve_box = nullptr;       // coherent host memory ...
+  KsimServeBox* serve_box_dev = nullptr;   // ... as the device addresses it
+  KsimCtx serve_base{};                    // h->ctx when the kernel was launched
+  int serve_npt = 0, serve_grid = 0;
+  uint64_t serve_seq = 0;
+  bool serve_shared = false;               // the last message committed state other blocks read
+  int64_t serve_post_ns = 0;               // steady clock of the last post (or of the launch)
+  char* serve_stage = nullptr;             // device: [grid] pods, [grid][KSIM_ONE_PORTS] ports, [grid][KSIM_MAX_SCALAR] scalars
+  int64_t serve_stats[4] = {0, 0, 0, 0};   // launches, messages, stops, relaunches after the idle bound
   int32_t* tcls = nullptr;
   int64_t tcls_cap = 0;
   KsimTreeClass* tclass = nullptr;
@@ -213,6 +231,12 @@ struct ksim_handle {
 };
 
 int ksim_fail(ksim_handle* h, int code, const char* fmt, ...);
+// Stop the resident per-pod kernel (an exit message and a stream drain); KSIM_OK when none runs.
+int ksim_serve_stop(ksim_handle* h);
+inline hipStream_t ksim_stream(ksim_handle* h) {
+  if (h->serve_live) (void)ksim_serve_stop(h);
+  return h->stream_raw;
+}
 
 #define HIPCHK(h, x)                                                                              \
   do {                                                                                            \
@@ -237,9 +261,9 @@ static int dev_upload(ksim_handle* h, T** out, const T* src, size_t count, bool 
   int rc = dev_alloc(h, out, count);
   if (rc) return rc;
   if (src && count) {
-    HIPCHK(h, hipMemcpyAsync(*out, src, count * sizeof(T), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(*out, src, count * sizeof(T), hipMemcpyHostToDevice, ksim_stream(h)));
   } else if (zero_if_null && count) {
-    HIPCHK(h, hipMemsetAsync(*out, 0, count * sizeof(T), h->stream));
+    HIPCHK(h, hipMemsetAsync(*out, 0, count * sizeof(T), ksim_stream(h)));
   }
   return KSIM_OK;
 }
@@ -247,7 +271,7 @@ static int dev_upload(ksim_handle* h, T** out, const T* src, size_t count, bool 
 // Free one buffer of the handle (the stream is drained first: hipFree must not race queued work).
 static inline void dev_free(ksim_handle* h, const void* p) {
   if (!p) return;
-  (void)hipStreamSynchronize(h->stream);
+  (void)hipStreamSynchronize(ksim_stream(h));
   (void)hipFree(const_cast<void*>(p));
   h->bufs.erase(std::remove_if(h->bufs.begin(), h->bufs.end(), [p](const DevBuf& b) { return b.p == p; }),
                 h->bufs.end());
@@ -259,7 +283,7 @@ static int dev_grow(ksim_handle* h, T** p, size_t keep, size_t new_cap) {
   T* q = nullptr;
   int rc = dev_alloc(h, &q, new_cap);
   if (rc) return rc;
-  if (*p && keep) HIPCHK(h, hipMemcpyAsync(q, *p, keep * sizeof(T), hipMemcpyDeviceToDevice, h->stream));
+  if (*p && keep) HIPCHK(h, hipMemcpyAsync(q, *p, keep * sizeof(T), hipMemcpyDeviceToDevice, ksim_stream(h)));
   dev_free(h, *p);
   *p = q;
   return KSIM_OK;

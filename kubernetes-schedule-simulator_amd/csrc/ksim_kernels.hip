@@ -1497,10 +1497,35 @@ __device__ __forceinline__ uint64_t pk_load(const uint64_t* g) {
   return __hip_atomic_load(g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 constexpr uint64_t PK_SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
+constexpr int PK_BATCH = 16;  // record words one lane keeps in flight (a cross-XCD load is ~1 µs)
+// the resident form (ksim_serve_kernel): the result block is host memory the host polls; `done`
+// takes the message number after every store of the answer (a system-scope release)
+// Always a system-scope release: an acknowledged system-scope store to host memory is not yet
+// visible to the host in order (measured: waiting for the acknowledgements of the answer's words
+// and then storing `done` let the host read the previous message's answer once in a few thousand
+// messages), so the release's write-back also orders the answer before `done`.
+__device__ __forceinline__ void pk_publish(uint64_t* done, uint64_t seq) {
+  __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// a word of the answer: the resident form's result block is host memory (system-scope store)
+__device__ __forceinline__ void pk_res(const uint64_t* done, int32_t* p, int32_t v) {
+  if (done) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  else *p = v;
+}
 }  // namespace
 
+// One pod of the pick form.  rec: this pod's record buffer (tag parity, KSIM_PICK_WORDS words);
+// ctr_keep: the block's own copy of lastNodeIndex (resident form; null: read *c.counter);
+// done / seq: the resident form's completion word (null: a one-pod launch).
 template <int NPT>
-__global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
+__device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod& P, const int64_t pod, const uint32_t tag,
+                                               const int32_t no_commit, uint64_t* const rec, uint64_t* ctr_keep,
+                                               uint64_t* done, const uint64_t seq, uint64_t* stamp = nullptr) {
+#ifdef KSIM_STAMPS
+#define PKST(k) do { if (stamp && threadIdx.x == 0) stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define PKST(k) do { (void)stamp; } while (0)
+#endif
   __shared__ uint64_t s_bm[KSIM_MAX_RCLASS + 1][NPT][KSIM_WAVES];  // per class (and [MAX] = fit) candidate masks
   __shared__ int64_t s_mx[KSIM_WAVES][KSIM_MAX_RCLASS];
   __shared__ int32_t s_cnt[KSIM_WAVES][KSIM_MAX_RCLASS];
@@ -1520,13 +1545,10 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int G = gridDim.x, me = blockIdx.x;
-  const ksim_pod P = c.one_pod;
-  const int64_t pod = c.first;
   const int k1 = P.reserved[0], k2 = P.reserved[1];
   const int K = k1 * k2;  // <= KSIM_MAX_RCLASS (host-checked)
-  const uint32_t tag = c.pick_tag;
-  uint64_t* const recA = c.pick;
-  uint64_t* const recB = c.pick + KSIM_PICK_MAXG * KSIM_PICK_RA;
+  uint64_t* const recA = rec;
+  uint64_t* const recB = rec + KSIM_PICK_MAXG * KSIM_PICK_RA;
   // the decision's inputs, loaded while the nodes are evaluated
   int64_t pre_tv = 0, pre_av = 0, pre_ad = 0;
   if (tid < K) {
@@ -1535,7 +1557,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
     pre_ad = c.na_add ? c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2] : 0;
   }
   uint64_t pre_ctr = 0;
-  if (tid == 0) pre_ctr = *c.counter;
+  if (tid == 0) pre_ctr = ctr_keep ? *ctr_keep : *c.counter;
   IpaNorm ipa = ipa_norm(c, P);  // which of pass A's priorities the pod reads (maxima below)
   IpaNorm ipa0 = ipa;
   ipa0.on = false;
@@ -1555,6 +1577,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
 #pragma unroll
   for (int k = 0; k < NPT; ++k) eval_one<true>(c, P, base + (int64_t)k * KSIM_BLOCK + tid, k1, k2, ipa0, fit[k], sc[k], cl[k], rm[k]);
 
+  PKST(2);
   // the first spin that hits its bound: err bit 2 (a consistency error; the grid is co-resident)
   auto spin_fail = [&]() {
     if (lane == 0) { atomicOr(c.err, 2); s_ok = 0; }
@@ -1609,12 +1632,18 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
       for (;;) {
         bool ok = true;
         acc = 0;  // (0 folded into every combine: the reference's accumulators start there)
-        for (int b = 0; b < G; ++b) {
-          if (lane >= W) break;
-          const uint64_t wd = pk_load(recA + (int64_t)b * KSIM_PICK_RA + lane);
-          ok &= pk_tag(wd) == tag;
-          const int64_t x = pk_dec(wd);
-          acc = lane == 0 ? (x < acc ? x : acc) : (lane < 4 ? (x > acc ? x : acc) : acc + x);
+        for (int b0 = 0; b0 < G && lane < W; b0 += PK_BATCH) {
+          uint64_t wd[PK_BATCH];  // one batch of blocks' words in flight: one round trip per batch
+#pragma unroll
+          for (int j = 0; j < PK_BATCH; ++j)
+            wd[j] = b0 + j < G ? pk_load(recA + (int64_t)(b0 + j) * KSIM_PICK_RA + lane) : pk_enc(tag, 0);
+#pragma unroll
+          for (int j = 0; j < PK_BATCH; ++j) {
+            if (b0 + j >= G) break;
+            ok &= pk_tag(wd[j]) == tag;
+            const int64_t x = pk_dec(wd[j]);
+            acc = lane == 0 ? (x < acc ? x : acc) : (lane < 4 ? (x > acc ? x : acc) : acc + x);
+          }
         }
         if (__all(ok)) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { spin_fail(); break; }
@@ -1639,6 +1668,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
     }
   }
 
+  PKST(3);
   if (tid < K) { s_tv[tid] = pre_tv; s_av[tid] = pre_av; s_ad[tid] = pre_ad; }
   if (tid == 0) s_ctr = pre_ctr;
   // ---- per wave: fit count and mask, per reduce class (max, count at max) and masks, reasons ----
@@ -1705,10 +1735,17 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
     for (;;) {
       bool ok = true;
       if (lane < G)
-        for (int x = 0; x <= 2 * K; ++x) {
-          const uint64_t w = pk_load(recB + (int64_t)lane * KSIM_PICK_RB + x);
-          ok &= pk_tag(w) == tag;
-          s_rec[lane][x] = pk_dec(w);
+        for (int x0 = 0; x0 <= 2 * K; x0 += PK_BATCH) {
+          uint64_t w[PK_BATCH];  // one batch of words in flight: one round trip per batch
+#pragma unroll
+          for (int j = 0; j < PK_BATCH; ++j)
+            w[j] = x0 + j <= 2 * K ? pk_load(recB + (int64_t)lane * KSIM_PICK_RB + x0 + j) : pk_enc(tag, 0);
+#pragma unroll
+          for (int j = 0; j < PK_BATCH; ++j) {
+            if (x0 + j > 2 * K) break;
+            ok &= pk_tag(w[j]) == tag;
+            s_rec[lane][x0 + j] = pk_dec(w[j]);
+          }
         }
       if (__all(ok)) break;
       if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { spin_fail(); break; }
@@ -1776,12 +1813,21 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
       s_F = F;
       s_win = win;
       s_ctr = (mode == 2) ? li + 1 : li;  // generic_scheduler.go:192-195
+      if (ctr_keep) *ctr_keep = s_ctr;
     }
     if (mode != 2 && lane < KSIM_MAX_RCLASS) s_M[lane] = INT64_MIN;
   }
   __syncthreads();
+  PKST(4);
   const int mode = s_mode;
-  if (mode < 0) return;  // a spin hit its bound (err set): nothing committed
+  if (mode < 0) {  // a spin hit its bound (err set): nothing committed
+    if (done && me == 0 && tid == 0) {  // (the resident form: the host must hear of it)
+      pk_res(done, &c.out_node[pod], INT32_MIN);
+      if (c.out_fit) pk_res(done, &c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT], __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | 2);
+      pk_publish(done, seq);
+    }
+    return;
+  }
 
   if (mode == 0) {
     if (me == 0 && wv == 0) {  // FitError: every block's reasons (each fitted nothing)
@@ -1790,24 +1836,33 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
       for (;;) {  // (the reason words went out in the same store as the words read above, tagged alike)
         bool ok = true;
         v = 0;
-        for (int b = 0; b < G && lane < KSIM_NREASONS; ++b) {
-          const uint64_t wd = pk_load(recB + (int64_t)b * KSIM_PICK_RB + 1 + 2 * K + lane);
-          ok &= pk_tag(wd) == tag;
-          v += (int32_t)pk_dec(wd);
+        for (int b0 = 0; b0 < G && lane < KSIM_NREASONS; b0 += PK_BATCH) {
+          uint64_t wd[PK_BATCH];  // one batch of blocks' words in flight
+#pragma unroll
+          for (int j = 0; j < PK_BATCH; ++j)
+            wd[j] = b0 + j < G ? pk_load(recB + (int64_t)(b0 + j) * KSIM_PICK_RB + 1 + 2 * K + lane) : pk_enc(tag, 0);
+#pragma unroll
+          for (int j = 0; j < PK_BATCH; ++j) {
+            if (b0 + j >= G) break;
+            ok &= pk_tag(wd[j]) == tag;
+            v += (int32_t)pk_dec(wd[j]);
+          }
         }
         if (__all(ok)) break;
         if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { atomicOr(c.err, 2); break; }
         __builtin_amdgcn_s_sleep(1);
       }
-      if (lane < KSIM_NREASONS) c.out_reasons[pod * KSIM_NREASONS + lane] = v;
+      if (lane < KSIM_NREASONS) pk_res(done, &c.out_reasons[pod * KSIM_NREASONS + lane], v);
       if (lane == 0) {
-        c.out_node[pod] = -1;
+        pk_res(done, &c.out_node[pod], -1);
         if (c.out_fit) {
-          c.out_fit[0] = 0;
-          c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT] = (int32_t)(uint32_t)s_ctr;
-          c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1] = (int32_t)(uint32_t)(s_ctr >> 32);
+          pk_res(done, &c.out_fit[0], 0);
+          pk_res(done, &c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT], __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          pk_res(done, &c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT], (int32_t)(uint32_t)s_ctr);
+          pk_res(done, &c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1], (int32_t)(uint32_t)(s_ctr >> 32));
         }
+        if (done) pk_publish(done, seq);  // (the wave's reason stores above are ordered before it)
+        PKST(7);
       }
     }
     return;
@@ -1849,13 +1904,14 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
     }
   }
   __syncthreads();
+  PKST(5);
   const int64_t node = s_node;
-  if (node >= 0 && !c.no_commit) {
+  if (node >= 0 && !no_commit) {
     if (wv == 0) {
       const int32_t st = ksim_commit_wave(c, P, node, lane);
       if (tid == 0) {
         if (ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, node, 1, c.err);
-        if (c.out_fit) c.out_fit[1] |= st;
+        if (c.out_fit && st) pk_res(done, &c.out_fit[1], done ? st : (c.out_fit[1] | st));  // (resident: the host zeroed it)
       }
     } else if (wv == 1 && ksim_is_aff_pod(c, P)) {
       if (lane == 0) ksim_svc_commit(*c.aff, P, node);  // reads the counts before this commit's adds
@@ -1863,16 +1919,169 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
     }
   }
   __syncthreads();
+  PKST(6);
   if (tid == 0) {
     if (mode == 2) *c.counter = s_ctr;
-    c.out_node[pod] = (int32_t)node;
+    pk_res(done, &c.out_node[pod], (int32_t)node);
     if (c.out_fit) {
-      c.out_fit[0] = s_F;
-      c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT] = (int32_t)(uint32_t)s_ctr;
-      c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1] = (int32_t)(uint32_t)(s_ctr >> 32);
+      pk_res(done, &c.out_fit[0], s_F);
+      pk_res(done, &c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT], __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+      pk_res(done, &c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT], (int32_t)(uint32_t)s_ctr);
+      pk_res(done, &c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1], (int32_t)(uint32_t)(s_ctr >> 32));
     }
+    if (done) pk_publish(done, seq);  // after the barrier: every wave's commit stores are issued before it
+    PKST(7);
   }
+#undef PKST
+}
+
+template <int NPT>
+__global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
+  ksim_pick_body<NPT>(c, c.one_pod, c.first, c.pick_tag, c.no_commit, c.pick + (c.pick_tag & 1u) * KSIM_PICK_WORDS,
+                      nullptr, nullptr, 0);
+}
+
+// ---------------------------------------------------------------------------------------
+// The resident per-pod service (ksim_schedule_one / ksim_pod_add between other calls): the pick
+// kernel's grid stays resident and takes one message at a time from a mailbox in coherent host
+// memory (KsimServeBox: tagged words, one PCIe round trip per poll), so a call costs the host's
+// stores, the device's poll and the answer's store instead of a kernel launch and a stream
+// synchronisation.  Each block copies the message's pod
+// into its own slot of the device staging (c.pods / c.pod_ports / c.pod_scalars, one slot per
+// block: the evaluation reads its ports / scalars there), keeps lastNodeIndex in LDS (every block
+// takes the same decision), and uses the record buffer of the message's tag parity, so a block
+// still reading pod k's records never sees them overwritten by pod k + 1's.  Every block leaves on
+// an exit message or after KSIM_SERVE_IDLE_TICKS without one (the host never posts a message that
+// late: it stops and relaunches the kernel instead, ksim_cache.cpp).
+template <int NPT>
+__global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimServeBox* box, uint64_t seq0,
+                                                                uint64_t idle_ticks) {
+  __shared__ uint64_t s_keep;
+  __shared__ ksim_pod s_P;
+  __shared__ int32_t s_type, s_nc;
+  __shared__ uint32_t s_tag;
+  __shared__ int64_t s_node;
+  __shared__ uint32_t s_msg[KSIM_SERVE_MSG_WORDS];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, me = blockIdx.x;
+  if (tid == 0) s_keep = *c.counter;
+#ifdef KSIM_STAMPS
+  // diagnostic builds: per phase, the sum of (stamp k - stamp k-1) and how often both were taken,
+  // over every block and message, into dbg[64 + k] / dbg[80 + k] at the exit (k = 0: the poll)
+  __shared__ uint64_t s_st[8], s_sum[8], s_cnt[8];
+  uint64_t* const stamp = s_st;
+  if (tid < 8) { s_sum[tid] = 0; s_cnt[tid] = 0; s_st[tid] = 0; }
+  uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+#else
+  uint64_t* const stamp = nullptr;
+#endif
+  uint64_t* const pod_ports = const_cast<uint64_t*>(c.pod_ports) + (int64_t)me * KSIM_ONE_PORTS;
+  ksim_scalar_req* const pod_scalars = const_cast<ksim_scalar_req*>(c.pod_scalars) + (int64_t)me * KSIM_MAX_SCALAR;
+  for (uint64_t seq = seq0 + 1;; ++seq) {
+    if (wv == 0) {
+      // poll: lane l reads payload words 2l, 2l+1 with their tags in one 16-byte system-scope load
+      typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+      const uint32_t s32 = (uint32_t)seq;
+      const uint64_t* src = box->msg + 2 * lane;
+      u4 q;
+      int32_t type = KSIM_SERVE_EXIT;
+      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+      for (;;) {
+        asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(q) : "v"(src) : "memory");
+        if (__all(q.y == s32 && q.w == s32)) {
+#ifdef KSIM_STAMPS
+          if (lane == 0) s_st[0] = __builtin_amdgcn_s_memrealtime();
+#endif
+          type = __builtin_amdgcn_readfirstlane((int32_t)q.x);  // word 0 (lane 0)
+          break;
+        }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;  // (uniform: one clock read per wave)
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (type == KSIM_SERVE_SCHEDULE || type == KSIM_SERVE_ASSUME) {
+        // the payload through LDS: the pod into s_P, ports / scalars into this block's staging
+        // slot (the evaluation reads them there)
+        s_msg[2 * lane] = q.x;
+        s_msg[2 * lane + 1] = q.z;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        constexpr int PW = (int)(sizeof(ksim_pod) / 4);
+        constexpr int XW = (int)(sizeof(ksim_scalar_req) / 4);
+        int32_t* dst = reinterpret_cast<int32_t*>(&s_P);
+        if (lane < PW) dst[lane] = (int32_t)s_msg[KSIM_SERVE_W_POD + lane];
+        const int32_t np = (int32_t)s_msg[KSIM_SERVE_W_POD + offsetof(ksim_pod, port_cnt) / 4];
+        const int32_t ns = (int32_t)s_msg[KSIM_SERVE_W_POD + offsetof(ksim_pod, scalar_cnt) / 4];
+        int32_t* qp = reinterpret_cast<int32_t*>(pod_ports);
+        int32_t* qs = reinterpret_cast<int32_t*>(pod_scalars);
+        if (lane < 2 * np) qp[lane] = (int32_t)s_msg[KSIM_SERVE_W_PORTS + lane];  // (np <= KSIM_ONE_PORTS = 16)
+        for (int k = lane; k < XW * ns; k += 64) qs[k] = (int32_t)s_msg[KSIM_SERVE_W_SCALARS + k];
+        const int32_t sy = (int32_t)s_msg[KSIM_SERVE_W_SYNC];
+        // the previous message committed counts other blocks read (affinity / volumes): acquire them
+        if (sy & KSIM_SERVE_SYNC_ACQUIRE) __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        // this CU's L1 holds lines of the staging slot and of the rows this block committed as they
+        // were when last read: the stores above (and the last commit's) are acknowledged, then the
+        // L1 is invalidated, so every wave's loads below fetch them from the L2
+        asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0\n\ts_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        if (lane == 0) {
+          s_P.port_off = me * KSIM_ONE_PORTS;
+          s_P.scalar_off = me * KSIM_MAX_SCALAR;
+          s_nc = (int32_t)s_msg[KSIM_SERVE_W_NOCOMMIT];
+          s_tag = s_msg[KSIM_SERVE_W_TAG];
+          s_node = (int64_t)(((uint64_t)s_msg[KSIM_SERVE_W_NODE + 1] << 32) | s_msg[KSIM_SERVE_W_NODE]);
+        }
+      }
+      if (lane == 0) s_type = type;
+    }
+    __syncthreads();
+#ifdef KSIM_STAMPS
+    if (tid == 0) s_st[1] = __builtin_amdgcn_s_memrealtime();
+#endif
+    const int32_t type = s_type;
+    if (type == KSIM_SERVE_SCHEDULE) {
+      const ksim_pod P = s_P;
+      ksim_pick_body<NPT>(c, P, 0, s_tag, s_nc, c.pick + (s_tag & 1u) * KSIM_PICK_WORDS, &s_keep, &box->done, seq, stamp);
+    } else if (type == KSIM_SERVE_ASSUME) {
+      // a resource delta onto a given node (ksim_pod_add): the block whose chunk holds it
+      const int64_t node = s_node;
+      if (node >= (int64_t)me * c.chunk && node < (int64_t)(me + 1) * c.chunk && wv == 0) {
+        const ksim_pod P = s_P;
+        const int32_t st = ksim_commit_wave(c, P, node, lane);
+        if (lane == 0 && ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, node, 1, c.err);
+        if (ksim_is_aff_pod(c, P)) {
+          if (lane == 0) ksim_svc_commit(*c.aff, P, node);
+          ksim_aff_commit_body(*c.aff, P, node, 1, lane, 64);
+        }
+        if (lane == 0) {
+          if (st) pk_res(&box->done, &c.out_fit[KSIM_RES_STATUS - KSIM_RES_FIT], st);
+          pk_res(&box->done, &c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT], __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+          pk_publish(&box->done, seq);
+        }
+      }
+    } else {
+      break;  // an exit message, an idle bound or a message out of sequence
+    }
+    __syncthreads();  // (the next poll overwrites the block's staging slot and s_P)
+#ifdef KSIM_STAMPS
+    if (tid == 0) {
+      if (s_st[0]) { s_sum[0] += s_st[0] - t_end; s_cnt[0] += 1; }
+      uint64_t prev = s_st[0];
+      for (int k = 1; k < 8; ++k) {
+        if (s_st[k] && prev) { s_sum[k] += s_st[k] - prev; s_cnt[k] += 1; }
+        if (s_st[k]) prev = s_st[k];
+        s_st[k] = 0;
+      }
+      s_st[0] = 0;
+      t_end = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+  }
+#ifdef KSIM_STAMPS
+  if (tid < 8) {
+    atomicAdd((unsigned long long*)&c.dbg[64 + tid], (unsigned long long)s_sum[tid]);
+    atomicAdd((unsigned long long*)&c.dbg[80 + tid], (unsigned long long)s_cnt[tid]);
+  }
+#endif
 }
 
 // Per-node evaluation of one pod without commit (ksim_evaluate).
@@ -2002,6 +2211,30 @@ extern "C" int ksim_pick_coresident(int npt, int grid) {
     case 8: e = ksim_check_coresident(ksim_pick_kernel<8>, grid, KSIM_BLOCK, 0); break;
   }
   return e == hipSuccess ? 1 : 0;
+}
+
+extern "C" int ksim_serve_coresident(int npt, int grid) {
+  hipError_t e = hipErrorInvalidValue;
+  switch (npt) {
+    case 1: e = ksim_check_coresident(ksim_serve_kernel<1>, grid, KSIM_BLOCK, 0); break;
+    case 2: e = ksim_check_coresident(ksim_serve_kernel<2>, grid, KSIM_BLOCK, 0); break;
+    case 4: e = ksim_check_coresident(ksim_serve_kernel<4>, grid, KSIM_BLOCK, 0); break;
+    case 8: e = ksim_check_coresident(ksim_serve_kernel<8>, grid, KSIM_BLOCK, 0); break;
+  }
+  return e == hipSuccess ? 1 : 0;
+}
+
+extern "C" hipError_t ksim_launch_serve(const KsimCtx* c, KsimServeBox* box, uint64_t seq0, uint64_t idle_ticks, int npt,
+                                        int grid, hipStream_t s) {
+  if (grid <= 0 || grid > KSIM_PICK_MAXG || !c->pick || !box || c->one) return hipErrorInvalidValue;
+  switch (npt) {
+    case 1: hipLaunchKernelGGL(ksim_serve_kernel<1>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, box, seq0, idle_ticks); break;
+    case 2: hipLaunchKernelGGL(ksim_serve_kernel<2>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, box, seq0, idle_ticks); break;
+    case 4: hipLaunchKernelGGL(ksim_serve_kernel<4>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, box, seq0, idle_ticks); break;
+    case 8: hipLaunchKernelGGL(ksim_serve_kernel<8>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, box, seq0, idle_ticks); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
 }
 
 extern "C" hipError_t ksim_launch_pick(const KsimCtx* c, int npt, int grid, hipStream_t s) {

@@ -55,7 +55,6 @@ constexpr int NSLOT = 8;         // pod slots of the published words (pod mod NS
 constexpr int NREP = 8;          // replicas of A (workgroup b polls replica b % NREP)
 constexpr int REP_STRIDE = NSLOT * MAXG + 64;
 constexpr int DR = 8;            // decision ring (LDS)
-constexpr int SR = 4;            // statistics ring (LDS, pod mod SR)
 constexpr int RING = 32;         // pod-descriptor ring (LDS)
 constexpr int RING_FILL = 8;
 constexpr uint64_t SPIN_LIMIT_TICKS = 200000000ull;  // s_memrealtime at 100 MHz = 2 s

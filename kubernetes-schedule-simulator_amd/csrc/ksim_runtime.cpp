@@ -44,7 +44,7 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
   ksim_handle* h = new ksim_handle();
   h->device = cfg->device;
   h->cfg = *cfg;
-  if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+  if (hipSetDevice(h->device) != hipSuccess || hipStreamCreateWithFlags(&h->stream_raw, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreate(&h->ev0) != hipSuccess || hipEventCreate(&h->ev1) != hipSuccess) {
     delete h;
     return ksim_fail(nullptr, KSIM_E_DEVICE, "ksim_create: stream/event creation failed");
@@ -56,15 +56,15 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
   for (int k = 0; k < KSIM_NW; ++k) c.w[k] = cfg->weights[k];
   int rc;
   if ((rc = dev_alloc(h, &c.cursor, 1)) || (rc = dev_alloc(h, &c.counter, 1)) || (rc = dev_alloc(h, &c.ticket, 4)) ||
-      (rc = dev_alloc(h, &c.err, 4)) || (rc = dev_alloc(h, &c.dbg, 64))) {
+      (rc = dev_alloc(h, &c.err, 4)) || (rc = dev_alloc(h, &c.dbg, 128))) {
     ksim_destroy(h);
     return rc;
   }
-  (void)hipMemsetAsync(c.ticket, 0, 16, h->stream);
-  (void)hipMemsetAsync(c.err, 0, 16, h->stream);
-  (void)hipMemsetAsync(c.dbg, 0, 64 * sizeof(uint64_t), h->stream);
-  (void)hipMemcpyAsync(c.counter, &cfg->last_node_index, 8, hipMemcpyHostToDevice, h->stream);
-  if (hipStreamSynchronize(h->stream) != hipSuccess) {
+  (void)hipMemsetAsync(c.ticket, 0, 16, ksim_stream(h));
+  (void)hipMemsetAsync(c.err, 0, 16, ksim_stream(h));
+  (void)hipMemsetAsync(c.dbg, 0, 128 * sizeof(uint64_t), ksim_stream(h));
+  (void)hipMemcpyAsync(c.counter, &cfg->last_node_index, 8, hipMemcpyHostToDevice, ksim_stream(h));
+  if (hipStreamSynchronize(ksim_stream(h)) != hipSuccess) {
     ksim_destroy(h);
     return ksim_fail(nullptr, KSIM_E_DEVICE, "ksim_create: initial copies failed");
   }
@@ -79,7 +79,11 @@ int ksim_create(const ksim_config* cfg, ksim_handle** out) {
 void ksim_destroy(ksim_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
-  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->stream_raw) (void)hipStreamSynchronize(ksim_stream(h));  // (stops the resident per-pod kernel)
+  if (h->serve_live) (void)hipStreamSynchronize(h->stream_raw);    // (its stop failed: let it reach its idle bound)
+  if (getenv("KSIM_SERVE_STATS") && h->serve_stats[0])
+    fprintf(stderr, "[ksim serve] launches %lld messages %lld stops %lld idle relaunches %lld\n", (long long)h->serve_stats[0],
+            (long long)h->serve_stats[1], (long long)h->serve_stats[2], (long long)h->serve_stats[3]);
 #ifdef KSIM_STAMPS
   if (h->ctx.dbg) {  // the scan kernel's phase stamps (ksim_kernels.hip SSTAMP)
     uint64_t d[64];
@@ -99,9 +103,10 @@ void ksim_destroy(ksim_handle* h) {
   if (h->graph) (void)hipGraphDestroy(h->graph);
   for (auto& b : h->bufs) (void)hipFree(b.p);
   if (h->stg_host) (void)hipHostFree(h->stg_host);  // res_host points into it
+  if (h->serve_box) (void)hipHostFree(h->serve_box);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
-  if (h->stream) (void)hipStreamDestroy(h->stream);
+  if (h->stream_raw) (void)hipStreamDestroy(h->stream_raw);
   delete h;
 }
 
@@ -162,7 +167,7 @@ int ksim_load_nodes(ksim_handle* h, const ksim_node_table* t) {
     return rc;
   c.alloc_cpu = ac; c.alloc_mem = am; c.alloc_gpu = ag; c.alloc_eph = ae; c.alloc_scalar = as;
   c.allowed_pods = ap; c.label_set = ls; c.taint_set = ts;
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   {
     const int64_t lim = (int64_t)1 << 48;
     for (const int64_t* col : {t->alloc_cpu, t->req_cpu, t->nz_cpu, t->alloc_mem, t->req_mem, t->nz_mem})
@@ -208,7 +213,7 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
       (t->na_add && (rc = dev_upload(h, &na, t->na_add, C * KSIM_MAX_RCLASS))) ||
       (t->svc_ok && (rc = dev_upload(h, &sv, t->svc_ok, C * lw))))
     return rc;
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   for (void* q : h->class_bufs) dev_free(h, q);  // the previous tables (reload)
   h->class_bufs.clear();
   for (size_t k = nb0; k < h->bufs.size(); ++k) h->class_bufs.push_back(h->bufs[k].p);
@@ -230,9 +235,9 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
   if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
   if (h->have_classes) ksim_rt_recompute_fast(h);  // reduce-class counts decide fast-kernel eligibility
   if (h->n_pods) {  // and ride in the queued descriptors (ksim_persistent.hip's ring)
-    hipError_t e = ksim_launch_pod_k(h->d_pods, h->n_pods, &c, h->stream);
+    hipError_t e = ksim_launch_pod_k(h->d_pods, h->n_pods, &c, ksim_stream(h));
     if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pod k launch: %s", hipGetErrorString(e));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   }
   h->have_classes = true;
   return KSIM_OK;
@@ -374,7 +379,7 @@ int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
     if (c.collect) {
       int32_t* orr = c.out_reasons;
       if ((rc = dev_grow(h, &orr, (size_t)P0 * KSIM_NREASONS, (size_t)cap * KSIM_NREASONS))) return rc;
-      HIPCHK(h, hipMemsetAsync(orr + P0 * KSIM_NREASONS, 0, (size_t)(cap - P0) * KSIM_NREASONS * 4, h->stream));
+      HIPCHK(h, hipMemsetAsync(orr + P0 * KSIM_NREASONS, 0, (size_t)(cap - P0) * KSIM_NREASONS * 4, ksim_stream(h)));
       c.out_reasons = orr;
     } else if (!c.out_reasons) {
       int32_t* orr;
@@ -399,13 +404,13 @@ int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
     p.port_off += (int32_t)K0;
     p.scalar_off += (int32_t)S0;
   }
-  if (n_pods) HIPCHK(h, hipMemcpyAsync(h->d_pods + P0, v.data(), n_pods * sizeof(ksim_pod), hipMemcpyHostToDevice, h->stream));
-  if (n_ports) HIPCHK(h, hipMemcpyAsync(h->d_pod_ports + K0, ports, n_ports * 8, hipMemcpyHostToDevice, h->stream));
+  if (n_pods) HIPCHK(h, hipMemcpyAsync(h->d_pods + P0, v.data(), n_pods * sizeof(ksim_pod), hipMemcpyHostToDevice, ksim_stream(h)));
+  if (n_ports) HIPCHK(h, hipMemcpyAsync(h->d_pod_ports + K0, ports, n_ports * 8, hipMemcpyHostToDevice, ksim_stream(h)));
   if (n_scalars)
-    HIPCHK(h, hipMemcpyAsync(h->d_pod_scalars + S0, scalars, n_scalars * sizeof(ksim_scalar_req), hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->d_pod_scalars + S0, scalars, n_scalars * sizeof(ksim_scalar_req), hipMemcpyHostToDevice, ksim_stream(h)));
   c.pods = h->d_pods; c.pod_ports = h->d_pod_ports; c.pod_scalars = h->d_pod_scalars;
   {
-    hipError_t e = ksim_launch_pod_k(h->d_pods + P0, n_pods, &c, h->stream);
+    hipError_t e = ksim_launch_pod_k(h->d_pods + P0, n_pods, &c, ksim_stream(h));
     if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pod k launch: %s", hipGetErrorString(e));
   }
   // host bookkeeping: fast-kernel eligibility, tree classes, float64 bounds
@@ -458,7 +463,7 @@ int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
       if ((rc = dev_grow(h, &h->tcls, (size_t)P0, (size_t)cap))) return rc;
       h->tcls_cap = cap;
     }
-    if (n_pods) HIPCHK(h, hipMemcpyAsync(h->tcls + P0, tc.data(), n_pods * 4, hipMemcpyHostToDevice, h->stream));
+    if (n_pods) HIPCHK(h, hipMemcpyAsync(h->tcls + P0, tc.data(), n_pods * 4, hipMemcpyHostToDevice, ksim_stream(h)));
     const int32_t ntc = (int32_t)h->tkeys.size();
     if (ntc != ntc0 || !h->tclass) {  // new classes: re-upload the inputs, re-plan the trees
       if (h->tclass) dev_free(h, h->tclass);
@@ -480,7 +485,7 @@ int ksim_rt_append(ksim_handle* h, const ksim_pod* pods, int64_t n_pods, const u
   // queue pointers are baked into the launch graph's kernel arguments
   if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
   if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   h->have_pods = true;
   return KSIM_OK;
 }
@@ -540,8 +545,8 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
   if (rc) return rc;
   c.first = first;
   c.end = first + count;
-  HIPCHK(h, hipMemcpyAsync(c.cursor, &first, 8, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemsetAsync(c.ticket, 0, 16, h->stream));
+  HIPCHK(h, hipMemcpyAsync(c.cursor, &first, 8, hipMemcpyHostToDevice, ksim_stream(h)));
+  HIPCHK(h, hipMemsetAsync(c.ticket, 0, 16, ksim_stream(h)));
   const int batch = (int)std::min<int64_t>(count, 256);
   const int ipa = ksim_rt_aff_count(h, first, count) > 0 &&
                   (c.w[KSIM_W_INTERPOD_AFFINITY] != 0 || c.w[KSIM_W_SELECTOR_SPREAD] != 0 || ksim_rt_aux_on(h)) &&
@@ -556,26 +561,26 @@ static int run_launch_mode(ksim_handle* h, int64_t first, int64_t count, ksim_st
       h->g_end != c.end || h->g_ipa != gkey) {
     if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
     if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    HIPCHK(h, hipStreamBeginCapture(h->stream, hipStreamCaptureModeThreadLocal));
+    HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
+    HIPCHK(h, hipStreamBeginCapture(ksim_stream(h), hipStreamCaptureModeThreadLocal));
     for (int k = 0; k < batch; ++k) {
-      hipError_t e = ipa && !c.fuse_a ? ksim_launch_ipa_pass(&c, npt, grid, h->stream) : hipSuccess;
-      if (e == hipSuccess) e = ksim_launch_scan(&c, npt, c.collect, grid, h->stream);
+      hipError_t e = ipa && !c.fuse_a ? ksim_launch_ipa_pass(&c, npt, grid, ksim_stream(h)) : hipSuccess;
+      if (e == hipSuccess) e = ksim_launch_scan(&c, npt, c.collect, grid, ksim_stream(h));
       if (e != hipSuccess) {
         hipGraph_t g = nullptr;
-        (void)hipStreamEndCapture(h->stream, &g);
+        (void)hipStreamEndCapture(ksim_stream(h), &g);
         if (g) (void)hipGraphDestroy(g);
         return ksim_fail(h, KSIM_E_DEVICE, "scan launch during capture: %s", hipGetErrorString(e));
       }
     }
-    HIPCHK(h, hipStreamEndCapture(h->stream, &h->graph));
+    HIPCHK(h, hipStreamEndCapture(ksim_stream(h), &h->graph));
     HIPCHK(h, hipGraphInstantiate(&h->gexec, h->graph, nullptr, nullptr, 0));
     h->g_batch = batch; h->g_npt = npt; h->g_collect = c.collect; h->g_first = first; h->g_end = c.end; h->g_ipa = gkey;
   }
   const int64_t reps = (count + batch - 1) / batch;
-  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  for (int64_t r = 0; r < reps; ++r) HIPCHK(h, hipGraphLaunch(h->gexec, h->stream));
-  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+  HIPCHK(h, hipEventRecord(h->ev0, ksim_stream(h)));
+  for (int64_t r = 0; r < reps; ++r) HIPCHK(h, hipGraphLaunch(h->gexec, ksim_stream(h)));
+  HIPCHK(h, hipEventRecord(h->ev1, ksim_stream(h)));
   HIPCHK(h, hipEventSynchronize(h->ev1));
   float ms = 0.f;
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
@@ -653,7 +658,7 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
       int rc = dev_alloc(h, &h->mirror, (size_t)6 * c.n);
       if (rc) return rc;
     }
-    hipError_t e = ksim_pstream_prepare(&c, h->mirror, h->stream);
+    hipError_t e = ksim_pstream_prepare(&c, h->mirror, ksim_stream(h));
     if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "stream prepare: %s", hipGetErrorString(e));
   }
   const size_t gb = ksim_pfast_granule_bytes();
@@ -694,15 +699,15 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
       if (rc) return rc;
       h->pipe_bytes = wb;
     }
-    HIPCHK(h, hipMemsetAsync(h->pipe_words, 0, wb, h->stream));
-    HIPCHK(h, hipMemsetAsync(c.dbg, 0, 16 * 8, h->stream));
+    HIPCHK(h, hipMemsetAsync(h->pipe_words, 0, wb, ksim_stream(h)));
+    HIPCHK(h, hipMemsetAsync(c.dbg, 0, 16 * 8, ksim_stream(h)));
   } else {
-    HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
+    HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, ksim_stream(h)));
   }
-  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipError_t e = pipe ? ksim_launch_pipe(&c, h->pipe_words, grid, lds_rows, pipe_spec, h->tcls, h->tclass, ncls, nb, h->stream)
+  HIPCHK(h, hipEventRecord(h->ev0, ksim_stream(h)));
+  hipError_t e = pipe ? ksim_launch_pipe(&c, h->pipe_words, grid, lds_rows, pipe_spec, h->tcls, h->tclass, ncls, nb, ksim_stream(h))
                       : ksim_launch_pfast(&c, h->granules, grid, lds_rows, stream ? h->mirror : nullptr, &h->shard,
-                                          h->tcls, h->tclass, ncls, h->stream);
+                                          h->tcls, h->tclass, ncls, ksim_stream(h));
   if (e == hipErrorCooperativeLaunchTooLarge) {
     // the grid cannot be co-resident here (a smaller or shared device): the general kernels instead
     if (h->cfg.mode != KSIM_MODE_PERSISTENT && h->shard.world == 1) {
@@ -712,7 +717,7 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
     return ksim_fail(h, KSIM_E_UNSUPPORTED, "persistent launch: %d workgroups cannot be co-resident on this device", grid);
   }
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
-  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+  HIPCHK(h, hipEventRecord(h->ev1, ksim_stream(h)));
   HIPCHK(h, hipEventSynchronize(h->ev1));
   float ms = 0.f;
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
@@ -884,21 +889,21 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, const PgP
   c.first = first;
   c.end = first + count;
   c.chunk = pl.chunk;
-  HIPCHK(h, hipMemsetAsync(h->pg_gran, 0, gb, h->stream));
+  HIPCHK(h, hipMemsetAsync(h->pg_gran, 0, gb, ksim_stream(h)));
   const int64_t end = first + count;  // the kernel lowers the cursor to the first pod it did not schedule
-  HIPCHK(h, hipMemcpyAsync(c.cursor, &end, 8, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipError_t e = ksim_pgen_pack(&c, &g, h->stream);
+  HIPCHK(h, hipMemcpyAsync(c.cursor, &end, 8, hipMemcpyHostToDevice, ksim_stream(h)));
+  HIPCHK(h, hipEventRecord(h->ev0, ksim_stream(h)));
+  hipError_t e = ksim_pgen_pack(&c, &g, ksim_stream(h));
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pgen pack: %s", hipGetErrorString(e));
-  e = pl.v2 ? ksim_launch_pgen2(&c, &g, pl.grid, pl.npt, pl.lds, h->stream)
-            : ksim_launch_pgen(&c, &g, pl.grid, pl.npt, pl.lds, h->stream);
+  e = pl.v2 ? ksim_launch_pgen2(&c, &g, pl.grid, pl.npt, pl.lds, ksim_stream(h))
+            : ksim_launch_pgen(&c, &g, pl.grid, pl.npt, pl.lds, ksim_stream(h));
   if (e == hipErrorCooperativeLaunchTooLarge) {
     if (h->cfg.mode != KSIM_MODE_PERSISTENT) return run_launch_mode(h, first, count, st);
     return ksim_fail(h, KSIM_E_UNSUPPORTED, "persistent launch: %d workgroups cannot be co-resident on this device", pl.grid);
   }
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pgen launch: %s", hipGetErrorString(e));
-  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipEventRecord(h->ev1, ksim_stream(h)));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   float ms = 0.f;
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
 #ifdef KSIM_STAMPS
@@ -1044,17 +1049,17 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
     int rc = dev_alloc(h, &h->ctx_dev, 1);
     if (rc) return rc;
   }
-  HIPCHK(h, hipMemcpyAsync(h->ctx_dev, &c, sizeof(KsimCtx), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, h->stream));
-  HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-  hipError_t e = ksim_launch_persistent(&c, h->ctx_dev, h->granules, grid, lds_rows, h->stream);
+  HIPCHK(h, hipMemcpyAsync(h->ctx_dev, &c, sizeof(KsimCtx), hipMemcpyHostToDevice, ksim_stream(h)));
+  HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, ksim_stream(h)));
+  HIPCHK(h, hipEventRecord(h->ev0, ksim_stream(h)));
+  hipError_t e = ksim_launch_persistent(&c, h->ctx_dev, h->granules, grid, lds_rows, ksim_stream(h));
   if (e == hipErrorCooperativeLaunchTooLarge) {
     // the grid cannot be co-resident here (a smaller or shared device): the launch form instead
     if (h->cfg.mode != KSIM_MODE_PERSISTENT && h->shard.world == 1) return run_launch_mode(h, first, count, st);
     return ksim_fail(h, KSIM_E_UNSUPPORTED, "persistent launch: %d workgroups cannot be co-resident on this device", grid);
   }
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "persistent launch: %s", hipGetErrorString(e));
-  HIPCHK(h, hipEventRecord(h->ev1, h->stream));
+  HIPCHK(h, hipEventRecord(h->ev1, ksim_stream(h)));
   HIPCHK(h, hipEventSynchronize(h->ev1));
   float ms = 0.f;
   HIPCHK(h, hipEventElapsedTime(&ms, h->ev0, h->ev1));
@@ -1172,19 +1177,19 @@ static int run_tree_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stat
       i = j;
       continue;
     }
-    HIPCHK(h, hipEventRecord(h->ev0, h->stream));
+    HIPCHK(h, hipEventRecord(h->ev0, ksim_stream(h)));
     if (!h->tree_valid) {
-      hipError_t e = ksim_tree_build(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, nullptr, h->stream);
+      hipError_t e = ksim_tree_build(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, nullptr, ksim_stream(h));
       if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "tree build: %s", hipGetErrorString(e));
     }
     c.first = i;
     c.end = j;
-    HIPCHK(h, hipEventRecord(h->ev1, h->stream));
-    hipError_t e = ksim_tree_launch(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, nullptr, h->stream);
+    HIPCHK(h, hipEventRecord(h->ev1, ksim_stream(h)));
+    hipError_t e = ksim_tree_launch(&c, &h->geo, h->tclass, h->tcls, h->t_leaves, h->t_levels, h->t_fit, h->t_y, nullptr, ksim_stream(h));
     if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "tree launch: %s", hipGetErrorString(e));
     hipEvent_t ev2 = nullptr;
     HIPCHK(h, hipEventCreate(&ev2));
-    HIPCHK(h, hipEventRecord(ev2, h->stream));
+    HIPCHK(h, hipEventRecord(ev2, ksim_stream(h)));
     HIPCHK(h, hipEventSynchronize(ev2));
     float build_ms = 0.f, run_ms = 0.f;
     HIPCHK(h, hipEventElapsedTime(&build_ms, h->ev0, h->ev1));
@@ -1356,9 +1361,9 @@ int ksim_evaluate(ksim_handle* h, int64_t pod, uint8_t* out_fit, uint32_t* out_r
   int rc;
   if ((rc = dev_alloc(h, &f, n)) || (rc = dev_alloc(h, &r, n)) || (rc = dev_alloc(h, &s, n)) || (rc = dev_alloc(h, &rcl, n)))
     return rc;
-  hipError_t e = ksim_launch_eval(&c, pod, f, r, s, rcl, h->stream);
+  hipError_t e = ksim_launch_eval(&c, pod, f, r, s, rcl, ksim_stream(h));
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "eval launch: %s", hipGetErrorString(e));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   if (out_fit) HIPCHK(h, hipMemcpy(out_fit, f, n, hipMemcpyDeviceToHost));
   if (out_reasons) HIPCHK(h, hipMemcpy(out_reasons, r, n * 4, hipMemcpyDeviceToHost));
   if (out_score) HIPCHK(h, hipMemcpy(out_score, s, n * 8, hipMemcpyDeviceToHost));
@@ -1485,17 +1490,17 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
       HIPCHK(h, hipMemcpy(&err0, c.err, 4, hipMemcpyDeviceToHost));
       for (int32_t s0 = 0; s0 < n_scen; s0 += chunk) {
         sw.nsc = std::min(chunk, n_scen - s0);
-        HIPCHK(h, hipMemcpyAsync(dcfg, cfgs.data() + s0, sw.nsc * sizeof(kf64::EvCfg), hipMemcpyHostToDevice, h->stream));
-        HIPCHK(h, hipEventRecord(h->ev0, h->stream));
-        hipError_t e = ksim_tree_sweep_init(&c, &sw, h->stream);
-        if (e == hipSuccess) e = ksim_tree_build(&c, &g, h->tclass, h->tcls, leaves, levels, fitc, h->t_y, &sw, h->stream);
+        HIPCHK(h, hipMemcpyAsync(dcfg, cfgs.data() + s0, sw.nsc * sizeof(kf64::EvCfg), hipMemcpyHostToDevice, ksim_stream(h)));
+        HIPCHK(h, hipEventRecord(h->ev0, ksim_stream(h)));
+        hipError_t e = ksim_tree_sweep_init(&c, &sw, ksim_stream(h));
+        if (e == hipSuccess) e = ksim_tree_build(&c, &g, h->tclass, h->tcls, leaves, levels, fitc, h->t_y, &sw, ksim_stream(h));
         if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "tree sweep build: %s", hipGetErrorString(e));
-        HIPCHK(h, hipEventRecord(h->ev1, h->stream));
-        e = ksim_tree_launch(&c, &g, h->tclass, h->tcls, leaves, levels, fitc, h->t_y, &sw, h->stream);
+        HIPCHK(h, hipEventRecord(h->ev1, ksim_stream(h)));
+        e = ksim_tree_launch(&c, &g, h->tclass, h->tcls, leaves, levels, fitc, h->t_y, &sw, ksim_stream(h));
         if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "tree sweep launch: %s", hipGetErrorString(e));
         hipEvent_t ev2 = nullptr;
         HIPCHK(h, hipEventCreate(&ev2));
-        HIPCHK(h, hipEventRecord(ev2, h->stream));
+        HIPCHK(h, hipEventRecord(ev2, ksim_stream(h)));
         HIPCHK(h, hipEventSynchronize(ev2));
         float b_ms = 0.f, r_ms = 0.f;
         HIPCHK(h, hipEventElapsedTime(&b_ms, h->ev0, h->ev1));
@@ -1534,7 +1539,7 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
     if ((rc = dev_alloc(h, &h->sw_dac, n)) || (rc = dev_alloc(h, &h->sw_dam, n)) || (rc = dev_alloc(h, &h->sw_yc, n)) ||
         (rc = dev_alloc(h, &h->sw_ym, n)))
       return rc;
-    hipError_t e = ksim_sweep_prepare(c.alloc_cpu, c.alloc_mem, n, h->sw_dac, h->sw_dam, h->sw_yc, h->sw_ym, h->stream);
+    hipError_t e = ksim_sweep_prepare(c.alloc_cpu, c.alloc_mem, n, h->sw_dac, h->sw_dam, h->sw_yc, h->sw_ym, ksim_stream(h));
     if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "sweep prepare: %s", hipGetErrorString(e));
   }
   // scratch: [S][n] x (4 float64 + int32), pods, weights, outputs
@@ -1572,9 +1577,9 @@ int ksim_sweep(ksim_handle* h, const int64_t* weights, int32_t n_scen, int64_t f
   a.out_counter = (uint64_t*)(q + b_pod + b_w + b_out);
   a.preds = c.preds; a.no_prio = c.no_prio;
   HIPCHK(h, hipMemcpy(&a.counter0, c.counter, 8, hipMemcpyDeviceToHost));
-  HIPCHK(h, hipMemcpyAsync(dw, w3.data(), S * 12, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(dw, w3.data(), S * 12, hipMemcpyHostToDevice, ksim_stream(h)));
   hipError_t e = ksim_sweep_launch(c.req_cpu, c.req_mem, c.nz_cpu, c.nz_mem, c.pod_count, c.pods + first,
-                                   (void*)a.pods, &a, n_scen, h->ev0, h->ev1, h->stream);
+                                   (void*)a.pods, &a, n_scen, h->ev0, h->ev1, ksim_stream(h));
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "sweep launch: %s", hipGetErrorString(e));
   HIPCHK(h, hipEventSynchronize(h->ev1));
   float ms = 0.f;
@@ -1671,7 +1676,7 @@ int ksim_read_nodes(ksim_handle* h, ksim_node_state* o) {
   if (!h || !o) return ksim_fail(h, KSIM_E_INVAL, "ksim_read_nodes: null argument");
   if (!h->have_nodes) return ksim_fail(h, KSIM_E_STATE, "ksim_read_nodes: no node table");
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   const KsimCtx& c = h->ctx;
   const size_t n = c.n;
   if (o->req_cpu) HIPCHK(h, hipMemcpy(o->req_cpu, c.req_cpu, n * 8, hipMemcpyDeviceToHost));
@@ -1691,7 +1696,7 @@ int ksim_read_nodes(ksim_handle* h, ksim_node_state* o) {
 int ksim_get_counter(ksim_handle* h, uint64_t* out) {
   if (!h || !out) return ksim_fail(h, KSIM_E_INVAL, "ksim_get_counter: null argument");
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   HIPCHK(h, hipMemcpy(out, h->ctx.counter, 8, hipMemcpyDeviceToHost));
   return KSIM_OK;
 }
@@ -1699,7 +1704,7 @@ int ksim_get_counter(ksim_handle* h, uint64_t* out) {
 int ksim_set_counter(ksim_handle* h, uint64_t v) {
   if (!h) return ksim_fail(h, KSIM_E_INVAL, "ksim_set_counter: null handle");
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   HIPCHK(h, hipMemcpy(h->ctx.counter, &v, 8, hipMemcpyHostToDevice));
   return KSIM_OK;
 }

@@ -118,9 +118,9 @@ static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
     sc = h->vol_h.slot_count;
   } else {  // [S][n] → [S'][n]: the first S rows are one contiguous block
     if ((rc = dev_alloc(h, &slots, (size_t)t->vol_slots * n)) || (rc = dev_alloc(h, &sc, (size_t)n))) return rc;
-    HIPCHK(h, hipMemsetAsync(slots, 0, (size_t)t->vol_slots * n * 8, h->stream));
-    HIPCHK(h, hipMemcpyAsync(slots, h->vol_h.slots, (size_t)h->vol_h.vol_slots * n * 8, hipMemcpyDeviceToDevice, h->stream));
-    HIPCHK(h, hipMemcpyAsync(sc, h->vol_h.slot_count, (size_t)n * 4, hipMemcpyDeviceToDevice, h->stream));
+    HIPCHK(h, hipMemsetAsync(slots, 0, (size_t)t->vol_slots * n * 8, ksim_stream(h)));
+    HIPCHK(h, hipMemcpyAsync(slots, h->vol_h.slots, (size_t)h->vol_h.vol_slots * n * 8, hipMemcpyDeviceToDevice, ksim_stream(h)));
+    HIPCHK(h, hipMemcpyAsync(sc, h->vol_h.slot_count, (size_t)n * 4, hipMemcpyDeviceToDevice, ksim_stream(h)));
   }
   V.n = n;
   V.slots = slots; V.slot_count = sc;
@@ -133,13 +133,13 @@ static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
   V.vol_slots = t->vol_slots;
   V.zone_words = t->zone_words;
   put(o_V, &V, sizeof V);
-  HIPCHK(h, hipMemcpyAsync(base, hb.data(), off, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(h, hipMemcpyAsync(base, hb.data(), off, hipMemcpyHostToDevice, ksim_stream(h)));
   KsimVol* dev = reinterpret_cast<KsimVol*>(base);
   std::vector<void*> fresh;  // this load's mount buffers (taken before any free shifts h->bufs)
   for (size_t k = nb0; k < h->bufs.size(); ++k) fresh.push_back(h->bufs[k].p);
   if (carry) { fresh.push_back(slots); fresh.push_back(sc); }
   const bool frees = old_small || !carry;
-  if (frees) HIPCHK(h, hipStreamSynchronize(h->stream));
+  if (frees) HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   for (void* q : h->vol_bufs)  // the previous mounts (reload / re-layout), unless carried over
     if (!(carry && (q == (void*)slots || q == (void*)sc))) dev_free(h, q);
   if (old_small) dev_free(h, old_small);
@@ -171,7 +171,7 @@ extern "C" int ksim_read_volumes(ksim_handle* h, uint64_t* slots, int32_t* slot_
   if (!h) return ksim_fail(h, KSIM_E_INVAL, "ksim_read_volumes: null handle");
   if (!h->have_vol) return ksim_fail(h, KSIM_E_STATE, "ksim_read_volumes: no volume tables loaded");
   HIPCHK(h, hipSetDevice(h->device));
-  HIPCHK(h, hipStreamSynchronize(h->stream));
+  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   const KsimVol& V = h->vol_h;
   if (slots && V.vol_slots)
     HIPCHK(h, hipMemcpy(slots, V.slots, (size_t)V.vol_slots * V.n * 8, hipMemcpyDeviceToHost));
