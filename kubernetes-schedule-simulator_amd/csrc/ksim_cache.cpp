@@ -352,9 +352,12 @@ int serve_post(ksim_handle* h, int32_t type, const ksim_pod& p, const uint64_t* 
   // the system-scope acquire only after commits of state other blocks read (inter-pod affinity /
   // service counts, volumes); KSIM_SERVE_LIGHT=0: before every message
   static const bool light_off = getenv("KSIM_SERVE_LIGHT") && getenv("KSIM_SERVE_LIGHT")[0] == '0';
+  // serve_shared: a commit of such state since the last SCHEDULE message.  Every block takes every
+  // SCHEDULE message (each publishes records for it), but a block may skip an ASSUME onto another
+  // block's node, so the pending acquire is cleared only by a SCHEDULE message.
   const bool shared = ksim_is_aff_host(h, p) || p.vol_class != 0;
   const int32_t sync = h->serve_shared || light_off ? KSIM_SERVE_SYNC_ACQUIRE : 0;
-  h->serve_shared = shared;
+  h->serve_shared = type == KSIM_SERVE_SCHEDULE ? shared : (h->serve_shared || shared);
   memset(b->res, 0, sizeof b->res);
   b->res[KSIM_RES_NODE] = INT32_MIN;
   const uint64_t seq = serve_write(h, type, &p, ports, scalars, no_commit, node, tag, sync);
@@ -482,16 +485,14 @@ int ksim_serve_stop(ksim_handle* h) {
   uint64_t d[32];
   HIPCHK(h, hipMemcpy(d, h->ctx.dbg + 64, sizeof d, hipMemcpyDeviceToHost));
   HIPCHK(h, hipMemset(h->ctx.dbg + 64, 0, sizeof d));
-  if (d[16 + 1])
-    fprintf(stderr, "[ksim stamps] serve: %llu block-messages, us per phase (count): poll %.2f (%llu) copy %.2f (%llu) "
-            "eval %.2f (%llu) passA %.2f (%llu) records+decision %.2f (%llu) owner-select %.2f (%llu) commit %.2f (%llu) "
-            "publish %.2f (%llu)\n", (unsigned long long)d[17],
-            d[0] / 100.0 / std::max<uint64_t>(d[16], 1), (unsigned long long)d[16], d[1] / 100.0 / std::max<uint64_t>(d[17], 1),
-            (unsigned long long)d[17], d[2] / 100.0 / std::max<uint64_t>(d[18], 1), (unsigned long long)d[18],
-            d[3] / 100.0 / std::max<uint64_t>(d[19], 1), (unsigned long long)d[19], d[4] / 100.0 / std::max<uint64_t>(d[20], 1),
-            (unsigned long long)d[20], d[5] / 100.0 / std::max<uint64_t>(d[21], 1), (unsigned long long)d[21],
-            d[6] / 100.0 / std::max<uint64_t>(d[22], 1), (unsigned long long)d[22], d[7] / 100.0 / std::max<uint64_t>(d[23], 1),
-            (unsigned long long)d[23]);
+  static const char* names[11] = {"idle+poll", "copy", "eval", "passA", "publish", "records-wait", "class-stats",
+                                  "decision", "owner-select", "commit", "answer"};
+  if (d[16 + 1]) {
+    fprintf(stderr, "[ksim stamps] serve: %llu block-messages, us per phase (count):", (unsigned long long)d[17]);
+    for (int k = 0; k < 11; ++k)
+      fprintf(stderr, " %s %.2f (%llu)", names[k], d[k] / 100.0 / std::max<uint64_t>(d[16 + k], 1), (unsigned long long)d[16 + k]);
+    fprintf(stderr, " | polls per message %.2f\n", (double)d[11] / std::max<uint64_t>(d[27], 1));
+  }
 #endif
   return KSIM_OK;
 }
@@ -609,8 +610,16 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
           memcpy(&out->last_node_index, r + KSIM_RES_CTR, 8);
           if (out->node < 0) memcpy(out->reasons, r + KSIM_RES_REASONS, sizeof out->reasons);
           if (r[KSIM_RES_ERR] & 128) return ksim_rt_svc_refusal(h);
-          if (r[KSIM_RES_ERR] || out->node == INT32_MIN)
-            return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x (resident pick)", r[KSIM_RES_ERR]);
+          if (r[KSIM_RES_ERR] || out->node == INT32_MIN) {
+            uint64_t d2[2] = {0, 0};  // the kernel's note of its first failure (site, block, tag, message)
+            if (h->serve_live) (void)ksim_serve_stop(h);
+            (void)hipMemcpy(d2, h->ctx.dbg + 96, sizeof d2, hipMemcpyDeviceToHost);
+            return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x (resident pick; site %llu block %llu tag %llu "
+                             "message %llu detail 0x%llx; this message %llu tag %u)", r[KSIM_RES_ERR],
+                             (unsigned long long)(d2[0] & 255), (unsigned long long)((d2[0] >> 8) & 255),
+                             (unsigned long long)((d2[0] >> 16) & 255), (unsigned long long)(d2[0] >> 24),
+                             (unsigned long long)d2[1], (unsigned long long)h->serve_seq, h->pick_tag);
+          }
           if (assume && out->node >= 0) {
             rc = after_commit(h, pod->port_cnt, r);
             oc.lap(3);

@@ -497,7 +497,7 @@ struct PhaseClock {
   }
 };
 
-void schedule(Cache* c, const PodObj& p, int32_t assume, ksim_result* out) {
+void schedule(Cache* c, PodObj p, int32_t assume, ksim_result* out) {
   PhaseClock pc(c);
   if (pc.on) c->prof[6] += 1;
   Enc e = encode(c, p);
@@ -522,14 +522,13 @@ void schedule(Cache* c, const PodObj& p, int32_t assume, ksim_result* out) {
   if (dup) fail(KSIM_E_STATE, "pod %s is in the cache, so can't be assumed", key.c_str());
   // the device already holds the commit: record it host-side with the assumed pod's encoding
   const Str& host = c->names[out->node];
-  PodObj a = p;
-  a.node_name = host;
+  p.node_name = host;  // (the call's own copy: moved into the cache below)
   e.row.host = out->node;
   Info& info = c->infos[host];
   mount(c, host, e, 1);
-  info.pods[key] = PodRec{a, std::move(e)};
-  c->pod_states[key] = a;
+  c->pod_states[key] = p;
   c->assumed.insert(key);
+  info.pods[key] = PodRec{std::move(p), std::move(e)};
   pc.lap(5);
 }
 

@@ -1564,9 +1564,10 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   ipa0.sp = -1;
   const bool pass_a = ipa.on || ipa.sp >= 0;
   const int NZ = (ipa.sp >= 0) ? c.aff->n_zone : 0;  // <= KSIM_PICK_ZMAX (host-checked)
+  __shared__ uint32_t s_dflag;  // the decision is in LDS (wave 0 → the other waves)
   if (tid < KSIM_NREASONS) s_hist[tid] = 0;
   if (tid < KSIM_PICK_ZMAX) s_z[tid] = 0;
-  if (tid == 0) s_ok = 1;
+  if (tid == 0) { s_ok = 1; s_dflag = 0; }
   __syncthreads();
 
   const int64_t base = (int64_t)me * c.chunk;
@@ -1579,8 +1580,15 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
 
   PKST(2);
   // the first spin that hits its bound: err bit 2 (a consistency error; the grid is co-resident)
-  auto spin_fail = [&]() {
-    if (lane == 0) { atomicOr(c.err, 2); s_ok = 0; }
+  // the first consistency failure of a handle, for the host's error message: dbg[96] =
+  // site | me << 8 | tag << 16 | seq << 24, dbg[97] = a detail (KSIM_PICK_NOTE)
+  auto note = [&](uint64_t site, uint64_t detail) {
+    if (c.dbg && atomicCAS((unsigned long long*)&c.dbg[96], 0ull,
+                           (unsigned long long)(site | (uint64_t)me << 8 | (uint64_t)tag << 16 | (seq & 0xffffffffull) << 24)) == 0ull)
+      atomicExch((unsigned long long*)&c.dbg[97], (unsigned long long)detail);
+  };
+  auto spin_fail = [&](int site) {
+    if (lane == 0) { atomicOr(c.err, 2); s_ok = 0; note(site, 0); }
   };
 
   if (pass_a) {  // (uniform) pass A over the fit nodes: the block's partial, then every block's
@@ -1614,8 +1622,11 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
     hz = ksimw::max_i64(hz);
     if (lane == 0) { s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz; }
     __syncthreads();
-    if (wv == 0) {
-      // publish: word x = lane x (0..3 the maxima over this block's waves, 4.. the zone sums)
+    const int W = 4 + NZ;
+    if (wv == 1) {
+      // publish: word x = lane x (0..3 the maxima over this block's waves, 4.. the zone sums).
+      // Wave 1 stores, wave 0 polls: a store counts in the storing wave's vmcnt until it is
+      // acknowledged, and the poll's loads would otherwise wait for that acknowledgement too.
       int64_t v = 0;
       if (lane < 4) {
         v = s_v[lane][0];
@@ -1624,8 +1635,9 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
       } else if (lane - 4 < NZ) {
         v = (int64_t)s_z[lane - 4];
       }
-      const int W = 4 + NZ;
       if (lane < W) pk_store(recA + (int64_t)me * KSIM_PICK_RA + lane, pk_enc(tag, v));
+    }
+    if (wv == 0) {
       // every block's record: lane x combines word x over the blocks
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       int64_t acc = 0;
@@ -1646,7 +1658,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
           }
         }
         if (__all(ok)) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { spin_fail(); break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { spin_fail(1); break; }
         __builtin_amdgcn_s_sleep(1);
       }
       if (lane < 4) s_pa[lane] = acc;
@@ -1695,20 +1707,25 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
     }
     if (lane == 0) { s_mx[wv][q] = wm; s_cnt[wv][q] = wm == INT64_MIN ? 0 : n; }
   }
+  __syncthreads();
+  // the reasons histogram only when this block fits nothing (it is published only then)
+  const int32_t F0 = s_fit[0] + s_fit[1] + s_fit[2] + s_fit[3];
+  if (F0 == 0) {  // (uniform)
 #pragma unroll
-  for (int k = 0; k < NPT; ++k) {
-    if (__ballot(rm[k] != 0)) {
-      for (int r = 0; r < KSIM_NREASONS; ++r) {
-        const int32_t n = __popcll(__ballot((rm[k] >> r) & 1u));
-        if (lane == 0 && n) atomicAdd(&s_hist[r], n);
+    for (int k = 0; k < NPT; ++k) {
+      if (__ballot(rm[k] != 0)) {
+        for (int r = 0; r < KSIM_NREASONS; ++r) {
+          const int32_t n = __popcll(__ballot((rm[k] >> r) & 1u));
+          if (lane == 0 && n) atomicAdd(&s_hist[r], n);
+        }
       }
     }
+    __syncthreads();
   }
-  __syncthreads();
 
-  if (wv == 0) {
-    // ---- this block's record: fit, per class (max, count), reasons when it fits nothing ----
-    const int32_t F0 = s_fit[0] + s_fit[1] + s_fit[2] + s_fit[3];
+  if (wv <= 1) {
+    // ---- this block's record: fit, per class (max, count), reasons when it fits nothing; wave 1
+    // stores it, wave 0 keeps the per-class maxima and polls (see pass A) ----
     int64_t bm = INT64_MIN;
     int32_t bc = 0;
     if (lane < K) {
@@ -1717,18 +1734,23 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
         if (s_mx[w][lane] > bm) { bm = s_mx[w][lane]; bc = s_cnt[w][lane]; }
         else if (s_mx[w][lane] == bm) bc += s_cnt[w][lane];
       }
-      s_bmax[lane] = bc ? bm : INT64_MIN;
+      if (wv == 0) s_bmax[lane] = bc ? bm : INT64_MIN;
     }
-    const int WB = 1 + 2 * K + (F0 == 0 ? KSIM_NREASONS : 0);
-    // word x = lane x: fit, then class q's max (word 1 + q), its count (word 1 + K + q), reasons
-    const int64_t mq = __shfl(bm, (lane - 1) & 63, 64);
-    const int32_t cq = __shfl(bc, (lane - 1) & 63, 64), cq2 = __shfl(bc, (lane - 1 - K) & 63, 64);
-    int64_t v = 0;
-    if (lane == 0) v = F0;
-    else if (lane <= K) v = cq ? mq : 0;  // (a class without fit nodes: count 0, max unread)
-    else if (lane <= 2 * K) v = cq2;
-    else if (lane < WB) v = s_hist[lane - 1 - 2 * K];
-    if (lane < WB) pk_store(recB + (int64_t)me * KSIM_PICK_RB + lane, pk_enc(tag, v));
+    if (wv == 1) {
+      const int WB = 1 + 2 * K + (F0 == 0 ? KSIM_NREASONS : 0);
+      // word x = lane x: fit, then class q's max (word 1 + q), its count (word 1 + K + q), reasons
+      const int64_t mq = __shfl(bm, (lane - 1) & 63, 64);
+      const int32_t cq = __shfl(bc, (lane - 1) & 63, 64), cq2 = __shfl(bc, (lane - 1 - K) & 63, 64);
+      int64_t v = 0;
+      if (lane == 0) v = F0;
+      else if (lane <= K) v = cq ? mq : 0;  // (a class without fit nodes: count 0, max unread)
+      else if (lane <= 2 * K) v = cq2;
+      else if (lane < WB) v = s_hist[lane - 1 - 2 * K];
+      if (lane < WB) pk_store(recB + (int64_t)me * KSIM_PICK_RB + lane, pk_enc(tag, v));
+    }
+  }
+  if (wv == 0) {
+    PKST(4);
     // ---- every block's record (lane b = block b, staged in LDS), then the decision, the same in
     // every block ----
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -1748,9 +1770,10 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
           }
         }
       if (__all(ok)) break;
-      if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { spin_fail(); break; }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { spin_fail(2); break; }
       __builtin_amdgcn_s_sleep(1);
     }
+    PKST(5);
     const bool in = lane < G;
     const int32_t fb = in ? (int32_t)s_rec[lane][0] : 0;
     const int32_t F = ksimw::sum_i32(fb);
@@ -1765,26 +1788,25 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
         const int32_t n = ksimw::sum_i32((cb && mb == m) ? cb : 0);
         if (lane == 0) { s_M[q] = m; s_C[q] = n; }
       }
-      // reduce priorities over the filtered set (NormalizeReduce), as ksim_scan_kernel (every lane
-      // the same values: LDS broadcasts)
-      int64_t mxT = 0, mxA = 0;
-      for (int q = 0; q < K; ++q) {
-        if (s_C[q] == 0) continue;
-        if (k1 > 1 || c.w[KSIM_W_TAINT_TOLERATION]) mxT = s_tv[q] > mxT ? s_tv[q] : mxT;
-        if (k2 > 1 || c.w[KSIM_W_NODE_AFFINITY]) mxA = s_av[q] > mxA ? s_av[q] : mxA;
+      PKST(6);
+      // reduce priorities over the filtered set (NormalizeReduce), as ksim_scan_kernel, lane q =
+      // class q: the maxima over the live classes and the winners by wave reductions
+      const bool live = lane < K && s_C[lane] > 0;
+      const int64_t tvq = lane < K ? s_tv[lane] : 0, avq = lane < K ? s_av[lane] : 0;
+      const int64_t mxT = ksimw::max_i64(live && (k1 > 1 || c.w[KSIM_W_TAINT_TOLERATION]) ? tvq : 0);
+      const int64_t mxA = ksimw::max_i64(live && (k2 > 1 || c.w[KSIM_W_NODE_AFFINITY]) ? avq : 0);
+      int64_t tot = INT64_MIN;
+      if (live) {
+        uint64_t t = (uint64_t)s_M[lane];
+        if (c.w[KSIM_W_TAINT_TOLERATION]) t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(tvq, mxT, true);
+        if (c.w[KSIM_W_NODE_AFFINITY]) t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(avq, mxA, false);
+        t += (uint64_t)s_ad[lane];  // NodePreferAvoidPods
+        tot = (int64_t)t;
       }
-      auto total_of = [&](int q) -> int64_t {
-        uint64_t t = (uint64_t)s_M[q];
-        if (c.w[KSIM_W_TAINT_TOLERATION]) t += (uint64_t)c.w[KSIM_W_TAINT_TOLERATION] * (uint64_t)ksim_norm(s_tv[q], mxT, true);
-        if (c.w[KSIM_W_NODE_AFFINITY]) t += (uint64_t)c.w[KSIM_W_NODE_AFFINITY] * (uint64_t)ksim_norm(s_av[q], mxA, false);
-        t += (uint64_t)s_ad[q];  // NodePreferAvoidPods
-        return (int64_t)t;
-      };
-      int64_t best = INT64_MIN;
-      for (int q = 0; q < K; ++q)
-        if (s_C[q]) { const int64_t t = total_of(q); best = t > best ? t : best; }
-      for (int q = 0; q < K; ++q)
-        if (s_C[q] && total_of(q) == best) { win |= 1u << q; C += s_C[q]; }
+      const int64_t best = ksimw::max_i64(tot);
+      const bool w_q = live && tot == best;
+      win = (uint32_t)__ballot(w_q);
+      C = ksimw::sum_i32(w_q ? s_C[lane] : 0);
     }
     // selectHost: the ix-th match counted from the largest name rank down (blocks from the top)
     const uint64_t li = s_ctr;
@@ -1806,7 +1828,11 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
     const int owner = hb ? 63 - __builtin_clzll(hb) : -1;
     const int32_t rank = owner >= 0 ? (int32_t)ix - __builtin_amdgcn_readlane(above, owner) : 0;
     if (lane == 0) {
-      if (mode != 0 && owner < 0) { atomicOr(c.err, 2); mode = 0; }  // inconsistent counts: must never happen
+      if (mode != 0 && owner < 0) {  // inconsistent counts: must never happen
+        atomicOr(c.err, 2);
+        note(4, (uint64_t)(uint32_t)total << 32 | (uint64_t)(uint32_t)C);
+        mode = 0;
+      }
       s_mode = s_ok ? mode : -1;
       s_owner = owner;
       s_rank = rank;
@@ -1816,9 +1842,13 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
       if (ctr_keep) *ctr_keep = s_ctr;
     }
     if (mode != 2 && lane < KSIM_MAX_RCLASS) s_M[lane] = INT64_MIN;
+    // the decision to the other waves through an LDS flag, not a barrier: a barrier would also
+    // wait for wave 1's record store to be acknowledged (the waits before s_barrier)
+    if (lane == 0) __hip_atomic_store(&s_dflag, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+  } else {
+    while (__hip_atomic_load(&s_dflag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) __builtin_amdgcn_s_sleep(1);
   }
-  __syncthreads();
-  PKST(4);
+  PKST(7);
   const int mode = s_mode;
   if (mode < 0) {  // a spin hit its bound (err set): nothing committed
     if (done && me == 0 && tid == 0) {  // (the resident form: the host must hear of it)
@@ -1849,7 +1879,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
           }
         }
         if (__all(ok)) break;
-        if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { atomicOr(c.err, 2); break; }
+        if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { atomicOr(c.err, 2); if (lane == 0) note(3, 0); break; }
         __builtin_amdgcn_s_sleep(1);
       }
       if (lane < KSIM_NREASONS) pk_res(done, &c.out_reasons[pod * KSIM_NREASONS + lane], v);
@@ -1862,7 +1892,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
           pk_res(done, &c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1], (int32_t)(uint32_t)(s_ctr >> 32));
         }
         if (done) pk_publish(done, seq);  // (the wave's reason stores above are ordered before it)
-        PKST(7);
+        PKST(10);
       }
     }
     return;
@@ -1899,12 +1929,12 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
       if (hb2) node = (int64_t)me * c.chunk + (int64_t)kt * KSIM_BLOCK + wt * 64 + __builtin_ctzll(hb2);
     }
     if (lane == 0) {
-      if (node < 0) atomicOr(c.err, 2);  // inconsistent masks: must never happen
+      if (node < 0) { atomicOr(c.err, 2); note(5, (uint64_t)(uint32_t)s_rank); }  // inconsistent masks: must never happen
       s_node = node;
     }
   }
   __syncthreads();
-  PKST(5);
+  PKST(8);
   const int64_t node = s_node;
   if (node >= 0 && !no_commit) {
     if (wv == 0) {
@@ -1919,7 +1949,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
     }
   }
   __syncthreads();
-  PKST(6);
+  PKST(9);
   if (tid == 0) {
     if (mode == 2) *c.counter = s_ctr;
     pk_res(done, &c.out_node[pod], (int32_t)node);
@@ -1930,7 +1960,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
       pk_res(done, &c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1], (int32_t)(uint32_t)(s_ctr >> 32));
     }
     if (done) pk_publish(done, seq);  // after the barrier: every wave's commit stores are issued before it
-    PKST(7);
+    PKST(10);
   }
 #undef PKST
 }
@@ -1962,32 +1992,41 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
   __shared__ uint32_t s_tag;
   __shared__ int64_t s_node;
   __shared__ uint32_t s_msg[KSIM_SERVE_MSG_WORDS];
+  __shared__ uint64_t s_seq;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, me = blockIdx.x;
   if (tid == 0) s_keep = *c.counter;
 #ifdef KSIM_STAMPS
   // diagnostic builds: per phase, the sum of (stamp k - stamp k-1) and how often both were taken,
   // over every block and message, into dbg[64 + k] / dbg[80 + k] at the exit (k = 0: the poll)
-  __shared__ uint64_t s_st[8], s_sum[8], s_cnt[8];
+  __shared__ uint64_t s_st[12], s_sum[12], s_cnt[12];
   uint64_t* const stamp = s_st;
-  if (tid < 8) { s_sum[tid] = 0; s_cnt[tid] = 0; s_st[tid] = 0; }
+  if (tid < 12) { s_sum[tid] = 0; s_cnt[tid] = 0; s_st[tid] = 0; }
+  uint64_t n_polls = 0;
   uint64_t t_end = __builtin_amdgcn_s_memrealtime();
 #else
   uint64_t* const stamp = nullptr;
 #endif
   uint64_t* const pod_ports = const_cast<uint64_t*>(c.pod_ports) + (int64_t)me * KSIM_ONE_PORTS;
   ksim_scalar_req* const pod_scalars = const_cast<ksim_scalar_req*>(c.pod_scalars) + (int64_t)me * KSIM_MAX_SCALAR;
-  for (uint64_t seq = seq0 + 1;; ++seq) {
+  // A block takes the newest complete message, which may be past the next one: a message answered
+  // by one block (an assume onto another block's node) does not wait for the others, so the host
+  // can post the next before this block has looked.  It never skips one it must answer or publish
+  // records for: the host waits for those.
+  uint64_t seq = seq0;
+  for (;;) {
     if (wv == 0) {
       // poll: lane l reads payload words 2l, 2l+1 with their tags in one 16-byte system-scope load
       typedef unsigned int u4 __attribute__((ext_vector_type(4)));
-      const uint32_t s32 = (uint32_t)seq;
+      const uint32_t s32 = (uint32_t)seq + 1u;  // the oldest message this block may take
       const uint64_t* src = box->msg + 2 * lane;
       u4 q;
       int32_t type = KSIM_SERVE_EXIT;
       const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
         asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(q) : "v"(src) : "memory");
-        if (__all(q.y == s32 && q.w == s32)) {
+        const uint32_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)q.y);
+        if ((int32_t)(t - s32) >= 0 && __all(q.y == t && q.w == t)) {
+          if (lane == 0) s_seq = seq + 1 + (uint64_t)(t - s32);
 #ifdef KSIM_STAMPS
           if (lane == 0) s_st[0] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1995,6 +2034,9 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
           break;
         }
         if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;  // (uniform: one clock read per wave)
+#ifdef KSIM_STAMPS
+        ++n_polls;
+#endif
         __builtin_amdgcn_s_sleep(1);
       }
       if (type == KSIM_SERVE_SCHEDULE || type == KSIM_SERVE_ASSUME) {
@@ -2038,6 +2080,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
     if (tid == 0) s_st[1] = __builtin_amdgcn_s_memrealtime();
 #endif
     const int32_t type = s_type;
+    if (type != KSIM_SERVE_EXIT) seq = s_seq;
     if (type == KSIM_SERVE_SCHEDULE) {
       const ksim_pod P = s_P;
       ksim_pick_body<NPT>(c, P, 0, s_tag, s_nc, c.pick + (s_tag & 1u) * KSIM_PICK_WORDS, &s_keep, &box->done, seq, stamp);
@@ -2066,7 +2109,10 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
     if (tid == 0) {
       if (s_st[0]) { s_sum[0] += s_st[0] - t_end; s_cnt[0] += 1; }
       uint64_t prev = s_st[0];
-      for (int k = 1; k < 8; ++k) {
+      s_sum[11] += n_polls;
+      s_cnt[11] += 1;
+      n_polls = 0;
+      for (int k = 1; k < 11; ++k) {
         if (s_st[k] && prev) { s_sum[k] += s_st[k] - prev; s_cnt[k] += 1; }
         if (s_st[k]) prev = s_st[k];
         s_st[k] = 0;
@@ -2077,7 +2123,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
 #endif
   }
 #ifdef KSIM_STAMPS
-  if (tid < 8) {
+  if (tid < 12) {
     atomicAdd((unsigned long long*)&c.dbg[64 + tid], (unsigned long long)s_sum[tid]);
     atomicAdd((unsigned long long*)&c.dbg[80 + tid], (unsigned long long)s_cnt[tid]);
   }

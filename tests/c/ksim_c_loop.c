@@ -336,16 +336,20 @@ static void event_loop(int steps) {
       host_remove(&nodes[w], &placed[k].pod, placed[k].port);
       placed[k] = placed[--np];
       ++n_rm;
-    } else if (r < 85) {  /* cache.AddPod of a pod bound elsewhere */
-      uint64_t port;
-      ksim_pod p = rnd_pod(&port);
-      const int64_t w = (int64_t)(rnd() % (uint64_t)n_nodes);
-      KS(h, ksim_pod_add(h, w, &p, &port, p.port_cnt, NULL, 0));
-      host_add(&nodes[w], &p, port);
-      placed[np].pod = p; placed[np].port = port;
-      strcpy(placed[np].node, nodes[w].name);
-      ++np;
-      ++n_add;
+    } else if (r < 85) {  /* cache.AddPod of a pod bound elsewhere (sometimes a burst: an informer
+                             resync; the resident per-pod kernel answers each from one block) */
+      const int burst = rnd() % 4 == 0 ? 12 : 1;
+      for (int b = 0; b < burst && np < steps; ++b) {
+        uint64_t port;
+        ksim_pod p = rnd_pod(&port);
+        const int64_t w = (int64_t)(rnd() % (uint64_t)n_nodes);
+        KS(h, ksim_pod_add(h, w, &p, &port, p.port_cnt, NULL, 0));
+        host_add(&nodes[w], &p, port);
+        placed[np].pod = p; placed[np].port = port;
+        strcpy(placed[np].node, nodes[w].name);
+        ++np;
+        ++n_add;
+      }
     } else if (r < 91 && n_nodes < MAXN - 1) {  /* cache.AddNode */
       HNode x = rnd_node(next_id++ % 997 * 1009 % 100003);
       if (rank_of(x.name) < n_nodes && strcmp(nodes[rank_of(x.name)].name, x.name) == 0) continue;
