@@ -2060,10 +2060,15 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
         const int32_t sy = (int32_t)s_msg[KSIM_SERVE_W_SYNC];
         // the previous message committed counts other blocks read (affinity / volumes): acquire them
         if (sy & KSIM_SERVE_SYNC_ACQUIRE) __atomic_thread_fence(__ATOMIC_ACQUIRE);
-        // this CU's L1 holds lines of the staging slot and of the rows this block committed as they
-        // were when last read: the stores above (and the last commit's) are acknowledged, then the
-        // L1 is invalidated, so every wave's loads below fetch them from the L2
+        // the staging stores (and the last commit's) are acknowledged before the barrier below; the
+        // CU's L1 needs no invalidation for them: every reader of a block's rows and staging slot is
+        // a wave of the same workgroup, i.e. on the same CU (workgroup-scope coherence, KSIM_SERVE_L1INV
+        // builds add the invalidation back for comparison)
+#ifdef KSIM_SERVE_L1INV
         asm volatile("s_waitcnt vmcnt(0)\n\tbuffer_inv sc0\n\ts_waitcnt vmcnt(0)" ::: "memory");
+#else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
         __builtin_amdgcn_wave_barrier();
         if (lane == 0) {
           s_P.port_off = me * KSIM_ONE_PORTS;
