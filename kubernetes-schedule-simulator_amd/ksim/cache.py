@@ -80,6 +80,7 @@ class SchedulerCache:
         self._aff_remap = None
         self._aff_check = False  # an affinity pod was cached on an unlisted node: re-check on the next call
         self.aff_reloads = 0     # affinity table loads so far (the per-pod path's amortised cost)
+        self._aff_tables = None  # the loaded affinity tables (host copy)
         self._aff_wanted = bool(self.cfg.predicates & abi.P_INTERPOD_AFFINITY or
                                 ((self.cfg.weights[abi.W_INTERPOD] or self.cfg.weights[abi.W_SPREAD])
                                  and not self.cfg.no_priorities))
@@ -435,6 +436,11 @@ class SchedulerCache:
         self._mount(name, enc, -1)
         if not info.pods and info.node is None:
             del self.infos[name]
+        if self._aff_tables is not None and self._aff_tables.get("svc_on"):
+            # the device only ever ORs service-affinity disagreements in (ksim_svc_commit): rebuild
+            # the tables (their conflict words from the pods still cached) at the next call, so a
+            # disagreement that left with this pod stops refusing its service identity
+            self._aff_check = True
 
     def assume_pod(self, pod):
         """cache.AssumePod (cache.go:125-143); pod.spec.nodeName is the chosen host."""
