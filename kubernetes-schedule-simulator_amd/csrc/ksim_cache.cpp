@@ -16,7 +16,10 @@
 // lastNodeIndex back the same way — one launch and one stream sync per call, no copies.  Node
 // events relayout the table in one kernel (rows stay in name-rank order).
 #include <chrono>
+#include <cstdarg>
 #include <cstdio>
+#include <mutex>
+#include <shared_mutex>
 
 #include "ksim_handle.h"
 #include "ksim_cache.h"
@@ -258,15 +261,21 @@ int after_commit(ksim_handle* h, int32_t port_cnt, const int32_t* r = nullptr) {
 }
 
 // ---- the resident per-pod service (ksim_serve_kernel in ksim_kernels.hip) ----
-// The kernel leaves after SERVE_IDLE_TICKS without a message; the host posts a message only within
-// SERVE_POST_NS of its previous post (or of the launch) and otherwise stops and relaunches it, so a
-// message never meets a grid that is on its way out.  KSIM_SERVE=0: per-pod launches only.
-constexpr uint64_t SERVE_IDLE_TICKS = 20000000ull;       // 200 ms of s_memrealtime (100 MHz)
-constexpr int64_t SERVE_POST_NS = 100000000;             // 100 ms
-constexpr int64_t SERVE_WAIT_NS = 10000000000ll;         // an answer's bound (the kernel's spins end in 2 s)
+// A block votes to leave after SERVE_IDLE_TICKS without a message; the grid leaves when the vote
+// is unanimous (KSIM_SERVE_ST_*, ksim_common.h), and a message the grid left before taking is
+// served by a fresh launch that finds it in the mailbox.  KSIM_SERVE=0: per-pod launches only.
+// KSIM_SERVE_IDLE_MS overrides the idle bound (tests).
+constexpr int64_t SERVE_WAIT_NS = 10000000000ll;  // an answer's bound (the kernel's spins end in 2 s)
+constexpr int SERVE_RELAUNCHES = 4;               // relaunches for one message (each finds it waiting)
 
 int64_t now_ns() {
   return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+uint64_t serve_idle_ticks() {
+  static const uint64_t t = getenv("KSIM_SERVE_IDLE_MS") ? strtoull(getenv("KSIM_SERVE_IDLE_MS"), nullptr, 10) * 100000ull
+                                                         : 20000000ull;  // 200 ms of s_memrealtime (100 MHz)
+  return t;
 }
 
 bool serve_wanted(const ksim_handle* h) {
@@ -278,7 +287,43 @@ size_t serve_stage_bytes(int grid) {
   return (size_t)grid * (sizeof(ksim_pod) + 8 * KSIM_ONE_PORTS + sizeof(ksim_scalar_req) * KSIM_MAX_SCALAR);
 }
 
-int serve_start(ksim_handle* h, int npt, int grid) {
+// ---- the device gate (KsimGate, ksim_handle.h) and the handles whose resident kernel runs ----
+struct DeviceGate {
+  std::shared_mutex mu;
+  std::mutex reg_mu;
+  std::vector<ksim_handle*> live;
+};
+DeviceGate& device_gate(int dev) {
+  static DeviceGate g[64];
+  return g[dev & 63];
+}
+thread_local int8_t t_gate_hold[64];  // per device: 0, 1 shared, 2 exclusive (this thread)
+
+void serve_register(ksim_handle* h, bool on) {
+  DeviceGate& g = device_gate(h->device);
+  std::lock_guard<std::mutex> lk(g.reg_mu);
+  g.live.erase(std::remove(g.live.begin(), g.live.end(), h), g.live.end());
+  if (on) g.live.push_back(h);
+}
+
+// The launch named in KsimServeBox::left: the grid left by its idle vote.
+bool serve_left(const ksim_handle* h) {
+  const uint64_t l = __atomic_load_n(&h->serve_box->left, __ATOMIC_ACQUIRE);
+  return (uint32_t)(l >> 32) == h->serve_launch_id;
+}
+
+// The grid left by its idle vote: drain the stream (its last blocks are on their way out).
+int serve_reap(ksim_handle* h) {
+  h->serve_live.store(false, std::memory_order_release);
+  serve_register(h, false);
+  HIPCHK(h, hipStreamSynchronize(h->stream_raw));
+  h->serve_stats[3] += 1;
+  return KSIM_OK;
+}
+
+// Launch the resident kernel over the current context; seq0 = the newest message already
+// handled (a relaunch for an untaken message passes the one before it).
+int serve_launch(ksim_handle* h, int npt, int grid, uint64_t seq0) {
   if (!h->serve_box) {
     KsimServeBox* b = nullptr;
     HIPCHK(h, hipHostMalloc((void**)&b, sizeof(KsimServeBox), hipHostMallocMapped | hipHostMallocCoherent));
@@ -287,7 +332,10 @@ int serve_start(ksim_handle* h, int npt, int grid) {
     HIPCHK(h, hipHostGetDevicePointer((void**)&d, b, 0));
     h->serve_box = b;
     h->serve_box_dev = d;
-    b->done = h->serve_seq;
+  }
+  if (!h->serve_state) {
+    int rc = dev_alloc(h, &h->serve_state, 1);
+    if (rc) return rc;
   }
   if (h->serve_grid < grid || !h->serve_stage) {
     dev_free(h, h->serve_stage);
@@ -305,20 +353,33 @@ int serve_start(ksim_handle* h, int npt, int grid) {
   cs.first = 0;
   cs.end = 1;
   cs.pick = h->pick_words;
-  KsimServeBox* bd = h->serve_box_dev;
-  cs.out_node = bd->res + KSIM_RES_NODE;
-  cs.out_fit = bd->res + KSIM_RES_FIT;
-  cs.out_reasons = bd->res + KSIM_RES_REASONS;
+  // (unused: the resident form answers in KsimServeBox::ans; the staging result block keeps the
+  // context's pointers valid for the pre-launch check)
+  int rc0 = ensure_staging(h, 0, 0);
+  if (rc0) return rc0;
+  cs.out_node = h->res_dev + KSIM_RES_NODE;
+  cs.out_fit = h->res_dev + KSIM_RES_FIT;
+  cs.out_reasons = h->res_dev + KSIM_RES_REASONS;
   int rc = ksim_rt_check_launch_ctx(h, cs, grid, "ksim_schedule_one (resident)");
   if (rc) return rc;
-  hipError_t e = ksim_launch_serve(&cs, bd, h->serve_seq, SERVE_IDLE_TICKS, npt, grid, h->stream_raw);
+  HIPCHK(h, hipMemsetAsync(h->serve_state, 0, 8, h->stream_raw));
+  KsimServeArgs a{};
+  a.box = h->serve_box_dev;
+  a.state = h->serve_state;
+  a.seq0 = seq0;
+  a.idle_ticks = serve_idle_ticks();
+  a.ctr0 = h->ctr_host;
+  a.ctr0_valid = h->ctr_known ? 1u : 0u;
+  if (++h->serve_launch_id == 0) h->serve_launch_id = 1;  // (0 = the `left` word's initial value)
+  a.launch_id = h->serve_launch_id;
+  hipError_t e = ksim_launch_serve(&cs, &a, npt, grid, h->stream_raw);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "resident per-pod kernel launch: %s", hipGetErrorString(e));
-  h->serve_live = true;
+  h->serve_live.store(true, std::memory_order_release);
+  serve_register(h, true);
   h->serve_shared = false;  // (the launch itself acquires)
   h->serve_base = h->ctx;
   h->serve_npt = npt;
   h->serve_grid = grid;
-  h->serve_post_ns = now_ns();
   h->serve_stats[0] += 1;
   return KSIM_OK;
 }
@@ -345,10 +406,44 @@ uint64_t serve_write(ksim_handle* h, int32_t type, const ksim_pod* p, const uint
   return seq;
 }
 
-// Post one message and wait for its answer (the result block of the mailbox).
+// The answer to message seq, when every word the host reads carries its number (node, fit,
+// status, error, lastNodeIndex; the reasons of a FitError).
+bool serve_answer(const ksim_handle* h, uint64_t seq, int32_t* r) {
+  const uint32_t s = (uint32_t)seq;
+  const uint64_t* a = h->serve_box->ans;
+  auto word = [&](int k) {
+    const uint64_t w = __atomic_load_n(&a[k], __ATOMIC_ACQUIRE);
+    r[k] = (int32_t)(uint32_t)w;
+    return (uint32_t)(w >> 32) == s;
+  };
+  for (int k : {KSIM_RES_NODE, KSIM_RES_FIT, KSIM_RES_STATUS, KSIM_RES_ERR, KSIM_RES_CTR, KSIM_RES_CTR + 1})
+    if (!word(k)) return false;
+  if (r[KSIM_RES_NODE] == -1) {
+    for (int k = 0; k < KSIM_NREASONS; ++k)
+      if (!word(KSIM_RES_REASONS + k)) return false;
+  } else {
+    memset(r + KSIM_RES_REASONS, 0, KSIM_NREASONS * 4);
+  }
+  return true;
+}
+
+// The resident kernel cannot serve this handle any more: per-pod launches from now on.
+int serve_fail(ksim_handle* h, const char* fmt, ...) {
+  char msg[256];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(msg, sizeof msg, fmt, ap);
+  va_end(ap);
+  h->serve_off = true;
+  if (h->serve_live.load() && !serve_left(h)) (void)ksim_serve_stop(h);
+  else if (h->serve_live.load()) (void)serve_reap(h);
+  return ksim_fail(h, KSIM_E_DEVICE, "%s", msg);
+}
+
+// Post one message and wait for its answer (r: KSIM_RES_WORDS result words).  Called under the
+// device gate (shared).
 int serve_post(ksim_handle* h, int32_t type, const ksim_pod& p, const uint64_t* ports, const ksim_scalar_req* scalars,
-               int32_t no_commit, int64_t node, uint32_t tag) {
-  KsimServeBox* b = h->serve_box;
+               int32_t no_commit, int64_t node, uint32_t tag, int32_t* r) {
   // the system-scope acquire only after commits of state other blocks read (inter-pod affinity /
   // service counts, volumes); KSIM_SERVE_LIGHT=0: before every message
   static const bool light_off = getenv("KSIM_SERVE_LIGHT") && getenv("KSIM_SERVE_LIGHT")[0] == '0';
@@ -358,43 +453,67 @@ int serve_post(ksim_handle* h, int32_t type, const ksim_pod& p, const uint64_t* 
   const bool shared = ksim_is_aff_host(h, p) || p.vol_class != 0;
   const int32_t sync = h->serve_shared || light_off ? KSIM_SERVE_SYNC_ACQUIRE : 0;
   h->serve_shared = type == KSIM_SERVE_SCHEDULE ? shared : (h->serve_shared || shared);
-  memset(b->res, 0, sizeof b->res);
-  b->res[KSIM_RES_NODE] = INT32_MIN;
   const uint64_t seq = serve_write(h, type, &p, ports, scalars, no_commit, node, tag, sync);
   h->serve_stats[1] += 1;
-  const int64_t t0 = now_ns();
-  int64_t next_check = t0 + 1000000;  // after 1 ms: is the kernel still there?
-  for (uint64_t spins = 0; __atomic_load_n(&b->done, __ATOMIC_ACQUIRE) != seq; ++spins) {
+  int64_t t0 = now_ns(), next_check = t0 + 1000000;  // every 1 ms: is the kernel still there?
+  int relaunches = 0;
+  for (uint64_t spins = 0; !serve_answer(h, seq, r); ++spins) {
     __builtin_ia32_pause();
-    if ((spins & 255) != 255) continue;
+    if ((spins & 63) != 63) continue;
+    if (serve_left(h)) {
+      // the grid agreed to leave before any block took this message (a block that voted takes a
+      // message only after withdrawing its vote, which fails once the vote is unanimous), so the
+      // message is still whole in the mailbox: a fresh launch takes it as its first
+      if (serve_answer(h, seq, r)) break;
+      if (++relaunches > SERVE_RELAUNCHES)
+        return serve_fail(h, "resident per-pod kernel: message %llu not taken after %d relaunches", (unsigned long long)seq,
+                          SERVE_RELAUNCHES);
+      int rc = serve_reap(h);
+      if (rc) return rc;
+      h->serve_stats[4] += 1;
+      if ((rc = serve_launch(h, h->serve_npt, h->serve_grid, seq - 1))) return rc;
+      t0 = now_ns();
+      next_check = t0 + 1000000;
+      continue;
+    }
     const int64_t t = now_ns();
     if (t < next_check) continue;
     next_check = t + 1000000;
     const bool gone = hipStreamQuery(h->stream_raw) == hipSuccess;
-    if (__atomic_load_n(&b->done, __ATOMIC_ACQUIRE) == seq) break;
-    if (gone || t - t0 > SERVE_WAIT_NS) {
-      h->serve_off = true;  // per-pod launches from now on
-      if (!gone) (void)ksim_serve_stop(h);
-      h->serve_live = false;
-      return ksim_fail(h, KSIM_E_DEVICE, "resident per-pod kernel %s (message %llu)", gone ? "left before answering" : "did not answer",
-                       (unsigned long long)seq);
-    }
+    if (serve_answer(h, seq, r) || serve_left(h)) continue;  // (the loop's checks take it from here)
+    if (gone || t - t0 > SERVE_WAIT_NS)
+      return serve_fail(h, "resident per-pod kernel %s (message %llu)", gone ? "left before answering" : "did not answer",
+                        (unsigned long long)seq);
   }
-  h->serve_post_ns = now_ns();
+  // lastNodeIndex: selectHost bumps it exactly when two or more nodes fit; an ASSUME leaves it
+  const int32_t err = r[KSIM_RES_ERR];
+  const uint64_t ctr = (uint64_t)(uint32_t)r[KSIM_RES_CTR] | ((uint64_t)(uint32_t)r[KSIM_RES_CTR + 1] << 32);
+  if (r[KSIM_RES_NODE] != INT32_MIN && err == 0) {
+    if (h->ctr_known) {
+      const uint64_t want = h->ctr_host + (type == KSIM_SERVE_SCHEDULE && r[KSIM_RES_FIT] >= 2 ? 1 : 0);
+      if (ctr != want)
+        return serve_fail(h, "resident per-pod kernel answered lastNodeIndex %llu, expected %llu (message %llu)",
+                          (unsigned long long)ctr, (unsigned long long)want, (unsigned long long)seq);
+    }
+    h->ctr_host = ctr;
+    h->ctr_known = true;
+  }
   return KSIM_OK;
 }
 
 // The resident kernel serves the current context with this geometry: (re)start it when not.
+// Called under the device gate (shared).
 int serve_ready(ksim_handle* h, int npt, int grid) {
-  if (h->serve_live) {
-    const bool stale = now_ns() - h->serve_post_ns > SERVE_POST_NS;
-    if (stale || h->serve_npt != npt || h->serve_grid != grid || memcmp(&h->ctx, &h->serve_base, sizeof(KsimCtx)) != 0) {
-      if (stale) h->serve_stats[3] += 1;
+  if (h->serve_live.load()) {
+    if (serve_left(h)) {  // the grid left by its idle vote while the host was away
+      int rc = serve_reap(h);
+      if (rc) return rc;
+    } else if (h->serve_npt != npt || h->serve_grid != grid || memcmp(&h->ctx, &h->serve_base, sizeof(KsimCtx)) != 0) {
       int rc = ksim_serve_stop(h);
       if (rc) return rc;
     }
   }
-  if (!h->serve_live) return serve_start(h, npt, grid);
+  if (!h->serve_live.load()) return serve_launch(h, npt, grid, h->serve_seq);
   return KSIM_OK;
 }
 
@@ -475,9 +594,46 @@ int node_shift(ksim_handle* h, int32_t op, int64_t index) {
 
 }  // namespace
 
+KsimGate::KsimGate(ksim_handle* h, bool exclusive) {
+  if (!h) return;
+  dev = h->device & 63;
+  if (t_gate_hold[dev]) return;  // held by this thread already (an exclusive holder's shared section)
+  DeviceGate& g = device_gate(dev);
+  if (!exclusive) {
+    g.mu.lock_shared();
+    mode = 1;
+    t_gate_hold[dev] = 1;
+    return;
+  }
+  g.mu.lock();
+  mode = 2;
+  t_gate_hold[dev] = 2;
+  // no other handle's call is inside its resident section now: stop their kernels on this device
+  std::vector<ksim_handle*> others;
+  {
+    std::lock_guard<std::mutex> lk(g.reg_mu);
+    for (ksim_handle* x : g.live)
+      if (x != h) others.push_back(x);
+  }
+  for (ksim_handle* x : others) (void)ksim_serve_stop(x);
+}
+
+KsimGate::~KsimGate() {
+  if (!mode) return;
+  DeviceGate& g = device_gate(dev);
+  t_gate_hold[dev] = 0;
+  if (mode == 2) g.mu.unlock();
+  else g.mu.unlock_shared();
+}
+
+void ksim_serve_forget(ksim_handle* h) { serve_register(h, false); }
+
 int ksim_serve_stop(ksim_handle* h) {
-  if (!h->serve_live) return KSIM_OK;
-  h->serve_live = false;  // (first: the drain below goes through the raw stream)
+  if (!h->serve_live.load(std::memory_order_acquire)) return KSIM_OK;
+  KsimGate gate(h, false);
+  if (!h->serve_live.load()) return KSIM_OK;
+  h->serve_live.store(false, std::memory_order_release);  // (first: the drain below goes through the raw stream)
+  serve_register(h, false);
   h->serve_stats[2] += 1;
   (void)serve_write(h, KSIM_SERVE_EXIT, nullptr, nullptr, nullptr, 0, -1, 0, 0);
   HIPCHK(h, hipStreamSynchronize(h->stream_raw));
@@ -580,54 +736,62 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
     for (int k = 0; k < KSIM_NW; ++k) sw += (c.w[k] > ((int64_t)1 << 40) ? ((int64_t)1 << 50) : c.w[k] * 10);
     if (h->pick_grid != grid || h->pick_npt != npt) {
       h->pick_ok = ksim_pick_coresident(npt, grid) != 0;
+      h->serve_fits = ksim_serve_coresident(npt, grid) != 0;
       h->pick_grid = grid;
       h->pick_npt = npt;
+      h->pick_clear = true;
     }
     if (sw < ((int64_t)1 << 54) && h->pick_ok) {
       if (!h->pick_words) {
         if ((rc = dev_alloc(h, &h->pick_words, (size_t)2 * KSIM_PICK_WORDS))) return rc;
+        h->pick_clear = true;
+      }
+      // A new geometry: a record slot of a block beyond the last call's grid still holds the tag of
+      // some older call, which the 8-bit tags (1..254) can come back to; both buffers are cleared
+      // (tag 0 is never used).  Within one geometry every call writes every word its readers read
+      // in the record buffer of its parity (pass-A words included), so a word always carries the
+      // tag of this call or of the previous call of that parity.
+      if (h->pick_clear) {
         HIPCHK(h, hipMemsetAsync(h->pick_words, 0, (size_t)2 * KSIM_PICK_WORDS * 8, ksim_stream(h)));
+        h->pick_clear = false;
       }
-      // 1..254, so consecutive calls alternate the record buffer (tag parity) and a buffer's words
-      // always carry the tag of an earlier call
       h->pick_tag = h->pick_tag % 254u + 1u;
-      if (serve_wanted(h) && pod->port_cnt <= KSIM_ONE_PORTS && pod->scalar_cnt <= KSIM_MAX_SCALAR) {
-        if (h->pick_grid != grid || !h->serve_live) {
-          if (!ksim_serve_coresident(npt, grid)) h->serve_off = true;
+      if (serve_wanted(h) && h->serve_fits && pod->port_cnt <= KSIM_ONE_PORTS && pod->scalar_cnt <= KSIM_MAX_SCALAR) {
+        KsimGate gate(h, false);
+        if ((rc = serve_ready(h, npt, grid))) return rc;
+        oc.lap(0);
+        const ksim_pod sp = staged_pod(h, *pod);
+        int32_t r[KSIM_RES_WORDS];
+        if ((rc = serve_post(h, KSIM_SERVE_SCHEDULE, sp, ports + pod->port_off, scalars + pod->scalar_off, assume ? 0 : 1, -1,
+                             h->pick_tag, r)))
+          return rc;
+        oc.lap(2);
+        memset(out, 0, sizeof *out);
+        out->node = r[KSIM_RES_NODE];
+        out->fit_nodes = r[KSIM_RES_FIT];
+        memcpy(&out->last_node_index, r + KSIM_RES_CTR, 8);
+        if (out->node < 0) memcpy(out->reasons, r + KSIM_RES_REASONS, sizeof out->reasons);
+        if (r[KSIM_RES_ERR] & 128) return ksim_rt_svc_refusal(h);
+        if (r[KSIM_RES_ERR] || out->node == INT32_MIN) {
+          uint64_t d2[2] = {0, 0};  // the kernel's note of its first failure (site, block, tag, message)
+          const int32_t err = r[KSIM_RES_ERR];
+          h->serve_off = true;
+          if (h->serve_live.load()) (void)ksim_serve_stop(h);
+          (void)hipMemcpy(d2, h->ctx.dbg + 96, sizeof d2, hipMemcpyDeviceToHost);
+          return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x (resident pick; site %llu block %llu tag %llu "
+                           "message %llu detail 0x%llx; this message %llu tag %u)", err,
+                           (unsigned long long)(d2[0] & 255), (unsigned long long)((d2[0] >> 8) & 255),
+                           (unsigned long long)((d2[0] >> 16) & 255), (unsigned long long)(d2[0] >> 24),
+                           (unsigned long long)d2[1], (unsigned long long)h->serve_seq, h->pick_tag);
         }
-        if (!h->serve_off) {
-          if ((rc = serve_ready(h, npt, grid))) return rc;
-          oc.lap(0);
-          const ksim_pod sp = staged_pod(h, *pod);
-          if ((rc = serve_post(h, KSIM_SERVE_SCHEDULE, sp, ports + pod->port_off, scalars + pod->scalar_off, assume ? 0 : 1, -1,
-                               h->pick_tag)))
-            return rc;
-          oc.lap(2);
-          const int32_t* r = h->serve_box->res;
-          memset(out, 0, sizeof *out);
-          out->node = r[KSIM_RES_NODE];
-          out->fit_nodes = r[KSIM_RES_FIT];
-          memcpy(&out->last_node_index, r + KSIM_RES_CTR, 8);
-          if (out->node < 0) memcpy(out->reasons, r + KSIM_RES_REASONS, sizeof out->reasons);
-          if (r[KSIM_RES_ERR] & 128) return ksim_rt_svc_refusal(h);
-          if (r[KSIM_RES_ERR] || out->node == INT32_MIN) {
-            uint64_t d2[2] = {0, 0};  // the kernel's note of its first failure (site, block, tag, message)
-            if (h->serve_live) (void)ksim_serve_stop(h);
-            (void)hipMemcpy(d2, h->ctx.dbg + 96, sizeof d2, hipMemcpyDeviceToHost);
-            return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x (resident pick; site %llu block %llu tag %llu "
-                             "message %llu detail 0x%llx; this message %llu tag %u)", r[KSIM_RES_ERR],
-                             (unsigned long long)(d2[0] & 255), (unsigned long long)((d2[0] >> 8) & 255),
-                             (unsigned long long)((d2[0] >> 16) & 255), (unsigned long long)(d2[0] >> 24),
-                             (unsigned long long)d2[1], (unsigned long long)h->serve_seq, h->pick_tag);
-          }
-          if (assume && out->node >= 0) {
-            rc = after_commit(h, pod->port_cnt, r);
-            oc.lap(3);
-            return rc;
-          }
-          return KSIM_OK;
+        if (assume && out->node >= 0) {
+          rc = after_commit(h, pod->port_cnt, r);
+          oc.lap(3);
+          return rc;
         }
+        return KSIM_OK;
       }
+      KsimGate gate(h, true);  // the pick kernel's blocks wait on each other
       cs.pick = h->pick_words;
       cs.pick_tag = h->pick_tag;
       h->res_host[KSIM_RES_NODE] = INT32_MIN;
@@ -670,6 +834,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   }
   h->res_host[KSIM_RES_NODE] = INT32_MIN;  // still there after the wait: the fused barrier gave up
   if ((rc = ksim_rt_check_launch_ctx(h, cs, grid, "ksim_schedule_one"))) return rc;
+  KsimGate gate(h, cs.fuse_a != 0);  // the fused pass A: a grid barrier
   hipError_t e = hipSuccess;
   oc.lap(0);
   if (ipa && !cs.fuse_a) e = ksim_launch_ipa_pass(&cs, npt, grid, ksim_stream(h));
@@ -710,6 +875,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
 
 static int pod_delta(ksim_handle* h, int64_t node, const ksim_pod* pod, const uint64_t* ports, int32_t n_ports,
                      const ksim_scalar_req* scalars, int32_t n_scalars, bool add, const char* where) {
+  KsimCtrKeep keep(h);  // (a cache event never moves lastNodeIndex)
   int rc = check_ready(h, where);
   if (rc) return rc;
   if ((rc = check_pod_args(h, pod, n_ports, n_scalars, ports, scalars, where))) return rc;
@@ -721,10 +887,14 @@ static int pod_delta(ksim_handle* h, int64_t node, const ksim_pod* pod, const ui
   if ((rc = ksim_rt_check_pod(h, p, n_ports, n_scalars, scalars, where))) return rc;
   // the resident per-pod kernel takes an assume as a message (the adapter's Schedule + AssumePod
   // pattern), when it serves the current context
-  if (add && h->serve_live && p.port_cnt <= KSIM_ONE_PORTS && p.scalar_cnt <= KSIM_MAX_SCALAR &&
-      now_ns() - h->serve_post_ns <= SERVE_POST_NS && memcmp(&h->ctx, &h->serve_base, sizeof(KsimCtx)) == 0) {
-    if ((rc = serve_post(h, KSIM_SERVE_ASSUME, staged_pod(h, p), ports + p.port_off, scalars + p.scalar_off, 0, node, 0))) return rc;
-    return after_commit(h, pod->port_cnt, h->serve_box->res);
+  if (add && h->serve_live.load() && p.port_cnt <= KSIM_ONE_PORTS && p.scalar_cnt <= KSIM_MAX_SCALAR) {
+    KsimGate gate(h, false);
+    if (h->serve_live.load() && memcmp(&h->ctx, &h->serve_base, sizeof(KsimCtx)) == 0) {
+      int32_t r[KSIM_RES_WORDS];
+      if ((rc = serve_post(h, KSIM_SERVE_ASSUME, staged_pod(h, p), ports + p.port_off, scalars + p.scalar_off, 0, node, 0, r)))
+        return rc;
+      return after_commit(h, pod->port_cnt, r);
+    }
   }
   KsimCtx cs;
   if ((rc = stage_pod(h, p, ports, scalars, &cs))) return rc;
@@ -766,6 +936,7 @@ int ksim_assume(ksim_handle* h, int64_t pod, int64_t node) {
 }
 
 int ksim_node_add(ksim_handle* h, int64_t index, const ksim_node_row* row) {
+  KsimCtrKeep keep(h);
   int rc = check_ready(h, "ksim_node_add");
   if (rc) return rc;
   if (index < 0 || index > h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "ksim_node_add: rank %lld out of range", (long long)index);
@@ -784,6 +955,7 @@ int ksim_node_add(ksim_handle* h, int64_t index, const ksim_node_row* row) {
 }
 
 int ksim_node_update(ksim_handle* h, int64_t index, const ksim_node_row* row) {
+  KsimCtrKeep keep(h);
   int rc = check_ready(h, "ksim_node_update");
   if (rc) return rc;
   if (index < 0 || index >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "ksim_node_update: rank %lld out of range", (long long)index);
@@ -797,6 +969,7 @@ int ksim_node_update(ksim_handle* h, int64_t index, const ksim_node_row* row) {
 }
 
 int ksim_node_remove(ksim_handle* h, int64_t index) {
+  KsimCtrKeep keep(h);
   int rc = check_ready(h, "ksim_node_remove");
   if (rc) return rc;
   if (index < 0 || index >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "ksim_node_remove: rank %lld out of range", (long long)index);

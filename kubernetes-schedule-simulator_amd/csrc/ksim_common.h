@@ -238,8 +238,11 @@ __device__ __forceinline__ ksim_scalar_req ksim_pod_scalar(const KsimCtx& c, con
 // into the device.  A message is KSIM_SERVE_MSG_WORDS 32-bit payload words, each stored by the
 // host as one 8-byte word `payload | (uint32)seq << 32`: the device reads the whole message with
 // one 16-byte load per lane (one PCIe round trip) and takes it when every word carries the
-// message's number — no separate sequence word, no second round trip for the body.  The block
-// that answers writes the result block and then the number into `done` (a system-scope release).
+// message's number — no separate sequence word, no second round trip for the body.  The answer
+// travels the same way: every result word the block that answers writes is one 8-byte store
+// `value | (uint32)seq << 32`, and the host accepts an answer only when every word it reads
+// carries its message's number, so a word of an earlier answer can never be taken for this one
+// (no completion flag, no ordering between the words needed).
 #define KSIM_SERVE_EXIT 0
 #define KSIM_SERVE_SCHEDULE 1
 #define KSIM_SERVE_ASSUME 2
@@ -257,11 +260,33 @@ __device__ __forceinline__ ksim_scalar_req ksim_pod_scalar(const KsimCtx& c, con
 static_assert(sizeof(ksim_pod) % 4 == 0 && sizeof(ksim_scalar_req) % 4 == 0, "mailbox words");
 static_assert(KSIM_SERVE_W_SCALARS + (int)(KSIM_MAX_SCALAR * sizeof(ksim_scalar_req) / 4) <= KSIM_SERVE_MSG_WORDS,
               "a mailbox message holds a pod with KSIM_ONE_PORTS ports and KSIM_MAX_SCALAR scalars");
+// Leaving.  The grid leaves on an EXIT message, or by agreement when idle: a block that has seen
+// no message for idle_ticks votes in a device word (KSIM_SERVE_ST_*, agent-scope CAS); the vote
+// that would make it unanimous instead sets LEFT, and a block that has voted takes a newly seen
+// message only after a veto (a CAS that bumps the epoch and clears the votes), which fails once
+// LEFT is set.  A block that has not voted never checks: LEFT needs its vote.  So a message is
+// taken by every block or by none, and a grid that left by agreement answered everything it took;
+// the LEFT voter then stores `left = launch id << 32 | last message` so the host knows that its
+// unanswered message was never taken and relaunches the kernel to serve it (ksim_cache.cpp).
+#define KSIM_SERVE_ST_LEFT (1ull << 63)
+#define KSIM_SERVE_ST_VOTES(s) ((uint32_t)((s) & 0xffffu))
+#define KSIM_SERVE_ST_EPOCH(s) ((uint32_t)(((s) >> 16) & 0xffffffffu))
+#define KSIM_SERVE_ST_MAKE(epoch, votes) ((((uint64_t)(uint32_t)(epoch)) << 16) | (uint64_t)(votes))
 struct KsimServeBox {
   uint64_t msg[KSIM_SERVE_MSG_WORDS];  // host: the current message (16-byte aligned)
-  uint64_t done;                       // device: the last message answered
+  uint64_t ans[KSIM_RES_WORDS];        // device: the answer, word k = KSIM_RES_* word | seq << 32
+  uint64_t left;                       // device: launch id << 32 | last message, when it left by agreement
   uint64_t pad1[7];
-  int32_t res[KSIM_RES_WORDS];         // the result block (KSIM_RES_*)
+};
+// The resident kernel's launch arguments beside the context.
+struct KsimServeArgs {
+  KsimServeBox* box;
+  uint64_t* state;      // device word: the idle vote (KSIM_SERVE_ST_*), zeroed before every launch
+  uint64_t seq0;        // the newest message number already handled (the kernel takes later ones)
+  uint64_t idle_ticks;  // a block votes to leave after this long without a message (s_memrealtime, 100 MHz)
+  uint64_t ctr0;        // lastNodeIndex as the host last saw it ...
+  uint32_t ctr0_valid;  // ... when the host knows it (else the kernel reads *c.counter, coherently)
+  uint32_t launch_id;
 };
 
 // Node-sharded mode (ksim_shard_*): this rank's place in the world and every rank's exchange

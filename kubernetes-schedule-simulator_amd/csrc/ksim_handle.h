@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <array>
 #include <cstdarg>
 #include <cstdio>
@@ -30,8 +31,7 @@ extern "C" hipError_t ksim_launch_one(const KsimCtx* c, int npt, hipStream_t s);
 extern "C" int ksim_pick_coresident(int npt, int grid);
 extern "C" hipError_t ksim_launch_pick(const KsimCtx* c, int npt, int grid, hipStream_t s);
 extern "C" int ksim_serve_coresident(int npt, int grid);
-extern "C" hipError_t ksim_launch_serve(const KsimCtx* c, KsimServeBox* box, uint64_t seq0, uint64_t idle_ticks, int npt,
-                                        int grid, hipStream_t s);
+extern "C" hipError_t ksim_launch_serve(const KsimCtx* c, const KsimServeArgs* a, int npt, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_ipa_pass(const KsimCtx* c, int npt, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, int32_t* status, hipStream_t s);
 extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
@@ -49,10 +49,6 @@ extern "C" size_t ksim_pfast_granule_bytes(void);
 extern "C" size_t ksim_shard_xchg_bytes(void);
 extern "C" size_t ksim_shard_lx_offset(void);
 extern "C" size_t ksim_pfast_cache_bytes(int lds_rows, int ncls);
-extern "C" size_t ksim_pipe_lds_bytes(int lds_rows, int ncls, int nb);
-extern "C" size_t ksim_pipe_word_bytes(int grid, int lds_rows);
-extern "C" hipError_t ksim_launch_pipe(const KsimCtx* c, uint64_t* words, int grid, int lds_rows, int spec, const int32_t* tcls,
-                                       const KsimTreeClass* tclass, int ncls, int nb, hipStream_t s);
 extern "C" hipError_t ksim_launch_pfast(const KsimCtx* c, uint64_t* granules, int grid, int lds_rows, double* mirror,
                                         const KsimShard* sh, const int32_t* tcls, const KsimTreeClass* tclass, int ncls,
                                         hipStream_t s);
@@ -140,26 +136,35 @@ struct ksim_handle {
   // node table (any other commit path clears it)
   int32_t n_tcls = 0;                      // -1: more classes than the tree supports
   bool last_pfast_cache = false;           // the last fast-kernel call took the cached form
-  bool last_pfast_pipe = false;
   uint64_t* pick_words = nullptr;          // the per-pod pick kernel's exchange records
   uint32_t pick_tag = 0;
   int pick_grid = -1, pick_npt = -1;
-  bool pick_ok = false;            // ... and its two-deep pipelined kernel (ksim_pipe.hip)
-  uint64_t* pipe_words = nullptr;          // the pipelined kernel's published words
-  size_t pipe_bytes = 0;
+  bool pick_ok = false;
+  bool pick_clear = false;                 // the record buffers must be zeroed before the next call (new geometry)
+  bool serve_fits = false;                 // the resident kernel's grid for (pick_npt, pick_grid) is co-resident
   // the resident per-pod service (ksim_serve_kernel, ksim_cache.cpp): mailbox, the context and
-  // geometry it was launched with, per-block pod staging, the last message posted and when
-  bool serve_live = false;
+  // geometry it was launched with, per-block pod staging, the last message posted.  serve_live is
+  // read without the device gate by ksim_stream (another handle's exclusive section may clear it)
+  std::atomic<bool> serve_live{false};
   bool serve_off = false;                  // KSIM_SERVE=0, or a failure: per-pod launches only
   KsimServeBox* serve_box = nullptr;       // coherent host memory ...
   KsimServeBox* serve_box_dev = nullptr;   // ... as the device addresses it
+  uint64_t* serve_state = nullptr;         // device: the grid's idle vote (KSIM_SERVE_ST_*)
   KsimCtx serve_base{};                    // h->ctx when the kernel was launched
   int serve_npt = 0, serve_grid = 0;
   uint64_t serve_seq = 0;
+  uint32_t serve_launch_id = 0;
   bool serve_shared = false;               // the last message committed state other blocks read
-  int64_t serve_post_ns = 0;               // steady clock of the last post (or of the launch)
   char* serve_stage = nullptr;             // device: [grid] pods, [grid][KSIM_ONE_PORTS] ports, [grid][KSIM_MAX_SCALAR] scalars
-  int64_t serve_stats[4] = {0, 0, 0, 0};   // launches, messages, stops, relaunches after the idle bound
+  // launches, messages, stops, relaunches after the grid left by its idle vote, messages served by
+  // such a relaunch (the grid left before taking them)
+  int64_t serve_stats[5] = {0, 0, 0, 0, 0};
+  // lastNodeIndex as the host last saw it in a resident kernel's answer, while nothing else can
+  // have changed the device word (cleared by ksim_stream, kept across counter-neutral calls): the
+  // next launch starts from it, and each answer is checked against it (selectHost bumps it by one
+  // exactly when two or more nodes fit, generic_scheduler.go:183-198)
+  uint64_t ctr_host = 0;
+  bool ctr_known = false;
   int32_t* tcls = nullptr;
   int64_t tcls_cap = 0;
   KsimTreeClass* tclass = nullptr;
@@ -179,7 +184,6 @@ struct ksim_handle {
   size_t stg_cap = 0;
   int32_t* res_dev = nullptr;   // result block (KSIM_RES_*), device view
   int32_t* res_host = nullptr;  // the same words, host view
-  uint64_t* ctr_host = nullptr; // unused (lastNodeIndex comes back in the result block)
   int64_t port_bound = 0;       // upper bound of max(port_count) over the nodes
   // inter-pod affinity (ksim_load_affinity): the device tables, their sizes for validation, and
   // per queued pod its identity / class (an affinity pod takes the launch-mode kernels)
@@ -233,10 +237,38 @@ struct ksim_handle {
 int ksim_fail(ksim_handle* h, int code, const char* fmt, ...);
 // Stop the resident per-pod kernel (an exit message and a stream drain); KSIM_OK when none runs.
 int ksim_serve_stop(ksim_handle* h);
+// The handle leaves the device gate's list of running resident kernels (ksim_destroy).
+void ksim_serve_forget(ksim_handle* h);
 inline hipStream_t ksim_stream(ksim_handle* h) {
-  if (h->serve_live) (void)ksim_serve_stop(h);
+  if (h->serve_live.load(std::memory_order_acquire)) (void)ksim_serve_stop(h);
+  h->ctr_known = false;  // (the stream's next use may change lastNodeIndex)
   return h->stream_raw;
 }
+// A call that cannot change lastNodeIndex (cache events, reads): the host's copy survives its
+// stream uses.
+struct KsimCtrKeep {
+  ksim_handle* h;
+  bool known;
+  uint64_t v;
+  explicit KsimCtrKeep(ksim_handle* hh) : h(hh), known(hh && hh->ctr_known), v(hh ? hh->ctr_host : 0) {}
+  ~KsimCtrKeep() {
+    if (h && known) { h->ctr_known = true; h->ctr_host = v; }
+  }
+};
+// The device gate (ksim_cache.cpp).  A kernel whose blocks wait on each other (the persistent
+// batch kernels, the per-pod pick kernel, the fused pass-A scan, the node-sharded kernels) must
+// not share the device with another handle's resident per-pod kernel, which holds CUs between
+// calls: such launches run under the gate held exclusively, which first stops every other
+// handle's resident kernel on the device; the resident kernels' calls hold it shared.  Nested
+// holds by one thread are free (an exclusive holder's own shared sections skip the lock).
+struct KsimGate {
+  int dev = -1;
+  int mode = 0;  // 0: not taken here, 1 shared, 2 exclusive
+  KsimGate(ksim_handle* h, bool exclusive);
+  ~KsimGate();
+  KsimGate(const KsimGate&) = delete;
+  KsimGate& operator=(const KsimGate&) = delete;
+};
 
 #define HIPCHK(h, x)                                                                              \
   do {                                                                                            \

@@ -1498,29 +1498,39 @@ __device__ __forceinline__ uint64_t pk_load(const uint64_t* g) {
 }
 constexpr uint64_t PK_SPIN_TICKS = 200000000ull;  // 2 s of s_memrealtime
 constexpr int PK_BATCH = 16;  // record words one lane keeps in flight (a cross-XCD load is ~1 µs)
-// the resident form (ksim_serve_kernel): the result block is host memory the host polls; `done`
-// takes the message number after every store of the answer (a system-scope release)
-// Always a system-scope release: an acknowledged system-scope store to host memory is not yet
-// visible to the host in order (measured: waiting for the acknowledgements of the answer's words
-// and then storing `done` let the host read the previous message's answer once in a few thousand
-// messages), so the release's write-back also orders the answer before `done`.
-__device__ __forceinline__ void pk_publish(uint64_t* done, uint64_t seq) {
-  __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+// The resident form's answer (ksim_serve_kernel; KsimServeBox::ans in host memory): lane k of the
+// answering wave stores result word k (KSIM_RES_*) as `value | seq << 32` in one 8-byte
+// system-scope store.  The host takes the answer when every word it reads carries the message's
+// number, so no word of an earlier answer can pass for this one whatever order the stores become
+// visible in (round 5's answer — untagged words, then a `done` word — needed a system-scope release
+// between them).  vr: lane r's FitError reason count (r < KSIM_NREASONS).
+__device__ __forceinline__ void pk_answer(uint64_t* ans, uint64_t seq, int lane, int32_t node, int32_t fit,
+                                          int32_t status, int32_t err, uint64_t ctr, int32_t vr) {
+  const int32_t reason = __shfl(vr, (lane - KSIM_RES_REASONS) & 63, 64);
+  int32_t v = 0;
+  if (lane == KSIM_RES_NODE) v = node;
+  else if (lane == KSIM_RES_FIT) v = fit;
+  else if (lane == KSIM_RES_STATUS) v = status;
+  else if (lane == KSIM_RES_ERR) v = err;
+  else if (lane >= KSIM_RES_REASONS && lane < KSIM_RES_REASONS + KSIM_NREASONS) v = reason;
+  else if (lane == KSIM_RES_CTR) v = (int32_t)(uint32_t)ctr;
+  else if (lane == KSIM_RES_CTR + 1) v = (int32_t)(uint32_t)(ctr >> 32);
+  // the reason words only for a FitError (the host reads them only then)
+  const bool want = lane < KSIM_RES_WORDS && (node == -1 || lane < KSIM_RES_REASONS || lane >= KSIM_RES_CTR);
+  if (want) __hip_atomic_store(ans + lane, ((uint64_t)(uint32_t)seq << 32) | (uint64_t)(uint32_t)v, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// a word of the answer: the resident form's result block is host memory (system-scope store)
-__device__ __forceinline__ void pk_res(const uint64_t* done, int32_t* p, int32_t v) {
-  if (done) __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  else *p = v;
-}
+static_assert(KSIM_RES_WORDS <= 64, "one answer word per lane");
 }  // namespace
 
 // One pod of the pick form.  rec: this pod's record buffer (tag parity, KSIM_PICK_WORDS words);
 // ctr_keep: the block's own copy of lastNodeIndex (resident form; null: read *c.counter);
-// done / seq: the resident form's completion word (null: a one-pod launch).
+// ans / seq: the resident form's answer words and message number (null: a one-pod launch, which
+// writes the result block and *c.counter directly).
 template <int NPT>
 __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod& P, const int64_t pod, const uint32_t tag,
                                                const int32_t no_commit, uint64_t* const rec, uint64_t* ctr_keep,
-                                               uint64_t* done, const uint64_t seq, uint64_t* stamp = nullptr) {
+                                               uint64_t* ans, const uint64_t seq, uint64_t* stamp = nullptr) {
 #ifdef KSIM_STAMPS
 #define PKST(k) do { if (stamp && threadIdx.x == 0) stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
@@ -1536,7 +1546,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   __shared__ int64_t s_pa[4];
   __shared__ int64_t s_tv[KSIM_MAX_RCLASS], s_av[KSIM_MAX_RCLASS], s_ad[KSIM_MAX_RCLASS];
   __shared__ int64_t s_bmax[KSIM_MAX_RCLASS];  // this block's max per class (after the decision: the winners')
-  __shared__ int32_t s_mode, s_owner, s_rank, s_F, s_ok;
+  __shared__ int32_t s_mode, s_owner, s_rank, s_F, s_ok, s_stat;
   __shared__ uint32_t s_win;
   __shared__ int64_t s_M[KSIM_MAX_RCLASS];
   __shared__ int32_t s_C[KSIM_MAX_RCLASS];
@@ -1567,7 +1577,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   __shared__ uint32_t s_dflag;  // the decision is in LDS (wave 0 → the other waves)
   if (tid < KSIM_NREASONS) s_hist[tid] = 0;
   if (tid < KSIM_PICK_ZMAX) s_z[tid] = 0;
-  if (tid == 0) { s_ok = 1; s_dflag = 0; }
+  if (tid == 0) { s_ok = 1; s_dflag = 0; s_stat = 0; }
   __syncthreads();
 
   const int64_t base = (int64_t)me * c.chunk;
@@ -1635,7 +1645,8 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
       } else if (lane - 4 < NZ) {
         v = (int64_t)s_z[lane - 4];
       }
-      if (lane < W) pk_store(recA + (int64_t)me * KSIM_PICK_RA + lane, pk_enc(tag, v));
+      // every word of the record, not only the W read now: see the record stores below
+      pk_store(recA + (int64_t)me * KSIM_PICK_RA + lane, pk_enc(tag, lane < W ? v : 0));
     }
     if (wv == 0) {
       // every block's record: lane x combines word x over the blocks
@@ -1737,6 +1748,10 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
       if (wv == 0) s_bmax[lane] = bc ? bm : INT64_MIN;
     }
     if (wv == 1) {
+      // Every word of both records carries this call's tag after this call, including words no
+      // block reads now (zeros): the tags (1..254) come back every 254 calls, so a word written
+      // by an older call and not since would pass for this call's if a later pod read further
+      // into the record (more reduce classes K, more zones, a pod with pass A after pods without).
       const int WB = 1 + 2 * K + (F0 == 0 ? KSIM_NREASONS : 0);
       // word x = lane x: fit, then class q's max (word 1 + q), its count (word 1 + K + q), reasons
       const int64_t mq = __shfl(bm, (lane - 1) & 63, 64);
@@ -1746,7 +1761,11 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
       else if (lane <= K) v = cq ? mq : 0;  // (a class without fit nodes: count 0, max unread)
       else if (lane <= 2 * K) v = cq2;
       else if (lane < WB) v = s_hist[lane - 1 - 2 * K];
-      if (lane < WB) pk_store(recB + (int64_t)me * KSIM_PICK_RB + lane, pk_enc(tag, v));
+      if (!pass_a) pk_store(recA + (int64_t)me * KSIM_PICK_RA + lane, pk_enc(tag, 0));
+      pk_store(recB + (int64_t)me * KSIM_PICK_RB + lane, pk_enc(tag, v));
+      // word 64 (the last reason when K = 16) from lane 0
+      static_assert(KSIM_PICK_RB == 65 && KSIM_PICK_RA == 64, "record words per lane");
+      if (lane == 0) pk_store(recB + (int64_t)me * KSIM_PICK_RB + 64, pk_enc(tag, 64 < WB ? s_hist[64 - 1 - 2 * K] : 0));
     }
   }
   if (wv == 0) {
@@ -1851,11 +1870,8 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   PKST(7);
   const int mode = s_mode;
   if (mode < 0) {  // a spin hit its bound (err set): nothing committed
-    if (done && me == 0 && tid == 0) {  // (the resident form: the host must hear of it)
-      pk_res(done, &c.out_node[pod], INT32_MIN);
-      if (c.out_fit) pk_res(done, &c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT], __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | 2);
-      pk_publish(done, seq);
-    }
+    if (ans && me == 0 && wv == 0)  // (the resident form: the host must hear of it)
+      pk_answer(ans, seq, lane, INT32_MIN, 0, 0, __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) | 2, s_ctr, 0);
     return;
   }
 
@@ -1882,18 +1898,22 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
         if (__builtin_amdgcn_s_memrealtime() - t0 > PK_SPIN_TICKS) { atomicOr(c.err, 2); if (lane == 0) note(3, 0); break; }
         __builtin_amdgcn_s_sleep(1);
       }
-      if (lane < KSIM_NREASONS) pk_res(done, &c.out_reasons[pod * KSIM_NREASONS + lane], v);
-      if (lane == 0) {
-        pk_res(done, &c.out_node[pod], -1);
-        if (c.out_fit) {
-          pk_res(done, &c.out_fit[0], 0);
-          pk_res(done, &c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT], __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          pk_res(done, &c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT], (int32_t)(uint32_t)s_ctr);
-          pk_res(done, &c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1], (int32_t)(uint32_t)(s_ctr >> 32));
+      const int32_t e = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (ans) {
+        pk_answer(ans, seq, lane, -1, 0, 0, e, s_ctr, v);
+      } else {
+        if (lane < KSIM_NREASONS) c.out_reasons[pod * KSIM_NREASONS + lane] = v;
+        if (lane == 0) {
+          c.out_node[pod] = -1;
+          if (c.out_fit) {
+            c.out_fit[0] = 0;
+            c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT] = e;
+            c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT] = (int32_t)(uint32_t)s_ctr;
+            c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1] = (int32_t)(uint32_t)(s_ctr >> 32);
+          }
         }
-        if (done) pk_publish(done, seq);  // (the wave's reason stores above are ordered before it)
-        PKST(10);
       }
+      PKST(10);
     }
     return;
   }
@@ -1937,31 +1957,41 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   PKST(8);
   const int64_t node = s_node;
   if (node >= 0 && !no_commit) {
+    // a commit of state other blocks read (volume mounts, inter-pod affinity / service counts): each
+    // committing wave releases it at agent scope before the answer, so the next message's acquire
+    // (KSIM_SERVE_SYNC_ACQUIRE) sees it (rows are read by this block's own waves only)
     if (wv == 0) {
       const int32_t st = ksim_commit_wave(c, P, node, lane);
       if (tid == 0) {
         if (ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, node, 1, c.err);
-        if (c.out_fit && st) pk_res(done, &c.out_fit[1], done ? st : (c.out_fit[1] | st));  // (resident: the host zeroed it)
+        s_stat = st;
       }
+      if (ans && ksim_is_vol_pod(c, P)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     } else if (wv == 1 && ksim_is_aff_pod(c, P)) {
       if (lane == 0) ksim_svc_commit(*c.aff, P, node);  // reads the counts before this commit's adds
       ksim_aff_commit_body(*c.aff, P, node, 1, lane, 64);
+      if (ans) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     }
   }
   __syncthreads();
   PKST(9);
-  if (tid == 0) {
-    if (mode == 2) *c.counter = s_ctr;
-    pk_res(done, &c.out_node[pod], (int32_t)node);
+  if (ans) {
+    // the answer; lastNodeIndex stays in the blocks' LDS (every block took the same decision) and
+    // reaches the host in the answer — no device store of it while the kernel is resident
+    if (wv == 0) pk_answer(ans, seq, lane, (int32_t)node, s_F, s_stat, __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           s_ctr, 0);
+  } else if (tid == 0) {
+    if (mode == 2) *c.counter = s_ctr;  // (a one-pod launch: this block is the call's only writer)
+    c.out_node[pod] = (int32_t)node;
     if (c.out_fit) {
-      pk_res(done, &c.out_fit[0], s_F);
-      pk_res(done, &c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT], __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-      pk_res(done, &c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT], (int32_t)(uint32_t)s_ctr);
-      pk_res(done, &c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1], (int32_t)(uint32_t)(s_ctr >> 32));
+      if (s_stat) c.out_fit[1] |= s_stat;
+      c.out_fit[0] = s_F;
+      c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT] = __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT] = (int32_t)(uint32_t)s_ctr;
+      c.out_fit[KSIM_RES_CTR - KSIM_RES_FIT + 1] = (int32_t)(uint32_t)(s_ctr >> 32);
     }
-    if (done) pk_publish(done, seq);  // after the barrier: every wave's commit stores are issued before it
-    PKST(10);
   }
+  if (tid == 0) PKST(10);
 #undef PKST
 }
 
@@ -1975,17 +2005,49 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
 // The resident per-pod service (ksim_schedule_one / ksim_pod_add between other calls): the pick
 // kernel's grid stays resident and takes one message at a time from a mailbox in coherent host
 // memory (KsimServeBox: tagged words, one PCIe round trip per poll), so a call costs the host's
-// stores, the device's poll and the answer's store instead of a kernel launch and a stream
-// synchronisation.  Each block copies the message's pod
-// into its own slot of the device staging (c.pods / c.pod_ports / c.pod_scalars, one slot per
-// block: the evaluation reads its ports / scalars there), keeps lastNodeIndex in LDS (every block
-// takes the same decision), and uses the record buffer of the message's tag parity, so a block
-// still reading pod k's records never sees them overwritten by pod k + 1's.  Every block leaves on
-// an exit message or after KSIM_SERVE_IDLE_TICKS without one (the host never posts a message that
-// late: it stops and relaunches the kernel instead, ksim_cache.cpp).
+// stores, the device's poll and the answer's stores instead of a kernel launch and a stream
+// synchronisation.  Each block copies the message's pod into its own slot of the device staging
+// (c.pods / c.pod_ports / c.pod_scalars, one slot per block: the evaluation reads its ports /
+// scalars there), keeps lastNodeIndex in LDS (every block takes every SCHEDULE message and the
+// same decision), and uses the record buffer of the message's tag parity, so a block still
+// reading pod k's records never sees them overwritten by pod k + 1's.  The grid leaves on an exit
+// message or by the idle vote (KSIM_SERVE_ST_*, ksim_common.h).
+namespace {
+// The idle vote, lane 0 of a block's wave 0 (agent-scope atomics on one device word).
+// serve_vote: this block's vote; 2 = it made the vote unanimous (LEFT set), 1 = counted in epoch
+// *ep, 0 = the grid had already left (cannot happen: LEFT needs this block's vote).
+__device__ uint32_t serve_vote(uint64_t* st, uint32_t G, uint32_t* ep) {
+  uint64_t s = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if (s & KSIM_SERVE_ST_LEFT) return 0;
+    const uint32_t v = KSIM_SERVE_ST_VOTES(s) + 1;
+    const uint64_t n = v >= G ? (s | KSIM_SERVE_ST_LEFT) : KSIM_SERVE_ST_MAKE(KSIM_SERVE_ST_EPOCH(s), v);
+    if (__hip_atomic_compare_exchange_strong(st, &s, n, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      *ep = KSIM_SERVE_ST_EPOCH(s);
+      return v >= G ? 2u : 1u;
+    }
+  }
+}
+// serve_veto: withdraw this block's vote of epoch ep before taking a message (bump the epoch,
+// clear the votes); 1 = take it, 0 = the grid agreed to leave before (the message is not taken).
+__device__ uint32_t serve_veto(uint64_t* st, uint32_t ep) {
+  uint64_t s = __hip_atomic_load(st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    if (s & KSIM_SERVE_ST_LEFT) return 0;
+    if (KSIM_SERVE_ST_EPOCH(s) != ep) return 1;  // another block's veto already cleared the votes
+    if (__hip_atomic_compare_exchange_strong(st, &s, KSIM_SERVE_ST_MAKE(ep + 1u, 0u), __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT))
+      return 1;
+  }
+}
+__device__ __forceinline__ uint64_t rfl64(uint64_t v) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(v >> 32)) << 32) |
+         (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)(uint32_t)v);
+}
+}  // namespace
+
 template <int NPT>
-__global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimServeBox* box, uint64_t seq0,
-                                                                uint64_t idle_ticks) {
+__global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimServeArgs a) {
   __shared__ uint64_t s_keep;
   __shared__ ksim_pod s_P;
   __shared__ int32_t s_type, s_nc;
@@ -1993,8 +2055,12 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
   __shared__ int64_t s_node;
   __shared__ uint32_t s_msg[KSIM_SERVE_MSG_WORDS];
   __shared__ uint64_t s_seq;
+  KsimServeBox* const box = a.box;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, me = blockIdx.x;
-  if (tid == 0) s_keep = *c.counter;
+  // lastNodeIndex: from the host's last answer, or (after calls of other forms) the device word,
+  // read coherently (system scope: never a stale line of this XCD's L2)
+  if (tid == 0)
+    s_keep = a.ctr0_valid ? a.ctr0 : __hip_atomic_load(c.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #ifdef KSIM_STAMPS
   // diagnostic builds: per phase, the sum of (stamp k - stamp k-1) and how often both were taken,
   // over every block and message, into dbg[64 + k] / dbg[80 + k] at the exit (k = 0: the poll)
@@ -2012,7 +2078,10 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
   // by one block (an assume onto another block's node) does not wait for the others, so the host
   // can post the next before this block has looked.  It never skips one it must answer or publish
   // records for: the host waits for those.
-  uint64_t seq = seq0;
+  uint64_t seq = a.seq0;
+  bool voted = false;  // (wave 0, uniform) this block's idle vote stands in epoch vote_ep
+  uint32_t vote_ep = 0;
+  uint64_t t_idle = __builtin_amdgcn_s_memrealtime();
   for (;;) {
     if (wv == 0) {
       // poll: lane l reads payload words 2l, 2l+1 with their tags in one 16-byte system-scope load
@@ -2021,19 +2090,48 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
       const uint64_t* src = box->msg + 2 * lane;
       u4 q;
       int32_t type = KSIM_SERVE_EXIT;
-      const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
       for (;;) {
         asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(q) : "v"(src) : "memory");
         const uint32_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)q.y);
         if ((int32_t)(t - s32) >= 0 && __all(q.y == t && q.w == t)) {
+          type = __builtin_amdgcn_readfirstlane((int32_t)q.x);  // word 0 (lane 0)
+          if (type != KSIM_SERVE_EXIT && voted) {
+            // this block voted to leave: withdraw the vote before taking the message
+            uint32_t ok = 0;
+            if (lane == 0) ok = serve_veto(a.state, vote_ep);
+            ok = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)ok);
+            voted = false;
+            if (!ok) type = KSIM_SERVE_EXIT;  // the grid left first: nobody takes it (the host relaunches)
+          }
           if (lane == 0) s_seq = seq + 1 + (uint64_t)(t - s32);
 #ifdef KSIM_STAMPS
           if (lane == 0) s_st[0] = __builtin_amdgcn_s_memrealtime();
 #endif
-          type = __builtin_amdgcn_readfirstlane((int32_t)q.x);  // word 0 (lane 0)
           break;
         }
-        if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) break;  // (uniform: one clock read per wave)
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();  // (uniform: one clock read per wave)
+        if (voted) {
+          // the vote stands until every block voted (LEFT) or a block saw a message (new epoch)
+          uint64_t sv = 0;
+          if (lane == 0) sv = __hip_atomic_load(a.state, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sv = rfl64(sv);
+          if (sv & KSIM_SERVE_ST_LEFT) break;
+          if (KSIM_SERVE_ST_EPOCH(sv) != vote_ep) { voted = false; t_idle = now; }
+        } else if (now - t_idle > a.idle_ticks) {
+          uint32_t r = 0, ep = 0;
+          if (lane == 0) r = serve_vote(a.state, gridDim.x, &ep);
+          r = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)r);
+          ep = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)ep);
+          if (r == 0) break;
+          if (r == 2) {  // unanimous: tell the host this launch left and the last message it saw
+            if (lane == 0)
+              __hip_atomic_store(&box->left, ((uint64_t)a.launch_id << 32) | (uint32_t)seq, __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          voted = true;
+          vote_ep = ep;
+        }
 #ifdef KSIM_STAMPS
         ++n_polls;
 #endif
@@ -2088,28 +2186,28 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
     if (type != KSIM_SERVE_EXIT) seq = s_seq;
     if (type == KSIM_SERVE_SCHEDULE) {
       const ksim_pod P = s_P;
-      ksim_pick_body<NPT>(c, P, 0, s_tag, s_nc, c.pick + (s_tag & 1u) * KSIM_PICK_WORDS, &s_keep, &box->done, seq, stamp);
+      ksim_pick_body<NPT>(c, P, 0, s_tag, s_nc, c.pick + (s_tag & 1u) * KSIM_PICK_WORDS, &s_keep, box->ans, seq, stamp);
     } else if (type == KSIM_SERVE_ASSUME) {
-      // a resource delta onto a given node (ksim_pod_add): the block whose chunk holds it
+      // a resource delta onto a given node (ksim_pod_add): the block whose chunk holds it answers
       const int64_t node = s_node;
       if (node >= (int64_t)me * c.chunk && node < (int64_t)(me + 1) * c.chunk && wv == 0) {
         const ksim_pod P = s_P;
-        const int32_t st = ksim_commit_wave(c, P, node, lane);
+        const int32_t st = __shfl(ksim_commit_wave(c, P, node, lane), 0, 64);
         if (lane == 0 && ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, node, 1, c.err);
         if (ksim_is_aff_pod(c, P)) {
           if (lane == 0) ksim_svc_commit(*c.aff, P, node);
           ksim_aff_commit_body(*c.aff, P, node, 1, lane, 64);
         }
-        if (lane == 0) {
-          if (st) pk_res(&box->done, &c.out_fit[KSIM_RES_STATUS - KSIM_RES_FIT], st);
-          pk_res(&box->done, &c.out_fit[KSIM_RES_ERR - KSIM_RES_FIT], __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-          pk_publish(&box->done, seq);
-        }
+        // shared counts / mounts: released before the answer (the next message acquires them)
+        if (ksim_is_aff_pod(c, P) || ksim_is_vol_pod(c, P)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        pk_answer(box->ans, seq, lane, (int32_t)node, 0, st, __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                  s_keep, 0);
       }
     } else {
-      break;  // an exit message, an idle bound or a message out of sequence
+      break;  // an exit message, or the grid left by the idle vote
     }
     __syncthreads();  // (the next poll overwrites the block's staging slot and s_P)
+    t_idle = __builtin_amdgcn_s_memrealtime();
 #ifdef KSIM_STAMPS
     if (tid == 0) {
       if (s_st[0]) { s_sum[0] += s_st[0] - t_end; s_cnt[0] += 1; }
@@ -2127,6 +2225,8 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
     }
 #endif
   }
+  // lastNodeIndex for the other forms (every block holds the same value): one writer, system scope
+  if (me == 0 && tid == 0) __hip_atomic_store(c.counter, s_keep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #ifdef KSIM_STAMPS
   if (tid < 12) {
     atomicAdd((unsigned long long*)&c.dbg[64 + tid], (unsigned long long)s_sum[tid]);
@@ -2275,14 +2375,13 @@ extern "C" int ksim_serve_coresident(int npt, int grid) {
   return e == hipSuccess ? 1 : 0;
 }
 
-extern "C" hipError_t ksim_launch_serve(const KsimCtx* c, KsimServeBox* box, uint64_t seq0, uint64_t idle_ticks, int npt,
-                                        int grid, hipStream_t s) {
-  if (grid <= 0 || grid > KSIM_PICK_MAXG || !c->pick || !box || c->one) return hipErrorInvalidValue;
+extern "C" hipError_t ksim_launch_serve(const KsimCtx* c, const KsimServeArgs* a, int npt, int grid, hipStream_t s) {
+  if (grid <= 0 || grid > KSIM_PICK_MAXG || !c->pick || !a->box || !a->state || c->one) return hipErrorInvalidValue;
   switch (npt) {
-    case 1: hipLaunchKernelGGL(ksim_serve_kernel<1>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, box, seq0, idle_ticks); break;
-    case 2: hipLaunchKernelGGL(ksim_serve_kernel<2>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, box, seq0, idle_ticks); break;
-    case 4: hipLaunchKernelGGL(ksim_serve_kernel<4>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, box, seq0, idle_ticks); break;
-    case 8: hipLaunchKernelGGL(ksim_serve_kernel<8>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, box, seq0, idle_ticks); break;
+    case 1: hipLaunchKernelGGL(ksim_serve_kernel<1>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a); break;
+    case 2: hipLaunchKernelGGL(ksim_serve_kernel<2>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a); break;
+    case 4: hipLaunchKernelGGL(ksim_serve_kernel<4>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a); break;
+    case 8: hipLaunchKernelGGL(ksim_serve_kernel<8>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

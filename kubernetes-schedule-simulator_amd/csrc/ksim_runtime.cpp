@@ -80,10 +80,12 @@ void ksim_destroy(ksim_handle* h) {
   if (!h) return;
   (void)hipSetDevice(h->device);
   if (h->stream_raw) (void)hipStreamSynchronize(ksim_stream(h));  // (stops the resident per-pod kernel)
-  if (h->serve_live) (void)hipStreamSynchronize(h->stream_raw);    // (its stop failed: let it reach its idle bound)
+  if (h->serve_live.load()) (void)hipStreamSynchronize(h->stream_raw);  // (its stop failed: let it leave by its idle vote)
+  ksim_serve_forget(h);
   if (getenv("KSIM_SERVE_STATS") && h->serve_stats[0])
-    fprintf(stderr, "[ksim serve] launches %lld messages %lld stops %lld idle relaunches %lld\n", (long long)h->serve_stats[0],
-            (long long)h->serve_stats[1], (long long)h->serve_stats[2], (long long)h->serve_stats[3]);
+    fprintf(stderr, "[ksim serve] launches %lld messages %lld stops %lld left-idle %lld untaken-relaunches %lld\n",
+            (long long)h->serve_stats[0], (long long)h->serve_stats[1], (long long)h->serve_stats[2],
+            (long long)h->serve_stats[3], (long long)h->serve_stats[4]);
 #ifdef KSIM_STAMPS
   if (h->ctx.dbg) {  // the scan kernel's phase stamps (ksim_kernels.hip SSTAMP)
     uint64_t d[64];
@@ -679,35 +681,10 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
     if (sw < 32767 && ksim_pfast_cache_bytes(lds_rows, h->n_tcls)) ncls = h->n_tcls;
   }
   h->last_pfast_cache = ncls > 0;
-  // one device: the two-deep pipelined form of the cached kernel (ksim_pipe.hip), KSIM_PIPE=1 (experimental)
-  const char* pe = getenv("KSIM_PIPE");
-  int nb = 1;  // the pipelined kernel's score bins (every map score < 64)
-  if (!c.no_prio)
-    nb = (int)(10 * (c.w[KSIM_W_LEAST_REQUESTED] + c.w[KSIM_W_MOST_REQUESTED] + c.w[KSIM_W_BALANCED])) + 1;
-  const bool pipe = ncls > 0 && h->shard.world == 1 && pe && pe[0] == '1' && nb <= 64 &&
-                    ksim_pipe_lds_bytes(lds_rows, ncls, nb) && (int64_t)grid * lds_rows >= c.n;
-  h->last_pfast_pipe = pipe;
-  const char* pse = getenv("KSIM_PIPE_SPEC");  // speculative row work before each decision (experimental)
-  const int pipe_spec = pse && pse[0] == '1';
-  if (pipe) {
-    const size_t wb = ksim_pipe_word_bytes(grid, lds_rows);
-    if (h->pipe_bytes < wb) {
-      dev_free(h, h->pipe_words);
-      h->pipe_words = nullptr;
-      h->pipe_bytes = 0;
-      int rc = dev_alloc(h, &h->pipe_words, wb / sizeof(uint64_t));
-      if (rc) return rc;
-      h->pipe_bytes = wb;
-    }
-    HIPCHK(h, hipMemsetAsync(h->pipe_words, 0, wb, ksim_stream(h)));
-    HIPCHK(h, hipMemsetAsync(c.dbg, 0, 16 * 8, ksim_stream(h)));
-  } else {
-    HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, ksim_stream(h)));
-  }
+  HIPCHK(h, hipMemsetAsync(h->granules, 0, gb, ksim_stream(h)));
   HIPCHK(h, hipEventRecord(h->ev0, ksim_stream(h)));
-  hipError_t e = pipe ? ksim_launch_pipe(&c, h->pipe_words, grid, lds_rows, pipe_spec, h->tcls, h->tclass, ncls, nb, ksim_stream(h))
-                      : ksim_launch_pfast(&c, h->granules, grid, lds_rows, stream ? h->mirror : nullptr, &h->shard,
-                                          h->tcls, h->tclass, ncls, ksim_stream(h));
+  hipError_t e = ksim_launch_pfast(&c, h->granules, grid, lds_rows, stream ? h->mirror : nullptr, &h->shard, h->tcls,
+                                   h->tclass, ncls, ksim_stream(h));
   if (e == hipErrorCooperativeLaunchTooLarge) {
     // the grid cannot be co-resident here (a smaller or shared device): the general kernels instead
     if (h->cfg.mode != KSIM_MODE_PERSISTENT && h->shard.world == 1) {
@@ -727,15 +704,7 @@ static int run_pfast_mode(ksim_handle* h, int64_t first, int64_t count, int grid
     HIPCHK(h, hipMemcpy(d, c.dbg, sizeof d, hipMemcpyDeviceToHost));
     HIPCHK(h, hipMemset(c.dbg, 0, sizeof d));
     const double nf = (double)(d[21] ? d[21] : 1);
-    if (h->last_pfast_pipe) {
-      const double np = (double)count * grid;
-      fprintf(stderr, "[ksim stamps] pipe pods=%lld (%.3f ms, %.3f us/pod) per pod, mean over workgroups: control pre %.0f "
-              "owner-wait %.0f post %.0f A-wait %.0f owner-retries %.2f prologue %.0f | wave1 wait %.0f after-decision %.0f "
-              "speculative %.0f - %.0f | wave7 wait %.0f after-decision %.0f speculative %.0f - %.0f\n",
-              (long long)count, ms, 1000.0 * ms / (double)count, d[18] / np, d[16] / np, d[17] / np, d[19] / np, d[22] / np,
-              d[23] / (double)grid,
-              d[24] / np, d[25] / np, d[26] / np, d[27] / np, d[32] / np, d[33] / np, d[34] / np, d[35] / np);
-    } else {
+    {
     fprintf(stderr, "[ksim stamps] pfast workgroup 0, per wave (0 = control) cycles/pod between main barriers busy/wait:");
     for (int w = 0; w < 8; ++w) fprintf(stderr, " %d:%.0f/%.0f", w, d[32 + w] / (double)count, d[40 + w] / (double)count);
     fprintf(stderr, "\n");
@@ -1245,6 +1214,7 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
   KsimCtx& c = h->ctx;
   if (c.n == 0) return ksim_fail(h, KSIM_E_NO_NODES, "no nodes available to schedule pods");
   if (int rc = ksim_rt_check_aff(h, "ksim_schedule")) return rc;
+  KsimGate gate(h, true);  // the persistent kernels' workgroups wait on each other
   if (h->shard.world > 1) {  // node-sharded: the fast persistent kernel on every rank, in lockstep
     for (int r = 0; r < h->shard.world; ++r)
       if (!h->shard.peers[r]) return ksim_fail(h, KSIM_E_STATE, "ksim_schedule: rank %d is not connected", r);
@@ -1327,18 +1297,6 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
   if (err & 1) return ksim_fail(h, KSIM_E_OVERFLOW, "a node's host-port or volume slots overflowed (raise port_slots / vol_slots)");
   if (err & 128) return ksim_rt_svc_refusal(h);
   if (err & ~1) {
-    if (h->last_pfast_pipe) {  // the pipelined kernel records its first failed spin in dbg[0]
-      uint64_t d0 = 0, dd[8] = {};
-      (void)hipMemcpy(&d0, c.dbg, 8, hipMemcpyDeviceToHost);
-      (void)hipMemcpy(dd, c.dbg + 8, sizeof dd, hipMemcpyDeviceToHost);
-      if (dd[0] || dd[1]) fprintf(stderr, "[ksim pipe] rel %llu X %llu A %016llx B %016llx F %016llx XR %llu\n",
-                                  (unsigned long long)(dd[0] & 0xffffffff), (unsigned long long)(dd[0] >> 32),
-                                  (unsigned long long)dd[1], (unsigned long long)dd[2], (unsigned long long)dd[3],
-                                  (unsigned long long)dd[4]);
-      return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x (pipe: wg %d wave %d site %d pod %d aux %d)", err,
-                       (int)(d0 >> 52), (int)((d0 >> 48) & 15), (int)((d0 >> 40) & 255), (int)(d0 & 0xFFFFFF),
-                       (int)((d0 >> 24) & 0xFFFF));
-    }
     return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x", err);
   }
   return KSIM_OK;
@@ -1695,9 +1653,14 @@ int ksim_read_nodes(ksim_handle* h, ksim_node_state* o) {
 
 int ksim_get_counter(ksim_handle* h, uint64_t* out) {
   if (!h || !out) return ksim_fail(h, KSIM_E_INVAL, "ksim_get_counter: null argument");
+  KsimCtrKeep keep(h);
   HIPCHK(h, hipSetDevice(h->device));
   HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
   HIPCHK(h, hipMemcpy(out, h->ctx.counter, 8, hipMemcpyDeviceToHost));
+  // the resident kernel's last answer and the word it stored when it left must agree
+  if (keep.known && *out != keep.v)
+    return ksim_fail(h, KSIM_E_DEVICE, "lastNodeIndex %llu on the device, %llu in the resident kernel's last answer",
+                     (unsigned long long)*out, (unsigned long long)keep.v);
   return KSIM_OK;
 }
 

@@ -11,12 +11,19 @@
  *   2. the final device node state equals the host copy column by column.
  * Exit status 0 = pass; prints one summary line.  Needs a GPU (run by tests/test_c_abi.py).
  *
+ *   ksim_c_loop <nodes> <steps> [gap_ms gap_every]
+ * gap_ms / gap_every: sleep gap_ms before every gap_every-th step of the event loop (a scheduler
+ * whose pods arrive sporadically: the resident per-pod kernel leaves by its idle vote and is
+ * relaunched, or a message meets a grid on its way out).
+ *
  * Build: tests/c/Makefile (gcc, links libksim.so and the oracle's libksim_ref.so).
  */
+#define _POSIX_C_SOURCE 199309L
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "ksim.h"
 
@@ -287,6 +294,8 @@ static void batch_parity(int n0, unsigned npods) {
 }
 
 /* ---- 2. scheduleOne loop with cache events vs the oracle ---- */
+static int gap_ms = 0, gap_every = 0;
+
 static void event_loop(int steps) {
   ksim_class_tables ct = one_class();
   ksim_config cfg = config(KSIM_MODE_AUTO);
@@ -301,6 +310,10 @@ static void event_loop(int steps) {
   uint64_t counter = 0;
   int n_sched = 0, n_fit_err = 0, n_add = 0, n_rm = 0, n_nadd = 0, n_nupd = 0, n_nrm = 0;
   for (int step = 0; step < steps; ++step) {
+    if (gap_every > 0 && gap_ms > 0 && step % gap_every == gap_every - 1) {
+      struct timespec ts = {gap_ms / 1000, (long)(gap_ms % 1000) * 1000000L};
+      nanosleep(&ts, NULL);
+    }
     const uint64_t r = rnd() % 100;
     if (r < 70 || n_nodes == 0) {  /* Schedule + assume */
       uint64_t port;
@@ -409,6 +422,10 @@ int main(int argc, char** argv) {
   int steps = argc > 2 ? atoi(argv[2]) : 3000;
   if (n0 < 1 || n0 > MAXN / 2) n0 = 300;
   if (steps < 1 || steps > 1000000) steps = 3000;
+  if (argc > 4) {
+    gap_ms = atoi(argv[3]);
+    gap_every = atoi(argv[4]);
+  }
   if (ksim_abi_version() != KSIM_ABI_VERSION) {
     fprintf(stderr, "FAIL: ABI %d vs header %d\n", ksim_abi_version(), KSIM_ABI_VERSION);
     return 1;

@@ -31,15 +31,77 @@ def test_c_loop_builds_and_links(tmp_path):
     assert out.exists()
 
 
-@pytest.mark.gpu
-def test_c_schedule_one_loop():
-    """scheduleOne loop with pod / node events vs the C oracle, batch vs per-pod parity, final
-    device state (exit 0 and PASS)."""
-    assert os.path.exists(BIN), "tests/c/build/ksim_c_loop not built (__graft_entry__.build())"
-    r = subprocess.run([BIN, "300", "3000"], capture_output=True, text=True, timeout=300)
+# The per-pod forms of ksim_schedule_one, all checked against the same oracle: the library's default
+# (the single-workgroup kernel at this size), the resident kernel (ksim_serve_kernel), the resident
+# kernel with a zero idle bound (its blocks vote to leave as soon as a poll finds nothing, so nearly
+# every message races the grid's exit: messages it left before taking are served by a relaunch),
+# the per-pod pick kernel launched per call, and the multi-block scan.
+PER_POD_FORMS = {
+    "default": {},
+    "resident": {"KSIM_ONE_WG": "0"},
+    "resident_idle0": {"KSIM_ONE_WG": "0", "KSIM_SERVE_IDLE_MS": "0"},
+    "pick_launch": {"KSIM_ONE_WG": "0", "KSIM_SERVE": "0"},
+    "scan": {"KSIM_ONE_WG": "0", "KSIM_NO_PICK": "1"},
+}
+
+
+def _serve_stats(stderr):
+    """Sum of the '[ksim serve]' lines (one per handle that launched the resident kernel)."""
+    keys = ("launches", "messages", "stops", "left-idle", "untaken-relaunches")
+    tot = dict.fromkeys(keys, 0)
+    for line in stderr.splitlines():
+        if line.startswith("[ksim serve]"):
+            w = line.split()
+            for k in keys:
+                tot[k] += int(w[w.index(k) + 1])
+    return tot
+
+
+def _run(args, env_extra, timeout=300):
+    env = dict(os.environ, KSIM_SERVE_STATS="1", **env_extra)
+    r = subprocess.run(args, capture_output=True, text=True, timeout=timeout, env=env)
     print(r.stdout, r.stderr)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "PASS" in r.stdout
+    return _serve_stats(r.stderr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("form", sorted(PER_POD_FORMS))
+def test_c_schedule_one_loop(form):
+    """scheduleOne loop with pod / node events vs the C oracle, batch vs per-pod parity, final
+    device state (exit 0 and PASS), in every per-pod form."""
+    assert os.path.exists(BIN), "tests/c/build/ksim_c_loop not built (__graft_entry__.build())"
+    st = _run([BIN, "300", "3000"], PER_POD_FORMS[form])
+    if form.startswith("resident"):
+        assert st["messages"] > 1000, st
+    if form == "resident_idle0":
+        assert st["left-idle"] > 0, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gap_ms", [150, 250])
+def test_c_schedule_one_loop_idle_gaps(gap_ms):
+    """Pods arriving sporadically: a 150 ms or 250 ms pause before every 4th step (the resident
+    kernel's blocks vote to leave after 200 ms without a message).  Every decision and
+    lastNodeIndex against the oracle; at 250 ms the grid left by its vote and was relaunched."""
+    st = _run([BIN, "300", "160", str(gap_ms), "4"], {"KSIM_ONE_WG": "0"}, timeout=120)
+    assert st["messages"] > 50, st
+    if gap_ms > 200:
+        assert st["left-idle"] > 0, st
+
+
+TWO_BIN = os.path.join(CDIR, "build", "ksim_c_two")
+
+
+@pytest.mark.gpu
+def test_c_two_handles_resident_beside_batch():
+    """A live resident per-pod kernel on one handle beside whole-queue persistent calls on another
+    handle of the same device, one after the other and from two threads at once: every per-pod
+    decision and every batch placement against the C oracle (tests/c/ksim_c_two.c)."""
+    assert os.path.exists(TWO_BIN), "tests/c/build/ksim_c_two not built (__graft_entry__.build())"
+    st = _run([TWO_BIN, "5000", "2000", "20000", "4000", "4"], {"KSIM_ONE_WG": "0"}, timeout=300)
+    assert st["messages"] >= 2000, st
 
 
 K8S_BIN = os.path.join(CDIR, "build", "ksim_k8s_loop")
