@@ -18,8 +18,8 @@
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
+#include <condition_variable>
 #include <mutex>
-#include <shared_mutex>
 
 #include "ksim_handle.h"
 #include "ksim_cache.h"
@@ -288,8 +288,16 @@ size_t serve_stage_bytes(int grid) {
 }
 
 // ---- the device gate (KsimGate, ksim_handle.h) and the handles whose resident kernel runs ----
+// Two classes of sections that exclude each other but not themselves: the resident kernels' calls
+// (shared) and the co-resident launches (exclusive towards the former only: node-sharded ranks on
+// one device run their kernels side by side, and waiting for each other is their protocol).  A
+// waiting co-resident launch holds back new resident sections, so a stream of per-pod calls cannot
+// starve it.
 struct DeviceGate {
-  std::shared_mutex mu;
+  std::mutex mu;
+  std::condition_variable cv;
+  int n_serve = 0, n_batch = 0, n_batch_waiting = 0;
+  std::mutex stop_mu;  // one stopper of other handles' resident kernels at a time
   std::mutex reg_mu;
   std::vector<ksim_handle*> live;
 };
@@ -313,12 +321,25 @@ bool serve_left(const ksim_handle* h) {
 }
 
 // The grid left by its idle vote: drain the stream (its last blocks are on their way out).
+// After the resident kernel drained: an undo it was told of but did not apply (the grid left
+// before its record's block took the message) is done by a launch.
+int tent_drained(ksim_handle* h) {
+  if (!h->tent.undo_inflight) return KSIM_OK;
+  h->tent.undo_inflight = false;
+  if ((uint32_t)__atomic_load_n(&h->serve_box->undo_ack, __ATOMIC_ACQUIRE) == h->tent.rec.seq) return KSIM_OK;
+  hipError_t e = ksim_launch_undo(&h->ctx, &h->tent.rec, h->stream_raw);
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "undo launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipStreamSynchronize(h->stream_raw));
+  h->tent_stats[2] += 1;
+  return KSIM_OK;
+}
+
 int serve_reap(ksim_handle* h) {
   h->serve_live.store(false, std::memory_order_release);
   serve_register(h, false);
   HIPCHK(h, hipStreamSynchronize(h->stream_raw));
   h->serve_stats[3] += 1;
-  return KSIM_OK;
+  return tent_drained(h);
 }
 
 // Launch the resident kernel over the current context; seq0 = the newest message already
@@ -394,6 +415,8 @@ uint64_t serve_write(ksim_handle* h, int32_t type, const ksim_pod* p, const uint
   w[KSIM_SERVE_W_SYNC] = (uint32_t)sync;
   w[KSIM_SERVE_W_NODE] = (uint32_t)(uint64_t)node;
   w[KSIM_SERVE_W_NODE + 1] = (uint32_t)((uint64_t)node >> 32);
+  w[KSIM_SERVE_W_TENT_SEQ] = h->tent.rec.seq;
+  w[KSIM_SERVE_W_TENT_ACT] = (uint32_t)h->tent.act;
   if (p) {
     memcpy(w + KSIM_SERVE_W_POD, p, sizeof *p);
     if (p->port_cnt) memcpy(w + KSIM_SERVE_W_PORTS, ports, (size_t)p->port_cnt * 8);
@@ -408,7 +431,7 @@ uint64_t serve_write(ksim_handle* h, int32_t type, const ksim_pod* p, const uint
 
 // The answer to message seq, when every word the host reads carries its number (node, fit,
 // status, error, lastNodeIndex; the reasons of a FitError).
-bool serve_answer(const ksim_handle* h, uint64_t seq, int32_t* r) {
+bool serve_answer(const ksim_handle* h, uint64_t seq, int32_t* r, bool tent = false) {
   const uint32_t s = (uint32_t)seq;
   const uint64_t* a = h->serve_box->ans;
   auto word = [&](int k) {
@@ -423,6 +446,9 @@ bool serve_answer(const ksim_handle* h, uint64_t seq, int32_t* r) {
       if (!word(KSIM_RES_REASONS + k)) return false;
   } else {
     memset(r + KSIM_RES_REASONS, 0, KSIM_NREASONS * 4);
+    if (tent && r[KSIM_RES_NODE] >= 0)  // the row's port count and flags before the commit
+      for (int k = 0; k < 2; ++k)
+        if (!word(KSIM_RES_REASONS + k)) return false;
   }
   return true;
 }
@@ -444,6 +470,7 @@ int serve_fail(ksim_handle* h, const char* fmt, ...) {
 // device gate (shared).
 int serve_post(ksim_handle* h, int32_t type, const ksim_pod& p, const uint64_t* ports, const ksim_scalar_req* scalars,
                int32_t no_commit, int64_t node, uint32_t tag, int32_t* r) {
+  const bool tent = type == KSIM_SERVE_SCHEDULE && no_commit == KSIM_SERVE_TENTATIVE;
   // the system-scope acquire only after commits of state other blocks read (inter-pod affinity /
   // service counts, volumes); KSIM_SERVE_LIGHT=0: before every message
   static const bool light_off = getenv("KSIM_SERVE_LIGHT") && getenv("KSIM_SERVE_LIGHT")[0] == '0';
@@ -457,14 +484,14 @@ int serve_post(ksim_handle* h, int32_t type, const ksim_pod& p, const uint64_t* 
   h->serve_stats[1] += 1;
   int64_t t0 = now_ns(), next_check = t0 + 1000000;  // every 1 ms: is the kernel still there?
   int relaunches = 0;
-  for (uint64_t spins = 0; !serve_answer(h, seq, r); ++spins) {
+  for (uint64_t spins = 0; !serve_answer(h, seq, r, tent); ++spins) {
     __builtin_ia32_pause();
     if ((spins & 63) != 63) continue;
     if (serve_left(h)) {
       // the grid agreed to leave before any block took this message (a block that voted takes a
       // message only after withdrawing its vote, which fails once the vote is unanimous), so the
       // message is still whole in the mailbox: a fresh launch takes it as its first
-      if (serve_answer(h, seq, r)) break;
+      if (serve_answer(h, seq, r, tent)) break;
       if (++relaunches > SERVE_RELAUNCHES)
         return serve_fail(h, "resident per-pod kernel: message %llu not taken after %d relaunches", (unsigned long long)seq,
                           SERVE_RELAUNCHES);
@@ -480,7 +507,7 @@ int serve_post(ksim_handle* h, int32_t type, const ksim_pod& p, const uint64_t* 
     if (t < next_check) continue;
     next_check = t + 1000000;
     const bool gone = hipStreamQuery(h->stream_raw) == hipSuccess;
-    if (serve_answer(h, seq, r) || serve_left(h)) continue;  // (the loop's checks take it from here)
+    if (serve_answer(h, seq, r, tent) || serve_left(h)) continue;  // (the loop's checks take it from here)
     if (gone || t - t0 > SERVE_WAIT_NS)
       return serve_fail(h, "resident per-pod kernel %s (message %llu)", gone ? "left before answering" : "did not answer",
                         (unsigned long long)seq);
@@ -497,6 +524,24 @@ int serve_post(ksim_handle* h, int32_t type, const ksim_pod& p, const uint64_t* 
     }
     h->ctr_host = ctr;
     h->ctr_known = true;
+  }
+  // the decision on the last tentative commit went out with this message: acknowledged yet?
+  if (h->tent.undo_inflight && (uint32_t)__atomic_load_n(&h->serve_box->undo_ack, __ATOMIC_ACQUIRE) == h->tent.rec.seq)
+    h->tent.undo_inflight = false;
+  if (tent && r[KSIM_RES_NODE] >= 0 && err == 0) {  // a tentative commit: the record's host copy
+    h->tent.live = true;
+    h->tent.launch = h->serve_launch_id;  // (the launch that answered: a relaunch's, when it served it)
+    h->tent.act = KSIM_TENT_NONE;
+    h->tent.rec.node = r[KSIM_RES_NODE];
+    h->tent.rec.seq = (uint32_t)seq;
+    h->tent.rec.cnt0 = r[KSIM_RES_REASONS];
+    h->tent.rec.fl0 = (uint32_t)r[KSIM_RES_REASONS + 1];
+    h->tent.rec.P = p;
+    h->tent.rec.valid = 1;
+    for (int32_t k = 0; k < p.scalar_cnt; ++k) h->tent.rec.sc[k] = scalars[k];
+    for (int32_t k = 0; k < p.port_cnt; ++k) h->tent.ports[k] = ports[k];
+    memcpy(h->tent.res, r, sizeof h->tent.res);
+    h->tent_stats[0] += 1;
   }
   return KSIM_OK;
 }
@@ -597,18 +642,26 @@ int node_shift(ksim_handle* h, int32_t op, int64_t index) {
 KsimGate::KsimGate(ksim_handle* h, bool exclusive) {
   if (!h) return;
   dev = h->device & 63;
-  if (t_gate_hold[dev]) return;  // held by this thread already (an exclusive holder's shared section)
+  if (t_gate_hold[dev]) return;  // held by this thread already (a co-resident launch's own resident stop)
   DeviceGate& g = device_gate(dev);
-  if (!exclusive) {
-    g.mu.lock_shared();
-    mode = 1;
-    t_gate_hold[dev] = 1;
-    return;
+  {
+    std::unique_lock<std::mutex> lk(g.mu);
+    if (!exclusive) {
+      g.cv.wait(lk, [&] { return g.n_batch == 0 && g.n_batch_waiting == 0; });
+      g.n_serve += 1;
+      mode = 1;
+      t_gate_hold[dev] = 1;
+      return;
+    }
+    g.n_batch_waiting += 1;
+    g.cv.wait(lk, [&] { return g.n_serve == 0; });
+    g.n_batch_waiting -= 1;
+    g.n_batch += 1;
   }
-  g.mu.lock();
   mode = 2;
   t_gate_hold[dev] = 2;
-  // no other handle's call is inside its resident section now: stop their kernels on this device
+  // no handle's call is inside its resident section now: stop the other handles' kernels here
+  std::lock_guard<std::mutex> sl(g.stop_mu);
   std::vector<ksim_handle*> others;
   {
     std::lock_guard<std::mutex> lk(g.reg_mu);
@@ -622,11 +675,50 @@ KsimGate::~KsimGate() {
   if (!mode) return;
   DeviceGate& g = device_gate(dev);
   t_gate_hold[dev] = 0;
-  if (mode == 2) g.mu.unlock();
-  else g.mu.unlock_shared();
+  std::lock_guard<std::mutex> lk(g.mu);
+  if (mode == 2) g.n_batch -= 1;
+  else g.n_serve -= 1;
+  g.cv.notify_all();
 }
 
 void ksim_serve_forget(ksim_handle* h) { serve_register(h, false); }
+
+int ksim_tent_undo(ksim_handle* h) {
+  if (!h->tent.live) return KSIM_OK;
+  h->tent.live = false;
+  h->tent_stats[1] += 1;
+  if (h->serve_live.load() && h->tent.launch == h->serve_launch_id && !serve_left(h)) {
+    // the kernel that holds the record runs: the next message (a stop's EXIT included) carries the
+    // undo, applied by the record's block before anything reads the row
+    h->tent.act = KSIM_TENT_UNDO;
+    h->tent.undo_inflight = true;
+    return KSIM_OK;
+  }
+  // the record left with an earlier launch: undo by a launch on the quiet stream
+  h->tent.act = KSIM_TENT_NONE;
+  if (h->serve_live.load()) {
+    int rc = serve_left(h) ? serve_reap(h) : ksim_serve_stop(h);
+    if (rc) return rc;
+  }
+  hipError_t e = ksim_launch_undo(&h->ctx, &h->tent.rec, h->stream_raw);
+  if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "undo launch: %s", hipGetErrorString(e));
+  HIPCHK(h, hipStreamSynchronize(h->stream_raw));
+  h->tent_stats[2] += 1;
+  return KSIM_OK;
+}
+
+// ksim_pod_add right after a tentative commit, naming the same pod and node: the commit stands.
+static bool tent_confirms(ksim_handle* h, int64_t node, const ksim_pod& pod, const uint64_t* ports, const ksim_scalar_req* scalars) {
+  if (!h->tent.live || node != h->tent.rec.node || pod.port_cnt > KSIM_ONE_PORTS || pod.scalar_cnt > KSIM_MAX_SCALAR) return false;
+  ksim_pod a = staged_pod(h, pod), b = h->tent.rec.P;
+  a.host = b.host = -1;  // (spec.nodeName plays no part in the commit)
+  if (memcmp(&a, &b, sizeof a) != 0) return false;
+  for (int32_t k = 0; k < pod.port_cnt; ++k)
+    if (ports[pod.port_off + k] != h->tent.ports[k]) return false;
+  for (int32_t k = 0; k < pod.scalar_cnt; ++k)
+    if (memcmp(&scalars[pod.scalar_off + k], &h->tent.rec.sc[k], sizeof(ksim_scalar_req)) != 0) return false;
+  return true;
+}
 
 int ksim_serve_stop(ksim_handle* h) {
   if (!h->serve_live.load(std::memory_order_acquire)) return KSIM_OK;
@@ -637,6 +729,7 @@ int ksim_serve_stop(ksim_handle* h) {
   h->serve_stats[2] += 1;
   (void)serve_write(h, KSIM_SERVE_EXIT, nullptr, nullptr, nullptr, 0, -1, 0, 0);
   HIPCHK(h, hipStreamSynchronize(h->stream_raw));
+  if (int rc = tent_drained(h)) return rc;
 #ifdef KSIM_STAMPS
   uint64_t d[32];
   HIPCHK(h, hipMemcpy(d, h->ctx.dbg + 64, sizeof d, hipMemcpyDeviceToHost));
@@ -758,12 +851,20 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
       h->pick_tag = h->pick_tag % 254u + 1u;
       if (serve_wanted(h) && h->serve_fits && pod->port_cnt <= KSIM_ONE_PORTS && pod->scalar_cnt <= KSIM_MAX_SCALAR) {
         KsimGate gate(h, false);
+        // the last SCHEDULE_ONLY was not followed by its AssumePod: undo its tentative commit (this
+        // message carries the undo)
+        if (h->tent.live && (rc = ksim_tent_undo(h))) return rc;
         if ((rc = serve_ready(h, npt, grid))) return rc;
         oc.lap(0);
         const ksim_pod sp = staged_pod(h, *pod);
+        // SCHEDULE_ONLY: a tentative commit when the commit touches the pod's row alone (no volume
+        // mounts, no affinity / service counts), so the AssumePod that normally follows costs no
+        // message (KSIM_TENTATIVE=0: decide only)
+        static const bool tent_off = getenv("KSIM_TENTATIVE") && getenv("KSIM_TENTATIVE")[0] == '0';
+        const int32_t nc = assume ? 0 : (!tent_off && !ksim_is_aff_host(h, *pod) && pod->vol_class == 0 ? KSIM_SERVE_TENTATIVE : 1);
         int32_t r[KSIM_RES_WORDS];
-        if ((rc = serve_post(h, KSIM_SERVE_SCHEDULE, sp, ports + pod->port_off, scalars + pod->scalar_off, assume ? 0 : 1, -1,
-                             h->pick_tag, r)))
+        if ((rc = serve_post(h, KSIM_SERVE_SCHEDULE, sp, ports + pod->port_off, scalars + pod->scalar_off, nc, -1, h->pick_tag,
+                             r)))
           return rc;
         oc.lap(2);
         memset(out, 0, sizeof *out);
@@ -880,6 +981,14 @@ static int pod_delta(ksim_handle* h, int64_t node, const ksim_pod* pod, const ui
   if (rc) return rc;
   if ((rc = check_pod_args(h, pod, n_ports, n_scalars, ports, scalars, where))) return rc;
   if (node < 0 || node >= h->ctx.n) return ksim_fail(h, KSIM_E_INVAL, "%s: node %lld out of range", where, (long long)node);
+  // Scheduler.assume after a SCHEDULE_ONLY of this pod onto this node (scheduler.go:366-397,
+  // cache.AssumePod cache.go:125-143): the resident kernel committed it tentatively, so it stands
+  if (add && h->tent.live && tent_confirms(h, node, *pod, ports, scalars)) {
+    h->tent.live = false;
+    h->tent.act = KSIM_TENT_CONFIRM;  // (the next message lets the record go)
+    h->tent_stats[3] += 1;
+    return after_commit(h, pod->port_cnt, h->tent.res);
+  }
   if ((rc = ksim_rt_check_aff(h, where))) return rc;
   if (add && (rc = ensure_port_room(h, pod->port_cnt))) return rc;
   ksim_pod p = *pod;
@@ -889,6 +998,7 @@ static int pod_delta(ksim_handle* h, int64_t node, const ksim_pod* pod, const ui
   // pattern), when it serves the current context
   if (add && h->serve_live.load() && p.port_cnt <= KSIM_ONE_PORTS && p.scalar_cnt <= KSIM_MAX_SCALAR) {
     KsimGate gate(h, false);
+    if (h->tent.live && (rc = ksim_tent_undo(h))) return rc;
     if (h->serve_live.load() && memcmp(&h->ctx, &h->serve_base, sizeof(KsimCtx)) == 0) {
       int32_t r[KSIM_RES_WORDS];
       if ((rc = serve_post(h, KSIM_SERVE_ASSUME, staged_pod(h, p), ports + p.port_off, scalars + p.scalar_off, 0, node, 0, r)))

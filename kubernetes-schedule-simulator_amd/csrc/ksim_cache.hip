@@ -81,6 +81,11 @@ __global__ void ksim_release_kernel(KsimCtx c, int64_t pod, int64_t node) {
   if (ksim_is_aff_pod(c, P)) ksim_aff_commit_body(*c.aff, P, node, -1, threadIdx.x, 64);
 }
 
+// Undo a tentative commit whose record left with the resident kernel (ksim_cache.cpp).
+__global__ void ksim_undo_kernel(KsimCtx c, KsimTentRec t) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) ksim_undo_commit(c, t);
+}
+
 // Queued pods' spec.nodeName name ranks after a node insert (op 1) or removal (op 2).
 __global__ __launch_bounds__(256) void ksim_remap_hosts_kernel(ksim_pod* pods, int64_t n_pods, int64_t idx, int32_t op) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -134,6 +139,12 @@ extern "C" hipError_t ksim_launch_relayout(const KsimRelayout* r, hipStream_t s)
 extern "C" hipError_t ksim_launch_set_row(const KsimCtx* c, int64_t node, const uint64_t* pack, int32_t full,
                                           hipStream_t s) {
   hipLaunchKernelGGL(ksim_set_row_kernel, dim3(1), dim3(64), 0, s, *c, node, pack, full);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t ksim_launch_undo(const KsimCtx* c, const KsimTentRec* t, hipStream_t s) {
+  if (t->node < 0 || t->node >= c->n) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(ksim_undo_kernel, dim3(1), dim3(64), 0, s, *c, *t);
   return hipGetLastError();
 }
 

@@ -257,8 +257,21 @@ __device__ __forceinline__ ksim_scalar_req ksim_pod_scalar(const KsimCtx& c, con
 #define KSIM_SERVE_W_POD 6       // ksim_pod (32 words)
 #define KSIM_SERVE_W_PORTS (KSIM_SERVE_W_POD + (int)(sizeof(ksim_pod) / 4))   // KSIM_ONE_PORTS keys
 #define KSIM_SERVE_W_SCALARS (KSIM_SERVE_W_PORTS + 2 * KSIM_ONE_PORTS)       // KSIM_MAX_SCALAR requests
+// Every message (EXIT included) also says what became of the last tentative commit (below): the
+// message number of its SCHEDULE and KSIM_TENT_* (the block holding its record acts on the first
+// message it takes after the host decided)
+#define KSIM_SERVE_W_TENT_SEQ 120
+#define KSIM_SERVE_W_TENT_ACT 121
+#define KSIM_TENT_NONE 0     // undecided (the record stays)
+#define KSIM_TENT_CONFIRM 1  // AssumePod named the same pod and node: the commit stands, drop the record
+#define KSIM_TENT_UNDO 2     // anything else came first: undo the commit, then drop the record
+// SCHEDULE's KSIM_SERVE_W_NOCOMMIT: 0 commit (SCHEDULE_ASSUME), 1 decide only, 2 tentative commit
+// (SCHEDULE_ONLY of a pod whose commit touches only its own row: the owner block commits it and
+// keeps a record, and answers the row's port count and flags before the commit in the first two
+// reason words, so the host can undo it without the kernel too)
+#define KSIM_SERVE_TENTATIVE 2
 static_assert(sizeof(ksim_pod) % 4 == 0 && sizeof(ksim_scalar_req) % 4 == 0, "mailbox words");
-static_assert(KSIM_SERVE_W_SCALARS + (int)(KSIM_MAX_SCALAR * sizeof(ksim_scalar_req) / 4) <= KSIM_SERVE_MSG_WORDS,
+static_assert(KSIM_SERVE_W_SCALARS + (int)(KSIM_MAX_SCALAR * sizeof(ksim_scalar_req) / 4) <= KSIM_SERVE_W_TENT_SEQ,
               "a mailbox message holds a pod with KSIM_ONE_PORTS ports and KSIM_MAX_SCALAR scalars");
 // Leaving.  The grid leaves on an EXIT message, or by agreement when idle: a block that has seen
 // no message for idle_ticks votes in a device word (KSIM_SERVE_ST_*, agent-scope CAS); the vote
@@ -276,7 +289,19 @@ struct KsimServeBox {
   uint64_t msg[KSIM_SERVE_MSG_WORDS];  // host: the current message (16-byte aligned)
   uint64_t ans[KSIM_RES_WORDS];        // device: the answer, word k = KSIM_RES_* word | seq << 32
   uint64_t left;                       // device: launch id << 32 | last message, when it left by agreement
-  uint64_t pad1[7];
+  uint64_t undo_ack;                   // device: the tentative commit (its message number) last undone
+  uint64_t pad1[6];
+};
+// A tentative commit as the resident kernel's owner block records it (LDS) and as the host keeps
+// it (to undo it with ksim_launch_undo when the kernel that holds the record is gone).
+struct KsimTentRec {
+  int64_t node;
+  uint32_t seq;
+  int32_t valid;
+  int32_t cnt0;  // the row's port count before the commit (the commit appends its new keys)
+  uint32_t fl0;  // the row's flags before the commit
+  ksim_pod P;
+  ksim_scalar_req sc[KSIM_MAX_SCALAR];
 };
 // The resident kernel's launch arguments beside the context.
 struct KsimServeArgs {
@@ -1057,6 +1082,24 @@ __device__ __forceinline__ int32_t ksim_commit_wave(const KsimCtx& c, const ksim
   }
   if (lane == 0 && cnt != cnt0) c.port_count[w] = cnt;
   return st | 2 | (cnt << 8);
+}
+
+// Undo a commit of pod P on row w exactly (a tentative commit the host did not confirm): the
+// arithmetic inverse of ksim_commit_wave — quantities back, pod count back, the row's port count
+// and flags as they were before (its new keys were appended past cnt0).  Single thread.
+__device__ __forceinline__ void ksim_undo_commit(const KsimCtx& c, const KsimTentRec& t) {
+  const int64_t w = t.node;
+  const ksim_pod& P = t.P;
+  c.req_cpu[w] -= P.add_cpu;
+  c.req_mem[w] -= P.add_mem;
+  c.req_gpu[w] -= P.add_gpu;
+  c.req_eph[w] -= P.add_eph;
+  c.nz_cpu[w] -= P.nz_cpu;
+  c.nz_mem[w] -= P.nz_mem;
+  c.pod_count[w] -= 1;
+  c.flags[w] = t.fl0;
+  for (int32_t s = 0; s < P.scalar_cnt; ++s) c.req_scalar[(int64_t)t.sc[s].col * c.n + w] -= t.sc[s].add;
+  if (P.port_cnt) c.port_count[w] = t.cnt0;
 }
 
 // Remove pod P from node w: NodeInfo.RemovePod (node_info.go:343-390) — the containers-only

@@ -65,6 +65,7 @@ extern "C" hipError_t ksim_launch_relayout(const KsimRelayout* r, hipStream_t s)
 extern "C" hipError_t ksim_launch_set_row(const KsimCtx* c, int64_t node, const uint64_t* pack, int32_t full,
                                           hipStream_t s);
 extern "C" hipError_t ksim_launch_release(const KsimCtx* c, int64_t pod, int64_t node, hipStream_t s);
+extern "C" hipError_t ksim_launch_undo(const KsimCtx* c, const KsimTentRec* t, hipStream_t s);
 extern "C" hipError_t ksim_launch_remap_hosts(ksim_pod* pods, int64_t n_pods, int64_t idx, int32_t op, hipStream_t s);
 extern "C" hipError_t ksim_launch_pod_k(ksim_pod* pods, int64_t n_pods, const KsimCtx* c, hipStream_t s);
 extern "C" hipError_t ksim_launch_port_max(const int32_t* port_count, int64_t n, int32_t* out, hipStream_t s);
@@ -101,7 +102,16 @@ struct ksim_handle {
   int32_t n_classes = 0;
   int32_t n_label_sets = 0, n_taint_sets = 0;   // of the loaded class tables
   int32_t max_label_set = -1, max_taint_set = -1;  // largest ids the node table uses
-  std::vector<void*> class_bufs;                 // class-table buffers (replaced on reload)
+  std::vector<void*> class_bufs;                 // class-table buffers (replaced when they grow)
+  // class tables at capacity strides + their pinned host mirror (ksim_load_classes)
+  struct {
+    int64_t cap_c = 0, cap_l = 0, cap_t = 0;  // capacities (the device strides)
+    int64_t c = 0, l = 0, t = 0;              // loaded
+    bool has_na = false, has_sv = false;
+    char* mirror = nullptr;
+    int64_t loads = 0, in_place = 0;          // reloads, and those written beside a running resident kernel
+  } cls;
+  hipStream_t side_stream = nullptr;             // table writes beside the resident per-pod kernel
   // launch-mode graph
   hipGraphExec_t gexec = nullptr;
   hipGraph_t graph = nullptr;
@@ -165,6 +175,19 @@ struct ksim_handle {
   // exactly when two or more nodes fit, generic_scheduler.go:183-198)
   uint64_t ctr_host = 0;
   bool ctr_known = false;
+  // the adapter's SCHEDULE_ONLY + AssumePod pattern in one message: a tentative commit (the resident
+  // kernel commits a SCHEDULE_ONLY pod and keeps a record; a ksim_pod_add naming the same pod and
+  // node confirms it without a message, anything else undoes it first — ksim_cache.cpp)
+  struct {
+    bool live = false;            // the rows hold a commit the host has not decided on
+    bool undo_inflight = false;   // decided "undo", carried by messages, not yet acknowledged
+    uint32_t launch = 0;          // the resident launch that holds the record
+    int32_t act = 0;              // what messages tell the kernel about rec.seq (KSIM_TENT_*)
+    KsimTentRec rec{};            // (ports: rec.P.port_cnt of them in ports)
+    uint64_t ports[KSIM_ONE_PORTS] = {};
+    int32_t res[KSIM_RES_WORDS] = {};  // its answer (status / error for the confirming assume)
+  } tent;
+  int64_t tent_stats[4] = {0, 0, 0, 0};  // tentative commits, undone, undone by a launch, confirmed
   int32_t* tcls = nullptr;
   int64_t tcls_cap = 0;
   KsimTreeClass* tclass = nullptr;
@@ -230,6 +253,7 @@ struct ksim_handle {
   char* vol_small = nullptr;
   size_t vol_small_cap = 0;
   std::vector<char> vol_small_host;
+  int64_t vol_in_place = 0;      // grows written beside a running resident per-pod kernel
   std::vector<int32_t> q_vclass;
   std::vector<int64_t> vol_pre;  // vol_pre[i] = volume / service-affinity pods among the first i queued
 };
@@ -239,7 +263,10 @@ int ksim_fail(ksim_handle* h, int code, const char* fmt, ...);
 int ksim_serve_stop(ksim_handle* h);
 // The handle leaves the device gate's list of running resident kernels (ksim_destroy).
 void ksim_serve_forget(ksim_handle* h);
+// Settle a tentative commit before any other use of the handle's state: undo it (ksim_cache.cpp).
+int ksim_tent_undo(ksim_handle* h);
 inline hipStream_t ksim_stream(ksim_handle* h) {
+  if (h->tent.live) (void)ksim_tent_undo(h);  // (the stop below carries the undo to the kernel)
   if (h->serve_live.load(std::memory_order_acquire)) (void)ksim_serve_stop(h);
   h->ctr_known = false;  // (the stream's next use may change lastNodeIndex)
   return h->stream_raw;
@@ -258,9 +285,10 @@ struct KsimCtrKeep {
 // The device gate (ksim_cache.cpp).  A kernel whose blocks wait on each other (the persistent
 // batch kernels, the per-pod pick kernel, the fused pass-A scan, the node-sharded kernels) must
 // not share the device with another handle's resident per-pod kernel, which holds CUs between
-// calls: such launches run under the gate held exclusively, which first stops every other
-// handle's resident kernel on the device; the resident kernels' calls hold it shared.  Nested
-// holds by one thread are free (an exclusive holder's own shared sections skip the lock).
+// calls: such launches run with the gate taken "exclusive", which waits for every resident
+// section to end, holds new ones back and stops every other handle's resident kernel on the
+// device; the resident kernels' calls take it "shared".  Exclusive holders do not exclude each
+// other (node-sharded ranks on one device).  Nested holds by one thread are free.
 struct KsimGate {
   int dev = -1;
   int mode = 0;  // 0: not taken here, 1 shared, 2 exclusive

@@ -1504,8 +1504,10 @@ constexpr int PK_BATCH = 16;  // record words one lane keeps in flight (a cross-
 // number, so no word of an earlier answer can pass for this one whatever order the stores become
 // visible in (round 5's answer — untagged words, then a `done` word — needed a system-scope release
 // between them).  vr: lane r's FitError reason count (r < KSIM_NREASONS).
+// tent: a tentative commit's answer, whose first two reason words carry the row's port count and
+// flags before the commit (vr of lanes 0 and 1)
 __device__ __forceinline__ void pk_answer(uint64_t* ans, uint64_t seq, int lane, int32_t node, int32_t fit,
-                                          int32_t status, int32_t err, uint64_t ctr, int32_t vr) {
+                                          int32_t status, int32_t err, uint64_t ctr, int32_t vr, bool tent = false) {
   const int32_t reason = __shfl(vr, (lane - KSIM_RES_REASONS) & 63, 64);
   int32_t v = 0;
   if (lane == KSIM_RES_NODE) v = node;
@@ -1516,7 +1518,8 @@ __device__ __forceinline__ void pk_answer(uint64_t* ans, uint64_t seq, int lane,
   else if (lane == KSIM_RES_CTR) v = (int32_t)(uint32_t)ctr;
   else if (lane == KSIM_RES_CTR + 1) v = (int32_t)(uint32_t)(ctr >> 32);
   // the reason words only for a FitError (the host reads them only then)
-  const bool want = lane < KSIM_RES_WORDS && (node == -1 || lane < KSIM_RES_REASONS || lane >= KSIM_RES_CTR);
+  const bool want = lane < KSIM_RES_WORDS && (node == -1 || lane < KSIM_RES_REASONS || lane >= KSIM_RES_CTR ||
+                                               (tent && lane < KSIM_RES_REASONS + 2));
   if (want) __hip_atomic_store(ans + lane, ((uint64_t)(uint32_t)seq << 32) | (uint64_t)(uint32_t)v, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -1526,11 +1529,13 @@ static_assert(KSIM_RES_WORDS <= 64, "one answer word per lane");
 // One pod of the pick form.  rec: this pod's record buffer (tag parity, KSIM_PICK_WORDS words);
 // ctr_keep: the block's own copy of lastNodeIndex (resident form; null: read *c.counter);
 // ans / seq: the resident form's answer words and message number (null: a one-pod launch, which
-// writes the result block and *c.counter directly).
+// writes the result block and *c.counter directly); tent: the block's tentative-commit record
+// (resident form; no_commit == KSIM_SERVE_TENTATIVE: commit, record, answer the row's prior state).
 template <int NPT>
 __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod& P, const int64_t pod, const uint32_t tag,
                                                const int32_t no_commit, uint64_t* const rec, uint64_t* ctr_keep,
-                                               uint64_t* ans, const uint64_t seq, uint64_t* stamp = nullptr) {
+                                               uint64_t* ans, const uint64_t seq, KsimTentRec* tent = nullptr,
+                                               uint64_t* stamp = nullptr) {
 #ifdef KSIM_STAMPS
 #define PKST(k) do { if (stamp && threadIdx.x == 0) stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
@@ -1956,15 +1961,32 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   __syncthreads();
   PKST(8);
   const int64_t node = s_node;
-  if (node >= 0 && !no_commit) {
+  const bool tentative = tent && no_commit == KSIM_SERVE_TENTATIVE;
+  __shared__ int32_t s_cnt0;
+  __shared__ uint32_t s_fl0;
+  if (node >= 0 && no_commit != 1) {
     // a commit of state other blocks read (volume mounts, inter-pod affinity / service counts): each
     // committing wave releases it at agent scope before the answer, so the next message's acquire
     // (KSIM_SERVE_SYNC_ACQUIRE) sees it (rows are read by this block's own waves only)
     if (wv == 0) {
+      int32_t cnt0 = 0;
+      uint32_t fl0 = 0;
+      if (tentative && lane == 0) { cnt0 = c.port_count[node]; fl0 = c.flags[node]; }
       const int32_t st = ksim_commit_wave(c, P, node, lane);
       if (tid == 0) {
         if (ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, node, 1, c.err);
         s_stat = st;
+        if (tentative) {  // (the host sends tentative commits only for pods without volumes / affinity terms)
+          s_cnt0 = cnt0;
+          s_fl0 = fl0;
+          tent->node = node;
+          tent->seq = (uint32_t)seq;
+          tent->cnt0 = cnt0;
+          tent->fl0 = fl0;
+          tent->P = P;
+          for (int32_t k = 0; k < P.scalar_cnt; ++k) tent->sc[k] = ksim_pod_scalar(c, P, k);
+          tent->valid = 1;
+        }
       }
       if (ans && ksim_is_vol_pod(c, P)) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     } else if (wv == 1 && ksim_is_aff_pod(c, P)) {
@@ -1978,8 +2000,11 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   if (ans) {
     // the answer; lastNodeIndex stays in the blocks' LDS (every block took the same decision) and
     // reaches the host in the answer — no device store of it while the kernel is resident
-    if (wv == 0) pk_answer(ans, seq, lane, (int32_t)node, s_F, s_stat, __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                           s_ctr, 0);
+    if (wv == 0) {
+      const bool tc = tentative && node >= 0;
+      pk_answer(ans, seq, lane, (int32_t)node, s_F, s_stat, __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                s_ctr, tc ? (lane == 0 ? s_cnt0 : (int32_t)s_fl0) : 0, tc);
+    }
   } else if (tid == 0) {
     if (mode == 2) *c.counter = s_ctr;  // (a one-pod launch: this block is the call's only writer)
     c.out_node[pod] = (int32_t)node;
@@ -2055,12 +2080,16 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
   __shared__ int64_t s_node;
   __shared__ uint32_t s_msg[KSIM_SERVE_MSG_WORDS];
   __shared__ uint64_t s_seq;
+  __shared__ KsimTentRec s_tent;  // this block's tentative commit awaiting the host's decision
+  __shared__ int32_t s_got;       // wave 0 took a message (an EXIT included)
   KsimServeBox* const box = a.box;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, me = blockIdx.x;
   // lastNodeIndex: from the host's last answer, or (after calls of other forms) the device word,
   // read coherently (system scope: never a stale line of this XCD's L2)
-  if (tid == 0)
+  if (tid == 0) {
     s_keep = a.ctr0_valid ? a.ctr0 : __hip_atomic_load(c.counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    s_tent.valid = 0;
+  }
 #ifdef KSIM_STAMPS
   // diagnostic builds: per phase, the sum of (stamp k - stamp k-1) and how often both were taken,
   // over every block and message, into dbg[64 + k] / dbg[80 + k] at the exit (k = 0: the poll)
@@ -2090,18 +2119,20 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
       const uint64_t* src = box->msg + 2 * lane;
       u4 q;
       int32_t type = KSIM_SERVE_EXIT;
+      bool got = false;
       for (;;) {
         asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"(q) : "v"(src) : "memory");
         const uint32_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)q.y);
         if ((int32_t)(t - s32) >= 0 && __all(q.y == t && q.w == t)) {
           type = __builtin_amdgcn_readfirstlane((int32_t)q.x);  // word 0 (lane 0)
+          got = true;
           if (type != KSIM_SERVE_EXIT && voted) {
             // this block voted to leave: withdraw the vote before taking the message
             uint32_t ok = 0;
             if (lane == 0) ok = serve_veto(a.state, vote_ep);
             ok = (uint32_t)__builtin_amdgcn_readfirstlane((int32_t)ok);
             voted = false;
-            if (!ok) type = KSIM_SERVE_EXIT;  // the grid left first: nobody takes it (the host relaunches)
+            if (!ok) { type = KSIM_SERVE_EXIT; got = false; }  // the grid left first: nobody takes it (the host relaunches)
           }
           if (lane == 0) s_seq = seq + 1 + (uint64_t)(t - s32);
 #ifdef KSIM_STAMPS
@@ -2137,11 +2168,13 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
 #endif
         __builtin_amdgcn_s_sleep(1);
       }
+      if (got) {  // (an EXIT too: it may carry the decision on a tentative commit)
+        s_msg[2 * lane] = q.x;
+        s_msg[2 * lane + 1] = q.z;
+      }
       if (type == KSIM_SERVE_SCHEDULE || type == KSIM_SERVE_ASSUME) {
         // the payload through LDS: the pod into s_P, ports / scalars into this block's staging
         // slot (the evaluation reads them there)
-        s_msg[2 * lane] = q.x;
-        s_msg[2 * lane + 1] = q.z;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2176,17 +2209,29 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
           s_node = (int64_t)(((uint64_t)s_msg[KSIM_SERVE_W_NODE + 1] << 32) | s_msg[KSIM_SERVE_W_NODE]);
         }
       }
-      if (lane == 0) s_type = type;
+      if (lane == 0) { s_type = type; s_got = got ? 1 : 0; }
     }
     __syncthreads();
 #ifdef KSIM_STAMPS
     if (tid == 0) s_st[1] = __builtin_amdgcn_s_memrealtime();
 #endif
     const int32_t type = s_type;
+    // the host's decision on this block's tentative commit, before anything else reads the row
+    if (s_got && s_tent.valid && s_msg[KSIM_SERVE_W_TENT_SEQ] == s_tent.seq && s_msg[KSIM_SERVE_W_TENT_ACT] != KSIM_TENT_NONE) {
+      if (tid == 0) {
+        if (s_msg[KSIM_SERVE_W_TENT_ACT] == KSIM_TENT_UNDO) {
+          ksim_undo_commit(c, s_tent);
+          __hip_atomic_store(&box->undo_ack, (uint64_t)s_tent.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        s_tent.valid = 0;
+      }
+      __syncthreads();
+    }
     if (type != KSIM_SERVE_EXIT) seq = s_seq;
     if (type == KSIM_SERVE_SCHEDULE) {
       const ksim_pod P = s_P;
-      ksim_pick_body<NPT>(c, P, 0, s_tag, s_nc, c.pick + (s_tag & 1u) * KSIM_PICK_WORDS, &s_keep, box->ans, seq, stamp);
+      ksim_pick_body<NPT>(c, P, 0, s_tag, s_nc, c.pick + (s_tag & 1u) * KSIM_PICK_WORDS, &s_keep, box->ans, seq, &s_tent,
+                          stamp);
     } else if (type == KSIM_SERVE_ASSUME) {
       // a resource delta onto a given node (ksim_pod_add): the block whose chunk holds it answers
       const int64_t node = s_node;

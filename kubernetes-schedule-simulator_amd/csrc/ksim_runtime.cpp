@@ -86,6 +86,9 @@ void ksim_destroy(ksim_handle* h) {
     fprintf(stderr, "[ksim serve] launches %lld messages %lld stops %lld left-idle %lld untaken-relaunches %lld\n",
             (long long)h->serve_stats[0], (long long)h->serve_stats[1], (long long)h->serve_stats[2],
             (long long)h->serve_stats[3], (long long)h->serve_stats[4]);
+  if (getenv("KSIM_SERVE_STATS") && h->tent_stats[0])
+    fprintf(stderr, "[ksim tentative] commits %lld undone %lld by-launch %lld confirmed %lld\n", (long long)h->tent_stats[0],
+            (long long)h->tent_stats[1], (long long)h->tent_stats[2], (long long)h->tent_stats[3]);
 #ifdef KSIM_STAMPS
   if (h->ctx.dbg) {  // the scan kernel's phase stamps (ksim_kernels.hip SSTAMP)
     uint64_t d[64];
@@ -106,6 +109,8 @@ void ksim_destroy(ksim_handle* h) {
   for (auto& b : h->bufs) (void)hipFree(b.p);
   if (h->stg_host) (void)hipHostFree(h->stg_host);  // res_host points into it
   if (h->serve_box) (void)hipHostFree(h->serve_box);
+  if (h->cls.mirror) (void)hipHostFree(h->cls.mirror);
+  if (h->side_stream) (void)hipStreamDestroy(h->side_stream);
   if (h->ev0) (void)hipEventDestroy(h->ev0);
   if (h->ev1) (void)hipEventDestroy(h->ev1);
   if (h->stream_raw) (void)hipStreamDestroy(h->stream_raw);
@@ -180,6 +185,23 @@ int ksim_load_nodes(ksim_handle* h, const ksim_node_table* t) {
   return KSIM_OK;
 }
 
+// The class tables live at capacity strides (h->cls, ksim_handle.h): a reload that fits the
+// capacities writes only the rows that changed (new pod classes: their rows; new label / taint sets:
+// every class's row) through a pinned host mirror, on a side stream when the resident per-pod kernel
+// runs (its next message acquires: KSIM_SERVE_SYNC_ACQUIRE), so the table pointers and strides stay
+// and the resident kernel keeps running.  A reload beyond the capacities doubles them (one stop).
+namespace {
+constexpr int32_t one = 1;  // n_tt / n_na when the caller passes none
+struct ClsArr {
+  const void* src;   // the caller's [C][width] array (null: the default)
+  int32_t esz;       // element bytes
+  int64_t width;     // elements per class (caller)
+  int64_t stride;    // elements per class (device, capacity)
+  void** dev;        // the ctx pointer
+  int64_t mirror;    // byte offset of this array in the pinned mirror
+};
+}  // namespace
+
 int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
   if (!h || !t) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_classes: null argument");
   HIPCHK(h, hipSetDevice(h->device));
@@ -190,51 +212,134 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
     return ksim_fail(h, KSIM_E_INVAL, "ksim_load_classes: the node table uses label / taint sets beyond the new tables");
   for (int32_t k : h->q_cls)
     if (k >= t->n_classes) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_classes: a queued pod uses class %d beyond the new tables", k);
-  const size_t C = t->n_classes, L = t->n_label_sets, T = t->n_taint_sets;
-  const size_t lw = (L + 31) / 32, tw = (T + 31) / 32;
-  for (size_t k = 0; k < C; ++k) {
+  const int64_t C = t->n_classes, L = t->n_label_sets, T = t->n_taint_sets;
+  const int64_t lw = (L + 31) / 32, tw = (T + 31) / 32;
+  for (int64_t k = 0; k < C; ++k) {
     const int a = t->n_tt ? t->n_tt[k] : 1, b = t->n_na ? t->n_na[k] : 1;
     if (a < 1 || b < 1 || a > KSIM_MAX_RCLASS || b > KSIM_MAX_RCLASS)
-      return ksim_fail(h, KSIM_E_UNSUPPORTED, "class %zu: %d x %d reduce classes exceed %d per dimension", k, a, b,
+      return ksim_fail(h, KSIM_E_UNSUPPORTED, "class %lld: %d x %d reduce classes exceed %d per dimension", (long long)k, a, b,
                        KSIM_MAX_RCLASS);
   }
   KsimCtx& c = h->ctx;
-  int rc;
-  uint32_t *so, *to, *no, *sv = nullptr;
-  uint8_t *tc, *nc;
-  int32_t *ntt, *nna;
-  int64_t *tv, *nv, *na = nullptr;
-  std::vector<int32_t> ones(C, 1);
-  const size_t nb0 = h->bufs.size();
-  if ((rc = dev_upload(h, &so, t->sel_ok, C * lw)) || (rc = dev_upload(h, &to, t->taint_ok, C * tw)) ||
-      (rc = dev_upload(h, &no, t->noexec_ok, C * tw)) || (rc = dev_upload(h, &tc, t->tt_class, C * T)) ||
-      (rc = dev_upload(h, &nc, t->na_class, C * L)) ||
-      (rc = dev_upload(h, &ntt, t->n_tt ? t->n_tt : ones.data(), C)) ||
-      (rc = dev_upload(h, &nna, t->n_na ? t->n_na : ones.data(), C)) ||
-      (rc = dev_upload(h, &tv, t->tt_val, C * KSIM_MAX_RCLASS)) || (rc = dev_upload(h, &nv, t->na_val, C * KSIM_MAX_RCLASS)) ||
-      (t->na_add && (rc = dev_upload(h, &na, t->na_add, C * KSIM_MAX_RCLASS))) ||
-      (t->svc_ok && (rc = dev_upload(h, &sv, t->svc_ok, C * lw))))
-    return rc;
-  HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));
-  for (void* q : h->class_bufs) dev_free(h, q);  // the previous tables (reload)
-  h->class_bufs.clear();
-  for (size_t k = nb0; k < h->bufs.size(); ++k) h->class_bufs.push_back(h->bufs[k].p);
-  c.sel_ok = so; c.taint_ok = to; c.noexec_ok = no; c.tt_class = tc; c.na_class = nc;
-  c.n_tt = ntt; c.n_na = nna; c.tt_val = tv; c.na_val = nv; c.na_add = na; c.svc_ok = sv;
-  c.use_na = (c.w[KSIM_W_NODE_AFFINITY] != 0 || na) ? 1 : 0;
-  c.lwords = (int32_t)lw; c.twords = (int32_t)tw;
-  c.n_label_sets = (int32_t)L; c.n_taint_sets = (int32_t)T;
-  c.n_classes_dev = t->n_classes;
+  auto& cl = h->cls;
+  const bool has_na = t->na_add != nullptr, has_sv = t->svc_ok != nullptr;
+  const bool fits = cl.mirror && C <= cl.cap_c && L <= cl.cap_l && T <= cl.cap_t && has_na == cl.has_na && has_sv == cl.has_sv;
+  // the row range to write: new classes only, unless the label / taint sets changed (every row)
+  int64_t from = fits && L == cl.l && T == cl.t ? std::min<int64_t>(cl.c, C) : 0;
+  if (!fits) {
+    // (re)allocate at capacity: exact on the first load (batch runs), doubled on growth
+    const bool grow = cl.mirror != nullptr;
+    const int64_t cc = grow ? std::max<int64_t>(C, 2 * cl.cap_c) : C;
+    const int64_t cL = grow ? std::max<int64_t>(L, L > cl.cap_l ? 2 * cl.cap_l : cl.cap_l) : L;
+    const int64_t cT = grow ? std::max<int64_t>(T, T > cl.cap_t ? 2 * cl.cap_t : cl.cap_t) : T;
+    HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));  // (stops the resident kernel: new pointers)
+    for (void* q : h->class_bufs) dev_free(h, q);
+    h->class_bufs.clear();
+    if (cl.mirror) { (void)hipHostFree(cl.mirror); cl.mirror = nullptr; }
+    c.sel_ok = c.taint_ok = c.noexec_ok = c.svc_ok = nullptr;
+    c.tt_class = c.na_class = nullptr;
+    c.n_tt = c.n_na = nullptr;
+    c.tt_val = c.na_val = c.na_add = nullptr;
+    cl.cap_c = cc; cl.cap_l = cL; cl.cap_t = cT;
+    cl.has_na = has_na; cl.has_sv = has_sv;
+  }
+  const int64_t lwc = (cl.cap_l + 31) / 32, twc = (cl.cap_t + 31) / 32;
+  ClsArr arr[] = {
+      {t->sel_ok, 4, lw, lwc, (void**)&c.sel_ok, 0},      {t->taint_ok, 4, tw, twc, (void**)&c.taint_ok, 0},
+      {t->noexec_ok, 4, tw, twc, (void**)&c.noexec_ok, 0}, {t->tt_class, 1, T, cl.cap_t, (void**)&c.tt_class, 0},
+      {t->na_class, 1, L, cl.cap_l, (void**)&c.na_class, 0}, {t->n_tt, 4, 1, 1, (void**)&c.n_tt, 0},
+      {t->n_na, 4, 1, 1, (void**)&c.n_na, 0},              {t->tt_val, 8, KSIM_MAX_RCLASS, KSIM_MAX_RCLASS, (void**)&c.tt_val, 0},
+      {t->na_val, 8, KSIM_MAX_RCLASS, KSIM_MAX_RCLASS, (void**)&c.na_val, 0},
+      {t->na_add, 8, KSIM_MAX_RCLASS, KSIM_MAX_RCLASS, (void**)&c.na_add, 0},
+      {t->svc_ok, 4, lw, lwc, (void**)&c.svc_ok, 0}};
+  const int n_arr = 9 + (has_na ? 1 : 0) + (has_sv ? 1 : 0);
+  if (!has_na) arr[9] = arr[10];  // (the optional arrays compacted to the end)
+  int64_t mb = 0;
+  for (int k = 0; k < n_arr; ++k) {
+    arr[k].mirror = mb;
+    mb += (cl.cap_c * arr[k].stride * arr[k].esz + 255) / 256 * 256;
+  }
+  if (!cl.mirror) {
+    HIPCHK(h, hipHostMalloc((void**)&cl.mirror, (size_t)mb, hipHostMallocDefault));
+    memset(cl.mirror, 0, (size_t)mb);
+    const size_t nb0 = h->bufs.size();
+    for (int k = 0; k < n_arr; ++k) {
+      char* q = nullptr;
+      int rc = dev_alloc(h, &q, (size_t)(cl.cap_c * arr[k].stride * arr[k].esz));
+      if (rc) return rc;
+      *arr[k].dev = q;
+    }
+    for (size_t k = nb0; k < h->bufs.size(); ++k) h->class_bufs.push_back(h->bufs[k].p);
+  }
+  // "A superset" is not trusted row by row: the first row any array changes (callers rebuild their
+  // tables, and a placeholder row may be filled in later) moves `from` back
+  for (int k = 0; k < n_arr && from > 0; ++k) {
+    const ClsArr& x = arr[k];
+    const size_t rb = (size_t)(x.width * x.esz), sb = (size_t)(x.stride * x.esz);
+    const char* m = cl.mirror + x.mirror;
+    for (int64_t r = 0; r < from; ++r) {
+      const char* src = static_cast<const char*>(x.src) + (size_t)r * rb;
+      const bool same = x.src ? memcmp(m + (size_t)r * sb, src, rb) == 0
+                              : (x.esz == 4 && x.width == 1 ? memcmp(m + (size_t)r * sb, &one, 4) == 0 : true);
+      if (!same) { from = r; break; }
+    }
+  }
+  // rows [from, C) into the mirror at capacity strides, then to the device
+  for (int k = 0; k < n_arr; ++k) {
+    const ClsArr& x = arr[k];
+    char* m = cl.mirror + x.mirror;
+    const size_t rb = (size_t)(x.width * x.esz), sb = (size_t)(x.stride * x.esz);
+    for (int64_t r = from; r < C; ++r) {
+      char* d = m + (size_t)r * sb;
+      if (x.src) memcpy(d, static_cast<const char*>(x.src) + (size_t)r * rb, rb);
+      else if (x.esz == 4 && x.width == 1) memcpy(d, &one, 4);  // n_tt / n_na default 1
+      else memset(d, 0, rb);
+      if (sb > rb) memset(d + rb, 0, sb - rb);
+    }
+  }
+  // the resident per-pod kernel keeps running when the pointers stay: the rows go on a side stream
+  // (it reads no class row between messages) and its next message acquires them
+  const bool side = fits && h->serve_live.load();
+  if (side && !h->side_stream) HIPCHK(h, hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking));
+  hipStream_t st = side ? h->side_stream : ksim_stream(h);
+  if (C > from)
+    for (int k = 0; k < n_arr; ++k) {
+      const ClsArr& x = arr[k];
+      const size_t sb = (size_t)(x.stride * x.esz);
+      HIPCHK(h, hipMemcpyAsync(static_cast<char*>(*x.dev) + (size_t)from * sb, cl.mirror + x.mirror + (size_t)from * sb,
+                               (size_t)(C - from) * sb, hipMemcpyHostToDevice, st));
+    }
+  HIPCHK(h, hipStreamSynchronize(st));
+  if (side) h->serve_shared = true;  // (the next message acquires the new rows)
+  cl.c = C; cl.l = L; cl.t = T;
+  cl.loads += 1;
+  cl.in_place += side ? 1 : 0;
+  if (!has_na) c.na_add = nullptr;
+  if (!has_sv) c.svc_ok = nullptr;
+  c.use_na = (c.w[KSIM_W_NODE_AFFINITY] != 0 || has_na) ? 1 : 0;
+  // strides are the capacities (every kernel indexes [class * stride + column])
+  c.lwords = (int32_t)lwc; c.twords = (int32_t)twc;
+  c.n_label_sets = (int32_t)cl.cap_l; c.n_taint_sets = (int32_t)cl.cap_t;
+  c.n_classes_dev = (int32_t)C;
+  // the resident kernel reads no class count (only rows through the strides above, which stayed)
+  if (side) h->serve_base.n_classes_dev = c.n_classes_dev;
   h->n_classes = t->n_classes;
   h->n_label_sets = t->n_label_sets;
   h->n_taint_sets = t->n_taint_sets;
-  h->h_n_tt.assign(t->n_tt ? t->n_tt : ones.data(), (t->n_tt ? t->n_tt : ones.data()) + C);
-  h->h_n_na.assign(t->n_na ? t->n_na : ones.data(), (t->n_na ? t->n_na : ones.data()) + C);
+  const int32_t* ntt = t->n_tt, *nna = t->n_na;
+  h->h_n_tt.resize(C);
+  h->h_n_na.resize(C);
+  for (int64_t k = 0; k < C; ++k) {
+    h->h_n_tt[k] = ntt ? ntt[k] : 1;
+    h->h_n_na[k] = nna ? nna[k] : 1;
+  }
   h->any_wide = false;
-  for (size_t k = 0; k < C; ++k) h->any_wide |= wide_k(h, (int32_t)k);
+  for (int64_t k = 0; k < C; ++k) h->any_wide |= wide_k(h, (int32_t)k);
   // class pointers are baked into the launch graph's kernel arguments
-  if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
-  if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
+  if (!fits) {
+    if (h->gexec) { (void)hipGraphExecDestroy(h->gexec); h->gexec = nullptr; }
+    if (h->graph) { (void)hipGraphDestroy(h->graph); h->graph = nullptr; }
+  }
   if (h->have_classes) ksim_rt_recompute_fast(h);  // reduce-class counts decide fast-kernel eligibility
   if (h->n_pods) {  // and ride in the queued descriptors (ksim_persistent.hip's ring)
     hipError_t e = ksim_launch_pod_k(h->d_pods, h->n_pods, &c, ksim_stream(h));

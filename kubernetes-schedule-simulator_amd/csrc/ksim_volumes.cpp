@@ -133,7 +133,16 @@ static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
   V.vol_slots = t->vol_slots;
   V.zone_words = t->zone_words;
   put(o_V, &V, sizeof V);
-  HIPCHK(h, hipMemcpyAsync(base, hb.data(), off, hipMemcpyHostToDevice, ksim_stream(h)));
+  // a grow in place (same buffers, same mounts) beside a running resident per-pod kernel: on the
+  // side stream (the kernel reads no volume table between messages) and the next message acquires
+  const bool side = carry && !old_small && h->serve_live.load();
+  if (side && !h->side_stream) HIPCHK(h, hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking));
+  HIPCHK(h, hipMemcpyAsync(base, hb.data(), off, hipMemcpyHostToDevice, side ? h->side_stream : ksim_stream(h)));
+  if (side) {
+    HIPCHK(h, hipStreamSynchronize(h->side_stream));
+    h->serve_shared = true;
+    h->vol_in_place += 1;
+  }
   KsimVol* dev = reinterpret_cast<KsimVol*>(base);
   std::vector<void*> fresh;  // this load's mount buffers (taken before any free shifts h->bufs)
   for (size_t k = nb0; k < h->bufs.size(); ++k) fresh.push_back(h->bufs[k].p);

@@ -11,10 +11,14 @@
  *   2. the final device node state equals the host copy column by column.
  * Exit status 0 = pass; prints one summary line.  Needs a GPU (run by tests/test_c_abi.py).
  *
- *   ksim_c_loop <nodes> <steps> [gap_ms gap_every]
+ *   ksim_c_loop <nodes> <steps> [gap_ms gap_every [adapter]]
  * gap_ms / gap_every: sleep gap_ms before every gap_every-th step of the event loop (a scheduler
  * whose pods arrive sporadically: the resident per-pod kernel leaves by its idle vote and is
  * relaunched, or a message meets a grid on its way out).
+ * adapter = 1: every Schedule is the cgo adapter's pattern — KSIM_SCHEDULE_ONLY, then (8 in 10)
+ * ksim_pod_add onto the chosen node (Scheduler.assume), (1 in 10) onto another node (the binding
+ * landed elsewhere), or (1 in 10) nothing (the pod is dropped) — so the resident kernel's
+ * tentative commits are confirmed, undone by a different assume, or undone by the next event.
  *
  * Build: tests/c/Makefile (gcc, links libksim.so and the oracle's libksim_ref.so).
  */
@@ -294,7 +298,7 @@ static void batch_parity(int n0, unsigned npods) {
 }
 
 /* ---- 2. scheduleOne loop with cache events vs the oracle ---- */
-static int gap_ms = 0, gap_every = 0;
+static int gap_ms = 0, gap_every = 0, adapter = 0;
 
 static void event_loop(int steps) {
   ksim_class_tables ct = one_class();
@@ -315,7 +319,41 @@ static void event_loop(int steps) {
       nanosleep(&ts, NULL);
     }
     const uint64_t r = rnd() % 100;
-    if (r < 70 || n_nodes == 0) {  /* Schedule + assume */
+    if ((r < 70 || n_nodes == 0) && adapter) {  /* Schedule (decide only), then the adapter's assume */
+      uint64_t port;
+      ksim_pod p = rnd_pod(&port);
+      ksim_result res;
+      int rc = ksim_schedule_one(h, &p, &port, p.port_cnt, NULL, 0, KSIM_SCHEDULE_ONLY, &res);
+      if (n_nodes == 0) {
+        CHECK(rc == KSIM_E_NO_NODES, "empty table: %d", rc);
+        continue;
+      }
+      KS(h, rc);
+      ksim_node_state st;
+      to_soa(&t, &st, HP);
+      int32_t want = -2, reasons[KSIM_NREASONS];
+      CHECK(ksim_ref_run(&cfg, &t, &st, &ct, &p, &port, NULL, 0, 1, 1, &want, reasons, &counter) == KSIM_OK, "oracle");
+      /* (no from_soa: the oracle's commit is not the cache's until the assume below) */
+      ++n_sched;
+      CHECK(res.node == want, "step %d: node %d, oracle %d", step, res.node, want);
+      CHECK(res.last_node_index == counter, "step %d: lastNodeIndex %llu, oracle %llu", step,
+            (unsigned long long)res.last_node_index, (unsigned long long)counter);
+      if (want < 0) {
+        ++n_fit_err;
+        CHECK(memcmp(res.reasons, reasons, sizeof reasons) == 0, "step %d: FitError histogram differs", step);
+        continue;
+      }
+      const uint64_t u = rnd() % 10;
+      const int64_t w = u < 8 ? want : (u < 9 ? (int64_t)(rnd() % (uint64_t)n_nodes) : -1);
+      if (w >= 0) {
+        KS(h, ksim_pod_add(h, w, &p, &port, p.port_cnt, NULL, 0));
+        host_add(&nodes[w], &p, port);
+        placed[np].pod = p; placed[np].port = port;
+        strcpy(placed[np].node, nodes[w].name);
+        ++np;
+        ++n_add;
+      }
+    } else if (r < 70 || n_nodes == 0) {  /* Schedule + assume */
       uint64_t port;
       ksim_pod p = rnd_pod(&port);
       ksim_result res;
@@ -426,6 +464,7 @@ int main(int argc, char** argv) {
     gap_ms = atoi(argv[3]);
     gap_every = atoi(argv[4]);
   }
+  if (argc > 5) adapter = atoi(argv[5]);
   if (ksim_abi_version() != KSIM_ABI_VERSION) {
     fprintf(stderr, "FAIL: ABI %d vs header %d\n", ksim_abi_version(), KSIM_ABI_VERSION);
     return 1;

@@ -47,13 +47,15 @@ PER_POD_FORMS = {
 
 def _serve_stats(stderr):
     """Sum of the '[ksim serve]' lines (one per handle that launched the resident kernel)."""
-    keys = ("launches", "messages", "stops", "left-idle", "untaken-relaunches")
-    tot = dict.fromkeys(keys, 0)
+    keys = {"[ksim serve]": ("launches", "messages", "stops", "left-idle", "untaken-relaunches"),
+            "[ksim tentative]": ("commits", "undone", "by-launch", "confirmed")}
+    tot = {k: 0 for ks in keys.values() for k in ks}
     for line in stderr.splitlines():
-        if line.startswith("[ksim serve]"):
-            w = line.split()
-            for k in keys:
-                tot[k] += int(w[w.index(k) + 1])
+        for head, ks in keys.items():
+            if line.startswith(head):
+                w = line.split()
+                for k in ks:
+                    tot[k] += int(w[w.index(k) + 1])
     return tot
 
 
@@ -77,6 +79,18 @@ def test_c_schedule_one_loop(form):
         assert st["messages"] > 1000, st
     if form == "resident_idle0":
         assert st["left-idle"] > 0, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("form", ["resident", "resident_idle0", "pick_launch"])
+def test_c_schedule_one_loop_adapter_pattern(form):
+    """The cgo adapter's pattern (SCHEDULE_ONLY, then ksim_pod_add onto the chosen node, another
+    node, or none) through the same event loop: the resident kernel's tentative commits confirmed
+    by the matching assume, undone by a different one or by the next event — every decision,
+    lastNodeIndex and the final device state against the oracle."""
+    st = _run([BIN, "300", "3000", "0", "0", "1"], PER_POD_FORMS[form])
+    if form.startswith("resident"):
+        assert st["commits"] > 500 and st["confirmed"] > 300 and st["undone"] > 50, st
 
 
 @pytest.mark.gpu

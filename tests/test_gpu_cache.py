@@ -15,7 +15,26 @@ from ksim.cache import SchedulerCache
 from ksim.frontend import K8sCache
 
 pytestmark = pytest.mark.gpu
-IMPLS = {"py": SchedulerCache, "cpp": K8sCache}
+
+
+class K8sCacheAdapter(K8sCache):
+    """The C++ cache driven the way the cgo adapter in INTEGRATION.md drives it (Scheduler.scheduleOne,
+    scheduler.go:431-484): Schedule with SCHEDULE_ONLY, then AssumePod of the pod with its nodeName
+    set — on the resident kernel the Schedule commits tentatively and the matching AssumePod confirms
+    it without a message; anything else in between undoes it."""
+
+    def schedule_one(self, pod):
+        from ksim.cache import FitError
+        try:
+            host = self.schedule(pod, assume=False)
+        except FitError as e:
+            return None, str(e)
+        q = dict(pod, spec=dict(pod["spec"], nodeName=host))
+        self.assume_pod(q)
+        return host, None
+
+
+IMPLS = {"py": SchedulerCache, "cpp": K8sCache, "adapter": K8sCacheAdapter}
 
 
 @pytest.fixture(autouse=True, params=["one_wg", "scan"])
