@@ -25,7 +25,7 @@
 extern "C" {
 #endif
 
-#define KSIM_ABI_VERSION 6
+#define KSIM_ABI_VERSION 7
 
 /* ---- status codes ---- */
 #define KSIM_OK 0
@@ -38,8 +38,9 @@ extern "C" {
 #define KSIM_E_NO_NODES (-7)    /* core.ErrNoNodesAvailable (generic_scheduler.go:64,124-125) */
 
 #define KSIM_MAX_SCALAR 8   /* extended / hugepage resource columns */
-#define KSIM_MAX_RCLASS 16  /* TaintToleration / NodeAffinity values per pod class (each dimension); a
-                               product above 16 takes the launch form's wide decision */
+#define KSIM_MAX_RCLASS 16  /* TaintToleration / NodeAffinity values per pod class (each dimension) in the
+                               default value rows; a product above 16 takes the launch form's wide
+                               decision, and ksim_class_tables.val_width widens the rows (ABI 7) */
 #define KSIM_MAX_WIDE 256   /* reduce classes per pod (TaintToleration x NodeAffinity) */
 #define KSIM_NREASONS 32    /* failure-reason histogram slots */
 #define KSIM_MAX_RANKS 8    /* devices of one node-sharded cluster */
@@ -203,9 +204,10 @@ typedef struct {
   const uint8_t* tt_class;     /* reduce class of each taint set (intolerable PreferNoSchedule count) */
   const uint8_t* na_class;     /* reduce class of each label set (preferred node-affinity weight) */
   const int32_t* n_tt;         /* [n_classes] number of TaintToleration classes K1 */
-  const int32_t* n_na;         /* [n_classes] number of NodeAffinity classes K2 (K1*K2 <= 16) */
-  const int64_t* tt_val;       /* [n_classes][KSIM_MAX_RCLASS] map value of each class */
-  const int64_t* na_val;       /* [n_classes][KSIM_MAX_RCLASS] */
+  const int32_t* n_na;         /* [n_classes] number of NodeAffinity classes K2 (each <= the value row
+                                  width, K1*K2 <= KSIM_MAX_WIDE; above 16 the launch form decides) */
+  const int64_t* tt_val;       /* [n_classes][width] map value of each class (width: val_width) */
+  const int64_t* na_val;       /* [n_classes][width] */
   /* Optional (NULL = none): a weighted constant added to the total of every node of NodeAffinity
    * class b, [n_classes][KSIM_MAX_RCLASS] — NodePreferAvoidPodsPriority's map score x weight
    * (node_prefer_avoid_pods.go:32-68), which is a function of (pod class, label set) like the
@@ -216,6 +218,11 @@ typedef struct {
    * [n_classes][words] like sel_ok — the pod's nodeSelector values of the predicate's labels must
    * be the node's (FindLabelsInSet, CreateSelectorFromLabels; no service selects the pod). */
   const uint32_t* svc_ok;
+  /* The row width of tt_val / na_val / na_add (0 = KSIM_MAX_RCLASS; at most KSIM_MAX_WIDE): a pod
+   * class with more than 16 TaintToleration or NodeAffinity values (NormalizeReduce has no such
+   * limit, reduce.go:29-64) needs rows as wide as its larger dimension. */
+  int32_t val_width;
+  int32_t reserved0;
 } ksim_class_tables;
 
 /* Pod descriptor, 128 bytes.  The three request vectors follow the reference exactly:

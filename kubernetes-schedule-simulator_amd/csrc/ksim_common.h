@@ -172,6 +172,7 @@ struct KsimCtx {
   const uint32_t* __restrict__ svc_ok; // [C][lwords] CheckServiceAffinity per label set, or null
   int32_t use_na;                      // NA class dimension in use: NodeAffinity weight or na_add
   int32_t lwords, twords, n_label_sets, n_taint_sets;
+  int32_t val_w;          // row width of tt_val / na_val / na_add (ksim_class_tables.val_width, >= 16)
   int32_t n_classes_dev;  // pod classes in the tables
   int32_t fuse_a;         // launch form: pass A fused into the scan (grid barrier; co-resident grid)
   uint64_t barrier_ticks; // fused pass A: bound of the grid-barrier wait (s_memrealtime ticks, 100 MHz)

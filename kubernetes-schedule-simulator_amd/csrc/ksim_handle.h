@@ -107,6 +107,7 @@ struct ksim_handle {
   struct {
     int64_t cap_c = 0, cap_l = 0, cap_t = 0;  // capacities (the device strides)
     int64_t c = 0, l = 0, t = 0;              // loaded
+    int64_t w = 0;                            // value row width (ksim_class_tables.val_width)
     bool has_na = false, has_sv = false;
     char* mirror = nullptr;
     int64_t loads = 0, in_place = 0;          // reloads, and those written beside a running resident kernel

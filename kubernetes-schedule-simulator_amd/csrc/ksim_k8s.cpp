@@ -506,7 +506,7 @@ extern "C" int64_t ksim_k8s_class_value(const ksim_k8s_cluster* c, int32_t kind,
     case 0: return set < t.L ? (t.sel_ok[(size_t)cls * t.lw + (set >> 5)] >> (set & 31)) & 1u : -1;
     case 1: return set < t.T ? (t.taint_ok[(size_t)cls * t.tw + (set >> 5)] >> (set & 31)) & 1u : -1;
     case 2: return set < t.T ? (t.noexec_ok[(size_t)cls * t.tw + (set >> 5)] >> (set & 31)) & 1u : -1;
-    case 3: return set < t.T ? t.tt_val[(size_t)cls * KSIM_MAX_RCLASS + t.tt_class[(size_t)cls * t.T + set]] : -1;
+    case 3: return set < t.T ? t.tt_val[(size_t)cls * t.val_w + t.tt_class[(size_t)cls * t.T + set]] : -1;
     case 4: return set < t.L ? t.na_w[(size_t)cls * t.L + set] : -1;
     case 5: return set < t.L ? t.im_s[(size_t)cls * t.L + set] : -1;
     default: return -1;
@@ -704,6 +704,7 @@ extern "C" int ksim_k8s_tables(ksim_k8s_cluster* c, ksim_node_table* nodes, ksim
     t.sel_ok = x.sel_ok.data(); t.taint_ok = x.taint_ok.data(); t.noexec_ok = x.noexec_ok.data();
     t.tt_class = x.tt_class.data(); t.na_class = x.na_class.data(); t.n_tt = x.n_tt.data(); t.n_na = x.n_na.data();
     t.tt_val = x.tt_val.data(); t.na_val = x.na_val.data();
+    t.val_width = x.val_w;
   }
   if (aff) {
     *aff = ksim_affinity_tables{};

@@ -1108,6 +1108,7 @@ struct Interns {
 // ImageLocality map scores) — ingest.build_class_tables.
 struct ClassTab {
   int32_t Cn = 0, L = 0, T = 0, lw = 0, tw = 0;
+  int32_t val_w = KSIM_MAX_RCLASS;  // row width of tt_val / na_val (ksim_class_tables.val_width)
   std::vector<uint32_t> sel_ok, taint_ok, noexec_ok;
   std::vector<uint8_t> tt_class, na_class;
   std::vector<int32_t> n_tt, n_na;
@@ -1129,8 +1130,6 @@ void build_class_tab(const Interns& in, ClassTab* c) {
   c->na_class.assign((size_t)Cn * L, 0);
   c->n_tt.assign(Cn, 1);
   c->n_na.assign(Cn, 1);
-  c->tt_val.assign((size_t)Cn * KSIM_MAX_RCLASS, 0);
-  c->na_val.assign((size_t)Cn * KSIM_MAX_RCLASS, 0);
   c->na_w.assign((size_t)Cn * L, 0);
   c->na_p.assign((size_t)Cn * L, 10);
   c->im_s.assign((size_t)Cn * L, 0);
@@ -1138,6 +1137,7 @@ void build_class_tab(const Interns& in, ClassTab* c) {
   c->bad_classes.clear();
   c->pa_split = false;
   c->im_any = false;
+  std::vector<std::vector<int64_t>> tvs(Cn), avs(Cn);  // per class: its distinct values (rows written below)
   for (int32_t k = 0; k < Cn; ++k) {
     const bool real = k < (int32_t)in.classes.items.size();
     const PodObj spec = real ? class_pod(in.classes.items[k]) : PodObj{};
@@ -1189,13 +1189,12 @@ void build_class_tab(const Interns& in, ClassTab* c) {
     std::sort(av.begin(), av.end()); av.erase(std::unique(av.begin(), av.end()), av.end());
     if (tv.empty()) tv.push_back(0);  // an empty taint-set list still has one class
     if (av.empty()) av.push_back(0);
-    if (tv.size() > KSIM_MAX_RCLASS || av.size() > KSIM_MAX_RCLASS)  // (a product above 16: the wide decision)
-      fail(KSIM_E_UNSUPPORTED, "pod class needs %zu x %zu reduce classes (> %d per dimension)", tv.size(), av.size(),
-           KSIM_MAX_RCLASS);
+    // NormalizeReduce takes any number of values (reduce.go:29-64); the reduce classes of one pod
+    // are bounded by the launch form's wide decision (a product above 16 decides there)
+    if (tv.size() * av.size() > KSIM_MAX_WIDE)
+      fail(KSIM_E_UNSUPPORTED, "pod class needs %zu x %zu reduce classes (> %d)", tv.size(), av.size(), KSIM_MAX_WIDE);
     c->n_tt[k] = (int32_t)tv.size();
     c->n_na[k] = (int32_t)av.size();
-    for (size_t q = 0; q < tv.size(); ++q) c->tt_val[(size_t)k * KSIM_MAX_RCLASS + q] = tv[q];
-    for (size_t q = 0; q < av.size(); ++q) c->na_val[(size_t)k * KSIM_MAX_RCLASS + q] = av[q];
     for (int32_t ti = 0; ti < T; ++ti)
       c->tt_class[(size_t)k * T + ti] = (uint8_t)(std::lower_bound(tv.begin(), tv.end(), counts[ti]) - tv.begin());
     for (int32_t li = 0; li < L; ++li) {
@@ -1205,6 +1204,17 @@ void build_class_tab(const Interns& in, ClassTab* c) {
     }
     for (int32_t li = 1; li < L; ++li) c->pa_split |= pas[li] != pas[0];
     c->need[k] = (all_sel ? 0u : KSIM_POD_NEED_SELECTOR) | (all_taint ? 0u : KSIM_POD_NEED_TAINTS);
+    tvs[k] = std::move(tv);
+    avs[k] = std::move(av);
+  }
+  int32_t W = KSIM_MAX_RCLASS;
+  for (int32_t k = 0; k < Cn; ++k) W = std::max<int32_t>(W, (int32_t)std::max(tvs[k].size(), avs[k].size()));
+  c->val_w = W;
+  c->tt_val.assign((size_t)Cn * W, 0);
+  c->na_val.assign((size_t)Cn * W, 0);
+  for (int32_t k = 0; k < Cn; ++k) {
+    for (size_t q = 0; q < tvs[k].size(); ++q) c->tt_val[(size_t)k * W + q] = tvs[k][q];
+    for (size_t q = 0; q < avs[k].size(); ++q) c->na_val[(size_t)k * W + q] = avs[k][q];
   }
 }
 
@@ -1267,9 +1277,10 @@ void policy_svc_ok(const Interns& in, const ClassTab& ct, const PolicyArgs& a, s
 // per-class addends when the policy weighs them and they tell some class's nodes apart — the
 // NodeAffinity class dimension re-keyed by (preferred weight, summed addend).  Returns whether the
 // addends apply; *pa_on: NodePreferAvoidPods rides them (its constant leaves const_score).
+// *val_w: the row width of nav / add (the class table's, or wider when an addend splits more classes).
 bool class_addends(const ClassTab& c, int64_t w_pa, int64_t w_im, bool use_w, std::vector<uint8_t>* nac,
                    std::vector<int32_t>* nna, std::vector<int64_t>* nav, std::vector<int64_t>* add, bool* pa_on_out,
-                   const std::vector<int64_t>* lab_add = nullptr) {
+                   const std::vector<int64_t>* lab_add = nullptr, int32_t* val_w = nullptr) {
   const bool pa_on = w_pa && c.pa_split, im_on = w_im && c.im_any;
   bool lab_on = false;  // a Policy's label priorities (per label set, weighted)
   if (lab_add)
@@ -1279,8 +1290,7 @@ bool class_addends(const ClassTab& c, int64_t w_pa, int64_t w_im, bool use_w, st
   const int32_t Cn = c.Cn, L = c.L;
   nac->assign((size_t)Cn * L, 0);
   nna->assign(Cn, 1);
-  nav->assign((size_t)Cn * KSIM_MAX_RCLASS, 0);
-  add->assign((size_t)Cn * KSIM_MAX_RCLASS, 0);
+  std::vector<std::vector<std::pair<int64_t, int64_t>>> avs(Cn);
   for (int32_t k = 0; k < Cn; ++k) {
     std::vector<std::pair<int64_t, int64_t>> keys;
     for (int32_t li = 0; li < L; ++li) {
@@ -1291,18 +1301,32 @@ bool class_addends(const ClassTab& c, int64_t w_pa, int64_t w_im, bool use_w, st
     std::vector<std::pair<int64_t, int64_t>> av(keys);
     std::sort(av.begin(), av.end());
     av.erase(std::unique(av.begin(), av.end()), av.end());
-    if (av.size() > KSIM_MAX_RCLASS)
-      fail(KSIM_E_UNSUPPORTED, "pod class needs %d x %zu reduce classes (> %d per dimension)", c.n_tt[k], av.size(),
-           KSIM_MAX_RCLASS);
+    if ((size_t)c.n_tt[k] * av.size() > KSIM_MAX_WIDE)
+      fail(KSIM_E_UNSUPPORTED, "pod class needs %d x %zu reduce classes (> %d)", c.n_tt[k], av.size(), KSIM_MAX_WIDE);
     (*nna)[k] = (int32_t)av.size();
-    for (size_t q = 0; q < av.size(); ++q) {
-      (*nav)[(size_t)k * KSIM_MAX_RCLASS + q] = av[q].first;
-      (*add)[(size_t)k * KSIM_MAX_RCLASS + q] = av[q].second;
-    }
     for (int32_t li = 0; li < L; ++li)
       (*nac)[(size_t)k * L + li] = (uint8_t)(std::lower_bound(av.begin(), av.end(), keys[li]) - av.begin());
+    avs[k] = std::move(av);
   }
+  int32_t W = c.val_w;
+  for (int32_t k = 0; k < Cn; ++k) W = std::max<int32_t>(W, (int32_t)avs[k].size());
+  nav->assign((size_t)Cn * W, 0);
+  add->assign((size_t)Cn * W, 0);
+  for (int32_t k = 0; k < Cn; ++k)
+    for (size_t q = 0; q < avs[k].size(); ++q) {
+      (*nav)[(size_t)k * W + q] = avs[k][q].first;
+      (*add)[(size_t)k * W + q] = avs[k][q].second;
+    }
+  if (val_w) *val_w = W;
   return true;
+}
+
+// tt_val rows of width c.val_w re-laid out at width w (>= c.val_w).
+std::vector<int64_t> widen_rows(const std::vector<int64_t>& v, int32_t Cn, int32_t from, int32_t w) {
+  std::vector<int64_t> o((size_t)Cn * w, 0);
+  for (int32_t k = 0; k < Cn; ++k)
+    for (int32_t q = 0; q < from; ++q) o[(size_t)k * w + q] = v[(size_t)k * from + q];
+  return o;
 }
 
 // ksim_load_classes over a ClassTab (with the addends of class_addends when they apply).
@@ -1311,8 +1335,12 @@ int load_class_tab(const ClassTab& c, ksim_handle* h, int64_t w_pa, int64_t w_im
   std::vector<uint8_t> nac;
   std::vector<int32_t> nna;
   std::vector<int64_t> nav, add;
-  const bool pa = class_addends(c, w_pa, w_im, use_w, &nac, &nna, &nav, &add, nullptr, lab_add);
+  int32_t W = c.val_w;
+  const bool pa = class_addends(c, w_pa, w_im, use_w, &nac, &nna, &nav, &add, nullptr, lab_add, &W);
+  // one row width for every value array (the addends may have split more NodeAffinity classes)
+  const std::vector<int64_t> ttw = W > c.val_w ? widen_rows(c.tt_val, c.Cn, c.val_w, W) : std::vector<int64_t>();
   ksim_class_tables t{};
+  t.val_width = W;
   t.n_classes = c.Cn;
   t.n_label_sets = c.L;
   t.n_taint_sets = c.T;
@@ -1323,7 +1351,7 @@ int load_class_tab(const ClassTab& c, ksim_handle* h, int64_t w_pa, int64_t w_im
   t.na_class = pa ? nac.data() : c.na_class.data();
   t.n_tt = c.n_tt.data();
   t.n_na = pa ? nna.data() : c.n_na.data();
-  t.tt_val = c.tt_val.data();
+  t.tt_val = W > c.val_w ? ttw.data() : c.tt_val.data();
   t.na_val = pa ? nav.data() : c.na_val.data();
   t.na_add = pa ? add.data() : nullptr;
   t.svc_ok = svc_ok;

@@ -143,6 +143,53 @@ __device__ __forceinline__ void eval_one(const KsimCtx& c, const ksim_pod& P, in
   cls = (k1 * k2 > 1) ? ksim_rclass(c, P, i, k1, k2) : 0;
 }
 
+// The resident per-pod kernel's rows between messages: each thread keeps the 60-byte rows of the
+// nodes it evaluates (and their label / taint set ids) in registers for the kernel's lifetime — the
+// block that owns a node is the only one that reads or commits it, and the committing block reloads
+// the row after each commit — so an evaluation starts without a dependent load chain.
+template <int NPT>
+struct KsimRowCache {
+  KsimRow r[NPT];
+  int32_t ls[NPT], ts[NPT];
+};
+
+// The pod class's table entries for one node, loaded together up front (the ids are in registers):
+// one round trip instead of a set id load followed by a table load per predicate.
+struct KsimPrefAcc {
+  const KsimCtx& c;
+  bool sel, tok, nok;
+  int ttc, nac;
+  __device__ __forceinline__ bool sel_ok(const ksim_pod&, int64_t) const { return sel; }
+  __device__ __forceinline__ bool taint_ok(const ksim_pod&, int64_t) const { return tok; }
+  __device__ __forceinline__ bool noexec_ok(const ksim_pod&, int64_t) const { return nok; }
+  __device__ __forceinline__ bool port_conflict(int64_t i, uint64_t want) const { return ksim_port_conflict(c, i, want); }
+  __device__ __forceinline__ uint64_t want(const ksim_pod& P, int32_t k) const { return ksim_pod_port(c, P, k); }
+  __device__ __forceinline__ int tt_class(const ksim_pod&, int64_t) const { return ttc; }
+  __device__ __forceinline__ int na_class(const ksim_pod&, int64_t) const { return nac; }
+};
+
+// eval_one over a cached row (the resident kernel): the same predicates, priorities and classes.
+template <bool COLLECT>
+__device__ __forceinline__ void eval_cached(const KsimCtx& c, const ksim_pod& P, int64_t i, const KsimRow& r, int32_t ls,
+                                            int32_t ts, int k1, int k2, bool& fit, int64_t& score, int& cls, uint32_t& rmask) {
+  fit = false; score = 0; cls = 0; rmask = 0;
+  if (i >= c.n) return;
+  KsimPrefAcc a{c, true, true, true, 0, 0};
+  const int64_t cl = P.cls;
+  if (P.flags & KSIM_POD_NEED_SELECTOR) a.sel = ksim_bit(c.sel_ok, cl, c.lwords, ls);
+  if (P.flags & KSIM_POD_NEED_TAINTS) {
+    a.tok = ksim_bit(c.taint_ok, cl, c.twords, ts);
+    a.nok = ksim_bit(c.noexec_ok, cl, c.twords, ts);
+  }
+  if (k1 > 1) a.ttc = c.tt_class[cl * c.n_taint_sets + ts];
+  if (k2 > 1) a.nac = c.na_class[cl * c.n_label_sets + ls];
+  const uint32_t m = ksim_predicates_a<KsimPrefAcc, true, true>(c, P, i, r, a);
+  fit = (m == 0);
+  if (COLLECT) rmask = m;
+  score = ksim_map_score(c, P, r);
+  cls = (k1 * k2 > 1) ? ksim_rclass_a(P, i, k1, k2, a) : 0;
+}
+
 // Pass A of an InterPodAffinityPriority / SelectorSpread pod, over the fit nodes: min / max of the
 // raw InterPodAffinity sums with 0 folded in as the reference's accumulators start there
 // (interpod_affinity.go:129-131, 218-226); SelectorSpread's maxCountByNodeName, haveZones and
@@ -530,9 +577,9 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_scan_kernel(KsimCtx c) {
   int64_t pre_tv = 0, pre_av = 0, pre_ad = 0;
   if (tid == 0) pre_ctr = *c.counter;
   if (tid < K) {
-    pre_tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid / k2];
-    pre_av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2];
-    pre_ad = c.na_add ? c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2] : 0;
+    pre_tv = c.tt_val[(int64_t)P.cls * c.val_w + tid / k2];
+    pre_av = c.na_val[(int64_t)P.cls * c.val_w + tid % k2];
+    pre_ad = c.na_add ? c.na_add[(int64_t)P.cls * c.val_w + tid % k2] : 0;
   }
   const int64_t base = (int64_t)blockIdx.x * c.chunk;
   IpaNorm ipa = ipa_norm(c, P);
@@ -1206,9 +1253,9 @@ __global__ __launch_bounds__(ONE_BLOCK) void ksim_one_kernel(KsimCtx c) {
   int64_t pre_tv = 0, pre_av = 0, pre_ad = 0;
   if (tid == 0) pre_ctr = *c.counter;
   if (tid < K) {
-    pre_tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid / k2];
-    pre_av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2];
-    pre_ad = c.na_add ? c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2] : 0;
+    pre_tv = c.tt_val[(int64_t)P.cls * c.val_w + tid / k2];
+    pre_av = c.na_val[(int64_t)P.cls * c.val_w + tid % k2];
+    pre_ad = c.na_add ? c.na_add[(int64_t)P.cls * c.val_w + tid % k2] : 0;
   }
   IpaNorm ipa = ipa_norm(c, P);  // which of pass A's priorities the pod reads (maxima below)
   IpaNorm ipa0 = ipa;
@@ -1526,6 +1573,17 @@ __device__ __forceinline__ void pk_answer(uint64_t* ans, uint64_t seq, int lane,
 static_assert(KSIM_RES_WORDS <= 64, "one answer word per lane");
 }  // namespace
 
+// The thread that caches row `node` (if this block holds it) reloads it after a commit / undo.
+template <int NPT>
+__device__ __forceinline__ void ksim_row_cache_reload(const KsimCtx& c, KsimRowCache<NPT>& rc, int64_t base, int64_t node) {
+  const int64_t j = node - base;
+  if (j < 0 || j >= (int64_t)NPT * KSIM_BLOCK || (int)(j % KSIM_BLOCK) != (int)threadIdx.x) return;
+  const int kk = (int)(j / KSIM_BLOCK);
+#pragma unroll
+  for (int k = 0; k < NPT; ++k)
+    if (k == kk) rc.r[k] = ksim_load_row(c, node);
+}
+
 // One pod of the pick form.  rec: this pod's record buffer (tag parity, KSIM_PICK_WORDS words);
 // ctr_keep: the block's own copy of lastNodeIndex (resident form; null: read *c.counter);
 // ans / seq: the resident form's answer words and message number (null: a one-pod launch, which
@@ -1535,7 +1593,7 @@ template <int NPT>
 __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod& P, const int64_t pod, const uint32_t tag,
                                                const int32_t no_commit, uint64_t* const rec, uint64_t* ctr_keep,
                                                uint64_t* ans, const uint64_t seq, KsimTentRec* tent = nullptr,
-                                               uint64_t* stamp = nullptr) {
+                                               KsimRowCache<NPT>* rcache = nullptr, uint64_t* stamp = nullptr) {
 #ifdef KSIM_STAMPS
 #define PKST(k) do { if (stamp && threadIdx.x == 0) stamp[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
 #else
@@ -1567,9 +1625,9 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   // the decision's inputs, loaded while the nodes are evaluated
   int64_t pre_tv = 0, pre_av = 0, pre_ad = 0;
   if (tid < K) {
-    pre_tv = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid / k2];
-    pre_av = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2];
-    pre_ad = c.na_add ? c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + tid % k2] : 0;
+    pre_tv = c.tt_val[(int64_t)P.cls * c.val_w + tid / k2];
+    pre_av = c.na_val[(int64_t)P.cls * c.val_w + tid % k2];
+    pre_ad = c.na_add ? c.na_add[(int64_t)P.cls * c.val_w + tid % k2] : 0;
   }
   uint64_t pre_ctr = 0;
   if (tid == 0) pre_ctr = ctr_keep ? *ctr_keep : *c.counter;
@@ -1590,8 +1648,15 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   int64_t sc[NPT];
   int cl[NPT];
   uint32_t rm[NPT];
+  if (rcache) {  // (uniform) the resident kernel: rows from registers
 #pragma unroll
-  for (int k = 0; k < NPT; ++k) eval_one<true>(c, P, base + (int64_t)k * KSIM_BLOCK + tid, k1, k2, ipa0, fit[k], sc[k], cl[k], rm[k]);
+    for (int k = 0; k < NPT; ++k)
+      eval_cached<true>(c, P, base + (int64_t)k * KSIM_BLOCK + tid, rcache->r[k], rcache->ls[k], rcache->ts[k], k1, k2, fit[k],
+                        sc[k], cl[k], rm[k]);
+  } else {
+#pragma unroll
+    for (int k = 0; k < NPT; ++k) eval_one<true>(c, P, base + (int64_t)k * KSIM_BLOCK + tid, k1, k2, ipa0, fit[k], sc[k], cl[k], rm[k]);
+  }
 
   PKST(2);
   // the first spin that hits its bound: err bit 2 (a consistency error; the grid is co-resident)
@@ -2005,6 +2070,9 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
       pk_answer(ans, seq, lane, (int32_t)node, s_F, s_stat, __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                 s_ctr, tc ? (lane == 0 ? s_cnt0 : (int32_t)s_fl0) : 0, tc);
     }
+    // the committed row's register copy (after the answer: off the decision chain; the commit's
+    // stores are this workgroup's own, ordered by the barrier above)
+    if (rcache && node >= 0 && no_commit != 1) ksim_row_cache_reload<NPT>(c, *rcache, base, node);
   } else if (tid == 0) {
     if (mode == 2) *c.counter = s_ctr;  // (a one-pod launch: this block is the call's only writer)
     c.out_node[pod] = (int32_t)node;
@@ -2103,6 +2171,21 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
 #endif
   uint64_t* const pod_ports = const_cast<uint64_t*>(c.pod_ports) + (int64_t)me * KSIM_ONE_PORTS;
   ksim_scalar_req* const pod_scalars = const_cast<ksim_scalar_req*>(c.pod_scalars) + (int64_t)me * KSIM_MAX_SCALAR;
+  // this thread's rows for the kernel's lifetime (KsimRowCache)
+  const int64_t base = (int64_t)me * c.chunk;
+  KsimRowCache<NPT> rcache;
+#pragma unroll
+  for (int k = 0; k < NPT; ++k) {
+    const int64_t i = base + (int64_t)k * KSIM_BLOCK + tid;
+    if (i < c.n) {
+      rcache.r[k] = ksim_load_row(c, i);
+      rcache.ls[k] = c.label_set[i];
+      rcache.ts[k] = c.taint_set[i];
+    } else {
+      rcache.r[k] = KsimRow{};
+      rcache.ls[k] = rcache.ts[k] = 0;
+    }
+  }
   // A block takes the newest complete message, which may be past the next one: a message answered
   // by one block (an assume onto another block's node) does not wait for the others, so the host
   // can post the next before this block has looked.  It never skips one it must answer or publish
@@ -2218,20 +2301,23 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
     const int32_t type = s_type;
     // the host's decision on this block's tentative commit, before anything else reads the row
     if (s_got && s_tent.valid && s_msg[KSIM_SERVE_W_TENT_SEQ] == s_tent.seq && s_msg[KSIM_SERVE_W_TENT_ACT] != KSIM_TENT_NONE) {
+      const bool undo = s_msg[KSIM_SERVE_W_TENT_ACT] == KSIM_TENT_UNDO;
       if (tid == 0) {
-        if (s_msg[KSIM_SERVE_W_TENT_ACT] == KSIM_TENT_UNDO) {
+        if (undo) {
           ksim_undo_commit(c, s_tent);
           __hip_atomic_store(&box->undo_ack, (uint64_t)s_tent.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
-        s_tent.valid = 0;
       }
       __syncthreads();
+      if (undo) ksim_row_cache_reload<NPT>(c, rcache, base, s_tent.node);
+      __syncthreads();
+      if (tid == 0) s_tent.valid = 0;
     }
     if (type != KSIM_SERVE_EXIT) seq = s_seq;
     if (type == KSIM_SERVE_SCHEDULE) {
       const ksim_pod P = s_P;
       ksim_pick_body<NPT>(c, P, 0, s_tag, s_nc, c.pick + (s_tag & 1u) * KSIM_PICK_WORDS, &s_keep, box->ans, seq, &s_tent,
-                          stamp);
+                          &rcache, stamp);
     } else if (type == KSIM_SERVE_ASSUME) {
       // a resource delta onto a given node (ksim_pod_add): the block whose chunk holds it answers
       const int64_t node = s_node;
@@ -2248,6 +2334,9 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
         pk_answer(box->ans, seq, lane, (int32_t)node, 0, st, __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
                   s_keep, 0);
       }
+      // the committed row's register copy: wave 0's stores, then the thread that caches the row
+      __syncthreads();
+      ksim_row_cache_reload<NPT>(c, rcache, base, s_node);
     } else {
       break;  // an exit message, or the grid left by the idle vote
     }

@@ -148,8 +148,8 @@ struct PLayout {
   int32_t ps;          // port slots staged per row (0: ports read from HBM)
   int32_t tables;      // 1: sel_ok / taint_ok / noexec_ok / tt_class / na_class staged
   int32_t off_pc, off_pk, off_sel, off_tok, off_nok, off_ttc, off_nac;  // byte offsets in ksim_smem
-  int32_t off_ttv, off_nav;  // [C][KSIM_MAX_RCLASS] reduce-class map values (int64)
-  int32_t off_nad;           // [C][KSIM_MAX_RCLASS] NodePreferAvoidPods addends (int64), staged when present
+  int32_t off_ttv, off_nav;  // [C][val_w] reduce-class map values (int64)
+  int32_t off_nad;           // [C][val_w] NodePreferAvoidPods addends (int64), staged when present
   // [C][rows] uint16 per (pod class, owned row), built at launch from the class tables: bit 0 the
   // selector does not match, bit 1 / 2 a NoSchedule+NoExecute / NoExecute taint is not
   // tolerated, bits 4-7 / 8-11 the TaintToleration / NodeAffinity reduce class — one LDS load
@@ -385,7 +385,7 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
     }
     for (int32_t k = tid; k < C * c.n_taint_sets; k += BS) (ksim_smem + L.off_ttc)[k] = (char)c.tt_class[k];
     for (int32_t k = tid; k < C * c.n_label_sets; k += BS) (ksim_smem + L.off_nac)[k] = (char)c.na_class[k];
-    for (int32_t k = tid; k < C * KSIM_MAX_RCLASS; k += BS) {
+    for (int32_t k = tid; k < C * c.val_w; k += BS) {
       reinterpret_cast<int64_t*>(ksim_smem + L.off_ttv)[k] = c.tt_val[k];
       reinterpret_cast<int64_t*>(ksim_smem + L.off_nav)[k] = c.na_val[k];
       if (c.na_add) reinterpret_cast<int64_t*>(ksim_smem + L.off_nad)[k] = c.na_add[k];
@@ -830,11 +830,11 @@ __global__ __launch_bounds__(BS) void ksim_persistent_kernel(KsimCtx c, const Ks
       if (K > 1 && lane < K) {
         const int64_t* ttv = L.tables ? reinterpret_cast<const int64_t*>(ksim_smem + L.off_ttv) : c.tt_val;
         const int64_t* nav = L.tables ? reinterpret_cast<const int64_t*>(ksim_smem + L.off_nav) : c.na_val;
-        tv_l = ttv[(int64_t)P.cls * KSIM_MAX_RCLASS + lane / k2];
-        av_l = nav[(int64_t)P.cls * KSIM_MAX_RCLASS + lane % k2];
+        tv_l = ttv[(int64_t)P.cls * c.val_w + lane / k2];
+        av_l = nav[(int64_t)P.cls * c.val_w + lane % k2];
         if (c.na_add) {
           const int64_t* nad = L.tables ? reinterpret_cast<const int64_t*>(ksim_smem + L.off_nad) : c.na_add;
-          ad_l = nad[(int64_t)P.cls * KSIM_MAX_RCLASS + lane % k2];
+          ad_l = nad[(int64_t)P.cls * c.val_w + lane % k2];
         }
       }
       // ---------------- a. sweep: every speculative partial of pod + the owner's correction ----
@@ -1400,7 +1400,7 @@ static hipError_t launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint6
   // the pod-class tables, when they fit
   const size_t C = (size_t)c->n_classes_dev;
   const size_t tb = al(C * c->lwords * 4) + 2 * al(C * c->twords * 4) + al(C * c->n_taint_sets) + al(C * c->n_label_sets) +
-                    3 * al(C * KSIM_MAX_RCLASS * 8);
+                    3 * al(C * c->val_w * 8);
   if (C > 0 && off + tb <= lds_max) {
     L.tables = 1;
     L.off_sel = (int32_t)off; off += al(C * c->lwords * 4);
@@ -1408,9 +1408,9 @@ static hipError_t launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint6
     L.off_nok = (int32_t)off; off += al(C * c->twords * 4);
     L.off_ttc = (int32_t)off; off += al(C * c->n_taint_sets);
     L.off_nac = (int32_t)off; off += al(C * c->n_label_sets);
-    L.off_ttv = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
-    L.off_nav = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
-    L.off_nad = (int32_t)off; off += al(C * KSIM_MAX_RCLASS * 8);
+    L.off_ttv = (int32_t)off; off += al(C * c->val_w * 8);
+    L.off_nav = (int32_t)off; off += al(C * c->val_w * 8);
+    L.off_nad = (int32_t)off; off += al(C * c->val_w * 8);
     const size_t sb = al(C * (size_t)lds_rows * 2);
     if (off + sb <= lds_max && !getenv("KSIM_NO_STATIC_TABLE")) {
       L.off_st = (int32_t)off;

@@ -587,9 +587,9 @@ __global__ __launch_bounds__(64) void ksim_pgen_pack_kernel(KsimCtx c, PGenArgs 
     if (lane == 0) *reinterpret_cast<PgHdr*>(R + 128) = H;
     if (lane < KSIM_MAX_RCLASS) {
       int64_t* v = reinterpret_cast<int64_t*>(R + 192);
-      v[lane] = c.tt_val[(int64_t)P.cls * KSIM_MAX_RCLASS + lane];
-      v[KSIM_MAX_RCLASS + lane] = c.na_val[(int64_t)P.cls * KSIM_MAX_RCLASS + lane];
-      v[2 * KSIM_MAX_RCLASS + lane] = c.na_add ? c.na_add[(int64_t)P.cls * KSIM_MAX_RCLASS + lane] : 0;
+      v[lane] = c.tt_val[(int64_t)P.cls * c.val_w + lane];
+      v[KSIM_MAX_RCLASS + lane] = c.na_val[(int64_t)P.cls * c.val_w + lane];
+      v[2 * KSIM_MAX_RCLASS + lane] = c.na_add ? c.na_add[(int64_t)P.cls * c.val_w + lane] : 0;
     }
     for (int32_t x = lane; x < H.n_anti; x += 64) reinterpret_cast<int32_t*>(R + so[PGS_ANTI])[x] = g.id_anti[a0 + x];
     for (int32_t x = lane; x < H.n_prio; x += 64) reinterpret_cast<int32_t*>(R + so[PGS_PRIO])[x] = g.id_prio[p0 + x];

@@ -214,16 +214,24 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
     if (k >= t->n_classes) return ksim_fail(h, KSIM_E_INVAL, "ksim_load_classes: a queued pod uses class %d beyond the new tables", k);
   const int64_t C = t->n_classes, L = t->n_label_sets, T = t->n_taint_sets;
   const int64_t lw = (L + 31) / 32, tw = (T + 31) / 32;
+  // the value rows' width: 16, or wider for classes with more values in one reduce dimension
+  const int64_t W = t->val_width ? t->val_width : KSIM_MAX_RCLASS;
+  if (W < KSIM_MAX_RCLASS || W > KSIM_MAX_WIDE)
+    return ksim_fail(h, KSIM_E_INVAL, "ksim_load_classes: val_width %d outside [%d, %d]", t->val_width, KSIM_MAX_RCLASS,
+                     KSIM_MAX_WIDE);
   for (int64_t k = 0; k < C; ++k) {
     const int a = t->n_tt ? t->n_tt[k] : 1, b = t->n_na ? t->n_na[k] : 1;
-    if (a < 1 || b < 1 || a > KSIM_MAX_RCLASS || b > KSIM_MAX_RCLASS)
-      return ksim_fail(h, KSIM_E_UNSUPPORTED, "class %lld: %d x %d reduce classes exceed %d per dimension", (long long)k, a, b,
-                       KSIM_MAX_RCLASS);
+    if (a < 1 || b < 1 || a > W || b > W)
+      return ksim_fail(h, KSIM_E_INVAL, "class %lld: %d x %d reduce classes exceed the value rows (%lld)", (long long)k, a, b,
+                       (long long)W);
+    if ((int64_t)a * b > KSIM_MAX_WIDE)
+      return ksim_fail(h, KSIM_E_UNSUPPORTED, "class %lld: %d x %d reduce classes exceed %d", (long long)k, a, b, KSIM_MAX_WIDE);
   }
   KsimCtx& c = h->ctx;
   auto& cl = h->cls;
   const bool has_na = t->na_add != nullptr, has_sv = t->svc_ok != nullptr;
-  const bool fits = cl.mirror && C <= cl.cap_c && L <= cl.cap_l && T <= cl.cap_t && has_na == cl.has_na && has_sv == cl.has_sv;
+  const bool fits = cl.mirror && C <= cl.cap_c && L <= cl.cap_l && T <= cl.cap_t && has_na == cl.has_na && has_sv == cl.has_sv &&
+                    W == cl.w;
   // the row range to write: new classes only, unless the label / taint sets changed (every row)
   int64_t from = fits && L == cl.l && T == cl.t ? std::min<int64_t>(cl.c, C) : 0;
   if (!fits) {
@@ -241,6 +249,7 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
     c.n_tt = c.n_na = nullptr;
     c.tt_val = c.na_val = c.na_add = nullptr;
     cl.cap_c = cc; cl.cap_l = cL; cl.cap_t = cT;
+    cl.w = W;
     cl.has_na = has_na; cl.has_sv = has_sv;
   }
   const int64_t lwc = (cl.cap_l + 31) / 32, twc = (cl.cap_t + 31) / 32;
@@ -248,9 +257,9 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
       {t->sel_ok, 4, lw, lwc, (void**)&c.sel_ok, 0},      {t->taint_ok, 4, tw, twc, (void**)&c.taint_ok, 0},
       {t->noexec_ok, 4, tw, twc, (void**)&c.noexec_ok, 0}, {t->tt_class, 1, T, cl.cap_t, (void**)&c.tt_class, 0},
       {t->na_class, 1, L, cl.cap_l, (void**)&c.na_class, 0}, {t->n_tt, 4, 1, 1, (void**)&c.n_tt, 0},
-      {t->n_na, 4, 1, 1, (void**)&c.n_na, 0},              {t->tt_val, 8, KSIM_MAX_RCLASS, KSIM_MAX_RCLASS, (void**)&c.tt_val, 0},
-      {t->na_val, 8, KSIM_MAX_RCLASS, KSIM_MAX_RCLASS, (void**)&c.na_val, 0},
-      {t->na_add, 8, KSIM_MAX_RCLASS, KSIM_MAX_RCLASS, (void**)&c.na_add, 0},
+      {t->n_na, 4, 1, 1, (void**)&c.n_na, 0},              {t->tt_val, 8, W, W, (void**)&c.tt_val, 0},
+      {t->na_val, 8, W, W, (void**)&c.na_val, 0},
+      {t->na_add, 8, W, W, (void**)&c.na_add, 0},
       {t->svc_ok, 4, lw, lwc, (void**)&c.svc_ok, 0}};
   const int n_arr = 9 + (has_na ? 1 : 0) + (has_sv ? 1 : 0);
   if (!has_na) arr[9] = arr[10];  // (the optional arrays compacted to the end)
@@ -321,6 +330,7 @@ int ksim_load_classes(ksim_handle* h, const ksim_class_tables* t) {
   c.lwords = (int32_t)lwc; c.twords = (int32_t)twc;
   c.n_label_sets = (int32_t)cl.cap_l; c.n_taint_sets = (int32_t)cl.cap_t;
   c.n_classes_dev = (int32_t)C;
+  c.val_w = (int32_t)W;
   // the resident kernel reads no class count (only rows through the strides above, which stayed)
   if (side) h->serve_base.n_classes_dev = c.n_classes_dev;
   h->n_classes = t->n_classes;

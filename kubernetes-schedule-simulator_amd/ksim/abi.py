@@ -14,9 +14,10 @@ LIB_PATH = os.environ.get("KSIM_LIB") or os.path.join(PKG_DIR, "lib", "libksim.s
 
 KSIM_OK = 0
 E_INVAL, E_DEVICE, E_NOMEM, E_UNSUPPORTED, E_STATE, E_OVERFLOW, E_NO_NODES = -1, -2, -3, -4, -5, -6, -7
-ABI_VERSION = 6
+ABI_VERSION = 7
 MAX_SCALAR = 8
 MAX_RCLASS = 16
+MAX_WIDE = 256  # reduce classes per pod (KSIM_MAX_WIDE)
 NREASONS = 32
 
 # predicate bits
@@ -92,7 +93,7 @@ class ClassTables(C.Structure):
     _fields_ = [("n_classes", C.c_int32), ("n_label_sets", C.c_int32), ("n_taint_sets", C.c_int32),
                 ("sel_ok", _u32p), ("taint_ok", _u32p), ("noexec_ok", _u32p), ("tt_class", _u8p),
                 ("na_class", _u8p), ("n_tt", _i32p), ("n_na", _i32p), ("tt_val", _i64p), ("na_val", _i64p),
-                ("na_add", _i64p), ("svc_ok", _u32p)]
+                ("na_add", _i64p), ("svc_ok", _u32p), ("val_width", C.c_int32), ("reserved0", C.c_int32)]
 
 
 class Pod(C.Structure):

@@ -824,8 +824,7 @@ def build_class_tables(label_items, taint_items, specs):
     nac = np.zeros((Cn, L), np.uint8)
     ntt = np.ones(Cn, np.int32)
     nna = np.ones(Cn, np.int32)
-    ttv = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
-    nav = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
+    tvs, avs = [], []  # per class: its distinct TaintToleration / NodeAffinity values
     na_w = np.zeros((Cn, L), np.int64)   # preferred node-affinity weight per (class, label set)
     na_p = np.full((Cn, L), 10, np.int64)  # NodePreferAvoidPods map score per (class, label set)
     im_s = np.zeros((Cn, L), np.int64)     # ImageLocality map score per (class, label set)
@@ -870,13 +869,13 @@ def build_class_tables(label_items, taint_items, specs):
                               and not any(tolerates(t, x) for t in prefer_tols)))
         tv = sorted(set(counts))
         av = sorted(set(weights))
-        if len(tv) > abi.MAX_RCLASS or len(av) > abi.MAX_RCLASS:
-            # more than 16 values in one dimension (a product above 16 takes the wide decision)
-            raise Unsupported("pod class needs %d x %d reduce classes (> %d per dimension)" % (len(tv), len(av),
-                                                                                          abi.MAX_RCLASS))
+        if len(tv) * len(av) > abi.MAX_WIDE:
+            # NormalizeReduce takes any number of values (reduce.go:29-64); one pod's reduce classes are
+            # bounded by the launch form's wide decision (a product above 16 decides there)
+            raise Unsupported("pod class needs %d x %d reduce classes (> %d)" % (len(tv), len(av), abi.MAX_WIDE))
         ntt[k], nna[k] = len(tv), len(av)
-        ttv[k, :len(tv)] = tv
-        nav[k, :len(av)] = av
+        tvs.append(tv)
+        avs.append(av)
         ttc[k, :] = [tv.index(x) for x in counts]
         nac[k, :] = [av.index(x) for x in weights]
         # raw per-label-set inputs of the NodeAffinity class dimension, for a scheduler whose
@@ -890,6 +889,13 @@ def build_class_tables(label_items, taint_items, specs):
         if not all_taint:
             f |= abi.POD_NEED_TAINTS
         need[k] = f
+    # the value rows: 16 wide, or as wide as the widest class's larger dimension
+    W = max([abi.MAX_RCLASS] + [max(len(a), len(b)) for a, b in zip(tvs, avs)])
+    ttv = np.zeros((Cn, W), np.int64)
+    nav = np.zeros((Cn, W), np.int64)
+    for k, (tv, av) in enumerate(zip(tvs, avs)):
+        ttv[k, :len(tv)] = tv
+        nav[k, :len(av)] = av
     tables = dict(n_classes=Cn, n_label_sets=L, n_taint_sets=T, sel_ok=sel, taint_ok=tok, noexec_ok=nok,
                   tt_class=ttc, na_class=nac, n_tt=ntt, n_na=nna, tt_val=ttv, na_val=nav, na_w=na_w, na_p=na_p,
                   pa_split=pa_split, im_s=im_s)
@@ -912,6 +918,9 @@ def class_tables_struct(d, na_add=None):
     if d.get("svc_ok") is not None:
         d["svc_ok"] = np.ascontiguousarray(d["svc_ok"], np.uint32)
         t.svc_ok = abi.ptr(d["svc_ok"], abi.C.c_uint32)
+    W = d["tt_val"].shape[1]  # one row width for every value array (ABI 7)
+    assert d["na_val"].shape[1] == W and (na_add is None or np.asarray(na_add).shape[1] == W)
+    t.val_width = W if W != abi.MAX_RCLASS else 0
     return t
 
 

@@ -217,23 +217,29 @@ def class_tables_for(tables, priorities, label_sets=(), custom=None):
     Cn = d["n_classes"]
     nac = np.zeros_like(tables["na_class"])
     nna = np.ones(Cn, np.int32)
-    nav = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
-    add = np.zeros((Cn, abi.MAX_RCLASS), np.int64)
+    avs = []
     for k in range(Cn):
         pa = [int(p) * w_pa if pa_on else 0 for p in tables["na_p"][k]]
         if im_on:
             pa = [a + w_im * int(x) for a, x in zip(pa, im_s[k])]
         keys = list(zip((int(x) if use_w else 0 for x in tables["na_w"][k]), (a + int(b) for a, b in zip(pa, lab_add))))
         av = sorted(set(keys))
-        if len(av) > abi.MAX_RCLASS:
-            raise Unsupported("pod class needs %d x %d reduce classes (> %d per dimension)" % (int(tables["n_tt"][k]), len(av),
-                                                                                              abi.MAX_RCLASS))
+        if int(tables["n_tt"][k]) * len(av) > abi.MAX_WIDE:
+            raise Unsupported("pod class needs %d x %d reduce classes (> %d)" % (int(tables["n_tt"][k]), len(av), abi.MAX_WIDE))
         nna[k] = len(av)
-        nav[k, :len(av)] = [w for w, _ in av]
-        add[k, :len(av)] = [p for _, p in av]
+        avs.append(av)
         pos = {x: i for i, x in enumerate(av)}
         nac[k, :] = [pos[x] for x in keys]
-    d.update(na_class=nac, n_na=nna, na_val=nav, pa_in_add=pa_on)
+    # one row width for every value array: the class table's, or wider when the addends split more classes
+    W = max([tables["tt_val"].shape[1]] + [len(av) for av in avs])
+    nav = np.zeros((Cn, W), np.int64)
+    add = np.zeros((Cn, W), np.int64)
+    for k, av in enumerate(avs):
+        nav[k, :len(av)] = [w for w, _ in av]
+        add[k, :len(av)] = [p for _, p in av]
+    ttv = np.zeros((Cn, W), np.int64)
+    ttv[:, :tables["tt_val"].shape[1]] = tables["tt_val"]
+    d.update(na_class=nac, n_na=nna, na_val=nav, tt_val=ttv, pa_in_add=pa_on)
     return d, add
 
 

@@ -45,6 +45,9 @@
 
 #include "../include/ksim.h"
 
+/* row width of the per-class value arrays (ksim_class_tables.val_width, ABI 7; 0 = 16) */
+#define VW(ct) ((int64_t)((ct)->val_width ? (ct)->val_width : KSIM_MAX_RCLASS))
+
 typedef struct {
   int64_t n;
   int32_t n_scalar, port_slots;
@@ -540,12 +543,12 @@ int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_nod
         if (wb) s += (uint64_t)wb * (uint64_t)balanced_score(rcpu, N.alloc_cpu[i], rmem, N.alloc_mem[i]);
         score[i] = (int64_t)s;
         if (wt) {
-          int64_t v = ct->tt_val[cls * KSIM_MAX_RCLASS + ct->tt_class[cls * ct->n_taint_sets + N.taint_set[i]]];
+          int64_t v = ct->tt_val[cls * VW(ct) + ct->tt_class[cls * ct->n_taint_sets + N.taint_set[i]]];
           ttv[i] = v;
           if (v > mxT) mxT = v;
         }
         if (wa) {
-          int64_t v = ct->na_val[cls * KSIM_MAX_RCLASS + ct->na_class[cls * ct->n_label_sets + N.label_set[i]]];
+          int64_t v = ct->na_val[cls * VW(ct) + ct->na_class[cls * ct->n_label_sets + N.label_set[i]]];
           nav[i] = v;
           if (v > mxA) mxA = v;
         }
@@ -654,7 +657,7 @@ int ksim_ref_run_ex(const ksim_config* cfg, const ksim_node_table* tab, ksim_nod
         /* NodePreferAvoidPods (node_prefer_avoid_pods.go:32-68): its weighted map score rides the
            node's NodeAffinity class (ksim_class_tables.na_add) */
         if (ct->na_add)
-          t += (uint64_t)ct->na_add[cls * KSIM_MAX_RCLASS + ct->na_class[cls * ct->n_label_sets + N.label_set[i]]];
+          t += (uint64_t)ct->na_add[cls * VW(ct) + ct->na_class[cls * ct->n_label_sets + N.label_set[i]]];
         if (ipa && gmx - gmn > 0)  /* fScore = MaxPriority * ((count - min) / (max - min)), :228-236 */
           t += (uint64_t)wi * (uint64_t)(int64_t)(10.0 * ((double)(raw[i] - gmn) / (double)(gmx - gmn)));
         if (sp >= 0) {

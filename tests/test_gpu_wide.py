@@ -10,7 +10,7 @@ import pytest
 
 import ksim_ref as R
 from ksim import abi, ingest, scheduler
-from test_oracle_c_features import wide_workload
+from test_oracle_c_features import very_wide_workload, wide_workload
 
 pytestmark = pytest.mark.gpu
 
@@ -78,6 +78,49 @@ def test_wide_at_scale_matches_c_oracle():
     g = scheduler.GenericScheduler(cl, preds, prios)
     try:
         assert _wide_pods(cl, g) > 20
+        out, _, _ = g.schedule()
+        assert (out == want).all(), int((out != want).argmax())
+        assert g.last_node_index == ctr
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("mode", [abi.MODE_AUTO, abi.MODE_LAUNCH])
+@pytest.mark.parametrize("seed", range(3))
+def test_very_wide_reduce_dimension_matches_oracle(seed, mode):
+    """More than 16 values in one reduce dimension (up to 64 NodeAffinity weight sums, 25
+    TaintToleration counts; formerly refused): the launch form's wide decision over value rows
+    wider than 16 (ABI 7), against the object oracle — placements, FitError text, lastNodeIndex."""
+    nodes, running, pods = very_wide_workload(seed)
+    preds, prios = scheduler.provider("DefaultProvider")
+    want, lni = R.simulate(nodes, running, pods, set(preds), list(prios))
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order)
+    g = scheduler.GenericScheduler(cl, preds, prios, mode=mode)
+    try:
+        assert _wide_pods(cl, g) > 0
+        out, reasons, st = g.schedule()
+        got = [(cl.pod_names[k], cl.names[w] if w >= 0 else None,
+                None if w >= 0 else scheduler.fit_error_message(cl.n_nodes, reasons[k], cl.scalar_names.items))
+               for k, w in enumerate(out)]
+        assert got == want
+        assert g.last_node_index == lni
+    finally:
+        g.close()
+
+
+def test_very_wide_at_scale_matches_c_oracle():
+    """2,000 nodes x 600 pods with > 16 values in one reduce dimension, against the C oracle."""
+    import cpu_ref
+    nodes, running, pods = very_wide_workload(5, n_nodes=2000, n_pods=600)
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order)
+    preds, prios = scheduler.provider("DefaultProvider")
+    p = scheduler.plan(cl, preds, prios)
+    assert p.tables["tt_val"].shape[1] > 16
+    want, _, _, ctr, _ = cpu_ref.run(cl, None, threads=8, plan=p)
+    g = scheduler.GenericScheduler(cl, preds, prios)
+    try:
         out, _, _ = g.schedule()
         assert (out == want).all(), int((out != want).argmax())
         assert g.last_node_index == ctr

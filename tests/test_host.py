@@ -25,7 +25,7 @@ def test_library_exports_every_header_symbol():
     for f in fns:
         assert hasattr(L, f), f
     assert sorted(fns) == sorted(abi.EXPORTS)
-    assert L.ksim_abi_version() == abi.ABI_VERSION == 6
+    assert L.ksim_abi_version() == abi.ABI_VERSION == 7
 
 
 def test_create_without_device_fails_loudly():

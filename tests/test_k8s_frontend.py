@@ -46,6 +46,7 @@ def _compare(cl, fe):
         assert np.array_equal(a[k], b[k]), k
     d = cl.tables
     assert (ct.n_classes, ct.n_label_sets, ct.n_taint_sets) == (d["n_classes"], d["n_label_sets"], d["n_taint_sets"])
+    assert (ct.val_width or abi.MAX_RCLASS) == d["tt_val"].shape[1] == d["na_val"].shape[1]
     for name, ctype in (("sel_ok", C.c_uint32), ("taint_ok", C.c_uint32), ("noexec_ok", C.c_uint32), ("tt_class", C.c_uint8),
                         ("na_class", C.c_uint8), ("n_tt", C.c_int32), ("n_na", C.c_int32), ("tt_val", C.c_int64),
                         ("na_val", C.c_int64)):
@@ -103,6 +104,14 @@ def _compare(cl, fe):
 @pytest.mark.parametrize("seed", range(6))
 def test_general_workloads(seed):
     nodes, running, pods = rnd_workload(seed, n_nodes=30, n_pods=90)
+    _compare(ingest.Cluster.from_objects(nodes, running, pods), frontend.K8sCluster(nodes, running, pods))
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_very_wide_reduce_dimension_workloads(seed):
+    """More than 16 values in one reduce dimension: value rows wider than 16 (ABI 7) alike."""
+    from test_oracle_c_features import very_wide_workload
+    nodes, running, pods = very_wide_workload(seed, n_nodes=40, n_pods=80)
     _compare(ingest.Cluster.from_objects(nodes, running, pods), frontend.K8sCluster(nodes, running, pods))
 
 

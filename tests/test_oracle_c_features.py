@@ -297,6 +297,53 @@ def wide_workload(seed, n_nodes=60, n_pods=300):
     return nodes, running, pods
 
 
+def very_wide_workload(seed, n_nodes=80, n_pods=300):
+    """More than 16 values in ONE reduce dimension (formerly refused): nodes carry a `w` label out of
+    40 values and 0..24 PreferNoSchedule taints; many pods prefer `w` values through six weighted
+    terms (weights 1..32: up to 64 distinct preferred-weight sums over the label sets) and tolerate
+    some of the taints (up to 25 distinct intolerable counts).  NormalizeReduce has no limit on the
+    values (priorities/reduce.go:29-64)."""
+    import random
+    from workloads import rnd_workload
+    rng = random.Random(seed * 104729 + 7)
+    nodes, running, pods = rnd_workload(seed, n_nodes=n_nodes, n_pods=n_pods)
+    for x in nodes:
+        x["metadata"].setdefault("labels", {})["w"] = str(rng.randrange(40))
+        k = rng.randrange(25)
+        x["spec"]["taints"] = [t for t in x["spec"].get("taints") or [] if t["effect"] != "PreferNoSchedule"] + \
+            [{"key": "pns-%d" % j, "value": "", "effect": "PreferNoSchedule"} for j in range(k)]
+    for p in pods:
+        spec = p["spec"]
+        # (a pod's TaintToleration x NodeAffinity classes stay <= 256, the wide decision's bound:
+        # the pods with many preferred-weight sums tolerate every PreferNoSchedule taint)
+        if rng.random() < 0.5:
+            terms = [{"weight": 1 << t, "preference": {"matchExpressions": [
+                {"key": "w", "operator": "In", "values": [str(v) for v in rng.sample(range(40), 20)]}]}} for t in range(6)]
+            spec.setdefault("affinity", {}).setdefault("nodeAffinity", {})[
+                "preferredDuringSchedulingIgnoredDuringExecution"] = terms
+            spec.setdefault("tolerations", []).append({"operator": "Exists", "effect": "PreferNoSchedule"})
+        elif rng.random() < 0.5:
+            spec.setdefault("tolerations", []).extend(
+                {"key": "pns-%d" % j, "operator": "Exists", "effect": "PreferNoSchedule"} for j in rng.sample(range(25), 6))
+    return nodes, running, pods
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_very_wide_reduce_dimension_matches_object_oracle(seed):
+    """More than 16 values in one reduce dimension: ingest (value rows wider than 16, ABI 7) + plan +
+    the C oracle against the object oracle."""
+    nodes, running, pods = very_wide_workload(seed)
+    preds, prios = scheduler.provider("DefaultProvider")
+    want, lni = R.simulate(nodes, running, pods, set(preds), list(prios))
+    got, ctr = c_oracle_objects(nodes, running, pods, preds, prios)
+    _same(want, got)
+    assert ctr == lni
+    cl = ingest.Cluster.from_objects(nodes, running, list(reversed(pods)))
+    t = scheduler.plan(cl, preds, prios).tables
+    dims = np.maximum(np.asarray(t["n_tt"]), np.asarray(t["n_na"]))[np.asarray(cl.pods["cls"])]
+    assert (dims > 16).any() and t["tt_val"].shape[1] > 16
+
+
 @pytest.mark.parametrize("seed", range(4))
 def test_wide_reduce_classes_match_object_oracle(seed):
     """More than 16 reduce classes per pod class (formerly refused): ingest + plan + the C oracle
