@@ -687,12 +687,27 @@ int ksim_tent_undo(ksim_handle* h) {
   if (!h->tent.live) return KSIM_OK;
   h->tent.live = false;
   h->tent_stats[1] += 1;
+  const ksim_pod& P = h->tent.rec.P;
+  const bool shared = ksim_is_aff_host(h, P) || P.vol_class != 0;
   if (h->serve_live.load() && h->tent.launch == h->serve_launch_id && !serve_left(h)) {
-    // the kernel that holds the record runs: the next message (a stop's EXIT included) carries the
-    // undo, applied by the record's block before anything reads the row
+    if (!shared) {
+      // the kernel that holds the record runs: the next message (a stop's EXIT included) carries
+      // the undo, applied by the record's block before anything reads the row
+      h->tent.act = KSIM_TENT_UNDO;
+      h->tent.undo_inflight = true;
+      return KSIM_OK;
+    }
+    // mounts / affinity counts other blocks read: an UNDO message of its own, answered once the
+    // undo is released (the next message acquires)
+    KsimGate gate(h, false);
     h->tent.act = KSIM_TENT_UNDO;
-    h->tent.undo_inflight = true;
-    return KSIM_OK;
+    int32_t r[KSIM_RES_WORDS];
+    int rc = serve_post(h, KSIM_SERVE_UNDO, P, h->tent.ports, h->tent.rec.sc, 0, h->tent.rec.node, 0, r);
+    h->tent.act = KSIM_TENT_NONE;
+    if (rc) return rc;
+    if (r[KSIM_RES_ERR]) return ksim_fail(h, KSIM_E_DEVICE, "device consistency error 0x%x (undo)", r[KSIM_RES_ERR]);
+    if (r[KSIM_RES_STATUS] == 1) return KSIM_OK;
+    // no block held the record (a relaunch served the message): the launch below
   }
   // the record left with an earlier launch: undo by a launch on the quiet stream
   h->tent.act = KSIM_TENT_NONE;
@@ -857,11 +872,10 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
         if ((rc = serve_ready(h, npt, grid))) return rc;
         oc.lap(0);
         const ksim_pod sp = staged_pod(h, *pod);
-        // SCHEDULE_ONLY: a tentative commit when the commit touches the pod's row alone (no volume
-        // mounts, no affinity / service counts), so the AssumePod that normally follows costs no
-        // message (KSIM_TENTATIVE=0: decide only)
+        // SCHEDULE_ONLY: a tentative commit, so the AssumePod that normally follows costs no message
+        // (KSIM_TENTATIVE=0: decide only)
         static const bool tent_off = getenv("KSIM_TENTATIVE") && getenv("KSIM_TENTATIVE")[0] == '0';
-        const int32_t nc = assume ? 0 : (!tent_off && !ksim_is_aff_host(h, *pod) && pod->vol_class == 0 ? KSIM_SERVE_TENTATIVE : 1);
+        const int32_t nc = assume ? 0 : (!tent_off ? KSIM_SERVE_TENTATIVE : 1);
         int32_t r[KSIM_RES_WORDS];
         if ((rc = serve_post(h, KSIM_SERVE_SCHEDULE, sp, ports + pod->port_off, scalars + pod->scalar_off, nc, -1, h->pick_tag,
                              r)))

@@ -83,7 +83,12 @@ __global__ void ksim_release_kernel(KsimCtx c, int64_t pod, int64_t node) {
 
 // Undo a tentative commit whose record left with the resident kernel (ksim_cache.cpp).
 __global__ void ksim_undo_kernel(KsimCtx c, KsimTentRec t) {
-  if (blockIdx.x == 0 && threadIdx.x == 0) ksim_undo_commit(c, t);
+  if (blockIdx.x != 0 || threadIdx.x >= 64) return;
+  if (threadIdx.x == 0) {
+    ksim_undo_commit(c, t);
+    if (ksim_is_vol_pod(c, t.P)) ksim_vol_commit_body(*c.vol, t.P, t.node, -1, c.err);
+  }
+  if (ksim_is_aff_pod(c, t.P)) ksim_aff_commit_body(*c.aff, t.P, t.node, -1, threadIdx.x, 64);
 }
 
 // Queued pods' spec.nodeName name ranks after a node insert (op 1) or removal (op 2).

@@ -247,6 +247,7 @@ __device__ __forceinline__ ksim_scalar_req ksim_pod_scalar(const KsimCtx& c, con
 #define KSIM_SERVE_EXIT 0
 #define KSIM_SERVE_SCHEDULE 1
 #define KSIM_SERVE_ASSUME 2
+#define KSIM_SERVE_UNDO 3   // undo a tentative commit of shared state (below); answered by the node's block
 #define KSIM_SERVE_SYNC_ACQUIRE 1  // the previous message committed state other blocks read: acquire first
 #define KSIM_SERVE_MSG_WORDS 128
 // payload word offsets
@@ -267,9 +268,12 @@ __device__ __forceinline__ ksim_scalar_req ksim_pod_scalar(const KsimCtx& c, con
 #define KSIM_TENT_CONFIRM 1  // AssumePod named the same pod and node: the commit stands, drop the record
 #define KSIM_TENT_UNDO 2     // anything else came first: undo the commit, then drop the record
 // SCHEDULE's KSIM_SERVE_W_NOCOMMIT: 0 commit (SCHEDULE_ASSUME), 1 decide only, 2 tentative commit
-// (SCHEDULE_ONLY of a pod whose commit touches only its own row: the owner block commits it and
-// keeps a record, and answers the row's port count and flags before the commit in the first two
-// reason words, so the host can undo it without the kernel too)
+// (SCHEDULE_ONLY: the owner block commits it and keeps a record, and answers the row's port count
+// and flags before the commit in the first two reason words, so the host can undo it without the
+// kernel too).  A commit of the pod's row alone is undone by the record's block before it reads
+// the row again (any later message carries the decision); a commit of state other blocks read
+// (volume mounts, inter-pod affinity / SelectorSpread counts) is undone by an UNDO message of its
+// own, answered after the undo is released, and the next message acquires.
 #define KSIM_SERVE_TENTATIVE 2
 static_assert(sizeof(ksim_pod) % 4 == 0 && sizeof(ksim_scalar_req) % 4 == 0, "mailbox words");
 static_assert(KSIM_SERVE_W_SCALARS + (int)(KSIM_MAX_SCALAR * sizeof(ksim_scalar_req) / 4) <= KSIM_SERVE_W_TENT_SEQ,

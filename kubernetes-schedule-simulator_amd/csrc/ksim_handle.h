@@ -81,6 +81,15 @@ struct DevBuf {
 // is one launch and one stream sync, with no copy either way.
 // (the result block layout KSIM_RES_* is in ksim_common.h: the kernels write it)
 
+// The small volume tables' segments in vol_small (ksim_volumes.cpp): capacities, the loaded ref
+// count and byte offsets, so a grow within the capacities writes only the new entries.
+struct VolSeg {
+  bool valid = false;
+  int64_t cap_keys = 0, cap_vclass = 0, cap_refs = 0;
+  int32_t n_refs = 0;
+  size_t o_kf = 0, o_vc = 0, o_vf = 0, o_refs = 0, o_zo = 0;
+};
+
 struct ksim_handle {
   int device = 0;
   // the handle's one stream: every launch and copy goes through ksim_stream(h), which first stops
@@ -255,6 +264,7 @@ struct ksim_handle {
   size_t vol_small_cap = 0;
   std::vector<char> vol_small_host;
   int64_t vol_in_place = 0;      // grows written beside a running resident per-pod kernel
+  VolSeg vol_seg;
   std::vector<int32_t> q_vclass;
   std::vector<int64_t> vol_pre;  // vol_pre[i] = volume / service-affinity pods among the first i queued
 };

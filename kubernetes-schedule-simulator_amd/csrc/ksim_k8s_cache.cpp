@@ -92,6 +92,7 @@ struct ksim_k8s_cache {
   size_t zoned_upto = 0;              // label sets scanned for zone / region labels
   ZoneGroups zone_groups;             // label sets by their zone / region labels (volume zone verdicts)
   bool zoned = false;
+  VolSmall vs;                        // the small volume tables as last loaded (grows append to them)
 };
 
 namespace {
@@ -178,7 +179,6 @@ void sync_volumes(Cache* c, bool need, const Enc* e) {
   const int32_t vc = e ? e->row.vol_class : 0;
   const size_t want = c->vol_max + (vc ? vi.class_refs[vc - 1].size() : 0);
   if (!c->vol_dirty && !c->vol_loaded && !need) return;
-  VolSmall vs;
   if (!c->vol_dirty && c->vol_loaded) {
     if (c->vol_key == key && (int64_t)want <= c->vol_S) return;
     if (c->vol_key[2] == key[2]) {
@@ -187,8 +187,8 @@ void sync_volumes(Cache* c, bool need, const Enc* e) {
         c->vol_zone_classes = key[1];
       }
       const int32_t S = std::max<int32_t>(c->vol_S, (int32_t)(2 * want));
-      vol_small(vi, &vs);
-      check(c, load_vol_tab(vs, (int64_t)c->names.size(), S, c->opt.max_vols, c->use_zone ? &c->vol_zone : nullptr,
+      vol_small_append(vi, &c->vs);
+      check(c, load_vol_tab(c->vs, (int64_t)c->names.size(), S, c->opt.max_vols, c->use_zone ? &c->vol_zone : nullptr,
                             c->vol_zone_words, false, nullptr, nullptr, c->h),
             "ksim_grow_volumes");
       c->vol_key = key;
@@ -218,8 +218,8 @@ void sync_volumes(Cache* c, bool need, const Enc* e) {
     }
     count[i] = s;
   }
-  vol_small(vi, &vs);
-  check(c, load_vol_tab(vs, n, S, c->opt.max_vols, c->use_zone ? &c->vol_zone : nullptr, c->vol_zone_words, true,
+  vol_small(vi, &c->vs);
+  check(c, load_vol_tab(c->vs, n, S, c->opt.max_vols, c->use_zone ? &c->vol_zone : nullptr, c->vol_zone_words, true,
                         slots.data(), count.data(), c->h),
         "ksim_load_volumes");
   c->vol_key = key;

@@ -1620,6 +1620,19 @@ void vol_small(const VolumeIndex& vi, VolSmall* t) {
   t->vc_filter = vi.class_filter;
 }
 
+// vol_small for a grow: only the keys / classes interned since `t` was built are appended (keys and
+// classes keep their entries once interned), so the cost is the new entries, not every cached pod's.
+void vol_small_append(const VolumeIndex& vi, VolSmall* t) {
+  for (size_t k = t->key_filter.size(); k < vi.key_filter.size(); ++k) t->key_filter.push_back(vi.key_filter[k]);
+  for (size_t c = t->vc_filter.size(); c < vi.class_refs.size(); ++c) {
+    const auto& cr = vi.class_refs[c];
+    t->vc.push_back((int32_t)t->refs.size());
+    t->vc.push_back((int32_t)cr.size());
+    for (const auto& e : cr) t->refs.push_back(ksim_vol_ref{e.first, e.second});
+    t->vc_filter.push_back(vi.class_filter[c]);
+  }
+}
+
 // ksim_load_volumes (full: with the slots) or ksim_grow_volumes (slots ignored) over the small tables.
 int load_vol_tab(const VolSmall& v, int64_t n, int32_t S, const int32_t* max_vols, const std::vector<uint32_t>* zone_ok,
                  int32_t zone_words, bool full, const uint64_t* slots, const int32_t* slot_count, ksim_handle* h) {

@@ -2041,7 +2041,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
       if (tid == 0) {
         if (ksim_is_vol_pod(c, P)) ksim_vol_commit_body(*c.vol, P, node, 1, c.err);
         s_stat = st;
-        if (tentative) {  // (the host sends tentative commits only for pods without volumes / affinity terms)
+        if (tentative) {
           s_cnt0 = cnt0;
           s_fl0 = fl0;
           tent->node = node;
@@ -2150,6 +2150,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
   __shared__ uint64_t s_seq;
   __shared__ KsimTentRec s_tent;  // this block's tentative commit awaiting the host's decision
   __shared__ int32_t s_got;       // wave 0 took a message (an EXIT included)
+  __shared__ int32_t s_undid;     // this message undid this block's tentative commit
   KsimServeBox* const box = a.box;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, me = blockIdx.x;
   // lastNodeIndex: from the host's last answer, or (after calls of other forms) the device word,
@@ -2255,7 +2256,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
         s_msg[2 * lane] = q.x;
         s_msg[2 * lane + 1] = q.z;
       }
-      if (type == KSIM_SERVE_SCHEDULE || type == KSIM_SERVE_ASSUME) {
+      if (type == KSIM_SERVE_SCHEDULE || type == KSIM_SERVE_ASSUME || type == KSIM_SERVE_UNDO) {
         // the payload through LDS: the pod into s_P, ports / scalars into this block's staging
         // slot (the evaluation reads them there)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -2292,7 +2293,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
           s_node = (int64_t)(((uint64_t)s_msg[KSIM_SERVE_W_NODE + 1] << 32) | s_msg[KSIM_SERVE_W_NODE]);
         }
       }
-      if (lane == 0) { s_type = type; s_got = got ? 1 : 0; }
+      if (lane == 0) { s_type = type; s_got = got ? 1 : 0; s_undid = 0; }
     }
     __syncthreads();
 #ifdef KSIM_STAMPS
@@ -2302,9 +2303,14 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
     // the host's decision on this block's tentative commit, before anything else reads the row
     if (s_got && s_tent.valid && s_msg[KSIM_SERVE_W_TENT_SEQ] == s_tent.seq && s_msg[KSIM_SERVE_W_TENT_ACT] != KSIM_TENT_NONE) {
       const bool undo = s_msg[KSIM_SERVE_W_TENT_ACT] == KSIM_TENT_UNDO;
-      if (tid == 0) {
-        if (undo) {
+      if (undo && wv == 0) {  // (shared state — mounts, affinity counts — only on an UNDO message: see ksim_common.h)
+        if (lane == 0) {
           ksim_undo_commit(c, s_tent);
+          if (ksim_is_vol_pod(c, s_tent.P)) ksim_vol_commit_body(*c.vol, s_tent.P, s_tent.node, -1, c.err);
+        }
+        if (ksim_is_aff_pod(c, s_tent.P)) ksim_aff_commit_body(*c.aff, s_tent.P, s_tent.node, -1, lane, 64);
+        if (lane == 0) {
+          s_undid = 1;
           __hip_atomic_store(&box->undo_ack, (uint64_t)s_tent.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
       }
@@ -2337,6 +2343,16 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
       // the committed row's register copy: wave 0's stores, then the thread that caches the row
       __syncthreads();
       ksim_row_cache_reload<NPT>(c, rcache, base, s_node);
+    } else if (type == KSIM_SERVE_UNDO) {
+      // the explicit undo of a tentative commit of shared state: applied above by the block that
+      // holds the record; the block owning the node answers (status 1: undone here, 0: no record
+      // here — a relaunched kernel — and the host undoes it by a launch)
+      const int64_t node = s_node;
+      if (node >= (int64_t)me * c.chunk && node < (int64_t)(me + 1) * c.chunk && wv == 0) {
+        if (s_undid) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");  // (the next message acquires)
+        pk_answer(box->ans, seq, lane, (int32_t)node, 0, s_undid ? 1 : 0,
+                  __hip_atomic_load(c.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), s_keep, 0);
+      }
     } else {
       break;  // an exit message, or the grid left by the idle vote
     }

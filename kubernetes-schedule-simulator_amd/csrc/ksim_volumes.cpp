@@ -10,7 +10,9 @@
 
 namespace {
 
-int validate(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
+// (k0, j0, c0): the keys, refs and volume classes already checked (an in-place grow: the header's
+// contract keeps existing entries unchanged, so only the new ones are checked)
+int validate(ksim_handle* h, const ksim_volume_tables* t, bool keep, int32_t k0 = 0, int32_t j0 = 0, int32_t c0 = 0) {
   const int64_t n = h->ctx.n;
   if (t->n_nodes != n)
     return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: tables for %lld nodes, table has %lld", (long long)t->n_nodes,
@@ -32,14 +34,14 @@ int validate(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
   if (t->zone_ok && t->zone_words != (h->n_label_sets + 31) / 32)
     return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: zone_words does not match the %d loaded label sets",
                      h->n_label_sets);
-  for (int32_t k = 0; k < t->n_keys; ++k)
+  for (int32_t k = k0; k < t->n_keys; ++k)
     if (t->key_filter[k] & ~(KSIM_VOL_EBS | KSIM_VOL_GCE_PD | KSIM_VOL_AZURE_DISK))
       return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: key %d has unknown filter bits", k);
   const uint32_t ref_bits = KSIM_VOL_CONFLICT_ANY | KSIM_VOL_CONFLICT_RW | KSIM_VOL_READ_ONLY | KSIM_VOL_NEW | KSIM_VOL_VIA_PVC;
-  for (int32_t j = 0; j < t->n_refs; ++j)
+  for (int32_t j = j0; j < t->n_refs; ++j)
     if (t->refs[j].key < 0 || t->refs[j].key >= t->n_keys || (t->refs[j].flags & ~ref_bits))
       return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: ref %d out of range", j);
-  for (int32_t c = 0; c < t->n_vclass; ++c) {
+  for (int32_t c = c0; c < t->n_vclass; ++c) {
     const int64_t off = t->vc[2 * (int64_t)c], cnt = t->vc[2 * (int64_t)c + 1];
     if (off < 0 || cnt < 0 || off + cnt > t->n_refs)
       return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: class %d refs out of bounds", c);
@@ -56,7 +58,7 @@ int validate(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
                          (long long)i, s);
     }
   }
-  for (size_t q = 0; q < h->q_vclass.size(); ++q)
+  for (size_t q = 0; c0 == 0 && q < h->q_vclass.size(); ++q)
     if (h->q_vclass[q] > t->n_vclass)
       return ksim_fail(h, KSIM_E_INVAL, "ksim_load_volumes: queued pod %zu uses a volume class beyond the tables", q);
   return KSIM_OK;
@@ -71,9 +73,46 @@ static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
   if (keep && (!h->have_vol || h->vol_stale))
     return ksim_fail(h, KSIM_E_STATE, "ksim_grow_volumes: no current volume tables (load them after a node event)");
   HIPCHK(h, hipSetDevice(h->device));
+  const int64_t n = h->ctx.n;
+  VolSeg& sg = h->vol_seg;
+  // A grow within the segments' capacities, with the same mounts and zone words: only the entries
+  // past the loaded counts are checked, written into the host mirror and uploaded (the descriptor,
+  // which holds no counts, and every earlier entry stay) — O(new entries), not O(cached pods).
+  if (keep && sg.valid && t->vol_slots == h->vol_h.vol_slots && t->n_keys <= sg.cap_keys && t->n_vclass <= sg.cap_vclass &&
+      t->n_refs <= sg.cap_refs && t->zone_words == h->vol_h.zone_words && (t->zone_ok != nullptr) == (h->vol_h.zone_ok != nullptr) &&
+      t->max_vols[0] == h->vol_h.max_vols[0] && t->max_vols[1] == h->vol_h.max_vols[1] && t->max_vols[2] == h->vol_h.max_vols[2]) {
+    const int32_t k0 = h->vol_n_keys, c0 = h->vol_n_class, j0 = sg.n_refs;
+    if (t->n_refs < j0) return ksim_fail(h, KSIM_E_INVAL, "ksim_grow_volumes: the tables may only grow (refs %d < %d)", t->n_refs, j0);
+    int rc = validate(h, t, keep, k0, j0, c0);
+    if (rc) return rc;
+    std::vector<char>& hb = h->vol_small_host;
+    struct Part { size_t off, esz; const void* src; int64_t from, to; };
+    const int32_t zw = t->zone_ok ? t->zone_words : 0;
+    const Part parts[] = {{sg.o_kf, 4, t->key_filter, k0, t->n_keys},
+                          {sg.o_vc, 8, t->vc, c0, t->n_vclass},  // (two int32 per class)
+                          {sg.o_vf, 4, t->vc_filter, c0, t->n_vclass},
+                          {sg.o_refs, sizeof(ksim_vol_ref), t->refs, j0, t->n_refs},
+                          {sg.o_zo, (size_t)zw * 4, t->zone_ok, c0, zw ? t->n_vclass : c0}};
+    const bool side = h->serve_live.load();
+    if (side && !h->side_stream) HIPCHK(h, hipStreamCreateWithFlags(&h->side_stream, hipStreamNonBlocking));
+    hipStream_t st = side ? h->side_stream : ksim_stream(h);
+    for (const Part& x : parts) {
+      if (x.to <= x.from || !x.esz) continue;
+      const size_t a = x.off + (size_t)x.from * x.esz, b = (size_t)(x.to - x.from) * x.esz;
+      memcpy(hb.data() + a, static_cast<const char*>(x.src) + (size_t)x.from * x.esz, b);
+      HIPCHK(h, hipMemcpyAsync(h->vol_small + a, hb.data() + a, b, hipMemcpyHostToDevice, st));
+    }
+    HIPCHK(h, hipStreamSynchronize(st));
+    if (side) h->serve_shared = true;  // (the resident kernel's next message acquires the new entries)
+    h->vol_in_place += side ? 1 : 0;
+    h->vol_n_class = t->n_vclass;
+    h->vol_n_keys = t->n_keys;
+    sg.n_refs = t->n_refs;
+    for (int32_t c = c0; c < t->n_vclass; ++c) h->vol_max_ref = std::max(h->vol_max_ref, t->vc[2 * (int64_t)c + 1]);
+    return KSIM_OK;
+  }
   int rc = validate(h, t, keep);
   if (rc) return rc;
-  const int64_t n = h->ctx.n;
   // the small tables, packed: [KsimVol][key_filter][vc][vc_filter][refs][zone_ok], 16-byte aligned
   size_t off = 0;
   auto seg = [&](size_t bytes) {
@@ -81,10 +120,14 @@ static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
     off = (off + bytes + 15) & ~(size_t)15;
     return o;
   };
-  const size_t o_V = seg(sizeof(KsimVol)), o_kf = seg(sizeof(*t->key_filter) * t->n_keys),
-               o_vc = seg(sizeof(*t->vc) * 2 * (size_t)t->n_vclass), o_vf = seg(sizeof(*t->vc_filter) * t->n_vclass),
-               o_refs = seg(sizeof(*t->refs) * t->n_refs),
-               o_zo = seg(t->zone_ok ? sizeof(*t->zone_ok) * (size_t)t->n_vclass * t->zone_words : 0);
+  // segment capacities: exact for a load, doubled for a grow (the next grows then go in place)
+  const int64_t f = keep ? 2 : 1;
+  const int64_t ck = std::max<int64_t>((int64_t)t->n_keys * f, 1), cv = std::max<int64_t>((int64_t)t->n_vclass * f, 1),
+                cr = std::max<int64_t>((int64_t)t->n_refs * f, 1);
+  const size_t o_V = seg(sizeof(KsimVol)), o_kf = seg(sizeof(*t->key_filter) * ck),
+               o_vc = seg(sizeof(*t->vc) * 2 * (size_t)cv), o_vf = seg(sizeof(*t->vc_filter) * cv),
+               o_refs = seg(sizeof(*t->refs) * cr),
+               o_zo = seg(t->zone_ok ? sizeof(*t->zone_ok) * (size_t)cv * t->zone_words : 0);
   char* old_small = nullptr;
   if (off > h->vol_small_cap) {  // grown geometrically: most grows reuse the buffer
     old_small = h->vol_small;
@@ -159,6 +202,7 @@ static int load(ksim_handle* h, const ksim_volume_tables* t, bool keep) {
   h->ctx.vol = dev;
   h->vol_n_class = t->n_vclass;
   h->vol_n_keys = t->n_keys;
+  sg = VolSeg{true, ck, cv, cr, t->n_refs, o_kf, o_vc, o_vf, o_refs, o_zo};
   h->vol_max_ref = 0;
   for (int32_t c = 0; c < t->n_vclass; ++c) h->vol_max_ref = std::max(h->vol_max_ref, t->vc[2 * (int64_t)c + 1]);
   h->have_vol = true;

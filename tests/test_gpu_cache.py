@@ -6,6 +6,8 @@ adapter drives: every rule in the library) — against the object-level oracle's
 streams that interleave Schedule + assume with node add / update / remove and pod add / confirm /
 update / remove / forget events.  Every decision (host or FitError text), lastNodeIndex and the
 final per-node state must be identical."""
+import ctypes as C
+
 import pytest
 
 import ksim_ref as R
@@ -34,7 +36,30 @@ class K8sCacheAdapter(K8sCache):
         return host, None
 
 
-IMPLS = {"py": SchedulerCache, "cpp": K8sCache, "adapter": K8sCacheAdapter}
+class K8sCacheAdapterUndo(K8sCacheAdapter):
+    """The adapter's pattern with a read of the device state between every other Schedule and its
+    AssumePod: the read first undoes the tentative commit (an explicit UNDO message when the commit
+    touched volume mounts or affinity counts, else the stop's exit message carries it), so the
+    AssumePod commits again through the ordinary path — the same decisions and final state."""
+
+    _k = 0
+
+    def schedule_one(self, pod):
+        from ksim.cache import FitError
+        try:
+            host = self.schedule(pod, assume=False)
+        except FitError as e:
+            return None, str(e)
+        self._k += 1
+        if self._k % 2:
+            v = C.c_uint64()
+            self._hcall("ksim_get_counter", C.byref(v))
+        q = dict(pod, spec=dict(pod["spec"], nodeName=host))
+        self.assume_pod(q)
+        return host, None
+
+
+IMPLS = {"py": SchedulerCache, "cpp": K8sCache, "adapter": K8sCacheAdapter, "adapter_undo": K8sCacheAdapterUndo}
 
 
 @pytest.fixture(autouse=True, params=["one_wg", "scan"])
