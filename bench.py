@@ -39,12 +39,12 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 def pmc_traffic(workload, evals_per_launch):
     """HBM traffic of the dominant kernel from the PMC profile collected at this round's code
-    (profiles/r5, r4 or r3 /pmc_<workload>.json: FETCH_SIZE (x2, the gfx950 correction) + WRITE_SIZE per
+    (profiles/r6, r5, r4 or r3 /pmc_<workload>.json: FETCH_SIZE (x2, the gfx950 correction) + WRITE_SIZE per
     dispatch in separate rocprofv3 --pmc passes of the bench command, tools/gpu_pmc.sh +
     tools/pmc_summary.py, as MI355X_MICROARCH.md prescribes), scaled to this launch's node-evals;
     None when no such profile exists.  Returns {"gb_per_launch", "bytes_per_node_eval", "source"}."""
     path = None
-    for rnd in ("r5", "r4", "r3"):  # the newest round's profile of this kernel
+    for rnd in ("r6", "r5", "r4", "r3"):  # the newest round's profile of this kernel
         path = os.path.join(ROOT, "profiles", rnd, "pmc_%s.json" % workload)
         if os.path.exists(path):
             break
