@@ -806,7 +806,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   const int one_npt = ksim_one_npt(c.n);
   const char* ko = getenv("KSIM_ONE_WG");
   const bool one_wg = ko ? ko[0] != '0' : c.n <= 1024;
-  if (cs.one && one_npt > 0 && one_wg && (!h->have_aff || h->aff_h.n_zone <= 512) && !ksim_rt_launch_tables(h) &&
+  if (cs.one && one_npt > 0 && one_wg && (!h->have_aff || h->aff_h.n_zone <= 512) && !ksim_rt_aux_on(h) &&
       cs.one_pod.reserved[0] * cs.one_pod.reserved[1] <= KSIM_MAX_RCLASS) {
     h->res_host[KSIM_RES_NODE] = INT32_MIN;
     if ((rc = ksim_rt_check_launch_ctx(h, cs, 1, "ksim_schedule_one"))) return rc;
@@ -834,10 +834,11 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   cs.chunk = (int64_t)KSIM_BLOCK * npt;
   // the pick kernel (<= 64 blocks, co-resident): one tagged-record exchange per reduction and a
   // redundant decision in every block instead of the scan's last-block round trips.  Not for the
-  // auxiliary priority / service-affinity lender tables, node sharding, > 60 spread zones or scores
-  // beyond its 56-bit record words.  KSIM_NO_PICK=1 disables it.
+  // auxiliary priority tables, node sharding, > 60 spread zones or scores beyond its 56-bit record
+  // words.  KSIM_NO_PICK=1 disables it.  (The service-affinity lender check reads only the global
+  // counts, which every block sees after the previous commit, as the inter-pod affinity terms do.)
   const char* npk = getenv("KSIM_NO_PICK");
-  if (cs.one && grid <= KSIM_PICK_MAXG && !(npk && npk[0] == '1') && !ksim_rt_launch_tables(h) && c.sh_world <= 1 &&
+  if (cs.one && grid <= KSIM_PICK_MAXG && !(npk && npk[0] == '1') && !ksim_rt_aux_on(h) && c.sh_world <= 1 &&
       cs.one_pod.reserved[0] * cs.one_pod.reserved[1] <= KSIM_MAX_RCLASS &&
       (!h->have_aff || h->aff_h.n_zone <= KSIM_PICK_ZMAX)) {
     int64_t sw = 0;
@@ -873,9 +874,11 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
         oc.lap(0);
         const ksim_pod sp = staged_pod(h, *pod);
         // SCHEDULE_ONLY: a tentative commit, so the AssumePod that normally follows costs no message
-        // (KSIM_TENTATIVE=0: decide only)
+        // (KSIM_TENTATIVE=0: decide only).  Not with the service-affinity lender tables: a commit
+        // records its label disagreements (ksim_svc_commit), which no undo takes back.
         static const bool tent_off = getenv("KSIM_TENTATIVE") && getenv("KSIM_TENTATIVE")[0] == '0';
-        const int32_t nc = assume ? 0 : (!tent_off ? KSIM_SERVE_TENTATIVE : 1);
+        const bool svc = ksim_rt_launch_tables(h);  // (aux is off on this path)
+        const int32_t nc = assume ? 0 : (!tent_off && !svc ? KSIM_SERVE_TENTATIVE : 1);
         int32_t r[KSIM_RES_WORDS];
         if ((rc = serve_post(h, KSIM_SERVE_SCHEDULE, sp, ports + pod->port_off, scalars + pod->scalar_off, nc, -1, h->pick_tag,
                              r)))
@@ -886,7 +889,12 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
         out->fit_nodes = r[KSIM_RES_FIT];
         memcpy(&out->last_node_index, r + KSIM_RES_CTR, 8);
         if (out->node < 0) memcpy(out->reasons, r + KSIM_RES_REASONS, sizeof out->reasons);
-        if (r[KSIM_RES_ERR] & 128) return ksim_rt_svc_refusal(h);
+        if (r[KSIM_RES_ERR] & 128) {
+          // the refusal clears its flag in the device error word: not under a resident kernel that
+          // reads it (the next message relaunches)
+          if ((rc = ksim_serve_stop(h))) return rc;
+          return ksim_rt_svc_refusal(h);
+        }
         if (r[KSIM_RES_ERR] || out->node == INT32_MIN) {
           uint64_t d2[2] = {0, 0};  // the kernel's note of its first failure (site, block, tag, message)
           const int32_t err = r[KSIM_RES_ERR];

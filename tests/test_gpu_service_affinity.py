@@ -112,3 +112,69 @@ def test_schedule_one_with_service_affinity_matches_batch():
     finally:
         batch.close()
         one.close()
+
+
+PER_POD_FORMS = {
+    "one_wg": {},                                            # <= 1,024 nodes: the single-workgroup kernel
+    "resident": {"KSIM_ONE_WG": "0"},                        # the pick body in the resident kernel
+    "scan": {"KSIM_ONE_WG": "0", "KSIM_NO_PICK": "1"},       # the multi-block scan
+}
+
+
+@pytest.mark.parametrize("pattern", ["assume", "adapter"])
+@pytest.mark.parametrize("form", sorted(PER_POD_FORMS))
+@pytest.mark.parametrize("variant", ["consistent", "mixed_labels", "conflicting_running"])
+@pytest.mark.parametrize("seed", range(2))
+def test_per_pod_forms_with_service_affinity_match_batch(seed, variant, form, pattern, monkeypatch):
+    """Every per-pod form evaluates the lender check on the global counts the previous commit left
+    (ksim_svc_lender) and records the lenders' disagreements at its commit (ksim_svc_commit):
+    placements and lastNodeIndex == the batch's; KSIM_E_UNSUPPORTED exactly when the batch refuses.
+    adapter: SCHEDULE_ONLY, then ksim_pod_add onto the chosen node (no tentative commit with these
+    tables: a commit's recorded disagreements are not undone)."""
+    import ctypes as C
+    for k, v in PER_POD_FORMS[form].items():
+        monkeypatch.setenv(k, v)
+    aff_labels = ["region", "rack"]
+    nodes, running, pods, services = rnd_svc_affinity_workload(seed, n_pods=60, mixed_labels=variant == "mixed_labels",
+                                                               conflicting_running=variant == "conflicting_running",
+                                                               full_labels=variant == "consistent")
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order, spread=spread.SpreadListers(services=services),
+                                     service_affinity=aff_labels)
+    batch = scheduler.GenericScheduler(cl, SVC_PREDS, SVC_PRIOS, mode=abi.MODE_LAUNCH, service_affinity=aff_labels)
+    one = scheduler.GenericScheduler(cl, SVC_PREDS, SVC_PRIOS, mode=abi.MODE_LAUNCH, service_affinity=aff_labels)
+    ports, sc = cl.pod_ports, cl.pod_scalars
+    try:
+        try:
+            out, _, _ = batch.schedule()
+        except abi.KsimUnsupported:
+            out = None
+        refused = False
+        for k in range(len(order)):
+            pod = abi.Pod.from_buffer_copy(cl.pods[k].tobytes())
+            res = abi.Result()
+            try:
+                one.h.call("ksim_schedule_one", C.byref(pod), abi.vptr(ports), len(ports), abi.vptr(sc), len(sc),
+                           abi.SCHEDULE_ASSUME if pattern == "assume" else abi.SCHEDULE_ONLY, C.byref(res))
+            except abi.KsimUnsupported:
+                refused = True
+                break
+            if out is not None:
+                assert res.node == out[k], k
+            if pattern == "adapter" and res.node >= 0:
+                one.h.call("ksim_pod_add", int(res.node), C.byref(pod), abi.vptr(ports), len(ports), abi.vptr(sc), len(sc))
+        assert refused == (out is None)
+        if out is not None:
+            assert one.last_node_index == batch.last_node_index
+        else:
+            # the refusal is the call's: the handle goes on deciding (the next pod through any form)
+            pod = abi.Pod.from_buffer_copy(cl.pods[0].tobytes())
+            res = abi.Result()
+            try:
+                one.h.call("ksim_schedule_one", C.byref(pod), abi.vptr(ports), len(ports), abi.vptr(sc), len(sc),
+                           abi.SCHEDULE_ONLY, C.byref(res))
+            except abi.KsimUnsupported:
+                pass
+    finally:
+        batch.close()
+        one.close()
