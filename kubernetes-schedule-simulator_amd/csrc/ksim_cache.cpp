@@ -806,7 +806,8 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   const int one_npt = ksim_one_npt(c.n);
   const char* ko = getenv("KSIM_ONE_WG");
   const bool one_wg = ko ? ko[0] != '0' : c.n <= 1024;
-  if (cs.one && one_npt > 0 && one_wg && (!h->have_aff || h->aff_h.n_zone <= 512) && !ksim_rt_aux_on(h) &&
+  if (cs.one && one_npt > 0 && one_wg && (!h->have_aff || h->aff_h.n_zone <= 512) &&
+      (!ksim_rt_aux_on(h) || h->aff_h.n_adom <= 512) &&
       cs.one_pod.reserved[0] * cs.one_pod.reserved[1] <= KSIM_MAX_RCLASS) {
     h->res_host[KSIM_RES_NODE] = INT32_MIN;
     if ((rc = ksim_rt_check_launch_ctx(h, cs, 1, "ksim_schedule_one"))) return rc;
@@ -833,16 +834,18 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
   }
   cs.chunk = (int64_t)KSIM_BLOCK * npt;
   // the pick kernel (<= 64 blocks, co-resident): one tagged-record exchange per reduction and a
-  // redundant decision in every block instead of the scan's last-block round trips.  Not for the
-  // auxiliary priority tables, node sharding, > 60 spread zones or scores beyond its 56-bit record
-  // words.  KSIM_NO_PICK=1 disables it.  (The service-affinity lender check reads only the global
-  // counts, which every block sees after the previous commit, as the inter-pod affinity terms do.)
+  // redundant decision in every block instead of the scan's last-block round trips.  Not for node
+  // sharding, more pass-A words than one record holds (4 + spread zones + with the auxiliary
+  // priority 3 + its domains <= 64) or scores beyond its 56-bit record words.  KSIM_NO_PICK=1
+  // disables it.  (The service-affinity lender check reads only the global counts, which every
+  // block sees after the previous commit, as the inter-pod affinity terms do.)
   const char* npk = getenv("KSIM_NO_PICK");
-  if (cs.one && grid <= KSIM_PICK_MAXG && !(npk && npk[0] == '1') && !ksim_rt_aux_on(h) && c.sh_world <= 1 &&
+  if (cs.one && grid <= KSIM_PICK_MAXG && !(npk && npk[0] == '1') && c.sh_world <= 1 &&
       cs.one_pod.reserved[0] * cs.one_pod.reserved[1] <= KSIM_MAX_RCLASS &&
-      (!h->have_aff || h->aff_h.n_zone <= KSIM_PICK_ZMAX)) {
+      (!h->have_aff || h->aff_h.n_zone + (ksim_rt_aux_on(h) ? 3 + h->aff_h.n_adom : 0) <= KSIM_PICK_ZMAX)) {
     int64_t sw = 0;
     for (int k = 0; k < KSIM_NW; ++k) sw += (c.w[k] > ((int64_t)1 << 40) ? ((int64_t)1 << 50) : c.w[k] * 10);
+    if (ksim_rt_aux_on(h)) sw += h->aff_h.aux_w > ((int64_t)1 << 40) ? ((int64_t)1 << 50) : h->aff_h.aux_w * 10;
     if (h->pick_grid != grid || h->pick_npt != npt) {
       h->pick_ok = ksim_pick_coresident(npt, grid) != 0;
       h->serve_fits = ksim_serve_coresident(npt, grid) != 0;

@@ -1236,11 +1236,13 @@ __global__ __launch_bounds__(ONE_BLOCK) void ksim_one_kernel(KsimCtx c) {
   __shared__ int32_t s_cnt[ONE_WAVES][KSIM_MAX_RCLASS];
   __shared__ int32_t s_fit[ONE_WAVES];
   __shared__ int32_t s_hist[KSIM_NREASONS];
-  __shared__ int64_t s_v[4][ONE_WAVES];
+  __shared__ int64_t s_v[7][ONE_WAVES];
   __shared__ unsigned long long s_z[KSIM_PASS_ZONES];
   __shared__ uint64_t s_bm[NPT][ONE_WAVES];
   __shared__ Decision D;
-  __shared__ int64_t s_pa[5];  // pass A: min / max raw InterPodAffinity sum, max spread count, haveZones, zone max
+  __shared__ int64_t s_pa[9];  // pass A: min / max raw InterPodAffinity sum, max spread count, haveZones, zone max,
+                               // the auxiliary priority's max count, summed count, haveZones, domain max
+  __shared__ unsigned long long s_az[KSIM_PASS_ZONES];  // the auxiliary priority's domain sums (<= 512, host-checked)
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const ksim_pod P = c.one_pod;
@@ -1261,11 +1263,14 @@ __global__ __launch_bounds__(ONE_BLOCK) void ksim_one_kernel(KsimCtx c) {
   IpaNorm ipa0 = ipa;
   ipa0.on = false;
   ipa0.sp = -1;
-  const bool pass_a = ipa.on || ipa.sp >= 0;
+  ipa0.aon = false;
+  const bool pass_a = ipa.on || ipa.sp >= 0 || ipa.aon;
   if (tid < KSIM_NREASONS) s_hist[tid] = 0;
   if (ipa.sp >= 0)
     for (int z = tid; z < c.aff->n_zone; z += ONE_BLOCK) s_z[z] = 0;
-  if (ipa.sp >= 0) __syncthreads();  // (uniform) the zone sums are zero before the atomics
+  if (ipa.ap >= 0)
+    for (int z = tid; z < c.aff->n_adom; z += ONE_BLOCK) s_az[z] = 0;
+  if (ipa.sp >= 0 || ipa.ap >= 0) __syncthreads();  // (uniform) the domain sums are zero before the atomics
 
   bool fit[NPT];
   int64_t sc[NPT];
@@ -1278,7 +1283,7 @@ __global__ __launch_bounds__(ONE_BLOCK) void ksim_one_kernel(KsimCtx c) {
     const KsimAff& A = *c.aff;
     int64_t raw[NPT], cnt[NPT];
     int32_t zz[NPT];
-    int64_t mn = 0, mx = 0, smx = 0, hz = 0;
+    int64_t mn = 0, mx = 0, smx = 0, hz = 0, amx = 0, atot = 0, ahz = 0;
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int64_t i = (int64_t)k * ONE_BLOCK + tid;
@@ -1298,6 +1303,16 @@ __global__ __launch_bounds__(ONE_BLOCK) void ksim_one_kernel(KsimCtx c) {
           if (cnt[k]) atomicAdd(&s_z[zz[k]], (unsigned long long)cnt[k]);
         }
       }
+      if (ipa.ap >= 0) {  // the auxiliary priority (passa_reduce's): max, sum, haveZones, domain sums
+        const int64_t v = A.cnt[A.pair_off[ipa.ap] + i];
+        const int32_t d = ksim_dom(A, A.aux_key, i);
+        amx = v > amx ? v : amx;
+        atot += v;
+        if (d >= 0) {
+          ahz = 1;
+          if (v) atomicAdd(&s_az[d], (unsigned long long)v);
+        }
+      }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -1307,25 +1322,43 @@ __global__ __launch_bounds__(ONE_BLOCK) void ksim_one_kernel(KsimCtx c) {
       mx = b > mx ? b : mx;
       smx = d > smx ? d : smx;
       hz = e > hz ? e : hz;
+      if (ipa.ap >= 0) {
+        const int64_t f = __shfl_xor(amx, o, 64), g = __shfl_xor(atot, o, 64), q = __shfl_xor(ahz, o, 64);
+        amx = f > amx ? f : amx;
+        atot += g;
+        ahz = q > ahz ? q : ahz;
+      }
     }
-    if (lane == 0) { s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz; }
+    if (lane == 0) {
+      s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz;
+      s_v[4][wv] = amx; s_v[5][wv] = atot; s_v[6][wv] = ahz;
+    }
     __syncthreads();
-    if (wv == 0) {  // wave 0: the waves' values, then the zone maximum
+    if (wv == 0) {  // wave 0: the waves' values, then the zone / domain maxima
       const bool in = lane < ONE_WAVES;
       int64_t a = in ? s_v[0][lane] : 0, b = in ? s_v[1][lane] : 0, d = in ? s_v[2][lane] : 0, e = in ? s_v[3][lane] : 0;
-      int64_t zm = 0;
+      int64_t f = in ? s_v[4][lane] : 0, g = in ? s_v[5][lane] : 0, q = in ? s_v[6][lane] : 0;
+      int64_t zm = 0, am = 0;
       if (ipa.sp >= 0)
         for (int z = lane; z < A.n_zone; z += 64) zm = (int64_t)s_z[z] > zm ? (int64_t)s_z[z] : zm;
+      if (ipa.ap >= 0)
+        for (int z = lane; z < A.n_adom; z += 64) am = (int64_t)s_az[z] > am ? (int64_t)s_az[z] : am;
 #pragma unroll
       for (int o = 32; o > 0; o >>= 1) {
         const int64_t a2 = __shfl_xor(a, o, 64), b2 = __shfl_xor(b, o, 64), d2 = __shfl_xor(d, o, 64);
         const int64_t e2 = __shfl_xor(e, o, 64), z2 = __shfl_xor(zm, o, 64);
         a = a2 < a ? a2 : a; b = b2 > b ? b2 : b; d = d2 > d ? d2 : d; e = e2 > e ? e2 : e; zm = z2 > zm ? z2 : zm;
+        const int64_t f2 = __shfl_xor(f, o, 64), g2 = __shfl_xor(g, o, 64), q2 = __shfl_xor(q, o, 64), m2 = __shfl_xor(am, o, 64);
+        f = f2 > f ? f2 : f; g += g2; q = q2 > q ? q2 : q; am = m2 > am ? m2 : am;
       }
-      if (lane == 0) { s_pa[0] = a; s_pa[1] = b; s_pa[2] = d; s_pa[3] = e; s_pa[4] = zm; }
+      if (lane == 0) {
+        s_pa[0] = a; s_pa[1] = b; s_pa[2] = d; s_pa[3] = e; s_pa[4] = zm;
+        s_pa[5] = f; s_pa[6] = g; s_pa[7] = q; s_pa[8] = am;
+      }
     }
     __syncthreads();
     ipa.mn = s_pa[0]; ipa.mx = s_pa[1]; ipa.smx = s_pa[2]; ipa.hz = s_pa[3] != 0; ipa.szmx = s_pa[4];
+    if (ipa.ap >= 0) { ipa.amx = s_pa[5]; ipa.atot = s_pa[6]; ipa.ahz = s_pa[7] != 0; ipa.azmx = s_pa[8]; }
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {  // eval_one's additions, same order
       if (!fit[k]) continue;
@@ -1333,6 +1366,14 @@ __global__ __launch_bounds__(ONE_BLOCK) void ksim_one_kernel(KsimCtx c) {
       if (ipa.sp >= 0) {
         const int64_t v = ksim_spread_score(cnt[k], ipa.smx, ipa.hz, zz[k], zz[k] >= 0 ? (int64_t)s_z[zz[k]] : 0, ipa.szmx);
         sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)ipa.sw * (uint64_t)v);
+      }
+      if (ipa.aon) {  // (count and domain loaded again: no registers held across pass A for them)
+        const int64_t i = (int64_t)k * ONE_BLOCK + tid;
+        const int32_t d = ksim_dom(A, A.aux_key, i);
+        const int64_t v = ipa.ap >= 0 ? A.cnt[A.pair_off[ipa.ap] + i] : 0;
+        const int64_t ds = (ipa.ap >= 0 && d >= 0) ? (int64_t)s_az[d] : 0;
+        sc[k] = (int64_t)((uint64_t)sc[k] +
+                          (uint64_t)ipa.aw * (uint64_t)ksim_aux_score(ipa.akind, v, d, ds, ipa.amx, ipa.atot, ipa.ahz, ipa.azmx));
       }
     }
   }
@@ -1604,9 +1645,10 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   __shared__ int32_t s_cnt[KSIM_WAVES][KSIM_MAX_RCLASS];
   __shared__ int32_t s_fit[KSIM_WAVES];
   __shared__ int32_t s_hist[KSIM_NREASONS];
-  __shared__ int64_t s_v[4][KSIM_WAVES];
+  __shared__ int64_t s_v[7][KSIM_WAVES];
   __shared__ unsigned long long s_z[KSIM_PICK_ZMAX];
-  __shared__ int64_t s_pa[4];
+  __shared__ unsigned long long s_az[KSIM_PICK_ZMAX];  // the auxiliary priority's domain sums
+  __shared__ int64_t s_pa[7];
   __shared__ int64_t s_tv[KSIM_MAX_RCLASS], s_av[KSIM_MAX_RCLASS], s_ad[KSIM_MAX_RCLASS];
   __shared__ int64_t s_bmax[KSIM_MAX_RCLASS];  // this block's max per class (after the decision: the winners')
   __shared__ int32_t s_mode, s_owner, s_rank, s_F, s_ok, s_stat;
@@ -1635,11 +1677,17 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   IpaNorm ipa0 = ipa;
   ipa0.on = false;
   ipa0.sp = -1;
-  const bool pass_a = ipa.on || ipa.sp >= 0;
-  const int NZ = (ipa.sp >= 0) ? c.aff->n_zone : 0;  // <= KSIM_PICK_ZMAX (host-checked)
+  ipa0.aon = false;
+  const bool pass_a = ipa.on || ipa.sp >= 0 || ipa.aon;
+  // pass-A record words: 4 maxima, NZ zone sums, then (a pod with an auxiliary count) 3 words and
+  // NA domain sums; 4 + NZ + 3 + NA <= KSIM_PICK_RA (host-checked)
+  const int NZ = (ipa.sp >= 0) ? c.aff->n_zone : 0;
+  const int NA = (ipa.ap >= 0) ? c.aff->n_adom : 0;
+  const int A0 = 4 + NZ;  // the auxiliary words
+  const bool AX = ipa.ap >= 0;
   __shared__ uint32_t s_dflag;  // the decision is in LDS (wave 0 → the other waves)
   if (tid < KSIM_NREASONS) s_hist[tid] = 0;
-  if (tid < KSIM_PICK_ZMAX) s_z[tid] = 0;
+  if (tid < KSIM_PICK_ZMAX) { s_z[tid] = 0; s_az[tid] = 0; }
   if (tid == 0) { s_ok = 1; s_dflag = 0; s_stat = 0; }
   __syncthreads();
 
@@ -1675,7 +1723,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
     const KsimAff& A = *c.aff;
     int64_t raw[NPT], cnt[NPT];
     int32_t zz[NPT];
-    int64_t mn = 0, mx = 0, smx = 0, hz = 0;
+    int64_t mn = 0, mx = 0, smx = 0, hz = 0, amx = 0, atot = 0, ahz = 0;
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {
       const int64_t i = base + (int64_t)k * KSIM_BLOCK + tid;
@@ -1695,25 +1743,51 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
           if (cnt[k]) atomicAdd(&s_z[zz[k]], (unsigned long long)cnt[k]);
         }
       }
+      if (ipa.ap >= 0) {  // the auxiliary priority (passa_reduce's): max, sum, haveZones, domain sums
+        const int64_t v = A.cnt[A.pair_off[ipa.ap] + i];
+        const int32_t d = ksim_dom(A, A.aux_key, i);
+        amx = v > amx ? v : amx;
+        atot += v;
+        if (d >= 0) {
+          ahz = 1;
+          if (v) atomicAdd(&s_az[d], (unsigned long long)v);
+        }
+      }
     }
     mn = ksimw::min_i64(mn);
     mx = ksimw::max_i64(mx);
     smx = ksimw::max_i64(smx);
     hz = ksimw::max_i64(hz);
-    if (lane == 0) { s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz; }
+    if (ipa.ap >= 0) {  // (uniform)
+      amx = ksimw::max_i64(amx);
+      atot = ksimw::sum_i64(atot);
+      ahz = ksimw::max_i64(ahz);
+    }
+    if (lane == 0) {
+      s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz;
+      s_v[4][wv] = amx; s_v[5][wv] = atot; s_v[6][wv] = ahz;
+    }
     __syncthreads();
-    const int W = 4 + NZ;
+    const int W = A0 + (AX ? 3 + NA : 0);
+    // word x's combine over waves and blocks: 0 = min, 1 = max, 2 = sum
+    const int op = lane == 0 ? 0 : (lane < 4 ? 1 : (lane < A0 ? 2 : (lane == A0 || lane == A0 + 2 ? 1 : 2)));
     if (wv == 1) {
-      // publish: word x = lane x (0..3 the maxima over this block's waves, 4.. the zone sums).
-      // Wave 1 stores, wave 0 polls: a store counts in the storing wave's vmcnt until it is
-      // acknowledged, and the poll's loads would otherwise wait for that acknowledgement too.
+      // publish: word x = lane x (0..3 the maxima over this block's waves, 4.. the zone sums, then
+      // the auxiliary max / sum / haveZones and domain sums).  Wave 1 stores, wave 0 polls: a store
+      // counts in the storing wave's vmcnt until it is acknowledged, and the poll's loads would
+      // otherwise wait for that acknowledgement too.
       int64_t v = 0;
-      if (lane < 4) {
-        v = s_v[lane][0];
-        for (int w = 1; w < KSIM_WAVES; ++w)
-          v = lane == 0 ? (s_v[0][w] < v ? s_v[0][w] : v) : (s_v[lane][w] > v ? s_v[lane][w] : v);
-      } else if (lane - 4 < NZ) {
+      if (lane < 4 || (AX && lane >= A0 && lane < A0 + 3)) {
+        const int row = lane < 4 ? lane : 4 + lane - A0;
+        v = s_v[row][0];
+        for (int w = 1; w < KSIM_WAVES; ++w) {
+          const int64_t x = s_v[row][w];
+          v = op == 0 ? (x < v ? x : v) : (op == 1 ? (x > v ? x : v) : v + x);
+        }
+      } else if (lane < A0) {
         v = (int64_t)s_z[lane - 4];
+      } else if (lane < W) {
+        v = (int64_t)s_az[lane - A0 - 3];
       }
       // every word of the record, not only the W read now: see the record stores below
       pk_store(recA + (int64_t)me * KSIM_PICK_RA + lane, pk_enc(tag, lane < W ? v : 0));
@@ -1735,7 +1809,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
             if (b0 + j >= G) break;
             ok &= pk_tag(wd[j]) == tag;
             const int64_t x = pk_dec(wd[j]);
-            acc = lane == 0 ? (x < acc ? x : acc) : (lane < 4 ? (x > acc ? x : acc) : acc + x);
+            acc = op == 0 ? (x < acc ? x : acc) : (op == 1 ? (x > acc ? x : acc) : acc + x);
           }
         }
         if (__all(ok)) break;
@@ -1743,13 +1817,20 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
         __builtin_amdgcn_s_sleep(1);
       }
       if (lane < 4) s_pa[lane] = acc;
-      else if (lane < W) s_z[lane - 4] = (unsigned long long)acc;
+      else if (lane < A0) s_z[lane - 4] = (unsigned long long)acc;
+      else if (lane < A0 + 3 && AX) s_pa[4 + lane - A0] = acc;
+      else if (lane < W) s_az[lane - A0 - 3] = (unsigned long long)acc;
     }
     __syncthreads();
     ipa.mn = s_pa[0]; ipa.mx = s_pa[1]; ipa.smx = s_pa[2]; ipa.hz = s_pa[3] != 0;
     int64_t zm = 0;  // the zone maximum (over every zone: zeros included, as the scan's pass A)
     for (int z = 0; z < NZ; ++z) zm = (int64_t)s_z[z] > zm ? (int64_t)s_z[z] : zm;
     ipa.szmx = zm;
+    if (AX) {  // (the auxiliary domain maximum likewise)
+      int64_t am = 0;
+      for (int z = 0; z < NA; ++z) am = (int64_t)s_az[z] > am ? (int64_t)s_az[z] : am;
+      ipa.amx = s_pa[4]; ipa.atot = s_pa[5]; ipa.ahz = s_pa[6] != 0; ipa.azmx = am;
+    }
 #pragma unroll
     for (int k = 0; k < NPT; ++k) {  // eval_one's additions, same order
       if (!fit[k]) continue;
@@ -1757,6 +1838,14 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
       if (ipa.sp >= 0) {
         const int64_t v = ksim_spread_score(cnt[k], ipa.smx, ipa.hz, zz[k], zz[k] >= 0 ? (int64_t)s_z[zz[k]] : 0, ipa.szmx);
         sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)ipa.sw * (uint64_t)v);
+      }
+      if (ipa.aon) {  // (count and domain loaded again: no registers held across pass A for them)
+        const int64_t i = base + (int64_t)k * KSIM_BLOCK + tid;
+        const int32_t d = ksim_dom(A, A.aux_key, i);
+        const int64_t v = AX ? A.cnt[A.pair_off[ipa.ap] + i] : 0;
+        const int64_t ds = (AX && d >= 0) ? (int64_t)s_az[d] : 0;
+        sc[k] = (int64_t)((uint64_t)sc[k] +
+                          (uint64_t)ipa.aw * (uint64_t)ksim_aux_score(ipa.akind, v, d, ds, ipa.amx, ipa.atot, ipa.ahz, ipa.azmx));
       }
     }
   }

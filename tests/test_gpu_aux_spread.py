@@ -126,8 +126,8 @@ def test_both_spreading_priorities_match_oracle(seed, fuse, monkeypatch):
 
 
 def test_schedule_one_with_aux_matches_batch():
-    """ksim_schedule_one (+ assume) pod by pod == ksim_schedule with the auxiliary priority: the
-    per-pod call takes the scan kernel (not the single-workgroup one) and zeroes its sums per pass."""
+    """ksim_schedule_one (+ assume) pod by pod == ksim_schedule with the auxiliary priority (18
+    nodes: the single-workgroup kernel, its pass A in LDS)."""
     import ctypes as C
     nodes, running, pods, objs = rnd_spread_workload(1, n_pods=60)
     order = list(reversed(pods))
@@ -176,3 +176,68 @@ def test_aux_at_scale_matches_c_oracle():
         assert g.last_node_index == ctr
     finally:
         g.close()
+
+
+PER_POD_FORMS = {
+    "one_wg": {},                                            # <= 1,024 nodes: the single-workgroup kernel
+    "resident": {"KSIM_ONE_WG": "0"},                        # the pick body in the resident kernel
+    "scan": {"KSIM_ONE_WG": "0", "KSIM_NO_PICK": "1"},       # the multi-block scan with its pass A
+}
+
+
+def _aux_setup(kind, seed):
+    """(workload, aux, prios, custom) of one auxiliary-priority family."""
+    if kind == "saa_zone":
+        return rnd_spread_workload(seed, n_pods=60), ("service_anti_affinity", ZONE), _saa_prios(seed), \
+            {"SAA": ("serviceAntiAffinity", ZONE)}
+    if kind == "saa_rack":  # 600 nodes (3 pick blocks), 40 rack domains next to the spread zones
+        import random
+        rng = random.Random(90 + seed)
+        w = rnd_spread_workload(seed, n_nodes=600, n_pods=80, n_running=60)
+        for x in w[0]:
+            if rng.random() < 0.7:
+                x["metadata"]["labels"]["rack"] = "r%d" % rng.randrange(40)
+        prios = [("SAA", 4), ("SelectorSpreadPriority", 1), ("LeastRequestedPriority", 1)]
+        return w, ("service_anti_affinity", "rack"), prios, {"SAA": ("serviceAntiAffinity", "rack")}
+    prios = [("SelectorSpreadPriority", 1), ("ServiceSpreadingPriority", 2 + seed), ("LeastRequestedPriority", 1)]
+    return rnd_spread_workload(seed, n_pods=60, zones=seed != 1), ("service_spreading",), prios, None
+
+
+@pytest.mark.parametrize("pattern", ["assume", "adapter"])
+@pytest.mark.parametrize("form", sorted(PER_POD_FORMS))
+@pytest.mark.parametrize("kind", ["saa_zone", "saa_rack", "service_spreading"])
+@pytest.mark.parametrize("seed", range(2))
+def test_per_pod_forms_with_aux_match_batch(seed, kind, form, pattern, monkeypatch, capfd):
+    """Every per-pod form reads the auxiliary priority: the single-workgroup kernel's pass A in LDS,
+    the pick / resident kernels' pass-A record words (3 words and the domain sums after the spread
+    zones), the scan's own pass A — placements and lastNodeIndex == the batch's.  adapter:
+    SCHEDULE_ONLY (a tentative commit on the resident kernel), then ksim_pod_add onto the node."""
+    import ctypes as C
+    for k, v in PER_POD_FORMS[form].items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("KSIM_SERVE_STATS", "1")
+    (nodes, running, pods, objs), aux, prios, custom = _aux_setup(kind, seed)
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order, spread=spread.SpreadListers(**objs), aux=aux)
+    assert cl.aux_active
+    preds, _ = scheduler.provider("DefaultProvider")
+    batch = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH, custom_priorities=custom)
+    one = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH, custom_priorities=custom)
+    ports, sc = cl.pod_ports, cl.pod_scalars
+    try:
+        out, _, _ = batch.schedule()
+        for k in range(len(order)):
+            pod = abi.Pod.from_buffer_copy(cl.pods[k].tobytes())
+            res = abi.Result()
+            one.h.call("ksim_schedule_one", C.byref(pod), abi.vptr(ports), len(ports), abi.vptr(sc), len(sc),
+                       abi.SCHEDULE_ASSUME if pattern == "assume" else abi.SCHEDULE_ONLY, C.byref(res))
+            assert res.node == out[k], k
+            if pattern == "adapter" and res.node >= 0:
+                one.h.call("ksim_pod_add", int(res.node), C.byref(pod), abi.vptr(ports), len(ports), abi.vptr(sc), len(sc))
+        assert one.last_node_index == batch.last_node_index
+    finally:
+        batch.close()
+        one.close()
+    # the form ran: the resident kernel took messages exactly in the resident form
+    served = "[ksim serve]" in capfd.readouterr().err
+    assert served == (form == "resident")

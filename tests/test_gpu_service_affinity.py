@@ -125,7 +125,7 @@ PER_POD_FORMS = {
 @pytest.mark.parametrize("form", sorted(PER_POD_FORMS))
 @pytest.mark.parametrize("variant", ["consistent", "mixed_labels", "conflicting_running"])
 @pytest.mark.parametrize("seed", range(2))
-def test_per_pod_forms_with_service_affinity_match_batch(seed, variant, form, pattern, monkeypatch):
+def test_per_pod_forms_with_service_affinity_match_batch(seed, variant, form, pattern, monkeypatch, capfd):
     """Every per-pod form evaluates the lender check on the global counts the previous commit left
     (ksim_svc_lender) and records the lenders' disagreements at its commit (ksim_svc_commit):
     placements and lastNodeIndex == the batch's; KSIM_E_UNSUPPORTED exactly when the batch refuses.
@@ -134,6 +134,7 @@ def test_per_pod_forms_with_service_affinity_match_batch(seed, variant, form, pa
     import ctypes as C
     for k, v in PER_POD_FORMS[form].items():
         monkeypatch.setenv(k, v)
+    monkeypatch.setenv("KSIM_SERVE_STATS", "1")
     aff_labels = ["region", "rack"]
     nodes, running, pods, services = rnd_svc_affinity_workload(seed, n_pods=60, mixed_labels=variant == "mixed_labels",
                                                                conflicting_running=variant == "conflicting_running",
@@ -178,3 +179,6 @@ def test_per_pod_forms_with_service_affinity_match_batch(seed, variant, form, pa
     finally:
         batch.close()
         one.close()
+    # the form ran: the resident kernel took messages exactly in the resident form
+    served = "[ksim serve]" in capfd.readouterr().err
+    assert served == (form == "resident")
