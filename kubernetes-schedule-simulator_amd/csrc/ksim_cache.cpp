@@ -880,7 +880,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
         // (KSIM_TENTATIVE=0: decide only).  Not with the service-affinity lender tables: a commit
         // records its label disagreements (ksim_svc_commit), which no undo takes back.
         static const bool tent_off = getenv("KSIM_TENTATIVE") && getenv("KSIM_TENTATIVE")[0] == '0';
-        const bool svc = ksim_rt_launch_tables(h);  // (aux is off on this path)
+        const bool svc = ksim_rt_svc_lender_on(h);
         const int32_t nc = assume ? 0 : (!tent_off && !svc ? KSIM_SERVE_TENTATIVE : 1);
         int32_t r[KSIM_RES_WORDS];
         if ((rc = serve_post(h, KSIM_SERVE_SCHEDULE, sp, ports + pod->port_off, scalars + pod->scalar_off, nc, -1, h->pick_tag,

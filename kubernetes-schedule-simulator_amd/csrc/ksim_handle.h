@@ -387,10 +387,12 @@ int ksim_rt_pick_npt(int64_t n);
 inline bool ksim_rt_aux_on(const ksim_handle* h) {
   return h->have_aff && h->aff_h.aux_pair != nullptr && h->aff_h.aux_w != 0 && !h->ctx.no_prio;
 }
-// ... and the service-affinity lender check (ksim_affinity_tables.svc_*).
-inline bool ksim_rt_launch_tables(const ksim_handle* h) {
-  return ksim_rt_aux_on(h) || (h->have_aff && h->aff_h.svc_class != nullptr && (h->ctx.preds & KSIM_P_SERVICE_AFFINITY));
+// The service-affinity lender check (ksim_affinity_tables.svc_*).
+inline bool ksim_rt_svc_lender_on(const ksim_handle* h) {
+  return h->have_aff && h->aff_h.svc_class != nullptr && (h->ctx.preds & KSIM_P_SERVICE_AFFINITY);
 }
+// Either of them.
+inline bool ksim_rt_launch_tables(const ksim_handle* h) { return ksim_rt_aux_on(h) || ksim_rt_svc_lender_on(h); }
 // Pod classes with more than KSIM_MAX_RCLASS reduce classes (the launch form's wide decision).
 bool wide_k(const ksim_handle* h, int32_t cls);
 int ksim_rt_check_launch_ctx(ksim_handle* h, const KsimCtx& c, int grid, const char* where);

@@ -28,6 +28,9 @@
 #define PGF_SHARED 4  // its commit changes counts in a topology domain several nodes share
 #define PGF_VOL 8     // has a volume class
 #define PGF_NOHYP 16  // its commit leaves the rows' LDS image (gpu / ephemeral / scalar requests, shared domains)
+#define PGF_AUX 32    // reads the auxiliary priority (ksim_affinity_tables.aux_*); its counted pair + 1 in
+                      // bits 8.. (0: none — serviceAntiAffinity still scores by the row's label)
+#define PGF_AUX_SHIFT 8
 
 struct PgHdr {
   int32_t K, k1, k2, sp;  // reduce classes (K = k1 * k2), SelectorSpread pair or -1
@@ -125,3 +128,4 @@ extern "C" size_t ksim_pgen_plan(int64_t chunk, const PgDims* d, uint32_t* off);
 extern "C" size_t ksim_pgen_lds_budget(void);
 extern "C" size_t ksim_pgen_gran_bytes(void);
 extern "C" int ksim_pgen_max_zones(void);
+extern "C" int ksim_pgen_max_aux_domains(void);

@@ -47,7 +47,10 @@
 #define PG_NSLOT 4
 #define PG_MAXG 256
 #define PG_MAXZ 28
-#define PG_RA (4 + PG_MAXZ)  // words of a pass-A record
+// words of a pass-A record: min, max, max count, haveZones, the spread zone sums, then the
+// auxiliary priority's max count, summed count, haveZones and domain sums
+#define PG_MAXAD 64  // the auxiliary priority's domains
+#define PG_RA (4 + PG_MAXZ + 3 + PG_MAXAD)
 #define PG_MAXL 256          // longest counted-pair / carry list of a pod (shared-domain commit)
 // exchange buffer: pass-A records, class granules, then one commit word per slot
 #define PG_COMMIT_OFF ((int64_t)PG_NSLOT * (PG_RA + KSIM_MAX_RCLASS) * PG_MAXG)
@@ -552,6 +555,10 @@ __global__ __launch_bounds__(64) void ksim_pgen_pack_kernel(KsimCtx c, PGenArgs 
     const bool aff = g.has_aff && (P.aff_ident > 0 || P.aff_class > 0);
     const int32_t* ac = (aff && P.aff_class > 0) ? g.A.ac + 6 * (int64_t)(P.aff_class - 1) : nullptr;
     H.sp = (g.has_aff && !c.no_prio && c.w[KSIM_W_SELECTOR_SPREAD] != 0) ? ksim_spread_pair(g.A, P) : -1;
+    if (g.has_aff && !c.no_prio && g.A.aux_pair && g.A.aux_w != 0) {  // (ipa_norm's aon / ap)
+      const int32_t ap = ksim_aux_pair(g.A, P);
+      if (ap >= 0 || g.A.aux_kind == KSIM_AUX_SERVICE_ANTI) H.fl |= PGF_AUX | ((ap + 1) << PGF_AUX_SHIFT);
+    }
     int32_t a0 = 0, p0 = 0, m0 = 0;
     if (aff && P.aff_ident > 0) {
       const int32_t id = P.aff_ident - 1;
@@ -624,10 +631,13 @@ __global__ __launch_bounds__(64) void ksim_pgen_pack_kernel(KsimCtx c, PGenArgs 
 template <int NPT, int MB>
 __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArgs g_arg) {
   extern __shared__ __attribute__((aligned(16))) char pg_smem[];
-  __shared__ int64_t s_a[4][PG_NW];                  // pass A per wave: min, max, max count, haveZones
+  __shared__ int64_t s_a[7][PG_NW];                  // pass A per wave: min, max, max count, haveZones, aux max / sum / haveZones
   __shared__ unsigned long long s_z[PG_MAXZ];        // pass A zone sums of this workgroup
-  __shared__ int64_t s_g[5];                         // pass A over the grid: min, max, max count, haveZones, max zone
+  __shared__ unsigned long long s_az[PG_MAXAD];      // the auxiliary priority's domain sums of this workgroup
+  __shared__ int64_t s_g[9];                         // pass A over the grid: min, max, max count, haveZones, max zone,
+                                                     // aux max count, summed count, haveZones, max domain sum
   __shared__ int64_t s_gz[PG_MAXZ];                  // countsByZone over the grid
+  __shared__ int64_t s_gaz[PG_MAXAD];                // the auxiliary domain sums over the grid
   __shared__ int32_t s_mx[PG_NW][KSIM_MAX_RCLASS];   // class partials per wave
   __shared__ int32_t s_cn[PG_NW][KSIM_MAX_RCLASS];
   __shared__ int32_t s_fit[PG_NW];
@@ -665,6 +675,7 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
   }
   if (tid == 0) s_abort = 0;
   if (tid < PG_MAXZ) s_z[tid] = 0;
+  if (tid < PG_MAXAD) s_az[tid] = 0;
   uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex (wave 0)
   __syncthreads();
   pg_stage_counts(c, g, L, nrows, chunk, tid, blockDim.x);
@@ -680,6 +691,8 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
     const int K = H.K, k1 = H.k1, k2 = H.k2;
     const bool ipa = (H.fl & PGF_IPA) != 0;
     const int32_t sp = H.sp;
+    const bool aon = (H.fl & PGF_AUX) != 0;
+    const int32_t ap = (H.fl >> PGF_AUX_SHIFT) - 1;  // (-1 without PGF_AUX too)
     const uint32_t tag = (uint32_t)((pod - c.first + 1) & 0xFF);
     const int slot = (int)(pod % PG_NSLOT);
     // waves 1-3: pod p+1's record, loaded now and stored into the other LDS record during the
@@ -726,9 +739,10 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
     }
     PG_STAMP(0);
 
-    // ---- 2. pass A over the grid (pods that read InterPodAffinity / SelectorSpread) ----
-    if (ipa || sp >= 0) {
-      int64_t mn = 0, mx = 0, smx = 0, hz = 0;
+    // ---- 2. pass A over the grid (pods that read InterPodAffinity / SelectorSpread / the
+    //         auxiliary priority) ----
+    if (ipa || sp >= 0 || ap >= 0) {
+      int64_t mn = 0, mx = 0, smx = 0, hz = 0, amx = 0, atot = 0, ahz = 0;
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
         if (!fit[k]) continue;
@@ -739,31 +753,58 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
           hz = 1;
           if (cnt[k]) atomicAdd(&s_z[zz[k]], (unsigned long long)cnt[k]);
         }
+        if (ap >= 0) {  // the auxiliary priority (passa_reduce's): max, sum, haveZones, domain sums
+          const int32_t j = k * PG_BS + tid;
+          const int64_t v = L.cnt[(int64_t)ap * chunk + j];
+          const int32_t d = L.dom[(int64_t)g.A.aux_key * chunk + j];
+          amx = v > amx ? v : amx;
+          atot += v;
+          if (d >= 0) {
+            ahz = 1;
+            if (v) atomicAdd(&s_az[d], (unsigned long long)v);
+          }
+        }
       }
       if (ipa) { mn = ksimw::min_i64(mn); mx = ksimw::max_i64(mx); }
       if (sp >= 0) { smx = ksimw::max_i32((int32_t)smx); hz = __ballot(hz != 0) ? 1 : 0; }
-      if (lane == 0) { s_a[0][wv] = mn; s_a[1][wv] = mx; s_a[2][wv] = smx; s_a[3][wv] = hz; }
+      if (ap >= 0) { amx = ksimw::max_i64(amx); atot = ksimw::sum_i64(atot); ahz = __ballot(ahz != 0) ? 1 : 0; }
+      if (lane == 0) {
+        s_a[0][wv] = mn; s_a[1][wv] = mx; s_a[2][wv] = smx; s_a[3][wv] = hz;
+        s_a[4][wv] = amx; s_a[5][wv] = atot; s_a[6][wv] = ahz;
+      }
       __syncthreads();
       PG_STAMP(6);
       if (wv == 0) {
         const int nz = sp >= 0 ? g.n_zone : 0;
-        const int RA = 4 + nz;
-        // publish this workgroup's record (lane w = word w), tagged; the zone sums are reset
-        // for the next pod by the same lane that read them
+        const int na = ap >= 0 ? g.A.n_adom : 0;  // <= PG_MAXAD (host-checked)
+        const int A0 = 4 + nz;                     // the auxiliary words
+        const int RA = A0 + (ap >= 0 ? 3 + na : 0);
+        // word w's combine: 0 = min, 1 = max, 2 = sum
+        auto wop = [&](int w) { return w == 0 ? 0 : (w < 4 ? 1 : (w < A0 ? 2 : (w == A0 || w == A0 + 2 ? 1 : 2))); };
+        // publish this workgroup's record (lane w = word w), tagged; the zone / domain sums are
+        // reset for the next pod by the same lane that read them
         if (lane < RA) {
           int64_t v;
-          if (lane < 4) {
-            v = s_a[lane][0];
+          if (lane < 4 || (lane >= A0 && lane < A0 + 3)) {
+            const int row = lane < 4 ? lane : 4 + lane - A0;
+            const int op = wop(lane);
+            v = s_a[row][0];
 #pragma unroll
-            for (int w = 1; w < PG_NW; ++w) v = lane == 0 ? (s_a[0][w] < v ? s_a[0][w] : v) : (s_a[lane][w] > v ? s_a[lane][w] : v);
-          } else {
+            for (int w = 1; w < PG_NW; ++w) {
+              const int64_t x = s_a[row][w];
+              v = op == 0 ? (x < v ? x : v) : (op == 1 ? (x > v ? x : v) : v + x);
+            }
+          } else if (lane < A0) {
             v = (int64_t)s_z[lane - 4];
             s_z[lane - 4] = 0;
+          } else {
+            v = (int64_t)s_az[lane - A0 - 3];
+            s_az[lane - A0 - 3] = 0;
           }
           pg_store(rec_at(g.gran, slot, lane, blockIdx.x), ((uint64_t)tag << 56) | ((uint64_t)(v + B55) & M56));
         }
         // sweep every record: lane l reads workgroups l, l + 64, ...; batches of 8 words
-        int64_t a_mn = 0, a_mx = 0, a_smx = 0, a_hz = 0;
+        int64_t a_mn = 0, a_mx = 0, a_smx = 0, a_hz = 0, a_amx = 0, a_atot = 0, a_ahz = 0;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         bool ok = true;
         for (int w0 = 0; w0 < RA && ok; w0 += 8) {
@@ -787,22 +828,29 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
           for (int u = 0; u < 8; ++u) {
             const int word = w0 + u;
             if (word >= RA) break;
-            int64_t acc = word == 0 ? INT64_MAX : (word < 4 ? INT64_MIN : 0);
+            const int op = wop(word);
+            int64_t acc = op == 0 ? INT64_MAX : (op == 1 ? INT64_MIN : 0);
 #pragma unroll
             for (int m = 0; m < MB; ++m) {
               if (lane + 64 * m >= G) continue;
               const int64_t x = (int64_t)(v[u][m] & M56) - B55;
-              if (word == 0) acc = x < acc ? x : acc;
-              else if (word < 4) acc = x > acc ? x : acc;
+              if (op == 0) acc = x < acc ? x : acc;
+              else if (op == 1) acc = x > acc ? x : acc;
               else acc += x;
             }
             if (word == 0) a_mn = ipa ? ksimw::min_i64(acc) : 0;
             else if (word == 1) a_mx = ipa ? ksimw::max_i64(acc) : 0;
             else if (word == 2) a_smx = sp >= 0 ? ksimw::max_i64(acc) : 0;
             else if (word == 3) a_hz = sp >= 0 ? ksimw::max_i64(acc) : 0;
-            else {
+            else if (word < A0) {
               const int64_t zsum = ksimw::sum_i64(acc);
               if (lane == 0) s_gz[word - 4] = zsum;
+            } else if (word == A0) a_amx = ksimw::max_i64(acc);
+            else if (word == A0 + 1) a_atot = ksimw::sum_i64(acc);
+            else if (word == A0 + 2) a_ahz = ksimw::max_i64(acc);
+            else {
+              const int64_t dsum = ksimw::sum_i64(acc);
+              if (lane == 0) s_gaz[word - A0 - 3] = dsum;
             }
           }
         }
@@ -815,11 +863,15 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
           int64_t zm = 0;
           for (int z = 0; z < nz; ++z) zm = s_gz[z] > zm ? s_gz[z] : zm;
           s_g[4] = zm;
+          int64_t am = 0;  // (over every domain: zeros included, as passa_reduce)
+          for (int z = 0; z < na; ++z) am = s_gaz[z] > am ? s_gaz[z] : am;
+          s_g[5] = a_amx; s_g[6] = a_atot; s_g[7] = a_ahz; s_g[8] = am;
         }
       }
       __syncthreads();
       if (s_abort) { stop_pod = pod; break; }
       const int64_t gmn = s_g[0], gmx = s_g[1], gsmx = s_g[2], ghz = s_g[3], gzm = s_g[4];
+      const int64_t gamx = s_g[5], gatot = s_g[6], gahz = s_g[7], gazm = s_g[8];
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
         if (!fit[k]) continue;
@@ -830,6 +882,22 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
           sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)c.w[KSIM_W_SELECTOR_SPREAD] *
                                                   (uint64_t)ksim_spread_score(cnt[k], gsmx, ghz != 0, zz[k],
                                                                               zz[k] >= 0 ? s_gz[zz[k]] : 0, gzm));
+        if (ap >= 0) {  // (aux_add's; count and domain from the rows' LDS image)
+          const int32_t j = k * PG_BS + tid;
+          const int32_t d = L.dom[(int64_t)g.A.aux_key * chunk + j];
+          const int64_t v = L.cnt[(int64_t)ap * chunk + j];
+          const int64_t ds = d >= 0 ? s_gaz[d] : 0;
+          sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)g.A.aux_w * (uint64_t)ksim_aux_score(g.A.aux_kind, v, d, ds, gamx, gatot,
+                                                                                           gahz != 0, gazm));
+        }
+      }
+    }
+    if (aon && ap < 0) {  // serviceAntiAffinity of a pod no service selects: 10 on a labelled row (no pass A)
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        if (!fit[k]) continue;
+        const int32_t d = L.dom[(int64_t)g.A.aux_key * chunk + k * PG_BS + tid];
+        sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)g.A.aux_w * (uint64_t)ksim_aux_score(g.A.aux_kind, 0, d, 0, 0, 0, false, 0));
       }
     }
     PG_STAMP(1);
@@ -2130,6 +2198,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
 
 extern "C" size_t ksim_pgen_gran_bytes(void) { return (size_t)PG_GRAN_WORDS * sizeof(uint64_t); }
 extern "C" int ksim_pgen_max_zones(void) { return PG_MAXZ; }
+extern "C" int ksim_pgen_max_aux_domains(void) { return PG_MAXAD; }
 extern "C" size_t ksim_pgen_lds_budget(void) { return PG_LDS_BUDGET; }
 
 // LDS layout for `chunk` rows per workgroup (the kernel rebuilds its pointers from off[]).

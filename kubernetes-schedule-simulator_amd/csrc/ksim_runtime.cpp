@@ -860,16 +860,24 @@ struct PgPlan {
 
 static bool pgen_plan(ksim_handle* h, PgPlan* pl, bool allow_v2 = true) {
   const KsimCtx& c = h->ctx;
-  if (getenv("KSIM_NO_PGEN") || h->pgen_off || h->shard.world > 1 || c.n <= 0 || ksim_rt_launch_tables(h)) return false;
+  if (getenv("KSIM_NO_PGEN") || h->pgen_off || h->shard.world > 1 || c.n <= 0 || ksim_rt_svc_lender_on(h)) return false;
+  const bool aux = ksim_rt_aux_on(h);
   int64_t s = 0;
   for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED, KSIM_W_INTERPOD_AFFINITY,
                 KSIM_W_SELECTOR_SPREAD}) {
     if (c.w[k] > ((int64_t)1 << 30)) return false;
     s += c.w[k] * 10;
   }
+  if (aux) {
+    if (h->aff_h.aux_w > ((int64_t)1 << 30)) return false;
+    s += h->aff_h.aux_w * 10;
+  }
   if (s >= ((int64_t)1 << 31)) return false;
   if (h->have_aff) {
     if (c.w[KSIM_W_SELECTOR_SPREAD] && h->aff_n_zone > ksim_pgen_max_zones()) return false;
+    // the auxiliary priority: its domain sums in one pass-A record, single-hypothesis kernel only
+    if (aux && h->aff_h.n_adom > ksim_pgen_max_aux_domains()) return false;
+    if (aux) allow_v2 = false;
     if (h->pg_max_mp + h->pg_max_car > 512) return false;  // the shared-domain commit's list
   }
   // the pod-context record bound (ksim_pgen.h): the longest list of every kind
@@ -1086,8 +1094,9 @@ static int run_f3_range(ksim_handle* h, int64_t first, int64_t count, ksim_stats
 
 static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   KsimCtx& c = h->ctx;
-  // inter-pod affinity, volume and service-affinity pods: the general persistent kernel (or the launch form)
-  if (ksim_rt_launch_only_count(h, first, count)) return run_f3_range(h, first, count, st);
+  // inter-pod affinity, volume and service-affinity pods, and every pod under the auxiliary
+  // priority: the general persistent kernel (or the launch form)
+  if (ksim_rt_aux_on(h) || ksim_rt_launch_only_count(h, first, count)) return run_f3_range(h, first, count, st);
   int grid = 0, lds_rows = 0;
   if (const int form = pfast_form(h, first, count, &grid, &lds_rows)) {
     int rc = run_pfast_mode(h, first, count, grid, lds_rows, form == 2, st);
@@ -1183,7 +1192,9 @@ static int run_persistent_mode(ksim_handle* h, int64_t first, int64_t count, ksi
 // kernel can take the range), else the launch form.
 static int run_auto_mode(ksim_handle* h, int64_t first, int64_t count, ksim_stats* st) {
   int g, l;
-  if (ksim_rt_launch_only_count(h, first, count)) {
+  // (the auxiliary priority: every pod to the general kernels — a serviceAntiAffinity priority
+  // scores pods no service selects too)
+  if (ksim_rt_aux_on(h) || ksim_rt_launch_only_count(h, first, count)) {
     h->tree_valid = false;
     return run_f3_range(h, first, count, st);
   }
@@ -1384,9 +1395,12 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
       return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded run stopped: a node's quantities left the exact float64 range");
     }
   } else {
-  // the auxiliary priority and the service-affinity lender check (ksim_affinity_tables.aux_* / svc_*)
-  // are read by the launch-form kernels alone
-  const int mode = (ksim_rt_launch_tables(h) || ksim_rt_range_wide(h, first, count)) ? KSIM_MODE_LAUNCH : h->cfg.mode;
+  // the service-affinity lender check (ksim_affinity_tables.svc_*) is read by the launch-form
+  // kernels alone; the auxiliary priority (aux_*) by them and the general persistent kernel (tree
+  // mode, for pods without it, gives way to the automatic choice)
+  const int mode = (ksim_rt_svc_lender_on(h) || ksim_rt_range_wide(h, first, count)) ? KSIM_MODE_LAUNCH
+                   : (ksim_rt_aux_on(h) && h->cfg.mode == KSIM_MODE_TREE) ? KSIM_MODE_AUTO
+                                                                           : h->cfg.mode;
   int rc = mode == KSIM_MODE_TREE         ? run_tree_mode(h, first, count, st)
            : mode == KSIM_MODE_AUTO       ? run_auto_mode(h, first, count, st)
            : mode == KSIM_MODE_PERSISTENT ? run_persistent_mode(h, first, count, st)

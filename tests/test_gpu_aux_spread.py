@@ -8,7 +8,8 @@ second spreading priority a Policy can configure next to SelectorSpread:
 - ServiceSpreadingPriority configured together with SelectorSpreadPriority (the services-only
   selectors as the auxiliary pair, zones from utilnode.GetZoneKey), the same way.
 
-Both launch forms (pass A fused into the scan, and as its own launch) and the per-pod call."""
+Both launch forms (pass A fused into the scan, and as its own launch), the general persistent
+kernel (ksim_pgen.hip: the auxiliary words of its pass-A record) and every per-pod form."""
 import copy
 
 import pytest
@@ -73,7 +74,8 @@ def _saa_prios(seed):
 
 
 def _run(nodes, running, pods, preds, prios, lst, aux, custom=None, mode=abi.MODE_AUTO):
-    """The simulator's loop (LIFO queue) through GenericScheduler on a cluster with `aux`."""
+    """The simulator's loop (LIFO queue) through GenericScheduler on a cluster with `aux`, in `mode`
+    (the launch form, or the general persistent kernel)."""
     order = list(reversed(pods))
     cl = ingest.Cluster.from_objects(nodes, running, order, spread=lst, aux=aux)
     assert cl.aux_active
@@ -83,7 +85,7 @@ def _run(nodes, running, pods, preds, prios, lst, aux, custom=None, mode=abi.MOD
         lni = g.last_node_index
     finally:
         g.close()
-    assert st.mode == abi.MODE_LAUNCH   # the auxiliary priority is read by the launch form alone
+    assert st.mode == (abi.MODE_LAUNCH if mode == abi.MODE_LAUNCH else abi.MODE_PERSISTENT), st.mode
     rep = scheduler.Report()
     for k, w in enumerate(out):
         if w >= 0:
@@ -94,33 +96,35 @@ def _run(nodes, running, pods, preds, prios, lst, aux, custom=None, mode=abi.MOD
     return rep
 
 
-@pytest.mark.parametrize("fuse", ["fused", "two_launch"])
+@pytest.mark.parametrize("fuse", ["fused", "two_launch", "persistent"])
 @pytest.mark.parametrize("seed", range(4))
 def test_service_anti_affinity_simulation_matches_oracle(seed, fuse, monkeypatch):
     if fuse == "two_launch":
         monkeypatch.setenv("KSIM_FUSE_A", "0")
+    mode = abi.MODE_PERSISTENT if fuse == "persistent" else abi.MODE_LAUNCH
     nodes, running, pods, objs = rnd_spread_workload(seed, zones=seed != 3)
     preds, _ = scheduler.provider("DefaultProvider")
     prios = _saa_prios(seed)
     want, want_lni = R.simulate(nodes, running, pods, set(preds), list(prios), spread=R.SpreadListers(**objs),
                                 custom_priorities={"SAA": R.service_anti_affinity_priority(ZONE, R.SpreadListers(**objs))})
     rep = _run(nodes, running, pods, preds, prios, spread.SpreadListers(**objs), ("service_anti_affinity", ZONE),
-               custom={"SAA": ("serviceAntiAffinity", ZONE)})
+               custom={"SAA": ("serviceAntiAffinity", ZONE)}, mode=mode)
     _check(rep, want, want_lni)
 
 
-@pytest.mark.parametrize("fuse", ["fused", "two_launch"])
+@pytest.mark.parametrize("fuse", ["fused", "two_launch", "persistent"])
 @pytest.mark.parametrize("seed", range(4))
 def test_both_spreading_priorities_match_oracle(seed, fuse, monkeypatch):
     """Through ClusterCapacity, which builds the cluster with the auxiliary pair itself."""
     if fuse == "two_launch":
         monkeypatch.setenv("KSIM_FUSE_A", "0")
+    mode = abi.MODE_PERSISTENT if fuse == "persistent" else abi.MODE_LAUNCH
     nodes, running, pods, objs = rnd_spread_workload(seed, zones=seed != 3)
     preds = list(scheduler.DEFAULT_PREDICATES)
     prios = [("SelectorSpreadPriority", 1), ("ServiceSpreadingPriority", 2 + seed), ("LeastRequestedPriority", 1)]
     want, want_lni = R.simulate(nodes, running, pods, set(preds), list(prios), spread=R.SpreadListers(**objs))
     cc = scheduler.ClusterCapacity(nodes, running, pods, predicates=preds, priorities=prios,
-                                   spread=spread.SpreadListers(**objs))
+                                   spread=spread.SpreadListers(**objs), mode=mode)
     assert cc.cluster.aux_active
     _check(cc.run(), want, want_lni)
 
@@ -153,91 +157,32 @@ def test_schedule_one_with_aux_matches_batch():
 
 
 def test_aux_at_scale_matches_c_oracle():
-    """2,000 nodes x 3,000 pods (8 blocks per pod, zone sums across blocks) against the C oracle."""
+    """2,000 nodes x 3,000 pods (8 blocks per pod, zone sums across blocks) against the C oracle, in
+    the launch form and the general persistent kernel (several workgroups' domain sums: 40 rack
+    domains; 80 exceed its pass-A record, and the persistent request runs in the launch form)."""
     import cpu_ref
     import random
-    rng = random.Random(77)
-    nodes, running, pods, objs = rnd_spread_workload(5, n_nodes=2000, n_pods=3000, n_running=400)
-    for x in nodes:
-        if rng.random() < 0.7:
-            x["metadata"]["labels"]["rack"] = "r%d" % rng.randrange(40)
-    order = list(reversed(pods))
-    lst = spread.SpreadListers(**objs)
-    preds, _ = scheduler.provider("DefaultProvider")
-    prios = [("SAA", 4), ("SelectorSpreadPriority", 1), ("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
-    custom = {"SAA": ("serviceAntiAffinity", "rack")}
-    cl = ingest.Cluster.from_objects(nodes, running, order, spread=lst, aux=("service_anti_affinity", "rack"))
-    p = scheduler.plan(cl, preds, prios, custom_priorities=custom)
-    want, _, _, ctr, _ = cpu_ref.run(cl, None, threads=8, plan=p)
-    g = scheduler.GenericScheduler(cl, preds, prios, custom_priorities=custom)
-    try:
-        out, _, _ = g.schedule()
-        assert (out == want).all(), int((out != want).argmax())
-        assert g.last_node_index == ctr
-    finally:
-        g.close()
-
-
-PER_POD_FORMS = {
-    "one_wg": {},                                            # <= 1,024 nodes: the single-workgroup kernel
-    "resident": {"KSIM_ONE_WG": "0"},                        # the pick body in the resident kernel
-    "scan": {"KSIM_ONE_WG": "0", "KSIM_NO_PICK": "1"},       # the multi-block scan with its pass A
-}
-
-
-def _aux_setup(kind, seed):
-    """(workload, aux, prios, custom) of one auxiliary-priority family."""
-    if kind == "saa_zone":
-        return rnd_spread_workload(seed, n_pods=60), ("service_anti_affinity", ZONE), _saa_prios(seed), \
-            {"SAA": ("serviceAntiAffinity", ZONE)}
-    if kind == "saa_rack":  # 600 nodes (3 pick blocks), 40 rack domains next to the spread zones
-        import random
-        rng = random.Random(90 + seed)
-        w = rnd_spread_workload(seed, n_nodes=600, n_pods=80, n_running=60)
-        for x in w[0]:
+    for racks in (40, 80):
+        rng = random.Random(77)
+        nodes, running, pods, objs = rnd_spread_workload(5, n_nodes=2000, n_pods=3000 if racks == 40 else 600,
+                                                         n_running=400)
+        for x in nodes:
             if rng.random() < 0.7:
-                x["metadata"]["labels"]["rack"] = "r%d" % rng.randrange(40)
-        prios = [("SAA", 4), ("SelectorSpreadPriority", 1), ("LeastRequestedPriority", 1)]
-        return w, ("service_anti_affinity", "rack"), prios, {"SAA": ("serviceAntiAffinity", "rack")}
-    prios = [("SelectorSpreadPriority", 1), ("ServiceSpreadingPriority", 2 + seed), ("LeastRequestedPriority", 1)]
-    return rnd_spread_workload(seed, n_pods=60, zones=seed != 1), ("service_spreading",), prios, None
-
-
-@pytest.mark.parametrize("pattern", ["assume", "adapter"])
-@pytest.mark.parametrize("form", sorted(PER_POD_FORMS))
-@pytest.mark.parametrize("kind", ["saa_zone", "saa_rack", "service_spreading"])
-@pytest.mark.parametrize("seed", range(2))
-def test_per_pod_forms_with_aux_match_batch(seed, kind, form, pattern, monkeypatch, capfd):
-    """Every per-pod form reads the auxiliary priority: the single-workgroup kernel's pass A in LDS,
-    the pick / resident kernels' pass-A record words (3 words and the domain sums after the spread
-    zones), the scan's own pass A — placements and lastNodeIndex == the batch's.  adapter:
-    SCHEDULE_ONLY (a tentative commit on the resident kernel), then ksim_pod_add onto the node."""
-    import ctypes as C
-    for k, v in PER_POD_FORMS[form].items():
-        monkeypatch.setenv(k, v)
-    monkeypatch.setenv("KSIM_SERVE_STATS", "1")
-    (nodes, running, pods, objs), aux, prios, custom = _aux_setup(kind, seed)
-    order = list(reversed(pods))
-    cl = ingest.Cluster.from_objects(nodes, running, order, spread=spread.SpreadListers(**objs), aux=aux)
-    assert cl.aux_active
-    preds, _ = scheduler.provider("DefaultProvider")
-    batch = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH, custom_priorities=custom)
-    one = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH, custom_priorities=custom)
-    ports, sc = cl.pod_ports, cl.pod_scalars
-    try:
-        out, _, _ = batch.schedule()
-        for k in range(len(order)):
-            pod = abi.Pod.from_buffer_copy(cl.pods[k].tobytes())
-            res = abi.Result()
-            one.h.call("ksim_schedule_one", C.byref(pod), abi.vptr(ports), len(ports), abi.vptr(sc), len(sc),
-                       abi.SCHEDULE_ASSUME if pattern == "assume" else abi.SCHEDULE_ONLY, C.byref(res))
-            assert res.node == out[k], k
-            if pattern == "adapter" and res.node >= 0:
-                one.h.call("ksim_pod_add", int(res.node), C.byref(pod), abi.vptr(ports), len(ports), abi.vptr(sc), len(sc))
-        assert one.last_node_index == batch.last_node_index
-    finally:
-        batch.close()
-        one.close()
-    # the form ran: the resident kernel took messages exactly in the resident form
-    served = "[ksim serve]" in capfd.readouterr().err
-    assert served == (form == "resident")
+                x["metadata"]["labels"]["rack"] = "r%d" % rng.randrange(racks)
+        order = list(reversed(pods))
+        lst = spread.SpreadListers(**objs)
+        preds, _ = scheduler.provider("DefaultProvider")
+        prios = [("SAA", 4), ("SelectorSpreadPriority", 1), ("LeastRequestedPriority", 1), ("BalancedResourceAllocation", 1)]
+        custom = {"SAA": ("serviceAntiAffinity", "rack")}
+        cl = ingest.Cluster.from_objects(nodes, running, order, spread=lst, aux=("service_anti_affinity", "rack"))
+        p = scheduler.plan(cl, preds, prios, custom_priorities=custom)
+        want, _, _, ctr, _ = cpu_ref.run(cl, None, threads=8, plan=p)
+        for mode in (abi.MODE_LAUNCH, abi.MODE_PERSISTENT):
+            g = scheduler.GenericScheduler(cl, preds, prios, custom_priorities=custom, mode=mode)
+            try:
+                out, _, st = g.schedule()
+                assert st.mode == (abi.MODE_PERSISTENT if mode == abi.MODE_PERSISTENT and racks <= 64 else abi.MODE_LAUNCH)
+                assert (out == want).all(), (racks, mode, int((out != want).argmax()))
+                assert g.last_node_index == ctr
+            finally:
+                g.close()
