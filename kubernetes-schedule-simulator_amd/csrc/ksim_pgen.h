@@ -114,7 +114,7 @@ struct PGenArgs {
   uint32_t off[PGO_N];
   int32_t has_aff, has_vol;
   int32_t n_zone;     // zones of the spread reduce (<= PG_MAXZ)
-  int32_t pad;
+  int32_t svc_on;     // CheckServiceAffinity's lender check (A.svc_*; single-hypothesis kernel, n_pair <= PG_SVC_PAIRS)
   uint64_t spin_ticks;
   int32_t test_stall;  // diagnostic (KSIM_PGEN_TEST_STALL): the last workgroup exits at once, as one
                        // that never became resident; the others must abort and the host recover
@@ -129,3 +129,4 @@ extern "C" size_t ksim_pgen_lds_budget(void);
 extern "C" size_t ksim_pgen_gran_bytes(void);
 extern "C" int ksim_pgen_max_zones(void);
 extern "C" int ksim_pgen_max_aux_domains(void);
+#define PG_SVC_PAIRS 256  // counted pairs whose domain-0 counts a workgroup keeps (the lender check's totals)

@@ -104,6 +104,7 @@ struct PgL {
   int32_t* hd;   // dense hypothesis deltas (null when not staged)
   int64_t* hc;
   int32_t* hk;
+  int32_t* g0;   // [n_pair] domain-0 counts of every counted pair (the lender check's totals; null: off)
   int32_t chunk;
 };
 
@@ -143,6 +144,7 @@ __device__ __forceinline__ ksim_pod pg_pod_u(const ksim_pod& x) {
   p.nz_cpu = rfl64(x.nz_cpu); p.nz_mem = rfl64(x.nz_mem);
   p.cls = rfl(x.cls); p.host = rfl(x.host); p.flags = (uint32_t)rfl((int32_t)x.flags);
   p.scalar_off = rfl(x.scalar_off); p.scalar_cnt = rfl(x.scalar_cnt);
+  p.aff_class = rfl(x.aff_class);  // (the lender check's affinity class)
   return p;
 }
 
@@ -247,6 +249,52 @@ __device__ __forceinline__ void pg_hyp_mounts(const PgHyp& y, int32_t key, uint3
   }
 }
 
+// CheckServiceAffinity's labels from the lender (ksim_svc_lender, predicates.go:986-1011) on row j:
+// the totals (key 0, every node in domain 0) and the label-presence counts from the workgroup's
+// domain-0 copies (L.g0), the count in j's domain of the label value's key from the row form.
+__device__ __forceinline__ uint32_t pg_svc_lender(const KsimCtx& c, const PGenArgs& g, const PgL& L, int32_t a, int32_t j) {
+  const KsimAff& A = g.A;
+  const int32_t v = A.svc_class[a];
+  if (v < 0) return 0;
+  const uint32_t miss = A.svc_miss[a];
+  const ksim_svc_ident& S = A.svc[v];
+  const int32_t total = L.g0[S.pair_all];
+  if (total == 0) return 0;  // no cached pod to lend labels
+  if (__hip_atomic_load(&A.svc_conflict[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) & miss) {
+    atomicOr(c.err, 128);
+    return 1u << KSIM_R_SERVICE_AFFINITY;
+  }
+  for (uint32_t mm = miss; mm; mm &= mm - 1) {
+    const int l = __builtin_ctz(mm);
+    if (L.g0[S.pair_present[l]] == 0) continue;  // the lender lacks l: no constraint
+    const int32_t pv = S.pair_value[l];
+    if (L.dom[(int64_t)A.pair_key[pv] * L.chunk + j] < 0 || L.cnt[(int64_t)pv * L.chunk + j] != total)
+      return 1u << KSIM_R_SERVICE_AFFINITY;
+  }
+  return 0;
+}
+
+// ksim_svc_commit on row j before the commit of an identity's pod adds its counts: the
+// service-affinity identities it matches record the labels on which the row disagrees with their
+// earlier cached pods.  One thread.
+__device__ __forceinline__ void pg_svc_commit(const PGenArgs& g, const PgL& L, int32_t ident, int32_t j) {
+  const KsimAff& A = g.A;
+  for (int32_t e = A.svc_of_off[ident - 1], end = A.svc_of_off[ident]; e < end; ++e) {
+    const int32_t v = A.svc_of[e];
+    const ksim_svc_ident& S = A.svc[v];
+    const int32_t total = L.g0[S.pair_all];
+    if (total == 0) continue;  // the first one: nothing to disagree with
+    uint32_t bad = 0;
+    for (int l = 0; l < A.n_svc_labels; ++l) {
+      const int32_t pv = S.pair_value[l];
+      const int32_t d = L.dom[(int64_t)A.pair_key[pv] * L.chunk + j];
+      const int32_t here = d >= 0 ? L.cnt[(int64_t)pv * L.chunk + j] : total - L.g0[S.pair_present[l]];
+      if (here != total) bad |= 1u << l;
+    }
+    if (bad) atomicOr(&A.svc_conflict[v], bad);
+  }
+}
+
 // The first failing predicate of predicatesOrdering (predicates.go:129-138) on row j (node i),
 // exactly the chain of ksim_predicates_a, over the LDS image and the pod's record (HYP: with the
 // hypothesis pod committed to the row: r carries its resources).  0 = fits.
@@ -333,6 +381,10 @@ __device__ __forceinline__ uint32_t pg_predicates(const KsimCtx& c, const PGenAr
   if ((pr & KSIM_P_LABEL_PRESENCE) && (r.fl & KSIM_N_LABEL_PRESENCE)) return 1u << KSIM_R_LABEL_PRESENCE;
   if ((pr & KSIM_P_SERVICE_AFFINITY) && (P.flags & KSIM_POD_NEED_SVC_AFFINITY) && (st & PG_ST_SVC))
     return 1u << KSIM_R_SERVICE_AFFINITY;
+  if (!HYP && L.g0 && (pr & KSIM_P_SERVICE_AFFINITY) && P.aff_class > 0) {
+    m = pg_svc_lender(c, g, L, P.aff_class - 1, j);
+    if (m) return m;
+  }
   if (vol) {
     // MaxEBS / MaxGCEPD / MaxAzureDiskVolumeCount (predicates.go:415-456): the row's mounted keys
     // each filter counts (LDS) plus the pod's new keys not mounted yet
@@ -426,6 +478,7 @@ __device__ __forceinline__ PgL pg_lds(char* sm, const PGenArgs& g, int64_t chunk
   L.hd = g.d.hdense ? (int32_t*)(sm + g.off[PGO_HD]) : nullptr;
   L.hc = g.d.hdense ? (int64_t*)(sm + g.off[PGO_HC]) : nullptr;
   L.hk = g.d.hdense ? (int32_t*)(sm + g.off[PGO_HK]) : nullptr;
+  L.g0 = nullptr;
   return L;
 }
 // pod-context record r & 1 (offset arithmetic on the LDS base keeps the accesses ds_*)
@@ -573,6 +626,10 @@ __global__ __launch_bounds__(64) void ksim_pgen_pack_kernel(KsimCtx c, PGenArgs 
       if (!c.no_commit && ((P.aff_ident > 0 && g.ident_shared[P.aff_ident - 1]) ||
                            (P.aff_class > 0 && g.aclass_shared[P.aff_class - 1])))
         H.fl |= PGF_SHARED;
+      // a lender (its identity matches a service-affinity selector): every workgroup follows its
+      // commit, for the domain-0 copies of the lender check's totals (even on node-like keys)
+      if (!c.no_commit && g.svc_on && P.aff_ident > 0 && g.A.svc_of_off[P.aff_ident - 1] < g.A.svc_of_off[P.aff_ident])
+        H.fl |= PGF_SHARED;
     }
     const int32_t* vc = nullptr;
     if (g.has_vol && P.vol_class > 0) {
@@ -647,6 +704,7 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
   __shared__ int64_t s_node;
   __shared__ int32_t s_dw[PG_MAXL * 2];              // shared-domain commit: the node's domain per list entry
   __shared__ uint64_t s_bal[NPT][PG_NW];             // owner: each wave's ballot of its rows at the chosen score
+  __shared__ int32_t s_g0[PG_SVC_PAIRS];             // the lender check: domain-0 counts of the counted pairs
 #ifdef KSIM_STAMPS
   uint64_t st_acc[16] = {};
   uint64_t t_prev = __builtin_amdgcn_s_memtime();
@@ -663,6 +721,10 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
   const int32_t nrows = (int32_t)(hi - lo);
   const int64_t n = c.n;
   PgL L = pg_lds(pg_smem, g, chunk);
+  if (g.svc_on) {  // (n_pair <= PG_SVC_PAIRS, host-checked)
+    L.g0 = s_g0;
+    for (int32_t cp = threadIdx.x; cp < g.d.n_pair; cp += PG_BS) s_g0[cp] = g.A.cnt[g.A.pair_off[cp]];
+  }
   auto xrec = [&](int64_t r) { return pg_xrec(pg_smem, g, r); };
   const int32_t vcap = g.d.vcap, psl = g.d.pslots;
 
@@ -1210,6 +1272,12 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
       c.out_node[pod] = (int32_t)w;
       if (shared) {
         s_node = w;
+        if (g.svc_on && aff_commit && Pr.aff_ident > 0) {
+          // the lenders' disagreements before the counts move, released ahead of the commit word
+          // the other workgroups acquire before their next evaluation reads them
+          pg_svc_commit(g, L, Pr.aff_ident, jsel);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        }
         pg_store(g.gran + PG_COMMIT_OFF + slot, ((uint64_t)tag << 56) | (uint64_t)w);
       }
       if (!c.no_commit) {
@@ -1291,6 +1359,7 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
           if (__builtin_amdgcn_s_memrealtime() - t0 > g.spin_ticks) { atomicOr(c.err, 4); s_abort = 1; break; }
           __builtin_amdgcn_s_sleep(1);
         }
+        if (g.svc_on) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // (the owner's svc_conflict bits)
         s_node = (int64_t)(v & M56);
       }
       __syncthreads();
@@ -1304,6 +1373,9 @@ __global__ __launch_bounds__(PG_BS) void ksim_pgen_kernel(KsimCtx c_arg, PGenArg
         s_dw[x] = g.A.dom[(int64_t)key * n + w];
       }
       __syncthreads();
+      if (g.svc_on)  // the domain-0 copies: the pod's pairs on keys where the node is in domain 0
+        for (int32_t x = tid; x < nm; x += PG_BS)
+          if (s_dw[x] == 0) atomicAdd(&s_g0[mp[x].x], 1);
       for (int32_t y = tid; y < (nm + ncr) * nrows; y += PG_BS) {
         const int32_t x = y / nrows, j = y - x * nrows;
         const int32_t dw = s_dw[x];

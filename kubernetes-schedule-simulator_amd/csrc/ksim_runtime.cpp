@@ -860,8 +860,11 @@ struct PgPlan {
 
 static bool pgen_plan(ksim_handle* h, PgPlan* pl, bool allow_v2 = true) {
   const KsimCtx& c = h->ctx;
-  if (getenv("KSIM_NO_PGEN") || h->pgen_off || h->shard.world > 1 || c.n <= 0 || ksim_rt_svc_lender_on(h)) return false;
-  const bool aux = ksim_rt_aux_on(h);
+  if (getenv("KSIM_NO_PGEN") || h->pgen_off || h->shard.world > 1 || c.n <= 0) return false;
+  const bool aux = ksim_rt_aux_on(h), lender = ksim_rt_svc_lender_on(h);
+  // the lender check: its totals' domain-0 copies in every workgroup, single-hypothesis kernel only
+  if (lender && h->aff_n_pair > PG_SVC_PAIRS) return false;
+  if (lender) allow_v2 = false;
   int64_t s = 0;
   for (int k : {KSIM_W_LEAST_REQUESTED, KSIM_W_MOST_REQUESTED, KSIM_W_BALANCED, KSIM_W_INTERPOD_AFFINITY,
                 KSIM_W_SELECTOR_SPREAD}) {
@@ -968,6 +971,7 @@ static int run_pgen_mode(ksim_handle* h, int64_t first, int64_t count, const PgP
   memcpy(g.off, pl.off, sizeof g.off);
   g.has_vol = h->have_vol ? 1 : 0;
   if (h->have_vol) g.V = h->vol_h;
+  g.svc_on = ksim_rt_svc_lender_on(h) ? 1 : 0;
   if (h->have_aff) {
     g.ident_shared = h->aff_ident_shared;
     g.aclass_shared = h->aff_aclass_shared;
@@ -1395,12 +1399,12 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
       return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded run stopped: a node's quantities left the exact float64 range");
     }
   } else {
-  // the service-affinity lender check (ksim_affinity_tables.svc_*) is read by the launch-form
-  // kernels alone; the auxiliary priority (aux_*) by them and the general persistent kernel (tree
-  // mode, for pods without it, gives way to the automatic choice)
-  const int mode = (ksim_rt_svc_lender_on(h) || ksim_rt_range_wide(h, first, count)) ? KSIM_MODE_LAUNCH
-                   : (ksim_rt_aux_on(h) && h->cfg.mode == KSIM_MODE_TREE) ? KSIM_MODE_AUTO
-                                                                           : h->cfg.mode;
+  // the auxiliary priority and the service-affinity lender check (ksim_affinity_tables.aux_* /
+  // svc_*) are read by the launch-form kernels and the general persistent kernel (tree mode, for
+  // pods without them, gives way to the automatic choice)
+  const int mode = ksim_rt_range_wide(h, first, count)                          ? KSIM_MODE_LAUNCH
+                   : (ksim_rt_launch_tables(h) && h->cfg.mode == KSIM_MODE_TREE) ? KSIM_MODE_AUTO
+                                                                                 : h->cfg.mode;
   int rc = mode == KSIM_MODE_TREE         ? run_tree_mode(h, first, count, st)
            : mode == KSIM_MODE_AUTO       ? run_auto_mode(h, first, count, st)
            : mode == KSIM_MODE_PERSISTENT ? run_persistent_mode(h, first, count, st)

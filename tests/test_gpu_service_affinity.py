@@ -7,7 +7,9 @@ lender check of include/ksim.h ksim_affinity_tables.svc_*):
   (tests/test_oracle_c_features.py svc_simulate): identical placements, FitError texts and
   lastNodeIndex, and KSIM_E_UNSUPPORTED exactly where the oracle meets lenders that disagree on an
   open label (the reference's answer would depend on the pod lister's map order);
-- the per-pod call (ksim_schedule_one + assume) against the batch."""
+- in the launch form and the general persistent kernel;
+- every per-pod form (ksim_schedule_one + assume, or the adapter's SCHEDULE_ONLY + ksim_pod_add)
+  against the batch."""
 import copy
 
 import pytest
@@ -70,9 +72,12 @@ def _gpu_run(nodes, running, pods, services, aff_labels, mode=abi.MODE_AUTO):
     return res, lni, st
 
 
+@pytest.mark.parametrize("mode", [abi.MODE_LAUNCH, abi.MODE_PERSISTENT])
 @pytest.mark.parametrize("variant", ["consistent", "mixed_labels", "conflicting_running"])
 @pytest.mark.parametrize("seed", range(4))
-def test_service_affinity_simulation_matches_oracle(seed, variant):
+def test_service_affinity_simulation_matches_oracle(seed, variant, mode):
+    """The launch form and the general persistent kernel (ksim_pgen.hip: the lender check over the
+    row form and each workgroup's domain-0 copies of the totals)."""
     aff_labels = ["region", "rack"]
     nodes, running, pods, services = rnd_svc_affinity_workload(seed, mixed_labels=variant == "mixed_labels",
                                                                conflicting_running=variant == "conflicting_running",
@@ -81,10 +86,10 @@ def test_service_affinity_simulation_matches_oracle(seed, variant):
         want, lni = svc_simulate(nodes, running, pods, SVC_PREDS, SVC_PRIOS, aff_labels, services)
     except Ambiguous:
         with pytest.raises(abi.KsimUnsupported):
-            _gpu_run(nodes, running, pods, services, aff_labels)
+            _gpu_run(nodes, running, pods, services, aff_labels, mode=mode)
         return
-    got, ctr, st = _gpu_run(nodes, running, pods, services, aff_labels)
-    assert st.mode == abi.MODE_LAUNCH
+    got, ctr, st = _gpu_run(nodes, running, pods, services, aff_labels, mode=mode)
+    assert st.mode == mode
     assert got == want
     assert ctr == lni
 
@@ -182,3 +187,26 @@ def test_per_pod_forms_with_service_affinity_match_batch(seed, variant, form, pa
     # the form ran: the resident kernel took messages exactly in the resident form
     served = "[ksim serve]" in capfd.readouterr().err
     assert served == (form == "resident")
+
+
+@pytest.mark.parametrize("variant", ["consistent", "mixed_labels", "conflicting_running"])
+def test_service_affinity_at_scale_persistent_matches_launch(variant):
+    """2,000 nodes (8 workgroups of the general persistent kernel: the lender's totals replicated in
+    each, the disagreement bits released with the commit word) == the launch form, refusals
+    included."""
+    aff_labels = ["region", "rack"]
+    nodes, running, pods, services = rnd_svc_affinity_workload(7, n_nodes=2000, n_pods=600,
+                                                               mixed_labels=variant == "mixed_labels",
+                                                               conflicting_running=variant == "conflicting_running",
+                                                               full_labels=variant == "consistent")
+    res = {}
+    for mode in (abi.MODE_LAUNCH, abi.MODE_PERSISTENT):
+        try:
+            got, ctr, st = _gpu_run(nodes, running, pods, services, aff_labels, mode=mode)
+            assert st.mode == mode
+            res[mode] = (got, ctr)
+        except abi.KsimUnsupported:
+            res[mode] = "refused"
+    assert res[abi.MODE_PERSISTENT] == res[abi.MODE_LAUNCH]
+    if variant == "consistent":  # (lenders on one region / rack each, full labels: nothing to refuse)
+        assert res[abi.MODE_LAUNCH] != "refused"
