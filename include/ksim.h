@@ -505,7 +505,9 @@ typedef struct {
    *    with a serviceAntiAffinity argument): the pair counts the pods of the pod's single selecting
    *    service; a fit node without the aux_key label scores 0, one with value v
    *    MaxPriority x (total - count(v)) / total over the fit nodes (MaxPriority when total = 0, and
-   *    for a class without a pair).  Scheduled by the launch-form kernels only. */
+   *    for a class without a pair).  Read by the launch-form kernels, the general persistent
+   *    kernel (<= 64 aux_key domains) and every per-pod form; with it loaded every pod of a batch
+   *    goes to those (a serviceAntiAffinity priority scores pods no service selects too). */
   const int32_t* aux_pair;         /* [n_aclass] or NULL */
   int32_t aux_key;                 /* -1 with aux_pair NULL */
   int32_t aux_kind;                /* KSIM_AUX_* */
@@ -518,7 +520,8 @@ typedef struct {
    * affinity identity v (namespace + labels of such pods): selector s_v (namespace, the labels as a
    * set selector) with counted pairs (s_v, key 0) — the matching cached pods — and per predicate
    * label l (s_v, presence key of l: domain 0 on nodes carrying l) and (s_v, key of l).  NULL
-   * svc_ident: none.  Scheduled by the launch-form kernels only. */
+   * svc_ident: none.  Read by the launch-form kernels, the general persistent kernel (<= 256
+   * counted pairs) and every per-pod form (the resident one without tentative commits). */
   int32_t n_svc;                   /* service-affinity identities */
   int32_t n_svc_labels;            /* the predicate's labels (<= KSIM_SVC_LABELS) */
   const ksim_svc_ident* svc_ident; /* [n_svc] */
