@@ -95,7 +95,8 @@ struct KsimAff {
 // ... and pass A's (after the launch region): min / max raw InterPodAffinity sum, max spread count,
 // haveZones, then the zone sums (<= KSIM_PX_ZONES zones), same word format
 #define KSIM_PX_ZONES 24
-#define KSIM_PX_REC (4 + KSIM_PX_ZONES)
+#define KSIM_PX_ADOMS 24  // the auxiliary priority's domains: its max / sum / haveZones and domain sums follow the zones
+#define KSIM_PX_REC (4 + KSIM_PX_ZONES + 3 + KSIM_PX_ADOMS)
 #define KSIM_AFF_PART 8    // pass-A block-partial words
 
 // Volume tables on the device (ksim_load_volumes; layout in include/ksim.h).

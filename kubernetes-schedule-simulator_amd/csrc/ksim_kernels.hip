@@ -322,10 +322,17 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, int64_t pod, bool
   int64_t zmx = 0, azm = 0;
   if (c.sh_world > 1) {
     // node-sharded (SURVEY.md §8e Phase A): this rank's pass-A words to every rank, the world's
-    // min / max / max / haveZones and zone sums back (the aux priority is refused when sharded)
-    const int nz = sp >= 0 ? A.n_zone : 0;  // <= KSIM_PX_ZONES (host-checked)
-    const int W = 4 + nz, me = c.sh_rank;
-    if (tid == 0) { s_v[0][0] = r0; s_v[1][0] = r1; s_v[2][0] = r2; s_v[3][0] = r3; }
+    // min / max / max / haveZones and zone sums back, then (a pod with an auxiliary count) the
+    // auxiliary priority's max / sum / haveZones and domain sums
+    const int nz = sp >= 0 ? A.n_zone : 0;   // <= KSIM_PX_ZONES (host-checked)
+    const int na = ap >= 0 ? A.n_adom : 0;   // <= KSIM_PX_ADOMS (host-checked)
+    const int A0 = 4 + nz, W = A0 + (ap >= 0 ? 3 + na : 0), me = c.sh_rank;
+    // word x's combine over the ranks: 0 = min, 1 = max, 2 = sum
+    const int op = lane == 0 ? 0 : (lane < 4 ? 1 : (lane < A0 ? 2 : (lane == A0 || lane == A0 + 2 ? 1 : 2)));
+    if (tid == 0) {
+      s_v[0][0] = r0; s_v[1][0] = r1; s_v[2][0] = r2; s_v[3][0] = r3;
+      s_v[4][0] = r5; s_v[5][0] = r6; s_v[6][0] = r7;
+    }
     __syncthreads();
     int64_t* px = reinterpret_cast<int64_t*>(s_z);  // [KSIM_MAX_RANKS][KSIM_PX_REC] (the zone scratch is free now)
     if (wv == 0) {
@@ -334,8 +341,11 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, int64_t pod, bool
       const int slot = (int)(pod % KSIM_LX_SLOTS);
       uint64_t* const base0 = c.sh_peers[me] + (int64_t)KSIM_LX_SLOTS * KSIM_MAX_RANKS * KSIM_LX_REC;
       if (lane < W) {
-        const int64_t v = lane < 4 ? s_v[lane][0]
-                                   : (int64_t)__hip_atomic_load(&A.zsum[lane - 4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int64_t v =
+            lane < 4    ? s_v[lane][0]
+            : lane < A0 ? (int64_t)__hip_atomic_load(&A.zsum[lane - 4], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+            : lane < A0 + 3 ? s_v[4 + lane - A0][0]
+                            : (int64_t)__hip_atomic_load(&A.asum[lane - A0 - 3], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         px[me * KSIM_PX_REC + lane] = v;
         for (int r = 0; r < c.sh_world; ++r)
           lx_store(c.sh_peers[r] + (int64_t)KSIM_LX_SLOTS * KSIM_MAX_RANKS * KSIM_LX_REC +
@@ -360,27 +370,38 @@ __device__ __forceinline__ bool passa_reduce(const KsimCtx& c, int64_t pod, bool
         }
         __builtin_amdgcn_s_sleep(1);
       }
-      // the world's: min, max, max, haveZones, then the zone sums and their maximum
+      // the world's words, then the zone / domain sums published and their maxima
       int64_t g = 0;
       if (lane < W) {
         g = px[lane];
         for (int r = 1; r < c.sh_world; ++r) {
           const int64_t v = px[r * KSIM_PX_REC + lane];
-          g = lane == 0 ? (v < g ? v : g) : (lane < 4 ? (v > g ? v : g) : g + v);
+          g = op == 0 ? (v < g ? v : g) : (op == 1 ? (v > g ? v : g) : g + v);
         }
-        if (lane >= 4) {
+        if (lane >= 4 && lane < A0) {
           A.zread[lane - 4] = g;
           A.zsum[lane - 4] = 0;
+        } else if (lane >= A0 + 3) {
+          A.aread[lane - A0 - 3] = g;
+          A.asum[lane - A0 - 3] = 0;
         }
       }
-      const int64_t zm = wave_max_i64(lane >= 4 && lane < W ? g : 0);
+      const int64_t zm = wave_max_i64(lane >= 4 && lane < A0 ? g : 0);
+      const int64_t am = wave_max_i64(lane >= A0 + 3 && lane < W ? g : 0);
       r0 = __shfl(g, 0, 64); r1 = __shfl(g, 1, 64); r2 = __shfl(g, 2, 64); r3 = __shfl(g, 3, 64);
+      const int64_t g5 = __shfl(g, A0 & 63, 64), g6 = __shfl(g, (A0 + 1) & 63, 64), g7 = __shfl(g, (A0 + 2) & 63, 64);
       if (lane == 0) {
         A.mm[0] = r0 < 0 ? r0 : 0;  // (the accumulators start at 0: every rank's are <= 0 / >= 0 already)
         A.mm[1] = r1;
         A.mm[2] = r2;
         A.mm[3] = r3;
         A.mm[4] = zm;
+        if (ap >= 0) {
+          A.mm[5] = g5;
+          A.mm[6] = g6;
+          A.mm[7] = g7;
+          A.mm[8] = am;
+        }
         *A.ticket = 0;
       }
     }

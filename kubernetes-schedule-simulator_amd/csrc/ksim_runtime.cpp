@@ -1349,7 +1349,9 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
     for (int r = 0; r < h->shard.world; ++r)
       if (!h->shard.peers[r]) return ksim_fail(h, KSIM_E_STATE, "ksim_schedule: rank %d is not connected", r);
     int grid = 0, lds_rows = 0;
-    const int form = pfast_form(h, first, count, &grid, &lds_rows);
+    // (the auxiliary priority: every pod to the launch form — a serviceAntiAffinity priority scores
+    // pods no service selects too)
+    const int form = ksim_rt_aux_on(h) ? 0 : pfast_form(h, first, count, &grid, &lds_rows);
     int rc;
     if (form) {
       rc = run_pfast_mode(h, first, count, grid, lds_rows, form == 2, st);
@@ -1359,9 +1361,11 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
       if (ksim_rt_range_wide(h, first, count))
         return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling of pods with more than %d reduce classes",
                          KSIM_MAX_RCLASS);
-      if (ksim_rt_launch_tables(h) || (h->have_aff && h->aff_h.n_zone > KSIM_PX_ZONES))
-        return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling with the auxiliary priority, the service-affinity "
-                                           "lender check or more than %d spread zones", KSIM_PX_ZONES);
+      if (ksim_rt_svc_lender_on(h) || (h->have_aff && h->aff_h.n_zone > KSIM_PX_ZONES) ||
+          (ksim_rt_aux_on(h) && h->aff_h.n_adom > KSIM_PX_ADOMS))
+        return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling with the service-affinity lender check, more than "
+                                           "%d spread zones or more than %d auxiliary-priority domains", KSIM_PX_ZONES,
+                         KSIM_PX_ADOMS);
       // per-node scores travel as 40-bit biased words (KSIM_LX_BIAS = 2^39): every weight that
       // reaches a node's score is bounded, and so is their sum x MaxPriority
       {
@@ -1371,6 +1375,11 @@ int ksim_schedule(ksim_handle* h, int64_t first, int64_t count, int32_t* out_nod
           if (c.w[k] > ((int64_t)1 << 30))
             return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling: a priority weight above 2^30");
           sw += c.w[k] * 10;
+        }
+        if (ksim_rt_aux_on(h)) {
+          if (h->aff_h.aux_w > ((int64_t)1 << 30))
+            return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling: a priority weight above 2^30");
+          sw += h->aff_h.aux_w * 10;
         }
         if (sw >= ((int64_t)1 << 39))
           return ksim_fail(h, KSIM_E_UNSUPPORTED, "node-sharded scheduling: weighted scores beyond the 40-bit exchange word");

@@ -153,6 +153,7 @@ SVC_IDENT_DTYPE = np.dtype([("pair_all", np.int32), ("pad", np.int32), ("pair_pr
 
 AUX_SPREAD, AUX_SERVICE_ANTI = 0, 1
 SHARD_MAX_ZONES = 24   # zones of the spread reduce a node-sharded pass A exchanges (KSIM_PX_ZONES)
+SHARD_MAX_AUX_DOMAINS = 24  # the auxiliary priority's domains it exchanges (KSIM_PX_ADOMS)
 
 
 class VolumeTables(C.Structure):

@@ -704,8 +704,13 @@ def _shard_affinity(d, lo, hi):
     if bad:
         raise Unsupported("node-sharded scheduling of inter-pod affinity / spread terms over topology domains several "
                           "nodes share (keys %s)" % bad)
-    if d.get("aux_pair") is not None or d.get("svc_on"):
-        raise Unsupported("node-sharded scheduling with the auxiliary spreading priority or CheckServiceAffinity lenders")
+    if d.get("svc_on"):
+        raise Unsupported("node-sharded scheduling with CheckServiceAffinity lenders")
+    # the auxiliary priority: its pair is node-keyed (a rank's own counts), its key only groups the
+    # fit nodes' counts — domain sums exchanged across ranks in pass A, like the spread zones
+    if d.get("aux_pair") is not None and int(np.asarray(d["n_dom"])[int(d["aux_key"])]) > abi.SHARD_MAX_AUX_DOMAINS:
+        raise Unsupported("node-sharded scheduling of the auxiliary priority over more than %d domains"
+                          % abi.SHARD_MAX_AUX_DOMAINS)
     if int(d["zone_key"]) >= 0 and int(np.asarray(d["n_dom"])[int(d["zone_key"])]) > abi.SHARD_MAX_ZONES:
         raise Unsupported("node-sharded scheduling of spread pods over more than %d zones" % abi.SHARD_MAX_ZONES)
     out = dict(d)

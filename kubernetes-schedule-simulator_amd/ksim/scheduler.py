@@ -542,7 +542,7 @@ class ShardedScheduler(GenericScheduler):
     (ranks driven from this process) or export_handle / connect (one process per device)."""
 
     def __init__(self, cluster: Cluster, predicates, priorities, rank, world, device=0, collect_reasons=False,
-                 last_node_index=0):
+                 last_node_index=0, custom_priorities=None):
         """collect_reasons: each rank's schedule() returns, for every pod no node of the world fits,
         the reason histogram of its own shard; merge_sharded_reasons sums the ranks' into the
         FitError histogram over every node (generic_scheduler.go:51-90 builds FitError from the
@@ -551,7 +551,8 @@ class ShardedScheduler(GenericScheduler):
         self.lo, self.hi = rank * n // world, (rank + 1) * n // world
         self.rank, self.world = rank, world
         super().__init__(cluster.shard(self.lo, self.hi), predicates, priorities, device=device,
-                         mode=abi.MODE_PERSISTENT, collect_reasons=collect_reasons, last_node_index=last_node_index)
+                         mode=abi.MODE_PERSISTENT, collect_reasons=collect_reasons, last_node_index=last_node_index,
+                         custom_priorities=custom_priorities)
         self.full_cluster = cluster
         self.h.call("ksim_shard_setup", rank, world, self.lo)
 

@@ -186,3 +186,134 @@ def test_aux_at_scale_matches_c_oracle():
                 assert g.last_node_index == ctr
             finally:
                 g.close()
+
+
+PER_POD_FORMS = {
+    "one_wg": {},                                            # <= 1,024 nodes: the single-workgroup kernel
+    "resident": {"KSIM_ONE_WG": "0"},                        # the pick body in the resident kernel
+    "scan": {"KSIM_ONE_WG": "0", "KSIM_NO_PICK": "1"},       # the multi-block scan with its pass A
+}
+
+
+def _aux_setup(kind, seed):
+    """(workload, aux, prios, custom) of one auxiliary-priority family."""
+    if kind == "saa_zone":
+        return rnd_spread_workload(seed, n_pods=60), ("service_anti_affinity", ZONE), _saa_prios(seed), \
+            {"SAA": ("serviceAntiAffinity", ZONE)}
+    if kind == "saa_rack":  # 600 nodes (3 pick blocks), 40 rack domains next to the spread zones
+        import random
+        rng = random.Random(90 + seed)
+        w = rnd_spread_workload(seed, n_nodes=600, n_pods=80, n_running=60)
+        for x in w[0]:
+            if rng.random() < 0.7:
+                x["metadata"]["labels"]["rack"] = "r%d" % rng.randrange(40)
+        prios = [("SAA", 4), ("SelectorSpreadPriority", 1), ("LeastRequestedPriority", 1)]
+        return w, ("service_anti_affinity", "rack"), prios, {"SAA": ("serviceAntiAffinity", "rack")}
+    prios = [("SelectorSpreadPriority", 1), ("ServiceSpreadingPriority", 2 + seed), ("LeastRequestedPriority", 1)]
+    return rnd_spread_workload(seed, n_pods=60, zones=seed != 1), ("service_spreading",), prios, None
+
+
+@pytest.mark.parametrize("pattern", ["assume", "adapter"])
+@pytest.mark.parametrize("form", sorted(PER_POD_FORMS))
+@pytest.mark.parametrize("kind", ["saa_zone", "saa_rack", "service_spreading"])
+@pytest.mark.parametrize("seed", range(2))
+def test_per_pod_forms_with_aux_match_batch(seed, kind, form, pattern, monkeypatch, capfd):
+    """Every per-pod form reads the auxiliary priority: the single-workgroup kernel's pass A in LDS,
+    the pick / resident kernels' pass-A record words (3 words and the domain sums after the spread
+    zones), the scan's own pass A — placements and lastNodeIndex == the batch's.  adapter:
+    SCHEDULE_ONLY (a tentative commit on the resident kernel), then ksim_pod_add onto the node."""
+    import ctypes as C
+    for k, v in PER_POD_FORMS[form].items():
+        monkeypatch.setenv(k, v)
+    monkeypatch.setenv("KSIM_SERVE_STATS", "1")
+    (nodes, running, pods, objs), aux, prios, custom = _aux_setup(kind, seed)
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order, spread=spread.SpreadListers(**objs), aux=aux)
+    assert cl.aux_active
+    preds, _ = scheduler.provider("DefaultProvider")
+    batch = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH, custom_priorities=custom)
+    one = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH, custom_priorities=custom)
+    ports, sc = cl.pod_ports, cl.pod_scalars
+    try:
+        out, _, _ = batch.schedule()
+        for k in range(len(order)):
+            pod = abi.Pod.from_buffer_copy(cl.pods[k].tobytes())
+            res = abi.Result()
+            one.h.call("ksim_schedule_one", C.byref(pod), abi.vptr(ports), len(ports), abi.vptr(sc), len(sc),
+                       abi.SCHEDULE_ASSUME if pattern == "assume" else abi.SCHEDULE_ONLY, C.byref(res))
+            assert res.node == out[k], k
+            if pattern == "adapter" and res.node >= 0:
+                one.h.call("ksim_pod_add", int(res.node), C.byref(pod), abi.vptr(ports), len(ports), abi.vptr(sc), len(sc))
+        assert one.last_node_index == batch.last_node_index
+    finally:
+        batch.close()
+        one.close()
+    # the form ran: the resident kernel took messages exactly in the resident form
+    served = "[ksim serve]" in capfd.readouterr().err
+    assert served == (form == "resident")
+
+
+def _sharded_threads(cl, preds, prios, world, ranges, custom=None):
+    """world node-sharded ranks of `cl` on this one device, driven from threads."""
+    import threading
+    import numpy as np
+    scheds = [scheduler.ShardedScheduler(cl, preds, prios, r, world, custom_priorities=custom) for r in range(world)]
+    scheduler.connect_local_world(scheds)
+    outs = [[] for _ in range(world)]
+    try:
+        for first, count in ranges:
+            errs = []
+
+            def go(r):
+                try:
+                    outs[r].append(scheds[r].schedule(first, count)[0])
+                except Exception as e:  # noqa: BLE001 — surfaced below
+                    errs.append(e)
+            ts = [threading.Thread(target=go, args=(r,)) for r in range(world)]
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+            assert not errs, errs
+        return scheduler.merge_sharded([np.concatenate(o) for o in outs]), [s.last_node_index for s in scheds]
+    finally:
+        for s in scheds:
+            s.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("kind", ["saa_zone", "saa_rack", "service_spreading"])
+def test_node_sharded_aux_matches_unsharded(kind, world, monkeypatch):
+    """Node-sharded with the auxiliary priority (SURVEY.md §8e Phase A): its pair is node-keyed (each
+    rank's own counts) and its key only groups the fit nodes' counts, so pass A exchanges its max /
+    sum / haveZones and domain sums across the ranks after the spread zones.  Merged placements and
+    every rank's lastNodeIndex == the unsharded launch form's (two calls: tags across calls)."""
+    import numpy as np
+    monkeypatch.setenv("KSIM_MAX_GRID", str(256 // world // 2))
+    (nodes, running, pods, objs), aux, prios, custom = _aux_setup(kind, 1)
+    if kind == "saa_rack":  # (<= 24 rack domains when sharded: SHARD_MAX_AUX_DOMAINS)
+        for x in nodes:
+            lab = x["metadata"]["labels"]
+            if "rack" in lab:
+                lab["rack"] = "r%d" % (int(lab["rack"][1:]) % 20)
+    order = list(reversed(pods))
+    cl = ingest.Cluster.from_objects(nodes, running, order, spread=spread.SpreadListers(**objs), aux=aux)
+    preds, _ = scheduler.provider("DefaultProvider")
+    g = scheduler.GenericScheduler(cl, preds, prios, mode=abi.MODE_LAUNCH, custom_priorities=custom)
+    try:
+        want, _, _ = g.schedule()
+        want_ctr = g.last_node_index
+    finally:
+        g.close()
+    half = len(order) // 2
+    got, ctrs = _sharded_threads(cl, preds, prios, world, [(0, half), (half, len(order) - half)], custom)
+    assert np.array_equal(got, want)
+    assert ctrs == [want_ctr] * world
+
+
+def test_node_sharded_aux_refuses_many_domains():
+    """More auxiliary-priority domains than a sharded pass-A record holds: refused at the shard."""
+    (nodes, running, pods, objs), aux, prios, custom = _aux_setup("saa_rack", 0)
+    cl = ingest.Cluster.from_objects(nodes, running, list(reversed(pods)), spread=spread.SpreadListers(**objs), aux=aux)
+    with pytest.raises(abi.KsimUnsupported):
+        cl.shard(0, 300)
