@@ -393,7 +393,8 @@ int serve_launch(ksim_handle* h, int npt, int grid, uint64_t seq0) {
   a.ctr0_valid = h->ctr_known ? 1u : 0u;
   if (++h->serve_launch_id == 0) h->serve_launch_id = 1;  // (0 = the `left` word's initial value)
   a.launch_id = h->serve_launch_id;
-  hipError_t e = ksim_launch_serve(&cs, &a, npt, grid, h->stream_raw);
+  h->serve_aux = ksim_rt_aux_on(h);
+  hipError_t e = ksim_launch_serve(&cs, &a, npt, grid, h->serve_aux ? 1 : 0, h->stream_raw);
   if (e != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "resident per-pod kernel launch: %s", hipGetErrorString(e));
   h->serve_live.store(true, std::memory_order_release);
   serve_register(h, true);
@@ -553,7 +554,8 @@ int serve_ready(ksim_handle* h, int npt, int grid) {
     if (serve_left(h)) {  // the grid left by its idle vote while the host was away
       int rc = serve_reap(h);
       if (rc) return rc;
-    } else if (h->serve_npt != npt || h->serve_grid != grid || memcmp(&h->ctx, &h->serve_base, sizeof(KsimCtx)) != 0) {
+    } else if (h->serve_npt != npt || h->serve_grid != grid || h->serve_aux != ksim_rt_aux_on(h) ||
+               memcmp(&h->ctx, &h->serve_base, sizeof(KsimCtx)) != 0) {
       int rc = ksim_serve_stop(h);
       if (rc) return rc;
     }
@@ -923,7 +925,7 @@ int ksim_schedule_one(ksim_handle* h, const ksim_pod* pod, const uint64_t* ports
       h->res_host[KSIM_RES_NODE] = INT32_MIN;
       if ((rc = ksim_rt_check_launch_ctx(h, cs, grid, "ksim_schedule_one"))) return rc;
       oc.lap(0);
-      hipError_t ep = ksim_launch_pick(&cs, npt, grid, ksim_stream(h));
+      hipError_t ep = ksim_launch_pick(&cs, npt, grid, ksim_rt_aux_on(h) ? 1 : 0, ksim_stream(h));
       if (ep != hipSuccess) return ksim_fail(h, KSIM_E_DEVICE, "pick launch: %s", hipGetErrorString(ep));
       oc.lap(1);
       HIPCHK(h, hipStreamSynchronize(ksim_stream(h)));

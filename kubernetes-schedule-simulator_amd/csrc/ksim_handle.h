@@ -29,9 +29,9 @@ extern "C" int ksim_scan_coresident(int npt, int collect, int grid);
 extern "C" int ksim_one_npt(int64_t n);
 extern "C" hipError_t ksim_launch_one(const KsimCtx* c, int npt, hipStream_t s);
 extern "C" int ksim_pick_coresident(int npt, int grid);
-extern "C" hipError_t ksim_launch_pick(const KsimCtx* c, int npt, int grid, hipStream_t s);
+extern "C" hipError_t ksim_launch_pick(const KsimCtx* c, int npt, int grid, int aux, hipStream_t s);
 extern "C" int ksim_serve_coresident(int npt, int grid);
-extern "C" hipError_t ksim_launch_serve(const KsimCtx* c, const KsimServeArgs* a, int npt, int grid, hipStream_t s);
+extern "C" hipError_t ksim_launch_serve(const KsimCtx* c, const KsimServeArgs* a, int npt, int grid, int aux, hipStream_t s);
 extern "C" hipError_t ksim_launch_ipa_pass(const KsimCtx* c, int npt, int grid, hipStream_t s);
 extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t node, int32_t* status, hipStream_t s);
 extern "C" hipError_t ksim_launch_persistent(const KsimCtx* c, const KsimCtx* cdev, uint64_t* granules, int grid,
@@ -172,6 +172,7 @@ struct ksim_handle {
   uint64_t* serve_state = nullptr;         // device: the grid's idle vote (KSIM_SERVE_ST_*)
   KsimCtx serve_base{};                    // h->ctx when the kernel was launched
   int serve_npt = 0, serve_grid = 0;
+  bool serve_aux = false;  // the resident kernel's instantiation reads the auxiliary priority
   uint64_t serve_seq = 0;
   uint32_t serve_launch_id = 0;
   bool serve_shared = false;               // the last message committed state other blocks read

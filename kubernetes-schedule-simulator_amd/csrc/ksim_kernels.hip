@@ -1651,7 +1651,7 @@ __device__ __forceinline__ void ksim_row_cache_reload(const KsimCtx& c, KsimRowC
 // ans / seq: the resident form's answer words and message number (null: a one-pod launch, which
 // writes the result block and *c.counter directly); tent: the block's tentative-commit record
 // (resident form; no_commit == KSIM_SERVE_TENTATIVE: commit, record, answer the row's prior state).
-template <int NPT>
+template <int NPT, bool AUX>
 __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod& P, const int64_t pod, const uint32_t tag,
                                                const int32_t no_commit, uint64_t* const rec, uint64_t* ctr_keep,
                                                uint64_t* ans, const uint64_t seq, KsimTentRec* tent = nullptr,
@@ -1699,16 +1699,21 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
   ipa0.on = false;
   ipa0.sp = -1;
   ipa0.aon = false;
-  const bool pass_a = ipa.on || ipa.sp >= 0 || ipa.aon;
+  // AUX (a compile-time instantiation: the handle has the auxiliary priority's tables): the pod
+  // may read the auxiliary priority (the kernels without it keep their registers for the rest)
+  const bool pass_a = ipa.on || ipa.sp >= 0 || (AUX && ipa.aon);
   // pass-A record words: 4 maxima, NZ zone sums, then (a pod with an auxiliary count) 3 words and
   // NA domain sums; 4 + NZ + 3 + NA <= KSIM_PICK_RA (host-checked)
   const int NZ = (ipa.sp >= 0) ? c.aff->n_zone : 0;
-  const int NA = (ipa.ap >= 0) ? c.aff->n_adom : 0;
+  const bool AX = AUX && ipa.ap >= 0;
+  const int NA = AX ? c.aff->n_adom : 0;
   const int A0 = 4 + NZ;  // the auxiliary words
-  const bool AX = ipa.ap >= 0;
   __shared__ uint32_t s_dflag;  // the decision is in LDS (wave 0 → the other waves)
   if (tid < KSIM_NREASONS) s_hist[tid] = 0;
-  if (tid < KSIM_PICK_ZMAX) { s_z[tid] = 0; s_az[tid] = 0; }
+  if (tid < KSIM_PICK_ZMAX) {
+    s_z[tid] = 0;
+    if (AUX) s_az[tid] = 0;
+  }
   if (tid == 0) { s_ok = 1; s_dflag = 0; s_stat = 0; }
   __syncthreads();
 
@@ -1764,7 +1769,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
           if (cnt[k]) atomicAdd(&s_z[zz[k]], (unsigned long long)cnt[k]);
         }
       }
-      if (ipa.ap >= 0) {  // the auxiliary priority (passa_reduce's): max, sum, haveZones, domain sums
+      if (AX) {  // the auxiliary priority (passa_reduce's): max, sum, haveZones, domain sums
         const int64_t v = A.cnt[A.pair_off[ipa.ap] + i];
         const int32_t d = ksim_dom(A, A.aux_key, i);
         amx = v > amx ? v : amx;
@@ -1779,19 +1784,19 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
     mx = ksimw::max_i64(mx);
     smx = ksimw::max_i64(smx);
     hz = ksimw::max_i64(hz);
-    if (ipa.ap >= 0) {  // (uniform)
+    if (AX) {  // (uniform)
       amx = ksimw::max_i64(amx);
       atot = ksimw::sum_i64(atot);
       ahz = ksimw::max_i64(ahz);
     }
     if (lane == 0) {
       s_v[0][wv] = mn; s_v[1][wv] = mx; s_v[2][wv] = smx; s_v[3][wv] = hz;
-      s_v[4][wv] = amx; s_v[5][wv] = atot; s_v[6][wv] = ahz;
+      if (AUX) { s_v[4][wv] = amx; s_v[5][wv] = atot; s_v[6][wv] = ahz; }
     }
     __syncthreads();
     const int W = A0 + (AX ? 3 + NA : 0);
     // word x's combine over waves and blocks: 0 = min, 1 = max, 2 = sum
-    const int op = lane == 0 ? 0 : (lane < 4 ? 1 : (lane < A0 ? 2 : (lane == A0 || lane == A0 + 2 ? 1 : 2)));
+    const int op = lane == 0 ? 0 : (lane < 4 ? 1 : ((!AUX || lane < A0) ? 2 : (lane == A0 || lane == A0 + 2 ? 1 : 2)));
     if (wv == 1) {
       // publish: word x = lane x (0..3 the maxima over this block's waves, 4.. the zone sums, then
       // the auxiliary max / sum / haveZones and domain sums).  Wave 1 stores, wave 0 polls: a store
@@ -1807,7 +1812,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
         }
       } else if (lane < A0) {
         v = (int64_t)s_z[lane - 4];
-      } else if (lane < W) {
+      } else if (AX && lane < W) {
         v = (int64_t)s_az[lane - A0 - 3];
       }
       // every word of the record, not only the W read now: see the record stores below
@@ -1840,7 +1845,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
       if (lane < 4) s_pa[lane] = acc;
       else if (lane < A0) s_z[lane - 4] = (unsigned long long)acc;
       else if (lane < A0 + 3 && AX) s_pa[4 + lane - A0] = acc;
-      else if (lane < W) s_az[lane - A0 - 3] = (unsigned long long)acc;
+      else if (AX && lane < W) s_az[lane - A0 - 3] = (unsigned long long)acc;
     }
     __syncthreads();
     ipa.mn = s_pa[0]; ipa.mx = s_pa[1]; ipa.smx = s_pa[2]; ipa.hz = s_pa[3] != 0;
@@ -1860,7 +1865,7 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
         const int64_t v = ksim_spread_score(cnt[k], ipa.smx, ipa.hz, zz[k], zz[k] >= 0 ? (int64_t)s_z[zz[k]] : 0, ipa.szmx);
         sc[k] = (int64_t)((uint64_t)sc[k] + (uint64_t)ipa.sw * (uint64_t)v);
       }
-      if (ipa.aon) {  // (count and domain loaded again: no registers held across pass A for them)
+      if (AUX && ipa.aon) {  // (count and domain loaded again: no registers held across pass A for them)
         const int64_t i = base + (int64_t)k * KSIM_BLOCK + tid;
         const int32_t d = ksim_dom(A, A.aux_key, i);
         const int64_t v = AX ? A.cnt[A.pair_off[ipa.ap] + i] : 0;
@@ -2198,9 +2203,9 @@ __device__ __forceinline__ void ksim_pick_body(const KsimCtx& c, const ksim_pod&
 #undef PKST
 }
 
-template <int NPT>
+template <int NPT, bool AUX>
 __global__ __launch_bounds__(KSIM_BLOCK) void ksim_pick_kernel(KsimCtx c) {
-  ksim_pick_body<NPT>(c, c.one_pod, c.first, c.pick_tag, c.no_commit, c.pick + (c.pick_tag & 1u) * KSIM_PICK_WORDS,
+  ksim_pick_body<NPT, AUX>(c, c.one_pod, c.first, c.pick_tag, c.no_commit, c.pick + (c.pick_tag & 1u) * KSIM_PICK_WORDS,
                       nullptr, nullptr, 0);
 }
 
@@ -2249,7 +2254,7 @@ __device__ __forceinline__ uint64_t rfl64(uint64_t v) {
 }
 }  // namespace
 
-template <int NPT>
+template <int NPT, bool AUX>
 __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimServeArgs a) {
   __shared__ uint64_t s_keep;
   __shared__ ksim_pod s_P;
@@ -2432,7 +2437,7 @@ __global__ __launch_bounds__(KSIM_BLOCK) void ksim_serve_kernel(KsimCtx c, KsimS
     if (type != KSIM_SERVE_EXIT) seq = s_seq;
     if (type == KSIM_SERVE_SCHEDULE) {
       const ksim_pod P = s_P;
-      ksim_pick_body<NPT>(c, P, 0, s_tag, s_nc, c.pick + (s_tag & 1u) * KSIM_PICK_WORDS, &s_keep, box->ans, seq, &s_tent,
+      ksim_pick_body<NPT, AUX>(c, P, 0, s_tag, s_nc, c.pick + (s_tag & 1u) * KSIM_PICK_WORDS, &s_keep, box->ans, seq, &s_tent,
                           &rcache, stamp);
     } else if (type == KSIM_SERVE_ASSUME) {
       // a resource delta onto a given node (ksim_pod_add): the block whose chunk holds it answers
@@ -2616,10 +2621,10 @@ extern "C" hipError_t ksim_launch_assume(const KsimCtx* c, int64_t pod, int64_t 
 extern "C" int ksim_pick_coresident(int npt, int grid) {
   hipError_t e = hipErrorInvalidValue;
   switch (npt) {
-    case 1: e = ksim_check_coresident(ksim_pick_kernel<1>, grid, KSIM_BLOCK, 0); break;
-    case 2: e = ksim_check_coresident(ksim_pick_kernel<2>, grid, KSIM_BLOCK, 0); break;
-    case 4: e = ksim_check_coresident(ksim_pick_kernel<4>, grid, KSIM_BLOCK, 0); break;
-    case 8: e = ksim_check_coresident(ksim_pick_kernel<8>, grid, KSIM_BLOCK, 0); break;
+    case 1: e = (ksim_check_coresident(ksim_pick_kernel<1, false>, grid, KSIM_BLOCK, 0) == hipSuccess ? ksim_check_coresident(ksim_pick_kernel<1, true>, grid, KSIM_BLOCK, 0) : hipErrorInvalidValue); break;
+    case 2: e = (ksim_check_coresident(ksim_pick_kernel<2, false>, grid, KSIM_BLOCK, 0) == hipSuccess ? ksim_check_coresident(ksim_pick_kernel<2, true>, grid, KSIM_BLOCK, 0) : hipErrorInvalidValue); break;
+    case 4: e = (ksim_check_coresident(ksim_pick_kernel<4, false>, grid, KSIM_BLOCK, 0) == hipSuccess ? ksim_check_coresident(ksim_pick_kernel<4, true>, grid, KSIM_BLOCK, 0) : hipErrorInvalidValue); break;
+    case 8: e = (ksim_check_coresident(ksim_pick_kernel<8, false>, grid, KSIM_BLOCK, 0) == hipSuccess ? ksim_check_coresident(ksim_pick_kernel<8, true>, grid, KSIM_BLOCK, 0) : hipErrorInvalidValue); break;
   }
   return e == hipSuccess ? 1 : 0;
 }
@@ -2627,33 +2632,57 @@ extern "C" int ksim_pick_coresident(int npt, int grid) {
 extern "C" int ksim_serve_coresident(int npt, int grid) {
   hipError_t e = hipErrorInvalidValue;
   switch (npt) {
-    case 1: e = ksim_check_coresident(ksim_serve_kernel<1>, grid, KSIM_BLOCK, 0); break;
-    case 2: e = ksim_check_coresident(ksim_serve_kernel<2>, grid, KSIM_BLOCK, 0); break;
-    case 4: e = ksim_check_coresident(ksim_serve_kernel<4>, grid, KSIM_BLOCK, 0); break;
-    case 8: e = ksim_check_coresident(ksim_serve_kernel<8>, grid, KSIM_BLOCK, 0); break;
+    case 1: e = (ksim_check_coresident(ksim_serve_kernel<1, false>, grid, KSIM_BLOCK, 0) == hipSuccess ? ksim_check_coresident(ksim_serve_kernel<1, true>, grid, KSIM_BLOCK, 0) : hipErrorInvalidValue); break;
+    case 2: e = (ksim_check_coresident(ksim_serve_kernel<2, false>, grid, KSIM_BLOCK, 0) == hipSuccess ? ksim_check_coresident(ksim_serve_kernel<2, true>, grid, KSIM_BLOCK, 0) : hipErrorInvalidValue); break;
+    case 4: e = (ksim_check_coresident(ksim_serve_kernel<4, false>, grid, KSIM_BLOCK, 0) == hipSuccess ? ksim_check_coresident(ksim_serve_kernel<4, true>, grid, KSIM_BLOCK, 0) : hipErrorInvalidValue); break;
+    case 8: e = (ksim_check_coresident(ksim_serve_kernel<8, false>, grid, KSIM_BLOCK, 0) == hipSuccess ? ksim_check_coresident(ksim_serve_kernel<8, true>, grid, KSIM_BLOCK, 0) : hipErrorInvalidValue); break;
   }
   return e == hipSuccess ? 1 : 0;
 }
 
-extern "C" hipError_t ksim_launch_serve(const KsimCtx* c, const KsimServeArgs* a, int npt, int grid, hipStream_t s) {
+extern "C" hipError_t ksim_launch_serve(const KsimCtx* c, const KsimServeArgs* a, int npt, int grid, int aux, hipStream_t s) {
   if (grid <= 0 || grid > KSIM_PICK_MAXG || !c->pick || !a->box || !a->state || c->one) return hipErrorInvalidValue;
   switch (npt) {
-    case 1: hipLaunchKernelGGL(ksim_serve_kernel<1>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a); break;
-    case 2: hipLaunchKernelGGL(ksim_serve_kernel<2>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a); break;
-    case 4: hipLaunchKernelGGL(ksim_serve_kernel<4>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a); break;
-    case 8: hipLaunchKernelGGL(ksim_serve_kernel<8>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a); break;
+    case 1:
+      if (aux) hipLaunchKernelGGL((ksim_serve_kernel<1, true>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a);
+      else hipLaunchKernelGGL((ksim_serve_kernel<1, false>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a);
+      break;
+    case 2:
+      if (aux) hipLaunchKernelGGL((ksim_serve_kernel<2, true>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a);
+      else hipLaunchKernelGGL((ksim_serve_kernel<2, false>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a);
+      break;
+    case 4:
+      if (aux) hipLaunchKernelGGL((ksim_serve_kernel<4, true>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a);
+      else hipLaunchKernelGGL((ksim_serve_kernel<4, false>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a);
+      break;
+    case 8:
+      if (aux) hipLaunchKernelGGL((ksim_serve_kernel<8, true>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a);
+      else hipLaunchKernelGGL((ksim_serve_kernel<8, false>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c, *a);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }
 
-extern "C" hipError_t ksim_launch_pick(const KsimCtx* c, int npt, int grid, hipStream_t s) {
+extern "C" hipError_t ksim_launch_pick(const KsimCtx* c, int npt, int grid, int aux, hipStream_t s) {
   if (grid <= 0 || grid > KSIM_PICK_MAXG || !c->pick) return hipErrorInvalidValue;
   switch (npt) {
-    case 1: hipLaunchKernelGGL(ksim_pick_kernel<1>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
-    case 2: hipLaunchKernelGGL(ksim_pick_kernel<2>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
-    case 4: hipLaunchKernelGGL(ksim_pick_kernel<4>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
-    case 8: hipLaunchKernelGGL(ksim_pick_kernel<8>, dim3(grid), dim3(KSIM_BLOCK), 0, s, *c); break;
+    case 1:
+      if (aux) hipLaunchKernelGGL((ksim_pick_kernel<1, true>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c);
+      else hipLaunchKernelGGL((ksim_pick_kernel<1, false>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c);
+      break;
+    case 2:
+      if (aux) hipLaunchKernelGGL((ksim_pick_kernel<2, true>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c);
+      else hipLaunchKernelGGL((ksim_pick_kernel<2, false>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c);
+      break;
+    case 4:
+      if (aux) hipLaunchKernelGGL((ksim_pick_kernel<4, true>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c);
+      else hipLaunchKernelGGL((ksim_pick_kernel<4, false>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c);
+      break;
+    case 8:
+      if (aux) hipLaunchKernelGGL((ksim_pick_kernel<8, true>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c);
+      else hipLaunchKernelGGL((ksim_pick_kernel<8, false>), dim3(grid), dim3(KSIM_BLOCK), 0, s, *c);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

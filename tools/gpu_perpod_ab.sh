@@ -1,11 +1,11 @@
 #!/bin/bash
 # Per-pod A/B of library builds on one box (the C2 workload's per-pod marks):
-#   tools/gpu_perpod_ab.sh lib1.so lib2.so ...
+#   [WL=c2x] tools/gpu_perpod_ab.sh lib1.so lib2.so ...
 cd /tmp && export TMPDIR=/tmp
 cd "$GRAFT_REPO_ROOT" || exit 1
 for rep in 1 2 3; do
   for L in "$@"; do
-    KSIM_LIB=$L timeout -k 10 200 python3 bench.py --workload c2 --cpu-sample 0 --steps 3 --warmup 1 > /tmp/ab.json 2>/dev/null || { echo "bench $L failed"; exit 1; }
+    KSIM_LIB=$L timeout -k 10 200 python3 bench.py --workload ${WL:-c2} --cpu-sample 0 --steps 3 --warmup 1 > /tmp/ab.json 2>/dev/null || { echo "bench $L failed"; exit 1; }
     python3 -c "
 import json,sys
 d=json.load(open('/tmp/ab.json'))
