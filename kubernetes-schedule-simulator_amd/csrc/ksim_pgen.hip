@@ -1423,12 +1423,13 @@ struct PgEv {
   int32_t cnt, cl, zz;
   uint32_t rmk;
   bool fit;
+  int32_t acnt;  // the auxiliary priority's count (PGF_AUX with a pair)
 };
 static_assert(sizeof(PgEv) == PG_EV_BYTES, "PgEv layout");
 
 namespace {
 
-template <bool HYP>
+template <bool HYP, bool AUX = false>
 __device__ __forceinline__ PgEv pg_eval(const KsimCtx& c, const PGenArgs& g, const PgL& L, const PgX& X, const ksim_pod& P,
                                         const PgHdr& H, int32_t j, int64_t i, const PgHyp& y, const ksim_pod& Py,
                                         uint64_t* sa = nullptr) {
@@ -1460,6 +1461,10 @@ __device__ __forceinline__ PgEv pg_eval(const KsimCtx& c, const PGenArgs& g, con
   if (H.sp >= 0) {
     e.cnt = pg_cnt<HYP>(L, y, H.sp, j);
     e.zz = g.A.zone_key >= 0 ? L.dom[(int64_t)g.A.zone_key * L.chunk + j] : -1;
+  }
+  if (AUX && (H.fl & PGF_AUX)) {
+    const int32_t ap = (H.fl >> PGF_AUX_SHIFT) - 1;
+    if (ap >= 0) e.acnt = pg_cnt<HYP>(L, y, ap, j);
   }
 #ifdef KSIM_STAMPS
   if (sa) sa[5] += __builtin_amdgcn_s_memtime() - t0_;
@@ -1555,13 +1560,15 @@ __device__ __forceinline__ char* pg_xrec4(char* sm, const PGenArgs& g, int64_t r
 
 }  // namespace
 
-template <int NPT, int MB>
+template <int NPT, int MB, bool AUX>
 __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenArgs g_arg) {
   extern __shared__ __attribute__((aligned(16))) char pg_smem[];
-  __shared__ int64_t s_a[4][PG2_NW];                  // pass A per wave: min, max, max count, haveZones
+  __shared__ int64_t s_a[7][PG2_NW];                  // pass A per wave: min, max, max count, haveZones, aux max / sum / haveZones
   __shared__ unsigned long long s_z[PG_MAXZ];        // pass A zone sums of this workgroup
-  __shared__ int64_t s_g[5];                         // pass A over the grid
+  __shared__ unsigned long long s_az[PG_MAXAD];      // the auxiliary priority's domain sums of this workgroup
+  __shared__ int64_t s_g[9];                         // pass A over the grid (+ aux max, sum, haveZones, max domain sum)
   __shared__ int64_t s_gz[PG_MAXZ];                  // countsByZone over the grid
+  __shared__ int64_t s_gaz[PG_MAXAD];                // the auxiliary domain sums over the grid
   __shared__ int32_t s_mx[PG2_NW][KSIM_MAX_RCLASS];  // class partials per wave (only waves 1-3 hold rows)
   __shared__ int32_t s_cn[PG2_NW][KSIM_MAX_RCLASS];
   __shared__ int32_t s_fit[PG2_NW];
@@ -1603,6 +1610,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
   }
   if (tid == 0) s_abort = 0;
   if (tid < PG_MAXZ) s_z[tid] = 0;
+  if (AUX && tid < PG_MAXAD) s_az[tid] = 0;
   uint64_t counter = *c.counter;  // replicated genericScheduler.lastNodeIndex (wave 0)
   __syncthreads();
   pg_stage_counts(c, g, L, nrows, chunk, tid, blockDim.x);
@@ -1624,7 +1632,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
     for (int k = 0; k < NPT; ++k) {
       const int32_t j = k * PG_RT + rt;
       cur[k] = PgEv{0, 0, 0, 0, -1, 0, false};
-      if (rowt && j < nrows) cur[k] = pg_eval<false>(c, g, L, X0, P0, H0, j, lo + j, PgHyp{}, P0);
+      if (rowt && j < nrows) cur[k] = pg_eval<false, AUX>(c, g, L, X0, P0, H0, j, lo + j, PgHyp{}, P0);
     }
   }
   int32_t pend_j = -1;   // deferred commit of pod pend_pod on row pend_j (its row thread)
@@ -1640,15 +1648,19 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
     const int K = H.K, k1 = H.k1, k2 = H.k2;
     const bool ipa = (H.fl & PGF_IPA) != 0;
     const int32_t sp = H.sp;
+    // AUX (an instantiation for handles with the auxiliary priority's tables): the pod may read it
+    const bool aon = AUX && (H.fl & PGF_AUX) != 0;
+    const int32_t ap = AUX ? (H.fl >> PGF_AUX_SHIFT) - 1 : -1;  // (-1 without PGF_AUX too)
     const uint32_t tag = (uint32_t)((pod - c.first + 1) & 0xFF);
     const int slot = (int)(pod % PG_NSLOT);
     const bool has_next = pod + 1 < c.end;
     // wave 4 copies pod p+2's record into LDS in the decision window (its buffer held pod p-2's)
     const bool pf = wv == 4 && pod + 2 < c.end;
 
-    // ---- pass A over the grid (pods that read InterPodAffinity / SelectorSpread) ----
-    if (ipa || sp >= 0) {
-      int64_t mn = 0, mx = 0, smx = 0, hz = 0;
+    // ---- pass A over the grid (pods that read InterPodAffinity / SelectorSpread / the
+    //      auxiliary priority with a pair) ----
+    if (ipa || sp >= 0 || ap >= 0) {
+      int64_t mn = 0, mx = 0, smx = 0, hz = 0, amx = 0, atot = 0, ahz = 0;
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
         if (!cur[k].fit) continue;
@@ -1659,24 +1671,50 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
           hz = 1;
           if (cur[k].cnt) atomicAdd(&s_z[cur[k].zz], (unsigned long long)cur[k].cnt);
         }
+        if (ap >= 0) {  // (passa_reduce's auxiliary words; the count as evaluated, E0 or E1)
+          const int64_t v = cur[k].acnt;
+          const int32_t d = L.dom[(int64_t)g.A.aux_key * chunk + k * PG_RT + rt];
+          amx = v > amx ? v : amx;
+          atot += v;
+          if (d >= 0) {
+            ahz = 1;
+            if (v) atomicAdd(&s_az[d], (unsigned long long)v);
+          }
+        }
       }
       if (ipa) { mn = ksimw::min_i64(mn); mx = ksimw::max_i64(mx); }
       if (sp >= 0) { smx = ksimw::max_i32((int32_t)smx); hz = __ballot(hz != 0) ? 1 : 0; }
-      if (lane == 0) { s_a[0][wv] = mn; s_a[1][wv] = mx; s_a[2][wv] = smx; s_a[3][wv] = hz; }
+      if (ap >= 0) { amx = ksimw::max_i64(amx); atot = ksimw::sum_i64(atot); ahz = __ballot(ahz != 0) ? 1 : 0; }
+      if (lane == 0) {
+        s_a[0][wv] = mn; s_a[1][wv] = mx; s_a[2][wv] = smx; s_a[3][wv] = hz;
+        if (AUX) { s_a[4][wv] = amx; s_a[5][wv] = atot; s_a[6][wv] = ahz; }
+      }
       __syncthreads();
       PG_STAMP(6);
       if (wv == 0) {
         const int nz = sp >= 0 ? g.n_zone : 0;
-        const int RA = 4 + nz;
+        const int na = ap >= 0 ? g.A.n_adom : 0;  // <= PG_MAXAD (host-checked)
+        const int A0 = 4 + nz;                     // the auxiliary words
+        const int RA = A0 + (ap >= 0 ? 3 + na : 0);
+        // word w's combine: 0 = min, 1 = max, 2 = sum
+        auto wop = [&](int w) { return w == 0 ? 0 : (w < 4 ? 1 : ((!AUX || w < A0) ? 2 : (w == A0 || w == A0 + 2 ? 1 : 2))); };
         if (lane < RA) {
           int64_t v;
-          if (lane < 4) {
-            v = s_a[lane][0];
+          if (lane < 4 || (AUX && lane >= A0 && lane < A0 + 3)) {
+            const int row = lane < 4 ? lane : 4 + lane - A0;
+            const int op = wop(lane);
+            v = s_a[row][0];
 #pragma unroll
-            for (int w = 1; w < PG2_NW; ++w) v = lane == 0 ? (s_a[0][w] < v ? s_a[0][w] : v) : (s_a[lane][w] > v ? s_a[lane][w] : v);
-          } else {
+            for (int w = 1; w < PG2_NW; ++w) {
+              const int64_t x = s_a[row][w];
+              v = op == 0 ? (x < v ? x : v) : (op == 1 ? (x > v ? x : v) : v + x);
+            }
+          } else if (!AUX || lane < A0) {
             v = (int64_t)s_z[lane - 4];
             s_z[lane - 4] = 0;
+          } else {
+            v = (int64_t)s_az[lane - A0 - 3];
+            s_az[lane - A0 - 3] = 0;
           }
           pg_store(rec_at(g.gran, slot, lane, blockIdx.x), ((uint64_t)tag << 56) | ((uint64_t)(v + B55) & M56));
         }
@@ -1685,7 +1723,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
 #endif
         // transposed sweep: lane l reads word w0 + l / 8 of workgroups l % 8, l % 8 + 8, ... (G <= 64),
         // folds them, and one 3-step DPP chain within each group of 8 lanes reduces every word at once
-        int64_t r0 = 0, zmax = 0;
+        int64_t r0 = 0, zmax = 0, azmax = 0;
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         bool ok = true;
         for (int w0 = 0; w0 < RA && ok; w0 += 8) {
@@ -1712,7 +1750,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
             t_pub = t_;
           }
 #endif
-          const int op = word == 0 ? 0 : (word < 4 ? 1 : 2);  // min, max, sum
+          const int op = wop(word);  // min, max, sum
           int64_t acc = op == 0 ? INT64_MAX : (op == 1 ? INT64_MIN : 0);
 #pragma unroll
           for (int m = 0; m < 8; ++m) {
@@ -1722,12 +1760,18 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
           }
           acc = pg_red8(acc, op);
           if (w0 == 0) r0 = acc;
-          if (wl && word >= 4) {
+          if (wl && word >= 4 && (!AUX || word < A0)) {
             zmax = acc > zmax ? acc : zmax;
             if ((lane & 7) == 0) s_gz[word - 4] = acc;
+          } else if (AUX && wl && word >= A0 && word < A0 + 3) {
+            if ((lane & 7) == 0) s_g[5 + word - A0] = acc;
+          } else if (AUX && wl && word >= A0 + 3) {
+            azmax = acc > azmax ? acc : azmax;
+            if ((lane & 7) == 0) s_gaz[word - A0 - 3] = acc;
           }
         }
         if (nz) zmax = ksimw::max_i64(zmax);
+        if (na) azmax = ksimw::max_i64(azmax);
         const int64_t a_mn = ipa ? ksimw::readlane64(r0, 0) : 0, a_mx = ipa ? ksimw::readlane64(r0, 8) : 0;
         const int64_t a_smx = sp >= 0 ? ksimw::readlane64(r0, 16) : 0, a_hz = sp >= 0 ? ksimw::readlane64(r0, 24) : 0;
 #ifdef KSIM_STAMPS
@@ -1740,6 +1784,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
           s_g[1] = a_mx > 0 ? a_mx : 0;
           s_g[2] = a_smx; s_g[3] = a_hz;
           s_g[4] = zmax;
+          if (AUX) s_g[8] = azmax;  // (over every domain: zeros included, as passa_reduce)
         }
       } else if (pend_j >= 0) {
         // the previous pod's deferred commit, inside this exchange window
@@ -1760,9 +1805,16 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
       __syncthreads();
       if (s_abort) { stop_pod = pod; break; }
       const int64_t gmn = s_g[0], gmx = s_g[1], gsmx = s_g[2], ghz = s_g[3], gzm = s_g[4];
+      const int64_t gamx = AUX ? s_g[5] : 0, gatot = AUX ? s_g[6] : 0, gahz = AUX ? s_g[7] : 0, gazm = AUX ? s_g[8] : 0;
 #pragma unroll
       for (int k = 0; k < NPT; ++k) {
         if (!cur[k].fit) continue;
+        if (ap >= 0) {  // (aux_add's)
+          const int32_t d = L.dom[(int64_t)g.A.aux_key * chunk + k * PG_RT + rt];
+          const int64_t ds = d >= 0 ? s_gaz[d] : 0;
+          cur[k].sc = (int64_t)((uint64_t)cur[k].sc + (uint64_t)g.A.aux_w * (uint64_t)ksim_aux_score(g.A.aux_kind, cur[k].acnt, d, ds,
+                                                                                                   gamx, gatot, gahz != 0, gazm));
+        }
         if (ipa)
           cur[k].sc = (int64_t)((uint64_t)cur[k].sc +
                                 (uint64_t)c.w[KSIM_W_INTERPOD_AFFINITY] * (uint64_t)ksim_interpod_score(cur[k].raw, gmn, gmx));
@@ -1771,6 +1823,14 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
                                 (uint64_t)c.w[KSIM_W_SELECTOR_SPREAD] *
                                     (uint64_t)ksim_spread_score(cur[k].cnt, gsmx, ghz != 0, cur[k].zz,
                                                                 cur[k].zz >= 0 ? s_gz[cur[k].zz] : 0, gzm));
+      }
+    }
+    if (aon && ap < 0) {  // serviceAntiAffinity of a pod no service selects: 10 on a labelled row (no pass A)
+#pragma unroll
+      for (int k = 0; k < NPT; ++k) {
+        if (!cur[k].fit) continue;
+        const int32_t d = L.dom[(int64_t)g.A.aux_key * chunk + k * PG_RT + rt];
+        cur[k].sc = (int64_t)((uint64_t)cur[k].sc + (uint64_t)g.A.aux_w * (uint64_t)ksim_aux_score(g.A.aux_kind, 0, d, 0, 0, 0, false, 0));
       }
     }
     if (pend_j >= 0) {  // the previous pod's deferred commit, when no pass-A window took it
@@ -2075,13 +2135,13 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
           const int32_t j = k * PG_RT + rt;
-          if (j < nrows) n0[k] = pg_eval<false>(c, g, L, X1, P1, H1, j, lo + j, y, P, k == 0 ? sa : nullptr);
+          if (j < nrows) n0[k] = pg_eval<false, AUX>(c, g, L, X1, P1, H1, j, lo + j, y, P, k == 0 ? sa : nullptr);
         }
       } else if (!(H.fl & PGF_NOHYP) && !c.no_commit) {
 #pragma unroll
         for (int k = 0; k < NPT; ++k) {
           const int32_t j = k * PG_RT + rt;
-          if (j < nrows) ev1[j] = pg_eval<true>(c, g, L, X1, P1, H1, j, lo + j, y, P, k == 0 ? sa : nullptr);
+          if (j < nrows) ev1[j] = pg_eval<true, AUX>(c, g, L, X1, P1, H1, j, lo + j, y, P, k == 0 ? sa : nullptr);
         }
       }
 #ifdef KSIM_STAMPS
@@ -2214,7 +2274,7 @@ __global__ __launch_bounds__(PG2_BS) void ksim_pgen2_kernel(KsimCtx c_arg, PGenA
       for (int k = 0; k < NPT; ++k) {
         const int32_t j = k * PG_RT + rt;
         // shared domains may have changed any row; otherwise only the chosen one
-        if (j < nrows && (shared || k == ksel)) cur[k] = pg_eval<false>(c, g, L, X1, P1, H1, j, lo + j, PgHyp{}, P1);
+        if (j < nrows && (shared || k == ksel)) cur[k] = pg_eval<false, AUX>(c, g, L, X1, P1, H1, j, lo + j, PgHyp{}, P1);
         else cur[k] = n0[k];
       }
     }
@@ -2321,11 +2381,11 @@ extern "C" hipError_t ksim_launch_pgen(const KsimCtx* c, const PGenArgs* g, int 
   }
 }
 
-template <int NPT, int MB>
+template <int NPT, int MB, bool AUX>
 static hipError_t launch_pgen2(const KsimCtx* c, const PGenArgs* g, int grid, size_t lds, hipStream_t s) {
-  hipError_t e = ksim_check_coresident(ksim_pgen2_kernel<NPT, MB>, grid, PG2_BS, lds);
+  hipError_t e = ksim_check_coresident(ksim_pgen2_kernel<NPT, MB, AUX>, grid, PG2_BS, lds);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL((ksim_pgen2_kernel<NPT, MB>), dim3(grid), dim3(PG2_BS), lds, s, *c, *g);
+  hipLaunchKernelGGL((ksim_pgen2_kernel<NPT, MB, AUX>), dim3(grid), dim3(PG2_BS), lds, s, *c, *g);
   return hipGetLastError();
 }
 
@@ -2334,10 +2394,12 @@ extern "C" hipError_t ksim_launch_pgen2(const KsimCtx* c, const PGenArgs* g, int
       (int64_t)grid * c->chunk < c->n || c->chunk > (int64_t)npt * PG_RT || (npt != 1 && npt != 2 && npt != 4) || !g->d.hyp ||
       grid > 64)
     return hipErrorInvalidValue;
+  // the auxiliary priority's instantiation only for handles with its tables
+  const bool aux = g->has_aff && g->A.aux_pair && g->A.aux_w != 0 && !c->no_prio;
   switch (npt) {  // one granule per lane in the sweeps (grid <= 64; larger grids take the single form)
-    case 1: return launch_pgen2<1, 1>(c, g, grid, lds, s);
-    case 2: return launch_pgen2<2, 1>(c, g, grid, lds, s);
-    default: return launch_pgen2<4, 1>(c, g, grid, lds, s);
+    case 1: return aux ? launch_pgen2<1, 1, true>(c, g, grid, lds, s) : launch_pgen2<1, 1, false>(c, g, grid, lds, s);
+    case 2: return aux ? launch_pgen2<2, 1, true>(c, g, grid, lds, s) : launch_pgen2<2, 1, false>(c, g, grid, lds, s);
+    default: return aux ? launch_pgen2<4, 1, true>(c, g, grid, lds, s) : launch_pgen2<4, 1, false>(c, g, grid, lds, s);
   }
 }
 

@@ -878,9 +878,8 @@ static bool pgen_plan(ksim_handle* h, PgPlan* pl, bool allow_v2 = true) {
   if (s >= ((int64_t)1 << 31)) return false;
   if (h->have_aff) {
     if (c.w[KSIM_W_SELECTOR_SPREAD] && h->aff_n_zone > ksim_pgen_max_zones()) return false;
-    // the auxiliary priority: its domain sums in one pass-A record, single-hypothesis kernel only
+    // the auxiliary priority: its domain sums in one pass-A record
     if (aux && h->aff_h.n_adom > ksim_pgen_max_aux_domains()) return false;
-    if (aux) allow_v2 = false;
     if (h->pg_max_mp + h->pg_max_car > 512) return false;  // the shared-domain commit's list
   }
   // the pod-context record bound (ksim_pgen.h): the longest list of every kind
