@@ -50,6 +50,7 @@ def test_c3_full_queue_matches_c_oracle():
     _invariants(cl, out, s)
 
 
+@pytest.mark.timeout(600)  # the tree form's 2.95M-pod head takes ~140 s
 @pytest.mark.parametrize("mode", [abi.MODE_AUTO, abi.MODE_TREE], ids=["scan", "tree"])
 def test_c3_saturated_tail_matches_c_oracle(mode):
     """C3 (100k nodes): 2,950,000 pods on the GPU (past cpu saturation), then the next 3,000 on
